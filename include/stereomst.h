@@ -1,0 +1,143 @@
+/*
+ * stereomst.h -- C-ABI of the MI355X-native Stereo3DMST cost-aggregation path.
+ *
+ * One entry point per reference operation on the hot path; plain pointers and sizes,
+ * integer status codes, no C++/torch/OpenCV types.  The reference-compatible C++
+ * surface (stereo3dmst / startTimer / getTimer, include/Stereo3DMST.h) is a thin shim
+ * over these calls (stereomatch_amd/csrc/shim/stereo3dmst_cv.cpp, built iff OpenCV
+ * is found); ctypes bindings live in stereomatch_amd/_lib.py.
+ *
+ * Reference interfaces replaced (file:line under /root/reference):
+ *   sm_match            <- stereo3dmst()                         src/Stereo3DMST.cpp:714-912
+ *                           (include/Stereo3DMST.h:7), per-slice restatement of the
+ *                           MST_PMS label search
+ *   sm_cost_volume      <- buildCostVolumeSharedMemoryBGR         src/PatchMatchStereoGPU.cu:1482-1550
+ *   sm_build_tree       <- segment_image_other_init (MST mode)    src/Stereo3DMST.cpp:213-543
+ *                           + segment_graph/universe              include/segment-graph.h:54-89
+ *   sm_aggregate_debug  <- aggregateCostFromChildren/Parent       src/Stereo3DMST.cpp:120-158
+ *   WTA inside sm_match <- MSTCostAggregationAndLabelUpdate :160-186 / selectDisparity
+ *                                                                 src/PatchMatchStereoGPU.cu:1688-1737
+ *   sm_start_timer/sm_get_timer_ms <- startTimer/getTimer         src/Stereo3DMST.cpp:15-26
+ *
+ * Threading: one sm_ctx per host thread; no global mutable state in the library.
+ * All calls are synchronous w.r.t. the host unless named *_async.
+ */
+#ifndef STEREOMST_H
+#define STEREOMST_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SM_OK = 0,
+    SM_ERR_ARG = 1,      /* bad argument (sizes, null pointers, unsupported mode)      */
+    SM_ERR_HIP = 2,      /* a HIP runtime call failed (message in sm_last_error)       */
+    SM_ERR_OOM = 3,      /* device allocation failed                                  */
+    SM_ERR_RCCL = 4,     /* an RCCL call failed                                       */
+    SM_ERR_STATE = 5,    /* call order violated (e.g. comm not initialised)           */
+    SM_ERR_NODEVICE = 6  /* no HIP device: the library never falls back to the CPU    */
+} sm_status;
+
+typedef enum { SM_VIEW_LEFT = 0, SM_VIEW_RIGHT = 1 } sm_view;
+
+typedef enum {
+    SM_COST_AGD = 0,     /* truncated colour-AD + gradient cost built on the GPU (.cu:1482) */
+    SM_COST_VOLUME = 1   /* caller-supplied [D][H][W] float volumes (MC-CNN .bin ingest)    */
+} sm_cost_kind;
+
+typedef struct {
+    int device;        /* HIP device ordinal                                        */
+    int max_width;     /* workspace capacity                                        */
+    int max_height;
+    int max_disp;      /* max slices per call on this device (after sharding)       */
+} sm_config;
+
+typedef struct {
+    float gamma;       /* S = exp(-w*gamma); reference 1/12 (Stereo3DMST.cpp:830)    */
+    float c;           /* segment threshold; +INFINITY = MST mode (only mode so far) */
+    int min_size;      /* min component size (Stereo3DMST.cpp:832); unused in MST mode */
+    int median_ksize;  /* 3 (Stereo3DMST.cpp:214); only 3 is supported             */
+    int cost_kind;     /* sm_cost_kind                                              */
+    int disp_begin;    /* first global disparity of this call (D sharding)          */
+    int disp_total;    /* total disparities across all shards (== D unsharded)      */
+} sm_params;
+
+typedef struct sm_ctx sm_ctx;
+
+/* Library / context --------------------------------------------------------- */
+const char* sm_version(void);
+void sm_default_params(sm_params* p);
+sm_status sm_create(sm_ctx** out, const sm_config* cfg);
+void sm_destroy(sm_ctx* ctx);
+const char* sm_last_error(const sm_ctx* ctx);
+sm_status sm_device_count(int* count);
+
+/* Whole path, host buffers (the stereo3dmst() boundary) ----------------------
+ * left_bgr/right_bgr: H rows of W packed BGR u8 pixels, row_stride bytes apart.
+ * Computes slices [p->disp_begin, p->disp_begin + D) for both views and returns,
+ * per view, the strict-< argmin slice (global index), its aggregated cost (fp64) and the
+ * disparity as float.  Any output pointer may be NULL.  When the context has an RCCL
+ * communicator (sm_comm_init) the per-rank results are reduced (min+argmin) across ranks
+ * and every rank receives the global answer. */
+sm_status sm_match(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
+                   int row_stride, int D, const sm_params* p,
+                   float* left_disp, float* right_disp, int32_t* left_idx, int32_t* right_idx,
+                   double* left_min, double* right_min);
+
+/* Device-resident variant for throughput runs: images already in device memory (uploaded
+ * with sm_upload_images); outputs stay on the device until sm_download_results.
+ * Enqueued on the context stream; returns without synchronising. */
+sm_status sm_upload_images(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
+                           int row_stride);
+sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p);
+sm_status sm_synchronize(sm_ctx* ctx);
+sm_status sm_download_results(sm_ctx* ctx, float* left_disp, float* right_disp, int32_t* left_idx,
+                              int32_t* right_idx, double* left_min, double* right_min);
+
+/* Stage entry points (parity tests, MC-CNN ingest) --------------------------- */
+/* AGD cost volumes [D][H][W] float for slices [d0, d0+D); host output buffers. */
+sm_status sm_cost_volume(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
+                         int row_stride, int d0, int D, float* left_vol, float* right_vol);
+
+/* MST of one view's image (MST mode), rooted at pixel 0.  Outputs (host, W*H each, any may
+ * be NULL): mask bit0 = edge (p,p+1) in MST, bit1 = edge (p,p+W); parent pixel (root: -1);
+ * subtree size; heavy-first preorder slot. */
+sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int row_stride, uint8_t* mst_mask,
+                        int32_t* parent_pix, int32_t* subtree_size, int32_t* slot_of_pix);
+
+/* Debug/parity: aggregated volumes of one view in [D][H][W] fp64 (A_up after the leaf->root
+ * pass, A after root->leaf), slices [d0, d0+D).  Memory-hungry: for small images. */
+sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
+                             int row_stride, int view, int d0, int D, double* A_up, double* A);
+
+/* Per-stage timings of the last sm_match/sm_match_async (ms, from HIP events on the ctx
+ * stream): [0] prep+median+weights, [1] MST, [2] tree layout, [3] up pass, [4] down pass+WTA,
+ * [5] cross-rank reduce, [6] total.  n = capacity of out. Returns entries written. */
+int sm_stage_times(sm_ctx* ctx, float* out, int n);
+
+/* Per-launch statistics for the roofline: bytes the dominant kernels must move
+ * (algorithmic), and their summed durations over the last call. */
+typedef struct {
+    double up_ms, down_ms;             /* summed kernel time of the tree-filter passes        */
+    double up_bytes, down_bytes;       /* algorithmic HBM bytes of those passes               */
+    int up_launches, down_launches;
+} sm_filter_stats;
+sm_status sm_get_filter_stats(sm_ctx* ctx, sm_filter_stats* out);
+
+/* Multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------- */
+#define SM_UNIQUE_ID_BYTES 128
+sm_status sm_comm_unique_id(uint8_t out[SM_UNIQUE_ID_BYTES]);
+sm_status sm_comm_init(sm_ctx* ctx, int nranks, int rank, const uint8_t id[SM_UNIQUE_ID_BYTES]);
+sm_status sm_comm_destroy(sm_ctx* ctx);
+
+/* Timers (reference startTimer/getTimer semantics, but per call site, no global). */
+void sm_start_timer(double* t0);
+double sm_get_timer_ms(const double* t0);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,187 @@
+"""oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes bindings for oracle/liboracle.so (the CPU restatement of the Stereo3DMST path,
+see sm_oracle.h) and for oracle/_ref/libref_segment.so (the reference's own
+segment-graph.h compiled from /root/reference, present only in the build container).
+
+Allowed importers: tests/, __graft_entry__.smoke(), bench.py's cpu_baseline leg.
+The product package stereomatch_amd never imports this module.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+c_int, c_float, vp = ctypes.c_int, ctypes.c_float, ctypes.c_void_p
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle not built: run `make -C oracle` (liboracle.so missing)")
+        L = ctypes.CDLL(path)
+        L.orc_median3.argtypes = [u8p, c_int, c_int, c_int, u8p]
+        L.orc_edge_weights.argtypes = [u8p, c_int, c_int, u16p, u16p]
+        L.orc_segment.argtypes = [c_int, c_int, u16p, u16p, c_float, c_int, u8p]
+        L.orc_segment.restype = c_int
+        L.orc_bfs.argtypes = [c_int, c_int, u16p, u16p, u8p, i32p, i32p, i32p, u16p, u8p, i32p]
+        L.orc_bfs.restype = c_int
+        L.orc_cost_agd.argtypes = [u8p, u8p, c_int, c_int, c_int, c_int, c_int, vp, vp]
+        L.orc_tree_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, i32p, i32p, i32p, u16p, u8p,
+                                      i32p, f32p, vp, vp, vp, vp, c_int]
+        L.orc_s_lut.restype = ctypes.POINTER(ctypes.c_double)
+        L.orc_s2_lut.restype = ctypes.POINTER(ctypes.c_double)
+        L.orc_agd_color_term.argtypes = [c_int]
+        L.orc_agd_color_term.restype = c_float
+        _LIB = L
+    return _LIB
+
+
+def ref_lib():
+    """The reference's segment_graph (oracle/_ref); None when not built (e.g. on the GPU box)."""
+    global _REF
+    if _REF is None:
+        path = os.path.join(HERE, "_ref", "libref_segment.so")
+        if not os.path.exists(path):
+            return None
+        R = ctypes.CDLL(path)
+        R.ref_segment_graph.argtypes = [c_int, c_int, i32p, i32p, f64p, c_float, i32p, i32p, f64p, i32p]
+        R.ref_segment_graph.restype = c_int
+        _REF = R
+    return _REF
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(vp)
+
+
+def s_lut():
+    L = lib()
+    return np.ctypeslib.as_array(L.orc_s_lut(), shape=(766,)).copy()
+
+
+def s2_lut():
+    L = lib()
+    return np.ctypeslib.as_array(L.orc_s2_lut(), shape=(766,)).copy()
+
+
+def median3(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W, _ = img.shape
+    out = np.empty((H, W, 3), np.uint8)
+    lib().orc_median3(img, W, H, W * 3, out)
+    return out
+
+
+def edge_weights(med):
+    med = np.ascontiguousarray(med, dtype=np.uint8)
+    H, W, _ = med.shape
+    wR = np.empty(H * W, np.uint16)
+    wD = np.empty(H * W, np.uint16)
+    lib().orc_edge_weights(med, W, H, wR, wD)
+    return wR, wD
+
+
+def segment(W, H, wR, wD, c=float("inf"), min_size=200):
+    mask = np.empty(H * W, np.uint8)
+    n = lib().orc_segment(W, H, wR, wD, c, min_size, mask)
+    return mask, n
+
+
+def bfs(W, H, wR, wD, mask):
+    N = W * H
+    tree_start = np.empty(N + 1, np.int32)
+    node_pix = np.empty(N, np.int32)
+    node_parent = np.empty(N, np.int32)
+    node_w = np.empty(N, np.uint16)
+    node_nch = np.empty(N, np.uint8)
+    node_child = np.empty(4 * N, np.int32)
+    nt = lib().orc_bfs(W, H, wR, wD, mask, tree_start, node_pix, node_parent, node_w, node_nch, node_child)
+    return dict(ntrees=nt, tree_start=tree_start[:nt + 1].copy(), node_pix=node_pix, node_parent=node_parent,
+                node_w=node_w, node_nch=node_nch, node_child=node_child)
+
+
+def cost_agd(left, right, d0, d1):
+    left = np.ascontiguousarray(left, dtype=np.uint8)
+    right = np.ascontiguousarray(right, dtype=np.uint8)
+    H, W, _ = left.shape
+    lv = np.empty((d1 - d0, H, W), np.float32)
+    rv = np.empty((d1 - d0, H, W), np.float32)
+    lib().orc_cost_agd(left, right, W, H, W * 3, d0, d1, _ptr(lv), _ptr(rv))
+    return lv, rv
+
+
+def tree_filter(W, H, tree, vol, d0=0, want_idx=True, want_volumes=False, nthreads=0):
+    nd = vol.shape[0]
+    N = W * H
+    idx = np.empty(N, np.int32) if want_idx else None
+    minc = np.empty(N, np.float64) if want_idx else None
+    Aup = np.empty((nd, H, W), np.float64) if want_volumes else None
+    A = np.empty((nd, H, W), np.float64) if want_volumes else None
+    lib().orc_tree_filter(W, H, nd, d0, tree["ntrees"], tree["tree_start"], tree["node_pix"], tree["node_parent"],
+                          tree["node_w"], tree["node_nch"], tree["node_child"],
+                          np.ascontiguousarray(vol, dtype=np.float32),
+                          _ptr(idx), _ptr(minc), _ptr(Aup), _ptr(A), nthreads)
+    return dict(idx=idx, minc=minc, Aup=Aup, A=A)
+
+
+def build_tree(img, c=float("inf"), min_size=200):
+    """median -> edge weights -> segment/MST -> BFS rooting, for one view."""
+    H, W, _ = img.shape
+    med = median3(img)
+    wR, wD = edge_weights(med)
+    mask, ncomp = segment(W, H, wR, wD, c, min_size)
+    tree = bfs(W, H, wR, wD, mask)
+    tree.update(med=med, wR=wR, wD=wD, mask=mask)
+    return tree
+
+
+def match(left, right, D, c=float("inf"), min_size=200, want_volumes=False, nthreads=0):
+    """The whole path on the CPU: both views, slices 0..D-1.  Returns per-view dicts."""
+    H, W, _ = left.shape
+    lv, rv = cost_agd(left, right, 0, D)
+    out = {}
+    for name, img, vol in (("left", left, lv), ("right", right, rv)):
+        tree = build_tree(img, c, min_size)
+        res = tree_filter(W, H, tree, vol, 0, True, want_volumes, nthreads)
+        res["tree"] = tree
+        res["vol"] = vol
+        out[name] = res
+    return out
+
+
+def ref_segment_graph(W, H, wR, wD, c):
+    """Run the reference's own segment_graph on the 4-connected edges of (wR, wD).
+    Returns the per-pixel mask in ORC_EDGE_* encoding and num_sets, or None if _ref is absent."""
+    R = ref_lib()
+    if R is None:
+        return None
+    a, b, w = [], [], []
+    for p in range(W * H):  # emission order of Stereo3DMST.cpp:244-262
+        x, y = p % W, p // W
+        if x < W - 1:
+            a.append(p); b.append(p + 1); w.append(float(wR[p]))
+        if y < H - 1:
+            a.append(p); b.append(p + W); w.append(float(wD[p]))
+    E = len(a)
+    a = np.array(a, np.int32); b = np.array(b, np.int32); w = np.array(w, np.float64)
+    oa = np.empty(E, np.int32); ob = np.empty(E, np.int32); ow = np.empty(E, np.float64); om = np.empty(E, np.int32)
+    nsets = R.ref_segment_graph(W * H, E, a, b, w, c, oa, ob, ow, om)
+    mask = np.zeros(W * H, np.uint8)
+    sel = om == 1
+    right = sel & (ob == oa + 1) & (W > 1)
+    down = sel & ~right
+    np.bitwise_or.at(mask, oa[right], 1)
+    np.bitwise_or.at(mask, oa[down], 2)
+    return dict(mask=mask, nsets=nsets, sorted_a=oa, sorted_b=ob, sorted_w=ow, sorted_mask=om)

@@ -1,0 +1,79 @@
+/*
+ * sm_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the lr-xiang/StereoMatch Stereo3DMST cost-aggregation path,
+ * used as the parity checker for the HIP product (stereomatch_amd/) and as the
+ * cpu_baseline leg of bench.py.  Nothing in the product links, loads or calls
+ * this library: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline.
+ *
+ * Parity status (details in DESIGN.md "Oracle"):
+ *  - MST (orc_segment) is pinned against the reference's own include/segment-graph.h
+ *    + include/disjoint-set.h, compiled here into oracle/_ref (tests/golden fixtures).
+ *  - Tree filter arithmetic is pinned by static disassembly of the shipped
+ *    build/StereoYin (vfmadd/vfnmadd pattern), not by executed reference outputs.
+ *  - AGD cost volume restates src/PatchMatchStereoGPU.cu:1482-1550; the reference
+ *    ships no fixtures for it (parity unpinned for that row).
+ *
+ * Layouts: images are packed BGR uint8 rows (OpenCV CV_8UC3) with a row stride in
+ * bytes; pixel index p = y*W + x; volumes are [d][y][x] (Stereo3DMST.cpp:117).
+ */
+#ifndef SM_ORACLE_H
+#define SM_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* mst/segment mask bits per pixel */
+#define ORC_EDGE_RIGHT 1u /* edge (p, p+1) */
+#define ORC_EDGE_DOWN 2u  /* edge (p, p+W) */
+
+/* cv::medianBlur(ksize=3) per channel, BORDER_REPLICATE (Stereo3DMST.cpp:226-228). out: packed W*3. */
+void orc_median3(const uint8_t* img, int W, int H, int stride, uint8_t* out);
+
+/* 4-connected edge weights, L1 RGB (Stereo3DMST.cpp:83-94, 242-262). wR[p] for x<W-1, wD[p] for y<H-1,
+ * 0xFFFF where the edge does not exist. */
+void orc_edge_weights(const uint8_t* med, int W, int H, uint16_t* wR, uint16_t* wD);
+
+/* segment_graph (include/segment-graph.h:54-89) + min-size merge (Stereo3DMST.cpp:293-307).
+ * c = +INFINITY is MST mode; min_size < 0 skips the merge (oracle-only).  Returns the number of components; mask gets ORC_EDGE_* bits. */
+int orc_segment(int W, int H, const uint16_t* wR, const uint16_t* wD, float c, int min_size, uint8_t* mask);
+
+/* Component enumeration + BFS rooting/renumbering (Stereo3DMST.cpp:342-369, 434-522).
+ * Trees in order of their first raster pixel; root = first pixel; children in ascending
+ * (w,a,b) edge order (Boost vecS insertion order).  Node arrays are indexed by global BFS
+ * node id (tree_start[t] + bfs id).  node_parent[root] = root; node_w[root] = 0.
+ * node_child[4*n+i] for i < node_nch[n], ascending BFS id.  Returns number of trees. */
+int orc_bfs(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t* mask,
+            int32_t* tree_start, int32_t* node_pix, int32_t* node_parent, uint16_t* node_w,
+            uint8_t* node_nch, int32_t* node_child);
+
+/* buildCostVolumeSharedMemoryBGR (PatchMatchStereoGPU.cu:1482-1550), slices d0..d1-1:
+ * right[d][y][x] (right reference) and left[d][y][x+d]; invalid = 3.0f; the left column
+ * the reference never writes (x = W-1, x >= d) is defined as 3.0f. Volumes [(d1-d0)][H][W]. */
+void orc_cost_agd(const uint8_t* left, const uint8_t* right, int W, int H, int stride, int d0, int d1,
+                  float* left_vol, float* right_vol);
+
+/* Per-slice tree filter in the shipped order (Stereo3DMST.cpp:120-186):
+ *   up   (descending BFS id): A[p] = A[p] + C ; A[parent] = fma(S, A[p], A[parent])
+ *   down (ascending BFS id) : A[c] = fma(S_c, A[p], S2_c * A[c])
+ * then strict-< argmin over slices (first minimum wins, init DBL_MAX); idx is absolute (d0+..).  vol: [nd][H][W]
+ * slices d0..d0+nd-1.  idx/minc: W*H (may be NULL); Aup/A: [nd][H][W] (may be NULL).
+ * OpenMP over slices with nthreads threads (<=0: default). */
+void orc_tree_filter(int W, int H, int nd, int d0, int ntrees, const int32_t* tree_start,
+                     const int32_t* node_pix, const int32_t* node_parent, const uint16_t* node_w,
+                     const uint8_t* node_nch, const int32_t* node_child, const float* vol,
+                     int32_t* idx, double* minc, double* Aup, double* A, int nthreads);
+
+/* The S / S2 tables the oracle uses (for tests). */
+const double* orc_s_lut(void);
+const double* orc_s2_lut(void);
+
+/* AGD color term table a(l1) = 0.11f*fminf((float)(l1*0.33333333333), 7.0f), l1 in [0,765]. */
+float orc_agd_color_term(int l1);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,61 @@
+"""stereomatch_amd -- MI355X-native Stereo3DMST cost-aggregation path.
+
+Python mirror of the reference's entry surface (include/Stereo3DMST.h:7-11):
+
+    stereo3dmst(left_name, right_name, left_img, right_img, data_cost, Dmax)
+        -> (left_disp, right_disp)                 # src/Stereo3DMST.cpp:714
+    startTimer() / getTimer()                      # src/Stereo3DMST.cpp:15-26
+
+backed by the HIP library libstereomst.so (C-ABI in include/stereomst.h).  The compute
+runs only on the GPU; a missing library or device raises.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import (SM_COST_AGD, Context, StereoMSTError, default_params, device_count, lib)  # noqa: F401
+
+__all__ = ["stereo3dmst", "startTimer", "getTimer", "Context", "default_params", "StereoMSTError", "device_count"]
+
+_default_ctx = None
+_timer = ctypes.c_double(0.0)
+
+
+def _ctx():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dmax=100):
+    """Reference-compatible entry (src/Stereo3DMST.cpp:714-912, per-slice restatement).
+
+    left_img/right_img: HxWx3 uint8 BGR (cv::Mat CV_8UC3).  Returns (left_disp, right_disp),
+    float32 HxW in [0, Dmax-1]: the strict-< winner-take-all slice of the MST-aggregated
+    AGD cost.  Like the reference, an unsupported data_cost prints a
+    message and returns allocated-but-unset maps (:756-759); the names are only forwarded
+    to the cost source and are unused by the AGD cost.
+    """
+    H, W = left_img.shape[:2]
+    left_disp = np.empty((H, W), np.float32)
+    right_disp = np.empty((H, W), np.float32)
+    if data_cost in ("MCCNN_fst", "MCCNN_acrt"):
+        # reference: chdir("mc-cnn-master") fails -> message and return (:727-731)
+        print("no mc-cnn-master folder")
+        return left_disp, right_disp
+    if data_cost != "AGD":
+        print("wrong data cost")
+        return left_disp, right_disp
+    out = _ctx().match(left_img, right_img, int(Dmax))
+    left_disp[...] = out["left"]["disp"]
+    right_disp[...] = out["right"]["disp"]
+    return left_disp, right_disp
+
+
+def startTimer():
+    lib().sm_start_timer(ctypes.byref(_timer))
+
+
+def getTimer():
+    return lib().sm_get_timer_ms(ctypes.byref(_timer))

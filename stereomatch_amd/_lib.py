@@ -1,0 +1,230 @@
+"""ctypes binding of libstereomst.so (include/stereomst.h).
+
+The HIP library is the only compute path: if it is missing or no GPU is present the
+calls raise -- there is no CPU fallback in this package.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libstereomst.so")
+
+SM_OK, SM_ERR_ARG, SM_ERR_HIP, SM_ERR_OOM, SM_ERR_RCCL, SM_ERR_STATE, SM_ERR_NODEVICE = range(7)
+STATUS_NAMES = {0: "SM_OK", 1: "SM_ERR_ARG", 2: "SM_ERR_HIP", 3: "SM_ERR_OOM", 4: "SM_ERR_RCCL",
+                5: "SM_ERR_STATE", 6: "SM_ERR_NODEVICE"}
+SM_COST_AGD, SM_COST_VOLUME = 0, 1
+SM_UNIQUE_ID_BYTES = 128
+
+
+class SmConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("max_width", ctypes.c_int), ("max_height", ctypes.c_int),
+                ("max_disp", ctypes.c_int)]
+
+
+class SmParams(ctypes.Structure):
+    _fields_ = [("gamma", ctypes.c_float), ("c", ctypes.c_float), ("min_size", ctypes.c_int),
+                ("median_ksize", ctypes.c_int), ("cost_kind", ctypes.c_int), ("disp_begin", ctypes.c_int),
+                ("disp_total", ctypes.c_int)]
+
+
+class SmFilterStats(ctypes.Structure):
+    _fields_ = [("up_ms", ctypes.c_double), ("down_ms", ctypes.c_double), ("up_bytes", ctypes.c_double),
+                ("down_bytes", ctypes.c_double), ("up_launches", ctypes.c_int), ("down_launches", ctypes.c_int)]
+
+
+class StereoMSTError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__("%s: %s" % (STATUS_NAMES.get(status, str(status)), msg))
+        self.status = status
+
+
+_lib = None
+vp = ctypes.c_void_p
+ci = ctypes.c_int
+
+
+def lib():
+    """Load the in-tree HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("stereomatch_amd HIP library missing (%s): run __graft_entry__.build() or "
+                           "`make -C stereomatch_amd/csrc`" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    sigs = {
+        "sm_version": ([], ctypes.c_char_p),
+        "sm_default_params": ([ctypes.POINTER(SmParams)], None),
+        "sm_device_count": ([ctypes.POINTER(ci)], ci),
+        "sm_create": ([ctypes.POINTER(vp), ctypes.POINTER(SmConfig)], ci),
+        "sm_destroy": ([vp], None),
+        "sm_last_error": ([vp], ctypes.c_char_p),
+        "sm_match": ([vp, vp, vp, ci, ci, ci, ci, ctypes.POINTER(SmParams), vp, vp, vp, vp, vp, vp], ci),
+        "sm_upload_images": ([vp, vp, vp, ci, ci, ci], ci),
+        "sm_match_async": ([vp, ci, ctypes.POINTER(SmParams)], ci),
+        "sm_synchronize": ([vp], ci),
+        "sm_download_results": ([vp, vp, vp, vp, vp, vp, vp], ci),
+        "sm_cost_volume": ([vp, vp, vp, ci, ci, ci, ci, ci, vp, vp], ci),
+        "sm_build_tree": ([vp, vp, ci, ci, ci, vp, vp, vp, vp], ci),
+        "sm_aggregate_debug": ([vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp], ci),
+        "sm_stage_times": ([vp, vp, ci], ci),
+        "sm_get_filter_stats": ([vp, ctypes.POINTER(SmFilterStats)], ci),
+        "sm_comm_unique_id": ([vp], ci),
+        "sm_comm_init": ([vp, ci, ci, vp], ci),
+        "sm_comm_destroy": ([vp], ci),
+        "sm_start_timer": ([ctypes.POINTER(ctypes.c_double)], None),
+        "sm_get_timer_ms": ([ctypes.POINTER(ctypes.c_double)], ctypes.c_double),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def default_params(**overrides):
+    p = SmParams()
+    lib().sm_default_params(ctypes.byref(p))
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+def device_count():
+    n = ci(0)
+    lib().sm_device_count(ctypes.byref(n))
+    return n.value
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(vp)
+
+
+def as_image(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    if img.ndim != 3 or img.shape[2] != 3:
+        raise ValueError("expected an HxWx3 uint8 BGR image")
+    return img
+
+
+class Context:
+    """One sm_ctx (one HIP device, one stream).  Not thread-safe: one per host thread."""
+
+    def __init__(self, device=0, max_width=0, max_height=0, max_disp=0):
+        L = lib()
+        cfg = SmConfig(device, max_width, max_height, max_disp)
+        h = vp()
+        st = L.sm_create(ctypes.byref(h), ctypes.byref(cfg))
+        if st != SM_OK:
+            raise StereoMSTError(st, "sm_create failed (no HIP device?)")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st):
+        if st != SM_OK:
+            msg = lib().sm_last_error(self.h)
+            raise StereoMSTError(st, msg.decode() if msg else "")
+
+    # -- whole path --------------------------------------------------------------------
+    def match(self, left, right, D, params=None):
+        left, right = as_image(left), as_image(right)
+        H, W, _ = left.shape
+        if right.shape != left.shape:
+            raise ValueError("left/right shapes differ")
+        p = params or default_params()
+        out = {v: dict(disp=np.empty((H, W), np.float32), idx=np.empty((H, W), np.int32),
+                       minc=np.empty((H, W), np.float64)) for v in ("left", "right")}
+        self._check(lib().sm_match(self.h, ptr(left), ptr(right), W, H, W * 3, D, ctypes.byref(p),
+                                   ptr(out["left"]["disp"]), ptr(out["right"]["disp"]), ptr(out["left"]["idx"]),
+                                   ptr(out["right"]["idx"]), ptr(out["left"]["minc"]), ptr(out["right"]["minc"])))
+        return out
+
+    def upload(self, left, right):
+        left, right = as_image(left), as_image(right)
+        H, W, _ = left.shape
+        self.shape = (H, W)
+        self._check(lib().sm_upload_images(self.h, ptr(left), ptr(right), W, H, W * 3))
+
+    def match_async(self, D, params=None):
+        p = params or default_params()
+        self._check(lib().sm_match_async(self.h, D, ctypes.byref(p)))
+
+    def synchronize(self):
+        self._check(lib().sm_synchronize(self.h))
+
+    def results(self):
+        H, W = self.shape
+        out = {v: dict(disp=np.empty((H, W), np.float32), idx=np.empty((H, W), np.int32),
+                       minc=np.empty((H, W), np.float64)) for v in ("left", "right")}
+        self._check(lib().sm_download_results(self.h, ptr(out["left"]["disp"]), ptr(out["right"]["disp"]),
+                                              ptr(out["left"]["idx"]), ptr(out["right"]["idx"]),
+                                              ptr(out["left"]["minc"]), ptr(out["right"]["minc"])))
+        return out
+
+    def stage_times(self):
+        buf = (ctypes.c_float * 7)()
+        n = lib().sm_stage_times(self.h, buf, 7)
+        names = ["prep_ms", "mst_ms", "layout_ms", "up_ms", "down_ms", "reduce_ms", "total_ms"]
+        return {names[i]: float(buf[i]) for i in range(n)}
+
+    def filter_stats(self):
+        s = SmFilterStats()
+        self._check(lib().sm_get_filter_stats(self.h, ctypes.byref(s)))
+        return {k: getattr(s, k) for k, _ in SmFilterStats._fields_}
+
+    # -- stages ---------------------------------------------------------------------------
+    def cost_volume(self, left, right, d0, D):
+        left, right = as_image(left), as_image(right)
+        H, W, _ = left.shape
+        lv = np.empty((D, H, W), np.float32)
+        rv = np.empty((D, H, W), np.float32)
+        self._check(lib().sm_cost_volume(self.h, ptr(left), ptr(right), W, H, W * 3, d0, D, ptr(lv), ptr(rv)))
+        return lv, rv
+
+    def build_tree(self, img):
+        img = as_image(img)
+        H, W, _ = img.shape
+        mask = np.empty(H * W, np.uint8)
+        parent = np.empty(H * W, np.int32)
+        size = np.empty(H * W, np.int32)
+        slot = np.empty(H * W, np.int32)
+        self._check(lib().sm_build_tree(self.h, ptr(img), W, H, W * 3, ptr(mask), ptr(parent), ptr(size), ptr(slot)))
+        return dict(mask=mask, parent_pix=parent, subtree_size=size, slot_of_pix=slot)
+
+    def aggregate_debug(self, left, right, view, d0, D):
+        left, right = as_image(left), as_image(right)
+        H, W, _ = left.shape
+        Aup = np.empty((D, H, W), np.float64)
+        A = np.empty((D, H, W), np.float64)
+        self._check(lib().sm_aggregate_debug(self.h, ptr(left), ptr(right), W, H, W * 3, view, d0, D, ptr(Aup),
+                                             ptr(A)))
+        return Aup, A
+
+    # -- multi-GPU ------------------------------------------------------------------------
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * SM_UNIQUE_ID_BYTES)()
+        st = lib().sm_comm_unique_id(buf)
+        if st != SM_OK:
+            raise StereoMSTError(st, "sm_comm_unique_id failed")
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (ctypes.c_uint8 * SM_UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        self._check(lib().sm_comm_init(self.h, nranks, rank, buf))
+
+    def comm_destroy(self):
+        self._check(lib().sm_comm_destroy(self.h))

@@ -1,0 +1,629 @@
+// sm_api.cpp -- C-ABI (include/stereomst.h): context, orchestration of the HIP stages,
+// RCCL min+argmin reduce for disparity sharding, timers.
+//
+// Pipeline of one frame (both views in every launch, blockIdx selects the view):
+//   prep -> median -> weights -> Boruvka MST -> tree layout -> up rounds -> down rounds (+WTA)
+//   [-> RCCL allreduce(min f64) + allreduce(min i32 candidate index) when sharded over ranks]
+// There is no CPU fallback: without a HIP device every entry returns SM_ERR_NODEVICE.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <sys/time.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/stereomst.h"
+#include "sm_common.h"
+#include "sm_launch.h"
+#include "sm_layout.h"
+#include "sm_tables.inc"
+
+hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N);
+hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gidx, double* minc, int32_t* idx, float* disp,
+                           size_t N);
+hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl);
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct sm_ctx {
+    int device = 0;
+    hipStream_t st = nullptr;
+    std::string err;
+    int W = 0, H = 0, stride = 0;
+    DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
+    DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], idx[2], minc[2], disp[2];
+    DevBuf cand[2], gmin[2], gidx[2], vol[2];
+    int* h_changed = nullptr;
+    SmLayout layout[2];
+    hipEvent_t ev[8] = {};
+    std::vector<hipEvent_t> up_ev, down_ev;
+    int n_up = 0, n_down = 0;
+    sm_filter_stats stats{};
+    float stage_ms[7] = {0};
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    bool reduced = false;
+};
+
+namespace {
+
+sm_status fail(sm_ctx* c, sm_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+#define HIPC(call)                                                                                    \
+    do {                                                                                              \
+        hipError_t e_ = (call);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? SM_ERR_OOM : SM_ERR_HIP,                     \
+                        std::string(#call) + ": " + hipGetErrorString(e_));                         \
+    } while (0)
+
+#define RCCLC(call)                                                                                   \
+    do {                                                                                              \
+        ncclResult_t r_ = (call);                                                                     \
+        if (r_ != ncclSuccess) return fail(ctx, SM_ERR_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+#define CHECK(expr)                  \
+    do {                             \
+        sm_status s_ = (expr);       \
+        if (s_ != SM_OK) return s_;  \
+    } while (0)
+
+sm_status ensure(sm_ctx* ctx, DevBuf& b, size_t bytes) {
+    if (b.n >= bytes && b.p) return SM_OK;
+    if (b.p) HIPC(hipFree(b.p));
+    b.p = nullptr;
+    b.n = 0;
+    HIPC(hipMalloc(&b.p, bytes ? bytes : 16));
+    b.n = bytes;
+    return SM_OK;
+}
+
+template <class T>
+T* P(DevBuf& b) {
+    return reinterpret_cast<T*>(b.p);
+}
+
+int spl_for(int D) { return D <= 64 ? 1 : D <= 128 ? 2 : 4; }
+
+float agd_color_term(int l1) {
+    // 0.11f*fminf(color_l1*0.33333333333, 7.0f) (PatchMatchStereoGPU.cu:1539)
+    const float scaled = (float)((double)(float)l1 * 0.33333333333);
+    return 0.11f * fminf(scaled, 7.0f);
+}
+
+sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
+    if (!p) return fail(ctx, SM_ERR_ARG, "null params");
+    if (!(std::isinf(p->c) && p->c > 0))
+        return fail(ctx, SM_ERR_ARG, "segment mode (finite c) is not implemented yet: use c=+INFINITY (MST mode)");
+    if (p->median_ksize != 3) return fail(ctx, SM_ERR_ARG, "only median_ksize=3 is supported");
+    if (p->cost_kind != SM_COST_AGD) return fail(ctx, SM_ERR_ARG, "only SM_COST_AGD is implemented");
+    if (p->gamma != 1.0f / 12.f)
+        return fail(ctx, SM_ERR_ARG, "only gamma=1/12 (embedded correctly-rounded tables) is supported");
+    if (D < 1 || D > 256) return fail(ctx, SM_ERR_ARG, "D must be in [1, 256] per call (shard larger ranges)");
+    if (p->disp_begin < 0) return fail(ctx, SM_ERR_ARG, "disp_begin < 0");
+    return SM_OK;
+}
+
+// ----------------------------------------------------------------------------- stages
+sm_status stage_prep(sm_ctx* ctx) {
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H;
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->bgrx[v], N * 4));
+        CHECK(ensure(ctx, ctx->gray[v], N * 4));
+        CHECK(ensure(ctx, ctx->med[v], N * 4));
+        CHECK(ensure(ctx, ctx->wR[v], N * 2));
+        CHECK(ensure(ctx, ctx->wD[v], N * 2));
+    }
+    HIPC(launch_prep(ctx->st, P<uint8_t>(ctx->img[0]), P<uint8_t>(ctx->img[1]), W, H, ctx->stride, P<uint32_t>(ctx->bgrx[0]),
+                     P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]), P<float>(ctx->gray[1])));
+    HIPC(launch_median_weights(ctx->st, P<uint32_t>(ctx->bgrx[0]), P<uint32_t>(ctx->bgrx[1]), P<uint32_t>(ctx->med[0]),
+                               P<uint32_t>(ctx->med[1]), P<uint16_t>(ctx->wR[0]), P<uint16_t>(ctx->wD[0]),
+                               P<uint16_t>(ctx->wR[1]), P<uint16_t>(ctx->wD[1]), W, H));
+    return SM_OK;
+}
+
+sm_status stage_mst(sm_ctx* ctx, int nviews) {
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H;
+    MstArgs a{};
+    a.nviews = nviews;
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->comp[v], N * 4));
+        CHECK(ensure(ctx, ctx->best[v], N * 8));
+        CHECK(ensure(ctx, ctx->root[v], N * 4));
+        CHECK(ensure(ctx, ctx->mR[v], N));
+        CHECK(ensure(ctx, ctx->mD[v], N));
+        HIPC(hipMemsetAsync(ctx->mR[v].p, 0, N, ctx->st));
+        HIPC(hipMemsetAsync(ctx->mD[v].p, 0, N, ctx->st));
+        HIPC(hipMemsetAsync(ctx->best[v].p, 0xFF, N * 8, ctx->st));
+        a.wR[v] = P<uint16_t>(ctx->wR[v]);
+        a.wD[v] = P<uint16_t>(ctx->wD[v]);
+        a.comp[v] = P<uint32_t>(ctx->comp[v]);
+        a.best[v] = P<unsigned long long>(ctx->best[v]);
+        a.root[v] = P<uint32_t>(ctx->root[v]);
+        a.mR[v] = P<uint8_t>(ctx->mR[v]);
+        a.mD[v] = P<uint8_t>(ctx->mD[v]);
+    }
+    CHECK(ensure(ctx, ctx->changed, 16));
+    a.changed = P<int>(ctx->changed);
+    HIPC(launch_bor_local(ctx->st, a, W, H));
+    for (int round = 0; round < 64; ++round) {
+        HIPC(hipMemsetAsync(ctx->changed.p, 0, sizeof(int), ctx->st));
+        HIPC(launch_bor_round(ctx->st, a, W, H));
+        HIPC(hipMemcpyAsync(ctx->h_changed, ctx->changed.p, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipStreamSynchronize(ctx->st));
+        if (*ctx->h_changed == 0) break;
+    }
+    return SM_OK;
+}
+
+sm_status stage_layout(sm_ctx* ctx, int nviews) {
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H;
+    std::vector<uint8_t> mR[2], mD[2];
+    std::vector<uint16_t> wR[2], wD[2];
+    for (int v = 0; v < nviews; ++v) {
+        mR[v].resize(N); mD[v].resize(N); wR[v].resize(N); wD[v].resize(N);
+        HIPC(hipMemcpyAsync(mR[v].data(), ctx->mR[v].p, N, hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipMemcpyAsync(mD[v].data(), ctx->mD[v].p, N, hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipMemcpyAsync(wR[v].data(), ctx->wR[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipMemcpyAsync(wD[v].data(), ctx->wD[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
+    }
+    HIPC(hipStreamSynchronize(ctx->st));
+    std::thread th[2];
+    for (int v = 0; v < nviews; ++v)
+        th[v] = std::thread([&, v] { sm_build_layout(W, H, mR[v].data(), mD[v].data(), wR[v].data(), wD[v].data(), ctx->layout[v]); });
+    for (int v = 0; v < nviews; ++v) th[v].join();
+    for (int v = 0; v < nviews; ++v) {
+        const SmLayout& L = ctx->layout[v];
+        CHECK(ensure(ctx, ctx->meta[v], N * sizeof(SmMeta)));
+        CHECK(ensure(ctx, ctx->paths[v], L.paths.size() * sizeof(SmPath) + 16));
+        HIPC(hipMemcpyAsync(ctx->meta[v].p, L.meta.data(), N * sizeof(SmMeta), hipMemcpyHostToDevice, ctx->st));
+        HIPC(hipMemcpyAsync(ctx->paths[v].p, L.paths.data(), L.paths.size() * sizeof(SmPath), hipMemcpyHostToDevice, ctx->st));
+    }
+    HIPC(hipStreamSynchronize(ctx->st));  // host vectors above are pageable and about to be freed
+    return SM_OK;
+}
+
+WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
+    WalkArgs a{};
+    for (int v = 0; v < 2; ++v) {
+        a.meta[v] = P<SmMeta>(ctx->meta[v]);
+        a.U[v] = P<double>(ctx->U[v]);
+        a.idx[v] = P<int32_t>(ctx->idx[v]);
+        a.minc[v] = P<double>(ctx->minc[v]);
+        a.disp[v] = P<float>(ctx->disp[v]);
+    }
+    a.Lb = P<uint32_t>(ctx->bgrx[0]);
+    a.Lg = P<float>(ctx->gray[0]);
+    a.Rb = P<uint32_t>(ctx->bgrx[1]);
+    a.Rg = P<float>(ctx->gray[1]);
+    a.atab = P<float>(ctx->atab);
+    a.slut = P<double>(ctx->slut);
+    a.s2lut = P<double>(ctx->s2lut);
+    a.W = ctx->W;
+    a.Dpad = Dpad;
+    a.dcall = D;
+    a.dglob0 = dglob0;
+    return a;
+}
+
+void set_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int nviews) {
+    for (int v = 0; v < 2; ++v) {
+        const SmLayout& L = ctx->layout[v];
+        if (v >= nviews || r >= L.nrounds) {
+            a.paths[v] = P<SmPath>(ctx->paths[v]);
+            a.npaths[v] = 0;
+        } else {
+            a.paths[v] = P<SmPath>(ctx->paths[v]) + L.round_path_begin[r];
+            a.npaths[v] = (int)(L.round_path_begin[r + 1] - L.round_path_begin[r]);
+        }
+    }
+}
+
+sm_status ensure_events(sm_ctx* ctx, std::vector<hipEvent_t>& evs, size_t n) {
+    while (evs.size() < n) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        evs.push_back(e);
+    }
+    return SM_OK;
+}
+
+// up + down passes over all rounds for nviews views; debug_store_all stores every A row
+sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_store_all) {
+    const size_t N = (size_t)ctx->W * ctx->H;
+    const int spl = spl_for(D);
+    const int Dpad = 64 * spl;
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
+        CHECK(ensure(ctx, ctx->idx[v], N * 4));
+        CHECK(ensure(ctx, ctx->minc[v], N * 8));
+        CHECK(ensure(ctx, ctx->disp[v], N * 4));
+    }
+    uint32_t nr = 0;
+    for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
+    CHECK(ensure_events(ctx, ctx->up_ev, 2 * nr));
+    CHECK(ensure_events(ctx, ctx->down_ev, 2 * nr));
+    WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
+    ctx->n_up = ctx->n_down = (int)nr;
+    for (uint32_t i = 0; i < nr; ++i) {
+        const uint32_t r = nr - 1 - i;  // deepest light depth first
+        set_round(ctx, a, r, nviews);
+        HIPC(hipEventRecord(ctx->up_ev[2 * i], ctx->st));
+        HIPC(launch_up(ctx->st, a, spl));
+        HIPC(hipEventRecord(ctx->up_ev[2 * i + 1], ctx->st));
+    }
+    for (uint32_t r = 0; r < nr; ++r) {
+        set_round(ctx, a, r, nviews);
+        HIPC(hipEventRecord(ctx->down_ev[2 * r], ctx->st));
+        if (debug_store_all)
+            HIPC(launch_down_debug(ctx->st, a, spl));
+        else
+            HIPC(launch_down(ctx->st, a, spl));
+        HIPC(hipEventRecord(ctx->down_ev[2 * r + 1], ctx->st));
+    }
+    // algorithmic bytes (see DESIGN.md "Roofline accounting")
+    double upb = 0, downb = 0;
+    for (int v = 0; v < nviews; ++v) {
+        const SmLayout& L = ctx->layout[v];
+        const double row = 8.0 * D;
+        const double heads = (double)L.paths.size(), roots = (double)L.nroots;
+        double has_light = 0;
+        for (const SmMeta& m : L.meta) has_light += sm_meta_has_light(m);
+        upb += row * (double)N + row * (double)L.n_light + 32.0 * (double)N;
+        downb += row * (double)N + row * (heads - roots) + row * has_light + 32.0 * (double)N + 16.0 * (double)N;
+    }
+    ctx->stats.up_bytes = upb;
+    ctx->stats.down_bytes = downb;
+    ctx->stats.up_launches = (int)nr;
+    ctx->stats.down_launches = (int)nr;
+    return SM_OK;
+}
+
+sm_status stage_reduce(sm_ctx* ctx) {
+    if (!ctx->comm || ctx->nranks <= 1) return SM_OK;
+    const size_t N = (size_t)ctx->W * ctx->H;
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->gmin[v], N * 8));
+        CHECK(ensure(ctx, ctx->cand[v], N * 4));
+        CHECK(ensure(ctx, ctx->gidx[v], N * 4));
+    }
+    // lexicographic (cost, global d) minimum: the reference's strict-< first-minimum rule
+    // (Stereo3DMST.cpp:177, PatchMatchStereoGPU.cu:1712) over contiguous ascending shards.
+    RCCLC(ncclGroupStart());
+    for (int v = 0; v < 2; ++v)
+        RCCLC(ncclAllReduce(ctx->minc[v].p, ctx->gmin[v].p, N, ncclFloat64, ncclMin, ctx->comm, ctx->st));
+    RCCLC(ncclGroupEnd());
+    for (int v = 0; v < 2; ++v)
+        HIPC(launch_cand(ctx->st, P<double>(ctx->minc[v]), P<double>(ctx->gmin[v]), P<int32_t>(ctx->idx[v]),
+                         P<int32_t>(ctx->cand[v]), N));
+    RCCLC(ncclGroupStart());
+    for (int v = 0; v < 2; ++v)
+        RCCLC(ncclAllReduce(ctx->cand[v].p, ctx->gidx[v].p, N, ncclInt32, ncclMin, ctx->comm, ctx->st));
+    RCCLC(ncclGroupEnd());
+    for (int v = 0; v < 2; ++v)
+        HIPC(launch_finalize(ctx->st, P<double>(ctx->gmin[v]), P<int32_t>(ctx->gidx[v]), P<double>(ctx->minc[v]),
+                             P<int32_t>(ctx->idx[v]), P<float>(ctx->disp[v]), N));
+    return SM_OK;
+}
+
+sm_status upload(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride) {
+    if (!l || !r) return fail(ctx, SM_ERR_ARG, "null image");
+    if (W < 1 || H < 1 || stride < 3 * W) return fail(ctx, SM_ERR_ARG, "bad image geometry");
+    if ((long long)W * H > (1ll << 30)) return fail(ctx, SM_ERR_ARG, "image too large");
+    ctx->W = W;
+    ctx->H = H;
+    ctx->stride = stride;
+    const size_t bytes = (size_t)H * stride;
+    for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->img[v], bytes));
+    HIPC(hipMemcpyAsync(ctx->img[0].p, l, bytes, hipMemcpyHostToDevice, ctx->st));
+    HIPC(hipMemcpyAsync(ctx->img[1].p, r, bytes, hipMemcpyHostToDevice, ctx->st));
+    return SM_OK;
+}
+
+double now_ms() {
+    struct timeval t;
+    gettimeofday(&t, nullptr);
+    return t.tv_sec * 1000.0 + t.tv_usec / 1000.0;
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+extern "C" {
+
+const char* sm_version(void) { return "stereomst-mi355x 0.1 (gfx950)"; }
+
+void sm_default_params(sm_params* p) {
+    if (!p) return;
+    p->gamma = 1.0f / 12.f;        // Stereo3DMST.cpp:830
+    p->c = INFINITY;               // MST mode (north star); reference segment mode uses 5000 (:831)
+    p->min_size = 200;             // :832
+    p->median_ksize = 3;           // :214
+    p->cost_kind = SM_COST_AGD;
+    p->disp_begin = 0;
+    p->disp_total = 0;
+}
+
+sm_status sm_device_count(int* count) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    if (count) *count = n;
+    return n > 0 ? SM_OK : SM_ERR_NODEVICE;
+}
+
+sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
+    if (!out) return SM_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return SM_ERR_NODEVICE;
+    sm_ctx* ctx = new sm_ctx();
+    ctx->device = cfg ? cfg->device : 0;
+    if (ctx->device < 0 || ctx->device >= n) { delete ctx; return SM_ERR_ARG; }
+    if (hipSetDevice(ctx->device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return SM_ERR_HIP;
+    }
+    if (hipHostMalloc((void**)&ctx->h_changed, sizeof(int)) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
+    for (auto& e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
+    // tables: S/S2 (correctly rounded, tools/gen_tables.py) and the AGD colour term
+    std::vector<float> atab(SM_MAX_W + 1);
+    for (int i = 0; i <= SM_MAX_W; ++i) atab[i] = agd_color_term(i);
+    if (ensure(ctx, ctx->atab, atab.size() * 4) != SM_OK || ensure(ctx, ctx->slut, 766 * 8) != SM_OK ||
+        ensure(ctx, ctx->s2lut, 766 * 8) != SM_OK ||
+        hipMemcpy(ctx->atab.p, atab.data(), atab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->slut.p, SM_S_LUT, 766 * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->s2lut.p, SM_S2_LUT, 766 * 8, hipMemcpyHostToDevice) != hipSuccess) {
+        sm_destroy(ctx);
+        return SM_ERR_HIP;
+    }
+    *out = ctx;
+    return SM_OK;
+}
+
+void sm_destroy(sm_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->st) (void)hipStreamSynchronize(ctx->st);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    DevBuf* all[] = {&ctx->changed, &ctx->atab, &ctx->slut, &ctx->s2lut};
+    for (DevBuf* b : all) if (b->p) (void)hipFree(b->p);
+    for (int v = 0; v < 2; ++v) {
+        DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
+                         &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v],
+                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v]};
+        for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
+    }
+    for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    for (auto e : ctx->up_ev) (void)hipEventDestroy(e);
+    for (auto e : ctx->down_ev) (void)hipEventDestroy(e);
+    if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
+    if (ctx->st) (void)hipStreamDestroy(ctx->st);
+    delete ctx;
+}
+
+const char* sm_last_error(const sm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+sm_status sm_upload_images(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride) {
+    if (!ctx) return SM_ERR_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    return upload(ctx, l, r, W, H, stride);
+}
+
+sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
+    if (!ctx) return SM_ERR_ARG;
+    if (ctx->W == 0) return fail(ctx, SM_ERR_STATE, "no images uploaded");
+    CHECK(check_params(ctx, p, D));
+    HIPC(hipSetDevice(ctx->device));
+    HIPC(hipEventRecord(ctx->ev[0], ctx->st));
+    CHECK(stage_prep(ctx));
+    HIPC(hipEventRecord(ctx->ev[1], ctx->st));
+    CHECK(stage_mst(ctx, 2));
+    HIPC(hipEventRecord(ctx->ev[2], ctx->st));
+    CHECK(stage_layout(ctx, 2));
+    HIPC(hipEventRecord(ctx->ev[3], ctx->st));
+    CHECK(stage_filter(ctx, D, p->disp_begin, 2, false));
+    HIPC(hipEventRecord(ctx->ev[4], ctx->st));
+    CHECK(stage_reduce(ctx));
+    HIPC(hipEventRecord(ctx->ev[5], ctx->st));
+    return SM_OK;
+}
+
+sm_status sm_synchronize(sm_ctx* ctx) {
+    if (!ctx) return SM_ERR_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    HIPC(hipStreamSynchronize(ctx->st));
+    float t[5];
+    for (int i = 0; i < 5; ++i) HIPC(hipEventElapsedTime(&t[i], ctx->ev[i], ctx->ev[i + 1]));
+    ctx->stage_ms[0] = t[0];
+    ctx->stage_ms[1] = t[1];
+    ctx->stage_ms[2] = t[2];
+    float up = 0, down = 0;
+    for (int i = 0; i < ctx->n_up; ++i) {
+        float x;
+        HIPC(hipEventElapsedTime(&x, ctx->up_ev[2 * i], ctx->up_ev[2 * i + 1]));
+        up += x;
+    }
+    for (int i = 0; i < ctx->n_down; ++i) {
+        float x;
+        HIPC(hipEventElapsedTime(&x, ctx->down_ev[2 * i], ctx->down_ev[2 * i + 1]));
+        down += x;
+    }
+    ctx->stage_ms[3] = up;
+    ctx->stage_ms[4] = down;
+    ctx->stage_ms[5] = t[4];
+    float tot;
+    HIPC(hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[5]));
+    ctx->stage_ms[6] = tot;
+    ctx->stats.up_ms = up;
+    ctx->stats.down_ms = down;
+    return SM_OK;
+}
+
+sm_status sm_download_results(sm_ctx* ctx, float* ld, float* rd, int32_t* li, int32_t* ri, double* lm, double* rm) {
+    if (!ctx) return SM_ERR_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    const size_t N = (size_t)ctx->W * ctx->H;
+    void* outs[2][3] = {{ld, li, lm}, {rd, ri, rm}};
+    for (int v = 0; v < 2; ++v) {
+        if (outs[v][0]) HIPC(hipMemcpyAsync(outs[v][0], ctx->disp[v].p, N * 4, hipMemcpyDeviceToHost, ctx->st));
+        if (outs[v][1]) HIPC(hipMemcpyAsync(outs[v][1], ctx->idx[v].p, N * 4, hipMemcpyDeviceToHost, ctx->st));
+        if (outs[v][2]) HIPC(hipMemcpyAsync(outs[v][2], ctx->minc[v].p, N * 8, hipMemcpyDeviceToHost, ctx->st));
+    }
+    HIPC(hipStreamSynchronize(ctx->st));
+    return SM_OK;
+}
+
+sm_status sm_match(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, int D, const sm_params* p,
+                   float* ld, float* rd, int32_t* li, int32_t* ri, double* lm, double* rm) {
+    CHECK(sm_upload_images(ctx, l, r, W, H, stride));
+    CHECK(sm_match_async(ctx, D, p));
+    CHECK(sm_synchronize(ctx));
+    return sm_download_results(ctx, ld, rd, li, ri, lm, rm);
+}
+
+sm_status sm_cost_volume(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, int d0, int D,
+                         float* lvol, float* rvol) {
+    if (!ctx) return SM_ERR_ARG;
+    if (D < 1 || d0 < 0) return fail(ctx, SM_ERR_ARG, "bad disparity range");
+    HIPC(hipSetDevice(ctx->device));
+    CHECK(upload(ctx, l, r, W, H, stride));
+    CHECK(stage_prep(ctx));
+    const size_t bytes = (size_t)W * H * D * 4;
+    for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->vol[v], bytes));
+    HIPC(launch_cost_volume(ctx->st, P<uint32_t>(ctx->bgrx[0]), P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]),
+                            P<float>(ctx->gray[1]), P<float>(ctx->atab), W, H, d0, D, P<float>(ctx->vol[0]),
+                            P<float>(ctx->vol[1])));
+    if (lvol) HIPC(hipMemcpyAsync(lvol, ctx->vol[0].p, bytes, hipMemcpyDeviceToHost, ctx->st));
+    if (rvol) HIPC(hipMemcpyAsync(rvol, ctx->vol[1].p, bytes, hipMemcpyDeviceToHost, ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));
+    return SM_OK;
+}
+
+sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int stride, uint8_t* mask, int32_t* parent_pix,
+                        int32_t* subtree_size, int32_t* slot_of_pix) {
+    if (!ctx) return SM_ERR_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    CHECK(upload(ctx, bgr, bgr, W, H, stride));
+    CHECK(stage_prep(ctx));
+    CHECK(stage_mst(ctx, 1));
+    CHECK(stage_layout(ctx, 1));
+    const size_t N = (size_t)W * H;
+    if (mask) {
+        std::vector<uint8_t> mR(N), mD(N);
+        HIPC(hipMemcpy(mR.data(), ctx->mR[0].p, N, hipMemcpyDeviceToHost));
+        HIPC(hipMemcpy(mD.data(), ctx->mD[0].p, N, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < N; ++i) mask[i] = (uint8_t)((mR[i] ? 1 : 0) | (mD[i] ? 2 : 0));
+    }
+    const SmLayout& L = ctx->layout[0];
+    for (size_t i = 0; i < N; ++i) {
+        if (parent_pix) parent_pix[i] = L.parent_pix[i] == SM_NONE ? -1 : (int32_t)L.parent_pix[i];
+        if (subtree_size) subtree_size[i] = (int32_t)L.subtree_size[i];
+        if (slot_of_pix) slot_of_pix[i] = (int32_t)L.slot_of_pix[i];
+    }
+    return SM_OK;
+}
+
+sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, int view, int d0,
+                             int D, double* A_up, double* A) {
+    if (!ctx) return SM_ERR_ARG;
+    if (view != 0 && view != 1) return fail(ctx, SM_ERR_ARG, "view must be 0 or 1");
+    if (D < 1 || D > 256 || d0 < 0) return fail(ctx, SM_ERR_ARG, "bad disparity range");
+    HIPC(hipSetDevice(ctx->device));
+    CHECK(upload(ctx, l, r, W, H, stride));
+    CHECK(stage_prep(ctx));
+    CHECK(stage_mst(ctx, 2));
+    CHECK(stage_layout(ctx, 2));
+    const size_t N = (size_t)W * H;
+    const int Dpad = 64 * spl_for(D);
+    CHECK(ensure(ctx, ctx->vol[0], N * (size_t)D * 8));
+    // up pass only, snapshot A_up
+    {
+        for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
+        WalkArgs a = walk_args(ctx, Dpad, D, d0);
+        uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
+        for (uint32_t i = 0; i < nr; ++i) {
+            set_round(ctx, a, nr - 1 - i, 2);
+            HIPC(launch_up(ctx->st, a, spl_for(D)));
+        }
+        HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
+                                   P<double>(ctx->vol[0])));
+        if (A_up) HIPC(hipMemcpyAsync(A_up, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipStreamSynchronize(ctx->st));
+    }
+    CHECK(stage_filter(ctx, D, d0, 2, true));
+    HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
+                               P<double>(ctx->vol[0])));
+    if (A) HIPC(hipMemcpyAsync(A, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));
+    return SM_OK;
+}
+
+int sm_stage_times(sm_ctx* ctx, float* out, int n) {
+    if (!ctx || !out) return 0;
+    int k = n < 7 ? n : 7;
+    for (int i = 0; i < k; ++i) out[i] = ctx->stage_ms[i];
+    return k;
+}
+
+sm_status sm_get_filter_stats(sm_ctx* ctx, sm_filter_stats* out) {
+    if (!ctx || !out) return SM_ERR_ARG;
+    *out = ctx->stats;
+    return SM_OK;
+}
+
+sm_status sm_comm_unique_id(uint8_t out[SM_UNIQUE_ID_BYTES]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SM_ERR_RCCL;
+    static_assert(sizeof(id) <= SM_UNIQUE_ID_BYTES, "unique id size");
+    memcpy(out, &id, sizeof(id));
+    return SM_OK;
+}
+
+sm_status sm_comm_init(sm_ctx* ctx, int nranks, int rank, const uint8_t id[SM_UNIQUE_ID_BYTES]) {
+    if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return SM_ERR_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    if (ctx->comm) RCCLC(ncclCommDestroy(ctx->comm));
+    ctx->comm = nullptr;
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    RCCLC(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return SM_OK;
+}
+
+sm_status sm_comm_destroy(sm_ctx* ctx) {
+    if (!ctx) return SM_ERR_ARG;
+    if (ctx->comm) RCCLC(ncclCommDestroy(ctx->comm));
+    ctx->comm = nullptr;
+    ctx->nranks = 1;
+    ctx->rank = 0;
+    return SM_OK;
+}
+
+void sm_start_timer(double* t0) {
+    if (t0) *t0 = now_ms();
+}
+
+double sm_get_timer_ms(const double* t0) { return t0 ? now_ms() - *t0 : 0.0; }
+
+}  // extern "C"

@@ -1,0 +1,720 @@
+// sm_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the Stereo3DMST path.
+//
+// Compiled with -ffp-contract=off: every fused multiply-add below is an explicit
+// __builtin_fma, mirroring exactly the ones the shipped reference binary performs
+// (DESIGN.md "Shipped arithmetic"); all other float/double ops round individually.
+//
+// Kernels (v = view: 0 left, 1 right; both views run in one launch via blockIdx.z):
+//   k_prep          packed BGR u8 -> bgrx u32 + gray f32 planes             (prep)
+//   k_median        3x3 median per channel, replicate border               (Stereo3DMST.cpp:226-228)
+//   k_weights       L1-RGB edge weights of the median image                 (:83-94, :242-262)
+//   k_cost_volume   AGD cost volume [d][y][x] from LDS-staged row tiles      (PatchMatchStereoGPU.cu:1482-1550)
+//   k_bor_*         Boruvka MST in (w,a,b) order: LDS tile phase + global    (segment-graph.h:54-89, c=+inf)
+//   k_up_walk       leaf->root pass, one wave per heavy path, AGD cost fused (Stereo3DMST.cpp:120-138)
+//   k_down_walk     root->leaf pass + strict-< WTA, one wave per heavy path  (:141-158, :160-186)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_common.h"
+
+#define WAVE 64
+
+// ---------------------------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float sm_gray(uint32_t bgrx) {
+    // 0.114f*B + 0.587f*G + 0.299f*R, left to right, no contraction (PatchMatchStereoGPU.cu:1529)
+    const float b = (float)(bgrx & 255u), g = (float)((bgrx >> 8) & 255u), r = (float)((bgrx >> 16) & 255u);
+    float t = 0.114f * b;
+    t = t + 0.587f * g;
+    t = t + 0.299f * r;
+    return t;
+}
+
+// AGD cost of right pixel x at disparity d: r0=right(x) r1=right(x+1) l0=left(x+d) l1=left(x+d+1)
+// (PatchMatchStereoGPU.cu:1518-1543).  color_l1 is an exact integer -> SAD + table.
+__device__ __forceinline__ float sm_agd(uint32_t r0, uint32_t l0, float gr0, float gr1, float gl0, float gl1,
+                                        const float* __restrict__ atab) {
+    const uint32_t l1 = __builtin_amdgcn_sad_u8(r0, l0, 0u);
+    const float a = atab[l1];
+    float g = gl0 - gr0;
+    g = g + (gr1 - gl1);
+    const float b = 0.89f * fminf(fabsf(g), 2.0f);
+    return a + b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// prep / median / weights
+// ---------------------------------------------------------------------------------------------
+struct ImgPair {
+    const uint8_t* src[2];  // packed BGR rows (device)
+    uint32_t* bgrx[2];      // W*H
+    float* gray[2];         // W*H
+};
+
+__global__ void k_prep(ImgPair P, int W, int H, int stride) {
+    const int v = blockIdx.z;
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint8_t* s = P.src[v] + (size_t)y * stride + 3 * (size_t)x;
+    const uint32_t w = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
+    const size_t p = (size_t)y * W + x;
+    P.bgrx[v][p] = w;
+    P.gray[v][p] = sm_gray(w);
+}
+
+__device__ __forceinline__ void cswap(int& a, int& b) {
+    const int lo = min(a, b), hi = max(a, b);
+    a = lo;
+    b = hi;
+}
+
+__device__ __forceinline__ int median9(int p0, int p1, int p2, int p3, int p4, int p5, int p6, int p7, int p8) {
+    // 19-exchange median network (same network as OpenCV's medianBlur_SortNet m=3).
+    cswap(p1, p2); cswap(p4, p5); cswap(p7, p8); cswap(p0, p1);
+    cswap(p3, p4); cswap(p6, p7); cswap(p1, p2); cswap(p4, p5);
+    cswap(p7, p8); cswap(p0, p3); cswap(p5, p8); cswap(p4, p7);
+    cswap(p3, p6); cswap(p1, p4); cswap(p2, p5); cswap(p4, p7);
+    cswap(p4, p2); cswap(p6, p4); cswap(p4, p2);
+    return p4;
+}
+
+struct MedPair {
+    const uint32_t* bgrx[2];
+    uint32_t* med[2];
+};
+
+__global__ void k_median(MedPair P, int W, int H) {
+    const int v = blockIdx.z;
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t* img = P.bgrx[v];
+    const int ys[3] = {y > 0 ? y - 1 : 0, y, y < H - 1 ? y + 1 : H - 1};
+    const int xs[3] = {x > 0 ? x - 1 : 0, x, x < W - 1 ? x + 1 : W - 1};
+    uint32_t q[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) q[3 * i + j] = img[(size_t)ys[i] * W + xs[j]];
+    uint32_t out = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int sh = 8 * c;
+        const int m = median9((q[0] >> sh) & 255, (q[1] >> sh) & 255, (q[2] >> sh) & 255, (q[3] >> sh) & 255,
+                              (q[4] >> sh) & 255, (q[5] >> sh) & 255, (q[6] >> sh) & 255, (q[7] >> sh) & 255,
+                              (q[8] >> sh) & 255);
+        out |= (uint32_t)m << sh;
+    }
+    P.med[v][(size_t)y * W + x] = out;
+}
+
+struct WeightPair {
+    const uint32_t* med[2];
+    uint16_t* wR[2];
+    uint16_t* wD[2];
+};
+
+__global__ void k_weights(WeightPair P, int W, int H) {
+    const int v = blockIdx.z;
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const size_t p = (size_t)y * W + x;
+    const uint32_t a = P.med[v][p];
+    P.wR[v][p] = x < W - 1 ? (uint16_t)__builtin_amdgcn_sad_u8(a, P.med[v][p + 1], 0u) : (uint16_t)SM_WEIGHT_NONE;
+    P.wD[v][p] = y < H - 1 ? (uint16_t)__builtin_amdgcn_sad_u8(a, P.med[v][p + W], 0u) : (uint16_t)SM_WEIGHT_NONE;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1: AGD cost volume, [d][y][x], both volumes (the sm_cost_volume entry / MC-CNN-shaped path)
+// block = 256 threads = one row segment of 256 pixels; grid = (ceil(W/256), H, ceil(D/DC)).
+// LDS holds the right row segment [x0-DC-d0', x0+256] and the left row segment
+// [x0+dc, x0+256+dc+DC] so every (x, d) pair is served from LDS; stores are coalesced rows.
+// ---------------------------------------------------------------------------------------------
+#define CV_TX 256
+#define CV_DC 64
+
+__global__ __launch_bounds__(CV_TX) void k_cost_volume(const uint32_t* __restrict__ Lb, const float* __restrict__ Lg,
+                                                       const uint32_t* __restrict__ Rb, const float* __restrict__ Rg,
+                                                       const float* __restrict__ atab_g, int W, int H, int d0, int D,
+                                                       float* __restrict__ lvol, float* __restrict__ rvol) {
+    __shared__ float atab[SM_MAX_W + 1];
+    __shared__ uint32_t sRb[CV_TX + 2 * CV_DC + 2];
+    __shared__ float sRg[CV_TX + 2 * CV_DC + 2];
+    __shared__ uint32_t sLb[CV_TX + 2 * CV_DC + 2];
+    __shared__ float sLg[CV_TX + 2 * CV_DC + 2];
+    for (int i = threadIdx.x; i <= SM_MAX_W; i += CV_TX) atab[i] = atab_g[i];
+    const int x0 = blockIdx.x * CV_TX;
+    const int y = blockIdx.y;
+    const int dc = d0 + blockIdx.z * CV_DC;               // first global disparity of this block
+    const int nd = min(CV_DC, d0 + D - dc);
+    const size_t row = (size_t)y * W;
+    // right segment for the left volume: xr in [x0 - (dc+nd-1), x0 + 256]   (+1 for the gradient)
+    const int rbeg = x0 - (dc + nd - 1);
+    const int rlen = CV_TX + nd + 1;
+    for (int i = threadIdx.x; i < rlen; i += CV_TX) {
+        const int xr = rbeg + i;
+        const bool ok = xr >= 0 && xr < W;
+        sRb[i] = ok ? Rb[row + xr] : 0u;
+        sRg[i] = ok ? Rg[row + xr] : 0.f;
+    }
+    // left segment for the right volume: xl in [x0 + dc, x0 + 256 + dc + nd]
+    const int lbeg = x0 + dc;
+    const int llen = CV_TX + nd + 1;
+    for (int i = threadIdx.x; i < llen; i += CV_TX) {
+        const int xl = lbeg + i;
+        const bool ok = xl >= 0 && xl < W;
+        sLb[i] = ok ? Lb[row + xl] : 0u;
+        sLg[i] = ok ? Lg[row + xl] : 0.f;
+    }
+    __syncthreads();
+    const int x = x0 + threadIdx.x;
+    if (x >= W) return;
+    // own pixels of both images (x is a right pixel for rvol and a left pixel for lvol)
+    const uint32_t Rx = Rb[row + x];
+    const float gRx = Rg[row + x], gRx1 = x + 1 < W ? Rg[row + x + 1] : 0.f;
+    const uint32_t Lx = Lb[row + x];
+    const float gLx = Lg[row + x], gLx1 = x + 1 < W ? Lg[row + x + 1] : 0.f;
+    const size_t N = (size_t)W * H;
+    for (int k = 0; k < nd; ++k) {
+        const int d = dc + k;
+        const size_t o = (size_t)(d - d0) * N + row + x;
+        // right reference: right(x) vs left(x+d)
+        float cr = 3.0f;
+        if (x + d + 1 < W) {
+            const int li = threadIdx.x + k;  // (x+d) - lbeg
+            cr = sm_agd(Rx, sLb[li], gRx, gRx1, sLg[li], sLg[li + 1], atab);
+        }
+        rvol[o] = cr;
+        // left pixel x: cost(x - d, d); invalid (x<d) and the column W-1 the reference never writes -> 3.0
+        float cl = 3.0f;
+        if (x - d >= 0 && x + 1 < W) {
+            const int ri = threadIdx.x + (nd - 1 - k);  // (x-d) - rbeg
+            cl = sm_agd(sRb[ri], Lx, sRg[ri], sRg[ri + 1], gLx, gLx1, atab);
+        }
+        lvol[o] = cl;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Boruvka MST (MST mode of segment_graph: every edge whose endpoints are in different trees is
+// taken in (w,a,b) order -> the unique MST under that total order).  A component's minimum
+// incident edge (by the 64-bit key) is always an MST edge (cut property), so:
+//   k_bor_local : per 32x32 tile, in LDS, hook components through their minimum edge while that
+//                 edge is inside the tile; a component whose minimum edge leaves the tile freezes.
+//   k_bor_min / k_bor_hook / k_bor_root / k_bor_relabel : global rounds on the remaining labels.
+// Mask output: mR[p]=1 <=> edge (p,p+1) in MST, mD[p]=1 <=> edge (p,p+W) in MST.
+// ---------------------------------------------------------------------------------------------
+#define BT 32                 // tile side
+#define BTN (BT * BT)         // 1024 pixels per tile
+#define BTHREADS 256
+
+struct MstView {
+    const uint16_t* wR;
+    const uint16_t* wD;
+    uint32_t* comp;           // component label (global pixel index of the representative)
+    unsigned long long* best; // per representative: min incident key
+    uint32_t* root;           // per representative: final root after hooking
+    uint8_t* mR;
+    uint8_t* mD;
+    int* changed;
+};
+struct MstPair {
+    MstView v[2];
+};
+
+__device__ __forceinline__ uint64_t key_of(const uint16_t* wR, const uint16_t* wD, int W, int p, int k) {
+    // k: 0 right, 1 down, 2 left, 3 up (caller guarantees existence)
+    switch (k) {
+        case 0: return sm_edge_key(wR[p], (uint32_t)p, 0u);
+        case 1: return sm_edge_key(wD[p], (uint32_t)p, 1u);
+        case 2: return sm_edge_key(wR[p - 1], (uint32_t)(p - 1), 0u);
+        default: return sm_edge_key(wD[p - W], (uint32_t)(p - W), 1u);
+    }
+}
+
+__global__ __launch_bounds__(BTHREADS) void k_bor_local(MstPair P, int W, int H) {
+    const MstView V = P.v[blockIdx.z];
+    __shared__ unsigned long long best[BTN];
+    __shared__ uint16_t comp[BTN];
+    __shared__ uint16_t hk[BTN];
+    __shared__ int flag;
+    const int tx0 = blockIdx.x * BT, ty0 = blockIdx.y * BT;
+    const int tw = min(BT, W - tx0), th = min(BT, H - ty0);
+    const int n = tw * th;
+    for (int i = threadIdx.x; i < BTN; i += BTHREADS) comp[i] = (uint16_t)i;
+    __syncthreads();
+    for (int iter = 0; iter < 64; ++iter) {
+        for (int i = threadIdx.x; i < BTN; i += BTHREADS) best[i] = SM_KEY_NONE;
+        if (threadIdx.x == 0) flag = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += BTHREADS) {
+            const int lx = i % tw, ly = i / tw;
+            const int x = tx0 + lx, y = ty0 + ly;
+            const int p = y * W + x;
+            const int c = comp[i];
+            unsigned long long mk = SM_KEY_NONE;
+            if (x + 1 < W) {
+                if (lx + 1 >= tw || comp[i + 1] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 0));
+            }
+            if (y + 1 < H) {
+                if (ly + 1 >= th || comp[i + tw] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 1));
+            }
+            if (x > 0) {
+                if (lx == 0 || comp[i - 1] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 2));
+            }
+            if (y > 0) {
+                if (ly == 0 || comp[i - tw] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 3));
+            }
+            if (mk != SM_KEY_NONE) atomicMin(&best[c], mk);
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < n; c += BTHREADS) {
+            hk[c] = (uint16_t)c;
+            if (comp[c] != c) continue;
+            const unsigned long long k = best[c];
+            if (k == SM_KEY_NONE) continue;
+            const uint32_t a = (uint32_t)(k >> 1) & 0xFFFFFFFFu;
+            const uint32_t vert = (uint32_t)(k & 1ull);
+            const uint32_t b = a + (vert ? (uint32_t)W : 1u);
+            const int ax = (int)(a % (uint32_t)W) - tx0, ay = (int)(a / (uint32_t)W) - ty0;
+            const int bx = (int)(b % (uint32_t)W) - tx0, by = (int)(b / (uint32_t)W) - ty0;
+            const bool ain = ax >= 0 && ax < tw && ay >= 0 && ay < th;
+            const bool bin = bx >= 0 && bx < tw && by >= 0 && by < th;
+            if (!ain || !bin) continue;  // minimum edge leaves the tile: frozen this phase
+            const int la = ay * tw + ax, lb = by * tw + bx;
+            const int ca = comp[la];
+            const int c2 = (ca == c) ? comp[lb] : ca;
+            if (best[c2] == k && c < c2) continue;  // mutual choice: the smaller label stays root
+            hk[c] = (uint16_t)c2;
+            if (vert) V.mD[a] = 1; else V.mR[a] = 1;
+            flag = 1;
+        }
+        __syncthreads();
+        if (flag == 0) break;
+        // pointer jumping to the roots of the hook forest
+        for (;;) {
+            __syncthreads();
+            int again = 0;
+            for (int c = threadIdx.x; c < n; c += BTHREADS) {
+                const int h = hk[c];
+                const int hh = hk[h];
+                if (hh != h) { hk[c] = (uint16_t)hh; again = 1; }
+            }
+            again = __syncthreads_or(again);
+            if (!again) break;
+        }
+        for (int i = threadIdx.x; i < n; i += BTHREADS) comp[i] = hk[comp[i]];
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < n; i += BTHREADS) {
+        const int lx = i % tw, ly = i / tw;
+        const int r = comp[i];
+        const uint32_t gr = (uint32_t)((ty0 + r / tw) * W + tx0 + r % tw);
+        V.comp[(size_t)(ty0 + ly) * W + tx0 + lx] = gr;
+    }
+}
+
+__global__ void k_bor_min(MstPair P, int W, int H) {
+    const MstView V = P.v[blockIdx.z];
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const int p = y * W + x;
+    const uint32_t c = V.comp[p];
+    unsigned long long mk = SM_KEY_NONE;
+    if (x + 1 < W && V.comp[p + 1] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 0));
+    if (y + 1 < H && V.comp[p + W] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 1));
+    if (x > 0 && V.comp[p - 1] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 2));
+    if (y > 0 && V.comp[p - W] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 3));
+    if (mk != SM_KEY_NONE) atomicMin(&V.best[c], mk);
+}
+
+__global__ void k_bor_hook(MstPair P, int W, int H) {
+    const MstView V = P.v[blockIdx.z];
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t c = (uint32_t)(y * W + x);
+    if (V.comp[c] != c) return;
+    uint32_t h = c;
+    const unsigned long long k = V.best[c];
+    if (k != SM_KEY_NONE) {
+        const uint32_t a = (uint32_t)(k >> 1) & 0xFFFFFFFFu;
+        const uint32_t vert = (uint32_t)(k & 1ull);
+        const uint32_t b = a + (vert ? (uint32_t)W : 1u);
+        const uint32_t ca = V.comp[a];
+        const uint32_t c2 = (ca == c) ? V.comp[b] : ca;
+        if (!(V.best[c2] == k && c < c2)) {
+            h = c2;
+            if (vert) V.mD[a] = 1; else V.mR[a] = 1;
+            *V.changed = 1;
+        }
+    }
+    V.root[c] = h;
+}
+
+__global__ void k_bor_root(MstPair P, int W, int H) {
+    // chase hook pointers to the root of each hook tree (hooks only point between old roots)
+    const MstView V = P.v[blockIdx.z];
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t c = (uint32_t)(y * W + x);
+    if (V.comp[c] != c) return;
+    uint32_t r = V.root[c];
+    for (int it = 0; it < (1 << 26); ++it) {
+        const uint32_t rr = V.root[r];
+        if (rr == r) break;
+        r = rr;
+    }
+    V.best[c] = SM_KEY_NONE;  // reset for the next round
+    V.root[c] = r;            // in-place shortcut: concurrent chasers still reach the same root
+}
+
+__global__ void k_bor_relabel(MstPair P, int W, int H) {
+    const MstView V = P.v[blockIdx.z];
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const int p = y * W + x;
+    V.comp[p] = V.root[V.comp[p]];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Tree filter walkers.  Aggregation rows U[slot][Dpad] (fp64), lane l owns slices
+// [l*SPL, l*SPL+SPL) of this call.  One wave walks one heavy path; a 256-thread block runs
+// four independent paths.  Arithmetic per node is exactly the shipped reference's:
+//   up  : acc = 0; for children c in descending key order: acc = fma(S_c, A_up(c), acc);
+//         A_up(v) = acc + C(v)                                        (Stereo3DMST.cpp:125-137)
+//   down: A(v) = fma(S_v, A(parent), S2_v * A_up(v)); A(root) = A_up(root)   (:145-157)
+// so the result is independent of the schedule (paths, rounds, waves).
+// ---------------------------------------------------------------------------------------------
+struct WalkView {
+    const SmMeta* meta;
+    const SmPath* paths;   // paths of this round
+    int npaths;
+    double* U;             // [slots][Dpad]
+    int32_t* idx;          // W*H   (down pass)
+    double* minc;          // W*H   (down pass)
+    float* disp;           // W*H   (down pass)
+};
+
+struct CostImgs {
+    const uint32_t* Lb;
+    const float* Lg;
+    const uint32_t* Rb;
+    const float* Rg;
+    const float* atab;     // 766 floats
+};
+
+template <int SPL>
+__device__ __forceinline__ void node_cost(int view, uint32_t pix, int W, int dbase, int dend, const CostImgs& I,
+                                          const float* __restrict__ atab, double (&c)[SPL]) {
+    const int y = (int)(pix / (uint32_t)W);
+    const int x = (int)(pix - (uint32_t)y * (uint32_t)W);
+    const size_t row = (size_t)y * W;
+    if (view == 1) {
+        // right view: right(x) vs left(x+d)
+        const uint32_t r0 = I.Rb[row + x];
+        const float gr0 = I.Rg[row + x];
+        const float gr1 = x + 1 < W ? I.Rg[row + x + 1] : 0.f;
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) {
+            const int d = dbase + k;
+            float v = 3.0f;
+            if (d < dend && x + d + 1 < W) {
+                const size_t q = row + x + d;
+                v = sm_agd(r0, I.Lb[q], gr0, gr1, I.Lg[q], I.Lg[q + 1], atab);
+            }
+            c[k] = (double)v;
+        }
+    } else {
+        // left view: left pixel x at d is cost(x-d, d); x-d<0 and column W-1 -> 3.0
+        const uint32_t l0 = I.Lb[row + x];
+        const float gl0 = I.Lg[row + x];
+        const float gl1 = x + 1 < W ? I.Lg[row + x + 1] : 0.f;
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) {
+            const int d = dbase + k;
+            float v = 3.0f;
+            if (d < dend && x - d >= 0 && x + 1 < W) {
+                const size_t q = row + x - d;
+                v = sm_agd(I.Rb[q], l0, I.Rg[q], I.Rg[q + 1], gl0, gl1, atab);
+            }
+            c[k] = (double)v;
+        }
+    }
+}
+
+template <int SPL>
+__device__ __forceinline__ void load_row(const double* __restrict__ U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
+    const double* p = U + (size_t)slot * Dpad + lane * SPL;
+    if constexpr (SPL == 1) {
+        r[0] = p[0];
+    } else if constexpr (SPL == 2) {
+        const double2 t = *reinterpret_cast<const double2*>(p);
+        r[0] = t.x; r[1] = t.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < SPL; k += 2) {
+            const double2 t = *reinterpret_cast<const double2*>(p + k);
+            r[k] = t.x; r[k + 1] = t.y;
+        }
+    }
+}
+
+template <int SPL>
+__device__ __forceinline__ void store_row(double* __restrict__ U, uint32_t slot, int Dpad, int lane, const double (&r)[SPL]) {
+    double* p = U + (size_t)slot * Dpad + lane * SPL;
+    if constexpr (SPL == 1) {
+        p[0] = r[0];
+    } else {
+#pragma unroll
+        for (int k = 0; k < SPL; k += 2) *reinterpret_cast<double2*>(p + k) = make_double2(r[k], r[k + 1]);
+    }
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <int SPL>
+__global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, CostImgs I, const double* __restrict__ slut,
+                                                 int W, int Dpad, int dcall, int dtotal_off) {
+    __shared__ float atab[SM_MAX_W + 1];
+    for (int i = threadIdx.x; i <= SM_MAX_W; i += 256) atab[i] = I.atab[i];
+    __syncthreads();
+    const int view = blockIdx.y;
+    const WalkView& V = view ? V1 : V0;
+    const int lane = threadIdx.x & 63;
+    const int pi = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (pi >= V.npaths) return;
+    const SmPath path = V.paths[pi];
+    const uint32_t head = uniform(path.head), len = uniform(path.len);
+    const int dbase = dtotal_off + lane * SPL;         // global disparity of this lane's first slice
+    const int dend = dtotal_off + dcall;
+    double x[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) x[k] = 0.0;
+    for (uint32_t s = head + len; s-- > head;) {
+        const SmMeta m = V.meta[s];
+        const uint32_t nch = sm_meta_nch(m), hidx = sm_meta_hidx(m);
+        double acc[SPL];
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) acc[k] = 0.0;
+        for (uint32_t j = 0; j < nch; ++j) {
+            const double S = slut[sm_meta_cw(m, (int)j)];
+            double v[SPL];
+            if (j == hidx) {
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) v[k] = x[k];
+            } else {
+                load_row<SPL>(V.U, m.cslot[j], Dpad, lane, v);
+            }
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S, v[k], acc[k]);
+        }
+        double c[SPL];
+        node_cost<SPL>(view, m.pix, W, dbase, dend, I, atab, c);
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) x[k] = acc[k] + c[k];
+        store_row<SPL>(V.U, s, Dpad, lane, x);
+    }
+}
+
+template <int SPL>
+__device__ __forceinline__ void wta_store(const double (&x)[SPL], int lane, int dloc0, int dcall, int dglob0, uint32_t pix,
+                                          const WalkView& V) {
+    // strict-< first-minimum over this lane's slices, then over lanes (lowest lane wins ties)
+    double bv = __builtin_huge_val();
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        if (dloc0 + k < dcall && x[k] < bv) { bv = x[k]; bi = dloc0 + k; }
+    }
+    double g = bv;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) g = fmin(g, __shfl_xor(g, off));
+    const unsigned long long ball = __ballot(bv == g && bi != 0x7fffffff);
+    const int win = ball ? (int)__builtin_ctzll(ball) : 0;
+    const int gi = __shfl(bi, win);
+    if (lane == 0) {
+        const int d = ball ? gi : 0;
+        V.idx[pix] = dglob0 + d;
+        V.minc[pix] = g;
+        V.disp[pix] = (float)(dglob0 + d);
+    }
+}
+
+template <int SPL>
+__global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, const double* __restrict__ slut,
+                                                   const double* __restrict__ s2lut, int Dpad, int dcall, int dglob0,
+                                                   int store_all) {
+    const int view = blockIdx.y;
+    const WalkView& V = view ? V1 : V0;
+    const int lane = threadIdx.x & 63;
+    const int pi = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (pi >= V.npaths) return;
+    const SmPath path = V.paths[pi];
+    const uint32_t head = uniform(path.head), len = uniform(path.len);
+    const int dloc0 = lane * SPL;
+    double x[SPL];
+    {
+        const SmMeta m = V.meta[head];
+        double u[SPL];
+        load_row<SPL>(V.U, head, Dpad, lane, u);
+        if (m.parent == SM_NONE) {
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) x[k] = u[k];
+        } else {
+            double xp[SPL];
+            load_row<SPL>(V.U, m.parent, Dpad, lane, xp);
+            const uint32_t wp = sm_meta_wp(m);
+            const double S = slut[wp], S2 = s2lut[wp];
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) x[k] = __builtin_fma(S, xp[k], S2 * u[k]);
+            if (store_all || sm_meta_has_light(m)) store_row<SPL>(V.U, head, Dpad, lane, x);
+        }
+        wta_store<SPL>(x, lane, dloc0, dcall, dglob0, m.pix, V);
+    }
+    for (uint32_t s = head + 1; s < head + len; ++s) {
+        const SmMeta m = V.meta[s];
+        double u[SPL];
+        load_row<SPL>(V.U, s, Dpad, lane, u);
+        const uint32_t wp = sm_meta_wp(m);
+        const double S = slut[wp], S2 = s2lut[wp];
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) x[k] = __builtin_fma(S, x[k], S2 * u[k]);
+        if (store_all || sm_meta_has_light(m)) store_row<SPL>(V.U, s, Dpad, lane, x);
+        wta_store<SPL>(x, lane, dloc0, dcall, dglob0, m.pix, V);
+    }
+}
+
+// cross-rank WTA helpers: candidate index where this rank holds the global minimum
+__global__ void k_cand(const double* __restrict__ minc, const double* __restrict__ gmin, const int32_t* __restrict__ idx,
+                       int32_t* __restrict__ cand, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) cand[i] = minc[i] == gmin[i] ? idx[i] : 0x7fffffff;
+}
+
+__global__ void k_finalize(const double* __restrict__ gmin, const int32_t* __restrict__ gidx, double* __restrict__ minc,
+                           int32_t* __restrict__ idx, float* __restrict__ disp, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) {
+        minc[i] = gmin[i];
+        idx[i] = gidx[i];
+        disp[i] = (float)gidx[i];
+    }
+}
+
+// debug: scatter the fp64 rows of slices [0, D) back to [d][y][x]
+__global__ void k_rows_to_volume(const SmMeta* __restrict__ meta, const double* __restrict__ U, int nslots, int Dpad,
+                                 int D, size_t N, double* __restrict__ out) {
+    const int s = blockIdx.x;
+    if (s >= nslots) return;
+    const uint32_t pix = meta[s].pix;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) out[(size_t)d * N + pix] = U[(size_t)s * Dpad + d];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host-callable launchers (extern "C++" within the library)
+// ---------------------------------------------------------------------------------------------
+#include "sm_launch.h"
+
+hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
+                       float* lg, uint32_t* rb, float* rg) {
+    ImgPair P{{l, r}, {lb, rb}, {lg, rg}};
+    dim3 g((W + 255) / 256, H, 2);
+    hipLaunchKernelGGL(k_prep, g, dim3(256), 0, st, P, W, H, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_median_weights(hipStream_t st, const uint32_t* lb, const uint32_t* rb, uint32_t* lmed, uint32_t* rmed,
+                                 uint16_t* lwR, uint16_t* lwD, uint16_t* rwR, uint16_t* rwD, int W, int H) {
+    MedPair M{{lb, rb}, {lmed, rmed}};
+    dim3 g((W + 255) / 256, H, 2);
+    hipLaunchKernelGGL(k_median, g, dim3(256), 0, st, M, W, H);
+    WeightPair P{{lmed, rmed}, {lwR, rwR}, {lwD, rwD}};
+    hipLaunchKernelGGL(k_weights, g, dim3(256), 0, st, P, W, H);
+    return hipGetLastError();
+}
+
+hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* lg, const uint32_t* rb, const float* rg,
+                              const float* atab, int W, int H, int d0, int D, float* lvol, float* rvol) {
+    dim3 g((W + CV_TX - 1) / CV_TX, H, (D + CV_DC - 1) / CV_DC);
+    hipLaunchKernelGGL(k_cost_volume, g, dim3(CV_TX), 0, st, lb, lg, rb, rg, atab, W, H, d0, D, lvol, rvol);
+    return hipGetLastError();
+}
+
+hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H) {
+    MstPair P;
+    for (int v = 0; v < 2; ++v)
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.changed};
+    dim3 g((W + BT - 1) / BT, (H + BT - 1) / BT, a.nviews);
+    hipLaunchKernelGGL(k_bor_local, g, dim3(BTHREADS), 0, st, P, W, H);
+    return hipGetLastError();
+}
+
+hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H) {
+    MstPair P;
+    for (int v = 0; v < 2; ++v)
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.changed};
+    dim3 g((W + 255) / 256, H, a.nviews);
+    hipLaunchKernelGGL(k_bor_min, g, dim3(256), 0, st, P, W, H);
+    hipLaunchKernelGGL(k_bor_hook, g, dim3(256), 0, st, P, W, H);
+    hipLaunchKernelGGL(k_bor_root, g, dim3(256), 0, st, P, W, H);
+    hipLaunchKernelGGL(k_bor_relabel, g, dim3(256), 0, st, P, W, H);
+    return hipGetLastError();
+}
+
+static WalkView to_view(const WalkArgs& a, int v) {
+    return WalkView{a.meta[v], a.paths[v], a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v]};
+}
+
+hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl) {
+    const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
+    if (np == 0) return hipSuccess;
+    CostImgs I{a.Lb, a.Lg, a.Rb, a.Rg, a.atab};
+    dim3 g((np + 3) / 4, 2);
+    WalkView v0 = to_view(a, 0), v1 = to_view(a, 1);
+    switch (spl) {
+        case 1: hipLaunchKernelGGL(k_up_walk<1>, g, dim3(256), 0, st, v0, v1, I, a.slut, a.W, a.Dpad, a.dcall, a.dglob0); break;
+        case 2: hipLaunchKernelGGL(k_up_walk<2>, g, dim3(256), 0, st, v0, v1, I, a.slut, a.W, a.Dpad, a.dcall, a.dglob0); break;
+        default: hipLaunchKernelGGL(k_up_walk<4>, g, dim3(256), 0, st, v0, v1, I, a.slut, a.W, a.Dpad, a.dcall, a.dglob0); break;
+    }
+    return hipGetLastError();
+}
+
+static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, int store_all) {
+    const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
+    if (np == 0) return hipSuccess;
+    dim3 g((np + 3) / 4, 2);
+    WalkView v0 = to_view(a, 0), v1 = to_view(a, 1);
+    switch (spl) {
+        case 1: hipLaunchKernelGGL(k_down_walk<1>, g, dim3(256), 0, st, v0, v1, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all); break;
+        case 2: hipLaunchKernelGGL(k_down_walk<2>, g, dim3(256), 0, st, v0, v1, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all); break;
+        default: hipLaunchKernelGGL(k_down_walk<4>, g, dim3(256), 0, st, v0, v1, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl) { return launch_down_impl(st, a, spl, 0); }
+hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl) { return launch_down_impl(st, a, spl, 1); }
+
+hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N) {
+    hipLaunchKernelGGL(k_cand, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, minc, gmin, idx, cand, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gidx, double* minc, int32_t* idx, float* disp,
+                           size_t N) {
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, gmin, gidx, minc, idx, disp, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_to_volume(hipStream_t st, const SmMeta* meta, const double* U, int nslots, int Dpad, int D,
+                                 size_t N, double* out) {
+    hipLaunchKernelGGL(k_rows_to_volume, dim3(nslots), dim3(64), 0, st, meta, U, nslots, Dpad, D, N, out);
+    return hipGetLastError();
+}

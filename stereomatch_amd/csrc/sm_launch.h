@@ -1,0 +1,50 @@
+// sm_launch.h -- host-side launchers of the kernels in sm_kernels.hip (library-internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "sm_common.h"
+
+struct MstArgs {
+    int nviews;
+    const uint16_t* wR[2];
+    const uint16_t* wD[2];
+    uint32_t* comp[2];
+    unsigned long long* best[2];
+    uint32_t* root[2];
+    uint8_t* mR[2];
+    uint8_t* mD[2];
+    int* changed;
+};
+
+struct WalkArgs {
+    const SmMeta* meta[2];
+    const SmPath* paths[2];
+    int npaths[2];
+    double* U[2];
+    int32_t* idx[2];
+    double* minc[2];
+    float* disp[2];
+    const uint32_t* Lb;
+    const float* Lg;
+    const uint32_t* Rb;
+    const float* Rg;
+    const float* atab;
+    const double* slut;
+    const double* s2lut;
+    int W, Dpad, dcall, dglob0;
+};
+
+hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
+                       float* lg, uint32_t* rb, float* rg);
+hipError_t launch_median_weights(hipStream_t st, const uint32_t* lb, const uint32_t* rb, uint32_t* lmed, uint32_t* rmed,
+                                 uint16_t* lwR, uint16_t* lwD, uint16_t* rwR, uint16_t* rwD, int W, int H);
+hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* lg, const uint32_t* rb, const float* rg,
+                              const float* atab, int W, int H, int d0, int D, float* lvol, float* rvol);
+hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H);
+hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H);
+hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl);
+hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl);
+hipError_t launch_rows_to_volume(hipStream_t st, const SmMeta* meta, const double* U, int nslots, int Dpad, int D,
+                                 size_t N, double* out);

@@ -1,0 +1,38 @@
+"""Test configuration.  Markers: `gpu` = needs an MI355X (run with -m gpu on the GPU box)."""
+import glob
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); parity tests through the C-ABI")
+    # the oracle (test infrastructure) is a tiny C library: make sure it is built
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+
+
+def golden_cases():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load_case(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import stereomatch_amd as sm
+    if sm.device_count() < 1:
+        pytest.fail("GPU test selected but no HIP device is visible")
+    ctx = sm.Context(0)
+    yield ctx
+    ctx.close()
