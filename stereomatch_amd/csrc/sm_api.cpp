@@ -19,7 +19,7 @@
 #include "../../include/stereomst.h"
 #include "sm_common.h"
 #include "sm_launch.h"
-#include "sm_layout.h"
+#include "sm_layout_gpu.h"
 #include "sm_tables.inc"
 
 hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N);
@@ -44,8 +44,16 @@ struct sm_ctx {
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
     DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2];
+    // GPU layout buffers (sm_layout_gpu.hip)
+    DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
+    DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
+    DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
-    SmLayout layout[2];
+    uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
+    struct HostRounds {
+        uint32_t nrounds = 0, npaths = 0, n_has_light = 0;
+        std::vector<uint32_t> begin;
+    } layout[2];
     hipEvent_t ev[8] = {};
     std::vector<hipEvent_t> up_ev, down_ev;
     int n_up = 0, n_down = 0;
@@ -173,31 +181,102 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     return SM_OK;
 }
 
+// device-side rounds record: [0, SM_MAX_ROUNDS] round_begin, then count, cursor, nrounds, n_has_light
+constexpr size_t RREC = (SM_MAX_ROUNDS + 1) + SM_MAX_ROUNDS + SM_MAX_ROUNDS + 2;
+
 sm_status stage_layout(sm_ctx* ctx, int nviews) {
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H;
-    std::vector<uint8_t> mR[2], mD[2];
-    std::vector<uint16_t> wR[2], wD[2];
+    const uint32_t ntiles = (uint32_t)(((W + 31) / 32) * ((H + 31) / 32));
+    const uint32_t max_chains = ntiles * 129u + 1u;
+    const size_t nscan = (2 * N + 8191) / 8192 + 1;
+    LayoutPair LP{};
     for (int v = 0; v < nviews; ++v) {
-        mR[v].resize(N); mD[v].resize(N); wR[v].resize(N); wD[v].resize(N);
-        HIPC(hipMemcpyAsync(mR[v].data(), ctx->mR[v].p, N, hipMemcpyDeviceToHost, ctx->st));
-        HIPC(hipMemcpyAsync(mD[v].data(), ctx->mD[v].p, N, hipMemcpyDeviceToHost, ctx->st));
-        HIPC(hipMemcpyAsync(wR[v].data(), ctx->wR[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
-        HIPC(hipMemcpyAsync(wD[v].data(), ctx->wD[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
-    }
-    HIPC(hipStreamSynchronize(ctx->st));
-    std::thread th[2];
-    for (int v = 0; v < nviews; ++v)
-        th[v] = std::thread([&, v] { sm_build_layout(W, H, mR[v].data(), mD[v].data(), wR[v].data(), wD[v].data(), ctx->layout[v]); });
-    for (int v = 0; v < nviews; ++v) th[v].join();
-    for (int v = 0; v < nviews; ++v) {
-        const SmLayout& L = ctx->layout[v];
+        CHECK(ensure(ctx, ctx->adj[v], N));
+        CHECK(ensure(ctx, ctx->pdir[v], N));
+        CHECK(ensure(ctx, ctx->heavy[v], N));
+        CHECK(ensure(ctx, ctx->size[v], N * 4));
+        CHECK(ensure(ctx, ctx->off_in[v], N * 4));
+        CHECK(ensure(ctx, ctx->light_in[v], N));
+        CHECK(ensure(ctx, ctx->pre[v], N * 4));
+        CHECK(ensure(ctx, ctx->ld[v], N * 4));
+        CHECK(ensure(ctx, ctx->a_dist[v], 4 * N * 2));
+        CHECK(ensure(ctx, ctx->a_cid[v], 4 * N * 4));
+        CHECK(ensure(ctx, ctx->a_head[v], 4 * N * 4));
+        CHECK(ensure(ctx, ctx->arank[v], 4 * N * 4));
+        CHECK(ensure(ctx, ctx->ccount[v], 16));
+        CHECK(ensure(ctx, ctx->c_last[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->c_len[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->c_head[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->cn0[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->cn1[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->cw0[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->cw1[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->tour[v], 2 * N * 8 + 16));
+        CHECK(ensure(ctx, ctx->bsum[v], nscan * 8));
+        CHECK(ensure(ctx, ctx->bsum32[v], nscan * 4));
         CHECK(ensure(ctx, ctx->meta[v], N * sizeof(SmMeta)));
-        CHECK(ensure(ctx, ctx->paths[v], L.paths.size() * sizeof(SmPath) + 16));
-        HIPC(hipMemcpyAsync(ctx->meta[v].p, L.meta.data(), N * sizeof(SmMeta), hipMemcpyHostToDevice, ctx->st));
-        HIPC(hipMemcpyAsync(ctx->paths[v].p, L.paths.data(), L.paths.size() * sizeof(SmPath), hipMemcpyHostToDevice, ctx->st));
+        CHECK(ensure(ctx, ctx->headflag[v], N * 4));
+        CHECK(ensure(ctx, ctx->headpos[v], N * 4));
+        CHECK(ensure(ctx, ctx->paths[v], N * sizeof(SmPath)));
+        CHECK(ensure(ctx, ctx->rounds[v], RREC * 4));
+        HIPC(hipMemsetAsync(ctx->ccount[v].p, 0, 16, ctx->st));
+        HIPC(hipMemsetAsync(ctx->rounds[v].p, 0, RREC * 4, ctx->st));
+        LayoutView& L = LP.v[v];
+        L.mR = P<uint8_t>(ctx->mR[v]);
+        L.mD = P<uint8_t>(ctx->mD[v]);
+        L.wR = P<uint16_t>(ctx->wR[v]);
+        L.wD = P<uint16_t>(ctx->wD[v]);
+        L.adj = P<uint8_t>(ctx->adj[v]);
+        L.pdir = P<int8_t>(ctx->pdir[v]);
+        L.heavy = P<int8_t>(ctx->heavy[v]);
+        L.size = P<uint32_t>(ctx->size[v]);
+        L.off_in = P<uint32_t>(ctx->off_in[v]);
+        L.light_in = P<uint8_t>(ctx->light_in[v]);
+        L.pre = P<uint32_t>(ctx->pre[v]);
+        L.ld = P<uint32_t>(ctx->ld[v]);
+        L.a_dist = P<uint16_t>(ctx->a_dist[v]);
+        L.a_cid = P<uint32_t>(ctx->a_cid[v]);
+        L.a_head = P<uint32_t>(ctx->a_head[v]);
+        L.rank = P<uint32_t>(ctx->arank[v]);
+        L.nchains = P<uint32_t>(ctx->ccount[v]);
+        L.c_last = P<uint32_t>(ctx->c_last[v]);
+        L.c_len = P<uint32_t>(ctx->c_len[v]);
+        L.c_head = P<uint32_t>(ctx->c_head[v]);
+        L.n0 = P<uint32_t>(ctx->cn0[v]);
+        L.n1 = P<uint32_t>(ctx->cn1[v]);
+        L.w0 = P<uint32_t>(ctx->cw0[v]);
+        L.w1 = P<uint32_t>(ctx->cw1[v]);
+        L.tour = P<long long>(ctx->tour[v]);
+        L.bsum = P<long long>(ctx->bsum[v]);
+        L.bsum32 = P<uint32_t>(ctx->bsum32[v]);
+        L.meta = P<SmMeta>(ctx->meta[v]);
+        L.headflag = P<uint32_t>(ctx->headflag[v]);
+        L.headpos = P<uint32_t>(ctx->headpos[v]);
+        L.paths = P<SmPath>(ctx->paths[v]);
+        uint32_t* R = P<uint32_t>(ctx->rounds[v]);
+        L.round_begin = R;
+        L.round_count = R + SM_MAX_ROUNDS + 1;
+        L.round_cursor = R + 2 * SM_MAX_ROUNDS + 1;
+        L.nrounds = R + 3 * SM_MAX_ROUNDS + 1;
+        L.n_has_light = R + 3 * SM_MAX_ROUNDS + 2;
     }
-    HIPC(hipStreamSynchronize(ctx->st));  // host vectors above are pageable and about to be freed
+    if (nviews == 1) LP.v[1] = LP.v[0];
+    HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains));
+    // the host needs the per-round path counts to size the walker grids
+    for (int v = 0; v < nviews; ++v)
+        HIPC(hipMemcpyAsync(ctx->h_rounds + v * RREC, ctx->rounds[v].p, RREC * 4, hipMemcpyDeviceToHost, ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));
+    for (int v = 0; v < 2; ++v) {
+        auto& L = ctx->layout[v];
+        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); continue; }
+        const uint32_t* R = ctx->h_rounds + v * RREC;
+        L.nrounds = R[3 * SM_MAX_ROUNDS + 1];
+        L.n_has_light = R[3 * SM_MAX_ROUNDS + 2];
+        L.begin.assign(R, R + SM_MAX_ROUNDS + 1);
+        L.npaths = R[SM_MAX_ROUNDS];
+        if (L.nrounds == 0 || L.npaths == 0) return fail(ctx, SM_ERR_STATE, "layout produced no paths");
+    }
     return SM_OK;
 }
 
@@ -226,13 +305,13 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
 
 void set_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int nviews) {
     for (int v = 0; v < 2; ++v) {
-        const SmLayout& L = ctx->layout[v];
+        const auto& L = ctx->layout[v];
         if (v >= nviews || r >= L.nrounds) {
             a.paths[v] = P<SmPath>(ctx->paths[v]);
             a.npaths[v] = 0;
         } else {
-            a.paths[v] = P<SmPath>(ctx->paths[v]) + L.round_path_begin[r];
-            a.npaths[v] = (int)(L.round_path_begin[r + 1] - L.round_path_begin[r]);
+            a.paths[v] = P<SmPath>(ctx->paths[v]) + L.begin[r];
+            a.npaths[v] = (int)(L.begin[r + 1] - L.begin[r]);
         }
     }
 }
@@ -282,13 +361,12 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     // algorithmic bytes (see DESIGN.md "Roofline accounting")
     double upb = 0, downb = 0;
     for (int v = 0; v < nviews; ++v) {
-        const SmLayout& L = ctx->layout[v];
+        const auto& L = ctx->layout[v];
         const double row = 8.0 * D;
-        const double heads = (double)L.paths.size(), roots = (double)L.nroots;
-        double has_light = 0;
-        for (const SmMeta& m : L.meta) has_light += sm_meta_has_light(m);
-        upb += row * (double)N + row * (double)L.n_light + 32.0 * (double)N;
-        downb += row * (double)N + row * (heads - roots) + row * has_light + 32.0 * (double)N + 16.0 * (double)N;
+        const double heads = (double)L.npaths, roots = 1.0;   // MST mode: one tree
+        const double n_light = heads - roots;                  // every non-root head is a light child
+        upb += row * (double)N + row * n_light + 32.0 * (double)N;
+        downb += row * (double)N + row * n_light + row * (double)L.n_has_light + 32.0 * (double)N + 16.0 * (double)N;
     }
     ctx->stats.up_bytes = upb;
     ctx->stats.down_bytes = downb;
@@ -381,7 +459,11 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         delete ctx;
         return SM_ERR_HIP;
     }
-    if (hipHostMalloc((void**)&ctx->h_changed, sizeof(int)) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
+    if (hipHostMalloc((void**)&ctx->h_changed, sizeof(int)) != hipSuccess ||
+        hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC * sizeof(uint32_t)) != hipSuccess) {
+        delete ctx;
+        return SM_ERR_HIP;
+    }
     for (auto& e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
     // tables: S/S2 (correctly rounded, tools/gen_tables.py) and the AGD colour term
@@ -416,6 +498,15 @@ void sm_destroy(sm_ctx* ctx) {
     for (auto e : ctx->up_ev) (void)hipEventDestroy(e);
     for (auto e : ctx->down_ev) (void)hipEventDestroy(e);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
+    if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
+    for (int v = 0; v < 2; ++v) {
+        DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->off_in[v], &ctx->light_in[v],
+                         &ctx->pre[v], &ctx->ld[v], &ctx->a_dist[v], &ctx->a_cid[v], &ctx->a_head[v], &ctx->arank[v],
+                         &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cn0[v], &ctx->cn1[v],
+                         &ctx->cw0[v], &ctx->cw1[v], &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
+                         &ctx->headpos[v], &ctx->rounds[v]};
+        for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
+    }
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     delete ctx;
 }
@@ -533,11 +624,18 @@ sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int strid
         HIPC(hipMemcpy(mD.data(), ctx->mD[0].p, N, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < N; ++i) mask[i] = (uint8_t)((mR[i] ? 1 : 0) | (mD[i] ? 2 : 0));
     }
-    const SmLayout& L = ctx->layout[0];
+    std::vector<int8_t> pdir(N);
+    std::vector<uint32_t> size(N), pre(N);
+    HIPC(hipMemcpy(pdir.data(), ctx->pdir[0].p, N, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(size.data(), ctx->size[0].p, N * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(pre.data(), ctx->pre[0].p, N * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < N; ++i) {
-        if (parent_pix) parent_pix[i] = L.parent_pix[i] == SM_NONE ? -1 : (int32_t)L.parent_pix[i];
-        if (subtree_size) subtree_size[i] = (int32_t)L.subtree_size[i];
-        if (slot_of_pix) slot_of_pix[i] = (int32_t)L.slot_of_pix[i];
+        if (parent_pix) {
+            const int k = pdir[i];
+            parent_pix[i] = k < 0 ? -1 : (int32_t)(k == 0 ? i + 1 : k == 1 ? i + W : k == 2 ? i - 1 : i - W);
+        }
+        if (subtree_size) subtree_size[i] = (int32_t)size[i];
+        if (slot_of_pix) slot_of_pix[i] = (int32_t)pre[i];
     }
     return SM_OK;
 }
@@ -559,7 +657,7 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
     {
         for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
         WalkArgs a = walk_args(ctx, Dpad, D, d0);
-        uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
+        const uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
         for (uint32_t i = 0; i < nr; ++i) {
             set_round(ctx, a, nr - 1 - i, 2);
             HIPC(launch_up(ctx->st, a, spl_for(D)));

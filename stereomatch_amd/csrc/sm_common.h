@@ -32,7 +32,7 @@ __host__ __device__ static inline uint32_t sm_meta_nch(const SmMeta& m) { return
 __host__ __device__ static inline uint32_t sm_meta_hidx(const SmMeta& m) { return (m.hi >> 23) & 3u; }
 __host__ __device__ static inline uint32_t sm_meta_has_light(const SmMeta& m) { return (m.hi >> 25) & 1u; }
 
-static inline SmMeta sm_make_meta(uint32_t pix, uint32_t parent, uint32_t wp, const uint32_t cw[4], uint32_t nch,
+__host__ __device__ static inline SmMeta sm_make_meta(uint32_t pix, uint32_t parent, uint32_t wp, const uint32_t cw[4], uint32_t nch,
                                   uint32_t hidx, uint32_t has_light, const uint32_t cslot[4]) {
     SmMeta m;
     m.pix = pix;

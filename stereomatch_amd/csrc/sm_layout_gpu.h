@@ -1,0 +1,57 @@
+// sm_layout_gpu.h -- device buffers of the GPU tree layout (sm_layout_gpu.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_common.h"
+
+#define SM_MAX_ROUNDS 64
+
+struct LayoutView {
+    // inputs
+    const uint8_t* mR;
+    const uint8_t* mD;
+    const uint16_t* wR;
+    const uint16_t* wD;
+    // per pixel
+    uint8_t* adj;
+    int8_t* pdir;       // direction to the parent (-1: root)
+    int8_t* heavy;      // direction of the heavy child (-1: leaf)
+    uint32_t* size;     // subtree size
+    uint32_t* off_in;   // heavy-first preorder offset within the parent
+    uint8_t* light_in;  // 1 if a light child
+    uint32_t* pre;      // preorder = slot
+    uint32_t* ld;       // light depth
+    // per arc (4N)
+    uint16_t* a_dist;
+    uint32_t* a_cid;
+    uint32_t* a_head;
+    uint32_t* rank;
+    // per chain
+    uint32_t* nchains;  // device counter
+    uint32_t* c_last;
+    uint32_t* c_len;
+    uint32_t* c_head;
+    uint32_t *n0, *n1, *w0, *w1;
+    // tour (2N-2) + scan scratch
+    long long* tour;
+    long long* bsum;
+    uint32_t* bsum32;
+    // per slot
+    SmMeta* meta;
+    uint32_t* headflag;
+    uint32_t* headpos;
+    // paths
+    SmPath* paths;
+    uint32_t* round_count;   // SM_MAX_ROUNDS
+    uint32_t* round_cursor;  // SM_MAX_ROUNDS
+    uint32_t* round_begin;   // SM_MAX_ROUNDS + 1
+    uint32_t* nrounds;
+    uint32_t* n_has_light;   // nodes with at least one light child (roofline accounting)
+};
+
+struct LayoutPair {
+    LayoutView v[2];
+};
+
+hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains);

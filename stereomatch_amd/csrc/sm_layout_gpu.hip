@@ -1,0 +1,542 @@
+// sm_layout_gpu.hip -- tree layout on the GPU: rooting at pixel 0, subtree sizes, heavy-light
+// decomposition, heavy-first preorder slots, light depth, per-slot metadata and per-round
+// heavy-path lists, from the MST edge mask produced by Boruvka.
+//
+// Method: Euler tour of the MST (arc a = 4*p + k, k: 0 right, 1 down, 2 left, 3 up; the tour
+// leaves a pixel through the next MST direction after the one it arrived from), ranked by
+//   L1  k_tour_tile   : per 32x32 tile, LDS pointer jumping contracts every maximal run of the
+//                       tour inside the tile into one chain (distance-to-chain-end, chain id)
+//   L2  k_chain_*     : pointer jumping (Wyllie) over the ~1e5 chains in global memory
+//   L3  k_tour_rank   : arc rank = chain rank + offset in chain
+// then orientation (an arc is "down" iff it precedes its reverse), subtree size
+// (rank distance / 2), heavy child (max size, ties -> smallest direction), and a single int64
+// prefix sum over the tour of (light<<32 | preorder offset) that yields every node's heavy-first
+// preorder number and light depth at once.  Slot = preorder.  This reproduces the rooting and
+// child order of Stereo3DMST.cpp:450-522 (root = first pixel; children by edge key), which is all
+// the exact arithmetic depends on; the heavy-light choice only schedules the work.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_common.h"
+#include "sm_layout_gpu.h"
+
+#define TL 32                 // tile side
+#define TLP (TL * TL)         // pixels per tile
+#define TLS (4 * TLP)         // arc slots per tile
+#define TL_THREADS 256
+#define L_EXIT 0xFFFFu        // successor leaves the tile
+#define L_NIL 0xFFFEu         // end of the tour (cut before the start arc)
+
+__device__ __forceinline__ uint32_t nbr_of(uint32_t p, int k, int W) {
+    return k == 0 ? p + 1 : k == 1 ? p + (uint32_t)W : k == 2 ? p - 1 : p - (uint32_t)W;
+}
+
+// next MST direction of pixel q after direction j, cyclic (j itself if q is a leaf)
+__device__ __forceinline__ int next_dir(uint32_t adjq, int j) {
+#pragma unroll
+    for (int t = 1; t <= 4; ++t) {
+        const int k = (j + t) & 3;
+        if (adjq & (1u << k)) return k;
+    }
+    return j;
+}
+
+__device__ __forceinline__ uint64_t key_dir(const uint16_t* wR, const uint16_t* wD, int W, uint32_t p, int k) {
+    switch (k) {
+        case 0: return sm_edge_key(wR[p], p, 0u);
+        case 1: return sm_edge_key(wD[p], p, 1u);
+        case 2: return sm_edge_key(wR[p - 1], p - 1, 0u);
+        default: return sm_edge_key(wD[p - W], p - (uint32_t)W, 1u);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ void k_adj(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t p = (uint32_t)(y * W + x);
+    uint32_t a = 0;
+    if (V.mR[p]) a |= 1u;
+    if (V.mD[p]) a |= 2u;
+    if (x > 0 && V.mR[p - 1]) a |= 4u;
+    if (y > 0 && V.mD[p - W]) a |= 8u;
+    V.adj[p] = (uint8_t)a;
+}
+
+// the global tour start: first MST direction out of pixel 0 (direction order 0..3)
+__device__ __forceinline__ uint32_t start_arc(const uint8_t* adj) {
+    const uint32_t a0 = adj[0];
+    for (int k = 0; k < 4; ++k)
+        if (a0 & (1u << k)) return (uint32_t)k;
+    return SM_NONE;
+}
+
+__device__ __forceinline__ uint32_t succ_arc(const uint8_t* adj, int W, uint32_t a, uint32_t start) {
+    const uint32_t p = a >> 2;
+    const int k = (int)(a & 3u);
+    const uint32_t q = nbr_of(p, k, W);
+    const int k2 = next_dir(adj[q], (k + 2) & 3);
+    const uint32_t s = 4u * q + (uint32_t)k2;
+    return s == start ? SM_NONE : s;
+}
+
+// L1: contract the tour inside each 32x32 tile.
+__global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    __shared__ uint16_t nxt[TLS];
+    __shared__ uint16_t dist[TLS];
+    __shared__ uint16_t last[TLS];
+    __shared__ uint16_t headof[TLS];  // indexed by a chain's last slot -> its head slot
+    __shared__ uint8_t haspred[TLS];
+    const int tx0 = blockIdx.x * TL, ty0 = blockIdx.y * TL;
+    const uint32_t start = start_arc(V.adj);
+    constexpr int PER = TLS / TL_THREADS;  // 16 slots per thread
+    for (int i = 0; i < PER; ++i) haspred[threadIdx.x + i * TL_THREADS] = 0;
+    __syncthreads();
+    for (int i = 0; i < PER; ++i) {
+        const int s = threadIdx.x + i * TL_THREADS;
+        const int lp = s >> 2, k = s & 3;
+        const int lx = lp % TL, ly = lp / TL;
+        const int x = tx0 + lx, y = ty0 + ly;
+        uint16_t n = L_NIL, dd = 0;
+        if (x < W && y < H) {
+            const uint32_t p = (uint32_t)(y * W + x);
+            if (V.adj[p] & (1u << k)) {
+                dd = 1;
+                const uint32_t sa = succ_arc(V.adj, W, 4u * p + (uint32_t)k, start);
+                if (sa == SM_NONE) {
+                    n = L_NIL;
+                } else {
+                    const uint32_t q = sa >> 2;
+                    const int qx = (int)(q % (uint32_t)W) - tx0, qy = (int)(q / (uint32_t)W) - ty0;
+                    if (qx >= 0 && qx < TL && qy >= 0 && qy < TL) {
+                        n = (uint16_t)(4 * (qy * TL + qx) + (int)(sa & 3u));
+                        haspred[n] = 1;
+                    } else {
+                        n = L_EXIT;
+                    }
+                }
+            }
+        }
+        nxt[s] = n;
+        dist[s] = dd;
+        last[s] = (uint16_t)s;
+    }
+    __syncthreads();
+    // pointer jumping: dist -> arcs to chain end (inclusive), last -> chain's last slot
+    for (int it = 0; it < 13; ++it) {
+        uint16_t nn[PER], nd[PER], nl[PER];
+        bool any = false;
+        for (int i = 0; i < PER; ++i) {
+            const int s = threadIdx.x + i * TL_THREADS;
+            const uint16_t n = nxt[s];
+            nn[i] = n; nd[i] = dist[s]; nl[i] = last[s];
+            if (n < L_NIL) {
+                nd[i] = (uint16_t)(nd[i] + dist[n]);
+                nl[i] = last[n];
+                nn[i] = nxt[n];
+                any = true;
+            }
+        }
+        any = __syncthreads_or(any);
+        if (!any) break;
+        for (int i = 0; i < PER; ++i) {
+            const int s = threadIdx.x + i * TL_THREADS;
+            nxt[s] = nn[i]; dist[s] = nd[i]; last[s] = nl[i];
+        }
+        __syncthreads();
+    }
+    // heads: existing arcs without an in-tile predecessor; register chains
+    for (int i = 0; i < PER; ++i) {
+        const int s = threadIdx.x + i * TL_THREADS;
+        if (dist[s] != 0 && !haspred[s]) headof[last[s]] = (uint16_t)s;
+    }
+    __syncthreads();
+    for (int i = 0; i < PER; ++i) {
+        const int s = threadIdx.x + i * TL_THREADS;
+        if (dist[s] == 0) continue;
+        const int lp = s >> 2, k = s & 3;
+        const uint32_t p = (uint32_t)((ty0 + lp / TL) * W + tx0 + lp % TL);
+        const uint32_t a = 4u * p + (uint32_t)k;
+        V.a_dist[a] = dist[s];
+        if (!haspred[s]) {
+            const uint32_t cid = atomicAdd(V.nchains, 1u);
+            V.a_cid[a] = cid;        // head's chain id (read below by the chain's other arcs: next kernel)
+            const int ls = last[s];
+            const int llp = ls >> 2;
+            const uint32_t lpix = (uint32_t)((ty0 + llp / TL) * W + tx0 + llp % TL);
+            V.c_last[cid] = 4u * lpix + (uint32_t)(ls & 3);
+            V.c_len[cid] = dist[s];
+            V.c_head[cid] = a;
+        }
+        // every arc remembers its chain head (global arc id)
+        const int hs = headof[last[s]];
+        const int hlp = hs >> 2;
+        const uint32_t hpix = (uint32_t)((ty0 + hlp / TL) * W + tx0 + hlp % TL);
+        V.a_head[a] = 4u * hpix + (uint32_t)(hs & 3);
+    }
+}
+
+// L2 init: chain successor + weight (suffix-sum Wyllie state)
+__global__ void k_chain_init(LayoutPair LP, int W) {
+    const LayoutView& V = LP.v[blockIdx.y];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= *V.nchains) return;
+    const uint32_t start = start_arc(V.adj);
+    const uint32_t s = succ_arc(V.adj, W, V.c_last[c], start);
+    V.w0[c] = V.c_len[c];
+    V.n0[c] = s == SM_NONE ? SM_NONE : V.a_cid[s];
+}
+
+// L2 step: ping-pong pointer jumping
+__global__ void k_chain_jump(LayoutPair LP, int parity) {
+    const LayoutView& V = LP.v[blockIdx.y];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= *V.nchains) return;
+    const uint32_t* nin = parity ? V.n1 : V.n0;
+    const uint32_t* win = parity ? V.w1 : V.w0;
+    uint32_t* nout = parity ? V.n0 : V.n1;
+    uint32_t* wout = parity ? V.w0 : V.w1;
+    const uint32_t n = nin[c];
+    if (n == SM_NONE) {
+        nout[c] = n;
+        wout[c] = win[c];
+    } else {
+        nout[c] = nin[n];
+        wout[c] = win[c] + win[n];
+    }
+}
+
+// L3: arc ranks.  suffix(c) = arcs from chain c's head to the tour end; rank = total - suffix + offset
+__global__ void k_tour_rank(LayoutPair LP, int W, int H, int parity) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t p = (uint32_t)(y * W + x);
+    const uint32_t adj = V.adj[p];
+    const uint32_t* wfin = parity ? V.w1 : V.w0;
+    const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
+    for (int k = 0; k < 4; ++k) {
+        if (!(adj & (1u << k))) continue;
+        const uint32_t a = 4u * p + (uint32_t)k;
+        const uint32_t c = V.a_cid[V.a_head[a]];
+        const uint32_t chain_rank = total - wfin[c];
+        V.rank[a] = chain_rank + (V.c_len[c] - V.a_dist[a]);
+    }
+}
+
+// orientation + subtree size
+__global__ void k_orient(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t q = (uint32_t)(y * W + x);
+    const uint32_t adj = V.adj[q];
+    int8_t pd = -1;
+    uint32_t sz = (uint32_t)(W * H);
+    for (int k = 0; k < 4; ++k) {
+        if (!(adj & (1u << k))) continue;
+        const uint32_t p = nbr_of(q, k, W);
+        const uint32_t a_in = 4u * p + (uint32_t)((k + 2) & 3);  // p -> q
+        const uint32_t a_out = 4u * q + (uint32_t)k;             // q -> p
+        const uint32_t ri = V.rank[a_in], ro = V.rank[a_out];
+        if (ri < ro) {
+            pd = (int8_t)k;
+            sz = (ro - ri + 1u) / 2u;
+        }
+    }
+    V.pdir[q] = pd;
+    V.size[q] = sz;
+}
+
+// heavy child + per-child preorder offset and light flag (written by the parent into the child)
+__global__ void k_heavy(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t v = (uint32_t)(y * W + x);
+    const uint32_t adj = V.adj[v];
+    const int pd = V.pdir[v];
+    int heavy = -1;
+    uint32_t best = 0;
+    uint32_t csz[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 4; ++k) {
+        if (!(adj & (1u << k)) || k == pd) continue;
+        csz[k] = V.size[nbr_of(v, k, W)];
+        if (csz[k] > best) { best = csz[k]; heavy = k; }
+    }
+    V.heavy[v] = (int8_t)heavy;
+    uint32_t off = 1u + (heavy >= 0 ? csz[heavy] : 0u);
+    for (int k = 0; k < 4; ++k) {
+        if (!(adj & (1u << k)) || k == pd) continue;
+        const uint32_t c = nbr_of(v, k, W);
+        if (k == heavy) {
+            V.off_in[c] = 1u;
+            V.light_in[c] = 0;
+        } else {
+            V.off_in[c] = off;
+            V.light_in[c] = 1;
+            off += csz[k];
+        }
+    }
+    if (pd < 0) { V.off_in[v] = 0u; V.light_in[v] = 0; }
+}
+
+// tour values: down arc into c: +(light<<32 | off), up arc out of c: -(...)
+__global__ void k_tour_values(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t p = (uint32_t)(y * W + x);
+    const uint32_t adj = V.adj[p];
+    for (int k = 0; k < 4; ++k) {
+        if (!(adj & (1u << k))) continue;
+        const uint32_t q = nbr_of(p, k, W);
+        const uint32_t a = 4u * p + (uint32_t)k;
+        const bool down = V.pdir[q] == ((k + 2) & 3);
+        const uint32_t c = down ? q : p;
+        const long long val = ((long long)V.light_in[c] << 32) + (long long)V.off_in[c];
+        V.tour[V.rank[a]] = down ? val : -val;
+    }
+}
+
+// ---- generic inclusive scan, 3 phases (block sums, scan of block sums, block scan + carry)
+#define SCAN_BLOCK 1024
+#define SCAN_ITEMS 8   // items per thread -> 8192 per block
+
+struct OpAdd {
+    template <class T> __device__ static T apply(T a, T b) { return a + b; }
+    template <class T> __device__ static T ident() { return T(0); }
+};
+struct OpMax {
+    template <class T> __device__ static T apply(T a, T b) { return a > b ? a : b; }
+    template <class T> __device__ static T ident() { return T(0); }
+};
+
+template <class T, class Op>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* sh, T* total) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    T x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const T y = __shfl_up(x, off);
+        if (lane >= off) x = Op::apply(x, y);
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        T s2 = lane < (SCAN_BLOCK / 64) ? sh[lane] : Op::template ident<T>();
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const T y = __shfl_up(s2, off);
+            if (lane >= off) s2 = Op::apply(s2, y);
+        }
+        if (lane < (SCAN_BLOCK / 64)) sh[lane] = s2;
+    }
+    __syncthreads();
+    const T wpre = wid ? sh[wid - 1] : Op::template ident<T>();
+    if (total) *total = sh[SCAN_BLOCK / 64 - 1];
+    // exclusive: combine warp prefix with the lane's exclusive prefix
+    T lex = __shfl_up(x, 1);
+    if (lane == 0) lex = Op::template ident<T>();
+    const T r = Op::apply(wpre, lex);
+    __syncthreads();
+    return r;
+}
+
+template <class T>
+struct ScanBufs {
+    T* data[2];
+    T* bsum[2];
+};
+
+template <class T, class Op>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(ScanBufs<T> B, int nelem) {
+    __shared__ T sh[SCAN_BLOCK / 64];
+    const T* d = B.data[blockIdx.y];
+    const size_t base = (size_t)blockIdx.x * SCAN_BLOCK * SCAN_ITEMS;
+    T s = Op::template ident<T>();
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        const size_t j = base + (size_t)threadIdx.x * SCAN_ITEMS + i;
+        if (j < (size_t)nelem) s = Op::apply(s, d[j]);
+    }
+    T tot;
+    block_exclusive_scan<T, Op>(s, sh, &tot);
+    if (threadIdx.x == 0) B.bsum[blockIdx.y][blockIdx.x] = tot;
+}
+
+template <class T, class Op>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_bsums(ScanBufs<T> B, int nblocks) {
+    __shared__ T sh[SCAN_BLOCK / 64];
+    T* bs = B.bsum[blockIdx.y];
+    T carry = Op::template ident<T>();
+    for (int b0 = 0; b0 < nblocks; b0 += SCAN_BLOCK) {
+        const int b = b0 + threadIdx.x;
+        const T v = b < nblocks ? bs[b] : Op::template ident<T>();
+        T tot;
+        const T ex = block_exclusive_scan<T, Op>(v, sh, &tot);
+        if (b < nblocks) bs[b] = Op::apply(carry, ex);  // exclusive block offsets
+        carry = Op::apply(carry, tot);
+    }
+}
+
+template <class T, class Op>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(ScanBufs<T> B, int nelem) {
+    __shared__ T sh[SCAN_BLOCK / 64];
+    T* d = B.data[blockIdx.y];
+    const size_t base = (size_t)blockIdx.x * SCAN_BLOCK * SCAN_ITEMS;
+    T loc[SCAN_ITEMS];
+    T s = Op::template ident<T>();
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        const size_t j = base + (size_t)threadIdx.x * SCAN_ITEMS + i;
+        loc[i] = j < (size_t)nelem ? d[j] : Op::template ident<T>();
+        s = Op::apply(s, loc[i]);
+    }
+    T acc = Op::apply(B.bsum[blockIdx.y][blockIdx.x], block_exclusive_scan<T, Op>(s, sh, nullptr));
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        const size_t j = base + (size_t)threadIdx.x * SCAN_ITEMS + i;
+        acc = Op::apply(acc, loc[i]);
+        if (j < (size_t)nelem) d[j] = acc;  // inclusive
+    }
+}
+
+template <class T, class Op>
+static void launch_scan(hipStream_t st, const ScanBufs<T>& B, int nviews, int nelem) {
+    if (nelem <= 0) return;
+    const int nblocks = (nelem + SCAN_BLOCK * SCAN_ITEMS - 1) / (SCAN_BLOCK * SCAN_ITEMS);
+    hipLaunchKernelGGL((k_scan_sums<T, Op>), dim3(nblocks, nviews), dim3(SCAN_BLOCK), 0, st, B, nelem);
+    hipLaunchKernelGGL((k_scan_bsums<T, Op>), dim3(1, nviews), dim3(SCAN_BLOCK), 0, st, B, nblocks);
+    hipLaunchKernelGGL((k_scan_apply<T, Op>), dim3(nblocks, nviews), dim3(SCAN_BLOCK), 0, st, B, nelem);
+}
+
+// preorder + light depth per pixel from the scanned tour
+__global__ void k_assign(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t q = (uint32_t)(y * W + x);
+    const int pd = V.pdir[q];
+    uint32_t pre = 0, ld = 0;
+    if (pd >= 0) {
+        const uint32_t p = nbr_of(q, pd, W);
+        const uint32_t a_in = 4u * p + (uint32_t)((pd + 2) & 3);
+        const long long v = V.tour[V.rank[a_in]];
+        pre = (uint32_t)(v & 0xFFFFFFFFll);
+        ld = (uint32_t)(v >> 32);
+    }
+    V.pre[q] = pre;
+    V.ld[q] = ld;
+}
+
+// per-slot metadata (slot = preorder) + path heads
+__global__ void k_meta(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t v = (uint32_t)(y * W + x);
+    const uint32_t adj = V.adj[v];
+    const int pd = V.pdir[v];
+    const int hv = V.heavy[v];
+    uint64_t ck[4];
+    uint32_t cs[4] = {SM_NONE, SM_NONE, SM_NONE, SM_NONE}, cw[4] = {0, 0, 0, 0};
+    int cq[4];
+    int nch = 0;
+    for (int k = 0; k < 4; ++k) {
+        if (!(adj & (1u << k)) || k == pd) continue;
+        ck[nch] = key_dir(V.wR, V.wD, W, v, k);
+        cq[nch] = k;
+        ++nch;
+    }
+    for (int i = 1; i < nch; ++i)  // descending key
+        for (int j = i; j > 0 && ck[j] > ck[j - 1]; --j) {
+            const uint64_t tk = ck[j]; ck[j] = ck[j - 1]; ck[j - 1] = tk;
+            const int tq = cq[j]; cq[j] = cq[j - 1]; cq[j - 1] = tq;
+        }
+    uint32_t hidx = 0, has_light = 0;
+    for (int i = 0; i < nch; ++i) {
+        cw[i] = (uint32_t)(ck[i] >> 33);
+        cs[i] = V.pre[nbr_of(v, cq[i], W)];
+        if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
+    }
+    uint32_t wp = 0, parent = SM_NONE;
+    if (pd >= 0) {
+        wp = (uint32_t)(key_dir(V.wR, V.wD, W, v, pd) >> 33);
+        parent = V.pre[nbr_of(v, pd, W)];
+    }
+    const uint32_t slot = V.pre[v];
+    V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
+    if (has_light) atomicAdd(V.n_has_light, 1u);
+    const bool head = pd < 0 || V.light_in[v];
+    V.headflag[slot] = head ? 1u + V.ld[v] : 0u;  // 0 = not a head, else 1 + light depth
+}
+
+// heads in slot order -> path lengths -> bucketed by light depth (order inside a round is free).
+// headpos[s] = s+1 at heads (0 elsewhere); after an inclusive max-scan it is 1 + the slot of
+// the head of s's path (heavy paths are contiguous in preorder).
+__global__ void k_path_prep(LayoutPair LP, int N) {
+    const LayoutView& V = LP.v[blockIdx.y];
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= (uint32_t)N) return;
+    const uint32_t h = V.headflag[s];
+    V.headpos[s] = h ? s + 1u : 0u;
+    if (h) atomicAdd(&V.round_count[h - 1], 1u);
+}
+
+__global__ void k_path_offsets(LayoutPair LP) {
+    const LayoutView& V = LP.v[blockIdx.x];
+    if (threadIdx.x != 0) return;
+    uint32_t acc = 0, nr = 0;
+    for (int r = 0; r < SM_MAX_ROUNDS; ++r) {
+        V.round_begin[r] = acc;
+        V.round_cursor[r] = acc;
+        acc += V.round_count[r];
+        if (V.round_count[r]) nr = (uint32_t)r + 1;
+    }
+    V.round_begin[SM_MAX_ROUNDS] = acc;
+    *V.nrounds = nr;
+}
+
+__global__ void k_path_emit(LayoutPair LP, int N) {
+    const LayoutView& V = LP.v[blockIdx.y];
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= (uint32_t)N) return;
+    const bool is_last = s + 1 == (uint32_t)N || V.headflag[s + 1] != 0;
+    if (!is_last) return;
+    const uint32_t head = V.headpos[s] - 1u;
+    const uint32_t r = V.headflag[head] - 1u;
+    const uint32_t pos = atomicAdd(&V.round_cursor[r], 1u);
+    V.paths[pos] = SmPath{head, s - head + 1u};
+}
+
+// ------------------------------------------------------------------------------------------
+static dim3 pix_grid(int W, int H, int nv) { return dim3((W + 255) / 256, H, nv); }
+
+hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains) {
+    const int N = W * H;
+    const dim3 pg = pix_grid(W, H, nviews);
+    hipLaunchKernelGGL(k_adj, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_tour_tile, dim3((W + TL - 1) / TL, (H + TL - 1) / TL, nviews), dim3(TL_THREADS), 0, st, LP, W, H);
+    const dim3 cg((max_chains + 255) / 256, nviews);
+    hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
+    int parity = 0;
+    for (uint32_t span = 1; span < max_chains; span <<= 1) {
+        hipLaunchKernelGGL(k_chain_jump, cg, dim3(256), 0, st, LP, parity);
+        parity ^= 1;
+    }
+    hipLaunchKernelGGL(k_tour_rank, pg, dim3(256), 0, st, LP, W, H, parity);
+    hipLaunchKernelGGL(k_orient, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_heavy, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_tour_values, pg, dim3(256), 0, st, LP, W, H);
+    ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}, {LP.v[0].bsum, LP.v[1].bsum}};
+    launch_scan<long long, OpAdd>(st, tb, nviews, 2 * N - 2);
+    hipLaunchKernelGGL(k_assign, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_meta, pg, dim3(256), 0, st, LP, W, H);
+    const dim3 sg((N + 255) / 256, nviews);
+    hipLaunchKernelGGL(k_path_prep, sg, dim3(256), 0, st, LP, N);
+    ScanBufs<uint32_t> hb{{LP.v[0].headpos, LP.v[1].headpos}, {LP.v[0].bsum32, LP.v[1].bsum32}};
+    launch_scan<uint32_t, OpMax>(st, hb, nviews, N);
+    hipLaunchKernelGGL(k_path_offsets, dim3(nviews), dim3(64), 0, st, LP);
+    hipLaunchKernelGGL(k_path_emit, sg, dim3(256), 0, st, LP, N);
+    return hipGetLastError();
+}

@@ -164,3 +164,48 @@ def test_reference_surface(gpu_ctx):
     ref = O.match(left, right, 16)
     np.testing.assert_array_equal(ld.ravel(), ref["left"]["idx"].astype(np.float32))
     np.testing.assert_array_equal(rd.ravel(), ref["right"]["idx"].astype(np.float32))
+
+
+def expected_layout(W, H, node_pix, node_parent):
+    """Subtree sizes and heavy-first preorder (ties: smallest direction R,D,L,U) from the
+    oracle's BFS tree -- the schedule layout the GPU builds (DESIGN.md "Tree layout")."""
+    N = W * H
+    parent = np.full(N, -1, np.int64)
+    parent[node_pix[1:]] = node_pix[node_parent[1:]]
+    size = np.ones(N, np.int64)
+    for n in range(N - 1, 0, -1):
+        size[node_pix[node_parent[n]]] += size[node_pix[n]]
+    children = [[] for _ in range(N)]
+    for q in range(N):
+        p = parent[q]
+        if p >= 0:
+            d = q - p
+            k = 0 if d == 1 else 1 if d == W else 2 if d == -1 else 3
+            children[p].append((k, q))
+    pre = np.zeros(N, np.int64)
+    stack, cnt = [0], 0
+    while stack:
+        v = stack.pop()
+        pre[v] = cnt
+        cnt += 1
+        ch = sorted(children[v])
+        heavy = None
+        for k, q in ch:
+            if heavy is None or size[q] > size[heavy]:
+                heavy = q
+        lights = [q for k, q in ch if q != heavy]
+        for q in reversed(lights):
+            stack.append(q)
+        if heavy is not None:
+            stack.append(heavy)
+    return size, pre
+
+
+@pytest.mark.parametrize("name", ["rand_37x23", "smooth_97x61", "flir_crop_256x192", "const_16x12", "col_1x15"])
+def test_gpu_layout_matches_restated_schedule(gpu_ctx, name):
+    z = load_case(name)
+    H, W, _ = z["left"].shape
+    t = gpu_ctx.build_tree(z["left"])
+    size, pre = expected_layout(W, H, z["left_node_pix"], z["left_node_parent"])
+    np.testing.assert_array_equal(t["subtree_size"], size)
+    np.testing.assert_array_equal(t["slot_of_pix"], pre)
