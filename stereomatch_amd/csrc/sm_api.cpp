@@ -25,9 +25,10 @@
 hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N);
 hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gidx, double* minc, int32_t* idx, float* disp,
                            size_t N);
-hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl);
 
 namespace {
+
+constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2;
 
 struct DevBuf {
     void* p = nullptr;
@@ -43,7 +44,7 @@ struct sm_ctx {
     int W = 0, H = 0, stride = 0;
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
     DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], idx[2], minc[2], disp[2];
-    DevBuf cand[2], gmin[2], gidx[2], vol[2];
+    DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
@@ -137,9 +138,13 @@ sm_status stage_prep(sm_ctx* ctx) {
         CHECK(ensure(ctx, ctx->med[v], N * 4));
         CHECK(ensure(ctx, ctx->wR[v], N * 2));
         CHECK(ensure(ctx, ctx->wD[v], N * 2));
+        CHECK(ensure(ctx, ctx->rec[v], (N + 2 * SM_REC_PAD) * 8));
+        HIPC(hipMemsetAsync(ctx->rec[v].p, 0, SM_REC_PAD * 8, ctx->st));
+        HIPC(hipMemsetAsync(P<uint2>(ctx->rec[v]) + SM_REC_PAD + N, 0, SM_REC_PAD * 8, ctx->st));
     }
     HIPC(launch_prep(ctx->st, P<uint8_t>(ctx->img[0]), P<uint8_t>(ctx->img[1]), W, H, ctx->stride, P<uint32_t>(ctx->bgrx[0]),
-                     P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]), P<float>(ctx->gray[1])));
+                     P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]), P<float>(ctx->gray[1]),
+                     P<uint2>(ctx->rec[0]) + SM_REC_PAD, P<uint2>(ctx->rec[1]) + SM_REC_PAD));
     HIPC(launch_median_weights(ctx->st, P<uint32_t>(ctx->bgrx[0]), P<uint32_t>(ctx->bgrx[1]), P<uint32_t>(ctx->med[0]),
                                P<uint32_t>(ctx->med[1]), P<uint16_t>(ctx->wR[0]), P<uint16_t>(ctx->wD[0]),
                                P<uint16_t>(ctx->wR[1]), P<uint16_t>(ctx->wD[1]), W, H));
@@ -168,21 +173,28 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
         a.mR[v] = P<uint8_t>(ctx->mR[v]);
         a.mD[v] = P<uint8_t>(ctx->mD[v]);
     }
-    CHECK(ensure(ctx, ctx->changed, 16));
-    a.changed = P<int>(ctx->changed);
+    CHECK(ensure(ctx, ctx->changed, 2 * SM_MST_MAX_ROUNDS * sizeof(int)));
+    HIPC(hipMemsetAsync(ctx->changed.p, 0, 2 * SM_MST_MAX_ROUNDS * sizeof(int), ctx->st));
+    a.flags[0] = P<int>(ctx->changed);
+    a.flags[1] = P<int>(ctx->changed) + SM_MST_MAX_ROUNDS;
     HIPC(launch_bor_local(ctx->st, a, W, H));
-    for (int round = 0; round < 64; ++round) {
-        HIPC(hipMemsetAsync(ctx->changed.p, 0, sizeof(int), ctx->st));
-        HIPC(launch_bor_round(ctx->st, a, W, H));
-        HIPC(hipMemcpyAsync(ctx->h_changed, ctx->changed.p, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-        HIPC(hipStreamSynchronize(ctx->st));
-        if (*ctx->h_changed == 0) break;
+    // global rounds: every kernel of round r exits at once if round r-1 hooked nothing, so the
+    // host only synchronises every 4 rounds to decide whether to enqueue more
+    for (int r = 0; r < SM_MST_MAX_ROUNDS; ++r) {
+        HIPC(launch_bor_round(ctx->st, a, W, H, r));
+        if ((r & 3) == 3) {
+            HIPC(hipMemcpyAsync(ctx->h_changed, P<int>(ctx->changed) + r, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+            HIPC(hipMemcpyAsync(ctx->h_changed + 1, P<int>(ctx->changed) + SM_MST_MAX_ROUNDS + r, sizeof(int),
+                                hipMemcpyDeviceToHost, ctx->st));
+            HIPC(hipStreamSynchronize(ctx->st));
+            if (ctx->h_changed[0] == 0 && (nviews < 2 || ctx->h_changed[1] == 0)) break;
+        }
     }
     return SM_OK;
 }
 
-// device-side rounds record: [0, SM_MAX_ROUNDS] round_begin, then count, cursor, nrounds, n_has_light
-constexpr size_t RREC = (SM_MAX_ROUNDS + 1) + SM_MAX_ROUNDS + SM_MAX_ROUNDS + 2;
+// device-side rounds record: [0, SM_NBUCKETS] bucket begin, then count, cursor, nrounds, n_has_light
+constexpr size_t RREC = RREC_FWD;
 
 sm_status stage_layout(sm_ctx* ctx, int nviews) {
     const int W = ctx->W, H = ctx->H;
@@ -256,10 +268,10 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.paths = P<SmPath>(ctx->paths[v]);
         uint32_t* R = P<uint32_t>(ctx->rounds[v]);
         L.round_begin = R;
-        L.round_count = R + SM_MAX_ROUNDS + 1;
-        L.round_cursor = R + 2 * SM_MAX_ROUNDS + 1;
-        L.nrounds = R + 3 * SM_MAX_ROUNDS + 1;
-        L.n_has_light = R + 3 * SM_MAX_ROUNDS + 2;
+        L.round_count = R + SM_NBUCKETS + 1;
+        L.round_cursor = R + 2 * SM_NBUCKETS + 1;
+        L.nrounds = R + 3 * SM_NBUCKETS + 1;
+        L.n_has_light = R + 3 * SM_NBUCKETS + 2;
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains));
@@ -271,10 +283,10 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         auto& L = ctx->layout[v];
         if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); continue; }
         const uint32_t* R = ctx->h_rounds + v * RREC;
-        L.nrounds = R[3 * SM_MAX_ROUNDS + 1];
-        L.n_has_light = R[3 * SM_MAX_ROUNDS + 2];
-        L.begin.assign(R, R + SM_MAX_ROUNDS + 1);
-        L.npaths = R[SM_MAX_ROUNDS];
+        L.nrounds = R[3 * SM_NBUCKETS + 1];
+        L.n_has_light = R[3 * SM_NBUCKETS + 2];
+        L.begin.assign(R, R + SM_NBUCKETS + 1);
+        L.npaths = R[SM_NBUCKETS];
         if (L.nrounds == 0 || L.npaths == 0) return fail(ctx, SM_ERR_STATE, "layout produced no paths");
     }
     return SM_OK;
@@ -289,10 +301,8 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
         a.minc[v] = P<double>(ctx->minc[v]);
         a.disp[v] = P<float>(ctx->disp[v]);
     }
-    a.Lb = P<uint32_t>(ctx->bgrx[0]);
-    a.Lg = P<float>(ctx->gray[0]);
-    a.Rb = P<uint32_t>(ctx->bgrx[1]);
-    a.Rg = P<float>(ctx->gray[1]);
+    a.Lrec = P<uint2>(ctx->rec[0]) + SM_REC_PAD;
+    a.Rrec = P<uint2>(ctx->rec[1]) + SM_REC_PAD;
     a.atab = P<float>(ctx->atab);
     a.slut = P<double>(ctx->slut);
     a.s2lut = P<double>(ctx->s2lut);
@@ -303,15 +313,16 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     return a;
 }
 
-void set_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int nviews) {
+void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int nviews) {
     for (int v = 0; v < 2; ++v) {
         const auto& L = ctx->layout[v];
         if (v >= nviews || r >= L.nrounds) {
             a.paths[v] = P<SmPath>(ctx->paths[v]);
             a.npaths[v] = 0;
         } else {
-            a.paths[v] = P<SmPath>(ctx->paths[v]) + L.begin[r];
-            a.npaths[v] = (int)(L.begin[r + 1] - L.begin[r]);
+            const uint32_t b = 2 * r + (long_paths ? 0 : 1);
+            a.paths[v] = P<SmPath>(ctx->paths[v]) + L.begin[b];
+            a.npaths[v] = (int)(L.begin[b + 1] - L.begin[b]);
         }
     }
 }
@@ -344,18 +355,22 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     ctx->n_up = ctx->n_down = (int)nr;
     for (uint32_t i = 0; i < nr; ++i) {
         const uint32_t r = nr - 1 - i;  // deepest light depth first
-        set_round(ctx, a, r, nviews);
         HIPC(hipEventRecord(ctx->up_ev[2 * i], ctx->st));
-        HIPC(launch_up(ctx->st, a, spl));
+        for (int lp = 0; lp < 2; ++lp) {
+            set_bucket(ctx, a, r, lp == 0, nviews);
+            HIPC(launch_up(ctx->st, a, spl, lp == 0));
+        }
         HIPC(hipEventRecord(ctx->up_ev[2 * i + 1], ctx->st));
     }
     for (uint32_t r = 0; r < nr; ++r) {
-        set_round(ctx, a, r, nviews);
         HIPC(hipEventRecord(ctx->down_ev[2 * r], ctx->st));
-        if (debug_store_all)
-            HIPC(launch_down_debug(ctx->st, a, spl));
-        else
-            HIPC(launch_down(ctx->st, a, spl));
+        for (int lp = 0; lp < 2; ++lp) {
+            set_bucket(ctx, a, r, lp == 0, nviews);
+            if (debug_store_all)
+                HIPC(launch_down_debug(ctx->st, a, spl, lp == 0));
+            else
+                HIPC(launch_down(ctx->st, a, spl, lp == 0));
+        }
         HIPC(hipEventRecord(ctx->down_ev[2 * r + 1], ctx->st));
     }
     // algorithmic bytes (see DESIGN.md "Roofline accounting")
@@ -459,8 +474,8 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         delete ctx;
         return SM_ERR_HIP;
     }
-    if (hipHostMalloc((void**)&ctx->h_changed, sizeof(int)) != hipSuccess ||
-        hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC * sizeof(uint32_t)) != hipSuccess) {
+    if (hipHostMalloc((void**)&ctx->h_changed, 2 * sizeof(int)) != hipSuccess ||
+        hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
         return SM_ERR_HIP;
     }
@@ -491,7 +506,7 @@ void sm_destroy(sm_ctx* ctx) {
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
                          &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v],
-                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v]};
+                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -659,8 +674,10 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
         WalkArgs a = walk_args(ctx, Dpad, D, d0);
         const uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
         for (uint32_t i = 0; i < nr; ++i) {
-            set_round(ctx, a, nr - 1 - i, 2);
-            HIPC(launch_up(ctx->st, a, spl_for(D)));
+            for (int lp = 0; lp < 2; ++lp) {
+                set_bucket(ctx, a, nr - 1 - i, lp == 0, 2);
+                HIPC(launch_up(ctx->st, a, spl_for(D), lp == 0));
+            }
         }
         HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
                                    P<double>(ctx->vol[0])));

@@ -10,8 +10,7 @@
 //   k_weights       L1-RGB edge weights of the median image                 (:83-94, :242-262)
 //   k_cost_volume   AGD cost volume [d][y][x] from LDS-staged row tiles      (PatchMatchStereoGPU.cu:1482-1550)
 //   k_bor_*         Boruvka MST in (w,a,b) order: LDS tile phase + global    (segment-graph.h:54-89, c=+inf)
-//   k_up_walk       leaf->root pass, one wave per heavy path, AGD cost fused (Stereo3DMST.cpp:120-138)
-//   k_down_walk     root->leaf pass + strict-< WTA, one wave per heavy path  (:141-158, :160-186)
+//   (tree-filter walkers: sm_walk.hip)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -50,6 +49,7 @@ struct ImgPair {
     const uint8_t* src[2];  // packed BGR rows (device)
     uint32_t* bgrx[2];      // W*H
     float* gray[2];         // W*H
+    uint2* rec[2];          // W*H {bgrx, gray bits}: one 8-byte load per pixel in the walkers
 };
 
 __global__ void k_prep(ImgPair P, int W, int H, int stride) {
@@ -60,8 +60,10 @@ __global__ void k_prep(ImgPair P, int W, int H, int stride) {
     const uint8_t* s = P.src[v] + (size_t)y * stride + 3 * (size_t)x;
     const uint32_t w = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
     const size_t p = (size_t)y * W + x;
+    const float g = sm_gray(w);
     P.bgrx[v][p] = w;
-    P.gray[v][p] = sm_gray(w);
+    P.gray[v][p] = g;
+    P.rec[v][p] = make_uint2(w, __float_as_uint(g));
 }
 
 __device__ __forceinline__ void cswap(int& a, int& b) {
@@ -207,9 +209,9 @@ __global__ __launch_bounds__(CV_TX) void k_cost_volume(const uint32_t* __restric
 //   k_bor_min / k_bor_hook / k_bor_root / k_bor_relabel : global rounds on the remaining labels.
 // Mask output: mR[p]=1 <=> edge (p,p+1) in MST, mD[p]=1 <=> edge (p,p+W) in MST.
 // ---------------------------------------------------------------------------------------------
-#define BT 32                 // tile side
-#define BTN (BT * BT)         // 1024 pixels per tile
-#define BTHREADS 256
+#define BT 64                 // tile side
+#define BTN (BT * BT)         // 4096 pixels per tile
+#define BTHREADS 1024
 
 struct MstView {
     const uint16_t* wR;
@@ -219,7 +221,7 @@ struct MstView {
     uint32_t* root;           // per representative: final root after hooking
     uint8_t* mR;
     uint8_t* mD;
-    int* changed;
+    int* flags;               // flags[r] = 1 if global round r hooked anything
 };
 struct MstPair {
     MstView v[2];
@@ -317,11 +319,15 @@ __global__ __launch_bounds__(BTHREADS) void k_bor_local(MstPair P, int W, int H)
     }
 }
 
-__global__ void k_bor_min(MstPair P, int W, int H) {
+__device__ __forceinline__ bool round_done(const MstView& V, int r) { return r > 0 && V.flags[r - 1] == 0; }
+
+__global__ void k_bor_min(MstPair P, int W, int H, int rnd) {
     const MstView V = P.v[blockIdx.z];
+    if (round_done(V, rnd)) return;
     const int y = blockIdx.y;
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
+    const int x0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = x0 < W;
+    const int x = live ? x0 : W - 1;
     const int p = y * W + x;
     const uint32_t c = V.comp[p];
     unsigned long long mk = SM_KEY_NONE;
@@ -329,11 +335,29 @@ __global__ void k_bor_min(MstPair P, int W, int H) {
     if (y + 1 < H && V.comp[p + W] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 1));
     if (x > 0 && V.comp[p - 1] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 2));
     if (y > 0 && V.comp[p - W] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 3));
-    if (mk != SM_KEY_NONE) atomicMin(&V.best[c], mk);
+    // wave-aggregated atomics: one atomicMin per distinct component among the lanes
+    bool active = live && mk != SM_KEY_NONE;
+    const int lane = threadIdx.x & 63;
+    while (true) {
+        const unsigned long long act = __ballot(active);
+        if (!act) break;
+        const int leader = __builtin_ctzll(act);
+        const uint32_t c0 = __shfl(c, leader);
+        const bool mine = active && c == c0;
+        unsigned long long v = mine ? mk : SM_KEY_NONE;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned long long o = __shfl_xor(v, off);
+            v = o < v ? o : v;
+        }
+        if (lane == leader) atomicMin(&V.best[c0], v);
+        active = active && !mine;
+    }
 }
 
-__global__ void k_bor_hook(MstPair P, int W, int H) {
+__global__ void k_bor_hook(MstPair P, int W, int H, int rnd) {
     const MstView V = P.v[blockIdx.z];
+    if (round_done(V, rnd)) return;
     const int y = blockIdx.y;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -350,15 +374,16 @@ __global__ void k_bor_hook(MstPair P, int W, int H) {
         if (!(V.best[c2] == k && c < c2)) {
             h = c2;
             if (vert) V.mD[a] = 1; else V.mR[a] = 1;
-            *V.changed = 1;
+            V.flags[rnd] = 1;
         }
     }
     V.root[c] = h;
 }
 
-__global__ void k_bor_root(MstPair P, int W, int H) {
+__global__ void k_bor_root(MstPair P, int W, int H, int rnd) {
     // chase hook pointers to the root of each hook tree (hooks only point between old roots)
     const MstView V = P.v[blockIdx.z];
+    if (round_done(V, rnd) || V.flags[rnd] == 0) return;
     const int y = blockIdx.y;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -374,221 +399,14 @@ __global__ void k_bor_root(MstPair P, int W, int H) {
     V.root[c] = r;            // in-place shortcut: concurrent chasers still reach the same root
 }
 
-__global__ void k_bor_relabel(MstPair P, int W, int H) {
+__global__ void k_bor_relabel(MstPair P, int W, int H, int rnd) {
     const MstView V = P.v[blockIdx.z];
+    if (round_done(V, rnd) || V.flags[rnd] == 0) return;
     const int y = blockIdx.y;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
     const int p = y * W + x;
     V.comp[p] = V.root[V.comp[p]];
-}
-
-// ---------------------------------------------------------------------------------------------
-// Tree filter walkers.  Aggregation rows U[slot][Dpad] (fp64), lane l owns slices
-// [l*SPL, l*SPL+SPL) of this call.  One wave walks one heavy path; a 256-thread block runs
-// four independent paths.  Arithmetic per node is exactly the shipped reference's:
-//   up  : acc = 0; for children c in descending key order: acc = fma(S_c, A_up(c), acc);
-//         A_up(v) = acc + C(v)                                        (Stereo3DMST.cpp:125-137)
-//   down: A(v) = fma(S_v, A(parent), S2_v * A_up(v)); A(root) = A_up(root)   (:145-157)
-// so the result is independent of the schedule (paths, rounds, waves).
-// ---------------------------------------------------------------------------------------------
-struct WalkView {
-    const SmMeta* meta;
-    const SmPath* paths;   // paths of this round
-    int npaths;
-    double* U;             // [slots][Dpad]
-    int32_t* idx;          // W*H   (down pass)
-    double* minc;          // W*H   (down pass)
-    float* disp;           // W*H   (down pass)
-};
-
-struct CostImgs {
-    const uint32_t* Lb;
-    const float* Lg;
-    const uint32_t* Rb;
-    const float* Rg;
-    const float* atab;     // 766 floats
-};
-
-template <int SPL>
-__device__ __forceinline__ void node_cost(int view, uint32_t pix, int W, int dbase, int dend, const CostImgs& I,
-                                          const float* __restrict__ atab, double (&c)[SPL]) {
-    const int y = (int)(pix / (uint32_t)W);
-    const int x = (int)(pix - (uint32_t)y * (uint32_t)W);
-    const size_t row = (size_t)y * W;
-    if (view == 1) {
-        // right view: right(x) vs left(x+d)
-        const uint32_t r0 = I.Rb[row + x];
-        const float gr0 = I.Rg[row + x];
-        const float gr1 = x + 1 < W ? I.Rg[row + x + 1] : 0.f;
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) {
-            const int d = dbase + k;
-            float v = 3.0f;
-            if (d < dend && x + d + 1 < W) {
-                const size_t q = row + x + d;
-                v = sm_agd(r0, I.Lb[q], gr0, gr1, I.Lg[q], I.Lg[q + 1], atab);
-            }
-            c[k] = (double)v;
-        }
-    } else {
-        // left view: left pixel x at d is cost(x-d, d); x-d<0 and column W-1 -> 3.0
-        const uint32_t l0 = I.Lb[row + x];
-        const float gl0 = I.Lg[row + x];
-        const float gl1 = x + 1 < W ? I.Lg[row + x + 1] : 0.f;
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) {
-            const int d = dbase + k;
-            float v = 3.0f;
-            if (d < dend && x - d >= 0 && x + 1 < W) {
-                const size_t q = row + x - d;
-                v = sm_agd(I.Rb[q], l0, I.Rg[q], I.Rg[q + 1], gl0, gl1, atab);
-            }
-            c[k] = (double)v;
-        }
-    }
-}
-
-template <int SPL>
-__device__ __forceinline__ void load_row(const double* __restrict__ U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
-    const double* p = U + (size_t)slot * Dpad + lane * SPL;
-    if constexpr (SPL == 1) {
-        r[0] = p[0];
-    } else if constexpr (SPL == 2) {
-        const double2 t = *reinterpret_cast<const double2*>(p);
-        r[0] = t.x; r[1] = t.y;
-    } else {
-#pragma unroll
-        for (int k = 0; k < SPL; k += 2) {
-            const double2 t = *reinterpret_cast<const double2*>(p + k);
-            r[k] = t.x; r[k + 1] = t.y;
-        }
-    }
-}
-
-template <int SPL>
-__device__ __forceinline__ void store_row(double* __restrict__ U, uint32_t slot, int Dpad, int lane, const double (&r)[SPL]) {
-    double* p = U + (size_t)slot * Dpad + lane * SPL;
-    if constexpr (SPL == 1) {
-        p[0] = r[0];
-    } else {
-#pragma unroll
-        for (int k = 0; k < SPL; k += 2) *reinterpret_cast<double2*>(p + k) = make_double2(r[k], r[k + 1]);
-    }
-}
-
-__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-template <int SPL>
-__global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, CostImgs I, const double* __restrict__ slut,
-                                                 int W, int Dpad, int dcall, int dtotal_off) {
-    __shared__ float atab[SM_MAX_W + 1];
-    for (int i = threadIdx.x; i <= SM_MAX_W; i += 256) atab[i] = I.atab[i];
-    __syncthreads();
-    const int view = blockIdx.y;
-    const WalkView& V = view ? V1 : V0;
-    const int lane = threadIdx.x & 63;
-    const int pi = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (pi >= V.npaths) return;
-    const SmPath path = V.paths[pi];
-    const uint32_t head = uniform(path.head), len = uniform(path.len);
-    const int dbase = dtotal_off + lane * SPL;         // global disparity of this lane's first slice
-    const int dend = dtotal_off + dcall;
-    double x[SPL];
-#pragma unroll
-    for (int k = 0; k < SPL; ++k) x[k] = 0.0;
-    for (uint32_t s = head + len; s-- > head;) {
-        const SmMeta m = V.meta[s];
-        const uint32_t nch = sm_meta_nch(m), hidx = sm_meta_hidx(m);
-        double acc[SPL];
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) acc[k] = 0.0;
-        for (uint32_t j = 0; j < nch; ++j) {
-            const double S = slut[sm_meta_cw(m, (int)j)];
-            double v[SPL];
-            if (j == hidx) {
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) v[k] = x[k];
-            } else {
-                load_row<SPL>(V.U, m.cslot[j], Dpad, lane, v);
-            }
-#pragma unroll
-            for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S, v[k], acc[k]);
-        }
-        double c[SPL];
-        node_cost<SPL>(view, m.pix, W, dbase, dend, I, atab, c);
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) x[k] = acc[k] + c[k];
-        store_row<SPL>(V.U, s, Dpad, lane, x);
-    }
-}
-
-template <int SPL>
-__device__ __forceinline__ void wta_store(const double (&x)[SPL], int lane, int dloc0, int dcall, int dglob0, uint32_t pix,
-                                          const WalkView& V) {
-    // strict-< first-minimum over this lane's slices, then over lanes (lowest lane wins ties)
-    double bv = __builtin_huge_val();
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-        if (dloc0 + k < dcall && x[k] < bv) { bv = x[k]; bi = dloc0 + k; }
-    }
-    double g = bv;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) g = fmin(g, __shfl_xor(g, off));
-    const unsigned long long ball = __ballot(bv == g && bi != 0x7fffffff);
-    const int win = ball ? (int)__builtin_ctzll(ball) : 0;
-    const int gi = __shfl(bi, win);
-    if (lane == 0) {
-        const int d = ball ? gi : 0;
-        V.idx[pix] = dglob0 + d;
-        V.minc[pix] = g;
-        V.disp[pix] = (float)(dglob0 + d);
-    }
-}
-
-template <int SPL>
-__global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, const double* __restrict__ slut,
-                                                   const double* __restrict__ s2lut, int Dpad, int dcall, int dglob0,
-                                                   int store_all) {
-    const int view = blockIdx.y;
-    const WalkView& V = view ? V1 : V0;
-    const int lane = threadIdx.x & 63;
-    const int pi = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (pi >= V.npaths) return;
-    const SmPath path = V.paths[pi];
-    const uint32_t head = uniform(path.head), len = uniform(path.len);
-    const int dloc0 = lane * SPL;
-    double x[SPL];
-    {
-        const SmMeta m = V.meta[head];
-        double u[SPL];
-        load_row<SPL>(V.U, head, Dpad, lane, u);
-        if (m.parent == SM_NONE) {
-#pragma unroll
-            for (int k = 0; k < SPL; ++k) x[k] = u[k];
-        } else {
-            double xp[SPL];
-            load_row<SPL>(V.U, m.parent, Dpad, lane, xp);
-            const uint32_t wp = sm_meta_wp(m);
-            const double S = slut[wp], S2 = s2lut[wp];
-#pragma unroll
-            for (int k = 0; k < SPL; ++k) x[k] = __builtin_fma(S, xp[k], S2 * u[k]);
-            if (store_all || sm_meta_has_light(m)) store_row<SPL>(V.U, head, Dpad, lane, x);
-        }
-        wta_store<SPL>(x, lane, dloc0, dcall, dglob0, m.pix, V);
-    }
-    for (uint32_t s = head + 1; s < head + len; ++s) {
-        const SmMeta m = V.meta[s];
-        double u[SPL];
-        load_row<SPL>(V.U, s, Dpad, lane, u);
-        const uint32_t wp = sm_meta_wp(m);
-        const double S = slut[wp], S2 = s2lut[wp];
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) x[k] = __builtin_fma(S, x[k], S2 * u[k]);
-        if (store_all || sm_meta_has_light(m)) store_row<SPL>(V.U, s, Dpad, lane, x);
-        wta_store<SPL>(x, lane, dloc0, dcall, dglob0, m.pix, V);
-    }
 }
 
 // cross-rank WTA helpers: candidate index where this rank holds the global minimum
@@ -623,8 +441,8 @@ __global__ void k_rows_to_volume(const SmMeta* __restrict__ meta, const double* 
 #include "sm_launch.h"
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
-                       float* lg, uint32_t* rb, float* rg) {
-    ImgPair P{{l, r}, {lb, rb}, {lg, rg}};
+                       float* lg, uint32_t* rb, float* rg, uint2* lrec, uint2* rrec) {
+    ImgPair P{{l, r}, {lb, rb}, {lg, rg}, {lrec, rrec}};
     dim3 g((W + 255) / 256, H, 2);
     hipLaunchKernelGGL(k_prep, g, dim3(256), 0, st, P, W, H, stride);
     return hipGetLastError();
@@ -650,57 +468,23 @@ hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* l
 hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H) {
     MstPair P;
     for (int v = 0; v < 2; ++v)
-        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.changed};
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v]};
     dim3 g((W + BT - 1) / BT, (H + BT - 1) / BT, a.nviews);
     hipLaunchKernelGGL(k_bor_local, g, dim3(BTHREADS), 0, st, P, W, H);
     return hipGetLastError();
 }
 
-hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H) {
+hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r) {
     MstPair P;
     for (int v = 0; v < 2; ++v)
-        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.changed};
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v]};
     dim3 g((W + 255) / 256, H, a.nviews);
-    hipLaunchKernelGGL(k_bor_min, g, dim3(256), 0, st, P, W, H);
-    hipLaunchKernelGGL(k_bor_hook, g, dim3(256), 0, st, P, W, H);
-    hipLaunchKernelGGL(k_bor_root, g, dim3(256), 0, st, P, W, H);
-    hipLaunchKernelGGL(k_bor_relabel, g, dim3(256), 0, st, P, W, H);
+    hipLaunchKernelGGL(k_bor_min, g, dim3(256), 0, st, P, W, H, r);
+    hipLaunchKernelGGL(k_bor_hook, g, dim3(256), 0, st, P, W, H, r);
+    hipLaunchKernelGGL(k_bor_root, g, dim3(256), 0, st, P, W, H, r);
+    hipLaunchKernelGGL(k_bor_relabel, g, dim3(256), 0, st, P, W, H, r);
     return hipGetLastError();
 }
-
-static WalkView to_view(const WalkArgs& a, int v) {
-    return WalkView{a.meta[v], a.paths[v], a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v]};
-}
-
-hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl) {
-    const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
-    if (np == 0) return hipSuccess;
-    CostImgs I{a.Lb, a.Lg, a.Rb, a.Rg, a.atab};
-    dim3 g((np + 3) / 4, 2);
-    WalkView v0 = to_view(a, 0), v1 = to_view(a, 1);
-    switch (spl) {
-        case 1: hipLaunchKernelGGL(k_up_walk<1>, g, dim3(256), 0, st, v0, v1, I, a.slut, a.W, a.Dpad, a.dcall, a.dglob0); break;
-        case 2: hipLaunchKernelGGL(k_up_walk<2>, g, dim3(256), 0, st, v0, v1, I, a.slut, a.W, a.Dpad, a.dcall, a.dglob0); break;
-        default: hipLaunchKernelGGL(k_up_walk<4>, g, dim3(256), 0, st, v0, v1, I, a.slut, a.W, a.Dpad, a.dcall, a.dglob0); break;
-    }
-    return hipGetLastError();
-}
-
-static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, int store_all) {
-    const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
-    if (np == 0) return hipSuccess;
-    dim3 g((np + 3) / 4, 2);
-    WalkView v0 = to_view(a, 0), v1 = to_view(a, 1);
-    switch (spl) {
-        case 1: hipLaunchKernelGGL(k_down_walk<1>, g, dim3(256), 0, st, v0, v1, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all); break;
-        case 2: hipLaunchKernelGGL(k_down_walk<2>, g, dim3(256), 0, st, v0, v1, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all); break;
-        default: hipLaunchKernelGGL(k_down_walk<4>, g, dim3(256), 0, st, v0, v1, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all); break;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl) { return launch_down_impl(st, a, spl, 0); }
-hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl) { return launch_down_impl(st, a, spl, 1); }
 
 hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N) {
     hipLaunchKernelGGL(k_cand, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, minc, gmin, idx, cand, N);

@@ -15,8 +15,11 @@ struct MstArgs {
     uint32_t* root[2];
     uint8_t* mR[2];
     uint8_t* mD[2];
-    int* changed;
+    int* flags[2];   // per view: flags[r] for r < SM_MST_MAX_ROUNDS
 };
+
+#define SM_MST_MAX_ROUNDS 64
+#define SM_REC_PAD 1024  // records of padding before/after each image (walker loads stay in bounds)
 
 struct WalkArgs {
     const SmMeta* meta[2];
@@ -26,10 +29,8 @@ struct WalkArgs {
     int32_t* idx[2];
     double* minc[2];
     float* disp[2];
-    const uint32_t* Lb;
-    const float* Lg;
-    const uint32_t* Rb;
-    const float* Rg;
+    const uint2* Lrec;   // {bgrx, gray} records, padded by SM_REC_PAD records on both sides
+    const uint2* Rrec;
     const float* atab;
     const double* slut;
     const double* s2lut;
@@ -37,14 +38,15 @@ struct WalkArgs {
 };
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
-                       float* lg, uint32_t* rb, float* rg);
+                       float* lg, uint32_t* rb, float* rg, uint2* lrec, uint2* rrec);
 hipError_t launch_median_weights(hipStream_t st, const uint32_t* lb, const uint32_t* rb, uint32_t* lmed, uint32_t* rmed,
                                  uint16_t* lwR, uint16_t* lwD, uint16_t* rwR, uint16_t* rwD, int W, int H);
 hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* lg, const uint32_t* rb, const float* rg,
                               const float* atab, int W, int H, int d0, int D, float* lvol, float* rvol);
 hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H);
-hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H);
-hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl);
-hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl);
+hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r);
+hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
+hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
+hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_rows_to_volume(hipStream_t st, const SmMeta* meta, const double* U, int nslots, int Dpad, int D,
                                  size_t N, double* out);

@@ -5,7 +5,9 @@
 
 #include "sm_common.h"
 
-#define SM_MAX_ROUNDS 64
+#define SM_MAX_ROUNDS 32  // light depth <= log2(N) < 31
+#define SM_NBUCKETS (2 * SM_MAX_ROUNDS)  // per round: [long paths | short paths]
+#define SM_LONG_PATH 32   // paths of >= this many nodes use the deep-chunk walker variants
 
 struct LayoutView {
     // inputs
@@ -43,9 +45,9 @@ struct LayoutView {
     uint32_t* headpos;
     // paths
     SmPath* paths;
-    uint32_t* round_count;   // SM_MAX_ROUNDS
-    uint32_t* round_cursor;  // SM_MAX_ROUNDS
-    uint32_t* round_begin;   // SM_MAX_ROUNDS + 1
+    uint32_t* round_count;   // SM_NBUCKETS
+    uint32_t* round_cursor;  // SM_NBUCKETS
+    uint32_t* round_begin;   // SM_NBUCKETS + 1
     uint32_t* nrounds;
     uint32_t* n_has_light;   // nodes with at least one light child (roofline accounting)
 };

@@ -148,10 +148,20 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
         __syncthreads();
     }
     // heads: existing arcs without an in-tile predecessor; register chains
+    __shared__ uint32_t nheads, cbase;
+    if (threadIdx.x == 0) nheads = 0;
+    __syncthreads();
+    uint32_t myhead[PER];
     for (int i = 0; i < PER; ++i) {
         const int s = threadIdx.x + i * TL_THREADS;
-        if (dist[s] != 0 && !haspred[s]) headof[last[s]] = (uint16_t)s;
+        myhead[i] = SM_NONE;
+        if (dist[s] != 0 && !haspred[s]) {
+            headof[last[s]] = (uint16_t)s;
+            myhead[i] = atomicAdd(&nheads, 1u);  // LDS atomic: rank of this chain inside the tile
+        }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) cbase = atomicAdd(V.nchains, nheads);  // one global atomic per tile
     __syncthreads();
     for (int i = 0; i < PER; ++i) {
         const int s = threadIdx.x + i * TL_THREADS;
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
         const uint32_t a = 4u * p + (uint32_t)k;
         V.a_dist[a] = dist[s];
         if (!haspred[s]) {
-            const uint32_t cid = atomicAdd(V.nchains, 1u);
+            const uint32_t cid = cbase + myhead[i];
             V.a_cid[a] = cid;        // head's chain id (read below by the chain's other arcs: next kernel)
             const int ls = last[s];
             const int llp = ls >> 2;
@@ -432,8 +442,9 @@ __global__ void k_assign(LayoutPair LP, int W, int H) {
 // per-slot metadata (slot = preorder) + path heads
 __global__ void k_meta(LayoutPair LP, int W, int H) {
     const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
+    const int y = blockIdx.y, x0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = x0 < W;
+    const int x = live ? x0 : W - 1;  // idle lanes recompute the last pixel but never store
     const uint32_t v = (uint32_t)(y * W + x);
     const uint32_t adj = V.adj[v];
     const int pd = V.pdir[v];
@@ -464,49 +475,100 @@ __global__ void k_meta(LayoutPair LP, int W, int H) {
         wp = (uint32_t)(key_dir(V.wR, V.wD, W, v, pd) >> 33);
         parent = V.pre[nbr_of(v, pd, W)];
     }
+    has_light = live ? has_light : 0u;
     const uint32_t slot = V.pre[v];
-    V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
-    if (has_light) atomicAdd(V.n_has_light, 1u);
+    if (live) V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
+    {
+        __shared__ uint32_t nl;
+        if (threadIdx.x == 0) nl = 0;
+        __syncthreads();
+        if (has_light) atomicAdd(&nl, 1u);
+        __syncthreads();
+        if (threadIdx.x == 0 && nl) atomicAdd(V.n_has_light, nl);
+    }
     const bool head = pd < 0 || V.light_in[v];
-    V.headflag[slot] = head ? 1u + V.ld[v] : 0u;  // 0 = not a head, else 1 + light depth
+    if (live) V.headflag[slot] = head ? 1u + V.ld[v] : 0u;  // 0 = not a head, else 1 + light depth
 }
 
 // heads in slot order -> path lengths -> bucketed by light depth (order inside a round is free).
 // headpos[s] = s+1 at heads (0 elsewhere); after an inclusive max-scan it is 1 + the slot of
 // the head of s's path (heavy paths are contiguous in preorder).
-__global__ void k_path_prep(LayoutPair LP, int N) {
+#define PATH_BLOCK 1024
+#define PATH_ITEMS 8   // slots per thread -> 8192 per block (few global atomics per round bin)
+
+__global__ __launch_bounds__(PATH_BLOCK) void k_path_prep(LayoutPair LP, int N) {
     const LayoutView& V = LP.v[blockIdx.y];
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= (uint32_t)N) return;
-    const uint32_t h = V.headflag[s];
-    V.headpos[s] = h ? s + 1u : 0u;
-    if (h) atomicAdd(&V.round_count[h - 1], 1u);
+    const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
+    for (int i = 0; i < PATH_ITEMS; ++i) {
+        const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
+        if (s >= (uint32_t)N) break;
+        const uint32_t h = V.headflag[s];
+        V.headpos[s] = h ? s + 1u : 0u;
+    }
+}
+
+// after the max-scan: count paths per (round, long/short) bucket at their last slot
+__global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N) {
+    const LayoutView& V = LP.v[blockIdx.y];
+    __shared__ uint32_t hist[SM_NBUCKETS];
+    if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
+    for (int i = 0; i < PATH_ITEMS; ++i) {
+        const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
+        if (s >= (uint32_t)N) break;
+        if (s + 1 == (uint32_t)N || V.headflag[s + 1] != 0) {
+            const uint32_t head = V.headpos[s] - 1u;
+            const uint32_t len = s - head + 1u;
+            const uint32_t b = 2u * (V.headflag[head] - 1u) + (len >= SM_LONG_PATH ? 0u : 1u);
+            atomicAdd(&hist[b], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < SM_NBUCKETS && hist[threadIdx.x]) atomicAdd(&V.round_count[threadIdx.x], hist[threadIdx.x]);
 }
 
 __global__ void k_path_offsets(LayoutPair LP) {
     const LayoutView& V = LP.v[blockIdx.x];
     if (threadIdx.x != 0) return;
     uint32_t acc = 0, nr = 0;
-    for (int r = 0; r < SM_MAX_ROUNDS; ++r) {
-        V.round_begin[r] = acc;
-        V.round_cursor[r] = acc;
-        acc += V.round_count[r];
-        if (V.round_count[r]) nr = (uint32_t)r + 1;
+    for (int b = 0; b < SM_NBUCKETS; ++b) {
+        V.round_begin[b] = acc;
+        V.round_cursor[b] = acc;
+        acc += V.round_count[b];
+        if (V.round_count[b]) nr = (uint32_t)(b / 2) + 1;
     }
-    V.round_begin[SM_MAX_ROUNDS] = acc;
+    V.round_begin[SM_NBUCKETS] = acc;
     *V.nrounds = nr;
 }
 
-__global__ void k_path_emit(LayoutPair LP, int N) {
+__global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) {
     const LayoutView& V = LP.v[blockIdx.y];
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= (uint32_t)N) return;
-    const bool is_last = s + 1 == (uint32_t)N || V.headflag[s + 1] != 0;
-    if (!is_last) return;
-    const uint32_t head = V.headpos[s] - 1u;
-    const uint32_t r = V.headflag[head] - 1u;
-    const uint32_t pos = atomicAdd(&V.round_cursor[r], 1u);
-    V.paths[pos] = SmPath{head, s - head + 1u};
+    __shared__ uint32_t hist[SM_NBUCKETS], gbase[SM_NBUCKETS];
+    if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
+    uint32_t myr[PATH_ITEMS], myrank[PATH_ITEMS], myhead[PATH_ITEMS];
+    for (int i = 0; i < PATH_ITEMS; ++i) {
+        const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
+        myr[i] = SM_NONE;
+        if (s >= (uint32_t)N) continue;
+        const bool is_last = s + 1 == (uint32_t)N || V.headflag[s + 1] != 0;
+        if (!is_last) continue;
+        const uint32_t head = V.headpos[s] - 1u;
+        myhead[i] = head;
+        myr[i] = 2u * (V.headflag[head] - 1u) + (s - head + 1u >= SM_LONG_PATH ? 0u : 1u);
+        myrank[i] = atomicAdd(&hist[myr[i]], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < SM_NBUCKETS && hist[threadIdx.x])
+        gbase[threadIdx.x] = atomicAdd(&V.round_cursor[threadIdx.x], hist[threadIdx.x]);
+    __syncthreads();
+    for (int i = 0; i < PATH_ITEMS; ++i) {
+        if (myr[i] == SM_NONE) continue;
+        const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
+        V.paths[gbase[myr[i]] + myrank[i]] = SmPath{myhead[i], s - myhead[i] + 1u};
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -532,11 +594,12 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     launch_scan<long long, OpAdd>(st, tb, nviews, 2 * N - 2);
     hipLaunchKernelGGL(k_assign, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_meta, pg, dim3(256), 0, st, LP, W, H);
-    const dim3 sg((N + 255) / 256, nviews);
-    hipLaunchKernelGGL(k_path_prep, sg, dim3(256), 0, st, LP, N);
+    const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
+    hipLaunchKernelGGL(k_path_prep, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     ScanBufs<uint32_t> hb{{LP.v[0].headpos, LP.v[1].headpos}, {LP.v[0].bsum32, LP.v[1].bsum32}};
     launch_scan<uint32_t, OpMax>(st, hb, nviews, N);
+    hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     hipLaunchKernelGGL(k_path_offsets, dim3(nviews), dim3(64), 0, st, LP);
-    hipLaunchKernelGGL(k_path_emit, sg, dim3(256), 0, st, LP, N);
+    hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     return hipGetLastError();
 }
