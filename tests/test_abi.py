@@ -23,10 +23,14 @@ def test_library_exports_all_declared_symbols():
     assert not missing, missing
 
 
-def test_library_is_gfx950_code_object():
+def test_library_is_gfx950_code_object(tmp_path):
+    import shutil
     import subprocess
-    so = os.path.join(ROOT, "stereomatch_amd", "libstereomst.so")
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", so], capture_output=True, text=True)
+    # --offloading extracts the bundles next to its input: work on a copy in a temp dir
+    so = str(tmp_path / "libstereomst.so")
+    shutil.copy(os.path.join(ROOT, "stereomatch_amd", "libstereomst.so"), so)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", so], capture_output=True, text=True,
+                         cwd=str(tmp_path))
     assert "gfx950" in (out.stdout + out.stderr)
 
 
