@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libstereomst.so")
+# SM_LIB: an alternative build of the same library (diagnostic builds, tools/chain_prof.sh)
+LIB_PATH = os.environ.get("SM_LIB") or os.path.join(HERE, "libstereomst.so")
 
 SM_OK, SM_ERR_ARG, SM_ERR_HIP, SM_ERR_OOM, SM_ERR_RCCL, SM_ERR_STATE, SM_ERR_NODEVICE = range(7)
 STATUS_NAMES = {0: "SM_OK", 1: "SM_ERR_ARG", 2: "SM_ERR_HIP", 3: "SM_ERR_OOM", 4: "SM_ERR_RCCL",

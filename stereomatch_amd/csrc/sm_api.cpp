@@ -28,7 +28,7 @@ hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gi
 
 namespace {
 
-constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2;
+constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2 + SM_NBUCKETS + (SM_NBUCKETS + 1);
 
 struct DevBuf {
     void* p = nullptr;
@@ -43,17 +43,18 @@ struct sm_ctx {
     std::string err;
     int W = 0, H = 0, stride = 0;
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
-    DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], idx[2], minc[2], disp[2];
+    DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
+    DevBuf segtab[2];
     DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
     struct HostRounds {
         uint32_t nrounds = 0, npaths = 0, n_has_light = 0;
-        std::vector<uint32_t> begin;
+        std::vector<uint32_t> begin, maxlen, seg_begin;  // per bucket
     } layout[2];
     hipEvent_t ev[8] = {};
     std::vector<hipEvent_t> up_ev, down_ev;
@@ -232,6 +233,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->headpos[v], N * 4));
         CHECK(ensure(ctx, ctx->paths[v], N * sizeof(SmPath)));
         CHECK(ensure(ctx, ctx->rounds[v], RREC * 4));
+        CHECK(ensure(ctx, ctx->segtab[v], (N / 16 + 64) * sizeof(uint2)));  // <= N/32 segments + N/32 long paths
         HIPC(hipMemsetAsync(ctx->ccount[v].p, 0, 16, ctx->st));
         HIPC(hipMemsetAsync(ctx->rounds[v].p, 0, RREC * 4, ctx->st));
         LayoutView& L = LP.v[v];
@@ -272,6 +274,9 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.round_cursor = R + 2 * SM_NBUCKETS + 1;
         L.nrounds = R + 3 * SM_NBUCKETS + 1;
         L.n_has_light = R + 3 * SM_NBUCKETS + 2;
+        L.round_maxlen = R + 3 * SM_NBUCKETS + 3;
+        L.seg_begin = R + 4 * SM_NBUCKETS + 3;
+        L.segtab = P<uint2>(ctx->segtab[v]);
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains));
@@ -281,11 +286,13 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
     HIPC(hipStreamSynchronize(ctx->st));
     for (int v = 0; v < 2; ++v) {
         auto& L = ctx->layout[v];
-        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); continue; }
+        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); continue; }
         const uint32_t* R = ctx->h_rounds + v * RREC;
         L.nrounds = R[3 * SM_NBUCKETS + 1];
         L.n_has_light = R[3 * SM_NBUCKETS + 2];
         L.begin.assign(R, R + SM_NBUCKETS + 1);
+        L.maxlen.assign(R + 3 * SM_NBUCKETS + 3, R + 4 * SM_NBUCKETS + 3);
+        L.seg_begin.assign(R + 4 * SM_NBUCKETS + 3, R + 5 * SM_NBUCKETS + 4);
         L.npaths = R[SM_NBUCKETS];
         if (L.nrounds == 0 || L.npaths == 0) return fail(ctx, SM_ERR_STATE, "layout produced no paths");
     }
@@ -297,6 +304,7 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     for (int v = 0; v < 2; ++v) {
         a.meta[v] = P<SmMeta>(ctx->meta[v]);
         a.U[v] = P<double>(ctx->U[v]);
+        a.Cst[v] = P<float>(ctx->Cst[v]);
         a.idx[v] = P<int32_t>(ctx->idx[v]);
         a.minc[v] = P<double>(ctx->minc[v]);
         a.disp[v] = P<float>(ctx->disp[v]);
@@ -314,15 +322,21 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
 }
 
 void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int nviews) {
+    a.maxlen = 0;
     for (int v = 0; v < 2; ++v) {
         const auto& L = ctx->layout[v];
         if (v >= nviews || r >= L.nrounds) {
             a.paths[v] = P<SmPath>(ctx->paths[v]);
             a.npaths[v] = 0;
+            a.segtab[v] = P<uint2>(ctx->segtab[v]);
+            a.nseg[v] = 0;
         } else {
             const uint32_t b = 2 * r + (long_paths ? 0 : 1);
             a.paths[v] = P<SmPath>(ctx->paths[v]) + L.begin[b];
             a.npaths[v] = (int)(L.begin[b + 1] - L.begin[b]);
+            a.maxlen = std::max(a.maxlen, (int)L.maxlen[b]);
+            a.segtab[v] = P<uint2>(ctx->segtab[v]) + L.seg_begin[b];
+            a.nseg[v] = (int)(L.seg_begin[b + 1] - L.seg_begin[b]);
         }
     }
 }
@@ -336,17 +350,45 @@ sm_status ensure_events(sm_ctx* ctx, std::vector<hipEvent_t>& evs, size_t n) {
     return SM_OK;
 }
 
+// one light-depth round of the up pass: short paths by the chunked walkers, long paths by the
+// chain engine (pre-fold kernel + one workgroup per path)
+sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
+    set_bucket(ctx, a, r, false, nviews);
+    HIPC(launch_up(ctx->st, a, spl, false));
+    set_bucket(ctx, a, r, true, nviews);
+    HIPC(launch_up_long(ctx->st, a, spl));
+    return SM_OK;
+}
+
+sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews, bool store_all) {
+    set_bucket(ctx, a, r, true, nviews);
+    HIPC(launch_down_long(ctx->st, a, spl, store_all ? 1 : 0));
+    set_bucket(ctx, a, r, false, nviews);
+    if (store_all)
+        HIPC(launch_down_debug(ctx->st, a, spl, false));
+    else
+        HIPC(launch_down(ctx->st, a, spl, false));
+    return SM_OK;
+}
+
+sm_status ensure_filter_bufs(sm_ctx* ctx, int Dpad) {
+    const size_t N = (size_t)ctx->W * ctx->H;
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
+        CHECK(ensure(ctx, ctx->Cst[v], N * (size_t)Dpad * 4));
+        CHECK(ensure(ctx, ctx->idx[v], N * 4));
+        CHECK(ensure(ctx, ctx->minc[v], N * 8));
+        CHECK(ensure(ctx, ctx->disp[v], N * 4));
+    }
+    return SM_OK;
+}
+
 // up + down passes over all rounds for nviews views; debug_store_all stores every A row
 sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_store_all) {
     const size_t N = (size_t)ctx->W * ctx->H;
     const int spl = spl_for(D);
     const int Dpad = 64 * spl;
-    for (int v = 0; v < 2; ++v) {
-        CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
-        CHECK(ensure(ctx, ctx->idx[v], N * 4));
-        CHECK(ensure(ctx, ctx->minc[v], N * 8));
-        CHECK(ensure(ctx, ctx->disp[v], N * 4));
-    }
+    CHECK(ensure_filter_bufs(ctx, Dpad));
     uint32_t nr = 0;
     for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
     CHECK(ensure_events(ctx, ctx->up_ev, 2 * nr));
@@ -354,23 +396,13 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
     ctx->n_up = ctx->n_down = (int)nr;
     for (uint32_t i = 0; i < nr; ++i) {
-        const uint32_t r = nr - 1 - i;  // deepest light depth first
         HIPC(hipEventRecord(ctx->up_ev[2 * i], ctx->st));
-        for (int lp = 0; lp < 2; ++lp) {
-            set_bucket(ctx, a, r, lp == 0, nviews);
-            HIPC(launch_up(ctx->st, a, spl, lp == 0));
-        }
+        CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest light depth first
         HIPC(hipEventRecord(ctx->up_ev[2 * i + 1], ctx->st));
     }
     for (uint32_t r = 0; r < nr; ++r) {
         HIPC(hipEventRecord(ctx->down_ev[2 * r], ctx->st));
-        for (int lp = 0; lp < 2; ++lp) {
-            set_bucket(ctx, a, r, lp == 0, nviews);
-            if (debug_store_all)
-                HIPC(launch_down_debug(ctx->st, a, spl, lp == 0));
-            else
-                HIPC(launch_down(ctx->st, a, spl, lp == 0));
-        }
+        CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all));
         HIPC(hipEventRecord(ctx->down_ev[2 * r + 1], ctx->st));
     }
     // algorithmic bytes (see DESIGN.md "Roofline accounting")
@@ -505,7 +537,7 @@ void sm_destroy(sm_ctx* ctx) {
     for (DevBuf* b : all) if (b->p) (void)hipFree(b->p);
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
-                         &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v],
+                         &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v], &ctx->Cst[v],
                          &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
@@ -519,7 +551,7 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->pre[v], &ctx->ld[v], &ctx->a_dist[v], &ctx->a_cid[v], &ctx->a_head[v], &ctx->arank[v],
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cn0[v], &ctx->cn1[v],
                          &ctx->cw0[v], &ctx->cw1[v], &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
-                         &ctx->headpos[v], &ctx->rounds[v]};
+                         &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v]};
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -670,15 +702,10 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
     CHECK(ensure(ctx, ctx->vol[0], N * (size_t)D * 8));
     // up pass only, snapshot A_up
     {
-        for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
+        CHECK(ensure_filter_bufs(ctx, Dpad));
         WalkArgs a = walk_args(ctx, Dpad, D, d0);
         const uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
-        for (uint32_t i = 0; i < nr; ++i) {
-            for (int lp = 0; lp < 2; ++lp) {
-                set_bucket(ctx, a, nr - 1 - i, lp == 0, 2);
-                HIPC(launch_up(ctx->st, a, spl_for(D), lp == 0));
-            }
-        }
+        for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl_for(D), 2));
         HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
                                    P<double>(ctx->vol[0])));
         if (A_up) HIPC(hipMemcpyAsync(A_up, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));

@@ -34,6 +34,10 @@ struct WalkArgs {
     const float* atab;
     const double* slut;
     const double* s2lut;
+    float* Cst[2];       // long-path AGD cost staging rows [slot][Dpad]
+    int maxlen;          // longest path of the current bucket (both views)
+    const uint2* segtab[2];  // long buckets: {path, segment} per SM_PRE_SEG-node segment
+    int nseg[2];
     int W, Dpad, dcall, dglob0;
 };
 
@@ -47,6 +51,9 @@ hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H);
 hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
+// long-path engine (sm_chain.hip): buckets of paths with >= SM_LONG_PATH nodes
+hipError_t launch_up_long(hipStream_t st, const WalkArgs& a, int spl);
+hipError_t launch_down_long(hipStream_t st, const WalkArgs& a, int spl, int store_all);
 hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_rows_to_volume(hipStream_t st, const SmMeta* meta, const double* U, int nslots, int Dpad, int D,
                                  size_t N, double* out);

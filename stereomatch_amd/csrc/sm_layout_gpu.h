@@ -7,7 +7,8 @@
 
 #define SM_MAX_ROUNDS 32  // light depth <= log2(N) < 31
 #define SM_NBUCKETS (2 * SM_MAX_ROUNDS)  // per round: [long paths | short paths]
-#define SM_LONG_PATH 32   // paths of >= this many nodes use the deep-chunk walker variants
+#define SM_LONG_PATH 32   // paths of >= this many nodes go to the long-path chain engine (sm_chain.hip)
+#define SM_PRE_SEG 32     // nodes per k_up_pre block (segment table granularity)
 
 struct LayoutView {
     // inputs
@@ -48,6 +49,9 @@ struct LayoutView {
     uint32_t* round_count;   // SM_NBUCKETS
     uint32_t* round_cursor;  // SM_NBUCKETS
     uint32_t* round_begin;   // SM_NBUCKETS + 1
+    uint32_t* round_maxlen;  // SM_NBUCKETS: longest path per bucket
+    uint32_t* seg_begin;     // SM_NBUCKETS + 1: first segment of each bucket in segtab
+    uint2* segtab;           // {path index within its bucket, segment within the path}
     uint32_t* nrounds;
     uint32_t* n_has_light;   // nodes with at least one light child (roofline accounting)
 };

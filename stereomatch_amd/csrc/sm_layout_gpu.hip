@@ -522,6 +522,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N)
             const uint32_t len = s - head + 1u;
             const uint32_t b = 2u * (V.headflag[head] - 1u) + (len >= SM_LONG_PATH ? 0u : 1u);
             atomicAdd(&hist[b], 1u);
+            if (len >= SM_LONG_PATH) atomicMax(&V.round_maxlen[b], len);  // few long paths: direct atomics
         }
     }
     __syncthreads();
@@ -571,6 +572,36 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
     }
 }
 
+// segment table of the long-path buckets: segment i of bucket b -> {path within b, SM_PRE_SEG-node
+// segment of that path}, so k_up_pre launches exactly one block per segment.  One block per view.
+__global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP) {
+    const LayoutView& V = LP.v[blockIdx.x];
+    __shared__ uint32_t sc[1024];
+    uint32_t running = 0;
+    for (int b = 0; b < SM_NBUCKETS; ++b) {
+        if (threadIdx.x == 0) V.seg_begin[b] = running;
+        if (b & 1) continue;  // short buckets have no segments
+        const uint32_t p0 = V.round_begin[b], p1 = V.round_begin[b + 1];
+        for (uint32_t c = p0; c < p1; c += 1024) {
+            const uint32_t p = c + threadIdx.x;
+            const uint32_t ns = p < p1 ? (V.paths[p].len + SM_PRE_SEG - 1) / SM_PRE_SEG : 0u;
+            sc[threadIdx.x] = ns;
+            __syncthreads();
+            for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+                const uint32_t t = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0u;
+                __syncthreads();
+                sc[threadIdx.x] += t;
+                __syncthreads();
+            }
+            const uint32_t start = running + sc[threadIdx.x] - ns;
+            for (uint32_t q = 0; q < ns; ++q) V.segtab[start + q] = make_uint2(p - p0, q);
+            running += sc[1023];
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) V.seg_begin[SM_NBUCKETS] = running;
+}
+
 // ------------------------------------------------------------------------------------------
 static dim3 pix_grid(int W, int H, int nv) { return dim3((W + 255) / 256, H, nv); }
 
@@ -601,5 +632,6 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     hipLaunchKernelGGL(k_path_offsets, dim3(nviews), dim3(64), 0, st, LP);
     hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
+    hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP);
     return hipGetLastError();
 }

@@ -25,107 +25,8 @@
 
 #include "sm_common.h"
 #include "sm_launch.h"
+#include "sm_walk_util.h"
 
-// per-view mutable state; the read-only metadata and path lists are separate __restrict__ kernel
-// arguments (kernarg-derived, provably unclobbered)
-struct WalkView {
-    int npaths;
-    double* U;             // [slots][Dpad]
-    int32_t* idx;          // W*H   (down pass)
-    double* minc;          // W*H   (down pass)
-    float* disp;           // W*H   (down pass)
-};
-
-#define SM_NUM_W 766
-#define S_ZERO SM_NUM_W    // LDS S-table entry holding 0.0 (absent children)
-
-__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ float rgray(uint2 r) { return __uint_as_float(r.y); }
-
-// AGD cost (PatchMatchStereoGPU.cu:1518-1543) from {bgrx, gray} records:
-// r0 = right(x), l0 = left(x+d), gr1 = gray(right(x+1)), gl1 = gray(left(x+d+1))
-__device__ __forceinline__ float agd_rec(uint2 r0, uint2 l0, float gr1, float gl1, const float* __restrict__ atab) {
-    const uint32_t l1 = __builtin_amdgcn_sad_u8(r0.x, l0.x, 0u);  // exact integer colour L1
-    const float a = atab[l1];
-    float g = rgray(l0) - rgray(r0);
-    g = g + (gr1 - gl1);
-    const float b = 0.89f * fminf(fabsf(g), 2.0f);
-    return a + b;
-}
-
-template <int SPL>
-__device__ __forceinline__ void load_row(const double* __restrict__ U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
-    const double* p = U + (size_t)slot * Dpad + lane * SPL;
-    if constexpr (SPL == 1) {
-        r[0] = p[0];
-    } else {
-#pragma unroll
-        for (int k = 0; k < SPL; k += 2) {
-            const double2 t = *reinterpret_cast<const double2*>(p + k);
-            r[k] = t.x;
-            r[k + 1] = t.y;
-        }
-    }
-}
-
-template <int SPL>
-__device__ __forceinline__ void store_row(double* __restrict__ U, uint32_t slot, int Dpad, int lane, const double (&r)[SPL]) {
-    double* p = U + (size_t)slot * Dpad + lane * SPL;
-    if constexpr (SPL == 1) {
-        p[0] = r[0];
-    } else {
-#pragma unroll
-        for (int k = 0; k < SPL; k += 2) *reinterpret_cast<double2*>(p + k) = make_double2(r[k], r[k + 1]);
-    }
-}
-
-// lane-distributed metadata of CH nodes: lane 8j+f holds word f of node j (8 nodes per VGPR)
-template <int CH>
-struct MetaVec {
-    uint32_t w[(CH + 7) / 8];
-};
-
-template <int CH>
-__device__ __forceinline__ void load_meta(MetaVec<CH>& mv, const uint32_t* __restrict__ meta32, int lane, int first,
-                                          int step, int n) {
-    // node j of the chunk = first + step*j (clamped to the chunk's valid nodes)
-#pragma unroll
-    for (int q = 0; q < (CH + 7) / 8; ++q) {
-        const int j = q * 8 + (lane >> 3);
-        const int jj = j < n ? j : n - 1;
-        mv.w[q] = meta32[(size_t)(first + step * jj) * 8 + (lane & 7)];
-    }
-}
-
-template <int CH>
-__device__ __forceinline__ uint32_t mfield(const MetaVec<CH>& mv, int j, int f) {
-    return __builtin_amdgcn_readlane(mv.w[j >> 3], ((j & 7) << 3) + f);
-}
-
-// SmMeta words: 0 pix, 1 parent, 2 lo (wp|cw0|cw1), 3 hi (cw2|cw3|nch|hidx|has_light), 4..7 cslot
-__device__ __forceinline__ uint32_t lo_wp(uint32_t lo) { return lo & 1023u; }
-__device__ __forceinline__ uint32_t cw_of(uint32_t lo, uint32_t hi, int i) {
-    return i == 0 ? (lo >> 10) & 1023u : i == 1 ? (lo >> 20) & 1023u : i == 2 ? hi & 1023u : (hi >> 10) & 1023u;
-}
-__device__ __forceinline__ uint32_t hi_nch(uint32_t hi) { return (hi >> 20) & 7u; }
-__device__ __forceinline__ uint32_t hi_hidx(uint32_t hi) { return (hi >> 23) & 3u; }
-__device__ __forceinline__ uint32_t hi_light(uint32_t hi) { return (hi >> 25) & 1u; }
-
-struct WalkShared {
-    float atab[SM_MAX_W + 1];
-    double slut[SM_NUM_W + 1];  // [SM_NUM_W] = 0.0
-    double s2lut[SM_NUM_W];
-};
-
-__device__ __forceinline__ void load_tables(WalkShared& sh, const float* atab_g, const double* slut_g, const double* s2lut_g) {
-    for (int i = threadIdx.x; i <= SM_MAX_W; i += blockDim.x) sh.atab[i] = atab_g[i];
-    for (int i = threadIdx.x; i < SM_NUM_W; i += blockDim.x) {
-        sh.slut[i] = slut_g[i];
-        sh.s2lut[i] = s2lut_g[i];
-    }
-    if (threadIdx.x == 0) sh.slut[SM_NUM_W] = 0.0;
-    __syncthreads();
-}
 
 // ---------------------------------------------------------------------------------------------
 // up pass
@@ -136,7 +37,6 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
                                          double* __restrict__ U, const WalkShared& sh, double (&xc)[SPL]) {
     // ---- all vector loads of the chunk
     double lr[CH][2][SPL];
-    uint2 ob[CH][SPL + 1], o0[CH], o1[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         if (j < n) {
@@ -147,45 +47,19 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
                 const uint32_t i = (uint32_t)k + ((uint32_t)k >= hidx ? 1u : 0u);  // child position of light slot k
                 if (i < nch) load_row<SPL>(U, mfield(mv, j, 4 + (int)i), Dpad, lane, lr[j][k]);
             }
-            const int pix = (int)mfield(mv, j, 0);
-            const int y = pix / W;
-            const int x = pix - y * W;
-            const size_t row = (size_t)y * W;
-            // own pixels x, x+1 through a lane-dependent (vector) load: a uniform address would become
-            // a scalar-cache load whose lgkmcnt waits serialise with the LDS table reads
-            const uint2 t = own[row + x + (lane & 1)];  // x+1 == W reads the next row / the pad: masked below
-            o0[j] = make_uint2(__builtin_amdgcn_readlane(t.x, 0), __builtin_amdgcn_readlane(t.y, 0));
-            o1[j] = make_uint2(__builtin_amdgcn_readlane(t.x, 1), __builtin_amdgcn_readlane(t.y, 1));
-            const long long base = view ? (long long)(row + x) + dbase : (long long)(row + x) - dbase - (SPL - 1);
-#pragma unroll
-            for (int q = 0; q <= SPL; ++q) ob[j][q] = oth[base + q];
         }
     }
+    ImgRecs<SPL, CH> rec;
+    load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
     // ---- off-chain work: costs and edge factors of every node of the chunk
     double c[CH][SPL], Sv[CH][4];
+    chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
         const uint32_t nch = hi_nch(hi);
 #pragma unroll
         for (int i = 0; i < 4; ++i) Sv[j][i] = sh.slut[(uint32_t)i < nch ? cw_of(lo, hi, i) : (uint32_t)S_ZERO];
-        const int pix = (int)mfield(mv, j, 0);
-        const int y = pix / W;
-        const int x = pix - y * W;
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) {
-            const int d = dbase + k;
-            float v;
-            bool ok;
-            if (view) {  // right reference: right(x) vs left(x+d)
-                ok = d < dend && x + d + 1 < W;
-                v = agd_rec(o0[j], ob[j][k], rgray(o1[j]), rgray(ob[j][k + 1]), sh.atab);
-            } else {     // left pixel x at d: cost(x-d, d); x-d<0 and column W-1 -> 3.0
-                ok = d < dend && x - d >= 0 && x + 1 < W;
-                v = agd_rec(ob[j][SPL - 1 - k], o0[j], rgray(ob[j][SPL - k]), rgray(o1[j]), sh.atab);
-            }
-            c[j][k] = (double)(ok ? v : 3.0f);
-        }
     }
     // ---- serial recurrence along the path (bottom -> top)
 #pragma unroll
@@ -271,58 +145,6 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
 // ---------------------------------------------------------------------------------------------
 // down pass + WTA
 // ---------------------------------------------------------------------------------------------
-// min of a double with the value DPP-moved from another lane (both 32-bit halves moved)
-template <int CTRL>
-__device__ __forceinline__ double dpp_min(double v) {
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, 0xF, 0xF, false);
-    const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, 0xF, 0xF, false);
-    return fmin(v, __hiloint2double(hi2, lo2));
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l), hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-
-// CH strict-< first-minimum reductions at once (independent -> their latencies overlap).
-// Returns, in lane j < CH, node j's argmin (slice index of this call) and minimum.
-template <int SPL, int CH>
-__device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, int dloc0, int dcall, double& out_min,
-                                          int& out_idx) {
-    double bv[CH], g[CH];
-    int bi[CH];
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        bv[j] = __builtin_huge_val();
-        bi[j] = 0x7fffffff;
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) {
-            if (dloc0 + k < dcall && x[j][k] < bv[j]) { bv[j] = x[j][k]; bi[j] = dloc0 + k; }
-        }
-        g[j] = bv[j];
-    }
-#pragma unroll
-    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0xB1>(g[j]);   // quad_perm [1,0,3,2]
-#pragma unroll
-    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0x4E>(g[j]);   // quad_perm [2,3,0,1]
-#pragma unroll
-    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0x141>(g[j]);  // row_half_mirror
-#pragma unroll
-    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0x140>(g[j]);  // row_mirror
-    out_min = 0.0;
-    out_idx = 0;
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        const double m = fmin(fmin(readlane_f64(g[j], 0), readlane_f64(g[j], 16)),
-                              fmin(readlane_f64(g[j], 32), readlane_f64(g[j], 48)));
-        const unsigned long long ball = __ballot(bv[j] == m && bi[j] != 0x7fffffff);
-        const int win = ball ? (int)__builtin_ctzll(ball) : 0;
-        const int gi = ball ? __builtin_amdgcn_readlane(bi[j], win) : 0;
-        if (lane == j) { out_min = m; out_idx = gi; }
-    }
-}
-
 template <int SPL, int CH>
 __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                    const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
