@@ -25,12 +25,9 @@
 // the chain; T(v) = S2*A_up is the product the reference rounds before its fma.  Results stay
 // bit-identical to the oracle and independent of the schedule.
 //
-// Ring protocol (per entry e, node j of the path, entry = j mod R):
-//   state[e] = 2j+1 : helper has written node j's inputs      (helper -> chain)
-//   state[e] = 2j+2 : chain has written node j's result       (chain  -> helper)
-// Entry e is owned by helper e / E, so the only cross-wave traffic is these two hand-offs.  LDS
-// operations of one wave complete in order; a publish is preceded by lgkmcnt(0) so the entry's
-// data is in LDS before its state word changes.
+// Group ring (see "Group ring" below): one state word per group of G nodes; a wave's LDS
+// operations complete in issue order, so a state word observed after data written before it
+// (or a state written after data read before it) orders the hand-off without extra waits.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -39,9 +36,6 @@
 #include "sm_layout_gpu.h"
 #include "sm_walk_util.h"
 
-#define CHN_HELPERS 15
-#define CHN_THREADS (64 * (CHN_HELPERS + 1))
-#define CHN_G 8  // nodes per chain group (one LDS round trip per group)
 
 // -DSM_CHAIN_PROF: the first path of each launch prints chain-wave cycles / failed polls and helper
 // wait cycles (device printf) -- a diagnostic build only (tools/chain_prof.sh)
@@ -189,246 +183,303 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
                 }
             }
             const uint32_t slot = (uint32_t)(head + first + j);
-            store_row<SPL>(U, slot, Dpad, lane, acc);
+            if (hidx > 0) store_row<SPL>(U, slot, Dpad, lane, acc);  // Pre = 0 rows are never read
             store_crow<SPL>(Cst, slot, Dpad, lane, c[j]);
         }
     }
 }
 
 // ---------------------------------------------------------------------------------------------
+// Group ring.  Chain node j (0 = first node the chain visits) belongs to group g = j / G; group g
+// is staged in LDS slot g % NS by helper (g % NH), which holds its next group's rows in registers
+// while it waits for the slot -- so the lead time of the global loads is ~NH groups of chain time,
+// independent of the LDS capacity.  The serial recurrence is split over NCW chain waves by slice
+// range (slices are independent chains): a lone wave's cost per node is dominated by the bytes it
+// moves through LDS, so each chain wave moves 1/NCW of the row.  Chain wave w, lane l owns slice
+// elements [(64w + l) * CS, +CS) of every row.
+// ---------------------------------------------------------------------------------------------
+#define CHN_WAVES 16
+#define CHN_THREADS (64 * CHN_WAVES)
+
+template <int SPL>
+struct Split {
+    static constexpr int NCW = SPL == 1 ? 1 : 2;  // chain waves
+    static constexpr int CS = SPL / NCW;          // slices per chain lane
+    static constexpr int NH = CHN_WAVES - NCW;    // helper waves
+};
+
+template <int CS>
+__device__ __forceinline__ void lds_read_at(const double* row, int e0, double (&r)[CS]) {
+#pragma unroll
+    for (int q = 0; q < CS; ++q) r[q] = row[e0 + q];
+}
+template <int CS>
+__device__ __forceinline__ void lds_write_at(double* row, int e0, const double (&r)[CS]) {
+#pragma unroll
+    for (int q = 0; q < CS; ++q) row[e0 + q] = r[q];
+}
+template <int CS>
+__device__ __forceinline__ void global_read_at(const double* __restrict__ U, uint32_t slot, int Dpad, int e0, double (&r)[CS]) {
+    const double* p = U + (size_t)slot * Dpad + e0;
+    if constexpr (CS == 1) {
+        r[0] = p[0];
+    } else {
+        const double2 t = *reinterpret_cast<const double2*>(p);
+        r[0] = t.x;
+        r[1] = t.y;
+    }
+}
+template <int CS>
+__device__ __forceinline__ void global_write_at(double* __restrict__ U, uint32_t slot, int Dpad, int e0, const double (&r)[CS]) {
+    double* p = U + (size_t)slot * Dpad + e0;
+    if constexpr (CS == 1)
+        p[0] = r[0];
+    else
+        *reinterpret_cast<double2*>(p) = make_double2(r[0], r[1]);
+}
+
+__device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n) == v
+    for (int w = 0; w < n; ++w) lds_wait(&p[w], v, true);
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_up_chain
+//
+// Branch-free node step:  acc = fma(Sh, x, Pre); acc = fma(Sp1, P1, acc); acc = fma(Sp2, P2, acc);
+// x = acc + C.  Absent children carry S = 0 and a dummy row: every aggregate is finite and >= +0,
+// so fma(0, r, acc) == acc exactly and the step equals the reference's fold with only the
+// children present (the bottom node has Sh = 0 and x = 0, i.e. acc = Pre).  A tree root may have a
+// third post-heavy child: its group takes the node-by-node path with one more fma.
 // ---------------------------------------------------------------------------------------------
 template <int SPL>
 struct UpCfg {
-    static constexpr int E = SPL == 1 ? 4 : SPL == 2 ? 2 : 1;  // ring entries per helper wave
-    static constexpr int R = CHN_HELPERS * E;
+    static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? 6 : 3;  // nodes per group (helper registers)
+    static constexpr int NS = 4;                               // LDS slots
 };
 
-// entry header: the state word sits next to the weights so one read batch fetches both
-struct UpHdr {
-    int state;
-    uint32_t fl;   // npost | has_heavy << 2
-    double s[4];   // S of the heavy child and of posts 0..2
+struct UpNodeS {
+    double Sh, Sp1, Sp2, pad;
 };
+
+template <int SPL>
+struct UpSlot {
+    static constexpr int G = UpCfg<SPL>::G;
+    double pre[G][64 * SPL];    // Pre (pre-heavy fold)
+    double post1[G][64 * SPL];  // first post-heavy child row (dummy if absent)
+    double post2[G][64 * SPL];  // second post-heavy child row (dummy if absent)
+    double post3[64 * SPL];     // a root's third post-heavy child
+    float c[G][64 * SPL];       // AGD cost
+    UpNodeS s[G];
+    double S3;
+    int k3;                     // node of the group with a third post-heavy child, or -1
+    int done[2];                // g+1: chain wave w finished group g (slot reusable when all have)
+    unsigned long long staged;  // (flags << 32) | (g+1): group g staged (helper -> chain waves);
+                                // flags: 3 bits per node (Pre, post1, post2 rows present) + UP_F3
+};
+#define UP_F_PRE 1u
+#define UP_F_P1 2u
+#define UP_F_P2 4u
+#define UP_F3 (1u << 31)  // the group has a third post-heavy child (node-by-node path)
+
+__device__ __forceinline__ unsigned long long lds_state64(unsigned long long* p) {
+    const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    return v;
+}
 
 template <int SPL>
 struct UpRing {
-    static constexpr int R = UpCfg<SPL>::R;
-    double x[R][64 * SPL];        // Pre in, A_up out
-    double post[R][2][64 * SPL];  // rows of the light children after the heavy one
-    float c[R][64 * SPL];         // AGD cost
-    UpHdr h[R];
-    double post3[64 * SPL];       // a tree root's third post-heavy child
+    UpSlot<SPL> s[UpCfg<SPL>::NS];
     double slut[SM_NUM_W + 1];
 };
 
-// The chain wave reads a whole group (state words first, then the rows: in-order LDS execution
-// makes rows read after a matching state current) with one wait, re-reading the group in the
-// rare case a helper is late.
+// NN consecutive nodes k0.. of a staged group; NN is a compile-time count so the LDS waits are
+// exact; THIRD = the node-by-node path that also applies a root's third post-heavy child.  Only the
+// rows a node has are read (flags, uniform); absent ones stay 0 with S = 0.
+template <int SPL, int NN, bool THIRD>
+__device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0, int j0, int top, int e0,
+                                         double (&x)[Split<SPL>::CS], double* __restrict__ U, int Dpad) {
+    constexpr int CS = Split<SPL>::CS;
+    double pr[NN][CS], p1[NN][CS], p2[NN][CS], Sh[NN], Sp1[NN], Sp2[NN];
+    float cv[NN][CS];
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+        const uint32_t f = flags >> (3 * (k0 + k));
+        Sh[k] = sl.s[k0 + k].Sh;
+#pragma unroll
+        for (int q = 0; q < CS; ++q) {
+            pr[k][q] = 0.0;
+            p1[k][q] = 0.0;
+            p2[k][q] = 0.0;
+            cv[k][q] = sl.c[k0 + k][e0 + q];
+        }
+        Sp1[k] = 0.0;
+        Sp2[k] = 0.0;
+        if (f & UP_F_PRE) lds_read_at<CS>(sl.pre[k0 + k], e0, pr[k]);
+        if (f & UP_F_P1) {
+            Sp1[k] = sl.s[k0 + k].Sp1;
+            lds_read_at<CS>(sl.post1[k0 + k], e0, p1[k]);
+        }
+        if (f & UP_F_P2) {
+            Sp2[k] = sl.s[k0 + k].Sp2;
+            lds_read_at<CS>(sl.post2[k0 + k], e0, p2[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+        double acc[CS];
+#pragma unroll
+        for (int q = 0; q < CS; ++q) {
+            acc[q] = __builtin_fma(Sh[k], x[q], pr[k][q]);
+            acc[q] = __builtin_fma(Sp1[k], p1[k][q], acc[q]);
+            acc[q] = __builtin_fma(Sp2[k], p2[k][q], acc[q]);
+        }
+        if (THIRD && k0 + k == sl.k3) {
+            double r[CS];
+            lds_read_at<CS>(sl.post3, e0, r);
+#pragma unroll
+            for (int q = 0; q < CS; ++q) acc[q] = __builtin_fma(sl.S3, r[q], acc[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < CS; ++q) x[q] = acc[q] + (double)cv[k][q];
+        global_write_at<CS>(U, (uint32_t)(top - (j0 + k)), Dpad, e0, x);
+    }
+}
+
 template <int SPL>
-__device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int len, int lane) {
-    constexpr int R = UpCfg<SPL>::R;
-    constexpr int G = SPL == 1 ? 8 : SPL == 2 ? 6 : 3;  // nodes per group (register budget: 128 VGPRs)
+__device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head, int len, int lane,
+                                              double* __restrict__ U, int Dpad) {
+    constexpr int G = UpCfg<SPL>::G, NS = UpCfg<SPL>::NS, CS = Split<SPL>::CS;
     __builtin_amdgcn_s_setprio(3);
     unsigned spins = 0;
 #ifdef SM_CHAIN_PROF
     const long long t0 = clock64();
     long long tr = 0, tc = 0;
 #endif
-    double x[SPL];
+    const int e0 = (w * 64 + lane) * CS;
+    const int top = head + len - 1;  // chain node j sits at slot top - j (bottom first)
+    const int ngroups = (len + G - 1) / G;
+    double x[CS];
 #pragma unroll
-    for (int k = 0; k < SPL; ++k) x[k] = 0.0;
-    int e0 = 0;  // entry of node j0
-    for (int j0 = 0; j0 < len; j0 += G) {
-        const int ng = min(G, len - j0);
-        int eg[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) eg[g] = e0 + g < R ? e0 + g : e0 + g - R;
-        double pr[G][SPL], p0[G][SPL], S[G][2];
-        float cv[G][SPL];
-        uint32_t fl[G];
-        bool ok;
+    for (int q = 0; q < CS; ++q) x[q] = 0.0;
+    for (int g = 0; g < ngroups; ++g) {
+        UpSlot<SPL>& sl = ring.s[g % NS];
+        const int n = min(G, len - g * G);
 #ifdef SM_CHAIN_PROF
         const long long ta = clock64();
 #endif
-        do {
-            int st[G];
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-                if (g < ng) st[g] = lds_state(&ring.h[eg[g]].state);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                if (g < ng) {
-                    const int e = eg[g];
-                    fl[g] = ring.h[e].fl;
-                    S[g][0] = ring.h[e].s[0];
-                    S[g][1] = ring.h[e].s[1];
-                    lds_row_read<SPL>(ring.x[e], lane, pr[g]);
-                    lds_row_read<SPL>(ring.post[e][0], lane, p0[g]);
-#pragma unroll
-                    for (int k = 0; k < SPL; ++k) cv[g][k] = ring.c[e][lane * SPL + k];
-                }
-            }
-            ok = true;
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-                if (g < ng) ok &= st[g] == 2 * (j0 + g) + 1;
-            PROF_SPIN(spins += ok ? 0 : 1);
-        } while (!ok);
+        unsigned long long st;
+        while ((uint32_t)(st = lds_state64(&sl.staged)) != (uint32_t)(g + 1)) PROF_SPIN(++spins);
+        const uint32_t flags = uniform((uint32_t)(st >> 32));
 #ifdef SM_CHAIN_PROF
         const long long tb = clock64();
         tr += tb - ta;
 #endif
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            if (g < ng) {
-                const int e = eg[g];
-                const uint32_t npost = fl[g] & 3u;
-                double acc[SPL];
-                if (fl[g] & 4u) {
-#pragma unroll
-                    for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S[g][0], x[k], pr[g][k]);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < SPL; ++k) acc[k] = pr[g][k];
-                }
-                if (npost) {
-#pragma unroll
-                    for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S[g][1], p0[g][k], acc[k]);
-                    if (npost > 1) {  // rare (a few % of nodes): one extra LDS round trip
-                        double p[SPL];
-                        const double S2 = ring.h[e].s[2];
-                        lds_row_read<SPL>(ring.post[e][1], lane, p);
-#pragma unroll
-                        for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S2, p[k], acc[k]);
-                        if (npost > 2) {
-                            const double S3 = ring.h[e].s[3];
-                            lds_row_read<SPL>(ring.post3, lane, p);
-#pragma unroll
-                            for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S3, p[k], acc[k]);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) x[k] = acc[k] + (double)cv[g][k];
-                lds_row_write<SPL>(ring.x[e], lane, x);
-            }
+        if (n == G && !(flags & UP_F3)) {
+            up_group<SPL, G, false>(sl, flags, 0, g * G, top, e0, x, U, Dpad);
+        } else {
+            for (int k = 0; k < n; ++k) up_group<SPL, 1, true>(sl, flags, k, g * G + k, top, e0, x, U, Dpad);
         }
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-            if (g < ng) lds_publish_ordered(&ring.h[eg[g]].state, 2 * (j0 + g) + 2);
+        lds_publish_ordered(&sl.done[w], g + 1);
 #ifdef SM_CHAIN_PROF
         tc += clock64() - tb;
 #endif
-        e0 = e0 + G < R ? e0 + G : e0 + G - R;
     }
 #ifdef SM_CHAIN_PROF
-    if (blockIdx.x == 0 && lane == 0)
-        printf("up chain view %d len %d cycles %lld spins %u read %lld compute %lld\n", (int)blockIdx.y, len, clock64() - t0, spins, tr, tc);
+    if (blockIdx.x == 0 && lane == 0 && w == 0)
+        printf("up chain view %d len %d cycles %lld spins %u wait %lld compute %lld\n", (int)blockIdx.y, len,
+               clock64() - t0, spins, tr, tc);
 #endif
     (void)spins;
 }
 
-// Helper waves: every global load of a batch is unconditional (indices clamped into the batch) and
-// all conditional stores come last in the iteration, so the compiler's vmcnt bookkeeping stays
-// exact and a batch's loads remain in flight while the helper waits for the chain.
+// Helper waves: every global load of a group is unconditional (indices clamped, absent children
+// read the path head's rows as L2-resident dummies), so the compiler's vmcnt bookkeeping stays
+// exact and the loads stay in flight while the helper waits for its slot.
 template <int SPL>
 __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int head, int len, int lane,
-                                               const uint32_t* __restrict__ meta32, double* __restrict__ U,
+                                               const uint32_t* __restrict__ meta32, const double* __restrict__ U,
                                                const float* __restrict__ Cst, int Dpad) {
-    constexpr int E = UpCfg<SPL>::E, R = UpCfg<SPL>::R;
-    const int top = head + len - 1;  // node j of the chain sits at slot top - j (bottom first)
-    const int b0 = hh * E;
-    if (b0 >= len) return;
-    MetaVec<E> mv;
-    load_meta<E>(mv, meta32, lane, top - b0, -1, min(E, len - b0));
-    double rp[E][SPL];  // finished rows of the previous occupants
-    int base = b0;
+    constexpr int G = UpCfg<SPL>::G, NS = UpCfg<SPL>::NS;
+    constexpr int NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
+    const int top = head + len - 1;
+    const int ngroups = (len + G - 1) / G;
+    int g = hh;
+    if (g >= ngroups) return;
+    MetaVec<G> mv;
+    load_meta<G>(mv, meta32, lane, top - g * G, -1, min(G, len - g * G));
     for (;;) {
-        const int n = min(E, len - base);
-        // ---- this batch's loads: Pre and C rows (slot-addressed), then the post-heavy children
-        double xr[E][SPL], p0[E][SPL], p1[E][SPL];
-        float cr[E][SPL];
+        const int n = min(G, len - g * G);
+        // ---- this group's loads (all unconditional)
+        double pr[G][SPL], p1[G][SPL], p2[G][SPL], p3[SPL];
+        float cr[G][SPL];
+        uint32_t s3 = (uint32_t)head;
 #pragma unroll
-        for (int k = 0; k < E; ++k) {
+        for (int k = 0; k < G; ++k) {
             const int kk = min(k, n - 1);
-            const uint32_t slot = (uint32_t)(top - (base + kk));
-            load_row<SPL>(U, slot, Dpad, lane, xr[k]);
-            load_crow<SPL>(Cst, slot, Dpad, lane, cr[k]);
-        }
-        uint32_t npost[E];
-#pragma unroll
-        for (int k = 0; k < E; ++k) {
-            const int kk = min(k, n - 1);
+            const uint32_t slot = (uint32_t)(top - (g * G + kk));
             const uint32_t hi = mfield(mv, kk, 3);
             const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-            npost[k] = base + kk > 0 ? nch - 1u - hidx : 0u;
-            // absent posts load the path head's rows (L2-resident dummies): a dummy equal to a
-            // slot loaded above would be folded into a register copy that waits for that load
-            const uint32_t s0 = npost[k] >= 1 ? mfield(mv, kk, 4 + (int)min(hidx + 1u, 3u)) : (uint32_t)head;
-            const uint32_t s1 = npost[k] >= 2 ? mfield(mv, kk, 4 + (int)min(hidx + 2u, 3u)) : (uint32_t)head + 1u;
-            load_row<SPL>(U, s0, Dpad, lane, p0[k]);
-            load_row<SPL>(U, s1, Dpad, lane, p1[k]);
+            const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
+            load_row<SPL>(U, hidx > 0 ? slot : (uint32_t)head + 2u, Dpad, lane, pr[k]);  // Pre rows exist iff hidx > 0
+            load_crow<SPL>(Cst, slot, Dpad, lane, cr[k]);
+            const uint32_t c1 = np >= 1 ? mfield(mv, kk, 4 + (int)min(hidx + 1u, 3u)) : (uint32_t)head;
+            const uint32_t c2 = np >= 2 ? mfield(mv, kk, 4 + (int)min(hidx + 2u, 3u)) : (uint32_t)head + 1u;
+            load_row<SPL>(U, c1, Dpad, lane, p1[k]);
+            load_row<SPL>(U, c2, Dpad, lane, p2[k]);
+            if (np >= 3) s3 = mfield(mv, kk, 7);
         }
-        // ---- previous occupants of this helper's entries (all E existed): wait, read back
-        if (base >= R) {
+        load_row<SPL>(U, s3, Dpad, lane, p3);
+        MetaVec<G> mnext;
+        const int gn = g + NH;
+        const int gl = gn < ngroups ? gn : g;  // unconditional prefetch (clamped)
+        load_meta<G>(mnext, meta32, lane, top - gl * G, -1, min(G, len - gl * G));
+        // ---- wait for the slot, fill it, publish
+        UpSlot<SPL>& sl = ring.s[g % NS];
+        if (g >= NS) lds_wait_all(sl.done, NCW, g - NS + 1);
+        int k3 = -1;
+        double S3 = 0.0;
+        uint32_t flags = 0;
 #pragma unroll
-            for (int k = 0; k < E; ++k) {
-                const int e = b0 + k;
-                lds_wait(&ring.h[e].state, 2 * (base - R + k) + 2, true);
-                lds_row_read<SPL>(ring.x[e], lane, rp[k]);
-            }
-        }
-        // ---- fill the entries and publish
-        vm_drain();
-#pragma unroll
-        for (int k = 0; k < E; ++k) {
+        for (int k = 0; k < G; ++k) {
             if (k < n) {
-                const int e = b0 + k;
-                lds_row_write<SPL>(ring.x[e], lane, xr[k]);
-#pragma unroll
-                for (int q = 0; q < SPL; ++q) ring.c[e][lane * SPL + q] = cr[k][q];
-                if (npost[k] >= 1) lds_row_write<SPL>(ring.post[e][0], lane, p0[k]);
-                if (npost[k] >= 2) lds_row_write<SPL>(ring.post[e][1], lane, p1[k]);
                 const uint32_t lo = mfield(mv, k, 2), hi = mfield(mv, k, 3);
                 const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-                if (npost[k] >= 3) {  // a tree root: one synchronous load per tree
-                    double p3[SPL];
-                    load_row<SPL>(U, mfield(mv, k, 7), Dpad, lane, p3);
-                    lds_row_write<SPL>(ring.post3, lane, p3);
+                const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
+                const uint32_t f = (hidx > 0 ? UP_F_PRE : 0u) | (np >= 1 ? UP_F_P1 : 0u) | (np >= 2 ? UP_F_P2 : 0u);
+                flags |= f << (3 * k);
+                if (f & UP_F_PRE) lds_row_write<SPL>(sl.pre[k], lane, pr[k]);
+                if (f & UP_F_P1) lds_row_write<SPL>(sl.post1[k], lane, p1[k]);
+                if (f & UP_F_P2) lds_row_write<SPL>(sl.post2[k], lane, p2[k]);
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) sl.c[k][lane * SPL + q] = cr[k][q];
+                if (lane < 3) {  // lane 0: heavy child, lanes 1, 2: posts 1, 2
+                    const uint32_t i = hidx + (uint32_t)lane;
+                    const bool live = lane == 0 ? (nch > 0 && g * G + k > 0) : (uint32_t)lane <= np;
+                    (&sl.s[k].Sh)[lane] = live ? ring.slut[cw_of(lo, hi, (int)min(i, 3u))] : 0.0;
                 }
-                const bool has_heavy = base + k > 0;
-                if (lane < 4) {
-                    const uint32_t i = hidx + (uint32_t)lane;  // lane 0: heavy child, lanes 1..3: posts
-                    const bool live = has_heavy && i < nch;
-                    ring.h[e].s[lane] = ring.slut[live ? cw_of(lo, hi, (int)i) : (uint32_t)S_ZERO];
+                if (np >= 3) {
+                    k3 = k;
+                    S3 = ring.slut[cw_of(lo, hi, 3)];
                 }
-                if (lane == 0) ring.h[e].fl = npost[k] | (has_heavy ? 4u : 0u);
             }
         }
-#pragma unroll
-        for (int k = 0; k < E; ++k)
-            if (k < n) lds_publish(&ring.h[b0 + k].state, 2 * (base + k) + 1);
-        // ---- store the previous occupants' A_up rows
-        if (base >= R) {
-#pragma unroll
-            for (int k = 0; k < E; ++k) store_row<SPL>(U, (uint32_t)(top - (base - R + k)), Dpad, lane, rp[k]);
+        if (k3 >= 0) {
+            lds_row_write<SPL>(sl.post3, lane, p3);
+            flags |= UP_F3;
         }
-        const int nb = base + R;
-        if (nb >= len) break;
-        load_meta<E>(mv, meta32, lane, top - nb, -1, min(E, len - nb));
-        base = nb;
-    }
-    // ---- retire the last batch
-    const int n = min(E, len - base);
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-        if (k < n) {
-            const int e = b0 + k;
-            lds_wait(&ring.h[e].state, 2 * (base + k) + 2, true);
-            lds_row_read<SPL>(ring.x[e], lane, rp[k]);
-            store_row<SPL>(U, (uint32_t)(top - (base + k)), Dpad, lane, rp[k]);
+        if (lane == 0) {
+            sl.k3 = k3;
+            sl.S3 = S3;
         }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the group's rows have landed
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __hip_atomic_store(&sl.staged, ((unsigned long long)flags << 32) | (unsigned)(g + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (gn >= ngroups) break;
+        g = gn;
+        mv = mnext;
     }
 }
 
@@ -445,218 +496,190 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     if ((int)blockIdx.x >= V.npaths) return;  // uniform over the block
     const SmPath path = (view ? paths1 : paths0)[blockIdx.x];
     const int head = (int)uniform(path.head), len = (int)uniform(path.len);
-    for (int i = threadIdx.x; i < UpCfg<SPL>::R; i += CHN_THREADS) ring.h[i].state = 0;
+    for (int i = threadIdx.x; i < UpCfg<SPL>::NS; i += CHN_THREADS) {
+        ring.s[i].staged = 0;
+        ring.s[i].done[0] = ring.s[i].done[1] = 0;
+    }
     for (int i = threadIdx.x; i < SM_NUM_W; i += CHN_THREADS) ring.slut[i] = slut_g[i];
     if (threadIdx.x == 0) ring.slut[SM_NUM_W] = 0.0;
     __syncthreads();
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wave == 0)
-        up_chain_wave<SPL>(ring, len, lane);
+    if (wave < Split<SPL>::NCW)
+        up_chain_wave<SPL>(ring, wave, head, len, lane, V.U, Dpad);
     else
-        up_helper_wave<SPL>(ring, wave - 1, head, len, lane, view ? meta1 : meta0, V.U, view ? Cst1 : Cst0, Dpad);
+        up_helper_wave<SPL>(ring, wave - Split<SPL>::NCW, head, len, lane, view ? meta1 : meta0, V.U,
+                            view ? Cst1 : Cst0, Dpad);
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_down_chain
+// k_down_chain.  Chain node j = slot head + j (root side first).
 // ---------------------------------------------------------------------------------------------
 template <int SPL>
 struct DownCfg {
-    static constexpr int E = SPL == 1 ? 8 : SPL == 2 ? 6 : 3;
-    static constexpr int R = CHN_HELPERS * E;
+    static constexpr int G = 8;
+    static constexpr int NS = SPL == 4 ? 4 : 8;
 };
 
-struct DownHdr {
-    int state;
-    uint32_t pix;
-    uint32_t store;  // row needed by light children (or the debug path)
-    uint32_t pad;
-    double S;
+template <int SPL>
+struct DownSlot {
+    static constexpr int G = DownCfg<SPL>::G;
+    double x[G][64 * SPL];  // T = S2 * A_up in, A out
+    double S[G];
+    uint32_t pix[G];
+    uint32_t st[G];         // row needed by light children (or the debug path)
+    int staged;             // g+1: group g staged          (helper -> chain waves)
+    int done[2];            // g+1: chain wave w computed g (chain wave -> owner helper)
+    int freed;              // g+1: slot of group g free     (owner helper -> next helper)
 };
 
 template <int SPL>
 struct DownRing {
-    static constexpr int R = DownCfg<SPL>::R;
-    double x[R][64 * SPL];  // T = S2 * A_up in, A out
-    DownHdr h[R];
+    DownSlot<SPL> s[DownCfg<SPL>::NS];
     double slut[SM_NUM_W + 1];
     double s2lut[SM_NUM_W];
 };
 
+template <int SPL, int NN>
+__device__ __forceinline__ void down_group(DownSlot<SPL>& sl, int k0, int e0, double (&x)[Split<SPL>::CS]) {
+    constexpr int CS = Split<SPL>::CS;
+    double t[NN][CS], S[NN];
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+        S[k] = sl.S[k0 + k];
+        lds_read_at<CS>(sl.x[k0 + k], e0, t[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+#pragma unroll
+        for (int q = 0; q < CS; ++q) x[q] = __builtin_fma(S[k], x[q], t[k][q]);
+        lds_write_at<CS>(sl.x[k0 + k], e0, x);
+    }
+}
+
 template <int SPL>
-__device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int len, int lane, const double* __restrict__ U,
-                                                uint32_t hparent, int Dpad) {
-    constexpr int R = DownCfg<SPL>::R;
+__device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int len, int lane,
+                                                const double* __restrict__ U, uint32_t hparent, int Dpad) {
+    constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, CS = Split<SPL>::CS;
     __builtin_amdgcn_s_setprio(3);
     unsigned spins = 0;
 #ifdef SM_CHAIN_PROF
     const long long t0 = clock64();
     long long tr = 0, tc = 0;
 #endif
-    double x[SPL];
+    const int e0 = (w * 64 + lane) * CS;
+    double x[CS];
     if (hparent != SM_NONE) {
-        load_row<SPL>(U, hparent, Dpad, lane, x);  // A(parent): finished in an earlier round
+        global_read_at<CS>(U, hparent, Dpad, e0, x);  // A(parent): finished in an earlier round
+        vm_drain();
     } else {
 #pragma unroll
-        for (int k = 0; k < SPL; ++k) x[k] = 0.0;  // root: S = 0, T = A_up -> A(root) = A_up(root)
+        for (int q = 0; q < CS; ++q) x[q] = 0.0;  // root: S = 0, T = A_up -> A(root) = A_up(root)
     }
-    int e0 = 0;
-    for (int j0 = 0; j0 < len; j0 += CHN_G) {
-        const int ng = min(CHN_G, len - j0);
-        int eg[CHN_G];
-#pragma unroll
-        for (int g = 0; g < CHN_G; ++g) eg[g] = e0 + g < R ? e0 + g : e0 + g - R;
-        double t[CHN_G][SPL], S[CHN_G];
-        bool ok;
+    const int ngroups = (len + G - 1) / G;
+    for (int g = 0; g < ngroups; ++g) {
+        DownSlot<SPL>& sl = ring.s[g % NS];
+        const int n = min(G, len - g * G);
 #ifdef SM_CHAIN_PROF
         const long long ta = clock64();
 #endif
-        do {
-            int st[CHN_G];
-#pragma unroll
-            for (int g = 0; g < CHN_G; ++g)
-                if (g < ng) st[g] = lds_state(&ring.h[eg[g]].state);
-#pragma unroll
-            for (int g = 0; g < CHN_G; ++g) {
-                if (g < ng) {
-                    S[g] = ring.h[eg[g]].S;
-                    lds_row_read<SPL>(ring.x[eg[g]], lane, t[g]);
-                }
-            }
-            ok = true;
-#pragma unroll
-            for (int g = 0; g < CHN_G; ++g)
-                if (g < ng) ok &= st[g] == 2 * (j0 + g) + 1;
-            PROF_SPIN(spins += ok ? 0 : 1);
-        } while (!ok);
+        while (lds_state(&sl.staged) != g + 1) PROF_SPIN(++spins);
 #ifdef SM_CHAIN_PROF
         const long long tb = clock64();
         tr += tb - ta;
 #endif
-#pragma unroll
-        for (int g = 0; g < CHN_G; ++g) {
-            if (g < ng) {
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) x[k] = __builtin_fma(S[g], x[k], t[g][k]);
-                lds_row_write<SPL>(ring.x[eg[g]], lane, x);
-            }
+        if (n == G) {
+            down_group<SPL, G>(sl, 0, e0, x);
+        } else {
+            for (int k = 0; k < n; ++k) down_group<SPL, 1>(sl, k, e0, x);
         }
-#pragma unroll
-        for (int g = 0; g < CHN_G; ++g)
-            if (g < ng) lds_publish_ordered(&ring.h[eg[g]].state, 2 * (j0 + g) + 2);
+        lds_publish_ordered(&sl.done[w], g + 1);
 #ifdef SM_CHAIN_PROF
         tc += clock64() - tb;
 #endif
-        e0 = e0 + CHN_G < R ? e0 + CHN_G : e0 + CHN_G - R;
     }
 #ifdef SM_CHAIN_PROF
-    if (blockIdx.x == 0 && lane == 0)
-        printf("down chain view %d len %d cycles %lld spins %u read %lld compute %lld\n", (int)blockIdx.y, len, clock64() - t0, spins, tr, tc);
+    if (blockIdx.x == 0 && lane == 0 && w == 0)
+        printf("down chain view %d len %d cycles %lld spins %u wait %lld compute %lld\n", (int)blockIdx.y, len,
+               clock64() - t0, spins, tr, tc);
 #endif
     (void)spins;
-}
-
-// finished entries of a helper: wait, read back, WTA (lane k < n gets node k's result)
-template <int SPL>
-struct DownDone {
-    double xs[DownCfg<SPL>::E][SPL];
-    double mn;
-    int mi;
-};
-
-template <int SPL>
-__device__ __forceinline__ void down_collect(DownRing<SPL>& ring, int b0, int jbase, int n, int lane, int dcall,
-                                             DownDone<SPL>& d) {
-    constexpr int E = DownCfg<SPL>::E;
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-        if (k < n) {
-            lds_wait(&ring.h[b0 + k].state, 2 * (jbase + k) + 2, true);
-            lds_row_read<SPL>(ring.x[b0 + k], lane, d.xs[k]);
-        } else {
-#pragma unroll
-            for (int q = 0; q < SPL; ++q) d.xs[k][q] = 0.0;
-        }
-    }
-    wta_chunk<SPL, E>(d.xs, lane, lane * SPL, dcall, d.mn, d.mi);
-}
-
-// stores of collected entries (must read ring.pix/store before the entries are refilled)
-template <int SPL>
-__device__ __forceinline__ void down_store(const DownDone<SPL>& d, int head, int jbase, int n, int lane,
-                                           const uint32_t (&st)[DownCfg<SPL>::E], uint32_t pix, double* __restrict__ U,
-                                           const WalkView& V, int Dpad, int dglob0, int store_all) {
-    constexpr int E = DownCfg<SPL>::E;
-#pragma unroll
-    for (int k = 0; k < E; ++k)
-        if (k < n && (store_all || st[k])) store_row<SPL>(U, (uint32_t)(head + jbase + k), Dpad, lane, d.xs[k]);
-    if (lane < n) {
-        V.idx[pix] = dglob0 + d.mi;
-        V.minc[pix] = d.mn;
-        V.disp[pix] = (float)(dglob0 + d.mi);
-    }
 }
 
 template <int SPL>
 __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, int head, int len, int lane,
                                                  uint32_t hparent, const uint32_t* __restrict__ meta32,
                                                  const WalkView& V, int Dpad, int dcall, int dglob0, int store_all) {
-    constexpr int E = DownCfg<SPL>::E, R = DownCfg<SPL>::R;
-    const int b0 = hh * E;
-    if (b0 >= len) return;
+    constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
+    const int ngroups = (len + G - 1) / G;
+    int g = hh;
+    if (g >= ngroups) return;
     double* __restrict__ U = V.U;
-    DownDone<SPL> done;
-    uint32_t st[E], pix = 0;
-    int base = b0;
+    double u[G][SPL];
+    MetaVec<G> mv;
+    auto issue = [&](int gg) {
+        const int n = min(G, len - gg * G);
+#pragma unroll
+        for (int k = 0; k < G; ++k) load_row<SPL>(U, (uint32_t)(head + gg * G + min(k, n - 1)), Dpad, lane, u[k]);
+        load_meta<G>(mv, meta32, lane, head + gg * G, 1, n);
+    };
+    issue(g);
     for (;;) {
-        const int n = min(E, len - base);
-        // ---- this batch's loads (unconditional): A_up rows and metadata
-        double u[E][SPL];
+        const int n = min(G, len - g * G);
+        DownSlot<SPL>& sl = ring.s[g % NS];
+        if (g >= NS) lds_wait(&sl.freed, g - NS + 1, true);
+        // ---- stage T = S2 * A_up and S (root: T = A_up, S = 0)
 #pragma unroll
-        for (int k = 0; k < E; ++k) load_row<SPL>(U, (uint32_t)(head + base + min(k, n - 1)), Dpad, lane, u[k]);
-        MetaVec<E> mv;
-        load_meta<E>(mv, meta32, lane, head + base, 1, n);
-        // ---- previous occupants: wait, read back, WTA; keep their store flags and pixels
-        if (base >= R) {
-            down_collect<SPL>(ring, b0, base - R, E, lane, dcall, done);
-#pragma unroll
-            for (int k = 0; k < E; ++k) st[k] = ring.h[b0 + k].store;
-            pix = ring.h[b0 + min(lane, E - 1)].pix;
-        }
-        // ---- fill and publish
-        vm_drain();
-#pragma unroll
-        for (int k = 0; k < E; ++k) {
+        for (int k = 0; k < G; ++k) {
             if (k < n) {
-                const int e = b0 + k;
-                const bool root = base + k == 0 && hparent == SM_NONE;
+                const bool root = g * G + k == 0 && hparent == SM_NONE;
                 const uint32_t wp = lo_wp(mfield(mv, k, 2));
-                const double S = root ? 0.0 : ring.slut[wp];
                 const double S2 = ring.s2lut[wp];
                 double t[SPL];
 #pragma unroll
                 for (int q = 0; q < SPL; ++q) t[q] = root ? u[k][q] : S2 * u[k][q];
-                lds_row_write<SPL>(ring.x[e], lane, t);
+                lds_row_write<SPL>(sl.x[k], lane, t);
                 if (lane == 0) {
-                    ring.h[e].S = S;
-                    ring.h[e].pix = mfield(mv, k, 0);
-                    ring.h[e].store = hi_light(mfield(mv, k, 3));
+                    sl.S[k] = root ? 0.0 : ring.slut[wp];
+                    sl.pix[k] = mfield(mv, k, 0);
+                    sl.st[k] = hi_light(mfield(mv, k, 3));
                 }
             }
         }
+        lds_publish(&sl.staged, g + 1);
+        // ---- next group's loads go out now (unconditional, clamped): a full chain lap of lead
+        const int gn = g + NH;
+        issue(gn < ngroups ? gn : g);
+        // ---- the chain's results: WTA, stores, free the slot
+        lds_wait_all(sl.done, NCW, g + 1);
+        double xs[G][SPL];
 #pragma unroll
-        for (int k = 0; k < E; ++k)
-            if (k < n) lds_publish(&ring.h[b0 + k].state, 2 * (base + k) + 1);
-        // ---- the previous occupants' stores
-        if (base >= R) down_store<SPL>(done, head, base - R, E, lane, st, pix, U, V, Dpad, dglob0, store_all);
-        if (base + R >= len) break;
-        base += R;
+        for (int k = 0; k < G; ++k) {
+            if (k < n) {
+                lds_row_read<SPL>(sl.x[k], lane, xs[k]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) xs[k][q] = 0.0;
+            }
+        }
+        const uint32_t pix = sl.pix[min(lane, G - 1)];
+        uint32_t st[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) st[k] = sl.st[k];
+        lds_publish(&sl.freed, g + 1);
+        double mn;
+        int mi;
+        wta_chunk<SPL, G>(xs, lane, lane * SPL, dcall, mn, mi);
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+            if (k < n && (store_all || st[k])) store_row<SPL>(U, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
+        if (lane < n) {
+            V.idx[pix] = dglob0 + mi;
+            V.minc[pix] = mn;
+            V.disp[pix] = (float)(dglob0 + mi);
+        }
+        if (gn >= ngroups) break;
+        g = gn;
     }
-    const int n = min(E, len - base);
-    down_collect<SPL>(ring, b0, base, n, lane, dcall, done);
-#pragma unroll
-    for (int k = 0; k < E; ++k) st[k] = ring.h[b0 + k].store;
-    pix = ring.h[b0 + min(lane, E - 1)].pix;
-    down_store<SPL>(done, head, base, n, lane, st, pix, U, V, Dpad, dglob0, store_all);
 }
 
 template <int SPL>
@@ -676,7 +699,10 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     const SmPath path = (view ? paths1 : paths0)[blockIdx.x];
     const int head = (int)uniform(path.head), len = (int)uniform(path.len);
     const uint32_t hparent = uniform(meta32[(size_t)head * 8 + 1]);
-    for (int i = threadIdx.x; i < DownCfg<SPL>::R; i += CHN_THREADS) ring.h[i].state = 0;
+    for (int i = threadIdx.x; i < DownCfg<SPL>::NS; i += CHN_THREADS) {
+        ring.s[i].staged = ring.s[i].freed = 0;
+        ring.s[i].done[0] = ring.s[i].done[1] = 0;
+    }
     for (int i = threadIdx.x; i < SM_NUM_W; i += CHN_THREADS) {
         ring.slut[i] = slut_g[i];
         ring.s2lut[i] = s2lut_g[i];
@@ -684,10 +710,11 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     if (threadIdx.x == 0) ring.slut[SM_NUM_W] = 0.0;
     __syncthreads();
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wave == 0)
-        down_chain_wave<SPL>(ring, len, lane, V.U, hparent, Dpad);
+    if (wave < Split<SPL>::NCW)
+        down_chain_wave<SPL>(ring, wave, len, lane, V.U, hparent, Dpad);
     else
-        down_helper_wave<SPL>(ring, wave - 1, head, len, lane, hparent, meta32, V, Dpad, dcall, dglob0, store_all);
+        down_helper_wave<SPL>(ring, wave - Split<SPL>::NCW, head, len, lane, hparent, meta32, V, Dpad, dcall, dglob0,
+                              store_all);
 }
 
 // ---------------------------------------------------------------------------------------------
