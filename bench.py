@@ -87,8 +87,7 @@ def main():
         dbeg = rank * Dloc
     elif args.mode == "strong":
         Dtot = 256 if args.disp == 128 else args.disp
-        Dloc = Dtot // world
-        dbeg = rank * Dloc
+        dbeg, Dloc = sm.shard_range(Dtot, world, rank)
     else:  # batch
         Dloc = Dtot = args.disp
         dbeg = 0
@@ -119,16 +118,18 @@ def main():
     ctx.synchronize()
     torch.cuda.synchronize()
     stage_acc = {}
-    up_ms = down_ms = up_b = down_b = 0.0
+    kacc = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.match_async(Dloc, params)
-        ctx.synchronize()  # per-step sync: the per-stage HIP-event timings are read here
-        st = ctx.stage_times()
-        for k, v in st.items():
+        ctx.synchronize()  # per-step sync: the per-launch HIP-event timings are read here
+        for k, v in ctx.stage_times().items():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
-        fs = ctx.filter_stats()
-        up_ms += fs["up_ms"]; down_ms += fs["down_ms"]; up_b += fs["up_bytes"]; down_b += fs["down_bytes"]
+        for k, v in ctx.kernel_stats().items():
+            a = kacc.setdefault(k, dict(launches=0, ms=0.0, voxels=0.0, bytes_per_voxel=v["bytes_per_voxel"]))
+            a["launches"] += v["launches"]
+            a["ms"] += v["ms"]
+            a["voxels"] += v["voxels"]
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -140,15 +141,20 @@ def main():
     ms_step = elapsed * 1e3 / args.steps
     units_per_step = W * H * (Dtot_frame * (world if args.mode == "batch" else 1))
     value = units_per_step * args.steps / elapsed
-    dom = "k_up_walk" if up_ms >= down_ms else "k_down_walk"
-    dom_ms, dom_b = (up_ms, up_b) if up_ms >= down_ms else (down_ms, down_b)
-    achieved = dom_b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    # roofline: the tree-filter kernel family with the largest summed launch time; algorithmic
+    # bytes = voxels it processed x SURVEY.md 8(d) bytes/voxel (DESIGN.md "Roofline accounting")
+    dom = max(kacc, key=lambda k: kacc[k]["ms"])
+    d = kacc[dom]
+    dom_bytes = d["voxels"] * d["bytes_per_voxel"]
+    achieved = dom_bytes / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
+    filt_ms = sum(v["ms"] for v in kacc.values())
+    filt_bytes = sum(v["voxels"] * v["bytes_per_voxel"] for v in kacc.values())
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
             with open(tf) as f:
-                traffic = json.load(f).get(dom)
+                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     line = {
@@ -170,7 +176,12 @@ def main():
                    "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "bytes_per_step": dom_b / args.steps, "kernel_ms_per_step": dom_ms / args.steps},
+                     "launches_per_step": d["launches"] / args.steps,
+                     "alg_bytes_per_launch": dom_bytes / max(d["launches"], 1),
+                     "avg_launch_ms": d["ms"] / max(d["launches"], 1),
+                     "tree_filter": {"alg_bytes_per_step": filt_bytes / args.steps, "ms_per_step": filt_ms / args.steps,
+                                     "achieved": filt_bytes / (filt_ms * 1e-3) / 1e9 if filt_ms > 0 else 0.0}},
+        "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in kacc.items()},
         "stages_ms": {k: v / args.steps for k, v in stage_acc.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -63,7 +63,16 @@ typedef struct {
     int cost_kind;     /* sm_cost_kind                                              */
     int disp_begin;    /* first global disparity of this call (D sharding)          */
     int disp_total;    /* total disparities across all shards (== D unsharded)      */
+    int post;          /* sm_post bits applied to the final maps (default 0)         */
 } sm_params;
+
+/* Post-processing of the final (cross-rank reduced) disparity maps. */
+typedef enum {
+    SM_POST_LR_CHECK = 1  /* stereo3dmst's left-right check, fill=false: a left pixel whose
+                             disparity d has x-d outside the image, d outside [0, disp_total),
+                             or |d - right(x-d)| > 1 is set to 0 in left_disp (idx/min untouched)
+                             (Stereo3DMST.cpp:632-662, applied at :904) */
+} sm_post;
 
 typedef struct sm_ctx sm_ctx;
 
@@ -118,14 +127,28 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t
  * [5] cross-rank reduce, [6] total.  n = capacity of out. Returns entries written. */
 int sm_stage_times(sm_ctx* ctx, float* out, int n);
 
-/* Per-launch statistics for the roofline: bytes the dominant kernels must move
- * (algorithmic), and their summed durations over the last call. */
+/* Tree-filter pass totals of the last call: summed HIP-event durations of the leaf->root
+ * and root->leaf passes, and their algorithmic HBM bytes at SURVEY.md 8(d)'s per-voxel
+ * figures (leaf->root = K1 cost 4 B + K2 up 8 B; root->leaf = K3 down 8 B + K4 WTA 4 B). */
 typedef struct {
-    double up_ms, down_ms;             /* summed kernel time of the tree-filter passes        */
-    double up_bytes, down_bytes;       /* algorithmic HBM bytes of those passes               */
+    double up_ms, down_ms;
+    double up_bytes, down_bytes;
     int up_launches, down_launches;
 } sm_filter_stats;
 sm_status sm_get_filter_stats(sm_ctx* ctx, sm_filter_stats* out);
+
+/* Per kernel family of the tree filter (k_up_walk, k_up_pre, k_up_chain, k_down_chain,
+ * k_down_walk): launches, summed HIP-event duration (ms) over the last call, voxels processed
+ * (path nodes x disparities, both views) and algorithmic bytes per voxel (DESIGN.md
+ * "Roofline accounting").  Returns the number of entries written (<= n). */
+typedef struct {
+    char name[32];
+    int launches;
+    double ms;
+    double voxels;
+    double bytes_per_voxel;
+} sm_kernel_stat;
+int sm_get_kernel_stats(sm_ctx* ctx, sm_kernel_stat* out, int n);
 
 /* Multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------- */
 #define SM_UNIQUE_ID_BYTES 128

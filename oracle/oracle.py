@@ -44,6 +44,7 @@ def lib():
         L.orc_s2_lut.restype = ctypes.POINTER(ctypes.c_double)
         L.orc_agd_color_term.argtypes = [c_int]
         L.orc_agd_color_term.restype = c_float
+        L.orc_lr_check.argtypes = [vp, vp, c_int, c_int, c_int]
         _LIB = L
     return _LIB
 
@@ -185,3 +186,12 @@ def ref_segment_graph(W, H, wR, wD, c):
     np.bitwise_or.at(mask, oa[right], 1)
     np.bitwise_or.at(mask, oa[down], 2)
     return dict(mask=mask, nsets=nsets, sorted_a=oa, sorted_b=ob, sorted_w=ow, sorted_mask=om)
+
+
+def lr_check(left_disp, right_disp, max_disp):
+    """Stereo3DMST.cpp:632-662 with fill=false (as at :904); returns a new left map."""
+    left = np.ascontiguousarray(left_disp, dtype=np.float32).copy()
+    right = np.ascontiguousarray(right_disp, dtype=np.float32)
+    H, W = left.shape
+    lib().orc_lr_check(_ptr(left), _ptr(right), W, H, int(max_disp))
+    return left

@@ -384,3 +384,21 @@ void orc_tree_filter(int W, int H, int nd, int d0, int ntrees, const int32_t* tr
         free(pidx);
     }
 }
+
+/* Left-right consistency check without fill (Stereo3DMST.cpp:632-662, called at :904 with
+ * fill=false): d = round(left); a pixel with x-d < 0, d < 0, d >= max_disp or
+ * |left - right(x-d)| > 1 becomes 0.  Only left is written and only right is read across
+ * pixels, so the serial loop equals the reference's OpenMP one. */
+void orc_lr_check(float* left, const float* right, int W, int H, int max_disp) {
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const long idx = (long)y * W + x;
+            const float df = left[idx];
+            const int d = (int)round(df);
+            if (x - d >= 0 && d >= 0 && d < max_disp) {
+                if (fabsf(df - right[idx - d]) > 1.0f) left[idx] = 0.0f;
+            } else {
+                left[idx] = 0.0f;
+            }
+        }
+}

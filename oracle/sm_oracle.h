@@ -73,6 +73,9 @@ const double* orc_s2_lut(void);
 /* AGD color term table a(l1) = 0.11f*fminf((float)(l1*0.33333333333), 7.0f), l1 in [0,765]. */
 float orc_agd_color_term(int l1);
 
+/* Stereo3DMST.cpp:632-662 (fill=false, as called at :904): in place on left. */
+void orc_lr_check(float* left, const float* right, int W, int H, int max_disp);
+
 #ifdef __cplusplus
 }
 #endif

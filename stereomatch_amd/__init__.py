@@ -13,9 +13,22 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (SM_COST_AGD, Context, StereoMSTError, default_params, device_count, lib)  # noqa: F401
+from ._lib import (SM_COST_AGD, SM_POST_LR_CHECK, Context, StereoMSTError, default_params, device_count,  # noqa: F401
+                   lib)
 
-__all__ = ["stereo3dmst", "startTimer", "getTimer", "Context", "default_params", "StereoMSTError", "device_count"]
+__all__ = ["stereo3dmst", "startTimer", "getTimer", "Context", "default_params", "StereoMSTError", "device_count",
+           "shard_range"]
+
+
+def shard_range(d_total, nranks, rank):
+    """Contiguous ascending disparity shard of `rank`: (d0, D).  Ranks take
+    [g*Dt/G, (g+1)*Dt/G) so the cross-rank (cost, global d) minimum reproduces the strict-<
+    first minimum over ascending d (PatchMatchStereoGPU.cu:1712)."""
+    if nranks < 1 or not 0 <= rank < nranks or d_total < nranks:
+        raise ValueError("need 0 <= rank < nranks <= d_total")
+    d0 = rank * d_total // nranks
+    d1 = (rank + 1) * d_total // nranks
+    return d0, d1 - d0
 
 _default_ctx = None
 _timer = ctypes.c_double(0.0)
@@ -33,9 +46,11 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
 
     left_img/right_img: HxWx3 uint8 BGR (cv::Mat CV_8UC3).  Returns (left_disp, right_disp),
     float32 HxW in [0, Dmax-1]: the strict-< winner-take-all slice of the MST-aggregated
-    AGD cost.  Like the reference, an unsupported data_cost prints a
-    message and returns allocated-but-unset maps (:756-759); the names are only forwarded
-    to the cost source and are unused by the AGD cost.
+    AGD cost, with the reference's output step applied: the left map is
+    left-right checked without fill (:904, :632-662), the right map is returned unchecked.
+    Like the reference, an unsupported data_cost prints a message and returns
+    allocated-but-unset maps (:756-759); the names are only forwarded to the cost source and
+    are unused by the AGD cost.
     """
     H, W = left_img.shape[:2]
     left_disp = np.empty((H, W), np.float32)
@@ -47,7 +62,7 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
     if data_cost != "AGD":
         print("wrong data cost")
         return left_disp, right_disp
-    out = _ctx().match(left_img, right_img, int(Dmax))
+    out = _ctx().match(left_img, right_img, int(Dmax), default_params(post=SM_POST_LR_CHECK))
     left_disp[...] = out["left"]["disp"]
     right_disp[...] = out["right"]["disp"]
     return left_disp, right_disp

@@ -16,6 +16,7 @@ SM_OK, SM_ERR_ARG, SM_ERR_HIP, SM_ERR_OOM, SM_ERR_RCCL, SM_ERR_STATE, SM_ERR_NOD
 STATUS_NAMES = {0: "SM_OK", 1: "SM_ERR_ARG", 2: "SM_ERR_HIP", 3: "SM_ERR_OOM", 4: "SM_ERR_RCCL",
                 5: "SM_ERR_STATE", 6: "SM_ERR_NODEVICE"}
 SM_COST_AGD, SM_COST_VOLUME = 0, 1
+SM_POST_LR_CHECK = 1
 SM_UNIQUE_ID_BYTES = 128
 
 
@@ -27,12 +28,17 @@ class SmConfig(ctypes.Structure):
 class SmParams(ctypes.Structure):
     _fields_ = [("gamma", ctypes.c_float), ("c", ctypes.c_float), ("min_size", ctypes.c_int),
                 ("median_ksize", ctypes.c_int), ("cost_kind", ctypes.c_int), ("disp_begin", ctypes.c_int),
-                ("disp_total", ctypes.c_int)]
+                ("disp_total", ctypes.c_int), ("post", ctypes.c_int)]
 
 
 class SmFilterStats(ctypes.Structure):
     _fields_ = [("up_ms", ctypes.c_double), ("down_ms", ctypes.c_double), ("up_bytes", ctypes.c_double),
                 ("down_bytes", ctypes.c_double), ("up_launches", ctypes.c_int), ("down_launches", ctypes.c_int)]
+
+
+class SmKernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int), ("ms", ctypes.c_double),
+                ("voxels", ctypes.c_double), ("bytes_per_voxel", ctypes.c_double)]
 
 
 class StereoMSTError(RuntimeError):
@@ -72,6 +78,7 @@ def lib():
         "sm_aggregate_debug": ([vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp], ci),
         "sm_stage_times": ([vp, vp, ci], ci),
         "sm_get_filter_stats": ([vp, ctypes.POINTER(SmFilterStats)], ci),
+        "sm_get_kernel_stats": ([vp, ctypes.POINTER(SmKernelStat), ci], ci),
         "sm_comm_unique_id": ([vp], ci),
         "sm_comm_init": ([vp, ci, ci, vp], ci),
         "sm_comm_destroy": ([vp], ci),
@@ -185,6 +192,13 @@ class Context:
         s = SmFilterStats()
         self._check(lib().sm_get_filter_stats(self.h, ctypes.byref(s)))
         return {k: getattr(s, k) for k, _ in SmFilterStats._fields_}
+
+    def kernel_stats(self):
+        """Per kernel family of the tree filter (last call): launches, ms, voxels, bytes/voxel."""
+        buf = (SmKernelStat * 8)()
+        n = lib().sm_get_kernel_stats(self.h, buf, 8)
+        return {buf[i].name.decode(): dict(launches=buf[i].launches, ms=buf[i].ms, voxels=buf[i].voxels,
+                                           bytes_per_voxel=buf[i].bytes_per_voxel) for i in range(n)}
 
     # -- stages ---------------------------------------------------------------------------
     def cost_volume(self, left, right, d0, D):

@@ -28,7 +28,7 @@ hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gi
 
 namespace {
 
-constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2 + SM_NBUCKETS + (SM_NBUCKETS + 1);
+constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2 + SM_NBUCKETS + (SM_NBUCKETS + 1) + SM_NBUCKETS;
 
 struct DevBuf {
     void* p = nullptr;
@@ -54,12 +54,16 @@ struct sm_ctx {
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
     struct HostRounds {
         uint32_t nrounds = 0, npaths = 0, n_has_light = 0;
-        std::vector<uint32_t> begin, maxlen, seg_begin;  // per bucket
+        std::vector<uint32_t> begin, maxlen, seg_begin, nodes;  // per bucket
     } layout[2];
     hipEvent_t ev[8] = {};
-    std::vector<hipEvent_t> up_ev, down_ev;
-    int n_up = 0, n_down = 0;
+    // tree-filter launch timing: event k brackets interval k = [fev[k], fev[k+1]) of family fam[k]
+    std::vector<hipEvent_t> fev;
+    std::vector<int> fam;
+    std::vector<double> fam_vox;  // voxels of interval k
+    int nfev = 0;
     sm_filter_stats stats{};
+    sm_kernel_stat kstats[5]{};
     float stage_ms[7] = {0};
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -126,6 +130,7 @@ sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
         return fail(ctx, SM_ERR_ARG, "only gamma=1/12 (embedded correctly-rounded tables) is supported");
     if (D < 1 || D > 256) return fail(ctx, SM_ERR_ARG, "D must be in [1, 256] per call (shard larger ranges)");
     if (p->disp_begin < 0) return fail(ctx, SM_ERR_ARG, "disp_begin < 0");
+    if (p->post & ~SM_POST_LR_CHECK) return fail(ctx, SM_ERR_ARG, "unknown post-processing bits");
     return SM_OK;
 }
 
@@ -276,6 +281,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.n_has_light = R + 3 * SM_NBUCKETS + 2;
         L.round_maxlen = R + 3 * SM_NBUCKETS + 3;
         L.seg_begin = R + 4 * SM_NBUCKETS + 3;
+        L.round_nodes = R + 5 * SM_NBUCKETS + 4;
         L.segtab = P<uint2>(ctx->segtab[v]);
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
@@ -286,13 +292,14 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
     HIPC(hipStreamSynchronize(ctx->st));
     for (int v = 0; v < 2; ++v) {
         auto& L = ctx->layout[v];
-        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); continue; }
+        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); L.nodes.assign(SM_NBUCKETS, 0); continue; }
         const uint32_t* R = ctx->h_rounds + v * RREC;
         L.nrounds = R[3 * SM_NBUCKETS + 1];
         L.n_has_light = R[3 * SM_NBUCKETS + 2];
         L.begin.assign(R, R + SM_NBUCKETS + 1);
         L.maxlen.assign(R + 3 * SM_NBUCKETS + 3, R + 4 * SM_NBUCKETS + 3);
         L.seg_begin.assign(R + 4 * SM_NBUCKETS + 3, R + 5 * SM_NBUCKETS + 4);
+        L.nodes.assign(R + 5 * SM_NBUCKETS + 4, R + 6 * SM_NBUCKETS + 4);
         L.npaths = R[SM_NBUCKETS];
         if (L.nrounds == 0 || L.npaths == 0) return fail(ctx, SM_ERR_STATE, "layout produced no paths");
     }
@@ -350,24 +357,58 @@ sm_status ensure_events(sm_ctx* ctx, std::vector<hipEvent_t>& evs, size_t n) {
     return SM_OK;
 }
 
+// kernel families of the tree filter and their algorithmic bytes per voxel (SURVEY.md 8(d):
+// K1 cost write 4 B, K2 up 8 B, K3 down 8 B, K4 WTA 4 B; DESIGN.md "Roofline accounting")
+enum { KF_UP_WALK, KF_UP_PRE, KF_UP_CHAIN, KF_DOWN_CHAIN, KF_DOWN_WALK, KF_N };
+const char* const kf_name[KF_N] = {"k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk"};
+const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0};
+
+// record the event that closes the current interval (family f, voxels) and opens the next
+sm_status mark(sm_ctx* ctx, int f, double vox) {
+    CHECK(ensure_events(ctx, ctx->fev, (size_t)ctx->nfev + 1));
+    HIPC(hipEventRecord(ctx->fev[ctx->nfev], ctx->st));
+    if (ctx->nfev > 0) {
+        ctx->fam.push_back(f);
+        ctx->fam_vox.push_back(vox);
+    }
+    ++ctx->nfev;
+    return SM_OK;
+}
+
+double bucket_voxels(sm_ctx* ctx, uint32_t r, bool long_paths, int nviews, int D) {
+    double n = 0;
+    for (int v = 0; v < nviews; ++v) {
+        const auto& L = ctx->layout[v];
+        if (r < L.nrounds) n += L.nodes[2 * r + (long_paths ? 0 : 1)];
+    }
+    return n * D;
+}
+
 // one light-depth round of the up pass: short paths by the chunked walkers, long paths by the
 // chain engine (pre-fold kernel + one workgroup per path)
 sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
     set_bucket(ctx, a, r, false, nviews);
     HIPC(launch_up(ctx->st, a, spl, false));
+    CHECK(mark(ctx, KF_UP_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall)));
     set_bucket(ctx, a, r, true, nviews);
-    HIPC(launch_up_long(ctx->st, a, spl));
+    const double vl = bucket_voxels(ctx, r, true, nviews, a.dcall);
+    HIPC(launch_up_pre(ctx->st, a, spl));
+    CHECK(mark(ctx, KF_UP_PRE, vl));
+    HIPC(launch_up_chain(ctx->st, a, spl));
+    CHECK(mark(ctx, KF_UP_CHAIN, vl));
     return SM_OK;
 }
 
 sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews, bool store_all) {
     set_bucket(ctx, a, r, true, nviews);
     HIPC(launch_down_long(ctx->st, a, spl, store_all ? 1 : 0));
+    CHECK(mark(ctx, KF_DOWN_CHAIN, bucket_voxels(ctx, r, true, nviews, a.dcall)));
     set_bucket(ctx, a, r, false, nviews);
     if (store_all)
         HIPC(launch_down_debug(ctx->st, a, spl, false));
     else
         HIPC(launch_down(ctx->st, a, spl, false));
+    CHECK(mark(ctx, KF_DOWN_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall)));
     return SM_OK;
 }
 
@@ -391,34 +432,41 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     CHECK(ensure_filter_bufs(ctx, Dpad));
     uint32_t nr = 0;
     for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
-    CHECK(ensure_events(ctx, ctx->up_ev, 2 * nr));
-    CHECK(ensure_events(ctx, ctx->down_ev, 2 * nr));
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
-    ctx->n_up = ctx->n_down = (int)nr;
-    for (uint32_t i = 0; i < nr; ++i) {
-        HIPC(hipEventRecord(ctx->up_ev[2 * i], ctx->st));
-        CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest light depth first
-        HIPC(hipEventRecord(ctx->up_ev[2 * i + 1], ctx->st));
+    ctx->nfev = 0;
+    ctx->fam.clear();
+    ctx->fam_vox.clear();
+    CHECK(mark(ctx, -1, 0));
+    for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest first
+    for (uint32_t r = 0; r < nr; ++r) CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all));
+    (void)N;
+    return SM_OK;
+}
+
+// per-family totals of the last filter call (after the stream has been synchronised)
+sm_status collect_filter_stats(sm_ctx* ctx) {
+    sm_kernel_stat ks[KF_N]{};
+    for (int f = 0; f < KF_N; ++f) {
+        snprintf(ks[f].name, sizeof(ks[f].name), "%s", kf_name[f]);
+        ks[f].bytes_per_voxel = kf_bytes[f];
     }
-    for (uint32_t r = 0; r < nr; ++r) {
-        HIPC(hipEventRecord(ctx->down_ev[2 * r], ctx->st));
-        CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all));
-        HIPC(hipEventRecord(ctx->down_ev[2 * r + 1], ctx->st));
+    for (size_t k = 0; k < ctx->fam.size(); ++k) {
+        float ms;
+        HIPC(hipEventElapsedTime(&ms, ctx->fev[k], ctx->fev[k + 1]));
+        const int f = ctx->fam[k];
+        if (ctx->fam_vox[k] > 0) ks[f].launches += 1;  // a bucket without paths launches nothing
+        ks[f].ms += ms;
+        ks[f].voxels += ctx->fam_vox[k];
     }
-    // algorithmic bytes (see DESIGN.md "Roofline accounting")
-    double upb = 0, downb = 0;
-    for (int v = 0; v < nviews; ++v) {
-        const auto& L = ctx->layout[v];
-        const double row = 8.0 * D;
-        const double heads = (double)L.npaths, roots = 1.0;   // MST mode: one tree
-        const double n_light = heads - roots;                  // every non-root head is a light child
-        upb += row * (double)N + row * n_light + 32.0 * (double)N;
-        downb += row * (double)N + row * n_light + row * (double)L.n_has_light + 32.0 * (double)N + 16.0 * (double)N;
+    memcpy(ctx->kstats, ks, sizeof(ks));
+    sm_filter_stats fs{};
+    for (int f = 0; f < KF_N; ++f) {
+        const bool up = f <= KF_UP_CHAIN;
+        (up ? fs.up_ms : fs.down_ms) += ks[f].ms;
+        (up ? fs.up_bytes : fs.down_bytes) += ks[f].voxels * ks[f].bytes_per_voxel;
+        (up ? fs.up_launches : fs.down_launches) += ks[f].launches;
     }
-    ctx->stats.up_bytes = upb;
-    ctx->stats.down_bytes = downb;
-    ctx->stats.up_launches = (int)nr;
-    ctx->stats.down_launches = (int)nr;
+    ctx->stats = fs;
     return SM_OK;
 }
 
@@ -485,6 +533,7 @@ void sm_default_params(sm_params* p) {
     p->cost_kind = SM_COST_AGD;
     p->disp_begin = 0;
     p->disp_total = 0;
+    p->post = 0;
 }
 
 sm_status sm_device_count(int* count) {
@@ -542,8 +591,7 @@ void sm_destroy(sm_ctx* ctx) {
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
-    for (auto e : ctx->up_ev) (void)hipEventDestroy(e);
-    for (auto e : ctx->down_ev) (void)hipEventDestroy(e);
+    for (auto e : ctx->fev) (void)hipEventDestroy(e);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
     if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
     for (int v = 0; v < 2; ++v) {
@@ -581,6 +629,10 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     CHECK(stage_filter(ctx, D, p->disp_begin, 2, false));
     HIPC(hipEventRecord(ctx->ev[4], ctx->st));
     CHECK(stage_reduce(ctx));
+    if (p->post & SM_POST_LR_CHECK) {
+        const int dmax = p->disp_total > 0 ? p->disp_total : p->disp_begin + D;
+        HIPC(launch_lr_check(ctx->st, P<float>(ctx->disp[0]), P<float>(ctx->disp[1]), ctx->W, ctx->H, dmax));
+    }
     HIPC(hipEventRecord(ctx->ev[5], ctx->st));
     return SM_OK;
 }
@@ -594,25 +646,13 @@ sm_status sm_synchronize(sm_ctx* ctx) {
     ctx->stage_ms[0] = t[0];
     ctx->stage_ms[1] = t[1];
     ctx->stage_ms[2] = t[2];
-    float up = 0, down = 0;
-    for (int i = 0; i < ctx->n_up; ++i) {
-        float x;
-        HIPC(hipEventElapsedTime(&x, ctx->up_ev[2 * i], ctx->up_ev[2 * i + 1]));
-        up += x;
-    }
-    for (int i = 0; i < ctx->n_down; ++i) {
-        float x;
-        HIPC(hipEventElapsedTime(&x, ctx->down_ev[2 * i], ctx->down_ev[2 * i + 1]));
-        down += x;
-    }
-    ctx->stage_ms[3] = up;
-    ctx->stage_ms[4] = down;
+    CHECK(collect_filter_stats(ctx));
+    ctx->stage_ms[3] = (float)ctx->stats.up_ms;
+    ctx->stage_ms[4] = (float)ctx->stats.down_ms;
     ctx->stage_ms[5] = t[4];
     float tot;
     HIPC(hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[5]));
     ctx->stage_ms[6] = tot;
-    ctx->stats.up_ms = up;
-    ctx->stats.down_ms = down;
     return SM_OK;
 }
 
@@ -705,6 +745,10 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
         CHECK(ensure_filter_bufs(ctx, Dpad));
         WalkArgs a = walk_args(ctx, Dpad, D, d0);
         const uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
+        ctx->nfev = 0;
+        ctx->fam.clear();
+        ctx->fam_vox.clear();
+        CHECK(mark(ctx, -1, 0));
         for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl_for(D), 2));
         HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
                                    P<double>(ctx->vol[0])));
@@ -723,6 +767,13 @@ int sm_stage_times(sm_ctx* ctx, float* out, int n) {
     if (!ctx || !out) return 0;
     int k = n < 7 ? n : 7;
     for (int i = 0; i < k; ++i) out[i] = ctx->stage_ms[i];
+    return k;
+}
+
+int sm_get_kernel_stats(sm_ctx* ctx, sm_kernel_stat* out, int n) {
+    if (!ctx || !out) return 0;
+    const int k = n < KF_N ? n : KF_N;
+    for (int i = 0; i < k; ++i) out[i] = ctx->kstats[i];
     return k;
 }
 

@@ -745,13 +745,22 @@ static void down_chain_launch(hipStream_t st, const WalkArgs& a, int np, int sto
                        a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all);
 }
 
-hipError_t launch_up_long(hipStream_t st, const WalkArgs& a, int spl) {
+hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {
+    switch (spl) {
+        case 1: up_pre_launch<1, 8>(st, a); break;
+        case 2: up_pre_launch<2, 8>(st, a); break;
+        default: up_pre_launch<4, 4>(st, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_up_chain(hipStream_t st, const WalkArgs& a, int spl) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
     switch (spl) {
-        case 1: up_pre_launch<1, 8>(st, a); up_chain_launch<1>(st, a, np); break;
-        case 2: up_pre_launch<2, 8>(st, a); up_chain_launch<2>(st, a, np); break;
-        default: up_pre_launch<4, 4>(st, a); up_chain_launch<4>(st, a, np); break;
+        case 1: up_chain_launch<1>(st, a, np); break;
+        case 2: up_chain_launch<2>(st, a, np); break;
+        default: up_chain_launch<4>(st, a, np); break;
     }
     return hipGetLastError();
 }

@@ -49,10 +49,12 @@ hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* l
                               const float* atab, int W, int H, int d0, int D, float* lvol, float* rvol);
 hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H);
 hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r);
+hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 // long-path engine (sm_chain.hip): buckets of paths with >= SM_LONG_PATH nodes
-hipError_t launch_up_long(hipStream_t st, const WalkArgs& a, int spl);
+hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl);
+hipError_t launch_up_chain(hipStream_t st, const WalkArgs& a, int spl);
 hipError_t launch_down_long(hipStream_t st, const WalkArgs& a, int spl, int store_all);
 hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_rows_to_volume(hipStream_t st, const SmMeta* meta, const double* U, int nslots, int Dpad, int D,

@@ -50,6 +50,7 @@ struct LayoutView {
     uint32_t* round_cursor;  // SM_NBUCKETS
     uint32_t* round_begin;   // SM_NBUCKETS + 1
     uint32_t* round_maxlen;  // SM_NBUCKETS: longest path per bucket
+    uint32_t* round_nodes;   // SM_NBUCKETS: nodes per bucket
     uint32_t* seg_begin;     // SM_NBUCKETS + 1: first segment of each bucket in segtab
     uint2* segtab;           // {path index within its bucket, segment within the path}
     uint32_t* nrounds;

@@ -510,8 +510,8 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_prep(LayoutPair LP, int N) 
 // after the max-scan: count paths per (round, long/short) bucket at their last slot
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N) {
     const LayoutView& V = LP.v[blockIdx.y];
-    __shared__ uint32_t hist[SM_NBUCKETS];
-    if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = 0;
+    __shared__ uint32_t hist[SM_NBUCKETS], nodes[SM_NBUCKETS];
+    if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = nodes[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
     for (int i = 0; i < PATH_ITEMS; ++i) {
@@ -522,11 +522,15 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N)
             const uint32_t len = s - head + 1u;
             const uint32_t b = 2u * (V.headflag[head] - 1u) + (len >= SM_LONG_PATH ? 0u : 1u);
             atomicAdd(&hist[b], 1u);
+            atomicAdd(&nodes[b], len);
             if (len >= SM_LONG_PATH) atomicMax(&V.round_maxlen[b], len);  // few long paths: direct atomics
         }
     }
     __syncthreads();
-    if (threadIdx.x < SM_NBUCKETS && hist[threadIdx.x]) atomicAdd(&V.round_count[threadIdx.x], hist[threadIdx.x]);
+    if (threadIdx.x < SM_NBUCKETS && hist[threadIdx.x]) {
+        atomicAdd(&V.round_count[threadIdx.x], hist[threadIdx.x]);
+        atomicAdd(&V.round_nodes[threadIdx.x], nodes[threadIdx.x]);
+    }
 }
 
 __global__ void k_path_offsets(LayoutPair LP) {

@@ -162,8 +162,24 @@ def test_reference_surface(gpu_ctx):
     ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "AGD", 16)
     assert sm.getTimer() >= 0
     ref = O.match(left, right, 16)
-    np.testing.assert_array_equal(ld.ravel(), ref["left"]["idx"].astype(np.float32))
-    np.testing.assert_array_equal(rd.ravel(), ref["right"]["idx"].astype(np.float32))
+    H, W = left.shape[:2]
+    lref = ref["left"]["idx"].astype(np.float32).reshape(H, W)
+    rref = ref["right"]["idx"].astype(np.float32).reshape(H, W)
+    np.testing.assert_array_equal(ld, O.lr_check(lref, rref, 16))  # Stereo3DMST.cpp:904
+    np.testing.assert_array_equal(rd, rref)
+
+
+@pytest.mark.parametrize("W,H,D", [(128, 80, 32), (301, 47, 100), (64, 9, 200)])
+def test_lr_check_post_bitexact(gpu_ctx, W, H, D):
+    import stereomatch_amd as sm
+    left, right, _ = make_pair(W, H, D, index=5)
+    out = gpu_ctx.match(left, right, D, sm.default_params(post=sm.SM_POST_LR_CHECK))
+    ref = O.match(left, right, D, nthreads=16)
+    lref = ref["left"]["idx"].astype(np.float32).reshape(H, W)
+    rref = ref["right"]["idx"].astype(np.float32).reshape(H, W)
+    np.testing.assert_array_equal(out["left"]["disp"], O.lr_check(lref, rref, D))
+    np.testing.assert_array_equal(out["right"]["disp"], rref)
+    np.testing.assert_array_equal(out["left"]["idx"].reshape(H, W), lref.astype(np.int32))  # idx untouched
 
 
 def expected_layout(W, H, node_pix, node_parent):

@@ -68,3 +68,15 @@ def test_bfs_children_in_ascending_key_order():
         ch = t["node_child"][4 * n:4 * n + k]
         ws = [int(t["node_w"][c]) for c in ch]
         assert ws == sorted(ws)
+
+
+def test_lr_check_semantics():
+    """Stereo3DMST.cpp:632-662 (fill=false): out-of-range / inconsistent left pixels -> 0."""
+    L = np.array([[0, 1, 2, 5], [3, 0, 1, 1], [1.5, 2.5, 0.5, 2]], np.float32)
+    R = np.array([[0, 1, 1, 2], [0, 0, 0, 1], [1, 1, 0, 2]], np.float32)
+    out = O.lr_check(L, R, 4)
+    # row 0: d=2 at x=2 reads R(0)=0 (|2-0|>1); d=5 >= max_disp
+    # row 1: x=0, d=3 -> x-d < 0
+    # row 2: round(1.5)=2 -> x-d<0; round(2.5)=3 -> x-d<0; round(0.5)=1 -> R(1)=1, |0.5-1|<=1; x=3,d=2 -> R(1)=1
+    exp = np.array([[0, 1, 0, 0], [0, 0, 1, 1], [0, 0, 0.5, 2]], np.float32)
+    np.testing.assert_array_equal(out, exp)
