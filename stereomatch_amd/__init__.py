@@ -10,6 +10,7 @@ backed by the HIP library libstereomst.so (C-ABI in include/stereomst.h).  The c
 runs only on the GPU; a missing library or device raises.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -56,8 +57,13 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
     left_disp = np.empty((H, W), np.float32)
     right_disp = np.empty((H, W), np.float32)
     if data_cost in ("MCCNN_fst", "MCCNN_acrt"):
-        # reference: chdir("mc-cnn-master") fails -> message and return (:727-731)
-        print("no mc-cnn-master folder")
+        # reference: without an mc-cnn-master folder MCCNN_fst prints and returns (:727-731),
+        # MCCNN_acrt returns silently (:744-745); volume ingest is not implemented yet
+        if not os.path.isdir("mc-cnn-master"):
+            if data_cost == "MCCNN_fst":
+                print("no mc-cnn-master folder")
+        else:
+            print("stereo3dmst: MC-CNN volume ingest is not implemented in this build; use data_cost=\"AGD\"")
         return left_disp, right_disp
     if data_cost != "AGD":
         print("wrong data cost")
