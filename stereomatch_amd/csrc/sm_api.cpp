@@ -48,7 +48,7 @@ struct sm_ctx {
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
-    DevBuf segtab[2];
+    DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2];
     DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
@@ -239,6 +239,11 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->paths[v], N * sizeof(SmPath)));
         CHECK(ensure(ctx, ctx->rounds[v], RREC * 4));
         CHECK(ensure(ctx, ctx->segtab[v], (N / 16 + 64) * sizeof(uint2)));  // <= N/32 segments + N/32 long paths
+        CHECK(ensure(ctx, ctx->pathpos[v], N * 4));
+        CHECK(ensure(ctx, ctx->plen[v], N * 4));
+        CHECK(ensure(ctx, ctx->nslot[v], N * 4));
+        CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
+        HIPC(hipMemsetAsync(ctx->plen[v].p, 0, N * 4, ctx->st));  // lengths past the last path stay 0
         HIPC(hipMemsetAsync(ctx->ccount[v].p, 0, 16, ctx->st));
         HIPC(hipMemsetAsync(ctx->rounds[v].p, 0, RREC * 4, ctx->st));
         LayoutView& L = LP.v[v];
@@ -273,6 +278,10 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.headflag = P<uint32_t>(ctx->headflag[v]);
         L.headpos = P<uint32_t>(ctx->headpos[v]);
         L.paths = P<SmPath>(ctx->paths[v]);
+        L.pathpos = P<uint32_t>(ctx->pathpos[v]);
+        L.plen = P<uint32_t>(ctx->plen[v]);
+        L.nslot = P<uint32_t>(ctx->nslot[v]);
+        L.slotpix = P<uint32_t>(ctx->slotpix[v]);
         uint32_t* R = P<uint32_t>(ctx->rounds[v]);
         L.round_begin = R;
         L.round_count = R + SM_NBUCKETS + 1;
@@ -599,7 +608,8 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->pre[v], &ctx->ld[v], &ctx->a_dist[v], &ctx->a_cid[v], &ctx->a_head[v], &ctx->arank[v],
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cn0[v], &ctx->cn1[v],
                          &ctx->cw0[v], &ctx->cw1[v], &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
-                         &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v]};
+                         &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
+                         &ctx->nslot[v], &ctx->slotpix[v]};
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -715,7 +725,7 @@ sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int strid
     std::vector<uint32_t> size(N), pre(N);
     HIPC(hipMemcpy(pdir.data(), ctx->pdir[0].p, N, hipMemcpyDeviceToHost));
     HIPC(hipMemcpy(size.data(), ctx->size[0].p, N * 4, hipMemcpyDeviceToHost));
-    HIPC(hipMemcpy(pre.data(), ctx->pre[0].p, N * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(pre.data(), ctx->slotpix[0].p, N * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < N; ++i) {
         if (parent_pix) {
             const int k = pdir[i];

@@ -254,7 +254,7 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 template <int SPL>
 struct UpCfg {
     static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? 6 : 3;  // nodes per group (helper registers)
-    static constexpr int NS = 4;                               // LDS slots
+    static constexpr int NS = SPL == 1 ? 8 : 6;                // LDS slots (~140 KB)
 };
 
 struct UpNodeS {
@@ -294,8 +294,10 @@ struct UpRing {
 };
 
 // NN consecutive nodes k0.. of a staged group; NN is a compile-time count so the LDS waits are
-// exact; THIRD = the node-by-node path that also applies a root's third post-heavy child.  Only the
-// rows a node has are read (flags, uniform); absent ones stay 0 with S = 0.
+// exact; THIRD = the node-by-node path that also applies a root's third post-heavy child.
+// Every row is read unconditionally (the ring is zeroed at kernel start, so rows a helper did
+// not stage are stale-but-finite): absent posts carry S = 0, and Pre is scaled by a 0/1 factor
+// from the presence flags -- exact, and off the serial chain.
 template <int SPL, int NN, bool THIRD>
 __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0, int j0, int top, int e0,
                                          double (&x)[Split<SPL>::CS], double* __restrict__ U, int Dpad) {
@@ -304,33 +306,22 @@ __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0
     float cv[NN][CS];
 #pragma unroll
     for (int k = 0; k < NN; ++k) {
-        const uint32_t f = flags >> (3 * (k0 + k));
         Sh[k] = sl.s[k0 + k].Sh;
+        Sp1[k] = sl.s[k0 + k].Sp1;
+        Sp2[k] = sl.s[k0 + k].Sp2;
+        lds_read_at<CS>(sl.pre[k0 + k], e0, pr[k]);
+        lds_read_at<CS>(sl.post1[k0 + k], e0, p1[k]);
+        lds_read_at<CS>(sl.post2[k0 + k], e0, p2[k]);
 #pragma unroll
-        for (int q = 0; q < CS; ++q) {
-            pr[k][q] = 0.0;
-            p1[k][q] = 0.0;
-            p2[k][q] = 0.0;
-            cv[k][q] = sl.c[k0 + k][e0 + q];
-        }
-        Sp1[k] = 0.0;
-        Sp2[k] = 0.0;
-        if (f & UP_F_PRE) lds_read_at<CS>(sl.pre[k0 + k], e0, pr[k]);
-        if (f & UP_F_P1) {
-            Sp1[k] = sl.s[k0 + k].Sp1;
-            lds_read_at<CS>(sl.post1[k0 + k], e0, p1[k]);
-        }
-        if (f & UP_F_P2) {
-            Sp2[k] = sl.s[k0 + k].Sp2;
-            lds_read_at<CS>(sl.post2[k0 + k], e0, p2[k]);
-        }
+        for (int q = 0; q < CS; ++q) cv[k][q] = sl.c[k0 + k][e0 + q];
     }
 #pragma unroll
     for (int k = 0; k < NN; ++k) {
+        const double fpre = (flags >> (3 * (k0 + k))) & UP_F_PRE ? 1.0 : 0.0;
         double acc[CS];
 #pragma unroll
         for (int q = 0; q < CS; ++q) {
-            acc[q] = __builtin_fma(Sh[k], x[q], pr[k][q]);
+            acc[q] = __builtin_fma(Sh[k], x[q], pr[k][q] * fpre);
             acc[q] = __builtin_fma(Sp1[k], p1[k][q], acc[q]);
             acc[q] = __builtin_fma(Sp2[k], p2[k][q], acc[q]);
         }
@@ -362,19 +353,24 @@ __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head
     double x[CS];
 #pragma unroll
     for (int q = 0; q < CS; ++q) x[q] = 0.0;
+    unsigned long long st = lds_state64(&ring.s[0].staged);  // poll-ahead: the next group's state
     for (int g = 0; g < ngroups; ++g) {
         UpSlot<SPL>& sl = ring.s[g % NS];
         const int n = min(G, len - g * G);
 #ifdef SM_CHAIN_PROF
         const long long ta = clock64();
 #endif
-        unsigned long long st;
-        while ((uint32_t)(st = lds_state64(&sl.staged)) != (uint32_t)(g + 1)) PROF_SPIN(++spins);
+        while ((uint32_t)st != (uint32_t)(g + 1)) {
+            PROF_SPIN(++spins);
+            st = lds_state64(&sl.staged);
+        }
         const uint32_t flags = uniform((uint32_t)(st >> 32));
 #ifdef SM_CHAIN_PROF
         const long long tb = clock64();
         tr += tb - ta;
 #endif
+        // issued now, consumed after this group: its latency hides behind the group's work
+        st = lds_state64(&ring.s[(g + 1) % NS].staged);
         if (n == G && !(flags & UP_F3)) {
             up_group<SPL, G, false>(sl, flags, 0, g * G, top, e0, x, U, Dpad);
         } else {
@@ -430,6 +426,28 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
             if (np >= 3) s3 = mfield(mv, kk, 7);
         }
         load_row<SPL>(U, s3, Dpad, lane, p3);
+        // ---- weights and presence flags (meta + LDS table only): before waiting for the slot;
+        // lane q < 3 holds S of the heavy child (q = 0) / post q of node k
+        double Sl[G];
+        int k3 = -1;
+        double S3 = 0.0;
+        uint32_t flags = 0;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const uint32_t lo = mfield(mv, k, 2), hi = mfield(mv, k, 3);
+            const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+            const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
+            const uint32_t i = hidx + (uint32_t)min(lane, 2);
+            const bool live = lane == 0 ? (nch > 0 && g * G + k > 0) : (uint32_t)lane <= np;
+            Sl[k] = ring.slut[live && lane < 3 ? cw_of(lo, hi, (int)min(i, 3u)) : (uint32_t)S_ZERO];
+            if (k < n) {
+                flags |= ((hidx > 0 ? UP_F_PRE : 0u) | (np >= 1 ? UP_F_P1 : 0u) | (np >= 2 ? UP_F_P2 : 0u)) << (3 * k);
+                if (np >= 3) {
+                    k3 = k;
+                    S3 = ring.slut[cw_of(lo, hi, 3)];
+                }
+            }
+        }
         MetaVec<G> mnext;
         const int gn = g + NH;
         const int gl = gn < ngroups ? gn : g;  // unconditional prefetch (clamped)
@@ -437,31 +455,16 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
         // ---- wait for the slot, fill it, publish
         UpSlot<SPL>& sl = ring.s[g % NS];
         if (g >= NS) lds_wait_all(sl.done, NCW, g - NS + 1);
-        int k3 = -1;
-        double S3 = 0.0;
-        uint32_t flags = 0;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             if (k < n) {
-                const uint32_t lo = mfield(mv, k, 2), hi = mfield(mv, k, 3);
-                const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-                const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
-                const uint32_t f = (hidx > 0 ? UP_F_PRE : 0u) | (np >= 1 ? UP_F_P1 : 0u) | (np >= 2 ? UP_F_P2 : 0u);
-                flags |= f << (3 * k);
+                const uint32_t f = flags >> (3 * k);
                 if (f & UP_F_PRE) lds_row_write<SPL>(sl.pre[k], lane, pr[k]);
                 if (f & UP_F_P1) lds_row_write<SPL>(sl.post1[k], lane, p1[k]);
                 if (f & UP_F_P2) lds_row_write<SPL>(sl.post2[k], lane, p2[k]);
 #pragma unroll
                 for (int q = 0; q < SPL; ++q) sl.c[k][lane * SPL + q] = cr[k][q];
-                if (lane < 3) {  // lane 0: heavy child, lanes 1, 2: posts 1, 2
-                    const uint32_t i = hidx + (uint32_t)lane;
-                    const bool live = lane == 0 ? (nch > 0 && g * G + k > 0) : (uint32_t)lane <= np;
-                    (&sl.s[k].Sh)[lane] = live ? ring.slut[cw_of(lo, hi, (int)min(i, 3u))] : 0.0;
-                }
-                if (np >= 3) {
-                    k3 = k;
-                    S3 = ring.slut[cw_of(lo, hi, 3)];
-                }
+                if (lane < 3) (&sl.s[k].Sh)[lane] = Sl[k];
             }
         }
         if (k3 >= 0) {
@@ -496,10 +499,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     if ((int)blockIdx.x >= V.npaths) return;  // uniform over the block
     const SmPath path = (view ? paths1 : paths0)[blockIdx.x];
     const int head = (int)uniform(path.head), len = (int)uniform(path.len);
-    for (int i = threadIdx.x; i < UpCfg<SPL>::NS; i += CHN_THREADS) {
-        ring.s[i].staged = 0;
-        ring.s[i].done[0] = ring.s[i].done[1] = 0;
-    }
+    // zero the ring: rows a helper does not stage are then always finite (see up_group)
+    for (int i = threadIdx.x; i < (int)(sizeof(ring.s) / 4); i += CHN_THREADS) reinterpret_cast<uint32_t*>(ring.s)[i] = 0u;
     for (int i = threadIdx.x; i < SM_NUM_W; i += CHN_THREADS) ring.slut[i] = slut_g[i];
     if (threadIdx.x == 0) ring.slut[SM_NUM_W] = 0.0;
     __syncthreads();
@@ -516,8 +517,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
 // ---------------------------------------------------------------------------------------------
 template <int SPL>
 struct DownCfg {
-    static constexpr int G = 8;
-    static constexpr int NS = SPL == 4 ? 4 : 8;
+    static constexpr int G = SPL == 4 ? 4 : 8;  // helper registers: next group's rows + WTA rows
+    static constexpr int NS = SPL == 4 ? 8 : 10;
 };
 
 template <int SPL>
@@ -576,17 +577,22 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
         for (int q = 0; q < CS; ++q) x[q] = 0.0;  // root: S = 0, T = A_up -> A(root) = A_up(root)
     }
     const int ngroups = (len + G - 1) / G;
+    int st = lds_state(&ring.s[0].staged);  // poll-ahead: the next group's state
     for (int g = 0; g < ngroups; ++g) {
         DownSlot<SPL>& sl = ring.s[g % NS];
         const int n = min(G, len - g * G);
 #ifdef SM_CHAIN_PROF
         const long long ta = clock64();
 #endif
-        while (lds_state(&sl.staged) != g + 1) PROF_SPIN(++spins);
+        while (st != g + 1) {
+            PROF_SPIN(++spins);
+            st = lds_state(&sl.staged);
+        }
 #ifdef SM_CHAIN_PROF
         const long long tb = clock64();
         tr += tb - ta;
 #endif
+        st = lds_state(&ring.s[(g + 1) % NS].staged);
         if (n == G) {
             down_group<SPL, G>(sl, 0, e0, x);
         } else {

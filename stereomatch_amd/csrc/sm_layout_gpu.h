@@ -23,7 +23,7 @@ struct LayoutView {
     uint32_t* size;     // subtree size
     uint32_t* off_in;   // heavy-first preorder offset within the parent
     uint8_t* light_in;  // 1 if a light child
-    uint32_t* pre;      // preorder = slot
+    uint32_t* pre;      // heavy-first preorder (layout-internal numbering)
     uint32_t* ld;       // light depth
     // per arc (4N)
     uint16_t* a_dist;
@@ -45,7 +45,11 @@ struct LayoutView {
     uint32_t* headflag;
     uint32_t* headpos;
     // paths
-    SmPath* paths;
+    SmPath* paths;           // {head slot, len}, bucket-major; slots of a bucket are contiguous
+    uint32_t* pathpos;       // [preorder of a head] -> index of its path in paths[]
+    uint32_t* plen;          // [path] -> len, inclusive-scanned into the path's end slot
+    uint32_t* nslot;         // [preorder] -> slot
+    uint32_t* slotpix;       // [pixel] -> slot
     uint32_t* round_count;   // SM_NBUCKETS
     uint32_t* round_cursor;  // SM_NBUCKETS
     uint32_t* round_begin;   // SM_NBUCKETS + 1

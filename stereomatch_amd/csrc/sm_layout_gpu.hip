@@ -439,7 +439,33 @@ __global__ void k_assign(LayoutPair LP, int W, int H) {
     V.ld[q] = ld;
 }
 
-// per-slot metadata (slot = preorder) + path heads
+// path heads in preorder numbering: headflag[pre] = 0 (not a head) or 1 + light depth
+__global__ void k_heads(LayoutPair LP, int W, int H) {
+    const LayoutView& V = LP.v[blockIdx.z];
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t v = (uint32_t)(y * W + x);
+    const bool head = V.pdir[v] < 0 || V.light_in[v];
+    V.headflag[V.pre[v]] = head ? 1u + V.ld[v] : 0u;
+}
+
+// slot of every preorder position: the paths of one (light depth, long/short) bucket occupy a
+// contiguous slot range, each path contiguous from its head (= preorder contiguity of heavy
+// paths), in paths[] order.  plen holds the inclusive scan of the lengths: end slot of a path.
+__global__ void k_newslot(LayoutPair LP, int N) {
+    const LayoutView& V = LP.v[blockIdx.y];
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= (uint32_t)N) return;
+    const uint32_t head = V.headpos[s] - 1u;
+    const uint32_t P = V.pathpos[head];
+    const uint32_t len = V.paths[P].len;
+    const uint32_t nh = V.plen[P] - len;
+    V.nslot[s] = nh + (s - head);
+    if (s == head) V.paths[P].head = nh;
+}
+
+// per-slot metadata in slot numbering: pixel, parent slot, child weights and slots in
+// descending (w,a,b) key order (the reference's fold order), heavy-child position, light flag
 __global__ void k_meta(LayoutPair LP, int W, int H) {
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -467,17 +493,20 @@ __global__ void k_meta(LayoutPair LP, int W, int H) {
     uint32_t hidx = 0, has_light = 0;
     for (int i = 0; i < nch; ++i) {
         cw[i] = (uint32_t)(ck[i] >> 33);
-        cs[i] = V.pre[nbr_of(v, cq[i], W)];
+        cs[i] = V.nslot[V.pre[nbr_of(v, cq[i], W)]];
         if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
     }
     uint32_t wp = 0, parent = SM_NONE;
     if (pd >= 0) {
         wp = (uint32_t)(key_dir(V.wR, V.wD, W, v, pd) >> 33);
-        parent = V.pre[nbr_of(v, pd, W)];
+        parent = V.nslot[V.pre[nbr_of(v, pd, W)]];
     }
     has_light = live ? has_light : 0u;
-    const uint32_t slot = V.pre[v];
-    if (live) V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
+    const uint32_t slot = V.nslot[V.pre[v]];
+    if (live) {
+        V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
+        V.slotpix[v] = slot;
+    }
     {
         __shared__ uint32_t nl;
         if (threadIdx.x == 0) nl = 0;
@@ -486,8 +515,6 @@ __global__ void k_meta(LayoutPair LP, int W, int H) {
         __syncthreads();
         if (threadIdx.x == 0 && nl) atomicAdd(V.n_has_light, nl);
     }
-    const bool head = pd < 0 || V.light_in[v];
-    if (live) V.headflag[slot] = head ? 1u + V.ld[v] : 0u;  // 0 = not a head, else 1 + light depth
 }
 
 // heads in slot order -> path lengths -> bucketed by light depth (order inside a round is free).
@@ -572,7 +599,11 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
     for (int i = 0; i < PATH_ITEMS; ++i) {
         if (myr[i] == SM_NONE) continue;
         const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
-        V.paths[gbase[myr[i]] + myrank[i]] = SmPath{myhead[i], s - myhead[i] + 1u};
+        const uint32_t P = gbase[myr[i]] + myrank[i];
+        const uint32_t len = s - myhead[i] + 1u;
+        V.paths[P] = SmPath{myhead[i], len};  // head in preorder numbering until k_newslot
+        V.pathpos[myhead[i]] = P;
+        V.plen[P] = len;
     }
 }
 
@@ -628,7 +659,7 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}, {LP.v[0].bsum, LP.v[1].bsum}};
     launch_scan<long long, OpAdd>(st, tb, nviews, 2 * N - 2);
     hipLaunchKernelGGL(k_assign, pg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_meta, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_heads, pg, dim3(256), 0, st, LP, W, H);
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
     hipLaunchKernelGGL(k_path_prep, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     ScanBufs<uint32_t> hb{{LP.v[0].headpos, LP.v[1].headpos}, {LP.v[0].bsum32, LP.v[1].bsum32}};
@@ -636,6 +667,12 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     hipLaunchKernelGGL(k_path_offsets, dim3(nviews), dim3(64), 0, st, LP);
     hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
+    // contiguous bucket slots: scan of path lengths in paths[] order (plen is zero past the last
+    // path), slot of every preorder position, then the metadata in slot numbering
+    ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}, {LP.v[0].bsum32, LP.v[1].bsum32}};
+    launch_scan<uint32_t, OpAdd>(st, lb, nviews, N);
+    hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
+    hipLaunchKernelGGL(k_meta, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP);
     return hipGetLastError();
 }

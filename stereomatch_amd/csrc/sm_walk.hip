@@ -27,6 +27,9 @@
 #include "sm_launch.h"
 #include "sm_walk_util.h"
 
+// paths per wave work item (a bucket's paths occupy consecutive slots: one contiguous range)
+#define WALK_PPW 8
+
 
 // ---------------------------------------------------------------------------------------------
 // up pass
@@ -113,10 +116,14 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
-    const int pi = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (pi >= V.npaths) return;
-    const SmPath path = (view ? paths1 : paths0)[pi];
-    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
+    // work item: WALK_PPW consecutive paths of the bucket = one contiguous slot range (the
+    // recurrence restarts by itself at every path bottom: a leaf has no heavy child)
+    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW);
+    if (pi0 >= V.npaths) return;
+    const int pi1 = min(pi0 + WALK_PPW, V.npaths);
+    const SmPath* __restrict__ pp = view ? paths1 : paths0;
+    const int head = (int)uniform(pp[pi0].head);
+    const int len = (int)uniform(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
     const int dbase = dglob0 + lane * SPL;  // global disparity of this lane's first slice
     const int dend = dglob0 + dcall;
     const uint2* __restrict__ own = view ? Rrec : Lrec;  // the view's reference image
@@ -157,29 +164,41 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
-    const int pi = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (pi >= V.npaths) return;
-    const SmPath path = (view ? paths1 : paths0)[pi];
-    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
+    // work item: WALK_PPW consecutive paths = one contiguous slot range, root side first; a node
+    // is a path head iff its parent is not the previous slot
+    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW);
+    if (pi0 >= V.npaths) return;
+    const int pi1 = min(pi0 + WALK_PPW, V.npaths);
+    const SmPath* __restrict__ pp = view ? paths1 : paths0;
+    const int head = (int)uniform(pp[pi0].head);
+    const int len = (int)uniform(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
     const int dloc0 = lane * SPL;
-    const uint32_t hparent = uniform(meta32[(size_t)head * 8 + 1]);
     double xc[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) xc[k] = 0.0;
     int c0 = head;
     int n = min(CH, len);
     MetaVec<CH> cur;
     load_meta<CH>(cur, meta32, lane, c0, 1, n);
-    bool first = true;
     while (true) {
         const int nc0 = c0 + CH;
         const int nn = nc0 < head + len ? min(CH, head + len - nc0) : 0;
         MetaVec<CH> nxt;
         if (nn > 0) load_meta<CH>(nxt, meta32, lane, nc0, 1, nn);  // prefetch the next chunk's metadata
-        // rows of the chunk (contiguous slots) + the parent's A row for the path head
-        double u[CH][SPL], xp[SPL];
+        // rows of the chunk (contiguous slots) and, for path heads, the parent's finished A row
+        // (earlier round); other nodes load their own row again (L1/L2 hit) so the count of
+        // loads is fixed
+        double u[CH][SPL], xp[CH][SPL];
+        uint32_t par[CH];
 #pragma unroll
-        for (int j = 0; j < CH; ++j)
-            if (j < n) load_row<SPL>(V.U, (uint32_t)(c0 + j), Dpad, lane, u[j]);
-        if (first && hparent != SM_NONE) load_row<SPL>(V.U, hparent, Dpad, lane, xp);
+        for (int j = 0; j < CH; ++j) {
+            const int jj = j < n ? j : n - 1;
+            const uint32_t slot = (uint32_t)(c0 + jj);
+            par[j] = mfield(cur, jj, 1);
+            const bool head_j = par[j] == SM_NONE || par[j] != slot - 1u;
+            load_row<SPL>(V.U, slot, Dpad, lane, u[j]);
+            load_row<SPL>(V.U, head_j && par[j] != SM_NONE ? par[j] : slot, Dpad, lane, xp[j]);
+        }
         double S[CH], S2[CH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -191,22 +210,20 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             if (j < n) {
-                const bool is_head = first && j == 0;
-                if (is_head) {
-                    if (hparent == SM_NONE) {
+                const uint32_t slot = (uint32_t)(c0 + j);
+                const bool root = par[j] == SM_NONE;
+                if (root) {
 #pragma unroll
-                        for (int k = 0; k < SPL; ++k) xc[k] = u[j][k];  // A(root) = A_up(root)
-                    } else {
+                    for (int k = 0; k < SPL; ++k) xc[k] = u[j][k];  // A(root) = A_up(root)
+                } else if (par[j] != slot - 1u) {                  // path head: parent from an earlier round
 #pragma unroll
-                        for (int k = 0; k < SPL; ++k) xc[k] = __builtin_fma(S[j], xp[k], S2[j] * u[j][k]);
-                    }
+                    for (int k = 0; k < SPL; ++k) xc[k] = __builtin_fma(S[j], xp[j][k], S2[j] * u[j][k]);
                 } else {
 #pragma unroll
                     for (int k = 0; k < SPL; ++k) xc[k] = __builtin_fma(S[j], xc[k], S2[j] * u[j][k]);
                 }
                 const uint32_t hi = mfield(cur, j, 3);
-                if (store_all || (hi_light(hi) && !(is_head && hparent == SM_NONE)))
-                    store_row<SPL>(V.U, (uint32_t)(c0 + j), Dpad, lane, xc);
+                if (store_all || (hi_light(hi) && !root)) store_row<SPL>(V.U, slot, Dpad, lane, xc);
             }
 #pragma unroll
             for (int k = 0; k < SPL; ++k) xs[j][k] = xc[k];
@@ -224,7 +241,6 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
         cur = nxt;
         c0 = nc0;
         n = nn;
-        first = false;
     }
 }
 
@@ -248,7 +264,8 @@ static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
-    const dim3 g((np + 3) / 4, 2);
+    const int items = (np + WALK_PPW - 1) / WALK_PPW;
+    const dim3 g((items + 3) / 4, 2);
     if (long_paths) {
         switch (spl) {
             case 1: up_launch<1, 8>(st, g, a); break;
@@ -268,7 +285,8 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
 static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, int store_all, bool long_paths) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
-    const dim3 g((np + 3) / 4, 2);
+    const int items = (np + WALK_PPW - 1) / WALK_PPW;
+    const dim3 g((items + 3) / 4, 2);
     if (long_paths) {
         switch (spl) {
             case 1: down_launch<1, 16>(st, g, a, store_all); break;

@@ -217,11 +217,58 @@ def expected_layout(W, H, node_pix, node_parent):
     return size, pre
 
 
+def expected_paths(W, H, node_pix, node_parent):
+    """Heavy child (largest subtree, ties: smallest direction R,D,L,U), light depth and heavy
+    paths restated from the oracle's BFS tree."""
+    N = W * H
+    parent = np.full(N, -1, np.int64)
+    parent[node_pix[1:]] = node_pix[node_parent[1:]]
+    size = np.ones(N, np.int64)
+    for n in range(N - 1, 0, -1):
+        size[node_pix[node_parent[n]]] += size[node_pix[n]]
+    heavy = np.full(N, -1, np.int64)
+    best = np.zeros(N, np.int64)
+    for q in range(N):
+        p = parent[q]
+        if p < 0:
+            continue
+        d = q - p
+        k = 0 if d == 1 else 1 if d == W else 2 if d == -1 else 3
+        key = size[q] * 4 + (3 - k)  # larger subtree wins, then the smaller direction
+        if key > best[p]:
+            best[p], heavy[p] = key, q
+    ld = np.zeros(N, np.int64)
+    for n in range(1, N):  # BFS order: parents first
+        q = node_pix[n]
+        p = parent[q]
+        ld[q] = ld[p] + (0 if heavy[p] == q else 1)
+    heads = [q for q in range(N) if parent[q] < 0 or heavy[parent[q]] != q]
+    paths = []
+    for h in heads:
+        nodes = [h]
+        while heavy[nodes[-1]] >= 0:
+            nodes.append(heavy[nodes[-1]])
+        paths.append((h, nodes))
+    return size, ld, paths
+
+
 @pytest.mark.parametrize("name", ["rand_37x23", "smooth_97x61", "flir_crop_256x192", "const_16x12", "col_1x15"])
 def test_gpu_layout_matches_restated_schedule(gpu_ctx, name):
+    """The GPU schedule layout: subtree sizes; every heavy path on consecutive
+    slots from its head; the paths of one (light depth, long/short) bucket on one contiguous
+    slot range, buckets in increasing order (order of paths inside a bucket is free)."""
     z = load_case(name)
     H, W, _ = z["left"].shape
     t = gpu_ctx.build_tree(z["left"])
-    size, pre = expected_layout(W, H, z["left_node_pix"], z["left_node_parent"])
+    size, ld, paths = expected_paths(W, H, z["left_node_pix"], z["left_node_parent"])
     np.testing.assert_array_equal(t["subtree_size"], size)
-    np.testing.assert_array_equal(t["slot_of_pix"], pre)
+    slot = t["slot_of_pix"].astype(np.int64)
+    assert np.array_equal(np.sort(slot), np.arange(W * H))
+    spans = []
+    for h, nodes in paths:
+        np.testing.assert_array_equal(slot[nodes], slot[h] + np.arange(len(nodes)))
+        bucket = 2 * ld[h] + (0 if len(nodes) >= 32 else 1)
+        spans.append((slot[h], len(nodes), bucket))
+    spans.sort()
+    buckets = [b for _, _, b in spans]
+    assert buckets == sorted(buckets)
