@@ -40,6 +40,11 @@ struct DevBuf {
 struct sm_ctx {
     int device = 0;
     hipStream_t st = nullptr;
+    // Stream of the long-path chain engine.  Measured (round 1): running it on a second stream
+    // concurrently with the short-path walkers loses -- every round boundary then costs a
+    // ~30 us cross-stream join and the throughput-bound k_up_pre only competes with the walkers --
+    // so it aliases st; the round code keeps the two-stream structure (join() is then a no-op).
+    hipStream_t st2 = nullptr;
     std::string err;
     int W = 0, H = 0, stride = 0;
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
@@ -57,11 +62,13 @@ struct sm_ctx {
         std::vector<uint32_t> begin, maxlen, seg_begin, nodes;  // per bucket
     } layout[2];
     hipEvent_t ev[8] = {};
-    // tree-filter launch timing: event k brackets interval k = [fev[k], fev[k+1]) of family fam[k]
+    // tree-filter launch timing: launch k is bracketed by events fev[2k], fev[2k+1] on its stream
     std::vector<hipEvent_t> fev;
     std::vector<int> fam;
-    std::vector<double> fam_vox;  // voxels of interval k
+    std::vector<double> fam_vox;  // voxels of launch k
     int nfev = 0;
+    std::vector<hipEvent_t> sev;  // stream-ordering events of the filter rounds
+    int nsev = 0;
     sm_filter_stats stats{};
     sm_kernel_stat kstats[5]{};
     float stage_ms[7] = {0};
@@ -372,15 +379,26 @@ enum { KF_UP_WALK, KF_UP_PRE, KF_UP_CHAIN, KF_DOWN_CHAIN, KF_DOWN_WALK, KF_N };
 const char* const kf_name[KF_N] = {"k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk"};
 const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0};
 
-// record the event that closes the current interval (family f, voxels) and opens the next
-sm_status mark(sm_ctx* ctx, int f, double vox) {
-    CHECK(ensure_events(ctx, ctx->fev, (size_t)ctx->nfev + 1));
-    HIPC(hipEventRecord(ctx->fev[ctx->nfev], ctx->st));
-    if (ctx->nfev > 0) {
-        ctx->fam.push_back(f);
-        ctx->fam_vox.push_back(vox);
-    }
-    ++ctx->nfev;
+// a timed launch of family f on stream s: events before and after (per-family HIP-event time)
+template <class F>
+sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch) {
+    CHECK(ensure_events(ctx, ctx->fev, (size_t)ctx->nfev + 2));
+    HIPC(hipEventRecord(ctx->fev[ctx->nfev], s));
+    HIPC(launch());
+    HIPC(hipEventRecord(ctx->fev[ctx->nfev + 1], s));
+    ctx->fam.push_back(f);
+    ctx->fam_vox.push_back(vox);
+    ctx->nfev += 2;
+    return SM_OK;
+}
+
+// make stream `waiter` wait for everything enqueued so far on stream `src`
+sm_status join(sm_ctx* ctx, hipStream_t waiter, hipStream_t src) {
+    if (waiter == src) return SM_OK;
+    CHECK(ensure_events(ctx, ctx->sev, (size_t)ctx->nsev + 1));
+    hipEvent_t e = ctx->sev[ctx->nsev++];
+    HIPC(hipEventRecord(e, src));
+    HIPC(hipStreamWaitEvent(waiter, e, 0));
     return SM_OK;
 }
 
@@ -393,31 +411,36 @@ double bucket_voxels(sm_ctx* ctx, uint32_t r, bool long_paths, int nviews, int D
     return n * D;
 }
 
-// one light-depth round of the up pass: short paths by the chunked walkers, long paths by the
-// chain engine (pre-fold kernel + one workgroup per path)
+// One light-depth round of a pass: short paths by the chunked walkers on st, long paths by the
+// chain engine on st2, concurrently (they touch disjoint rows; both only read rows finished in
+// earlier rounds).  Rounds are ordered by joining the two streams at every round boundary.
 sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
+    CHECK(join(ctx, ctx->st, ctx->st2));
+    CHECK(join(ctx, ctx->st2, ctx->st));
     set_bucket(ctx, a, r, false, nviews);
-    HIPC(launch_up(ctx->st, a, spl, false));
-    CHECK(mark(ctx, KF_UP_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall)));
+    const WalkArgs as = a;
+    CHECK(timed(ctx, ctx->st, KF_UP_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall),
+                [&] { return launch_up(ctx->st, as, spl, false); }));
     set_bucket(ctx, a, r, true, nviews);
+    const WalkArgs al = a;
     const double vl = bucket_voxels(ctx, r, true, nviews, a.dcall);
-    HIPC(launch_up_pre(ctx->st, a, spl));
-    CHECK(mark(ctx, KF_UP_PRE, vl));
-    HIPC(launch_up_chain(ctx->st, a, spl));
-    CHECK(mark(ctx, KF_UP_CHAIN, vl));
+    CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }));
+    CHECK(timed(ctx, ctx->st2, KF_UP_CHAIN, vl, [&] { return launch_up_chain(ctx->st2, al, spl); }));
     return SM_OK;
 }
 
 sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews, bool store_all) {
+    CHECK(join(ctx, ctx->st, ctx->st2));
+    CHECK(join(ctx, ctx->st2, ctx->st));
     set_bucket(ctx, a, r, true, nviews);
-    HIPC(launch_down_long(ctx->st, a, spl, store_all ? 1 : 0));
-    CHECK(mark(ctx, KF_DOWN_CHAIN, bucket_voxels(ctx, r, true, nviews, a.dcall)));
+    const WalkArgs al = a;
+    CHECK(timed(ctx, ctx->st2, KF_DOWN_CHAIN, bucket_voxels(ctx, r, true, nviews, a.dcall),
+                [&] { return launch_down_long(ctx->st2, al, spl, store_all ? 1 : 0); }));
     set_bucket(ctx, a, r, false, nviews);
-    if (store_all)
-        HIPC(launch_down_debug(ctx->st, a, spl, false));
-    else
-        HIPC(launch_down(ctx->st, a, spl, false));
-    CHECK(mark(ctx, KF_DOWN_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall)));
+    const WalkArgs as = a;
+    CHECK(timed(ctx, ctx->st, KF_DOWN_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall), [&] {
+        return store_all ? launch_down_debug(ctx->st, as, spl, false) : launch_down(ctx->st, as, spl, false);
+    }));
     return SM_OK;
 }
 
@@ -442,12 +465,12 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     uint32_t nr = 0;
     for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
-    ctx->nfev = 0;
+    ctx->nfev = ctx->nsev = 0;
     ctx->fam.clear();
     ctx->fam_vox.clear();
-    CHECK(mark(ctx, -1, 0));
     for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest first
     for (uint32_t r = 0; r < nr; ++r) CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all));
+    CHECK(join(ctx, ctx->st, ctx->st2));  // everything after the filter runs on st
     (void)N;
     return SM_OK;
 }
@@ -461,7 +484,7 @@ sm_status collect_filter_stats(sm_ctx* ctx) {
     }
     for (size_t k = 0; k < ctx->fam.size(); ++k) {
         float ms;
-        HIPC(hipEventElapsedTime(&ms, ctx->fev[k], ctx->fev[k + 1]));
+        HIPC(hipEventElapsedTime(&ms, ctx->fev[2 * k], ctx->fev[2 * k + 1]));
         const int f = ctx->fam[k];
         if (ctx->fam_vox[k] > 0) ks[f].launches += 1;  // a bucket without paths launches nothing
         ks[f].ms += ms;
@@ -564,6 +587,7 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         delete ctx;
         return SM_ERR_HIP;
     }
+    ctx->st2 = ctx->st;
     if (hipHostMalloc((void**)&ctx->h_changed, 2 * sizeof(int)) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
@@ -601,6 +625,7 @@ void sm_destroy(sm_ctx* ctx) {
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
     for (auto e : ctx->fev) (void)hipEventDestroy(e);
+    for (auto e : ctx->sev) (void)hipEventDestroy(e);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
     if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
     for (int v = 0; v < 2; ++v) {
@@ -612,6 +637,7 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->nslot[v], &ctx->slotpix[v]};
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
+    if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamDestroy(ctx->st2);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     delete ctx;
 }
@@ -755,11 +781,11 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
         CHECK(ensure_filter_bufs(ctx, Dpad));
         WalkArgs a = walk_args(ctx, Dpad, D, d0);
         const uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
-        ctx->nfev = 0;
+        ctx->nfev = ctx->nsev = 0;
         ctx->fam.clear();
         ctx->fam_vox.clear();
-        CHECK(mark(ctx, -1, 0));
         for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl_for(D), 2));
+        CHECK(join(ctx, ctx->st, ctx->st2));
         HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
                                    P<double>(ctx->vol[0])));
         if (A_up) HIPC(hipMemcpyAsync(A_up, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));

@@ -152,15 +152,15 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     MetaVec<CH> mv;
     load_meta<CH>(mv, meta32, lane, head + first, 1, n);
     // pre-heavy light child rows (positions 0 .. hidx-1; up to 3 at a tree root)
+    // unconditional loads (absent rows read row 0, an L2-resident dummy): no wait splits them
     double lr[CH][3][SPL];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-        if (j < n) {
-            const uint32_t hidx = hi_hidx(mfield(mv, j, 3));
+        const int jj = j < n ? j : n - 1;
+        const uint32_t hidx = hi_hidx(mfield(mv, jj, 3));
 #pragma unroll
-            for (int i = 0; i < 3; ++i)
-                if ((uint32_t)i < hidx) load_row<SPL>(U, mfield(mv, j, 4 + i), Dpad, lane, lr[j][i]);
-        }
+        for (int i = 0; i < 3; ++i)
+            load_row<SPL>(U, (uint32_t)i < hidx ? mfield(mv, jj, 4 + i) : 0u, Dpad, lane, lr[j][i]);
     }
     ImgRecs<SPL, CH> rec;
     load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);

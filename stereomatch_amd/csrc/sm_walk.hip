@@ -28,28 +28,41 @@
 #include "sm_walk_util.h"
 
 // paths per wave work item (a bucket's paths occupy consecutive slots: one contiguous range)
+#ifndef WALK_PPW
 #define WALK_PPW 8
+#endif
+// chunk sizes (nodes per software-pipeline stage) of the short-path walkers, per SPL
+#ifndef WALK_UP_CH2
+#define WALK_UP_CH2 4
+#endif
+#ifndef WALK_DN_CH2
+#define WALK_DN_CH2 4
+#endif
 
 
 // ---------------------------------------------------------------------------------------------
 // up pass
 // ---------------------------------------------------------------------------------------------
-template <int SPL, int CH>
+// ROOT: the chunk holds a tree root with three light children (4 children); only that variant
+// carries the extra synchronous load, so the common chunk has no load inside its recurrence
+template <int SPL, int CH, bool ROOT>
 __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, int view, int lane, int W, int Dpad,
                                          int dbase, int dend, const uint2* __restrict__ own, const uint2* __restrict__ oth,
                                          double* __restrict__ U, const WalkShared& sh, double (&xc)[SPL]) {
     // ---- all vector loads of the chunk
+    // light-child rows: unconditional loads (absent children read row 0, an L2-resident dummy) so
+    // that no wait splits the chunk's loads
     double lr[CH][2][SPL];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-        if (j < n) {
-            const uint32_t hi = mfield(mv, j, 3);
-            const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+        const int jj = j < n ? j : n - 1;
+        const uint32_t hi = mfield(mv, jj, 3);
+        const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t i = (uint32_t)k + ((uint32_t)k >= hidx ? 1u : 0u);  // child position of light slot k
-                if (i < nch) load_row<SPL>(U, mfield(mv, j, 4 + (int)i), Dpad, lane, lr[j][k]);
-            }
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t i = (uint32_t)k + ((uint32_t)k >= hidx ? 1u : 0u);  // child position of light slot k
+            const uint32_t cs = i < nch ? mfield(mv, jj, 4 + (int)min(i, 3u)) : 0u;
+            load_row<SPL>(U, cs, Dpad, lane, lr[j][k]);
         }
     }
     ImgRecs<SPL, CH> rec;
@@ -88,7 +101,7 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
                         } else if (kk == 1) {
 #pragma unroll
                             for (int k = 0; k < SPL; ++k) v[k] = lr[j][1][k];
-                        } else {
+                        } else if (ROOT) {
                             load_row<SPL>(U, mfield(mv, j, 4 + (int)i), Dpad, lane, v);  // root's third light child
                         }
                     }
@@ -141,7 +154,13 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
         const int nn = ntop >= head ? min(CH, ntop - head + 1) : 0;
         MetaVec<CH> nxt;
         if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);  // prefetch the next chunk's metadata
-        up_chunk<SPL, CH>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, sh, xc);
+        bool root = false;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) root |= j < n && hi_nch(mfield(cur, j, 3)) == 4u;
+        if (root)
+            up_chunk<SPL, CH, true>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, sh, xc);
+        else
+            up_chunk<SPL, CH, false>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, sh, xc);
         if (nn == 0) break;
         cur = nxt;
         top = ntop;
@@ -206,33 +225,37 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
             S[j] = sh.slut[wp];
             S2[j] = sh.s2lut[wp];
         }
+        // the chunk's recurrence first (registers only), then its stores: no store sits between
+        // two uses of loaded rows, so the loads are waited for once
         double xs[CH][SPL];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             if (j < n) {
+                // branch-free (selects): every loaded row is used on every path, so the compiler
+                // keeps the loads in the chunk's batch instead of sinking them into a branch
                 const uint32_t slot = (uint32_t)(c0 + j);
                 const bool root = par[j] == SM_NONE;
-                if (root) {
+                const bool head = !root && par[j] != slot - 1u;  // parent from an earlier round
 #pragma unroll
-                    for (int k = 0; k < SPL; ++k) xc[k] = u[j][k];  // A(root) = A_up(root)
-                } else if (par[j] != slot - 1u) {                  // path head: parent from an earlier round
-#pragma unroll
-                    for (int k = 0; k < SPL; ++k) xc[k] = __builtin_fma(S[j], xp[j][k], S2[j] * u[j][k]);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < SPL; ++k) xc[k] = __builtin_fma(S[j], xc[k], S2[j] * u[j][k]);
+                for (int k = 0; k < SPL; ++k) {
+                    const double b = head ? xp[j][k] : xc[k];
+                    const double f = __builtin_fma(S[j], b, S2[j] * u[j][k]);
+                    xc[k] = root ? u[j][k] : f;  // A(root) = A_up(root)
                 }
-                const uint32_t hi = mfield(cur, j, 3);
-                if (store_all || (hi_light(hi) && !root)) store_row<SPL>(V.U, slot, Dpad, lane, xc);
             }
 #pragma unroll
             for (int k = 0; k < SPL; ++k) xs[j][k] = xc[k];
         }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (j < n && (store_all || (hi_light(mfield(cur, j, 3)) && par[j] != SM_NONE)))
+                store_row<SPL>(V.U, (uint32_t)(c0 + j), Dpad, lane, xs[j]);
+        }
         double mn;
         int mi;
         wta_chunk<SPL, CH>(xs, lane, dloc0, dcall, mn, mi);
-        if (lane < n) {
-            const uint32_t pix = meta32[(size_t)(c0 + lane) * 8];  // lane j stores node j's result
+        const uint32_t pix = meta_pix_of_lane<CH>(cur, lane);  // all lanes active: bpermute sources
+        if (lane < n) {  // lane j stores node j's result
             V.idx[pix] = dglob0 + mi;
             V.minc[pix] = mn;
             V.disp[pix] = (float)(dglob0 + mi);
@@ -275,7 +298,7 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
     } else {
         switch (spl) {
             case 1: up_launch<1, 4>(st, g, a); break;
-            case 2: up_launch<2, 4>(st, g, a); break;
+            case 2: up_launch<2, WALK_UP_CH2>(st, g, a); break;
             default: up_launch<4, 2>(st, g, a); break;
         }
     }
@@ -296,7 +319,7 @@ static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, i
     } else {
         switch (spl) {
             case 1: down_launch<1, 4>(st, g, a, store_all); break;
-            case 2: down_launch<2, 4>(st, g, a, store_all); break;
+            case 2: down_launch<2, WALK_DN_CH2>(st, g, a, store_all); break;
             default: down_launch<4, 4>(st, g, a, store_all); break;
         }
     }

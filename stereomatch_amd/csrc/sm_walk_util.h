@@ -83,6 +83,20 @@ __device__ __forceinline__ uint32_t mfield(const MetaVec<CH>& mv, int j, int f) 
     return __builtin_amdgcn_readlane(mv.w[j >> 3], ((j & 7) << 3) + f);
 }
 
+// lane j (< CH) gets node j's pixel (word 0) from the lane-distributed metadata, no memory access.
+// Call with every lane active: ds_bpermute reads nothing from inactive source lanes.
+template <int CH>
+__device__ __forceinline__ uint32_t meta_pix_of_lane(const MetaVec<CH>& mv, int lane) {
+    const int src = ((lane & 7) << 3) << 2;  // byte address of lane 8*(lane%8)
+    uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)mv.w[0]);
+#pragma unroll
+    for (int q = 1; q < (CH + 7) / 8; ++q) {
+        const uint32_t t = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)mv.w[q]);
+        r = (lane >> 3) == q ? t : r;
+    }
+    return r;
+}
+
 // SmMeta words: 0 pix, 1 parent, 2 lo (wp|cw0|cw1), 3 hi (cw2|cw3|nch|hidx|has_light), 4..7 cslot
 __device__ __forceinline__ uint32_t lo_wp(uint32_t lo) { return lo & 1023u; }
 __device__ __forceinline__ uint32_t cw_of(uint32_t lo, uint32_t hi, int i) {
@@ -161,10 +175,13 @@ __device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, 
 }
 
 
-// image records of CH path nodes: own(x), own(x+1) and the SPL+1 matched-image records a lane needs
+// image records of CH path nodes: own(x), own(x+1) (one lane-dependent load: lanes 2m / 2m+1 hold
+// x / x+1) and the SPL+1 matched-image records a lane needs.  All loads are unconditional (rows of
+// absent nodes are clamped to the last valid one) and nothing reads the loaded values here, so a
+// chunk's loads are all in flight before the first wait.
 template <int SPL, int CH>
 struct ImgRecs {
-    uint2 ob[CH][SPL + 1], o0[CH], o1[CH];
+    uint2 ob[CH][SPL + 1], own[CH];
 };
 
 template <int SPL, int CH>
@@ -172,20 +189,17 @@ __device__ __forceinline__ void load_recs(const MetaVec<CH>& mv, int n, int view
                                           const uint2* __restrict__ own, const uint2* __restrict__ oth, ImgRecs<SPL, CH>& r) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-        if (j < n) {
-            const int pix = (int)mfield(mv, j, 0);
-            const int y = pix / W;
-            const int x = pix - y * W;
-            const size_t row = (size_t)y * W;
-            // own pixels x, x+1 through a lane-dependent (vector) load: a uniform address would become
-            // a scalar-cache load whose lgkmcnt waits serialise with the LDS table reads
-            const uint2 t = own[row + x + (lane & 1)];  // x+1 == W reads the next row / the pad: masked below
-            r.o0[j] = make_uint2(__builtin_amdgcn_readlane(t.x, 0), __builtin_amdgcn_readlane(t.y, 0));
-            r.o1[j] = make_uint2(__builtin_amdgcn_readlane(t.x, 1), __builtin_amdgcn_readlane(t.y, 1));
-            const long long base = view ? (long long)(row + x) + dbase : (long long)(row + x) - dbase - (SPL - 1);
+        const int jj = j < n ? j : n - 1;
+        const int pix = (int)mfield(mv, jj, 0);
+        const int y = pix / W;
+        const int x = pix - y * W;
+        const size_t row = (size_t)y * W;
+        // own pixels x, x+1 through a lane-dependent (vector) load: a uniform address would become
+        // a scalar-cache load whose lgkmcnt waits serialise with the LDS table reads
+        r.own[j] = own[row + x + (lane & 1)];  // x+1 == W reads the next row / the pad: masked below
+        const long long base = view ? (long long)(row + x) + dbase : (long long)(row + x) - dbase - (SPL - 1);
 #pragma unroll
-            for (int q = 0; q <= SPL; ++q) r.ob[j][q] = oth[base + q];
-        }
+        for (int q = 0; q <= SPL; ++q) r.ob[j][q] = oth[base + q];
     }
 }
 
@@ -199,6 +213,8 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
         const int pix = (int)mfield(mv, j, 0);
         const int y = pix / W;
         const int x = pix - y * W;
+        const uint2 o0 = make_uint2(__builtin_amdgcn_readlane(r.own[j].x, 0), __builtin_amdgcn_readlane(r.own[j].y, 0));
+        const uint2 o1 = make_uint2(__builtin_amdgcn_readlane(r.own[j].x, 1), __builtin_amdgcn_readlane(r.own[j].y, 1));
 #pragma unroll
         for (int k = 0; k < SPL; ++k) {
             const int d = dbase + k;
@@ -206,10 +222,10 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
             bool ok;
             if (view) {  // right reference: right(x) vs left(x+d)
                 ok = d < dend && x + d + 1 < W;
-                v = agd_rec(r.o0[j], r.ob[j][k], rgray(r.o1[j]), rgray(r.ob[j][k + 1]), atab);
+                v = agd_rec(o0, r.ob[j][k], rgray(o1), rgray(r.ob[j][k + 1]), atab);
             } else {     // left pixel x at d: cost(x-d, d); x-d<0 and column W-1 -> 3.0
                 ok = d < dend && x - d >= 0 && x + 1 < W;
-                v = agd_rec(r.ob[j][SPL - 1 - k], r.o0[j], rgray(r.ob[j][SPL - k]), rgray(r.o1[j]), atab);
+                v = agd_rec(r.ob[j][SPL - 1 - k], o0, rgray(r.ob[j][SPL - k]), rgray(o1), atab);
             }
             c[j][k] = (double)(ok ? v : 3.0f);
         }
