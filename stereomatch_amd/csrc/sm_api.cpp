@@ -50,12 +50,14 @@ struct sm_ctx {
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
     DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
+    DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
     DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2];
     DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
+    uint32_t mst_components = 0, mst_edges = 0;  // after the tile phase (max over views)
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
     struct HostRounds {
         uint32_t nrounds = 0, npaths = 0, n_has_light = 0;
@@ -177,7 +179,6 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->mD[v], N));
         HIPC(hipMemsetAsync(ctx->mR[v].p, 0, N, ctx->st));
         HIPC(hipMemsetAsync(ctx->mD[v].p, 0, N, ctx->st));
-        HIPC(hipMemsetAsync(ctx->best[v].p, 0xFF, N * 8, ctx->st));
         a.wR[v] = P<uint16_t>(ctx->wR[v]);
         a.wD[v] = P<uint16_t>(ctx->wD[v]);
         a.comp[v] = P<uint32_t>(ctx->comp[v]);
@@ -191,10 +192,53 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     a.flags[0] = P<int>(ctx->changed);
     a.flags[1] = P<int>(ctx->changed) + SM_MST_MAX_ROUNDS;
     HIPC(launch_bor_local(ctx->st, a, W, H));
-    // global rounds: every kernel of round r exits at once if round r-1 hooked nothing, so the
-    // host only synchronises every 4 rounds to decide whether to enqueue more
+    static const bool pixel_rounds = getenv("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B switch
+    if (pixel_rounds) {
+        for (int v = 0; v < nviews; ++v) HIPC(hipMemsetAsync(ctx->best[v].p, 0xFF, N * 8, ctx->st));
+        // global rounds: every kernel of round r exits at once if round r-1 hooked nothing, so the
+        // host only synchronises every 4 rounds to decide whether to enqueue more
+        for (int r = 0; r < SM_MST_MAX_ROUNDS; ++r) {
+            HIPC(launch_bor_round(ctx->st, a, W, H, r));
+            if ((r & 3) == 3) {
+                HIPC(hipMemcpyAsync(ctx->h_changed, P<int>(ctx->changed) + r, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+                HIPC(hipMemcpyAsync(ctx->h_changed + 1, P<int>(ctx->changed) + SM_MST_MAX_ROUNDS + r, sizeof(int),
+                                    hipMemcpyDeviceToHost, ctx->st));
+                HIPC(hipStreamSynchronize(ctx->st));
+                if (ctx->h_changed[0] == 0 && (nviews < 2 || ctx->h_changed[1] == 0)) break;
+            }
+        }
+        return SM_OK;
+    }
+    // contracted rounds on the component graph left by the tile phase
+    MstCompact c{};
+    c.emax = 2 * N;
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->cedge[v], 2 * (2 * N) * 16));
+        CHECK(ensure(ctx, ctx->clab[v], N * 4));
+        CHECK(ensure(ctx, ctx->chook[v], N * 4));
+        CHECK(ensure(ctx, ctx->ccnt[v], 16));
+        HIPC(hipMemsetAsync(ctx->ccnt[v].p, 0, 16, ctx->st));
+        c.cid[v] = P<uint32_t>(ctx->root[v]);
+        c.counts[v] = P<uint32_t>(ctx->ccnt[v]);
+        c.edges[v] = ctx->cedge[v].p;
+        c.lab[v] = P<uint32_t>(ctx->clab[v]);
+        c.hook[v] = P<uint32_t>(ctx->chook[v]);
+    }
+    HIPC(launch_bor_compact(ctx->st, a, c, W, H));
+    for (int v = 0; v < nviews; ++v)
+        HIPC(hipMemcpyAsync(ctx->h_changed + 2 + 2 * v, c.counts[v], 8, hipMemcpyDeviceToHost, ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));
+    uint32_t kmax = 0, emax = 0;
+    for (int v = 0; v < nviews; ++v) {
+        kmax = std::max(kmax, (uint32_t)ctx->h_changed[2 + 2 * v]);
+        emax = std::max(emax, (uint32_t)ctx->h_changed[3 + 2 * v]);
+    }
+    ctx->mst_components = kmax;
+    ctx->mst_edges = emax;
+    if (emax == 0) return SM_OK;
+    HIPC(launch_bor_cinit(ctx->st, a, c, kmax));
     for (int r = 0; r < SM_MST_MAX_ROUNDS; ++r) {
-        HIPC(launch_bor_round(ctx->st, a, W, H, r));
+        HIPC(launch_bor_cround(ctx->st, a, c, W, kmax, emax, r));
         if ((r & 3) == 3) {
             HIPC(hipMemcpyAsync(ctx->h_changed, P<int>(ctx->changed) + r, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
             HIPC(hipMemcpyAsync(ctx->h_changed + 1, P<int>(ctx->changed) + SM_MST_MAX_ROUNDS + r, sizeof(int),
@@ -588,7 +632,7 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         return SM_ERR_HIP;
     }
     ctx->st2 = ctx->st;
-    if (hipHostMalloc((void**)&ctx->h_changed, 2 * sizeof(int)) != hipSuccess ||
+    if (hipHostMalloc((void**)&ctx->h_changed, 8 * sizeof(int)) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
         return SM_ERR_HIP;
@@ -620,7 +664,8 @@ void sm_destroy(sm_ctx* ctx) {
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
                          &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v], &ctx->Cst[v],
-                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v]};
+                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v],
+                         &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);

@@ -409,6 +409,215 @@ __global__ void k_bor_relabel(MstPair P, int W, int H, int rnd) {
     V.comp[p] = V.root[V.comp[p]];
 }
 
+// ---------------------------------------------------------------------------------------------
+// Contracted Boruvka.  After k_bor_local most pixels share a tile component; the remaining rounds
+// run on the component graph: compact component ids (k_cid), the list of inter-component pixel
+// edges (k_cedges, same 64-bit keys), then per round min over edges (k_cmin), hook (k_chook),
+// root chase (k_croot) and relabel (k_crelabel) over K components / E' edges instead of N pixels.
+// The keys and the mutual-choice rule are those of the pixel rounds, so the MST is identical.
+// ---------------------------------------------------------------------------------------------
+struct CEdge {
+    unsigned long long key;
+    uint32_t u, v;  // compact ids of the endpoint components after the tile phase
+};
+
+struct CView {
+    const uint16_t* wR;
+    const uint16_t* wD;
+    const uint32_t* comp;  // pixel -> tile-phase representative pixel
+    uint32_t* cid;         // representative pixel -> compact id (only at representatives)
+    uint32_t* counts;      // [0] K components, [1] / [2] live edges in list 0 / 1
+    CEdge* edges;          // two lists of emax edges
+    size_t emax;
+    uint32_t* lab;         // compact id -> current root id
+    uint32_t* hook;        // root id -> hooked root
+    unsigned long long* best;
+    uint8_t* mR;
+    uint8_t* mD;
+    int* flags;
+};
+struct CPair {
+    CView v[2];
+};
+
+// Compaction appends: every block reserves its whole range with ONE atomic (same-address
+// atomics serialise in L2 at ~10 ns each; a per-wave append over 2.3M pixels cost 0.6-1.5 ms).
+#define CBLK 256   // threads per compaction block
+#define CPT 16     // pixels per thread (k_cid, k_cedges)
+#define EPT 4      // edges per thread (k_cmin: latency-bound, wants more waves)
+
+// exclusive block scan of cnt + one atomicAdd on counter: returns this thread's first slot
+__device__ __forceinline__ uint32_t block_append(uint32_t cnt, uint32_t* counter) {
+    __shared__ uint32_t s_w[CBLK / 64];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < CBLK / 64; ++w) {
+            const uint32_t u = s_w[w];
+            s_w[w] = t;
+            t += u;
+        }
+        s_base = t ? atomicAdd(counter, t) : 0u;
+    }
+    __syncthreads();
+    return s_base + s_w[wave] + x - cnt;
+}
+
+__global__ __launch_bounds__(CBLK) void k_cid(CPair P, uint32_t N) {
+    const CView V = P.v[blockIdx.y];
+    const uint32_t base = blockIdx.x * (CBLK * CPT) + threadIdx.x;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const uint32_t p = base + i * CBLK;
+        if (p < N && V.comp[p] == p) bits |= 1u << i;
+    }
+    uint32_t id = block_append(__builtin_popcount(bits), &V.counts[0]);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i)
+        if (bits & (1u << i)) V.cid[base + i * CBLK] = id++;
+}
+
+__global__ __launch_bounds__(CBLK) void k_cedges(CPair P, int W, int H) {
+    const CView V = P.v[blockIdx.y];
+    const uint32_t N = (uint32_t)W * (uint32_t)H;
+    const uint32_t base = blockIdx.x * (CBLK * CPT) + threadIdx.x;
+    uint32_t bits = 0;  // bit 2i: right edge of pixel i, bit 2i+1: down edge
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const uint32_t p = base + i * CBLK;
+        if (p >= N) continue;
+        const uint32_t x = p % (uint32_t)W;
+        const uint32_t c = V.comp[p];
+        if (x + 1 < (uint32_t)W && V.comp[p + 1] != c) bits |= 1u << (2 * i);
+        if (p + W < N && V.comp[p + W] != c) bits |= 2u << (2 * i);
+    }
+    uint32_t slot = block_append(__builtin_popcount(bits), &V.counts[1]);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        if (!(bits & (3u << (2 * i)))) continue;
+        const uint32_t p = base + i * CBLK;
+        const uint32_t cu = V.cid[V.comp[p]];
+        if (bits & (1u << (2 * i))) V.edges[slot++] = CEdge{sm_edge_key(V.wR[p], p, 0u), cu, V.cid[V.comp[p + 1]]};
+        if (bits & (2u << (2 * i))) V.edges[slot++] = CEdge{sm_edge_key(V.wD[p], p, 1u), cu, V.cid[V.comp[p + W]]};
+    }
+}
+
+__global__ void k_cinit(CPair P) {
+    const CView V = P.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= V.counts[0]) return;
+    V.lab[i] = i;
+    V.best[i] = SM_KEY_NONE;
+}
+
+__device__ __forceinline__ bool cround_done(const CView& V, int r) { return r > 0 && V.flags[r - 1] == 0; }
+
+// Segmented min over runs of equal target among consecutive lanes (shfl_up scan where a lane
+// only folds in a value from a lane with the same target: any such subset is valid, and a run's
+// last lane ends up with the whole run's minimum), then one atomicMin per run.  Fixed cost,
+// unlike a ballot loop over distinct targets (edges of a wave touch ~30 components in round 0).
+__device__ __forceinline__ void wave_atomic_min(bool active, uint32_t c, unsigned long long k, unsigned long long* best) {
+    const int lane = threadIdx.x & 63;
+    if (!active) { c = 0xFFFFFFFFu; k = SM_KEY_NONE; }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long y = __shfl_up(k, off);
+        const uint32_t cy = __shfl_up(c, off);
+        if (lane >= off && cy == c && y < k) k = y;
+    }
+    const uint32_t cn = __shfl_down(c, 1);
+    if (active && (lane == 63 || cn != c)) atomicMin(&best[c], k);
+}
+
+// round r reads the edge list (r & 1) and appends the edges that still join two components to
+// list (r & 1) ^ 1 (endpoints relabelled), so each round only sweeps live edges
+__global__ __launch_bounds__(CBLK) void k_cmin(CPair P, int rnd) {
+    const CView V = P.v[blockIdx.y];
+    if (cround_done(V, rnd)) return;
+    const int ib = rnd & 1;
+    const uint32_t ne = V.counts[1 + ib];
+    const uint32_t base = blockIdx.x * (CBLK * EPT) + threadIdx.x;
+    if (blockIdx.x * (CBLK * EPT) >= ne) return;  // block-uniform
+    const CEdge* in = V.edges + (size_t)ib * V.emax;
+    CEdge* out = V.edges + (size_t)(ib ^ 1) * V.emax;
+    uint32_t bits = 0;
+    CEdge keep[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const uint32_t e = base + i * CBLK;
+        const bool live = e < ne;
+        CEdge E{SM_KEY_NONE, 0u, 0u};
+        if (live) E = in[e];
+        const uint32_t lu = live ? V.lab[E.u] : 0u, lv = live ? V.lab[E.v] : 0u;
+        const bool act = live && lu != lv;
+        wave_atomic_min(act, lu, E.key, V.best);
+        wave_atomic_min(act, lv, E.key, V.best);
+        keep[i] = CEdge{E.key, lu, lv};
+        if (act) bits |= 1u << i;
+    }
+    uint32_t slot = block_append(__builtin_popcount(bits), &V.counts[2 - ib]);
+#pragma unroll
+    for (int i = 0; i < EPT; ++i)
+        if (bits & (1u << i)) out[slot++] = keep[i];
+}
+
+__global__ void k_chook(CPair P, int W, int rnd) {
+    const CView V = P.v[blockIdx.y];
+    if (cround_done(V, rnd)) return;
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0) V.counts[1 + (rnd & 1)] = 0;  // list just read by k_cmin: next round's output
+    if (c >= V.counts[0] || V.lab[c] != c) return;  // current roots only
+    uint32_t h = c;
+    const unsigned long long k = V.best[c];
+    if (k != SM_KEY_NONE) {
+        const uint32_t a = (uint32_t)(k >> 1) & 0xFFFFFFFFu;
+        const uint32_t vert = (uint32_t)(k & 1ull);
+        const uint32_t b = a + (vert ? (uint32_t)W : 1u);
+        const uint32_t la = V.lab[V.cid[V.comp[a]]];
+        const uint32_t c2 = la == c ? V.lab[V.cid[V.comp[b]]] : la;
+        if (!(V.best[c2] == k && c < c2)) {  // mutual choice: the smaller id stays root
+            h = c2;
+            if (vert) V.mD[a] = 1; else V.mR[a] = 1;
+            V.flags[rnd] = 1;
+        }
+    }
+    V.hook[c] = h;
+}
+
+__global__ void k_croot(CPair P, int rnd) {
+    const CView V = P.v[blockIdx.y];
+    if (cround_done(V, rnd) || V.flags[rnd] == 0) return;
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= V.counts[0] || V.lab[c] != c) return;
+    uint32_t r = V.hook[c];
+    for (int it = 0; it < (1 << 26); ++it) {
+        const uint32_t rr = V.hook[r];
+        if (rr == r) break;
+        r = rr;
+    }
+    V.best[c] = SM_KEY_NONE;  // reset for the next round
+    V.hook[c] = r;            // in-place shortcut: concurrent chasers still reach the same root
+}
+
+__global__ void k_crelabel(CPair P, int rnd) {
+    const CView V = P.v[blockIdx.y];
+    if (cround_done(V, rnd) || V.flags[rnd] == 0) return;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= V.counts[0]) return;
+    V.lab[i] = V.hook[V.lab[i]];
+}
+
 // cross-rank WTA helpers: candidate index where this rank holds the global minimum
 __global__ void k_cand(const double* __restrict__ minc, const double* __restrict__ gmin, const int32_t* __restrict__ idx,
                        int32_t* __restrict__ cand, size_t N) {
@@ -520,5 +729,39 @@ __global__ void k_lr_check(float* __restrict__ left, const float* __restrict__ r
 
 hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp) {
     hipLaunchKernelGGL(k_lr_check, dim3((W + 255) / 256, H), dim3(256), 0, st, left, right, W, H, max_disp);
+    return hipGetLastError();
+}
+
+static CPair make_cpair(const MstArgs& a, const MstCompact& c) {
+    CPair P;
+    for (int v = 0; v < 2; ++v)
+        P.v[v] = CView{a.wR[v], a.wD[v], a.comp[v], c.cid[v], c.counts[v], reinterpret_cast<CEdge*>(c.edges[v]), c.emax,
+                       c.lab[v], c.hook[v], a.best[v], a.mR[v], a.mD[v], a.flags[v]};
+    return P;
+}
+
+hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int H) {
+    const CPair P = make_cpair(a, c);
+    const uint32_t N = (uint32_t)W * (uint32_t)H;
+    const dim3 g((N + CBLK * CPT - 1) / (CBLK * CPT), a.nviews);
+    hipLaunchKernelGGL(k_cid, g, dim3(CBLK), 0, st, P, N);
+    hipLaunchKernelGGL(k_cedges, g, dim3(CBLK), 0, st, P, W, H);
+    return hipGetLastError();
+}
+
+hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c, uint32_t kmax) {
+    const CPair P = make_cpair(a, c);
+    hipLaunchKernelGGL(k_cinit, dim3((kmax + 255) / 256, a.nviews), dim3(256), 0, st, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, uint32_t kmax, uint32_t emax,
+                             int r) {
+    const CPair P = make_cpair(a, c);
+    const dim3 gk((kmax + 255) / 256, a.nviews), ge((emax + CBLK * EPT - 1) / (CBLK * EPT), a.nviews);
+    hipLaunchKernelGGL(k_cmin, ge, dim3(CBLK), 0, st, P, r);
+    hipLaunchKernelGGL(k_chook, gk, dim3(256), 0, st, P, W, r);
+    hipLaunchKernelGGL(k_croot, gk, dim3(256), 0, st, P, r);
+    hipLaunchKernelGGL(k_crelabel, gk, dim3(256), 0, st, P, r);
     return hipGetLastError();
 }

@@ -18,6 +18,16 @@ struct MstArgs {
     int* flags[2];   // per view: flags[r] for r < SM_MST_MAX_ROUNDS
 };
 
+// contracted Boruvka (after the tile phase): component graph buffers per view
+struct MstCompact {
+    uint32_t* cid[2];     // [pixel] compact id of a tile-phase representative
+    uint32_t* counts[2];  // [0] K, [1] E' of edge list 0, [2] of list 1
+    void* edges[2];       // two CEdge lists of emax (16 B each)
+    size_t emax;
+    uint32_t* lab[2];     // [K]
+    uint32_t* hook[2];    // [K]
+};
+
 #define SM_MST_MAX_ROUNDS 64
 #define SM_REC_PAD 1024  // records of padding before/after each image (walker loads stay in bounds)
 
@@ -49,6 +59,10 @@ hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* l
                               const float* atab, int W, int H, int d0, int D, float* lvol, float* rvol);
 hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H);
 hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r);
+hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int H);
+hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c, uint32_t kmax);
+hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, uint32_t kmax, uint32_t emax,
+                             int r);
 hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
