@@ -57,7 +57,7 @@ struct sm_ctx {
     DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2];
     DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
-    uint32_t mst_components = 0, mst_edges = 0;  // after the tile phase (max over views)
+    int mst_rounds = 12;  // contracted Boruvka rounds the previous frame enqueued
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
     struct HostRounds {
         uint32_t nrounds = 0, npaths = 0, n_has_light = 0;
@@ -166,6 +166,10 @@ sm_status stage_prep(sm_ctx* ctx) {
     return SM_OK;
 }
 
+static bool hooked_any(const int* hf, int nviews, int q) {
+    return hf[q] != 0 || (nviews > 1 && hf[SM_MST_MAX_ROUNDS + q] != 0);
+}
+
 sm_status stage_mst(sm_ctx* ctx, int nviews) {
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H;
@@ -173,7 +177,7 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     a.nviews = nviews;
     for (int v = 0; v < 2; ++v) {
         CHECK(ensure(ctx, ctx->comp[v], N * 4));
-        CHECK(ensure(ctx, ctx->best[v], N * 8));
+        CHECK(ensure(ctx, ctx->best[v], 2 * N * 8));
         CHECK(ensure(ctx, ctx->root[v], N * 4));
         CHECK(ensure(ctx, ctx->mR[v], N));
         CHECK(ensure(ctx, ctx->mD[v], N));
@@ -212,6 +216,7 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     // contracted rounds on the component graph left by the tile phase
     MstCompact c{};
     c.emax = 2 * N;
+    c.bstride = N;
     for (int v = 0; v < 2; ++v) {
         CHECK(ensure(ctx, ctx->cedge[v], 2 * (2 * N) * 16));
         CHECK(ensure(ctx, ctx->clab[v], N * 4));
@@ -225,28 +230,32 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
         c.hook[v] = P<uint32_t>(ctx->chook[v]);
     }
     HIPC(launch_bor_compact(ctx->st, a, c, W, H));
-    for (int v = 0; v < nviews; ++v)
-        HIPC(hipMemcpyAsync(ctx->h_changed + 2 + 2 * v, c.counts[v], 8, hipMemcpyDeviceToHost, ctx->st));
-    HIPC(hipStreamSynchronize(ctx->st));
-    uint32_t kmax = 0, emax = 0;
-    for (int v = 0; v < nviews; ++v) {
-        kmax = std::max(kmax, (uint32_t)ctx->h_changed[2 + 2 * v]);
-        emax = std::max(emax, (uint32_t)ctx->h_changed[3 + 2 * v]);
-    }
-    ctx->mst_components = kmax;
-    ctx->mst_edges = emax;
-    if (emax == 0) return SM_OK;
-    HIPC(launch_bor_cinit(ctx->st, a, c, kmax));
-    for (int r = 0; r < SM_MST_MAX_ROUNDS; ++r) {
-        HIPC(launch_bor_cround(ctx->st, a, c, W, kmax, emax, r));
-        if ((r & 3) == 3) {
-            HIPC(hipMemcpyAsync(ctx->h_changed, P<int>(ctx->changed) + r, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-            HIPC(hipMemcpyAsync(ctx->h_changed + 1, P<int>(ctx->changed) + SM_MST_MAX_ROUNDS + r, sizeof(int),
-                                hipMemcpyDeviceToHost, ctx->st));
-            HIPC(hipStreamSynchronize(ctx->st));
-            if (ctx->h_changed[0] == 0 && (nviews < 2 || ctx->h_changed[1] == 0)) break;
+    HIPC(launch_bor_cinit(ctx->st, a, c));
+    // Enqueue as many rounds as the previous frame needed (the last one hooks nothing), then
+    // check once: every kernel of round r exits at once when round r-1 hooked nothing.
+    static const bool dbg = getenv("SM_MST_DEBUG") != nullptr;
+    int r = 0, batch = std::max(ctx->mst_rounds, 2);
+    for (;;) {
+        const int end = std::min(r + batch, SM_MST_MAX_ROUNDS);
+        for (; r < end; ++r) {
+            HIPC(launch_bor_cround(ctx->st, a, c, W, r));
+            if (dbg) {
+                uint32_t h[4];
+                HIPC(hipMemcpyAsync(h, c.counts[0], 16, hipMemcpyDeviceToHost, ctx->st));
+                HIPC(hipStreamSynchronize(ctx->st));
+                fprintf(stderr, "mst round %d: K %u live edges %u / %u\n", r, h[0], h[1], h[2]);
+            }
         }
+        int* hf = ctx->h_changed;  // [view][round] hook flags
+        HIPC(hipMemcpyAsync(hf, ctx->changed.p, 2 * SM_MST_MAX_ROUNDS * sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipStreamSynchronize(ctx->st));
+        if (!hooked_any(hf, nviews, r - 1) || r >= SM_MST_MAX_ROUNDS) break;
+        batch = 4;
     }
+    // rounds needed: through the first one that hooked nothing in any view
+    int need = 1;
+    while (need < r && hooked_any(ctx->h_changed, nviews, need - 1)) ++need;
+    ctx->mst_rounds = need;
     return SM_OK;
 }
 
@@ -632,7 +641,7 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         return SM_ERR_HIP;
     }
     ctx->st2 = ctx->st;
-    if (hipHostMalloc((void**)&ctx->h_changed, 8 * sizeof(int)) != hipSuccess ||
+    if (hipHostMalloc((void**)&ctx->h_changed, (2 * SM_MST_MAX_ROUNDS + 8) * sizeof(int)) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
         return SM_ERR_HIP;

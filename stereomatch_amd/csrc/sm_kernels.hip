@@ -431,7 +431,8 @@ struct CView {
     size_t emax;
     uint32_t* lab;         // compact id -> current root id
     uint32_t* hook;        // root id -> hooked root
-    unsigned long long* best;
+    unsigned long long* best;  // two arrays: round r uses best + (r & 1) * bstride
+    size_t bstride;
     uint8_t* mR;
     uint8_t* mD;
     int* flags;
@@ -515,19 +516,20 @@ __global__ __launch_bounds__(CBLK) void k_cedges(CPair P, int W, int H) {
 
 __global__ void k_cinit(CPair P) {
     const CView V = P.v[blockIdx.y];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= V.counts[0]) return;
-    V.lab[i] = i;
-    V.best[i] = SM_KEY_NONE;
+    const uint32_t K = V.counts[0];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < K; i += gridDim.x * blockDim.x) {
+        V.lab[i] = i;
+        V.best[i] = SM_KEY_NONE;
+        V.best[V.bstride + i] = SM_KEY_NONE;
+    }
 }
 
 __device__ __forceinline__ bool cround_done(const CView& V, int r) { return r > 0 && V.flags[r - 1] == 0; }
 
 // Segmented min over runs of equal target among consecutive lanes (shfl_up scan where a lane
 // only folds in a value from a lane with the same target: any such subset is valid, and a run's
-// last lane ends up with the whole run's minimum), then one atomicMin per run.  Fixed cost,
-// unlike a ballot loop over distinct targets (edges of a wave touch ~30 components in round 0).
-__device__ __forceinline__ void wave_atomic_min(bool active, uint32_t c, unsigned long long k, unsigned long long* best) {
+// last lane ends up with the whole run's minimum).  True on the lanes holding a run's minimum.
+__device__ __forceinline__ bool wave_seg_min(bool active, uint32_t& c, unsigned long long& k) {
     const int lane = threadIdx.x & 63;
     if (!active) { c = 0xFFFFFFFFu; k = SM_KEY_NONE; }
 #pragma unroll
@@ -537,85 +539,115 @@ __device__ __forceinline__ void wave_atomic_min(bool active, uint32_t c, unsigne
         if (lane >= off && cy == c && y < k) k = y;
     }
     const uint32_t cn = __shfl_down(c, 1);
-    if (active && (lane == 63 || cn != c)) atomicMin(&best[c], k);
+    return active && (lane == 63 || cn != c);
 }
 
-// round r reads the edge list (r & 1) and appends the edges that still join two components to
-// list (r & 1) ^ 1 (endpoints relabelled), so each round only sweeps live edges
+// Per-block direct-mapped LDS table of component minima: late rounds have few components with
+// thousands of incident edges each, and global atomics on one best[] word serialise in L2.  A
+// slot is claimed by CAS on its tag; a collision falls through to the global atomic.
+#define CTAB 2048
+struct CTable {
+    uint32_t tag[CTAB];
+    unsigned long long mn[CTAB];
+};
+__device__ __forceinline__ void ctab_min(CTable& T, uint32_t c, unsigned long long k, unsigned long long* best) {
+    const uint32_t slot = (c * 2654435761u) >> 21;  // 11-bit multiplicative hash
+    const uint32_t old = atomicCAS(&T.tag[slot], 0xFFFFFFFFu, c);
+    if (old == 0xFFFFFFFFu || old == c) atomicMin(&T.mn[slot], k);
+    else atomicMin(&best[c], k);
+}
+
+// Round r reads edge list (r & 1) and appends the edges that still join two components, with
+// relabelled endpoints, to list (r & 1) ^ 1, so each round sweeps only live edges.  Grid-stride
+// over a fixed grid: the host never needs the edge count.
 __global__ __launch_bounds__(CBLK) void k_cmin(CPair P, int rnd) {
     const CView V = P.v[blockIdx.y];
     if (cround_done(V, rnd)) return;
+    __shared__ CTable T;
     const int ib = rnd & 1;
     const uint32_t ne = V.counts[1 + ib];
-    const uint32_t base = blockIdx.x * (CBLK * EPT) + threadIdx.x;
     if (blockIdx.x * (CBLK * EPT) >= ne) return;  // block-uniform
+    unsigned long long* best = V.best + (size_t)ib * V.bstride;
+    for (int i = threadIdx.x; i < CTAB; i += CBLK) {
+        T.tag[i] = 0xFFFFFFFFu;
+        T.mn[i] = SM_KEY_NONE;
+    }
+    __syncthreads();
     const CEdge* in = V.edges + (size_t)ib * V.emax;
     CEdge* out = V.edges + (size_t)(ib ^ 1) * V.emax;
-    uint32_t bits = 0;
-    CEdge keep[EPT];
+    for (uint32_t b0 = blockIdx.x * (CBLK * EPT); b0 < ne; b0 += gridDim.x * (CBLK * EPT)) {
+        uint32_t bits = 0;
+        CEdge keep[EPT];
 #pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-        const uint32_t e = base + i * CBLK;
-        const bool live = e < ne;
-        CEdge E{SM_KEY_NONE, 0u, 0u};
-        if (live) E = in[e];
-        const uint32_t lu = live ? V.lab[E.u] : 0u, lv = live ? V.lab[E.v] : 0u;
-        const bool act = live && lu != lv;
-        wave_atomic_min(act, lu, E.key, V.best);
-        wave_atomic_min(act, lv, E.key, V.best);
-        keep[i] = CEdge{E.key, lu, lv};
-        if (act) bits |= 1u << i;
+        for (int i = 0; i < EPT; ++i) {
+            const uint32_t e = b0 + i * CBLK + threadIdx.x;
+            const bool live = e < ne;
+            CEdge E{SM_KEY_NONE, 0u, 0u};
+            if (live) E = in[e];
+            uint32_t lu = live ? V.lab[E.u] : 0u, lv = live ? V.lab[E.v] : 0u;
+            const bool act = live && lu != lv;
+            keep[i] = CEdge{E.key, lu, lv};
+            if (act) bits |= 1u << i;
+            unsigned long long ku = E.key, kv = E.key;
+            if (wave_seg_min(act, lu, ku)) ctab_min(T, lu, ku, best);
+            if (wave_seg_min(act, lv, kv)) ctab_min(T, lv, kv, best);
+        }
+        uint32_t slot = block_append(__builtin_popcount(bits), &V.counts[2 - ib]);
+#pragma unroll
+        for (int i = 0; i < EPT; ++i)
+            if (bits & (1u << i)) out[slot++] = keep[i];
     }
-    uint32_t slot = block_append(__builtin_popcount(bits), &V.counts[2 - ib]);
-#pragma unroll
-    for (int i = 0; i < EPT; ++i)
-        if (bits & (1u << i)) out[slot++] = keep[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < CTAB; i += CBLK)
+        if (T.tag[i] != 0xFFFFFFFFu) atomicMin(&best[T.tag[i]], T.mn[i]);
 }
 
 __global__ void k_chook(CPair P, int W, int rnd) {
     const CView V = P.v[blockIdx.y];
     if (cround_done(V, rnd)) return;
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c == 0) V.counts[1 + (rnd & 1)] = 0;  // list just read by k_cmin: next round's output
-    if (c >= V.counts[0] || V.lab[c] != c) return;  // current roots only
-    uint32_t h = c;
-    const unsigned long long k = V.best[c];
-    if (k != SM_KEY_NONE) {
-        const uint32_t a = (uint32_t)(k >> 1) & 0xFFFFFFFFu;
-        const uint32_t vert = (uint32_t)(k & 1ull);
-        const uint32_t b = a + (vert ? (uint32_t)W : 1u);
-        const uint32_t la = V.lab[V.cid[V.comp[a]]];
-        const uint32_t c2 = la == c ? V.lab[V.cid[V.comp[b]]] : la;
-        if (!(V.best[c2] == k && c < c2)) {  // mutual choice: the smaller id stays root
-            h = c2;
-            if (vert) V.mD[a] = 1; else V.mR[a] = 1;
-            V.flags[rnd] = 1;
+    const int ib = rnd & 1;
+    const unsigned long long* best = V.best + (size_t)ib * V.bstride;
+    unsigned long long* best_next = V.best + (size_t)(ib ^ 1) * V.bstride;
+    if (blockIdx.x == 0 && threadIdx.x == 0) V.counts[1 + ib] = 0;  // list k_cmin just read: next output
+    const uint32_t K = V.counts[0];
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < K; c += gridDim.x * blockDim.x) {
+        if (V.lab[c] != c) continue;  // current roots only
+        uint32_t h = c;
+        const unsigned long long k = best[c];
+        if (k != SM_KEY_NONE) {
+            const uint32_t a = (uint32_t)(k >> 1) & 0xFFFFFFFFu;
+            const uint32_t vert = (uint32_t)(k & 1ull);
+            const uint32_t b = a + (vert ? (uint32_t)W : 1u);
+            const uint32_t la = V.lab[V.cid[V.comp[a]]];
+            const uint32_t c2 = la == c ? V.lab[V.cid[V.comp[b]]] : la;
+            if (!(best[c2] == k && c < c2)) {  // mutual choice: the smaller id stays root
+                h = c2;
+                if (vert) V.mD[a] = 1; else V.mR[a] = 1;
+                V.flags[rnd] = 1;
+            }
         }
+        V.hook[c] = h;
+        best_next[c] = SM_KEY_NONE;  // next round's roots are a subset of this round's
     }
-    V.hook[c] = h;
 }
 
-__global__ void k_croot(CPair P, int rnd) {
-    const CView V = P.v[blockIdx.y];
-    if (cround_done(V, rnd) || V.flags[rnd] == 0) return;
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= V.counts[0] || V.lab[c] != c) return;
-    uint32_t r = V.hook[c];
-    for (int it = 0; it < (1 << 26); ++it) {
-        const uint32_t rr = V.hook[r];
-        if (rr == r) break;
-        r = rr;
-    }
-    V.best[c] = SM_KEY_NONE;  // reset for the next round
-    V.hook[c] = r;            // in-place shortcut: concurrent chasers still reach the same root
-}
-
+// Chase every label to the root of its hook tree; shortcut the old root's hook in place
+// (concurrent chasers then still reach the same root).
 __global__ void k_crelabel(CPair P, int rnd) {
     const CView V = P.v[blockIdx.y];
     if (cround_done(V, rnd) || V.flags[rnd] == 0) return;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= V.counts[0]) return;
-    V.lab[i] = V.hook[V.lab[i]];
+    const uint32_t K = V.counts[0];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < K; i += gridDim.x * blockDim.x) {
+        const uint32_t l = V.lab[i];
+        uint32_t r = V.hook[l];
+        for (int it = 0; it < (1 << 26); ++it) {
+            const uint32_t rr = V.hook[r];
+            if (rr == r) break;
+            r = rr;
+        }
+        if (r != l) V.hook[l] = r;
+        V.lab[i] = r;
+    }
 }
 
 // cross-rank WTA helpers: candidate index where this rank holds the global minimum
@@ -736,7 +768,7 @@ static CPair make_cpair(const MstArgs& a, const MstCompact& c) {
     CPair P;
     for (int v = 0; v < 2; ++v)
         P.v[v] = CView{a.wR[v], a.wD[v], a.comp[v], c.cid[v], c.counts[v], reinterpret_cast<CEdge*>(c.edges[v]), c.emax,
-                       c.lab[v], c.hook[v], a.best[v], a.mR[v], a.mD[v], a.flags[v]};
+                       c.lab[v], c.hook[v], a.best[v], c.bstride, a.mR[v], a.mD[v], a.flags[v]};
     return P;
 }
 
@@ -749,19 +781,20 @@ hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact
     return hipGetLastError();
 }
 
-hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c, uint32_t kmax) {
+// fixed grids (grid-stride kernels): K and E' stay on the device
+#define CGRID_K 256    // blocks of 256 over components
+#define CGRID_E 512    // blocks of CBLK * EPT over edges
+
+hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c) {
     const CPair P = make_cpair(a, c);
-    hipLaunchKernelGGL(k_cinit, dim3((kmax + 255) / 256, a.nviews), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(k_cinit, dim3(CGRID_K, a.nviews), dim3(256), 0, st, P);
     return hipGetLastError();
 }
 
-hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, uint32_t kmax, uint32_t emax,
-                             int r) {
+hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r) {
     const CPair P = make_cpair(a, c);
-    const dim3 gk((kmax + 255) / 256, a.nviews), ge((emax + CBLK * EPT - 1) / (CBLK * EPT), a.nviews);
-    hipLaunchKernelGGL(k_cmin, ge, dim3(CBLK), 0, st, P, r);
-    hipLaunchKernelGGL(k_chook, gk, dim3(256), 0, st, P, W, r);
-    hipLaunchKernelGGL(k_croot, gk, dim3(256), 0, st, P, r);
-    hipLaunchKernelGGL(k_crelabel, gk, dim3(256), 0, st, P, r);
+    hipLaunchKernelGGL(k_cmin, dim3(CGRID_E, a.nviews), dim3(CBLK), 0, st, P, r);
+    hipLaunchKernelGGL(k_chook, dim3(CGRID_K, a.nviews), dim3(256), 0, st, P, W, r);
+    hipLaunchKernelGGL(k_crelabel, dim3(CGRID_K, a.nviews), dim3(256), 0, st, P, r);
     return hipGetLastError();
 }

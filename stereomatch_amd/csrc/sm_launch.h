@@ -24,6 +24,7 @@ struct MstCompact {
     uint32_t* counts[2];  // [0] K, [1] E' of edge list 0, [2] of list 1
     void* edges[2];       // two CEdge lists of emax (16 B each)
     size_t emax;
+    size_t bstride;  // second best[] array at best + bstride (best holds 2 * bstride keys)
     uint32_t* lab[2];     // [K]
     uint32_t* hook[2];    // [K]
 };
@@ -60,9 +61,8 @@ hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* l
 hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H);
 hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r);
 hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int H);
-hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c, uint32_t kmax);
-hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, uint32_t kmax, uint32_t emax,
-                             int r);
+hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c);
+hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r);
 hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
