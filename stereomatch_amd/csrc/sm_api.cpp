@@ -196,7 +196,7 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     a.flags[0] = P<int>(ctx->changed);
     a.flags[1] = P<int>(ctx->changed) + SM_MST_MAX_ROUNDS;
     HIPC(launch_bor_local(ctx->st, a, W, H));
-    static const bool pixel_rounds = getenv("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B switch
+    const bool pixel_rounds = getenv("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B path (tests, tools)
     if (pixel_rounds) {
         for (int v = 0; v < nviews; ++v) HIPC(hipMemsetAsync(ctx->best[v].p, 0xFF, N * 8, ctx->st));
         // global rounds: every kernel of round r exits at once if round r-1 hooked nothing, so the

@@ -237,7 +237,7 @@ __device__ __forceinline__ uint64_t key_of(const uint16_t* wR, const uint16_t* w
     }
 }
 
-__global__ __launch_bounds__(BTHREADS) void k_bor_local(MstPair P, int W, int H) {
+__global__ __launch_bounds__(BTHREADS) void k_bor_local(MstPair P, int W, int H, int max_iter) {
     const MstView V = P.v[blockIdx.z];
     __shared__ unsigned long long best[BTN];
     __shared__ uint16_t comp[BTN];
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(BTHREADS) void k_bor_local(MstPair P, int W, int H)
     const int n = tw * th;
     for (int i = threadIdx.x; i < BTN; i += BTHREADS) comp[i] = (uint16_t)i;
     __syncthreads();
-    for (int iter = 0; iter < 64; ++iter) {
+    for (int iter = 0; iter < max_iter; ++iter) {
         for (int i = threadIdx.x; i < BTN; i += BTHREADS) best[i] = SM_KEY_NONE;
         if (threadIdx.x == 0) flag = 0;
         __syncthreads();
@@ -679,6 +679,7 @@ __global__ void k_rows_to_volume(const SmMeta* __restrict__ meta, const double* 
 // ---------------------------------------------------------------------------------------------
 // host-callable launchers (extern "C++" within the library)
 // ---------------------------------------------------------------------------------------------
+#include <cstdlib>
 #include "sm_launch.h"
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
@@ -711,7 +712,11 @@ hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H) {
     for (int v = 0; v < 2; ++v)
         P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v]};
     dim3 g((W + BT - 1) / BT, (H + BT - 1) / BT, a.nviews);
-    hipLaunchKernelGGL(k_bor_local, g, dim3(BTHREADS), 0, st, P, W, H);
+    // Tile-phase Boruvka iterations: any cap is exact (unfinished components continue in the
+    // contracted rounds); 4 is the measured optimum at C2 (tools/gpu_mst_sweep.sh).
+    const char* e = getenv("SM_MST_LOCAL_ITERS");
+    const int max_iter = e ? atoi(e) : 4;
+    hipLaunchKernelGGL(k_bor_local, g, dim3(BTHREADS), 0, st, P, W, H, max_iter);
     return hipGetLastError();
 }
 

@@ -54,6 +54,23 @@ def test_mst_matches_reference_segment_graph(gpu_ctx, name):
         assert t["subtree_size"][0] == W * H
 
 
+@pytest.mark.parametrize("iters", ["0", "1", "64"])
+@pytest.mark.parametrize("pixel_rounds", [False, True])
+def test_mst_phase_split_exact(gpu_ctx, monkeypatch, iters, pixel_rounds):
+    """Any tile-phase iteration cap (SM_MST_LOCAL_ITERS: 0 = pure global Boruvka, 64 = tile
+    phase to completion) and either global-round engine (contracted component graph, or the
+    pixel rounds kept as the SM_MST_PIXEL_ROUNDS A/B path) gives the reference's MST."""
+    monkeypatch.setenv("SM_MST_LOCAL_ITERS", iters)
+    if pixel_rounds:
+        monkeypatch.setenv("SM_MST_PIXEL_ROUNDS", "1")
+    else:
+        monkeypatch.delenv("SM_MST_PIXEL_ROUNDS", raising=False)
+    z = load_case(CASES[-1])
+    for v in ("left", "right"):
+        t = gpu_ctx.build_tree(z[v])
+        np.testing.assert_array_equal(t["mask"], z[v + "_ref_mst_mask"])
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_aggregate_bitexact_golden(gpu_ctx, name):
     z = load_case(name)
