@@ -371,6 +371,11 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.nodes.assign(R + 5 * SM_NBUCKETS + 4, R + 6 * SM_NBUCKETS + 4);
         L.npaths = R[SM_NBUCKETS];
         if (L.nrounds == 0 || L.npaths == 0) return fail(ctx, SM_ERR_STATE, "layout produced no paths");
+        if (getenv("SM_LAYOUT_DEBUG"))  // per-round path statistics (tools/gpu_layout_dbg.sh)
+            for (uint32_t r = 0; r < L.nrounds; ++r)
+                fprintf(stderr, "view %d round %u: long %u paths %u nodes maxlen %u | short %u paths %u nodes maxlen %u\n", v, r,
+                        L.begin[2 * r + 1] - L.begin[2 * r], L.nodes[2 * r], L.maxlen[2 * r], L.begin[2 * r + 2] - L.begin[2 * r + 1],
+                        L.nodes[2 * r + 1], L.maxlen[2 * r + 1]);
     }
     return SM_OK;
 }

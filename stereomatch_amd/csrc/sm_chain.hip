@@ -296,8 +296,8 @@ struct UpRing {
 // NN consecutive nodes k0.. of a staged group; NN is a compile-time count so the LDS waits are
 // exact; THIRD = the node-by-node path that also applies a root's third post-heavy child.
 // Every row is read unconditionally (the ring is zeroed at kernel start, so rows a helper did
-// not stage are stale-but-finite): absent posts carry S = 0, and Pre is scaled by a 0/1 factor
-// from the presence flags -- exact, and off the serial chain.
+// not stage are stale-but-finite): absent posts carry S = 0, and an absent Pre is replaced by +0
+// through a select on the presence flags -- exact, and off the serial chain.
 template <int SPL, int NN, bool THIRD>
 __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0, int j0, int top, int e0,
                                          double (&x)[Split<SPL>::CS], double* __restrict__ U, int Dpad) {
@@ -317,11 +317,11 @@ __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0
     }
 #pragma unroll
     for (int k = 0; k < NN; ++k) {
-        const double fpre = (flags >> (3 * (k0 + k))) & UP_F_PRE ? 1.0 : 0.0;
+        const bool hpre = (flags >> (3 * (k0 + k))) & UP_F_PRE;
         double acc[CS];
 #pragma unroll
         for (int q = 0; q < CS; ++q) {
-            acc[q] = __builtin_fma(Sh[k], x[q], pr[k][q] * fpre);
+            acc[q] = __builtin_fma(Sh[k], x[q], hpre ? pr[k][q] : 0.0);  // select: exact +0 whatever the stale row holds
             acc[q] = __builtin_fma(Sp1[k], p1[k][q], acc[q]);
             acc[q] = __builtin_fma(Sp2[k], p2[k][q], acc[q]);
         }

@@ -1,6 +1,6 @@
 """Per-round MST statistics (SM_MST_DEBUG) on the bench workload; GPU only."""
 import os, sys
-os.environ["SM_MST_DEBUG"] = "1"
+os.environ[os.environ.get("DBG", "SM_MST_DEBUG")] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import stereomatch_amd as sm
 from bench import make_pair
