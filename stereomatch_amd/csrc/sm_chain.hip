@@ -205,7 +205,15 @@ template <int SPL>
 struct Split {
     static constexpr int NCW = SPL == 1 ? 1 : 2;  // chain waves
     static constexpr int CS = SPL / NCW;          // slices per chain lane
+#ifdef SM_CHAIN_EXCL
+    // chain waves own their SIMDs (wave w runs on SIMD w % 4): helpers only on the other SIMDs
+    static constexpr int NH = CHN_WAVES / 4 * (4 - NCW);
+    // role of wave w: chain wave w (w < NCW), helper index, or -1 (idle)
+    __device__ static int helper_of(int w) { return (w & 3) < NCW ? -1 : (w >> 2) * (4 - NCW) + (w & 3) - NCW; }
+#else
     static constexpr int NH = CHN_WAVES - NCW;    // helper waves
+    __device__ static int helper_of(int w) { return w - NCW; }
+#endif
 };
 
 template <int CS>
@@ -309,11 +317,21 @@ __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0
         Sh[k] = sl.s[k0 + k].Sh;
         Sp1[k] = sl.s[k0 + k].Sp1;
         Sp2[k] = sl.s[k0 + k].Sp2;
+#ifdef SM_PROF_NOROWS
+#pragma unroll
+        for (int q = 0; q < CS; ++q) {
+            pr[k][q] = 0.25 * (k + q);
+            p1[k][q] = 0.5 * (k + q);
+            p2[k][q] = 0.125 * (k + q);
+            cv[k][q] = 0.75f;
+        }
+#else
         lds_read_at<CS>(sl.pre[k0 + k], e0, pr[k]);
         lds_read_at<CS>(sl.post1[k0 + k], e0, p1[k]);
         lds_read_at<CS>(sl.post2[k0 + k], e0, p2[k]);
 #pragma unroll
         for (int q = 0; q < CS; ++q) cv[k][q] = sl.c[k0 + k][e0 + q];
+#endif
     }
 #pragma unroll
     for (int k = 0; k < NN; ++k) {
@@ -333,7 +351,9 @@ __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0
         }
 #pragma unroll
         for (int q = 0; q < CS; ++q) x[q] = acc[q] + (double)cv[k][q];
+#ifndef SM_PROF_NOSTORE
         global_write_at<CS>(U, (uint32_t)(top - (j0 + k)), Dpad, e0, x);
+#endif
     }
 }
 
@@ -381,6 +401,9 @@ __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head
         tc += clock64() - tb;
 #endif
     }
+#ifdef SM_PROF_NOSTORE
+    global_write_at<CS>(U, (uint32_t)top, Dpad, e0, x);  // keeps the recurrence alive
+#endif
 #ifdef SM_CHAIN_PROF
     if (blockIdx.x == 0 && lane == 0 && w == 0)
         printf("up chain view %d len %d cycles %lld spins %u wait %lld compute %lld\n", (int)blockIdx.y, len,
@@ -507,8 +530,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (wave < Split<SPL>::NCW)
         up_chain_wave<SPL>(ring, wave, head, len, lane, V.U, Dpad);
-    else
-        up_helper_wave<SPL>(ring, wave - Split<SPL>::NCW, head, len, lane, view ? meta1 : meta0, V.U,
+    else if (Split<SPL>::helper_of(wave) >= 0)
+        up_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, view ? meta1 : meta0, V.U,
                             view ? Cst1 : Cst0, Dpad);
 }
 
@@ -559,7 +582,8 @@ __device__ __forceinline__ void down_group(DownSlot<SPL>& sl, int k0, int e0, do
 
 template <int SPL>
 __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int len, int lane,
-                                                const double* __restrict__ U, uint32_t hparent, int Dpad) {
+                                                const double* __restrict__ U, uint32_t hparent, int Dpad,
+                                                const uint32_t* ready, uint32_t epoch) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, CS = Split<SPL>::CS;
     __builtin_amdgcn_s_setprio(3);
     unsigned spins = 0;
@@ -569,8 +593,21 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
 #endif
     const int e0 = (w * 64 + lane) * CS;
     double x[CS];
-    if (hparent != SM_NONE) {
-        global_read_at<CS>(U, hparent, Dpad, e0, x);  // A(parent): finished in an earlier round
+    if (hparent != SM_NONE && ready) {
+        // merged launch, consumer: A(parent) is produced by a chain of this same launch; wait for
+        // its readiness word, then read the row at device scope (written through by the producer)
+        // bounded (~1 s): a missing readiness word must show up as a parity failure, not a hang
+        for (int it = 0; it < (1 << 24); ++it) {
+            if (__hip_atomic_load(ready + hparent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        vm_drain();
+#pragma unroll
+        for (int q = 0; q < CS; ++q)
+            x[q] = __hip_atomic_load(U + (size_t)hparent * Dpad + e0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vm_drain();
+    } else if (hparent != SM_NONE) {
+        global_read_at<CS>(U, hparent, Dpad, e0, x);  // A(parent): finished in an earlier launch
         vm_drain();
     } else {
 #pragma unroll
@@ -614,7 +651,8 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
 template <int SPL>
 __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, int head, int len, int lane,
                                                  uint32_t hparent, const uint32_t* __restrict__ meta32,
-                                                 const WalkView& V, int Dpad, int dcall, int dglob0, int store_all) {
+                                                 const WalkView& V, int Dpad, int dcall, int dglob0, int store_all,
+                                                 uint32_t* ready, uint32_t epoch) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
     const int ngroups = (len + G - 1) / G;
     int g = hh;
@@ -675,9 +713,27 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
         double mn;
         int mi;
         wta_chunk<SPL, G>(xs, lane, lane * SPL, dcall, mn, mi);
+        if (ready) {
+            // merged launch, producer: rows that light children (the launch's consumer chains) read
+            // are written through at device scope, then each node's readiness word is published
 #pragma unroll
-        for (int k = 0; k < G; ++k)
-            if (k < n && (store_all || st[k])) store_row<SPL>(U, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
+            for (int k = 0; k < G; ++k)
+                if (k < n && (store_all || st[k])) {
+                    double* row = U + (size_t)(head + g * G + k) * Dpad + lane * SPL;
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q)
+                        __hip_atomic_store(row + q, xs[k][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            vm_drain();  // the rows are at device scope before any readiness word
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                if (k < n && st[k] && lane == 0)
+                    __hip_atomic_store(ready + head + g * G + k, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                if (k < n && (store_all || st[k])) store_row<SPL>(U, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
+        }
         if (lane < n) {
             V.idx[pix] = dglob0 + mi;
             V.minc[pix] = mn;
@@ -696,13 +752,39 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
                                                             const SmPath* __restrict__ paths1,
                                                             const double* __restrict__ slut_g,
                                                             const double* __restrict__ s2lut_g, int Dpad, int dcall,
-                                                            int dglob0, int store_all) {
+                                                            int dglob0, int store_all, uint32_t* ready0,
+                                                            uint32_t* ready1, uint32_t epoch, int nprod0, int nprod1) {
     __shared__ DownRing<SPL> ring;
-    const int view = blockIdx.y;
+    // merged launch (nprod0 + nprod1 > 0, flat grid): per view, paths [0, nprod) produce rows for
+    // the paths after them (their light children's chains), which wait per path for their
+    // parent's readiness word.  Producers of both views take the first block ids, so they are
+    // dispatched before any consumer that waits for them.
+    int view, pidx;
+    const int P = nprod0 + nprod1;
+    if (P > 0) {
+        const int b = blockIdx.x;
+        if (b < P) {
+            view = b < nprod0 ? 0 : 1;
+            pidx = view ? b - nprod0 : b;
+        } else {
+            const int c = b - P, c0 = V0.npaths - nprod0;
+            view = c < c0 ? 0 : 1;
+            pidx = view ? nprod1 + (c - c0) : nprod0 + c;
+        }
+    } else {
+        view = blockIdx.y;
+        pidx = blockIdx.x;
+    }
+    view = (int)uniform((uint32_t)view);
+    pidx = (int)uniform((uint32_t)pidx);
     const WalkView& V = view ? V1 : V0;
-    if ((int)blockIdx.x >= V.npaths) return;
+    if (pidx >= V.npaths) return;
+    const int nprod = view ? nprod1 : nprod0;
+    uint32_t* ready = nprod > 0 ? (view ? ready1 : ready0) : nullptr;
+    uint32_t* prod_ready = pidx < nprod ? ready : nullptr;
+    const uint32_t* cons_ready = pidx >= nprod ? ready : nullptr;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
-    const SmPath path = (view ? paths1 : paths0)[blockIdx.x];
+    const SmPath path = (view ? paths1 : paths0)[pidx];
     const int head = (int)uniform(path.head), len = (int)uniform(path.len);
     const uint32_t hparent = uniform(meta32[(size_t)head * 8 + 1]);
     for (int i = threadIdx.x; i < DownCfg<SPL>::NS; i += CHN_THREADS) {
@@ -717,10 +799,10 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     __syncthreads();
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (wave < Split<SPL>::NCW)
-        down_chain_wave<SPL>(ring, wave, len, lane, V.U, hparent, Dpad);
-    else
-        down_helper_wave<SPL>(ring, wave - Split<SPL>::NCW, head, len, lane, hparent, meta32, V, Dpad, dcall, dglob0,
-                              store_all);
+        down_chain_wave<SPL>(ring, wave, len, lane, V.U, hparent, Dpad, cons_ready, epoch);
+    else if (Split<SPL>::helper_of(wave) >= 0)
+        down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, hparent, meta32, V, Dpad, dcall, dglob0,
+                              store_all, prod_ready, epoch);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -746,9 +828,12 @@ static void up_chain_launch(hipStream_t st, const WalkArgs& a, int np) {
 
 template <int SPL>
 static void down_chain_launch(hipStream_t st, const WalkArgs& a, int np, int store_all) {
-    hipLaunchKernelGGL((k_down_chain<SPL>), dim3(np, 2), dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
+    const bool merged = a.nprod[0] + a.nprod[1] > 0;
+    const dim3 grid = merged ? dim3(a.npaths[0] + a.npaths[1], 1) : dim3(np, 2);
+    hipLaunchKernelGGL((k_down_chain<SPL>), grid, dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all);
+                       a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all, a.ready[0],
+                       a.ready[1], a.epoch, a.nprod[0], a.nprod[1]);
 }
 
 hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {

@@ -50,6 +50,12 @@ struct WalkArgs {
     const uint2* segtab[2];  // long buckets: {path, segment} per SM_PRE_SEG-node segment
     int nseg[2];
     int W, Dpad, dcall, dglob0;
+    // merged chain launches (a round's chains with the next round's, dataflow through readiness
+    // words): ready[v][slot] == epoch once the row of slot is final; nprod[v] = producer paths
+    // at the start of the launch's path range (0: not a merged launch)
+    uint32_t* ready[2];
+    uint32_t epoch;
+    int nprod[2];
 };
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
