@@ -492,7 +492,9 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
 // The down pass's first two rounds in one chain launch: round 0 (the root's heavy path) produces
 // rows, round 1's long paths (light children of it) start as soon as their parent's row is
 // final instead of after the whole root chain.  Needs an empty short bucket in round 0 so the
-// two long buckets are one contiguous path range.
+// two long buckets are one contiguous path range.  (The mirror image for the up pass -- the root
+// chain consuming round 1's heads as they finish -- was measured slower at C2: the root chain
+// waits for its longest light subtree near the bottom of the path either way.)
 bool can_merge_down(sm_ctx* ctx, int nviews) {
     static const bool off = getenv("SM_NO_MERGE") != nullptr;  // A/B switch
     if (off) return false;

@@ -250,6 +250,17 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
     for (int w = 0; w < n; ++w) lds_wait(&p[w], v, true);
 }
 
+// Merged launches (a round's chains with the next round's): rows crossing workgroups inside one
+// launch are written and read at device scope (coherent across the XCDs' L2s), and a per-slot
+// readiness word (== the filter call's epoch) orders them.  Waits are bounded (~1 s): a missing
+// word shows up as a parity failure, never as a hang.
+__device__ __forceinline__ void wait_ready(const uint32_t* ready, uint32_t slot, uint32_t epoch) {
+    for (int it = 0; it < (1 << 24); ++it) {
+        if (__hip_atomic_load(ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_up_chain
 //
@@ -272,7 +283,7 @@ struct UpNodeS {
 template <int SPL>
 struct UpSlot {
     static constexpr int G = UpCfg<SPL>::G;
-    double pre[G][64 * SPL];    // Pre (pre-heavy fold)
+    double pre[G][64 * SPL];    // Pre (pre-heavy fold) in; the chain's A_up rows out
     double post1[G][64 * SPL];  // first post-heavy child row (dummy if absent)
     double post2[G][64 * SPL];  // second post-heavy child row (dummy if absent)
     double post3[64 * SPL];     // a root's third post-heavy child
@@ -280,7 +291,8 @@ struct UpSlot {
     UpNodeS s[G];
     double S3;
     int k3;                     // node of the group with a third post-heavy child, or -1
-    int done[2];                // g+1: chain wave w finished group g (slot reusable when all have)
+    int done[2];                // g+1: chain wave w finished group g  (chain wave -> owner helper)
+    int freed;                  // g+1: slot of group g reusable        (owner helper -> next helper)
     unsigned long long staged;  // (flags << 32) | (g+1): group g staged (helper -> chain waves);
                                 // flags: 3 bits per node (Pre, post1, post2 rows present) + UP_F3
 };
@@ -351,9 +363,14 @@ __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0
         }
 #pragma unroll
         for (int q = 0; q < CS; ++q) x[q] = acc[q] + (double)cv[k][q];
-#ifndef SM_PROF_NOSTORE
-        global_write_at<CS>(U, (uint32_t)(top - (j0 + k)), Dpad, e0, x);
-#endif
+        // the result row goes back through LDS and the owner helper stores it: a global store per
+        // node on the chain wave makes the chain wait on store completions (vmcnt), which are slow
+        // whenever the rest of the GPU is busy
+        lds_write_at<CS>(sl.pre[k0 + k], e0, x);
+        (void)U;
+        (void)top;
+        (void)j0;
+        (void)Dpad;
     }
 }
 
@@ -417,7 +434,7 @@ __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head
 // exact and the loads stay in flight while the helper waits for its slot.
 template <int SPL>
 __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int head, int len, int lane,
-                                               const uint32_t* __restrict__ meta32, const double* __restrict__ U,
+                                               const uint32_t* __restrict__ meta32, double* __restrict__ U,
                                                const float* __restrict__ Cst, int Dpad) {
     constexpr int G = UpCfg<SPL>::G, NS = UpCfg<SPL>::NS;
     constexpr int NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
@@ -425,30 +442,42 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
     const int ngroups = (len + G - 1) / G;
     int g = hh;
     if (g >= ngroups) return;
-    MetaVec<G> mv;
-    load_meta<G>(mv, meta32, lane, top - g * G, -1, min(G, len - g * G));
-    for (;;) {
-        const int n = min(G, len - g * G);
-        // ---- this group's loads (all unconditional)
-        double pr[G][SPL], p1[G][SPL], p2[G][SPL], p3[SPL];
-        float cr[G][SPL];
+    // meta runs two groups ahead of the rows: the rows of group g + NH are issued from meta that
+    // was loaded before this group's stores, so their address wait never waits on stores
+    auto meta_of = [&](MetaVec<G>& m, int gg) {
+        const int gc = gg < ngroups ? gg : g;  // unconditional prefetch (clamped)
+        load_meta<G>(m, meta32, lane, top - gc * G, -1, min(G, len - gc * G));
+    };
+    MetaVec<G> mv, mnext;
+    meta_of(mv, g);
+    meta_of(mnext, g + NH);
+    double pr[G][SPL], p1[G][SPL], p2[G][SPL], p3[SPL];
+    float cr[G][SPL];
+    // a group's row loads (all unconditional: indices clamped, absent children read the path
+    // head's rows as L2-resident dummies)
+    auto issue = [&](int gg, const MetaVec<G>& m) {
+        const int n = min(G, len - gg * G);
         uint32_t s3 = (uint32_t)head;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const int kk = min(k, n - 1);
-            const uint32_t slot = (uint32_t)(top - (g * G + kk));
-            const uint32_t hi = mfield(mv, kk, 3);
+            const uint32_t slot = (uint32_t)(top - (gg * G + kk));
+            const uint32_t hi = mfield(m, kk, 3);
             const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
             const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
             load_row<SPL>(U, hidx > 0 ? slot : (uint32_t)head + 2u, Dpad, lane, pr[k]);  // Pre rows exist iff hidx > 0
             load_crow<SPL>(Cst, slot, Dpad, lane, cr[k]);
-            const uint32_t c1 = np >= 1 ? mfield(mv, kk, 4 + (int)min(hidx + 1u, 3u)) : (uint32_t)head;
-            const uint32_t c2 = np >= 2 ? mfield(mv, kk, 4 + (int)min(hidx + 2u, 3u)) : (uint32_t)head + 1u;
+            const uint32_t c1 = np >= 1 ? mfield(m, kk, 4 + (int)min(hidx + 1u, 3u)) : (uint32_t)head;
+            const uint32_t c2 = np >= 2 ? mfield(m, kk, 4 + (int)min(hidx + 2u, 3u)) : (uint32_t)head + 1u;
             load_row<SPL>(U, c1, Dpad, lane, p1[k]);
             load_row<SPL>(U, c2, Dpad, lane, p2[k]);
-            if (np >= 3) s3 = mfield(mv, kk, 7);
+            if (np >= 3) s3 = mfield(m, kk, 7);
         }
         load_row<SPL>(U, s3, Dpad, lane, p3);
+    };
+    issue(g, mv);
+    for (;;) {
+        const int n = min(G, len - g * G);
         // ---- weights and presence flags (meta + LDS table only): before waiting for the slot;
         // lane q < 3 holds S of the heavy child (q = 0) / post q of node k
         double Sl[G];
@@ -471,13 +500,13 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
                 }
             }
         }
-        MetaVec<G> mnext;
+        MetaVec<G> mnn;
+        meta_of(mnn, g + 2 * NH);
         const int gn = g + NH;
-        const int gl = gn < ngroups ? gn : g;  // unconditional prefetch (clamped)
-        load_meta<G>(mnext, meta32, lane, top - gl * G, -1, min(G, len - gl * G));
+        const int gl = gn < ngroups ? gn : g;
         // ---- wait for the slot, fill it, publish
         UpSlot<SPL>& sl = ring.s[g % NS];
-        if (g >= NS) lds_wait_all(sl.done, NCW, g - NS + 1);
+        if (g >= NS) lds_wait(&sl.freed, g - NS + 1, true);
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             if (k < n) {
@@ -503,9 +532,21 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
         __hip_atomic_store(&sl.staged, ((unsigned long long)flags << 32) | (unsigned)(g + 1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        // ---- the next group's loads go out now: in flight while this group is computed
+        issue(gl, mnext);
+        // ---- the chain's results: read back, store, free the slot
+        lds_wait_all(sl.done, NCW, g + 1);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {  // unconditional (clamped rows are stored twice, same value)
+            double xr[SPL];
+            lds_row_read<SPL>(sl.pre[min(k, n - 1)], lane, xr);
+            store_row<SPL>(U, (uint32_t)(top - (g * G + min(k, n - 1))), Dpad, lane, xr);
+        }
+        lds_publish(&sl.freed, g + 1);  // the rows are in flight from registers
         if (gn >= ngroups) break;
         g = gn;
         mv = mnext;
+        mnext = mnn;
     }
 }
 
@@ -596,11 +637,7 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
     if (hparent != SM_NONE && ready) {
         // merged launch, consumer: A(parent) is produced by a chain of this same launch; wait for
         // its readiness word, then read the row at device scope (written through by the producer)
-        // bounded (~1 s): a missing readiness word must show up as a parity failure, not a hang
-        for (int it = 0; it < (1 << 24); ++it) {
-            if (__hip_atomic_load(ready + hparent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
+        wait_ready(ready, hparent, epoch);
         vm_drain();
 #pragma unroll
         for (int q = 0; q < CS; ++q)
