@@ -700,6 +700,10 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         return SM_ERR_HIP;
     }
     ctx->st2 = ctx->st;
+    if (getenv("SM_TWO_STREAMS") && hipStreamCreateWithFlags(&ctx->st2, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return SM_ERR_HIP;
+    }
     if (hipHostMalloc((void**)&ctx->h_changed, (2 * SM_MST_MAX_ROUNDS + 8) * sizeof(int)) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;

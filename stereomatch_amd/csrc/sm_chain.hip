@@ -177,7 +177,7 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 if ((uint32_t)i < hidx) {
-                    const double S = sh.slut[cw_of(lo, hi, i)];
+                    const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);  // uniform
 #pragma unroll
                     for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S, lr[j][i][k], acc[k]);
                 }
@@ -845,6 +845,9 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
 // ---------------------------------------------------------------------------------------------
 static WalkView chain_view(const WalkArgs& a, int v) { return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v]}; }
 
+#ifndef UP_PRE_CH2
+#define UP_PRE_CH2 8  // nodes per wave of k_up_pre at SPL=2
+#endif
 template <int SPL, int CH>
 static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
     const int ns = a.nseg[0] > a.nseg[1] ? a.nseg[0] : a.nseg[1];
@@ -876,7 +879,7 @@ static void down_chain_launch(hipStream_t st, const WalkArgs& a, int np, int sto
 hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {
     switch (spl) {
         case 1: up_pre_launch<1, 8>(st, a); break;
-        case 2: up_pre_launch<2, 8>(st, a); break;
+        case 2: up_pre_launch<2, UP_PRE_CH2>(st, a); break;
         default: up_pre_launch<4, 4>(st, a); break;
     }
     return hipGetLastError();

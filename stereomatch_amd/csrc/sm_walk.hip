@@ -68,14 +68,20 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
     ImgRecs<SPL, CH> rec;
     load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
     // ---- off-chain work: costs and edge factors of every node of the chunk
-    double c[CH][SPL], Sv[CH][4];
+    float c[CH][SPL];  // float until the add: half the registers of the converted values
+    double Sv[CH][4];
     chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
         const uint32_t nch = hi_nch(hi);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Sv[j][i] = sh.slut[(uint32_t)i < nch ? cw_of(lo, hi, i) : (uint32_t)S_ZERO];
+        for (int i = 0; i < 4; ++i)  // uniform: SGPR pairs (v_fma_f64 takes one), not 2 VGPRs each
+#ifdef SM_WALK_SV_VGPR
+            Sv[j][i] = sh.slut[(uint32_t)i < nch ? cw_of(lo, hi, i) : (uint32_t)S_ZERO];
+#else
+            Sv[j][i] = readlane_f64(sh.slut[(uint32_t)i < nch ? cw_of(lo, hi, i) : (uint32_t)S_ZERO], 0);
+#endif
     }
     // ---- serial recurrence along the path (bottom -> top)
 #pragma unroll
@@ -110,7 +116,7 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
                 }
             }
 #pragma unroll
-            for (int k = 0; k < SPL; ++k) xc[k] = acc[k] + c[j][k];
+            for (int k = 0; k < SPL; ++k) xc[k] = acc[k] + (double)c[j][k];
             store_row<SPL>(U, (uint32_t)(top - j), Dpad, lane, xc);
         }
     }
@@ -222,8 +228,8 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const uint32_t wp = lo_wp(mfield(cur, j, 2));
-            S[j] = sh.slut[wp];
-            S2[j] = sh.s2lut[wp];
+            S[j] = readlane_f64(sh.slut[wp], 0);  // uniform: SGPR pairs
+            S2[j] = readlane_f64(sh.s2lut[wp], 0);
         }
         // the chunk's recurrence first (registers only), then its stores: no store sits between
         // two uses of loaded rows, so the loads are waited for once

@@ -205,9 +205,9 @@ __device__ __forceinline__ void load_recs(const MetaVec<CH>& mv, int n, int view
 
 // AGD costs C(v, d) of the chunk's nodes for this lane's SPL slices; invalid (x-d<0, column W-1,
 // d beyond the call's range) -> 3.0 as the reference (PatchMatchStereoGPU.cu:1501-1549)
-template <int SPL, int CH>
+template <int SPL, int CH, class T>
 __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int W, int dbase, int dend,
-                                            const ImgRecs<SPL, CH>& r, const float* __restrict__ atab, double (&c)[CH][SPL]) {
+                                            const ImgRecs<SPL, CH>& r, const float* __restrict__ atab, T (&c)[CH][SPL]) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const int pix = (int)mfield(mv, j, 0);
@@ -227,7 +227,7 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
                 ok = d < dend && x - d >= 0 && x + 1 < W;
                 v = agd_rec(r.ob[j][SPL - 1 - k], o0, rgray(r.ob[j][SPL - k]), rgray(o1), atab);
             }
-            c[j][k] = (double)(ok ? v : 3.0f);
+            c[j][k] = (T)(ok ? v : 3.0f);
         }
     }
 }
