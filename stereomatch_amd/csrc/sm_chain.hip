@@ -374,6 +374,53 @@ __device__ __forceinline__ void up_group(UpSlot<SPL>& sl, uint32_t flags, int k0
     }
 }
 
+// Software-pipelined chain (even G): a group is two halves of H = G/2 nodes held in two register
+// sets A and B.  The LDS reads of the next half are issued before the current half's recurrence,
+// so their latency hides behind it; the loop is unrolled by one group so A and B swap roles
+// without register copies, and every read is unconditional (exact lgkm counts).
+template <int SPL, int H>
+struct UpHalf {
+    static constexpr int CS = Split<SPL>::CS;
+    double pr[H][CS], p1[H][CS], p2[H][CS], S[H][3];
+    float cv[H][CS];
+};
+
+template <int SPL, int H>
+__device__ __forceinline__ void up_half_read(const UpSlot<SPL>& sl, int k0, int e0, UpHalf<SPL, H>& r) {
+    constexpr int CS = Split<SPL>::CS;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+        r.S[k][0] = sl.s[k0 + k].Sh;
+        r.S[k][1] = sl.s[k0 + k].Sp1;
+        r.S[k][2] = sl.s[k0 + k].Sp2;
+        lds_read_at<CS>(sl.pre[k0 + k], e0, r.pr[k]);
+        lds_read_at<CS>(sl.post1[k0 + k], e0, r.p1[k]);
+        lds_read_at<CS>(sl.post2[k0 + k], e0, r.p2[k]);
+#pragma unroll
+        for (int q = 0; q < CS; ++q) r.cv[k][q] = sl.c[k0 + k][e0 + q];
+    }
+}
+
+template <int SPL, int H>
+__device__ __forceinline__ void up_half_step(UpSlot<SPL>& sl, uint32_t flags, int k0, int e0, const UpHalf<SPL, H>& r,
+                                             double (&x)[Split<SPL>::CS]) {
+    constexpr int CS = Split<SPL>::CS;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+        const bool hpre = (flags >> (3 * (k0 + k))) & UP_F_PRE;
+        double acc[CS];
+#pragma unroll
+        for (int q = 0; q < CS; ++q) {
+            acc[q] = __builtin_fma(r.S[k][0], x[q], hpre ? r.pr[k][q] : 0.0);
+            acc[q] = __builtin_fma(r.S[k][1], r.p1[k][q], acc[q]);
+            acc[q] = __builtin_fma(r.S[k][2], r.p2[k][q], acc[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < CS; ++q) x[q] = acc[q] + (double)r.cv[k][q];
+        lds_write_at<CS>(sl.pre[k0 + k], e0, x);
+    }
+}
+
 template <int SPL>
 __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head, int len, int lane,
                                               double* __restrict__ U, int Dpad) {
@@ -391,7 +438,39 @@ __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head
 #pragma unroll
     for (int q = 0; q < CS; ++q) x[q] = 0.0;
     unsigned long long st = lds_state64(&ring.s[0].staged);  // poll-ahead: the next group's state
-    for (int g = 0; g < ngroups; ++g) {
+    int g0 = 0;
+#ifdef SM_NO_PIPE
+    if constexpr (false) {
+#else
+    if constexpr (G % 2 == 0) {
+#endif
+        // all full groups but the last through the pipeline; the last group (partial, or the tree
+        // root's with a third post-heavy child) takes the generic path below
+        constexpr int H = G / 2;
+        UpHalf<SPL, H> A, B;
+        while ((uint32_t)st != 1u) st = lds_state64(&ring.s[0].staged);
+        uint32_t flags = uniform((uint32_t)(st >> 32));
+        up_half_read<SPL, H>(ring.s[0], 0, e0, A);
+        for (int g = 0; g + 1 < ngroups; ++g) {
+            UpSlot<SPL>& sl = ring.s[g % NS];
+            UpSlot<SPL>& sn = ring.s[(g + 1) % NS];
+            st = lds_state64(&sn.staged);  // poll-ahead for group g+1
+            up_half_read<SPL, H>(sl, H, e0, B);
+            up_half_step<SPL, H>(sl, flags, 0, e0, A, x);
+            while ((uint32_t)st != (uint32_t)(g + 2)) {
+                PROF_SPIN(++spins);
+                st = lds_state64(&sn.staged);
+            }
+            const uint32_t fnext = uniform((uint32_t)(st >> 32));
+            up_half_read<SPL, H>(sn, 0, e0, A);
+            up_half_step<SPL, H>(sl, flags, H, e0, B, x);
+            lds_publish_ordered(&sl.done[w], g + 1);
+            flags = fnext;
+        }
+        g0 = ngroups - 1;
+        st = lds_state64(&ring.s[g0 % NS].staged);
+    }
+    for (int g = g0; g < ngroups; ++g) {
         UpSlot<SPL>& sl = ring.s[g % NS];
         const int n = min(G, len - g * G);
 #ifdef SM_CHAIN_PROF
