@@ -28,7 +28,8 @@ hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gi
 
 namespace {
 
-constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2 + SM_NBUCKETS + (SM_NBUCKETS + 1) + SM_NBUCKETS;
+constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2 + SM_NBUCKETS + (SM_NBUCKETS + 1) + SM_NBUCKETS +
+                            (SM_NBUCKETS + 1);
 
 struct DevBuf {
     void* p = nullptr;
@@ -57,13 +58,14 @@ struct sm_ctx {
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
     DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2];
+    DevBuf pieces[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
     DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
     int mst_rounds = 12;  // contracted Boruvka rounds the previous frame enqueued
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
     struct HostRounds {
         uint32_t nrounds = 0, npaths = 0, n_has_light = 0;
-        std::vector<uint32_t> begin, maxlen, seg_begin, nodes;  // per bucket
+        std::vector<uint32_t> begin, maxlen, seg_begin, nodes, piece_begin;  // per bucket
     } layout[2];
     hipEvent_t ev[8] = {};
     // tree-filter launch timing: launch k is bracketed by events fev[2k], fev[2k+1] on its stream
@@ -261,6 +263,13 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     return SM_OK;
 }
 
+// nodes per piece: SM_PIECE, or env SM_PIECE_LEN (multiple of SM_PRE_SEG, >= 64)
+int piece_len() {  // read per call: tests switch it between matches
+    const char* e = getenv("SM_PIECE_LEN");
+    const int v = e ? atoi(e) : SM_PIECE;
+    return (v >= 64 && v % SM_PRE_SEG == 0) ? v : SM_PIECE;
+}
+
 // device-side rounds record: [0, SM_NBUCKETS] bucket begin, then count, cursor, nrounds, n_has_light
 constexpr size_t RREC = RREC_FWD;
 
@@ -301,6 +310,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->paths[v], N * sizeof(SmPath)));
         CHECK(ensure(ctx, ctx->rounds[v], RREC * 4));
         CHECK(ensure(ctx, ctx->segtab[v], (N / 16 + 64) * sizeof(uint2)));  // <= N/32 segments + N/32 long paths
+        CHECK(ensure(ctx, ctx->pieces[v], (N / 16 + 64) * sizeof(uint4)));  // <= N/32 long paths + N/SM_PIECE
         CHECK(ensure(ctx, ctx->pathpos[v], N * 4));
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
         CHECK(ensure(ctx, ctx->nslot[v], N * 4));
@@ -354,16 +364,18 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.seg_begin = R + 4 * SM_NBUCKETS + 3;
         L.round_nodes = R + 5 * SM_NBUCKETS + 4;
         L.segtab = P<uint2>(ctx->segtab[v]);
+        L.piece_begin = R + 6 * SM_NBUCKETS + 4;
+        L.pieces = P<uint4>(ctx->pieces[v]);
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
-    HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains));
+    HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains, (uint32_t)piece_len()));
     // the host needs the per-round path counts to size the walker grids
     for (int v = 0; v < nviews; ++v)
         HIPC(hipMemcpyAsync(ctx->h_rounds + v * RREC, ctx->rounds[v].p, RREC * 4, hipMemcpyDeviceToHost, ctx->st));
     HIPC(hipStreamSynchronize(ctx->st));
     for (int v = 0; v < 2; ++v) {
         auto& L = ctx->layout[v];
-        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); L.nodes.assign(SM_NBUCKETS, 0); continue; }
+        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); L.nodes.assign(SM_NBUCKETS, 0); L.piece_begin.assign(SM_NBUCKETS + 1, 0); continue; }
         const uint32_t* R = ctx->h_rounds + v * RREC;
         L.nrounds = R[3 * SM_NBUCKETS + 1];
         L.n_has_light = R[3 * SM_NBUCKETS + 2];
@@ -371,6 +383,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.maxlen.assign(R + 3 * SM_NBUCKETS + 3, R + 4 * SM_NBUCKETS + 3);
         L.seg_begin.assign(R + 4 * SM_NBUCKETS + 3, R + 5 * SM_NBUCKETS + 4);
         L.nodes.assign(R + 5 * SM_NBUCKETS + 4, R + 6 * SM_NBUCKETS + 4);
+        L.piece_begin.assign(R + 6 * SM_NBUCKETS + 4, R + 7 * SM_NBUCKETS + 5);
         L.npaths = R[SM_NBUCKETS];
         if (L.nrounds == 0 || L.npaths == 0) return fail(ctx, SM_ERR_STATE, "layout produced no paths");
         if (getenv("SM_LAYOUT_DEBUG"))  // per-round path statistics (tools/gpu_layout_dbg.sh)
@@ -404,6 +417,11 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     return a;
 }
 
+bool no_pieces() { return getenv("SM_NO_PIECES") != nullptr; }
+
+// capacity of the per-view piece arrays (<= N/32 long paths + N/SM_PIECE pieces)
+size_t piece_cap(size_t N) { return N / 16 + 64; }
+
 void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int nviews) {
     a.maxlen = 0;
     for (int v = 0; v < 2; ++v) {
@@ -413,6 +431,8 @@ void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int nview
             a.npaths[v] = 0;
             a.segtab[v] = P<uint2>(ctx->segtab[v]);
             a.nseg[v] = 0;
+            a.pieces[v] = nullptr;
+            a.npieces[v] = 0;
         } else {
             const uint32_t b = 2 * r + (long_paths ? 0 : 1);
             a.paths[v] = P<SmPath>(ctx->paths[v]) + L.begin[b];
@@ -420,6 +440,12 @@ void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int nview
             a.maxlen = std::max(a.maxlen, (int)L.maxlen[b]);
             a.segtab[v] = P<uint2>(ctx->segtab[v]) + L.seg_begin[b];
             a.nseg[v] = (int)(L.seg_begin[b + 1] - L.seg_begin[b]);
+            // long buckets: pieces (sm_chain.hip "Pieces"), unless SM_NO_PIECES (A/B)
+            const bool pieces = long_paths && ctx->agg[v].p && !no_pieces();
+            a.pieces[v] = pieces ? P<uint4>(ctx->pieces[v]) + L.piece_begin[b] : nullptr;
+            a.npieces[v] = pieces ? (int)(L.piece_begin[b + 1] - L.piece_begin[b]) : 0;
+            a.agg[v] = pieces ? P<double>(ctx->agg[v]) + (size_t)L.seg_begin[b] * 2 * a.Dpad : nullptr;
+            a.pstat[v] = pieces ? P<uint32_t>(ctx->pstat[v]) + L.piece_begin[b] : nullptr;
         }
     }
 }
@@ -549,6 +575,53 @@ sm_status ensure_filter_bufs(sm_ctx* ctx, int Dpad) {
     return SM_OK;
 }
 
+// cross-workgroup synchronisation state of one filter call: readiness words (merged down launch),
+// piece aggregates and status words, and the call's epoch (no per-call reset of any word)
+sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
+    for (int v = 0; v < 2; ++v) {
+        const bool fresh = ctx->ready[v].n < N * 4;
+        CHECK(ensure(ctx, ctx->ready[v], N * 4));
+        if (fresh) HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
+        a.ready[v] = P<uint32_t>(ctx->ready[v]);
+    }
+    // piece buffers: segment aggregates and 6 status-word arrays (up: done/merged/final, down: same)
+    const size_t pcap = piece_cap(N);
+    a.pstride = (int)pcap;
+    a.piece_len = piece_len();
+    {
+        const char* e = getenv("SM_REPAIR_MAX");
+        a.repair_max = e ? std::max(1, atoi(e)) : 1 << 30;
+    }
+    a.piece_dbg = nullptr;
+    if (getenv("SM_PIECE_DEBUG")) {  // per-call repair statistics on stderr (tools)
+        CHECK(ensure(ctx, ctx->pdbg, 128));
+        HIPC(hipMemsetAsync(ctx->pdbg.p, 0, 128, ctx->st));
+        if (atoi(getenv("SM_PIECE_DEBUG")) == 2) {
+            const unsigned long long one = 1;
+            HIPC(hipMemcpyAsync(P<unsigned long long>(ctx->pdbg) + 15, &one, 8, hipMemcpyHostToDevice, ctx->st));
+            HIPC(hipStreamSynchronize(ctx->st));
+        }
+        a.piece_dbg = P<unsigned long long>(ctx->pdbg);
+    }
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->agg[v], pcap * 2 * (size_t)Dpad * 8));
+        CHECK(ensure(ctx, ctx->fix[v], N * (size_t)Dpad * 8));
+        a.fix[v] = P<double>(ctx->fix[v]);
+        const bool fresh = ctx->pstat[v].n < pcap * 6 * 4;
+        CHECK(ensure(ctx, ctx->pstat[v], pcap * 6 * 4));
+        if (fresh) HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 6 * 4, ctx->st));
+    }
+    a.epoch = ++ctx->epoch;
+    if (a.epoch == 0 || a.epoch >= 0x7FFFFFFFu) {  // wrapped (merged words hold 2*epoch+1): clear every word
+        for (int v = 0; v < 2; ++v) {
+            HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
+            HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 6 * 4, ctx->st));
+        }
+        a.epoch = ctx->epoch = 1;
+    }
+    return SM_OK;
+}
+
 // up + down passes over all rounds for nviews views; debug_store_all stores every A row
 sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_store_all) {
     const size_t N = (size_t)ctx->W * ctx->H;
@@ -558,17 +631,7 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     uint32_t nr = 0;
     for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
-    for (int v = 0; v < 2; ++v) {
-        const bool fresh = ctx->ready[v].n < N * 4;
-        CHECK(ensure(ctx, ctx->ready[v], N * 4));
-        if (fresh) HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
-        a.ready[v] = P<uint32_t>(ctx->ready[v]);
-    }
-    a.epoch = ++ctx->epoch;
-    if (a.epoch == 0) {  // wrapped: clear every word so no stale value equals a new epoch
-        for (int v = 0; v < 2; ++v) HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
-        a.epoch = ctx->epoch = 1;
-    }
+    CHECK(setup_sync(ctx, a, N, Dpad));
     ctx->nfev = ctx->nsev = 0;
     ctx->fam.clear();
     ctx->fam_vox.clear();
@@ -583,6 +646,13 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
         }
     }
     CHECK(join(ctx, ctx->st, ctx->st2));  // everything after the filter runs on st
+    if (a.piece_dbg) {
+        unsigned long long h[16];
+        HIPC(hipMemcpyAsync(h, a.piece_dbg, 128, hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipStreamSynchronize(ctx->st));
+        fprintf(stderr, "pieces: fast %llu slow %llu repair nodes sum %llu max %llu | merge <8 %llu <16 %llu <32 %llu <64 %llu <128 %llu >=128 %llu never %llu\n",
+                h[0], h[1], h[2], h[3], h[8], h[9], h[10], h[11], h[12], h[13], h[14]);
+    }
     (void)N;
     return SM_OK;
 }
@@ -751,7 +821,8 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cn0[v], &ctx->cn1[v],
                          &ctx->cw0[v], &ctx->cw1[v], &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
                          &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
-                         &ctx->nslot[v], &ctx->slotpix[v]};
+                         &ctx->nslot[v], &ctx->slotpix[v], &ctx->pieces[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
+        if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
     if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamDestroy(ctx->st2);
@@ -897,6 +968,7 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
     {
         CHECK(ensure_filter_bufs(ctx, Dpad));
         WalkArgs a = walk_args(ctx, Dpad, D, d0);
+        CHECK(setup_sync(ctx, a, N, Dpad));
         const uint32_t nr = std::max(ctx->layout[0].nrounds, ctx->layout[1].nrounds);
         ctx->nfev = ctx->nsev = 0;
         ctx->fam.clear();

@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "sm_common.h"
 #include "sm_launch.h"
 #include "sm_layout_gpu.h"
@@ -129,63 +131,144 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     const SmPath* __restrict__ paths0, const SmPath* __restrict__ paths1, const uint2* __restrict__ seg0,
     const uint2* __restrict__ seg1, int nseg0, int nseg1, float* __restrict__ Cst0, float* __restrict__ Cst1,
     const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec, const float* __restrict__ atab_g,
-    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g, int W, int Dpad, int dcall, int dglob0) {
+    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g, int W, int Dpad, int dcall, int dglob0,
+    double* __restrict__ agg0, double* __restrict__ agg1, int piece_len) {
+    constexpr int NW = SM_PRE_SEG / CH;
     const int view = blockIdx.y;
     if ((int)blockIdx.x >= (view ? nseg1 : nseg0)) return;  // uniform over the block
     __shared__ WalkShared sh;
+    __shared__ double aggsh[NW][2][64 * SPL];
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
+    const int wv = (int)uniform(threadIdx.x >> 6);
     const uint2 sg = (view ? seg1 : seg0)[blockIdx.x];
     const SmPath path = (view ? paths1 : paths0)[uniform(sg.x)];
     const int head = (int)uniform(path.head), len = (int)uniform(path.len);
-    const int first = (int)uniform(sg.y * SM_PRE_SEG + (threadIdx.x >> 6) * CH);
-    if (first >= len) return;
-    const int n = min(CH, len - first);
+    double* __restrict__ agg = view ? agg1 : agg0;
+    // segments of a path cut into pieces also produce the segment's affine aggregate (the piece
+    // chains' guessed inputs, "Pieces" below)
+    const bool agg_mode = agg != nullptr && len >= 2 * piece_len;
+    const int first = (int)uniform(sg.y * SM_PRE_SEG + wv * CH);
+    if (first >= len && !agg_mode) return;
+    const int n = max(0, min(CH, len - first));
     const int dbase = dglob0 + lane * SPL;
     const int dend = dglob0 + dcall;
     const uint2* __restrict__ own = view ? Rrec : Lrec;
     const uint2* __restrict__ oth = view ? Lrec : Rrec;
     double* __restrict__ U = V.U;
     float* __restrict__ Cst = view ? Cst1 : Cst0;
+    double pre[CH][SPL], c[CH][SPL];
     MetaVec<CH> mv;
-    load_meta<CH>(mv, meta32, lane, head + first, 1, n);
-    // pre-heavy light child rows (positions 0 .. hidx-1; up to 3 at a tree root)
-    // unconditional loads (absent rows read row 0, an L2-resident dummy): no wait splits them
-    double lr[CH][3][SPL];
+    if (n > 0) {
+        load_meta<CH>(mv, meta32, lane, head + first, 1, n);
+        // pre-heavy light child rows (positions 0 .. hidx-1; up to 3 at a tree root)
+        // unconditional loads (absent rows read row 0, an L2-resident dummy): no wait splits them
+        double lr[CH][3][SPL];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        const int jj = j < n ? j : n - 1;
-        const uint32_t hidx = hi_hidx(mfield(mv, jj, 3));
+        for (int j = 0; j < CH; ++j) {
+            const int jj = j < n ? j : n - 1;
+            const uint32_t hidx = hi_hidx(mfield(mv, jj, 3));
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-            load_row<SPL>(U, (uint32_t)i < hidx ? mfield(mv, jj, 4 + i) : 0u, Dpad, lane, lr[j][i]);
+            for (int i = 0; i < 3; ++i)
+                load_row<SPL>(U, (uint32_t)i < hidx ? mfield(mv, jj, 4 + i) : 0u, Dpad, lane, lr[j][i]);
+        }
+        ImgRecs<SPL, CH> rec;
+        load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+        chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (j < n) {
+                const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
+                const uint32_t hidx = hi_hidx(hi);
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) pre[j][k] = 0.0;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if ((uint32_t)i < hidx) {
+                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);  // uniform
+#pragma unroll
+                        for (int k = 0; k < SPL; ++k) pre[j][k] = __builtin_fma(S, lr[j][i][k], pre[j][k]);
+                    }
+                }
+                const uint32_t slot = (uint32_t)(head + first + j);
+                if (hidx > 0) store_row<SPL>(U, slot, Dpad, lane, pre[j]);  // Pre = 0 rows are never read
+                store_crow<SPL>(Cst, slot, Dpad, lane, c[j]);
+            }
+        }
     }
-    ImgRecs<SPL, CH> rec;
-    load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
-    double c[CH][SPL];
-    chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+    if (!agg_mode) return;
+    // ---- affine aggregate of this wave's nodes (bottom up): x_first = P * x_below + B with
+    // b = Pre + sum(S_post * A_post) + C and x = S_heavy * x_below + b.  Approximate (any rounding
+    // only moves the guess; the chains' results are repaired exactly), so no order constraint.
+    double P[SPL], B[SPL];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        if (j < n) {
-            const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
-            const uint32_t hidx = hi_hidx(hi);
-            double acc[SPL];
+    for (int k = 0; k < SPL; ++k) {
+        P[k] = 1.0;
+        B[k] = 0.0;
+    }
+    if (n > 0) {
+        double pr[CH][3][SPL];
 #pragma unroll
-            for (int k = 0; k < SPL; ++k) acc[k] = 0.0;
+        for (int j = 0; j < CH; ++j) {
+            const int jj = j < n ? j : n - 1;
+            const uint32_t hi = mfield(mv, jj, 3);
+            const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+            const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                if ((uint32_t)i < hidx) {
-                    const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);  // uniform
+            for (int i = 0; i < 3; ++i)
+                load_row<SPL>(U, (uint32_t)i < np ? mfield(mv, jj, 4 + (int)min(hidx + 1u + (uint32_t)i, 3u)) : 0u, Dpad, lane,
+                              pr[j][i]);
+        }
 #pragma unroll
-                    for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(S, lr[j][i][k], acc[k]);
+        for (int j = CH - 1; j >= 0; --j) {
+            if (j < n) {
+                const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
+                const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+                const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
+                const double Sh = nch > 0 ? readlane_f64(sh.slut[cw_of(lo, hi, (int)hidx)], 0) : 0.0;
+                double b[SPL];
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) b[k] = pre[j][k];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if ((uint32_t)i < np) {
+                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, (int)min(hidx + 1u + (uint32_t)i, 3u))], 0);
+#pragma unroll
+                        for (int k = 0; k < SPL; ++k) b[k] = __builtin_fma(S, pr[j][i][k], b[k]);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) {
+                    B[k] = __builtin_fma(Sh, B[k], b[k] + c[j][k]);
+                    P[k] = Sh * P[k];
                 }
             }
-            const uint32_t slot = (uint32_t)(head + first + j);
-            if (hidx > 0) store_row<SPL>(U, slot, Dpad, lane, acc);  // Pre = 0 rows are never read
-            store_crow<SPL>(Cst, slot, Dpad, lane, c[j]);
         }
+    }
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        aggsh[wv][0][lane * SPL + k] = P[k];
+        aggsh[wv][1][lane * SPL + k] = B[k];
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    // segment = wave 0 o wave 1 o ... (the last wave holds the bottom-most nodes)
+    for (int w = NW - 2; w >= 0; --w) {
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) {
+            const double Pw = aggsh[w][0][lane * SPL + k], Bw = aggsh[w][1][lane * SPL + k];
+            const double Pn = aggsh[w + 1][0][lane * SPL + k], Bn = aggsh[w + 1][1][lane * SPL + k];
+            aggsh[w][0][lane * SPL + k] = Pw * Pn;
+            aggsh[w][1][lane * SPL + k] = __builtin_fma(Pw, Bn, Bw);
+        }
+    }
+    double* out = agg + (size_t)blockIdx.x * 2 * Dpad;  // segment index within the bucket
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        out[lane * SPL + k] = aggsh[0][0][lane * SPL + k];
+        out[Dpad + lane * SPL + k] = aggsh[0][1][lane * SPL + k];
     }
 }
 
@@ -423,7 +506,7 @@ __device__ __forceinline__ void up_half_step(UpSlot<SPL>& sl, uint32_t flags, in
 
 template <int SPL>
 __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head, int len, int lane,
-                                              double* __restrict__ U, int Dpad) {
+                                              double* __restrict__ U, int Dpad, const double* x0) {
     constexpr int G = UpCfg<SPL>::G, NS = UpCfg<SPL>::NS, CS = Split<SPL>::CS;
     __builtin_amdgcn_s_setprio(3);
     unsigned spins = 0;
@@ -436,7 +519,7 @@ __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head
     const int ngroups = (len + G - 1) / G;
     double x[CS];
 #pragma unroll
-    for (int q = 0; q < CS; ++q) x[q] = 0.0;
+    for (int q = 0; q < CS; ++q) x[q] = x0 ? x0[e0 + q] : 0.0;  // a piece with a lower piece: its guessed input
     unsigned long long st = lds_state64(&ring.s[0].staged);  // poll-ahead: the next group's state
     int g0 = 0;
 #ifdef SM_NO_PIPE
@@ -514,7 +597,8 @@ __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head
 template <int SPL>
 __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int head, int len, int lane,
                                                const uint32_t* __restrict__ meta32, double* __restrict__ U,
-                                               const float* __restrict__ Cst, int Dpad) {
+                                               const float* __restrict__ Cst, int Dpad, bool lower,
+                                               uint32_t* done_word, uint32_t epoch) {
     constexpr int G = UpCfg<SPL>::G, NS = UpCfg<SPL>::NS;
     constexpr int NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
     const int top = head + len - 1;
@@ -569,7 +653,7 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
             const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
             const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
             const uint32_t i = hidx + (uint32_t)min(lane, 2);
-            const bool live = lane == 0 ? (nch > 0 && g * G + k > 0) : (uint32_t)lane <= np;
+            const bool live = lane == 0 ? (nch > 0 && (g * G + k > 0 || lower)) : (uint32_t)lane <= np;
             Sl[k] = ring.slut[live && lane < 3 ? cw_of(lo, hi, (int)min(i, 3u)) : (uint32_t)S_ZERO];
             if (k < n) {
                 flags |= ((hidx > 0 ? UP_F_PRE : 0u) | (np >= 1 ? UP_F_P1 : 0u) | (np >= 2 ? UP_F_P2 : 0u)) << (3 * k);
@@ -621,6 +705,17 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
             lds_row_read<SPL>(sl.pre[min(k, n - 1)], lane, xr);
             store_row<SPL>(U, (uint32_t)(top - (g * G + min(k, n - 1))), Dpad, lane, xr);
         }
+        if (done_word && g == ngroups - 1) {
+            // the piece's top row is the next piece's input: written through at device scope, then
+            // its done word
+            double xr[SPL];
+            lds_row_read<SPL>(sl.pre[n - 1], lane, xr);
+            double* row = U + (size_t)head * Dpad + lane * SPL;
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            vm_drain();
+            if (lane == 0) __hip_atomic_store(done_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         lds_publish(&sl.freed, g + 1);  // the rows are in flight from registers
         if (gn >= ngroups) break;
         g = gn;
@@ -629,30 +724,332 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Pieces.  A long path of L >= 2*SM_PIECE nodes is cut into M = L / SM_PIECE pieces (piece 0 at
+// the head; the bottom piece takes the remainder), one workgroup each, so the serial critical
+// path of a round is ~SM_PIECE nodes instead of L.  A piece other than the bottom one does not
+// know its input (the top row of the piece below) when it starts, so:
+//   1. guess: k_up_pre left per-segment affine aggregates (x_top = P * x_below + B, approximate)
+//      for the path; the piece folds those of every segment below it into a guessed input;
+//   2. speculate: the chain runs the piece from the guess with the exact per-node arithmetic,
+//      and the piece's top row goes out at device scope with a done word;
+//   3. repair: once the piece below is done, one wave re-runs the piece's first nodes from the
+//      true input with the same operations and compares bitwise with the stored rows.  Two
+//      trajectories of the same deterministic recurrence that agree at one node agree from there
+//      on, so the first node whose recomputed row equals the stored row ends the repair (the
+//      guess is within a few ulp, so this takes a handful of nodes);
+//   4. decoupled look-back: the repair is exact iff the input was, i.e. iff every piece below
+//      merged.  Each piece publishes merged / not merged, then reads the words of the pieces
+//      below: all merged -> commit the buffered corrections.  Otherwise (never seen; correctness
+//      only) it waits for the piece below to be final and re-walks the whole piece from the now
+//      exact input, writing through, and publishes final.
+// A piece waits only on pieces of lower block index (listed bottom first), so the lowest
+// unfinished piece always progresses.  All waits are bounded (~1 s): a bug shows up as a parity
+// failure, not a hang.  Status words hold the filter call's epoch, so nothing is reset per call.
+// ---------------------------------------------------------------------------------------------
+
+struct PieceView {
+    const uint4* pieces;  // {path, j, M, first segment of the path} per piece, bottom piece first
+    int npieces;
+    const double* agg;    // per bucket segment: [P row | B row]
+    double* fix;          // buffered repair rows (by slot, like U)
+    uint32_t* stat;       // done [i], merged [i + stride], final [i + 2 * stride]
+    int stride;
+    int plen;             // nodes per piece
+    int rmax;             // nodes a fast repair may take (tests: force the slow path)
+    unsigned long long* dbg;  // SM_PIECE_DEBUG: [fast, slow, sum of repair nodes, max, guess cycles, finish cycles]
+};
+
+__device__ __forceinline__ uint32_t wait_word(const uint32_t* p, uint32_t lo, uint32_t hi) {
+    uint32_t v = 0;
+    for (int it = 0; it < (1 << 24); ++it) {
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= lo && v <= hi) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return v;
+}
+__device__ __forceinline__ void publish_word(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int SPL>
+__device__ __forceinline__ void agent_row_read(const double* U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
+    const double* p = U + (size_t)slot * Dpad + lane * SPL;
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) r[q] = __hip_atomic_load(p + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int SPL>
+__device__ __forceinline__ void agent_row_write(double* U, uint32_t slot, int Dpad, int lane, const double (&r)[SPL]) {
+    double* p = U + (size_t)slot * Dpad + lane * SPL;
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) __hip_atomic_store(p + q, r[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// guessed input of a piece: fold of the ns segment aggregates below it (agg = the first of them,
+// the top-most), split over the 16 waves and combined in LDS (scratch: 16 x 2 rows).  Ends with a
+// barrier; the result row is in guess[].
+template <int SPL>
+__device__ void up_guess(double* scratch, double* guess, const double* __restrict__ agg, int ns, int Dpad, int wave,
+                         int lane) {
+    const int per = (ns + CHN_WAVES - 1) / CHN_WAVES;
+    const int s0 = min(ns, wave * per), s1 = min(ns, s0 + per);
+    double P[SPL], B[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        P[k] = 1.0;
+        B[k] = 0.0;
+    }
+    for (int s = s1 - 1; s >= s0; s -= 4) {  // bottom up, 4 segments' loads at a time
+        double pr[4][SPL], br[4][SPL];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ss = max(s - q, s0);
+            load_row<SPL>(agg + (size_t)ss * 2 * Dpad, 0, Dpad, lane, pr[q]);
+            load_row<SPL>(agg + (size_t)ss * 2 * Dpad + Dpad, 0, Dpad, lane, br[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (s - q >= s0) {
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) {
+                    B[k] = __builtin_fma(pr[q][k], B[k], br[q][k]);
+                    P[k] = pr[q][k] * P[k];
+                }
+            }
+        }
+    }
+    double* my = scratch + (size_t)wave * 2 * 64 * SPL;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        my[lane * SPL + k] = P[k];
+        my[64 * SPL + lane * SPL + k] = B[k];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        double x[SPL];
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) x[k] = 0.0;
+        for (int w = CHN_WAVES - 1; w >= 0; --w) {
+            const double* t = scratch + (size_t)w * 2 * 64 * SPL;
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) x[k] = __builtin_fma(t[lane * SPL + k], x[k], t[64 * SPL + lane * SPL + k]);
+        }
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) guess[lane * SPL + k] = x[k];
+    }
+    __syncthreads();
+}
+
+// Exact re-walk of a piece's chain nodes 0 .. nmax-1 (slot top - n, bottom first) from the input
+// row x (lane * SPL layout), with the reference's operations in the chain engine's order:
+// the light children before the heavy one folded from +0 (k_up_pre's Pre), acc = fma(S_h, x, .),
+// the light children after it, x = acc + C.  Compares every node with the stored row; returns the
+// first node where all lanes agree (the nodes before it were corrected), or -1.  Corrections go
+// to the same slot of fix[] or, with fix == nullptr, straight to U at device scope.  Batches of
+// CHR nodes: the next batch's metadata is in flight during a batch, the first light child row of
+// every node is loaded with the batch, further light children (rare) on demand.
+#ifndef UP_WALK_CH
+#define UP_WALK_CH(SPL) ((SPL) == 4 ? 4 : 8)  // nodes per repair batch (registers)
+#endif
+template <int SPL, int CHR>
+__device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32, double* __restrict__ U,
+                                          const float* __restrict__ Cst, const double* slut, int top, int nmax, int Dpad,
+                                          int lane, double* xio, double* __restrict__ fix, bool write) {
+    double x[SPL];
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) x[q] = xio[q];
+    MetaVec<CHR> mv;
+    load_meta<CHR>(mv, meta32, lane, top, -1, min(CHR, nmax));
+    for (int n0 = 0; n0 < nmax; n0 += CHR) {
+        const int nb = min(CHR, nmax - n0);
+        MetaVec<CHR> mn;
+        const int n1 = n0 + CHR < nmax ? n0 + CHR : n0;
+        load_meta<CHR>(mn, meta32, lane, top - n1, -1, min(CHR, nmax - n1));
+        double spec[CHR][SPL], r0[CHR][SPL];
+        float cr[CHR][SPL];
+#pragma unroll
+        for (int k = 0; k < CHR; ++k) {
+            const int kk = min(k, nb - 1);
+            const uint32_t slot = (uint32_t)(top - (n0 + kk));
+            const uint32_t hi = mfield(mv, kk, 3);
+            const int nch = (int)hi_nch(hi), hidx = (int)hi_hidx(hi);
+            load_row<SPL>(U, nch >= 2 ? mfield(mv, kk, hidx > 0 ? 4 : 5) : slot, Dpad, lane, r0[k]);  // first light child
+            load_crow<SPL>(Cst, slot, Dpad, lane, cr[k]);
+            agent_row_read<SPL>(U, slot, Dpad, lane, spec[k]);  // own piece's rows (this launch)
+        }
+#pragma unroll
+        for (int k = 0; k < CHR; ++k) {
+            if (k >= nb) break;
+            const uint32_t lo = mfield(mv, k, 2), hi = mfield(mv, k, 3);
+            const int nch = (int)hi_nch(hi), hidx = (int)hi_hidx(hi);
+            double acc[SPL];
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) acc[q] = 0.0;
+            bool first = true;
+#pragma unroll
+            for (int pos = 0; pos < 4; ++pos) {
+                if (pos >= nch) break;
+                const double S = slut[cw_of(lo, hi, pos)];
+                if (pos == hidx) {
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) acc[q] = __builtin_fma(S, x[q], acc[q]);
+                } else {
+                    double r[SPL];
+                    if (first) {
+#pragma unroll
+                        for (int q = 0; q < SPL; ++q) r[q] = r0[k][q];
+                        first = false;
+                    } else {
+                        load_row<SPL>(U, mfield(mv, k, 4 + pos), Dpad, lane, r);
+                    }
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) acc[q] = __builtin_fma(S, r[q], acc[q]);
+                }
+            }
+            bool eq = true;
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) {
+                x[q] = acc[q] + (double)cr[k][q];
+                eq = eq && __double_as_longlong(x[q]) == __double_as_longlong(spec[k][q]);
+            }
+            if (__all(eq)) return n0 + k;
+            if (!write) continue;
+            const uint32_t slot = (uint32_t)(top - (n0 + k));
+            if (fix)
+                store_row<SPL>(fix, slot, Dpad, lane, x);
+            else
+                agent_row_write<SPL>(U, slot, Dpad, lane, x);
+        }
+        mv = mn;
+    }
+    return -1;
+}
+
+// Repair + look-back of piece e (one wave, after its chain).  j of M, bottom piece first: the
+// pieces below are entries e - (M-1-j) .. e - 1, the bottom one exact by construction.  A piece
+// "merged" iff its repair met the stored trajectory below its top node, i.e. its top row (the
+// next piece's input) never changes; every input of a piece is then exact iff all pieces below
+// merged.
+template <int SPL>
+__device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restrict__ meta32, double* __restrict__ U,
+                          double* __restrict__ fix, const float* __restrict__ Cst, int Dpad, int lane, int head, int len,
+                          int j, int M, int e, const PieceView& Q, uint32_t epoch) {
+    uint32_t* done = Q.stat;
+    uint32_t* merged = Q.stat + Q.stride;
+    uint32_t* fin = Q.stat + 2 * Q.stride;
+    if (j + 1 == M) {  // bottom piece
+        if (lane == 0) publish_word(fin + e, epoch);
+        return;
+    }
+    // the helpers are done: this piece's rows are stored
+    while (__hip_atomic_load(hdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < Split<SPL>::NH) __builtin_amdgcn_s_sleep(1);
+    const int top = head + len - 1;
+    const uint32_t below = (uint32_t)(head + len);  // top node of the piece below
+    double x[SPL];
+    wait_word(done + e - 1, epoch, epoch);
+    vm_drain();
+    agent_row_read<SPL>(U, below, Dpad, lane, x);
+    vm_drain();
+    if (Q.dbg && Q.dbg[15] == 1) {  // probe (SM_PIECE_DEBUG=2): merge distance histogram, no writes
+        const int mp = up_exact_walk<SPL, UP_WALK_CH(SPL)>(meta32, U, Cst, ring.slut, top, len, Dpad, lane, x, nullptr, false);
+        int b = 8;  // 8: < 8 nodes, 9: < 16, ... 13: >= 128 (merged), 14: never merged
+        while (b < 13 && mp >= (8 << (b - 8))) ++b;
+        if (lane == 0) atomicAdd(Q.dbg + (mp < 0 ? 14 : b), 1ull);
+    }
+    const int m = up_exact_walk<SPL, UP_WALK_CH(SPL)>(meta32, U, Cst, ring.slut, top, min(Q.rmax, len), Dpad, lane, x, fix, true);
+    if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
+    bool all = m >= 0;
+    for (int q = e - 1; all && q > e - (M - 1 - j); --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u) == 2u * epoch;
+    if (Q.dbg && lane == 0) {
+        atomicAdd(Q.dbg + (all ? 0 : 1), 1ull);
+        if (m >= 0) {
+            atomicAdd(Q.dbg + 2, (unsigned long long)m);
+            atomicMax(Q.dbg + 3, (unsigned long long)m);
+        }
+    }
+    if (all) {  // commit the corrections
+        for (int k = 0; k < m; ++k) {
+            double r[SPL];
+            load_row<SPL>(fix, (uint32_t)(top - k), Dpad, lane, r);
+            store_row<SPL>(U, (uint32_t)(top - k), Dpad, lane, r);
+        }
+        if (lane == 0) publish_word(fin + e, epoch);
+        return;
+    }
+    // slow path: the piece below is final (exact); repair again from its final top row, writing
+    // through (the stored rows are still the chain's trajectory: nothing was committed)
+    wait_word(fin + e - 1, epoch, epoch);
+    vm_drain();
+    agent_row_read<SPL>(U, below, Dpad, lane, x);
+    vm_drain();
+    up_exact_walk<SPL, UP_WALK_CH(SPL)>(meta32, U, Cst, ring.slut, top, len, Dpad, lane, x, nullptr, true);
+    vm_drain();
+    if (lane == 0) publish_word(fin + e, epoch);
+}
+
 template <int SPL>
 __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                           const uint32_t* __restrict__ meta1,
                                                           const SmPath* __restrict__ paths0,
                                                           const SmPath* __restrict__ paths1,
                                                           const float* __restrict__ Cst0, const float* __restrict__ Cst1,
-                                                          const double* __restrict__ slut_g, int Dpad) {
+                                                          const double* __restrict__ slut_g, int Dpad, PieceView Q0,
+                                                          PieceView Q1, uint32_t epoch) {
     __shared__ UpRing<SPL> ring;
+    __shared__ double guess[64 * SPL];
+    __shared__ int hdone;
     const int view = blockIdx.y;
-    const WalkView& V = view ? V1 : V0;
-    if ((int)blockIdx.x >= V.npaths) return;  // uniform over the block
-    const SmPath path = (view ? paths1 : paths0)[blockIdx.x];
-    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
+    const WalkView V{view ? V1.npaths : V0.npaths, view ? V1.U : V0.U, nullptr, nullptr, nullptr};
+    // field-wise select: a reference to one of two by-value kernel arguments would copy both to
+    // scratch
+    PieceView Q;
+    Q.pieces = view ? Q1.pieces : Q0.pieces;
+    Q.npieces = view ? Q1.npieces : Q0.npieces;
+    Q.agg = view ? Q1.agg : Q0.agg;
+    Q.fix = view ? Q1.fix : Q0.fix;
+    Q.stat = view ? Q1.stat : Q0.stat;
+    Q.stride = Q0.stride;
+    Q.plen = Q0.plen;
+    Q.rmax = Q0.rmax;
+    Q.dbg = Q0.dbg;
+    const int e = blockIdx.x;
+    uint4 pc = make_uint4((uint32_t)e, 0u, 1u, 0u);  // without pieces: block = path, one piece
+    if (Q.pieces) {
+        if (e >= Q.npieces) return;  // uniform over the block
+        pc = Q.pieces[e];
+    } else if (e >= V.npaths) {
+        return;
+    }
+    const SmPath path = (view ? paths1 : paths0)[uniform(pc.x)];
+    const int j = (int)uniform(pc.y), M = (int)uniform(pc.z);
+    const int plen = (int)uniform(path.len);
+    const int o0 = j * Q.plen, o1 = j + 1 == M ? plen : (j + 1) * Q.plen;
+    const int head = (int)uniform(path.head) + o0, len = o1 - o0;
+    const bool lower = j + 1 < M;
+    const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (lower) {  // guessed input: the aggregates of the segments below the piece
+        const int sb = o1 / SM_PRE_SEG, ns = (plen + SM_PRE_SEG - 1) / SM_PRE_SEG - sb;
+        up_guess<SPL>(reinterpret_cast<double*>(ring.s), guess, Q.agg + (size_t)(pc.w + sb) * 2 * Dpad, ns, Dpad, wave, lane);
+    }
     // zero the ring: rows a helper does not stage are then always finite (see up_group)
     for (int i = threadIdx.x; i < (int)(sizeof(ring.s) / 4); i += CHN_THREADS) reinterpret_cast<uint32_t*>(ring.s)[i] = 0u;
     for (int i = threadIdx.x; i < SM_NUM_W; i += CHN_THREADS) ring.slut[i] = slut_g[i];
-    if (threadIdx.x == 0) ring.slut[SM_NUM_W] = 0.0;
+    if (threadIdx.x == 0) {
+        ring.slut[SM_NUM_W] = 0.0;
+        hdone = 0;
+    }
     __syncthreads();
-    const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wave < Split<SPL>::NCW)
-        up_chain_wave<SPL>(ring, wave, head, len, lane, V.U, Dpad);
-    else if (Split<SPL>::helper_of(wave) >= 0)
-        up_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, view ? meta1 : meta0, V.U,
-                            view ? Cst1 : Cst0, Dpad);
+    const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
+    if (wave < Split<SPL>::NCW) {
+        up_chain_wave<SPL>(ring, wave, head, len, lane, V.U, Dpad, lower ? guess : nullptr);
+        if (wave == 0 && M > 1)
+            up_finish<SPL>(ring, &hdone, meta32, V.U, Q.fix, view ? Cst1 : Cst0, Dpad, lane, head, len, j, M, e, Q, epoch);
+    } else if (Split<SPL>::helper_of(wave) >= 0) {
+        up_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V.U, view ? Cst1 : Cst0, Dpad, lower,
+                            j > 0 ? Q.stat + e : nullptr, epoch);
+        vm_drain();  // this helper's stores are complete before the repair reads or overwrites them
+        if (lane == 0) atomicAdd(&hdone, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -941,14 +1338,19 @@ static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
                        chain_view(a, 1), reinterpret_cast<const uint32_t*>(a.meta[0]),
                        reinterpret_cast<const uint32_t*>(a.meta[1]), a.paths[0], a.paths[1], a.segtab[0], a.segtab[1],
                        a.nseg[0], a.nseg[1], a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad,
-                       a.dcall, a.dglob0);
+                       a.dcall, a.dglob0, a.pieces[0] ? a.agg[0] : nullptr, a.pieces[1] ? a.agg[1] : nullptr, a.piece_len);
+}
+
+static PieceView piece_view(const WalkArgs& a, int v) {
+    return PieceView{a.pieces[v], a.npieces[v], a.agg[v], a.fix[v], a.pstat[v], a.pstride, a.piece_len, a.repair_max, a.piece_dbg};
 }
 
 template <int SPL>
 static void up_chain_launch(hipStream_t st, const WalkArgs& a, int np) {
     hipLaunchKernelGGL((k_up_chain<SPL>), dim3(np, 2), dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.Cst[0], a.Cst[1], a.slut, a.Dpad);
+                       a.paths[0], a.paths[1], a.Cst[0], a.Cst[1], a.slut, a.Dpad, piece_view(a, 0), piece_view(a, 1),
+                       a.epoch);
 }
 
 template <int SPL>
@@ -971,7 +1373,8 @@ hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {
 }
 
 hipError_t launch_up_chain(hipStream_t st, const WalkArgs& a, int spl) {
-    const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
+    int np = 0;
+    for (int v = 0; v < 2; ++v) np = std::max(np, a.pieces[v] ? a.npieces[v] : a.npaths[v]);
     if (np == 0) return hipSuccess;
     switch (spl) {
         case 1: up_chain_launch<1>(st, a, np); break;

@@ -56,6 +56,17 @@ struct WalkArgs {
     uint32_t* ready[2];
     uint32_t epoch;
     int nprod[2];
+    // long-path pieces of the current long bucket (sm_chain.hip "Pieces"); pieces[v] == nullptr:
+    // one workgroup per path, no pieces
+    const uint4* pieces[2];
+    int npieces[2];
+    double* fix[2];       // buffered repair rows, like U (by slot)
+    double* agg[2];       // per bucket segment: [P row | B row] (2 * Dpad doubles), affine aggregates
+    uint32_t* pstat[2];   // status words of the bucket's first piece: done / merged / final at
+    int pstride;          // offsets 0, pstride, 2 * pstride
+    int piece_len;
+    int repair_max;       // fast-repair node cap (env SM_REPAIR_MAX; tests force the slow path)
+    unsigned long long* piece_dbg;  // SM_PIECE_DEBUG counters (nullptr otherwise)
 };
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,

@@ -9,6 +9,13 @@
 #define SM_NBUCKETS (2 * SM_MAX_ROUNDS)  // per round: [long paths | short paths]
 #define SM_LONG_PATH 32   // paths of >= this many nodes go to the long-path chain engine (sm_chain.hip)
 #define SM_PRE_SEG 32     // nodes per k_up_pre block (segment table granularity)
+// A long path of >= 2*P nodes is cut into len/P pieces of P nodes (the bottom piece takes the
+// remainder); the pieces' chains run concurrently from guessed inputs and are then repaired
+// exactly (sm_chain.hip, "Pieces").  P = SM_PIECE by default (env SM_PIECE_LEN: a multiple of
+// SM_PRE_SEG, >= 64; tests use short pieces to exercise the repair on small images).
+#ifndef SM_PIECE
+#define SM_PIECE 512
+#endif
 
 struct LayoutView {
     // inputs
@@ -57,6 +64,9 @@ struct LayoutView {
     uint32_t* round_nodes;   // SM_NBUCKETS: nodes per bucket
     uint32_t* seg_begin;     // SM_NBUCKETS + 1: first segment of each bucket in segtab
     uint2* segtab;           // {path index within its bucket, segment within the path}
+    uint32_t* piece_begin;   // SM_NBUCKETS + 1: first piece of each bucket in pieces
+    uint4* pieces;           // {path index within its bucket, j, M, first segment of the path
+                             //  within the bucket}; piece j of M (0 = top), per path bottom first
     uint32_t* nrounds;
     uint32_t* n_has_light;   // nodes with at least one light child (roofline accounting)
 };
@@ -65,4 +75,5 @@ struct LayoutPair {
     LayoutView v[2];
 };
 
-hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains);
+hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains,
+                         uint32_t piece_len);

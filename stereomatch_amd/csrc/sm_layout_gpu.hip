@@ -608,39 +608,58 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
 }
 
 // segment table of the long-path buckets: segment i of bucket b -> {path within b, SM_PRE_SEG-node
-// segment of that path}, so k_up_pre launches exactly one block per segment.  One block per view.
-__global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP) {
+// segment of that path}, so k_up_pre launches exactly one block per segment; and the piece table:
+// a path of len >= 2*plen nodes has M = len / plen pieces, listed bottom piece first (the
+// chain launches wait only on lower entries), every other long path is one piece.  One block per
+// view.
+__global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t plen) {
     const LayoutView& V = LP.v[blockIdx.x];
-    __shared__ uint32_t sc[1024];
-    uint32_t running = 0;
+    __shared__ uint32_t sc[1024], sp[1024];
+    uint32_t running = 0, prun = 0;
     for (int b = 0; b < SM_NBUCKETS; ++b) {
-        if (threadIdx.x == 0) V.seg_begin[b] = running;
+        if (threadIdx.x == 0) {
+            V.seg_begin[b] = running;
+            V.piece_begin[b] = prun;
+        }
         if (b & 1) continue;  // short buckets have no segments
         const uint32_t p0 = V.round_begin[b], p1 = V.round_begin[b + 1];
+        const uint32_t sbase = running;  // the bucket's first segment
         for (uint32_t c = p0; c < p1; c += 1024) {
             const uint32_t p = c + threadIdx.x;
-            const uint32_t ns = p < p1 ? (V.paths[p].len + SM_PRE_SEG - 1) / SM_PRE_SEG : 0u;
+            const uint32_t len = p < p1 ? V.paths[p].len : 0u;
+            const uint32_t ns = (len + SM_PRE_SEG - 1) / SM_PRE_SEG;
+            const uint32_t np = p < p1 ? (len >= 2u * plen ? len / plen : 1u) : 0u;
             sc[threadIdx.x] = ns;
+            sp[threadIdx.x] = np;
             __syncthreads();
-            for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+            for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scans
                 const uint32_t t = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0u;
+                const uint32_t u = threadIdx.x >= (unsigned)off ? sp[threadIdx.x - off] : 0u;
                 __syncthreads();
                 sc[threadIdx.x] += t;
+                sp[threadIdx.x] += u;
                 __syncthreads();
             }
             const uint32_t start = running + sc[threadIdx.x] - ns;
             for (uint32_t q = 0; q < ns; ++q) V.segtab[start + q] = make_uint2(p - p0, q);
+            const uint32_t pstart = prun + sp[threadIdx.x] - np;
+            for (uint32_t i = 0; i < np; ++i) V.pieces[pstart + i] = make_uint4(p - p0, np - 1u - i, np, start - sbase);
             running += sc[1023];
+            prun += sp[1023];
             __syncthreads();
         }
     }
-    if (threadIdx.x == 0) V.seg_begin[SM_NBUCKETS] = running;
+    if (threadIdx.x == 0) {
+        V.seg_begin[SM_NBUCKETS] = running;
+        V.piece_begin[SM_NBUCKETS] = prun;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
 static dim3 pix_grid(int W, int H, int nv) { return dim3((W + 255) / 256, H, nv); }
 
-hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains) {
+hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains,
+                         uint32_t piece_len) {
     const int N = W * H;
     const dim3 pg = pix_grid(W, H, nviews);
     hipLaunchKernelGGL(k_adj, pg, dim3(256), 0, st, LP, W, H);
@@ -673,6 +692,6 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     launch_scan<uint32_t, OpAdd>(st, lb, nviews, N);
     hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
     hipLaunchKernelGGL(k_meta, pg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP);
+    hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP, piece_len);
     return hipGetLastError();
 }

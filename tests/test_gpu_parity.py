@@ -104,6 +104,44 @@ def test_match_bitexact_synthetic(gpu_ctx, W, H, D):
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
 
 
+@pytest.mark.parametrize("plen,rmax", [("64", None), ("96", None), ("64", "1"), ("128", "2")])
+@pytest.mark.parametrize("W,H,D", [(320, 240, 64), (256, 160, 128), (200, 120, 200)])
+def test_pieces_match_bitexact(gpu_ctx, monkeypatch, plen, rmax, W, H, D):
+    """Long heavy paths cut into pieces of SM_PIECE_LEN nodes that run from guessed inputs and are
+    repaired exactly (sm_chain.hip "Pieces"); SM_REPAIR_MAX=1/2 makes most repairs give up, which
+    sends those pieces through the serial slow path.  SPL = 1, 2, 4."""
+    monkeypatch.setenv("SM_PIECE_LEN", plen)
+    if rmax:
+        monkeypatch.setenv("SM_REPAIR_MAX", rmax)
+    else:
+        monkeypatch.delenv("SM_REPAIR_MAX", raising=False)
+    left, right, _ = make_pair(W, H, D, index=4)
+    out = gpu_ctx.match(left, right, D)
+    ref = O.match(left, right, D, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+@pytest.mark.parametrize("plen,rmax", [("64", None), ("64", "1")])
+def test_pieces_rows_bitexact(gpu_ctx, monkeypatch, plen, rmax):
+    """Every fp64 A_up / A value of 4 slices with short pieces, bitwise."""
+    monkeypatch.setenv("SM_PIECE_LEN", plen)
+    if rmax:
+        monkeypatch.setenv("SM_REPAIR_MAX", rmax)
+    else:
+        monkeypatch.delenv("SM_REPAIR_MAX", raising=False)
+    W, H, d0, D = 400, 300, 20, 4
+    left, right, _ = make_pair(W, H, 64, index=5)
+    lv, rv = O.cost_agd(left, right, d0, d0 + D)
+    for vi, (img, vol) in enumerate(((left, lv), (right, rv))):
+        Aup, A = gpu_ctx.aggregate_debug(left, right, vi, d0, D)
+        t = O.build_tree(img)
+        r = O.tree_filter(W, H, t, vol, d0, False, True, 16)
+        assert np.array_equal(bits(Aup), bits(r["Aup"]))
+        assert np.array_equal(bits(A), bits(r["A"]))
+
+
 def test_match_shard_offset_bitexact(gpu_ctx):
     """A disparity shard [d0, d0+D) (what one rank computes under D sharding)."""
     import stereomatch_amd as sm
