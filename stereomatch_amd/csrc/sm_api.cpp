@@ -400,6 +400,7 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     for (int v = 0; v < 2; ++v) {
         a.meta[v] = P<SmMeta>(ctx->meta[v]);
         a.U[v] = P<double>(ctx->U[v]);
+        a.A[v] = nullptr;  // set by setup_sync (the fix buffer)
         a.Cst[v] = P<float>(ctx->Cst[v]);
         a.idx[v] = P<int32_t>(ctx->idx[v]);
         a.minc[v] = P<double>(ctx->minc[v]);
@@ -523,7 +524,7 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
 // waits for its longest light subtree near the bottom of the path either way.)
 bool can_merge_down(sm_ctx* ctx, int nviews) {
     static const bool off = getenv("SM_NO_MERGE") != nullptr;  // A/B switch
-    if (off) return false;
+    if (off || !no_pieces()) return false;  // pieces shorten the root chain instead
     for (int v = 0; v < nviews; ++v) {
         const auto& L = ctx->layout[v];
         if (L.nrounds < 2 || L.begin[1] == L.begin[0] || L.begin[2] != L.begin[1] || L.begin[3] == L.begin[2]) return false;
@@ -584,7 +585,8 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
         if (fresh) HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
         a.ready[v] = P<uint32_t>(ctx->ready[v]);
     }
-    // piece buffers: segment aggregates and 6 status-word arrays (up: done/merged/final, down: same)
+    // piece buffers: segment aggregates and 8 status-word arrays (up: done/merged/final, down: same
+    // + aggregate published)
     const size_t pcap = piece_cap(N);
     a.pstride = (int)pcap;
     a.piece_len = piece_len();
@@ -606,16 +608,17 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
     for (int v = 0; v < 2; ++v) {
         CHECK(ensure(ctx, ctx->agg[v], pcap * 2 * (size_t)Dpad * 8));
         CHECK(ensure(ctx, ctx->fix[v], N * (size_t)Dpad * 8));
-        a.fix[v] = P<double>(ctx->fix[v]);
-        const bool fresh = ctx->pstat[v].n < pcap * 6 * 4;
-        CHECK(ensure(ctx, ctx->pstat[v], pcap * 6 * 4));
-        if (fresh) HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 6 * 4, ctx->st));
+        a.fix[v] = P<double>(ctx->fix[v]);  // up pass: buffered repair rows
+        a.A[v] = a.fix[v];                  // down pass: A rows
+        const bool fresh = ctx->pstat[v].n < pcap * 8 * 4;
+        CHECK(ensure(ctx, ctx->pstat[v], pcap * 8 * 4));
+        if (fresh) HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 8 * 4, ctx->st));
     }
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0 || a.epoch >= 0x7FFFFFFFu) {  // wrapped (merged words hold 2*epoch+1): clear every word
         for (int v = 0; v < 2; ++v) {
             HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
-            HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 6 * 4, ctx->st));
+            HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 8 * 4, ctx->st));
         }
         a.epoch = ctx->epoch = 1;
     }
@@ -652,6 +655,7 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
         HIPC(hipStreamSynchronize(ctx->st));
         fprintf(stderr, "pieces: fast %llu slow %llu repair nodes sum %llu max %llu | merge <8 %llu <16 %llu <32 %llu <64 %llu <128 %llu >=128 %llu never %llu\n",
                 h[0], h[1], h[2], h[3], h[8], h[9], h[10], h[11], h[12], h[13], h[14]);
+        fprintf(stderr, "down pieces: fast %llu slow %llu repair nodes sum %llu max %llu\n", h[4], h[5], h[6], h[7]);
     }
     (void)N;
     return SM_OK;
@@ -981,7 +985,7 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
         HIPC(hipStreamSynchronize(ctx->st));
     }
     CHECK(stage_filter(ctx, D, d0, 2, true));
-    HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
+    HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->fix[view]), (int)N, Dpad, D, N,
                                P<double>(ctx->vol[0])));
     if (A) HIPC(hipMemcpyAsync(A, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));
     HIPC(hipStreamSynchronize(ctx->st));

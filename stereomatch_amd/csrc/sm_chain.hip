@@ -999,7 +999,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     __shared__ double guess[64 * SPL];
     __shared__ int hdone;
     const int view = blockIdx.y;
-    const WalkView V{view ? V1.npaths : V0.npaths, view ? V1.U : V0.U, nullptr, nullptr, nullptr};
+    const WalkView V{view ? V1.npaths : V0.npaths, view ? V1.U : V0.U, nullptr, nullptr, nullptr, nullptr};
     // field-wise select: a reference to one of two by-value kernel arguments would copy both to
     // scratch
     PieceView Q;
@@ -1027,6 +1027,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
     const bool lower = j + 1 < M;
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    static_assert(sizeof(ring.s) >= (size_t)CHN_WAVES * 2 * 64 * SPL * sizeof(double), "prologue scratch");
     if (lower) {  // guessed input: the aggregates of the segments below the piece
         const int sb = o1 / SM_PRE_SEG, ns = (plen + SM_PRE_SEG - 1) / SM_PRE_SEG - sb;
         up_guess<SPL>(reinterpret_cast<double*>(ring.s), guess, Q.agg + (size_t)(pc.w + sb) * 2 * Dpad, ns, Dpad, wave, lane);
@@ -1106,7 +1107,7 @@ __device__ __forceinline__ void down_group(DownSlot<SPL>& sl, int k0, int e0, do
 template <int SPL>
 __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int len, int lane,
                                                 const double* __restrict__ U, uint32_t hparent, int Dpad,
-                                                const uint32_t* ready, uint32_t epoch) {
+                                                const uint32_t* ready, uint32_t epoch, const double* x0) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, CS = Split<SPL>::CS;
     __builtin_amdgcn_s_setprio(3);
     unsigned spins = 0;
@@ -1116,7 +1117,10 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
 #endif
     const int e0 = (w * 64 + lane) * CS;
     double x[CS];
-    if (hparent != SM_NONE && ready) {
+    if (x0) {  // a piece below the path's first piece: its guessed input (the repair follows)
+#pragma unroll
+        for (int q = 0; q < CS; ++q) x[q] = x0[e0 + q];
+    } else if (hparent != SM_NONE && ready) {
         // merged launch, consumer: A(parent) is produced by a chain of this same launch; wait for
         // its readiness word, then read the row at device scope (written through by the producer)
         wait_ready(ready, hparent, epoch);
@@ -1171,7 +1175,7 @@ template <int SPL>
 __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, int head, int len, int lane,
                                                  uint32_t hparent, const uint32_t* __restrict__ meta32,
                                                  const WalkView& V, int Dpad, int dcall, int dglob0, int store_all,
-                                                 uint32_t* ready, uint32_t epoch) {
+                                                 uint32_t* ready, uint32_t epoch, uint32_t* done_word) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
     const int ngroups = (len + G - 1) / G;
     int g = hh;
@@ -1238,7 +1242,7 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
 #pragma unroll
             for (int k = 0; k < G; ++k)
                 if (k < n && (store_all || st[k])) {
-                    double* row = U + (size_t)(head + g * G + k) * Dpad + lane * SPL;
+                    double* row = V.A + (size_t)(head + g * G + k) * Dpad + lane * SPL;
 #pragma unroll
                     for (int q = 0; q < SPL; ++q)
                         __hip_atomic_store(row + q, xs[k][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1251,16 +1255,273 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
         } else {
 #pragma unroll
             for (int k = 0; k < G; ++k)
-                if (k < n && (store_all || st[k])) store_row<SPL>(U, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
+                if (k < n && (store_all || st[k])) store_row<SPL>(V.A, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
         }
         if (lane < n) {
             V.idx[pix] = dglob0 + mi;
             V.minc[pix] = mn;
             V.disp[pix] = (float)(dglob0 + mi);
         }
+        if (done_word && g == ngroups - 1) {
+            // the piece's last row is the next piece's input: device scope, then the done word
+            double* row = V.A + (size_t)(head + len - 1) * Dpad + lane * SPL;
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                if (k == n - 1)
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xs[k][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            vm_drain();
+            if (lane == 0) publish_word(done_word, epoch);
+        }
         if (gn >= ngroups) break;
         g = gn;
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Down-pass pieces (see "Pieces" above; pieces top first).  The guess of piece i is the fold of
+// the piece-level affine aggregates of pieces 0 .. i-1 (A(last) = P * A(before) + B, with the
+// reference's per-node map A = S * A(parent) + S2 * A_up) applied to the path's input row; every
+// piece computes its own aggregate in the prologue (16 waves in parallel) and publishes it, so
+// the guess waits for no chain.  The repair re-runs the piece's first nodes from the true input
+// and compares at the nodes whose rows are stored (light children's parents, the piece's last
+// node): equal there -> equal from there on.  Corrections (WTA outputs, stored rows) are written
+// directly; when the look-back finds a piece above that did not merge, the piece is re-walked
+// completely from the final input (correctness only), overwriting everything it wrote.
+// ---------------------------------------------------------------------------------------------
+// per-piece aggregate: all 16 waves fold a contiguous node range (top first), combined in LDS;
+// ends with a barrier, the result (P row | B row) is in scratch[0 .. 2 * 64 * SPL)
+template <int SPL>
+__device__ void down_piece_agg(double* scratch, const uint32_t* __restrict__ meta32, const double* __restrict__ U,
+                               const double* slut, const double* s2lut, int head, int len, int Dpad, int wave, int lane) {
+    const int per = (len + CHN_WAVES - 1) / CHN_WAVES;
+    const int n0 = min(len, wave * per), n1 = min(len, n0 + per);
+    double P[SPL], B[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        P[k] = 1.0;
+        B[k] = 0.0;
+    }
+    for (int n = n0; n < n1; n += 8) {
+        const int nb = min(8, n1 - n);
+        MetaVec<8> mv;
+        load_meta<8>(mv, meta32, lane, head + n, 1, nb);
+        double u[8][SPL];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) load_row<SPL>(U, (uint32_t)(head + n + min(k, nb - 1)), Dpad, lane, u[k]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k < nb) {
+                const bool root = mfield(mv, k, 1) == SM_NONE;
+                const uint32_t wp = lo_wp(mfield(mv, k, 2));
+                const double S = root ? 0.0 : slut[wp], S2 = s2lut[wp];
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) {
+                    B[q] = __builtin_fma(S, B[q], root ? u[k][q] : S2 * u[k][q]);
+                    P[q] = S * P[q];
+                }
+            }
+        }
+    }
+    double* my = scratch + (size_t)wave * 2 * 64 * SPL;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        my[lane * SPL + k] = P[k];
+        my[64 * SPL + lane * SPL + k] = B[k];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int q = 0; q < SPL; ++q) {
+            double p = scratch[lane * SPL + q], b = scratch[64 * SPL + lane * SPL + q];
+            for (int w = 1; w < CHN_WAVES; ++w) {
+                const double* t = scratch + (size_t)w * 2 * 64 * SPL;
+                b = __builtin_fma(t[lane * SPL + q], b, t[64 * SPL + lane * SPL + q]);
+                p = t[lane * SPL + q] * p;
+            }
+            scratch[lane * SPL + q] = p;
+            scratch[64 * SPL + lane * SPL + q] = b;
+        }
+    }
+    __syncthreads();
+}
+
+// guessed input of piece e (index i >= 1 within its path): x_path (the path's input row: A of
+// the head's parent) through the aggregates of the pieces above, entries e - i .. e - 1, split
+// over the 16 waves.  Ends with a barrier; the result is in guess[].
+template <int SPL>
+__device__ void down_guess(double* scratch, double* guess, const double* __restrict__ A, const double* __restrict__ agg,
+                           const uint32_t* aggw, uint32_t hp, int e, int i, int Dpad, int wave, int lane,
+                           uint32_t epoch) {
+    const int per = (i + CHN_WAVES - 1) / CHN_WAVES;
+    const int q0 = min(i, wave * per), q1 = min(i, q0 + per);
+    double P[SPL], B[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        P[k] = 1.0;
+        B[k] = 0.0;
+    }
+    for (int q = q0; q < q1; ++q) {
+        const int eq = e - i + q;
+        wait_word(aggw + eq, epoch, epoch);
+        vm_drain();
+        double p[SPL], b[SPL];
+        agent_row_read<SPL>(agg + (size_t)eq * 2 * Dpad, 0, Dpad, lane, p);
+        agent_row_read<SPL>(agg + (size_t)eq * 2 * Dpad + Dpad, 0, Dpad, lane, b);
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) {
+            B[k] = __builtin_fma(p[k], B[k], b[k]);
+            P[k] = p[k] * P[k];
+        }
+    }
+    double* my = scratch + (size_t)wave * 2 * 64 * SPL;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        my[lane * SPL + k] = P[k];
+        my[64 * SPL + lane * SPL + k] = B[k];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        double x[SPL];
+        if (hp != SM_NONE) {
+            load_row<SPL>(A, hp, Dpad, lane, x);  // finished in an earlier launch
+        } else {
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) x[k] = 0.0;  // the root's S is 0
+        }
+        for (int w = 0; w < CHN_WAVES; ++w) {
+            const double* t = scratch + (size_t)w * 2 * 64 * SPL;
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) x[k] = __builtin_fma(t[lane * SPL + k], x[k], t[64 * SPL + lane * SPL + k]);
+        }
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) guess[lane * SPL + k] = x[k];
+    }
+    __syncthreads();
+}
+
+// Exact re-walk of a down piece's nodes 0 .. nmax-1 (slot head + n) from the input row x:
+// A = fma(S, x, S2 * A_up) as the chain, WTA outputs and the stored rows (light children's
+// parents, every row with store_all, the piece's last node at device scope when last_pub) of
+// every node before the merge.  check: compare at stored nodes and return the first node equal
+// in all lanes (nothing is written from there on); otherwise / no merge: -1.
+template <int SPL, int CHR>
+__device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta32, const double* __restrict__ U,
+                                               const WalkView& V, const double* slut, const double* s2lut, int head,
+                                               int len, int nmax, int Dpad, int lane, double* xio, int dcall, int dglob0,
+                                               int store_all, bool last_pub, bool check) {
+    double x[SPL];
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) x[q] = xio[q];
+    MetaVec<CHR> mv;
+    load_meta<CHR>(mv, meta32, lane, head, 1, min(CHR, nmax));
+    for (int n0 = 0; n0 < nmax; n0 += CHR) {
+        const int nb = min(CHR, nmax - n0);
+        MetaVec<CHR> mn;
+        const int n1 = n0 + CHR < nmax ? n0 + CHR : n0;
+        load_meta<CHR>(mn, meta32, lane, head + n1, 1, min(CHR, nmax - n1));
+        double u[CHR][SPL], spec[CHR][SPL], ys[CHR][SPL];
+#pragma unroll
+        for (int k = 0; k < CHR; ++k) {
+            const uint32_t slot = (uint32_t)(head + n0 + min(k, nb - 1));
+            load_row<SPL>(U, slot, Dpad, lane, u[k]);
+            if (check) agent_row_read<SPL>(V.A, slot, Dpad, lane, spec[k]);
+        }
+        int mk = nb;  // nodes of this batch before the merge
+#pragma unroll
+        for (int k = 0; k < CHR; ++k) {
+            if (k < mk) {
+                const uint32_t wp = lo_wp(mfield(mv, k, 2));
+                const double S = slut[wp], S2 = s2lut[wp];
+                bool eq = true;
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) {
+                    x[q] = __builtin_fma(S, x[q], S2 * u[k][q]);
+                    ys[k][q] = x[q];
+                    eq = eq && __double_as_longlong(x[q]) == __double_as_longlong(spec[k][q]);
+                }
+                const bool stored = store_all || hi_light(mfield(mv, k, 3)) || (last_pub && n0 + k == len - 1);
+                if (check && stored && __all(eq)) mk = k;
+            } else {
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) ys[k][q] = 0.0;
+            }
+        }
+        double mnv;
+        int mi;
+        wta_chunk<SPL, CHR>(ys, lane, lane * SPL, dcall, mnv, mi);
+        const uint32_t pix = meta_pix_of_lane<CHR>(mv, lane);
+        if (lane < mk) {
+            V.idx[pix] = dglob0 + mi;
+            V.minc[pix] = mnv;
+            V.disp[pix] = (float)(dglob0 + mi);
+        }
+#pragma unroll
+        for (int k = 0; k < CHR; ++k) {
+            if (k < mk) {
+                const uint32_t slot = (uint32_t)(head + n0 + k);
+                if (last_pub && n0 + k == len - 1)
+                    agent_row_write<SPL>(V.A, slot, Dpad, lane, ys[k]);
+                else if (store_all || hi_light(mfield(mv, k, 3)))
+                    store_row<SPL>(V.A, slot, Dpad, lane, ys[k]);
+            }
+        }
+        if (mk < nb) return n0 + mk;
+        mv = mn;
+    }
+    return -1;
+}
+
+#ifndef DN_WALK_CH
+#define DN_WALK_CH(SPL) ((SPL) == 4 ? 4 : 8)  // nodes per down-repair batch (registers)
+#endif
+
+// Repair + look-back of down piece e (index i of M, pieces top first: the pieces above are
+// entries e - i .. e - 1, the top one exact by construction).
+template <int SPL>
+__device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __restrict__ meta32, const WalkView& V,
+                            int Dpad, int dcall, int dglob0, int store_all, int lane, int head, int len, int i, int M,
+                            int e, const PieceView& Q, uint32_t epoch) {
+    uint32_t* done = Q.stat;
+    uint32_t* merged = Q.stat + Q.stride;
+    uint32_t* fin = Q.stat + 2 * Q.stride;
+    if (i == 0) {
+        if (lane == 0) publish_word(fin + e, epoch);
+        return;
+    }
+    while (__hip_atomic_load(hdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < Split<SPL>::NH) __builtin_amdgcn_s_sleep(1);
+    const bool last_pub = i + 1 < M;
+    const uint32_t above = (uint32_t)(head - 1);  // last node of the piece above
+    double x[SPL];
+    wait_word(done + e - 1, epoch, epoch);
+    vm_drain();
+    agent_row_read<SPL>(V.A, above, Dpad, lane, x);
+    vm_drain();
+    const int m = down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, min(Q.rmax, len), Dpad,
+                                                        lane, x, dcall, dglob0, store_all, last_pub, true);
+    vm_drain();
+    if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
+    bool all = m >= 0;
+    for (int q = e - 1; all && q > e - i; --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u) == 2u * epoch;
+    if (Q.dbg && lane == 0) {
+        atomicAdd(Q.dbg + (all ? 4 : 5), 1ull);
+        if (m >= 0) {
+            atomicAdd(Q.dbg + 6, (unsigned long long)m);
+            atomicMax(Q.dbg + 7, (unsigned long long)m);
+        }
+    }
+    if (all) {
+        if (lane == 0) publish_word(fin + e, epoch);
+        return;
+    }
+    wait_word(fin + e - 1, epoch, epoch);
+    vm_drain();
+    agent_row_read<SPL>(V.A, above, Dpad, lane, x);
+    vm_drain();
+    down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, len, Dpad, lane, x, dcall, dglob0,
+                                          store_all, last_pub, false);
+    vm_drain();
+    if (lane == 0) publish_word(fin + e, epoch);
 }
 
 template <int SPL>
@@ -1272,8 +1533,11 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
                                                             const double* __restrict__ slut_g,
                                                             const double* __restrict__ s2lut_g, int Dpad, int dcall,
                                                             int dglob0, int store_all, uint32_t* ready0,
-                                                            uint32_t* ready1, uint32_t epoch, int nprod0, int nprod1) {
+                                                            uint32_t* ready1, uint32_t epoch, int nprod0, int nprod1,
+                                                            PieceView Q0, PieceView Q1) {
     __shared__ DownRing<SPL> ring;
+    __shared__ double guess[64 * SPL];
+    __shared__ int hdone;
     // merged launch (nprod0 + nprod1 > 0, flat grid): per view, paths [0, nprod) produce rows for
     // the paths after them (their light children's chains), which wait per path for their
     // parent's readiness word.  Producers of both views take the first block ids, so they are
@@ -1296,36 +1560,98 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     }
     view = (int)uniform((uint32_t)view);
     pidx = (int)uniform((uint32_t)pidx);
-    const WalkView& V = view ? V1 : V0;
-    if (pidx >= V.npaths) return;
+    // field-wise selects (a reference to one of two by-value arguments would go to scratch)
+    WalkView V;
+    V.npaths = view ? V1.npaths : V0.npaths;
+    V.U = view ? V1.U : V0.U;
+    V.idx = view ? V1.idx : V0.idx;
+    V.minc = view ? V1.minc : V0.minc;
+    V.disp = view ? V1.disp : V0.disp;
+    V.A = view ? V1.A : V0.A;
+    PieceView Q;
+    Q.pieces = view ? Q1.pieces : Q0.pieces;
+    Q.npieces = view ? Q1.npieces : Q0.npieces;
+    Q.agg = view ? Q1.agg : Q0.agg;
+    Q.fix = nullptr;
+    Q.stat = view ? Q1.stat : Q0.stat;
+    Q.stride = Q0.stride;
+    Q.plen = Q0.plen;
+    Q.rmax = Q0.rmax;
+    Q.dbg = Q0.dbg;
+    // pieces: block e = piece i of M of its path, pieces top first (entries list a path's pieces
+    // bottom first with index j: i = M - 1 - j)
+    uint4 pc = make_uint4((uint32_t)pidx, 0u, 1u, 0u);
+    if (Q.pieces) {
+        if (pidx >= Q.npieces) return;  // uniform over the block
+        pc = Q.pieces[pidx];
+    } else if (pidx >= V.npaths) {
+        return;
+    }
+    const int M = (int)uniform(pc.z), i = M - 1 - (int)uniform(pc.y);
     const int nprod = view ? nprod1 : nprod0;
     uint32_t* ready = nprod > 0 ? (view ? ready1 : ready0) : nullptr;
     uint32_t* prod_ready = pidx < nprod ? ready : nullptr;
     const uint32_t* cons_ready = pidx >= nprod ? ready : nullptr;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
-    const SmPath path = (view ? paths1 : paths0)[pidx];
-    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
+    const SmPath path = (view ? paths1 : paths0)[uniform(pc.x)];
+    const int plen = (int)uniform(path.len);
+    const int o0 = i * Q.plen, o1 = i + 1 == M ? plen : (i + 1) * Q.plen;
+    const int head = (int)uniform(path.head) + o0, len = o1 - o0;
     const uint32_t hparent = uniform(meta32[(size_t)head * 8 + 1]);
-    for (int i = threadIdx.x; i < DownCfg<SPL>::NS; i += CHN_THREADS) {
-        ring.s[i].staged = ring.s[i].freed = 0;
-        ring.s[i].done[0] = ring.s[i].done[1] = 0;
-    }
-    for (int i = threadIdx.x; i < SM_NUM_W; i += CHN_THREADS) {
-        ring.slut[i] = slut_g[i];
-        ring.s2lut[i] = s2lut_g[i];
+    const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (int k = threadIdx.x; k < SM_NUM_W; k += CHN_THREADS) {
+        ring.slut[k] = slut_g[k];
+        ring.s2lut[k] = s2lut_g[k];
     }
     if (threadIdx.x == 0) ring.slut[SM_NUM_W] = 0.0;
     __syncthreads();
-    const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wave < Split<SPL>::NCW)
-        down_chain_wave<SPL>(ring, wave, len, lane, V.U, hparent, Dpad, cons_ready, epoch);
-    else if (Split<SPL>::helper_of(wave) >= 0)
+    if (M > 1) {
+        uint32_t* aggw = Q.stat + 3 * Q.stride;
+        double* scratch = reinterpret_cast<double*>(ring.s);
+        static_assert(sizeof(ring.s) >= (size_t)CHN_WAVES * 2 * 64 * SPL * sizeof(double), "prologue scratch");
+        if (i + 1 < M) {  // this piece's aggregate, for the pieces below
+            down_piece_agg<SPL>(scratch, meta32, V.U, ring.slut, ring.s2lut, head, len, Dpad, wave, lane);
+            if (wave == 0) {
+                double p[SPL], b[SPL];
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) {
+                    p[q] = scratch[lane * SPL + q];
+                    b[q] = scratch[64 * SPL + lane * SPL + q];
+                }
+                double* out = const_cast<double*>(Q.agg) + (size_t)pidx * 2 * Dpad;
+                agent_row_write<SPL>(out, 0, Dpad, lane, p);
+                agent_row_write<SPL>(out + Dpad, 0, Dpad, lane, b);
+                vm_drain();
+                if (lane == 0) publish_word(aggw + pidx, epoch);
+            }
+            __syncthreads();
+        }
+        if (i > 0)
+            down_guess<SPL>(scratch, guess, V.A, Q.agg, aggw, uniform(meta32[(size_t)path.head * 8 + 1]), pidx, i, Dpad, wave,
+                            lane, epoch);
+    }
+    for (int k = threadIdx.x; k < DownCfg<SPL>::NS; k += CHN_THREADS) {
+        ring.s[k].staged = ring.s[k].freed = 0;
+        ring.s[k].done[0] = ring.s[k].done[1] = 0;
+    }
+    if (threadIdx.x == 0) hdone = 0;
+    __syncthreads();
+    if (wave < Split<SPL>::NCW) {
+        down_chain_wave<SPL>(ring, wave, len, lane, V.A, hparent, Dpad, cons_ready, epoch, i > 0 ? guess : nullptr);
+        if (wave == 0 && M > 1)
+            down_finish<SPL>(ring, &hdone, meta32, V, Dpad, dcall, dglob0, store_all, lane, head, len, i, M, pidx, Q, epoch);
+    } else if (Split<SPL>::helper_of(wave) >= 0) {
         down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, hparent, meta32, V, Dpad, dcall, dglob0,
-                              store_all, prod_ready, epoch);
+                              store_all, prod_ready, epoch, (M > 1 && i + 1 < M) ? Q.stat + pidx : nullptr);
+        vm_drain();  // this helper's stores are complete before the repair overwrites them
+        if (lane == 0) atomicAdd(&hdone, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
-static WalkView chain_view(const WalkArgs& a, int v) { return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v]}; }
+static WalkView chain_view(const WalkArgs& a, int v) {
+    return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v]};
+}
 
 #ifndef UP_PRE_CH2
 #define UP_PRE_CH2 8  // nodes per wave of k_up_pre at SPL=2
@@ -1357,10 +1683,13 @@ template <int SPL>
 static void down_chain_launch(hipStream_t st, const WalkArgs& a, int np, int store_all) {
     const bool merged = a.nprod[0] + a.nprod[1] > 0;
     const dim3 grid = merged ? dim3(a.npaths[0] + a.npaths[1], 1) : dim3(np, 2);
+    PieceView q0 = piece_view(a, 0), q1 = piece_view(a, 1);
+    for (PieceView* q : {&q0, &q1})  // the down pass's status words: arrays 3..6 (up: 0..2)
+        if (q->stat) q->stat += 3 * (size_t)q->stride;
     hipLaunchKernelGGL((k_down_chain<SPL>), grid, dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                        a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all, a.ready[0],
-                       a.ready[1], a.epoch, a.nprod[0], a.nprod[1]);
+                       a.ready[1], a.epoch, a.nprod[0], a.nprod[1], q0, q1);
 }
 
 hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {
@@ -1385,7 +1714,8 @@ hipError_t launch_up_chain(hipStream_t st, const WalkArgs& a, int spl) {
 }
 
 hipError_t launch_down_long(hipStream_t st, const WalkArgs& a, int spl, int store_all) {
-    const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
+    int np = 0;
+    for (int v = 0; v < 2; ++v) np = std::max(np, a.pieces[v] ? a.npieces[v] : a.npaths[v]);
     if (np == 0) return hipSuccess;
     switch (spl) {
         case 1: down_chain_launch<1>(st, a, np, store_all); break;

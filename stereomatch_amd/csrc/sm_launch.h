@@ -37,6 +37,7 @@ struct WalkArgs {
     const SmPath* paths[2];
     int npaths[2];
     double* U[2];
+    double* A[2];        // down-pass A rows (the up repair's scratch: free during the down pass)
     int32_t* idx[2];
     double* minc[2];
     float* disp[2];

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
             par[j] = mfield(cur, jj, 1);
             const bool head_j = par[j] == SM_NONE || par[j] != slot - 1u;
             load_row<SPL>(V.U, slot, Dpad, lane, u[j]);
-            load_row<SPL>(V.U, head_j && par[j] != SM_NONE ? par[j] : slot, Dpad, lane, xp[j]);
+            load_row<SPL>(head_j && par[j] != SM_NONE ? V.A : V.U, head_j && par[j] != SM_NONE ? par[j] : slot, Dpad, lane, xp[j]);
         }
         double S[CH], S2[CH];
 #pragma unroll
@@ -254,8 +254,8 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            if (j < n && (store_all || (hi_light(mfield(cur, j, 3)) && par[j] != SM_NONE)))
-                store_row<SPL>(V.U, (uint32_t)(c0 + j), Dpad, lane, xs[j]);
+            if (j < n && (store_all || hi_light(mfield(cur, j, 3))))  // the root too: A is a separate buffer
+                store_row<SPL>(V.A, (uint32_t)(c0 + j), Dpad, lane, xs[j]);
         }
         double mn;
         int mi;
@@ -274,7 +274,9 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
 }
 
 // ---------------------------------------------------------------------------------------------
-static WalkView to_view(const WalkArgs& a, int v) { return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v]}; }
+static WalkView to_view(const WalkArgs& a, int v) {
+    return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v]};
+}
 
 template <int SPL, int CH>
 static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a) {

@@ -11,10 +11,12 @@
 // arguments (kernarg-derived, provably unclobbered)
 struct WalkView {
     int npaths;
-    double* U;             // [slots][Dpad]
+    double* U;             // [slots][Dpad]: A_up (the up pass writes, the down pass reads)
     int32_t* idx;          // W*H   (down pass)
     double* minc;          // W*H   (down pass)
     float* disp;           // W*H   (down pass)
+    double* A;             // [slots][Dpad]: A rows of the down pass (rows light children or the
+                           // debug path read); separate from U so A_up stays intact (down repair)
 };
 
 #define SM_NUM_W 766
