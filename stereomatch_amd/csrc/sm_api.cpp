@@ -52,8 +52,7 @@ struct sm_ctx {
     DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
     DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
-    DevBuf ready[2];         // merged chain launches: per-slot readiness words (epoch values)
-    uint32_t epoch = 0;      // bumped per filter call; ready[] is zeroed only on (re)allocation
+    uint32_t epoch = 0;      // bumped per filter call; status words are zeroed only on (re)allocation
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
@@ -516,46 +515,13 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
     return SM_OK;
 }
 
-// The down pass's first two rounds in one chain launch: round 0 (the root's heavy path) produces
-// rows, round 1's long paths (light children of it) start as soon as their parent's row is
-// final instead of after the whole root chain.  Needs an empty short bucket in round 0 so the
-// two long buckets are one contiguous path range.  (The mirror image for the up pass -- the root
-// chain consuming round 1's heads as they finish -- was measured slower at C2: the root chain
-// waits for its longest light subtree near the bottom of the path either way.)
-bool can_merge_down(sm_ctx* ctx, int nviews) {
-    static const bool off = getenv("SM_NO_MERGE") != nullptr;  // A/B switch
-    if (off || !no_pieces()) return false;  // pieces shorten the root chain instead
-    for (int v = 0; v < nviews; ++v) {
-        const auto& L = ctx->layout[v];
-        if (L.nrounds < 2 || L.begin[1] == L.begin[0] || L.begin[2] != L.begin[1] || L.begin[3] == L.begin[2]) return false;
-    }
-    return true;
-}
-
-sm_status down_merged_01(sm_ctx* ctx, WalkArgs& a, int spl, int nviews, bool store_all) {
-    CHECK(join(ctx, ctx->st, ctx->st2));
-    CHECK(join(ctx, ctx->st2, ctx->st));
-    set_bucket(ctx, a, 0, true, nviews);
-    for (int v = 0; v < nviews; ++v) {
-        const auto& L = ctx->layout[v];
-        a.npaths[v] = (int)(L.begin[3] - L.begin[0]);
-        a.nprod[v] = (int)(L.begin[1] - L.begin[0]);
-    }
-    const WalkArgs al = a;
-    a.nprod[0] = a.nprod[1] = 0;
-    const double vox = bucket_voxels(ctx, 0, true, nviews, a.dcall) + bucket_voxels(ctx, 1, true, nviews, a.dcall);
-    CHECK(timed(ctx, ctx->st2, KF_DOWN_CHAIN, vox, [&] { return launch_down_long(ctx->st2, al, spl, store_all ? 1 : 0); }));
-    return SM_OK;
-}
-
-sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews, bool store_all, bool chains = true) {
+sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews, bool store_all) {
     CHECK(join(ctx, ctx->st, ctx->st2));
     CHECK(join(ctx, ctx->st2, ctx->st));
     set_bucket(ctx, a, r, true, nviews);
     const WalkArgs al = a;
-    if (chains)
-        CHECK(timed(ctx, ctx->st2, KF_DOWN_CHAIN, bucket_voxels(ctx, r, true, nviews, a.dcall),
-                    [&] { return launch_down_long(ctx->st2, al, spl, store_all ? 1 : 0); }));
+    CHECK(timed(ctx, ctx->st2, KF_DOWN_CHAIN, bucket_voxels(ctx, r, true, nviews, a.dcall),
+                [&] { return launch_down_long(ctx->st2, al, spl, store_all ? 1 : 0); }));
     set_bucket(ctx, a, r, false, nviews);
     const WalkArgs as = a;
     CHECK(timed(ctx, ctx->st, KF_DOWN_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall), [&] {
@@ -576,15 +542,9 @@ sm_status ensure_filter_bufs(sm_ctx* ctx, int Dpad) {
     return SM_OK;
 }
 
-// cross-workgroup synchronisation state of one filter call: readiness words (merged down launch),
-// piece aggregates and status words, and the call's epoch (no per-call reset of any word)
+// cross-workgroup synchronisation state of one filter call: piece aggregates and status words, and
+// the call's epoch (no per-call reset of any word)
 sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
-    for (int v = 0; v < 2; ++v) {
-        const bool fresh = ctx->ready[v].n < N * 4;
-        CHECK(ensure(ctx, ctx->ready[v], N * 4));
-        if (fresh) HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
-        a.ready[v] = P<uint32_t>(ctx->ready[v]);
-    }
     // piece buffers: segment aggregates and 8 status-word arrays (up: done/merged/final, down: same
     // + aggregate published)
     const size_t pcap = piece_cap(N);
@@ -616,10 +576,7 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
     }
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0 || a.epoch >= 0x7FFFFFFFu) {  // wrapped (merged words hold 2*epoch+1): clear every word
-        for (int v = 0; v < 2; ++v) {
-            HIPC(hipMemsetAsync(ctx->ready[v].p, 0, N * 4, ctx->st));
-            HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 8 * 4, ctx->st));
-        }
+        for (int v = 0; v < 2; ++v) HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 8 * 4, ctx->st));
         a.epoch = ctx->epoch = 1;
     }
     return SM_OK;
@@ -639,15 +596,7 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     ctx->fam.clear();
     ctx->fam_vox.clear();
     for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest first
-    const bool mdown = can_merge_down(ctx, nviews);
-    for (uint32_t r = 0; r < nr; ++r) {
-        if (mdown && r == 0) {
-            CHECK(down_merged_01(ctx, a, spl, nviews, debug_store_all));
-            CHECK(down_round(ctx, a, 0, spl, nviews, debug_store_all, false));
-        } else {
-            CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all, !(mdown && r == 1)));
-        }
-    }
+    for (uint32_t r = 0; r < nr; ++r) CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all));
     CHECK(join(ctx, ctx->st, ctx->st2));  // everything after the filter runs on st
     if (a.piece_dbg) {
         unsigned long long h[16];
@@ -811,7 +760,7 @@ void sm_destroy(sm_ctx* ctx) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
                          &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v], &ctx->Cst[v],
                          &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v],
-                         &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v], &ctx->ready[v]};
+                         &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);

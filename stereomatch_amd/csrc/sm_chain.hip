@@ -333,17 +333,6 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
     for (int w = 0; w < n; ++w) lds_wait(&p[w], v, true);
 }
 
-// Merged launches (a round's chains with the next round's): rows crossing workgroups inside one
-// launch are written and read at device scope (coherent across the XCDs' L2s), and a per-slot
-// readiness word (== the filter call's epoch) orders them.  Waits are bounded (~1 s): a missing
-// word shows up as a parity failure, never as a hang.
-__device__ __forceinline__ void wait_ready(const uint32_t* ready, uint32_t slot, uint32_t epoch) {
-    for (int it = 0; it < (1 << 24); ++it) {
-        if (__hip_atomic_load(ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // k_up_chain
 //
@@ -1020,9 +1009,15 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     } else if (e >= V.npaths) {
         return;
     }
-    const SmPath path = (view ? paths1 : paths0)[uniform(pc.x)];
+    const SmPath* __restrict__ pp = view ? paths1 : paths0;
+    const SmPath path = pp[uniform(pc.x)];
     const int j = (int)uniform(pc.y), M = (int)uniform(pc.z);
-    const int plen = (int)uniform(path.len);
+    int plen = (int)uniform(path.len);
+    if (Q.pieces && M == 1) {  // a run of consecutive paths: one contiguous slot range (every path's
+                               // bottom node has S_heavy = 0, which restarts the recurrence)
+        const SmPath last = pp[uniform(pc.x + pc.w - 1u)];
+        plen = (int)uniform(last.head + last.len - path.head);
+    }
     const int o0 = j * Q.plen, o1 = j + 1 == M ? plen : (j + 1) * Q.plen;
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
     const bool lower = j + 1 < M;
@@ -1105,9 +1100,7 @@ __device__ __forceinline__ void down_group(DownSlot<SPL>& sl, int k0, int e0, do
 }
 
 template <int SPL>
-__device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int len, int lane,
-                                                const double* __restrict__ U, uint32_t hparent, int Dpad,
-                                                const uint32_t* ready, uint32_t epoch, const double* x0) {
+__device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int len, int lane, const double* x0) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, CS = Split<SPL>::CS;
     __builtin_amdgcn_s_setprio(3);
     unsigned spins = 0;
@@ -1116,26 +1109,11 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
     long long tr = 0, tc = 0;
 #endif
     const int e0 = (w * 64 + lane) * CS;
+    // a piece below the path's first piece starts from its guessed input (the repair follows);
+    // otherwise the first node is a path head or the root, staged with S = 0
     double x[CS];
-    if (x0) {  // a piece below the path's first piece: its guessed input (the repair follows)
 #pragma unroll
-        for (int q = 0; q < CS; ++q) x[q] = x0[e0 + q];
-    } else if (hparent != SM_NONE && ready) {
-        // merged launch, consumer: A(parent) is produced by a chain of this same launch; wait for
-        // its readiness word, then read the row at device scope (written through by the producer)
-        wait_ready(ready, hparent, epoch);
-        vm_drain();
-#pragma unroll
-        for (int q = 0; q < CS; ++q)
-            x[q] = __hip_atomic_load(U + (size_t)hparent * Dpad + e0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vm_drain();
-    } else if (hparent != SM_NONE) {
-        global_read_at<CS>(U, hparent, Dpad, e0, x);  // A(parent): finished in an earlier launch
-        vm_drain();
-    } else {
-#pragma unroll
-        for (int q = 0; q < CS; ++q) x[q] = 0.0;  // root: S = 0, T = A_up -> A(root) = A_up(root)
-    }
+    for (int q = 0; q < CS; ++q) x[q] = x0 ? x0[e0 + q] : 0.0;
     const int ngroups = (len + G - 1) / G;
     int st = lds_state(&ring.s[0].staged);  // poll-ahead: the next group's state
     for (int g = 0; g < ngroups; ++g) {
@@ -1173,9 +1151,9 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
 
 template <int SPL>
 __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, int head, int len, int lane,
-                                                 uint32_t hparent, const uint32_t* __restrict__ meta32,
-                                                 const WalkView& V, int Dpad, int dcall, int dglob0, int store_all,
-                                                 uint32_t* ready, uint32_t epoch, uint32_t* done_word) {
+                                                 const uint32_t* __restrict__ meta32, const WalkView& V, int Dpad,
+                                                 int dcall, int dglob0, int store_all, uint32_t epoch,
+                                                 uint32_t* done_word) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
     const int ngroups = (len + G - 1) / G;
     int g = hh;
@@ -1193,20 +1171,34 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
     for (;;) {
         const int n = min(G, len - g * G);
         DownSlot<SPL>& sl = ring.s[g % NS];
+        // ---- stage T = S2 * A_up and S.  A path head (its parent finished in an earlier round)
+        // folds its parent row here: T = fma(S, A(parent), S2 * A_up), staged with S = 0, so the
+        // chain's fma(0, x, T) == T exactly; the root: T = A_up, S = 0.
+        double t[G][SPL], Sk[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const uint32_t par = mfield(mv, k, 1);
+            const uint32_t slot = (uint32_t)(head + g * G + k);
+            const uint32_t wp = lo_wp(mfield(mv, k, 2));
+            const double S = ring.slut[wp], S2 = ring.s2lut[wp];
+            const bool root = par == SM_NONE, phead = !root && par != slot - 1u;
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) t[k][q] = root ? u[k][q] : S2 * u[k][q];
+            Sk[k] = root || phead ? 0.0 : S;
+            if (k < n && phead) {  // uniform; one node per path
+                double ap[SPL];
+                load_row<SPL>(V.A, par, Dpad, lane, ap);
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) t[k][q] = __builtin_fma(S, ap[q], t[k][q]);
+            }
+        }
         if (g >= NS) lds_wait(&sl.freed, g - NS + 1, true);
-        // ---- stage T = S2 * A_up and S (root: T = A_up, S = 0)
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             if (k < n) {
-                const bool root = g * G + k == 0 && hparent == SM_NONE;
-                const uint32_t wp = lo_wp(mfield(mv, k, 2));
-                const double S2 = ring.s2lut[wp];
-                double t[SPL];
-#pragma unroll
-                for (int q = 0; q < SPL; ++q) t[q] = root ? u[k][q] : S2 * u[k][q];
-                lds_row_write<SPL>(sl.x[k], lane, t);
+                lds_row_write<SPL>(sl.x[k], lane, t[k]);
                 if (lane == 0) {
-                    sl.S[k] = root ? 0.0 : ring.slut[wp];
+                    sl.S[k] = Sk[k];
                     sl.pix[k] = mfield(mv, k, 0);
                     sl.st[k] = hi_light(mfield(mv, k, 3));
                 }
@@ -1236,27 +1228,9 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
         double mn;
         int mi;
         wta_chunk<SPL, G>(xs, lane, lane * SPL, dcall, mn, mi);
-        if (ready) {
-            // merged launch, producer: rows that light children (the launch's consumer chains) read
-            // are written through at device scope, then each node's readiness word is published
 #pragma unroll
-            for (int k = 0; k < G; ++k)
-                if (k < n && (store_all || st[k])) {
-                    double* row = V.A + (size_t)(head + g * G + k) * Dpad + lane * SPL;
-#pragma unroll
-                    for (int q = 0; q < SPL; ++q)
-                        __hip_atomic_store(row + q, xs[k][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            vm_drain();  // the rows are at device scope before any readiness word
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-                if (k < n && st[k] && lane == 0)
-                    __hip_atomic_store(ready + head + g * G + k, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-                if (k < n && (store_all || st[k])) store_row<SPL>(V.A, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
-        }
+        for (int k = 0; k < G; ++k)
+            if (k < n && (store_all || st[k])) store_row<SPL>(V.A, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
         if (lane < n) {
             V.idx[pix] = dglob0 + mi;
             V.minc[pix] = mn;
@@ -1532,34 +1506,12 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
                                                             const SmPath* __restrict__ paths1,
                                                             const double* __restrict__ slut_g,
                                                             const double* __restrict__ s2lut_g, int Dpad, int dcall,
-                                                            int dglob0, int store_all, uint32_t* ready0,
-                                                            uint32_t* ready1, uint32_t epoch, int nprod0, int nprod1,
-                                                            PieceView Q0, PieceView Q1) {
+                                                            int dglob0, int store_all, uint32_t epoch, PieceView Q0,
+                                                            PieceView Q1) {
     __shared__ DownRing<SPL> ring;
     __shared__ double guess[64 * SPL];
     __shared__ int hdone;
-    // merged launch (nprod0 + nprod1 > 0, flat grid): per view, paths [0, nprod) produce rows for
-    // the paths after them (their light children's chains), which wait per path for their
-    // parent's readiness word.  Producers of both views take the first block ids, so they are
-    // dispatched before any consumer that waits for them.
-    int view, pidx;
-    const int P = nprod0 + nprod1;
-    if (P > 0) {
-        const int b = blockIdx.x;
-        if (b < P) {
-            view = b < nprod0 ? 0 : 1;
-            pidx = view ? b - nprod0 : b;
-        } else {
-            const int c = b - P, c0 = V0.npaths - nprod0;
-            view = c < c0 ? 0 : 1;
-            pidx = view ? nprod1 + (c - c0) : nprod0 + c;
-        }
-    } else {
-        view = blockIdx.y;
-        pidx = blockIdx.x;
-    }
-    view = (int)uniform((uint32_t)view);
-    pidx = (int)uniform((uint32_t)pidx);
+    const int view = blockIdx.y, pidx = blockIdx.x;
     // field-wise selects (a reference to one of two by-value arguments would go to scratch)
     WalkView V;
     V.npaths = view ? V1.npaths : V0.npaths;
@@ -1578,9 +1530,9 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     Q.plen = Q0.plen;
     Q.rmax = Q0.rmax;
     Q.dbg = Q0.dbg;
-    // pieces: block e = piece i of M of its path, pieces top first (entries list a path's pieces
-    // bottom first with index j: i = M - 1 - j)
-    uint4 pc = make_uint4((uint32_t)pidx, 0u, 1u, 0u);
+    // work item: piece i of M of a cut path (entries list a path's pieces bottom first with index
+    // j: i = M - 1 - j, pieces top first), or a run of w whole paths (M == 1)
+    uint4 pc = make_uint4((uint32_t)pidx, 0u, 1u, 1u);
     if (Q.pieces) {
         if (pidx >= Q.npieces) return;  // uniform over the block
         pc = Q.pieces[pidx];
@@ -1588,16 +1540,16 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
         return;
     }
     const int M = (int)uniform(pc.z), i = M - 1 - (int)uniform(pc.y);
-    const int nprod = view ? nprod1 : nprod0;
-    uint32_t* ready = nprod > 0 ? (view ? ready1 : ready0) : nullptr;
-    uint32_t* prod_ready = pidx < nprod ? ready : nullptr;
-    const uint32_t* cons_ready = pidx >= nprod ? ready : nullptr;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
-    const SmPath path = (view ? paths1 : paths0)[uniform(pc.x)];
-    const int plen = (int)uniform(path.len);
+    const SmPath* __restrict__ pp = view ? paths1 : paths0;
+    const SmPath path = pp[uniform(pc.x)];
+    int plen = (int)uniform(path.len);
+    if (M == 1) {  // a run: slots of consecutive paths are contiguous
+        const SmPath last = pp[uniform(pc.x + pc.w - 1u)];
+        plen = (int)uniform(last.head + last.len - path.head);
+    }
     const int o0 = i * Q.plen, o1 = i + 1 == M ? plen : (i + 1) * Q.plen;
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
-    const uint32_t hparent = uniform(meta32[(size_t)head * 8 + 1]);
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (int k = threadIdx.x; k < SM_NUM_W; k += CHN_THREADS) {
         ring.slut[k] = slut_g[k];
@@ -1637,12 +1589,12 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     if (threadIdx.x == 0) hdone = 0;
     __syncthreads();
     if (wave < Split<SPL>::NCW) {
-        down_chain_wave<SPL>(ring, wave, len, lane, V.A, hparent, Dpad, cons_ready, epoch, i > 0 ? guess : nullptr);
+        down_chain_wave<SPL>(ring, wave, len, lane, i > 0 ? guess : nullptr);
         if (wave == 0 && M > 1)
             down_finish<SPL>(ring, &hdone, meta32, V, Dpad, dcall, dglob0, store_all, lane, head, len, i, M, pidx, Q, epoch);
     } else if (Split<SPL>::helper_of(wave) >= 0) {
-        down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, hparent, meta32, V, Dpad, dcall, dglob0,
-                              store_all, prod_ready, epoch, (M > 1 && i + 1 < M) ? Q.stat + pidx : nullptr);
+        down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V, Dpad, dcall, dglob0, store_all,
+                              epoch, (M > 1 && i + 1 < M) ? Q.stat + pidx : nullptr);
         vm_drain();  // this helper's stores are complete before the repair overwrites them
         if (lane == 0) atomicAdd(&hdone, 1);
     }
@@ -1681,15 +1633,13 @@ static void up_chain_launch(hipStream_t st, const WalkArgs& a, int np) {
 
 template <int SPL>
 static void down_chain_launch(hipStream_t st, const WalkArgs& a, int np, int store_all) {
-    const bool merged = a.nprod[0] + a.nprod[1] > 0;
-    const dim3 grid = merged ? dim3(a.npaths[0] + a.npaths[1], 1) : dim3(np, 2);
+    const dim3 grid(np, 2);
     PieceView q0 = piece_view(a, 0), q1 = piece_view(a, 1);
     for (PieceView* q : {&q0, &q1})  // the down pass's status words: arrays 3..6 (up: 0..2)
         if (q->stat) q->stat += 3 * (size_t)q->stride;
     hipLaunchKernelGGL((k_down_chain<SPL>), grid, dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all, a.ready[0],
-                       a.ready[1], a.epoch, a.nprod[0], a.nprod[1], q0, q1);
+                       a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all, a.epoch, q0, q1);
 }
 
 hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {

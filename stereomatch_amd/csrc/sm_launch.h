@@ -51,12 +51,7 @@ struct WalkArgs {
     const uint2* segtab[2];  // long buckets: {path, segment} per SM_PRE_SEG-node segment
     int nseg[2];
     int W, Dpad, dcall, dglob0;
-    // merged chain launches (a round's chains with the next round's, dataflow through readiness
-    // words): ready[v][slot] == epoch once the row of slot is final; nprod[v] = producer paths
-    // at the start of the launch's path range (0: not a merged launch)
-    uint32_t* ready[2];
-    uint32_t epoch;
-    int nprod[2];
+    uint32_t epoch;       // filter call counter (status words hold it)
     // long-path pieces of the current long bucket (sm_chain.hip "Pieces"); pieces[v] == nullptr:
     // one workgroup per path, no pieces
     const uint4* pieces[2];

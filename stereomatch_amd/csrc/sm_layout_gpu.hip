@@ -608,13 +608,18 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
 }
 
 // segment table of the long-path buckets: segment i of bucket b -> {path within b, SM_PRE_SEG-node
-// segment of that path}, so k_up_pre launches exactly one block per segment; and the piece table:
-// a path of len >= 2*plen nodes has M = len / plen pieces, listed bottom piece first (the
-// chain launches wait only on lower entries), every other long path is one piece.  One block per
-// view.
+// segment of that path}, so k_up_pre launches exactly one block per segment; and the chain work
+// items of the bucket ("pieces"):
+//  * a path of len >= 2*plen nodes gives M = len / plen pieces {path, j, M, first segment of the
+//    path}, listed bottom piece first (the chain launches wait only on lower entries);
+//  * the other paths are packed into runs of consecutive paths (one contiguous slot range): a
+//    path starts a new run when its bucket slot offset enters a new window of rwin nodes (or
+//    after a cut path) -> item {first path, 0, 1, number of paths}.
+// One block per view.
 __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t plen) {
     const LayoutView& V = LP.v[blockIdx.x];
     __shared__ uint32_t sc[1024], sp[1024];
+    __shared__ uint32_t prev_win, prev_cut;
     uint32_t running = 0, prun = 0;
     for (int b = 0; b < SM_NBUCKETS; ++b) {
         if (threadIdx.x == 0) {
@@ -624,14 +629,35 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
         if (b & 1) continue;  // short buckets have no segments
         const uint32_t p0 = V.round_begin[b], p1 = V.round_begin[b + 1];
         const uint32_t sbase = running;  // the bucket's first segment
+        const uint32_t hbase = p0 < p1 ? V.paths[p0].head : 0u;
+        // run window: ~3 runs per CU over both views (256 CUs), 64 .. plen nodes
+        const uint32_t rwin = min(plen, max(64u, V.round_nodes[b] / 384u));
+        if (threadIdx.x == 0) {
+            prev_win = 0xFFFFFFFFu;
+            prev_cut = 1u;
+        }
+        __syncthreads();
         for (uint32_t c = p0; c < p1; c += 1024) {
             const uint32_t p = c + threadIdx.x;
-            const uint32_t len = p < p1 ? V.paths[p].len : 0u;
+            const SmPath path = p < p1 ? V.paths[p] : SmPath{0u, 0u};
+            const uint32_t len = path.len;
             const uint32_t ns = (len + SM_PRE_SEG - 1) / SM_PRE_SEG;
-            const uint32_t np = p < p1 ? (len >= 2u * plen ? len / plen : 1u) : 0u;
+            const bool cut = len >= 2u * plen;
+            const uint32_t win = (path.head - hbase) / rwin;
+            // previous path's window / cut flag (the chunk's first thread: from the last chunk)
+            sp[threadIdx.x] = (win << 1) | (cut ? 1u : 0u);
+            __syncthreads();
+            const uint32_t pv = threadIdx.x ? sp[threadIdx.x - 1] : ((prev_win << 1) | prev_cut);
+            __syncthreads();
+            const bool start = !cut && ((pv & 1u) || (pv >> 1) != win);
+            const uint32_t np = p < p1 ? (cut ? len / plen : (start ? 1u : 0u)) : 0u;
             sc[threadIdx.x] = ns;
             sp[threadIdx.x] = np;
             __syncthreads();
+            if (threadIdx.x == 1023) {
+                prev_win = win;
+                prev_cut = cut ? 1u : 0u;
+            }
             for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scans
                 const uint32_t t = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0u;
                 const uint32_t u = threadIdx.x >= (unsigned)off ? sp[threadIdx.x - off] : 0u;
@@ -640,12 +666,20 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
                 sp[threadIdx.x] += u;
                 __syncthreads();
             }
-            const uint32_t start = running + sc[threadIdx.x] - ns;
-            for (uint32_t q = 0; q < ns; ++q) V.segtab[start + q] = make_uint2(p - p0, q);
+            const uint32_t start_seg = running + sc[threadIdx.x] - ns;
+            for (uint32_t q = 0; q < ns; ++q) V.segtab[start_seg + q] = make_uint2(p - p0, q);
             const uint32_t pstart = prun + sp[threadIdx.x] - np;
-            for (uint32_t i = 0; i < np; ++i) V.pieces[pstart + i] = make_uint4(p - p0, np - 1u - i, np, start - sbase);
+            if (cut) {
+                for (uint32_t i = 0; i < np; ++i) V.pieces[pstart + i] = make_uint4(p - p0, np - 1u - i, np, start_seg - sbase);
+            } else if (start) {
+                V.pieces[pstart] = make_uint4(p - p0, 0u, 1u, 0u);
+            }
             running += sc[1023];
             prun += sp[1023];
+            __syncthreads();
+            // count the paths of each run: every uncut path adds itself to the run it belongs to
+            // (the latest item, which is a run start since this path is not cut)
+            if (p < p1 && !cut) atomicAdd(reinterpret_cast<uint32_t*>(V.pieces + (prun - sp[1023] + sp[threadIdx.x] - 1u)) + 3, 1u);
             __syncthreads();
         }
     }
