@@ -36,6 +36,13 @@ struct DevBuf {
     size_t n = 0;
 };
 
+struct MstPending {
+    bool active = false;
+    int nviews = 0, r = 0;  // contracted rounds enqueued
+    MstArgs a{};
+    MstCompact c{};
+};
+
 }  // namespace
 
 struct sm_ctx {
@@ -49,7 +56,7 @@ struct sm_ctx {
     std::string err;
     int W = 0, H = 0, stride = 0;
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
-    DevBuf changed, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
+    DevBuf changed, mst_ok, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
     DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
     uint32_t epoch = 0;      // bumped per filter call; status words are zeroed only on (re)allocation
@@ -60,18 +67,22 @@ struct sm_ctx {
     DevBuf pieces[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
     DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
-    int mst_rounds = 12;  // contracted Boruvka rounds the previous frame enqueued
+    int mst_rounds = 12;  // contracted Boruvka rounds the previous frame needed
+    MstPending mst_pend;  // rounds enqueued without a host check (stage_mst -> mst_finish)
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
     struct HostRounds {
         uint32_t nrounds = 0, npaths = 0, n_has_light = 0;
         std::vector<uint32_t> begin, maxlen, seg_begin, nodes, piece_begin;  // per bucket
     } layout[2];
     hipEvent_t ev[8] = {};
-    // tree-filter launch timing: launch k is bracketed by events fev[2k], fev[2k+1] on its stream
+    // tree-filter launch timing: timed launch k runs between events fev[fam_ev[k]] on its stream
     std::vector<hipEvent_t> fev;
     std::vector<int> fam;
     std::vector<double> fam_vox;  // voxels of launch k
+    std::vector<std::pair<int, int>> fam_ev;  // its start / end event
     int nfev = 0;
+    bool ev_open = false;  // the last op on ev_stream was a timed launch's end event
+    hipStream_t ev_stream = nullptr;
     std::vector<hipEvent_t> sev;  // stream-ordering events of the filter rounds
     int nsev = 0;
     sm_filter_stats stats{};
@@ -195,6 +206,7 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
         a.mD[v] = P<uint8_t>(ctx->mD[v]);
     }
     CHECK(ensure(ctx, ctx->changed, 2 * SM_MST_MAX_ROUNDS * sizeof(int)));
+    CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
     HIPC(hipMemsetAsync(ctx->changed.p, 0, 2 * SM_MST_MAX_ROUNDS * sizeof(int), ctx->st));
     a.flags[0] = P<int>(ctx->changed);
     a.flags[1] = P<int>(ctx->changed) + SM_MST_MAX_ROUNDS;
@@ -214,6 +226,8 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
                 if (ctx->h_changed[0] == 0 && (nviews < 2 || ctx->h_changed[1] == 0)) break;
             }
         }
+        HIPC(hipMemsetAsync(ctx->mst_ok.p, 1, sizeof(int), ctx->st));  // checked on the host above
+        ctx->mst_pend.active = false;
         return SM_OK;
     }
     // contracted rounds on the component graph left by the tile phase
@@ -234,30 +248,49 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     }
     HIPC(launch_bor_compact(ctx->st, a, c, W, H));
     HIPC(launch_bor_cinit(ctx->st, a, c));
-    // Enqueue as many rounds as the previous frame needed (the last one hooks nothing), then
-    // check once: every kernel of round r exits at once when round r-1 hooked nothing.
+    // Enqueue the rounds the previous frame needed (the last of them hooked nothing) and the copy
+    // of the hook flags, without waiting: the layout is enqueued behind them and the flags are
+    // checked after the layout's own synchronisation (mst_finish).  Every kernel of round r exits
+    // at once when round r-1 hooked nothing.
+    const int first = std::min(std::max(ctx->mst_rounds, 2), SM_MST_MAX_ROUNDS);
     static const bool dbg = getenv("SM_MST_DEBUG") != nullptr;
-    int r = 0, batch = std::max(ctx->mst_rounds, 2);
-    for (;;) {
-        const int end = std::min(r + batch, SM_MST_MAX_ROUNDS);
-        for (; r < end; ++r) {
-            HIPC(launch_bor_cround(ctx->st, a, c, W, r));
-            if (dbg) {
-                uint32_t h[4];
-                HIPC(hipMemcpyAsync(h, c.counts[0], 16, hipMemcpyDeviceToHost, ctx->st));
-                HIPC(hipStreamSynchronize(ctx->st));
-                fprintf(stderr, "mst round %d: K %u live edges %u / %u\n", r, h[0], h[1], h[2]);
-            }
+    int r = 0;
+    for (; r < first; ++r) {
+        HIPC(launch_bor_cround(ctx->st, a, c, W, r));
+        if (dbg) {
+            uint32_t h[4];
+            HIPC(hipMemcpyAsync(h, c.counts[0], 16, hipMemcpyDeviceToHost, ctx->st));
+            HIPC(hipStreamSynchronize(ctx->st));
+            fprintf(stderr, "mst round %d: K %u live edges %u / %u\n", r, h[0], h[1], h[2]);
         }
-        int* hf = ctx->h_changed;  // [view][round] hook flags
-        HIPC(hipMemcpyAsync(hf, ctx->changed.p, 2 * SM_MST_MAX_ROUNDS * sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-        HIPC(hipStreamSynchronize(ctx->st));
-        if (!hooked_any(hf, nviews, r - 1) || r >= SM_MST_MAX_ROUNDS) break;
-        batch = 4;
     }
+    HIPC(launch_mst_done(ctx->st, a, r - 1, P<int>(ctx->mst_ok)));
+    HIPC(hipMemcpyAsync(ctx->h_changed, ctx->changed.p, 2 * SM_MST_MAX_ROUNDS * sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+    ctx->mst_pend = MstPending{true, nviews, r, a, c};
+    return SM_OK;
+}
+
+// After a synchronisation that covers stage_mst's flag copy: if the last enqueued round still
+// hooked an edge, run more rounds (synchronously) and report that the MST grew (the layout built
+// on the incomplete forest must then be redone).  Records the rounds needed for the next frame.
+sm_status mst_finish(sm_ctx* ctx, bool* grew) {
+    *grew = false;
+    MstPending& m = ctx->mst_pend;
+    if (!m.active) return SM_OK;
+    m.active = false;
+    int r = m.r;
+    while (hooked_any(ctx->h_changed, m.nviews, r - 1) && r < SM_MST_MAX_ROUNDS) {
+        *grew = true;
+        const int end = std::min(r + 4, SM_MST_MAX_ROUNDS);
+        for (; r < end; ++r) HIPC(launch_bor_cround(ctx->st, m.a, m.c, ctx->W, r));
+        HIPC(hipMemcpyAsync(ctx->h_changed, ctx->changed.p, 2 * SM_MST_MAX_ROUNDS * sizeof(int), hipMemcpyDeviceToHost,
+                            ctx->st));
+        HIPC(hipStreamSynchronize(ctx->st));
+    }
+    if (*grew) HIPC(launch_mst_done(ctx->st, m.a, r - 1, P<int>(ctx->mst_ok)));
     // rounds needed: through the first one that hooked nothing in any view
     int need = 1;
-    while (need < r && hooked_any(ctx->h_changed, nviews, need - 1)) ++need;
+    while (need < r && hooked_any(ctx->h_changed, m.nviews, need - 1)) ++need;
     ctx->mst_rounds = need;
     return SM_OK;
 }
@@ -367,11 +400,15 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.pieces = P<uint4>(ctx->pieces[v]);
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
+    LP.mst_ok = P<int>(ctx->mst_ok);
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains, (uint32_t)piece_len()));
     // the host needs the per-round path counts to size the walker grids
     for (int v = 0; v < nviews; ++v)
         HIPC(hipMemcpyAsync(ctx->h_rounds + v * RREC, ctx->rounds[v].p, RREC * 4, hipMemcpyDeviceToHost, ctx->st));
     HIPC(hipStreamSynchronize(ctx->st));
+    bool grew = false;
+    CHECK(mst_finish(ctx, &grew));
+    if (grew) return stage_layout(ctx, nviews);  // the forest was incomplete: lay out the final MST
     for (int v = 0; v < 2; ++v) {
         auto& L = ctx->layout[v];
         if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); L.nodes.assign(SM_NBUCKETS, 0); L.piece_begin.assign(SM_NBUCKETS + 1, 0); continue; }
@@ -465,16 +502,38 @@ enum { KF_UP_WALK, KF_UP_PRE, KF_UP_CHAIN, KF_DOWN_CHAIN, KF_DOWN_WALK, KF_N };
 const char* const kf_name[KF_N] = {"k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk"};
 const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0};
 
-// a timed launch of family f on stream s: events before and after (per-family HIP-event time)
+// A timed launch of family f on stream s.  HIP events bracket the launch, but consecutive timed
+// launches on the filter stream share the event between them (the end of one is the start of
+// the next), and launches too small to matter (< SM_TIMED_MIN_VOX voxels, the deep rounds where
+// the host's issue rate, not the GPU, sets the pace) run without events: each event record costs
+// the host ~3 us, and bracketing every launch with two of them added ~0.45 ms per C2 frame.
+// Untimed launches are left out of the per-family stats (bytes and time alike).
+#define SM_TIMED_MIN_VOX 4.0e6
 template <class F>
 sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch) {
+    static const bool off = getenv("SM_NO_KTIMING") != nullptr;  // A/B: no events at all
+    if (vox <= 0) return SM_OK;                                   // empty bucket: nothing to launch
+    if (off || vox < SM_TIMED_MIN_VOX) {
+        HIPC(launch());
+        ctx->ev_open = false;
+        return SM_OK;
+    }
     CHECK(ensure_events(ctx, ctx->fev, (size_t)ctx->nfev + 2));
-    HIPC(hipEventRecord(ctx->fev[ctx->nfev], s));
+    int start;
+    if (ctx->ev_open && s == ctx->ev_stream) {
+        start = ctx->nfev - 1;  // the previous timed launch's end event
+    } else {
+        start = ctx->nfev;
+        HIPC(hipEventRecord(ctx->fev[ctx->nfev++], s));
+    }
     HIPC(launch());
-    HIPC(hipEventRecord(ctx->fev[ctx->nfev + 1], s));
+    HIPC(hipEventRecord(ctx->fev[ctx->nfev], s));
     ctx->fam.push_back(f);
     ctx->fam_vox.push_back(vox);
-    ctx->nfev += 2;
+    ctx->fam_ev.push_back(std::make_pair(start, ctx->nfev));
+    ctx->nfev += 1;
+    ctx->ev_open = true;
+    ctx->ev_stream = s;
     return SM_OK;
 }
 
@@ -595,7 +654,12 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     ctx->nfev = ctx->nsev = 0;
     ctx->fam.clear();
     ctx->fam_vox.clear();
+    ctx->fam_ev.clear();
+    ctx->ev_open = false;
     for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest first
+    CHECK(join(ctx, ctx->st, ctx->st2));
+    HIPC(hipEventRecord(ctx->ev[6], ctx->st));  // up | down boundary (stage times)
+    ctx->ev_open = false;
     for (uint32_t r = 0; r < nr; ++r) CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all));
     CHECK(join(ctx, ctx->st, ctx->st2));  // everything after the filter runs on st
     if (a.piece_dbg) {
@@ -619,7 +683,7 @@ sm_status collect_filter_stats(sm_ctx* ctx) {
     }
     for (size_t k = 0; k < ctx->fam.size(); ++k) {
         float ms;
-        HIPC(hipEventElapsedTime(&ms, ctx->fev[2 * k], ctx->fev[2 * k + 1]));
+        HIPC(hipEventElapsedTime(&ms, ctx->fev[ctx->fam_ev[k].first], ctx->fev[ctx->fam_ev[k].second]));
         const int f = ctx->fam[k];
         if (ctx->fam_vox[k] > 0) ks[f].launches += 1;  // a bucket without paths launches nothing
         ks[f].ms += ms;
@@ -754,7 +818,7 @@ void sm_destroy(sm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
-    DevBuf* all[] = {&ctx->changed, &ctx->atab, &ctx->slut, &ctx->s2lut};
+    DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut};
     for (DevBuf* b : all) if (b->p) (void)hipFree(b->p);
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
@@ -824,8 +888,9 @@ sm_status sm_synchronize(sm_ctx* ctx) {
     ctx->stage_ms[1] = t[1];
     ctx->stage_ms[2] = t[2];
     CHECK(collect_filter_stats(ctx));
-    ctx->stage_ms[3] = (float)ctx->stats.up_ms;
-    ctx->stage_ms[4] = (float)ctx->stats.down_ms;
+    // up / down pass wall time (events at the filter's start, the pass boundary and its end)
+    HIPC(hipEventElapsedTime(&ctx->stage_ms[3], ctx->ev[3], ctx->ev[6]));
+    HIPC(hipEventElapsedTime(&ctx->stage_ms[4], ctx->ev[6], ctx->ev[4]));
     ctx->stage_ms[5] = t[4];
     float tot;
     HIPC(hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[5]));
@@ -926,6 +991,8 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
         ctx->nfev = ctx->nsev = 0;
         ctx->fam.clear();
         ctx->fam_vox.clear();
+        ctx->fam_ev.clear();
+        ctx->ev_open = false;
         for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl_for(D), 2));
         CHECK(join(ctx, ctx->st, ctx->st2));
         HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,

@@ -732,6 +732,17 @@ hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int 
     return hipGetLastError();
 }
 
+// MST completeness word read by every layout kernel: the last enqueued contracted round r hooked
+// nothing in any view (stage_mst enqueues rounds without a host check)
+__global__ void k_mst_done(const int* __restrict__ f0, const int* __restrict__ f1, int r, int nviews, int* ok) {
+    if (threadIdx.x == 0) *ok = (f0[r] == 0 && (nviews < 2 || f1[r] == 0)) ? 1 : 0;
+}
+
+hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok) {
+    hipLaunchKernelGGL(k_mst_done, dim3(1), dim3(64), 0, st, a.flags[0], a.flags[1], r, a.nviews, ok);
+    return hipGetLastError();
+}
+
 hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N) {
     hipLaunchKernelGGL(k_cand, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, minc, gmin, idx, cand, N);
     return hipGetLastError();

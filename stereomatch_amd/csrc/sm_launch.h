@@ -76,6 +76,7 @@ hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int 
 hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int H);
 hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c);
 hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r);
+hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok);
 hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);

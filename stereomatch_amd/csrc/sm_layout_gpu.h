@@ -73,6 +73,7 @@ struct LayoutView {
 
 struct LayoutPair {
     LayoutView v[2];
+    const int* mst_ok;  // != 0 once the MST is complete (k_mst_done); every layout kernel checks it
 };
 
 hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains,

@@ -52,6 +52,7 @@ __device__ __forceinline__ uint64_t key_dir(const uint16_t* wR, const uint16_t* 
 
 // ------------------------------------------------------------------------------------------
 __global__ void k_adj(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -83,6 +84,7 @@ __device__ __forceinline__ uint32_t succ_arc(const uint8_t* adj, int W, uint32_t
 
 // L1: contract the tour inside each 32x32 tile.
 __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     __shared__ uint16_t nxt[TLS];
     __shared__ uint16_t dist[TLS];
@@ -190,6 +192,7 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
 
 // L2 init: chain successor + weight (suffix-sum Wyllie state)
 __global__ void k_chain_init(LayoutPair LP, int W) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= *V.nchains) return;
@@ -201,6 +204,7 @@ __global__ void k_chain_init(LayoutPair LP, int W) {
 
 // L2 step: ping-pong pointer jumping
 __global__ void k_chain_jump(LayoutPair LP, int parity) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= *V.nchains) return;
@@ -220,6 +224,7 @@ __global__ void k_chain_jump(LayoutPair LP, int parity) {
 
 // L3: arc ranks.  suffix(c) = arcs from chain c's head to the tour end; rank = total - suffix + offset
 __global__ void k_tour_rank(LayoutPair LP, int W, int H, int parity) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -238,6 +243,7 @@ __global__ void k_tour_rank(LayoutPair LP, int W, int H, int parity) {
 
 // orientation + subtree size
 __global__ void k_orient(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -262,6 +268,7 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
 
 // heavy child + per-child preorder offset and light flag (written by the parent into the child)
 __global__ void k_heavy(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -295,6 +302,7 @@ __global__ void k_heavy(LayoutPair LP, int W, int H) {
 
 // tour values: down arc into c: +(light<<32 | off), up arc out of c: -(...)
 __global__ void k_tour_values(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -422,6 +430,7 @@ static void launch_scan(hipStream_t st, const ScanBufs<T>& B, int nviews, int ne
 
 // preorder + light depth per pixel from the scanned tour
 __global__ void k_assign(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -441,6 +450,7 @@ __global__ void k_assign(LayoutPair LP, int W, int H) {
 
 // path heads in preorder numbering: headflag[pre] = 0 (not a head) or 1 + light depth
 __global__ void k_heads(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
@@ -453,6 +463,7 @@ __global__ void k_heads(LayoutPair LP, int W, int H) {
 // contiguous slot range, each path contiguous from its head (= preorder contiguity of heavy
 // paths), in paths[] order.  plen holds the inclusive scan of the lengths: end slot of a path.
 __global__ void k_newslot(LayoutPair LP, int N) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= (uint32_t)N) return;
@@ -467,6 +478,7 @@ __global__ void k_newslot(LayoutPair LP, int N) {
 // per-slot metadata in slot numbering: pixel, parent slot, child weights and slots in
 // descending (w,a,b) key order (the reference's fold order), heavy-child position, light flag
 __global__ void k_meta(LayoutPair LP, int W, int H) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x0 = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = x0 < W;
@@ -524,6 +536,7 @@ __global__ void k_meta(LayoutPair LP, int W, int H) {
 #define PATH_ITEMS 8   // slots per thread -> 8192 per block (few global atomics per round bin)
 
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_prep(LayoutPair LP, int N) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
     for (int i = 0; i < PATH_ITEMS; ++i) {
@@ -536,6 +549,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_prep(LayoutPair LP, int N) 
 
 // after the max-scan: count paths per (round, long/short) bucket at their last slot
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     __shared__ uint32_t hist[SM_NBUCKETS], nodes[SM_NBUCKETS];
     if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = nodes[threadIdx.x] = 0;
@@ -561,6 +575,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N)
 }
 
 __global__ void k_path_offsets(LayoutPair LP) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.x];
     if (threadIdx.x != 0) return;
     uint32_t acc = 0, nr = 0;
@@ -575,6 +590,7 @@ __global__ void k_path_offsets(LayoutPair LP) {
 }
 
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     __shared__ uint32_t hist[SM_NBUCKETS], gbase[SM_NBUCKETS];
     if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = 0;
@@ -617,6 +633,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
 //    after a cut path) -> item {first path, 0, 1, number of paths}.
 // One block per view.
 __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t plen) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.x];
     __shared__ uint32_t sc[1024], sp[1024];
     __shared__ uint32_t prev_win, prev_cut;
