@@ -154,7 +154,11 @@ def main():
     if os.path.exists(tf):
         try:
             with open(tf) as f:
-                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+                fam = json.load(f).get(dom, {})
+            # PMC HBM bytes of the family per frame over the launches timed here (an empty bucket
+            # launches nothing, so both count the same launches)
+            if fam.get("hbm_bytes_per_frame") and d["launches"]:
+                traffic = fam["hbm_bytes_per_frame"] / (d["launches"] / args.steps)
         except Exception:
             traffic = None
     line = {

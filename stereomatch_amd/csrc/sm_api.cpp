@@ -504,11 +504,14 @@ const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0};
 
 // A timed launch of family f on stream s.  HIP events bracket the launch, but consecutive timed
 // launches on the filter stream share the event between them (the end of one is the start of
-// the next), and launches too small to matter (< SM_TIMED_MIN_VOX voxels, the deep rounds where
-// the host's issue rate, not the GPU, sets the pace) run without events: each event record costs
-// the host ~3 us, and bracketing every launch with two of them added ~0.45 ms per C2 frame.
-// Untimed launches are left out of the per-family stats (bytes and time alike).
-#define SM_TIMED_MIN_VOX 4.0e6
+// the next, so a launch's time includes the dispatch gap before it); empty buckets launch
+// nothing and record nothing.  Each event record costs the host ~3 us and the deep rounds are
+// host-bound: two events per launch added ~0.45 ms per C2 frame, one adds ~0.15 ms.  Launches
+// below SM_TIMED_MIN_VOX voxels may be left untimed (and out of the per-family stats); 0 keeps
+// every launch timed so rocprof's per-kernel averages compare launch for launch.
+#ifndef SM_TIMED_MIN_VOX
+#define SM_TIMED_MIN_VOX 0.0
+#endif
 template <class F>
 sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch) {
     static const bool off = getenv("SM_NO_KTIMING") != nullptr;  // A/B: no events at all
