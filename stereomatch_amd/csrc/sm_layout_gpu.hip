@@ -637,6 +637,15 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
     const LayoutView& V = LP.v[blockIdx.x];
     __shared__ uint32_t sc[1024], sp[1024];
     __shared__ uint32_t prev_win, prev_cut;
+    // the bucket tables and each long bucket's first head, loaded once (a dependent global load
+    // per bucket made this single-block kernel latency-bound: 89 us at C2)
+    __shared__ uint32_t rb[SM_NBUCKETS + 1], rn[SM_NBUCKETS], hb[SM_NBUCKETS];
+    if (threadIdx.x <= SM_NBUCKETS) rb[threadIdx.x] = V.round_begin[threadIdx.x];
+    if (threadIdx.x < SM_NBUCKETS) rn[threadIdx.x] = V.round_nodes[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x < SM_NBUCKETS)
+        hb[threadIdx.x] = rb[threadIdx.x] < rb[threadIdx.x + 1] ? V.paths[rb[threadIdx.x]].head : 0u;
+    __syncthreads();
     uint32_t running = 0, prun = 0;
     for (int b = 0; b < SM_NBUCKETS; ++b) {
         if (threadIdx.x == 0) {
@@ -644,11 +653,12 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
             V.piece_begin[b] = prun;
         }
         if (b & 1) continue;  // short buckets have no segments
-        const uint32_t p0 = V.round_begin[b], p1 = V.round_begin[b + 1];
+        const uint32_t p0 = rb[b], p1 = rb[b + 1];
+        if (p0 == p1) continue;  // uniform
         const uint32_t sbase = running;  // the bucket's first segment
-        const uint32_t hbase = p0 < p1 ? V.paths[p0].head : 0u;
+        const uint32_t hbase = hb[b];
         // run window: ~3 runs per CU over both views (256 CUs), 64 .. plen nodes
-        const uint32_t rwin = min(plen, max(64u, V.round_nodes[b] / 384u));
+        const uint32_t rwin = min(plen, max(64u, rn[b] / 384u));
         if (threadIdx.x == 0) {
             prev_win = 0xFFFFFFFFu;
             prev_cut = 1u;

@@ -177,6 +177,18 @@ __device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, 
 }
 
 
+// column of pixel index pix: a float estimate of pix / W is off by at most one while pix < 2^24
+// (exact in float; W <= 2 exact, W >= 3: |error| <= 2^24/W * 2^-22 < 1), fixed with one compare
+// each way -- an integer division costs ~25 VALU per node.  Larger images take the division.
+__device__ __forceinline__ int pix_col(int pix, int W) {
+    if (pix >= (1 << 24)) return pix % W;
+    const int y = (int)((float)pix * __builtin_amdgcn_rcpf((float)W));
+    int x = pix - y * W;
+    x = x < 0 ? x + W : x;
+    x = x >= W ? x - W : x;
+    return x;
+}
+
 // image records of CH path nodes: own(x), own(x+1) (one lane-dependent load: lanes 2m / 2m+1 hold
 // x / x+1) and the SPL+1 matched-image records a lane needs.  All loads are unconditional (rows of
 // absent nodes are clamped to the last valid one) and nothing reads the loaded values here, so a
@@ -192,14 +204,11 @@ __device__ __forceinline__ void load_recs(const MetaVec<CH>& mv, int n, int view
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const int jj = j < n ? j : n - 1;
-        const int pix = (int)mfield(mv, jj, 0);
-        const int y = pix / W;
-        const int x = pix - y * W;
-        const size_t row = (size_t)y * W;
+        const long long pix = (long long)mfield(mv, jj, 0);  // = y*W + x: no division needed here
         // own pixels x, x+1 through a lane-dependent (vector) load: a uniform address would become
         // a scalar-cache load whose lgkmcnt waits serialise with the LDS table reads
-        r.own[j] = own[row + x + (lane & 1)];  // x+1 == W reads the next row / the pad: masked below
-        const long long base = view ? (long long)(row + x) + dbase : (long long)(row + x) - dbase - (SPL - 1);
+        r.own[j] = own[pix + (lane & 1)];  // x+1 == W reads the next row / the pad: masked below
+        const long long base = view ? pix + dbase : pix - dbase - (SPL - 1);
 #pragma unroll
         for (int q = 0; q <= SPL; ++q) r.ob[j][q] = oth[base + q];
     }
@@ -212,9 +221,7 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
                                             const ImgRecs<SPL, CH>& r, const float* __restrict__ atab, T (&c)[CH][SPL]) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-        const int pix = (int)mfield(mv, j, 0);
-        const int y = pix / W;
-        const int x = pix - y * W;
+        const int x = pix_col((int)mfield(mv, j, 0), W);
         const uint2 o0 = make_uint2(__builtin_amdgcn_readlane(r.own[j].x, 0), __builtin_amdgcn_readlane(r.own[j].y, 0));
         const uint2 o1 = make_uint2(__builtin_amdgcn_readlane(r.own[j].x, 1), __builtin_amdgcn_readlane(r.own[j].y, 1));
 #pragma unroll
