@@ -12,6 +12,7 @@
  *                           (include/Stereo3DMST.h:7), per-slice restatement of the
  *                           MST_PMS label search
  *   sm_cost_volume      <- buildCostVolumeSharedMemoryBGR         src/PatchMatchStereoGPU.cu:1482-1550
+ *   sm_upload_cost_volumes <- MC-CNN volume mmap + clamp          src/Stereo3DMST.cpp:764-803
  *   sm_build_tree       <- segment_image_other_init (MST mode)    src/Stereo3DMST.cpp:213-543
  *                           + segment_graph/universe              include/segment-graph.h:54-89
  *   sm_aggregate_debug  <- aggregateCostFromChildren/Parent       src/Stereo3DMST.cpp:120-158
@@ -105,6 +106,15 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p);
 sm_status sm_synchronize(sm_ctx* ctx);
 sm_status sm_download_results(sm_ctx* ctx, float* left_disp, float* right_disp, int32_t* left_idx,
                               int32_t* right_idx, double* left_min, double* right_min);
+
+/* MC-CNN ingest (SM_COST_VOLUME): the raw matching-cost volumes stereo3dmst mmaps from
+ * mc-cnn-master/{left,right}.bin (src/Stereo3DMST.cpp:764-775), [D][H][W] float per view, host
+ * buffers.  Copied to the device (synchronously: the caller may free them on return); every
+ * following sm_match / sm_match_async with p->cost_kind == SM_COST_VOLUME on images of the same
+ * W x H filters slices [p->disp_begin, p->disp_begin + D) of them after the reference's clamp,
+ * NaN -> 0.5 else min(0.5, x) (:785-803), instead of the AGD cost.  The tree still comes from
+ * the images. */
+sm_status sm_upload_cost_volumes(sm_ctx* ctx, const float* left_vol, const float* right_vol, int W, int H, int D);
 
 /* Stage entry points (parity tests, MC-CNN ingest) --------------------------- */
 /* AGD cost volumes [D][H][W] float for slices [d0, d0+D); host output buffers. */

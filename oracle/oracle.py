@@ -137,6 +137,13 @@ def tree_filter(W, H, tree, vol, d0=0, want_idx=True, want_volumes=False, nthrea
     return dict(idx=idx, minc=minc, Aup=Aup, A=A)
 
 
+def mccnn_clamp(vol):
+    """MC-CNN ingest clamp of Stereo3DMST.cpp:785-803: NaN -> 0.5, else min(0.5f, x)
+    (std::min(a, b) returns b only if b < a)."""
+    v = np.asarray(vol, dtype=np.float32)
+    return np.where(np.isnan(v), np.float32(0.5), np.where(v < np.float32(0.5), v, np.float32(0.5))).astype(np.float32)
+
+
 def build_tree(img, c=float("inf"), min_size=200):
     """median -> edge weights -> segment/MST -> BFS rooting, for one view."""
     H, W, _ = img.shape

@@ -14,7 +14,7 @@ import os
 
 import numpy as np
 
-from ._lib import (SM_COST_AGD, SM_POST_LR_CHECK, Context, StereoMSTError, default_params, device_count,  # noqa: F401
+from ._lib import (SM_COST_AGD, SM_COST_VOLUME, SM_POST_LR_CHECK, Context, StereoMSTError, default_params, device_count,  # noqa: F401
                    lib)
 
 __all__ = ["stereo3dmst", "startTimer", "getTimer", "Context", "default_params", "StereoMSTError", "device_count",
@@ -47,23 +47,34 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
 
     left_img/right_img: HxWx3 uint8 BGR (cv::Mat CV_8UC3).  Returns (left_disp, right_disp),
     float32 HxW in [0, Dmax-1]: the strict-< winner-take-all slice of the MST-aggregated
-    AGD cost, with the reference's output step applied: the left map is
+    cost, with the reference's output step applied: the left map is
     left-right checked without fill (:904, :632-662), the right map is returned unchecked.
+    data_cost "AGD" builds the cost on the GPU; "MCCNN_fst"/"MCCNN_acrt" take the MC-CNN volumes
+    from mc-cnn-master/{left,right}.bin (after running the network there, as the reference does).
     Like the reference, an unsupported data_cost prints a message and returns
-    allocated-but-unset maps (:756-759); the names are only forwarded to the cost source and
-    are unused by the AGD cost.
+    allocated-but-unset maps (:756-759); the names are only forwarded to the cost source.
     """
     H, W = left_img.shape[:2]
     left_disp = np.empty((H, W), np.float32)
     right_disp = np.empty((H, W), np.float32)
     if data_cost in ("MCCNN_fst", "MCCNN_acrt"):
         # reference: without an mc-cnn-master folder MCCNN_fst prints and returns (:727-731),
-        # MCCNN_acrt returns silently (:744-745); volume ingest is not implemented yet
+        # MCCNN_acrt returns silently (:744-745); otherwise it runs the network (./main.lua, a
+        # subprocess: :733-750) and maps mc-cnn-master/{left,right}.bin, [Dmax][rows][cols] float
+        # (:764-775), whose clamp and filter run here on the GPU (SM_COST_VOLUME)
         if not os.path.isdir("mc-cnn-master"):
             if data_cost == "MCCNN_fst":
                 print("no mc-cnn-master folder")
-        else:
-            print("stereo3dmst: MC-CNN volume ingest is not implemented in this build; use data_cost=\"AGD\"")
+            return left_disp, right_disp
+        vols = _mccnn_volumes(left_name, right_name, data_cost, H, W, int(Dmax))
+        if vols is None:
+            return left_disp, right_disp
+        ctx = _ctx()
+        ctx.upload_cost_volumes(*vols)
+        out = ctx.match(left_img, right_img, int(Dmax),
+                        default_params(post=SM_POST_LR_CHECK, cost_kind=SM_COST_VOLUME, disp_total=int(Dmax)))
+        left_disp[...] = out["left"]["disp"]
+        right_disp[...] = out["right"]["disp"]
         return left_disp, right_disp
     if data_cost != "AGD":
         print("wrong data cost")
@@ -72,6 +83,30 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
     left_disp[...] = out["left"]["disp"]
     right_disp[...] = out["right"]["disp"]
     return left_disp, right_disp
+
+
+def _mccnn_volumes(left_name, right_name, data_cost, H, W, Dmax):
+    """The reference's MC-CNN step (Stereo3DMST.cpp:725-775): run mc-cnn-master/main.lua when it
+    is present (its failure is ignored, as system()'s exit status is), then read left.bin and
+    right.bin.  Returns the two [Dmax][H][W] volumes, or None (message printed) without them."""
+    import subprocess
+    net = "fast" if data_cost == "MCCNN_fst" else "slow"
+    if os.path.exists(os.path.join("mc-cnn-master", "main.lua")):
+        cmd = ["./main.lua", "mb", net, "-a", "predict", "-net_fname", "net/net_mb_%s_-a_train_all.t7" % net,
+               "-left", "../" + left_name, "-right", "../" + right_name, "-disp_max", str(Dmax), "-sm_terminate", "cnn"]
+        try:
+            subprocess.run(cmd, cwd="mc-cnn-master", check=False)
+        except OSError:
+            pass
+    n = Dmax * H * W
+    vols = []
+    for side in ("left", "right"):
+        path = os.path.join("mc-cnn-master", side + ".bin")
+        if not os.path.exists(path) or os.path.getsize(path) < 4 * n:
+            print("stereo3dmst: %s missing or shorter than %d x %d x %d floats" % (path, Dmax, H, W))
+            return None
+        vols.append(np.fromfile(path, dtype=np.float32, count=n).reshape(Dmax, H, W))
+    return vols
 
 
 def startTimer():

@@ -70,6 +70,7 @@ def lib():
         "sm_last_error": ([vp], ctypes.c_char_p),
         "sm_match": ([vp, vp, vp, ci, ci, ci, ci, ctypes.POINTER(SmParams), vp, vp, vp, vp, vp, vp], ci),
         "sm_upload_images": ([vp, vp, vp, ci, ci, ci], ci),
+        "sm_upload_cost_volumes": ([vp, vp, vp, ci, ci, ci], ci),
         "sm_match_async": ([vp, ci, ctypes.POINTER(SmParams)], ci),
         "sm_synchronize": ([vp], ci),
         "sm_download_results": ([vp, vp, vp, vp, vp, vp, vp], ci),
@@ -165,6 +166,16 @@ class Context:
         H, W, _ = left.shape
         self.shape = (H, W)
         self._check(lib().sm_upload_images(self.h, ptr(left), ptr(right), W, H, W * 3))
+
+    def upload_cost_volumes(self, left_vol, right_vol):
+        """Raw [D][H][W] float32 matching-cost volumes (MC-CNN left.bin / right.bin layout) for
+        matches with cost_kind=SM_COST_VOLUME (clamped as Stereo3DMST.cpp:785-803 on the GPU)."""
+        lv = np.ascontiguousarray(left_vol, dtype=np.float32)
+        rv = np.ascontiguousarray(right_vol, dtype=np.float32)
+        if lv.ndim != 3 or lv.shape != rv.shape:
+            raise ValueError("expected two same-shaped [D][H][W] volumes")
+        D, H, W = lv.shape
+        self._check(lib().sm_upload_cost_volumes(self.h, ptr(lv), ptr(rv), W, H, D))
 
     def match_async(self, D, params=None):
         p = params or default_params()

@@ -58,6 +58,9 @@ struct sm_ctx {
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
     DevBuf changed, mst_ok, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
+    DevBuf vin[2];               // MC-CNN ingest: caller volumes [vin_D][H][W] f32 per view
+    int vin_W = 0, vin_H = 0, vin_D = 0;
+    bool use_vol = false;        // the current call takes its costs from vin (SM_COST_VOLUME)
     DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
     uint32_t epoch = 0;      // bumped per filter call; status words are zeroed only on (re)allocation
     // GPU layout buffers (sm_layout_gpu.hip)
@@ -148,7 +151,7 @@ sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
     if (!(std::isinf(p->c) && p->c > 0))
         return fail(ctx, SM_ERR_ARG, "segment mode (finite c) is not implemented yet: use c=+INFINITY (MST mode)");
     if (p->median_ksize != 3) return fail(ctx, SM_ERR_ARG, "only median_ksize=3 is supported");
-    if (p->cost_kind != SM_COST_AGD) return fail(ctx, SM_ERR_ARG, "only SM_COST_AGD is implemented");
+    if (p->cost_kind != SM_COST_AGD && p->cost_kind != SM_COST_VOLUME) return fail(ctx, SM_ERR_ARG, "unknown cost_kind");
     if (p->gamma != 1.0f / 12.f)
         return fail(ctx, SM_ERR_ARG, "only gamma=1/12 (embedded correctly-rounded tables) is supported");
     if (D < 1 || D > 256) return fail(ctx, SM_ERR_ARG, "D must be in [1, 256] per call (shard larger ranges)");
@@ -654,6 +657,11 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
     CHECK(setup_sync(ctx, a, N, Dpad));
+    a.vol = ctx->use_vol ? 1 : 0;
+    if (a.vol)  // cost rows of every slot from the caller's volumes (slots come from the layout)
+        for (int v = 0; v < nviews; ++v)
+            HIPC(launch_vol_rows(ctx->st, P<float>(ctx->vin[v]), N, dglob0, D, Dpad, P<uint32_t>(ctx->slotpix[v]),
+                                 P<float>(ctx->Cst[v])));
     ctx->nfev = ctx->nsev = 0;
     ctx->fam.clear();
     ctx->fam_vox.clear();
@@ -826,7 +834,7 @@ void sm_destroy(sm_ctx* ctx) {
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
                          &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v], &ctx->Cst[v],
-                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v],
+                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v], &ctx->vin[v],
                          &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
@@ -858,10 +866,32 @@ sm_status sm_upload_images(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int 
     return upload(ctx, l, r, W, H, stride);
 }
 
+sm_status sm_upload_cost_volumes(sm_ctx* ctx, const float* left_vol, const float* right_vol, int W, int H, int D) {
+    if (!ctx) return SM_ERR_ARG;
+    if (!left_vol || !right_vol) return fail(ctx, SM_ERR_ARG, "null volume");
+    if (W < 1 || H < 1 || D < 1 || (long long)W * H > (1ll << 30)) return fail(ctx, SM_ERR_ARG, "bad volume geometry");
+    HIPC(hipSetDevice(ctx->device));
+    const size_t bytes = (size_t)W * H * D * sizeof(float);
+    for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->vin[v], bytes));
+    HIPC(hipMemcpyAsync(ctx->vin[0].p, left_vol, bytes, hipMemcpyHostToDevice, ctx->st));
+    HIPC(hipMemcpyAsync(ctx->vin[1].p, right_vol, bytes, hipMemcpyHostToDevice, ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));  // the caller may free or reuse its buffers on return
+    ctx->vin_W = W;
+    ctx->vin_H = H;
+    ctx->vin_D = D;
+    return SM_OK;
+}
+
 sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     if (!ctx) return SM_ERR_ARG;
     if (ctx->W == 0) return fail(ctx, SM_ERR_STATE, "no images uploaded");
     CHECK(check_params(ctx, p, D));
+    ctx->use_vol = p->cost_kind == SM_COST_VOLUME;
+    if (ctx->use_vol) {
+        if (ctx->vin_D == 0) return fail(ctx, SM_ERR_STATE, "SM_COST_VOLUME: no volumes uploaded (sm_upload_cost_volumes)");
+        if (ctx->vin_W != ctx->W || ctx->vin_H != ctx->H) return fail(ctx, SM_ERR_ARG, "cost volumes and images differ in size");
+        if (p->disp_begin + D > ctx->vin_D) return fail(ctx, SM_ERR_ARG, "slices beyond the uploaded cost volumes");
+    }
     HIPC(hipSetDevice(ctx->device));
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
@@ -976,6 +1006,7 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
                              int D, double* A_up, double* A) {
     if (!ctx) return SM_ERR_ARG;
     if (view != 0 && view != 1) return fail(ctx, SM_ERR_ARG, "view must be 0 or 1");
+    ctx->use_vol = false;  // AGD costs
     if (D < 1 || D > 256 || d0 < 0) return fail(ctx, SM_ERR_ARG, "bad disparity range");
     HIPC(hipSetDevice(ctx->device));
     CHECK(upload(ctx, l, r, W, H, stride));

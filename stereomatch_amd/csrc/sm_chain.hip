@@ -125,7 +125,7 @@ __device__ __forceinline__ void store_crow(float* __restrict__ C, uint32_t slot,
 // k_up_pre: one block per SM_PRE_SEG-node segment of a long path (segment table from the layout),
 // SM_PRE_SEG / CH waves of CH nodes each; grid.y = view
 // ---------------------------------------------------------------------------------------------
-template <int SPL, int CH>
+template <int SPL, int CH, bool VOL>
 __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0, const uint32_t* __restrict__ meta1,
     const SmPath* __restrict__ paths0, const SmPath* __restrict__ paths1, const uint2* __restrict__ seg0,
@@ -174,9 +174,21 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
             for (int i = 0; i < 3; ++i)
                 load_row<SPL>(U, (uint32_t)i < hidx ? mfield(mv, jj, 4 + i) : 0u, Dpad, lane, lr[j][i]);
         }
-        ImgRecs<SPL, CH> rec;
-        load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
-        chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+        if constexpr (VOL) {  // cost rows already in Cst (k_vol_rows): needed by the aggregate only
+            if (agg_mode) {
+#pragma unroll
+                for (int j = 0; j < CH; ++j) {
+                    float t[SPL];
+                    load_cost_row<SPL>(Cst, (uint32_t)(head + first + (j < n ? j : n - 1)), Dpad, lane, t);
+#pragma unroll
+                    for (int k = 0; k < SPL; ++k) c[j][k] = t[k];
+                }
+            }
+        } else {
+            ImgRecs<SPL, CH> rec;
+            load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+            chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+        }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             if (j < n) {
@@ -194,7 +206,7 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
                 }
                 const uint32_t slot = (uint32_t)(head + first + j);
                 if (hidx > 0) store_row<SPL>(U, slot, Dpad, lane, pre[j]);  // Pre = 0 rows are never read
-                store_crow<SPL>(Cst, slot, Dpad, lane, c[j]);
+                if constexpr (!VOL) store_crow<SPL>(Cst, slot, Dpad, lane, c[j]);
             }
         }
     }
@@ -1608,15 +1620,23 @@ static WalkView chain_view(const WalkArgs& a, int v) {
 #ifndef UP_PRE_CH2
 #define UP_PRE_CH2 8  // nodes per wave of k_up_pre at SPL=2
 #endif
-template <int SPL, int CH>
-static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
+template <int SPL, int CH, bool VOL>
+static void up_pre_launch_k(hipStream_t st, const WalkArgs& a) {
     const int ns = a.nseg[0] > a.nseg[1] ? a.nseg[0] : a.nseg[1];
     if (ns == 0) return;
-    hipLaunchKernelGGL((k_up_pre<SPL, CH>), dim3(ns, 2), dim3(64 * SM_PRE_SEG / CH), 0, st, chain_view(a, 0),
+    hipLaunchKernelGGL((k_up_pre<SPL, CH, VOL>), dim3(ns, 2), dim3(64 * SM_PRE_SEG / CH), 0, st, chain_view(a, 0),
                        chain_view(a, 1), reinterpret_cast<const uint32_t*>(a.meta[0]),
                        reinterpret_cast<const uint32_t*>(a.meta[1]), a.paths[0], a.paths[1], a.segtab[0], a.segtab[1],
                        a.nseg[0], a.nseg[1], a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad,
                        a.dcall, a.dglob0, a.pieces[0] ? a.agg[0] : nullptr, a.pieces[1] ? a.agg[1] : nullptr, a.piece_len);
+}
+
+template <int SPL, int CH>
+static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
+    if (a.vol)
+        up_pre_launch_k<SPL, CH, true>(st, a);
+    else
+        up_pre_launch_k<SPL, CH, false>(st, a);
 }
 
 static PieceView piece_view(const WalkArgs& a, int v) {

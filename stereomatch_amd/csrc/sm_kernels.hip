@@ -667,6 +667,41 @@ __global__ void k_finalize(const double* __restrict__ gmin, const int32_t* __res
     }
 }
 
+// MC-CNN ingest (Stereo3DMST.cpp:764-803): slices [d0, d0 + D) of a caller-supplied raw volume
+// [Dv][H][W] -> f32 cost rows Cst[slot][Dpad] after the reference's clamp, NaN -> 0.5 else
+// min(0.5, x) (:785-803; std::min(0.5f, x) returns 0.5 unless x < 0.5).  Row padding (d >= D)
+// gets 3.0, like the AGD path's out-of-range slices (finite; never reaches the WTA).  A block
+// moves 64 consecutive pixels x 64 slices through LDS: 256-B coalesced reads along x per slice,
+// one 256-B row segment written per pixel at its slot.
+__global__ __launch_bounds__(256) void k_vol_rows(const float* __restrict__ vin, size_t N, int d0, int D, int Dpad,
+                                                  const uint32_t* __restrict__ slotpix, float* __restrict__ Cst) {
+    __shared__ float t[64][65];
+    const size_t p0 = (size_t)blockIdx.x * 64;
+    const int dc = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int dd = ty; dd < 64; dd += 4) {
+        const int d = dc + dd;
+        float v = 3.0f;
+        if (d < D && p0 + tx < N) {
+            const float r = vin[(size_t)(d0 + d) * N + p0 + tx];
+            v = r != r ? 0.5f : (r < 0.5f ? r : 0.5f);
+        }
+        t[dd][tx] = v;
+    }
+    __syncthreads();
+    for (int px = ty; px < 64; px += 4) {
+        if (p0 + px >= N) break;
+        Cst[(size_t)slotpix[p0 + px] * Dpad + dc + tx] = t[tx][px];
+    }
+}
+
+hipError_t launch_vol_rows(hipStream_t st, const float* vin, size_t N, int d0, int D, int Dpad, const uint32_t* slotpix,
+                           float* Cst) {
+    const dim3 g((unsigned)((N + 63) / 64), (unsigned)(Dpad / 64));
+    hipLaunchKernelGGL(k_vol_rows, g, dim3(256), 0, st, vin, N, d0, D, Dpad, slotpix, Cst);
+    return hipGetLastError();
+}
+
 // debug: scatter the fp64 rows of slices [0, D) back to [d][y][x]
 __global__ void k_rows_to_volume(const SmMeta* __restrict__ meta, const double* __restrict__ U, int nslots, int Dpad,
                                  int D, size_t N, double* __restrict__ out) {

@@ -46,7 +46,8 @@ struct WalkArgs {
     const float* atab;
     const double* slut;
     const double* s2lut;
-    float* Cst[2];       // long-path AGD cost staging rows [slot][Dpad]
+    float* Cst[2];       // cost rows [slot][Dpad]: long-path AGD staging, or every slot's volume row
+    int vol;             // costs from Cst rows (MC-CNN ingest, k_vol_rows) instead of the AGD cost
     int maxlen;          // longest path of the current bucket (both views)
     const uint2* segtab[2];  // long buckets: {path, segment} per SM_PRE_SEG-node segment
     int nseg[2];
@@ -77,6 +78,8 @@ hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact
 hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c);
 hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r);
 hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok);
+hipError_t launch_vol_rows(hipStream_t st, const float* vin, size_t N, int d0, int D, int Dpad, const uint32_t* slotpix,
+                           float* Cst);
 hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);

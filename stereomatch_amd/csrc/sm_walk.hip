@@ -45,10 +45,13 @@
 // ---------------------------------------------------------------------------------------------
 // ROOT: the chunk holds a tree root with three light children (4 children); only that variant
 // carries the extra synchronous load, so the common chunk has no load inside its recurrence
-template <int SPL, int CH, bool ROOT>
+// VOL: the costs are caller-supplied volume rows (MC-CNN ingest, k_vol_rows) instead of the AGD
+// cost computed from the image records
+template <int SPL, int CH, bool ROOT, bool VOL>
 __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, int view, int lane, int W, int Dpad,
                                          int dbase, int dend, const uint2* __restrict__ own, const uint2* __restrict__ oth,
-                                         double* __restrict__ U, const WalkShared& sh, double (&xc)[SPL]) {
+                                         double* __restrict__ U, const float* __restrict__ Cv, const WalkShared& sh,
+                                         double (&xc)[SPL]) {
     // ---- all vector loads of the chunk
     // light-child rows: unconditional loads (absent children read row 0, an L2-resident dummy) so
     // that no wait splits the chunk's loads
@@ -65,12 +68,17 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
             load_row<SPL>(U, cs, Dpad, lane, lr[j][k]);
         }
     }
-    ImgRecs<SPL, CH> rec;
-    load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
     // ---- off-chain work: costs and edge factors of every node of the chunk
     float c[CH][SPL];  // float until the add: half the registers of the converted values
     double Sv[CH][4];
-    chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+    if constexpr (VOL) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) load_cost_row<SPL>(Cv, (uint32_t)(top - (j < n ? j : n - 1)), Dpad, lane, c[j]);
+    } else {
+        ImgRecs<SPL, CH> rec;
+        load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+        chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+    }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
@@ -122,13 +130,14 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
     }
 }
 
-template <int SPL, int CH>
+template <int SPL, int CH, bool VOL>
 __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                  const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
                                                  const SmPath* __restrict__ paths1, const uint2* __restrict__ Lrec,
                                                  const uint2* __restrict__ Rrec, const float* __restrict__ atab_g,
                                                  const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
-                                                 int W, int Dpad, int dcall, int dglob0) {
+                                                 int W, int Dpad, int dcall, int dglob0, const float* __restrict__ Cv0,
+                                                 const float* __restrict__ Cv1) {
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
@@ -163,10 +172,11 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
         bool root = false;
 #pragma unroll
         for (int j = 0; j < CH; ++j) root |= j < n && hi_nch(mfield(cur, j, 3)) == 4u;
+        const float* __restrict__ Cv = view ? Cv1 : Cv0;
         if (root)
-            up_chunk<SPL, CH, true>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, sh, xc);
+            up_chunk<SPL, CH, true, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc);
         else
-            up_chunk<SPL, CH, false>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, sh, xc);
+            up_chunk<SPL, CH, false, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc);
         if (nn == 0) break;
         cur = nxt;
         top = ntop;
@@ -280,9 +290,16 @@ static WalkView to_view(const WalkArgs& a, int v) {
 
 template <int SPL, int CH>
 static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a) {
-    hipLaunchKernelGGL((k_up_walk<SPL, CH>), g, dim3(256), 0, st, to_view(a, 0), to_view(a, 1),
-                       reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall, a.dglob0);
+    if (a.vol)
+        hipLaunchKernelGGL((k_up_walk<SPL, CH, true>), g, dim3(256), 0, st, to_view(a, 0), to_view(a, 1),
+                           reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
+                           a.dglob0, a.Cst[0], a.Cst[1]);
+    else
+        hipLaunchKernelGGL((k_up_walk<SPL, CH, false>), g, dim3(256), 0, st, to_view(a, 0), to_view(a, 1),
+                           reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
+                           a.dglob0, a.Cst[0], a.Cst[1]);
 }
 
 template <int SPL, int CH>

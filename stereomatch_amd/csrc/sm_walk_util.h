@@ -177,6 +177,25 @@ __device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, 
 }
 
 
+// f32 cost row of one slot (this lane's SPL slices): MC-CNN ingest rows, or the chain staging rows
+template <int SPL>
+__device__ __forceinline__ void load_cost_row(const float* __restrict__ C, uint32_t slot, int Dpad, int lane, float (&c)[SPL]) {
+    const float* p = C + (size_t)slot * Dpad + lane * SPL;
+    if constexpr (SPL == 1) {
+        c[0] = p[0];
+    } else if constexpr (SPL == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(p);
+        c[0] = t.x;
+        c[1] = t.y;
+    } else {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        c[0] = t.x;
+        c[1] = t.y;
+        c[2] = t.z;
+        c[3] = t.w;
+    }
+}
+
 // column of pixel index pix: a float estimate of pix / W is off by at most one while pix < 2^24
 // (exact in float; W <= 2 exact, W >= 3: |error| <= 2^24/W * 2^-22 < 1), fixed with one compare
 // each way -- an integer division costs ~25 VALU per node.  Larger images take the division.

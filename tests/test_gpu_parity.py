@@ -327,3 +327,83 @@ def test_gpu_layout_matches_restated_schedule(gpu_ctx, name):
     spans.sort()
     buckets = [b for _, _, b in spans]
     assert buckets == sorted(buckets)
+
+
+# ---- MC-CNN volume ingest (SM_COST_VOLUME; Stereo3DMST.cpp:764-803) ----
+def _mccnn_like(Dv, H, W, seed):
+    """Raw volumes like MC-CNN's accurate output (0..1) with NaNs and values above the 0.5 clamp."""
+    rng = np.random.default_rng(seed)
+    v = rng.random((Dv, H, W), dtype=np.float32)
+    v[rng.random(v.shape) < 0.01] = np.nan
+    v[rng.random(v.shape) < 0.01] = np.float32(0.5)
+    return v
+
+
+@pytest.mark.parametrize("W,H,D,Dv,d0", [(200, 150, 64, 64, 0), (160, 120, 100, 128, 20), (97, 61, 33, 40, 5),
+                                         (256, 160, 128, 128, 0), (120, 80, 200, 256, 56)])
+def test_volume_ingest_bitexact(gpu_ctx, W, H, D, Dv, d0):
+    """Costs from caller volumes: the GPU's clamp + tree filter + WTA equal the oracle's tree filter
+    over the reference clamp of the same slices, bitwise (SPL 1, 2, 4; shard offsets)."""
+    import stereomatch_amd as sm
+    left, right, _ = make_pair(W, H, 64, index=8)
+    lv, rv = _mccnn_like(Dv, H, W, 1), _mccnn_like(Dv, H, W, 2)
+    gpu_ctx.upload_cost_volumes(lv, rv)
+    out = gpu_ctx.match(left, right, D, sm.default_params(cost_kind=sm.SM_COST_VOLUME, disp_begin=d0))
+    for v, img, vol in (("left", left, lv), ("right", right, rv)):
+        t = O.build_tree(img)
+        r = O.tree_filter(W, H, t, O.mccnn_clamp(vol[d0:d0 + D]), d0, True, False, 16)
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), r["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
+
+
+def test_volume_ingest_pieces_bitexact(gpu_ctx, monkeypatch):
+    """Volume costs through cut paths (64-node pieces) and runs."""
+    import stereomatch_amd as sm
+    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    W, H, D = 320, 240, 64
+    left, right, _ = make_pair(W, H, D, index=9)
+    lv, rv = _mccnn_like(D, H, W, 3), _mccnn_like(D, H, W, 4)
+    gpu_ctx.upload_cost_volumes(lv, rv)
+    out = gpu_ctx.match(left, right, D, sm.default_params(cost_kind=sm.SM_COST_VOLUME))
+    for v, img, vol in (("left", left, lv), ("right", right, rv)):
+        r = O.tree_filter(W, H, O.build_tree(img), O.mccnn_clamp(vol), 0, True, False, 16)
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), r["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
+
+
+def test_volume_ingest_errors():
+    import stereomatch_amd as sm
+    ctx = sm.Context(0)
+    left, right, _ = make_pair(40, 30, 8, index=1)
+    p = sm.default_params(cost_kind=sm.SM_COST_VOLUME)
+    with pytest.raises(sm.StereoMSTError, match="SM_ERR_STATE"):  # nothing uploaded
+        ctx.match(left, right, 8, p)
+    ctx.upload_cost_volumes(np.zeros((8, 30, 40), np.float32), np.zeros((8, 30, 40), np.float32))
+    with pytest.raises(sm.StereoMSTError, match="SM_ERR_ARG"):  # beyond the uploaded slices
+        ctx.match(left, right, 8, sm.default_params(cost_kind=sm.SM_COST_VOLUME, disp_begin=1))
+    l2, r2, _ = make_pair(41, 30, 8, index=1)
+    with pytest.raises(sm.StereoMSTError, match="SM_ERR_ARG"):  # size mismatch
+        ctx.match(l2, r2, 8, p)
+    ctx.close()
+
+
+def test_stereo3dmst_mccnn_ingest(gpu_ctx, tmp_path, monkeypatch):
+    """The reference surface with data_cost="MCCNN_acrt": volumes read from
+    mc-cnn-master/{left,right}.bin ([Dmax][rows][cols] float, Stereo3DMST.cpp:769-775; no network
+    present, so the main.lua step is skipped), clamped and filtered on the GPU, then the output
+    step (left map L-R checked without fill, :900-904)."""
+    import stereomatch_amd as sm
+    W, H, D = 120, 90, 48
+    left, right, _ = make_pair(W, H, D, index=10)
+    lv, rv = _mccnn_like(D, H, W, 5), _mccnn_like(D, H, W, 6)
+    (tmp_path / "mc-cnn-master").mkdir()
+    lv.tofile(str(tmp_path / "mc-cnn-master" / "left.bin"))
+    rv.tofile(str(tmp_path / "mc-cnn-master" / "right.bin"))
+    monkeypatch.chdir(tmp_path)
+    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "MCCNN_acrt", D)
+    ref = {}
+    for v, img, vol in (("left", left, lv), ("right", right, rv)):
+        ref[v] = O.tree_filter(W, H, O.build_tree(img), O.mccnn_clamp(vol), 0, True, False, 16)["idx"]
+    rdisp = ref["right"].reshape(H, W).astype(np.float32)
+    np.testing.assert_array_equal(rd, rdisp)
+    np.testing.assert_array_equal(ld, O.lr_check(ref["left"].reshape(H, W).astype(np.float32), rdisp, D))

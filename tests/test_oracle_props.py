@@ -80,3 +80,12 @@ def test_lr_check_semantics():
     # row 2: round(1.5)=2 -> x-d<0; round(2.5)=3 -> x-d<0; round(0.5)=1 -> R(1)=1, |0.5-1|<=1; x=3,d=2 -> R(1)=1
     exp = np.array([[0, 1, 0, 0], [0, 0, 1, 1], [0, 0, 0.5, 2]], np.float32)
     np.testing.assert_array_equal(out, exp)
+
+
+def test_mccnn_clamp_follows_reference():
+    """Stereo3DMST.cpp:785-803: NaN -> 0.5, otherwise std::min(0.5f, x) (returns 0.5 unless x < 0.5)."""
+    x = np.array([np.nan, -1.0, 0.25, 0.5, 0.7, np.inf, -np.inf, -0.0, 0.49999997], np.float32)
+    y = O.mccnn_clamp(x)
+    exp = np.array([0.5, -1.0, 0.25, 0.5, 0.5, 0.5, -np.inf, -0.0, 0.49999997], np.float32)
+    assert y.dtype == np.float32
+    np.testing.assert_array_equal(y.view(np.uint32), exp.view(np.uint32))
