@@ -21,5 +21,5 @@ def test_shim_compiles_and_exports_reference_symbols(tmp_path):
     for s in ("stereo3dmst", "_Z10startTimerv", "_Z8getTimerv"):
         assert s in syms, s
     undef = subprocess.run(["nm", "-D", "--undefined-only", str(so)], capture_output=True, text=True).stdout
-    for s in ("sm_match", "sm_create", "sm_default_params", "sm_start_timer", "sm_get_timer_ms"):
+    for s in ("sm_match", "sm_create", "sm_default_params", "sm_start_timer", "sm_get_timer_ms", "sm_upload_cost_volumes"):
         assert s in undef, s
