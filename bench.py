@@ -31,6 +31,8 @@ import stereomatch_amd as sm  # noqa: E402
 from tools.synth import make_pair  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+CONFIG_NAMES = {(1920, 1200, 128): " (BASELINE C2)", (3840, 2160, 256): " (BASELINE C3)",
+                (1920, 1200, 256): " (BASELINE C4 size, unsharded)"}
 
 
 def cpu_baseline(W, H, D, slices, threads):
@@ -174,7 +176,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded slanted-plane stereo pair, tools/synth.py)",
-        "config": {"workload": "%dx%d D=%d both views (BASELINE C2)" % (W, H, Dtot_frame) if world == 1 else
+        "config": {"workload": "%dx%d D=%d both views%s" % (W, H, Dtot_frame, CONFIG_NAMES.get((W, H, Dtot_frame), ""))
+                   if world == 1 else
                    "%dx%d D=%d, %s mode, %d disparities/rank" % (W, H, Dtot_frame, args.mode, Dloc),
                    "W": W, "H": H, "D": Dtot_frame, "disparities_per_rank": Dloc,
                    "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world},

@@ -293,7 +293,9 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
 // moves through LDS, so each chain wave moves 1/NCW of the row.  Chain wave w, lane l owns slice
 // elements [(64w + l) * CS, +CS) of every row.
 // ---------------------------------------------------------------------------------------------
+#ifndef CHN_WAVES
 #define CHN_WAVES 16
+#endif
 #define CHN_THREADS (64 * CHN_WAVES)
 
 template <int SPL>
@@ -354,10 +356,13 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 // children present (the bottom node has Sh = 0 and x = 0, i.e. acc = Pre).  A tree root may have a
 // third post-heavy child: its group takes the node-by-node path with one more fma.
 // ---------------------------------------------------------------------------------------------
+#ifndef UP_NS2
+#define UP_NS2 6
+#endif
 template <int SPL>
 struct UpCfg {
     static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? 6 : 3;  // nodes per group (helper registers)
-    static constexpr int NS = SPL == 1 ? 8 : 6;                // LDS slots (~140 KB)
+    static constexpr int NS = SPL == 1 ? 8 : SPL == 2 ? UP_NS2 : 6;  // LDS slots (~140 KB)
 };
 
 struct UpNodeS {

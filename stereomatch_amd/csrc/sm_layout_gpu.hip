@@ -20,6 +20,9 @@
 #include "sm_common.h"
 #include "sm_layout_gpu.h"
 
+#ifndef SM_RUN_DIV
+#define SM_RUN_DIV 384  // run window = bucket nodes / SM_RUN_DIV (~3 runs per CU, both views)
+#endif
 #define TL 32                 // tile side
 #define TLP (TL * TL)         // pixels per tile
 #define TLS (4 * TLP)         // arc slots per tile
@@ -658,7 +661,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
         const uint32_t sbase = running;  // the bucket's first segment
         const uint32_t hbase = hb[b];
         // run window: ~3 runs per CU over both views (256 CUs), 64 .. plen nodes
-        const uint32_t rwin = min(plen, max(64u, rn[b] / 384u));
+        const uint32_t rwin = min(plen, max(64u, rn[b] / (uint32_t)SM_RUN_DIV));
         if (threadIdx.x == 0) {
             prev_win = 0xFFFFFFFFu;
             prev_cut = 1u;

@@ -169,6 +169,17 @@ def test_full_size_c2_slices_bitexact(gpu_ctx):
         assert np.array_equal(bits(A), bits(r["A"]))
 
 
+def test_full_size_c4_match_bitexact(gpu_ctx):
+    """1920x1200 D=256 (BASELINE config C4 unsharded; SPL=4, cut root paths), bitwise."""
+    W, H, D = 1920, 1200, 256
+    left, right, _ = make_pair(W, H, D, index=11)
+    out = gpu_ctx.match(left, right, D)
+    ref = O.match(left, right, D, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
 def test_full_size_c2_match_bitexact(gpu_ctx):
     """1920x1200 D=128 (the headline config): WTA indices and fp64 minima, bitwise."""
     W, H, D = 1920, 1200, 128
