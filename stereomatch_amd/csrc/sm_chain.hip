@@ -163,15 +163,16 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     MetaVec<CH> mv;
     if (n > 0) {
         load_meta<CH>(mv, meta32, lane, head + first, 1, n);
-        // pre-heavy light child rows (positions 0 .. hidx-1; up to 3 at a tree root)
-        // unconditional loads (absent rows read row 0, an L2-resident dummy): no wait splits them
-        double lr[CH][3][SPL];
+        // pre-heavy light child rows (positions 0 .. hidx-1): the first two with unconditional
+        // loads (absent rows read row 0, an L2-resident dummy: no wait splits them); a third one
+        // (hidx == 3, a four-child node whose heavy child is the last) is loaded where it is used
+        double lr[CH][2][SPL];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int jj = j < n ? j : n - 1;
             const uint32_t hidx = hi_hidx(mfield(mv, jj, 3));
 #pragma unroll
-            for (int i = 0; i < 3; ++i)
+            for (int i = 0; i < 2; ++i)
                 load_row<SPL>(U, (uint32_t)i < hidx ? mfield(mv, jj, 4 + i) : 0u, Dpad, lane, lr[j][i]);
         }
         if constexpr (VOL) {  // cost rows already in Cst (k_vol_rows): needed by the aggregate only
@@ -200,8 +201,15 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
                 for (int i = 0; i < 3; ++i) {
                     if ((uint32_t)i < hidx) {
                         const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);  // uniform
+                        double r[SPL];
+                        if (i < 2) {
 #pragma unroll
-                        for (int k = 0; k < SPL; ++k) pre[j][k] = __builtin_fma(S, lr[j][i][k], pre[j][k]);
+                            for (int k = 0; k < SPL; ++k) r[k] = lr[j][i][k];
+                        } else {
+                            load_row<SPL>(U, mfield(mv, j, 6), Dpad, lane, r);
+                        }
+#pragma unroll
+                        for (int k = 0; k < SPL; ++k) pre[j][k] = __builtin_fma(S, r[k], pre[j][k]);
                     }
                 }
                 const uint32_t slot = (uint32_t)(head + first + j);
@@ -220,19 +228,7 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
         P[k] = 1.0;
         B[k] = 0.0;
     }
-    if (n > 0) {
-        double pr[CH][3][SPL];
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int jj = j < n ? j : n - 1;
-            const uint32_t hi = mfield(mv, jj, 3);
-            const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-            const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                load_row<SPL>(U, (uint32_t)i < np ? mfield(mv, jj, 4 + (int)min(hidx + 1u + (uint32_t)i, 3u)) : 0u, Dpad, lane,
-                              pr[j][i]);
-        }
+    if (n > 0) {  // cut paths only (rare): post rows loaded where used, to keep registers low
 #pragma unroll
         for (int j = CH - 1; j >= 0; --j) {
             if (j < n) {
@@ -246,9 +242,12 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     if ((uint32_t)i < np) {
-                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, (int)min(hidx + 1u + (uint32_t)i, 3u))], 0);
+                        const int pos = (int)min(hidx + 1u + (uint32_t)i, 3u);
+                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, pos)], 0);
+                        double r[SPL];
+                        load_row<SPL>(U, mfield(mv, j, 4 + pos), Dpad, lane, r);
 #pragma unroll
-                        for (int k = 0; k < SPL; ++k) b[k] = __builtin_fma(S, pr[j][i][k], b[k]);
+                        for (int k = 0; k < SPL; ++k) b[k] = __builtin_fma(S, r[k], b[k]);
                     }
                 }
 #pragma unroll
