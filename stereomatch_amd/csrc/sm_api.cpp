@@ -68,7 +68,7 @@ struct sm_ctx {
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
     DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2];
     DevBuf pieces[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
-    DevBuf cn0[2], cn1[2], cw0[2], cw1[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
+    DevBuf cnw[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
     int mst_rounds = 12;  // contracted Boruvka rounds the previous frame needed
     MstPending mst_pend;  // rounds enqueued without a host check (stage_mst -> mst_finish)
@@ -332,10 +332,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->c_last[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->c_len[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->c_head[v], max_chains * 4));
-        CHECK(ensure(ctx, ctx->cn0[v], max_chains * 4));
-        CHECK(ensure(ctx, ctx->cn1[v], max_chains * 4));
-        CHECK(ensure(ctx, ctx->cw0[v], max_chains * 4));
-        CHECK(ensure(ctx, ctx->cw1[v], max_chains * 4));
+        CHECK(ensure(ctx, ctx->cnw[v], max_chains * 8));
         CHECK(ensure(ctx, ctx->tour[v], 2 * N * 8 + 16));
         CHECK(ensure(ctx, ctx->bsum[v], nscan * 8));
         CHECK(ensure(ctx, ctx->bsum32[v], nscan * 4));
@@ -374,10 +371,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.c_last = P<uint32_t>(ctx->c_last[v]);
         L.c_len = P<uint32_t>(ctx->c_len[v]);
         L.c_head = P<uint32_t>(ctx->c_head[v]);
-        L.n0 = P<uint32_t>(ctx->cn0[v]);
-        L.n1 = P<uint32_t>(ctx->cn1[v]);
-        L.w0 = P<uint32_t>(ctx->cw0[v]);
-        L.w1 = P<uint32_t>(ctx->cw1[v]);
+        L.cnw = P<uint64_t>(ctx->cnw[v]);
         L.tour = P<long long>(ctx->tour[v]);
         L.bsum = P<long long>(ctx->bsum[v]);
         L.bsum32 = P<uint32_t>(ctx->bsum32[v]);
@@ -846,8 +840,8 @@ void sm_destroy(sm_ctx* ctx) {
     for (int v = 0; v < 2; ++v) {
         DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->off_in[v], &ctx->light_in[v],
                          &ctx->pre[v], &ctx->ld[v], &ctx->a_dist[v], &ctx->a_cid[v], &ctx->a_head[v], &ctx->arank[v],
-                         &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cn0[v], &ctx->cn1[v],
-                         &ctx->cw0[v], &ctx->cw1[v], &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
+                         &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cnw[v],
+                         &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
                          &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
                          &ctx->nslot[v], &ctx->slotpix[v], &ctx->pieces[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);

@@ -42,7 +42,7 @@ struct LayoutView {
     uint32_t* c_last;
     uint32_t* c_len;
     uint32_t* c_head;
-    uint32_t *n0, *n1, *w0, *w1;
+    uint64_t* cnw;      // per chain: successor chain (low 32 bits) | arcs to it (high 32 bits)
     // tour (2N-2) + scan scratch
     long long* tour;
     long long* bsum;

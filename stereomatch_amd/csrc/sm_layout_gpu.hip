@@ -6,7 +6,7 @@
 // leaves a pixel through the next MST direction after the one it arrived from), ranked by
 //   L1  k_tour_tile   : per 32x32 tile, LDS pointer jumping contracts every maximal run of the
 //                       tour inside the tile into one chain (distance-to-chain-end, chain id)
-//   L2  k_chain_*     : pointer jumping (Wyllie) over the ~1e5 chains in global memory
+//   L2  k_chain_*     : in-place pointer jumping over the ~1e5 chains in global memory
 //   L3  k_tour_rank   : arc rank = chain rank + offset in chain
 // then orientation (an arc is "down" iff it precedes its reverse), subtree size
 // (rank distance / 2), heavy child (max size, ties -> smallest direction), and a single int64
@@ -85,38 +85,39 @@ __device__ __forceinline__ uint32_t succ_arc(const uint8_t* adj, int W, uint32_t
     return s == start ? SM_NONE : s;
 }
 
-// L1: contract the tour inside each 32x32 tile.
+// L1: contract the tour inside each 32x32 tile.  One 64-bit LDS word per arc slot,
+// nxt | dist << 16 | last << 32 (bits 48..63: the chain head, written once the jumping is done),
+// so a jump is one gathered word; every thread keeps its 16 words in registers.
 __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    __shared__ uint16_t nxt[TLS];
-    __shared__ uint16_t dist[TLS];
-    __shared__ uint16_t last[TLS];
-    __shared__ uint16_t headof[TLS];  // indexed by a chain's last slot -> its head slot
+    __shared__ union {
+        uint64_t w[TLS];
+        uint16_t h[4 * TLS];  // h[4*s + 3]: head slot of the chain whose last slot is s
+    } st;
     __shared__ uint8_t haspred[TLS];
     const int tx0 = blockIdx.x * TL, ty0 = blockIdx.y * TL;
     const uint32_t start = start_arc(V.adj);
     constexpr int PER = TLS / TL_THREADS;  // 16 slots per thread
     for (int i = 0; i < PER; ++i) haspred[threadIdx.x + i * TL_THREADS] = 0;
     __syncthreads();
+    uint64_t own[PER];
     for (int i = 0; i < PER; ++i) {
         const int s = threadIdx.x + i * TL_THREADS;
         const int lp = s >> 2, k = s & 3;
         const int lx = lp % TL, ly = lp / TL;
         const int x = tx0 + lx, y = ty0 + ly;
-        uint16_t n = L_NIL, dd = 0;
+        uint32_t n = L_NIL, dd = 0;
         if (x < W && y < H) {
             const uint32_t p = (uint32_t)(y * W + x);
             if (V.adj[p] & (1u << k)) {
                 dd = 1;
                 const uint32_t sa = succ_arc(V.adj, W, 4u * p + (uint32_t)k, start);
-                if (sa == SM_NONE) {
-                    n = L_NIL;
-                } else {
+                if (sa != SM_NONE) {
                     const uint32_t q = sa >> 2;
                     const int qx = (int)(q % (uint32_t)W) - tx0, qy = (int)(q / (uint32_t)W) - ty0;
                     if (qx >= 0 && qx < TL && qy >= 0 && qy < TL) {
-                        n = (uint16_t)(4 * (qy * TL + qx) + (int)(sa & 3u));
+                        n = (uint32_t)(4 * (qy * TL + qx) + (int)(sa & 3u));
                         haspred[n] = 1;
                     } else {
                         n = L_EXIT;
@@ -124,32 +125,25 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
                 }
             }
         }
-        nxt[s] = n;
-        dist[s] = dd;
-        last[s] = (uint16_t)s;
+        own[i] = (uint64_t)n | ((uint64_t)dd << 16) | ((uint64_t)s << 32);
+        st.w[s] = own[i];
     }
     __syncthreads();
     // pointer jumping: dist -> arcs to chain end (inclusive), last -> chain's last slot
     for (int it = 0; it < 13; ++it) {
-        uint16_t nn[PER], nd[PER], nl[PER];
         bool any = false;
         for (int i = 0; i < PER; ++i) {
-            const int s = threadIdx.x + i * TL_THREADS;
-            const uint16_t n = nxt[s];
-            nn[i] = n; nd[i] = dist[s]; nl[i] = last[s];
+            const uint32_t n = (uint32_t)own[i] & 0xFFFFu;
             if (n < L_NIL) {
-                nd[i] = (uint16_t)(nd[i] + dist[n]);
-                nl[i] = last[n];
-                nn[i] = nxt[n];
+                const uint64_t nb = st.w[n];
+                const uint32_t d = (uint32_t)(own[i] >> 16) + (uint32_t)(nb >> 16);  // low 16 bits: the sum
+                own[i] = (nb & 0xFFFF0000FFFFull) | ((uint64_t)(d & 0xFFFFu) << 16);
                 any = true;
             }
         }
         any = __syncthreads_or(any);
         if (!any) break;
-        for (int i = 0; i < PER; ++i) {
-            const int s = threadIdx.x + i * TL_THREADS;
-            nxt[s] = nn[i]; dist[s] = nd[i]; last[s] = nl[i];
-        }
+        for (int i = 0; i < PER; ++i) st.w[threadIdx.x + i * TL_THREADS] = own[i];
         __syncthreads();
     }
     // heads: existing arcs without an in-tile predecessor; register chains
@@ -159,9 +153,10 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
     uint32_t myhead[PER];
     for (int i = 0; i < PER; ++i) {
         const int s = threadIdx.x + i * TL_THREADS;
+        const uint32_t dist = (uint32_t)(own[i] >> 16) & 0xFFFFu, last = (uint32_t)(own[i] >> 32) & 0xFFFFu;
         myhead[i] = SM_NONE;
-        if (dist[s] != 0 && !haspred[s]) {
-            headof[last[s]] = (uint16_t)s;
+        if (dist != 0 && !haspred[s]) {
+            st.h[4 * last + 3] = (uint16_t)s;
             myhead[i] = atomicAdd(&nheads, 1u);  // LDS atomic: rank of this chain inside the tile
         }
     }
@@ -170,30 +165,30 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
     __syncthreads();
     for (int i = 0; i < PER; ++i) {
         const int s = threadIdx.x + i * TL_THREADS;
-        if (dist[s] == 0) continue;
+        const uint32_t dist = (uint32_t)(own[i] >> 16) & 0xFFFFu, last = (uint32_t)(own[i] >> 32) & 0xFFFFu;
+        if (dist == 0) continue;
         const int lp = s >> 2, k = s & 3;
         const uint32_t p = (uint32_t)((ty0 + lp / TL) * W + tx0 + lp % TL);
         const uint32_t a = 4u * p + (uint32_t)k;
-        V.a_dist[a] = dist[s];
-        if (!haspred[s]) {
+        V.a_dist[a] = (uint16_t)dist;
+        if (myhead[i] != SM_NONE) {
             const uint32_t cid = cbase + myhead[i];
             V.a_cid[a] = cid;        // head's chain id (read below by the chain's other arcs: next kernel)
-            const int ls = last[s];
-            const int llp = ls >> 2;
+            const int llp = (int)last >> 2;
             const uint32_t lpix = (uint32_t)((ty0 + llp / TL) * W + tx0 + llp % TL);
-            V.c_last[cid] = 4u * lpix + (uint32_t)(ls & 3);
-            V.c_len[cid] = dist[s];
+            V.c_last[cid] = 4u * lpix + (last & 3u);
+            V.c_len[cid] = dist;
             V.c_head[cid] = a;
         }
         // every arc remembers its chain head (global arc id)
-        const int hs = headof[last[s]];
+        const int hs = st.h[4 * last + 3];
         const int hlp = hs >> 2;
         const uint32_t hpix = (uint32_t)((ty0 + hlp / TL) * W + tx0 + hlp % TL);
         V.a_head[a] = 4u * hpix + (uint32_t)(hs & 3);
     }
 }
 
-// L2 init: chain successor + weight (suffix-sum Wyllie state)
+// L2 init: chain successor + weight
 __global__ void k_chain_init(LayoutPair LP, int W) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
@@ -201,45 +196,45 @@ __global__ void k_chain_init(LayoutPair LP, int W) {
     if (c >= *V.nchains) return;
     const uint32_t start = start_arc(V.adj);
     const uint32_t s = succ_arc(V.adj, W, V.c_last[c], start);
-    V.w0[c] = V.c_len[c];
-    V.n0[c] = s == SM_NONE ? SM_NONE : V.a_cid[s];
+    const uint32_t n = s == SM_NONE ? SM_NONE : V.a_cid[s];
+    V.cnw[c] = ((uint64_t)V.c_len[c] << 32) | n;
 }
 
-// L2 step: ping-pong pointer jumping
-__global__ void k_chain_jump(LayoutPair LP, int parity) {
+// L2: suffix sums over the chain list by in-place pointer jumping, one launch.  Every word
+// {n, w} satisfies "w = arcs from this chain up to (not including) chain n" whichever update of
+// it a reader sees (the pair is one 64-bit access), so no step needs a grid barrier: a thread
+// jumps until its successor is the tour end.  Every jump moves strictly forward, so the loop
+// ends; with fresh words it takes ~log2(chains) steps.  Integer sums: the result is exact.
+__global__ void k_chain_rank(LayoutPair LP) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= *V.nchains) return;
-    const uint32_t* nin = parity ? V.n1 : V.n0;
-    const uint32_t* win = parity ? V.w1 : V.w0;
-    uint32_t* nout = parity ? V.n0 : V.n1;
-    uint32_t* wout = parity ? V.w0 : V.w1;
-    const uint32_t n = nin[c];
-    if (n == SM_NONE) {
-        nout[c] = n;
-        wout[c] = win[c];
-    } else {
-        nout[c] = nin[n];
-        wout[c] = win[c] + win[n];
+    uint64_t* nw = V.cnw;
+    const uint64_t me = nw[c];
+    uint32_t n = (uint32_t)me, w = (uint32_t)(me >> 32);
+    while (n != SM_NONE) {
+        const uint64_t nb = __hip_atomic_load(nw + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        n = (uint32_t)nb;
+        w += (uint32_t)(nb >> 32);
+        __hip_atomic_store(nw + c, ((uint64_t)w << 32) | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 // L3: arc ranks.  suffix(c) = arcs from chain c's head to the tour end; rank = total - suffix + offset
-__global__ void k_tour_rank(LayoutPair LP, int W, int H, int parity) {
+__global__ void k_tour_rank(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
     const uint32_t p = (uint32_t)(y * W + x);
     const uint32_t adj = V.adj[p];
-    const uint32_t* wfin = parity ? V.w1 : V.w0;
     const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
     for (int k = 0; k < 4; ++k) {
         if (!(adj & (1u << k))) continue;
         const uint32_t a = 4u * p + (uint32_t)k;
         const uint32_t c = V.a_cid[V.a_head[a]];
-        const uint32_t chain_rank = total - wfin[c];
+        const uint32_t chain_rank = total - (uint32_t)(V.cnw[c] >> 32);
         V.rank[a] = chain_rank + (V.c_len[c] - V.a_dist[a]);
     }
 }
@@ -730,12 +725,8 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_tour_tile, dim3((W + TL - 1) / TL, (H + TL - 1) / TL, nviews), dim3(TL_THREADS), 0, st, LP, W, H);
     const dim3 cg((max_chains + 255) / 256, nviews);
     hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
-    int parity = 0;
-    for (uint32_t span = 1; span < max_chains; span <<= 1) {
-        hipLaunchKernelGGL(k_chain_jump, cg, dim3(256), 0, st, LP, parity);
-        parity ^= 1;
-    }
-    hipLaunchKernelGGL(k_tour_rank, pg, dim3(256), 0, st, LP, W, H, parity);
+    hipLaunchKernelGGL(k_chain_rank, cg, dim3(256), 0, st, LP);
+    hipLaunchKernelGGL(k_tour_rank, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_orient, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_heavy, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_tour_values, pg, dim3(256), 0, st, LP, W, H);
