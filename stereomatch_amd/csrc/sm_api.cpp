@@ -58,6 +58,7 @@ struct sm_ctx {
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
     DevBuf changed, mst_ok, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
+    size_t rec_pad_n[2] = {0, 0};  // pixel count the record pads were zeroed for
     DevBuf vin[2];               // MC-CNN ingest: caller volumes [vin_D][H][W] f32 per view
     int vin_W = 0, vin_H = 0, vin_D = 0;
     bool use_vol = false;        // the current call takes its costs from vin (SM_COST_VOLUME)
@@ -170,9 +171,13 @@ sm_status stage_prep(sm_ctx* ctx) {
         CHECK(ensure(ctx, ctx->med[v], N * 4));
         CHECK(ensure(ctx, ctx->wR[v], N * 2));
         CHECK(ensure(ctx, ctx->wD[v], N * 2));
+        const void* old = ctx->rec[v].p;
         CHECK(ensure(ctx, ctx->rec[v], (N + 2 * SM_REC_PAD) * 8));
-        HIPC(hipMemsetAsync(ctx->rec[v].p, 0, SM_REC_PAD * 8, ctx->st));
-        HIPC(hipMemsetAsync(P<uint2>(ctx->rec[v]) + SM_REC_PAD + N, 0, SM_REC_PAD * 8, ctx->st));
+        if (ctx->rec[v].p != old || ctx->rec_pad_n[v] != N) {  // zero pads around the records: once per allocation and size
+            ctx->rec_pad_n[v] = N;
+            HIPC(hipMemsetAsync(ctx->rec[v].p, 0, SM_REC_PAD * 8, ctx->st));
+            HIPC(hipMemsetAsync(P<uint2>(ctx->rec[v]) + SM_REC_PAD + N, 0, SM_REC_PAD * 8, ctx->st));
+        }
     }
     HIPC(launch_prep(ctx->st, P<uint8_t>(ctx->img[0]), P<uint8_t>(ctx->img[1]), W, H, ctx->stride, P<uint32_t>(ctx->bgrx[0]),
                      P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]), P<float>(ctx->gray[1]),
@@ -198,8 +203,6 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->root[v], N * 4));
         CHECK(ensure(ctx, ctx->mR[v], N));
         CHECK(ensure(ctx, ctx->mD[v], N));
-        HIPC(hipMemsetAsync(ctx->mR[v].p, 0, N, ctx->st));
-        HIPC(hipMemsetAsync(ctx->mD[v].p, 0, N, ctx->st));
         a.wR[v] = P<uint16_t>(ctx->wR[v]);
         a.wD[v] = P<uint16_t>(ctx->wD[v]);
         a.comp[v] = P<uint32_t>(ctx->comp[v]);
@@ -210,7 +213,15 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     }
     CHECK(ensure(ctx, ctx->changed, 2 * SM_MST_MAX_ROUNDS * sizeof(int)));
     CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
-    HIPC(hipMemsetAsync(ctx->changed.p, 0, 2 * SM_MST_MAX_ROUNDS * sizeof(int), ctx->st));
+    ZeroList z{};
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->ccnt[v], 16));
+        z.add(ctx->mR[v].p, N);
+        z.add(ctx->mD[v].p, N);
+        z.add(ctx->ccnt[v].p, 16);
+    }
+    z.add(ctx->changed.p, 2 * SM_MST_MAX_ROUNDS * sizeof(int));
+    HIPC(launch_zero(ctx->st, z));
     a.flags[0] = P<int>(ctx->changed);
     a.flags[1] = P<int>(ctx->changed) + SM_MST_MAX_ROUNDS;
     HIPC(launch_bor_local(ctx->st, a, W, H));
@@ -241,8 +252,6 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->cedge[v], 2 * (2 * N) * 16));
         CHECK(ensure(ctx, ctx->clab[v], N * 4));
         CHECK(ensure(ctx, ctx->chook[v], N * 4));
-        CHECK(ensure(ctx, ctx->ccnt[v], 16));
-        HIPC(hipMemsetAsync(ctx->ccnt[v].p, 0, 16, ctx->st));
         c.cid[v] = P<uint32_t>(ctx->root[v]);
         c.counts[v] = P<uint32_t>(ctx->ccnt[v]);
         c.edges[v] = ctx->cedge[v].p;
@@ -315,6 +324,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
     const uint32_t max_chains = ntiles * 129u + 1u;
     const size_t nscan = (2 * N + 8191) / 8192 + 1;
     LayoutPair LP{};
+    ZeroList z{};
     for (int v = 0; v < nviews; ++v) {
         CHECK(ensure(ctx, ctx->adj[v], N));
         CHECK(ensure(ctx, ctx->pdir[v], N));
@@ -347,9 +357,9 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
         CHECK(ensure(ctx, ctx->nslot[v], N * 4));
         CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
-        HIPC(hipMemsetAsync(ctx->plen[v].p, 0, N * 4, ctx->st));  // lengths past the last path stay 0
-        HIPC(hipMemsetAsync(ctx->ccount[v].p, 0, 16, ctx->st));
-        HIPC(hipMemsetAsync(ctx->rounds[v].p, 0, RREC * 4, ctx->st));
+        z.add(ctx->plen[v].p, N * 4);  // lengths past the last path stay 0
+        z.add(ctx->ccount[v].p, 16);
+        z.add(ctx->rounds[v].p, RREC * 4);
         LayoutView& L = LP.v[v];
         L.mR = P<uint8_t>(ctx->mR[v]);
         L.mD = P<uint8_t>(ctx->mD[v]);
@@ -398,6 +408,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
     LP.mst_ok = P<int>(ctx->mst_ok);
+    HIPC(launch_zero(ctx->st, z));
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains, (uint32_t)piece_len()));
     // the host needs the per-round path counts to size the walker grids
     for (int v = 0; v < nviews; ++v)

@@ -12,6 +12,8 @@
 //   k_bor_*         Boruvka MST in (w,a,b) order: LDS tile phase + global    (segment-graph.h:54-89, c=+inf)
 //   (tree-filter walkers: sm_walk.hip)
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "sm_common.h"
@@ -771,6 +773,27 @@ hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int 
 // nothing in any view (stage_mst enqueues rounds without a host check)
 __global__ void k_mst_done(const int* __restrict__ f0, const int* __restrict__ f1, int r, int nviews, int* ok) {
     if (threadIdx.x == 0) *ok = (f0[r] == 0 && (nviews < 2 || f1[r] == 0)) ? 1 : 0;
+}
+
+// one launch for a frame stage's zero-fills (each hipMemsetAsync is its own dispatch)
+__global__ __launch_bounds__(256) void k_zero(ZeroList z) {
+    uint8_t* p = static_cast<uint8_t*>(z.p[blockIdx.y]);
+    const size_t n = z.n[blockIdx.y], n16 = n / 16;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+        reinterpret_cast<uint4*>(p)[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == 0 && threadIdx.x < n - n16 * 16) p[n16 * 16 + threadIdx.x] = 0;
+}
+
+hipError_t launch_zero(hipStream_t st, const ZeroList& z) {
+    if (z.count <= 0) return hipSuccess;
+    size_t mx = 0;
+    for (int i = 0; i < z.count; ++i) {
+        if (reinterpret_cast<uintptr_t>(z.p[i]) & 15u) return hipErrorInvalidValue;
+        mx = mx > z.n[i] ? mx : z.n[i];
+    }
+    const unsigned gx = (unsigned)std::min<size_t>(std::max<size_t>((mx / 16 + 255) / 256, 1), 512);
+    hipLaunchKernelGGL(k_zero, dim3(gx, z.count), dim3(256), 0, st, z);
+    return hipGetLastError();
 }
 
 hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok) {

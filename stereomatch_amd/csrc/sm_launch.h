@@ -6,6 +6,15 @@
 
 #include "sm_common.h"
 
+// byte ranges zeroed by one launch (each base 16-byte aligned: hipMalloc'd buffers)
+#define SM_ZERO_MAX 12
+struct ZeroList {
+    void* p[SM_ZERO_MAX];
+    size_t n[SM_ZERO_MAX];
+    int count;
+    void add(void* ptr, size_t bytes) { p[count] = ptr; n[count] = bytes; ++count; }
+};
+
 struct MstArgs {
     int nviews;
     const uint16_t* wR[2];
@@ -77,6 +86,7 @@ hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int 
 hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int H);
 hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c);
 hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r);
+hipError_t launch_zero(hipStream_t st, const ZeroList& z);
 hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok);
 hipError_t launch_vol_rows(hipStream_t st, const float* vin, size_t N, int d0, int D, int Dpad, const uint32_t* slotpix,
                            float* Cst);
