@@ -57,6 +57,7 @@ struct LayoutView {
     uint32_t* plen;          // [path] -> len, inclusive-scanned into the path's end slot
     uint32_t* nslot;         // [preorder] -> slot
     uint32_t* slotpix;       // [pixel] -> slot
+    uint32_t* slot2pix;      // [slot] -> pixel
     uint32_t* round_count;   // SM_NBUCKETS
     uint32_t* round_cursor;  // SM_NBUCKETS
     uint32_t* round_begin;   // SM_NBUCKETS + 1

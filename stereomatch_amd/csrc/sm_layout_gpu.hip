@@ -473,15 +473,30 @@ __global__ void k_newslot(LayoutPair LP, int N) {
     if (s == head) V.paths[P].head = nh;
 }
 
-// per-slot metadata in slot numbering: pixel, parent slot, child weights and slots in
-// descending (w,a,b) key order (the reference's fold order), heavy-child position, light flag
-__global__ void k_meta(LayoutPair LP, int W, int H) {
+// slot of every pixel and pixel of every slot (one random gather and one scattered 4-byte store
+// per pixel), so that k_meta runs in slot order: consecutive slots walk heavy paths, i.e.
+// neighbouring pixels, and the 32-byte metadata records are written contiguously
+__global__ void k_slotpix(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = x0 < W;
-    const int x = live ? x0 : W - 1;  // idle lanes recompute the last pixel but never store
+    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
     const uint32_t v = (uint32_t)(y * W + x);
+    const uint32_t slot = V.nslot[V.pre[v]];
+    V.slotpix[v] = slot;
+    V.slot2pix[slot] = v;
+}
+
+// per-slot metadata in slot numbering: pixel, parent slot, child weights and slots in
+// descending (w,a,b) key order (the reference's fold order), heavy-child position, light flag
+#define META_BLOCKS 1024  // blocks per view (grid-stride): one has-light atomic per block
+
+__global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
+    const LayoutView& V = LP.v[blockIdx.y];
+    uint32_t nlight = 0;
+    for (uint32_t slot = blockIdx.x * 256 + threadIdx.x; slot < (uint32_t)N; slot += META_BLOCKS * 256) {
+    const uint32_t v = V.slot2pix[slot];
     const uint32_t adj = V.adj[v];
     const int pd = V.pdir[v];
     const int hv = V.heavy[v];
@@ -503,28 +518,23 @@ __global__ void k_meta(LayoutPair LP, int W, int H) {
     uint32_t hidx = 0, has_light = 0;
     for (int i = 0; i < nch; ++i) {
         cw[i] = (uint32_t)(ck[i] >> 33);
-        cs[i] = V.nslot[V.pre[nbr_of(v, cq[i], W)]];
+        cs[i] = V.slotpix[nbr_of(v, cq[i], W)];
         if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
     }
     uint32_t wp = 0, parent = SM_NONE;
     if (pd >= 0) {
         wp = (uint32_t)(key_dir(V.wR, V.wD, W, v, pd) >> 33);
-        parent = V.nslot[V.pre[nbr_of(v, pd, W)]];
+        parent = V.slotpix[nbr_of(v, pd, W)];
     }
-    has_light = live ? has_light : 0u;
-    const uint32_t slot = V.nslot[V.pre[v]];
-    if (live) {
-        V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
-        V.slotpix[v] = slot;
+    V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
+    nlight += has_light;
     }
-    {
-        __shared__ uint32_t nl;
-        if (threadIdx.x == 0) nl = 0;
-        __syncthreads();
-        if (has_light) atomicAdd(&nl, 1u);
-        __syncthreads();
-        if (threadIdx.x == 0 && nl) atomicAdd(V.n_has_light, nl);
-    }
+    __shared__ uint32_t nl;
+    if (threadIdx.x == 0) nl = 0;
+    __syncthreads();
+    if (nlight) atomicAdd(&nl, nlight);
+    __syncthreads();
+    if (threadIdx.x == 0 && nl) atomicAdd(V.n_has_light, nl);
 }
 
 // heads in slot order -> path lengths -> bucketed by light depth (order inside a round is free).
@@ -549,8 +559,8 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_prep(LayoutPair LP, int N) 
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
-    __shared__ uint32_t hist[SM_NBUCKETS], nodes[SM_NBUCKETS];
-    if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = nodes[threadIdx.x] = 0;
+    __shared__ uint32_t hist[SM_NBUCKETS], nodes[SM_NBUCKETS], mlen[SM_NBUCKETS];
+    if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = nodes[threadIdx.x] = mlen[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
     for (int i = 0; i < PATH_ITEMS; ++i) {
@@ -562,13 +572,14 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N)
             const uint32_t b = 2u * (V.headflag[head] - 1u) + (len >= SM_LONG_PATH ? 0u : 1u);
             atomicAdd(&hist[b], 1u);
             atomicAdd(&nodes[b], len);
-            if (len >= SM_LONG_PATH) atomicMax(&V.round_maxlen[b], len);  // few long paths: direct atomics
+            if (len >= SM_LONG_PATH) atomicMax(&mlen[b], len);
         }
     }
     __syncthreads();
     if (threadIdx.x < SM_NBUCKETS && hist[threadIdx.x]) {
         atomicAdd(&V.round_count[threadIdx.x], hist[threadIdx.x]);
         atomicAdd(&V.round_nodes[threadIdx.x], nodes[threadIdx.x]);
+        if (mlen[threadIdx.x]) atomicMax(&V.round_maxlen[threadIdx.x], mlen[threadIdx.x]);
     }
 }
 
@@ -746,7 +757,8 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}, {LP.v[0].bsum32, LP.v[1].bsum32}};
     launch_scan<uint32_t, OpAdd>(st, lb, nviews, N);
     hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
-    hipLaunchKernelGGL(k_meta, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_slotpix, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, N);
     hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP, piece_len);
     return hipGetLastError();
 }
