@@ -644,7 +644,8 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
 __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t plen) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.x];
-    __shared__ uint32_t sc[1024], sp[1024];
+    __shared__ unsigned long long sc[SCAN_BLOCK / 64];  // the block scan's per-wave totals
+    __shared__ uint32_t sp[1024];
     __shared__ uint32_t prev_win, prev_cut;
     // the bucket tables and each long bucket's first head, loaded once (a dependent global load
     // per bucket made this single-block kernel latency-bound: 89 us at C2)
@@ -673,49 +674,66 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
             prev_cut = 1u;
         }
         __syncthreads();
-        for (uint32_t c = p0; c < p1; c += 1024) {
-            const uint32_t p = c + threadIdx.x;
-            const SmPath path = p < p1 ? V.paths[p] : SmPath{0u, 0u};
-            const uint32_t len = path.len;
-            const uint32_t ns = (len + SM_PRE_SEG - 1) / SM_PRE_SEG;
-            const bool cut = len >= 2u * plen;
-            const uint32_t win = (path.head - hbase) / rwin;
-            // previous path's window / cut flag (the chunk's first thread: from the last chunk)
-            sp[threadIdx.x] = (win << 1) | (cut ? 1u : 0u);
+        // chunks of 4096 paths, 4 consecutive paths per thread, one shuffle-based block scan of
+        // (segments << 32 | items) per chunk
+        for (uint32_t c = p0; c < p1; c += 4 * 1024) {
+            const uint32_t pb = c + 4u * threadIdx.x;
+            uint32_t len[4], ns[4], np[4], win[4];
+            bool cut[4], start[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t p = pb + (uint32_t)i;
+                const SmPath path = p < p1 ? V.paths[p] : SmPath{hbase, 0u};
+                len[i] = path.len;
+                ns[i] = (len[i] + SM_PRE_SEG - 1) / SM_PRE_SEG;
+                cut[i] = len[i] >= 2u * plen;
+                win[i] = (path.head - hbase) / rwin;
+            }
+            // previous path's window / cut flag (thread 0: the last path of the previous chunk)
+            sp[threadIdx.x] = (win[3] << 1) | (cut[3] ? 1u : 0u);
             __syncthreads();
-            const uint32_t pv = threadIdx.x ? sp[threadIdx.x - 1] : ((prev_win << 1) | prev_cut);
-            __syncthreads();
-            const bool start = !cut && ((pv & 1u) || (pv >> 1) != win);
-            const uint32_t np = p < p1 ? (cut ? len / plen : (start ? 1u : 0u)) : 0u;
-            sc[threadIdx.x] = ns;
-            sp[threadIdx.x] = np;
-            __syncthreads();
+            uint32_t pv = threadIdx.x ? sp[threadIdx.x - 1] : ((prev_win << 1) | prev_cut);
+            uint32_t tns = 0, tnp = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                start[i] = !cut[i] && ((pv & 1u) || (pv >> 1) != win[i]);
+                np[i] = pb + (uint32_t)i < p1 ? (cut[i] ? len[i] / plen : (start[i] ? 1u : 0u)) : 0u;
+                pv = (win[i] << 1) | (cut[i] ? 1u : 0u);
+                tns += ns[i];
+                tnp += np[i];
+            }
+            unsigned long long tot;
+            const unsigned long long ex = block_exclusive_scan<unsigned long long, OpAdd>(
+                ((unsigned long long)tns << 32) | tnp, sc, &tot);
             if (threadIdx.x == 1023) {
-                prev_win = win;
-                prev_cut = cut ? 1u : 0u;
+                prev_win = win[3];
+                prev_cut = cut[3] ? 1u : 0u;
             }
-            for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scans
-                const uint32_t t = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0u;
-                const uint32_t u = threadIdx.x >= (unsigned)off ? sp[threadIdx.x - off] : 0u;
-                __syncthreads();
-                sc[threadIdx.x] += t;
-                sp[threadIdx.x] += u;
-                __syncthreads();
+            uint32_t seg = running + (uint32_t)(ex >> 32), item = prun + (uint32_t)ex;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t p = pb + (uint32_t)i;
+                if (p >= p1) break;
+                for (uint32_t q = 0; q < ns[i]; ++q) V.segtab[seg + q] = make_uint2(p - p0, q);
+                if (cut[i]) {
+                    for (uint32_t j = 0; j < np[i]; ++j) V.pieces[item + j] = make_uint4(p - p0, np[i] - 1u - j, np[i], seg - sbase);
+                } else if (start[i]) {
+                    V.pieces[item] = make_uint4(p - p0, 0u, 1u, 0u);
+                }
+                seg += ns[i];
+                item += np[i];
             }
-            const uint32_t start_seg = running + sc[threadIdx.x] - ns;
-            for (uint32_t q = 0; q < ns; ++q) V.segtab[start_seg + q] = make_uint2(p - p0, q);
-            const uint32_t pstart = prun + sp[threadIdx.x] - np;
-            if (cut) {
-                for (uint32_t i = 0; i < np; ++i) V.pieces[pstart + i] = make_uint4(p - p0, np - 1u - i, np, start_seg - sbase);
-            } else if (start) {
-                V.pieces[pstart] = make_uint4(p - p0, 0u, 1u, 0u);
-            }
-            running += sc[1023];
-            prun += sp[1023];
+            running += (uint32_t)(tot >> 32);
+            prun += (uint32_t)tot;
             __syncthreads();
             // count the paths of each run: every uncut path adds itself to the run it belongs to
             // (the latest item, which is a run start since this path is not cut)
-            if (p < p1 && !cut) atomicAdd(reinterpret_cast<uint32_t*>(V.pieces + (prun - sp[1023] + sp[threadIdx.x] - 1u)) + 3, 1u);
+            item = prun - (uint32_t)tot + (uint32_t)ex;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                item += np[i];
+                if (pb + (uint32_t)i < p1 && !cut[i]) atomicAdd(reinterpret_cast<uint32_t*>(V.pieces + (item - 1u)) + 3, 1u);
+            }
             __syncthreads();
         }
     }
