@@ -163,17 +163,22 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     MetaVec<CH> mv;
     if (n > 0) {
         load_meta<CH>(mv, meta32, lane, head + first, 1, n);
-        // pre-heavy light child rows (positions 0 .. hidx-1): the first two with unconditional
-        // loads (absent rows read row 0, an L2-resident dummy: no wait splits them); a third one
-        // (hidx == 3, a four-child node whose heavy child is the last) is loaded where it is used
+        // pre-heavy light child rows (positions 0 .. hidx-1): the first two issued together under
+        // wave-uniform branches (only present rows travel); a third one (hidx == 3, a four-child
+        // node whose heavy child is the last) is loaded where it is used
         double lr[CH][2][SPL];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            const int jj = j < n ? j : n - 1;
-            const uint32_t hidx = hi_hidx(mfield(mv, jj, 3));
+            const uint32_t hidx = j < n ? hi_hidx(mfield(mv, j, 3)) : 0u;
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
-                load_row<SPL>(U, (uint32_t)i < hidx ? mfield(mv, jj, 4 + i) : 0u, Dpad, lane, lr[j][i]);
+            for (int i = 0; i < 2; ++i) {
+                if ((uint32_t)i < hidx) {
+                    load_row<SPL>(U, mfield(mv, j, 4 + i), Dpad, lane, lr[j][i]);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) lr[j][i][q] = 0.0;
+                }
+            }
         }
         if constexpr (VOL) {  // cost rows already in Cst (k_vol_rows): needed by the aggregate only
             if (agg_mode) {

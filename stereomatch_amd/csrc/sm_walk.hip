@@ -53,8 +53,7 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
                                          double* __restrict__ U, const float* __restrict__ Cv, const WalkShared& sh,
                                          double (&xc)[SPL]) {
     // ---- all vector loads of the chunk
-    // light-child rows: unconditional loads (absent children read row 0, an L2-resident dummy) so
-    // that no wait splits the chunk's loads
+    // light-child rows: all issued before the chunk's one wait
     double lr[CH][2][SPL];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
@@ -64,8 +63,13 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint32_t i = (uint32_t)k + ((uint32_t)k >= hidx ? 1u : 0u);  // child position of light slot k
-            const uint32_t cs = i < nch ? mfield(mv, jj, 4 + (int)min(i, 3u)) : 0u;
-            load_row<SPL>(U, cs, Dpad, lane, lr[j][k]);
+            // wave-uniform branch: only present rows travel through L1 (~70% of nodes have none)
+            if (j < n && i < nch) {
+                load_row<SPL>(U, mfield(mv, jj, 4 + (int)min(i, 3u)), Dpad, lane, lr[j][k]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) lr[j][k][q] = 0.0;
+            }
         }
     }
     // ---- off-chain work: costs and edge factors of every node of the chunk
@@ -221,8 +225,7 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
         MetaVec<CH> nxt;
         if (nn > 0) load_meta<CH>(nxt, meta32, lane, nc0, 1, nn);  // prefetch the next chunk's metadata
         // rows of the chunk (contiguous slots) and, for path heads, the parent's finished A row
-        // (earlier round); other nodes load their own row again (L1/L2 hit) so the count of
-        // loads is fixed
+        // (earlier round)
         double u[CH][SPL], xp[CH][SPL];
         uint32_t par[CH];
 #pragma unroll
@@ -232,7 +235,13 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
             par[j] = mfield(cur, jj, 1);
             const bool head_j = par[j] == SM_NONE || par[j] != slot - 1u;
             load_row<SPL>(V.U, slot, Dpad, lane, u[j]);
-            load_row<SPL>(head_j && par[j] != SM_NONE ? V.A : V.U, head_j && par[j] != SM_NONE ? par[j] : slot, Dpad, lane, xp[j]);
+            if (head_j && par[j] != SM_NONE) {  // wave-uniform: only path heads read their parent's row
+                load_row<SPL>(V.A, par[j], Dpad, lane, xp[j]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) xp[j][q] = 0.0;
+            }
+
         }
         double S[CH], S2[CH];
 #pragma unroll
