@@ -40,6 +40,18 @@
 #endif
 
 
+// One explicit vmcnt(0) per chunk, right after the chunk's loads (rows, image records, next
+// metadata) are issued.  gfx9 counts loads and stores in one counter and the compiler treats
+// their completion as unordered: any wait for a load while a store is pending becomes vmcnt(0).
+// Letting the compiler place the waits put such full waits behind the chunk's own stores (and
+// behind a metadata prefetch issued first), i.e. two memory latencies per chunk.  Draining here
+// costs one: the previous chunk's stores were issued a whole chunk earlier.
+__device__ __forceinline__ void walk_vm_drain() {
+#ifndef SM_WALK_NO_DRAIN
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
+}
+
 // ---------------------------------------------------------------------------------------------
 // up pass
 // ---------------------------------------------------------------------------------------------
@@ -51,7 +63,8 @@ template <int SPL, int CH, bool ROOT, bool VOL>
 __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, int view, int lane, int W, int Dpad,
                                          int dbase, int dend, const uint2* __restrict__ own, const uint2* __restrict__ oth,
                                          double* __restrict__ U, const float* __restrict__ Cv, const WalkShared& sh,
-                                         double (&xc)[SPL]) {
+                                         double (&xc)[SPL], MetaVec<CH>& nxt, const uint32_t* __restrict__ meta32, int ntop,
+                                         int nn) {
     // ---- all vector loads of the chunk
     // light-child rows: all issued before the chunk's one wait
     double lr[CH][2][SPL];
@@ -78,9 +91,16 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
     if constexpr (VOL) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) load_cost_row<SPL>(Cv, (uint32_t)(top - (j < n ? j : n - 1)), Dpad, lane, c[j]);
+        if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);
+        walk_vm_drain();
     } else {
         ImgRecs<SPL, CH> rec;
         load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+        // the next chunk's metadata, issued behind this chunk's loads: it completes with them, so
+        // the next chunk starts without a wait (a prefetch issued first made the chunk's first
+        // wait a vmcnt(0) over the prefetch and the previous chunk's stores)
+        if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);
+        walk_vm_drain();
         chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
     }
 #pragma unroll
@@ -168,19 +188,21 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
     int n = min(CH, top - head + 1);
     MetaVec<CH> cur;
     load_meta<CH>(cur, meta32, lane, top, -1, n);
+    walk_vm_drain();  // nothing pending on loop entry: the loop top then needs no wait at all
     while (true) {
         const int ntop = top - CH;
         const int nn = ntop >= head ? min(CH, ntop - head + 1) : 0;
-        MetaVec<CH> nxt;
-        if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);  // prefetch the next chunk's metadata
+        MetaVec<CH> nxt;  // the next chunk's metadata: loaded inside up_chunk
         bool root = false;
 #pragma unroll
         for (int j = 0; j < CH; ++j) root |= j < n && hi_nch(mfield(cur, j, 3)) == 4u;
         const float* __restrict__ Cv = view ? Cv1 : Cv0;
         if (root)
-            up_chunk<SPL, CH, true, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc);
+            up_chunk<SPL, CH, true, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc, nxt, meta32,
+                                         ntop, nn);
         else
-            up_chunk<SPL, CH, false, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc);
+            up_chunk<SPL, CH, false, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc, nxt, meta32,
+                                          ntop, nn);
         if (nn == 0) break;
         cur = nxt;
         top = ntop;
@@ -219,11 +241,11 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
     int n = min(CH, len);
     MetaVec<CH> cur;
     load_meta<CH>(cur, meta32, lane, c0, 1, n);
+    walk_vm_drain();  // nothing pending on loop entry: the loop top then needs no wait at all
     while (true) {
         const int nc0 = c0 + CH;
         const int nn = nc0 < head + len ? min(CH, head + len - nc0) : 0;
         MetaVec<CH> nxt;
-        if (nn > 0) load_meta<CH>(nxt, meta32, lane, nc0, 1, nn);  // prefetch the next chunk's metadata
         // rows of the chunk (contiguous slots) and, for path heads, the parent's finished A row
         // (earlier round)
         double u[CH][SPL], xp[CH][SPL];
@@ -243,6 +265,9 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
             }
 
         }
+        // the next chunk's metadata, behind this chunk's row loads (see up_chunk)
+        if (nn > 0) load_meta<CH>(nxt, meta32, lane, nc0, 1, nn);
+        walk_vm_drain();
         double S[CH], S2[CH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -297,15 +322,21 @@ static WalkView to_view(const WalkArgs& a, int v) {
     return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v]};
 }
 
+// A/B knob: extra dynamic LDS per block (limits walker occupancy; experiments only)
+static size_t walk_lds_pad() {
+    static const char* e = getenv("SM_WALK_LDS_PAD");
+    return e ? (size_t)atoi(e) : 0;
+}
+
 template <int SPL, int CH>
 static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a) {
     if (a.vol)
-        hipLaunchKernelGGL((k_up_walk<SPL, CH, true>), g, dim3(256), 0, st, to_view(a, 0), to_view(a, 1),
+        hipLaunchKernelGGL((k_up_walk<SPL, CH, true>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
                            a.dglob0, a.Cst[0], a.Cst[1]);
     else
-        hipLaunchKernelGGL((k_up_walk<SPL, CH, false>), g, dim3(256), 0, st, to_view(a, 0), to_view(a, 1),
+        hipLaunchKernelGGL((k_up_walk<SPL, CH, false>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
                            a.dglob0, a.Cst[0], a.Cst[1]);
@@ -313,7 +344,7 @@ static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a) {
 
 template <int SPL, int CH>
 static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all) {
-    hipLaunchKernelGGL((k_down_walk<SPL, CH>), g, dim3(256), 0, st, to_view(a, 0), to_view(a, 1),
+    hipLaunchKernelGGL((k_down_walk<SPL, CH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                        a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all);
 }
