@@ -28,15 +28,18 @@
 #include "sm_walk_util.h"
 
 // paths per wave work item (a bucket's paths occupy consecutive slots: one contiguous range)
-#ifndef WALK_PPW
-#define WALK_PPW 8
+#ifndef WALK_PPW_UP
+#define WALK_PPW_UP 6
+#endif
+#ifndef WALK_PPW_DN
+#define WALK_PPW_DN 4
 #endif
 // chunk sizes (nodes per software-pipeline stage) of the short-path walkers, per SPL
 #ifndef WALK_UP_CH2
 #define WALK_UP_CH2 4
 #endif
 #ifndef WALK_DN_CH2
-#define WALK_DN_CH2 4
+#define WALK_DN_CH2 8
 #endif
 
 
@@ -168,11 +171,11 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
-    // work item: WALK_PPW consecutive paths of the bucket = one contiguous slot range (the
+    // work item: WALK_PPW_UP consecutive paths of the bucket = one contiguous slot range (the
     // recurrence restarts by itself at every path bottom: a leaf has no heavy child)
-    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW);
+    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW_UP);
     if (pi0 >= V.npaths) return;
-    const int pi1 = min(pi0 + WALK_PPW, V.npaths);
+    const int pi1 = min(pi0 + WALK_PPW_UP, V.npaths);
     const SmPath* __restrict__ pp = view ? paths1 : paths0;
     const int head = (int)uniform(pp[pi0].head);
     const int len = (int)uniform(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
@@ -225,11 +228,11 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
-    // work item: WALK_PPW consecutive paths = one contiguous slot range, root side first; a node
+    // work item: WALK_PPW_DN consecutive paths = one contiguous slot range, root side first; a node
     // is a path head iff its parent is not the previous slot
-    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW);
+    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW_DN);
     if (pi0 >= V.npaths) return;
-    const int pi1 = min(pi0 + WALK_PPW, V.npaths);
+    const int pi1 = min(pi0 + WALK_PPW_DN, V.npaths);
     const SmPath* __restrict__ pp = view ? paths1 : paths0;
     const int head = (int)uniform(pp[pi0].head);
     const int len = (int)uniform(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
@@ -352,7 +355,7 @@ static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
-    const int items = (np + WALK_PPW - 1) / WALK_PPW;
+    const int items = (np + WALK_PPW_UP - 1) / WALK_PPW_UP;
     const dim3 g((items + 3) / 4, 2);
     if (long_paths) {
         switch (spl) {
@@ -373,7 +376,7 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
 static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, int store_all, bool long_paths) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
-    const int items = (np + WALK_PPW - 1) / WALK_PPW;
+    const int items = (np + WALK_PPW_DN - 1) / WALK_PPW_DN;
     const dim3 g((items + 3) / 4, 2);
     if (long_paths) {
         switch (spl) {
