@@ -67,7 +67,7 @@ struct sm_ctx {
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
-    DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2], slot2pix[2];
+    DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2], slot2pix[2], prec[2];
     DevBuf pieces[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
     DevBuf cnw[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
@@ -358,6 +358,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         CHECK(ensure(ctx, ctx->nslot[v], N * 4));
         CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
         CHECK(ensure(ctx, ctx->slot2pix[v], N * 4));
+        CHECK(ensure(ctx, ctx->prec[v], N * 8));
         z.add(ctx->plen[v].p, N * 4);  // lengths past the last path stay 0
         z.add(ctx->ccount[v].p, 16);
         z.add(ctx->rounds[v].p, RREC * 4);
@@ -395,6 +396,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         L.nslot = P<uint32_t>(ctx->nslot[v]);
         L.slotpix = P<uint32_t>(ctx->slotpix[v]);
         L.slot2pix = P<uint32_t>(ctx->slot2pix[v]);
+        L.prec = P<uint64_t>(ctx->prec[v]);
         uint32_t* R = P<uint32_t>(ctx->rounds[v]);
         L.round_begin = R;
         L.round_count = R + SM_NBUCKETS + 1;
@@ -856,7 +858,7 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cnw[v],
                          &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
                          &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
-                         &ctx->nslot[v], &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->pieces[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
+                         &ctx->nslot[v], &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->prec[v], &ctx->pieces[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }

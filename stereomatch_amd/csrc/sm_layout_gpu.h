@@ -58,6 +58,7 @@ struct LayoutView {
     uint32_t* nslot;         // [preorder] -> slot
     uint32_t* slotpix;       // [pixel] -> slot
     uint32_t* slot2pix;      // [slot] -> pixel
+    uint64_t* prec;          // [pixel] -> packed record (k_slotpix)
     uint32_t* round_count;   // SM_NBUCKETS
     uint32_t* round_cursor;  // SM_NBUCKETS
     uint32_t* round_begin;   // SM_NBUCKETS + 1

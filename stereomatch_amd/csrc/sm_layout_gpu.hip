@@ -473,9 +473,18 @@ __global__ void k_newslot(LayoutPair LP, int N) {
     if (s == head) V.paths[P].head = nh;
 }
 
-// slot of every pixel and pixel of every slot (one random gather and one scattered 4-byte store
-// per pixel), so that k_meta runs in slot order: consecutive slots walk heavy paths, i.e.
-// neighbouring pixels, and the 32-byte metadata records are written contiguously
+// Per pixel: its slot, the pixel of every slot, and one packed 64-bit record
+//   slot:32 | adj:4 | pdir+1:3 | heavy+1:3 | wR:10 | wD:10
+// so that k_meta, which runs in slot order (consecutive slots walk heavy paths, i.e. neighbouring
+// pixels, and the 32-byte metadata records are written contiguously), reads one word for itself
+// and one per tree neighbour instead of ~15 scattered byte / short / word loads.
+#define PR_SLOT(r) ((uint32_t)(r))
+#define PR_ADJ(r) ((uint32_t)((r) >> 32) & 15u)
+#define PR_PDIR(r) ((int)((uint32_t)((r) >> 36) & 7u) - 1)
+#define PR_HEAVY(r) ((int)((uint32_t)((r) >> 39) & 7u) - 1)
+#define PR_WR(r) ((uint32_t)((r) >> 42) & 1023u)
+#define PR_WD(r) ((uint32_t)((r) >> 52) & 1023u)
+
 __global__ void k_slotpix(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
@@ -485,6 +494,9 @@ __global__ void k_slotpix(LayoutPair LP, int W, int H) {
     const uint32_t slot = V.nslot[V.pre[v]];
     V.slotpix[v] = slot;
     V.slot2pix[slot] = v;
+    V.prec[v] = (uint64_t)slot | ((uint64_t)V.adj[v] << 32) | ((uint64_t)(V.pdir[v] + 1) << 36) |
+                ((uint64_t)(V.heavy[v] + 1) << 39) | ((uint64_t)(V.wR[v] & 1023u) << 42) |
+                ((uint64_t)(V.wD[v] & 1023u) << 52);
 }
 
 // per-slot metadata in slot numbering: pixel, parent slot, child weights and slots in
@@ -496,38 +508,49 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
     const LayoutView& V = LP.v[blockIdx.y];
     uint32_t nlight = 0;
     for (uint32_t slot = blockIdx.x * 256 + threadIdx.x; slot < (uint32_t)N; slot += META_BLOCKS * 256) {
-    const uint32_t v = V.slot2pix[slot];
-    const uint32_t adj = V.adj[v];
-    const int pd = V.pdir[v];
-    const int hv = V.heavy[v];
-    uint64_t ck[4];
-    uint32_t cs[4] = {SM_NONE, SM_NONE, SM_NONE, SM_NONE}, cw[4] = {0, 0, 0, 0};
-    int cq[4];
-    int nch = 0;
-    for (int k = 0; k < 4; ++k) {
-        if (!(adj & (1u << k)) || k == pd) continue;
-        ck[nch] = key_dir(V.wR, V.wD, W, v, k);
-        cq[nch] = k;
-        ++nch;
-    }
-    for (int i = 1; i < nch; ++i)  // descending key
-        for (int j = i; j > 0 && ck[j] > ck[j - 1]; --j) {
-            const uint64_t tk = ck[j]; ck[j] = ck[j - 1]; ck[j - 1] = tk;
-            const int tq = cq[j]; cq[j] = cq[j - 1]; cq[j - 1] = tq;
+        const uint32_t v = V.slot2pix[slot];
+        const uint64_t me = V.prec[v];
+        const uint32_t adj = PR_ADJ(me);
+        const int pd = PR_PDIR(me), hv = PR_HEAVY(me);
+        // the tree neighbours' records: slot, and the weight of the edge to v for left / up ones
+        uint64_t nr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nr[k] = (adj & (1u << k)) ? V.prec[nbr_of(v, k, W)] : 0ull;
+        uint64_t ck[4];
+        uint32_t cs[4] = {SM_NONE, SM_NONE, SM_NONE, SM_NONE}, cw[4] = {0, 0, 0, 0};
+        int cq[4];
+        int nch = 0;
+        uint32_t wp = 0, parent = SM_NONE;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!(adj & (1u << k))) continue;
+            // key_dir without the weight loads: right / down edges are v's own, left / up the neighbour's
+            const uint32_t w = k == 0 ? PR_WR(me) : k == 1 ? PR_WD(me) : k == 2 ? PR_WR(nr[k]) : PR_WD(nr[k]);
+            const uint32_t a = k == 0 || k == 1 ? v : nbr_of(v, k, W);
+            const uint64_t key = sm_edge_key(w, a, (uint32_t)(k & 1));
+            if (k == pd) {
+                wp = (uint32_t)(key >> 33);
+                parent = PR_SLOT(nr[k]);
+                continue;
+            }
+            ck[nch] = key;
+            cq[nch] = k;
+            cs[nch] = PR_SLOT(nr[k]);
+            ++nch;
         }
-    uint32_t hidx = 0, has_light = 0;
-    for (int i = 0; i < nch; ++i) {
-        cw[i] = (uint32_t)(ck[i] >> 33);
-        cs[i] = V.slotpix[nbr_of(v, cq[i], W)];
-        if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
-    }
-    uint32_t wp = 0, parent = SM_NONE;
-    if (pd >= 0) {
-        wp = (uint32_t)(key_dir(V.wR, V.wD, W, v, pd) >> 33);
-        parent = V.slotpix[nbr_of(v, pd, W)];
-    }
-    V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
-    nlight += has_light;
+        for (int i = 1; i < nch; ++i)  // descending key
+            for (int j = i; j > 0 && ck[j] > ck[j - 1]; --j) {
+                const uint64_t tk = ck[j]; ck[j] = ck[j - 1]; ck[j - 1] = tk;
+                const int tq = cq[j]; cq[j] = cq[j - 1]; cq[j - 1] = tq;
+                const uint32_t ts = cs[j]; cs[j] = cs[j - 1]; cs[j - 1] = ts;
+            }
+        uint32_t hidx = 0, has_light = 0;
+        for (int i = 0; i < nch; ++i) {
+            cw[i] = (uint32_t)(ck[i] >> 33);
+            if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
+        }
+        V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
+        nlight += has_light;
     }
     __shared__ uint32_t nl;
     if (threadIdx.x == 0) nl = 0;
