@@ -7,7 +7,9 @@
 
 #define SM_MAX_ROUNDS 32  // light depth <= log2(N) < 31
 #define SM_NBUCKETS (2 * SM_MAX_ROUNDS)  // per round: [long paths | short paths]
+#ifndef SM_LONG_PATH
 #define SM_LONG_PATH 32   // paths of >= this many nodes go to the long-path chain engine (sm_chain.hip)
+#endif
 #define SM_PRE_SEG 32     // nodes per k_up_pre block (segment table granularity)
 // A long path of >= 2*P nodes is cut into len/P pieces of P nodes (the bottom piece takes the
 // remainder); the pieces' chains run concurrently from guessed inputs and are then repaired

@@ -36,7 +36,7 @@
 #endif
 // chunk sizes (nodes per software-pipeline stage) of the short-path walkers, per SPL
 #ifndef WALK_UP_CH2
-#define WALK_UP_CH2 4
+#define WALK_UP_CH2 3
 #endif
 #ifndef WALK_DN_CH2
 #define WALK_DN_CH2 8
