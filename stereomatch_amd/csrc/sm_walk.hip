@@ -39,7 +39,7 @@
 #define WALK_UP_CH2 3
 #endif
 #ifndef WALK_DN_CH2
-#define WALK_DN_CH2 8
+#define WALK_DN_CH2 6
 #endif
 
 
