@@ -148,7 +148,7 @@ typedef struct {
 sm_status sm_get_filter_stats(sm_ctx* ctx, sm_filter_stats* out);
 
 /* Per kernel family of the tree filter (k_up_walk, k_up_pre, k_up_chain, k_down_chain,
- * k_down_walk): launches, summed HIP-event duration (ms) over the last call, voxels processed
+ * k_down_walk, k_long_costs -- the long paths' AGD cost rows, computed up front): launches, summed HIP-event duration (ms) over the last call, voxels processed
  * (path nodes x disparities, both views) and algorithmic bytes per voxel (DESIGN.md
  * "Roofline accounting").  Returns the number of entries written (<= n). */
 typedef struct {

@@ -90,7 +90,7 @@ struct sm_ctx {
     std::vector<hipEvent_t> sev;  // stream-ordering events of the filter rounds
     int nsev = 0;
     sm_filter_stats stats{};
-    sm_kernel_stat kstats[5]{};
+    sm_kernel_stat kstats[8]{};  // >= KF_N
     float stage_ms[7] = {0};
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -510,9 +510,12 @@ sm_status ensure_events(sm_ctx* ctx, std::vector<hipEvent_t>& evs, size_t n) {
 
 // kernel families of the tree filter and their algorithmic bytes per voxel (SURVEY.md 8(d):
 // K1 cost write 4 B, K2 up 8 B, K3 down 8 B, K4 WTA 4 B; DESIGN.md "Roofline accounting")
-enum { KF_UP_WALK, KF_UP_PRE, KF_UP_CHAIN, KF_DOWN_CHAIN, KF_DOWN_WALK, KF_N };
-const char* const kf_name[KF_N] = {"k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk"};
-const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0};
+// K1 of the long paths is k_long_costs when the costs are computed up front (then k_up_pre's
+// launches account no bytes), else k_up_pre
+enum { KF_UP_WALK, KF_UP_PRE, KF_UP_CHAIN, KF_DOWN_CHAIN, KF_DOWN_WALK, KF_LONG_COST, KF_N };
+const char* const kf_name[KF_N] = {"k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk", "k_long_costs"};
+const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0, 4.0};
+static bool kf_up(int f) { return f <= KF_UP_CHAIN || f == KF_LONG_COST; }
 
 // A timed launch of family f on stream s.  HIP events bracket the launch, but consecutive timed
 // launches on the filter stream share the event between them (the end of one is the start of
@@ -525,7 +528,9 @@ const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0};
 #define SM_TIMED_MIN_VOX 0.0
 #endif
 template <class F>
-sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch) {
+sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch, double acct = -1.0) {
+    // vox: voxels of the launch (0: nothing to launch); acct: voxels its algorithmic bytes count
+    // (default vox)
     static const bool off = getenv("SM_NO_KTIMING") != nullptr;  // A/B: no events at all
     if (vox <= 0) return SM_OK;                                   // empty bucket: nothing to launch
     if (off || vox < SM_TIMED_MIN_VOX) {
@@ -544,7 +549,7 @@ sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch) {
     HIPC(launch());
     HIPC(hipEventRecord(ctx->fev[ctx->nfev], s));
     ctx->fam.push_back(f);
-    ctx->fam_vox.push_back(vox);
+    ctx->fam_vox.push_back(acct < 0 ? vox : acct);
     ctx->fam_ev.push_back(std::make_pair(start, ctx->nfev));
     ctx->nfev += 1;
     ctx->ev_open = true;
@@ -584,7 +589,7 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
     set_bucket(ctx, a, r, true, nviews);
     const WalkArgs al = a;
     const double vl = bucket_voxels(ctx, r, true, nviews, a.dcall);
-    CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }));
+    CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, al.pre_costs ? 0.0 : vl));
     CHECK(timed(ctx, ctx->st2, KF_UP_CHAIN, vl, [&] { return launch_up_chain(ctx->st2, al, spl); }));
     return SM_OK;
 }
@@ -676,6 +681,33 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     ctx->fam_vox.clear();
     ctx->fam_ev.clear();
     ctx->ev_open = false;
+    // AGD cost rows of every long-path slot in one launch up front (SM_NO_PRECOST: per round in
+    // k_up_pre, A/B).  Bucket slots are contiguous and bucket-major: long bucket 2r of a view starts
+    // after the nodes of all lower buckets.
+    a.pre_costs = 0;
+    static const bool no_precost = getenv("SM_NO_PRECOST") != nullptr;
+    if (!a.vol && !no_precost) {
+        CostRanges cr{};
+        for (int v = 0; v < nviews; ++v) {
+            const auto& L = ctx->layout[v];
+            uint32_t s0 = 0;
+            for (uint32_t b = 0; b < 2 * L.nrounds && b < (uint32_t)L.nodes.size(); ++b) {
+                if ((b & 1) == 0 && L.nodes[b] > 0 && cr.n < SM_COST_RANGES) {
+                    cr.view[cr.n] = (uint32_t)v;
+                    cr.start[cr.n] = s0;
+                    cr.len[cr.n] = L.nodes[b];
+                    ++cr.n;
+                }
+                s0 += L.nodes[b];
+            }
+        }
+        if (cr.n < SM_COST_RANGES) {  // else (> 31 rounds with long paths: never) k_up_pre computes them
+            double vox = 0;
+            for (int i = 0; i < cr.n; ++i) vox += (double)cr.len[i] * D;
+            CHECK(timed(ctx, ctx->st, KF_LONG_COST, vox, [&] { return launch_long_costs(ctx->st, a, spl, cr); }));
+            a.pre_costs = 1;
+        }
+    }
     for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest first
     CHECK(join(ctx, ctx->st, ctx->st2));
     HIPC(hipEventRecord(ctx->ev[6], ctx->st));  // up | down boundary (stage times)
@@ -705,14 +737,15 @@ sm_status collect_filter_stats(sm_ctx* ctx) {
         float ms;
         HIPC(hipEventElapsedTime(&ms, ctx->fev[ctx->fam_ev[k].first], ctx->fev[ctx->fam_ev[k].second]));
         const int f = ctx->fam[k];
-        if (ctx->fam_vox[k] > 0) ks[f].launches += 1;  // a bucket without paths launches nothing
+        ks[f].launches += 1;  // only launches are recorded (a bucket without paths launches nothing)
         ks[f].ms += ms;
         ks[f].voxels += ctx->fam_vox[k];
     }
+    static_assert(sizeof(ctx->kstats) >= sizeof(ks), "kstats holds every family");
     memcpy(ctx->kstats, ks, sizeof(ks));
     sm_filter_stats fs{};
     for (int f = 0; f < KF_N; ++f) {
-        const bool up = f <= KF_UP_CHAIN;
+        const bool up = kf_up(f);
         (up ? fs.up_ms : fs.down_ms) += ks[f].ms;
         (up ? fs.up_bytes : fs.down_bytes) += ks[f].voxels * ks[f].bytes_per_voxel;
         (up ? fs.up_launches : fs.down_launches) += ks[f].launches;

@@ -289,6 +289,73 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_long_costs: the AGD cost rows of every long-path slot of every round, in one launch before
+// the up pass (they depend on nothing but the images and the layout).  k_up_pre then only folds
+// the pre-heavy light children round by round, and the chain helpers read the rows as before.
+// One block = 4 waves x CH consecutive slots of one range.
+// ---------------------------------------------------------------------------------------------
+template <int SPL, int CH>
+__global__ __launch_bounds__(256) void k_long_costs(const uint32_t* __restrict__ meta0, const uint32_t* __restrict__ meta1,
+                                                    const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec,
+                                                    const float* __restrict__ atab_g, int W, int Dpad, int dcall, int dglob0,
+                                                    float* __restrict__ Cst0, float* __restrict__ Cst1, CostRanges R) {
+    __shared__ float atab[SM_MAX_W + 1];
+    for (int i = threadIdx.x; i <= SM_MAX_W; i += blockDim.x) atab[i] = atab_g[i];
+    __syncthreads();
+    int ri = 0;
+    while (ri + 1 < R.n && R.bfirst[ri + 1] <= blockIdx.x) ++ri;  // uniform
+    const int view = (int)R.view[ri];
+    const int lane = threadIdx.x & 63, wv = (int)uniform(threadIdx.x >> 6);
+    const uint32_t off = (blockIdx.x - R.bfirst[ri]) * (4 * CH) + (uint32_t)(wv * CH);
+    if (off >= R.len[ri]) return;
+    const int first = (int)(R.start[ri] + off);
+    const int n = (int)min((uint32_t)CH, R.len[ri] - off);
+    const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
+    const uint2* __restrict__ own = view ? Rrec : Lrec;
+    const uint2* __restrict__ oth = view ? Lrec : Rrec;
+    float* __restrict__ Cst = view ? Cst1 : Cst0;
+    const int dbase = dglob0 + lane * SPL, dend = dglob0 + dcall;
+    MetaVec<CH> mv;
+    load_meta<CH>(mv, meta32, lane, first, 1, n);
+    ImgRecs<SPL, CH> rec;
+    load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+    float c[CH][SPL];
+    chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, atab, c);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        if (j < n) {
+            float* p = Cst + (size_t)(first + j) * Dpad + lane * SPL;
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) p[k] = c[j][k];
+        }
+    }
+}
+
+template <int SPL, int CH>
+static void long_costs_launch(hipStream_t st, const WalkArgs& a, const CostRanges& r, unsigned nblocks) {
+    hipLaunchKernelGGL((k_long_costs<SPL, CH>), dim3(nblocks), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(a.meta[0]),
+                       reinterpret_cast<const uint32_t*>(a.meta[1]), a.Lrec, a.Rrec, a.atab, a.W, a.Dpad, a.dcall, a.dglob0,
+                       a.Cst[0], a.Cst[1], r);
+}
+
+hipError_t launch_long_costs(hipStream_t st, const WalkArgs& a, int spl, CostRanges r) {
+    const int ch = spl == 4 ? 4 : 8;  // nodes per wave
+    uint32_t nb = 0;
+    for (int i = 0; i < r.n; ++i) {
+        r.bfirst[i] = nb;
+        nb += (r.len[i] + 4u * ch - 1) / (4u * ch);
+    }
+    r.bfirst[r.n] = nb;
+    if (nb == 0) return hipSuccess;
+    switch (spl) {
+        case 1: long_costs_launch<1, 8>(st, a, r, nb); break;
+        case 2: long_costs_launch<2, 8>(st, a, r, nb); break;
+        default: long_costs_launch<4, 4>(st, a, r, nb); break;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Group ring.  Chain node j (0 = first node the chain visits) belongs to group g = j / G; group g
 // is staged in LDS slot g % NS by helper (g % NH), which holds its next group's rows in registers
 // while it waits for the slot -- so the lead time of the global loads is ~NH groups of chain time,
@@ -1642,7 +1709,7 @@ static void up_pre_launch_k(hipStream_t st, const WalkArgs& a) {
 
 template <int SPL, int CH>
 static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
-    if (a.vol)
+    if (a.vol || a.pre_costs)  // cost rows already in Cst
         up_pre_launch_k<SPL, CH, true>(st, a);
     else
         up_pre_launch_k<SPL, CH, false>(st, a);
