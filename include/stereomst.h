@@ -148,9 +148,11 @@ typedef struct {
 sm_status sm_get_filter_stats(sm_ctx* ctx, sm_filter_stats* out);
 
 /* Per kernel family of the tree filter (k_up_walk, k_up_pre, k_up_chain, k_down_chain,
- * k_down_walk, k_long_costs -- the long paths' AGD cost rows, computed up front): launches, summed HIP-event duration (ms) over the last call, voxels processed
- * (path nodes x disparities, both views) and algorithmic bytes per voxel (DESIGN.md
- * "Roofline accounting").  Returns the number of entries written (<= n). */
+ * k_down_walk, k_long_costs -- the long paths' AGD cost rows, computed up front): launches,
+ * summed HIP-event duration (ms) over the last call, voxels processed (path nodes x
+ * disparities, both views) and algorithmic bytes per voxel (DESIGN.md "Roofline accounting").
+ * Only timed families report (see sm_set_kernel_timing).  Returns the number of entries
+ * written (<= n). */
 typedef struct {
     char name[32];
     int launches;
@@ -159,6 +161,12 @@ typedef struct {
     double bytes_per_voxel;
 } sm_kernel_stat;
 int sm_get_kernel_stats(sm_ctx* ctx, sm_kernel_stat* out, int n);
+
+/* Which kernel families the following calls time with HIP events: bit i = entry i of
+ * sm_get_kernel_stats (default: all).  Each timed launch costs one event record (~2 us of
+ * GPU time per launch at C2); untimed families launch back to back.  No reference
+ * counterpart: measurement plumbing of this library. */
+sm_status sm_set_kernel_timing(sm_ctx* ctx, unsigned family_mask);
 
 /* Multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------- */
 #define SM_UNIQUE_ID_BYTES 128

@@ -80,6 +80,7 @@ def lib():
         "sm_stage_times": ([vp, vp, ci], ci),
         "sm_get_filter_stats": ([vp, ctypes.POINTER(SmFilterStats)], ci),
         "sm_get_kernel_stats": ([vp, ctypes.POINTER(SmKernelStat), ci], ci),
+        "sm_set_kernel_timing": ([vp, ctypes.c_uint], ci),
         "sm_comm_unique_id": ([vp], ci),
         "sm_comm_init": ([vp, ci, ci, vp], ci),
         "sm_comm_destroy": ([vp], ci),
@@ -210,6 +211,16 @@ class Context:
         n = lib().sm_get_kernel_stats(self.h, buf, 8)
         return {buf[i].name.decode(): dict(launches=buf[i].launches, ms=buf[i].ms, voxels=buf[i].voxels,
                                            bytes_per_voxel=buf[i].bytes_per_voxel) for i in range(n)}
+
+    def set_kernel_timing(self, families=None):
+        """Time only these kernel families with HIP events (names as in kernel_stats(); None = all)."""
+        mask = 0xFFFFFFFF
+        if families is not None:
+            names = list(self.kernel_stats().keys())
+            mask = 0
+            for f in families:
+                mask |= 1 << names.index(f)
+        self._check(lib().sm_set_kernel_timing(self.h, ctypes.c_uint(mask)))
 
     # -- stages ---------------------------------------------------------------------------
     def cost_volume(self, left, right, d0, D):

@@ -91,6 +91,7 @@ struct sm_ctx {
     int nsev = 0;
     sm_filter_stats stats{};
     sm_kernel_stat kstats[8]{};  // >= KF_N
+    unsigned ktiming = ~0u;      // families timed with events (sm_set_kernel_timing)
     float stage_ms[7] = {0};
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -533,7 +534,7 @@ sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch, doubl
     // (default vox)
     static const bool off = getenv("SM_NO_KTIMING") != nullptr;  // A/B: no events at all
     if (vox <= 0) return SM_OK;                                   // empty bucket: nothing to launch
-    if (off || vox < SM_TIMED_MIN_VOX) {
+    if (off || vox < SM_TIMED_MIN_VOX || !((ctx->ktiming >> f) & 1u)) {
         HIPC(launch());
         ctx->ev_open = false;
         return SM_OK;
@@ -1091,10 +1092,20 @@ int sm_stage_times(sm_ctx* ctx, float* out, int n) {
     return k;
 }
 
+sm_status sm_set_kernel_timing(sm_ctx* ctx, unsigned family_mask) {
+    if (!ctx) return SM_ERR_ARG;
+    ctx->ktiming = family_mask;
+    return SM_OK;
+}
+
 int sm_get_kernel_stats(sm_ctx* ctx, sm_kernel_stat* out, int n) {
     if (!ctx || !out) return 0;
     const int k = n < KF_N ? n : KF_N;
-    for (int i = 0; i < k; ++i) out[i] = ctx->kstats[i];
+    for (int i = 0; i < k; ++i) {
+        out[i] = ctx->kstats[i];
+        snprintf(out[i].name, sizeof(out[i].name), "%s", kf_name[i]);  // also before the first call
+        out[i].bytes_per_voxel = kf_bytes[i];
+    }
     return k;
 }
 
