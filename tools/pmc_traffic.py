@@ -1,7 +1,8 @@
 """Per-kernel-family HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE, run
 separately as MI355X_MICROARCH.md "rocprofv3 PMC slots" requires) of `bench.py --steps S --warmup W`.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <frames> [out.json]
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <frames|auto> [out.json]
+(auto: frames = dispatches of k_prep, one per frame, in the fetch pass)
 
 FETCH_SIZE / WRITE_SIZE are read as KiB per dispatch.  On gfx950 FETCH_SIZE reports half the bytes
 of a 16-B/lane streaming read (MI355X_MICROARCH.md "HBM"), so fetch bytes are doubled; the write
@@ -16,6 +17,18 @@ from collections import defaultdict
 
 FAMILIES = ["k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk", "k_long_costs", "k_median"]
 
+
+
+def frames_of(d):
+    """Frames in a rocprofv3 counter-collection directory: k_prep runs once per frame."""
+    n = 0
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        seen = set()
+        for r in csv.DictReader(open(f)):
+            if r["Kernel_Name"].startswith("k_prep") and r.get("Dispatch_Id") not in seen:
+                seen.add(r.get("Dispatch_Id"))
+        n += len(seen)
+    return n
 
 def family(name):
     base = name.split("(")[0].replace("void ", "").split("<")[0].strip()
@@ -39,7 +52,8 @@ def load(d, counter):
 
 
 def main():
-    fdir, wdir, frames = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    fdir, wdir = sys.argv[1], sys.argv[2]
+    frames = int(sys.argv[3]) if sys.argv[3] != "auto" else frames_of(fdir)
     out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
     fetch, nf = load(fdir, "FETCH_SIZE")
     write, nw = load(wdir, "WRITE_SIZE")
