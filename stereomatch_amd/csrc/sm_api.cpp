@@ -686,7 +686,7 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     // k_up_pre, A/B).  Bucket slots are contiguous and bucket-major: long bucket 2r of a view starts
     // after the nodes of all lower buckets.
     a.pre_costs = 0;
-    static const bool no_precost = getenv("SM_NO_PRECOST") != nullptr;
+    const bool no_precost = getenv("SM_NO_PRECOST") != nullptr;  // read per call: tests switch it
     if (!a.vol && !no_precost) {
         CostRanges cr{};
         for (int v = 0; v < nviews; ++v) {

@@ -142,6 +142,47 @@ def test_pieces_rows_bitexact(gpu_ctx, monkeypatch, plen, rmax):
         assert np.array_equal(bits(A), bits(r["A"]))
 
 
+@pytest.mark.parametrize("plen", ["64", "512"])
+def test_long_costs_modes_bitexact(gpu_ctx, monkeypatch, plen):
+    """Long-path AGD costs computed up front (k_long_costs, default) or per round inside k_up_pre
+    (SM_NO_PRECOST=1): both bit-exact against the oracle, cut paths (aggregates read the cost
+    rows) included."""
+    monkeypatch.setenv("SM_PIECE_LEN", plen)
+    W, H, D = 400, 300, 64
+    left, right, _ = make_pair(W, H, D, index=6)
+    ref = O.match(left, right, D, nthreads=16)
+    for mode in ("precost", "inline"):
+        if mode == "inline":
+            monkeypatch.setenv("SM_NO_PRECOST", "1")
+        else:
+            monkeypatch.delenv("SM_NO_PRECOST", raising=False)
+        out = gpu_ctx.match(left, right, D)
+        for v in ("left", "right"):
+            np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+            assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+def test_kernel_timing_mask(gpu_ctx):
+    """sm_set_kernel_timing: untimed families report no launches, timed ones do; the results do
+    not depend on the timing."""
+    W, H, D = 160, 120, 32
+    left, right, _ = make_pair(W, H, D, index=2)
+    base = gpu_ctx.match(left, right, D)
+    gpu_ctx.set_kernel_timing(["k_up_walk"])
+    try:
+        out = gpu_ctx.match(left, right, D)
+        ks = gpu_ctx.kernel_stats()
+    finally:
+        gpu_ctx.set_kernel_timing(None)
+    assert ks["k_up_walk"]["launches"] > 0 and ks["k_up_walk"]["ms"] > 0
+    assert all(v["launches"] == 0 for k, v in ks.items() if k != "k_up_walk")
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"], base[v]["idx"])
+    ks = None
+    gpu_ctx.match(left, right, D)
+    assert sum(v["launches"] for v in gpu_ctx.kernel_stats().values()) > 0
+
+
 def test_match_shard_offset_bitexact(gpu_ctx):
     """A disparity shard [d0, d0+D) (what one rank computes under D sharding)."""
     import stereomatch_amd as sm
