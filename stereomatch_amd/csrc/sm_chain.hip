@@ -428,11 +428,14 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 // third post-heavy child: its group takes the node-by-node path with one more fma.
 // ---------------------------------------------------------------------------------------------
 #ifndef UP_NS2
-#define UP_NS2 6
+#define UP_NS2 9
+#endif
+#ifndef UP_G2
+#define UP_G2 4  // even: the chain's two-half pipeline
 #endif
 template <int SPL>
 struct UpCfg {
-    static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? 6 : 3;  // nodes per group (helper registers)
+    static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? UP_G2 : 3;  // nodes per group (helper registers)
     static constexpr int NS = SPL == 1 ? 8 : SPL == 2 ? UP_NS2 : 6;  // LDS slots (~140 KB)
 };
 
