@@ -239,9 +239,19 @@ __device__ __forceinline__ uint64_t key_of(const uint16_t* wR, const uint16_t* w
     }
 }
 
-__global__ __launch_bounds__(BTHREADS) void k_bor_local(MstPair P, int W, int H, int max_iter) {
+// Tile keys: inside one tile every candidate edge (a, a+1 or a+W) has its lower endpoint a in the
+// tile, its left column or the row above, so (w, a, vertical) order is the order of the 32-bit
+//   w << 14 | ((ly_a + 1) * 66 + (lx_a + 1)) << 1 | vertical
+// (a = y*W + x is lexicographic in (y, x), and w <= SM_MAX_W < 2^18).  Each thread keeps its 4
+// pixels' 4 edge keys in registers across the iterations, and the LDS minima are 32-bit.
+#define TK_NONE 0xFFFFFFFFu
+__device__ __forceinline__ uint32_t tile_key(uint32_t w, int lxa, int lya, uint32_t vert) {
+    return (w << 14) | ((uint32_t)((lya + 1) * 66 + (lxa + 1)) << 1) | vert;
+}
+
+__global__ __launch_bounds__(BTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bor_local(MstPair P, int W, int H, int max_iter) {
     const MstView V = P.v[blockIdx.z];
-    __shared__ unsigned long long best[BTN];
+    __shared__ uint32_t best[BTN];
     __shared__ uint16_t comp[BTN];
     __shared__ uint16_t hk[BTN];
     __shared__ int flag;
@@ -249,50 +259,57 @@ __global__ __launch_bounds__(BTHREADS) void k_bor_local(MstPair P, int W, int H,
     const int tw = min(BT, W - tx0), th = min(BT, H - ty0);
     const int n = tw * th;
     for (int i = threadIdx.x; i < BTN; i += BTHREADS) comp[i] = (uint16_t)i;
+    constexpr int PPT = BTN / BTHREADS;  // thread t, slot j: tile pixel (lx, ly) = ((t + 1024 j) % 64, (t + 1024 j) / 64)
+    uint32_t ek[PPT][4];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const int t = threadIdx.x + j * BTHREADS;
+        const int lx = t & (BT - 1), ly = t / BT;
+        const int x = tx0 + lx, y = ty0 + ly;
+        const bool ok = lx < tw && ly < th;
+        const int p = y * W + x;
+        ek[j][0] = ok && x + 1 < W ? tile_key(V.wR[p], lx, ly, 0u) : TK_NONE;
+        ek[j][1] = ok && y + 1 < H ? tile_key(V.wD[p], lx, ly, 1u) : TK_NONE;
+        ek[j][2] = ok && x > 0 ? tile_key(V.wR[p - 1], lx - 1, ly, 0u) : TK_NONE;
+        ek[j][3] = ok && y > 0 ? tile_key(V.wD[p - W], lx, ly - 1, 1u) : TK_NONE;
+    }
     __syncthreads();
     for (int iter = 0; iter < max_iter; ++iter) {
-        for (int i = threadIdx.x; i < BTN; i += BTHREADS) best[i] = SM_KEY_NONE;
+        for (int i = threadIdx.x; i < BTN; i += BTHREADS) best[i] = TK_NONE;
         if (threadIdx.x == 0) flag = 0;
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += BTHREADS) {
-            const int lx = i % tw, ly = i / tw;
-            const int x = tx0 + lx, y = ty0 + ly;
-            const int p = y * W + x;
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const int t = threadIdx.x + j * BTHREADS;
+            const int lx = t & (BT - 1), ly = t / BT;
+            if (lx >= tw || ly >= th) continue;
+            const int i = ly * tw + lx;
             const int c = comp[i];
-            unsigned long long mk = SM_KEY_NONE;
-            if (x + 1 < W) {
-                if (lx + 1 >= tw || comp[i + 1] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 0));
-            }
-            if (y + 1 < H) {
-                if (ly + 1 >= th || comp[i + tw] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 1));
-            }
-            if (x > 0) {
-                if (lx == 0 || comp[i - 1] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 2));
-            }
-            if (y > 0) {
-                if (ly == 0 || comp[i - tw] != c) mk = min(mk, (unsigned long long)key_of(V.wR, V.wD, W, p, 3));
-            }
-            if (mk != SM_KEY_NONE) atomicMin(&best[c], mk);
+            uint32_t mk = TK_NONE;
+            if (ek[j][0] != TK_NONE && (lx + 1 >= tw || comp[i + 1] != c)) mk = min(mk, ek[j][0]);
+            if (ek[j][1] != TK_NONE && (ly + 1 >= th || comp[i + tw] != c)) mk = min(mk, ek[j][1]);
+            if (ek[j][2] != TK_NONE && (lx == 0 || comp[i - 1] != c)) mk = min(mk, ek[j][2]);
+            if (ek[j][3] != TK_NONE && (ly == 0 || comp[i - tw] != c)) mk = min(mk, ek[j][3]);
+            if (mk != TK_NONE) atomicMin(&best[c], mk);
         }
         __syncthreads();
         for (int c = threadIdx.x; c < n; c += BTHREADS) {
             hk[c] = (uint16_t)c;
             if (comp[c] != c) continue;
-            const unsigned long long k = best[c];
-            if (k == SM_KEY_NONE) continue;
-            const uint32_t a = (uint32_t)(k >> 1) & 0xFFFFFFFFu;
-            const uint32_t vert = (uint32_t)(k & 1ull);
-            const uint32_t b = a + (vert ? (uint32_t)W : 1u);
-            const int ax = (int)(a % (uint32_t)W) - tx0, ay = (int)(a / (uint32_t)W) - ty0;
-            const int bx = (int)(b % (uint32_t)W) - tx0, by = (int)(b / (uint32_t)W) - ty0;
-            const bool ain = ax >= 0 && ax < tw && ay >= 0 && ay < th;
-            const bool bin = bx >= 0 && bx < tw && by >= 0 && by < th;
+            const uint32_t k = best[c];
+            if (k == TK_NONE) continue;
+            const uint32_t vert = k & 1u, idx = (k >> 1) & 0x1FFFu;
+            const int lya = (int)(idx / 66u) - 1, lxa = (int)(idx % 66u) - 1;
+            const int lyb = lya + (int)vert, lxb = lxa + 1 - (int)vert;
+            const bool ain = lxa >= 0 && lxa < tw && lya >= 0 && lya < th;
+            const bool bin = lxb >= 0 && lxb < tw && lyb >= 0 && lyb < th;
             if (!ain || !bin) continue;  // minimum edge leaves the tile: frozen this phase
-            const int la = ay * tw + ax, lb = by * tw + bx;
+            const int la = lya * tw + lxa, lb = lyb * tw + lxb;
             const int ca = comp[la];
             const int c2 = (ca == c) ? comp[lb] : ca;
             if (best[c2] == k && c < c2) continue;  // mutual choice: the smaller label stays root
             hk[c] = (uint16_t)c2;
+            const uint32_t a = (uint32_t)((ty0 + lya) * W + tx0 + lxa);
             if (vert) V.mD[a] = 1; else V.mR[a] = 1;
             flag = 1;
         }
