@@ -116,8 +116,9 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
                 dd = 1;
                 const uint32_t sa = succ_arc(V.adj, W, 4u * p + (uint32_t)k, start);
                 if (sa != SM_NONE) {
-                    const uint32_t q = sa >> 2;
-                    const int qx = (int)(q % (uint32_t)W) - tx0, qy = (int)(q / (uint32_t)W) - ty0;
+                    // the successor leaves from q = the neighbour of p in direction k: its tile
+                    // coordinates follow from p's without a division by W
+                    const int qx = lx + (k == 0 ? 1 : k == 2 ? -1 : 0), qy = ly + (k == 1 ? 1 : k == 3 ? -1 : 0);
                     if (qx >= 0 && qx < TL && qy >= 0 && qy < TL) {
                         n = (uint32_t)(4 * (qy * TL + qx) + (int)(sa & 3u));
                         haspred[n] = 1;
