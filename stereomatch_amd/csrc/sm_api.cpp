@@ -500,10 +500,19 @@ void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int nview
     }
 }
 
-sm_status ensure_events(sm_ctx* ctx, std::vector<hipEvent_t>& evs, size_t n) {
+// Timing-only events skip the system-scope fence on record (hipEventDisableSystemFence): the
+// default record writes back and invalidates the caches, which put ~5.7 us of idle GPU between
+// the bracketed launches and left the next kernel with cold caches.  Elapsed times are read after
+// a stream synchronisation, so nothing needs the fence.  SM_EVENT_FENCE=1: default events (A/B).
+static unsigned timing_event_flags() {
+    static const bool fence = getenv("SM_EVENT_FENCE") != nullptr;
+    return fence ? hipEventDefault : hipEventDisableSystemFence;
+}
+
+sm_status ensure_events(sm_ctx* ctx, std::vector<hipEvent_t>& evs, size_t n, unsigned flags = hipEventDefault) {
     while (evs.size() < n) {
         hipEvent_t e;
-        HIPC(hipEventCreate(&e));
+        HIPC(hipEventCreateWithFlags(&e, flags));
         evs.push_back(e);
     }
     return SM_OK;
@@ -539,7 +548,7 @@ sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch, doubl
         ctx->ev_open = false;
         return SM_OK;
     }
-    CHECK(ensure_events(ctx, ctx->fev, (size_t)ctx->nfev + 2));
+    CHECK(ensure_events(ctx, ctx->fev, (size_t)ctx->nfev + 2, timing_event_flags()));
     int start;
     if (ctx->ev_open && s == ctx->ev_stream) {
         start = ctx->nfev - 1;  // the previous timed launch's end event
@@ -850,8 +859,8 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         delete ctx;
         return SM_ERR_HIP;
     }
-    for (auto& e : ctx->ev)
-        if (hipEventCreate(&e) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
+    for (auto& e : ctx->ev)  // stage-boundary timing events
+        if (hipEventCreateWithFlags(&e, timing_event_flags()) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
     // tables: S/S2 (correctly rounded, tools/gen_tables.py) and the AGD colour term
     std::vector<float> atab(SM_MAX_W + 1);
     for (int i = 0; i <= SM_MAX_W; ++i) atab[i] = agd_color_term(i);
