@@ -38,6 +38,12 @@
 #ifndef WALK_UP_CH2
 #define WALK_UP_CH2 3
 #endif
+#ifndef WALK_UP_CH4
+#define WALK_UP_CH4 3
+#endif
+#ifndef WALK_DN_CH4
+#define WALK_DN_CH4 4
+#endif
 #ifndef WALK_DN_CH2
 #define WALK_DN_CH2 6
 #endif
@@ -367,7 +373,7 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
         switch (spl) {
             case 1: up_launch<1, 4>(st, g, a); break;
             case 2: up_launch<2, WALK_UP_CH2>(st, g, a); break;
-            default: up_launch<4, 2>(st, g, a); break;
+            default: up_launch<4, WALK_UP_CH4>(st, g, a); break;
         }
     }
     return hipGetLastError();
@@ -388,7 +394,7 @@ static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, i
         switch (spl) {
             case 1: down_launch<1, 4>(st, g, a, store_all); break;
             case 2: down_launch<2, WALK_DN_CH2>(st, g, a, store_all); break;
-            default: down_launch<4, 4>(st, g, a, store_all); break;
+            default: down_launch<4, WALK_DN_CH4>(st, g, a, store_all); break;
         }
     }
     return hipGetLastError();
