@@ -430,13 +430,19 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 #ifndef UP_NS2
 #define UP_NS2 9
 #endif
+#ifndef UP_G4
+#define UP_G4 3
+#endif
+#ifndef UP_NS4
+#define UP_NS4 6
+#endif
 #ifndef UP_G2
 #define UP_G2 4  // even: the chain's two-half pipeline
 #endif
 template <int SPL>
 struct UpCfg {
-    static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? UP_G2 : 3;  // nodes per group (helper registers)
-    static constexpr int NS = SPL == 1 ? 8 : SPL == 2 ? UP_NS2 : 6;  // LDS slots (~140 KB)
+    static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? UP_G2 : UP_G4;  // nodes per group (helper registers)
+    static constexpr int NS = SPL == 1 ? 8 : SPL == 2 ? UP_NS2 : UP_NS4;  // LDS slots (~140 KB)
 };
 
 struct UpNodeS {
