@@ -67,12 +67,20 @@ typedef struct {
     int post;          /* sm_post bits applied to the final maps (default 0)         */
 } sm_params;
 
-/* Post-processing of the final (cross-rank reduced) disparity maps. */
+/* Post-processing of the final (cross-rank reduced) float disparity maps (idx / min untouched),
+ * applied in this order.  Dmax below = p->disp_total (or disp_begin + D when 0).  stereo3dmst's
+ * own output step is SM_POST_LABEL_TO_DISP | SM_POST_LR_CHECK (Stereo3DMST.cpp:900-904). */
 typedef enum {
-    SM_POST_LR_CHECK = 1  /* stereo3dmst's left-right check, fill=false: a left pixel whose
-                             disparity d has x-d outside the image, d outside [0, disp_total),
-                             or |d - right(x-d)| > 1 is set to 0 in left_disp (idx/min untouched)
-                             (Stereo3DMST.cpp:632-662, applied at :904) */
+    SM_POST_LR_CHECK = 1,       /* left-right check: a left pixel whose disparity d (rounded) has x-d
+                                   outside the image, d outside [0, Dmax), or |d - right(x-d)| > 1 is
+                                   set to 0 in left_disp (Stereo3DMST.cpp:632-662, at :904) */
+    SM_POST_LABEL_TO_DISP = 2,  /* LabelToDisp + scaling, both maps: disp = clamp(d / (Dmax-1.f), 0, 1)
+                                   * (Dmax-1.f) in float (:189-201, :900-902); applied before the check */
+    SM_POST_LR_FILL = 4,        /* with SM_POST_LR_CHECK: the check's fill step, fill=true (:664-709) */
+    SM_POST_OCCLUSION = 8,      /* handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288),
+                                   both maps: occluded pixels take the min of the nearest valid
+                                   neighbours in the row (255 if none) */
+    SM_POST_OCCLUSION_ZERO = 16 /* the same check with remove_occlusion=true: occluded pixels = 0 */
 } sm_post;
 
 typedef struct sm_ctx sm_ctx;

@@ -45,6 +45,9 @@ def lib():
         L.orc_agd_color_term.argtypes = [c_int]
         L.orc_agd_color_term.restype = c_float
         L.orc_lr_check.argtypes = [vp, vp, c_int, c_int, c_int]
+        L.orc_lr_check_fill.argtypes = [vp, vp, c_int, c_int, c_int, c_int]
+        L.orc_label_to_disp.argtypes = [vp, ctypes.c_long, c_int]
+        L.orc_occlusion.argtypes = [vp, vp, c_int, c_int, c_int, c_float, c_int]
         _LIB = L
     return _LIB
 
@@ -195,10 +198,34 @@ def ref_segment_graph(W, H, wR, wD, c):
     return dict(mask=mask, nsets=nsets, sorted_a=oa, sorted_b=ob, sorted_w=ow, sorted_mask=om)
 
 
-def lr_check(left_disp, right_disp, max_disp):
-    """Stereo3DMST.cpp:632-662 with fill=false (as at :904); returns a new left map."""
+def lr_check(left_disp, right_disp, max_disp, fill=False):
+    """Stereo3DMST.cpp:632-709 (fill=false as at :904); returns a new left map."""
     left = np.ascontiguousarray(left_disp, dtype=np.float32).copy()
     right = np.ascontiguousarray(right_disp, dtype=np.float32)
     H, W = left.shape
-    lib().orc_lr_check(_ptr(left), _ptr(right), W, H, int(max_disp))
+    lib().orc_lr_check_fill(_ptr(left), _ptr(right), W, H, int(max_disp), 1 if fill else 0)
     return left
+
+
+def label_to_disp(disp, dmax):
+    """LabelToDisp of the label (0, 0, d) + the *= (Dmax-1) scaling (Stereo3DMST.cpp:189-201, 900-902)."""
+    d = np.ascontiguousarray(disp, dtype=np.float32).copy()
+    lib().orc_label_to_disp(_ptr(d), d.size, int(dmax))
+    return d
+
+
+def stereo3dmst_output(left_idx, right_idx, dmax, fill=False):
+    """stereo3dmst's output step on the per-slice WTA maps: LabelToDisp + scaling of both maps, then
+    the L-R check of the left map (Stereo3DMST.cpp:900-904).  Returns (left_disp, right_disp)."""
+    ld = label_to_disp(np.asarray(left_idx).astype(np.float32), dmax)
+    rd = label_to_disp(np.asarray(right_idx).astype(np.float32), dmax)
+    return lr_check(ld, rd, dmax, fill), rd
+
+
+def occlusion(left_disp, right_disp, min_disp=0, thresh=1.0, remove=False):
+    """handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288); returns new (left, right)."""
+    L = np.ascontiguousarray(left_disp, dtype=np.float32).copy()
+    R = np.ascontiguousarray(right_disp, dtype=np.float32).copy()
+    H, W = L.shape
+    lib().orc_occlusion(_ptr(L), _ptr(R), W, H, int(min_disp), float(thresh), 1 if remove else 0)
+    return L, R

@@ -385,20 +385,97 @@ void orc_tree_filter(int W, int H, int nd, int d0, int ntrees, const int32_t* tr
     }
 }
 
-/* Left-right consistency check without fill (Stereo3DMST.cpp:632-662, called at :904 with
- * fill=false): d = round(left); a pixel with x-d < 0, d < 0, d >= max_disp or
- * |left - right(x-d)| > 1 becomes 0.  Only left is written and only right is read across
- * pixels, so the serial loop equals the reference's OpenMP one. */
-void orc_lr_check(float* left, const float* right, int W, int H, int max_disp) {
+/* LabelToDisp (Stereo3DMST.cpp:189-201) of the per-slice label a = b = 0, c = d:
+ * MAX(0.0f, min(1.0f, (x*a + y*b + c)/(max_disp-1.0f))), x*0 + y*0 + d == d exactly; then
+ * leftDisp *= (Dmax-1.f) (:900-902), OpenCV convertTo with scale: one float multiply. */
+void orc_label_to_disp(float* disp, long n, int dmax) {
+    const float dm1 = (float)dmax - 1.0f;
+    for (long i = 0; i < n; ++i) {
+        float v = disp[i] / dm1;
+        v = (v < 1.0f) ? v : 1.0f;  /* std::min(1.0f, v) */
+        v = (0.0f < v) ? v : 0.0f;  /* MAX(0.0f, v) (OpenCV: a < b ? b : a) */
+        disp[i] = v * dm1;
+    }
+}
+
+/* Left-right consistency check (Stereo3DMST.cpp:632-709), literal: d = round(left); a pixel with
+ * x-d < 0, d < 0, d >= max_disp or |left - right(x-d)| > 1 becomes 0 and is masked (:642-662);
+ * with fill, each row is walked left to right: a masked pixel copies the nearest pixel to its left
+ * whose mask is 0 and clears its mask, then takes the nearest mask-0 pixel to its right if that is
+ * smaller or if its own mask is still 1 (:664-709).  Rows are independent (the OpenMP loop is over
+ * y), so the serial loop equals the reference. */
+void orc_lr_check_fill(float* left, const float* right, int W, int H, int max_disp, int fill) {
+    unsigned char* mask = (unsigned char*)calloc((size_t)W * H, 1);
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             const long idx = (long)y * W + x;
             const float df = left[idx];
-            const int d = (int)round(df);
+            const int d = (int)roundf(df);
             if (x - d >= 0 && d >= 0 && d < max_disp) {
-                if (fabsf(df - right[idx - d]) > 1.0f) left[idx] = 0.0f;
+                if (fabsf(df - right[idx - d]) > 1.0f) { mask[idx] = 1; left[idx] = 0.0f; }
             } else {
+                mask[idx] = 1;
                 left[idx] = 0.0f;
             }
         }
+    if (fill) {
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                const long idx = (long)y * W + x;
+                if (mask[idx] == 0) continue;
+                for (int i = 1; x - i >= 0; ++i)
+                    if (mask[idx - i] == 0) { left[idx] = left[idx - i]; mask[idx] = 0; break; }
+                for (int i = 1; x + i < W; ++i)
+                    if (mask[idx + i] == 0) {
+                        if (left[idx + i] < left[idx] || mask[idx] == 1) left[idx] = left[idx + i];
+                        break;
+                    }
+            }
+    }
+    free(mask);
+}
+
+void orc_lr_check(float* left, const float* right, int W, int H, int max_disp) {
+    orc_lr_check_fill(left, right, W, H, max_disp, 0); /* as called at :904 */
+}
+
+/* handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288), literal per row with the copy
+ * tile: marks (1e18f) are written into the copies for both maps first (the race-free reading of
+ * the kernel, which has no barrier between marking and searching), then every marked pixel is
+ * set to min_disp (remove) or to fminf of the nearest unmarked ORIGINAL values to its left and
+ * right (1e18f when absent; 255 when both are absent). */
+void orc_occlusion(float* left, float* right, int W, int H, int min_disp, float thresh, int remove) {
+    const float inv = 1e18f;
+    float* t = (float*)malloc(sizeof(float) * 4 * (size_t)W);
+    for (int y = 0; y < H; ++y) {
+        float* L = left + (size_t)y * W;
+        float* R = right + (size_t)y * W;
+        for (int x = 0; x < W; ++x) { t[x] = L[x]; t[x + W] = R[x]; t[x + 2 * W] = L[x]; t[x + 3 * W] = R[x]; }
+        for (int x = 0; x < W; ++x) {
+            int right_x = (int)((float)x - t[x]);
+            int left_x = x;
+            if ((right_x >= 0 && fabsf(t[right_x + W] - t[left_x]) > thresh) || right_x < 0) t[left_x + 2 * W] = inv;
+            left_x = (int)((float)x + t[x + W]);
+            right_x = x;
+            if ((left_x < W && fabsf(t[right_x + W] - t[left_x]) > thresh) || left_x >= W) t[right_x + 3 * W] = inv;
+        }
+        for (int x = 0; x < W; ++x) {
+            if (remove) {
+                if (t[x + 2 * W] == inv) L[x] = (float)min_disp;
+                if (t[x + 3 * W] == inv) R[x] = (float)min_disp;
+                continue;
+            }
+            for (int v = 0; v < 2; ++v) {
+                const float* orig = t + v * W;
+                const float* marks = t + (2 + v) * W;
+                float* out = v ? R : L;
+                if (marks[x] != inv) continue;
+                float ls = inv, rs = inv;
+                for (int q = x - 1; q >= 0; --q) if (marks[q] != inv) { ls = orig[q]; break; }
+                for (int q = x + 1; q < W; ++q) if (marks[q] != inv) { rs = orig[q]; break; }
+                out[x] = (ls == inv && rs == inv) ? 255.f : fminf(ls, rs);
+            }
+        }
+    }
+    free(t);
 }

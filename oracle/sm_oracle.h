@@ -75,6 +75,12 @@ float orc_agd_color_term(int l1);
 
 /* Stereo3DMST.cpp:632-662 (fill=false, as called at :904): in place on left. */
 void orc_lr_check(float* left, const float* right, int W, int H, int max_disp);
+/* leftRightConsistencyCheck with the fill step (Stereo3DMST.cpp:632-709), fill = 0 / 1. */
+void orc_lr_check_fill(float* left, const float* right, int W, int H, int max_disp, int fill);
+/* LabelToDisp of the per-slice label (0, 0, d) and the *= (Dmax-1) scaling (:189-201, 900-902). */
+void orc_label_to_disp(float* disp, long n, int dmax);
+/* handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288), marks computed before the search. */
+void orc_occlusion(float* left, float* right, int W, int H, int min_disp, float thresh, int remove);
 
 #ifdef __cplusplus
 }

@@ -14,11 +14,15 @@ import os
 
 import numpy as np
 
-from ._lib import (SM_COST_AGD, SM_COST_VOLUME, SM_POST_LR_CHECK, Context, StereoMSTError, default_params, device_count,  # noqa: F401
-                   lib)
+from ._lib import (SM_COST_AGD, SM_COST_VOLUME, SM_POST_LABEL_TO_DISP, SM_POST_LR_CHECK, SM_POST_LR_FILL,  # noqa: F401
+                   SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO, Context, StereoMSTError, default_params, device_count, lib)
+
+# stereo3dmst's output step: LabelToDisp + *= (Dmax-1) on both maps, then the fill-less L-R check of
+# the left map (Stereo3DMST.cpp:189-201, 900-904)
+STEREO3DMST_POST = SM_POST_LABEL_TO_DISP | SM_POST_LR_CHECK
 
 __all__ = ["stereo3dmst", "startTimer", "getTimer", "Context", "default_params", "StereoMSTError", "device_count",
-           "shard_range"]
+           "shard_range", "STEREO3DMST_POST"]
 
 
 def shard_range(d_total, nranks, rank):
@@ -47,8 +51,9 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
 
     left_img/right_img: HxWx3 uint8 BGR (cv::Mat CV_8UC3).  Returns (left_disp, right_disp),
     float32 HxW in [0, Dmax-1]: the strict-< winner-take-all slice of the MST-aggregated
-    cost, with the reference's output step applied: the left map is
-    left-right checked without fill (:904, :632-662), the right map is returned unchecked.
+    cost, with the reference's output step applied: both maps go through
+    LabelToDisp's clamp(d/(Dmax-1.f), 0, 1) and *= (Dmax-1.f) in float (:189-201, :900-902), then
+    the left map is left-right checked without fill (:904, :632-662); the right map is unchecked.
     data_cost "AGD" builds the cost on the GPU; "MCCNN_fst"/"MCCNN_acrt" take the MC-CNN volumes
     from mc-cnn-master/{left,right}.bin (after running the network there, as the reference does).
     Like the reference, an unsupported data_cost prints a message and returns
@@ -72,14 +77,14 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
         ctx = _ctx()
         ctx.upload_cost_volumes(*vols)
         out = ctx.match(left_img, right_img, int(Dmax),
-                        default_params(post=SM_POST_LR_CHECK, cost_kind=SM_COST_VOLUME, disp_total=int(Dmax)))
+                        default_params(post=STEREO3DMST_POST, cost_kind=SM_COST_VOLUME, disp_total=int(Dmax)))
         left_disp[...] = out["left"]["disp"]
         right_disp[...] = out["right"]["disp"]
         return left_disp, right_disp
     if data_cost != "AGD":
         print("wrong data cost")
         return left_disp, right_disp
-    out = _ctx().match(left_img, right_img, int(Dmax), default_params(post=SM_POST_LR_CHECK))
+    out = _ctx().match(left_img, right_img, int(Dmax), default_params(post=STEREO3DMST_POST, disp_total=int(Dmax)))
     left_disp[...] = out["left"]["disp"]
     right_disp[...] = out["right"]["disp"]
     return left_disp, right_disp

@@ -16,7 +16,7 @@ SM_OK, SM_ERR_ARG, SM_ERR_HIP, SM_ERR_OOM, SM_ERR_RCCL, SM_ERR_STATE, SM_ERR_NOD
 STATUS_NAMES = {0: "SM_OK", 1: "SM_ERR_ARG", 2: "SM_ERR_HIP", 3: "SM_ERR_OOM", 4: "SM_ERR_RCCL",
                 5: "SM_ERR_STATE", 6: "SM_ERR_NODEVICE"}
 SM_COST_AGD, SM_COST_VOLUME = 0, 1
-SM_POST_LR_CHECK = 1
+SM_POST_LR_CHECK, SM_POST_LABEL_TO_DISP, SM_POST_LR_FILL, SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO = 1, 2, 4, 8, 16
 SM_UNIQUE_ID_BYTES = 128
 
 

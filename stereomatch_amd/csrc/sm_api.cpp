@@ -58,7 +58,12 @@ struct sm_ctx {
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
     DevBuf changed, mst_ok, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
+    DevBuf post_mask, post_scratch;  // output step (sm_post.hip): marks, scan positions
     size_t rec_pad_n[2] = {0, 0};  // pixel count the record pads were zeroed for
+    size_t rec_pad_z[2] = {0, 0};  // pad length (records) they were zeroed with
+    // records of padding on each side of the image records: the walkers read the matched image
+    // at pix +- (disp_begin + Dpad) (sm_walk_util.h load_recs), so the pad follows the call's range
+    size_t rec_pad = SM_REC_PAD;
     DevBuf vin[2];               // MC-CNN ingest: caller volumes [vin_D][H][W] f32 per view
     int vin_W = 0, vin_H = 0, vin_D = 0;
     bool use_vol = false;        // the current call takes its costs from vin (SM_COST_VOLUME)
@@ -71,6 +76,8 @@ struct sm_ctx {
     DevBuf pieces[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
     DevBuf cnw[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
+    uint32_t* h_err = nullptr;  // pinned, device-visible error word of the chain engine's waits
+    uint32_t* d_err = nullptr;  // its device address
     int mst_rounds = 12;  // contracted Boruvka rounds the previous frame needed
     MstPending mst_pend;  // rounds enqueued without a host check (stage_mst -> mst_finish)
     uint32_t* h_rounds = nullptr;  // pinned: per view [SM_MAX_ROUNDS+1 begin | nrounds | n_has_light]
@@ -158,8 +165,23 @@ sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
         return fail(ctx, SM_ERR_ARG, "only gamma=1/12 (embedded correctly-rounded tables) is supported");
     if (D < 1 || D > 256) return fail(ctx, SM_ERR_ARG, "D must be in [1, 256] per call (shard larger ranges)");
     if (p->disp_begin < 0) return fail(ctx, SM_ERR_ARG, "disp_begin < 0");
-    if (p->post & ~SM_POST_LR_CHECK) return fail(ctx, SM_ERR_ARG, "unknown post-processing bits");
+    if (p->disp_begin > (1 << 20)) return fail(ctx, SM_ERR_ARG, "disp_begin > 2^20");
+    if (p->disp_total != 0 && p->disp_total < p->disp_begin + D)
+        return fail(ctx, SM_ERR_ARG, "disp_total < disp_begin + D (shard beyond the total range)");
+    const int known = SM_POST_LR_CHECK | SM_POST_LABEL_TO_DISP | SM_POST_LR_FILL | SM_POST_OCCLUSION | SM_POST_OCCLUSION_ZERO;
+    if (p->post & ~known) return fail(ctx, SM_ERR_ARG, "unknown post-processing bits");
+    if ((p->post & SM_POST_LR_FILL) && !(p->post & SM_POST_LR_CHECK))
+        return fail(ctx, SM_ERR_ARG, "SM_POST_LR_FILL needs SM_POST_LR_CHECK");
+    if ((p->post & SM_POST_OCCLUSION) && (p->post & SM_POST_OCCLUSION_ZERO))
+        return fail(ctx, SM_ERR_ARG, "SM_POST_OCCLUSION and SM_POST_OCCLUSION_ZERO are exclusive");
     return SM_OK;
+}
+
+// image-record pad for a call over slices [disp_begin, disp_begin + Dpad): load_recs reads records
+// pix - disp_begin - Dpad .. pix + disp_begin + Dpad + 1 (sm_walk_util.h)
+size_t rec_pad_for(int disp_begin, int D) {
+    const size_t need = (size_t)disp_begin + 64 * (size_t)spl_for(D) + 64;
+    return need <= SM_REC_PAD ? SM_REC_PAD : (need + 1023) / 1024 * 1024;
 }
 
 // ----------------------------------------------------------------------------- stages
@@ -173,16 +195,19 @@ sm_status stage_prep(sm_ctx* ctx) {
         CHECK(ensure(ctx, ctx->wR[v], N * 2));
         CHECK(ensure(ctx, ctx->wD[v], N * 2));
         const void* old = ctx->rec[v].p;
-        CHECK(ensure(ctx, ctx->rec[v], (N + 2 * SM_REC_PAD) * 8));
-        if (ctx->rec[v].p != old || ctx->rec_pad_n[v] != N) {  // zero pads around the records: once per allocation and size
+        const size_t pad = ctx->rec_pad;
+        CHECK(ensure(ctx, ctx->rec[v], (N + 2 * pad) * 8));
+        if (ctx->rec[v].p != old || ctx->rec_pad_n[v] != N || ctx->rec_pad_z[v] != pad) {
+            // zero pads around the records: once per allocation, size and pad
             ctx->rec_pad_n[v] = N;
-            HIPC(hipMemsetAsync(ctx->rec[v].p, 0, SM_REC_PAD * 8, ctx->st));
-            HIPC(hipMemsetAsync(P<uint2>(ctx->rec[v]) + SM_REC_PAD + N, 0, SM_REC_PAD * 8, ctx->st));
+            ctx->rec_pad_z[v] = pad;
+            HIPC(hipMemsetAsync(ctx->rec[v].p, 0, pad * 8, ctx->st));
+            HIPC(hipMemsetAsync(P<uint2>(ctx->rec[v]) + pad + N, 0, pad * 8, ctx->st));
         }
     }
     HIPC(launch_prep(ctx->st, P<uint8_t>(ctx->img[0]), P<uint8_t>(ctx->img[1]), W, H, ctx->stride, P<uint32_t>(ctx->bgrx[0]),
                      P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]), P<float>(ctx->gray[1]),
-                     P<uint2>(ctx->rec[0]) + SM_REC_PAD, P<uint2>(ctx->rec[1]) + SM_REC_PAD));
+                     P<uint2>(ctx->rec[0]) + ctx->rec_pad, P<uint2>(ctx->rec[1]) + ctx->rec_pad));
     HIPC(launch_median_weights(ctx->st, P<uint32_t>(ctx->bgrx[0]), P<uint32_t>(ctx->bgrx[1]), P<uint32_t>(ctx->med[0]),
                                P<uint32_t>(ctx->med[1]), P<uint16_t>(ctx->wR[0]), P<uint16_t>(ctx->wD[0]),
                                P<uint16_t>(ctx->wR[1]), P<uint16_t>(ctx->wD[1]), W, H));
@@ -455,8 +480,8 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
         a.minc[v] = P<double>(ctx->minc[v]);
         a.disp[v] = P<float>(ctx->disp[v]);
     }
-    a.Lrec = P<uint2>(ctx->rec[0]) + SM_REC_PAD;
-    a.Rrec = P<uint2>(ctx->rec[1]) + SM_REC_PAD;
+    a.Lrec = P<uint2>(ctx->rec[0]) + ctx->rec_pad;
+    a.Rrec = P<uint2>(ctx->rec[1]) + ctx->rec_pad;
     a.atab = P<float>(ctx->atab);
     a.slut = P<double>(ctx->slut);
     a.s2lut = P<double>(ctx->s2lut);
@@ -643,6 +668,11 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
         const char* e = getenv("SM_REPAIR_MAX");
         a.repair_max = e ? std::max(1, atoi(e)) : 1 << 30;
     }
+    a.err = ctx->d_err;
+    {
+        const char* e = getenv("SM_WAIT_ITERS");  // read per call: the forced-timeout test lowers it
+        a.wait_iters = e ? std::max(0, atoi(e)) : 1 << 24;
+    }
     a.piece_dbg = nullptr;
     if (getenv("SM_PIECE_DEBUG")) {  // per-call repair statistics on stderr (tools)
         CHECK(ensure(ctx, ctx->pdbg, 128));
@@ -764,8 +794,10 @@ sm_status collect_filter_stats(sm_ctx* ctx) {
     return SM_OK;
 }
 
+// Runs whenever the context has a communicator, a one-rank one included (the exchange then reduces
+// over that rank alone: tests drive k_cand / k_finalize and the RCCL calls on one GPU).
 sm_status stage_reduce(sm_ctx* ctx) {
-    if (!ctx->comm || ctx->nranks <= 1) return SM_OK;
+    if (!ctx->comm) return SM_OK;
     const size_t N = (size_t)ctx->W * ctx->H;
     for (int v = 0; v < 2; ++v) {
         CHECK(ensure(ctx, ctx->gmin[v], N * 8));
@@ -791,6 +823,31 @@ sm_status stage_reduce(sm_ctx* ctx) {
     return SM_OK;
 }
 
+// output step on the final (reduced) float maps, in the reference's order: LabelToDisp + scaling
+// (Stereo3DMST.cpp:189-201, 900-902), L-R check (+ fill) (:632-709, 904), then the GPU PatchMatch's
+// occlusion handling (PatchMatchStereoGPU.cu:1128-1288).  dmax = the total disparity range.
+sm_status stage_post(sm_ctx* ctx, int post, int dmax) {
+    if (!post) return SM_OK;
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H;
+    float* L = P<float>(ctx->disp[0]);
+    float* R = P<float>(ctx->disp[1]);
+    if (post & (SM_POST_LR_FILL | SM_POST_OCCLUSION | SM_POST_OCCLUSION_ZERO)) {
+        CHECK(ensure(ctx, ctx->post_mask, 2 * N));
+        CHECK(ensure(ctx, ctx->post_scratch, 2 * N * 4));
+    }
+    if (post & SM_POST_LABEL_TO_DISP) HIPC(launch_label_to_disp(ctx->st, L, R, N, dmax));
+    if (post & SM_POST_LR_CHECK) {
+        const bool fill = (post & SM_POST_LR_FILL) != 0;
+        HIPC(launch_lr_check(ctx->st, L, R, W, H, dmax, fill ? P<uint8_t>(ctx->post_mask) : nullptr));
+        if (fill) HIPC(launch_lr_fill(ctx->st, L, P<uint8_t>(ctx->post_mask), W, H, P<int>(ctx->post_scratch)));
+    }
+    if (post & (SM_POST_OCCLUSION | SM_POST_OCCLUSION_ZERO))
+        HIPC(launch_occlusion(ctx->st, L, R, W, H, 1.0f, (post & SM_POST_OCCLUSION_ZERO) ? 1 : 0, 0.0f,
+                              P<uint8_t>(ctx->post_mask), P<int>(ctx->post_scratch)));
+    return SM_OK;
+}
+
 sm_status upload(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride) {
     if (!l || !r) return fail(ctx, SM_ERR_ARG, "null image");
     if (W < 1 || H < 1 || stride < 3 * W) return fail(ctx, SM_ERR_ARG, "bad image geometry");
@@ -803,6 +860,17 @@ sm_status upload(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, 
     HIPC(hipMemcpyAsync(ctx->img[0].p, l, bytes, hipMemcpyHostToDevice, ctx->st));
     HIPC(hipMemcpyAsync(ctx->img[1].p, r, bytes, hipMemcpyHostToDevice, ctx->st));
     return SM_OK;
+}
+
+// the chain engine's error word (written by the device through the host mapping): reported once,
+// then cleared so the context stays usable
+sm_status check_device_error(sm_ctx* ctx) {
+    const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE);
+    if (!e) return SM_OK;
+    __atomic_store_n(ctx->h_err, 0u, __ATOMIC_RELEASE);
+    return fail(ctx, SM_ERR_STATE,
+                "long-path chain engine: a cross-workgroup wait timed out (piece status word never published); "
+                "the results of this call are invalid");
 }
 
 double now_ms() {
@@ -854,6 +922,12 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         delete ctx;
         return SM_ERR_HIP;
     }
+    if (hipHostMalloc((void**)&ctx->h_err, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&ctx->d_err, ctx->h_err, 0) != hipSuccess) {
+        delete ctx;
+        return SM_ERR_HIP;
+    }
+    ctx->h_err[0] = 0;
     if (hipHostMalloc((void**)&ctx->h_changed, (2 * SM_MST_MAX_ROUNDS + 8) * sizeof(int)) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
@@ -881,7 +955,7 @@ void sm_destroy(sm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
-    DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut};
+    DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut, &ctx->post_mask, &ctx->post_scratch};
     for (DevBuf* b : all) if (b->p) (void)hipFree(b->p);
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
@@ -894,6 +968,7 @@ void sm_destroy(sm_ctx* ctx) {
     for (auto e : ctx->fev) (void)hipEventDestroy(e);
     for (auto e : ctx->sev) (void)hipEventDestroy(e);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
+    if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
     for (int v = 0; v < 2; ++v) {
         DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->off_in[v], &ctx->light_in[v],
@@ -945,6 +1020,7 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
         if (p->disp_begin + D > ctx->vin_D) return fail(ctx, SM_ERR_ARG, "slices beyond the uploaded cost volumes");
     }
     HIPC(hipSetDevice(ctx->device));
+    ctx->rec_pad = rec_pad_for(p->disp_begin, D);
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
     HIPC(hipEventRecord(ctx->ev[1], ctx->st));
@@ -955,10 +1031,7 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     CHECK(stage_filter(ctx, D, p->disp_begin, 2, false));
     HIPC(hipEventRecord(ctx->ev[4], ctx->st));
     CHECK(stage_reduce(ctx));
-    if (p->post & SM_POST_LR_CHECK) {
-        const int dmax = p->disp_total > 0 ? p->disp_total : p->disp_begin + D;
-        HIPC(launch_lr_check(ctx->st, P<float>(ctx->disp[0]), P<float>(ctx->disp[1]), ctx->W, ctx->H, dmax));
-    }
+    CHECK(stage_post(ctx, p->post, p->disp_total > 0 ? p->disp_total : p->disp_begin + D));
     HIPC(hipEventRecord(ctx->ev[5], ctx->st));
     return SM_OK;
 }
@@ -967,6 +1040,7 @@ sm_status sm_synchronize(sm_ctx* ctx) {
     if (!ctx) return SM_ERR_ARG;
     HIPC(hipSetDevice(ctx->device));
     HIPC(hipStreamSynchronize(ctx->st));
+    CHECK(check_device_error(ctx));
     float t[5];
     for (int i = 0; i < 5; ++i) HIPC(hipEventElapsedTime(&t[i], ctx->ev[i], ctx->ev[i + 1]));
     ctx->stage_ms[0] = t[0];
@@ -1059,8 +1133,9 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
     if (!ctx) return SM_ERR_ARG;
     if (view != 0 && view != 1) return fail(ctx, SM_ERR_ARG, "view must be 0 or 1");
     ctx->use_vol = false;  // AGD costs
-    if (D < 1 || D > 256 || d0 < 0) return fail(ctx, SM_ERR_ARG, "bad disparity range");
+    if (D < 1 || D > 256 || d0 < 0 || d0 > (1 << 20)) return fail(ctx, SM_ERR_ARG, "bad disparity range");
     HIPC(hipSetDevice(ctx->device));
+    ctx->rec_pad = rec_pad_for(d0, D);
     CHECK(upload(ctx, l, r, W, H, stride));
     CHECK(stage_prep(ctx));
     CHECK(stage_mst(ctx, 2));
@@ -1085,13 +1160,14 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
                                    P<double>(ctx->vol[0])));
         if (A_up) HIPC(hipMemcpyAsync(A_up, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));
         HIPC(hipStreamSynchronize(ctx->st));
+        CHECK(check_device_error(ctx));
     }
     CHECK(stage_filter(ctx, D, d0, 2, true));
     HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->fix[view]), (int)N, Dpad, D, N,
                                P<double>(ctx->vol[0])));
     if (A) HIPC(hipMemcpyAsync(A, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));
     HIPC(hipStreamSynchronize(ctx->st));
-    return SM_OK;
+    return check_device_error(ctx);
 }
 
 int sm_stage_times(sm_ctx* ctx, float* out, int n) {

@@ -73,6 +73,35 @@ __device__ __forceinline__ void lds_publish(int* p, int v) {
 // all of this wave's vector-memory loads have returned (stores issued later are not waited for)
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
+// Cross-workgroup hand-off (status words of pieces), the agent-scope release/acquire protocol:
+//   producer: its stores (rows: agent-scope stores) -> release fence at agent scope (writes back the
+//             XCD's L2) -> s_waitcnt vmcnt(0) in asm (ROCm 7.2 can drop the fence's own wait) ->
+//             relaxed agent-scope store of the word;
+//   consumer: relaxed agent-scope polls of the word -> one acquire fence at agent scope (invalidates
+//             this CU's L1) -> s_waitcnt vmcnt(0) -> its loads (rows: agent-scope loads).
+// A wait gives up after SM_WAIT_ITERS polls (~1 s by default; tests lower it): it then sets the
+// call's device error word, which sm_synchronize turns into an error status -- a missed publication
+// can never return SM_OK with wrong disparities.
+__device__ __forceinline__ uint32_t wait_word(const uint32_t* p, uint32_t lo, uint32_t hi, uint32_t* err, int iters) {
+    uint32_t v = 0;
+    for (int it = 0; it < iters; ++it) {
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= lo && v <= hi) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return v;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return v;
+}
+__device__ __forceinline__ void publish_word(uint32_t* p, uint32_t v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void lds_wait(int* p, int v, bool sleep, unsigned* spins = nullptr) {
     while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v) {
         PROF_SPIN(spins && ++*spins);
@@ -800,7 +829,7 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
 #pragma unroll
             for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             vm_drain();
-            if (lane == 0) __hip_atomic_store(done_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) publish_word(done_word, epoch);
         }
         lds_publish(&sl.freed, g + 1);  // the rows are in flight from registers
         if (gn >= ngroups) break;
@@ -844,20 +873,10 @@ struct PieceView {
     int plen;             // nodes per piece
     int rmax;             // nodes a fast repair may take (tests: force the slow path)
     unsigned long long* dbg;  // SM_PIECE_DEBUG: [fast, slow, sum of repair nodes, max, guess cycles, finish cycles]
+    uint32_t* err;        // the call's error word (host-mapped): bit 0 = a cross-workgroup wait timed out
+    int wait_iters;       // polls before a wait gives up
 };
 
-__device__ __forceinline__ uint32_t wait_word(const uint32_t* p, uint32_t lo, uint32_t hi) {
-    uint32_t v = 0;
-    for (int it = 0; it < (1 << 24); ++it) {
-        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v >= lo && v <= hi) break;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return v;
-}
-__device__ __forceinline__ void publish_word(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 template <int SPL>
 __device__ __forceinline__ void agent_row_read(const double* U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
     const double* p = U + (size_t)slot * Dpad + lane * SPL;
@@ -1032,7 +1051,7 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     const int top = head + len - 1;
     const uint32_t below = (uint32_t)(head + len);  // top node of the piece below
     double x[SPL];
-    wait_word(done + e - 1, epoch, epoch);
+    wait_word(done + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
     agent_row_read<SPL>(U, below, Dpad, lane, x);
     vm_drain();
@@ -1045,7 +1064,7 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     const int m = up_exact_walk<SPL, UP_WALK_CH(SPL)>(meta32, U, Cst, ring.slut, top, min(Q.rmax, len), Dpad, lane, x, fix, true);
     if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
     bool all = m >= 0;
-    for (int q = e - 1; all && q > e - (M - 1 - j); --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u) == 2u * epoch;
+    for (int q = e - 1; all && q > e - (M - 1 - j); --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u, Q.err, Q.wait_iters) == 2u * epoch;
     if (Q.dbg && lane == 0) {
         atomicAdd(Q.dbg + (all ? 0 : 1), 1ull);
         if (m >= 0) {
@@ -1064,7 +1083,7 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     }
     // slow path: the piece below is final (exact); repair again from its final top row, writing
     // through (the stored rows are still the chain's trajectory: nothing was committed)
-    wait_word(fin + e - 1, epoch, epoch);
+    wait_word(fin + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
     agent_row_read<SPL>(U, below, Dpad, lane, x);
     vm_drain();
@@ -1098,6 +1117,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     Q.plen = Q0.plen;
     Q.rmax = Q0.rmax;
     Q.dbg = Q0.dbg;
+    Q.err = Q0.err;
+    Q.wait_iters = Q0.wait_iters;
     const int e = blockIdx.x;
     uint4 pc = make_uint4((uint32_t)e, 0u, 1u, 0u);  // without pieces: block = path, one piece
     if (Q.pieces) {
@@ -1423,7 +1444,7 @@ __device__ void down_piece_agg(double* scratch, const uint32_t* __restrict__ met
 template <int SPL>
 __device__ void down_guess(double* scratch, double* guess, const double* __restrict__ A, const double* __restrict__ agg,
                            const uint32_t* aggw, uint32_t hp, int e, int i, int Dpad, int wave, int lane,
-                           uint32_t epoch) {
+                           uint32_t epoch, uint32_t* err, int wait_iters) {
     const int per = (i + CHN_WAVES - 1) / CHN_WAVES;
     const int q0 = min(i, wave * per), q1 = min(i, q0 + per);
     double P[SPL], B[SPL];
@@ -1434,7 +1455,7 @@ __device__ void down_guess(double* scratch, double* guess, const double* __restr
     }
     for (int q = q0; q < q1; ++q) {
         const int eq = e - i + q;
-        wait_word(aggw + eq, epoch, epoch);
+        wait_word(aggw + eq, epoch, epoch, err, wait_iters);
         vm_drain();
         double p[SPL], b[SPL];
         agent_row_read<SPL>(agg + (size_t)eq * 2 * Dpad, 0, Dpad, lane, p);
@@ -1564,7 +1585,7 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
     const bool last_pub = i + 1 < M;
     const uint32_t above = (uint32_t)(head - 1);  // last node of the piece above
     double x[SPL];
-    wait_word(done + e - 1, epoch, epoch);
+    wait_word(done + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
     agent_row_read<SPL>(V.A, above, Dpad, lane, x);
     vm_drain();
@@ -1573,7 +1594,7 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
     vm_drain();
     if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
     bool all = m >= 0;
-    for (int q = e - 1; all && q > e - i; --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u) == 2u * epoch;
+    for (int q = e - 1; all && q > e - i; --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u, Q.err, Q.wait_iters) == 2u * epoch;
     if (Q.dbg && lane == 0) {
         atomicAdd(Q.dbg + (all ? 4 : 5), 1ull);
         if (m >= 0) {
@@ -1585,7 +1606,7 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
         if (lane == 0) publish_word(fin + e, epoch);
         return;
     }
-    wait_word(fin + e - 1, epoch, epoch);
+    wait_word(fin + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
     agent_row_read<SPL>(V.A, above, Dpad, lane, x);
     vm_drain();
@@ -1627,6 +1648,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     Q.plen = Q0.plen;
     Q.rmax = Q0.rmax;
     Q.dbg = Q0.dbg;
+    Q.err = Q0.err;
+    Q.wait_iters = Q0.wait_iters;
     // work item: piece i of M of a cut path (entries list a path's pieces bottom first with index
     // j: i = M - 1 - j, pieces top first), or a run of w whole paths (M == 1)
     uint4 pc = make_uint4((uint32_t)pidx, 0u, 1u, 1u);
@@ -1677,7 +1700,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
         }
         if (i > 0)
             down_guess<SPL>(scratch, guess, V.A, Q.agg, aggw, uniform(meta32[(size_t)path.head * 8 + 1]), pidx, i, Dpad, wave,
-                            lane, epoch);
+                            lane, epoch, Q.err, Q.wait_iters);
     }
     for (int k = threadIdx.x; k < DownCfg<SPL>::NS; k += CHN_THREADS) {
         ring.s[k].staged = ring.s[k].freed = 0;
@@ -1725,7 +1748,8 @@ static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
 }
 
 static PieceView piece_view(const WalkArgs& a, int v) {
-    return PieceView{a.pieces[v], a.npieces[v], a.agg[v], a.fix[v], a.pstat[v], a.pstride, a.piece_len, a.repair_max, a.piece_dbg};
+    return PieceView{a.pieces[v], a.npieces[v], a.agg[v], a.fix[v], a.pstat[v], a.pstride, a.piece_len, a.repair_max, a.piece_dbg,
+                     a.err, a.wait_iters};
 }
 
 template <int SPL>

@@ -835,26 +835,6 @@ hipError_t launch_rows_to_volume(hipStream_t st, const SmMeta* meta, const doubl
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------------------------
-// left-right consistency check, fill = false (Stereo3DMST.cpp:632-662 as called at :904): each left
-// pixel reads only right(x-d), so the in-place update is order-independent
-// ---------------------------------------------------------------------------------------------
-__global__ void k_lr_check(float* __restrict__ left, const float* __restrict__ right, int W, int H, int max_disp) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    if (x >= W) return;
-    const size_t idx = (size_t)y * W + x;
-    const float df = left[idx];
-    const int d = (int)roundf(df);  // round half away from zero, as round() on the float
-    bool bad = true;
-    if (x - d >= 0 && d >= 0 && d < max_disp) bad = fabsf(df - right[idx - d]) > 1.0f;
-    if (bad) left[idx] = 0.0f;
-}
-
-hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp) {
-    hipLaunchKernelGGL(k_lr_check, dim3((W + 255) / 256, H), dim3(256), 0, st, left, right, W, H, max_disp);
-    return hipGetLastError();
-}
-
 static CPair make_cpair(const MstArgs& a, const MstCompact& c) {
     CPair P;
     for (int v = 0; v < 2; ++v)

@@ -74,6 +74,8 @@ struct WalkArgs {
     int piece_len;
     int repair_max;       // fast-repair node cap (env SM_REPAIR_MAX; tests force the slow path)
     unsigned long long* piece_dbg;  // SM_PIECE_DEBUG counters (nullptr otherwise)
+    uint32_t* err;        // device error word of the call (host-mapped; sm_synchronize checks it)
+    int wait_iters;       // polls before a cross-workgroup wait gives up (env SM_WAIT_ITERS, tests)
 };
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
@@ -91,7 +93,12 @@ hipError_t launch_zero(hipStream_t st, const ZeroList& z);
 hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok);
 hipError_t launch_vol_rows(hipStream_t st, const float* vin, size_t N, int d0, int D, int Dpad, const uint32_t* slotpix,
                            float* Cst);
-hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp);
+// output step (sm_post.hip)
+hipError_t launch_label_to_disp(hipStream_t st, float* d0, float* d1, size_t N, int dmax);
+hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp, uint8_t* mask);
+hipError_t launch_lr_fill(hipStream_t st, float* left, const uint8_t* mask, int W, int H, int* scratch);
+hipError_t launch_occlusion(hipStream_t st, float* left, float* right, int W, int H, float thresh, int remove, float min_disp,
+                            uint8_t* occ, int* scratch);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 // long-path engine (sm_chain.hip): buckets of paths with >= SM_LONG_PATH nodes

@@ -93,7 +93,7 @@ extern "C" void stereo3dmst(std::string left_name, std::string right_name, cv::M
     sm_params p;
     sm_default_params(&p);
     p.disp_total = Dmax;
-    p.post = SM_POST_LR_CHECK;
+    p.post = SM_POST_LABEL_TO_DISP | SM_POST_LR_CHECK;  // LabelToDisp + scaling, then the L-R check (:900-904)
     if (mccnn) {
         if (sm_upload_cost_volumes(g_ctx, lv.data(), rv.data(), cols, rows, Dmax) != SM_OK) {
             std::cout << "stereo3dmst: " << sm_last_error(g_ctx) << "\n";

@@ -236,6 +236,100 @@ def test_full_size_c2_match_bitexact(gpu_ctx):
         assert np.array_equal(bits(out2[v]["minc"]), bits(out[v]["minc"]))
 
 
+def test_full_size_c3_match_bitexact(gpu_ctx):
+    """3840x2160 D=256 (BASELINE config C3: SPL=4, ~30k-node cut root paths, 4K MST and layout):
+    full WTA indices and fp64 minima of both views, bitwise against the oracle."""
+    W, H, D = 3840, 2160, 256
+    left, right, _ = make_pair(W, H, D, index=12)
+    out = gpu_ctx.match(left, right, D)
+    ref = O.match(left, right, D, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+def test_full_size_c3_slices_bitexact(gpu_ctx):
+    """C3 size: every fp64 A_up / A value of 4 slices (SPL=1 rows over the C3 tree), bitwise."""
+    W, H, d0, D = 3840, 2160, 150, 4
+    left, right, _ = make_pair(W, H, 256, index=12)
+    lv, rv = O.cost_agd(left, right, d0, d0 + D)
+    for vi, (img, vol) in enumerate(((left, lv), (right, rv))):
+        Aup, A = gpu_ctx.aggregate_debug(left, right, vi, d0, D)
+        r = O.tree_filter(W, H, O.build_tree(img), vol, d0, False, True, 16)
+        assert np.array_equal(bits(Aup), bits(r["Aup"]))
+        assert np.array_equal(bits(A), bits(r["A"]))
+
+
+@pytest.mark.parametrize("rank", [0, 3, 7])
+def test_full_size_c4_shard_with_reduce_bitexact(rank):
+    """BASELINE C4 as sharded: one 32-slice shard of 1920x1200 D=256 (rank r of 8 owns
+    [32r, 32r+32)), at full size, through a one-rank RCCL communicator so that the cross-rank
+    exchange (grouped all-reduce MIN of the fp64 minima, k_cand, all-reduce MIN of the candidate
+    index, k_finalize; sm_api.cpp stage_reduce) runs on the GPU.  With one rank the exchange must
+    return the shard's own strict-< minimum, so the result equals the oracle's tree filter over the
+    shard's slices, bitwise; the output step then scales with the TOTAL range (Dmax = 256)."""
+    import stereomatch_amd as sm
+    W, H, Dt = 1920, 1200, 256
+    d0, D = sm.shard_range(Dt, 8, rank)
+    left, right, _ = make_pair(W, H, Dt, index=13)
+    ctx = sm.Context(0)
+    try:
+        ctx.comm_init(1, 0, sm.Context.unique_id())
+        out = ctx.match(left, right, D, sm.default_params(disp_begin=d0, disp_total=Dt))
+        outp = ctx.match(left, right, D, sm.default_params(disp_begin=d0, disp_total=Dt, post=sm.STEREO3DMST_POST))
+        assert ctx.stage_times()["reduce_ms"] > 0
+    finally:
+        ctx.close()
+    lv, rv = O.cost_agd(left, right, d0, d0 + D)
+    ref = {}
+    for v, img, vol in (("left", left, lv), ("right", right, rv)):
+        r = O.tree_filter(W, H, O.build_tree(img), vol, d0, True, False, 16)
+        ref[v] = r["idx"].reshape(H, W)
+        np.testing.assert_array_equal(out[v]["idx"], ref[v])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
+        np.testing.assert_array_equal(out[v]["disp"], ref[v].astype(np.float32))
+    lref, rref = O.stereo3dmst_output(ref["left"], ref["right"], Dt)
+    np.testing.assert_array_equal(outp["left"]["disp"], lref)
+    np.testing.assert_array_equal(outp["right"]["disp"], rref)
+
+
+def test_chain_wait_timeout_is_an_error(monkeypatch):
+    """A cross-workgroup wait of the chain engine that never sees its status word must not return
+    SM_OK: SM_WAIT_ITERS=0 makes every such wait give up at once, which sets the call's device error
+    word; sm_synchronize reports SM_ERR_STATE.  The next call (normal waits) is exact again."""
+    import stereomatch_amd as sm
+    monkeypatch.setenv("SM_PIECE_LEN", "64")  # cut paths: pieces wait for their neighbours
+    W, H, D = 320, 240, 64
+    left, right, _ = make_pair(W, H, D, index=4)
+    ctx = sm.Context(0)
+    try:
+        monkeypatch.setenv("SM_WAIT_ITERS", "0")
+        with pytest.raises(sm.StereoMSTError, match="SM_ERR_STATE.*timed out"):
+            ctx.match(left, right, D)
+        monkeypatch.delenv("SM_WAIT_ITERS")
+        out = ctx.match(left, right, D)
+    finally:
+        ctx.close()
+    ref = O.match(left, right, D, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+def test_large_disp_begin_pads(gpu_ctx):
+    """A shard far into the disparity range (disp_begin + 64*SPL > the default 1024-record image
+    pad): the record pad grows with the call's range, results stay exact."""
+    import stereomatch_amd as sm
+    W, H, d0, D = 1400, 40, 1100, 24
+    left, right, _ = make_pair(W, H, 64, index=3)
+    out = gpu_ctx.match(left, right, D, sm.default_params(disp_begin=d0))
+    lv, rv = O.cost_agd(left, right, d0, d0 + D)
+    for v, vol in (("left", lv), ("right", rv)):
+        r = O.tree_filter(W, H, O.build_tree(left if v == "left" else right), vol, d0, True, False, 16)
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), r["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
+
+
 def test_flir_c1_bitexact(gpu_ctx):
     """BASELINE config 0: the FLIR 000020 pair, 2048x1536, D=64."""
     from PIL import Image
@@ -257,23 +351,63 @@ def test_errors_are_loud(gpu_ctx):
     import stereomatch_amd as sm
     left, right, _ = make_pair(32, 16, 8)
     with pytest.raises(sm.StereoMSTError):
-        gpu_ctx.match(left, right, 8, sm.default_params(c=5000.0))  # segment mode: not yet
-    with pytest.raises(sm.StereoMSTError):
         gpu_ctx.match(left, right, 0)
+    with pytest.raises(sm.StereoMSTError):  # shard beyond the declared total range
+        gpu_ctx.match(left, right, 8, sm.default_params(disp_begin=4, disp_total=8))
+    with pytest.raises(sm.StereoMSTError):  # fill without the check
+        gpu_ctx.match(left, right, 8, sm.default_params(post=sm.SM_POST_LR_FILL))
+    with pytest.raises(sm.StereoMSTError):
+        gpu_ctx.match(left, right, 8, sm.default_params(post=sm.SM_POST_OCCLUSION | sm.SM_POST_OCCLUSION_ZERO))
 
 
-def test_reference_surface(gpu_ctx):
+@pytest.mark.parametrize("Dmax", [16, 48, 100, 128])
+def test_reference_surface(gpu_ctx, Dmax):
+    """stereo3dmst's output contract: LabelToDisp + *= (Dmax-1.f) in float on both maps, then the
+    fill-less L-R check of the left map (Stereo3DMST.cpp:189-201, 900-904).  At Dmax = 48 / 100 the
+    float round trip moves some integer disparities by an ulp, which the check then sees."""
     import stereomatch_amd as sm
-    left, right, _ = make_pair(96, 64, 16, index=4)
+    left, right, _ = make_pair(160, 96, Dmax, index=4)
     sm.startTimer()
-    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "AGD", 16)
+    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "AGD", Dmax)
     assert sm.getTimer() >= 0
-    ref = O.match(left, right, 16)
+    ref = O.match(left, right, Dmax, nthreads=16)
     H, W = left.shape[:2]
-    lref = ref["left"]["idx"].astype(np.float32).reshape(H, W)
-    rref = ref["right"]["idx"].astype(np.float32).reshape(H, W)
-    np.testing.assert_array_equal(ld, O.lr_check(lref, rref, 16))  # Stereo3DMST.cpp:904
+    lref, rref = O.stereo3dmst_output(ref["left"]["idx"].reshape(H, W), ref["right"]["idx"].reshape(H, W), Dmax)
+    np.testing.assert_array_equal(ld, lref)
     np.testing.assert_array_equal(rd, rref)
+
+
+@pytest.mark.parametrize("W,H,D", [(200, 120, 48), (301, 47, 100), (256, 128, 128)])
+@pytest.mark.parametrize("fill", [False, True])
+def test_output_step_bitexact(gpu_ctx, W, H, D, fill):
+    """SM_POST_LABEL_TO_DISP | SM_POST_LR_CHECK [| SM_POST_LR_FILL] against the oracle's literal
+    restatement of :189-201, :632-709, :900-904; idx stays the integral WTA index."""
+    import stereomatch_amd as sm
+    post = sm.SM_POST_LABEL_TO_DISP | sm.SM_POST_LR_CHECK | (sm.SM_POST_LR_FILL if fill else 0)
+    left, right, _ = make_pair(W, H, D, index=5)
+    out = gpu_ctx.match(left, right, D, sm.default_params(post=post, disp_total=D))
+    ref = O.match(left, right, D, nthreads=16)
+    li, ri = ref["left"]["idx"].reshape(H, W), ref["right"]["idx"].reshape(H, W)
+    lref, rref = O.stereo3dmst_output(li, ri, D, fill)
+    np.testing.assert_array_equal(out["left"]["disp"], lref)
+    np.testing.assert_array_equal(out["right"]["disp"], rref)
+    np.testing.assert_array_equal(out["left"]["idx"], li)
+
+
+@pytest.mark.parametrize("remove", [False, True])
+@pytest.mark.parametrize("W,H,D", [(200, 120, 48), (1500, 16, 64)])
+def test_occlusion_post_bitexact(gpu_ctx, W, H, D, remove):
+    """SM_POST_OCCLUSION[_ZERO] = handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288) on the
+    WTA maps, against the oracle (rows wider than the reference's 1024-thread limit included)."""
+    import stereomatch_amd as sm
+    post = sm.SM_POST_OCCLUSION_ZERO if remove else sm.SM_POST_OCCLUSION
+    left, right, _ = make_pair(W, H, D, index=6)
+    out = gpu_ctx.match(left, right, D, sm.default_params(post=post))
+    ref = O.match(left, right, D, nthreads=16)
+    Lr, Rr = O.occlusion(ref["left"]["idx"].reshape(H, W).astype(np.float32),
+                         ref["right"]["idx"].reshape(H, W).astype(np.float32), 0, 1.0, remove)
+    np.testing.assert_array_equal(out["left"]["disp"], Lr)
+    np.testing.assert_array_equal(out["right"]["disp"], Rr)
 
 
 @pytest.mark.parametrize("W,H,D", [(128, 80, 32), (301, 47, 100), (64, 9, 200)])
@@ -456,6 +590,6 @@ def test_stereo3dmst_mccnn_ingest(gpu_ctx, tmp_path, monkeypatch):
     ref = {}
     for v, img, vol in (("left", left, lv), ("right", right, rv)):
         ref[v] = O.tree_filter(W, H, O.build_tree(img), O.mccnn_clamp(vol), 0, True, False, 16)["idx"]
-    rdisp = ref["right"].reshape(H, W).astype(np.float32)
-    np.testing.assert_array_equal(rd, rdisp)
-    np.testing.assert_array_equal(ld, O.lr_check(ref["left"].reshape(H, W).astype(np.float32), rdisp, D))
+    lref, rref = O.stereo3dmst_output(ref["left"].reshape(H, W), ref["right"].reshape(H, W), D)
+    np.testing.assert_array_equal(rd, rref)
+    np.testing.assert_array_equal(ld, lref)
