@@ -2,20 +2,23 @@
 """bench.py -- BASELINE.json metric: cost-volume voxels/s (W*H*D per frame = both views)
 and ms/frame, 1920x1200 D=128 synthetic pair on one MI355X; D-sharded over N GPUs.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode weak|strong|batch]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode strong|weak|batch]
     torchrun ... bench.py --gpus N ...   (one process per GPU, RCCL over xGMI)
 
 One step = one frame: both views through the whole path with the images already in HBM
 (median, weights, Boruvka MST, tree layout, leaf->root and root->leaf passes, WTA, and for
-N>1 the RCCL min+argmin reduce).  Modes for N>1:
-  weak   (default): each rank owns 128 disparities, total D = 128*N, one cross-rank reduce
-  strong          : total D = 256 split over N ranks (BASELINE config C4)
-  batch           : one independent pair per rank, no collective (config C5 shape)
-Rank 0 prints ONE JSON line.
+N>1 the RCCL min+argmin reduce).  N=1 runs BASELINE config C2 (1920x1200 D=128).  Modes for N>1:
+  strong (default): total D = 256 split over N ranks (BASELINE config C4, 32 disparities/GPU at N=8)
+  weak            : each rank owns 128 disparities, total D = 128*N, one cross-rank reduce
+  batch           : one independent 3840x2160 D=256 pair per rank, no collective (config C5)
+Launched without torchrun, --gpus N > 1 starts the N rank processes itself (before any GPU call);
+under torchrun, WORLD_SIZE must equal --gpus.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,29 +38,83 @@ CONFIG_NAMES = {(1920, 1200, 128): " (BASELINE C2)", (3840, 2160, 256): " (BASEL
                 (1920, 1200, 256): " (BASELINE C4 size, unsharded)"}
 
 
-def cpu_baseline(W, H, D, slices, threads):
-    """Oracle (CPU restatement, reference order, fp64) on a bounded sample of the workload:
-    the full MST build of both views + `slices` disparity slices of cost and tree filter,
-    extrapolated to D slices.  Test infrastructure, used only as the reported baseline."""
+def host_cpu_info():
+    """nproc, the cores this process may use, the CPU model and OMP_NUM_THREADS."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return dict(nproc=os.cpu_count(), affinity=usable, model=model, OMP_NUM_THREADS=omp)
+
+
+def cpu_baseline(W, H, D, slices, slices_1t):
+    """Oracle (CPU restatement, reference order, fp64) on a bounded sample of the workload: the full
+    MST build of both views (one thread: Kruskal is serial), then `slices` disparity slices of AGD cost
+    + tree filter + WTA with all usable host cores (OpenMP over slices; the box's share: OMP_NUM_THREADS when set) and `slices_1t`
+    slices with one thread, each extrapolated to D slices.  Test infrastructure, used only as the
+    reported baseline (never inside the timed region)."""
     from oracle import oracle as O
+    info = host_cpu_info()
+    threads = int(info["OMP_NUM_THREADS"] or 0) or info["affinity"]
+    threads = max(1, min(threads, info["affinity"]))
     left, right, _ = make_pair(W, H, D, index=0)
     t0 = time.perf_counter()
     trees = [O.build_tree(left), O.build_tree(right)]
     t_tree = time.perf_counter() - t0
-    d0 = D // 2 - slices // 2
-    t0 = time.perf_counter()
-    lv, rv = O.cost_agd(left, right, d0, d0 + slices)
-    t_cost = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    for t, vol in zip(trees, (lv, rv)):
-        O.tree_filter(W, H, t, vol, d0, True, False, threads)
-    t_filter = time.perf_counter() - t0
-    frame = t_tree + (t_cost + t_filter) * (D / slices)
+
+    def sample(n, nt):
+        d0 = D // 2 - n // 2
+        t0 = time.perf_counter()
+        lv, rv = O.cost_agd(left, right, d0, d0 + n, nt)  # OpenMP over slices
+        t_cost = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for t, vol in zip(trees, (lv, rv)):
+            O.tree_filter(W, H, t, vol, d0, True, False, nt)
+        return t_cost, time.perf_counter() - t0
+
+    tc, tf = sample(slices, threads)
+    frame = t_tree + (tc + tf) * (D / slices)
+    tc1, tf1 = sample(slices_1t, 1)
+    frame1 = t_tree + (tc1 + tf1) * (D / slices_1t)
     return dict(value=W * H * D / frame, unit="voxels/s", cores=threads, kind="port",
-                sample="full %dx%d frame: MST+layout of both views (1 thread) + %d of %d slices of AGD cost (1 thread) "
-                       "and tree filter (%d threads, OpenMP over slices), extrapolated to D=%d; stage s: tree %.2f, "
-                       "cost %.2f, filter %.2f; est. ms/frame %.0f" % (W, H, slices, D, threads, D, t_tree, t_cost,
-                                                                      t_filter, frame * 1e3))
+                one_thread=dict(value=W * H * D / frame1, ms_per_frame=frame1 * 1e3, cost_s=tc1, filter_s=tf1,
+                                slices=slices_1t),
+                host=info,
+                stages_s=dict(tree_both_views=t_tree, cost=tc, filter_up_down_wta=tf),
+                sample="full %dx%d frame: MST+BFS of both views (1 thread) + %d of %d slices of AGD cost, "
+                       "tree filter and WTA (%d threads, OpenMP over slices), extrapolated to D=%d; est. ms/frame %.0f "
+                       "(1 thread: %d slices, %.0f ms/frame)" % (W, H, slices, D, threads, D, frame * 1e3, slices_1t,
+                                                                  frame1 * 1e3))
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """One process per GPU, started before this process touches a GPU (no exec: children)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def main():
@@ -65,19 +122,35 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--mode", default="weak", choices=["weak", "strong", "batch"])
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1200)
-    ap.add_argument("--disp", type=int, default=128, help="disparities per rank (weak) / total (strong: 256 default)")
+    ap.add_argument("--mode", default=None, choices=["strong", "weak", "batch"],
+                    help="N>1 partitioning (default strong = BASELINE C4)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--disp", type=int, default=None,
+                    help="disparities: total (N=1, strong, batch) or per rank (weak); default per config")
     ap.add_argument("--cpu-slices", type=int, default=32)
+    ap.add_argument("--cpu-slices-1t", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-io", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        args.gpus = world
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    if args.mode is None:
+        args.mode = "strong" if world > 1 else "weak"
+    big = args.mode == "batch"  # C5: 3840x2160 D=256 pairs
+    if args.width is None:
+        args.width = 3840 if big else 1920
+    if args.height is None:
+        args.height = 2160 if big else 1200
+    if args.disp is None:
+        args.disp = 256 if (big or (args.mode == "strong" and world > 1)) else 128
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -88,7 +161,7 @@ def main():
         Dtot = Dloc * world if args.mode == "weak" else Dloc
         dbeg = rank * Dloc
     elif args.mode == "strong":
-        Dtot = 256 if args.disp == 128 else args.disp
+        Dtot = args.disp
         dbeg, Dloc = sm.shard_range(Dtot, world, rank)
     else:  # batch
         Dloc = Dtot = args.disp
@@ -156,6 +229,21 @@ def main():
         ctx.match_async(Dloc, params)
         ctx.synchronize()
         accumulate(kall)
+    # end to end with host buffers (sm_match: image upload + frame + result download over PCIe);
+    # reported beside the resident-input value, never as it
+    host_io = None
+    if not args.no_host_io:
+        ctx.match(left, right, Dloc, params)
+        barrier()
+        th = time.perf_counter()
+        nh = 3
+        for _ in range(nh):
+            ctx.match(left, right, Dloc, params)
+        barrier()
+        host_ms = (time.perf_counter() - th) * 1e3 / nh
+        host_io = {"ms_per_frame": host_ms, "value": W * H * Dtot_frame / (host_ms * 1e-3),
+                   "what": "sm_match with host buffers: 2 x %d B images up, disp f32 + idx i32 + min f64 of both "
+                           "views down (%d B), synchronous, %d frames" % (W * H * 3, W * H * 16 * 2, nh)}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -198,7 +286,11 @@ def main():
         "data": "synthetic (seeded slanted-plane stereo pair, tools/synth.py)",
         "config": {"workload": "%dx%d D=%d both views%s" % (W, H, Dtot_frame, CONFIG_NAMES.get((W, H, Dtot_frame), ""))
                    if world == 1 else
-                   "%dx%d D=%d, %s mode, %d disparities/rank" % (W, H, Dtot_frame, args.mode, Dloc),
+                   "%dx%d D=%d, %s mode, %d disparities/rank%s" % (
+                       W, H, Dtot_frame, args.mode, Dloc,
+                       " (BASELINE C4)" if (args.mode == "strong" and (W, H, Dtot_frame) == (1920, 1200, 256)) else
+                       " (BASELINE C5: one pair per GPU)" if (args.mode == "batch" and (W, H, Dtot_frame) == (3840, 2160, 256))
+                       else ""),
                    "W": W, "H": H, "D": Dtot_frame, "disparities_per_rank": Dloc,
                    "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -211,10 +303,10 @@ def main():
                                      "timing": "diagnostic pass of %d frames after the timed region, every launch timed" % diag_steps}},
         "kernels_ms_per_step": {k: v["ms"] / diag_steps for k, v in kall.items()},
         "stages_ms": {k: v / args.steps for k, v in stage_acc.items()},
+        "host_io": host_io,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame, args.cpu_slices, threads)
+        line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame, args.cpu_slices, args.cpu_slices_1t)
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -37,7 +37,7 @@ def lib():
         L.orc_segment.restype = c_int
         L.orc_bfs.argtypes = [c_int, c_int, u16p, u16p, u8p, i32p, i32p, i32p, u16p, u8p, i32p]
         L.orc_bfs.restype = c_int
-        L.orc_cost_agd.argtypes = [u8p, u8p, c_int, c_int, c_int, c_int, c_int, vp, vp]
+        L.orc_cost_agd.argtypes = [u8p, u8p, c_int, c_int, c_int, c_int, c_int, vp, vp, c_int]
         L.orc_tree_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, i32p, i32p, i32p, u16p, u8p,
                                       i32p, f32p, vp, vp, vp, vp, c_int]
         L.orc_s_lut.restype = ctypes.POINTER(ctypes.c_double)
@@ -47,6 +47,7 @@ def lib():
         L.orc_lr_check.argtypes = [vp, vp, c_int, c_int, c_int]
         L.orc_lr_check_fill.argtypes = [vp, vp, c_int, c_int, c_int, c_int]
         L.orc_label_to_disp.argtypes = [vp, ctypes.c_long, c_int]
+        L.orc_set_agd_contract.argtypes = [c_int]
         L.orc_occlusion.argtypes = [vp, vp, c_int, c_int, c_int, c_float, c_int]
         _LIB = L
     return _LIB
@@ -116,13 +117,18 @@ def bfs(W, H, wR, wD, mask):
                 node_w=node_w, node_nch=node_nch, node_child=node_child)
 
 
-def cost_agd(left, right, d0, d1):
+def set_agd_contract(mode):
+    """Oracle-only switch: 1 = the AGD cost with the FMAs nvcc's default --fmad=true forms."""
+    lib().orc_set_agd_contract(int(mode))
+
+
+def cost_agd(left, right, d0, d1, nthreads=0):
     left = np.ascontiguousarray(left, dtype=np.uint8)
     right = np.ascontiguousarray(right, dtype=np.uint8)
     H, W, _ = left.shape
     lv = np.empty((d1 - d0, H, W), np.float32)
     rv = np.empty((d1 - d0, H, W), np.float32)
-    lib().orc_cost_agd(left, right, W, H, W * 3, d0, d1, _ptr(lv), _ptr(rv))
+    lib().orc_cost_agd(left, right, W, H, W * 3, d0, d1, _ptr(lv), _ptr(rv), int(nthreads))
     return lv, rv
 
 
@@ -161,7 +167,7 @@ def build_tree(img, c=float("inf"), min_size=200):
 def match(left, right, D, c=float("inf"), min_size=200, want_volumes=False, nthreads=0):
     """The whole path on the CPU: both views, slices 0..D-1.  Returns per-view dicts."""
     H, W, _ = left.shape
-    lv, rv = cost_agd(left, right, 0, D)
+    lv, rv = cost_agd(left, right, 0, D, nthreads)
     out = {}
     for name, img, vol in (("left", left, lv), ("right", right, rv)):
         tree = build_tree(img, c, min_size)

@@ -261,9 +261,17 @@ float orc_agd_color_term(int l1) {
     return 0.11f * fminf(scaled, 7.0f);
 }
 
+/* Contraction variant (oracle-only switch, DESIGN.md "AGD contraction"): 0 = the shipped restatement,
+ * no contraction; 1 = what an LLVM-based CUDA compiler with --fmad=true (nvcc's default; the
+ * reference's CMakeLists.txt:19-20 sets no --fmad) forms from the same expressions:
+ * a*b + c*d -> fma(a, b, c*d) and (..) + e*f -> fma(e, f, ..). */
+static int g_agd_contract = 0;
+void orc_set_agd_contract(int mode) { g_agd_contract = mode; }
+
 static inline float gray_of(const uint8_t* bgr) {
     /* 0.114f*B + 0.587f*G + 0.299f*R, left-to-right, no contraction (:1529-1530) */
     const float b = (float)bgr[0], g = (float)bgr[1], r = (float)bgr[2];
+    if (g_agd_contract) return fmaf(0.299f, r, fmaf(0.114f, b, 0.587f * g));
     float t = 0.114f * b;
     t = t + 0.587f * g;
     t = t + 0.299f * r;
@@ -279,16 +287,26 @@ static inline float agd_cost(const uint8_t* r0, const uint8_t* l0) {
     ref_gray = gray_of(r0 + 3);
     match_gray = gray_of(l0 + 3);
     g += ref_gray - match_gray;
-    const float a = 0.11f * fminf((float)((double)color_l1 * 0.33333333333), 7.0f);
-    const float b = 0.89f * fminf(fabsf(g), 2.0f);
+    const float x = fminf((float)((double)color_l1 * 0.33333333333), 7.0f);
+    const float y = fminf(fabsf(g), 2.0f);
+    if (g_agd_contract) return 0.f + fmaf(0.11f, x, 0.89f * y);
+    const float a = 0.11f * x;
+    const float b = 0.89f * y;
     float cost = 0.f;
     cost += a + b;
     return cost;
 }
 
 void orc_cost_agd(const uint8_t* left, const uint8_t* right, int W, int H, int stride, int d0, int d1,
-                  float* left_vol, float* right_vol) {
+                  float* left_vol, float* right_vol, int nthreads) {
+    /* slices are independent: OpenMP over d (nthreads <= 0: the OpenMP default) */
     const size_t N = (size_t)W * H;
+#ifdef _OPENMP
+    const int nt = nthreads > 0 ? nthreads : omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#else
+    (void)nthreads;
+#endif
     for (int d = d0; d < d1; ++d) {
         float* rv = right_vol ? right_vol + (size_t)(d - d0) * N : NULL;
         float* lv = left_vol ? left_vol + (size_t)(d - d0) * N : NULL;
