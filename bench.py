@@ -7,7 +7,9 @@ and ms/frame, 1920x1200 D=128 synthetic pair on one MI355X; D-sharded over N GPU
 
 One step = one frame: both views through the whole path with the images already in HBM
 (median, weights, Boruvka MST, tree layout, leaf->root and root->leaf passes, WTA, and for
-N>1 the RCCL min+argmin reduce).  N=1 runs BASELINE config C2 (1920x1200 D=128).  Modes for N>1:
+N>1 the RCCL min+argmin reduce).  Frames are streamed with up to 3 in flight (--inflight): each
+in-flight frame has its own context (buffers + HIP stream), so the next frame's prep / MST / layout
+runs while the previous frame's tree filter does; every frame is computed in full.  N=1 runs BASELINE config C2 (1920x1200 D=128).  Modes for N>1:
   strong (default): total D = 256 split over N ranks (BASELINE config C4, 32 disparities/GPU at N=8)
   weak            : each rank owns 128 disparities, total D = 128*N, one cross-rank reduce
   batch           : one independent 3840x2160 D=256 pair per rank, no collective (config C5)
@@ -132,6 +134,8 @@ def main():
     ap.add_argument("--cpu-slices-1t", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-io", action="store_true")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight (contexts on their own streams); 0 = 3, fewer where memory needs it")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -171,64 +175,83 @@ def main():
     else:
         Dtot_frame = Dtot
 
-    ctx = sm.Context(local)
+    # frames in flight: each context is a full pipeline on its own stream; frame i goes to context
+    # i % n, so frame i+1's prep / MST / layout overlaps frame i's tree filter on the GPU
+    per_ctx_gb = W * H * (64 * (1 if Dloc <= 64 else 2 if Dloc <= 128 else 4)) * 20 * 2 / 1e9 + W * H * 400 / 1e9
+    inflight = args.inflight if args.inflight > 0 else max(1, min(3, int(200.0 // per_ctx_gb)))
+    ctxs = [sm.Context(local) for _ in range(inflight)]
     if world > 1 and args.mode != "batch":
-        uid = [sm.Context.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(world, rank, uid[0])
+        for c in ctxs:  # one communicator per context: its reduce runs on its own stream
+            uid = [sm.Context.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            c.comm_init(world, rank, uid[0])
     pair_index = rank if args.mode == "batch" else 0
     left, right, _ = make_pair(W, H, Dtot_frame, index=pair_index)
-    ctx.upload(left, right)
+    for c in ctxs:
+        c.upload(left, right)
     params = sm.default_params(disp_begin=dbeg, disp_total=Dtot_frame)
     torch.cuda.set_device(local)
+    ctx = ctxs[0]
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    def accumulate(acc):
-        for k, v in ctx.kernel_stats().items():
+    def accumulate(acc, c):
+        for k, v in c.kernel_stats().items():
             a = acc.setdefault(k, dict(launches=0, ms=0.0, voxels=0.0, bytes_per_voxel=v["bytes_per_voxel"]))
             a["launches"] += v["launches"]
             a["ms"] += v["ms"]
             a["voxels"] += v["voxels"]
 
-    for _ in range(args.warmup):
-        ctx.match_async(Dloc, params)
-        ctx.synchronize()
-    if args.warmup == 0:  # one untimed call to find the dominant kernel family
-        ctx.match_async(Dloc, params)
-        ctx.synchronize()
+    for _ in range(max(args.warmup, 1)):
+        for c in ctxs:
+            c.match_async(Dloc, params)
+            c.synchronize()
     # roofline kernel: the tree-filter family with the largest summed launch time.  Inside the
     # timed region only its launches carry HIP events (each event record costs GPU time between
     # launches: timing every family adds ~0.14 ms per C2 frame); the other families are timed
     # in a diagnostic pass after the timed region (kernels_ms_per_step, tree_filter)
     warm = {}
-    accumulate(warm)
+    accumulate(warm, ctx)
     dom = max(warm, key=lambda k: warm[k]["ms"])
-    ctx.set_kernel_timing([dom])
+    for c in ctxs:
+        c.set_kernel_timing([dom])
+        c.synchronize()
     barrier()
-    ctx.synchronize()
     torch.cuda.synchronize()
     stage_acc = {}
     kacc = {}
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.match_async(Dloc, params)
-        ctx.synchronize()  # per-step sync: the per-launch HIP-event timings are read here
-        for k, v in ctx.stage_times().items():
+
+    def retire(c):  # wait for context c's frame; its per-launch HIP-event timings are read here
+        c.synchronize()
+        for k, v in c.stage_times().items():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
-        accumulate(kacc)
+        accumulate(kacc, c)
+
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ctxs[i % inflight].match_async(Dloc, params)  # returns once the frame's filter is enqueued
+        if i >= inflight - 1:
+            retire(ctxs[(i - inflight + 1) % inflight])
+    for i in range(max(0, args.steps - inflight + 1), args.steps):
+        retire(ctxs[i % inflight])
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_kernel_timing(None)
+    # diagnostic pass, one frame at a time: every family timed (kernels_ms_per_step, tree_filter,
+    # roofline.isolated) and the single-frame latency
+    for c in ctxs:
+        c.set_kernel_timing(None)
     diag_steps = 2
     kall = {}
+    lat = []
     for _ in range(diag_steps):
+        tl = time.perf_counter()
         ctx.match_async(Dloc, params)
         ctx.synchronize()
-        accumulate(kall)
+        lat.append((time.perf_counter() - tl) * 1e3)
+        accumulate(kall, ctx)
     # end to end with host buffers (sm_match: image upload + frame + result download over PCIe);
     # reported beside the resident-input value, never as it
     host_io = None
@@ -257,6 +280,9 @@ def main():
     d = kacc[dom]
     dom_bytes = d["voxels"] * d["bytes_per_voxel"]
     achieved = dom_bytes / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
+    di = kall[dom]
+    iso_ms = di["ms"] / max(di["launches"], 1)
+    iso_bytes = di["voxels"] * di["bytes_per_voxel"] / max(di["launches"], 1)
     filt_ms = sum(v["ms"] for v in kall.values()) / diag_steps  # per frame, diagnostic pass
     filt_bytes = sum(v["voxels"] * v["bytes_per_voxel"] for v in kall.values()) / diag_steps
     traffic = None
@@ -292,24 +318,33 @@ def main():
                        " (BASELINE C5: one pair per GPU)" if (args.mode == "batch" and (W, H, Dtot_frame) == (3840, 2160, 256))
                        else ""),
                    "W": W, "H": H, "D": Dtot_frame, "disparities_per_rank": Dloc,
-                   "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world},
+                   "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world,
+                   "frames_in_flight": inflight},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "launches_per_step": d["launches"] / args.steps,
                      "alg_bytes_per_launch": dom_bytes / max(d["launches"], 1),
                      "avg_launch_ms": d["ms"] / max(d["launches"], 1),
+                     "timing": "HIP events on the launch stream around every %s launch of the timed region, "
+                               "%d frames in flight (launches share the GPU with the other frames' work)" % (dom, inflight),
+                     "isolated": {"avg_launch_ms": iso_ms, "achieved": iso_bytes / (iso_ms * 1e-3) / 1e9 if iso_ms > 0 else 0.0,
+                                  "frac": iso_bytes / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if iso_ms > 0 else 0.0,
+                                  "timing": "diagnostic pass, one frame at a time"},
                      "tree_filter": {"alg_bytes_per_step": filt_bytes, "ms_per_step": filt_ms,
                                      "achieved": filt_bytes / (filt_ms * 1e-3) / 1e9 if filt_ms > 0 else 0.0,
                                      "timing": "diagnostic pass of %d frames after the timed region, every launch timed" % diag_steps}},
         "kernels_ms_per_step": {k: v["ms"] / diag_steps for k, v in kall.items()},
         "stages_ms": {k: v / args.steps for k, v in stage_acc.items()},
+        "latency_ms_per_frame": min(lat),
+        "frames_in_flight": inflight,
         "host_io": host_io,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame, args.cpu_slices, args.cpu_slices_1t)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

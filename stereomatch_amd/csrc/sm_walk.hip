@@ -158,6 +158,9 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
             }
 #pragma unroll
             for (int k = 0; k < SPL; ++k) xc[k] = acc[k] + (double)c[j][k];
+#ifdef SM_EXP_UP_HEADS_ONLY  // timing experiment only (wrong results): store path heads' rows only
+            if (mfield(mv, j, 1) != (uint32_t)(top - j) - 1u)
+#endif
             store_row<SPL>(U, (uint32_t)(top - j), Dpad, lane, xc);
         }
     }
@@ -265,7 +268,11 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
             const uint32_t slot = (uint32_t)(c0 + jj);
             par[j] = mfield(cur, jj, 1);
             const bool head_j = par[j] == SM_NONE || par[j] != slot - 1u;
+#ifdef SM_EXP_DN_HEADS_ONLY  // timing experiment only (wrong results): read path heads' rows only
+            if (head_j) load_row<SPL>(V.U, slot, Dpad, lane, u[j]); else for (int q = 0; q < SPL; ++q) u[j][q] = 0.0;
+#else
             load_row<SPL>(V.U, slot, Dpad, lane, u[j]);
+#endif
             if (head_j && par[j] != SM_NONE) {  // wave-uniform: only path heads read their parent's row
                 load_row<SPL>(V.A, par[j], Dpad, lane, xp[j]);
             } else {
