@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--cpu-slices-1t", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-io", action="store_true")
+    ap.add_argument("--segment-c", type=float, default=float("inf"),
+                    help="finite: segment mode (Stereo3DMST's c, e.g. 5000) instead of the MST")
+    ap.add_argument("--min-size", type=int, default=200)
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight (contexts on their own streams); 0 = 3, fewer where memory needs it")
     args = ap.parse_args()
@@ -189,7 +192,7 @@ def main():
     left, right, _ = make_pair(W, H, Dtot_frame, index=pair_index)
     for c in ctxs:
         c.upload(left, right)
-    params = sm.default_params(disp_begin=dbeg, disp_total=Dtot_frame)
+    params = sm.default_params(disp_begin=dbeg, disp_total=Dtot_frame, c=args.segment_c, min_size=args.min_size)
     torch.cuda.set_device(local)
     ctx = ctxs[0]
 
@@ -319,6 +322,8 @@ def main():
                        else ""),
                    "W": W, "H": H, "D": Dtot_frame, "disparities_per_rank": Dloc,
                    "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world,
+                   "tree": "MST" if args.segment_c == float("inf") else "segment forest c=%g min_size=%d" % (
+                       args.segment_c, args.min_size),
                    "frames_in_flight": inflight},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -13,7 +13,7 @@
  *                           MST_PMS label search
  *   sm_cost_volume      <- buildCostVolumeSharedMemoryBGR         src/PatchMatchStereoGPU.cu:1482-1550
  *   sm_upload_cost_volumes <- MC-CNN volume mmap + clamp          src/Stereo3DMST.cpp:764-803
- *   sm_build_tree       <- segment_image_other_init (MST mode)    src/Stereo3DMST.cpp:213-543
+ *   sm_build_tree[_p]   <- segment_image_other_init (MST / segment mode) src/Stereo3DMST.cpp:213-543
  *                           + segment_graph/universe              include/segment-graph.h:54-89
  *   sm_aggregate_debug  <- aggregateCostFromChildren/Parent       src/Stereo3DMST.cpp:120-158
  *   WTA inside sm_match <- MSTCostAggregationAndLabelUpdate :160-186 / selectDisparity
@@ -58,8 +58,10 @@ typedef struct {
 
 typedef struct {
     float gamma;       /* S = exp(-w*gamma); reference 1/12 (Stereo3DMST.cpp:830)    */
-    float c;           /* segment threshold; +INFINITY = MST mode (only mode so far) */
-    int min_size;      /* min component size (Stereo3DMST.cpp:832); unused in MST mode */
+    float c;           /* segment threshold: +INFINITY = MST mode (one tree); finite c >= 0 = segment
+                          mode, the forest of segment_graph(c) + the min-size merge, filtered per tree
+                          (segment-graph.h:54-89, Stereo3DMST.cpp:242-384; the reference uses 5000, :831) */
+    int min_size;      /* min component size of the merge (Stereo3DMST.cpp:293-307, 832); segment mode */
     int median_ksize;  /* 3 (Stereo3DMST.cpp:214); only 3 is supported             */
     int cost_kind;     /* sm_cost_kind                                              */
     int disp_begin;    /* first global disparity of this call (D sharding)          */
@@ -135,10 +137,22 @@ sm_status sm_cost_volume(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* ri
 sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int row_stride, uint8_t* mst_mask,
                         int32_t* parent_pix, int32_t* subtree_size, int32_t* slot_of_pix);
 
+/* The same with the tree of params p (NULL: MST mode): for finite p->c the segment forest of
+ * segment_graph(c) + the min-size merge (segment-graph.h:54-89, Stereo3DMST.cpp:242-307), each tree
+ * rooted at its first pixel (:342-384).  mask / parent_pix report the forest (roots: -1); subtree
+ * size and slot refer to the schedule tree the GPU builds (the forest linked at its roots);
+ * ntrees (may be NULL) gets the number of trees. */
+sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int row_stride, const sm_params* p,
+                          uint8_t* mst_mask, int32_t* parent_pix, int32_t* subtree_size, int32_t* slot_of_pix,
+                          int32_t* ntrees);
+
 /* Debug/parity: aggregated volumes of one view in [D][H][W] fp64 (A_up after the leaf->root
  * pass, A after root->leaf), slices [d0, d0+D).  Memory-hungry: for small images. */
 sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
                              int row_stride, int view, int d0, int D, double* A_up, double* A);
+/* ... over the tree of params p (NULL: MST mode; finite c: the segment forest, filtered per tree). */
+sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
+                               int row_stride, const sm_params* p, int view, int d0, int D, double* A_up, double* A);
 
 /* Per-stage timings of the last sm_match/sm_match_async (ms, from HIP events on the ctx
  * stream): [0] prep+median+weights, [1] MST, [2] tree layout, [3] up pass, [4] down pass+WTA,

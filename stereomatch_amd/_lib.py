@@ -76,7 +76,9 @@ def lib():
         "sm_download_results": ([vp, vp, vp, vp, vp, vp, vp], ci),
         "sm_cost_volume": ([vp, vp, vp, ci, ci, ci, ci, ci, vp, vp], ci),
         "sm_build_tree": ([vp, vp, ci, ci, ci, vp, vp, vp, vp], ci),
+        "sm_build_tree_p": ([vp, vp, ci, ci, ci, ctypes.POINTER(SmParams), vp, vp, vp, vp, vp], ci),
         "sm_aggregate_debug": ([vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp], ci),
+        "sm_aggregate_debug_p": ([vp, vp, vp, ci, ci, ci, ctypes.POINTER(SmParams), ci, ci, ci, vp, vp], ci),
         "sm_stage_times": ([vp, vp, ci], ci),
         "sm_get_filter_stats": ([vp, ctypes.POINTER(SmFilterStats)], ci),
         "sm_get_kernel_stats": ([vp, ctypes.POINTER(SmKernelStat), ci], ci),
@@ -231,23 +233,34 @@ class Context:
         self._check(lib().sm_cost_volume(self.h, ptr(left), ptr(right), W, H, W * 3, d0, D, ptr(lv), ptr(rv)))
         return lv, rv
 
-    def build_tree(self, img):
+    def build_tree(self, img, params=None):
+        """The tree of one view: the MST, or with params.c finite the segment forest (roots: parent -1)."""
         img = as_image(img)
         H, W, _ = img.shape
         mask = np.empty(H * W, np.uint8)
         parent = np.empty(H * W, np.int32)
         size = np.empty(H * W, np.int32)
         slot = np.empty(H * W, np.int32)
-        self._check(lib().sm_build_tree(self.h, ptr(img), W, H, W * 3, ptr(mask), ptr(parent), ptr(size), ptr(slot)))
-        return dict(mask=mask, parent_pix=parent, subtree_size=size, slot_of_pix=slot)
+        nt = ctypes.c_int32(0)
+        if params is None:
+            self._check(lib().sm_build_tree(self.h, ptr(img), W, H, W * 3, ptr(mask), ptr(parent), ptr(size), ptr(slot)))
+            nt.value = 1
+        else:
+            self._check(lib().sm_build_tree_p(self.h, ptr(img), W, H, W * 3, ctypes.byref(params), ptr(mask), ptr(parent),
+                                              ptr(size), ptr(slot), ctypes.byref(nt)))
+        return dict(mask=mask, parent_pix=parent, subtree_size=size, slot_of_pix=slot, ntrees=nt.value)
 
-    def aggregate_debug(self, left, right, view, d0, D):
+    def aggregate_debug(self, left, right, view, d0, D, params=None):
         left, right = as_image(left), as_image(right)
         H, W, _ = left.shape
         Aup = np.empty((D, H, W), np.float64)
         A = np.empty((D, H, W), np.float64)
-        self._check(lib().sm_aggregate_debug(self.h, ptr(left), ptr(right), W, H, W * 3, view, d0, D, ptr(Aup),
-                                             ptr(A)))
+        if params is None:
+            self._check(lib().sm_aggregate_debug(self.h, ptr(left), ptr(right), W, H, W * 3, view, d0, D, ptr(Aup),
+                                                 ptr(A)))
+        else:
+            self._check(lib().sm_aggregate_debug_p(self.h, ptr(left), ptr(right), W, H, W * 3, ctypes.byref(params), view,
+                                                   d0, D, ptr(Aup), ptr(A)))
         return Aup, A
 
     # -- multi-GPU ------------------------------------------------------------------------

@@ -20,6 +20,7 @@
 #include "sm_common.h"
 #include "sm_launch.h"
 #include "sm_layout_gpu.h"
+#include "sm_segment.h"
 #include "sm_tables.inc"
 
 hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N);
@@ -59,6 +60,12 @@ struct sm_ctx {
     DevBuf changed, mst_ok, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
     DevBuf post_mask, post_scratch;  // output step (sm_post.hip): marks, scan positions
+    // segment mode (finite c, sm_segment.cpp): layout weights with the virtual edges, and host copies
+    DevBuf fwR[2], fwD[2];
+    bool seg = false;  // the current tree is a segment forest (layout reads fwR / fwD)
+    int seg_trees[2] = {0, 0};
+    std::vector<uint16_t> h_w[2][2], h_fw[2][2];
+    std::vector<uint8_t> h_m[2][2];
     size_t rec_pad_n[2] = {0, 0};  // pixel count the record pads were zeroed for
     size_t rec_pad_z[2] = {0, 0};  // pad length (records) they were zeroed with
     // records of padding on each side of the image records: the walkers read the matched image
@@ -157,8 +164,7 @@ float agd_color_term(int l1) {
 
 sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
     if (!p) return fail(ctx, SM_ERR_ARG, "null params");
-    if (!(std::isinf(p->c) && p->c > 0))
-        return fail(ctx, SM_ERR_ARG, "segment mode (finite c) is not implemented yet: use c=+INFINITY (MST mode)");
+    if (std::isnan(p->c) || p->c < 0) return fail(ctx, SM_ERR_ARG, "c must be >= 0 (finite: segment mode) or +INFINITY (MST mode)");
     if (p->median_ksize != 3) return fail(ctx, SM_ERR_ARG, "only median_ksize=3 is supported");
     if (p->cost_kind != SM_COST_AGD && p->cost_kind != SM_COST_VOLUME) return fail(ctx, SM_ERR_ARG, "unknown cost_kind");
     if (p->gamma != 1.0f / 12.f)
@@ -216,6 +222,58 @@ sm_status stage_prep(sm_ctx* ctx) {
 
 static bool hooked_any(const int* hf, int nviews, int q) {
     return hf[q] != 0 || (nviews > 1 && hf[SM_MST_MAX_ROUNDS + q] != 0);
+}
+
+sm_status stage_mst(sm_ctx* ctx, int nviews);
+
+// Segment mode: the reference's order-dependent Felzenszwalb segmentation + min-size merge on the host
+// (sm_segment.cpp), from the GPU's edge weights; the forest, linked into one tree by S = 0 virtual
+// edges, goes back as the MST masks and the layout's weights.  Replaces stage_mst.
+sm_status stage_segment(sm_ctx* ctx, int nviews, float c, int min_size) {
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H;
+    for (int v = 0; v < nviews; ++v) {
+        CHECK(ensure(ctx, ctx->mR[v], N));
+        CHECK(ensure(ctx, ctx->mD[v], N));
+        CHECK(ensure(ctx, ctx->fwR[v], N * 2));
+        CHECK(ensure(ctx, ctx->fwD[v], N * 2));
+        for (int k = 0; k < 2; ++k) {
+            ctx->h_w[v][k].resize(N);
+            ctx->h_fw[v][k].resize(N);
+            ctx->h_m[v][k].resize(N);
+        }
+        HIPC(hipMemcpyAsync(ctx->h_w[v][0].data(), ctx->wR[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipMemcpyAsync(ctx->h_w[v][1].data(), ctx->wD[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
+    }
+    CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
+    HIPC(hipStreamSynchronize(ctx->st));
+    std::thread other;
+    auto run = [ctx, W, H, c, min_size](int v) {
+        ctx->seg_trees[v] = sm_segment_forest(ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), W, H, c, min_size,
+                                              ctx->h_m[v][0].data(), ctx->h_m[v][1].data(), ctx->h_fw[v][0].data(),
+                                              ctx->h_fw[v][1].data());
+    };
+    if (nviews > 1) other = std::thread(run, 1);
+    run(0);
+    if (other.joinable()) other.join();
+    for (int v = 0; v < nviews; ++v) {
+        HIPC(hipMemcpyAsync(ctx->mR[v].p, ctx->h_m[v][0].data(), N, hipMemcpyHostToDevice, ctx->st));
+        HIPC(hipMemcpyAsync(ctx->mD[v].p, ctx->h_m[v][1].data(), N, hipMemcpyHostToDevice, ctx->st));
+        HIPC(hipMemcpyAsync(ctx->fwR[v].p, ctx->h_fw[v][0].data(), N * 2, hipMemcpyHostToDevice, ctx->st));
+        HIPC(hipMemcpyAsync(ctx->fwD[v].p, ctx->h_fw[v][1].data(), N * 2, hipMemcpyHostToDevice, ctx->st));
+    }
+    HIPC(hipMemsetAsync(ctx->mst_ok.p, 1, sizeof(int), ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));  // the host buffers are reused by the next call
+    ctx->mst_pend.active = false;
+    ctx->seg = true;
+    return SM_OK;
+}
+
+// tree of the call: the MST (Boruvka) or, for finite c, the segment forest
+sm_status stage_tree(sm_ctx* ctx, int nviews, const sm_params* p) {
+    if (p && !std::isinf(p->c)) return stage_segment(ctx, nviews, p->c, p->min_size);
+    ctx->seg = false;
+    return stage_mst(ctx, nviews);
 }
 
 sm_status stage_mst(sm_ctx* ctx, int nviews) {
@@ -391,8 +449,8 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         LayoutView& L = LP.v[v];
         L.mR = P<uint8_t>(ctx->mR[v]);
         L.mD = P<uint8_t>(ctx->mD[v]);
-        L.wR = P<uint16_t>(ctx->wR[v]);
-        L.wD = P<uint16_t>(ctx->wD[v]);
+        L.wR = P<uint16_t>(ctx->seg ? ctx->fwR[v] : ctx->wR[v]);
+        L.wD = P<uint16_t>(ctx->seg ? ctx->fwD[v] : ctx->wD[v]);
         L.adj = P<uint8_t>(ctx->adj[v]);
         L.pdir = P<int8_t>(ctx->pdir[v]);
         L.heavy = P<int8_t>(ctx->heavy[v]);
@@ -961,7 +1019,7 @@ void sm_destroy(sm_ctx* ctx) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
                          &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v], &ctx->Cst[v],
                          &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v], &ctx->vin[v],
-                         &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v]};
+                         &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v], &ctx->fwR[v], &ctx->fwD[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -1024,7 +1082,7 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
     HIPC(hipEventRecord(ctx->ev[1], ctx->st));
-    CHECK(stage_mst(ctx, 2));
+    CHECK(stage_tree(ctx, 2, p));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
     CHECK(stage_layout(ctx, 2));
     HIPC(hipEventRecord(ctx->ev[3], ctx->st));
@@ -1097,20 +1155,25 @@ sm_status sm_cost_volume(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W,
     return SM_OK;
 }
 
-sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int stride, uint8_t* mask, int32_t* parent_pix,
-                        int32_t* subtree_size, int32_t* slot_of_pix) {
+sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int stride, const sm_params* p, uint8_t* mask,
+                          int32_t* parent_pix, int32_t* subtree_size, int32_t* slot_of_pix, int32_t* ntrees) {
     if (!ctx) return SM_ERR_ARG;
+    if (p && (std::isnan(p->c) || p->c < 0)) return fail(ctx, SM_ERR_ARG, "c must be >= 0 or +INFINITY");
     HIPC(hipSetDevice(ctx->device));
     CHECK(upload(ctx, bgr, bgr, W, H, stride));
     CHECK(stage_prep(ctx));
-    CHECK(stage_mst(ctx, 1));
+    CHECK(stage_tree(ctx, 1, p));
     CHECK(stage_layout(ctx, 1));
     const size_t N = (size_t)W * H;
+    // segment mode: the virtual edges that link the trees are not part of the reported forest
+    const bool seg = ctx->seg;
+    auto virt = [&](size_t i, int k) { return seg && ctx->h_fw[0][k][i] == SM_VIRTUAL_W; };
     if (mask) {
         std::vector<uint8_t> mR(N), mD(N);
         HIPC(hipMemcpy(mR.data(), ctx->mR[0].p, N, hipMemcpyDeviceToHost));
         HIPC(hipMemcpy(mD.data(), ctx->mD[0].p, N, hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < N; ++i) mask[i] = (uint8_t)((mR[i] ? 1 : 0) | (mD[i] ? 2 : 0));
+        for (size_t i = 0; i < N; ++i)
+            mask[i] = (uint8_t)((mR[i] && !virt(i, 0) ? 1 : 0) | (mD[i] && !virt(i, 1) ? 2 : 0));
     }
     std::vector<int8_t> pdir(N);
     std::vector<uint32_t> size(N), pre(N);
@@ -1120,17 +1183,32 @@ sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int strid
     for (size_t i = 0; i < N; ++i) {
         if (parent_pix) {
             const int k = pdir[i];
-            parent_pix[i] = k < 0 ? -1 : (int32_t)(k == 0 ? i + 1 : k == 1 ? i + W : k == 2 ? i - 1 : i - W);
+            const size_t q = k == 0 ? i + 1 : k == 1 ? i + W : k == 2 ? i - 1 : i - W;
+            // the edge to the parent is stored at its left / upper pixel
+            const bool v = k >= 0 && (k == 0 ? virt(i, 0) : k == 1 ? virt(i, 1) : k == 2 ? virt(q, 0) : virt(q, 1));
+            parent_pix[i] = (k < 0 || v) ? -1 : (int32_t)q;
         }
         if (subtree_size) subtree_size[i] = (int32_t)size[i];
         if (slot_of_pix) slot_of_pix[i] = (int32_t)pre[i];
     }
+    if (ntrees) *ntrees = seg ? ctx->seg_trees[0] : 1;
     return SM_OK;
+}
+
+sm_status sm_build_tree(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int stride, uint8_t* mask, int32_t* parent_pix,
+                        int32_t* subtree_size, int32_t* slot_of_pix) {
+    return sm_build_tree_p(ctx, bgr, W, H, stride, nullptr, mask, parent_pix, subtree_size, slot_of_pix, nullptr);
 }
 
 sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, int view, int d0,
                              int D, double* A_up, double* A) {
+    return sm_aggregate_debug_p(ctx, l, r, W, H, stride, nullptr, view, d0, D, A_up, A);
+}
+
+sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, const sm_params* p,
+                               int view, int d0, int D, double* A_up, double* A) {
     if (!ctx) return SM_ERR_ARG;
+    if (p && (std::isnan(p->c) || p->c < 0)) return fail(ctx, SM_ERR_ARG, "c must be >= 0 or +INFINITY");
     if (view != 0 && view != 1) return fail(ctx, SM_ERR_ARG, "view must be 0 or 1");
     ctx->use_vol = false;  // AGD costs
     if (D < 1 || D > 256 || d0 < 0 || d0 > (1 << 20)) return fail(ctx, SM_ERR_ARG, "bad disparity range");
@@ -1138,7 +1216,7 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
     ctx->rec_pad = rec_pad_for(d0, D);
     CHECK(upload(ctx, l, r, W, H, stride));
     CHECK(stage_prep(ctx));
-    CHECK(stage_mst(ctx, 2));
+    CHECK(stage_tree(ctx, 2, p));
     CHECK(stage_layout(ctx, 2));
     const size_t N = (size_t)W * H;
     const int Dpad = 64 * spl_for(D);

@@ -1197,7 +1197,7 @@ template <int SPL>
 struct DownRing {
     DownSlot<SPL> s[DownCfg<SPL>::NS];
     double slut[SM_NUM_W + 1];
-    double s2lut[SM_NUM_W];
+    double s2lut[SM_NUM_W + 1];  // [SM_NUM_W]: S = 0, S2 = 1 (absent children; segment mode's virtual edges)
 };
 
 template <int SPL, int NN>
@@ -1675,7 +1675,10 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
         ring.slut[k] = slut_g[k];
         ring.s2lut[k] = s2lut_g[k];
     }
-    if (threadIdx.x == 0) ring.slut[SM_NUM_W] = 0.0;
+    if (threadIdx.x == 0) {
+        ring.slut[SM_NUM_W] = 0.0;
+        ring.s2lut[SM_NUM_W] = 1.0;
+    }
     __syncthreads();
     if (M > 1) {
         uint32_t* aggw = Q.stat + 3 * Q.stride;

@@ -111,7 +111,7 @@ __device__ __forceinline__ uint32_t hi_light(uint32_t hi) { return (hi >> 25) & 
 struct WalkShared {
     float atab[SM_MAX_W + 1];
     double slut[SM_NUM_W + 1];  // [SM_NUM_W] = 0.0
-    double s2lut[SM_NUM_W];
+    double s2lut[SM_NUM_W + 1];  // [SM_NUM_W] = 1.0 (segment mode's virtual edges: S = 0, S2 = 1)
 };
 
 __device__ __forceinline__ void load_tables(WalkShared& sh, const float* atab_g, const double* slut_g, const double* s2lut_g) {
@@ -120,7 +120,10 @@ __device__ __forceinline__ void load_tables(WalkShared& sh, const float* atab_g,
         sh.slut[i] = slut_g[i];
         sh.s2lut[i] = s2lut_g[i];
     }
-    if (threadIdx.x == 0) sh.slut[SM_NUM_W] = 0.0;
+    if (threadIdx.x == 0) {
+        sh.slut[SM_NUM_W] = 0.0;
+        sh.s2lut[SM_NUM_W] = 1.0;
+    }
     __syncthreads();
 }
 

@@ -352,6 +352,10 @@ def test_errors_are_loud(gpu_ctx):
     left, right, _ = make_pair(32, 16, 8)
     with pytest.raises(sm.StereoMSTError):
         gpu_ctx.match(left, right, 0)
+    with pytest.raises(sm.StereoMSTError):  # negative / NaN segment threshold
+        gpu_ctx.match(left, right, 8, sm.default_params(c=-1.0))
+    with pytest.raises(sm.StereoMSTError):
+        gpu_ctx.match(left, right, 8, sm.default_params(c=float("nan")))
     with pytest.raises(sm.StereoMSTError):  # shard beyond the declared total range
         gpu_ctx.match(left, right, 8, sm.default_params(disp_begin=4, disp_total=8))
     with pytest.raises(sm.StereoMSTError):  # fill without the check
@@ -593,3 +597,90 @@ def test_stereo3dmst_mccnn_ingest(gpu_ctx, tmp_path, monkeypatch):
     lref, rref = O.stereo3dmst_output(ref["left"].reshape(H, W), ref["right"].reshape(H, W), D)
     np.testing.assert_array_equal(rd, rref)
     np.testing.assert_array_equal(ld, lref)
+
+
+# ---- segment mode: the Felzenszwalb forest (c, min_size) filtered per tree (SURVEY.md 8f rank 1;
+# segment-graph.h:54-89, Stereo3DMST.cpp:242-384, 120-158 per tree) ----
+SEG = [(5000.0, 200), (300.0, 20), (0.0, 2)]
+
+
+def _forest_parent(W, H, t):
+    """parent pixel per pixel from the oracle's per-tree BFS (roots: -1)."""
+    par = np.full(W * H, -1, np.int32)
+    pix, parent = t["node_pix"], t["node_parent"]
+    roots = set(int(x) for x in t["tree_start"][:-1])
+    for n in range(W * H):
+        if n not in roots:
+            par[pix[n]] = pix[parent[n]]
+    return par
+
+
+@pytest.mark.parametrize("name", ["rand_37x23", "smooth_97x61", "flir_crop_256x192", "const_16x12", "col_1x15"])
+@pytest.mark.parametrize("c,min_size", SEG)
+def test_segment_forest_tree(gpu_ctx, name, c, min_size):
+    """The GPU path's forest (host segmentation, virtual links removed) and per-tree rooting against
+    the oracle's segmentation and BFS (each tree rooted at its first raster pixel)."""
+    import stereomatch_amd as sm
+    z = load_case(name)
+    H, W, _ = z["left"].shape
+    for v in ("left", "right"):
+        t = gpu_ctx.build_tree(z[v], sm.default_params(c=c, min_size=min_size))
+        ot = O.build_tree(z[v], c, min_size)
+        np.testing.assert_array_equal(t["mask"], ot["mask"])
+        assert t["ntrees"] == ot["ntrees"]
+        np.testing.assert_array_equal(t["parent_pix"], _forest_parent(W, H, ot))
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("c,min_size", SEG)
+def test_segment_match_bitexact_golden(gpu_ctx, name, c, min_size):
+    import stereomatch_amd as sm
+    z = load_case(name)
+    D = int(z["D"])
+    out = gpu_ctx.match(z["left"], z["right"], D, sm.default_params(c=c, min_size=min_size))
+    ref = O.match(z["left"], z["right"], D, c=c, min_size=min_size, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+@pytest.mark.parametrize("c,min_size", SEG)
+def test_segment_aggregate_bitexact(gpu_ctx, c, min_size):
+    """Every fp64 A_up / A value of the forest filter (4 slices), bitwise: virtual links carry S = 0,
+    S2 = 1, so each tree's root gets A = A_up as in the reference."""
+    import stereomatch_amd as sm
+    W, H, d0, D = 320, 240, 30, 4
+    left, right, _ = make_pair(W, H, 64, index=5)
+    lv, rv = O.cost_agd(left, right, d0, d0 + D)
+    for vi, (img, vol) in enumerate(((left, lv), (right, rv))):
+        Aup, A = gpu_ctx.aggregate_debug(left, right, vi, d0, D, sm.default_params(c=c, min_size=min_size))
+        r = O.tree_filter(W, H, O.build_tree(img, c, min_size), vol, d0, False, True, 16)
+        assert np.array_equal(bits(Aup), bits(r["Aup"]))
+        assert np.array_equal(bits(A), bits(r["A"]))
+
+
+@pytest.mark.parametrize("W,H,D,c", [(320, 240, 64, 5000.0), (200, 150, 128, 5000.0), (160, 90, 256, 5000.0),
+                                     (256, 160, 128, 800.0)])
+def test_segment_match_bitexact_synthetic(gpu_ctx, monkeypatch, W, H, D, c):
+    """Segment mode at SPL 1 / 2 / 4 with short pieces (cut paths inside the trees)."""
+    import stereomatch_amd as sm
+    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    left, right, _ = make_pair(W, H, D, index=7)
+    out = gpu_ctx.match(left, right, D, sm.default_params(c=c, min_size=200))
+    ref = O.match(left, right, D, c=c, min_size=200, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+def test_full_size_c2_segment_match_bitexact(gpu_ctx):
+    """1920x1200 D=128 in Stereo3DMST's own segment mode (c = 5000, min_size = 200; :831-832)."""
+    import stereomatch_amd as sm
+    W, H, D = 1920, 1200, 128
+    left, right, _ = make_pair(W, H, D, index=0)
+    out = gpu_ctx.match(left, right, D, sm.default_params(c=5000.0, min_size=200))
+    ref = O.match(left, right, D, c=5000.0, min_size=200, nthreads=16)
+    for v in ("left", "right"):
+        assert ref[v]["tree"]["ntrees"] > 1
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
