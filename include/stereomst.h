@@ -82,7 +82,13 @@ typedef enum {
     SM_POST_OCCLUSION = 8,      /* handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288),
                                    both maps: occluded pixels take the min of the nearest valid
                                    neighbours in the row (255 if none) */
-    SM_POST_OCCLUSION_ZERO = 16 /* the same check with remove_occlusion=true: occluded pixels = 0 */
+    SM_POST_OCCLUSION_ZERO = 16, /* the same check with remove_occlusion=true: occluded pixels = 0 */
+    SM_POST_SUBPIXEL = 32       /* the float disparity of the WTA gets selectDisparity's parabola through
+                                   the neighbouring slices' aggregated costs (as float), d - s when
+                                   |s| < 1 (PatchMatchStereoGPU.cu:1726-1736); a shard computes a
+                                   1-slice halo on each inner side and the cross-rank exchange carries
+                                   the winner's disparity (idx / min unchanged).  Applied in the WTA,
+                                   i.e. before the steps above */
 } sm_post;
 
 typedef struct sm_ctx sm_ctx;

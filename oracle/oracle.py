@@ -228,6 +228,25 @@ def stereo3dmst_output(left_idx, right_idx, dmax, fill=False):
     return lr_check(ld, rd, dmax, fill), rd
 
 
+def subpixel(A, idx, dglob0, dtot):
+    """selectDisparity's parabola (PatchMatchStereoGPU.cu:1726-1736) on the WTA winners, float32:
+    A = [nd][H][W] fp64 aggregated costs of global slices dglob0.., idx = global winners; the
+    neighbours' costs as float (0 at the ends of [0, dtot)); disp = d - s if |s| < 1 else d."""
+    nd = A.shape[0]
+    flat = A.reshape(nd, -1)
+    i = np.asarray(idx).ravel().astype(np.int64)
+    m = i - dglob0
+    p = np.arange(flat.shape[1])
+    f32 = np.float32
+    cur = flat[m, p].astype(f32)
+    pre = np.where(i > 0, flat[np.clip(m - 1, 0, nd - 1), p].astype(f32), f32(0))
+    nxt = np.where(i < dtot - 1, flat[np.clip(m + 1, 0, nd - 1), p].astype(f32), f32(0))
+    with np.errstate(all="ignore"):
+        s = ((nxt - pre) * f32(0.5) / ((nxt - f32(2.0) * cur) + pre)).astype(f32)
+    g = i.astype(f32)
+    return np.where(np.abs(s) < f32(1.0), g - s, g).astype(f32)
+
+
 def occlusion(left_disp, right_disp, min_disp=0, thresh=1.0, remove=False):
     """handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288); returns new (left, right)."""
     L = np.ascontiguousarray(left_disp, dtype=np.float32).copy()

@@ -17,6 +17,7 @@ STATUS_NAMES = {0: "SM_OK", 1: "SM_ERR_ARG", 2: "SM_ERR_HIP", 3: "SM_ERR_OOM", 4
                 5: "SM_ERR_STATE", 6: "SM_ERR_NODEVICE"}
 SM_COST_AGD, SM_COST_VOLUME = 0, 1
 SM_POST_LR_CHECK, SM_POST_LABEL_TO_DISP, SM_POST_LR_FILL, SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO = 1, 2, 4, 8, 16
+SM_POST_SUBPIXEL = 32
 SM_UNIQUE_ID_BYTES = 128
 
 

@@ -26,6 +26,10 @@
 hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N);
 hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gidx, double* minc, int32_t* idx, float* disp,
                            size_t N);
+hipError_t launch_cand64(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, const float* disp,
+                         unsigned long long* cand, size_t N);
+hipError_t launch_finalize64(hipStream_t st, const double* gmin, const unsigned long long* gkey, double* minc, int32_t* idx,
+                             float* disp, size_t N);
 
 namespace {
 
@@ -63,6 +67,7 @@ struct sm_ctx {
     // segment mode (finite c, sm_segment.cpp): layout weights with the virtual edges, and host copies
     DevBuf fwR[2], fwD[2];
     bool seg = false;  // the current tree is a segment forest (layout reads fwR / fwD)
+    bool sub = false;  // the current call's WTA carries subpixel disparities (SM_POST_SUBPIXEL)
     int seg_trees[2] = {0, 0};
     std::vector<uint16_t> h_w[2][2], h_fw[2][2];
     std::vector<uint8_t> h_m[2][2];
@@ -174,13 +179,38 @@ sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
     if (p->disp_begin > (1 << 20)) return fail(ctx, SM_ERR_ARG, "disp_begin > 2^20");
     if (p->disp_total != 0 && p->disp_total < p->disp_begin + D)
         return fail(ctx, SM_ERR_ARG, "disp_total < disp_begin + D (shard beyond the total range)");
-    const int known = SM_POST_LR_CHECK | SM_POST_LABEL_TO_DISP | SM_POST_LR_FILL | SM_POST_OCCLUSION | SM_POST_OCCLUSION_ZERO;
+    const int known = SM_POST_LR_CHECK | SM_POST_LABEL_TO_DISP | SM_POST_LR_FILL | SM_POST_OCCLUSION | SM_POST_OCCLUSION_ZERO |
+                      SM_POST_SUBPIXEL;
     if (p->post & ~known) return fail(ctx, SM_ERR_ARG, "unknown post-processing bits");
     if ((p->post & SM_POST_LR_FILL) && !(p->post & SM_POST_LR_CHECK))
         return fail(ctx, SM_ERR_ARG, "SM_POST_LR_FILL needs SM_POST_LR_CHECK");
     if ((p->post & SM_POST_OCCLUSION) && (p->post & SM_POST_OCCLUSION_ZERO))
         return fail(ctx, SM_ERR_ARG, "SM_POST_OCCLUSION and SM_POST_OCCLUSION_ZERO are exclusive");
+    if (p->post & SM_POST_SUBPIXEL) {
+        const int dtot = p->disp_total > 0 ? p->disp_total : p->disp_begin + D;
+        const int halo = (p->disp_begin > 0) + (p->disp_begin + D < dtot);
+        if (D + halo > 256)
+            return fail(ctx, SM_ERR_ARG, "SM_POST_SUBPIXEL on a shard needs D + its 1-slice halos <= 256");
+    }
     return SM_OK;
+}
+
+// the slices a call computes: [disp_begin, disp_begin + D), plus for SM_POST_SUBPIXEL on a shard a
+// one-slice halo on each inner side, so the parabola of the shard's winner has both neighbours
+// locally; the WTA itself covers the shard only
+struct CallRange {
+    int d0, D;  // computed slices (global first, count)
+    WtaCfg w;
+};
+CallRange call_range(const sm_params* p, int D) {
+    const int dtot = p->disp_total > 0 ? p->disp_total : p->disp_begin + D;
+    const int sub = (p->post & SM_POST_SUBPIXEL) ? 1 : 0;
+    const int h0 = sub && p->disp_begin > 0 ? 1 : 0, h1 = sub && p->disp_begin + D < dtot ? 1 : 0;
+    CallRange r;
+    r.d0 = p->disp_begin - h0;
+    r.D = D + h0 + h1;
+    r.w = WtaCfg{h0, h0 + D, r.d0, dtot, sub};
+    return r;
 }
 
 // image-record pad for a call over slices [disp_begin, disp_begin + Dpad): load_recs reads records
@@ -547,6 +577,7 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     a.Dpad = Dpad;
     a.dcall = D;
     a.dglob0 = dglob0;
+    a.wta = WtaCfg{0, D, dglob0, dglob0 + D, 0};  // stage_filter sets the call's own
     return a;
 }
 
@@ -760,7 +791,7 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
 }
 
 // up + down passes over all rounds for nviews views; debug_store_all stores every A row
-sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_store_all) {
+sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_store_all, const WtaCfg* wta = nullptr) {
     const size_t N = (size_t)ctx->W * ctx->H;
     const int spl = spl_for(D);
     const int Dpad = 64 * spl;
@@ -768,6 +799,7 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     uint32_t nr = 0;
     for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
+    if (wta) a.wta = *wta;
     CHECK(setup_sync(ctx, a, N, Dpad));
     a.vol = ctx->use_vol ? 1 : 0;
     if (a.vol)  // cost rows of every slot from the caller's volumes (slots come from the layout)
@@ -868,9 +900,28 @@ sm_status stage_reduce(sm_ctx* ctx) {
     for (int v = 0; v < 2; ++v)
         RCCLC(ncclAllReduce(ctx->minc[v].p, ctx->gmin[v].p, N, ncclFloat64, ncclMin, ctx->comm, ctx->st));
     RCCLC(ncclGroupEnd());
-    for (int v = 0; v < 2; ++v)
-        HIPC(launch_cand(ctx->st, P<double>(ctx->minc[v]), P<double>(ctx->gmin[v]), P<int32_t>(ctx->idx[v]),
-                         P<int32_t>(ctx->cand[v]), N));
+    if (!ctx->sub)
+        for (int v = 0; v < 2; ++v)
+            HIPC(launch_cand(ctx->st, P<double>(ctx->minc[v]), P<double>(ctx->gmin[v]), P<int32_t>(ctx->idx[v]),
+                             P<int32_t>(ctx->cand[v]), N));
+    if (ctx->sub) {
+        // subpixel: the candidate is (global index << 32 | float bits of the rank's subpixel disparity),
+        // so the MIN over ranks carries the winning rank's disparity with the lowest index
+        for (int v = 0; v < 2; ++v) {
+            CHECK(ensure(ctx, ctx->cand[v], N * 8));
+            CHECK(ensure(ctx, ctx->gidx[v], N * 8));
+            HIPC(launch_cand64(ctx->st, P<double>(ctx->minc[v]), P<double>(ctx->gmin[v]), P<int32_t>(ctx->idx[v]),
+                               P<float>(ctx->disp[v]), P<unsigned long long>(ctx->cand[v]), N));
+        }
+        RCCLC(ncclGroupStart());
+        for (int v = 0; v < 2; ++v)
+            RCCLC(ncclAllReduce(ctx->cand[v].p, ctx->gidx[v].p, N, ncclUint64, ncclMin, ctx->comm, ctx->st));
+        RCCLC(ncclGroupEnd());
+        for (int v = 0; v < 2; ++v)
+            HIPC(launch_finalize64(ctx->st, P<double>(ctx->gmin[v]), P<unsigned long long>(ctx->gidx[v]), P<double>(ctx->minc[v]),
+                                   P<int32_t>(ctx->idx[v]), P<float>(ctx->disp[v]), N));
+        return SM_OK;
+    }
     RCCLC(ncclGroupStart());
     for (int v = 0; v < 2; ++v)
         RCCLC(ncclAllReduce(ctx->cand[v].p, ctx->gidx[v].p, N, ncclInt32, ncclMin, ctx->comm, ctx->st));
@@ -1071,14 +1122,16 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     if (!ctx) return SM_ERR_ARG;
     if (ctx->W == 0) return fail(ctx, SM_ERR_STATE, "no images uploaded");
     CHECK(check_params(ctx, p, D));
+    const CallRange cr = call_range(p, D);
     ctx->use_vol = p->cost_kind == SM_COST_VOLUME;
     if (ctx->use_vol) {
         if (ctx->vin_D == 0) return fail(ctx, SM_ERR_STATE, "SM_COST_VOLUME: no volumes uploaded (sm_upload_cost_volumes)");
         if (ctx->vin_W != ctx->W || ctx->vin_H != ctx->H) return fail(ctx, SM_ERR_ARG, "cost volumes and images differ in size");
-        if (p->disp_begin + D > ctx->vin_D) return fail(ctx, SM_ERR_ARG, "slices beyond the uploaded cost volumes");
+        if (cr.d0 + cr.D > ctx->vin_D) return fail(ctx, SM_ERR_ARG, "slices beyond the uploaded cost volumes");
     }
     HIPC(hipSetDevice(ctx->device));
-    ctx->rec_pad = rec_pad_for(p->disp_begin, D);
+    ctx->rec_pad = rec_pad_for(cr.d0, cr.D);
+    ctx->sub = cr.w.sub != 0;
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
     HIPC(hipEventRecord(ctx->ev[1], ctx->st));
@@ -1086,7 +1139,7 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
     CHECK(stage_layout(ctx, 2));
     HIPC(hipEventRecord(ctx->ev[3], ctx->st));
-    CHECK(stage_filter(ctx, D, p->disp_begin, 2, false));
+    CHECK(stage_filter(ctx, cr.D, cr.d0, 2, false, &cr.w));
     HIPC(hipEventRecord(ctx->ev[4], ctx->st));
     CHECK(stage_reduce(ctx));
     CHECK(stage_post(ctx, p->post, p->disp_total > 0 ? p->disp_total : p->disp_begin + D));

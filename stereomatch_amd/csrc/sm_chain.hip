@@ -1270,7 +1270,7 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
 template <int SPL>
 __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, int head, int len, int lane,
                                                  const uint32_t* __restrict__ meta32, const WalkView& V, int Dpad,
-                                                 int dcall, int dglob0, int store_all, uint32_t epoch,
+                                                 const WtaCfg& w, int store_all, uint32_t epoch,
                                                  uint32_t* done_word) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
     const int ngroups = (len + G - 1) / G;
@@ -1344,15 +1344,16 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
         for (int k = 0; k < G; ++k) st[k] = sl.st[k];
         lds_publish(&sl.freed, g + 1);
         double mn;
-        int mi;
-        wta_chunk<SPL, G>(xs, lane, lane * SPL, dcall, mn, mi);
+        int gi;
+        float dsp;
+        wta_nodes<SPL, G>(xs, lane, w, mn, gi, dsp);
 #pragma unroll
         for (int k = 0; k < G; ++k)
             if (k < n && (store_all || st[k])) store_row<SPL>(V.A, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
         if (lane < n) {
-            V.idx[pix] = dglob0 + mi;
+            V.idx[pix] = gi;
             V.minc[pix] = mn;
-            V.disp[pix] = (float)(dglob0 + mi);
+            V.disp[pix] = dsp;
         }
         if (done_word && g == ngroups - 1) {
             // the piece's last row is the next piece's input: device scope, then the done word
@@ -1500,7 +1501,7 @@ __device__ void down_guess(double* scratch, double* guess, const double* __restr
 template <int SPL, int CHR>
 __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta32, const double* __restrict__ U,
                                                const WalkView& V, const double* slut, const double* s2lut, int head,
-                                               int len, int nmax, int Dpad, int lane, double* xio, int dcall, int dglob0,
+                                               int len, int nmax, int Dpad, int lane, double* xio, const WtaCfg& w,
                                                int store_all, bool last_pub, bool check) {
     double x[SPL];
 #pragma unroll
@@ -1540,13 +1541,14 @@ __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta
             }
         }
         double mnv;
-        int mi;
-        wta_chunk<SPL, CHR>(ys, lane, lane * SPL, dcall, mnv, mi);
+        int gi;
+        float dsp;
+        wta_nodes<SPL, CHR>(ys, lane, w, mnv, gi, dsp);
         const uint32_t pix = meta_pix_of_lane<CHR>(mv, lane);
         if (lane < mk) {
-            V.idx[pix] = dglob0 + mi;
+            V.idx[pix] = gi;
             V.minc[pix] = mnv;
-            V.disp[pix] = (float)(dglob0 + mi);
+            V.disp[pix] = dsp;
         }
 #pragma unroll
         for (int k = 0; k < CHR; ++k) {
@@ -1572,7 +1574,7 @@ __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta
 // entries e - i .. e - 1, the top one exact by construction).
 template <int SPL>
 __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __restrict__ meta32, const WalkView& V,
-                            int Dpad, int dcall, int dglob0, int store_all, int lane, int head, int len, int i, int M,
+                            int Dpad, const WtaCfg& w, int store_all, int lane, int head, int len, int i, int M,
                             int e, const PieceView& Q, uint32_t epoch) {
     uint32_t* done = Q.stat;
     uint32_t* merged = Q.stat + Q.stride;
@@ -1590,7 +1592,7 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
     agent_row_read<SPL>(V.A, above, Dpad, lane, x);
     vm_drain();
     const int m = down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, min(Q.rmax, len), Dpad,
-                                                        lane, x, dcall, dglob0, store_all, last_pub, true);
+                                                        lane, x, w, store_all, last_pub, true);
     vm_drain();
     if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
     bool all = m >= 0;
@@ -1610,7 +1612,7 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
     vm_drain();
     agent_row_read<SPL>(V.A, above, Dpad, lane, x);
     vm_drain();
-    down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, len, Dpad, lane, x, dcall, dglob0,
+    down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, len, Dpad, lane, x, w,
                                           store_all, last_pub, false);
     vm_drain();
     if (lane == 0) publish_word(fin + e, epoch);
@@ -1623,8 +1625,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
                                                             const SmPath* __restrict__ paths0,
                                                             const SmPath* __restrict__ paths1,
                                                             const double* __restrict__ slut_g,
-                                                            const double* __restrict__ s2lut_g, int Dpad, int dcall,
-                                                            int dglob0, int store_all, uint32_t epoch, PieceView Q0,
+                                                            const double* __restrict__ s2lut_g, int Dpad, WtaCfg w,
+                                                            int store_all, uint32_t epoch, PieceView Q0,
                                                             PieceView Q1) {
     __shared__ DownRing<SPL> ring;
     __shared__ double guess[64 * SPL];
@@ -1714,9 +1716,9 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     if (wave < Split<SPL>::NCW) {
         down_chain_wave<SPL>(ring, wave, len, lane, i > 0 ? guess : nullptr);
         if (wave == 0 && M > 1)
-            down_finish<SPL>(ring, &hdone, meta32, V, Dpad, dcall, dglob0, store_all, lane, head, len, i, M, pidx, Q, epoch);
+            down_finish<SPL>(ring, &hdone, meta32, V, Dpad, w, store_all, lane, head, len, i, M, pidx, Q, epoch);
     } else if (Split<SPL>::helper_of(wave) >= 0) {
-        down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V, Dpad, dcall, dglob0, store_all,
+        down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V, Dpad, w, store_all,
                               epoch, (M > 1 && i + 1 < M) ? Q.stat + pidx : nullptr);
         vm_drain();  // this helper's stores are complete before the repair overwrites them
         if (lane == 0) atomicAdd(&hdone, 1);
@@ -1771,7 +1773,7 @@ static void down_chain_launch(hipStream_t st, const WalkArgs& a, int np, int sto
         if (q->stat) q->stat += 3 * (size_t)q->stride;
     hipLaunchKernelGGL((k_down_chain<SPL>), grid, dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all, a.epoch, q0, q1);
+                       a.paths[0], a.paths[1], a.slut, a.s2lut, a.Dpad, a.wta, store_all, a.epoch, q0, q1);
 }
 
 hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {

@@ -686,6 +686,25 @@ __global__ void k_finalize(const double* __restrict__ gmin, const int32_t* __res
     }
 }
 
+// subpixel variant: the candidate carries the rank's subpixel disparity in its low word
+__global__ void k_cand64(const double* __restrict__ minc, const double* __restrict__ gmin, const int32_t* __restrict__ idx,
+                         const float* __restrict__ disp, unsigned long long* __restrict__ cand, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N)
+        cand[i] = minc[i] == gmin[i] ? ((unsigned long long)(uint32_t)idx[i] << 32) | __float_as_uint(disp[i]) : ~0ull;
+}
+
+__global__ void k_finalize64(const double* __restrict__ gmin, const unsigned long long* __restrict__ gkey,
+                             double* __restrict__ minc, int32_t* __restrict__ idx, float* __restrict__ disp, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) {
+        const unsigned long long k = gkey[i];
+        minc[i] = gmin[i];
+        idx[i] = (int32_t)(k >> 32);
+        disp[i] = __uint_as_float((uint32_t)k);
+    }
+}
+
 // MC-CNN ingest (Stereo3DMST.cpp:764-803): slices [d0, d0 + D) of a caller-supplied raw volume
 // [Dv][H][W] -> f32 cost rows Cst[slot][Dpad] after the reference's clamp, NaN -> 0.5 else
 // min(0.5, x) (:785-803; std::min(0.5f, x) returns 0.5 unless x < 0.5).  Row padding (d >= D)
@@ -826,6 +845,18 @@ hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, c
 hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gidx, double* minc, int32_t* idx, float* disp,
                            size_t N) {
     hipLaunchKernelGGL(k_finalize, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, gmin, gidx, minc, idx, disp, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_cand64(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, const float* disp,
+                         unsigned long long* cand, size_t N) {
+    hipLaunchKernelGGL(k_cand64, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, minc, gmin, idx, disp, cand, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize64(hipStream_t st, const double* gmin, const unsigned long long* gkey, double* minc, int32_t* idx,
+                             float* disp, size_t N) {
+    hipLaunchKernelGGL(k_finalize64, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, gmin, gkey, minc, idx, disp, N);
     return hipGetLastError();
 }
 

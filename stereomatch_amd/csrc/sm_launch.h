@@ -6,6 +6,15 @@
 
 #include "sm_common.h"
 
+// WTA configuration of the down pass (sm_walk_util.h wta_nodes): the call computes local slices
+// [0, dcall) = global [dglob0, dglob0 + dcall); the WTA takes local [lo, hi); dtot = the total range
+#ifndef SM_WTACFG_DEFINED
+#define SM_WTACFG_DEFINED
+struct WtaCfg {
+    int lo, hi, dglob0, dtot, sub;
+};
+#endif
+
 // byte ranges zeroed by one launch (each base 16-byte aligned: hipMalloc'd buffers)
 #define SM_ZERO_MAX 12
 struct ZeroList {
@@ -62,6 +71,7 @@ struct WalkArgs {
     const uint2* segtab[2];  // long buckets: {path, segment} per SM_PRE_SEG-node segment
     int nseg[2];
     int W, Dpad, dcall, dglob0;
+    WtaCfg wta;          // down pass: the WTA's slice range, output offset, subpixel (sm_walk_util.h)
     uint32_t epoch;       // filter call counter (status words hold it)
     // long-path pieces of the current long bucket (sm_chain.hip "Pieces"); pieces[v] == nullptr:
     // one workgroup per path, no pieces

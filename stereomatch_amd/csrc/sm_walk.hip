@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
                                                    const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
                                                    const SmPath* __restrict__ paths1, const float* __restrict__ atab_g,
                                                    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
-                                                   int Dpad, int dcall, int dglob0, int store_all) {
+                                                   int Dpad, WtaCfg w, int store_all) {
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
@@ -245,7 +245,6 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
     const SmPath* __restrict__ pp = view ? paths1 : paths0;
     const int head = (int)uniform(pp[pi0].head);
     const int len = (int)uniform(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
-    const int dloc0 = lane * SPL;
     double xc[SPL];
 #pragma unroll
     for (int k = 0; k < SPL; ++k) xc[k] = 0.0;
@@ -318,13 +317,14 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
                 store_row<SPL>(V.A, (uint32_t)(c0 + j), Dpad, lane, xs[j]);
         }
         double mn;
-        int mi;
-        wta_chunk<SPL, CH>(xs, lane, dloc0, dcall, mn, mi);
+        int gi;
+        float dsp;
+        wta_nodes<SPL, CH>(xs, lane, w, mn, gi, dsp);
         const uint32_t pix = meta_pix_of_lane<CH>(cur, lane);  // all lanes active: bpermute sources
         if (lane < n) {  // lane j stores node j's result
-            V.idx[pix] = dglob0 + mi;
+            V.idx[pix] = gi;
             V.minc[pix] = mn;
-            V.disp[pix] = (float)(dglob0 + mi);
+            V.disp[pix] = dsp;
         }
         if (nn == 0) break;
         cur = nxt;
@@ -362,7 +362,7 @@ template <int SPL, int CH>
 static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all) {
     hipLaunchKernelGGL((k_down_walk<SPL, CH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.Dpad, a.dcall, a.dglob0, store_all);
+                       a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.Dpad, a.wta, store_all);
 }
 
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths) {

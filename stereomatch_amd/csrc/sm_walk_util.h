@@ -141,10 +141,11 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
-// CH strict-< first-minimum reductions at once (independent -> their latencies overlap).
+// CH strict-< first-minimum reductions at once (independent -> their latencies overlap), over the
+// slices [lo, hi) of this call (slices outside: padding, or a shard's subpixel halo).
 // Returns, in lane j < CH, node j's argmin (slice index of this call) and minimum.
 template <int SPL, int CH>
-__device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, int dloc0, int dcall, double& out_min,
+__device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, int dloc0, int lo, int hi, double& out_min,
                                           int& out_idx) {
     double bv[CH], g[CH];
     int bi[CH];
@@ -154,7 +155,8 @@ __device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, 
         bi[j] = 0x7fffffff;
 #pragma unroll
         for (int k = 0; k < SPL; ++k) {
-            if (dloc0 + k < dcall && x[j][k] < bv[j]) { bv[j] = x[j][k]; bi[j] = dloc0 + k; }
+            const int d = dloc0 + k;
+            if (d >= lo && d < hi && x[j][k] < bv[j]) { bv[j] = x[j][k]; bi[j] = d; }
         }
         g[j] = bv[j];
     }
@@ -176,6 +178,57 @@ __device__ __forceinline__ void wta_chunk(const double (&x)[CH][SPL], int lane, 
         const int win = ball ? (int)__builtin_ctzll(ball) : 0;
         const int gi = ball ? __builtin_amdgcn_readlane(bi[j], win) : 0;
         if (lane == j) { out_min = m; out_idx = gi; }
+    }
+}
+
+// WTA configuration of a down-pass launch: the call computes slices [dglob0, dglob0 + dcall) (local
+// 0 ..), the WTA takes local slices [lo, hi); dtot = the total disparity range (subpixel edge rule)
+#ifndef SM_WTACFG_DEFINED
+#define SM_WTACFG_DEFINED
+struct WtaCfg {
+    int lo, hi, dglob0, dtot, sub;
+};
+#endif
+
+template <int SPL>
+__device__ __forceinline__ double sel_slice(const double (&r)[SPL], int k) {
+    double v = r[0];
+#pragma unroll
+    for (int q = 1; q < SPL; ++q) v = k == q ? r[q] : v;
+    return v;
+}
+
+// WTA of CH nodes: lane j < CH gets node j's global index, minimum and float disparity.  With w.sub
+// the disparity gets selectDisparity's parabola (PatchMatchStereoGPU.cu:1726-1736) through the
+// neighbouring slices' aggregated costs rounded to float (pre / next = 0 at the ends of the total
+// range): s = (next - pre) * 0.5f / (next - 2 cur + pre); disp = d - s if |s| < 1, else d.  The
+// neighbours sit in other lanes (lane t / SPL, element t % SPL): one readlane each.
+template <int SPL, int CH>
+__device__ __forceinline__ void wta_nodes(const double (&x)[CH][SPL], int lane, const WtaCfg& w, double& mn, int& gi,
+                                          float& disp) {
+    int mi;
+    wta_chunk<SPL, CH>(x, lane, lane * SPL, w.lo, w.hi, mn, mi);
+    gi = w.dglob0 + mi;
+    disp = (float)gi;
+    if (w.sub) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int m = __builtin_amdgcn_readlane(mi, j);
+            const int g = w.dglob0 + m;
+            const float cur = (float)readlane_f64(mn, j);
+            float pre = 0.0f, nxt = 0.0f;
+            if (g > 0) {
+                const int t = m - 1;
+                pre = (float)readlane_f64(sel_slice<SPL>(x[j], t % SPL), t / SPL);
+            }
+            if (g < w.dtot - 1) {
+                const int t = m + 1;
+                nxt = (float)readlane_f64(sel_slice<SPL>(x[j], t % SPL), t / SPL);
+            }
+            const float s = (nxt - pre) * 0.5f / (nxt - 2.0f * cur + pre);
+            const float dj = fabsf(s) < 1.0f ? (float)g - s : (float)g;
+            if (lane == j) disp = dj;
+        }
     }
 }
 

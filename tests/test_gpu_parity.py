@@ -684,3 +684,48 @@ def test_full_size_c2_segment_match_bitexact(gpu_ctx):
         assert ref[v]["tree"]["ntrees"] > 1
         np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+# ---- subpixel WTA (SM_POST_SUBPIXEL; PatchMatchStereoGPU.cu:1726-1736) ----
+@pytest.mark.parametrize("W,H,D", [(160, 120, 48), (200, 96, 100), (256, 128, 128), (128, 64, 200)])
+def test_subpixel_bitexact(gpu_ctx, monkeypatch, W, H, D):
+    """Subpixel disparities of both views (SPL 1 / 2 / 4, cut paths through the chain engine and
+    its repair walks) against the oracle's parabola over its own aggregated volumes; idx / min are
+    the integral WTA's."""
+    import stereomatch_amd as sm
+    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    left, right, _ = make_pair(W, H, D, index=9)
+    out = gpu_ctx.match(left, right, D, sm.default_params(post=sm.SM_POST_SUBPIXEL))
+    ref = O.match(left, right, D, want_volumes=True, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+        exp = O.subpixel(ref[v]["A"], ref[v]["idx"], 0, D)
+        np.testing.assert_array_equal(out[v]["disp"].ravel(), exp)
+        assert np.count_nonzero(exp != ref[v]["idx"].astype(np.float32)) > 0
+
+
+@pytest.mark.parametrize("d0,D,Dt", [(0, 32, 96), (32, 32, 96), (64, 32, 96), (40, 30, 100)])
+def test_subpixel_shard_halo_with_reduce(d0, D, Dt):
+    """A subpixel shard through a one-rank communicator: the shard computes a 1-slice halo on each
+    inner side, the WTA covers [d0, d0+D) only, the parabola of its winner uses the halo slices, and
+    the 64-bit (index, disparity) exchange carries the disparity (stage_reduce)."""
+    import stereomatch_amd as sm
+    W, H = 180, 120
+    left, right, _ = make_pair(W, H, Dt, index=11)
+    ctx = sm.Context(0)
+    try:
+        ctx.comm_init(1, 0, sm.Context.unique_id())
+        out = ctx.match(left, right, D, sm.default_params(disp_begin=d0, disp_total=Dt, post=sm.SM_POST_SUBPIXEL))
+    finally:
+        ctx.close()
+    lo, hi = max(0, d0 - 1), min(Dt, d0 + D + 1)
+    lv, rv = O.cost_agd(left, right, lo, hi)
+    for v, img, vol in (("left", left, lv), ("right", right, rv)):
+        r = O.tree_filter(W, H, O.build_tree(img), vol, lo, False, True, 16)
+        A = r["A"]
+        sh = A[d0 - lo:d0 - lo + D].reshape(D, -1)
+        am = np.argmin(sh, axis=0)  # first minimum over the shard = strict-< over ascending d
+        idx = (d0 + am).astype(np.int32)
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), idx)
+        np.testing.assert_array_equal(out[v]["disp"].ravel(), O.subpixel(A, idx, lo, Dt))
