@@ -160,6 +160,12 @@ T* P(DevBuf& b) {
 }
 
 int spl_for(int D) { return D <= 64 ? 1 : D <= 128 ? 2 : 4; }
+// row length of a call of D slices: 64 * SPL, or 32 for D <= 32 (a 32-slice shard moves 32-slice
+// rows; SM_NO_DPAD32=1 restores 64 for A/B)
+int dpad_for(int D) {
+    static const bool off = getenv("SM_NO_DPAD32") != nullptr;
+    return (D <= 32 && !off) ? 32 : 64 * spl_for(D);
+}
 
 float agd_color_term(int l1) {
     // 0.11f*fminf(color_l1*0.33333333333, 7.0f) (PatchMatchStereoGPU.cu:1539)
@@ -794,7 +800,7 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
 sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_store_all, const WtaCfg* wta = nullptr) {
     const size_t N = (size_t)ctx->W * ctx->H;
     const int spl = spl_for(D);
-    const int Dpad = 64 * spl;
+    const int Dpad = dpad_for(D);
     CHECK(ensure_filter_bufs(ctx, Dpad));
     uint32_t nr = 0;
     for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
@@ -1272,7 +1278,7 @@ sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, 
     CHECK(stage_tree(ctx, 2, p));
     CHECK(stage_layout(ctx, 2));
     const size_t N = (size_t)W * H;
-    const int Dpad = 64 * spl_for(D);
+    const int Dpad = dpad_for(D);
     CHECK(ensure(ctx, ctx->vol[0], N * (size_t)D * 8));
     // up pass only, snapshot A_up
     {

@@ -125,7 +125,7 @@ template <int SPL>
 __device__ __forceinline__ void load_crow(const float* __restrict__ C, uint32_t slot, int Dpad, int lane, float (&c)[SPL]) {
     const float* p = C + (size_t)slot * Dpad + lane * SPL;
     if constexpr (SPL == 1) {
-        c[0] = p[0];
+        c[0] = lane < Dpad ? p[0] : 0.0f;
     } else if constexpr (SPL == 2) {
         const float2 t = *reinterpret_cast<const float2*>(p);
         c[0] = t.x;
@@ -142,7 +142,7 @@ template <int SPL>
 __device__ __forceinline__ void store_crow(float* __restrict__ C, uint32_t slot, int Dpad, int lane, const double (&c)[SPL]) {
     float* p = C + (size_t)slot * Dpad + lane * SPL;
     if constexpr (SPL == 1) {
-        p[0] = (float)c[0];
+        if (lane < Dpad) p[0] = (float)c[0];
     } else if constexpr (SPL == 2) {
         *reinterpret_cast<float2*>(p) = make_float2((float)c[0], (float)c[1]);
     } else {
@@ -310,11 +310,12 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
         }
     }
     double* out = agg + (size_t)blockIdx.x * 2 * Dpad;  // segment index within the bucket
+    if (row_lane<SPL>(lane, Dpad))
 #pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-        out[lane * SPL + k] = aggsh[0][0][lane * SPL + k];
-        out[Dpad + lane * SPL + k] = aggsh[0][1][lane * SPL + k];
-    }
+        for (int k = 0; k < SPL; ++k) {
+            out[lane * SPL + k] = aggsh[0][0][lane * SPL + k];
+            out[Dpad + lane * SPL + k] = aggsh[0][1][lane * SPL + k];
+        }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -354,8 +355,9 @@ __global__ __launch_bounds__(256) void k_long_costs(const uint32_t* __restrict__
     for (int j = 0; j < CH; ++j) {
         if (j < n) {
             float* p = Cst + (size_t)(first + j) * Dpad + lane * SPL;
+            if (row_lane<SPL>(lane, Dpad))
 #pragma unroll
-            for (int k = 0; k < SPL; ++k) p[k] = c[j][k];
+                for (int k = 0; k < SPL; ++k) p[k] = c[j][k];
         }
     }
 }
@@ -826,8 +828,9 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
             double xr[SPL];
             lds_row_read<SPL>(sl.pre[n - 1], lane, xr);
             double* row = U + (size_t)head * Dpad + lane * SPL;
+            if (row_lane<SPL>(lane, Dpad))
 #pragma unroll
-            for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             vm_drain();
             if (lane == 0) publish_word(done_word, epoch);
         }
@@ -881,13 +884,15 @@ template <int SPL>
 __device__ __forceinline__ void agent_row_read(const double* U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
     const double* p = U + (size_t)slot * Dpad + lane * SPL;
 #pragma unroll
-    for (int q = 0; q < SPL; ++q) r[q] = __hip_atomic_load(p + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = 0; q < SPL; ++q)
+        r[q] = row_lane<SPL>(lane, Dpad) ? __hip_atomic_load(p + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
 }
 template <int SPL>
 __device__ __forceinline__ void agent_row_write(double* U, uint32_t slot, int Dpad, int lane, const double (&r)[SPL]) {
     double* p = U + (size_t)slot * Dpad + lane * SPL;
+    if (row_lane<SPL>(lane, Dpad))
 #pragma unroll
-    for (int q = 0; q < SPL; ++q) __hip_atomic_store(p + q, r[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int q = 0; q < SPL; ++q) __hip_atomic_store(p + q, r[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // guessed input of a piece: fold of the ns segment aggregates below it (agg = the first of them,
@@ -1360,7 +1365,7 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
             double* row = V.A + (size_t)(head + len - 1) * Dpad + lane * SPL;
 #pragma unroll
             for (int k = 0; k < G; ++k)
-                if (k == n - 1)
+                if (k == n - 1 && row_lane<SPL>(lane, Dpad))
 #pragma unroll
                     for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xs[k][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             vm_drain();

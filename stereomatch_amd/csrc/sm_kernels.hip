@@ -729,13 +729,13 @@ __global__ __launch_bounds__(256) void k_vol_rows(const float* __restrict__ vin,
     __syncthreads();
     for (int px = ty; px < 64; px += 4) {
         if (p0 + px >= N) break;
-        Cst[(size_t)slotpix[p0 + px] * Dpad + dc + tx] = t[tx][px];
+        if (dc + tx < Dpad) Cst[(size_t)slotpix[p0 + px] * Dpad + dc + tx] = t[tx][px];
     }
 }
 
 hipError_t launch_vol_rows(hipStream_t st, const float* vin, size_t N, int d0, int D, int Dpad, const uint32_t* slotpix,
                            float* Cst) {
-    const dim3 g((unsigned)((N + 63) / 64), (unsigned)(Dpad / 64));
+    const dim3 g((unsigned)((N + 63) / 64), (unsigned)((Dpad + 63) / 64));
     hipLaunchKernelGGL(k_vol_rows, g, dim3(256), 0, st, vin, N, d0, D, Dpad, slotpix, Cst);
     return hipGetLastError();
 }

@@ -36,11 +36,20 @@ __device__ __forceinline__ float agd_rec(uint2 r0, uint2 l0, float gr1, float gl
     return a + b;
 }
 
+// Rows are Dpad doubles: 64*SPL, or 32 at SPL = 1 for calls of <= 32 slices (a 32-slice shard then
+// moves 32 slices of rows, not 64).  At SPL = 1 lanes >= Dpad neither load (they read +0, outside the
+// WTA's range) nor store.
+template <int SPL>
+__device__ __forceinline__ bool row_lane(int lane, int Dpad) {
+    if constexpr (SPL == 1) return lane < Dpad;
+    return true;
+}
+
 template <int SPL>
 __device__ __forceinline__ void load_row(const double* __restrict__ U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
     const double* p = U + (size_t)slot * Dpad + lane * SPL;
     if constexpr (SPL == 1) {
-        r[0] = p[0];
+        r[0] = lane < Dpad ? p[0] : 0.0;
     } else {
 #pragma unroll
         for (int k = 0; k < SPL; k += 2) {
@@ -55,7 +64,7 @@ template <int SPL>
 __device__ __forceinline__ void store_row(double* __restrict__ U, uint32_t slot, int Dpad, int lane, const double (&r)[SPL]) {
     double* p = U + (size_t)slot * Dpad + lane * SPL;
     if constexpr (SPL == 1) {
-        p[0] = r[0];
+        if (lane < Dpad) p[0] = r[0];
     } else {
 #pragma unroll
         for (int k = 0; k < SPL; k += 2) *reinterpret_cast<double2*>(p + k) = make_double2(r[k], r[k + 1]);
@@ -238,7 +247,7 @@ template <int SPL>
 __device__ __forceinline__ void load_cost_row(const float* __restrict__ C, uint32_t slot, int Dpad, int lane, float (&c)[SPL]) {
     const float* p = C + (size_t)slot * Dpad + lane * SPL;
     if constexpr (SPL == 1) {
-        c[0] = p[0];
+        c[0] = lane < Dpad ? p[0] : 0.0f;
     } else if constexpr (SPL == 2) {
         const float2 t = *reinterpret_cast<const float2*>(p);
         c[0] = t.x;

@@ -729,3 +729,42 @@ def test_subpixel_shard_halo_with_reduce(d0, D, Dt):
         idx = (d0 + am).astype(np.int32)
         np.testing.assert_array_equal(out[v]["idx"].ravel(), idx)
         np.testing.assert_array_equal(out[v]["disp"].ravel(), O.subpixel(A, idx, lo, Dt))
+
+
+# ---- 32-slice rows (Dpad = 32 for calls of <= 32 slices: a C4 shard moves 32 slices of rows) ----
+@pytest.mark.parametrize("W,H,D,plen", [(320, 240, 32, "64"), (256, 160, 17, "64"), (200, 150, 32, None)])
+def test_dpad32_match_bitexact(gpu_ctx, monkeypatch, W, H, D, plen):
+    """Calls of <= 32 slices use 32-double rows (lanes 32..63 load nothing, store nothing): matches
+    with cut paths (fast and forced-slow repair) against the oracle, bitwise."""
+    if plen:
+        monkeypatch.setenv("SM_PIECE_LEN", plen)
+    left, right, _ = make_pair(W, H, D, index=12)
+    ref = O.match(left, right, D, nthreads=16)
+    for rmax in (None, "1"):
+        if rmax:
+            monkeypatch.setenv("SM_REPAIR_MAX", rmax)
+        out = gpu_ctx.match(left, right, D)
+        for v in ("left", "right"):
+            np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+            assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+def test_dpad32_volume_ingest_and_rows(gpu_ctx, monkeypatch):
+    """MC-CNN volume rows and every A_up / A value at 32-slice rows, with 64-node pieces."""
+    import stereomatch_amd as sm
+    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    W, H, D, d0 = 240, 160, 30, 2
+    left, right, _ = make_pair(W, H, 64, index=13)
+    lv, rv = _mccnn_like(40, H, W, 7), _mccnn_like(40, H, W, 8)
+    gpu_ctx.upload_cost_volumes(lv, rv)
+    out = gpu_ctx.match(left, right, D, sm.default_params(cost_kind=sm.SM_COST_VOLUME, disp_begin=d0))
+    for v, img, vol in (("left", left, lv), ("right", right, rv)):
+        r = O.tree_filter(W, H, O.build_tree(img), O.mccnn_clamp(vol[d0:d0 + D]), d0, True, False, 16)
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), r["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
+    cl, cr = O.cost_agd(left, right, 5, 5 + 20)
+    for vi, (img, vol) in enumerate(((left, cl), (right, cr))):
+        Aup, A = gpu_ctx.aggregate_debug(left, right, vi, 5, 20)
+        r = O.tree_filter(W, H, O.build_tree(img), vol, 5, False, True, 16)
+        assert np.array_equal(bits(Aup), bits(r["Aup"]))
+        assert np.array_equal(bits(A), bits(r["A"]))
