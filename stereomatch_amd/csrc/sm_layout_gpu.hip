@@ -15,6 +15,7 @@
 // child order of Stereo3DMST.cpp:450-522 (root = first pixel; children by edge key), which is all
 // the exact arithmetic depends on; the heavy-light choice only schedules the work.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -677,7 +678,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
 //    path starts a new run when its bucket slot offset enters a new window of rwin nodes (or
 //    after a cut path) -> item {first path, 0, 1, number of paths}.
 // One block per view.
-__global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t plen) {
+__global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t plen, uint32_t rdiv, uint32_t rcap) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.x];
     __shared__ unsigned long long sc[SCAN_BLOCK / 64];  // the block scan's per-wave totals
@@ -704,7 +705,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
         const uint32_t sbase = running;  // the bucket's first segment
         const uint32_t hbase = hb[b];
         // run window: ~3 runs per CU over both views (256 CUs), 64 .. plen nodes
-        const uint32_t rwin = min(plen, max(64u, rn[b] / (uint32_t)SM_RUN_DIV));
+        const uint32_t rwin = min(rcap, max(64u, rn[b] / rdiv));
         if (threadIdx.x == 0) {
             prev_win = 0xFFFFFFFFu;
             prev_cut = 1u;
@@ -813,6 +814,11 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
     hipLaunchKernelGGL(k_slotpix, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, N);
-    hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP, piece_len);
+    // run sizing (A/B knobs: SM_RUN_DIV, SM_RUN_CAP = the window cap in nodes)
+    const char* ed = getenv("SM_RUN_DIV");
+    const char* ec = getenv("SM_RUN_CAP");
+    const uint32_t rdiv = ed && atoi(ed) > 0 ? (uint32_t)atoi(ed) : (uint32_t)SM_RUN_DIV;
+    const uint32_t rcap = ec && atoi(ec) >= 64 ? (uint32_t)atoi(ec) : piece_len;
+    hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP, piece_len, rdiv, rcap);
     return hipGetLastError();
 }
