@@ -137,6 +137,8 @@ def main():
     ap.add_argument("--segment-c", type=float, default=float("inf"),
                     help="finite: segment mode (Stereo3DMST's c, e.g. 5000) instead of the MST")
     ap.add_argument("--min-size", type=int, default=200)
+    ap.add_argument("--aggregator", default="tree", choices=["tree", "guided"],
+                    help="cost aggregator: the MST/forest tree filter (default) or the colour guided filter")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight (contexts on their own streams); 0 = 3, fewer where memory needs it")
     args = ap.parse_args()
@@ -192,7 +194,8 @@ def main():
     left, right, _ = make_pair(W, H, Dtot_frame, index=pair_index)
     for c in ctxs:
         c.upload(left, right)
-    params = sm.default_params(disp_begin=dbeg, disp_total=Dtot_frame, c=args.segment_c, min_size=args.min_size)
+    params = sm.default_params(disp_begin=dbeg, disp_total=Dtot_frame, c=args.segment_c, min_size=args.min_size,
+                               aggregator=sm.SM_AGG_GUIDED if args.aggregator == "guided" else sm.SM_AGG_TREE)
     torch.cuda.set_device(local)
     ctx = ctxs[0]
 
@@ -217,7 +220,7 @@ def main():
     # in a diagnostic pass after the timed region (kernels_ms_per_step, tree_filter)
     warm = {}
     accumulate(warm, ctx)
-    dom = max(warm, key=lambda k: warm[k]["ms"])
+    dom = max(warm, key=lambda k: warm[k]["ms"])  # (guided aggregator: no tree families, all zero)
     for c in ctxs:
         c.set_kernel_timing([dom])
         c.synchronize()
@@ -324,6 +327,7 @@ def main():
                    "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world,
                    "tree": "MST" if args.segment_c == float("inf") else "segment forest c=%g min_size=%d" % (
                        args.segment_c, args.min_size),
+                   "aggregator": args.aggregator,
                    "frames_in_flight": inflight},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

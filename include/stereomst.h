@@ -49,6 +49,15 @@ typedef enum {
     SM_COST_VOLUME = 1   /* caller-supplied [D][H][W] float volumes (MC-CNN .bin ingest)    */
 } sm_cost_kind;
 
+/* Cost aggregator of a call (sm_params.aggregator). */
+typedef enum {
+    SM_AGG_TREE = 0,   /* the MST / segment-forest tree filter (Stereo3DMST.cpp:120-186)          */
+    SM_AGG_GUIDED = 1  /* the colour guided filter of the cost volume, each view guided by its own
+                          image, then selectDisparity (PatchMatchStereoGPU.cu:8251-8470, 1688-1737);
+                          float arithmetic; radius gf_radius, eps gf_eps (the reference: 9 and
+                          0.01^2*255^2, :9000-9001); AGD cost only */
+} sm_aggregator;
+
 typedef struct {
     int device;        /* HIP device ordinal                                        */
     int max_width;     /* workspace capacity                                        */
@@ -67,6 +76,9 @@ typedef struct {
     int disp_begin;    /* first global disparity of this call (D sharding)          */
     int disp_total;    /* total disparities across all shards (== D unsharded)      */
     int post;          /* sm_post bits applied to the final maps (default 0)         */
+    int aggregator;    /* sm_aggregator (default SM_AGG_TREE)                        */
+    int gf_radius;     /* SM_AGG_GUIDED: box radius (default 9)                      */
+    float gf_eps;      /* SM_AGG_GUIDED: regularisation (default 6.5025 = 0.01^2*255^2) */
 } sm_params;
 
 /* Post-processing of the final (cross-rank reduced) float disparity maps (idx / min untouched),

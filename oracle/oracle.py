@@ -48,6 +48,9 @@ def lib():
         L.orc_lr_check_fill.argtypes = [vp, vp, c_int, c_int, c_int, c_int]
         L.orc_label_to_disp.argtypes = [vp, ctypes.c_long, c_int]
         L.orc_set_agd_contract.argtypes = [c_int]
+        L.orc_guided_filter.argtypes = [u8p, c_int, c_int, c_int, vp, c_int, c_int, c_float, vp, c_int]
+        L.orc_box_mean.argtypes = [vp, vp, c_int, c_int, c_int]
+        L.orc_select_disparity.argtypes = [vp, c_int, c_int, c_int, ctypes.c_size_t, c_int, vp, vp, vp]
         L.orc_occlusion.argtypes = [vp, vp, c_int, c_int, c_int, c_float, c_int]
         _LIB = L
     return _LIB
@@ -245,6 +248,49 @@ def subpixel(A, idx, dglob0, dtot):
         s = ((nxt - pre) * f32(0.5) / ((nxt - f32(2.0) * cur) + pre)).astype(f32)
     g = i.astype(f32)
     return np.where(np.abs(s) < f32(1.0), g - s, g).astype(f32)
+
+
+def guided_filter(img, vol, radius=9, eps=6.5025, nthreads=0):
+    """Colour guided filter of a [nd][H][W] float cost volume, guided by the view's BGR image
+    (PatchMatchStereoGPU.cu:8251-8470)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W, _ = img.shape
+    v = np.ascontiguousarray(vol, dtype=np.float32)
+    out = np.empty_like(v)
+    lib().orc_guided_filter(img, W, H, W * 3, _ptr(v), v.shape[0], int(radius), float(eps), _ptr(out), int(nthreads))
+    return out
+
+
+def box_mean(a, r):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    out = np.empty_like(a)
+    lib().orc_box_mean(_ptr(a), _ptr(out), a.shape[1], a.shape[0], int(r))
+    return out
+
+
+def select_disparity(vol, d0=0, dtot=None, sub=False):
+    """selectDisparity (PatchMatchStereoGPU.cu:1688-1737) of a float [nd][H][W] volume."""
+    v = np.ascontiguousarray(vol, dtype=np.float32)
+    nd = v.shape[0]
+    N = v[0].size
+    idx = np.empty(N, np.int32)
+    mn = np.empty(N, np.float32)
+    disp = np.empty(N, np.float32)
+    lib().orc_select_disparity(_ptr(v), nd, int(d0), int(dtot if dtot else d0 + nd), N, 1 if sub else 0, _ptr(idx),
+                               _ptr(mn), _ptr(disp))
+    return idx, mn, disp
+
+
+def guided_match(left, right, D, radius=9, eps=6.5025, sub=False, nthreads=0):
+    """The guided-filter aggregator end to end: AGD cost, colour guided filter per view (guide: the
+    view's own image), selectDisparity.  Returns per-view dicts idx / minc / disp / vol."""
+    lv, rv = cost_agd(left, right, 0, D, nthreads)
+    out = {}
+    for name, img, vol in (("left", left, lv), ("right", right, rv)):
+        f = guided_filter(img, vol, radius, eps, nthreads)
+        idx, mn, disp = select_disparity(f, 0, D, sub)
+        out[name] = dict(idx=idx, minc=mn, disp=disp, vol=f)
+    return out
 
 
 def occlusion(left_disp, right_disp, min_disp=0, thresh=1.0, remove=False):

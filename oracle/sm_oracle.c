@@ -497,3 +497,197 @@ void orc_occlusion(float* left, float* right, int W, int H, int min_disp, float 
     }
     free(t);
 }
+
+/* ------------------------------------------------------------------ guided-filter aggregation */
+/* Sliding box mean of radius r (boxFilter_x_global_shared / boxFilter_y_global,
+ * PatchMatchStereoGPU.cu:495-580): the running sum restarts at every 32-pixel block (the kernels'
+ * block width), starts as sum_{i=x0-r}^{x0+r} in ascending i (0 outside the image), then slides
+ * t += in[x+r]; t -= in[x-r-1] (0 outside); out = t * (1.0f/(2r+1)). */
+#define ORC_GF_BLOCK 32
+static void orc_box_x(const float* in, float* out, int W, int H, int r) {
+    const float scale = 1.0f / (float)((r << 1) + 1);
+    for (int y = 0; y < H; ++y) {
+        const float* row = in + (size_t)y * W;
+        float* o = out + (size_t)y * W;
+        for (int x0 = 0; x0 < W; x0 += ORC_GF_BLOCK) {
+            float t = 0.0f;
+            for (int i = x0 - r; i <= x0 + r; ++i) t += (i < 0 || i >= W) ? 0.0f : row[i];
+            o[x0] = t * scale;
+            const int end = W - x0 < ORC_GF_BLOCK ? W : x0 + ORC_GF_BLOCK;
+            for (int x = x0 + 1; x < end; ++x) {
+                t += (x + r >= W) ? 0.0f : row[x + r];
+                t -= (x - r - 1 < 0) ? 0.0f : row[x - r - 1];
+                o[x] = t * scale;
+            }
+        }
+    }
+}
+
+static void orc_box_y(const float* in, float* out, int W, int H, int r) {
+    const float scale = 1.0f / (float)((r << 1) + 1);
+    for (int x = 0; x < W; ++x)
+        for (int y0 = 0; y0 < H; y0 += ORC_GF_BLOCK) {
+            float t = 0.0f;
+            for (int i = y0 - r; i <= y0 + r; ++i) t += (i < 0 || i >= H) ? 0.0f : in[(size_t)i * W + x];
+            out[(size_t)y0 * W + x] = t * scale;
+            const int end = H - y0 < ORC_GF_BLOCK ? H : y0 + ORC_GF_BLOCK;
+            for (int y = y0 + 1; y < end; ++y) {
+                t += (y + r >= H) ? 0.0f : in[(size_t)(y + r) * W + x];
+                t -= (y - r - 1 < 0) ? 0.0f : in[(size_t)(y - r - 1) * W + x];
+                out[(size_t)y * W + x] = t * scale;
+            }
+        }
+}
+
+static void orc_box(const float* in, float* out, float* tmp, int W, int H, int r) {
+    orc_box_x(in, tmp, W, H, r);
+    orc_box_y(tmp, out, W, H, r);
+}
+
+/* Colour guided filter of one cost slice p with guide planes (r, g, b) -- the per-pixel steps of
+ * costVolumeColorGuidedFilterCUDA2Streams (PatchMatchStereoGPU.cu:8251-8470) in source order,
+ * no contraction: the guide statistics st[] (mean_r, mean_g, mean_b, inv_rr, inv_rg, inv_rb,
+ * inv_gg, inv_gb, inv_bb; see orc_gf_guide) are precomputed. */
+static void orc_gf_slice(const float* p, const float* gr, const float* gg, const float* gb, const float* const* st,
+                         int W, int H, int rad, float* q, float* w /* 12 planes of N */) {
+    const size_t N = (size_t)W * H;
+    float *mp = w, *mr = w + N, *mg = w + 2 * N, *mb = w + 3 * N, *t = w + 4 * N, *ar = w + 5 * N, *ag = w + 6 * N,
+          *ab = w + 7 * N, *bb = w + 8 * N, *x = w + 9 * N;
+    orc_box(p, mp, t, W, H, rad);                               /* mean_p */
+    for (size_t i = 0; i < N; ++i) x[i] = gr[i] * p[i];
+    orc_box(x, mr, t, W, H, rad);                               /* mean_I_r = box(r .* p) */
+    for (size_t i = 0; i < N; ++i) x[i] = gg[i] * p[i];
+    orc_box(x, mg, t, W, H, rad);
+    for (size_t i = 0; i < N; ++i) x[i] = gb[i] * p[i];
+    orc_box(x, mb, t, W, H, rad);
+    const float *m_r = st[0], *m_g = st[1], *m_b = st[2];
+    const float *irr = st[3], *irg = st[4], *irb = st[5], *igg = st[6], *igb = st[7], *ibb = st[8];
+    for (size_t i = 0; i < N; ++i) {
+        const float cr = mr[i] - m_r[i] * mp[i];                /* Helper3: s1 - s2*s3 */
+        const float cg = mg[i] - m_g[i] * mp[i];
+        const float cb = mb[i] - m_b[i] * mp[i];
+        ar[i] = irr[i] * cr + irg[i] * cg + irb[i] * cb;        /* Helper2 */
+        ag[i] = irg[i] * cr + igg[i] * cg + igb[i] * cb;
+        ab[i] = irb[i] * cr + igb[i] * cg + ibb[i] * cb;
+        bb[i] = mp[i] - ar[i] * m_r[i] - ag[i] * m_g[i] - ab[i] * m_b[i];  /* Helper4 */
+    }
+    orc_box(ar, mr, t, W, H, rad);
+    orc_box(ag, mg, t, W, H, rad);
+    orc_box(ab, mb, t, W, H, rad);
+    orc_box(bb, x, t, W, H, rad);
+    for (size_t i = 0; i < N; ++i) q[i] = x[i] + mr[i] * gr[i] + mg[i] * gg[i] + mb[i] * gb[i];  /* Helper5 */
+}
+
+/* guide statistics of one view (PatchMatchStereoGPU.cu:8261-8420), eps added to the diagonal */
+static void orc_gf_guide(const float* gr, const float* gg, const float* gb, int W, int H, int rad, float eps, float** st,
+                         float* w /* 4 planes */) {
+    const size_t N = (size_t)W * H;
+    float *t = w, *x = w + N, *m = w + 2 * N;
+    float *vrr = malloc(sizeof(float) * N), *vgg = malloc(sizeof(float) * N), *vbb = malloc(sizeof(float) * N);
+    float *vrg = malloc(sizeof(float) * N), *vrb = malloc(sizeof(float) * N), *vgb = malloc(sizeof(float) * N);
+    orc_box(gr, st[0], t, W, H, rad);
+    orc_box(gg, st[1], t, W, H, rad);
+    orc_box(gb, st[2], t, W, H, rad);
+    const float* pl[3] = {gr, gg, gb};
+    float* var[6] = {vrr, vgg, vbb, vrg, vrb, vgb};
+    const int pa[6] = {0, 1, 2, 0, 0, 1}, pb[6] = {0, 1, 2, 1, 2, 2};
+    for (int k = 0; k < 6; ++k) {
+        for (size_t i = 0; i < N; ++i) x[i] = pl[pa[k]][i] * pl[pb[k]][i];
+        orc_box(x, m, t, W, H, rad);
+        for (size_t i = 0; i < N; ++i) {
+            const float mm = st[pa[k]][i] * st[pb[k]][i];
+            var[k][i] = k < 3 ? m[i] - mm + eps : m[i] - mm;      /* Helper0 */
+        }
+    }
+    for (size_t i = 0; i < N; ++i) {                              /* Helper1 ... */
+        float irr = vgg[i] * vbb[i] - vgb[i] * vgb[i];
+        float igg = vrr[i] * vbb[i] - vrb[i] * vrb[i];
+        float ibb = vrr[i] * vgg[i] - vrg[i] * vrg[i];
+        float irg = vgb[i] * vrb[i] - vrg[i] * vbb[i];
+        float irb = vrg[i] * vgb[i] - vgg[i] * vrb[i];
+        float igb = vrb[i] * vrg[i] - vrr[i] * vgb[i];
+        const float det = irr * vrr[i] + irg * vrg[i] + irb * vrb[i];  /* Helper2 */
+        st[3][i] = irr / det;
+        st[4][i] = irg / det;
+        st[5][i] = irb / det;
+        st[6][i] = igg / det;
+        st[7][i] = igb / det;
+        st[8][i] = ibb / det;
+    }
+    free(vrr); free(vgg); free(vbb); free(vrg); free(vrb); free(vgb);
+}
+
+void orc_guided_filter(const uint8_t* img, int W, int H, int stride, const float* vol, int nd, int rad, float eps,
+                       float* out, int nthreads) {
+    const size_t N = (size_t)W * H;
+    float* g3 = malloc(sizeof(float) * 3 * N);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const uint8_t* px = img + (size_t)y * stride + 3 * x;
+            g3[(size_t)y * W + x] = (float)px[2];          /* r */
+            g3[N + (size_t)y * W + x] = (float)px[1];      /* g */
+            g3[2 * N + (size_t)y * W + x] = (float)px[0];  /* b */
+        }
+    float* stb = malloc(sizeof(float) * 9 * N);
+    float* st[9];
+    for (int k = 0; k < 9; ++k) st[k] = stb + k * N;
+    float* w0 = malloc(sizeof(float) * 3 * N);
+    orc_gf_guide(g3, g3 + N, g3 + 2 * N, W, H, rad, eps, st, w0);
+    free(w0);
+    int nt = 1;
+#ifdef _OPENMP
+    nt = nthreads > 0 ? nthreads : omp_get_max_threads();
+#else
+    (void)nthreads;
+#endif
+#pragma omp parallel num_threads(nt)
+    {
+        float* w = malloc(sizeof(float) * 10 * N);
+#pragma omp for schedule(dynamic, 1)
+        for (int d = 0; d < nd; ++d)
+            orc_gf_slice(vol + (size_t)d * N, g3, g3 + N, g3 + 2 * N, (const float* const*)st, W, H, rad, out + (size_t)d * N, w);
+        free(w);
+    }
+    free(stb);
+    free(g3);
+}
+
+/* selectDisparity (PatchMatchStereoGPU.cu:1688-1737) on a float volume of slices d0..: strict <
+ * from 1e10f over ascending d; no minimum -> disp 0 (idx 0); with sub the parabola through the
+ * neighbouring slices (0 at the ends of [0, dtot)). */
+void orc_select_disparity(const float* vol, int nd, int d0, int dtot, size_t N, int sub, int32_t* idx, float* mn,
+                          float* disp) {
+    for (size_t p = 0; p < N; ++p) {
+        float m = 1e10f;
+        int best = -1;
+        for (int d = 0; d < nd; ++d) {
+            const float c = vol[(size_t)d * N + p];
+            if (c < m) { m = c; best = d; }
+        }
+        if (best < 0) {
+            idx[p] = 0;
+            mn[p] = m;
+            disp[p] = 0.0f;
+            continue;
+        }
+        const int g = d0 + best;
+        idx[p] = g;
+        mn[p] = m;
+        float dd = (float)g;
+        if (sub) {
+            const float pre = g == 0 ? 0.0f : vol[(size_t)(best - 1) * N + p];
+            const float cur = vol[(size_t)best * N + p];
+            const float nxt = g == dtot - 1 ? 0.0f : vol[(size_t)(best + 1) * N + p];
+            const float s = (nxt - pre) * 0.5f / (nxt - 2.0f * cur + pre);
+            if (fabsf(s) < 1.0f) dd = (float)g - s;
+        }
+        disp[p] = dd;
+    }
+}
+
+/* box mean of one plane (x pass, then y pass): test access to orc_box */
+void orc_box_mean(const float* in, float* out, int W, int H, int r) {
+    float* t = malloc(sizeof(float) * (size_t)W * H);
+    orc_box(in, out, t, W, H, r);
+    free(t);
+}

@@ -19,6 +19,7 @@
  */
 #ifndef SM_ORACLE_H
 #define SM_ORACLE_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -81,6 +82,16 @@ void orc_lr_check_fill(float* left, const float* right, int W, int H, int max_di
 /* LabelToDisp of the per-slice label (0, 0, d) and the *= (Dmax-1) scaling (:189-201, 900-902). */
 void orc_label_to_disp(float* disp, long n, int dmax);
 /* handleOcclusionSharedMemory (PatchMatchStereoGPU.cu:1128-1288), marks computed before the search. */
+/* Colour guided filter of a cost volume [nd][H][W] with the view's own BGR image as guide, radius
+ * rad, eps (costVolumeColorGuidedFilterCUDA2Streams, PatchMatchStereoGPU.cu:8251-8470; box means of
+ * :495-580); OpenMP over slices. */
+void orc_guided_filter(const uint8_t* img, int W, int H, int stride, const float* vol, int nd, int rad, float eps,
+                       float* out, int nthreads);
+/* the reference's box mean of one plane: 32-block sliding sums, x pass then y pass (.cu:495-580) */
+void orc_box_mean(const float* in, float* out, int W, int H, int r);
+/* selectDisparity (PatchMatchStereoGPU.cu:1688-1737), with the subpixel parabola when sub. */
+void orc_select_disparity(const float* vol, int nd, int d0, int dtot, size_t N, int sub, int32_t* idx, float* mn,
+                          float* disp);
 void orc_occlusion(float* left, float* right, int W, int H, int min_disp, float thresh, int remove);
 
 #ifdef __cplusplus

@@ -18,6 +18,7 @@ STATUS_NAMES = {0: "SM_OK", 1: "SM_ERR_ARG", 2: "SM_ERR_HIP", 3: "SM_ERR_OOM", 4
 SM_COST_AGD, SM_COST_VOLUME = 0, 1
 SM_POST_LR_CHECK, SM_POST_LABEL_TO_DISP, SM_POST_LR_FILL, SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO = 1, 2, 4, 8, 16
 SM_POST_SUBPIXEL = 32
+SM_AGG_TREE, SM_AGG_GUIDED = 0, 1
 SM_UNIQUE_ID_BYTES = 128
 
 
@@ -29,7 +30,8 @@ class SmConfig(ctypes.Structure):
 class SmParams(ctypes.Structure):
     _fields_ = [("gamma", ctypes.c_float), ("c", ctypes.c_float), ("min_size", ctypes.c_int),
                 ("median_ksize", ctypes.c_int), ("cost_kind", ctypes.c_int), ("disp_begin", ctypes.c_int),
-                ("disp_total", ctypes.c_int), ("post", ctypes.c_int)]
+                ("disp_total", ctypes.c_int), ("post", ctypes.c_int), ("aggregator", ctypes.c_int),
+                ("gf_radius", ctypes.c_int), ("gf_eps", ctypes.c_float)]
 
 
 class SmFilterStats(ctypes.Structure):

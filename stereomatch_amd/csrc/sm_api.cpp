@@ -64,6 +64,9 @@ struct sm_ctx {
     DevBuf changed, mst_ok, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
     DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
     DevBuf post_mask, post_scratch;  // output step (sm_post.hip): marks, scan positions
+    // guided-filter aggregator (sm_guided.hip): guide planes / means, per-view statistics, batch
+    // planes, box scratch, WTA state
+    DevBuf gf_planes, gf_means, gf_stats[2], gf_pl, gf_tmp, gf_state[2];
     // segment mode (finite c, sm_segment.cpp): layout weights with the virtual edges, and host copies
     DevBuf fwR[2], fwD[2];
     bool seg = false;  // the current tree is a segment forest (layout reads fwR / fwD)
@@ -192,6 +195,14 @@ sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
         return fail(ctx, SM_ERR_ARG, "SM_POST_LR_FILL needs SM_POST_LR_CHECK");
     if ((p->post & SM_POST_OCCLUSION) && (p->post & SM_POST_OCCLUSION_ZERO))
         return fail(ctx, SM_ERR_ARG, "SM_POST_OCCLUSION and SM_POST_OCCLUSION_ZERO are exclusive");
+    if (p->aggregator != SM_AGG_TREE && p->aggregator != SM_AGG_GUIDED) return fail(ctx, SM_ERR_ARG, "unknown aggregator");
+    if (p->aggregator == SM_AGG_GUIDED) {
+        if (p->cost_kind != SM_COST_AGD) return fail(ctx, SM_ERR_ARG, "SM_AGG_GUIDED filters the AGD cost only");
+        if (p->gf_radius < 1 || p->gf_radius > 64 || !(p->gf_eps > 0)) return fail(ctx, SM_ERR_ARG, "bad guided-filter radius / eps");
+        if ((p->post & SM_POST_SUBPIXEL) && (p->disp_begin > 0 || (p->disp_total > 0 && p->disp_total != D)))
+            return fail(ctx, SM_ERR_ARG, "SM_AGG_GUIDED: subpixel on a shard is not supported");
+        return SM_OK;
+    }
     if (p->post & SM_POST_SUBPIXEL) {
         const int dtot = p->disp_total > 0 ? p->disp_total : p->disp_begin + D;
         const int halo = (p->disp_begin > 0) + (p->disp_begin + D < dtot);
@@ -938,6 +949,47 @@ sm_status stage_reduce(sm_ctx* ctx) {
     return SM_OK;
 }
 
+// Guided-filter aggregator (sm_guided.hip): guide statistics per view, then batches of up to 32
+// slices of AGD cost (k_cost_volume), each through the colour guided filter and the running WTA.
+sm_status stage_guided(sm_ctx* ctx, int D, int d0, int dtot, int sub, int rad, float eps) {
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H;
+    const int S = std::min(D, 32);
+    CHECK(ensure(ctx, ctx->gf_planes, 9 * N * 4));
+    CHECK(ensure(ctx, ctx->gf_means, 9 * N * 4));
+    CHECK(ensure(ctx, ctx->gf_pl, 4 * (size_t)S * N * 4));
+    CHECK(ensure(ctx, ctx->gf_tmp, std::max<size_t>(9, 4 * (size_t)S) * N * 4));
+    for (int v = 0; v < 2; ++v) {
+        CHECK(ensure(ctx, ctx->gf_stats[v], 9 * N * 4));
+        CHECK(ensure(ctx, ctx->gf_state[v], 5 * N * 4));
+        CHECK(ensure(ctx, ctx->vol[v], (size_t)S * N * 4));
+        CHECK(ensure(ctx, ctx->idx[v], N * 4));
+        CHECK(ensure(ctx, ctx->minc[v], N * 8));
+        CHECK(ensure(ctx, ctx->disp[v], N * 4));
+    }
+    GfStateArgs sa[2];
+    for (int v = 0; v < 2; ++v) {
+        float* b = P<float>(ctx->gf_state[v]);
+        sa[v] = GfStateArgs{b, reinterpret_cast<int32_t*>(b + N), b + 2 * N, b + 3 * N, b + 4 * N};
+        HIPC(launch_gf_guide(ctx->st, P<uint32_t>(ctx->bgrx[v]), W, H, rad, eps, P<float>(ctx->gf_planes), P<float>(ctx->gf_tmp),
+                             P<float>(ctx->gf_means), P<float>(ctx->gf_stats[v])));
+        HIPC(launch_gf_init(ctx->st, sa[v], N));
+    }
+    for (int b = 0; b < D; b += S) {
+        const int s = std::min(S, D - b);
+        HIPC(launch_cost_volume(ctx->st, P<uint32_t>(ctx->bgrx[0]), P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]),
+                                P<float>(ctx->gray[1]), P<float>(ctx->atab), W, H, d0 + b, s, P<float>(ctx->vol[0]),
+                                P<float>(ctx->vol[1])));
+        for (int v = 0; v < 2; ++v)
+            HIPC(launch_gf_batch(ctx->st, P<float>(ctx->vol[v]), P<uint32_t>(ctx->bgrx[v]), P<float>(ctx->gf_stats[v]), W, H,
+                                 rad, s, b, P<float>(ctx->gf_pl), P<float>(ctx->gf_tmp), sa[v]));
+    }
+    for (int v = 0; v < 2; ++v)
+        HIPC(launch_gf_out(ctx->st, sa[v], N, d0, dtot, sub, P<int32_t>(ctx->idx[v]), P<double>(ctx->minc[v]),
+                           P<float>(ctx->disp[v])));
+    return SM_OK;
+}
+
 // output step on the final (reduced) float maps, in the reference's order: LabelToDisp + scaling
 // (Stereo3DMST.cpp:189-201, 900-902), L-R check (+ fill) (:632-709, 904), then the GPU PatchMatch's
 // occlusion handling (PatchMatchStereoGPU.cu:1128-1288).  dmax = the total disparity range.
@@ -1011,6 +1063,9 @@ void sm_default_params(sm_params* p) {
     p->disp_begin = 0;
     p->disp_total = 0;
     p->post = 0;
+    p->aggregator = SM_AGG_TREE;
+    p->gf_radius = 9;                                  // PatchMatchStereoGPU.cu:9001
+    p->gf_eps = (float)(std::pow(0.01, 2.0) * 255 * 255);  // :9000
 }
 
 sm_status sm_device_count(int* count) {
@@ -1070,7 +1125,9 @@ void sm_destroy(sm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
-    DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut, &ctx->post_mask, &ctx->post_scratch};
+    DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut, &ctx->post_mask, &ctx->post_scratch,
+                     &ctx->gf_planes, &ctx->gf_means, &ctx->gf_pl, &ctx->gf_tmp, &ctx->gf_stats[0], &ctx->gf_stats[1],
+                     &ctx->gf_state[0], &ctx->gf_state[1]};
     for (DevBuf* b : all) if (b->p) (void)hipFree(b->p);
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
@@ -1141,6 +1198,23 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
     HIPC(hipEventRecord(ctx->ev[1], ctx->st));
+    if (p->aggregator == SM_AGG_GUIDED) {  // no tree: stage times MST / layout / down read 0
+        ctx->sub = false;
+        ctx->nfev = ctx->nsev = 0;
+        ctx->fam.clear();
+        ctx->fam_vox.clear();
+        ctx->fam_ev.clear();
+        HIPC(hipEventRecord(ctx->ev[2], ctx->st));
+        HIPC(hipEventRecord(ctx->ev[3], ctx->st));
+        CHECK(stage_guided(ctx, D, p->disp_begin, p->disp_total > 0 ? p->disp_total : p->disp_begin + D,
+                           (p->post & SM_POST_SUBPIXEL) ? 1 : 0, p->gf_radius, p->gf_eps));
+        HIPC(hipEventRecord(ctx->ev[6], ctx->st));
+        HIPC(hipEventRecord(ctx->ev[4], ctx->st));
+        CHECK(stage_reduce(ctx));
+        CHECK(stage_post(ctx, p->post, p->disp_total > 0 ? p->disp_total : p->disp_begin + D));
+        HIPC(hipEventRecord(ctx->ev[5], ctx->st));
+        return SM_OK;
+    }
     CHECK(stage_tree(ctx, 2, p));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
     CHECK(stage_layout(ctx, 2));

@@ -1,0 +1,281 @@
+// sm_guided.hip -- the guided-filter cost aggregator: the reference's colour
+// guided filter of the AGD cost volume, each view guided by its own BGR image, then selectDisparity
+// (PatchMatchStereoGPU.cu:8251-8470 costVolumeColorGuidedFilterCUDA2Streams, box means :495-580,
+// WTA :1688-1737; radius 9 and eps = 0.01^2 * 255^2 at :9000-9001).  A second aggregator behind the
+// same C-ABI (sm_params.aggregator = SM_AGG_GUIDED): no tree, no MST.
+//
+// Arithmetic (the reference's float operations in source order, uncontracted):
+//   box mean  : per 32-pixel block (the reference kernels' block width) a sliding sum -- the first
+//               output sums in[x0-r .. x0+r] in ascending order (0 outside the image), then
+//               t += in[x+r]; t -= in[x-r-1]; out = t * (1.0f / (2r+1)) -- x pass, then y pass;
+//   guide     : mean_c = box(c); var_cc' = box(c*c') - mean_c*mean_c' (+ eps on the diagonal);
+//               inv = adjugate / det with det = inv_rr*var_rr + inv_rg*var_rg + inv_rb*var_rb;
+//   per slice : mean_p = box(p), mean_Ip_c = box(c*p), cov_c = mean_Ip_c - mean_c*mean_p,
+//               a = inv * cov, b = mean_p - a_r*mean_r - a_g*mean_g - a_b*mean_b,
+//               q = box(b) + box(a_r)*r + box(a_g)*g + box(a_b)*b;
+//   WTA       : strict < from 1e10f over ascending d, optional parabola (selectDisparity).
+//
+// Layout: planes [k][N] f32 in HBM; a batch of S slices moves through the box passes as 4*S planes
+// (grid.z).  The x pass runs one thread per (row, 32-column block), the y pass one thread per
+// (column, 32-row block) -- adjacent lanes read adjacent columns, so it is coalesced.  All passes
+// are HBM-streaming kernels (no MFMA: per-pixel scalar arithmetic).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_launch.h"
+
+#define GF_BLOCK 32
+
+// x pass of nplanes planes (plane stride N): thread = (row, 32-column block, plane)
+__global__ __launch_bounds__(64) void k_gf_box_x(const float* __restrict__ in, float* __restrict__ out, int W, int H, int r,
+                                                 size_t N) {
+    const int y = blockIdx.x * 64 + threadIdx.x;
+    if (y >= H) return;
+    const int x0 = blockIdx.y * GF_BLOCK;
+    const float* row = in + (size_t)blockIdx.z * N + (size_t)y * W;
+    float* o = out + (size_t)blockIdx.z * N + (size_t)y * W;
+    const float scale = 1.0f / (float)((r << 1) + 1);
+    float t = 0.0f;
+    for (int i = x0 - r; i <= x0 + r; ++i) t += (i < 0 || i >= W) ? 0.0f : row[i];
+    o[x0] = t * scale;
+    const int end = W - x0 < GF_BLOCK ? W : x0 + GF_BLOCK;
+    for (int x = x0 + 1; x < end; ++x) {
+        t += (x + r >= W) ? 0.0f : row[x + r];
+        t -= (x - r - 1 < 0) ? 0.0f : row[x - r - 1];
+        o[x] = t * scale;
+    }
+}
+
+// y pass: thread = (column, 32-row block, plane)
+__global__ __launch_bounds__(256) void k_gf_box_y(const float* __restrict__ in, float* __restrict__ out, int W, int H, int r,
+                                                  size_t N) {
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    if (x >= W) return;
+    const int y0 = blockIdx.y * GF_BLOCK;
+    const float* col = in + (size_t)blockIdx.z * N + x;
+    float* o = out + (size_t)blockIdx.z * N + x;
+    const float scale = 1.0f / (float)((r << 1) + 1);
+    float t = 0.0f;
+    for (int i = y0 - r; i <= y0 + r; ++i) t += (i < 0 || i >= H) ? 0.0f : col[(size_t)i * W];
+    o[(size_t)y0 * W] = t * scale;
+    const int end = H - y0 < GF_BLOCK ? H : y0 + GF_BLOCK;
+    for (int y = y0 + 1; y < end; ++y) {
+        t += (y + r >= H) ? 0.0f : col[(size_t)(y + r) * W];
+        t -= (y - r - 1 < 0) ? 0.0f : col[(size_t)(y - r - 1) * W];
+        o[(size_t)y * W] = t * scale;
+    }
+}
+
+__device__ __forceinline__ void guide_of(uint32_t bgrx, float& r, float& g, float& b) {
+    b = (float)(bgrx & 255u);
+    g = (float)((bgrx >> 8) & 255u);
+    r = (float)((bgrx >> 16) & 255u);
+}
+
+// the 9 guide planes r, g, b, rr, gg, bb, rg, rb, gb (pointWiseMul: one rounding each)
+__global__ void k_gf_guide_in(const uint32_t* __restrict__ bgrx, float* __restrict__ pl, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    float r, g, b;
+    guide_of(bgrx[i], r, g, b);
+    pl[i] = r;
+    pl[N + i] = g;
+    pl[2 * N + i] = b;
+    pl[3 * N + i] = r * r;
+    pl[4 * N + i] = g * g;
+    pl[5 * N + i] = b * b;
+    pl[6 * N + i] = r * g;
+    pl[7 * N + i] = r * b;
+    pl[8 * N + i] = g * b;
+}
+
+// guide statistics from the 9 box means m[]: st = mean_r, mean_g, mean_b, inv_rr, inv_rg, inv_rb,
+// inv_gg, inv_gb, inv_bb (colorGuidedFilterHelper0 / 1 / 2, pointWiseDivison)
+__global__ void k_gf_stats(const float* __restrict__ m, float* __restrict__ st, size_t N, float eps) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float mr = m[i], mg = m[N + i], mb = m[2 * N + i];
+    const float vrr = m[3 * N + i] - mr * mr + eps;
+    const float vgg = m[4 * N + i] - mg * mg + eps;
+    const float vbb = m[5 * N + i] - mb * mb + eps;
+    const float vrg = m[6 * N + i] - mr * mg;
+    const float vrb = m[7 * N + i] - mr * mb;
+    const float vgb = m[8 * N + i] - mg * mb;
+    const float irr = vgg * vbb - vgb * vgb;
+    const float igg = vrr * vbb - vrb * vrb;
+    const float ibb = vrr * vgg - vrg * vrg;
+    const float irg = vgb * vrb - vrg * vbb;
+    const float irb = vrg * vgb - vgg * vrb;
+    const float igb = vrb * vrg - vrr * vgb;
+    const float det = irr * vrr + irg * vrg + irb * vrb;
+    st[i] = mr;
+    st[N + i] = mg;
+    st[2 * N + i] = mb;
+    st[3 * N + i] = irr / det;
+    st[4 * N + i] = irg / det;
+    st[5 * N + i] = irb / det;
+    st[6 * N + i] = igg / det;
+    st[7 * N + i] = igb / det;
+    st[8 * N + i] = ibb / det;
+}
+
+// per slice s of the batch: planes [0..S) p, [S..2S) r*p, [2S..3S) g*p, [3S..4S) b*p
+__global__ void k_gf_slice_in(const float* __restrict__ cost, const uint32_t* __restrict__ bgrx, float* __restrict__ pl,
+                              size_t N, int S) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const int s = blockIdx.y;
+    float r, g, b;
+    guide_of(bgrx[i], r, g, b);
+    const float p = cost[(size_t)s * N + i];
+    pl[(size_t)s * N + i] = p;
+    pl[(size_t)(S + s) * N + i] = r * p;
+    pl[(size_t)(2 * S + s) * N + i] = g * p;
+    pl[(size_t)(3 * S + s) * N + i] = b * p;
+}
+
+// means -> a_r, a_g, a_b, b (colorGuidedFilterHelper3 / 2 / 4), in place over the 4S planes
+__global__ void k_gf_ab(float* __restrict__ pl, const float* __restrict__ st, size_t N, int S) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const int s = blockIdx.y;
+    float* mp = pl + (size_t)s * N;
+    float* mIr = pl + (size_t)(S + s) * N;
+    float* mIg = pl + (size_t)(2 * S + s) * N;
+    float* mIb = pl + (size_t)(3 * S + s) * N;
+    const float m_p = mp[i];
+    const float mr = st[i], mg = st[N + i], mb = st[2 * N + i];
+    const float irr = st[3 * N + i], irg = st[4 * N + i], irb = st[5 * N + i];
+    const float igg = st[6 * N + i], igb = st[7 * N + i], ibb = st[8 * N + i];
+    const float cr = mIr[i] - mr * m_p;
+    const float cg = mIg[i] - mg * m_p;
+    const float cb = mIb[i] - mb * m_p;
+    const float ar = irr * cr + irg * cg + irb * cb;
+    const float ag = irg * cr + igg * cg + igb * cb;
+    const float ab = irb * cr + igb * cg + ibb * cb;
+    const float bb = m_p - ar * mr - ag * mg - ab * mb;
+    mIr[i] = ar;
+    mIg[i] = ag;
+    mIb[i] = ab;
+    mp[i] = bb;
+}
+
+// q = box(b) + box(a_r)*r + box(a_g)*g + box(a_b)*b (colorGuidedFilterHelper5), fused with the
+// strict-< WTA over the batch's slices in ascending order (selectDisparity), state per pixel:
+// min (1e10f), best (-1), pre / next of best (the parabola's neighbours), q of the previous slice
+struct GfState {
+    float* mn;
+    int32_t* best;
+    float* pre;
+    float* nxt;
+    float* prevq;
+};
+
+__global__ void k_gf_q_wta(const float* __restrict__ pl, const uint32_t* __restrict__ bgrx, GfState st, size_t N, int S,
+                           int dloc0, int dtot_loc) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    float r, g, b;
+    guide_of(bgrx[i], r, g, b);
+    float mn = st.mn[i], pre = st.pre[i], nxt = st.nxt[i], pq = st.prevq[i];
+    int best = st.best[i];
+    for (int s = 0; s < S; ++s) {
+        const int d = dloc0 + s;
+        const float q = pl[(size_t)s * N + i] + pl[(size_t)(S + s) * N + i] * r + pl[(size_t)(2 * S + s) * N + i] * g +
+                        pl[(size_t)(3 * S + s) * N + i] * b;
+        if (best >= 0 && best == d - 1) nxt = q;  // the winner's right neighbour (until replaced)
+        if (q < mn) {
+            mn = q;
+            best = d;
+            pre = d == 0 ? 0.0f : pq;
+            nxt = 0.0f;
+        }
+        pq = q;
+    }
+    (void)dtot_loc;
+    st.mn[i] = mn;
+    st.best[i] = best;
+    st.pre[i] = pre;
+    st.nxt[i] = nxt;
+    st.prevq[i] = pq;
+}
+
+// final maps: idx (global), min, disp with the optional parabola (0 at the total range's ends)
+__global__ void k_gf_out(GfState st, size_t N, int dglob0, int dtot, int sub, int32_t* __restrict__ idx,
+                         double* __restrict__ minc, float* __restrict__ disp) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const int best = st.best[i];
+    const float mn = st.mn[i];
+    minc[i] = (double)mn;
+    if (best < 0) {
+        idx[i] = 0;
+        disp[i] = 0.0f;
+        return;
+    }
+    const int g = dglob0 + best;
+    idx[i] = g;
+    float dd = (float)g;
+    if (sub) {
+        const float pre = g == 0 ? 0.0f : st.pre[i];
+        const float nxt = g == dtot - 1 ? 0.0f : st.nxt[i];
+        const float s = (nxt - pre) * 0.5f / (nxt - 2.0f * mn + pre);
+        if (fabsf(s) < 1.0f) dd = (float)g - s;
+    }
+    disp[i] = dd;
+}
+
+__global__ void k_gf_init(GfState st, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    st.mn[i] = 1e10f;
+    st.best[i] = -1;
+    st.pre[i] = 0.0f;
+    st.nxt[i] = 0.0f;
+    st.prevq[i] = 0.0f;
+}
+
+// ---------------------------------------------------------------------------------------------
+static dim3 pix_grid1(size_t N, int y = 1) { return dim3((unsigned)((N + 255) / 256), (unsigned)y); }
+
+static void box(hipStream_t st, const float* in, float* tmp, float* out, int W, int H, int r, int planes) {
+    const size_t N = (size_t)W * H;
+    hipLaunchKernelGGL(k_gf_box_x, dim3((H + 63) / 64, (W + GF_BLOCK - 1) / GF_BLOCK, planes), dim3(64), 0, st, in, tmp, W, H,
+                       r, N);
+    hipLaunchKernelGGL(k_gf_box_y, dim3((W + 255) / 256, (H + GF_BLOCK - 1) / GF_BLOCK, planes), dim3(256), 0, st, tmp, out, W,
+                       H, r, N);
+}
+
+hipError_t launch_gf_guide(hipStream_t st, const uint32_t* bgrx, int W, int H, int r, float eps, float* planes, float* tmp,
+                           float* means, float* stats) {
+    const size_t N = (size_t)W * H;
+    hipLaunchKernelGGL(k_gf_guide_in, pix_grid1(N), dim3(256), 0, st, bgrx, planes, N);
+    box(st, planes, tmp, means, W, H, r, 9);
+    hipLaunchKernelGGL(k_gf_stats, pix_grid1(N), dim3(256), 0, st, means, stats, N, eps);
+    return hipGetLastError();
+}
+
+hipError_t launch_gf_batch(hipStream_t st, const float* cost, const uint32_t* bgrx, const float* stats, int W, int H, int r,
+                           int S, int dloc0, float* pl, float* tmp, GfStateArgs sa) {
+    const size_t N = (size_t)W * H;
+    hipLaunchKernelGGL(k_gf_slice_in, pix_grid1(N, S), dim3(256), 0, st, cost, bgrx, pl, N, S);
+    box(st, pl, tmp, pl, W, H, r, 4 * S);   // means of p, r*p, g*p, b*p
+    hipLaunchKernelGGL(k_gf_ab, pix_grid1(N, S), dim3(256), 0, st, pl, stats, N, S);
+    box(st, pl, tmp, pl, W, H, r, 4 * S);   // box(b), box(a_r), box(a_g), box(a_b)
+    const GfState gs{sa.mn, sa.best, sa.pre, sa.nxt, sa.prevq};
+    hipLaunchKernelGGL(k_gf_q_wta, pix_grid1(N), dim3(256), 0, st, pl, bgrx, gs, N, S, dloc0, 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_gf_init(hipStream_t st, GfStateArgs sa, size_t N) {
+    const GfState gs{sa.mn, sa.best, sa.pre, sa.nxt, sa.prevq};
+    hipLaunchKernelGGL(k_gf_init, pix_grid1(N), dim3(256), 0, st, gs, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_gf_out(hipStream_t st, GfStateArgs sa, size_t N, int dglob0, int dtot, int sub, int32_t* idx, double* minc,
+                         float* disp) {
+    const GfState gs{sa.mn, sa.best, sa.pre, sa.nxt, sa.prevq};
+    hipLaunchKernelGGL(k_gf_out, pix_grid1(N), dim3(256), 0, st, gs, N, dglob0, dtot, sub, idx, minc, disp);
+    return hipGetLastError();
+}

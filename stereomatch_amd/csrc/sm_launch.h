@@ -103,6 +103,22 @@ hipError_t launch_zero(hipStream_t st, const ZeroList& z);
 hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok);
 hipError_t launch_vol_rows(hipStream_t st, const float* vin, size_t N, int d0, int D, int Dpad, const uint32_t* slotpix,
                            float* Cst);
+// guided-filter aggregator (sm_guided.hip): per-pixel WTA state of one view
+struct GfStateArgs {
+    float* mn;
+    int32_t* best;
+    float* pre;
+    float* nxt;
+    float* prevq;
+};
+hipError_t launch_gf_guide(hipStream_t st, const uint32_t* bgrx, int W, int H, int r, float eps, float* planes, float* tmp,
+                           float* means, float* stats);
+hipError_t launch_gf_batch(hipStream_t st, const float* cost, const uint32_t* bgrx, const float* stats, int W, int H, int r,
+                           int S, int dloc0, float* pl, float* tmp, GfStateArgs sa);
+hipError_t launch_gf_init(hipStream_t st, GfStateArgs sa, size_t N);
+hipError_t launch_gf_out(hipStream_t st, GfStateArgs sa, size_t N, int dglob0, int dtot, int sub, int32_t* idx, double* minc,
+                         float* disp);
+
 // output step (sm_post.hip)
 hipError_t launch_label_to_disp(hipStream_t st, float* d0, float* d1, size_t N, int dmax);
 hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int W, int H, int max_disp, uint8_t* mask);

@@ -768,3 +768,42 @@ def test_dpad32_volume_ingest_and_rows(gpu_ctx, monkeypatch):
         r = O.tree_filter(W, H, O.build_tree(img), vol, 5, False, True, 16)
         assert np.array_equal(bits(Aup), bits(r["Aup"]))
         assert np.array_equal(bits(A), bits(r["A"]))
+
+
+# ---- guided-filter aggregator (SM_AGG_GUIDED; PatchMatchStereoGPU.cu:8251-8470) ----
+@pytest.mark.parametrize("W,H,D,rad", [(160, 120, 32, 9), (203, 97, 48, 4), (70, 33, 40, 9), (256, 64, 100, 9)])
+@pytest.mark.parametrize("sub", [False, True])
+def test_guided_match_bitexact(gpu_ctx, W, H, D, rad, sub):
+    """The colour guided filter of the AGD cost (each view guided by its own image) + selectDisparity,
+    against the oracle's literal float restatement: indices, minima and disparities bitwise (ragged
+    32-pixel blocks, batches of 32 slices with a partial last one, radius 4 and 9)."""
+    import stereomatch_amd as sm
+    left, right, _ = make_pair(W, H, D, index=14)
+    post = sm.SM_POST_SUBPIXEL if sub else 0
+    out = gpu_ctx.match(left, right, D, sm.default_params(aggregator=sm.SM_AGG_GUIDED, gf_radius=rad, post=post))
+    ref = O.guided_match(left, right, D, radius=rad, sub=sub, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        np.testing.assert_array_equal(out[v]["minc"].ravel(), ref[v]["minc"].astype(np.float64))
+        np.testing.assert_array_equal(out[v]["disp"].ravel(), ref[v]["disp"])
+
+
+def test_guided_match_full_size_c2(gpu_ctx):
+    """1920x1200 D=128 through the guided aggregator, bitwise against the oracle."""
+    import stereomatch_amd as sm
+    W, H, D = 1920, 1200, 128
+    left, right, _ = make_pair(W, H, D, index=0)
+    out = gpu_ctx.match(left, right, D, sm.default_params(aggregator=sm.SM_AGG_GUIDED, post=sm.SM_POST_SUBPIXEL))
+    ref = O.guided_match(left, right, D, sub=True, nthreads=16)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        np.testing.assert_array_equal(out[v]["disp"].ravel(), ref[v]["disp"])
+
+
+def test_guided_errors(gpu_ctx):
+    import stereomatch_amd as sm
+    left, right, _ = make_pair(40, 30, 8)
+    for bad in (dict(gf_radius=0), dict(gf_eps=0.0), dict(cost_kind=sm.SM_COST_VOLUME),
+                dict(post=sm.SM_POST_SUBPIXEL, disp_begin=2, disp_total=16)):
+        with pytest.raises(sm.StereoMSTError):
+            gpu_ctx.match(left, right, 8, sm.default_params(aggregator=sm.SM_AGG_GUIDED, **bad))
