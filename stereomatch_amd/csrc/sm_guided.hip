@@ -21,6 +21,7 @@
 // are HBM-streaming kernels (no MFMA: per-pixel scalar arithmetic).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sm_launch.h"
 
@@ -43,6 +44,53 @@ __global__ __launch_bounds__(64) void k_gf_box_x(const float* __restrict__ in, f
         t += (x + r >= W) ? 0.0f : row[x + r];
         t -= (x - r - 1 < 0) ? 0.0f : row[x - r - 1];
         o[x] = t * scale;
+    }
+}
+
+// x pass through LDS: a workgroup stages `rows` whole rows of one plane (coalesced loads), each
+// thread runs one (row, 32-column block) sliding sum out of LDS -- the same operations in the same
+// order as k_gf_box_x -- and the results leave through LDS again as coalesced stores.  Rows are
+// padded by one float per 32 (index i + i/32), so the 64 lanes' block starts (stride 33) hit 64
+// different banks.  grid = (ceil(H / rows), planes).
+__global__ __launch_bounds__(256) void k_gf_box_x_lds(const float* __restrict__ in, float* __restrict__ out, int W, int H, int r,
+                                                      size_t N, int rows) {
+    extern __shared__ float lds[];
+    const int nblk = (W + GF_BLOCK - 1) / GF_BLOCK;
+    const int rl = W + nblk;  // padded row length
+    float* li = lds;
+    float* lo = lds + rows * rl;
+    const int ya = blockIdx.x * rows;
+    const int nr = H - ya < rows ? H - ya : rows;
+    const float* src = in + (size_t)blockIdx.y * N + (size_t)ya * W;
+    float* dst = out + (size_t)blockIdx.y * N + (size_t)ya * W;
+    const int tot = nr * W;
+    for (int i = threadIdx.x; i < tot; i += 256) {
+        const int y = i / W, x = i - y * W;
+        li[y * rl + x + (x >> 5)] = src[i];
+    }
+    __syncthreads();
+    const int t_id = threadIdx.x;
+    if (t_id < nr * nblk) {
+        const int y = t_id / nblk, blk = t_id - y * nblk;
+        const float* row = li + y * rl;
+        float* o = lo + y * rl;
+        const int x0 = blk * GF_BLOCK;
+        const float scale = 1.0f / (float)((r << 1) + 1);
+        float t = 0.0f;
+        for (int i = x0 - r; i <= x0 + r; ++i) t += (i < 0 || i >= W) ? 0.0f : row[i + (i >> 5)];
+        o[x0 + blk] = t * scale;
+        const int end = W - x0 < GF_BLOCK ? W : x0 + GF_BLOCK;
+        for (int x = x0 + 1; x < end; ++x) {
+            const int a = x + r, b = x - r - 1;
+            t += (a >= W) ? 0.0f : row[a + (a >> 5)];
+            t -= (b < 0) ? 0.0f : row[b + (b >> 5)];
+            o[x + blk] = t * scale;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < tot; i += 256) {
+        const int y = i / W, x = i - y * W;
+        dst[i] = lo[y * rl + x + (x >> 5)];
     }
 }
 
@@ -240,8 +288,17 @@ static dim3 pix_grid1(size_t N, int y = 1) { return dim3((unsigned)((N + 255) / 
 
 static void box(hipStream_t st, const float* in, float* tmp, float* out, int W, int H, int r, int planes) {
     const size_t N = (size_t)W * H;
-    hipLaunchKernelGGL(k_gf_box_x, dim3((H + 63) / 64, (W + GF_BLOCK - 1) / GF_BLOCK, planes), dim3(64), 0, st, in, tmp, W, H,
-                       r, N);
+    // x pass: the LDS kernel when two row tiles of at least one row fit in 64 KB (W <= 7943), else
+    // the direct one (same arithmetic)
+    const int nblk = (W + GF_BLOCK - 1) / GF_BLOCK;
+    int rows = 256 / nblk;
+    if (rows < 1) rows = 1;
+    while (rows > 1 && (size_t)2 * rows * (W + nblk) * 4 > 65536) --rows;
+    const size_t lds = (size_t)2 * rows * (W + nblk) * 4;
+    if (lds <= 65536 && getenv("SM_GF_DIRECT_X") == nullptr)
+        hipLaunchKernelGGL(k_gf_box_x_lds, dim3((H + rows - 1) / rows, planes), dim3(256), lds, st, in, tmp, W, H, r, N, rows);
+    else
+        hipLaunchKernelGGL(k_gf_box_x, dim3((H + 63) / 64, nblk, planes), dim3(64), 0, st, in, tmp, W, H, r, N);
     hipLaunchKernelGGL(k_gf_box_y, dim3((W + 255) / 256, (H + GF_BLOCK - 1) / GF_BLOCK, planes), dim3(256), 0, st, tmp, out, W,
                        H, r, N);
 }

@@ -800,6 +800,25 @@ def test_guided_match_full_size_c2(gpu_ctx):
         np.testing.assert_array_equal(out[v]["disp"].ravel(), ref[v]["disp"])
 
 
+def test_guided_direct_x_pass(gpu_ctx, monkeypatch):
+    """The direct x box pass (the path for rows too wide for the LDS tile) gives the same bits as the
+    LDS-tiled one; a 7 px wide and a 1 px high image exercise the tile edges."""
+    import stereomatch_amd as sm
+    for W, H, D in ((203, 97, 24), (7, 40, 4), (90, 1, 16)):
+        left, right, _ = make_pair(W, H, D, index=3)
+        p = sm.default_params(aggregator=sm.SM_AGG_GUIDED, gf_radius=5, post=sm.SM_POST_SUBPIXEL)
+        a = gpu_ctx.match(left, right, D, p)
+        monkeypatch.setenv("SM_GF_DIRECT_X", "1")
+        b = gpu_ctx.match(left, right, D, p)
+        monkeypatch.delenv("SM_GF_DIRECT_X")
+        ref = O.guided_match(left, right, D, radius=5, sub=True, nthreads=16)
+        for v in ("left", "right"):
+            np.testing.assert_array_equal(a[v]["idx"].ravel(), ref[v]["idx"])
+            np.testing.assert_array_equal(a[v]["disp"].ravel(), ref[v]["disp"])
+            np.testing.assert_array_equal(b[v]["idx"], a[v]["idx"])
+            np.testing.assert_array_equal(b[v]["disp"], a[v]["disp"])
+
+
 def test_guided_errors(gpu_ctx):
     import stereomatch_amd as sm
     left, right, _ = make_pair(40, 30, 8)
