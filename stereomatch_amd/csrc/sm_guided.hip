@@ -4,7 +4,7 @@
 // WTA :1688-1737; radius 9 and eps = 0.01^2 * 255^2 at :9000-9001).  A second aggregator behind the
 // same C-ABI (sm_params.aggregator = SM_AGG_GUIDED): no tree, no MST.
 //
-// Arithmetic (the reference's float operations in source order, uncontracted, DESIGN.md 4.8):
+// Arithmetic (the reference's float operations in source order, uncontracted, DESIGN.md 4.7):
 //   box mean  : per 32-pixel block (the reference kernels' block width) a sliding sum -- the first
 //               output sums in[x0-r .. x0+r] in ascending order (0 outside the image), then
 //               t += in[x+r]; t -= in[x-r-1]; out = t * (1.0f / (2r+1)) -- x pass, then y pass;
