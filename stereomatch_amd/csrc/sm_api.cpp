@@ -650,13 +650,13 @@ sm_status ensure_events(sm_ctx* ctx, std::vector<hipEvent_t>& evs, size_t n, uns
 }
 
 // kernel families of the tree filter and their algorithmic bytes per voxel (SURVEY.md 8(d):
-// K1 cost write 4 B, K2 up 8 B, K3 down 8 B, K4 WTA 4 B; DESIGN.md "Roofline accounting")
-// K1 of the long paths is k_long_costs when the costs are computed up front (then k_up_pre's
-// launches account no bytes), else k_up_pre
-enum { KF_UP_WALK, KF_UP_PRE, KF_UP_CHAIN, KF_DOWN_CHAIN, KF_DOWN_WALK, KF_LONG_COST, KF_N };
-const char* const kf_name[KF_N] = {"k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk", "k_long_costs"};
-const double kf_bytes[KF_N] = {12.0, 4.0, 8.0, 12.0, 12.0, 4.0};
-static bool kf_up(int f) { return f <= KF_UP_CHAIN || f == KF_LONG_COST; }
+// K1 cost write 4 B, K2 up 8 B, K3 down 8 B, K4 WTA 4 B; DESIGN.md "Roofline accounting").
+// Both up families compute the cost on the fly (K1 + K2); k_up_pre only folds the cut paths'
+// segment aggregates and accounts no bytes.
+enum { KF_UP_WALK, KF_UP_PRE, KF_UP_CHAIN, KF_DOWN_CHAIN, KF_DOWN_WALK, KF_N };
+const char* const kf_name[KF_N] = {"k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk"};
+const double kf_bytes[KF_N] = {12.0, 0.0, 12.0, 12.0, 12.0};
+static bool kf_up(int f) { return f <= KF_UP_CHAIN; }
 
 // A timed launch of family f on stream s.  HIP events bracket the launch, but consecutive timed
 // launches on the filter stream share the event between them (the end of one is the start of
@@ -730,7 +730,9 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
     set_bucket(ctx, a, r, true, nviews);
     const WalkArgs al = a;
     const double vl = bucket_voxels(ctx, r, true, nviews, a.dcall);
-    CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, al.pre_costs ? 0.0 : vl));
+    // segment aggregates: only buckets with a path cut into pieces need them
+    const bool cut = (al.pieces[0] || al.pieces[1]) && al.maxlen >= 2 * al.piece_len;
+    if (cut) CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, 0.0));
     CHECK(timed(ctx, ctx->st2, KF_UP_CHAIN, vl, [&] { return launch_up_chain(ctx->st2, al, spl); }));
     return SM_OK;
 }
@@ -754,7 +756,7 @@ sm_status ensure_filter_bufs(sm_ctx* ctx, int Dpad) {
     const size_t N = (size_t)ctx->W * ctx->H;
     for (int v = 0; v < 2; ++v) {
         CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
-        CHECK(ensure(ctx, ctx->Cst[v], N * (size_t)Dpad * 4));
+        if (ctx->use_vol) CHECK(ensure(ctx, ctx->Cst[v], N * (size_t)Dpad * 4));  // ingested cost rows only
         CHECK(ensure(ctx, ctx->idx[v], N * 4));
         CHECK(ensure(ctx, ctx->minc[v], N * 8));
         CHECK(ensure(ctx, ctx->disp[v], N * 4));
@@ -828,33 +830,6 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_st
     ctx->fam_vox.clear();
     ctx->fam_ev.clear();
     ctx->ev_open = false;
-    // AGD cost rows of every long-path slot in one launch up front (SM_NO_PRECOST: per round in
-    // k_up_pre, A/B).  Bucket slots are contiguous and bucket-major: long bucket 2r of a view starts
-    // after the nodes of all lower buckets.
-    a.pre_costs = 0;
-    const bool no_precost = getenv("SM_NO_PRECOST") != nullptr;  // read per call: tests switch it
-    if (!a.vol && !no_precost) {
-        CostRanges cr{};
-        for (int v = 0; v < nviews; ++v) {
-            const auto& L = ctx->layout[v];
-            uint32_t s0 = 0;
-            for (uint32_t b = 0; b < 2 * L.nrounds && b < (uint32_t)L.nodes.size(); ++b) {
-                if ((b & 1) == 0 && L.nodes[b] > 0 && cr.n < SM_COST_RANGES) {
-                    cr.view[cr.n] = (uint32_t)v;
-                    cr.start[cr.n] = s0;
-                    cr.len[cr.n] = L.nodes[b];
-                    ++cr.n;
-                }
-                s0 += L.nodes[b];
-            }
-        }
-        if (cr.n < SM_COST_RANGES) {  // else (> 31 rounds with long paths: never) k_up_pre computes them
-            double vox = 0;
-            for (int i = 0; i < cr.n; ++i) vox += (double)cr.len[i] * D;
-            CHECK(timed(ctx, ctx->st, KF_LONG_COST, vox, [&] { return launch_long_costs(ctx->st, a, spl, cr); }));
-            a.pre_costs = 1;
-        }
-    }
     for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest first
     CHECK(join(ctx, ctx->st, ctx->st2));
     HIPC(hipEventRecord(ctx->ev[6], ctx->st));  // up | down boundary (stage times)

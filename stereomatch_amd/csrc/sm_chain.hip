@@ -138,33 +138,29 @@ __device__ __forceinline__ void load_crow(const float* __restrict__ C, uint32_t 
         c[3] = t.w;
     }
 }
-template <int SPL>
-__device__ __forceinline__ void store_crow(float* __restrict__ C, uint32_t slot, int Dpad, int lane, const double (&c)[SPL]) {
-    float* p = C + (size_t)slot * Dpad + lane * SPL;
-    if constexpr (SPL == 1) {
-        if (lane < Dpad) p[0] = (float)c[0];
-    } else if constexpr (SPL == 2) {
-        *reinterpret_cast<float2*>(p) = make_float2((float)c[0], (float)c[1]);
-    } else {
-        *reinterpret_cast<float4*>(p) = make_float4((float)c[0], (float)c[1], (float)c[2], (float)c[3]);
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
-// k_up_pre: one block per SM_PRE_SEG-node segment of a long path (segment table from the layout),
-// SM_PRE_SEG / CH waves of CH nodes each; grid.y = view
+// k_up_pre: the per-segment affine aggregates of the long paths that are cut into pieces (the
+// pieces' guessed inputs, "Pieces" below).  One block per SM_PRE_SEG-node segment of the bucket's
+// long paths (segment table from the layout), SM_PRE_SEG / CH waves of CH nodes each; grid.y = view.
+// Segments of uncut paths return at once.  Nothing else of the up pass runs here: the chain
+// helpers fold the pre-heavy children and compute the costs themselves.
 // ---------------------------------------------------------------------------------------------
 template <int SPL, int CH, bool VOL>
 __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0, const uint32_t* __restrict__ meta1,
     const SmPath* __restrict__ paths0, const SmPath* __restrict__ paths1, const uint2* __restrict__ seg0,
-    const uint2* __restrict__ seg1, int nseg0, int nseg1, float* __restrict__ Cst0, float* __restrict__ Cst1,
+    const uint2* __restrict__ seg1, int nseg0, int nseg1, const float* __restrict__ Cst0, const float* __restrict__ Cst1,
     const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec, const float* __restrict__ atab_g,
     const double* __restrict__ slut_g, const double* __restrict__ s2lut_g, int W, int Dpad, int dcall, int dglob0,
     double* __restrict__ agg0, double* __restrict__ agg1, int piece_len) {
     constexpr int NW = SM_PRE_SEG / CH;
     const int view = blockIdx.y;
     if ((int)blockIdx.x >= (view ? nseg1 : nseg0)) return;  // uniform over the block
+    const uint2 sg = (view ? seg1 : seg0)[blockIdx.x];
+    const SmPath path = (view ? paths1 : paths0)[uniform(sg.x)];
+    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
+    double* __restrict__ agg = view ? agg1 : agg0;
+    if (agg == nullptr || len < 2 * piece_len) return;  // an uncut path: uniform over the block
     __shared__ WalkShared sh;
     __shared__ double aggsh[NW][2][64 * SPL];
     load_tables(sh, atab_g, slut_g, s2lut_g);
@@ -172,121 +168,58 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
     const int wv = (int)uniform(threadIdx.x >> 6);
-    const uint2 sg = (view ? seg1 : seg0)[blockIdx.x];
-    const SmPath path = (view ? paths1 : paths0)[uniform(sg.x)];
-    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
-    double* __restrict__ agg = view ? agg1 : agg0;
-    // segments of a path cut into pieces also produce the segment's affine aggregate (the piece
-    // chains' guessed inputs, "Pieces" below)
-    const bool agg_mode = agg != nullptr && len >= 2 * piece_len;
     const int first = (int)uniform(sg.y * SM_PRE_SEG + wv * CH);
-    if (first >= len && !agg_mode) return;
     const int n = max(0, min(CH, len - first));
     const int dbase = dglob0 + lane * SPL;
     const int dend = dglob0 + dcall;
     const uint2* __restrict__ own = view ? Rrec : Lrec;
     const uint2* __restrict__ oth = view ? Lrec : Rrec;
     double* __restrict__ U = V.U;
-    float* __restrict__ Cst = view ? Cst1 : Cst0;
-    double pre[CH][SPL], c[CH][SPL];
-    MetaVec<CH> mv;
-    if (n > 0) {
-        load_meta<CH>(mv, meta32, lane, head + first, 1, n);
-        // pre-heavy light child rows (positions 0 .. hidx-1): the first two issued together under
-        // wave-uniform branches (only present rows travel); a third one (hidx == 3, a four-child
-        // node whose heavy child is the last) is loaded where it is used
-        double lr[CH][2][SPL];
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const uint32_t hidx = j < n ? hi_hidx(mfield(mv, j, 3)) : 0u;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if ((uint32_t)i < hidx) {
-                    load_row<SPL>(U, mfield(mv, j, 4 + i), Dpad, lane, lr[j][i]);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < SPL; ++q) lr[j][i][q] = 0.0;
-                }
-            }
-        }
-        if constexpr (VOL) {  // cost rows already in Cst (k_vol_rows): needed by the aggregate only
-            if (agg_mode) {
-#pragma unroll
-                for (int j = 0; j < CH; ++j) {
-                    float t[SPL];
-                    load_cost_row<SPL>(Cst, (uint32_t)(head + first + (j < n ? j : n - 1)), Dpad, lane, t);
-#pragma unroll
-                    for (int k = 0; k < SPL; ++k) c[j][k] = t[k];
-                }
-            }
-        } else {
-            ImgRecs<SPL, CH> rec;
-            load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
-            chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
-        }
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            if (j < n) {
-                const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
-                const uint32_t hidx = hi_hidx(hi);
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) pre[j][k] = 0.0;
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    if ((uint32_t)i < hidx) {
-                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);  // uniform
-                        double r[SPL];
-                        if (i < 2) {
-#pragma unroll
-                            for (int k = 0; k < SPL; ++k) r[k] = lr[j][i][k];
-                        } else {
-                            load_row<SPL>(U, mfield(mv, j, 6), Dpad, lane, r);
-                        }
-#pragma unroll
-                        for (int k = 0; k < SPL; ++k) pre[j][k] = __builtin_fma(S, r[k], pre[j][k]);
-                    }
-                }
-                const uint32_t slot = (uint32_t)(head + first + j);
-                if (hidx > 0) store_row<SPL>(U, slot, Dpad, lane, pre[j]);  // Pre = 0 rows are never read
-                if constexpr (!VOL) store_crow<SPL>(Cst, slot, Dpad, lane, c[j]);
-            }
-        }
-    }
-    if (!agg_mode) return;
+    const float* __restrict__ Cst = view ? Cst1 : Cst0;
     // ---- affine aggregate of this wave's nodes (bottom up): x_first = P * x_below + B with
     // b = Pre + sum(S_post * A_post) + C and x = S_heavy * x_below + b.  Approximate (any rounding
-    // only moves the guess; the chains' results are repaired exactly), so no order constraint.
+    // only moves the guess; the chains' results are repaired exactly), so no order constraint; rows
+    // are loaded where used, to keep registers low (cut paths only: rare)
     double P[SPL], B[SPL];
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
         P[k] = 1.0;
         B[k] = 0.0;
     }
-    if (n > 0) {  // cut paths only (rare): post rows loaded where used, to keep registers low
+    if (n > 0) {
+        MetaVec<CH> mv;
+        load_meta<CH>(mv, meta32, lane, head + first, 1, n);
+        float c[CH][SPL];
+        if constexpr (VOL) {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) load_cost_row<SPL>(Cst, (uint32_t)(head + first + (j < n ? j : n - 1)), Dpad, lane, c[j]);
+        } else {
+            ImgRecs<SPL, CH> rec;
+            load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+            chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+        }
 #pragma unroll
         for (int j = CH - 1; j >= 0; --j) {
             if (j < n) {
                 const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
                 const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-                const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
                 const double Sh = nch > 0 ? readlane_f64(sh.slut[cw_of(lo, hi, (int)hidx)], 0) : 0.0;
                 double b[SPL];
 #pragma unroll
-                for (int k = 0; k < SPL; ++k) b[k] = pre[j][k];
+                for (int k = 0; k < SPL; ++k) b[k] = 0.0;
 #pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    if ((uint32_t)i < np) {
-                        const int pos = (int)min(hidx + 1u + (uint32_t)i, 3u);
-                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, pos)], 0);
+                for (int i = 0; i < 4; ++i) {  // every light child, in key order
+                    if ((uint32_t)i < nch && (uint32_t)i != hidx) {
+                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);
                         double r[SPL];
-                        load_row<SPL>(U, mfield(mv, j, 4 + pos), Dpad, lane, r);
+                        load_row<SPL>(U, mfield(mv, j, 4 + i), Dpad, lane, r);
 #pragma unroll
                         for (int k = 0; k < SPL; ++k) b[k] = __builtin_fma(S, r[k], b[k]);
                     }
                 }
 #pragma unroll
                 for (int k = 0; k < SPL; ++k) {
-                    B[k] = __builtin_fma(Sh, B[k], b[k] + c[j][k]);
+                    B[k] = __builtin_fma(Sh, B[k], b[k] + (double)c[j][k]);
                     P[k] = Sh * P[k];
                 }
             }
@@ -316,74 +249,6 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
             out[lane * SPL + k] = aggsh[0][0][lane * SPL + k];
             out[Dpad + lane * SPL + k] = aggsh[0][1][lane * SPL + k];
         }
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_long_costs: the AGD cost rows of every long-path slot of every round, in one launch before
-// the up pass (they depend on nothing but the images and the layout).  k_up_pre then only folds
-// the pre-heavy light children round by round, and the chain helpers read the rows as before.
-// One block = 4 waves x CH consecutive slots of one range.
-// ---------------------------------------------------------------------------------------------
-template <int SPL, int CH>
-__global__ __launch_bounds__(256) void k_long_costs(const uint32_t* __restrict__ meta0, const uint32_t* __restrict__ meta1,
-                                                    const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec,
-                                                    const float* __restrict__ atab_g, int W, int Dpad, int dcall, int dglob0,
-                                                    float* __restrict__ Cst0, float* __restrict__ Cst1, CostRanges R) {
-    __shared__ float atab[SM_MAX_W + 1];
-    for (int i = threadIdx.x; i <= SM_MAX_W; i += blockDim.x) atab[i] = atab_g[i];
-    __syncthreads();
-    int ri = 0;
-    while (ri + 1 < R.n && R.bfirst[ri + 1] <= blockIdx.x) ++ri;  // uniform
-    const int view = (int)R.view[ri];
-    const int lane = threadIdx.x & 63, wv = (int)uniform(threadIdx.x >> 6);
-    const uint32_t off = (blockIdx.x - R.bfirst[ri]) * (4 * CH) + (uint32_t)(wv * CH);
-    if (off >= R.len[ri]) return;
-    const int first = (int)(R.start[ri] + off);
-    const int n = (int)min((uint32_t)CH, R.len[ri] - off);
-    const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
-    const uint2* __restrict__ own = view ? Rrec : Lrec;
-    const uint2* __restrict__ oth = view ? Lrec : Rrec;
-    float* __restrict__ Cst = view ? Cst1 : Cst0;
-    const int dbase = dglob0 + lane * SPL, dend = dglob0 + dcall;
-    MetaVec<CH> mv;
-    load_meta<CH>(mv, meta32, lane, first, 1, n);
-    ImgRecs<SPL, CH> rec;
-    load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
-    float c[CH][SPL];
-    chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, atab, c);
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        if (j < n) {
-            float* p = Cst + (size_t)(first + j) * Dpad + lane * SPL;
-            if (row_lane<SPL>(lane, Dpad))
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) p[k] = c[j][k];
-        }
-    }
-}
-
-template <int SPL, int CH>
-static void long_costs_launch(hipStream_t st, const WalkArgs& a, const CostRanges& r, unsigned nblocks) {
-    hipLaunchKernelGGL((k_long_costs<SPL, CH>), dim3(nblocks), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(a.meta[0]),
-                       reinterpret_cast<const uint32_t*>(a.meta[1]), a.Lrec, a.Rrec, a.atab, a.W, a.Dpad, a.dcall, a.dglob0,
-                       a.Cst[0], a.Cst[1], r);
-}
-
-hipError_t launch_long_costs(hipStream_t st, const WalkArgs& a, int spl, CostRanges r) {
-    const int ch = spl == 4 ? 4 : 8;  // nodes per wave
-    uint32_t nb = 0;
-    for (int i = 0; i < r.n; ++i) {
-        r.bfirst[i] = nb;
-        nb += (r.len[i] + 4u * ch - 1) / (4u * ch);
-    }
-    r.bfirst[r.n] = nb;
-    if (nb == 0) return hipSuccess;
-    switch (spl) {
-        case 1: long_costs_launch<1, 8>(st, a, r, nb); break;
-        case 2: long_costs_launch<2, 8>(st, a, r, nb); break;
-        default: long_costs_launch<4, 4>(st, a, r, nb); break;
-    }
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -462,18 +327,18 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 #define UP_NS2 9
 #endif
 #ifndef UP_G4
-#define UP_G4 3
+#define UP_G4 2
 #endif
 #ifndef UP_NS4
-#define UP_NS4 6
+#define UP_NS4 8
 #endif
 #ifndef UP_G2
 #define UP_G2 4  // even: the chain's two-half pipeline
 #endif
 template <int SPL>
 struct UpCfg {
-    static constexpr int G = SPL == 1 ? 8 : SPL == 2 ? UP_G2 : UP_G4;  // nodes per group (helper registers)
-    static constexpr int NS = SPL == 1 ? 8 : SPL == 2 ? UP_NS2 : UP_NS4;  // LDS slots (~140 KB)
+    static constexpr int G = SPL == 1 ? 6 : SPL == 2 ? UP_G2 : UP_G4;  // nodes per group (helper registers)
+    static constexpr int NS = SPL == 1 ? 10 : SPL == 2 ? UP_NS2 : UP_NS4;  // LDS slots (~140 KB)
 };
 
 struct UpNodeS {
@@ -511,6 +376,17 @@ template <int SPL>
 struct UpRing {
     UpSlot<SPL> s[UpCfg<SPL>::NS];
     double slut[SM_NUM_W + 1];
+    float atab[SM_MAX_W + 1];  // AGD colour term by integer L1 (helpers compute the cost rows)
+};
+
+// where the up chain's cost rows come from: computed by the helpers from the image records (the
+// AGD cost, PatchMatchStereoGPU.cu:1482-1550), or read from the f32 rows k_vol_rows filled
+// (MC-CNN ingest)
+struct UpCost {
+    const uint2* own;  // the view's reference image records
+    const uint2* oth;  // the matched image's records
+    const float* Cst;  // cost rows [slot][Dpad] (ingest)
+    int W, dbase, dend, view;
 };
 
 // NN consecutive nodes k0.. of a staged group; NN is a compile-time count so the LDS waits are
@@ -710,12 +586,19 @@ __device__ __forceinline__ void up_chain_wave(UpRing<SPL>& ring, int w, int head
 
 // Helper waves: every global load of a group is unconditional (indices clamped, absent children
 // read the path head's rows as L2-resident dummies), so the compiler's vmcnt bookkeeping stays
-// exact and the loads stay in flight while the helper waits for its slot.
-template <int SPL>
+// exact and the loads stay in flight while the helper waits for its slot.  Per node a helper loads
+// the light children's rows (at most two; a tree root's third through one row per group) and the
+// image records, and computes off the chain, in registers:
+//   Pre = the fold of the light children before the heavy one, from +0 in key order
+//         (Stereo3DMST.cpp:125-137: acc = fma(S_c, A_up(c), acc));
+//   C   = the AGD cost of the node's slices (or its ingested cost row);
+// then stages Pre, the post-heavy rows, C and the weights into the slot.  Nothing of the up pass
+// makes an HBM round trip other than the A_up rows themselves.
+template <int SPL, bool AGD>
 __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int head, int len, int lane,
                                                const uint32_t* __restrict__ meta32, double* __restrict__ U,
-                                               const float* __restrict__ Cst, int Dpad, bool lower,
-                                               uint32_t* done_word, uint32_t epoch) {
+                                               const UpCost& cs, int Dpad, bool lower, uint32_t* done_word,
+                                               uint32_t epoch) {
     constexpr int G = UpCfg<SPL>::G, NS = UpCfg<SPL>::NS;
     constexpr int NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
     const int top = head + len - 1;
@@ -731,29 +614,30 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
     MetaVec<G> mv, mnext;
     meta_of(mv, g);
     meta_of(mnext, g + NH);
-    double pr[G][SPL], p1[G][SPL], p2[G][SPL], p3[SPL];
+    // light children of node k in key order: l0, l1; a third one (only a tree root with four
+    // children) in l2 -- at most one such node per group
+    double l0[G][SPL], l1[G][SPL], l2[SPL];
     float cr[G][SPL];
-    // a group's row loads (all unconditional: indices clamped, absent children read the path
-    // head's rows as L2-resident dummies)
+    ImgRecs<SPL, G> rec;
     auto issue = [&](int gg, const MetaVec<G>& m) {
         const int n = min(G, len - gg * G);
-        uint32_t s3 = (uint32_t)head;
+        uint32_t s2 = (uint32_t)head;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const int kk = min(k, n - 1);
             const uint32_t slot = (uint32_t)(top - (gg * G + kk));
             const uint32_t hi = mfield(m, kk, 3);
             const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-            const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
-            load_row<SPL>(U, hidx > 0 ? slot : (uint32_t)head + 2u, Dpad, lane, pr[k]);  // Pre rows exist iff hidx > 0
-            load_crow<SPL>(Cst, slot, Dpad, lane, cr[k]);
-            const uint32_t c1 = np >= 1 ? mfield(m, kk, 4 + (int)min(hidx + 1u, 3u)) : (uint32_t)head;
-            const uint32_t c2 = np >= 2 ? mfield(m, kk, 4 + (int)min(hidx + 2u, 3u)) : (uint32_t)head + 1u;
-            load_row<SPL>(U, c1, Dpad, lane, p1[k]);
-            load_row<SPL>(U, c2, Dpad, lane, p2[k]);
-            if (np >= 3) s3 = mfield(m, kk, 7);
+            const uint32_t nl = nch > 0 ? nch - 1u : 0u;
+            const uint32_t c0 = nl >= 1 ? mfield(m, kk, hidx == 0 ? 5 : 4) : (uint32_t)head;
+            const uint32_t c1 = nl >= 2 ? mfield(m, kk, hidx <= 1 ? 6 : 5) : (uint32_t)head + 1u;
+            load_row<SPL>(U, c0, Dpad, lane, l0[k]);
+            load_row<SPL>(U, c1, Dpad, lane, l1[k]);
+            if constexpr (!AGD) load_crow<SPL>(cs.Cst, slot, Dpad, lane, cr[k]);
+            if (nl >= 3) s2 = mfield(m, kk, hidx == 3 ? 6 : 7);
         }
-        load_row<SPL>(U, s3, Dpad, lane, p3);
+        load_row<SPL>(U, s2, Dpad, lane, l2);
+        if constexpr (AGD) load_recs<SPL, G>(m, n, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
     };
     issue(g, mv);
     for (;;) {
@@ -784,6 +668,30 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
         meta_of(mnn, g + 2 * NH);
         const int gn = g + NH;
         const int gl = gn < ngroups ? gn : g;
+        // ---- Pre and C of the group (registers; the loads have landed by now in all but the
+        // first group, whose wait is here)
+        if constexpr (AGD) chunk_costs<SPL, G>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, ring.atab, cr);
+        // Pre replaces l0 (with hidx >= 1 the first light child is a pre-heavy one, folded here)
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const uint32_t lo = mfield(mv, k, 2), hi = mfield(mv, k, 3);
+            const uint32_t hidx = hi_hidx(hi);
+            if (hidx >= 1) {  // uniform: positions 0 .. hidx-1 are the light children l0, l1, l2
+                const double S0 = ring.slut[cw_of(lo, hi, 0)];
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) l0[k][q] = __builtin_fma(S0, l0[k][q], 0.0);
+                if (hidx >= 2) {
+                    const double S1 = ring.slut[cw_of(lo, hi, 1)];
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) l0[k][q] = __builtin_fma(S1, l1[k][q], l0[k][q]);
+                    if (hidx >= 3) {
+                        const double S2 = ring.slut[cw_of(lo, hi, 2)];
+#pragma unroll
+                        for (int q = 0; q < SPL; ++q) l0[k][q] = __builtin_fma(S2, l2[q], l0[k][q]);
+                    }
+                }
+            }
+        }
         // ---- wait for the slot, fill it, publish
         UpSlot<SPL>& sl = ring.s[g % NS];
         if (g >= NS) lds_wait(&sl.freed, g - NS + 1, true);
@@ -791,16 +699,30 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
         for (int k = 0; k < G; ++k) {
             if (k < n) {
                 const uint32_t f = flags >> (3 * k);
-                if (f & UP_F_PRE) lds_row_write<SPL>(sl.pre[k], lane, pr[k]);
-                if (f & UP_F_P1) lds_row_write<SPL>(sl.post1[k], lane, p1[k]);
-                if (f & UP_F_P2) lds_row_write<SPL>(sl.post2[k], lane, p2[k]);
+                const uint32_t hidx = hi_hidx(mfield(mv, k, 3));
+                if (f & UP_F_PRE) lds_row_write<SPL>(sl.pre[k], lane, l0[k]);
+                // post-heavy rows: the light children from index hidx on
+                if (f & UP_F_P1) {
+                    if (hidx == 0)
+                        lds_row_write<SPL>(sl.post1[k], lane, l0[k]);
+                    else if (hidx == 1)
+                        lds_row_write<SPL>(sl.post1[k], lane, l1[k]);
+                    else
+                        lds_row_write<SPL>(sl.post1[k], lane, l2);
+                }
+                if (f & UP_F_P2) {
+                    if (hidx == 0)
+                        lds_row_write<SPL>(sl.post2[k], lane, l1[k]);
+                    else
+                        lds_row_write<SPL>(sl.post2[k], lane, l2);
+                }
 #pragma unroll
                 for (int q = 0; q < SPL; ++q) sl.c[k][lane * SPL + q] = cr[k][q];
                 if (lane < 3) (&sl.s[k].Sh)[lane] = Sl[k];
             }
         }
-        if (k3 >= 0) {
-            lds_row_write<SPL>(sl.post3, lane, p3);
+        if (k3 >= 0) {  // a third post-heavy child: hidx == 0 and three light children
+            lds_row_write<SPL>(sl.post3, lane, l2);
             flags |= UP_F3;
         }
         if (lane == 0) {
@@ -959,12 +881,12 @@ __device__ void up_guess(double* scratch, double* guess, const double* __restric
 // CHR nodes: the next batch's metadata is in flight during a batch, the first light child row of
 // every node is loaded with the batch, further light children (rare) on demand.
 #ifndef UP_WALK_CH
-#define UP_WALK_CH(SPL) ((SPL) == 4 ? 4 : 8)  // nodes per repair batch (registers)
+#define UP_WALK_CH(SPL) ((SPL) == 4 ? 2 : 4)  // nodes per repair batch (registers: the image records)
 #endif
-template <int SPL, int CHR>
+template <int SPL, int CHR, bool AGD>
 __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32, double* __restrict__ U,
-                                          const float* __restrict__ Cst, const double* slut, int top, int nmax, int Dpad,
-                                          int lane, double* xio, double* __restrict__ fix, bool write) {
+                                          const UpCost& cs, const double* slut, const float* atab, int top, int nmax,
+                                          int Dpad, int lane, double* xio, double* __restrict__ fix, bool write) {
     double x[SPL];
 #pragma unroll
     for (int q = 0; q < SPL; ++q) x[q] = xio[q];
@@ -977,6 +899,7 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
         load_meta<CHR>(mn, meta32, lane, top - n1, -1, min(CHR, nmax - n1));
         double spec[CHR][SPL], r0[CHR][SPL];
         float cr[CHR][SPL];
+        ImgRecs<SPL, CHR> rec;
 #pragma unroll
         for (int k = 0; k < CHR; ++k) {
             const int kk = min(k, nb - 1);
@@ -984,8 +907,12 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
             const uint32_t hi = mfield(mv, kk, 3);
             const int nch = (int)hi_nch(hi), hidx = (int)hi_hidx(hi);
             load_row<SPL>(U, nch >= 2 ? mfield(mv, kk, hidx > 0 ? 4 : 5) : slot, Dpad, lane, r0[k]);  // first light child
-            load_crow<SPL>(Cst, slot, Dpad, lane, cr[k]);
+            if constexpr (!AGD) load_crow<SPL>(cs.Cst, slot, Dpad, lane, cr[k]);
             agent_row_read<SPL>(U, slot, Dpad, lane, spec[k]);  // own piece's rows (this launch)
+        }
+        if constexpr (AGD) {
+            load_recs<SPL, CHR>(mv, nb, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
+            chunk_costs<SPL, CHR>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, atab, cr);
         }
 #pragma unroll
         for (int k = 0; k < CHR; ++k) {
@@ -1040,10 +967,10 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
 // "merged" iff its repair met the stored trajectory below its top node, i.e. its top row (the
 // next piece's input) never changes; every input of a piece is then exact iff all pieces below
 // merged.
-template <int SPL>
+template <int SPL, bool AGD>
 __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restrict__ meta32, double* __restrict__ U,
-                          double* __restrict__ fix, const float* __restrict__ Cst, int Dpad, int lane, int head, int len,
-                          int j, int M, int e, const PieceView& Q, uint32_t epoch) {
+                          double* __restrict__ fix, const UpCost& cs, int Dpad, int lane, int head, int len, int j, int M,
+                          int e, const PieceView& Q, uint32_t epoch) {
     uint32_t* done = Q.stat;
     uint32_t* merged = Q.stat + Q.stride;
     uint32_t* fin = Q.stat + 2 * Q.stride;
@@ -1061,12 +988,12 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     agent_row_read<SPL>(U, below, Dpad, lane, x);
     vm_drain();
     if (Q.dbg && Q.dbg[15] == 1) {  // probe (SM_PIECE_DEBUG=2): merge distance histogram, no writes
-        const int mp = up_exact_walk<SPL, UP_WALK_CH(SPL)>(meta32, U, Cst, ring.slut, top, len, Dpad, lane, x, nullptr, false);
+        const int mp = up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, len, Dpad, lane, x, nullptr, false);
         int b = 8;  // 8: < 8 nodes, 9: < 16, ... 13: >= 128 (merged), 14: never merged
         while (b < 13 && mp >= (8 << (b - 8))) ++b;
         if (lane == 0) atomicAdd(Q.dbg + (mp < 0 ? 14 : b), 1ull);
     }
-    const int m = up_exact_walk<SPL, UP_WALK_CH(SPL)>(meta32, U, Cst, ring.slut, top, min(Q.rmax, len), Dpad, lane, x, fix, true);
+    const int m = up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, min(Q.rmax, len), Dpad, lane, x, fix, true);
     if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
     bool all = m >= 0;
     for (int q = e - 1; all && q > e - (M - 1 - j); --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u, Q.err, Q.wait_iters) == 2u * epoch;
@@ -1092,17 +1019,19 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     vm_drain();
     agent_row_read<SPL>(U, below, Dpad, lane, x);
     vm_drain();
-    up_exact_walk<SPL, UP_WALK_CH(SPL)>(meta32, U, Cst, ring.slut, top, len, Dpad, lane, x, nullptr, true);
+    up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, len, Dpad, lane, x, nullptr, true);
     vm_drain();
     if (lane == 0) publish_word(fin + e, epoch);
 }
 
-template <int SPL>
+template <int SPL, bool AGD>
 __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                           const uint32_t* __restrict__ meta1,
                                                           const SmPath* __restrict__ paths0,
                                                           const SmPath* __restrict__ paths1,
                                                           const float* __restrict__ Cst0, const float* __restrict__ Cst1,
+                                                          const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec,
+                                                          const float* __restrict__ atab_g, int W, int dcall, int dglob0,
                                                           const double* __restrict__ slut_g, int Dpad, PieceView Q0,
                                                           PieceView Q1, uint32_t epoch) {
     __shared__ UpRing<SPL> ring;
@@ -1153,19 +1082,29 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     // zero the ring: rows a helper does not stage are then always finite (see up_group)
     for (int i = threadIdx.x; i < (int)(sizeof(ring.s) / 4); i += CHN_THREADS) reinterpret_cast<uint32_t*>(ring.s)[i] = 0u;
     for (int i = threadIdx.x; i < SM_NUM_W; i += CHN_THREADS) ring.slut[i] = slut_g[i];
+    if constexpr (AGD)
+        for (int i = threadIdx.x; i <= SM_MAX_W; i += CHN_THREADS) ring.atab[i] = atab_g[i];
     if (threadIdx.x == 0) {
         ring.slut[SM_NUM_W] = 0.0;
         hdone = 0;
     }
     __syncthreads();
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
+    UpCost cs;
+    cs.own = view ? Rrec : Lrec;
+    cs.oth = view ? Lrec : Rrec;
+    cs.Cst = view ? Cst1 : Cst0;
+    cs.W = W;
+    cs.dbase = dglob0 + lane * SPL;
+    cs.dend = dglob0 + dcall;
+    cs.view = view;
     if (wave < Split<SPL>::NCW) {
         up_chain_wave<SPL>(ring, wave, head, len, lane, V.U, Dpad, lower ? guess : nullptr);
         if (wave == 0 && M > 1)
-            up_finish<SPL>(ring, &hdone, meta32, V.U, Q.fix, view ? Cst1 : Cst0, Dpad, lane, head, len, j, M, e, Q, epoch);
+            up_finish<SPL, AGD>(ring, &hdone, meta32, V.U, Q.fix, cs, Dpad, lane, head, len, j, M, e, Q, epoch);
     } else if (Split<SPL>::helper_of(wave) >= 0) {
-        up_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V.U, view ? Cst1 : Cst0, Dpad, lower,
-                            j > 0 ? Q.stat + e : nullptr, epoch);
+        up_helper_wave<SPL, AGD>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V.U, cs, Dpad, lower,
+                                 j > 0 ? Q.stat + e : nullptr, epoch);
         vm_drain();  // this helper's stores are complete before the repair reads or overwrites them
         if (lane == 0) atomicAdd(&hdone, 1);
     }
@@ -1751,7 +1690,7 @@ static void up_pre_launch_k(hipStream_t st, const WalkArgs& a) {
 
 template <int SPL, int CH>
 static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
-    if (a.vol || a.pre_costs)  // cost rows already in Cst
+    if (a.vol)  // cost rows in Cst (k_vol_rows)
         up_pre_launch_k<SPL, CH, true>(st, a);
     else
         up_pre_launch_k<SPL, CH, false>(st, a);
@@ -1762,12 +1701,19 @@ static PieceView piece_view(const WalkArgs& a, int v) {
                      a.err, a.wait_iters};
 }
 
+template <int SPL, bool AGD>
+static void up_chain_launch_k(hipStream_t st, const WalkArgs& a, int np) {
+    hipLaunchKernelGGL((k_up_chain<SPL, AGD>), dim3(np, 2), dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
+                       reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                       a.paths[0], a.paths[1], a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.atab, a.W, a.dcall, a.dglob0, a.slut,
+                       a.Dpad, piece_view(a, 0), piece_view(a, 1), a.epoch);
+}
 template <int SPL>
 static void up_chain_launch(hipStream_t st, const WalkArgs& a, int np) {
-    hipLaunchKernelGGL((k_up_chain<SPL>), dim3(np, 2), dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
-                       reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.Cst[0], a.Cst[1], a.slut, a.Dpad, piece_view(a, 0), piece_view(a, 1),
-                       a.epoch);
+    if (a.vol)
+        up_chain_launch_k<SPL, false>(st, a, np);
+    else
+        up_chain_launch_k<SPL, true>(st, a, np);
 }
 
 template <int SPL>

@@ -66,7 +66,6 @@ struct WalkArgs {
     const double* s2lut;
     float* Cst[2];       // cost rows [slot][Dpad]: long-path AGD staging, or every slot's volume row
     int vol;             // costs from Cst rows (MC-CNN ingest, k_vol_rows) instead of the AGD cost
-    int pre_costs;       // long-path AGD cost rows already in Cst (k_long_costs): k_up_pre reads them
     int maxlen;          // longest path of the current bucket (both views)
     const uint2* segtab[2];  // long buckets: {path, segment} per SM_PRE_SEG-node segment
     int nseg[2];
@@ -127,16 +126,9 @@ hipError_t launch_occlusion(hipStream_t st, float* left, float* right, int W, in
                             uint8_t* occ, int* scratch);
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
-// long-path engine (sm_chain.hip): buckets of paths with >= SM_LONG_PATH nodes
+// long-path engine (sm_chain.hip): buckets of paths with >= SM_LONG_PATH nodes; k_up_pre only
+// computes the segment aggregates of paths cut into pieces
 hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl);
-// slot ranges of the long-path buckets of both views (bucket slots are contiguous, bucket-major)
-#define SM_COST_RANGES 64
-struct CostRanges {
-    int n;
-    uint32_t view[SM_COST_RANGES], start[SM_COST_RANGES], len[SM_COST_RANGES];
-    uint32_t bfirst[SM_COST_RANGES + 1];  // first block of each range (filled by launch_long_costs)
-};
-hipError_t launch_long_costs(hipStream_t st, const WalkArgs& a, int spl, CostRanges r);
 hipError_t launch_up_chain(hipStream_t st, const WalkArgs& a, int spl);
 hipError_t launch_down_long(hipStream_t st, const WalkArgs& a, int spl, int store_all);
 hipError_t launch_down_debug(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);

@@ -86,7 +86,11 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
         for (int k = 0; k < 2; ++k) {
             const uint32_t i = (uint32_t)k + ((uint32_t)k >= hidx ? 1u : 0u);  // child position of light slot k
             // wave-uniform branch: only present rows travel through L1 (~70% of nodes have none)
+#ifdef SM_EXP_UP_NO_LIGHT  // timing experiment only (wrong results): no light-child row loads
+            if (false) {
+#else
             if (j < n && i < nch) {
+#endif
                 load_row<SPL>(U, mfield(mv, jj, 4 + (int)min(i, 3u)), Dpad, lane, lr[j][k]);
             } else {
 #pragma unroll
@@ -103,6 +107,14 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
         if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);
         walk_vm_drain();
     } else {
+#ifdef SM_EXP_UP_NO_COST  // timing experiment only (wrong results): no image records, constant cost
+        if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);
+        walk_vm_drain();
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) c[j][k] = 0.25f;
+#else
         ImgRecs<SPL, CH> rec;
         load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
         // the next chunk's metadata, issued behind this chunk's loads: it completes with them, so
@@ -111,6 +123,7 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
         if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);
         walk_vm_drain();
         chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+#endif
     }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
@@ -319,7 +332,13 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
         double mn;
         int gi;
         float dsp;
+#ifdef SM_EXP_DN_NO_WTA  // timing experiment only (wrong results): no WTA reduction
+        mn = xs[0][0];
+        gi = 0;
+        dsp = 0.0f;
+#else
         wta_nodes<SPL, CH>(xs, lane, w, mn, gi, dsp);
+#endif
         const uint32_t pix = meta_pix_of_lane<CH>(cur, lane);  // all lanes active: bpermute sources
         if (lane < n) {  // lane j stores node j's result
             V.idx[pix] = gi;

@@ -143,23 +143,19 @@ def test_pieces_rows_bitexact(gpu_ctx, monkeypatch, plen, rmax):
 
 
 @pytest.mark.parametrize("plen", ["64", "512"])
-def test_long_costs_modes_bitexact(gpu_ctx, monkeypatch, plen):
-    """Long-path AGD costs computed up front (k_long_costs, default) or per round inside k_up_pre
-    (SM_NO_PRECOST=1): both bit-exact against the oracle, cut paths (aggregates read the cost
-    rows) included."""
+@pytest.mark.parametrize("D", [32, 64, 100, 200])
+def test_chain_helper_costs_bitexact(gpu_ctx, monkeypatch, plen, D):
+    """The up chain's helpers fold the pre-heavy children and compute the AGD cost rows from the
+    image records themselves (SPL 1, 2, 4; 32-double rows at D=32): bit-exact against the oracle,
+    cut paths (k_up_pre's aggregates and the repair walks compute costs too) included."""
     monkeypatch.setenv("SM_PIECE_LEN", plen)
-    W, H, D = 400, 300, 64
+    W, H = 400, 300
     left, right, _ = make_pair(W, H, D, index=6)
     ref = O.match(left, right, D, nthreads=16)
-    for mode in ("precost", "inline"):
-        if mode == "inline":
-            monkeypatch.setenv("SM_NO_PRECOST", "1")
-        else:
-            monkeypatch.delenv("SM_NO_PRECOST", raising=False)
-        out = gpu_ctx.match(left, right, D)
-        for v in ("left", "right"):
-            np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
-            assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+    out = gpu_ctx.match(left, right, D)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
 
 
 def test_kernel_timing_mask(gpu_ctx):

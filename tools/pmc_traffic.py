@@ -15,7 +15,7 @@ import json
 import sys
 from collections import defaultdict
 
-FAMILIES = ["k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk", "k_long_costs", "k_median"]
+FAMILIES = ["k_up_walk", "k_up_pre", "k_up_chain", "k_down_chain", "k_down_walk", "k_median"]
 
 
 
