@@ -335,6 +335,9 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 #ifndef UP_G2
 #define UP_G2 4  // even: the chain's two-half pipeline
 #endif
+#ifndef UP_STORERS
+#define UP_STORERS 2  // helper waves that only store the chain's results (the others load and stage)
+#endif
 template <int SPL>
 struct UpCfg {
     static constexpr int G = SPL == 1 ? 6 : SPL == 2 ? UP_G2 : UP_G4;  // nodes per group (helper registers)
@@ -600,20 +603,64 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
                                                const UpCost& cs, int Dpad, bool lower, uint32_t* done_word,
                                                uint32_t epoch) {
     constexpr int G = UpCfg<SPL>::G, NS = UpCfg<SPL>::NS;
-    constexpr int NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
+    constexpr int NCW = Split<SPL>::NCW;
+    constexpr int NST = UP_STORERS, NL = Split<SPL>::NH - NST;  // storer / loader waves
     const int top = head + len - 1;
     const int ngroups = (len + G - 1) / G;
+    if (hh >= NL) {
+        // ---- storer: the chain's results of groups hh - NL (mod NST) go back to U, then the slot
+        // is freed.  Its waves hold no loads, so its stores never delay a loader's load wait (gfx9
+        // counts loads and stores in one vmcnt: a wave with both pending must wait for all of them)
+#ifdef SM_CHAIN_PROF
+        long long h_done = 0, h_t0 = clock64();
+#endif
+        for (int g = hh - NL; g < ngroups; g += NST) {
+            const int n = min(G, len - g * G);
+            UpSlot<SPL>& sl = ring.s[g % NS];
+#ifdef SM_CHAIN_PROF
+            long long h_d = clock64();
+#endif
+            lds_wait_all(sl.done, NCW, g + 1);
+#ifdef SM_CHAIN_PROF
+            h_done += clock64() - h_d;
+#endif
+#pragma unroll
+            for (int k = 0; k < G; ++k) {  // unconditional (clamped rows are stored twice, same value)
+                double xr[SPL];
+                lds_row_read<SPL>(sl.pre[min(k, n - 1)], lane, xr);
+                store_row<SPL>(U, (uint32_t)(top - (g * G + min(k, n - 1))), Dpad, lane, xr);
+            }
+            if (done_word && g == ngroups - 1) {
+                // the piece's top row is the next piece's input: written through at device scope,
+                // then its done word
+                double xr[SPL];
+                lds_row_read<SPL>(sl.pre[n - 1], lane, xr);
+                double* row = U + (size_t)head * Dpad + lane * SPL;
+                if (row_lane<SPL>(lane, Dpad))
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vm_drain();
+                if (lane == 0) publish_word(done_word, epoch);
+            }
+            lds_publish(&sl.freed, g + 1);  // the rows are in flight from registers
+        }
+#ifdef SM_CHAIN_PROF
+        if (blockIdx.x == 0 && lane == 0 && hh == NL)
+            printf("up storer view %d len %d cycles %lld done %lld\n", (int)blockIdx.y, len, clock64() - h_t0, h_done);
+#endif
+        return;
+    }
+    // ---- loader: groups hh, hh + NL, ...
     int g = hh;
     if (g >= ngroups) return;
-    // meta runs two groups ahead of the rows: the rows of group g + NH are issued from meta that
-    // was loaded before this group's stores, so their address wait never waits on stores
+    // meta runs two groups ahead of the rows
     auto meta_of = [&](MetaVec<G>& m, int gg) {
         const int gc = gg < ngroups ? gg : g;  // unconditional prefetch (clamped)
         load_meta<G>(m, meta32, lane, top - gc * G, -1, min(G, len - gc * G));
     };
     MetaVec<G> mv, mnext;
     meta_of(mv, g);
-    meta_of(mnext, g + NH);
+    meta_of(mnext, g + NL);
     // light children of node k in key order: l0, l1; a third one (only a tree root with four
     // children) in l2 -- at most one such node per group
     double l0[G][SPL], l1[G][SPL], l2[SPL];
@@ -640,8 +687,14 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
         if constexpr (AGD) load_recs<SPL, G>(m, n, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
     };
     issue(g, mv);
+#ifdef SM_CHAIN_PROF
+    long long h_cost = 0, h_slot = 0, h_rest = 0, h_t0 = clock64();
+#endif
     for (;;) {
         const int n = min(G, len - g * G);
+#ifdef SM_CHAIN_PROF
+        long long h_a = clock64();
+#endif
         // ---- weights and presence flags (meta + LDS table only): before waiting for the slot;
         // lane q < 3 holds S of the heavy child (q = 0) / post q of node k
         double Sl[G];
@@ -665,12 +718,20 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
             }
         }
         MetaVec<G> mnn;
-        meta_of(mnn, g + 2 * NH);
-        const int gn = g + NH;
+        meta_of(mnn, g + 2 * NL);
+        const int gn = g + NL;
         const int gl = gn < ngroups ? gn : g;
         // ---- Pre and C of the group (registers; the loads have landed by now in all but the
         // first group, whose wait is here)
+#ifdef SM_EXP_HELPER_NOCOST  // timing experiment only (wrong results): no cost computation
+        if constexpr (AGD)
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) cr[k][q] = 0.5f + 0.0f * __uint_as_float(rec.ob[k][q].y);
+#else
         if constexpr (AGD) chunk_costs<SPL, G>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, ring.atab, cr);
+#endif
         // Pre replaces l0 (with hidx >= 1 the first light child is a pre-heavy one, folded here)
 #pragma unroll
         for (int k = 0; k < G; ++k) {
@@ -692,9 +753,23 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
                 }
             }
         }
+#ifdef SM_CHAIN_PROF
+        {
+            double t = 0;
+#pragma unroll
+            for (int k = 0; k < G; ++k) t += l0[k][0] + (double)cr[k][0];
+            if (t == -1.0) h_rest += 1;  // keeps the stamp after the values are ready
+        }
+        long long h_b = clock64();
+        h_cost += h_b - h_a;
+#endif
         // ---- wait for the slot, fill it, publish
         UpSlot<SPL>& sl = ring.s[g % NS];
         if (g >= NS) lds_wait(&sl.freed, g - NS + 1, true);
+#ifdef SM_CHAIN_PROF
+        long long h_c = clock64();
+        h_slot += h_c - h_b;
+#endif
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             if (k < n) {
@@ -734,34 +809,18 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
         __hip_atomic_store(&sl.staged, ((unsigned long long)flags << 32) | (unsigned)(g + 1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        // ---- the next group's loads go out now: in flight while this group is computed
+        // ---- the next group's loads go out now
         issue(gl, mnext);
-        // ---- the chain's results: read back, store, free the slot
-        lds_wait_all(sl.done, NCW, g + 1);
-#pragma unroll
-        for (int k = 0; k < G; ++k) {  // unconditional (clamped rows are stored twice, same value)
-            double xr[SPL];
-            lds_row_read<SPL>(sl.pre[min(k, n - 1)], lane, xr);
-            store_row<SPL>(U, (uint32_t)(top - (g * G + min(k, n - 1))), Dpad, lane, xr);
-        }
-        if (done_word && g == ngroups - 1) {
-            // the piece's top row is the next piece's input: written through at device scope, then
-            // its done word
-            double xr[SPL];
-            lds_row_read<SPL>(sl.pre[n - 1], lane, xr);
-            double* row = U + (size_t)head * Dpad + lane * SPL;
-            if (row_lane<SPL>(lane, Dpad))
-#pragma unroll
-                for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            vm_drain();
-            if (lane == 0) publish_word(done_word, epoch);
-        }
-        lds_publish(&sl.freed, g + 1);  // the rows are in flight from registers
         if (gn >= ngroups) break;
         g = gn;
         mv = mnext;
         mnext = mnn;
     }
+#ifdef SM_CHAIN_PROF
+    if (blockIdx.x == 0 && lane == 0 && hh == 0)
+        printf("up loader view %d len %d cycles %lld cost+loads %lld slot %lld\n", (int)blockIdx.y, len, clock64() - h_t0,
+               h_cost, h_slot);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -912,7 +971,14 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
         }
         if constexpr (AGD) {
             load_recs<SPL, CHR>(mv, nb, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
+#ifdef SM_EXP_HELPER_NOCOST
+#pragma unroll
+            for (int k = 0; k < CHR; ++k)
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) cr[k][q] = 0.5f + 0.0f * __uint_as_float(rec.ob[k][q].y);
+#else
             chunk_costs<SPL, CHR>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, atab, cr);
+#endif
         }
 #pragma unroll
         for (int k = 0; k < CHR; ++k) {

@@ -29,7 +29,11 @@ __device__ __forceinline__ float rgray(uint2 r) { return __uint_as_float(r.y); }
 // r0 = right(x), l0 = left(x+d), gr1 = gray(right(x+1)), gl1 = gray(left(x+d+1))
 __device__ __forceinline__ float agd_rec(uint2 r0, uint2 l0, float gr1, float gl1, const float* __restrict__ atab) {
     const uint32_t l1 = __builtin_amdgcn_sad_u8(r0.x, l0.x, 0u);  // exact integer colour L1
+#ifdef SM_AGD_NO_TABLE
+    const float a = 0.11f * fminf((float)((double)(float)l1 * 0.33333333333), 7.0f);
+#else
     const float a = atab[l1];
+#endif
     float g = rgray(l0) - rgray(r0);
     g = g + (gr1 - gl1);
     const float b = 0.89f * fminf(fabsf(g), 2.0f);
