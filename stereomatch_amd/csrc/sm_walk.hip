@@ -64,38 +64,52 @@ __device__ __forceinline__ void walk_vm_drain() {
 // ---------------------------------------------------------------------------------------------
 // up pass
 // ---------------------------------------------------------------------------------------------
-// ROOT: the chunk holds a tree root with three light children (4 children); only that variant
-// carries the extra synchronous load, so the common chunk has no load inside its recurrence
+// Light-child rows of a chunk are compacted: the chunk's light children, in node order and key
+// order within a node, take row registers 0 .. LR-1 (wave-uniform bookkeeping from the metadata).
+// ~75% of nodes have none, so LR = 2 register rows cover almost every chunk; the rest (and a
+// tree root's third light child) are loaded where the recurrence uses them.  Holding CH x 2 rows
+// instead cost 16 VGPRs at SPL = 2, i.e. two of eight waves per SIMD.
+#ifndef WALK_UP_LR
+#define WALK_UP_LR 2
+#endif
 // VOL: the costs are caller-supplied volume rows (MC-CNN ingest, k_vol_rows) instead of the AGD
 // cost computed from the image records
-template <int SPL, int CH, bool ROOT, bool VOL>
+template <int SPL, int CH, bool VOL>
 __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, int view, int lane, int W, int Dpad,
                                          int dbase, int dend, const uint2* __restrict__ own, const uint2* __restrict__ oth,
                                          double* __restrict__ U, const float* __restrict__ Cv, const WalkShared& sh,
                                          double (&xc)[SPL], MetaVec<CH>& nxt, const uint32_t* __restrict__ meta32, int ntop,
                                          int nn) {
-    // ---- all vector loads of the chunk
-    // light-child rows: all issued before the chunk's one wait
-    double lr[CH][2][SPL];
+    constexpr int LR = WALK_UP_LR;
+    // ---- light-row bookkeeping (uniform): node j's light children are compact rows off[j] ..
+    int off[CH];
+    int tot = 0;
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-        const int jj = j < n ? j : n - 1;
-        const uint32_t hi = mfield(mv, jj, 3);
-        const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+        const uint32_t nch = j < n ? hi_nch(mfield(mv, j, 3)) : 0u;
+        off[j] = tot;
+        tot += nch > 0 ? (int)nch - 1 : 0;
+    }
+    // ---- all vector loads of the chunk
+    double lr[LR][SPL];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t i = (uint32_t)k + ((uint32_t)k >= hidx ? 1u : 0u);  // child position of light slot k
-            // wave-uniform branch: only present rows travel through L1 (~70% of nodes have none)
+    for (int q = 0; q < LR; ++q) {
 #ifdef SM_EXP_UP_NO_LIGHT  // timing experiment only (wrong results): no light-child row loads
-            if (false) {
+        if (false) {
 #else
-            if (j < n && i < nch) {
+        if (q < tot) {  // wave-uniform: only present rows travel through L1
 #endif
-                load_row<SPL>(U, mfield(mv, jj, 4 + (int)min(i, 3u)), Dpad, lane, lr[j][k]);
-            } else {
+            // the node j and light index kk of compact row q
+            int jq = 0;
 #pragma unroll
-                for (int q = 0; q < SPL; ++q) lr[j][k][q] = 0.0;
-            }
+            for (int j = 1; j < CH; ++j) jq = off[j] <= q ? j : jq;
+            const uint32_t hidx = hi_hidx(mfield(mv, jq, 3));
+            const int kk = q - off[jq];
+            const int pos = kk + (kk >= (int)hidx ? 1 : 0);
+            load_row<SPL>(U, mfield(mv, jq, 4 + min(pos, 3)), Dpad, lane, lr[q]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) lr[q][k] = 0.0;
         }
     }
     // ---- off-chain work: costs and edge factors of every node of the chunk
@@ -154,16 +168,17 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
 #pragma unroll
                         for (int k = 0; k < SPL; ++k) v[k] = xc[k];
                     } else {
-                        const uint32_t kk = i - (i > hidx ? 1u : 0u);
-                        if (kk == 0) {
+                        const int q = off[j] + (int)i - (i > hidx ? 1 : 0);  // compact light row
+                        bool held = false;
 #pragma unroll
-                            for (int k = 0; k < SPL; ++k) v[k] = lr[j][0][k];
-                        } else if (kk == 1) {
+                        for (int r = 0; r < LR; ++r) {
+                            if (q == r) {
 #pragma unroll
-                            for (int k = 0; k < SPL; ++k) v[k] = lr[j][1][k];
-                        } else if (ROOT) {
-                            load_row<SPL>(U, mfield(mv, j, 4 + (int)i), Dpad, lane, v);  // root's third light child
+                                for (int k = 0; k < SPL; ++k) v[k] = lr[r][k];
+                                held = true;
+                            }
                         }
+                        if (!held) load_row<SPL>(U, mfield(mv, j, 4 + (int)i), Dpad, lane, v);  // rare: loaded here
                     }
 #pragma unroll
                     for (int k = 0; k < SPL; ++k) acc[k] = __builtin_fma(Sv[j][i], v[k], acc[k]);
@@ -218,16 +233,8 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
         const int ntop = top - CH;
         const int nn = ntop >= head ? min(CH, ntop - head + 1) : 0;
         MetaVec<CH> nxt;  // the next chunk's metadata: loaded inside up_chunk
-        bool root = false;
-#pragma unroll
-        for (int j = 0; j < CH; ++j) root |= j < n && hi_nch(mfield(cur, j, 3)) == 4u;
         const float* __restrict__ Cv = view ? Cv1 : Cv0;
-        if (root)
-            up_chunk<SPL, CH, true, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc, nxt, meta32,
-                                         ntop, nn);
-        else
-            up_chunk<SPL, CH, false, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc, nxt, meta32,
-                                          ntop, nn);
+        up_chunk<SPL, CH, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc, nxt, meta32, ntop, nn);
         if (nn == 0) break;
         cur = nxt;
         top = ntop;

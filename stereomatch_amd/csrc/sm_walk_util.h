@@ -277,28 +277,47 @@ __device__ __forceinline__ int pix_col(int pix, int W) {
     return x;
 }
 
-// image records of CH path nodes: own(x), own(x+1) (one lane-dependent load: lanes 2m / 2m+1 hold
-// x / x+1) and the SPL+1 matched-image records a lane needs.  All loads are unconditional (rows of
-// absent nodes are clamped to the last valid one) and nothing reads the loaded values here, so a
-// chunk's loads are all in flight before the first wait.
+// image records of CH path nodes: own(x), own(x+1) of all CH nodes in ONE lane-distributed load
+// (lane j: node j's x, lane 32 + j: its x+1; one VMEM instruction instead of CH) and the SPL+1
+// matched-image records a lane needs per node (of the last one only its gray word).  All loads are
+// unconditional (rows of absent nodes are clamped to the last valid one) and nothing reads the
+// loaded values here, so a chunk's loads are all in flight before the first wait.
 template <int SPL, int CH>
 struct ImgRecs {
-    uint2 ob[CH][SPL + 1], own[CH];
+    uint2 ob[CH][SPL], own;
+    float obg[CH];  // gray of the matched record after the last one (only its gray is used)
 };
 
 template <int SPL, int CH>
 __device__ __forceinline__ void load_recs(const MetaVec<CH>& mv, int n, int view, int lane, int W, int dbase,
                                           const uint2* __restrict__ own, const uint2* __restrict__ oth, ImgRecs<SPL, CH>& r) {
+    static_assert(CH <= 32, "own records: lanes j and 32 + j hold node j");
+    {
+        // lane l: node min(l & 31, n - 1), by selects over the uniform pixels (a ds_bpermute would
+        // queue the address behind LDS traffic, heavy in the chain helpers); x+1 == W reads the
+        // next row / the pad: masked in chunk_costs
+        const int node = min(lane & 31, n - 1);
+        uint32_t pl = mfield(mv, 0, 0);
+#pragma unroll
+        for (int j = 1; j < CH; ++j) pl = node == j ? mfield(mv, j, 0) : pl;
+#ifdef SM_EXP_NO_OWN  // timing experiment only (wrong results): no own-record loads
+        r.own = make_uint2(pl, (uint32_t)lane);
+#else
+        r.own = own[(long long)pl + (lane >> 5)];
+#endif
+    }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const int jj = j < n ? j : n - 1;
         const long long pix = (long long)mfield(mv, jj, 0);  // = y*W + x: no division needed here
-        // own pixels x, x+1 through a lane-dependent (vector) load: a uniform address would become
-        // a scalar-cache load whose lgkmcnt waits serialise with the LDS table reads
-        r.own[j] = own[pix + (lane & 1)];  // x+1 == W reads the next row / the pad: masked below
         const long long base = view ? pix + dbase : pix - dbase - (SPL - 1);
 #pragma unroll
-        for (int q = 0; q <= SPL; ++q) r.ob[j][q] = oth[base + q];
+        for (int q = 0; q < SPL; ++q) r.ob[j][q] = oth[base + q];
+#ifdef SM_EXP_NO_OBG  // timing experiment only (wrong results): no extra gray load
+        r.obg[j] = __uint_as_float(r.ob[j][0].y);
+#else
+        r.obg[j] = __uint_as_float(reinterpret_cast<const uint32_t*>(oth + base + SPL)[1]);
+#endif
     }
 }
 
@@ -310,8 +329,8 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const int x = pix_col((int)mfield(mv, j, 0), W);
-        const uint2 o0 = make_uint2(__builtin_amdgcn_readlane(r.own[j].x, 0), __builtin_amdgcn_readlane(r.own[j].y, 0));
-        const uint2 o1 = make_uint2(__builtin_amdgcn_readlane(r.own[j].x, 1), __builtin_amdgcn_readlane(r.own[j].y, 1));
+        const uint2 o0 = make_uint2(__builtin_amdgcn_readlane(r.own.x, j), __builtin_amdgcn_readlane(r.own.y, j));
+        const uint2 o1 = make_uint2(__builtin_amdgcn_readlane(r.own.x, 32 + j), __builtin_amdgcn_readlane(r.own.y, 32 + j));
 #pragma unroll
         for (int k = 0; k < SPL; ++k) {
             const int d = dbase + k;
@@ -319,10 +338,10 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
             bool ok;
             if (view) {  // right reference: right(x) vs left(x+d)
                 ok = d < dend && x + d + 1 < W;
-                v = agd_rec(o0, r.ob[j][k], rgray(o1), rgray(r.ob[j][k + 1]), atab);
+                v = agd_rec(o0, r.ob[j][k], rgray(o1), k + 1 < SPL ? rgray(r.ob[j][k + 1 < SPL ? k + 1 : 0]) : r.obg[j], atab);
             } else {     // left pixel x at d: cost(x-d, d); x-d<0 and column W-1 -> 3.0
                 ok = d < dend && x - d >= 0 && x + 1 < W;
-                v = agd_rec(r.ob[j][SPL - 1 - k], o0, rgray(r.ob[j][SPL - k]), rgray(o1), atab);
+                v = agd_rec(r.ob[j][SPL - 1 - k], o0, k > 0 ? rgray(r.ob[j][k > 0 ? SPL - k : 0]) : r.obg[j], rgray(o1), atab);
             }
             c[j][k] = (T)(ok ? v : 3.0f);
         }
