@@ -1227,6 +1227,34 @@ __device__ __forceinline__ void down_group(DownSlot<SPL>& sl, int k0, int e0, do
     }
 }
 
+// rows and S of a full group, read from its slot into registers
+template <int SPL>
+struct DownRegs {
+    static constexpr int G = DownCfg<SPL>::G, CS = Split<SPL>::CS;
+    double t[G][CS], S[G];
+};
+template <int SPL>
+__device__ __forceinline__ void down_read(const DownSlot<SPL>& sl, int e0, DownRegs<SPL>& r) {
+#pragma unroll
+    for (int k = 0; k < DownRegs<SPL>::G; ++k) {
+        r.S[k] = sl.S[k];
+        lds_read_at<Split<SPL>::CS>(sl.x[k], e0, r.t[k]);
+    }
+}
+template <int SPL>
+__device__ __forceinline__ void down_step(DownSlot<SPL>& sl, int e0, const DownRegs<SPL>& r, double (&x)[Split<SPL>::CS]) {
+    constexpr int CS = Split<SPL>::CS;
+#pragma unroll
+    for (int k = 0; k < DownRegs<SPL>::G; ++k) {
+#pragma unroll
+        for (int q = 0; q < CS; ++q) x[q] = __builtin_fma(r.S[k], x[q], r.t[k][q]);
+        lds_write_at<CS>(sl.x[k], e0, x);
+    }
+}
+
+// The chain wave reads a full group's rows one group ahead: when the next group is already staged
+// at the top of a group, its LDS reads are issued before the group's recurrence and complete
+// behind it (otherwise right after it).  Two register sets, the loop unrolled by two groups.
 template <int SPL>
 __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int len, int lane, const double* x0) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, CS = Split<SPL>::CS;
@@ -1243,31 +1271,58 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
 #pragma unroll
     for (int q = 0; q < CS; ++q) x[q] = x0 ? x0[e0 + q] : 0.0;
     const int ngroups = (len + G - 1) / G;
-    int st = lds_state(&ring.s[0].staged);  // poll-ahead: the next group's state
-    for (int g = 0; g < ngroups; ++g) {
-        DownSlot<SPL>& sl = ring.s[g % NS];
-        const int n = min(G, len - g * G);
+    const int nfull = len / G;  // full groups take the pipeline; a partial last one node by node
+    auto wait_staged = [&](int g) {
 #ifdef SM_CHAIN_PROF
         const long long ta = clock64();
 #endif
-        while (st != g + 1) {
-            PROF_SPIN(++spins);
-            st = lds_state(&sl.staged);
-        }
+        while (lds_state(&ring.s[g % NS].staged) != g + 1) PROF_SPIN(++spins);
 #ifdef SM_CHAIN_PROF
-        const long long tb = clock64();
-        tr += tb - ta;
+        tr += clock64() - ta;
 #endif
-        st = lds_state(&ring.s[(g + 1) % NS].staged);
-        if (n == G) {
-            down_group<SPL, G>(sl, 0, e0, x);
-        } else {
-            for (int k = 0; k < n; ++k) down_group<SPL, 1>(sl, k, e0, x);
+    };
+    DownRegs<SPL> A, B;
+    int g = 0;
+    if (nfull > 0) {
+        wait_staged(0);
+        down_read<SPL>(ring.s[0], e0, A);
+    }
+    // invariant at the top: group g (< nfull) is in A
+    while (g < nfull) {
+        // ---- group g (A); group g+1 into B, ahead when it is staged already
+        bool ahead = false;
+        if (g + 1 < nfull && lds_state(&ring.s[(g + 1) % NS].staged) == g + 2) {
+            down_read<SPL>(ring.s[(g + 1) % NS], e0, B);
+            ahead = true;
         }
-        lds_publish_ordered(&sl.done[w], g + 1);
-#ifdef SM_CHAIN_PROF
-        tc += clock64() - tb;
-#endif
+        down_step<SPL>(ring.s[g % NS], e0, A, x);
+        lds_publish_ordered(&ring.s[g % NS].done[w], g + 1);
+        ++g;
+        if (g >= nfull) break;
+        if (!ahead) {
+            wait_staged(g);
+            down_read<SPL>(ring.s[g % NS], e0, B);
+        }
+        // ---- group g (B); group g+1 into A
+        ahead = false;
+        if (g + 1 < nfull && lds_state(&ring.s[(g + 1) % NS].staged) == g + 2) {
+            down_read<SPL>(ring.s[(g + 1) % NS], e0, A);
+            ahead = true;
+        }
+        down_step<SPL>(ring.s[g % NS], e0, B, x);
+        lds_publish_ordered(&ring.s[g % NS].done[w], g + 1);
+        ++g;
+        if (g >= nfull) break;
+        if (!ahead) {
+            wait_staged(g);
+            down_read<SPL>(ring.s[g % NS], e0, A);
+        }
+    }
+    if (nfull < ngroups) {  // the partial last group
+        DownSlot<SPL>& sl = ring.s[nfull % NS];
+        wait_staged(nfull);
+        for (int k = 0; k < len - nfull * G; ++k) down_group<SPL, 1>(sl, k, e0, x);
+        lds_publish_ordered(&sl.done[w], nfull + 1);
     }
 #ifdef SM_CHAIN_PROF
     if (blockIdx.x == 0 && lane == 0 && w == 0)
@@ -1277,13 +1332,68 @@ __device__ __forceinline__ void down_chain_wave(DownRing<SPL>& ring, int w, int 
     (void)spins;
 }
 
+// Helper waves of the down chain, split like the up chain's: loaders (load A_up rows + metadata,
+// stage T and S) and storers (WTA of the chain's results, output and row stores, free the slot).
+// A loader then never waits on store completions (gfx9: one vmcnt for loads and stores).
+#ifndef DN_STORERS
+#define DN_STORERS 8
+#endif
 template <int SPL>
 __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, int head, int len, int lane,
                                                  const uint32_t* __restrict__ meta32, const WalkView& V, int Dpad,
                                                  const WtaCfg& w, int store_all, uint32_t epoch,
                                                  uint32_t* done_word) {
-    constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NH = Split<SPL>::NH, NCW = Split<SPL>::NCW;
+    constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NCW = Split<SPL>::NCW;
+    constexpr int NST = DN_STORERS, NL = Split<SPL>::NH - NST;
     const int ngroups = (len + G - 1) / G;
+    if (hh >= NL) {
+        // ---- storer: groups hh - NL (mod NST)
+        for (int g = hh - NL; g < ngroups; g += NST) {
+            const int n = min(G, len - g * G);
+            DownSlot<SPL>& sl = ring.s[g % NS];
+            lds_wait_all(sl.done, NCW, g + 1);
+            double xs[G][SPL];
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (k < n) {
+                    lds_row_read<SPL>(sl.x[k], lane, xs[k]);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) xs[k][q] = 0.0;
+                }
+            }
+            const uint32_t pix = sl.pix[min(lane, G - 1)];
+            uint32_t st[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k) st[k] = sl.st[k];
+            lds_publish(&sl.freed, g + 1);
+            double mn;
+            int gi;
+            float dsp;
+            wta_nodes<SPL, G>(xs, lane, w, mn, gi, dsp);
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                if (k < n && (store_all || st[k])) store_row<SPL>(V.A, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
+            if (lane < n) {
+                V.idx[pix] = gi;
+                V.minc[pix] = mn;
+                V.disp[pix] = dsp;
+            }
+            if (done_word && g == ngroups - 1) {
+                // the piece's last row is the next piece's input: device scope, then the done word
+                double* row = V.A + (size_t)(head + len - 1) * Dpad + lane * SPL;
+#pragma unroll
+                for (int k = 0; k < G; ++k)
+                    if (k == n - 1 && row_lane<SPL>(lane, Dpad))
+#pragma unroll
+                        for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xs[k][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vm_drain();
+                if (lane == 0) publish_word(done_word, epoch);
+            }
+        }
+        return;
+    }
+    // ---- loader: groups hh, hh + NL, ...
     int g = hh;
     if (g >= ngroups) return;
     double* __restrict__ U = V.U;
@@ -1320,6 +1430,15 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
                 for (int q = 0; q < SPL; ++q) t[k][q] = __builtin_fma(S, ap[q], t[k][q]);
             }
         }
+        uint32_t pixk[G], stk[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            pixk[k] = mfield(mv, k, 0);
+            stk[k] = hi_light(mfield(mv, k, 3));
+        }
+        // ---- next group's loads go out now (unconditional, clamped)
+        const int gn = g + NL;
+        issue(gn < ngroups ? gn : g);
         if (g >= NS) lds_wait(&sl.freed, g - NS + 1, true);
 #pragma unroll
         for (int k = 0; k < G; ++k) {
@@ -1327,55 +1446,12 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
                 lds_row_write<SPL>(sl.x[k], lane, t[k]);
                 if (lane == 0) {
                     sl.S[k] = Sk[k];
-                    sl.pix[k] = mfield(mv, k, 0);
-                    sl.st[k] = hi_light(mfield(mv, k, 3));
+                    sl.pix[k] = pixk[k];
+                    sl.st[k] = stk[k];
                 }
             }
         }
         lds_publish(&sl.staged, g + 1);
-        // ---- next group's loads go out now (unconditional, clamped): a full chain lap of lead
-        const int gn = g + NH;
-        issue(gn < ngroups ? gn : g);
-        // ---- the chain's results: WTA, stores, free the slot
-        lds_wait_all(sl.done, NCW, g + 1);
-        double xs[G][SPL];
-#pragma unroll
-        for (int k = 0; k < G; ++k) {
-            if (k < n) {
-                lds_row_read<SPL>(sl.x[k], lane, xs[k]);
-            } else {
-#pragma unroll
-                for (int q = 0; q < SPL; ++q) xs[k][q] = 0.0;
-            }
-        }
-        const uint32_t pix = sl.pix[min(lane, G - 1)];
-        uint32_t st[G];
-#pragma unroll
-        for (int k = 0; k < G; ++k) st[k] = sl.st[k];
-        lds_publish(&sl.freed, g + 1);
-        double mn;
-        int gi;
-        float dsp;
-        wta_nodes<SPL, G>(xs, lane, w, mn, gi, dsp);
-#pragma unroll
-        for (int k = 0; k < G; ++k)
-            if (k < n && (store_all || st[k])) store_row<SPL>(V.A, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
-        if (lane < n) {
-            V.idx[pix] = gi;
-            V.minc[pix] = mn;
-            V.disp[pix] = dsp;
-        }
-        if (done_word && g == ngroups - 1) {
-            // the piece's last row is the next piece's input: device scope, then the done word
-            double* row = V.A + (size_t)(head + len - 1) * Dpad + lane * SPL;
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-                if (k == n - 1 && row_lane<SPL>(lane, Dpad))
-#pragma unroll
-                    for (int q = 0; q < SPL; ++q) __hip_atomic_store(row + q, xs[k][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            vm_drain();
-            if (lane == 0) publish_word(done_word, epoch);
-        }
         if (gn >= ngroups) break;
         g = gn;
     }
