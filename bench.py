@@ -139,6 +139,12 @@ def main():
     ap.add_argument("--min-size", type=int, default=200)
     ap.add_argument("--aggregator", default="tree", choices=["tree", "guided"],
                     help="cost aggregator: the MST/forest tree filter (default) or the colour guided filter")
+    ap.add_argument("--shard", default="vd", choices=["vd", "d"],
+                    help="strong mode partition: vd = view groups x disparity shards (even N: half the ranks per "
+                         "view, D split inside each group), d = disparity shards of both views")
+    ap.add_argument("--emulate-rank", default=None, metavar="R/N",
+                    help="one GPU runs rank R's share of an N-rank strong-mode frame (no collective): the per-rank "
+                         "cost of the partition, for the multi-GPU estimate in DESIGN.md 7")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight (contexts on their own streams); 0 = 3, fewer where memory needs it")
     args = ap.parse_args()
@@ -165,13 +171,26 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     W, H = args.width, args.height
+    views, group, gsize, grank = 3, 0, world, rank  # this rank's views and its reduce group
+    emu = None
+    if args.emulate_rank:
+        if world != 1:
+            print("bench.py: --emulate-rank runs on one GPU without torchrun", file=sys.stderr)
+            sys.exit(2)
+        er, en = (int(x) for x in args.emulate_rank.split("/"))
+        if args.disp is None or args.disp == 128:
+            args.disp = 256
+        emu = sm.partition(args.disp, en, er, split_views=args.shard == "vd")
+        emu.update(rank=er, nranks=en)
     if world == 1 or args.mode == "weak":
         Dloc = args.disp
         Dtot = Dloc * world if args.mode == "weak" else Dloc
         dbeg = rank * Dloc
     elif args.mode == "strong":
         Dtot = args.disp
-        dbeg, Dloc = sm.shard_range(Dtot, world, rank)
+        part = sm.partition(Dtot, world, rank, split_views=args.shard == "vd")
+        dbeg, Dloc, views = part["d0"], part["D"], part["views"]
+        group, gsize, grank = part["group"], part["group_size"], part["group_rank"]
     else:  # batch
         Dloc = Dtot = args.disp
         dbeg = 0
@@ -179,6 +198,9 @@ def main():
         Dtot_frame = Dloc
     else:
         Dtot_frame = Dtot
+    if emu:  # one rank's share of an N-rank frame: its views and slices of the total range
+        Dtot = Dtot_frame = args.disp
+        dbeg, Dloc, views = emu["d0"], emu["D"], emu["views"]
 
     # frames in flight: each context is a full pipeline on its own stream; frame i goes to context
     # i % n, so frame i+1's prep / MST / layout overlaps frame i's tree filter on the GPU
@@ -186,16 +208,18 @@ def main():
     inflight = args.inflight if args.inflight > 0 else max(1, min(3, int(200.0 // per_ctx_gb)))
     ctxs = [sm.Context(local) for _ in range(inflight)]
     if world > 1 and args.mode != "batch":
-        for c in ctxs:  # one communicator per context: its reduce runs on its own stream
-            uid = [sm.Context.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            c.comm_init(world, rank, uid[0])
+        for c in ctxs:  # one communicator per context (its reduce runs on its own stream) and group
+            ids = [None] * world
+            dist.all_gather_object(ids, sm.Context.unique_id() if grank == 0 else None)
+            leader = next(r for r in range(world) if ids[r] is not None and (r // gsize if gsize < world else 0) == group)
+            c.comm_init(gsize, grank, ids[leader])
     pair_index = rank if args.mode == "batch" else 0
     left, right, _ = make_pair(W, H, Dtot_frame, index=pair_index)
     for c in ctxs:
         c.upload(left, right)
     params = sm.default_params(disp_begin=dbeg, disp_total=Dtot_frame, c=args.segment_c, min_size=args.min_size,
-                               aggregator=sm.SM_AGG_GUIDED if args.aggregator == "guided" else sm.SM_AGG_TREE)
+                               aggregator=sm.SM_AGG_GUIDED if args.aggregator == "guided" else sm.SM_AGG_TREE,
+                               views=views)
     torch.cuda.set_device(local)
     ctx = ctxs[0]
 
@@ -318,13 +342,14 @@ def main():
         "data": "synthetic (seeded slanted-plane stereo pair, tools/synth.py)",
         "config": {"workload": "%dx%d D=%d both views%s" % (W, H, Dtot_frame, CONFIG_NAMES.get((W, H, Dtot_frame), ""))
                    if world == 1 else
-                   "%dx%d D=%d, %s mode, %d disparities/rank%s" % (
-                       W, H, Dtot_frame, args.mode, Dloc,
+                   "%dx%d D=%d, %s mode, %d disparities/rank%s%s" % (
+                       W, H, Dtot_frame, args.mode, Dloc, " of one view (view groups)" if views != 3 else "",
                        " (BASELINE C4)" if (args.mode == "strong" and (W, H, Dtot_frame) == (1920, 1200, 256)) else
                        " (BASELINE C5: one pair per GPU)" if (args.mode == "batch" and (W, H, Dtot_frame) == (3840, 2160, 256))
                        else ""),
                    "W": W, "H": H, "D": Dtot_frame, "disparities_per_rank": Dloc,
-                   "parallelism": "replicas" if args.mode == "batch" else "d-shard%d" % world,
+                   "parallelism": "replicas" if args.mode == "batch" else
+                   ("view2 x d-shard%d" % gsize if views != 3 else "d-shard%d" % world),
                    "tree": "MST" if args.segment_c == float("inf") else "segment forest c=%g min_size=%d" % (
                        args.segment_c, args.min_size),
                    "aggregator": args.aggregator,
@@ -348,7 +373,13 @@ def main():
         "frames_in_flight": inflight,
         "host_io": host_io,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if emu:
+        line["emulated_rank"] = dict(emu, note="one rank's share of an N-rank strong-mode frame on one GPU, no "
+                                               "collective; value counts the rank's own voxels")
+        line["value"] = W * H * Dloc * bin(views).count("1") * args.steps / elapsed
+        line["config"]["workload"] = "rank %d/%d of %dx%d D=%d: views %d, slices [%d, %d)" % (
+            emu["rank"], emu["nranks"], W, H, Dtot_frame, views, dbeg, dbeg + Dloc)
+    if rank == 0 and world == 1 and not args.no_cpu and not emu:
         line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame, args.cpu_slices, args.cpu_slices_1t)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -79,6 +79,10 @@ typedef struct {
     int aggregator;    /* sm_aggregator (default SM_AGG_TREE)                        */
     int gf_radius;     /* SM_AGG_GUIDED: box radius (default 9)                      */
     float gf_eps;      /* SM_AGG_GUIDED: regularisation (default 6.5025 = 0.01^2*255^2) */
+    int views;         /* views this call computes: 1 = left, 2 = right, 3 = both (default; 0 = both).
+                          A one-view call builds that view's tree only, filters it and (with a
+                          communicator) reduces it across the ranks of its group; the other view's
+                          outputs are left untouched.  Multi-GPU partitioning: see DESIGN.md 7 */
 } sm_params;
 
 /* Post-processing of the final (cross-rank reduced) float disparity maps (idx / min untouched),

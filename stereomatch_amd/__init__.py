@@ -22,7 +22,7 @@ from ._lib import (SM_AGG_GUIDED, SM_AGG_TREE, SM_COST_AGD, SM_COST_VOLUME, SM_P
 STEREO3DMST_POST = SM_POST_LABEL_TO_DISP | SM_POST_LR_CHECK
 
 __all__ = ["stereo3dmst", "startTimer", "getTimer", "Context", "default_params", "StereoMSTError", "device_count",
-           "shard_range", "STEREO3DMST_POST"]
+           "shard_range", "partition", "STEREO3DMST_POST"]
 
 
 def shard_range(d_total, nranks, rank):
@@ -34,6 +34,23 @@ def shard_range(d_total, nranks, rank):
     d0 = rank * d_total // nranks
     d1 = (rank + 1) * d_total // nranks
     return d0, d1 - d0
+
+
+def partition(d_total, nranks, rank, split_views=True):
+    """The share of one frame (both views, d_total disparities each) that `rank` of `nranks` owns
+    (DESIGN.md 7).  With split_views and an even nranks, the ranks form two view groups -- ranks
+    [0, N/2) the left view, [N/2, N) the right view -- and each group D-shards its view over its
+    N/2 ranks: a rank builds one tree and filters d_total / (N/2) slices of one view, and the WTA
+    reduce runs inside its group.  Otherwise every rank takes both views and d_total / N slices.
+    Returns dict(views, d0, D, group, group_size, group_rank): views is the sm_params.views mask."""
+    if split_views and nranks >= 2 and nranks % 2 == 0:
+        half = nranks // 2
+        group, grank = divmod(rank, half)
+        d0, D = shard_range(d_total, half, grank)
+        return dict(views=1 << group, d0=d0, D=D, group=group, group_size=half, group_rank=grank)
+    d0, D = shard_range(d_total, nranks, rank)
+    return dict(views=3, d0=d0, D=D, group=0, group_size=nranks, group_rank=rank)
+
 
 _default_ctx = None
 _timer = ctypes.c_double(0.0)

@@ -31,7 +31,7 @@ class SmParams(ctypes.Structure):
     _fields_ = [("gamma", ctypes.c_float), ("c", ctypes.c_float), ("min_size", ctypes.c_int),
                 ("median_ksize", ctypes.c_int), ("cost_kind", ctypes.c_int), ("disp_begin", ctypes.c_int),
                 ("disp_total", ctypes.c_int), ("post", ctypes.c_int), ("aggregator", ctypes.c_int),
-                ("gf_radius", ctypes.c_int), ("gf_eps", ctypes.c_float)]
+                ("gf_radius", ctypes.c_int), ("gf_eps", ctypes.c_float), ("views", ctypes.c_int)]
 
 
 class SmFilterStats(ctypes.Structure):
@@ -108,6 +108,11 @@ def default_params(**overrides):
     return p
 
 
+def _active(out, views):
+    """The views a call computed (sm_params.views: 1 left, 2 right, 3 both)."""
+    return {v: out[v] for i, v in enumerate(("left", "right")) if (views >> i) & 1}
+
+
 def device_count():
     n = ci(0)
     lib().sm_device_count(ctypes.byref(n))
@@ -162,10 +167,11 @@ class Context:
         p = params or default_params()
         out = {v: dict(disp=np.empty((H, W), np.float32), idx=np.empty((H, W), np.int32),
                        minc=np.empty((H, W), np.float64)) for v in ("left", "right")}
+        self._views = p.views or 3
         self._check(lib().sm_match(self.h, ptr(left), ptr(right), W, H, W * 3, D, ctypes.byref(p),
                                    ptr(out["left"]["disp"]), ptr(out["right"]["disp"]), ptr(out["left"]["idx"]),
                                    ptr(out["right"]["idx"]), ptr(out["left"]["minc"]), ptr(out["right"]["minc"])))
-        return out
+        return _active(out, self._views)
 
     def upload(self, left, right):
         left, right = as_image(left), as_image(right)
@@ -185,6 +191,7 @@ class Context:
 
     def match_async(self, D, params=None):
         p = params or default_params()
+        self._views = p.views or 3
         self._check(lib().sm_match_async(self.h, D, ctypes.byref(p)))
 
     def synchronize(self):
@@ -197,7 +204,7 @@ class Context:
         self._check(lib().sm_download_results(self.h, ptr(out["left"]["disp"]), ptr(out["right"]["disp"]),
                                               ptr(out["left"]["idx"]), ptr(out["right"]["idx"]),
                                               ptr(out["left"]["minc"]), ptr(out["right"]["minc"])))
-        return out
+        return _active(out, getattr(self, "_views", 3))
 
     def stage_times(self):
         buf = (ctypes.c_float * 7)()

@@ -82,6 +82,7 @@ struct sm_ctx {
     DevBuf vin[2];               // MC-CNN ingest: caller volumes [vin_D][H][W] f32 per view
     int vin_W = 0, vin_H = 0, vin_D = 0;
     bool use_vol = false;        // the current call takes its costs from vin (SM_COST_VOLUME)
+    int views = 3;               // views of the last call (sm_params.views; bit 0 left, bit 1 right)
     DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
     uint32_t epoch = 0;      // bumped per filter call; status words are zeroed only on (re)allocation
     // GPU layout buffers (sm_layout_gpu.hip)
@@ -196,6 +197,12 @@ sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
     if ((p->post & SM_POST_OCCLUSION) && (p->post & SM_POST_OCCLUSION_ZERO))
         return fail(ctx, SM_ERR_ARG, "SM_POST_OCCLUSION and SM_POST_OCCLUSION_ZERO are exclusive");
     if (p->aggregator != SM_AGG_TREE && p->aggregator != SM_AGG_GUIDED) return fail(ctx, SM_ERR_ARG, "unknown aggregator");
+    if (p->views < 0 || p->views > 3) return fail(ctx, SM_ERR_ARG, "views must be 1 (left), 2 (right) or 3 / 0 (both)");
+    if (p->views == 1 || p->views == 2) {
+        if (p->aggregator != SM_AGG_TREE) return fail(ctx, SM_ERR_ARG, "a one-view call needs SM_AGG_TREE");
+        if (p->post & ~SM_POST_SUBPIXEL)
+            return fail(ctx, SM_ERR_ARG, "a one-view call takes no post-processing that needs both maps (only SM_POST_SUBPIXEL)");
+    }
     if (p->aggregator == SM_AGG_GUIDED) {
         if (p->cost_kind != SM_COST_AGD) return fail(ctx, SM_ERR_ARG, "SM_AGG_GUIDED filters the AGD cost only");
         if (p->gf_radius < 1 || p->gf_radius > 64 || !(p->gf_eps > 0)) return fail(ctx, SM_ERR_ARG, "bad guided-filter radius / eps");
@@ -237,6 +244,18 @@ size_t rec_pad_for(int disp_begin, int D) {
     return need <= SM_REC_PAD ? SM_REC_PAD : (need + 1023) / 1024 * 1024;
 }
 
+// views of a call: bit 0 = left, bit 1 = right (sm_params.views); stages that run view-agnostic
+// kernels (MST, layout) pack the active views into the kernels' view slots 0 .. n-1
+struct ViewSet {
+    int n = 0;
+    int v[2] = {0, 1};
+    explicit ViewSet(int mask) {
+        for (int q = 0; q < 2; ++q)
+            if ((mask >> q) & 1) v[n++] = q;
+    }
+};
+inline bool view_on(int mask, int v) { return ((mask >> v) & 1) != 0; }
+
 // ----------------------------------------------------------------------------- stages
 sm_status stage_prep(sm_ctx* ctx) {
     const int W = ctx->W, H = ctx->H;
@@ -271,15 +290,17 @@ static bool hooked_any(const int* hf, int nviews, int q) {
     return hf[q] != 0 || (nviews > 1 && hf[SM_MST_MAX_ROUNDS + q] != 0);
 }
 
-sm_status stage_mst(sm_ctx* ctx, int nviews);
+sm_status stage_mst(sm_ctx* ctx, int views);
 
 // Segment mode: the reference's order-dependent Felzenszwalb segmentation + min-size merge on the host
 // (sm_segment.cpp), from the GPU's edge weights; the forest, linked into one tree by S = 0 virtual
 // edges, goes back as the MST masks and the layout's weights.  Replaces stage_mst.
-sm_status stage_segment(sm_ctx* ctx, int nviews, float c, int min_size) {
+sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size) {
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H;
-    for (int v = 0; v < nviews; ++v) {
+    const ViewSet vs(views);
+    for (int i = 0; i < vs.n; ++i) {
+        const int v = vs.v[i];
         CHECK(ensure(ctx, ctx->mR[v], N));
         CHECK(ensure(ctx, ctx->mD[v], N));
         CHECK(ensure(ctx, ctx->fwR[v], N * 2));
@@ -300,10 +321,11 @@ sm_status stage_segment(sm_ctx* ctx, int nviews, float c, int min_size) {
                                               ctx->h_m[v][0].data(), ctx->h_m[v][1].data(), ctx->h_fw[v][0].data(),
                                               ctx->h_fw[v][1].data());
     };
-    if (nviews > 1) other = std::thread(run, 1);
-    run(0);
+    if (vs.n > 1) other = std::thread(run, vs.v[1]);
+    run(vs.v[0]);
     if (other.joinable()) other.join();
-    for (int v = 0; v < nviews; ++v) {
+    for (int i = 0; i < vs.n; ++i) {
+        const int v = vs.v[i];
         HIPC(hipMemcpyAsync(ctx->mR[v].p, ctx->h_m[v][0].data(), N, hipMemcpyHostToDevice, ctx->st));
         HIPC(hipMemcpyAsync(ctx->mD[v].p, ctx->h_m[v][1].data(), N, hipMemcpyHostToDevice, ctx->st));
         HIPC(hipMemcpyAsync(ctx->fwR[v].p, ctx->h_fw[v][0].data(), N * 2, hipMemcpyHostToDevice, ctx->st));
@@ -317,30 +339,33 @@ sm_status stage_segment(sm_ctx* ctx, int nviews, float c, int min_size) {
 }
 
 // tree of the call: the MST (Boruvka) or, for finite c, the segment forest
-sm_status stage_tree(sm_ctx* ctx, int nviews, const sm_params* p) {
-    if (p && !std::isinf(p->c)) return stage_segment(ctx, nviews, p->c, p->min_size);
+sm_status stage_tree(sm_ctx* ctx, int views, const sm_params* p) {
+    if (p && !std::isinf(p->c)) return stage_segment(ctx, views, p->c, p->min_size);
     ctx->seg = false;
-    return stage_mst(ctx, nviews);
+    return stage_mst(ctx, views);
 }
 
-sm_status stage_mst(sm_ctx* ctx, int nviews) {
+sm_status stage_mst(sm_ctx* ctx, int views) {
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H;
+    const ViewSet vs(views);
+    const int nviews = vs.n;
     MstArgs a{};
     a.nviews = nviews;
-    for (int v = 0; v < 2; ++v) {
+    for (int i = 0; i < 2; ++i) {  // kernel view slot i = view vs.v[i] (slot 1 unused for one view)
+        const int v = vs.v[i];
         CHECK(ensure(ctx, ctx->comp[v], N * 4));
         CHECK(ensure(ctx, ctx->best[v], 2 * N * 8));
         CHECK(ensure(ctx, ctx->root[v], N * 4));
         CHECK(ensure(ctx, ctx->mR[v], N));
         CHECK(ensure(ctx, ctx->mD[v], N));
-        a.wR[v] = P<uint16_t>(ctx->wR[v]);
-        a.wD[v] = P<uint16_t>(ctx->wD[v]);
-        a.comp[v] = P<uint32_t>(ctx->comp[v]);
-        a.best[v] = P<unsigned long long>(ctx->best[v]);
-        a.root[v] = P<uint32_t>(ctx->root[v]);
-        a.mR[v] = P<uint8_t>(ctx->mR[v]);
-        a.mD[v] = P<uint8_t>(ctx->mD[v]);
+        a.wR[i] = P<uint16_t>(ctx->wR[v]);
+        a.wD[i] = P<uint16_t>(ctx->wD[v]);
+        a.comp[i] = P<uint32_t>(ctx->comp[v]);
+        a.best[i] = P<unsigned long long>(ctx->best[v]);
+        a.root[i] = P<uint32_t>(ctx->root[v]);
+        a.mR[i] = P<uint8_t>(ctx->mR[v]);
+        a.mD[i] = P<uint8_t>(ctx->mD[v]);
     }
     CHECK(ensure(ctx, ctx->changed, 2 * SM_MST_MAX_ROUNDS * sizeof(int)));
     CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
@@ -358,7 +383,7 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     HIPC(launch_bor_local(ctx->st, a, W, H));
     const bool pixel_rounds = getenv("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B path (tests, tools)
     if (pixel_rounds) {
-        for (int v = 0; v < nviews; ++v) HIPC(hipMemsetAsync(ctx->best[v].p, 0xFF, N * 8, ctx->st));
+        for (int i = 0; i < nviews; ++i) HIPC(hipMemsetAsync(ctx->best[vs.v[i]].p, 0xFF, N * 8, ctx->st));
         // global rounds: every kernel of round r exits at once if round r-1 hooked nothing, so the
         // host only synchronises every 4 rounds to decide whether to enqueue more
         for (int r = 0; r < SM_MST_MAX_ROUNDS; ++r) {
@@ -379,15 +404,16 @@ sm_status stage_mst(sm_ctx* ctx, int nviews) {
     MstCompact c{};
     c.emax = 2 * N;
     c.bstride = N;
-    for (int v = 0; v < 2; ++v) {
+    for (int i = 0; i < 2; ++i) {
+        const int v = vs.v[i];
         CHECK(ensure(ctx, ctx->cedge[v], 2 * (2 * N) * 16));
         CHECK(ensure(ctx, ctx->clab[v], N * 4));
         CHECK(ensure(ctx, ctx->chook[v], N * 4));
-        c.cid[v] = P<uint32_t>(ctx->root[v]);
-        c.counts[v] = P<uint32_t>(ctx->ccnt[v]);
-        c.edges[v] = ctx->cedge[v].p;
-        c.lab[v] = P<uint32_t>(ctx->clab[v]);
-        c.hook[v] = P<uint32_t>(ctx->chook[v]);
+        c.cid[i] = P<uint32_t>(ctx->root[v]);
+        c.counts[i] = P<uint32_t>(ctx->ccnt[v]);
+        c.edges[i] = ctx->cedge[v].p;
+        c.lab[i] = P<uint32_t>(ctx->clab[v]);
+        c.hook[i] = P<uint32_t>(ctx->chook[v]);
     }
     HIPC(launch_bor_compact(ctx->st, a, c, W, H));
     HIPC(launch_bor_cinit(ctx->st, a, c));
@@ -448,7 +474,9 @@ int piece_len() {  // read per call: tests switch it between matches
 // device-side rounds record: [0, SM_NBUCKETS] bucket begin, then count, cursor, nrounds, n_has_light
 constexpr size_t RREC = RREC_FWD;
 
-sm_status stage_layout(sm_ctx* ctx, int nviews) {
+sm_status stage_layout(sm_ctx* ctx, int views) {
+    const ViewSet vs(views);
+    const int nviews = vs.n;
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H;
     const uint32_t ntiles = (uint32_t)(((W + 31) / 32) * ((H + 31) / 32));
@@ -456,7 +484,8 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
     const size_t nscan = (2 * N + 8191) / 8192 + 1;
     LayoutPair LP{};
     ZeroList z{};
-    for (int v = 0; v < nviews; ++v) {
+    for (int i = 0; i < nviews; ++i) {
+        const int v = vs.v[i];
         CHECK(ensure(ctx, ctx->adj[v], N));
         CHECK(ensure(ctx, ctx->pdir[v], N));
         CHECK(ensure(ctx, ctx->heavy[v], N));
@@ -493,7 +522,7 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
         z.add(ctx->plen[v].p, N * 4);  // lengths past the last path stay 0
         z.add(ctx->ccount[v].p, 16);
         z.add(ctx->rounds[v].p, RREC * 4);
-        LayoutView& L = LP.v[v];
+        LayoutView& L = LP.v[i];
         L.mR = P<uint8_t>(ctx->mR[v]);
         L.mD = P<uint8_t>(ctx->mD[v]);
         L.wR = P<uint16_t>(ctx->seg ? ctx->fwR[v] : ctx->wR[v]);
@@ -546,15 +575,15 @@ sm_status stage_layout(sm_ctx* ctx, int nviews) {
     HIPC(launch_zero(ctx->st, z));
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains, (uint32_t)piece_len()));
     // the host needs the per-round path counts to size the walker grids
-    for (int v = 0; v < nviews; ++v)
-        HIPC(hipMemcpyAsync(ctx->h_rounds + v * RREC, ctx->rounds[v].p, RREC * 4, hipMemcpyDeviceToHost, ctx->st));
+    for (int i = 0; i < nviews; ++i)
+        HIPC(hipMemcpyAsync(ctx->h_rounds + vs.v[i] * RREC, ctx->rounds[vs.v[i]].p, RREC * 4, hipMemcpyDeviceToHost, ctx->st));
     HIPC(hipStreamSynchronize(ctx->st));
     bool grew = false;
     CHECK(mst_finish(ctx, &grew));
-    if (grew) return stage_layout(ctx, nviews);  // the forest was incomplete: lay out the final MST
+    if (grew) return stage_layout(ctx, views);  // the forest was incomplete: lay out the final MST
     for (int v = 0; v < 2; ++v) {
         auto& L = ctx->layout[v];
-        if (v >= nviews) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); L.nodes.assign(SM_NBUCKETS, 0); L.piece_begin.assign(SM_NBUCKETS + 1, 0); continue; }
+        if (!view_on(views, v)) { L.nrounds = 0; L.npaths = 0; L.begin.assign(1, 0); L.maxlen.assign(SM_NBUCKETS, 0); L.seg_begin.assign(SM_NBUCKETS + 1, 0); L.nodes.assign(SM_NBUCKETS, 0); L.piece_begin.assign(SM_NBUCKETS + 1, 0); continue; }
         const uint32_t* R = ctx->h_rounds + v * RREC;
         L.nrounds = R[3 * SM_NBUCKETS + 1];
         L.n_has_light = R[3 * SM_NBUCKETS + 2];
@@ -603,11 +632,11 @@ bool no_pieces() { return getenv("SM_NO_PIECES") != nullptr; }
 // capacity of the per-view piece arrays (<= N/32 long paths + N/SM_PIECE pieces)
 size_t piece_cap(size_t N) { return N / 16 + 64; }
 
-void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int nviews) {
+void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int views) {
     a.maxlen = 0;
     for (int v = 0; v < 2; ++v) {
         const auto& L = ctx->layout[v];
-        if (v >= nviews || r >= L.nrounds) {
+        if (!view_on(views, v) || r >= L.nrounds) {
             a.paths[v] = P<SmPath>(ctx->paths[v]);
             a.npaths[v] = 0;
             a.segtab[v] = P<uint2>(ctx->segtab[v]);
@@ -708,11 +737,11 @@ sm_status join(sm_ctx* ctx, hipStream_t waiter, hipStream_t src) {
     return SM_OK;
 }
 
-double bucket_voxels(sm_ctx* ctx, uint32_t r, bool long_paths, int nviews, int D) {
+double bucket_voxels(sm_ctx* ctx, uint32_t r, bool long_paths, int views, int D) {
     double n = 0;
-    for (int v = 0; v < nviews; ++v) {
+    for (int v = 0; v < 2; ++v) {
         const auto& L = ctx->layout[v];
-        if (r < L.nrounds) n += L.nodes[2 * r + (long_paths ? 0 : 1)];
+        if (view_on(views, v) && r < L.nrounds) n += L.nodes[2 * r + (long_paths ? 0 : 1)];
     }
     return n * D;
 }
@@ -720,16 +749,16 @@ double bucket_voxels(sm_ctx* ctx, uint32_t r, bool long_paths, int nviews, int D
 // One light-depth round of a pass: short paths by the chunked walkers on st, long paths by the
 // chain engine on st2, concurrently (they touch disjoint rows; both only read rows finished in
 // earlier rounds).  Rounds are ordered by joining the two streams at every round boundary.
-sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
+sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views) {
     CHECK(join(ctx, ctx->st, ctx->st2));
     CHECK(join(ctx, ctx->st2, ctx->st));
-    set_bucket(ctx, a, r, false, nviews);
+    set_bucket(ctx, a, r, false, views);
     const WalkArgs as = a;
-    CHECK(timed(ctx, ctx->st, KF_UP_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall),
+    CHECK(timed(ctx, ctx->st, KF_UP_WALK, bucket_voxels(ctx, r, false, views, a.dcall),
                 [&] { return launch_up(ctx->st, as, spl, false); }));
-    set_bucket(ctx, a, r, true, nviews);
+    set_bucket(ctx, a, r, true, views);
     const WalkArgs al = a;
-    const double vl = bucket_voxels(ctx, r, true, nviews, a.dcall);
+    const double vl = bucket_voxels(ctx, r, true, views, a.dcall);
     // segment aggregates: only buckets with a path cut into pieces need them
     const bool cut = (al.pieces[0] || al.pieces[1]) && al.maxlen >= 2 * al.piece_len;
     if (cut) CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, 0.0));
@@ -737,16 +766,16 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews) {
     return SM_OK;
 }
 
-sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int nviews, bool store_all) {
+sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views, bool store_all) {
     CHECK(join(ctx, ctx->st, ctx->st2));
     CHECK(join(ctx, ctx->st2, ctx->st));
-    set_bucket(ctx, a, r, true, nviews);
+    set_bucket(ctx, a, r, true, views);
     const WalkArgs al = a;
-    CHECK(timed(ctx, ctx->st2, KF_DOWN_CHAIN, bucket_voxels(ctx, r, true, nviews, a.dcall),
+    CHECK(timed(ctx, ctx->st2, KF_DOWN_CHAIN, bucket_voxels(ctx, r, true, views, a.dcall),
                 [&] { return launch_down_long(ctx->st2, al, spl, store_all ? 1 : 0); }));
-    set_bucket(ctx, a, r, false, nviews);
+    set_bucket(ctx, a, r, false, views);
     const WalkArgs as = a;
-    CHECK(timed(ctx, ctx->st, KF_DOWN_WALK, bucket_voxels(ctx, r, false, nviews, a.dcall), [&] {
+    CHECK(timed(ctx, ctx->st, KF_DOWN_WALK, bucket_voxels(ctx, r, false, views, a.dcall), [&] {
         return store_all ? launch_down_debug(ctx->st, as, spl, false) : launch_down(ctx->st, as, spl, false);
     }));
     return SM_OK;
@@ -810,31 +839,33 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
 }
 
 // up + down passes over all rounds for nviews views; debug_store_all stores every A row
-sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int nviews, bool debug_store_all, const WtaCfg* wta = nullptr) {
+sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int views, bool debug_store_all, const WtaCfg* wta = nullptr) {
     const size_t N = (size_t)ctx->W * ctx->H;
     const int spl = spl_for(D);
     const int Dpad = dpad_for(D);
     CHECK(ensure_filter_bufs(ctx, Dpad));
     uint32_t nr = 0;
-    for (int v = 0; v < nviews; ++v) nr = std::max(nr, ctx->layout[v].nrounds);
+    for (int v = 0; v < 2; ++v)
+        if (view_on(views, v)) nr = std::max(nr, ctx->layout[v].nrounds);
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
     if (wta) a.wta = *wta;
     CHECK(setup_sync(ctx, a, N, Dpad));
     a.vol = ctx->use_vol ? 1 : 0;
     if (a.vol)  // cost rows of every slot from the caller's volumes (slots come from the layout)
-        for (int v = 0; v < nviews; ++v)
-            HIPC(launch_vol_rows(ctx->st, P<float>(ctx->vin[v]), N, dglob0, D, Dpad, P<uint32_t>(ctx->slotpix[v]),
+        for (int v = 0; v < 2; ++v)
+            if (view_on(views, v))
+                HIPC(launch_vol_rows(ctx->st, P<float>(ctx->vin[v]), N, dglob0, D, Dpad, P<uint32_t>(ctx->slotpix[v]),
                                  P<float>(ctx->Cst[v])));
     ctx->nfev = ctx->nsev = 0;
     ctx->fam.clear();
     ctx->fam_vox.clear();
     ctx->fam_ev.clear();
     ctx->ev_open = false;
-    for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, nviews));  // deepest first
+    for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl, views));  // deepest first
     CHECK(join(ctx, ctx->st, ctx->st2));
     HIPC(hipEventRecord(ctx->ev[6], ctx->st));  // up | down boundary (stage times)
     ctx->ev_open = false;
-    for (uint32_t r = 0; r < nr; ++r) CHECK(down_round(ctx, a, r, spl, nviews, debug_store_all));
+    for (uint32_t r = 0; r < nr; ++r) CHECK(down_round(ctx, a, r, spl, views, debug_store_all));
     CHECK(join(ctx, ctx->st, ctx->st2));  // everything after the filter runs on st
     if (a.piece_dbg) {
         unsigned long long h[16];
@@ -881,7 +912,8 @@ sm_status collect_filter_stats(sm_ctx* ctx) {
 sm_status stage_reduce(sm_ctx* ctx) {
     if (!ctx->comm) return SM_OK;
     const size_t N = (size_t)ctx->W * ctx->H;
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v)) {
         CHECK(ensure(ctx, ctx->gmin[v], N * 8));
         CHECK(ensure(ctx, ctx->cand[v], N * 4));
         CHECK(ensure(ctx, ctx->gidx[v], N * 4));
@@ -890,16 +922,19 @@ sm_status stage_reduce(sm_ctx* ctx) {
     // (Stereo3DMST.cpp:177, PatchMatchStereoGPU.cu:1712) over contiguous ascending shards.
     RCCLC(ncclGroupStart());
     for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v))
         RCCLC(ncclAllReduce(ctx->minc[v].p, ctx->gmin[v].p, N, ncclFloat64, ncclMin, ctx->comm, ctx->st));
     RCCLC(ncclGroupEnd());
     if (!ctx->sub)
         for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v))
             HIPC(launch_cand(ctx->st, P<double>(ctx->minc[v]), P<double>(ctx->gmin[v]), P<int32_t>(ctx->idx[v]),
                              P<int32_t>(ctx->cand[v]), N));
     if (ctx->sub) {
         // subpixel: the candidate is (global index << 32 | float bits of the rank's subpixel disparity),
         // so the MIN over ranks carries the winning rank's disparity with the lowest index
-        for (int v = 0; v < 2; ++v) {
+        for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v)) {
             CHECK(ensure(ctx, ctx->cand[v], N * 8));
             CHECK(ensure(ctx, ctx->gidx[v], N * 8));
             HIPC(launch_cand64(ctx->st, P<double>(ctx->minc[v]), P<double>(ctx->gmin[v]), P<int32_t>(ctx->idx[v]),
@@ -907,18 +942,22 @@ sm_status stage_reduce(sm_ctx* ctx) {
         }
         RCCLC(ncclGroupStart());
         for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v))
             RCCLC(ncclAllReduce(ctx->cand[v].p, ctx->gidx[v].p, N, ncclUint64, ncclMin, ctx->comm, ctx->st));
         RCCLC(ncclGroupEnd());
         for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v))
             HIPC(launch_finalize64(ctx->st, P<double>(ctx->gmin[v]), P<unsigned long long>(ctx->gidx[v]), P<double>(ctx->minc[v]),
                                    P<int32_t>(ctx->idx[v]), P<float>(ctx->disp[v]), N));
         return SM_OK;
     }
     RCCLC(ncclGroupStart());
     for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v))
         RCCLC(ncclAllReduce(ctx->cand[v].p, ctx->gidx[v].p, N, ncclInt32, ncclMin, ctx->comm, ctx->st));
     RCCLC(ncclGroupEnd());
     for (int v = 0; v < 2; ++v)
+        if (view_on(ctx->views, v))
         HIPC(launch_finalize(ctx->st, P<double>(ctx->gmin[v]), P<int32_t>(ctx->gidx[v]), P<double>(ctx->minc[v]),
                              P<int32_t>(ctx->idx[v]), P<float>(ctx->disp[v]), N));
     return SM_OK;
@@ -1041,6 +1080,7 @@ void sm_default_params(sm_params* p) {
     p->aggregator = SM_AGG_TREE;
     p->gf_radius = 9;                                  // PatchMatchStereoGPU.cu:9001
     p->gf_eps = (float)(std::pow(0.01, 2.0) * 255 * 255);  // :9000
+    p->views = 3;                                      // both views
 }
 
 sm_status sm_device_count(int* count) {
@@ -1162,6 +1202,7 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     CHECK(check_params(ctx, p, D));
     const CallRange cr = call_range(p, D);
     ctx->use_vol = p->cost_kind == SM_COST_VOLUME;
+    ctx->views = p->views == 0 ? 3 : p->views;
     if (ctx->use_vol) {
         if (ctx->vin_D == 0) return fail(ctx, SM_ERR_STATE, "SM_COST_VOLUME: no volumes uploaded (sm_upload_cost_volumes)");
         if (ctx->vin_W != ctx->W || ctx->vin_H != ctx->H) return fail(ctx, SM_ERR_ARG, "cost volumes and images differ in size");
@@ -1190,11 +1231,11 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
         HIPC(hipEventRecord(ctx->ev[5], ctx->st));
         return SM_OK;
     }
-    CHECK(stage_tree(ctx, 2, p));
+    CHECK(stage_tree(ctx, ctx->views, p));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
-    CHECK(stage_layout(ctx, 2));
+    CHECK(stage_layout(ctx, ctx->views));
     HIPC(hipEventRecord(ctx->ev[3], ctx->st));
-    CHECK(stage_filter(ctx, cr.D, cr.d0, 2, false, &cr.w));
+    CHECK(stage_filter(ctx, cr.D, cr.d0, ctx->views, false, &cr.w));
     HIPC(hipEventRecord(ctx->ev[4], ctx->st));
     CHECK(stage_reduce(ctx));
     CHECK(stage_post(ctx, p->post, p->disp_total > 0 ? p->disp_total : p->disp_begin + D));
@@ -1229,6 +1270,7 @@ sm_status sm_download_results(sm_ctx* ctx, float* ld, float* rd, int32_t* li, in
     const size_t N = (size_t)ctx->W * ctx->H;
     void* outs[2][3] = {{ld, li, lm}, {rd, ri, rm}};
     for (int v = 0; v < 2; ++v) {
+        if (!view_on(ctx->views, v)) continue;  // a one-view call: the other view's buffers are untouched
         if (outs[v][0]) HIPC(hipMemcpyAsync(outs[v][0], ctx->disp[v].p, N * 4, hipMemcpyDeviceToHost, ctx->st));
         if (outs[v][1]) HIPC(hipMemcpyAsync(outs[v][1], ctx->idx[v].p, N * 4, hipMemcpyDeviceToHost, ctx->st));
         if (outs[v][2]) HIPC(hipMemcpyAsync(outs[v][2], ctx->minc[v].p, N * 8, hipMemcpyDeviceToHost, ctx->st));
@@ -1270,7 +1312,7 @@ sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int str
     HIPC(hipSetDevice(ctx->device));
     CHECK(upload(ctx, bgr, bgr, W, H, stride));
     CHECK(stage_prep(ctx));
-    CHECK(stage_tree(ctx, 1, p));
+    CHECK(stage_tree(ctx, 1, p));  // the image is uploaded as both views: view 0 only
     CHECK(stage_layout(ctx, 1));
     const size_t N = (size_t)W * H;
     // segment mode: the virtual edges that link the trees are not part of the reported forest
@@ -1324,8 +1366,9 @@ sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, 
     ctx->rec_pad = rec_pad_for(d0, D);
     CHECK(upload(ctx, l, r, W, H, stride));
     CHECK(stage_prep(ctx));
-    CHECK(stage_tree(ctx, 2, p));
-    CHECK(stage_layout(ctx, 2));
+    ctx->views = 3;
+    CHECK(stage_tree(ctx, 3, p));
+    CHECK(stage_layout(ctx, 3));
     const size_t N = (size_t)W * H;
     const int Dpad = dpad_for(D);
     CHECK(ensure(ctx, ctx->vol[0], N * (size_t)D * 8));
@@ -1340,7 +1383,7 @@ sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, 
         ctx->fam_vox.clear();
         ctx->fam_ev.clear();
         ctx->ev_open = false;
-        for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl_for(D), 2));
+        for (uint32_t i = 0; i < nr; ++i) CHECK(up_round(ctx, a, nr - 1 - i, spl_for(D), 3));
         CHECK(join(ctx, ctx->st, ctx->st2));
         HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->U[view]), (int)N, Dpad, D, N,
                                    P<double>(ctx->vol[0])));
@@ -1348,7 +1391,7 @@ sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, 
         HIPC(hipStreamSynchronize(ctx->st));
         CHECK(check_device_error(ctx));
     }
-    CHECK(stage_filter(ctx, D, d0, 2, true));
+    CHECK(stage_filter(ctx, D, d0, 3, true));
     HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->fix[view]), (int)N, Dpad, D, N,
                                P<double>(ctx->vol[0])));
     if (A) HIPC(hipMemcpyAsync(A, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));

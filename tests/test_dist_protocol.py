@@ -89,3 +89,75 @@ def test_shard_range_partitions():
             assert all(rs[i][0] + rs[i][1] == rs[i + 1][0] for i in range(G - 1))
     with pytest.raises(ValueError):
         shard_range(4, 8, 0)
+
+
+def _worker_vd(rank, world, port, W, H, D, out_q):
+    """View groups x disparity shards (stereomatch_amd.partition, bench.py --shard vd): the rank
+    filters its view's shard and the reduce runs inside its view group only."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from stereomatch_amd import partition
+        from tools.synth import make_pair
+        left, right, _ = make_pair(W, H, D, index=7)
+        part = partition(D, world, rank)
+        half = part["group_size"]
+        groups = [dist.new_group(list(range(g * half, (g + 1) * half))) for g in range(world // half)]
+        grp = groups[part["group"]]
+        v = "left" if part["views"] == 1 else "right"
+        d0, Dl = part["d0"], part["D"]
+        tree = O.build_tree(left if v == "left" else right)
+        lv, rv = O.cost_agd(left, right, d0, d0 + Dl)
+        tf = O.tree_filter(W, H, tree, lv if v == "left" else rv, d0, True, False, 2)
+        gmin = torch.from_numpy(tf["minc"].copy())
+        dist.all_reduce(gmin, op=dist.ReduceOp.MIN, group=grp)
+        cand = torch.where(torch.from_numpy(tf["minc"]) == gmin, torch.from_numpy(tf["idx"]),
+                           torch.tensor(0x7FFFFFFF, dtype=torch.int32))
+        dist.all_reduce(cand, op=dist.ReduceOp.MIN, group=grp)
+        out_q.put((rank, (v, gmin.numpy().tolist(), cand.numpy().tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,H,D,world", [(40, 24, 19, 2), (36, 20, 13, 4)])
+def test_view_group_partition_equals_unsharded(W, H, D, world):
+    from oracle import oracle as O
+    from tools.synth import make_pair
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_vd, args=(r, world, port, W, H, D, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    left, right, _ = make_pair(W, H, D, index=7)
+    ref = O.match(left, right, D, nthreads=2)
+    seen = set()
+    for r in range(world):
+        v, gmin, gidx = got[r]
+        seen.add(v)
+        np.testing.assert_array_equal(np.array(gidx, np.int32), ref[v]["idx"])
+        np.testing.assert_array_equal(np.array(gmin, np.float64), ref[v]["minc"])
+    assert seen == {"left", "right"}
+
+
+def test_partition_plans():
+    from stereomatch_amd import partition
+    # even N: two view groups, each covering the full range in ascending shards
+    for Dt, N in ((256, 8), (256, 2), (100, 4), (7, 6)):
+        parts = [partition(Dt, N, r) for r in range(N)]
+        for g, mask in ((0, 1), (1, 2)):
+            mine = [p for p in parts if p["group"] == g]
+            assert len(mine) == N // 2 and all(p["views"] == mask for p in mine)
+            assert sum(p["D"] for p in mine) == Dt and mine[0]["d0"] == 0
+            assert [p["group_rank"] for p in mine] == list(range(N // 2))
+    # odd N or split_views=False: both views, D over all ranks
+    for N in (1, 3):
+        parts = [partition(12, N, r) for r in range(N)]
+        assert all(p["views"] == 3 and p["group_size"] == N for p in parts)
+    assert partition(256, 8, 5, split_views=False) == dict(views=3, d0=160, D=32, group=0, group_size=8, group_rank=5)

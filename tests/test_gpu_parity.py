@@ -289,6 +289,61 @@ def test_full_size_c4_shard_with_reduce_bitexact(rank):
     np.testing.assert_array_equal(outp["right"]["disp"], rref)
 
 
+@pytest.mark.parametrize("c", [float("inf"), 5000.0])
+@pytest.mark.parametrize("W,H,D,plen", [(320, 240, 64, "64"), (256, 160, 128, None), (160, 90, 200, "64"), (200, 150, 32, None)])
+def test_one_view_calls_bitexact(gpu_ctx, monkeypatch, W, H, D, plen, c):
+    """sm_params.views = 1 / 2: a call builds and filters only that view (the multi-GPU view
+    groups); bit-exact against the oracle, MST and segment forest, cut paths too."""
+    import stereomatch_amd as sm
+    if plen:
+        monkeypatch.setenv("SM_PIECE_LEN", plen)
+    else:
+        monkeypatch.delenv("SM_PIECE_LEN", raising=False)
+    left, right, _ = make_pair(W, H, D, index=9)
+    ref = O.match(left, right, D, nthreads=16, c=c)
+    for views, v in ((1, "left"), (2, "right")):
+        out = gpu_ctx.match(left, right, D, sm.default_params(views=views, c=c))
+        assert list(out) == [v]
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+@pytest.mark.parametrize("rank", [0, 6])
+def test_full_size_c4_view_group_shard_with_reduce(rank):
+    """BASELINE C4 frame under the view-group partition (stereomatch_amd.partition, bench.py
+    --shard vd): rank r of 8 filters 64 slices of ONE view at full size and reduces through a
+    one-rank RCCL communicator (stage_reduce over its view only); bitwise equal to the oracle's
+    tree filter over that view's shard."""
+    import stereomatch_amd as sm
+    W, H, Dt = 1920, 1200, 256
+    part = sm.partition(Dt, 8, rank)
+    d0, D, views = part["d0"], part["D"], part["views"]
+    v = "left" if views == 1 else "right"
+    left, right, _ = make_pair(W, H, Dt, index=13)
+    ctx = sm.Context(0)
+    try:
+        ctx.comm_init(1, 0, sm.Context.unique_id())
+        out = ctx.match(left, right, D, sm.default_params(disp_begin=d0, disp_total=Dt, views=views))
+        assert ctx.stage_times()["reduce_ms"] > 0
+    finally:
+        ctx.close()
+    lv, rv = O.cost_agd(left, right, d0, d0 + D)
+    r = O.tree_filter(W, H, O.build_tree(left if v == "left" else right), lv if v == "left" else rv, d0, True, False, 16)
+    assert list(out) == [v]
+    np.testing.assert_array_equal(out[v]["idx"].ravel(), r["idx"])
+    assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
+
+
+def test_one_view_rejects_two_map_post(gpu_ctx):
+    import stereomatch_amd as sm
+    left, right, _ = make_pair(64, 48, 16, index=2)
+    for post in (sm.STEREO3DMST_POST, 8):
+        with pytest.raises(sm.StereoMSTError):
+            gpu_ctx.match(left, right, 16, sm.default_params(views=1, post=post))
+    with pytest.raises(sm.StereoMSTError):
+        gpu_ctx.match(left, right, 16, sm.default_params(views=4))
+
+
 def test_chain_wait_timeout_is_an_error(monkeypatch):
     """A cross-workgroup wait of the chain engine that never sees its status word must not return
     SM_OK: SM_WAIT_ITERS=0 makes every such wait give up at once, which sets the call's device error
