@@ -252,6 +252,7 @@ struct ViewSet {
     explicit ViewSet(int mask) {
         for (int q = 0; q < 2; ++q)
             if ((mask >> q) & 1) v[n++] = q;
+        if (n == 1) v[1] = v[0];  // an unused kernel slot aliases the active view: never an unallocated buffer
     }
 };
 inline bool view_on(int mask, int v) { return ((mask >> v) & 1) != 0; }
@@ -370,7 +371,8 @@ sm_status stage_mst(sm_ctx* ctx, int views) {
     CHECK(ensure(ctx, ctx->changed, 2 * SM_MST_MAX_ROUNDS * sizeof(int)));
     CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
     ZeroList z{};
-    for (int v = 0; v < 2; ++v) {
+    for (int i = 0; i < nviews; ++i) {  // the active views only: an inactive view's buffers may not exist
+        const int v = vs.v[i];
         CHECK(ensure(ctx, ctx->ccnt[v], 16));
         z.add(ctx->mR[v].p, N);
         z.add(ctx->mD[v].p, N);
@@ -784,6 +786,7 @@ sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views, b
 sm_status ensure_filter_bufs(sm_ctx* ctx, int Dpad) {
     const size_t N = (size_t)ctx->W * ctx->H;
     for (int v = 0; v < 2; ++v) {
+        if (!view_on(ctx->views, v)) continue;  // a one-view call: the kernels never touch the other view's rows
         CHECK(ensure(ctx, ctx->U[v], N * (size_t)Dpad * 8));
         if (ctx->use_vol) CHECK(ensure(ctx, ctx->Cst[v], N * (size_t)Dpad * 4));  // ingested cost rows only
         CHECK(ensure(ctx, ctx->idx[v], N * 4));
@@ -822,8 +825,10 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
         a.piece_dbg = P<unsigned long long>(ctx->pdbg);
     }
     for (int v = 0; v < 2; ++v) {
-        CHECK(ensure(ctx, ctx->agg[v], pcap * 2 * (size_t)Dpad * 8));
-        CHECK(ensure(ctx, ctx->fix[v], N * (size_t)Dpad * 8));
+        if (view_on(ctx->views, v)) {
+            CHECK(ensure(ctx, ctx->agg[v], pcap * 2 * (size_t)Dpad * 8));
+            CHECK(ensure(ctx, ctx->fix[v], N * (size_t)Dpad * 8));
+        }
         a.fix[v] = P<double>(ctx->fix[v]);  // up pass: buffered repair rows
         a.A[v] = a.fix[v];                  // down pass: A rows
         const bool fresh = ctx->pstat[v].n < pcap * 8 * 4;

@@ -1013,7 +1013,8 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
 #pragma unroll
             for (int q = 0; q < SPL; ++q) {
                 x[q] = acc[q] + (double)cr[k][q];
-                eq = eq && __double_as_longlong(x[q]) == __double_as_longlong(spec[k][q]);
+                // lanes beyond a 32-double row hold nothing (cost 3.0 there, stored rows read 0)
+                eq = eq && (!row_lane<SPL>(lane, Dpad) || __double_as_longlong(x[q]) == __double_as_longlong(spec[k][q]));
             }
             if (__all(eq)) return n0 + k;
             if (!write) continue;
@@ -1617,7 +1618,8 @@ __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta
                 for (int q = 0; q < SPL; ++q) {
                     x[q] = __builtin_fma(S, x[q], S2 * u[k][q]);
                     ys[k][q] = x[q];
-                    eq = eq && __double_as_longlong(x[q]) == __double_as_longlong(spec[k][q]);
+                    // lanes beyond a 32-double row hold nothing (cost 3.0 there, stored rows read 0)
+                eq = eq && (!row_lane<SPL>(lane, Dpad) || __double_as_longlong(x[q]) == __double_as_longlong(spec[k][q]));
                 }
                 const bool stored = store_all || hi_light(mfield(mv, k, 3)) || (last_pub && n0 + k == len - 1);
                 if (check && stored && __all(eq)) mk = k;

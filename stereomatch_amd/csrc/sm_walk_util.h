@@ -23,19 +23,7 @@ struct WalkView {
 #define S_ZERO SM_NUM_W    // LDS S-table entry holding 0.0 (absent children)
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-// 0.114f*B + 0.587f*G + 0.299f*R, left to right, no contraction (PatchMatchStereoGPU.cu:1529)
-__device__ __forceinline__ float gray_of(uint32_t bgrx) {
-    const float b = (float)(bgrx & 255u), g = (float)((bgrx >> 8) & 255u), r = (float)((bgrx >> 16) & 255u);
-    float t = 0.114f * b;
-    t = t + 0.587f * g;
-    t = t + 0.299f * r;
-    return t;
-}
-#ifdef SM_EXP_RECX  // timing experiment: records' colour word only, gray recomputed (bit-identical)
-__device__ __forceinline__ float rgray(uint2 r) { return gray_of(r.x); }
-#else
 __device__ __forceinline__ float rgray(uint2 r) { return __uint_as_float(r.y); }
-#endif
 
 // AGD cost (PatchMatchStereoGPU.cu:1518-1543) from {bgrx, gray} records:
 // r0 = right(x), l0 = left(x+d), gr1 = gray(right(x+1)), gl1 = gray(left(x+d+1))
@@ -323,15 +311,9 @@ __device__ __forceinline__ void load_recs(const MetaVec<CH>& mv, int n, int view
         const int jj = j < n ? j : n - 1;
         const long long pix = (long long)mfield(mv, jj, 0);  // = y*W + x: no division needed here
         const long long base = view ? pix + dbase : pix - dbase - (SPL - 1);
-#ifdef SM_EXP_RECX
-#pragma unroll
-        for (int q = 0; q < SPL; ++q) r.ob[j][q] = make_uint2(reinterpret_cast<const uint32_t*>(oth + base + q)[0], 0u);
-        r.obg[j] = __uint_as_float(reinterpret_cast<const uint32_t*>(oth + base + SPL)[0]);  // colour: gray below
-#else
 #pragma unroll
         for (int q = 0; q < SPL; ++q) r.ob[j][q] = oth[base + q];
         r.obg[j] = __uint_as_float(reinterpret_cast<const uint32_t*>(oth + base + SPL)[1]);
-#endif
     }
 }
 
@@ -339,14 +321,7 @@ __device__ __forceinline__ void load_recs(const MetaVec<CH>& mv, int n, int view
 // d beyond the call's range) -> 3.0 as the reference (PatchMatchStereoGPU.cu:1501-1549)
 template <int SPL, int CH, class T>
 __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int W, int dbase, int dend,
-                                            const ImgRecs<SPL, CH>& r0, const float* __restrict__ atab, T (&c)[CH][SPL]) {
-#ifdef SM_EXP_RECX
-    ImgRecs<SPL, CH> r = r0;
-#pragma unroll
-    for (int j = 0; j < CH; ++j) r.obg[j] = gray_of(__float_as_uint(r0.obg[j]));
-#else
-    const ImgRecs<SPL, CH>& r = r0;
-#endif
+                                            const ImgRecs<SPL, CH>& r, const float* __restrict__ atab, T (&c)[CH][SPL]) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const int x = pix_col((int)mfield(mv, j, 0), W);
