@@ -38,12 +38,14 @@ def shard_range(d_total, nranks, rank):
 
 def partition(d_total, nranks, rank, split_views=True):
     """The share of one frame (both views, d_total disparities each) that `rank` of `nranks` owns
-    (DESIGN.md 7).  With split_views and an even nranks, the ranks form two view groups -- ranks
-    [0, N/2) the left view, [N/2, N) the right view -- and each group D-shards its view over its
-    N/2 ranks: a rank builds one tree and filters d_total / (N/2) slices of one view, and the WTA
-    reduce runs inside its group.  Otherwise every rank takes both views and d_total / N slices.
+    (DESIGN.md 7).  With split_views, an even nranks and at most 128 slices per rank after the
+    split, the ranks form two view groups -- ranks [0, N/2) the left view, [N/2, N) the right view
+    -- and each group D-shards its view over its N/2 ranks: a rank builds one tree and filters
+    d_total / (N/2) slices of one view, and the WTA reduce runs inside its group.  Otherwise every
+    rank takes both views and d_total / N slices (measured at C4: one view of 256 slices is slower
+    than both views of 128, so N = 2 keeps both views).
     Returns dict(views, d0, D, group, group_size, group_rank): views is the sm_params.views mask."""
-    if split_views and nranks >= 2 and nranks % 2 == 0:
+    if split_views and nranks >= 2 and nranks % 2 == 0 and -(-d_total // (nranks // 2)) <= 128:
         half = nranks // 2
         group, grank = divmod(rank, half)
         d0, D = shard_range(d_total, half, grank)

@@ -149,7 +149,7 @@ def test_view_group_partition_equals_unsharded(W, H, D, world):
 def test_partition_plans():
     from stereomatch_amd import partition
     # even N: two view groups, each covering the full range in ascending shards
-    for Dt, N in ((256, 8), (256, 2), (100, 4), (7, 6)):
+    for Dt, N in ((256, 8), (256, 4), (128, 2), (100, 4), (7, 6)):
         parts = [partition(Dt, N, r) for r in range(N)]
         for g, mask in ((0, 1), (1, 2)):
             mine = [p for p in parts if p["group"] == g]
@@ -161,3 +161,5 @@ def test_partition_plans():
         parts = [partition(12, N, r) for r in range(N)]
         assert all(p["views"] == 3 and p["group_size"] == N for p in parts)
     assert partition(256, 8, 5, split_views=False) == dict(views=3, d0=160, D=32, group=0, group_size=8, group_rank=5)
+    # one view of more than 128 slices per rank: both views instead (N = 2 at D = 256)
+    assert [partition(256, 2, r)["views"] for r in range(2)] == [3, 3]
