@@ -762,7 +762,7 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views) {
     const WalkArgs al = a;
     const double vl = bucket_voxels(ctx, r, true, views, a.dcall);
     // segment aggregates: only buckets with a path cut into pieces need them
-    const bool cut = (al.pieces[0] || al.pieces[1]) && al.maxlen >= 2 * al.piece_len;
+    const bool cut = (al.pieces[0] || al.pieces[1]) && sm_piece_cut((uint32_t)al.maxlen, (uint32_t)al.piece_len);
     if (cut) CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, 0.0));
     CHECK(timed(ctx, ctx->st2, KF_UP_CHAIN, vl, [&] { return launch_up_chain(ctx->st2, al, spl); }));
     return SM_OK;

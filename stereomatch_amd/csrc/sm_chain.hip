@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     const SmPath path = (view ? paths1 : paths0)[uniform(sg.x)];
     const int head = (int)uniform(path.head), len = (int)uniform(path.len);
     double* __restrict__ agg = view ? agg1 : agg0;
-    if (agg == nullptr || len < 2 * piece_len) return;  // an uncut path: uniform over the block
+    if (agg == nullptr || !sm_piece_cut((uint32_t)len, (uint32_t)piece_len)) return;  // an uncut path: uniform over the block
     __shared__ WalkShared sh;
     __shared__ double aggsh[NW][2][64 * SPL];
     load_tables(sh, atab_g, slut_g, s2lut_g);
@@ -1137,7 +1137,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
         const SmPath last = pp[uniform(pc.x + pc.w - 1u)];
         plen = (int)uniform(last.head + last.len - path.head);
     }
-    const int o0 = j * Q.plen, o1 = j + 1 == M ? plen : (j + 1) * Q.plen;
+    const int o0 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)j, (uint32_t)Q.plen);
+    const int o1 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)j + 1u, (uint32_t)Q.plen);
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
     const bool lower = j + 1 < M;
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1758,7 +1759,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
         const SmPath last = pp[uniform(pc.x + pc.w - 1u)];
         plen = (int)uniform(last.head + last.len - path.head);
     }
-    const int o0 = i * Q.plen, o1 = i + 1 == M ? plen : (i + 1) * Q.plen;
+    const int o0 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)i, (uint32_t)Q.plen);
+    const int o1 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)i + 1u, (uint32_t)Q.plen);
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (int k = threadIdx.x; k < SM_NUM_W; k += CHN_THREADS) {

@@ -11,12 +11,36 @@
 #define SM_LONG_PATH 32   // paths of >= this many nodes go to the long-path chain engine (sm_chain.hip)
 #endif
 #define SM_PRE_SEG 32     // nodes per k_up_pre block (segment table granularity)
-// A long path of >= 2*P nodes is cut into len/P pieces of P nodes (the bottom piece takes the
-// remainder); the pieces' chains run concurrently from guessed inputs and are then repaired
+// A long path of >= 2P nodes is cut into len/P pieces of P nodes (the bottom piece takes the
+// remainder, < 2P); the pieces' chains run concurrently from guessed inputs and are then repaired
 // exactly (sm_chain.hip, "Pieces").  P = SM_PIECE by default (env SM_PIECE_LEN: a multiple of
 // SM_PRE_SEG, >= 64; tests use short pieces to exercise the repair on small images).
+// -DSM_PIECE_BALANCED (A/B): cut every path of > P nodes into ceil(len/P) balanced pieces.  Measured
+// at C2 it is slower (up pre + chain 1.23 vs 1.12 ms): more cut paths need segment aggregates and
+// repairs, and a round's time is set by the CUs' queues of work items, not by its longest piece.
 #ifndef SM_PIECE
 #define SM_PIECE 512
+#endif
+#ifndef SM_PIECE_BALANCED
+__host__ __device__ static inline bool sm_piece_cut(uint32_t len, uint32_t plen) { return len >= 2 * plen; }
+__host__ __device__ static inline uint32_t sm_piece_count(uint32_t len, uint32_t plen) {
+    return len >= 2 * plen ? len / plen : 1u;
+}
+__host__ __device__ static inline uint32_t sm_piece_begin_p(uint32_t len, uint32_t M, uint32_t j, uint32_t plen) {
+    return j >= M ? len : j * plen;
+}
+#else
+__host__ __device__ static inline bool sm_piece_cut(uint32_t len, uint32_t plen) { return len > plen; }
+__host__ __device__ static inline uint32_t sm_piece_count(uint32_t len, uint32_t plen) {
+    return len > plen ? (len + plen - 1) / plen : 1u;
+}
+// first node (from the path head) of piece j of M; j == M gives len
+__host__ __device__ static inline uint32_t sm_piece_begin_p(uint32_t len, uint32_t M, uint32_t j, uint32_t plen) {
+    (void)plen;
+    if (j >= M) return len;
+    const uint32_t b = (uint32_t)(((uint64_t)len * j / M + SM_PRE_SEG / 2) / SM_PRE_SEG * SM_PRE_SEG);
+    return b < len ? b : len;
+}
 #endif
 
 struct LayoutView {

@@ -672,7 +672,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
 // segment table of the long-path buckets: segment i of bucket b -> {path within b, SM_PRE_SEG-node
 // segment of that path}, so k_up_pre launches exactly one block per segment; and the chain work
 // items of the bucket ("pieces"):
-//  * a path of len >= 2*plen nodes gives M = len / plen pieces {path, j, M, first segment of the
+//  * a path of len > plen nodes gives M = ceil(len / plen) balanced pieces {path, j, M, first segment of the
 //    path}, listed bottom piece first (the chain launches wait only on lower entries);
 //  * the other paths are packed into runs of consecutive paths (one contiguous slot range): a
 //    path starts a new run when its bucket slot offset enters a new window of rwin nodes (or
@@ -723,7 +723,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
                 const SmPath path = p < p1 ? V.paths[p] : SmPath{hbase, 0u};
                 len[i] = path.len;
                 ns[i] = (len[i] + SM_PRE_SEG - 1) / SM_PRE_SEG;
-                cut[i] = len[i] >= 2u * plen;
+                cut[i] = sm_piece_cut(len[i], plen);
                 win[i] = (path.head - hbase) / rwin;
             }
             // previous path's window / cut flag (thread 0: the last path of the previous chunk)
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 start[i] = !cut[i] && ((pv & 1u) || (pv >> 1) != win[i]);
-                np[i] = pb + (uint32_t)i < p1 ? (cut[i] ? len[i] / plen : (start[i] ? 1u : 0u)) : 0u;
+                np[i] = pb + (uint32_t)i < p1 ? (cut[i] ? sm_piece_count(len[i], plen) : (start[i] ? 1u : 0u)) : 0u;
                 pv = (win[i] << 1) | (cut[i] ? 1u : 0u);
                 tns += ns[i];
                 tnp += np[i];
