@@ -645,6 +645,7 @@ void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int views
             a.nseg[v] = 0;
             a.pieces[v] = nullptr;
             a.npieces[v] = 0;
+            a.bucket_plen[v] = a.piece_len;
         } else {
             const uint32_t b = 2 * r + (long_paths ? 0 : 1);
             a.paths[v] = P<SmPath>(ctx->paths[v]) + L.begin[b];
@@ -655,6 +656,7 @@ void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int views
             // long buckets: pieces (sm_chain.hip "Pieces"), unless SM_NO_PIECES (A/B)
             const bool pieces = long_paths && ctx->agg[v].p && !no_pieces();
             a.pieces[v] = pieces ? P<uint4>(ctx->pieces[v]) + L.piece_begin[b] : nullptr;
+            a.bucket_plen[v] = (int)sm_bucket_piece_len(L.nodes[b], (uint32_t)a.piece_len);
             a.npieces[v] = pieces ? (int)(L.piece_begin[b + 1] - L.piece_begin[b]) : 0;
             a.agg[v] = pieces ? P<double>(ctx->agg[v]) + (size_t)L.seg_begin[b] * 2 * a.Dpad : nullptr;
             a.pstat[v] = pieces ? P<uint32_t>(ctx->pstat[v]) + L.piece_begin[b] : nullptr;
@@ -762,7 +764,9 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views) {
     const WalkArgs al = a;
     const double vl = bucket_voxels(ctx, r, true, views, a.dcall);
     // segment aggregates: only buckets with a path cut into pieces need them
-    const bool cut = (al.pieces[0] || al.pieces[1]) && sm_piece_cut((uint32_t)al.maxlen, (uint32_t)al.piece_len);
+    bool cut = false;
+    for (int v = 0; v < 2; ++v)
+        cut = cut || (al.pieces[v] && sm_piece_cut((uint32_t)al.maxlen, (uint32_t)al.bucket_plen[v]));
     if (cut) CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, 0.0));
     CHECK(timed(ctx, ctx->st2, KF_UP_CHAIN, vl, [&] { return launch_up_chain(ctx->st2, al, spl); }));
     return SM_OK;

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     const uint2* __restrict__ seg1, int nseg0, int nseg1, const float* __restrict__ Cst0, const float* __restrict__ Cst1,
     const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec, const float* __restrict__ atab_g,
     const double* __restrict__ slut_g, const double* __restrict__ s2lut_g, int W, int Dpad, int dcall, int dglob0,
-    double* __restrict__ agg0, double* __restrict__ agg1, int piece_len) {
+    double* __restrict__ agg0, double* __restrict__ agg1, int plen0, int plen1) {
     constexpr int NW = SM_PRE_SEG / CH;
     const int view = blockIdx.y;
     if ((int)blockIdx.x >= (view ? nseg1 : nseg0)) return;  // uniform over the block
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
     const SmPath path = (view ? paths1 : paths0)[uniform(sg.x)];
     const int head = (int)uniform(path.head), len = (int)uniform(path.len);
     double* __restrict__ agg = view ? agg1 : agg0;
-    if (agg == nullptr || !sm_piece_cut((uint32_t)len, (uint32_t)piece_len)) return;  // an uncut path: uniform over the block
+    if (agg == nullptr || !sm_piece_cut((uint32_t)len, (uint32_t)(view ? plen1 : plen0))) return;  // uncut: uniform
     __shared__ WalkShared sh;
     __shared__ double aggsh[NW][2][64 * SPL];
     load_tables(sh, atab_g, slut_g, s2lut_g);
@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     Q.fix = view ? Q1.fix : Q0.fix;
     Q.stat = view ? Q1.stat : Q0.stat;
     Q.stride = Q0.stride;
-    Q.plen = Q0.plen;
+    Q.plen = view ? Q1.plen : Q0.plen;
     Q.rmax = Q0.rmax;
     Q.dbg = Q0.dbg;
     Q.err = Q0.err;
@@ -1736,7 +1736,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     Q.fix = nullptr;
     Q.stat = view ? Q1.stat : Q0.stat;
     Q.stride = Q0.stride;
-    Q.plen = Q0.plen;
+    Q.plen = view ? Q1.plen : Q0.plen;
     Q.rmax = Q0.rmax;
     Q.dbg = Q0.dbg;
     Q.err = Q0.err;
@@ -1831,7 +1831,8 @@ static void up_pre_launch_k(hipStream_t st, const WalkArgs& a) {
                        chain_view(a, 1), reinterpret_cast<const uint32_t*>(a.meta[0]),
                        reinterpret_cast<const uint32_t*>(a.meta[1]), a.paths[0], a.paths[1], a.segtab[0], a.segtab[1],
                        a.nseg[0], a.nseg[1], a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad,
-                       a.dcall, a.dglob0, a.pieces[0] ? a.agg[0] : nullptr, a.pieces[1] ? a.agg[1] : nullptr, a.piece_len);
+                       a.dcall, a.dglob0, a.pieces[0] ? a.agg[0] : nullptr, a.pieces[1] ? a.agg[1] : nullptr, a.bucket_plen[0],
+                       a.bucket_plen[1]);
 }
 
 template <int SPL, int CH>
@@ -1843,7 +1844,7 @@ static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
 }
 
 static PieceView piece_view(const WalkArgs& a, int v) {
-    return PieceView{a.pieces[v], a.npieces[v], a.agg[v], a.fix[v], a.pstat[v], a.pstride, a.piece_len, a.repair_max, a.piece_dbg,
+    return PieceView{a.pieces[v], a.npieces[v], a.agg[v], a.fix[v], a.pstat[v], a.pstride, a.bucket_plen[v], a.repair_max, a.piece_dbg,
                      a.err, a.wait_iters};
 }
 

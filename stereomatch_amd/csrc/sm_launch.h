@@ -80,7 +80,8 @@ struct WalkArgs {
     double* agg[2];       // per bucket segment: [P row | B row] (2 * Dpad doubles), affine aggregates
     uint32_t* pstat[2];   // status words of the bucket's first piece: done / merged / final at
     int pstride;          // offsets 0, pstride, 2 * pstride
-    int piece_len;
+    int piece_len;        // P (SM_PIECE or env SM_PIECE_LEN)
+    int bucket_plen[2];   // the current long bucket's piece length per view (sm_bucket_piece_len)
     int repair_max;       // fast-repair node cap (env SM_REPAIR_MAX; tests force the slow path)
     unsigned long long* piece_dbg;  // SM_PIECE_DEBUG counters (nullptr otherwise)
     uint32_t* err;        // device error word of the call (host-mapped; sm_synchronize checks it)

@@ -21,6 +21,21 @@
 #ifndef SM_PIECE
 #define SM_PIECE 512
 #endif
+// Piece length of a long bucket of `nodes` nodes (one view).  P everywhere by default.  With
+// -DSM_ADAPT_PIECES (A/B), a bucket too small to give every CU a work item (the root path's round:
+// ~15k nodes per view) gets pieces of ~nodes/128 (two views share 256 CUs), not below 256 nodes.
+// Measured at C2: the down chain gains 0.03 ms, the up chain loses 0.75 ms -- at 256 nodes the up
+// pieces' repairs stop merging inside their pieces and take the serial slow path.
+__host__ __device__ static inline uint32_t sm_bucket_piece_len(uint32_t nodes, uint32_t plen) {
+#ifndef SM_ADAPT_PIECES
+    (void)nodes;
+    return plen;
+#endif
+    if (plen < SM_PIECE || nodes >= 128u * plen) return plen;
+    uint32_t p = (nodes / 128u + SM_PRE_SEG - 1) / SM_PRE_SEG * SM_PRE_SEG;
+    p = p < 256u ? 256u : p;
+    return p < plen ? p : plen;
+}
 #ifndef SM_PIECE_BALANCED
 __host__ __device__ static inline bool sm_piece_cut(uint32_t len, uint32_t plen) { return len >= 2 * plen; }
 __host__ __device__ static inline uint32_t sm_piece_count(uint32_t len, uint32_t plen) {

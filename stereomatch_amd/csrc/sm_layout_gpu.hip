@@ -704,6 +704,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
         if (p0 == p1) continue;  // uniform
         const uint32_t sbase = running;  // the bucket's first segment
         const uint32_t hbase = hb[b];
+        const uint32_t pl = sm_bucket_piece_len(rn[b], plen);  // this bucket's piece length
         // run window: ~3 runs per CU over both views (256 CUs), 64 .. plen nodes
         const uint32_t rwin = min(rcap, max(64u, rn[b] / rdiv));
         if (threadIdx.x == 0) {
@@ -723,7 +724,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
                 const SmPath path = p < p1 ? V.paths[p] : SmPath{hbase, 0u};
                 len[i] = path.len;
                 ns[i] = (len[i] + SM_PRE_SEG - 1) / SM_PRE_SEG;
-                cut[i] = sm_piece_cut(len[i], plen);
+                cut[i] = sm_piece_cut(len[i], pl);
                 win[i] = (path.head - hbase) / rwin;
             }
             // previous path's window / cut flag (thread 0: the last path of the previous chunk)
@@ -734,7 +735,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 start[i] = !cut[i] && ((pv & 1u) || (pv >> 1) != win[i]);
-                np[i] = pb + (uint32_t)i < p1 ? (cut[i] ? sm_piece_count(len[i], plen) : (start[i] ? 1u : 0u)) : 0u;
+                np[i] = pb + (uint32_t)i < p1 ? (cut[i] ? sm_piece_count(len[i], pl) : (start[i] ? 1u : 0u)) : 0u;
                 pv = (win[i] << 1) | (cut[i] ? 1u : 0u);
                 tns += ns[i];
                 tnp += np[i];
