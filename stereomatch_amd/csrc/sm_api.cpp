@@ -89,7 +89,7 @@ struct sm_ctx {
     DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
     DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
     DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2], slot2pix[2], prec[2];
-    DevBuf pieces[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
+    DevBuf pieces[2], pieces_tmp[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
     DevBuf cnw[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
     uint32_t* h_err = nullptr;  // pinned, device-visible error word of the chain engine's waits
@@ -515,6 +515,7 @@ sm_status stage_layout(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->rounds[v], RREC * 4));
         CHECK(ensure(ctx, ctx->segtab[v], (N / 16 + 64) * sizeof(uint2)));  // <= N/32 segments + N/32 long paths
         CHECK(ensure(ctx, ctx->pieces[v], (N / 16 + 64) * sizeof(uint4)));  // <= N/32 long paths + N/SM_PIECE
+        CHECK(ensure(ctx, ctx->pieces_tmp[v], (N / 16 + 64) * sizeof(uint4)));
         CHECK(ensure(ctx, ctx->pathpos[v], N * 4));
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
         CHECK(ensure(ctx, ctx->nslot[v], N * 4));
@@ -571,6 +572,7 @@ sm_status stage_layout(sm_ctx* ctx, int views) {
         L.segtab = P<uint2>(ctx->segtab[v]);
         L.piece_begin = R + 6 * SM_NBUCKETS + 4;
         L.pieces = P<uint4>(ctx->pieces[v]);
+        L.pieces_tmp = P<uint4>(ctx->pieces_tmp[v]);
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
     LP.mst_ok = P<int>(ctx->mst_ok);
@@ -1172,7 +1174,7 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cnw[v],
                          &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
                          &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
-                         &ctx->nslot[v], &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->prec[v], &ctx->pieces[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
+                         &ctx->nslot[v], &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->prec[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }

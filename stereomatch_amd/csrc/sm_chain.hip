@@ -43,6 +43,35 @@
 // wait cycles (device printf) -- a diagnostic build only (tools/chain_prof.sh)
 #ifdef SM_CHAIN_PROF
 #include <stdio.h>
+#endif
+#ifdef SM_CHAIN_TIMES
+// diagnostic build: every chain workgroup appends {tag | view | M | len, start, end, item} (100 MHz
+// s_memrealtime) to a device log, read by sm_chain_times_dump (tools/chain_times.py)
+#define SM_CT_CAP 65536
+__device__ unsigned long long g_ct[4 * SM_CT_CAP];
+__device__ unsigned int g_ct_n;
+__device__ __forceinline__ void ct_log(int down, int view, int M, int len, int item, unsigned long long t0) {
+    const unsigned k = atomicAdd(&g_ct_n, 1u);
+    if (k < SM_CT_CAP) {
+        g_ct[4 * k] = (unsigned long long)down | ((unsigned long long)view << 1) | ((unsigned long long)M << 8) |
+                      ((unsigned long long)len << 32);
+        g_ct[4 * k + 1] = t0;
+        g_ct[4 * k + 2] = __builtin_amdgcn_s_memrealtime();
+        g_ct[4 * k + 3] = (unsigned long long)item;
+    }
+}
+extern "C" int sm_chain_times_dump(unsigned long long* out, int cap) {
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_ct_n), sizeof(n)) != hipSuccess) return -1;
+    n = n < SM_CT_CAP ? n : SM_CT_CAP;
+    n = (int)n < cap ? n : (unsigned)cap;
+    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ct), (size_t)n * 32) != hipSuccess) return -1;
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ct_n), &z, sizeof(z)) != hipSuccess) return -1;
+    return (int)n;
+}
+#endif
+#ifdef SM_CHAIN_PROF
 __device__ unsigned long long g_spins;
 #define PROF_SPIN(x) (x)
 #else
@@ -940,7 +969,7 @@ __device__ void up_guess(double* scratch, double* guess, const double* __restric
 // CHR nodes: the next batch's metadata is in flight during a batch, the first light child row of
 // every node is loaded with the batch, further light children (rare) on demand.
 #ifndef UP_WALK_CH
-#define UP_WALK_CH(SPL) ((SPL) == 4 ? 2 : 4)  // nodes per repair batch (registers: the image records)
+#define UP_WALK_CH(SPL) ((SPL) == 4 ? 2 : 6)  // nodes per repair batch (registers: the image records)
 #endif
 template <int SPL, int CHR, bool AGD>
 __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32, double* __restrict__ U,
@@ -1142,6 +1171,9 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
     const bool lower = j + 1 < M;
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#ifdef SM_CHAIN_TIMES  // diagnostic build: per-workgroup start / end (100 MHz) of every chain launch
+    const unsigned long long tt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     static_assert(sizeof(ring.s) >= (size_t)CHN_WAVES * 2 * 64 * SPL * sizeof(double), "prologue scratch");
     if (lower) {  // guessed input: the aggregates of the segments below the piece
         const int sb = o1 / SM_PRE_SEG, ns = (plen + SM_PRE_SEG - 1) / SM_PRE_SEG - sb;
@@ -1176,6 +1208,10 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
         vm_drain();  // this helper's stores are complete before the repair reads or overwrites them
         if (lane == 0) atomicAdd(&hdone, 1);
     }
+#ifdef SM_CHAIN_TIMES
+    __syncthreads();
+    if (threadIdx.x == 0) ct_log(0, (int)blockIdx.y, M, len, e, tt0);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1762,6 +1798,9 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     const int o0 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)i, (uint32_t)Q.plen);
     const int o1 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)i + 1u, (uint32_t)Q.plen);
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (int k = threadIdx.x; k < SM_NUM_W; k += CHN_THREADS) {
         ring.slut[k] = slut_g[k];
@@ -1813,6 +1852,10 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
         vm_drain();  // this helper's stores are complete before the repair overwrites them
         if (lane == 0) atomicAdd(&hdone, 1);
     }
+#ifdef SM_CHAIN_TIMES
+    __syncthreads();
+    if (threadIdx.x == 0) ct_log(1, (int)blockIdx.y, M, len, pidx, tt0);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -108,6 +108,7 @@ struct LayoutView {
     uint32_t* seg_begin;     // SM_NBUCKETS + 1: first segment of each bucket in segtab
     uint2* segtab;           // {path index within its bucket, segment within the path}
     uint32_t* piece_begin;   // SM_NBUCKETS + 1: first piece of each bucket in pieces
+    uint4* pieces_tmp;       // scratch of the items' longest-first reordering (k_long_segments)
     uint4* pieces;           // {path index within its bucket, j, M, first segment of the path
                              //  within the bucket}; piece j of M (0 = top), per path bottom first
     uint32_t* nrounds;

@@ -703,6 +703,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
         const uint32_t p0 = rb[b], p1 = rb[b + 1];
         if (p0 == p1) continue;  // uniform
         const uint32_t sbase = running;  // the bucket's first segment
+        const uint32_t ibase = prun;     // and its first work item
         const uint32_t hbase = hb[b];
         const uint32_t pl = sm_bucket_piece_len(rn[b], plen);  // this bucket's piece length
         // run window: ~3 runs per CU over both views (256 CUs), 64 .. plen nodes
@@ -727,16 +728,21 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
                 cut[i] = sm_piece_cut(len[i], pl);
                 win[i] = (path.head - hbase) / rwin;
             }
-            // previous path's window / cut flag (thread 0: the last path of the previous chunk)
-            sp[threadIdx.x] = (win[3] << 1) | (cut[3] ? 1u : 0u);
+            // previous path's window / alone flag (thread 0: the last path of the previous chunk).
+            // A path is alone -- never shares a run -- when it is cut or longer than the run window:
+            // a long uncut path then is one item, not the tail of a run of up to 2.5 windows
+            bool alone[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) alone[i] = cut[i] || len[i] > rwin;
+            sp[threadIdx.x] = (win[3] << 1) | (alone[3] ? 1u : 0u);
             __syncthreads();
             uint32_t pv = threadIdx.x ? sp[threadIdx.x - 1] : ((prev_win << 1) | prev_cut);
             uint32_t tns = 0, tnp = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                start[i] = !cut[i] && ((pv & 1u) || (pv >> 1) != win[i]);
+                start[i] = !cut[i] && (alone[i] || (pv & 1u) || (pv >> 1) != win[i]);
                 np[i] = pb + (uint32_t)i < p1 ? (cut[i] ? sm_piece_count(len[i], pl) : (start[i] ? 1u : 0u)) : 0u;
-                pv = (win[i] << 1) | (cut[i] ? 1u : 0u);
+                pv = (win[i] << 1) | (alone[i] ? 1u : 0u);
                 tns += ns[i];
                 tnp += np[i];
             }
@@ -745,7 +751,7 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
                 ((unsigned long long)tns << 32) | tnp, sc, &tot);
             if (threadIdx.x == 1023) {
                 prev_win = win[3];
-                prev_cut = cut[3] ? 1u : 0u;
+                prev_cut = alone[3] ? 1u : 0u;
             }
             uint32_t seg = running + (uint32_t)(ex >> 32), item = prun + (uint32_t)ex;
 #pragma unroll
@@ -772,6 +778,48 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
                 item += np[i];
                 if (pb + (uint32_t)i < p1 && !cut[i]) atomicAdd(reinterpret_cast<uint32_t*>(V.pieces + (item - 1u)) + 3, 1u);
             }
+            __syncthreads();
+        }
+        // Longest first: a chain launch runs one workgroup per CU and the CUs take items in index
+        // order, so a long item that starts late sets the round's end.  Items are regrouped as
+        // [pieces of cut paths, in their order (the look-back needs a path's pieces contiguous,
+        // bottom first) | runs longer than the run window | the other runs], each group stable.
+        {
+            const uint32_t ib = ibase, ie = prun;
+            auto klass = [&](uint32_t it) -> uint32_t {
+                const uint4 pc = V.pieces[it];
+                if (pc.z > 1u) return 0u;
+                const SmPath f = V.paths[p0 + pc.x], l = V.paths[p0 + pc.x + pc.w - 1u];
+                return (l.head + l.len - f.head) > rwin ? 1u : 2u;
+            };
+            // pass 1: class totals; pass 2: stable scatter into the scratch; then copy back
+            unsigned long long tall = 0;
+            for (uint32_t c = ib; c < ie; c += 1024) {
+                const uint32_t it = c + threadIdx.x;
+                const unsigned long long f = it < ie ? 1ull << (21 * klass(it)) : 0ull;
+                unsigned long long t;
+                block_exclusive_scan<unsigned long long, OpAdd>(f, sc, &t);
+                tall += t;
+            }
+            const uint32_t n0 = (uint32_t)(tall & 0x1FFFFF), n1 = (uint32_t)((tall >> 21) & 0x1FFFFF);
+            unsigned long long run = 0;
+            for (uint32_t c = ib; c < ie; c += 1024) {
+                const uint32_t it = c + threadIdx.x;
+                const uint32_t k = it < ie ? klass(it) : 3u;
+                const unsigned long long f = k < 3u ? 1ull << (21 * k) : 0ull;
+                unsigned long long t;
+                const unsigned long long e = run + block_exclusive_scan<unsigned long long, OpAdd>(f, sc, &t);
+                run += t;
+                if (k < 3u) {
+                    const uint32_t r = (uint32_t)((e >> (21 * k)) & 0x1FFFFF);
+                    const uint32_t dst = k == 0u ? r : k == 1u ? n0 + r : n0 + n1 + r;
+                    V.pieces_tmp[ib + dst] = V.pieces[it];
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            for (uint32_t it = ib + threadIdx.x; it < ie; it += 1024) V.pieces[it] = V.pieces_tmp[it];
+            __threadfence_block();
             __syncthreads();
         }
     }

@@ -12,3 +12,14 @@ l, r, _ = make_pair(1920, 1200, 128)
 ctx = _lib.Context(0)
 ctx.match(l, r, D)
 print("stages", ctx.stage_times(), flush=True)
+fn = getattr(_lib.lib(), "sm_chain_times_dump", None)  # -DSM_CHAIN_TIMES builds only
+if fn is not None:
+    import ctypes
+    fn(ctypes.cast(None, ctypes.POINTER(ctypes.c_ulonglong)), 0)  # drop the first call's entries
+    ctx.match(l, r, D)
+    buf = (ctypes.c_ulonglong * (4 * 65536))()
+    n = fn(buf, 65536)
+    for k in range(max(n, 0)):
+        a, t0, t1, item = buf[4 * k], buf[4 * k + 1], buf[4 * k + 2], buf[4 * k + 3]
+        print("CT %s %d %d %d %d %d %d" % ("D" if a & 1 else "U", (a >> 1) & 1, item, a >> 32, (a >> 8) & 0xFFFFFF, t0, t1))
+

@@ -1,0 +1,35 @@
+"""Chain-engine occupancy from a -DSM_CHAIN_TIMES build's device prints ("CT U|D view item len M
+t0 t1", 100 MHz): per launch, its span, the summed workgroup time / (256 CUs x span) (one chain
+workgroup per CU), the item count and the longest item.  Usage: python tools/chain_times.py <log>"""
+import sys
+
+rows = []
+for ln in open(sys.argv[1]):
+    p = ln.split()
+    if len(p) == 8 and p[0] == "CT":
+        rows.append((p[1], int(p[2]), int(p[3]), int(p[4]), int(p[5]), int(p[6]), int(p[7])))
+rows.sort(key=lambda r: r[5])
+launches, cur, end = [], [], 0
+for r in rows:
+    if cur and (r[5] >= end or r[0] != cur[0][0]):
+        launches.append(cur)
+        cur = []
+    cur.append(r)
+    end = max(end if cur[1:] else 0, r[6])
+if cur:
+    launches.append(cur)
+tot = {"U": [0.0, 0.0], "D": [0.0, 0.0]}
+for L in launches:
+    t0 = min(r[5] for r in L)
+    t1 = max(r[6] for r in L)
+    span = (t1 - t0) / 100.0  # us
+    busy = sum(r[6] - r[5] for r in L) / 100.0
+    longest = max(L, key=lambda r: r[6] - r[5])
+    nodes = sum(r[3] for r in L)
+    tot[L[0][0]][0] += span
+    tot[L[0][0]][1] += busy
+    print("%s items %4d nodes %7d span %7.1f us  util %4.0f%%  longest %6.1f us (len %d, M %d)  mean %5.1f us" % (
+        L[0][0], len(L), nodes, span, 100 * busy / (256 * span) if span else 0, (longest[6] - longest[5]) / 100.0,
+        longest[3], longest[4], busy / len(L)))
+for k, (sp, bu) in tot.items():
+    print("%s total span %.1f us, busy/256 %.1f us" % (k, sp, bu / 256))
