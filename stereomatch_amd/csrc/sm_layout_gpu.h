@@ -12,8 +12,9 @@
 #endif
 #define SM_PRE_SEG 32     // nodes per k_up_pre block (segment table granularity)
 // A long path of >= 2P nodes is cut into len/P pieces of P nodes (the bottom piece takes the
-// remainder, < 2P); the pieces' chains run concurrently from guessed inputs and are then repaired
-// exactly (sm_chain.hip, "Pieces").  P = SM_PIECE by default (env SM_PIECE_LEN: a multiple of
+// remainder, < 2P; -DSM_PIECE_EVEN balances the sizes instead: up chain 0.94 -> 1.01 ms at C2); the
+// pieces' chains run concurrently from guessed inputs and are then repaired exactly (sm_chain.hip,
+// "Pieces").  P = SM_PIECE by default (env SM_PIECE_LEN: a multiple of
 // SM_PRE_SEG, >= 64; tests use short pieces to exercise the repair on small images).
 // -DSM_PIECE_BALANCED (A/B): cut every path of > P nodes into ceil(len/P) balanced pieces.  Measured
 // at C2 it is slower (up pre + chain 1.23 vs 1.12 ms): more cut paths need segment aggregates and
@@ -41,9 +42,18 @@ __host__ __device__ static inline bool sm_piece_cut(uint32_t len, uint32_t plen)
 __host__ __device__ static inline uint32_t sm_piece_count(uint32_t len, uint32_t plen) {
     return len >= 2 * plen ? len / plen : 1u;
 }
+#ifndef SM_PIECE_EVEN  // P-node pieces, the bottom one takes the remainder (< 2P)
 __host__ __device__ static inline uint32_t sm_piece_begin_p(uint32_t len, uint32_t M, uint32_t j, uint32_t plen) {
     return j >= M ? len : j * plen;
 }
+#else  // A/B: the same M pieces, balanced (boundaries on SM_PRE_SEG multiples): none longer than ~1.5P
+__host__ __device__ static inline uint32_t sm_piece_begin_p(uint32_t len, uint32_t M, uint32_t j, uint32_t plen) {
+    (void)plen;
+    if (j >= M) return len;
+    const uint32_t b = (uint32_t)(((uint64_t)len * j / M + SM_PRE_SEG / 2) / SM_PRE_SEG * SM_PRE_SEG);
+    return b < len ? b : len;
+}
+#endif
 #else
 __host__ __device__ static inline bool sm_piece_cut(uint32_t len, uint32_t plen) { return len > plen; }
 __host__ __device__ static inline uint32_t sm_piece_count(uint32_t len, uint32_t plen) {
