@@ -50,13 +50,14 @@
 #define SM_CT_CAP 65536
 __device__ unsigned long long g_ct[4 * SM_CT_CAP];
 __device__ unsigned int g_ct_n;
-__device__ __forceinline__ void ct_log(int down, int view, int M, int len, int item, unsigned long long t0) {
+__device__ __forceinline__ void ct_log(int down, int view, int M, int len, int item, unsigned long long t0,
+                                       unsigned long long t1 = 0) {
     const unsigned k = atomicAdd(&g_ct_n, 1u);
     if (k < SM_CT_CAP) {
-        g_ct[4 * k] = (unsigned long long)down | ((unsigned long long)view << 1) | ((unsigned long long)M << 8) |
+        g_ct[4 * k] = (unsigned long long)down | ((unsigned long long)view << 2) | ((unsigned long long)M << 8) |
                       ((unsigned long long)len << 32);
         g_ct[4 * k + 1] = t0;
-        g_ct[4 * k + 2] = __builtin_amdgcn_s_memrealtime();
+        g_ct[4 * k + 2] = t1 ? t1 : __builtin_amdgcn_s_memrealtime();
         g_ct[4 * k + 3] = (unsigned long long)item;
     }
 }
@@ -974,7 +975,8 @@ __device__ void up_guess(double* scratch, double* guess, const double* __restric
 template <int SPL, int CHR, bool AGD>
 __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32, double* __restrict__ U,
                                           const UpCost& cs, const double* slut, const float* atab, int top, int nmax,
-                                          int Dpad, int lane, double* xio, double* __restrict__ fix, bool write) {
+                                          int Dpad, int lane, double* xio, double* __restrict__ fix, bool write,
+                                          double* lfix = nullptr, int lcap = 0) {
     double x[SPL];
 #pragma unroll
     for (int q = 0; q < SPL; ++q) x[q] = xio[q];
@@ -1048,7 +1050,9 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
             if (__all(eq)) return n0 + k;
             if (!write) continue;
             const uint32_t slot = (uint32_t)(top - (n0 + k));
-            if (fix)
+            if (n0 + k < lcap)  // buffered in LDS (the free ring): no global store between the batches'
+                lds_row_write<SPL>(lfix + (size_t)(n0 + k) * 64 * SPL, lane, x);  // loads and their waits
+            else if (fix)
                 store_row<SPL>(fix, slot, Dpad, lane, x);
             else
                 agent_row_write<SPL>(U, slot, Dpad, lane, x);
@@ -1079,18 +1083,37 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     const int top = head + len - 1;
     const uint32_t below = (uint32_t)(head + len);  // top node of the piece below
     double x[SPL];
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+#endif
     wait_word(done + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
     agent_row_read<SPL>(U, below, Dpad, lane, x);
     vm_drain();
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tf1 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (Q.dbg && Q.dbg[15] == 1) {  // probe (SM_PIECE_DEBUG=2): merge distance histogram, no writes
         const int mp = up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, len, Dpad, lane, x, nullptr, false);
         int b = 8;  // 8: < 8 nodes, 9: < 16, ... 13: >= 128 (merged), 14: never merged
         while (b < 13 && mp >= (8 << (b - 8))) ++b;
         if (lane == 0) atomicAdd(Q.dbg + (mp < 0 ? 14 : b), 1ull);
     }
-    const int m = up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, min(Q.rmax, len), Dpad, lane, x, fix, true);
+    // corrections of the first lcap nodes stay in the ring's LDS (free now: the helpers are done);
+    // a global store per corrected node made every batch's loads wait for the previous batch's
+    // stores (one vmcnt for both), two memory latencies per batch on the round's critical path
+    double* lfix = reinterpret_cast<double*>(ring.s);
+    constexpr int lcap = (int)(sizeof(ring.s) / (64 * SPL * sizeof(double)));
+    const int m = up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, min(Q.rmax, len), Dpad, lane, x,
+                                                           fix, true, lfix, lcap);
     if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tf2 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        ct_log(2, (int)blockIdx.y, M, m, e, tf0, tf1);  // waiting for the piece below
+        ct_log(3, (int)blockIdx.y, M, m, e, tf1, tf2);  // the repair walk (len field: merge node)
+    }
+#endif
     bool all = m >= 0;
     for (int q = e - 1; all && q > e - (M - 1 - j); --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u, Q.err, Q.wait_iters) == 2u * epoch;
     if (Q.dbg && lane == 0) {
@@ -1103,7 +1126,10 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     if (all) {  // commit the corrections
         for (int k = 0; k < m; ++k) {
             double r[SPL];
-            load_row<SPL>(fix, (uint32_t)(top - k), Dpad, lane, r);
+            if (k < lcap)
+                lds_row_read<SPL>(lfix + (size_t)k * 64 * SPL, lane, r);
+            else
+                load_row<SPL>(fix, (uint32_t)(top - k), Dpad, lane, r);
             store_row<SPL>(U, (uint32_t)(top - k), Dpad, lane, r);
         }
         if (lane == 0) publish_word(fin + e, epoch);
