@@ -1062,6 +1062,199 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
     return -1;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Cooperative up repair (round 2).  A piece's repair re-walks its first nodes from the true input
+// until the trajectory meets the stored one (see "Pieces").  One wave doing that alone pays a
+// memory round trip per batch of nodes (loads, costs, then the recurrence): ~0.6 us per node, and a
+// 210-node repair set the end of its whole round.  Here all 16 waves of the workgroup (idle once
+// the chain is done) stage the inputs of B nodes at a time into the free ring's LDS -- exactly
+// what the loaders stage for the chain: Pre, the post-heavy rows, the cost row, the weights, plus
+// the stored row to compare with -- and wave 0 runs the recurrence over them from LDS.
+// ---------------------------------------------------------------------------------------------
+template <int SPL>
+struct RepNode {
+    double pre[64 * SPL];   // Pre (pre-heavy fold), valid iff flags & UP_F_PRE
+    double p1[64 * SPL];    // first post-heavy row (iff UP_F_P1)
+    double p2[64 * SPL];    // second post-heavy row (iff UP_F_P2)
+    double spec[64 * SPL];  // the row the chain stored (speculative trajectory)
+    float c[64 * SPL];      // cost row
+    double S[4];            // S of the heavy child (0 if none), post 1, post 2, post 3
+    uint32_t flags;         // UP_F_PRE | UP_F_P1 | UP_F_P2 | UP_F3 (third post row: loaded by wave 0)
+    uint32_t c3;            // slot of the third post-heavy child (UP_F3)
+};
+
+template <int SPL>
+struct RepCfg {
+    static constexpr size_t RING = sizeof(UpRing<SPL>::s);
+    static constexpr int B0 = (int)(RING / sizeof(RepNode<SPL>));
+    static constexpr int B = B0 < 32 ? B0 : 32;  // nodes per pass
+    // waves 1 .. 15 stage (wave 0's correction stores then never share a vmcnt with loads)
+    static constexpr int NSW = CHN_WAVES - 1;
+    static constexpr int CHR = (B + NSW - 1) / NSW;  // nodes staged per wave
+    static_assert(B0 >= 8, "repair pass");
+};
+
+// one wave stages nodes k0 .. k0+nb-1 (node k = slot top - k) of the repair into rn[k - kb]
+template <int SPL, bool AGD, int CHR>
+__device__ __forceinline__ void up_repair_stage(RepNode<SPL>* rn, int kb, int k0, int nb, int top, int lane,
+                                                const uint32_t* __restrict__ meta32, const double* __restrict__ U,
+                                                const UpCost& cs, const double* slut, const float* atab, int Dpad,
+                                                int head) {
+    MetaVec<CHR> mv;
+    load_meta<CHR>(mv, meta32, lane, top - k0, -1, nb);
+    double l0[CHR][SPL], l1[CHR][SPL], l2[SPL], sp[CHR][SPL];
+    float cr[CHR][SPL];
+    ImgRecs<SPL, CHR> rec;
+    uint32_t s2 = (uint32_t)head;
+#pragma unroll
+    for (int k = 0; k < CHR; ++k) {
+        const int kk = min(k, nb - 1);
+        const uint32_t slot = (uint32_t)(top - (k0 + kk));
+        const uint32_t hi = mfield(mv, kk, 3);
+        const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+        const uint32_t nl = nch > 0 ? nch - 1u : 0u;
+        load_row<SPL>(U, nl >= 1 ? mfield(mv, kk, hidx == 0 ? 5 : 4) : (uint32_t)head, Dpad, lane, l0[k]);
+        load_row<SPL>(U, nl >= 2 ? mfield(mv, kk, hidx <= 1 ? 6 : 5) : (uint32_t)head, Dpad, lane, l1[k]);
+        if constexpr (!AGD) load_crow<SPL>(cs.Cst, slot, Dpad, lane, cr[k]);
+        agent_row_read<SPL>(U, slot, Dpad, lane, sp[k]);  // this launch's stored rows
+        if (nl >= 3) s2 = mfield(mv, kk, hidx == 3 ? 6 : 7);  // a root's third light row
+    }
+    load_row<SPL>(U, s2, Dpad, lane, l2);
+    if constexpr (AGD) {
+        load_recs<SPL, CHR>(mv, nb, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
+        chunk_costs<SPL, CHR>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, atab, cr);
+    }
+#pragma unroll
+    for (int k = 0; k < CHR; ++k) {
+        if (k >= nb) break;
+        RepNode<SPL>& r = rn[k0 + k - kb];
+        const uint32_t lo = mfield(mv, k, 2), hi = mfield(mv, k, 3);
+        const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+        const uint32_t np = nch > 0 ? nch - 1u - hidx : 0u;
+        // Pre: the light children before the heavy one, from +0 in key order (uniform branches)
+        double pre[SPL];
+#pragma unroll
+        for (int q = 0; q < SPL; ++q) pre[q] = 0.0;
+        if (hidx >= 1) {
+            const double S0 = slut[cw_of(lo, hi, 0)];
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) pre[q] = __builtin_fma(S0, l0[k][q], 0.0);
+            if (hidx >= 2) {
+                const double S1 = slut[cw_of(lo, hi, 1)];
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) pre[q] = __builtin_fma(S1, l1[k][q], pre[q]);
+                if (hidx >= 3) {
+                    const double S2 = slut[cw_of(lo, hi, 2)];
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) pre[q] = __builtin_fma(S2, l2[q], pre[q]);
+                }
+            }
+        }
+        uint32_t flags = (hidx > 0 ? UP_F_PRE : 0u) | (np >= 1 ? UP_F_P1 : 0u) | (np >= 2 ? UP_F_P2 : 0u);
+        if (flags & UP_F_PRE) lds_row_write<SPL>(r.pre, lane, pre);
+        if (np >= 1) {
+            if (hidx == 0)
+                lds_row_write<SPL>(r.p1, lane, l0[k]);
+            else if (hidx == 1)
+                lds_row_write<SPL>(r.p1, lane, l1[k]);
+            else
+                lds_row_write<SPL>(r.p1, lane, l2);
+        }
+        if (np >= 2) {
+            if (hidx == 0)
+                lds_row_write<SPL>(r.p2, lane, l1[k]);
+            else
+                lds_row_write<SPL>(r.p2, lane, l2);
+        }
+        lds_row_write<SPL>(r.spec, lane, sp[k]);
+#pragma unroll
+        for (int q = 0; q < SPL; ++q) r.c[lane * SPL + q] = cr[k][q];
+        if (lane < 4) {
+            // lane 0: the heavy child (always live here: a repaired piece has a lower piece), 1..3:
+            // the post-heavy children
+            const bool live = lane == 0 ? nch > 0 : (uint32_t)lane <= np;
+            const uint32_t pos = min(hidx + (uint32_t)lane, 3u);
+            r.S[lane] = slut[live ? cw_of(lo, hi, (int)pos) : (uint32_t)S_ZERO];
+        }
+        if (np >= 3) flags |= UP_F3;
+        if (lane == 0) {
+            r.flags = flags;
+            r.c3 = np >= 3 ? mfield(mv, k, 7) : 0u;
+        }
+    }
+}
+
+// All waves: the repair walk of nodes 0 .. nmax-1 from the input row in xin (LDS).  Corrections go
+// to fix[] (write == 1) or through U at device scope (write == 2), none with write == 0 (probe).
+// Returns (to every wave) the first node where the recomputed row equals the stored one, or -1.
+template <int SPL, bool AGD>
+__device__ int up_repair_coop(UpRing<SPL>& ring, int* res, const double* xin, const uint32_t* __restrict__ meta32,
+                              double* __restrict__ U, double* __restrict__ fix, const UpCost& cs, int Dpad, int wave,
+                              int lane, int top, int nmax, int head, int write) {
+    constexpr int B = RepCfg<SPL>::B, CHR = RepCfg<SPL>::CHR;
+    RepNode<SPL>* rn = reinterpret_cast<RepNode<SPL>*>(ring.s);
+    double x[SPL];
+    if (wave == 0)
+#pragma unroll
+        for (int q = 0; q < SPL; ++q) x[q] = xin[lane * SPL + q];
+    int out = -1;
+    for (int n0 = 0; n0 < nmax; n0 += B) {
+        const int nb = min(B, nmax - n0);
+        const int sw = (wave - 1) * CHR;  // this wave's first node of the pass
+        if (wave > 0 && sw < nb)
+            up_repair_stage<SPL, AGD, CHR>(rn, n0, n0 + sw, min(CHR, nb - sw), top, lane, meta32, U, cs, ring.slut,
+                                           ring.atab, Dpad, head);
+        __syncthreads();
+        if (wave == 0) {
+            int m = -1;
+            for (int k = 0; k < nb; ++k) {
+                const RepNode<SPL>& r = rn[k];
+                const uint32_t flags = uniform(r.flags);
+                const double Sh = r.S[0], S1 = r.S[1], S2 = r.S[2];
+                double acc[SPL];
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) {
+                    acc[q] = __builtin_fma(Sh, x[q], (flags & UP_F_PRE) ? r.pre[lane * SPL + q] : 0.0);
+                    acc[q] = __builtin_fma(S1, (flags & UP_F_P1) ? r.p1[lane * SPL + q] : 0.0, acc[q]);
+                    acc[q] = __builtin_fma(S2, (flags & UP_F_P2) ? r.p2[lane * SPL + q] : 0.0, acc[q]);
+                }
+                if (flags & UP_F3) {  // a tree root's third post-heavy child (rare): loaded here
+                    double r3[SPL];
+                    load_row<SPL>(U, uniform(r.c3), Dpad, lane, r3);
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) acc[q] = __builtin_fma(r.S[3], r3[q], acc[q]);
+                }
+                bool eq = true;
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) {
+                    x[q] = acc[q] + (double)r.c[lane * SPL + q];
+                    eq = eq && (!row_lane<SPL>(lane, Dpad) ||
+                                __double_as_longlong(x[q]) == __double_as_longlong(r.spec[lane * SPL + q]));
+                }
+                if (__all(eq)) {
+                    m = n0 + k;
+                    break;
+                }
+                const uint32_t slot = (uint32_t)(top - (n0 + k));
+                if (write == 1)
+                    store_row<SPL>(fix, slot, Dpad, lane, x);
+                else if (write == 2)
+                    agent_row_write<SPL>(U, slot, Dpad, lane, x);
+            }
+            if (lane == 0) *res = m >= 0 ? m : (n0 + nb >= nmax ? -1 : -2);
+        }
+        __syncthreads();
+        const int r = *res;
+        __syncthreads();  // every wave has read res before wave 0 may write the next pass's
+        if (r != -2) {
+            out = r;
+            break;
+        }
+    }
+    if (wave == 0) vm_drain();  // corrections stored
+    return out;
+}
+
 // Repair + look-back of piece e (one wave, after its chain).  j of M, bottom piece first: the
 // pieces below are entries e - (M-1-j) .. e - 1, the bottom one exact by construction.  A piece
 // "merged" iff its repair met the stored trajectory below its top node, i.e. its top row (the
@@ -1146,6 +1339,95 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     if (lane == 0) publish_word(fin + e, epoch);
 }
 
+// Repair + look-back of piece e with all waves (see up_finish for the protocol; wave 0 handles the
+// status words, the walk is up_repair_coop).  xin: the guess buffer, free after the chain.
+template <int SPL, bool AGD>
+__device__ void up_finish_coop(UpRing<SPL>& ring, double* xin, const uint32_t* __restrict__ meta32, double* __restrict__ U,
+                               double* __restrict__ fix, const UpCost& cs, int Dpad, int wave, int lane, int head, int len,
+                               int j, int M, int e, const PieceView& Q, uint32_t epoch) {
+    uint32_t* done = Q.stat;
+    uint32_t* merged = Q.stat + Q.stride;
+    uint32_t* fin = Q.stat + 2 * Q.stride;
+    __shared__ int res;
+    if (j + 1 == M) {  // bottom piece
+        if (wave == 0 && lane == 0) publish_word(fin + e, epoch);
+        return;
+    }
+    const int top = head + len - 1;
+    const uint32_t below = (uint32_t)(head + len);  // top node of the piece below
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (wave == 0) {
+        wait_word(done + e - 1, epoch, epoch, Q.err, Q.wait_iters);
+        vm_drain();
+        double x[SPL];
+        agent_row_read<SPL>(U, below, Dpad, lane, x);
+        vm_drain();
+        lds_row_write<SPL>(xin, lane, x);
+    }
+    __syncthreads();
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tf1 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (Q.dbg && Q.dbg[15] == 1) {  // probe (SM_PIECE_DEBUG=2): merge distance histogram, no writes
+        const int mp = up_repair_coop<SPL, AGD>(ring, &res, xin, meta32, U, fix, cs, Dpad, wave, lane, top, len, head, 0);
+        int b = 8;  // 8: < 8 nodes, 9: < 16, ... 13: >= 128 (merged), 14: never merged
+        while (b < 13 && mp >= (8 << (b - 8))) ++b;
+        if (wave == 0 && lane == 0) atomicAdd(Q.dbg + (mp < 0 ? 14 : b), 1ull);
+    }
+    const int m = up_repair_coop<SPL, AGD>(ring, &res, xin, meta32, U, fix, cs, Dpad, wave, lane, top, min(Q.rmax, len),
+                                           head, 1);
+#ifdef SM_CHAIN_TIMES
+    if (wave == 0 && lane == 0) {
+        const unsigned long long tf2 = __builtin_amdgcn_s_memrealtime();
+        ct_log(2, (int)blockIdx.y, M, m, e, tf0, tf1);
+        ct_log(3, (int)blockIdx.y, M, m, e, tf1, tf2);
+    }
+#endif
+    __shared__ int all_s;
+    if (wave == 0) {
+        if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
+        bool all = m >= 0;
+        for (int q = e - 1; all && q > e - (M - 1 - j); --q)
+            all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u, Q.err, Q.wait_iters) == 2u * epoch;
+        if (Q.dbg && lane == 0) {
+            atomicAdd(Q.dbg + (all ? 0 : 1), 1ull);
+            if (m >= 0) {
+                atomicAdd(Q.dbg + 2, (unsigned long long)m);
+                atomicMax(Q.dbg + 3, (unsigned long long)m);
+            }
+        }
+        if (lane == 0) all_s = all ? 1 : 0;
+    }
+    __syncthreads();
+    if (all_s) {  // commit the corrections: rows 0 .. m-1 from fix, spread over the waves
+        for (int k = wave; k < m; k += CHN_WAVES) {
+            double r[SPL];
+            load_row<SPL>(fix, (uint32_t)(top - k), Dpad, lane, r);
+            store_row<SPL>(U, (uint32_t)(top - k), Dpad, lane, r);
+        }
+        vm_drain();
+        __syncthreads();
+        if (wave == 0 && lane == 0) publish_word(fin + e, epoch);
+        return;
+    }
+    // slow path: the piece below is final (exact); repair again from its final top row, writing
+    // through (the stored rows are still the chain's trajectory: nothing was committed)
+    if (wave == 0) {
+        wait_word(fin + e - 1, epoch, epoch, Q.err, Q.wait_iters);
+        vm_drain();
+        double x[SPL];
+        agent_row_read<SPL>(U, below, Dpad, lane, x);
+        vm_drain();
+        lds_row_write<SPL>(xin, lane, x);
+    }
+    __syncthreads();
+    up_repair_coop<SPL, AGD>(ring, &res, xin, meta32, U, fix, cs, Dpad, wave, lane, top, len, head, 2);
+    __syncthreads();
+    if (wave == 0 && lane == 0) publish_word(fin + e, epoch);
+}
+
 template <int SPL, bool AGD>
 __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                           const uint32_t* __restrict__ meta1,
@@ -1226,14 +1508,22 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     cs.view = view;
     if (wave < Split<SPL>::NCW) {
         up_chain_wave<SPL>(ring, wave, head, len, lane, V.U, Dpad, lower ? guess : nullptr);
+#ifdef SM_UP_SOLO_REPAIR  // A/B: round 1's repair, wave 0 alone
         if (wave == 0 && M > 1)
             up_finish<SPL, AGD>(ring, &hdone, meta32, V.U, Q.fix, cs, Dpad, lane, head, len, j, M, e, Q, epoch);
+#endif
     } else if (Split<SPL>::helper_of(wave) >= 0) {
         up_helper_wave<SPL, AGD>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V.U, cs, Dpad, lower,
                                  j > 0 ? Q.stat + e : nullptr, epoch);
         vm_drain();  // this helper's stores are complete before the repair reads or overwrites them
         if (lane == 0) atomicAdd(&hdone, 1);
     }
+#ifndef SM_UP_SOLO_REPAIR
+    if (M > 1) {  // uniform over the block
+        __syncthreads();  // the chain is done and every helper's stores have completed (vm_drain)
+        up_finish_coop<SPL, AGD>(ring, guess, meta32, V.U, Q.fix, cs, Dpad, wave, lane, head, len, j, M, e, Q, epoch);
+    }
+#endif
 #ifdef SM_CHAIN_TIMES
     __syncthreads();
     if (threadIdx.x == 0) ct_log(0, (int)blockIdx.y, M, len, e, tt0);
