@@ -1087,21 +1087,18 @@ template <int SPL>
 struct RepCfg {
     static constexpr size_t RING = sizeof(UpRing<SPL>::s);
     static constexpr int B0 = (int)(RING / sizeof(RepNode<SPL>));
-    static constexpr int B = B0 < 32 ? B0 : 32;  // nodes per pass
+    static constexpr int BB = B0 / 2 < 16 ? B0 / 2 : 16;  // nodes per pass; two passes' buffers
     // waves 1 .. 15 stage (wave 0's correction stores then never share a vmcnt with loads)
     static constexpr int NSW = CHN_WAVES - 1;
-    static constexpr int CHR = (B + NSW - 1) / NSW;  // nodes staged per wave
-    static_assert(B0 >= 8, "repair pass");
+    static constexpr int CHR = (BB + NSW - 1) / NSW;  // nodes staged per wave and pass
+    static_assert(BB >= 4, "repair pass");
 };
 
-// one wave stages nodes k0 .. k0+nb-1 (node k = slot top - k) of the repair into rn[k - kb]
+// one wave stages nodes k0 .. k0+nb-1 (node k = slot top - k; metadata in mv) into rn[k - kb]
 template <int SPL, bool AGD, int CHR>
-__device__ __forceinline__ void up_repair_stage(RepNode<SPL>* rn, int kb, int k0, int nb, int top, int lane,
-                                                const uint32_t* __restrict__ meta32, const double* __restrict__ U,
-                                                const UpCost& cs, const double* slut, const float* atab, int Dpad,
-                                                int head) {
-    MetaVec<CHR> mv;
-    load_meta<CHR>(mv, meta32, lane, top - k0, -1, nb);
+__device__ __forceinline__ void up_repair_stage(RepNode<SPL>* rn, int kb, int k0, int nb, const MetaVec<CHR>& mv,
+                                                int top, int lane, const double* __restrict__ U, const UpCost& cs,
+                                                const double* slut, const float* atab, int Dpad, int head) {
     double l0[CHR][SPL], l1[CHR][SPL], l2[SPL], sp[CHR][SPL];
     float cr[CHR][SPL];
     ImgRecs<SPL, CHR> rec;
@@ -1184,31 +1181,49 @@ __device__ __forceinline__ void up_repair_stage(RepNode<SPL>* rn, int kb, int k0
     }
 }
 
-// All waves: the repair walk of nodes 0 .. nmax-1 from the input row in xin (LDS).  Corrections go
-// to fix[] (write == 1) or through U at device scope (write == 2), none with write == 0 (probe).
-// Returns (to every wave) the first node where the recomputed row equals the stored one, or -1.
-template <int SPL, bool AGD>
-__device__ int up_repair_coop(UpRing<SPL>& ring, int* res, const double* xin, const uint32_t* __restrict__ meta32,
-                              double* __restrict__ U, double* __restrict__ fix, const UpCost& cs, int Dpad, int wave,
-                              int lane, int top, int nmax, int head, int write) {
-    constexpr int B = RepCfg<SPL>::B, CHR = RepCfg<SPL>::CHR;
+// All waves: the repair walk of nodes 0 .. nmax-1.  Waves 1 .. 15 stage pass p+1 (metadata one
+// pass further ahead, so one memory round trip per pass) while wave 0 runs the recurrence over
+// pass p from LDS; pass 0 is staged while wave 0 runs pro(x), which produces the input row (the
+// wait for the piece below).  Corrections go to fix[] (write == 1) or through U at device scope
+// (write == 2), none with write == 0 (probe).  Returns (to every wave) the first node where the
+// recomputed row equals the stored one, or -1.
+template <int SPL, bool AGD, class Pro>
+__device__ int up_repair_coop(UpRing<SPL>& ring, int* res2, const uint32_t* __restrict__ meta32, double* __restrict__ U,
+                              double* __restrict__ fix, const UpCost& cs, int Dpad, int wave, int lane, int top, int nmax,
+                              int head, int write, Pro&& pro) {
+    constexpr int BB = RepCfg<SPL>::BB, CHR = RepCfg<SPL>::CHR;
     RepNode<SPL>* rn = reinterpret_cast<RepNode<SPL>*>(ring.s);
-    double x[SPL];
-    if (wave == 0)
-#pragma unroll
-        for (int q = 0; q < SPL; ++q) x[q] = xin[lane * SPL + q];
-    int out = -1;
-    for (int n0 = 0; n0 < nmax; n0 += B) {
-        const int nb = min(B, nmax - n0);
-        const int sw = (wave - 1) * CHR;  // this wave's first node of the pass
-        if (wave > 0 && sw < nb)
-            up_repair_stage<SPL, AGD, CHR>(rn, n0, n0 + sw, min(CHR, nb - sw), top, lane, meta32, U, cs, ring.slut,
+    const int npass = (nmax + BB - 1) / BB;
+    const int sw = (wave - 1) * CHR;  // a stager's first node within a pass
+    MetaVec<CHR> mv, mn;
+    auto meta = [&](MetaVec<CHR>& m, int p) {
+        const int n = min(CHR, min(nmax, (p + 1) * BB) - (p * BB + sw));
+        if (p < npass && n > 0) load_meta<CHR>(m, meta32, lane, top - (p * BB + sw), -1, n);
+    };
+    auto stage = [&](int p) {
+        const int n = min(CHR, min(nmax, (p + 1) * BB) - (p * BB + sw));
+        if (n > 0)
+            up_repair_stage<SPL, AGD, CHR>(rn + (p & 1) * BB, p * BB, p * BB + sw, n, mv, top, lane, U, cs, ring.slut,
                                            ring.atab, Dpad, head);
-        __syncthreads();
+    };
+    double x[SPL];
+    if (wave > 0) {
+        meta(mv, 0);
+        meta(mn, 1);
+        stage(0);
+        mv = mn;
+    } else {
+        pro(x);
+    }
+    __syncthreads();
+    int out = -1;
+    for (int p = 0; p < npass; ++p) {
         if (wave == 0) {
+            const int n0 = p * BB, nb = min(BB, nmax - n0);
+            const RepNode<SPL>* rb = rn + (p & 1) * BB;
             int m = -1;
             for (int k = 0; k < nb; ++k) {
-                const RepNode<SPL>& r = rn[k];
+                const RepNode<SPL>& r = rb[k];
                 const uint32_t flags = uniform(r.flags);
                 const double Sh = r.S[0], S1 = r.S[1], S2 = r.S[2];
                 double acc[SPL];
@@ -1241,11 +1256,15 @@ __device__ int up_repair_coop(UpRing<SPL>& ring, int* res, const double* xin, co
                 else if (write == 2)
                     agent_row_write<SPL>(U, slot, Dpad, lane, x);
             }
-            if (lane == 0) *res = m >= 0 ? m : (n0 + nb >= nmax ? -1 : -2);
+            // res2[p & 1]: rewritten two passes later, after every wave has passed the barrier below
+            if (lane == 0) res2[p & 1] = m >= 0 ? m : (p + 1 >= npass ? -1 : -2);
+        } else if (p + 1 < npass) {
+            meta(mn, p + 2);
+            stage(p + 1);
+            mv = mn;
         }
         __syncthreads();
-        const int r = *res;
-        __syncthreads();  // every wave has read res before wave 0 may write the next pass's
+        const int r = res2[p & 1];
         if (r != -2) {
             out = r;
             break;
@@ -1348,7 +1367,7 @@ __device__ void up_finish_coop(UpRing<SPL>& ring, double* xin, const uint32_t* _
     uint32_t* done = Q.stat;
     uint32_t* merged = Q.stat + Q.stride;
     uint32_t* fin = Q.stat + 2 * Q.stride;
-    __shared__ int res;
+    __shared__ int res2[2];
     if (j + 1 == M) {  // bottom piece
         if (wave == 0 && lane == 0) publish_word(fin + e, epoch);
         return;
@@ -1357,32 +1376,41 @@ __device__ void up_finish_coop(UpRing<SPL>& ring, double* xin, const uint32_t* _
     const uint32_t below = (uint32_t)(head + len);  // top node of the piece below
 #ifdef SM_CHAIN_TIMES
     const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long tf1 = tf0;
 #endif
-    if (wave == 0) {
-        wait_word(done + e - 1, epoch, epoch, Q.err, Q.wait_iters);
+    // wave 0: the true input, the final row of the piece below's top node once it is stored
+    auto input = [&](double (&x)[SPL], const uint32_t* word) {
+        wait_word(word, epoch, epoch, Q.err, Q.wait_iters);
         vm_drain();
-        double x[SPL];
         agent_row_read<SPL>(U, below, Dpad, lane, x);
         vm_drain();
-        lds_row_write<SPL>(xin, lane, x);
-    }
-    __syncthreads();
 #ifdef SM_CHAIN_TIMES
-    const unsigned long long tf1 = __builtin_amdgcn_s_memrealtime();
+        tf1 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (Q.dbg && Q.dbg[15] == 1) {  // probe (SM_PIECE_DEBUG=2): merge distance histogram, no writes
-        const int mp = up_repair_coop<SPL, AGD>(ring, &res, xin, meta32, U, fix, cs, Dpad, wave, lane, top, len, head, 0);
+    };
+    const bool probe = Q.dbg && Q.dbg[15] == 1;  // SM_PIECE_DEBUG=2: merge distance histogram, no writes
+    if (probe) {
+        const int mp = up_repair_coop<SPL, AGD>(ring, res2, meta32, U, fix, cs, Dpad, wave, lane, top, len, head, 0,
+                                                [&](double (&x)[SPL]) {
+                                                    input(x, done + e - 1);
+                                                    lds_row_write<SPL>(xin, lane, x);
+                                                });
         int b = 8;  // 8: < 8 nodes, 9: < 16, ... 13: >= 128 (merged), 14: never merged
         while (b < 13 && mp >= (8 << (b - 8))) ++b;
         if (wave == 0 && lane == 0) atomicAdd(Q.dbg + (mp < 0 ? 14 : b), 1ull);
     }
-    const int m = up_repair_coop<SPL, AGD>(ring, &res, xin, meta32, U, fix, cs, Dpad, wave, lane, top, min(Q.rmax, len),
-                                           head, 1);
+    const int m = up_repair_coop<SPL, AGD>(ring, res2, meta32, U, fix, cs, Dpad, wave, lane, top, min(Q.rmax, len), head, 1,
+                                           [&](double (&x)[SPL]) {
+                                               if (probe)
+                                                   lds_row_read<SPL>(xin, lane, x);
+                                               else
+                                                   input(x, done + e - 1);
+                                           });
 #ifdef SM_CHAIN_TIMES
     if (wave == 0 && lane == 0) {
         const unsigned long long tf2 = __builtin_amdgcn_s_memrealtime();
-        ct_log(2, (int)blockIdx.y, M, m, e, tf0, tf1);
-        ct_log(3, (int)blockIdx.y, M, m, e, tf1, tf2);
+        ct_log(2, (int)blockIdx.y, M, m, e, tf0, tf1);  // waiting for the piece below
+        ct_log(3, (int)blockIdx.y, M, m, e, tf1, tf2);  // the repair walk (len field: merge node)
     }
 #endif
     __shared__ int all_s;
@@ -1414,16 +1442,8 @@ __device__ void up_finish_coop(UpRing<SPL>& ring, double* xin, const uint32_t* _
     }
     // slow path: the piece below is final (exact); repair again from its final top row, writing
     // through (the stored rows are still the chain's trajectory: nothing was committed)
-    if (wave == 0) {
-        wait_word(fin + e - 1, epoch, epoch, Q.err, Q.wait_iters);
-        vm_drain();
-        double x[SPL];
-        agent_row_read<SPL>(U, below, Dpad, lane, x);
-        vm_drain();
-        lds_row_write<SPL>(xin, lane, x);
-    }
-    __syncthreads();
-    up_repair_coop<SPL, AGD>(ring, &res, xin, meta32, U, fix, cs, Dpad, wave, lane, top, len, head, 2);
+    up_repair_coop<SPL, AGD>(ring, res2, meta32, U, fix, cs, Dpad, wave, lane, top, len, head, 2,
+                             [&](double (&x)[SPL]) { input(x, fin + e - 1); });
     __syncthreads();
     if (wave == 0 && lane == 0) publish_word(fin + e, epoch);
 }
