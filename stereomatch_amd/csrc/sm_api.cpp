@@ -758,10 +758,8 @@ double bucket_voxels(sm_ctx* ctx, uint32_t r, bool long_paths, int views, int D)
 sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views) {
     CHECK(join(ctx, ctx->st, ctx->st2));
     CHECK(join(ctx, ctx->st2, ctx->st));
-    set_bucket(ctx, a, r, false, views);
-    const WalkArgs as = a;
-    CHECK(timed(ctx, ctx->st, KF_UP_WALK, bucket_voxels(ctx, r, false, views, a.dcall),
-                [&] { return launch_up(ctx->st, as, spl, false); }));
+    // long paths first: with two streams a chain workgroup needs a whole CU, which it only gets
+    // before the walker's grid fills the GPU
     set_bucket(ctx, a, r, true, views);
     const WalkArgs al = a;
     const double vl = bucket_voxels(ctx, r, true, views, a.dcall);
@@ -771,6 +769,10 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views) {
         cut = cut || (al.pieces[v] && sm_piece_cut((uint32_t)al.maxlen, (uint32_t)al.bucket_plen[v]));
     if (cut) CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, 0.0));
     CHECK(timed(ctx, ctx->st2, KF_UP_CHAIN, vl, [&] { return launch_up_chain(ctx->st2, al, spl); }));
+    set_bucket(ctx, a, r, false, views);
+    const WalkArgs as = a;
+    CHECK(timed(ctx, ctx->st, KF_UP_WALK, bucket_voxels(ctx, r, false, views, a.dcall),
+                [&] { return launch_up(ctx->st, as, spl, false); }));
     return SM_OK;
 }
 

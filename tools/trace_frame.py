@@ -1,7 +1,9 @@
 """Per-launch timeline of one frame in a rocprofv3 kernel trace (tools/gpu_trace.sh output).
 Usage: python tools/trace_frame.py gpurun_out/<dir>/run_kernel_trace.csv [--frame K] [substring filter...]
---frame K: the K-th frame (negative: from the end; default -1).  bench.py runs warmup, timed and
-then 2 diagnostic frames (every launch timed with HIP events): -3 is the last timed frame."""
+--frame K: the K-th frame (negative: from the end; default -1).  bench.py runs warmup, timed, 2
+diagnostic frames (every launch timed with HIP events) and 3 wall-clock frames (one at a time, no
+per-launch events; then the host-I/O frames unless --no-host-io): with --no-host-io, -1 is the last
+wall-clock frame and -6 the last timed one."""
 import csv
 import sys
 
