@@ -2131,8 +2131,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
         const SmPath last = pp[uniform(pc.x + pc.w - 1u)];
         plen = (int)uniform(last.head + last.len - path.head);
     }
-    const int o0 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)i, (uint32_t)Q.plen);
-    const int o1 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)i + 1u, (uint32_t)Q.plen);
+    const int o0 = (int)sm_piece_begin_dn((uint32_t)plen, (uint32_t)M, (uint32_t)i, (uint32_t)Q.plen);
+    const int o1 = (int)sm_piece_begin_dn((uint32_t)plen, (uint32_t)M, (uint32_t)i + 1u, (uint32_t)Q.plen);
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
 #ifdef SM_CHAIN_TIMES
     const unsigned long long tt0 = __builtin_amdgcn_s_memrealtime();

@@ -68,6 +68,19 @@ __host__ __device__ static inline uint32_t sm_piece_begin_p(uint32_t len, uint32
 }
 #endif
 
+// Down pass: the same M pieces (same work items and status words), cut evenly.  The down pass
+// has no segment table and its exact piece is the top one, so the floor rule would make the
+// bottom piece -- the last to repair -- also the longest (up to 2P - 1 nodes).
+// -DSM_DN_PIECE_FLOOR (A/B): the up pass's boundaries.
+__host__ __device__ static inline uint32_t sm_piece_begin_dn(uint32_t len, uint32_t M, uint32_t i, uint32_t plen) {
+#ifdef SM_DN_PIECE_FLOOR
+    return sm_piece_begin_p(len, M, i, plen);
+#else
+    (void)plen;
+    return i >= M ? len : (uint32_t)((uint64_t)len * i / M);
+#endif
+}
+
 struct LayoutView {
     // inputs
     const uint8_t* mR;

@@ -201,18 +201,18 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
                                                  const uint2* __restrict__ Rrec, const float* __restrict__ atab_g,
                                                  const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
                                                  int W, int Dpad, int dcall, int dglob0, const float* __restrict__ Cv0,
-                                                 const float* __restrict__ Cv1) {
+                                                 const float* __restrict__ Cv1, int ppw) {
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
-    // work item: WALK_PPW_UP consecutive paths of the bucket = one contiguous slot range (the
-    // recurrence restarts by itself at every path bottom: a leaf has no heavy child)
-    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW_UP);
+    // work item: ppw consecutive paths of the bucket = one contiguous slot range (the recurrence
+    // restarts by itself at every path bottom: a leaf has no heavy child)
+    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw);
     if (pi0 >= V.npaths) return;
-    const int pi1 = min(pi0 + WALK_PPW_UP, V.npaths);
+    const int pi1 = min(pi0 + ppw, V.npaths);
     const SmPath* __restrict__ pp = view ? paths1 : paths0;
     const int head = (int)uniform(pp[pi0].head);
     const int len = (int)uniform(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
@@ -250,18 +250,18 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
                                                    const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
                                                    const SmPath* __restrict__ paths1, const float* __restrict__ atab_g,
                                                    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
-                                                   int Dpad, WtaCfg w, int store_all) {
+                                                   int Dpad, WtaCfg w, int store_all, int ppw) {
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
-    // work item: WALK_PPW_DN consecutive paths = one contiguous slot range, root side first; a node
-    // is a path head iff its parent is not the previous slot
-    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * WALK_PPW_DN);
+    // work item: ppw consecutive paths = one contiguous slot range, root side first; a node is a
+    // path head iff its parent is not the previous slot
+    const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw);
     if (pi0 >= V.npaths) return;
-    const int pi1 = min(pi0 + WALK_PPW_DN, V.npaths);
+    const int pi1 = min(pi0 + ppw, V.npaths);
     const SmPath* __restrict__ pp = view ? paths1 : paths0;
     const int head = (int)uniform(pp[pi0].head);
     const int len = (int)uniform(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
@@ -370,43 +370,63 @@ static size_t walk_lds_pad() {
     return e ? (size_t)atoi(e) : 0;
 }
 
+// Paths per work item.  A round whose items at the default size would not give the GPU ~8k
+// waves (a small, deep round: its time is the latency of its longest item, not bytes) gets fewer
+// paths per item, down to one.  SM_WALK_FILL / SM_WALK_FILL_DN: the target item count of the up /
+// down walker (0: always the default).
+static int walk_ppw(int np, int dflt, bool down) {
+    static const int fill_up = [] {
+        const char* e = getenv("SM_WALK_FILL");
+        return e ? atoi(e) : 8192;
+    }();
+    static const int fill_dn = [] {
+        const char* e = getenv("SM_WALK_FILL_DN");
+        return e ? atoi(e) : 8192;
+    }();
+    const int fill = down ? fill_dn : fill_up;
+    if (fill <= 0 || (np + dflt - 1) / dflt >= fill) return dflt;
+    const int p = (np + fill - 1) / fill;
+    return p < 1 ? 1 : p;
+}
+
 template <int SPL, int CH>
-static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a) {
+static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a, int ppw) {
     if (a.vol)
         hipLaunchKernelGGL((k_up_walk<SPL, CH, true>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
-                           a.dglob0, a.Cst[0], a.Cst[1]);
+                           a.dglob0, a.Cst[0], a.Cst[1], ppw);
     else
         hipLaunchKernelGGL((k_up_walk<SPL, CH, false>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
-                           a.dglob0, a.Cst[0], a.Cst[1]);
+                           a.dglob0, a.Cst[0], a.Cst[1], ppw);
 }
 
 template <int SPL, int CH>
-static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all) {
+static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all, int ppw) {
     hipLaunchKernelGGL((k_down_walk<SPL, CH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.Dpad, a.wta, store_all);
+                       a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.Dpad, a.wta, store_all, ppw);
 }
 
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
-    const int items = (np + WALK_PPW_UP - 1) / WALK_PPW_UP;
+    const int ppw = walk_ppw(np, WALK_PPW_UP, false);
+    const int items = (np + ppw - 1) / ppw;
     const dim3 g((items + 3) / 4, 2);
     if (long_paths) {
         switch (spl) {
-            case 1: up_launch<1, 8>(st, g, a); break;
-            case 2: up_launch<2, 8>(st, g, a); break;
-            default: up_launch<4, 4>(st, g, a); break;
+            case 1: up_launch<1, 8>(st, g, a, ppw); break;
+            case 2: up_launch<2, 8>(st, g, a, ppw); break;
+            default: up_launch<4, 4>(st, g, a, ppw); break;
         }
     } else {
         switch (spl) {
-            case 1: up_launch<1, 4>(st, g, a); break;
-            case 2: up_launch<2, WALK_UP_CH2>(st, g, a); break;
-            default: up_launch<4, WALK_UP_CH4>(st, g, a); break;
+            case 1: up_launch<1, 4>(st, g, a, ppw); break;
+            case 2: up_launch<2, WALK_UP_CH2>(st, g, a, ppw); break;
+            default: up_launch<4, WALK_UP_CH4>(st, g, a, ppw); break;
         }
     }
     return hipGetLastError();
@@ -415,19 +435,20 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
 static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, int store_all, bool long_paths) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
-    const int items = (np + WALK_PPW_DN - 1) / WALK_PPW_DN;
+    const int ppw = walk_ppw(np, WALK_PPW_DN, true);
+    const int items = (np + ppw - 1) / ppw;
     const dim3 g((items + 3) / 4, 2);
     if (long_paths) {
         switch (spl) {
-            case 1: down_launch<1, 16>(st, g, a, store_all); break;
-            case 2: down_launch<2, 16>(st, g, a, store_all); break;
-            default: down_launch<4, 8>(st, g, a, store_all); break;
+            case 1: down_launch<1, 16>(st, g, a, store_all, ppw); break;
+            case 2: down_launch<2, 16>(st, g, a, store_all, ppw); break;
+            default: down_launch<4, 8>(st, g, a, store_all, ppw); break;
         }
     } else {
         switch (spl) {
-            case 1: down_launch<1, 4>(st, g, a, store_all); break;
-            case 2: down_launch<2, WALK_DN_CH2>(st, g, a, store_all); break;
-            default: down_launch<4, WALK_DN_CH4>(st, g, a, store_all); break;
+            case 1: down_launch<1, 4>(st, g, a, store_all, ppw); break;
+            case 2: down_launch<2, WALK_DN_CH2>(st, g, a, store_all, ppw); break;
+            default: down_launch<4, WALK_DN_CH4>(st, g, a, store_all, ppw); break;
         }
     }
     return hipGetLastError();
