@@ -2048,13 +2048,25 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
     const bool last_pub = i + 1 < M;
     const uint32_t above = (uint32_t)(head - 1);  // last node of the piece above
     double x[SPL];
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+#endif
     wait_word(done + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
     agent_row_read<SPL>(V.A, above, Dpad, lane, x);
     vm_drain();
+#ifdef SM_CHAIN_TIMES
+    const unsigned long long tf1 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int m = down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, min(Q.rmax, len), Dpad,
                                                         lane, x, w, store_all, last_pub, true);
     vm_drain();
+#ifdef SM_CHAIN_TIMES
+    if (lane == 0) {
+        ct_log(2 | 8, (int)blockIdx.y, M, m, e, tf0, tf1);  // waiting for the piece above
+        ct_log(3 | 8, (int)blockIdx.y, M, m, e, tf1);       // the repair walk (len field: merge node)
+    }
+#endif
     if (lane == 0) publish_word(merged + e, 2u * epoch + (m >= 0 ? 0u : 1u));
     bool all = m >= 0;
     for (int q = e - 1; all && q > e - i; --q) all = wait_word(merged + q, 2u * epoch, 2u * epoch + 1u, Q.err, Q.wait_iters) == 2u * epoch;
@@ -2178,6 +2190,9 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     }
     if (threadIdx.x == 0) hdone = 0;
     __syncthreads();
+#ifdef SM_CHAIN_TIMES
+    if (threadIdx.x == 0 && M > 1) ct_log(0 | 8, (int)blockIdx.y, M, len, pidx, tt0);  // prologue: aggregate + guess
+#endif
     if (wave < Split<SPL>::NCW) {
         down_chain_wave<SPL>(ring, wave, len, lane, i > 0 ? guess : nullptr);
         if (wave == 0 && M > 1)

@@ -129,7 +129,7 @@ struct LayoutView {
     uint32_t* round_maxlen;  // SM_NBUCKETS: longest path per bucket
     uint32_t* round_nodes;   // SM_NBUCKETS: nodes per bucket
     uint32_t* seg_begin;     // SM_NBUCKETS + 1: first segment of each bucket in segtab
-    uint2* segtab;           // {path index within its bucket, segment within the path}
+    uint2* segtab;           // cut long paths: {path index within its bucket, segment within the path}
     uint32_t* piece_begin;   // SM_NBUCKETS + 1: first piece of each bucket in pieces
     uint4* pieces_tmp;       // scratch of the items' longest-first reordering (k_long_segments)
     uint4* pieces;           // {path index within its bucket, j, M, first segment of the path

@@ -724,8 +724,9 @@ __global__ __launch_bounds__(1024) void k_long_segments(LayoutPair LP, uint32_t 
                 const uint32_t p = pb + (uint32_t)i;
                 const SmPath path = p < p1 ? V.paths[p] : SmPath{hbase, 0u};
                 len[i] = path.len;
-                ns[i] = (len[i] + SM_PRE_SEG - 1) / SM_PRE_SEG;
                 cut[i] = sm_piece_cut(len[i], pl);
+                // segments (k_up_pre / k_dn_pre aggregates, the pieces' guesses): cut paths only
+                ns[i] = cut[i] ? (len[i] + SM_PRE_SEG - 1) / SM_PRE_SEG : 0u;
                 win[i] = (path.head - hbase) / rwin;
             }
             // previous path's window / alone flag (thread 0: the last path of the previous chunk).

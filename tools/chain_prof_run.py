@@ -21,5 +21,5 @@ if fn is not None:
     n = fn(buf, 65536)
     for k in range(max(n, 0)):
         a, t0, t1, item = buf[4 * k], buf[4 * k + 1], buf[4 * k + 2], buf[4 * k + 3]
-        print("CT %s %d %d %d %d %d %d" % ("UDWR"[a & 3], (a >> 2) & 1, item, a >> 32, (a >> 8) & 0xFFFFFF, t0, t1))
+        print("CT %s %d %d %d %d %d %d" % (("pcwr" if a & 8 else "UDWR")[a & 3], (a >> 2) & 1, item, a >> 32, (a >> 8) & 0xFFFFFF, t0, t1))
 
