@@ -62,7 +62,7 @@ struct sm_ctx {
     int W = 0, H = 0, stride = 0;
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
     DevBuf changed, mst_ok, atab, slut, s2lut, meta[2], paths[2], U[2], Cst[2], idx[2], minc[2], disp[2];
-    DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2];
+    DevBuf cand[2], gmin[2], gidx[2], vol[2], rec[2], rec4[2];
     DevBuf post_mask, post_scratch;  // output step (sm_post.hip): marks, scan positions
     // guided-filter aggregator (sm_guided.hip): guide planes / means, per-view statistics, batch
     // planes, box scratch, WTA state
@@ -268,19 +268,24 @@ sm_status stage_prep(sm_ctx* ctx) {
         CHECK(ensure(ctx, ctx->wR[v], N * 2));
         CHECK(ensure(ctx, ctx->wD[v], N * 2));
         const void* old = ctx->rec[v].p;
+        const void* old4 = ctx->rec4[v].p;
         const size_t pad = ctx->rec_pad;
         CHECK(ensure(ctx, ctx->rec[v], (N + 2 * pad) * 8));
-        if (ctx->rec[v].p != old || ctx->rec_pad_n[v] != N || ctx->rec_pad_z[v] != pad) {
+        CHECK(ensure(ctx, ctx->rec4[v], (N + 2 * pad) * 4));
+        if (ctx->rec[v].p != old || ctx->rec4[v].p != old4 || ctx->rec_pad_n[v] != N || ctx->rec_pad_z[v] != pad) {
             // zero pads around the records: once per allocation, size and pad
             ctx->rec_pad_n[v] = N;
             ctx->rec_pad_z[v] = pad;
             HIPC(hipMemsetAsync(ctx->rec[v].p, 0, pad * 8, ctx->st));
             HIPC(hipMemsetAsync(P<uint2>(ctx->rec[v]) + pad + N, 0, pad * 8, ctx->st));
+            HIPC(hipMemsetAsync(ctx->rec4[v].p, 0, pad * 4, ctx->st));
+            HIPC(hipMemsetAsync(P<uint32_t>(ctx->rec4[v]) + pad + N, 0, pad * 4, ctx->st));
         }
     }
     HIPC(launch_prep(ctx->st, P<uint8_t>(ctx->img[0]), P<uint8_t>(ctx->img[1]), W, H, ctx->stride, P<uint32_t>(ctx->bgrx[0]),
                      P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]), P<float>(ctx->gray[1]),
-                     P<uint2>(ctx->rec[0]) + ctx->rec_pad, P<uint2>(ctx->rec[1]) + ctx->rec_pad));
+                     P<uint2>(ctx->rec[0]) + ctx->rec_pad, P<uint2>(ctx->rec[1]) + ctx->rec_pad,
+                     P<uint32_t>(ctx->rec4[0]) + ctx->rec_pad, P<uint32_t>(ctx->rec4[1]) + ctx->rec_pad));
     HIPC(launch_median_weights(ctx->st, P<uint32_t>(ctx->bgrx[0]), P<uint32_t>(ctx->bgrx[1]), P<uint32_t>(ctx->med[0]),
                                P<uint32_t>(ctx->med[1]), P<uint16_t>(ctx->wR[0]), P<uint16_t>(ctx->wD[0]),
                                P<uint16_t>(ctx->wR[1]), P<uint16_t>(ctx->wD[1]), W, H));
@@ -620,6 +625,8 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     }
     a.Lrec = P<uint2>(ctx->rec[0]) + ctx->rec_pad;
     a.Rrec = P<uint2>(ctx->rec[1]) + ctx->rec_pad;
+    a.Lrec4 = P<uint32_t>(ctx->rec4[0]) + ctx->rec_pad;
+    a.Rrec4 = P<uint32_t>(ctx->rec4[1]) + ctx->rec_pad;
     a.atab = P<float>(ctx->atab);
     a.slut = P<double>(ctx->slut);
     a.s2lut = P<double>(ctx->s2lut);
@@ -1160,7 +1167,7 @@ void sm_destroy(sm_ctx* ctx) {
     for (int v = 0; v < 2; ++v) {
         DevBuf* per[] = {&ctx->img[v], &ctx->bgrx[v], &ctx->gray[v], &ctx->med[v], &ctx->wR[v], &ctx->wD[v], &ctx->comp[v],
                          &ctx->best[v], &ctx->root[v], &ctx->mR[v], &ctx->mD[v], &ctx->meta[v], &ctx->paths[v], &ctx->U[v], &ctx->Cst[v],
-                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v], &ctx->vin[v],
+                         &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v], &ctx->rec4[v], &ctx->vin[v],
                          &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v], &ctx->fwR[v], &ctx->fwD[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }

@@ -51,7 +51,8 @@ struct ImgPair {
     const uint8_t* src[2];  // packed BGR rows (device)
     uint32_t* bgrx[2];      // W*H
     float* gray[2];         // W*H
-    uint2* rec[2];          // W*H {bgrx, gray bits}: one 8-byte load per pixel in the walkers
+    uint2* rec[2];          // W*H {bgrx, gray bits}: one 8-byte load per pixel (chain helpers)
+    uint32_t* rec4[2];      // W*H bgrx, padded like rec (the up walker recomputes the gray)
 };
 
 __global__ void k_prep(ImgPair P, int W, int H, int stride) {
@@ -66,6 +67,7 @@ __global__ void k_prep(ImgPair P, int W, int H, int stride) {
     P.bgrx[v][p] = w;
     P.gray[v][p] = g;
     P.rec[v][p] = make_uint2(w, __float_as_uint(g));
+    P.rec4[v][p] = w;
 }
 
 __device__ __forceinline__ void cswap(int& a, int& b) {
@@ -756,8 +758,8 @@ __global__ void k_rows_to_volume(const SmMeta* __restrict__ meta, const double* 
 #include "sm_launch.h"
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
-                       float* lg, uint32_t* rb, float* rg, uint2* lrec, uint2* rrec) {
-    ImgPair P{{l, r}, {lb, rb}, {lg, rg}, {lrec, rrec}};
+                       float* lg, uint32_t* rb, float* rg, uint2* lrec, uint2* rrec, uint32_t* lrec4, uint32_t* rrec4) {
+    ImgPair P{{l, r}, {lb, rb}, {lg, rg}, {lrec, rrec}, {lrec4, rrec4}};
     dim3 g((W + 255) / 256, H, 2);
     hipLaunchKernelGGL(k_prep, g, dim3(256), 0, st, P, W, H, stride);
     return hipGetLastError();

@@ -61,6 +61,8 @@ struct WalkArgs {
     float* disp[2];
     const uint2* Lrec;   // {bgrx, gray} records, padded by SM_REC_PAD records on both sides
     const uint2* Rrec;
+    const uint32_t* Lrec4;  // bgrx alone, same padding: the up walker recomputes the gray
+    const uint32_t* Rrec4;
     const float* atab;
     const double* slut;
     const double* s2lut;
@@ -89,7 +91,7 @@ struct WalkArgs {
 };
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
-                       float* lg, uint32_t* rb, float* rg, uint2* lrec, uint2* rrec);
+                       float* lg, uint32_t* rb, float* rg, uint2* lrec, uint2* rrec, uint32_t* lrec4, uint32_t* rrec4);
 hipError_t launch_median_weights(hipStream_t st, const uint32_t* lb, const uint32_t* rb, uint32_t* lmed, uint32_t* rmed,
                                  uint16_t* lwR, uint16_t* lwD, uint16_t* rwR, uint16_t* rwD, int W, int H);
 hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* lg, const uint32_t* rb, const float* rg,

@@ -77,7 +77,7 @@ __device__ __forceinline__ void walk_vm_drain() {
 template <int SPL, int CH, bool VOL>
 __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, int view, int lane, int W, int Dpad,
                                          int dbase, int dend, const uint2* __restrict__ own, const uint2* __restrict__ oth,
-                                         double* __restrict__ U, const float* __restrict__ Cv, const WalkShared& sh,
+                                         const uint32_t* __restrict__ oth4, double* __restrict__ U, const float* __restrict__ Cv, const WalkShared& sh,
                                          double (&xc)[SPL], MetaVec<CH>& nxt, const uint32_t* __restrict__ meta32, int ntop,
                                          int nn) {
     constexpr int LR = WALK_UP_LR;
@@ -128,15 +128,23 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
         for (int j = 0; j < CH; ++j)
 #pragma unroll
             for (int k = 0; k < SPL; ++k) c[j][k] = 0.25f;
-#else
+#elif defined(SM_WALK_REC8)  // A/B: {bgrx, gray} records (2.5x the record bytes)
+        (void)oth4;
         ImgRecs<SPL, CH> rec;
         load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+        if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);
+        walk_vm_drain();
+        chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+#else
+        (void)oth;
+        ImgRecs4<SPL, CH> rec;
+        load_recs4<SPL, CH>(mv, n, view, lane, dbase, own, oth4, rec);
         // the next chunk's metadata, issued behind this chunk's loads: it completes with them, so
         // the next chunk starts without a wait (a prefetch issued first made the chunk's first
         // wait a vmcnt(0) over the prefetch and the previous chunk's stores)
         if (nn > 0) load_meta<CH>(nxt, meta32, lane, ntop, -1, nn);
         walk_vm_drain();
-        chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+        chunk_costs4<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
 #endif
     }
 #pragma unroll
@@ -198,7 +206,8 @@ template <int SPL, int CH, bool VOL>
 __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                  const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
                                                  const SmPath* __restrict__ paths1, const uint2* __restrict__ Lrec,
-                                                 const uint2* __restrict__ Rrec, const float* __restrict__ atab_g,
+                                                 const uint2* __restrict__ Rrec, const uint32_t* __restrict__ Lrec4,
+                                                 const uint32_t* __restrict__ Rrec4, const float* __restrict__ atab_g,
                                                  const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
                                                  int W, int Dpad, int dcall, int dglob0, const float* __restrict__ Cv0,
                                                  const float* __restrict__ Cv1, int ppw) {
@@ -220,6 +229,7 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
     const int dend = dglob0 + dcall;
     const uint2* __restrict__ own = view ? Rrec : Lrec;  // the view's reference image
     const uint2* __restrict__ oth = view ? Lrec : Rrec;  // the matched image
+    const uint32_t* __restrict__ oth4 = view ? Lrec4 : Rrec4;
     double xc[SPL];
 #pragma unroll
     for (int k = 0; k < SPL; ++k) xc[k] = 0.0;
@@ -234,7 +244,7 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
         const int nn = ntop >= head ? min(CH, ntop - head + 1) : 0;
         MetaVec<CH> nxt;  // the next chunk's metadata: loaded inside up_chunk
         const float* __restrict__ Cv = view ? Cv1 : Cv0;
-        up_chunk<SPL, CH, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, V.U, Cv, sh, xc, nxt, meta32, ntop, nn);
+        up_chunk<SPL, CH, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, oth4, V.U, Cv, sh, xc, nxt, meta32, ntop, nn);
         if (nn == 0) break;
         cur = nxt;
         top = ntop;
@@ -394,12 +404,12 @@ static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a, int ppw) {
     if (a.vol)
         hipLaunchKernelGGL((k_up_walk<SPL, CH, true>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
+                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
                            a.dglob0, a.Cst[0], a.Cst[1], ppw);
     else
         hipLaunchKernelGGL((k_up_walk<SPL, CH, false>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
+                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
                            a.dglob0, a.Cst[0], a.Cst[1], ppw);
 }
 

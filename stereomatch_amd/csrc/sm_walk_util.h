@@ -317,6 +317,89 @@ __device__ __forceinline__ void load_recs(const MetaVec<CH>& mv, int n, int view
     }
 }
 
+// The up walker's 4-byte records: bgrx alone, the gray recomputed as k_prep computes it
+// (sm_kernels.hip sm_gray: 0.114f*B + 0.587f*G + 0.299f*R, left to right, no contraction), so the
+// costs are bit-identical.  Per node a lane loads SPL + 1 dwords instead of SPL {bgrx, gray}
+// pairs and one gray word: 0.5 KB instead of 1.3 KB per node through L1 / L2 / the Infinity Cache.
+__device__ __forceinline__ float gray4(uint32_t bgrx) {
+    const float b = (float)(bgrx & 255u), g = (float)((bgrx >> 8) & 255u), r = (float)((bgrx >> 16) & 255u);
+    float t = 0.114f * b;
+    t = t + 0.587f * g;
+    t = t + 0.299f * r;
+    return t;
+}
+// agd_rec with the grays given: r0 = right(x), l0 = left(x+d) (bgrx), their grays gr0 / gl0, and
+// gr1 = gray(right(x+1)), gl1 = gray(left(x+d+1)); same operations in the same order
+__device__ __forceinline__ float agd4(uint32_t r0, uint32_t l0, float gr0, float gl0, float gr1, float gl1,
+                                      const float* __restrict__ atab) {
+    const uint32_t l1 = __builtin_amdgcn_sad_u8(r0, l0, 0u);
+#ifdef SM_AGD_NO_TABLE
+    const float a = 0.11f * fminf((float)((double)(float)l1 * 0.33333333333), 7.0f);
+#else
+    const float a = atab[l1];
+#endif
+    float g = gl0 - gr0;
+    g = g + (gr1 - gl1);
+    const float b = 0.89f * fminf(fabsf(g), 2.0f);
+    return a + b;
+}
+
+template <int SPL, int CH>
+struct ImgRecs4 {
+    uint32_t ob[CH][SPL + 1];  // matched-image bgrx, records base .. base + SPL
+    uint2 own;
+};
+
+template <int SPL, int CH>
+__device__ __forceinline__ void load_recs4(const MetaVec<CH>& mv, int n, int view, int lane, int dbase,
+                                           const uint2* __restrict__ own, const uint32_t* __restrict__ oth,
+                                           ImgRecs4<SPL, CH>& r) {
+    static_assert(CH <= 32, "own records: lanes j and 32 + j hold node j");
+    {
+        const int node = min(lane & 31, n - 1);
+        uint32_t pl = mfield(mv, 0, 0);
+#pragma unroll
+        for (int j = 1; j < CH; ++j) pl = node == j ? mfield(mv, j, 0) : pl;
+        r.own = own[(long long)pl + (lane >> 5)];
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const int jj = j < n ? j : n - 1;
+        const long long pix = (long long)mfield(mv, jj, 0);
+        const long long base = view ? pix + dbase : pix - dbase - (SPL - 1);
+#pragma unroll
+        for (int q = 0; q <= SPL; ++q) r.ob[j][q] = oth[base + q];
+    }
+}
+
+template <int SPL, int CH, class T>
+__device__ __forceinline__ void chunk_costs4(const MetaVec<CH>& mv, int view, int W, int dbase, int dend,
+                                             const ImgRecs4<SPL, CH>& r, const float* __restrict__ atab, T (&c)[CH][SPL]) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const int x = pix_col((int)mfield(mv, j, 0), W);
+        const uint2 o0 = make_uint2(__builtin_amdgcn_readlane(r.own.x, j), __builtin_amdgcn_readlane(r.own.y, j));
+        const uint2 o1 = make_uint2(__builtin_amdgcn_readlane(r.own.x, 32 + j), __builtin_amdgcn_readlane(r.own.y, 32 + j));
+        float g[SPL + 1];
+#pragma unroll
+        for (int q = 0; q <= SPL; ++q) g[q] = gray4(r.ob[j][q]);
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) {
+            const int d = dbase + k;
+            float v;
+            bool ok;
+            if (view) {  // right reference: right(x) vs left(x+d)
+                ok = d < dend && x + d + 1 < W;
+                v = agd4(o0.x, r.ob[j][k], rgray(o0), g[k], rgray(o1), g[k + 1], atab);
+            } else {     // left pixel x at d: cost(x-d, d); x-d<0 and column W-1 -> 3.0
+                ok = d < dend && x - d >= 0 && x + 1 < W;
+                v = agd4(r.ob[j][SPL - 1 - k], o0.x, g[SPL - 1 - k], rgray(o0), g[SPL - k], rgray(o1), atab);
+            }
+            c[j][k] = (T)(ok ? v : 3.0f);
+        }
+    }
+}
+
 // AGD costs C(v, d) of the chunk's nodes for this lane's SPL slices; invalid (x-d<0, column W-1,
 // d beyond the call's range) -> 3.0 as the reference (PatchMatchStereoGPU.cu:1501-1549)
 template <int SPL, int CH, class T>
@@ -339,6 +422,10 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
                 ok = d < dend && x - d >= 0 && x + 1 < W;
                 v = agd_rec(r.ob[j][SPL - 1 - k], o0, k > 0 ? rgray(r.ob[j][k > 0 ? SPL - k : 0]) : r.obg[j], rgray(o1), atab);
             }
+#ifdef SM_EXP_COST_CHEAP  // timing experiment only (wrong results): the records' loads, trivial arithmetic
+            v = rgray(r.ob[j][k]) + rgray(o0) + r.obg[j] + rgray(o1);
+            ok = true;
+#endif
             c[j][k] = (T)(ok ? v : 3.0f);
         }
     }
