@@ -871,6 +871,7 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int views, bool debug_sto
     if (wta) a.wta = *wta;
     CHECK(setup_sync(ctx, a, N, Dpad));
     a.vol = ctx->use_vol ? 1 : 0;
+    a.leaf_cost = (!a.vol && !debug_store_all && !getenv("SM_NO_LEAF_COST")) ? 1 : 0;  // SM_NO_LEAF_COST: A/B
     if (a.vol)  // cost rows of every slot from the caller's volumes (slots come from the layout)
         for (int v = 0; v < 2; ++v)
             if (view_on(views, v))

@@ -2180,6 +2180,9 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
             }
             __syncthreads();
         }
+#ifdef SM_CHAIN_TIMES
+        if (threadIdx.x == 0) ct_log(1 | 8, (int)blockIdx.y, M, len, pidx, tt0);  // tables + own aggregate published
+#endif
         if (i > 0)
             down_guess<SPL>(scratch, guess, V.A, Q.agg, aggw, uniform(meta32[(size_t)path.head * 8 + 1]), pidx, i, Dpad, wave,
                             lane, epoch, Q.err, Q.wait_iters);

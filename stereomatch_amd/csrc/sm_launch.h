@@ -68,6 +68,12 @@ struct WalkArgs {
     const double* s2lut;
     float* Cst[2];       // cost rows [slot][Dpad]: long-path AGD staging, or every slot's volume row
     int vol;             // costs from Cst rows (MC-CNN ingest, k_vol_rows) instead of the AGD cost
+    // 1: the short-path walkers treat leaves specially.  A leaf's A_up is its cost ((double)C, no
+    // children), so the up walker does not store the rows of heavy leaves (read by nobody: their
+    // parent takes the value from registers, light children are path heads) and the down walker
+    // recomputes every leaf's A_up from the image records instead of reading U.  0: AGD costs
+    // unavailable (vol) or a debug call that reads every U row.
+    int leaf_cost;
     int maxlen;          // longest path of the current bucket (both views)
     const uint2* segtab[2];  // long buckets: {path, segment} per SM_PRE_SEG-node segment
     int nseg[2];

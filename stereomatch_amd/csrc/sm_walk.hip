@@ -79,7 +79,7 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
                                          int dbase, int dend, const uint2* __restrict__ own, const uint2* __restrict__ oth,
                                          const uint32_t* __restrict__ oth4, double* __restrict__ U, const float* __restrict__ Cv, const WalkShared& sh,
                                          double (&xc)[SPL], MetaVec<CH>& nxt, const uint32_t* __restrict__ meta32, int ntop,
-                                         int nn) {
+                                         int nn, int leaf_cost) {
     constexpr int LR = WALK_UP_LR;
     // ---- light-row bookkeeping (uniform): node j's light children are compact rows off[j] ..
     int off[CH];
@@ -197,7 +197,13 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
 #ifdef SM_EXP_UP_HEADS_ONLY  // timing experiment only (wrong results): store path heads' rows only
             if (mfield(mv, j, 1) != (uint32_t)(top - j) - 1u)
 #endif
-            store_row<SPL>(U, (uint32_t)(top - j), Dpad, lane, xc);
+            // a heavy leaf (no children, its parent the previous slot): only the down walker reads its
+            // row, and its A_up is exactly (double)C: the f32 cost row, half the bytes
+            // (WalkArgs::leaf_cost)
+            if (leaf_cost && nch == 0 && mfield(mv, j, 1) == (uint32_t)(top - j) - 1u)
+                store_leaf_row<SPL>(U, (uint32_t)(top - j), Dpad, lane, c[j]);
+            else
+                store_row<SPL>(U, (uint32_t)(top - j), Dpad, lane, xc);
         }
     }
 }
@@ -210,7 +216,7 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
                                                  const uint32_t* __restrict__ Rrec4, const float* __restrict__ atab_g,
                                                  const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
                                                  int W, int Dpad, int dcall, int dglob0, const float* __restrict__ Cv0,
-                                                 const float* __restrict__ Cv1, int ppw) {
+                                                 const float* __restrict__ Cv1, int ppw, int leaf_cost) {
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
@@ -244,7 +250,8 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
         const int nn = ntop >= head ? min(CH, ntop - head + 1) : 0;
         MetaVec<CH> nxt;  // the next chunk's metadata: loaded inside up_chunk
         const float* __restrict__ Cv = view ? Cv1 : Cv0;
-        up_chunk<SPL, CH, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, oth4, V.U, Cv, sh, xc, nxt, meta32, ntop, nn);
+        up_chunk<SPL, CH, VOL>(cur, n, top, view, lane, W, Dpad, dbase, dend, own, oth, oth4, V.U, Cv, sh, xc, nxt, meta32, ntop, nn,
+                               VOL ? 0 : leaf_cost);
         if (nn == 0) break;
         cur = nxt;
         top = ntop;
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
                                                    const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
                                                    const SmPath* __restrict__ paths1, const float* __restrict__ atab_g,
                                                    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
-                                                   int Dpad, WtaCfg w, int store_all, int ppw) {
+                                                   int Dpad, WtaCfg w, int store_all, int ppw, int leaf_cost) {
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
@@ -291,16 +298,22 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
         // (earlier round)
         double u[CH][SPL], xp[CH][SPL];
         uint32_t par[CH];
+        // heavy leaves (WalkArgs::leaf_cost): their slot holds the f32 cost row (A_up = (double)C)
+        bool leaf[CH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int jj = j < n ? j : n - 1;
             const uint32_t slot = (uint32_t)(c0 + jj);
             par[j] = mfield(cur, jj, 1);
             const bool head_j = par[j] == SM_NONE || par[j] != slot - 1u;
+            leaf[j] = leaf_cost && !head_j && hi_nch(mfield(cur, jj, 3)) == 0u;
 #ifdef SM_EXP_DN_HEADS_ONLY  // timing experiment only (wrong results): read path heads' rows only
             if (head_j) load_row<SPL>(V.U, slot, Dpad, lane, u[j]); else for (int q = 0; q < SPL; ++q) u[j][q] = 0.0;
 #else
-            load_row<SPL>(V.U, slot, Dpad, lane, u[j]);
+            if (!leaf[j])  // uniform
+                load_row<SPL>(V.U, slot, Dpad, lane, u[j]);
+            else
+                load_leaf_row<SPL>(V.U, slot, Dpad, lane, u[j]);  // f32 bits in u[j]'s registers
 #endif
             if (head_j && par[j] != SM_NONE) {  // wave-uniform: only path heads read their parent's row
                 load_row<SPL>(V.A, par[j], Dpad, lane, xp[j]);
@@ -313,6 +326,9 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
         // the next chunk's metadata, behind this chunk's row loads (see up_chunk)
         if (nn > 0) load_meta<CH>(nxt, meta32, lane, nc0, 1, nn);
         walk_vm_drain();
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+            if (leaf[j]) widen_leaf_row<SPL>(u[j]);  // uniform
         double S[CH], S2[CH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -405,19 +421,20 @@ static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a, int ppw) {
         hipLaunchKernelGGL((k_up_walk<SPL, CH, true>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
-                           a.dglob0, a.Cst[0], a.Cst[1], ppw);
+                           a.dglob0, a.Cst[0], a.Cst[1], ppw, a.leaf_cost);
     else
         hipLaunchKernelGGL((k_up_walk<SPL, CH, false>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
-                           a.dglob0, a.Cst[0], a.Cst[1], ppw);
+                           a.dglob0, a.Cst[0], a.Cst[1], ppw, a.leaf_cost);
 }
 
 template <int SPL, int CH>
 static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all, int ppw) {
     hipLaunchKernelGGL((k_down_walk<SPL, CH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.Dpad, a.wta, store_all, ppw);
+                       a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.Dpad, a.wta, store_all, ppw,
+                       store_all ? 0 : a.leaf_cost);
 }
 
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths) {

@@ -246,6 +246,49 @@ __device__ __forceinline__ void wta_nodes(const double (&x)[CH][SPL], int lane, 
 }
 
 
+// A heavy leaf's slot in U holds its f32 cost row (the first half of the slot; WalkArgs::leaf_cost):
+// store_leaf_row writes it, load_leaf_row loads its bits into the registers of a double row, and
+// widen_leaf_row turns them into the doubles 0.0 + (double)C the up walker computed.
+template <int SPL>
+__device__ __forceinline__ void store_leaf_row(double* __restrict__ U, uint32_t slot, int Dpad, int lane, const float (&c)[SPL]) {
+    float* p = reinterpret_cast<float*>(U + (size_t)slot * Dpad) + lane * SPL;
+    if constexpr (SPL == 1) {
+        if (lane < Dpad) p[0] = c[0];
+    } else if constexpr (SPL == 2) {
+        *reinterpret_cast<float2*>(p) = make_float2(c[0], c[1]);
+    } else {
+        *reinterpret_cast<float4*>(p) = make_float4(c[0], c[1], c[2], c[3]);
+    }
+}
+template <int SPL>
+__device__ __forceinline__ void load_leaf_row(const double* __restrict__ U, uint32_t slot, int Dpad, int lane, double (&r)[SPL]) {
+    const float* p = reinterpret_cast<const float*>(U + (size_t)slot * Dpad) + lane * SPL;
+    if constexpr (SPL == 1) {
+        r[0] = __longlong_as_double((long long)(lane < Dpad ? __float_as_uint(p[0]) : 0u));
+    } else if constexpr (SPL == 2) {
+        const uint2 t = *reinterpret_cast<const uint2*>(p);
+        r[0] = __longlong_as_double((long long)(((unsigned long long)t.y << 32) | t.x));
+        r[1] = 0.0;
+    } else {
+        const uint4 t = *reinterpret_cast<const uint4*>(p);
+        r[0] = __longlong_as_double((long long)(((unsigned long long)t.y << 32) | t.x));
+        r[1] = __longlong_as_double((long long)(((unsigned long long)t.w << 32) | t.z));
+        r[2] = 0.0;
+        r[3] = 0.0;
+    }
+}
+template <int SPL>
+__device__ __forceinline__ void widen_leaf_row(double (&r)[SPL]) {
+    float f[SPL];
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) {
+        const unsigned long long b = (unsigned long long)__double_as_longlong(r[q / 2]);
+        f[q] = __uint_as_float((uint32_t)(q & 1 ? b >> 32 : b));
+    }
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) r[q] = 0.0 + (double)f[q];  // the up walker's acc + C
+}
+
 // f32 cost row of one slot (this lane's SPL slices): MC-CNN ingest rows, or the chain staging rows
 template <int SPL>
 __device__ __forceinline__ void load_cost_row(const float* __restrict__ C, uint32_t slot, int Dpad, int lane, float (&c)[SPL]) {
