@@ -9,7 +9,7 @@ for ln in open(sys.argv[1]):
     if len(p) == 8 and p[0] == "CT":
         rows.append((p[1], int(p[2]), int(p[3]), int(p[4]), int(p[5]), int(p[6]), int(p[7])))
 fin = [r for r in rows if r[0] in "WR"]  # up pieces: W = waiting for the piece below, R = repair walk
-dfin = [r for r in rows if r[0] in "pwr"]  # down pieces: p = prologue, w = wait for the piece above, r = repair
+dfin = [r for r in rows if r[0] in "cpwr"]  # down pieces: p = prologue, w = wait for the piece above, r = repair
 rows = [r for r in rows if r[0] in "UD"]
 if fin:
     for tag, what in (("W", "wait for the piece below"), ("R", "repair walk")):
@@ -17,7 +17,8 @@ if fin:
         print("%s: %d pieces, max %.1f us, mean %.1f us; longest: merge at node %s" % (
             what, len(f), (f[0][6] - f[0][5]) / 100.0 if f else 0, sum(r[6] - r[5] for r in f) / 100.0 / max(len(f), 1),
             [(r[3], round((r[6] - r[5]) / 100.0, 1)) for r in f[:5]]))
-for tag, what in (("p", "down prologue (aggregate + guess)"), ("w", "down wait for the piece above"),
+for tag, what in (("c", "down prologue to its own aggregate"), ("p", "down prologue (aggregate + guess)"),
+                  ("w", "down wait for the piece above"),
                   ("r", "down repair walk")):
     f = sorted([r for r in dfin if r[0] == tag], key=lambda r: r[5] - r[6])
     if f:
