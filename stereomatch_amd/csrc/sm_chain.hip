@@ -1559,10 +1559,16 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
 #ifndef DN_NS2
 #define DN_NS2 12
 #endif
+#ifndef DN_G4
+#define DN_G4 4
+#endif
+#ifndef DN_NS4
+#define DN_NS4 8
+#endif
 template <int SPL>
 struct DownCfg {
-    static constexpr int G = SPL == 4 ? 4 : SPL == 2 ? DN_G2 : 8;  // helper registers: next group's rows + WTA rows
-    static constexpr int NS = SPL == 4 ? 8 : SPL == 2 ? DN_NS2 : 10;
+    static constexpr int G = SPL == 4 ? DN_G4 : SPL == 2 ? DN_G2 : 8;  // helper registers: next group's rows + WTA rows
+    static constexpr int NS = SPL == 4 ? DN_NS4 : SPL == 2 ? DN_NS2 : 10;
 };
 
 template <int SPL>

@@ -47,6 +47,12 @@
 #ifndef WALK_DN_CH2
 #define WALK_DN_CH2 6
 #endif
+#ifndef WALK_UP_CH1
+#define WALK_UP_CH1 4
+#endif
+#ifndef WALK_DN_CH1
+#define WALK_DN_CH1 4
+#endif
 
 
 // One explicit vmcnt(0) per chunk, right after the chunk's loads (rows, image records, next
@@ -451,7 +457,7 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
         }
     } else {
         switch (spl) {
-            case 1: up_launch<1, 4>(st, g, a, ppw); break;
+            case 1: up_launch<1, WALK_UP_CH1>(st, g, a, ppw); break;
             case 2: up_launch<2, WALK_UP_CH2>(st, g, a, ppw); break;
             default: up_launch<4, WALK_UP_CH4>(st, g, a, ppw); break;
         }
@@ -473,7 +479,7 @@ static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, i
         }
     } else {
         switch (spl) {
-            case 1: down_launch<1, 4>(st, g, a, store_all, ppw); break;
+            case 1: down_launch<1, WALK_DN_CH1>(st, g, a, store_all, ppw); break;
             case 2: down_launch<2, WALK_DN_CH2>(st, g, a, store_all, ppw); break;
             default: down_launch<4, WALK_DN_CH4>(st, g, a, store_all, ppw); break;
         }
