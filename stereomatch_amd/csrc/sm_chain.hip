@@ -1560,10 +1560,10 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
 #define DN_NS2 12
 #endif
 #ifndef DN_G4
-#define DN_G4 4
+#define DN_G4 3  // SPL = 4 (C3 / C4): 4 x 8 -> 3 x 20, k_down_chain 5.76 -> 5.43 ms at C3, 1.91 -> 1.79 ms at C4 size
 #endif
 #ifndef DN_NS4
-#define DN_NS4 8
+#define DN_NS4 20
 #endif
 template <int SPL>
 struct DownCfg {
