@@ -206,7 +206,8 @@ __device__ __forceinline__ void up_chunk(const MetaVec<CH>& mv, int n, int top, 
             // a heavy leaf (no children, its parent the previous slot): only the down walker reads its
             // row, and its A_up is exactly (double)C: the f32 cost row, half the bytes
             // (WalkArgs::leaf_cost)
-            if (leaf_cost && nch == 0 && mfield(mv, j, 1) == (uint32_t)(top - j) - 1u)
+            const uint32_t par = mfield(mv, j, 1);
+            if (leaf_cost && nch == 0 && par != SM_NONE && par == (uint32_t)(top - j) - 1u)
                 store_leaf_row<SPL>(U, (uint32_t)(top - j), Dpad, lane, c[j]);
             else
                 store_row<SPL>(U, (uint32_t)(top - j), Dpad, lane, xc);
