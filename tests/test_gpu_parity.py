@@ -158,6 +158,27 @@ def test_chain_helper_costs_bitexact(gpu_ctx, monkeypatch, plen, D):
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
 
 
+@pytest.mark.parametrize("D", [32, 64, 128, 256])
+def test_leaf_f32_rows_bitexact(gpu_ctx, monkeypatch, D):
+    """Heavy leaves keep an f32 cost row in their U slot (WalkArgs::leaf_cost): the walkers' results
+    with it equal the full-row path (SM_NO_LEAF_COST=1) and the oracle bitwise (SPL 1, 2, 4; 32-double
+    rows at D=32; segment forest too)."""
+    import stereomatch_amd as sm
+    W, H = 320, 240
+    left, right, _ = make_pair(W, H, D, index=7)
+    for params, ref in ((None, O.match(left, right, D, nthreads=16)),
+                        (sm.default_params(c=5000.0, min_size=200), O.match(left, right, D, c=5000.0, nthreads=16))):
+        out = gpu_ctx.match(left, right, D, params)
+        monkeypatch.setenv("SM_NO_LEAF_COST", "1")
+        full = gpu_ctx.match(left, right, D, params)
+        monkeypatch.delenv("SM_NO_LEAF_COST")
+        for v in ("left", "right"):
+            np.testing.assert_array_equal(out[v]["idx"], full[v]["idx"])
+            assert np.array_equal(bits(out[v]["minc"]), bits(full[v]["minc"]))
+            np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+            assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
 def test_kernel_timing_mask(gpu_ctx):
     """sm_set_kernel_timing: untimed families report no launches, timed ones do; the results do
     not depend on the timing."""
