@@ -169,116 +169,24 @@ __device__ __forceinline__ void load_crow(const float* __restrict__ C, uint32_t 
     }
 }
 // ---------------------------------------------------------------------------------------------
-// k_up_pre: the per-segment affine aggregates of the long paths that are cut into pieces (the
-// pieces' guessed inputs, "Pieces" below).  One block per SM_PRE_SEG-node segment of the bucket's
-// long paths (segment table from the layout), SM_PRE_SEG / CH waves of CH nodes each; grid.y = view.
-// Segments of uncut paths return at once.  Nothing else of the up pass runs here: the chain
-// helpers fold the pre-heavy children and compute the costs themselves.
+// k_up_pre: the segment aggregates of the round's cut long paths (up_pre_segment) in a launch of
+// their own, before the round's chains.  -DSM_PRE_FUSED (A/B) runs them as extra blocks of the
+// round's walker launch instead (sm_walk.hip).
 // ---------------------------------------------------------------------------------------------
-template <int SPL, int CH, bool VOL>
-__global__ __launch_bounds__(64 * SM_PRE_SEG / CH) void k_up_pre(
-    WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0, const uint32_t* __restrict__ meta1,
-    const SmPath* __restrict__ paths0, const SmPath* __restrict__ paths1, const uint2* __restrict__ seg0,
-    const uint2* __restrict__ seg1, int nseg0, int nseg1, const float* __restrict__ Cst0, const float* __restrict__ Cst1,
-    const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec, const float* __restrict__ atab_g,
-    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g, int W, int Dpad, int dcall, int dglob0,
-    double* __restrict__ agg0, double* __restrict__ agg1, int plen0, int plen1) {
-    constexpr int NW = SM_PRE_SEG / CH;
+template <int SPL, int CH, int NSUB, bool VOL>
+__global__ __launch_bounds__(256) void k_up_pre(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
+                                                const uint32_t* __restrict__ meta1, UpPreArgs pa,
+                                                const float* __restrict__ Cst0, const float* __restrict__ Cst1,
+                                                const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec,
+                                                const float* __restrict__ atab_g, const double* __restrict__ slut_g,
+                                                const double* __restrict__ s2lut_g, int W, int Dpad, int dcall, int dglob0) {
     const int view = blockIdx.y;
-    if ((int)blockIdx.x >= (view ? nseg1 : nseg0)) return;  // uniform over the block
-    const uint2 sg = (view ? seg1 : seg0)[blockIdx.x];
-    const SmPath path = (view ? paths1 : paths0)[uniform(sg.x)];
-    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
-    double* __restrict__ agg = view ? agg1 : agg0;
-    if (agg == nullptr || !sm_piece_cut((uint32_t)len, (uint32_t)(view ? plen1 : plen0))) return;  // uncut: uniform
+    if ((int)blockIdx.x >= pa.nseg[view]) return;  // uniform over the block
     __shared__ WalkShared sh;
-    __shared__ double aggsh[NW][2][64 * SPL];
     load_tables(sh, atab_g, slut_g, s2lut_g);
-    const WalkView& V = view ? V1 : V0;
-    const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
-    const int lane = threadIdx.x & 63;
-    const int wv = (int)uniform(threadIdx.x >> 6);
-    const int first = (int)uniform(sg.y * SM_PRE_SEG + wv * CH);
-    const int n = max(0, min(CH, len - first));
-    const int dbase = dglob0 + lane * SPL;
-    const int dend = dglob0 + dcall;
-    const uint2* __restrict__ own = view ? Rrec : Lrec;
-    const uint2* __restrict__ oth = view ? Lrec : Rrec;
-    double* __restrict__ U = V.U;
-    const float* __restrict__ Cst = view ? Cst1 : Cst0;
-    // ---- affine aggregate of this wave's nodes (bottom up): x_first = P * x_below + B with
-    // b = Pre + sum(S_post * A_post) + C and x = S_heavy * x_below + b.  Approximate (any rounding
-    // only moves the guess; the chains' results are repaired exactly), so no order constraint; rows
-    // are loaded where used, to keep registers low (cut paths only: rare)
-    double P[SPL], B[SPL];
-#pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-        P[k] = 1.0;
-        B[k] = 0.0;
-    }
-    if (n > 0) {
-        MetaVec<CH> mv;
-        load_meta<CH>(mv, meta32, lane, head + first, 1, n);
-        float c[CH][SPL];
-        if constexpr (VOL) {
-#pragma unroll
-            for (int j = 0; j < CH; ++j) load_cost_row<SPL>(Cst, (uint32_t)(head + first + (j < n ? j : n - 1)), Dpad, lane, c[j]);
-        } else {
-            ImgRecs<SPL, CH> rec;
-            load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
-            chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
-        }
-#pragma unroll
-        for (int j = CH - 1; j >= 0; --j) {
-            if (j < n) {
-                const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
-                const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-                const double Sh = nch > 0 ? readlane_f64(sh.slut[cw_of(lo, hi, (int)hidx)], 0) : 0.0;
-                double b[SPL];
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) b[k] = 0.0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {  // every light child, in key order
-                    if ((uint32_t)i < nch && (uint32_t)i != hidx) {
-                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);
-                        double r[SPL];
-                        load_row<SPL>(U, mfield(mv, j, 4 + i), Dpad, lane, r);
-#pragma unroll
-                        for (int k = 0; k < SPL; ++k) b[k] = __builtin_fma(S, r[k], b[k]);
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) {
-                    B[k] = __builtin_fma(Sh, B[k], b[k] + (double)c[j][k]);
-                    P[k] = Sh * P[k];
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-        aggsh[wv][0][lane * SPL + k] = P[k];
-        aggsh[wv][1][lane * SPL + k] = B[k];
-    }
-    __syncthreads();
-    if (wv != 0) return;
-    // segment = wave 0 o wave 1 o ... (the last wave holds the bottom-most nodes)
-    for (int w = NW - 2; w >= 0; --w) {
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) {
-            const double Pw = aggsh[w][0][lane * SPL + k], Bw = aggsh[w][1][lane * SPL + k];
-            const double Pn = aggsh[w + 1][0][lane * SPL + k], Bn = aggsh[w + 1][1][lane * SPL + k];
-            aggsh[w][0][lane * SPL + k] = Pw * Pn;
-            aggsh[w][1][lane * SPL + k] = __builtin_fma(Pw, Bn, Bw);
-        }
-    }
-    double* out = agg + (size_t)blockIdx.x * 2 * Dpad;  // segment index within the bucket
-    if (row_lane<SPL>(lane, Dpad))
-#pragma unroll
-        for (int k = 0; k < SPL; ++k) {
-            out[lane * SPL + k] = aggsh[0][0][lane * SPL + k];
-            out[Dpad + lane * SPL + k] = aggsh[0][1][lane * SPL + k];
-        }
+    up_pre_segment<SPL, CH, NSUB, VOL>(pa, view, (int)blockIdx.x, view ? V1.U : V0.U, view ? meta1 : meta0, view ? Cst1 : Cst0,
+                                       view ? Rrec : Lrec, view ? Lrec : Rrec, W, Dpad, dcall, dglob0, sh, sh.s2lut,
+                                       threadIdx.x & 63, (int)uniform(threadIdx.x >> 6));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2223,27 +2131,34 @@ static WalkView chain_view(const WalkArgs& a, int v) {
     return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v]};
 }
 
-#ifndef UP_PRE_CH2
-#define UP_PRE_CH2 8  // nodes per wave of k_up_pre at SPL=2
-#endif
-template <int SPL, int CH, bool VOL>
+UpPreArgs up_pre_args(const WalkArgs& a) {
+    UpPreArgs pa{};
+    for (int v = 0; v < 2; ++v) {
+        pa.paths[v] = a.paths[v];
+        pa.seg[v] = a.segtab[v];
+        pa.nseg[v] = a.nseg[v];
+        pa.agg[v] = a.pieces[v] ? a.agg[v] : nullptr;
+        pa.plen[v] = a.bucket_plen[v];
+    }
+    return pa;
+}
+
+template <int SPL, int CH, int NSUB, bool VOL>
 static void up_pre_launch_k(hipStream_t st, const WalkArgs& a) {
     const int ns = a.nseg[0] > a.nseg[1] ? a.nseg[0] : a.nseg[1];
     if (ns == 0) return;
-    hipLaunchKernelGGL((k_up_pre<SPL, CH, VOL>), dim3(ns, 2), dim3(64 * SM_PRE_SEG / CH), 0, st, chain_view(a, 0),
-                       chain_view(a, 1), reinterpret_cast<const uint32_t*>(a.meta[0]),
-                       reinterpret_cast<const uint32_t*>(a.meta[1]), a.paths[0], a.paths[1], a.segtab[0], a.segtab[1],
-                       a.nseg[0], a.nseg[1], a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad,
-                       a.dcall, a.dglob0, a.pieces[0] ? a.agg[0] : nullptr, a.pieces[1] ? a.agg[1] : nullptr, a.bucket_plen[0],
-                       a.bucket_plen[1]);
+    hipLaunchKernelGGL((k_up_pre<SPL, CH, NSUB, VOL>), dim3(ns, 2), dim3(256), 0, st, chain_view(a, 0), chain_view(a, 1),
+                       reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                       up_pre_args(a), a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
+                       a.dglob0);
 }
 
-template <int SPL, int CH>
+template <int SPL, int CH, int NSUB>
 static void up_pre_launch(hipStream_t st, const WalkArgs& a) {
     if (a.vol)  // cost rows in Cst (k_vol_rows)
-        up_pre_launch_k<SPL, CH, true>(st, a);
+        up_pre_launch_k<SPL, CH, NSUB, true>(st, a);
     else
-        up_pre_launch_k<SPL, CH, false>(st, a);
+        up_pre_launch_k<SPL, CH, NSUB, false>(st, a);
 }
 
 static PieceView piece_view(const WalkArgs& a, int v) {
@@ -2279,9 +2194,9 @@ static void down_chain_launch(hipStream_t st, const WalkArgs& a, int np, int sto
 
 hipError_t launch_up_pre(hipStream_t st, const WalkArgs& a, int spl) {
     switch (spl) {
-        case 1: up_pre_launch<1, 8>(st, a); break;
-        case 2: up_pre_launch<2, UP_PRE_CH2>(st, a); break;
-        default: up_pre_launch<4, 4>(st, a); break;
+        case 1: up_pre_launch<1, 8, 1>(st, a); break;
+        case 2: up_pre_launch<2, 8, 1>(st, a); break;
+        default: up_pre_launch<4, 4, 2>(st, a); break;
     }
     return hipGetLastError();
 }

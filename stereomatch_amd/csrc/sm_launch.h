@@ -133,7 +133,18 @@ hipError_t launch_lr_check(hipStream_t st, float* left, const float* right, int 
 hipError_t launch_lr_fill(hipStream_t st, float* left, const uint8_t* mask, int W, int H, int* scratch);
 hipError_t launch_occlusion(hipStream_t st, float* left, float* right, int W, int H, float thresh, int remove, float min_disp,
                             uint8_t* occ, int* scratch);
-hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
+// The segment aggregates of a round's cut long paths (sm_walk_util.h up_pre_segment).
+struct UpPreArgs {
+    const SmPath* paths[2];  // the round's long bucket
+    const uint2* seg[2];     // its segment table (cut paths only)
+    int nseg[2];
+    double* agg[2];          // segment aggregates (nullptr: no pieces in that view)
+    int plen[2];             // the bucket's piece length
+    int walk_blocks;         // fused walker launch: blocks [0, walk_blocks) walk, the rest are segments
+};
+UpPreArgs up_pre_args(const WalkArgs& long_bucket);
+// pre: the round's long bucket when its segment aggregates run as extra blocks of this launch
+hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths, const WalkArgs* pre = nullptr);
 hipError_t launch_down(hipStream_t st, const WalkArgs& a, int spl, bool long_paths);
 // long-path engine (sm_chain.hip): buckets of paths with >= SM_LONG_PATH nodes; k_up_pre only
 // computes the segment aggregates of paths cut into pieces

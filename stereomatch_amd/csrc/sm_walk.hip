@@ -27,6 +27,9 @@
 #include "sm_launch.h"
 #include "sm_walk_util.h"
 
+// segment blocks of the fused up launch (up_pre_segment): 4 waves x CH x NSUB nodes
+#define UP_PRE_CH(SPL) ((SPL) == 4 ? 4 : 8)
+#define UP_PRE_NSUB(SPL) ((SPL) == 4 ? 2 : 1)
 // paths per wave work item (a bucket's paths occupy consecutive slots: one contiguous range)
 #ifndef WALK_PPW_UP
 #define WALK_PPW_UP 6
@@ -223,13 +226,25 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
                                                  const uint32_t* __restrict__ Rrec4, const float* __restrict__ atab_g,
                                                  const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
                                                  int W, int Dpad, int dcall, int dglob0, const float* __restrict__ Cv0,
-                                                 const float* __restrict__ Cv1, int ppw, int leaf_cost) {
+                                                 const float* __restrict__ Cv1, int ppw, int leaf_cost, UpPreArgs pa) {
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
     const WalkView& V = view ? V1 : V0;
     const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
     const int lane = threadIdx.x & 63;
+#ifdef SM_PRE_FUSED  // A/B (sm_api.cpp up_round): the round's segment aggregates as extra blocks
+    if ((int)blockIdx.x >= pa.walk_blocks) {  // uniform: a segment of the round's cut long paths
+        const int sidx = (int)blockIdx.x - pa.walk_blocks;
+        if (sidx < pa.nseg[view])
+            up_pre_segment<SPL, UP_PRE_CH(SPL), UP_PRE_NSUB(SPL), VOL>(
+                pa, view, sidx, V.U, meta32, view ? Cv1 : Cv0, view ? Rrec : Lrec, view ? Lrec : Rrec, W, Dpad, dcall,
+                dglob0, sh, sh.s2lut, lane, (int)uniform(threadIdx.x >> 6));  // s2lut: unused by the up pass
+        return;
+    }
+#else
+    (void)pa;
+#endif
     // work item: ppw consecutive paths of the bucket = one contiguous slot range (the recurrence
     // restarts by itself at every path bottom: a leaf has no heavy child)
     const int pi0 = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw);
@@ -423,17 +438,17 @@ static int walk_ppw(int np, int dflt, bool down) {
 }
 
 template <int SPL, int CH>
-static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a, int ppw) {
+static void up_launch(hipStream_t st, dim3 g, const WalkArgs& a, int ppw, const UpPreArgs& pa) {
     if (a.vol)
         hipLaunchKernelGGL((k_up_walk<SPL, CH, true>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
-                           a.dglob0, a.Cst[0], a.Cst[1], ppw, a.leaf_cost);
+                           a.dglob0, a.Cst[0], a.Cst[1], ppw, a.leaf_cost, pa);
     else
         hipLaunchKernelGGL((k_up_walk<SPL, CH, false>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
                            reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
                            a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.Dpad, a.dcall,
-                           a.dglob0, a.Cst[0], a.Cst[1], ppw, a.leaf_cost);
+                           a.dglob0, a.Cst[0], a.Cst[1], ppw, a.leaf_cost, pa);
 }
 
 template <int SPL, int CH>
@@ -444,23 +459,27 @@ static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all
                        store_all ? 0 : a.leaf_cost);
 }
 
-hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths) {
+hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths, const WalkArgs* pre) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
-    if (np == 0) return hipSuccess;
     const int ppw = walk_ppw(np, WALK_PPW_UP, false);
     const int items = (np + ppw - 1) / ppw;
-    const dim3 g((items + 3) / 4, 2);
+    UpPreArgs pa{};
+    if (pre) pa = up_pre_args(*pre);
+    pa.walk_blocks = (items + 3) / 4;
+    const int ns = pa.nseg[0] > pa.nseg[1] ? pa.nseg[0] : pa.nseg[1];
+    if (pa.walk_blocks + ns == 0) return hipSuccess;
+    const dim3 g(pa.walk_blocks + ns, 2);
     if (long_paths) {
         switch (spl) {
-            case 1: up_launch<1, 8>(st, g, a, ppw); break;
-            case 2: up_launch<2, 8>(st, g, a, ppw); break;
-            default: up_launch<4, 4>(st, g, a, ppw); break;
+            case 1: up_launch<1, 8>(st, g, a, ppw, pa); break;
+            case 2: up_launch<2, 8>(st, g, a, ppw, pa); break;
+            default: up_launch<4, 4>(st, g, a, ppw, pa); break;
         }
     } else {
         switch (spl) {
-            case 1: up_launch<1, WALK_UP_CH1>(st, g, a, ppw); break;
-            case 2: up_launch<2, WALK_UP_CH2>(st, g, a, ppw); break;
-            default: up_launch<4, WALK_UP_CH4>(st, g, a, ppw); break;
+            case 1: up_launch<1, WALK_UP_CH1>(st, g, a, ppw, pa); break;
+            case 2: up_launch<2, WALK_UP_CH2>(st, g, a, ppw, pa); break;
+            default: up_launch<4, WALK_UP_CH4>(st, g, a, ppw, pa); break;
         }
     }
     return hipGetLastError();

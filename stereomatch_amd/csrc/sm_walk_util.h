@@ -6,6 +6,8 @@
 #include <stdint.h>
 
 #include "sm_common.h"
+#include "sm_launch.h"      // UpPreArgs
+#include "sm_layout_gpu.h"  // sm_piece_cut
 
 // per-view mutable state; the read-only metadata and path lists are separate __restrict__ kernel
 // arguments (kernarg-derived, provably unclobbered)
@@ -471,5 +473,105 @@ __device__ __forceinline__ void chunk_costs(const MetaVec<CH>& mv, int view, int
 #endif
             c[j][k] = (T)(ok ? v : 3.0f);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Segment aggregates of the up pass (the pieces' guessed inputs, sm_chain.hip "Pieces"): the
+// affine map x_first = P * x_below + B of one SM_PRE_SEG-node segment of a cut long path, with
+// b = Pre + sum(S_post * A_post) + C per node and x = S_heavy * x_below + b.  Approximate (any
+// rounding only moves a guess; the chains' results are repaired exactly).  Four waves of
+// CH * NSUB nodes each; run by k_up_pre or by the extra blocks of the round's fused walker launch.
+// ---------------------------------------------------------------------------------------------
+
+// scratch: >= 6 * 64 doubles of LDS (the up pass's idle s2lut table)
+template <int SPL, int CH, int NSUB, bool VOL>
+__device__ __forceinline__ void up_pre_segment(const UpPreArgs& pa, int view, int sidx, const double* __restrict__ U,
+                                               const uint32_t* __restrict__ meta32, const float* __restrict__ Cst,
+                                               const uint2* __restrict__ own, const uint2* __restrict__ oth, int W, int Dpad,
+                                               int dcall, int dglob0, const WalkShared& sh, double* scratch, int lane, int wv) {
+    static_assert(CH * NSUB * 4 == SM_PRE_SEG, "four waves per segment");
+    const uint2 sg = pa.seg[view][sidx];
+    const SmPath path = pa.paths[view][uniform(sg.x)];
+    const int head = (int)uniform(path.head), len = (int)uniform(path.len);
+    double* __restrict__ agg = pa.agg[view];
+    if (agg == nullptr || !sm_piece_cut((uint32_t)len, (uint32_t)pa.plen[view])) return;  // uniform over the block
+    const int dbase = dglob0 + lane * SPL;
+    const int dend = dglob0 + dcall;
+    double P[SPL], B[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        P[k] = 1.0;
+        B[k] = 0.0;
+    }
+#pragma unroll
+    for (int s = NSUB - 1; s >= 0; --s) {  // bottom-most nodes first
+        const int first = (int)uniform(sg.y * SM_PRE_SEG + (wv * NSUB + s) * CH);
+        const int n = max(0, min(CH, len - first));
+        if (n == 0) continue;  // uniform
+        MetaVec<CH> mv;
+        load_meta<CH>(mv, meta32, lane, head + first, 1, n);
+        float c[CH][SPL];
+        if constexpr (VOL) {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) load_cost_row<SPL>(Cst, (uint32_t)(head + first + (j < n ? j : n - 1)), Dpad, lane, c[j]);
+        } else {
+            ImgRecs<SPL, CH> rec;
+            load_recs<SPL, CH>(mv, n, view, lane, W, dbase, own, oth, rec);
+            chunk_costs<SPL, CH>(mv, view, W, dbase, dend, rec, sh.atab, c);
+        }
+#pragma unroll
+        for (int j = CH - 1; j >= 0; --j) {
+            if (j < n) {
+                const uint32_t lo = mfield(mv, j, 2), hi = mfield(mv, j, 3);
+                const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+                const double Sh = nch > 0 ? readlane_f64(sh.slut[cw_of(lo, hi, (int)hidx)], 0) : 0.0;
+                double b[SPL];
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) b[k] = 0.0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {  // every light child, in key order (rows loaded where used)
+                    if ((uint32_t)i < nch && (uint32_t)i != hidx) {
+                        const double S = readlane_f64(sh.slut[cw_of(lo, hi, i)], 0);
+                        double r[SPL];
+                        load_row<SPL>(U, mfield(mv, j, 4 + i), Dpad, lane, r);
+#pragma unroll
+                        for (int k = 0; k < SPL; ++k) b[k] = __builtin_fma(S, r[k], b[k]);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) {
+                    B[k] = __builtin_fma(Sh, B[k], b[k] + (double)c[j][k]);
+                    P[k] = Sh * P[k];
+                }
+            }
+        }
+    }
+    // segment = wave 0 o wave 1 o wave 2 o wave 3 (wave 3 holds the bottom-most nodes), one slice
+    // column at a time through the scratch
+    double* out = agg + (size_t)sidx * 2 * Dpad;  // segment index within the bucket
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        if (wv > 0) {
+            scratch[(wv - 1) * 128 + lane] = P[k];
+            scratch[(wv - 1) * 128 + 64 + lane] = B[k];
+        }
+        __syncthreads();
+        if (wv == 0) {
+            double Pr = scratch[2 * 128 + lane], Br = scratch[2 * 128 + 64 + lane];  // wave 3
+#pragma unroll
+            for (int w = 2; w >= 1; --w) {
+                const double Pw = scratch[(w - 1) * 128 + lane], Bw = scratch[(w - 1) * 128 + 64 + lane];
+                Br = __builtin_fma(Pw, Br, Bw);
+                Pr = Pw * Pr;
+            }
+            Br = __builtin_fma(P[k], Br, B[k]);
+            Pr = P[k] * Pr;
+            if (row_lane<SPL>(lane, Dpad)) {
+                out[lane * SPL + k] = Pr;
+                out[Dpad + lane * SPL + k] = Br;
+            }
+        }
+        __syncthreads();
     }
 }
