@@ -282,6 +282,223 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
 }
 
 // ---------------------------------------------------------------------------------------------
+// Half-wave walkers (SPL = 1 calls with 64-double rows, e.g. a 64-slice view-group shard at N = 8).
+// At SPL = 1 a node step costs a wave the same instructions as at SPL = 2: the per-node metadata,
+// LUT and branch work does not shrink with the slices.  Here each half-wave of 32 lanes walks its
+// own work item with 2 slices per lane, i.e. two paths per wave-step.  Values the full-wave
+// walkers keep wave-uniform are per half (two readlanes and a select, or a ds_bpermute); rows are
+// the same [slot][64] rows (lane l of a half holds slices 2(l%32), 2(l%32)+1) and the arithmetic
+// is the full-wave walkers' exactly.  A half whose item is finished (or empty) re-reads its last
+// chunk and stores nothing.  Metadata: lane 32h + 8j + f holds word f of half h's node j.
+// ---------------------------------------------------------------------------------------------
+template <int CH>
+__device__ __forceinline__ uint32_t hfield(uint32_t w, int hl, int j, int f) {
+    const uint32_t a = __builtin_amdgcn_readlane(w, 8 * j + f), b = __builtin_amdgcn_readlane(w, 32 + 8 * j + f);
+    return hl ? b : a;
+}
+// word f of node j of this lane's half, j and f per lane (call with every lane active)
+__device__ __forceinline__ uint32_t hfield_v(uint32_t w, int hl, int j, int f) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(((hl << 5) + 8 * j + f) << 2, (int)w);
+}
+
+#ifndef WALK_UP_CHH
+#define WALK_UP_CHH 3
+#endif
+
+template <int CH>
+__device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int view, int lane, int W, int dbase, int dend,
+                                            const uint2* __restrict__ own, const uint32_t* __restrict__ oth4,
+                                            double* __restrict__ U, const WalkShared& sh, double (&xc)[2], uint32_t& nxt,
+                                            const uint32_t* __restrict__ meta32, int mtop, int mn, int leaf_cost) {
+    static_assert(CH <= 4, "lane 32h + 8j + f holds word f of half h's node j");
+    constexpr int LR = WALK_UP_LR;
+    constexpr int DP = 64;
+    const int hl = lane >> 5, hlane = lane & 31;
+    const int nv = n > 0 ? n : 1;  // rows / records of a finished half: its chunk's first node
+    // ---- light-row bookkeeping (per half): node j's light children are compact rows off[j] ..
+    int off[CH];
+    int tot = 0;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const uint32_t nch = j < n ? hi_nch(hfield<CH>(mv, hl, j, 3)) : 0u;
+        off[j] = tot;
+        tot += nch > 0 ? (int)nch - 1 : 0;
+    }
+    double lr[LR][2];
+#pragma unroll
+    for (int q = 0; q < LR; ++q) {
+        int jq = 0, oq = off[0];
+#pragma unroll
+        for (int j = 1; j < CH; ++j) {
+            jq = off[j] <= q ? j : jq;
+            oq = off[j] <= q ? off[j] : oq;
+        }
+        const uint32_t hidx = hi_hidx(hfield_v(mv, hl, jq, 3));
+        const int kk = q - oq;
+        const int pos = kk + (kk >= (int)hidx ? 1 : 0);
+        const uint32_t slot = hfield_v(mv, hl, jq, 4 + min(max(pos, 0), 3));
+        if (q < tot) {
+            load_row<2>(U, slot, DP, hlane, lr[q]);
+        } else {
+            lr[q][0] = 0.0;
+            lr[q][1] = 0.0;
+        }
+    }
+    // ---- image records: lane 32h + i (i < 16) own(x) of node min(i, n-1), lane 32h + 16 + i own(x+1)
+    uint2 ownr;
+    {
+        const int node = min(hlane & 15, nv - 1);
+        uint32_t pl = hfield<CH>(mv, hl, 0, 0);
+#pragma unroll
+        for (int j = 1; j < CH; ++j) pl = node == j ? hfield<CH>(mv, hl, j, 0) : pl;
+        ownr = own[(long long)pl + (hlane >> 4)];
+    }
+    uint32_t ob[CH][3];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        // node j >= n: its metadata lanes already hold node n - 1's words (clamped load); the
+        // readlane index must stay uniform
+        const long long pix = (long long)hfield<CH>(mv, hl, j, 0);
+        const long long base = view ? pix + dbase : pix - dbase - 1;
+#pragma unroll
+        for (int q = 0; q <= 2; ++q) ob[j][q] = oth4[base + q];
+    }
+    nxt = meta32[(size_t)(mtop - min(hlane >> 3, mn - 1)) * 8 + (lane & 7)];
+    walk_vm_drain();
+    // ---- costs (chunk_costs4 at SPL = 2, per half) and edge factors
+    float c[CH][2];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const int x = pix_col((int)hfield<CH>(mv, hl, j, 0), W);
+        const uint32_t ox0 = hfield<CH>(ownr.x, hl, 0, j), oy0 = hfield<CH>(ownr.y, hl, 0, j);
+        const uint32_t ox1 = hfield<CH>(ownr.x, hl, 2, j), oy1 = hfield<CH>(ownr.y, hl, 2, j);  // lanes 32h + 16 + j
+        const float go0 = __uint_as_float(oy0), go1 = __uint_as_float(oy1);
+        float g[3];
+#pragma unroll
+        for (int q = 0; q <= 2; ++q) g[q] = gray4(ob[j][q]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int d = dbase + k;
+            float v;
+            bool ok;
+            if (view) {
+                ok = d < dend && x + d + 1 < W;
+                v = agd4(ox0, ob[j][k], go0, g[k], go1, g[k + 1], sh.atab);
+            } else {
+                ok = d < dend && x - d >= 0 && x + 1 < W;
+                v = agd4(ob[j][1 - k], ox0, g[1 - k], go0, g[2 - k], go1, sh.atab);
+            }
+            c[j][k] = ok ? v : 3.0f;
+        }
+        (void)ox1;
+    }
+    // edge factors of the first two children up front (per lane: LDS reads); a third or fourth
+    // child (rare) reads its factor where the recurrence uses it
+    double Sv[CH][2];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const uint32_t lo = hfield<CH>(mv, hl, j, 2), hi = hfield<CH>(mv, hl, j, 3);
+        const uint32_t nch = hi_nch(hi);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) Sv[j][i] = sh.slut[(uint32_t)i < nch ? cw_of(lo, hi, i) : (uint32_t)S_ZERO];
+    }
+    // ---- serial recurrence along the path (bottom -> top)
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const uint32_t hi = hfield<CH>(mv, hl, j, 3);
+        const uint32_t par = hfield<CH>(mv, hl, j, 1);
+        uint32_t cs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cs[i] = hfield<CH>(mv, hl, j, 4 + i);
+        if (j < n) {
+            const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
+            double acc[2] = {0.0, 0.0};
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                if (i < nch) {
+                    double v[2];
+                    if (i == hidx) {
+                        v[0] = xc[0];
+                        v[1] = xc[1];
+                    } else {
+                        const int q = off[j] + (int)i - (i > hidx ? 1 : 0);
+                        bool held = false;
+#pragma unroll
+                        for (int r = 0; r < LR; ++r) {
+                            if (q == r) {
+                                v[0] = lr[r][0];
+                                v[1] = lr[r][1];
+                                held = true;
+                            }
+                        }
+                        if (!held) load_row<2>(U, cs[i], DP, hlane, v);  // rare: loaded here
+                    }
+                    const double S = i < 2 ? Sv[j][i < 2 ? i : 0] : sh.slut[cw_of(hfield<CH>(mv, hl, j, 2), hi, (int)i)];
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) acc[k] = __builtin_fma(S, v[k], acc[k]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) xc[k] = acc[k] + (double)c[j][k];
+            if (leaf_cost && nch == 0 && par != SM_NONE && par == (uint32_t)(top - j) - 1u)
+                store_leaf_row<2>(U, (uint32_t)(top - j), DP, hlane, c[j]);
+            else
+                store_row<2>(U, (uint32_t)(top - j), DP, hlane, xc);
+        }
+    }
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_up_walk_h2(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
+                                                    const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
+                                                    const SmPath* __restrict__ paths1, const uint2* __restrict__ Lrec,
+                                                    const uint2* __restrict__ Rrec, const uint32_t* __restrict__ Lrec4,
+                                                    const uint32_t* __restrict__ Rrec4, const float* __restrict__ atab_g,
+                                                    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
+                                                    int W, int dcall, int dglob0, int ppw, int leaf_cost) {
+    __shared__ WalkShared sh;
+    load_tables(sh, atab_g, slut_g, s2lut_g);
+    const int view = blockIdx.y;
+    const WalkView& V = view ? V1 : V0;
+    const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
+    const int lane = threadIdx.x & 63, hl = lane >> 5, hlane = lane & 31;
+    const int wave = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (2 * wave * ppw >= V.npaths) return;  // uniform: both halves empty
+    const SmPath* __restrict__ pp = view ? paths1 : paths0;
+    const int pi0 = (2 * wave + hl) * ppw;
+    int head = 0, len = 0;
+    if (pi0 < V.npaths) {
+        const int pi1 = min(pi0 + ppw, V.npaths);
+        head = (int)pp[pi0].head;
+        len = (int)(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
+    }
+    const int dbase = dglob0 + hlane * 2;
+    const int dend = dglob0 + dcall;
+    const uint2* __restrict__ own = view ? Rrec : Lrec;
+    const uint32_t* __restrict__ oth4 = view ? Lrec4 : Rrec4;
+    double xc[2] = {0.0, 0.0};
+    int top = len > 0 ? head + len - 1 : 0;
+    int n = min(CH, len);
+    uint32_t cur = meta32[(size_t)(top - min(hlane >> 3, max(n, 1) - 1)) * 8 + (lane & 7)];
+    walk_vm_drain();
+    while (true) {
+        const int ntop = top - CH;
+        const int nn = (n > 0 && ntop >= head) ? min(CH, ntop - head + 1) : 0;
+        uint32_t nxt;
+        up_chunk_h2<CH>(cur, n, top, view, lane, W, dbase, dend, own, oth4, V.U, sh, xc, nxt, meta32, nn > 0 ? ntop : top,
+                        nn > 0 ? nn : max(n, 1), leaf_cost);
+        if (__ballot(nn > 0) == 0) break;
+        cur = nxt;
+        if (nn > 0) {
+            top = ntop;
+            n = nn;
+        } else {
+            n = 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // down pass + WTA
 // ---------------------------------------------------------------------------------------------
 template <int SPL, int CH>
@@ -408,6 +625,171 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
 }
 
 // ---------------------------------------------------------------------------------------------
+// Half-wave down walker: SPL = 1 calls with 64-double rows (a 64-slice shard, e.g. a view-group
+// rank at N = 8).  At SPL = 1 a node step costs a wave the same instructions as at SPL = 2 (the
+// per-node metadata, LUT and branch work does not shrink with the slices), so here each half-wave
+// of 32 lanes walks its own work item with 2 slices per lane: two paths per wave-step.  Per-node
+// values that k_down_walk keeps wave-uniform are per half (two readlanes and a select); rows are
+// the same [slot][64] rows (lane l of a half holds slices 2(l%32), 2(l%32)+1), the arithmetic is
+// k_down_walk's exactly.  A half whose item is finished keeps re-reading its last chunk and stores
+// nothing.
+// wta_chunk per half-wave: lane 32h + j (< CH) gets node j of half h's strict-< first minimum
+template <int CH>
+__device__ __forceinline__ void wta_half(const double (&x)[CH][2], int lane, int lo, int hi, double& out_min, int& out_idx) {
+    const int hl = lane >> 5, hlane = lane & 31, dloc0 = hlane * 2;
+    double bv[CH], g[CH];
+    int bi[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        bv[j] = __builtin_huge_val();
+        bi[j] = 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int d = dloc0 + k;
+            if (d >= lo && d < hi && x[j][k] < bv[j]) { bv[j] = x[j][k]; bi[j] = d; }
+        }
+        g[j] = bv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0xB1>(g[j]);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0x4E>(g[j]);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0x141>(g[j]);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) g[j] = dpp_min<0x140>(g[j]);  // min over each row of 16 lanes
+    out_min = 0.0;
+    out_idx = 0;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const double m0 = fmin(readlane_f64(g[j], 0), readlane_f64(g[j], 16));
+        const double m1 = fmin(readlane_f64(g[j], 32), readlane_f64(g[j], 48));
+        const double m = hl ? m1 : m0;
+        const unsigned long long ball = __ballot(bv[j] == m && bi[j] != 0x7fffffff);
+        const uint32_t b0 = (uint32_t)ball, b1 = (uint32_t)(ball >> 32);
+        const int g0 = b0 ? __builtin_amdgcn_readlane(bi[j], (int)__builtin_ctz(b0)) : 0;
+        const int g1 = b1 ? __builtin_amdgcn_readlane(bi[j], 32 + (int)__builtin_ctz(b1)) : 0;
+        if (hlane == j) { out_min = m; out_idx = hl ? g1 : g0; }
+    }
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
+                                                      const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
+                                                      const SmPath* __restrict__ paths1, const float* __restrict__ atab_g,
+                                                      const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
+                                                      WtaCfg w, int store_all, int ppw, int leaf_cost) {
+    static_assert(CH <= 4, "lane 32h + 8j + f holds word f of half h's node j");
+    constexpr int DP = 64;  // row length (doubles)
+    __shared__ WalkShared sh;
+    load_tables(sh, atab_g, slut_g, s2lut_g);
+    const int view = blockIdx.y;
+    const WalkView& V = view ? V1 : V0;
+    const uint32_t* __restrict__ meta32 = view ? meta1 : meta0;
+    const int lane = threadIdx.x & 63, hl = lane >> 5, hlane = lane & 31;
+    // work items 2*wave (lanes 0-31) and 2*wave+1 (lanes 32-63); an empty half has len 0
+    const int wave = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (2 * wave * ppw >= V.npaths) return;  // uniform: both halves empty
+    const SmPath* __restrict__ pp = view ? paths1 : paths0;
+    const int pi0 = (2 * wave + hl) * ppw;
+    int head = 0, len = 0;
+    if (pi0 < V.npaths) {
+        const int pi1 = min(pi0 + ppw, V.npaths);
+        head = (int)pp[pi0].head;
+        len = (int)(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
+    }
+    double xc[2] = {0.0, 0.0};
+    int c0 = head;
+    int n = min(CH, len);  // 0: this half is finished (or empty)
+    // metadata: lane 32h + 8j + f holds word f of node j of half h (clamped to a valid node)
+    uint32_t cur = meta32[(size_t)(c0 + min(hlane >> 3, max(n, 1) - 1)) * 8 + (lane & 7)];
+    walk_vm_drain();
+    while (true) {
+        const int nc0 = c0 + CH;
+        const int nn = (n > 0 && nc0 < head + len) ? min(CH, head + len - nc0) : 0;
+        double u[CH][2], xp[CH][2];
+        uint32_t par[CH], hiw[CH];
+        bool leaf[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            // node j >= n: the metadata lanes of node j already hold node n - 1's words (clamped
+            // load), so readlane indices stay uniform; only the slot is clamped per lane
+            const uint32_t slot = (uint32_t)(c0 + min(j, max(n, 1) - 1));
+            par[j] = hfield<CH>(cur, hl, j, 1);
+            hiw[j] = hfield<CH>(cur, hl, j, 3);
+            const bool head_j = par[j] == SM_NONE || par[j] != slot - 1u;
+            leaf[j] = leaf_cost && !head_j && hi_nch(hiw[j]) == 0u;
+            if (!leaf[j])
+                load_row<2>(V.U, slot, DP, hlane, u[j]);
+            else
+                load_leaf_row<2>(V.U, slot, DP, hlane, u[j]);
+            if (head_j && par[j] != SM_NONE) {
+                load_row<2>(V.A, par[j], DP, hlane, xp[j]);
+            } else {
+                xp[j][0] = 0.0;
+                xp[j][1] = 0.0;
+            }
+        }
+        // the next chunk's metadata behind the rows (a finished half re-reads its last chunk's)
+        const int mc0 = nn > 0 ? nc0 : c0;
+        const int mn_ = nn > 0 ? nn : max(n, 1);
+        const uint32_t nxt = meta32[(size_t)(mc0 + min(hlane >> 3, mn_ - 1)) * 8 + (lane & 7)];
+        walk_vm_drain();
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+            if (leaf[j]) widen_leaf_row<2>(u[j]);
+        double S[CH], S2[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const uint32_t wp = lo_wp(hfield<CH>(cur, hl, j, 2));
+            S[j] = sh.slut[wp];
+            S2[j] = sh.s2lut[wp];
+        }
+        double xs[CH][2];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (j < n) {
+                const uint32_t slot = (uint32_t)(c0 + j);
+                const bool root = par[j] == SM_NONE;
+                const bool hd = !root && par[j] != slot - 1u;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const double b = hd ? xp[j][k] : xc[k];
+                    const double f = __builtin_fma(S[j], b, S2[j] * u[j][k]);
+                    xc[k] = root ? u[j][k] : f;
+                }
+            }
+            xs[j][0] = xc[0];
+            xs[j][1] = xc[1];
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (j < n && (store_all || hi_light(hiw[j]))) store_row<2>(V.A, (uint32_t)(c0 + j), DP, hlane, xs[j]);
+        }
+        double mn;
+        int mi;
+        wta_half<CH>(xs, lane, w.lo, w.hi, mn, mi);
+        const int gi = w.dglob0 + mi;
+        // lane 32h + j (< CH) stores node j of half h: its pixel is word 0 at lane 32h + 8j
+        const int src = ((hl << 5) + ((hlane & 3) << 3)) << 2;
+        const uint32_t pix = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cur);
+        if (hlane < n) {
+            V.idx[pix] = gi;
+            V.minc[pix] = mn;
+            V.disp[pix] = (float)gi;
+        }
+        if (__ballot(nn > 0) == 0) break;
+        cur = nxt;
+        if (nn > 0) {
+            c0 = nc0;
+            n = nn;
+        } else {
+            n = 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 static WalkView to_view(const WalkArgs& a, int v) {
     return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v]};
 }
@@ -459,8 +841,26 @@ static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all
                        store_all ? 0 : a.leaf_cost);
 }
 
+// SPL = 1 calls with 64-double rows take the half-wave walkers (env SM_NO_HALF_WAVE: A/B)
+static bool half_wave(const WalkArgs& a, int spl) {
+    static const bool off = getenv("SM_NO_HALF_WAVE") != nullptr;
+    return !off && spl == 1 && a.Dpad == 64;
+}
+
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths, const WalkArgs* pre) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
+    if (!long_paths && !pre && !a.vol && half_wave(a, spl)) {
+        if (np == 0) return hipSuccess;
+        const int ppw = walk_ppw(np, WALK_PPW_UP, false);
+        const int items = (np + ppw - 1) / ppw;
+        const int waves = (items + 1) / 2;
+        const dim3 g((waves + 3) / 4, 2);
+        hipLaunchKernelGGL((k_up_walk_h2<WALK_UP_CHH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
+                           reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.dcall,
+                           a.dglob0, ppw, a.leaf_cost);
+        return hipGetLastError();
+    }
     const int ppw = walk_ppw(np, WALK_PPW_UP, false);
     const int items = (np + ppw - 1) / ppw;
     UpPreArgs pa{};
@@ -485,9 +885,25 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
     return hipGetLastError();
 }
 
+// SPL = 1 calls with 64-double rows take the half-wave down walker (env SM_NO_HALF_WAVE: A/B)
+#ifndef WALK_DN_CHH
+#define WALK_DN_CHH 4
+#endif
+static bool half_wave_down(const WalkArgs& a, int spl) { return half_wave(a, spl) && !a.wta.sub; }
+
 static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, int store_all, bool long_paths) {
     const int np = a.npaths[0] > a.npaths[1] ? a.npaths[0] : a.npaths[1];
     if (np == 0) return hipSuccess;
+    if (!long_paths && half_wave_down(a, spl)) {
+        const int ppw = walk_ppw(np, WALK_PPW_DN, true);
+        const int items = (np + ppw - 1) / ppw;
+        const int waves = (items + 1) / 2;
+        const dim3 g((waves + 3) / 4, 2);
+        hipLaunchKernelGGL((k_down_walk_h2<WALK_DN_CHH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
+                           reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                           a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.wta, store_all, ppw, store_all ? 0 : a.leaf_cost);
+        return hipGetLastError();
+    }
     const int ppw = walk_ppw(np, WALK_PPW_DN, true);
     const int items = (np + ppw - 1) / ppw;
     const dim3 g((items + 3) / 4, 2);
