@@ -145,6 +145,8 @@ def main():
     ap.add_argument("--emulate-rank", default=None, metavar="R/N",
                     help="one GPU runs rank R's share of an N-rank strong-mode frame (no collective): the per-rank "
                          "cost of the partition, for the multi-GPU estimate in DESIGN.md 7")
+    ap.add_argument("--no-split", action="store_true",
+                    help="A/B: stream frames with sm_match_async instead of sm_match_begin/finish")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight (contexts on their own streams); 0 = 3, fewer where memory needs it")
     args = ap.parse_args()
@@ -260,10 +262,22 @@ def main():
         accumulate(kacc, c)
 
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ctxs[i % inflight].match_async(Dloc, params)  # returns once the frame's filter is enqueued
-        if i >= inflight - 1:
-            retire(ctxs[(i - inflight + 1) % inflight])
+    if inflight == 1 or args.no_split:
+        for i in range(args.steps):
+            ctxs[i % inflight].match_async(Dloc, params)  # returns once the frame's filter is enqueued
+            if i >= inflight - 1:
+                retire(ctxs[(i - inflight + 1) % inflight])
+    else:
+        # split calls: frame i's tree is enqueued (match_begin) before the host waits for frame
+        # i-1's layout and enqueues its filter (match_finish), so the GPU never idles on the host
+        for i in range(args.steps):
+            ctxs[i % inflight].match_begin(Dloc, params)
+            if i >= 1:
+                ctxs[(i - 1) % inflight].match_finish()
+            if i >= inflight - 1:
+                retire(ctxs[(i - inflight + 1) % inflight])
+        if args.steps > 0:
+            ctxs[(args.steps - 1) % inflight].match_finish()
     for i in range(max(0, args.steps - inflight + 1), args.steps):
         retire(ctxs[i % inflight])
     torch.cuda.synchronize()

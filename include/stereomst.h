@@ -135,6 +135,14 @@ sm_status sm_match(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bg
 sm_status sm_upload_images(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
                            int row_stride);
 sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p);
+/* sm_match_async in two halves.  sm_match_begin enqueues prep, MST and tree layout and returns
+ * without waiting; sm_match_finish waits for the layout's per-round counts (the host sizes the
+ * filter launches from them) and enqueues the filter, the cross-rank reduce and the output step.
+ * A caller streaming frames over several contexts begins frame i+1 before it finishes frame i,
+ * so the GPU has the next frame's tree queued while the host waits.  One begin per finish, per
+ * context (SM_ERR_STATE otherwise); sm_match_async == begin + finish. */
+sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p);
+sm_status sm_match_finish(sm_ctx* ctx);
 sm_status sm_synchronize(sm_ctx* ctx);
 sm_status sm_download_results(sm_ctx* ctx, float* left_disp, float* right_disp, int32_t* left_idx,
                               int32_t* right_idx, double* left_min, double* right_min);

@@ -75,6 +75,8 @@ def lib():
         "sm_upload_images": ([vp, vp, vp, ci, ci, ci], ci),
         "sm_upload_cost_volumes": ([vp, vp, vp, ci, ci, ci], ci),
         "sm_match_async": ([vp, ci, ctypes.POINTER(SmParams)], ci),
+        "sm_match_begin": ([vp, ci, ctypes.POINTER(SmParams)], ci),
+        "sm_match_finish": ([vp], ci),
         "sm_synchronize": ([vp], ci),
         "sm_download_results": ([vp, vp, vp, vp, vp, vp, vp], ci),
         "sm_cost_volume": ([vp, vp, vp, ci, ci, ci, ci, ci, vp, vp], ci),
@@ -193,6 +195,16 @@ class Context:
         p = params or default_params()
         self._views = p.views or 3
         self._check(lib().sm_match_async(self.h, D, ctypes.byref(p)))
+
+    def match_begin(self, D, params=None):
+        """sm_match_begin: enqueue prep, MST and layout; the filter follows in match_finish."""
+        p = params or default_params()
+        self._views = p.views or 3
+        self._check(lib().sm_match_begin(self.h, D, ctypes.byref(p)))
+
+    def match_finish(self):
+        """sm_match_finish: wait for the layout's round counts, enqueue filter, reduce, output step."""
+        self._check(lib().sm_match_finish(self.h))
 
     def synchronize(self):
         self._check(lib().sm_synchronize(self.h))

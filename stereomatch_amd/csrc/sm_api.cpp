@@ -102,6 +102,12 @@ struct sm_ctx {
         std::vector<uint32_t> begin, maxlen, seg_begin, nodes, piece_begin;  // per bucket
     } layout[2];
     hipEvent_t ev[8] = {};
+    hipEvent_t ev_layout = nullptr;  // after the layout's round-count copy (stage_layout_finish waits)
+    // sm_match_begin -> sm_match_finish: the call in between (0: none, 1: tree enqueued, 2: guided,
+    // fully enqueued by begin)
+    int pending = 0;
+    int pend_D = 0;
+    sm_params pend_p{};
     // tree-filter launch timing: timed launch k runs between events fev[fam_ev[k]] on its stream
     std::vector<hipEvent_t> fev;
     std::vector<int> fam;
@@ -481,7 +487,18 @@ int piece_len() {  // read per call: tests switch it between matches
 // device-side rounds record: [0, SM_NBUCKETS] bucket begin, then count, cursor, nrounds, n_has_light
 constexpr size_t RREC = RREC_FWD;
 
+// The layout in two halves: stage_layout_enqueue launches it and the copy of the per-round
+// counts; stage_layout_finish waits for that copy (the host sizes the walker grids from it) and
+// reads it.  sm_match_begin / sm_match_finish put the host wait between them, so a caller can
+// enqueue the next frame's tree before it waits for this frame's layout.
+sm_status stage_layout_enqueue(sm_ctx* ctx, int views);
+sm_status stage_layout_finish(sm_ctx* ctx, int views);
 sm_status stage_layout(sm_ctx* ctx, int views) {
+    CHECK(stage_layout_enqueue(ctx, views));
+    return stage_layout_finish(ctx, views);
+}
+
+sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
     const ViewSet vs(views);
     const int nviews = vs.n;
     const int W = ctx->W, H = ctx->H;
@@ -586,7 +603,12 @@ sm_status stage_layout(sm_ctx* ctx, int views) {
     // the host needs the per-round path counts to size the walker grids
     for (int i = 0; i < nviews; ++i)
         HIPC(hipMemcpyAsync(ctx->h_rounds + vs.v[i] * RREC, ctx->rounds[vs.v[i]].p, RREC * 4, hipMemcpyDeviceToHost, ctx->st));
-    HIPC(hipStreamSynchronize(ctx->st));
+    HIPC(hipEventRecord(ctx->ev_layout, ctx->st));
+    return SM_OK;
+}
+
+sm_status stage_layout_finish(sm_ctx* ctx, int views) {
+    HIPC(hipEventSynchronize(ctx->ev_layout));
     bool grew = false;
     CHECK(mst_finish(ctx, &grew));
     if (grew) return stage_layout(ctx, views);  // the forest was incomplete: lay out the final MST
@@ -1148,6 +1170,7 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
     }
     for (auto& e : ctx->ev)  // stage-boundary timing events
         if (hipEventCreateWithFlags(&e, timing_event_flags()) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
+    if (hipEventCreateWithFlags(&ctx->ev_layout, hipEventDisableTiming) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
     // tables: S/S2 (correctly rounded, tools/gen_tables.py) and the AGD colour term
     std::vector<float> atab(SM_MAX_W + 1);
     for (int i = 0; i <= SM_MAX_W; ++i) atab[i] = agd_color_term(i);
@@ -1180,6 +1203,7 @@ void sm_destroy(sm_ctx* ctx) {
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    if (ctx->ev_layout) (void)hipEventDestroy(ctx->ev_layout);
     for (auto e : ctx->fev) (void)hipEventDestroy(e);
     for (auto e : ctx->sev) (void)hipEventDestroy(e);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
@@ -1224,8 +1248,9 @@ sm_status sm_upload_cost_volumes(sm_ctx* ctx, const float* left_vol, const float
     return SM_OK;
 }
 
-sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
+sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_match_begin: the previous call was not finished (sm_match_finish)");
     if (ctx->W == 0) return fail(ctx, SM_ERR_STATE, "no images uploaded");
     CHECK(check_params(ctx, p, D));
     const CallRange cr = call_range(p, D);
@@ -1257,11 +1282,29 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
         CHECK(stage_reduce(ctx));
         CHECK(stage_post(ctx, p->post, p->disp_total > 0 ? p->disp_total : p->disp_begin + D));
         HIPC(hipEventRecord(ctx->ev[5], ctx->st));
+        ctx->pending = 2;
         return SM_OK;
     }
     CHECK(stage_tree(ctx, ctx->views, p));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
-    CHECK(stage_layout(ctx, ctx->views));
+    CHECK(stage_layout_enqueue(ctx, ctx->views));
+    ctx->pending = 1;
+    ctx->pend_D = D;
+    ctx->pend_p = *p;
+    return SM_OK;
+}
+
+sm_status sm_match_finish(sm_ctx* ctx) {
+    if (!ctx) return SM_ERR_ARG;
+    if (!ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_match_finish without sm_match_begin");
+    const int kind = ctx->pending;
+    ctx->pending = 0;
+    if (kind == 2) return SM_OK;  // guided: enqueued in full by sm_match_begin
+    HIPC(hipSetDevice(ctx->device));
+    const sm_params* p = &ctx->pend_p;
+    const int D = ctx->pend_D;
+    const CallRange cr = call_range(p, D);
+    CHECK(stage_layout_finish(ctx, ctx->views));
     HIPC(hipEventRecord(ctx->ev[3], ctx->st));
     CHECK(stage_filter(ctx, cr.D, cr.d0, ctx->views, false, &cr.w));
     HIPC(hipEventRecord(ctx->ev[4], ctx->st));
@@ -1269,6 +1312,11 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
     CHECK(stage_post(ctx, p->post, p->disp_total > 0 ? p->disp_total : p->disp_begin + D));
     HIPC(hipEventRecord(ctx->ev[5], ctx->st));
     return SM_OK;
+}
+
+sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
+    CHECK(sm_match_begin(ctx, D, p));
+    return sm_match_finish(ctx);
 }
 
 sm_status sm_synchronize(sm_ctx* ctx) {

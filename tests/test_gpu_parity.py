@@ -898,3 +898,37 @@ def test_guided_errors(gpu_ctx):
                 dict(post=sm.SM_POST_SUBPIXEL, disp_begin=2, disp_total=16)):
         with pytest.raises(sm.StereoMSTError):
             gpu_ctx.match(left, right, 8, sm.default_params(aggregator=sm.SM_AGG_GUIDED, **bad))
+
+
+def test_split_calls_interleaved_bitexact():
+    """sm_match_begin / sm_match_finish interleaved over two contexts (frame i+1's tree enqueued
+    before frame i's filter, as bench.py streams frames) give the oracle's answer bitwise; a
+    finish without a begin and a second begin are SM_ERR_STATE."""
+    import stereomatch_amd as sm
+    from stereomatch_amd._lib import SM_ERR_STATE, StereoMSTError
+    pairs = [make_pair(256, 160, D, index=i) for i, D in ((3, 64), (4, 128))]
+    ctxs = [sm.Context(0), sm.Context(0)]
+    try:
+        for c, (l, r, _) in zip(ctxs, pairs):
+            c.upload(l, r)
+        Ds = (64, 128)
+        ctxs[0].match_begin(Ds[0])
+        ctxs[1].match_begin(Ds[1])
+        with pytest.raises(StereoMSTError) as e:
+            ctxs[1].match_begin(Ds[1])
+        assert e.value.status == SM_ERR_STATE
+        ctxs[0].match_finish()
+        ctxs[1].match_finish()
+        with pytest.raises(StereoMSTError) as e:
+            ctxs[0].match_finish()
+        assert e.value.status == SM_ERR_STATE
+        for c, (l, r, _), D in zip(ctxs, pairs, Ds):
+            c.synchronize()
+            out = c.results()
+            ref = O.match(l, r, D, nthreads=16)
+            for v in ("left", "right"):
+                np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
+                assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+    finally:
+        for c in ctxs:
+            c.close()
