@@ -58,6 +58,13 @@ struct sm_ctx {
     // ~30 us cross-stream join and the throughput-bound k_up_pre only competes with the walkers --
     // so it aliases st; the round code keeps the two-stream structure (join() is then a no-op).
     hipStream_t st2 = nullptr;
+    // A/B (env SM_TREE_STREAM=1): sm_match_begin's prep / MST / layout on st_tree, a lower-priority
+    // stream, with st (the filter) waiting for the layout by event, so that with frames in flight
+    // the filter's launches dispatch ahead of the other frames' tree kernels.  Measured slower
+    // (C2 4.82 -> 5.43-5.50 ms/frame, N = 8 share 2.28 -> 2.90 ms; GPU_MAX_HW_QUEUES=8 the same):
+    // nullptr by default, everything on st.
+    hipStream_t st_tree = nullptr;
+    hipEvent_t ev_enq = nullptr;  // recorded on st at sm_match_begin: st_tree waits for it
     std::string err;
     int W = 0, H = 0, stride = 0;
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
@@ -1153,6 +1160,21 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         return SM_ERR_HIP;
     }
     ctx->st2 = ctx->st;
+    {
+        const char* e = getenv("SM_TREE_STREAM");
+        if (e && atoi(e) == 1) {
+            int least = 0, greatest = 0;
+            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                hipStreamDestroy(ctx->st) != hipSuccess ||
+                hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, greatest) != hipSuccess ||
+                hipStreamCreateWithPriority(&ctx->st_tree, hipStreamNonBlocking, least) != hipSuccess ||
+                hipEventCreateWithFlags(&ctx->ev_enq, hipEventDisableTiming) != hipSuccess) {
+                delete ctx;
+                return SM_ERR_HIP;
+            }
+            ctx->st2 = ctx->st;
+        }
+    }
     if (getenv("SM_TWO_STREAMS") && hipStreamCreateWithFlags(&ctx->st2, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return SM_ERR_HIP;
@@ -1219,6 +1241,9 @@ void sm_destroy(sm_ctx* ctx) {
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
+    if (ctx->st_tree) (void)hipStreamSynchronize(ctx->st_tree);
+    if (ctx->st_tree) (void)hipStreamDestroy(ctx->st_tree);
+    if (ctx->ev_enq) (void)hipEventDestroy(ctx->ev_enq);
     if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamDestroy(ctx->st2);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     delete ctx;
@@ -1264,6 +1289,19 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipSetDevice(ctx->device));
     ctx->rec_pad = rec_pad_for(cr.d0, cr.D);
     ctx->sub = cr.w.sub != 0;
+    // the tree stages on st_tree (after everything enqueued on st so far: the image upload and the
+    // previous frame, whose buffers the tree overwrites); st waits for the layout's event
+    struct TreeStream {
+        sm_ctx* c;
+        hipStream_t main = nullptr;
+        ~TreeStream() { if (main) c->st = main; }
+    } ts{ctx};
+    if (ctx->st_tree && p->aggregator != SM_AGG_GUIDED) {
+        HIPC(hipEventRecord(ctx->ev_enq, ctx->st));
+        HIPC(hipStreamWaitEvent(ctx->st_tree, ctx->ev_enq, 0));
+        ts.main = ctx->st;
+        ctx->st = ctx->st_tree;
+    }
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
     HIPC(hipEventRecord(ctx->ev[1], ctx->st));
@@ -1288,6 +1326,11 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
     CHECK(stage_tree(ctx, ctx->views, p));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
     CHECK(stage_layout_enqueue(ctx, ctx->views));
+    if (ts.main) {
+        ctx->st = ts.main;
+        ts.main = nullptr;
+        HIPC(hipStreamWaitEvent(ctx->st, ctx->ev_layout, 0));
+    }
     ctx->pending = 1;
     ctx->pend_D = D;
     ctx->pend_p = *p;
