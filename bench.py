@@ -99,6 +99,30 @@ def cpu_baseline(W, H, D, slices, slices_1t):
                                                                   frame1 * 1e3))
 
 
+def stream_frames(ctxs, steps, D, params, retire, split=True):
+    """Stream `steps` frames over the contexts, frame i on context i mod len(ctxs), keeping up to
+    len(ctxs) in flight; retire(c) waits for context c's frame.  split: frame i's tree is enqueued
+    (match_begin) before the host waits for frame i-1's layout and enqueues its filter
+    (match_finish), so the GPU never idles on the host; otherwise one match_async per frame."""
+    n = len(ctxs)
+    if n == 1 or not split:
+        for i in range(steps):
+            ctxs[i % n].match_async(D, params)  # returns once the frame's filter is enqueued
+            if i >= n - 1:
+                retire(ctxs[(i - n + 1) % n])
+    else:
+        for i in range(steps):
+            ctxs[i % n].match_begin(D, params)
+            if i >= 1:
+                ctxs[(i - 1) % n].match_finish()
+            if i >= n - 1:
+                retire(ctxs[(i - n + 1) % n])
+        if steps > 0:
+            ctxs[(steps - 1) % n].match_finish()
+    for i in range(max(0, steps - n + 1), steps):
+        retire(ctxs[i % n])
+
+
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -262,24 +286,7 @@ def main():
         accumulate(kacc, c)
 
     t0 = time.perf_counter()
-    if inflight == 1 or args.no_split:
-        for i in range(args.steps):
-            ctxs[i % inflight].match_async(Dloc, params)  # returns once the frame's filter is enqueued
-            if i >= inflight - 1:
-                retire(ctxs[(i - inflight + 1) % inflight])
-    else:
-        # split calls: frame i's tree is enqueued (match_begin) before the host waits for frame
-        # i-1's layout and enqueues its filter (match_finish), so the GPU never idles on the host
-        for i in range(args.steps):
-            ctxs[i % inflight].match_begin(Dloc, params)
-            if i >= 1:
-                ctxs[(i - 1) % inflight].match_finish()
-            if i >= inflight - 1:
-                retire(ctxs[(i - inflight + 1) % inflight])
-        if args.steps > 0:
-            ctxs[(args.steps - 1) % inflight].match_finish()
-    for i in range(max(0, args.steps - inflight + 1), args.steps):
-        retire(ctxs[i % inflight])
+    stream_frames(ctxs, args.steps, Dloc, params, retire, split=not args.no_split)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
