@@ -372,7 +372,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded slanted-plane stereo pair, tools/synth.py)",
-        "config": {"workload": "%dx%d D=%d both views%s" % (W, H, Dtot_frame, CONFIG_NAMES.get((W, H, Dtot_frame), ""))
+        "config": {"workload": "%dx%d D=%d both views%s%s" % (
+                       W, H, Dtot_frame, CONFIG_NAMES.get((W, H, Dtot_frame), ""),
+                       " = BASELINE C5's per-GPU pair" if args.mode == "batch" and (W, H, Dtot_frame) == (3840, 2160, 256) else "")
                    if world == 1 else
                    "%dx%d D=%d, %s mode, %d disparities/rank%s%s" % (
                        W, H, Dtot_frame, args.mode, Dloc, " of one view (view groups)" if views != 3 else "",
