@@ -370,8 +370,9 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const int x = pix_col((int)hfield<CH>(mv, hl, j, 0), W);
+        // own(x) of node j at lane 32h + j, own(x+1) (only its gray) at lane 32h + 16 + j
         const uint32_t ox0 = hfield<CH>(ownr.x, hl, 0, j), oy0 = hfield<CH>(ownr.y, hl, 0, j);
-        const uint32_t ox1 = hfield<CH>(ownr.x, hl, 2, j), oy1 = hfield<CH>(ownr.y, hl, 2, j);  // lanes 32h + 16 + j
+        const uint32_t oy1 = hfield<CH>(ownr.y, hl, 2, j);
         const float go0 = __uint_as_float(oy0), go1 = __uint_as_float(oy1);
         float g[3];
 #pragma unroll
@@ -390,7 +391,6 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
             }
             c[j][k] = ok ? v : 3.0f;
         }
-        (void)ox1;
     }
     // edge factors of the first two children up front (per lane: LDS reads); a third or fourth
     // child (rare) reads its factor where the recurrence uses it
