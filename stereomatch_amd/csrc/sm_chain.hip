@@ -270,6 +270,12 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 #ifndef UP_NS4
 #define UP_NS4 8
 #endif
+#ifndef UP_G1
+#define UP_G1 6  // SPL = 1 (one-view 64-slice shares, D <= 64)
+#endif
+#ifndef UP_NS1
+#define UP_NS1 10
+#endif
 #ifndef UP_G2
 #define UP_G2 4  // even: the chain's two-half pipeline
 #endif
@@ -278,8 +284,8 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 #endif
 template <int SPL>
 struct UpCfg {
-    static constexpr int G = SPL == 1 ? 6 : SPL == 2 ? UP_G2 : UP_G4;  // nodes per group (helper registers)
-    static constexpr int NS = SPL == 1 ? 10 : SPL == 2 ? UP_NS2 : UP_NS4;  // LDS slots (~140 KB)
+    static constexpr int G = SPL == 1 ? UP_G1 : SPL == 2 ? UP_G2 : UP_G4;  // nodes per group (helper registers)
+    static constexpr int NS = SPL == 1 ? UP_NS1 : SPL == 2 ? UP_NS2 : UP_NS4;  // LDS slots (~140 KB)
 };
 
 struct UpNodeS {
@@ -1461,6 +1467,12 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
 // ---------------------------------------------------------------------------------------------
 // k_down_chain.  Chain node j = slot head + j (root side first).
 // ---------------------------------------------------------------------------------------------
+#ifndef DN_G1
+#define DN_G1 8  // SPL = 1
+#endif
+#ifndef DN_NS1
+#define DN_NS1 10
+#endif
 #ifndef DN_G2
 #define DN_G2 6
 #endif
@@ -1475,8 +1487,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
 #endif
 template <int SPL>
 struct DownCfg {
-    static constexpr int G = SPL == 4 ? DN_G4 : SPL == 2 ? DN_G2 : 8;  // helper registers: next group's rows + WTA rows
-    static constexpr int NS = SPL == 4 ? DN_NS4 : SPL == 2 ? DN_NS2 : 10;
+    static constexpr int G = SPL == 4 ? DN_G4 : SPL == 2 ? DN_G2 : DN_G1;  // helper registers: next group's rows + WTA rows
+    static constexpr int NS = SPL == 4 ? DN_NS4 : SPL == 2 ? DN_NS2 : DN_NS1;
 };
 
 template <int SPL>
