@@ -271,10 +271,10 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 #define UP_NS4 8
 #endif
 #ifndef UP_G1
-#define UP_G1 6  // SPL = 1 (one-view 64-slice shares, D <= 64)
+#define UP_G1 4  // SPL = 1 (one-view 64-slice shares, D <= 64); 6 x 10 -> 4 x 18: k_up_chain 0.529 -> 0.504 ms at the N = 8 share
 #endif
 #ifndef UP_NS1
-#define UP_NS1 10
+#define UP_NS1 18
 #endif
 #ifndef UP_G2
 #define UP_G2 4  // even: the chain's two-half pipeline
