@@ -19,6 +19,7 @@
  *   WTA inside sm_match <- MSTCostAggregationAndLabelUpdate :160-186 / selectDisparity
  *                                                                 src/PatchMatchStereoGPU.cu:1688-1737
  *   sm_start_timer/sm_get_timer_ms <- startTimer/getTimer         src/Stereo3DMST.cpp:15-26
+ *   SM_AGG_PMS, sm_download_labels <- MST_PMS label search + abc_map  src/Stereo3DMST.cpp:546-629, 851-889
  *
  * Threading: one sm_ctx per host thread; no global mutable state in the library.
  * All calls are synchronous w.r.t. the host unless named *_async.
@@ -52,10 +53,18 @@ typedef enum {
 /* Cost aggregator of a call (sm_params.aggregator). */
 typedef enum {
     SM_AGG_TREE = 0,   /* the MST / segment-forest tree filter (Stereo3DMST.cpp:120-186)          */
-    SM_AGG_GUIDED = 1  /* the colour guided filter of the cost volume, each view guided by its own
+    SM_AGG_GUIDED = 1, /* the colour guided filter of the cost volume, each view guided by its own
                           image, then selectDisparity (PatchMatchStereoGPU.cu:8251-8470, 1688-1737);
                           float arithmetic; radius gf_radius, eps gf_eps (the reference: 9 and
                           0.01^2*255^2, :9000-9001); AGD cost only */
+    SM_AGG_PMS = 2     /* Stereo3DMST's own label search: the segment forest (c, min_size; c = +INFINITY
+                          gives the MST), random slanted-plane labels (Stereo3DMST.cpp:390-430), then
+                          pms_iters MST_PMS calls per view (:546-629, :851-889) -- neighbour-tree
+                          propagation and random refinement, each label aggregated over its tree with
+                          the lerp data term (:103-118) and taken per pixel with strict <.  The float
+                          disparity is the plane's, fma(x, a, y*b) + c (LabelToDisp before its clamp,
+                          :197; SM_POST_LABEL_TO_DISP applies the clamp and scaling); min = each pixel's
+                          aggregated cost; idx = -1.  Both views, unsharded (disp_begin 0), D = Dmax */
 } sm_aggregator;
 
 typedef struct {
@@ -83,6 +92,7 @@ typedef struct {
                           A one-view call builds that view's tree only, filters it and (with a
                           communicator) reduces it across the ranks of its group; the other view's
                           outputs are left untouched.  Multi-GPU partitioning: see DESIGN.md 7 */
+    int pms_iters;     /* SM_AGG_PMS: MST_PMS calls per view (default 100, Stereo3DMST.cpp:854)    */
 } sm_params;
 
 /* Post-processing of the final (cross-rank reduced) float disparity maps (idx / min untouched),
@@ -219,6 +229,27 @@ int sm_get_kernel_stats(sm_ctx* ctx, sm_kernel_stat* out, int n);
  * GPU time per launch at C2); untimed families launch back to back.  No reference
  * counterpart: measurement plumbing of this library. */
 sm_status sm_set_kernel_timing(sm_ctx* ctx, unsigned family_mask);
+
+/* MST_PMS (SM_AGG_PMS) ----------------------------------------------------------
+ * The plane labels (a, b, c) of every pixel after the last SM_AGG_PMS call, [H*W][3] float per view
+ * (abc_map, Stereo3DMST.cpp:814-815); either pointer may be NULL. */
+sm_status sm_download_labels(sm_ctx* ctx, float* left_abc, float* right_abc);
+/* Timings and counters of the last SM_AGG_PMS call.  The first MST_PMS call of a view runs its trees
+ * one after the other (serial); later calls run every tree at once from guessed dice offsets and the
+ * labels at the start of the call, validate, and redo from the first tree whose inputs differed
+ * (spec_rounds counts those passes; serial_trees the trees run one by one). */
+typedef struct {
+    int iters;              /* MST_PMS calls per view */
+    int ntrees[2];          /* trees per view */
+    int spec_rounds;        /* speculative passes, both views */
+    int serial_trees;       /* trees run in serial mode, both views */
+    double prep_ms;         /* host: segmentation, forests, schedules, tables (wall) */
+    double setup_ms;        /* device: uploads, cost rows, labels (wall) */
+    double iter0_ms;        /* the first call of both views (wall) */
+    double iters_ms;        /* the remaining calls of both views (wall) */
+    double total_ms;        /* the whole SM_AGG_PMS call (wall) */
+} sm_pms_stats;
+sm_status sm_get_pms_stats(sm_ctx* ctx, sm_pms_stats* out);
 
 /* Multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------- */
 #define SM_UNIQUE_ID_BYTES 128

@@ -52,6 +52,18 @@ def lib():
         L.orc_box_mean.argtypes = [vp, vp, c_int, c_int, c_int]
         L.orc_select_disparity.argtypes = [vp, c_int, c_int, c_int, ctypes.c_size_t, c_int, vp, vp, vp]
         L.orc_occlusion.argtypes = [vp, vp, c_int, c_int, c_int, c_float, c_int]
+        L.orc_pms_dice.argtypes = [ctypes.c_long, f32p]
+        L.orc_glibc_random.argtypes = [ctypes.c_uint, ctypes.c_long, ctypes.c_long, i32p]
+        L.orc_pms_init_labels.argtypes = [c_int, c_int, c_int, f32p]
+        L.orc_label_cost.argtypes = [f32p, c_float, c_float, c_float, c_int, c_int, c_int, ctypes.c_size_t]
+        L.orc_label_cost.restype = c_float
+        L.orc_pms_label_to_disp.argtypes = [f32p, c_int, c_int, c_int, f32p]
+        L.orc_pms_plane_disp.argtypes = [f32p, c_int, c_int, f32p]
+        L.orc_tree_graph.argtypes = [c_int, c_int, c_int, i32p, i32p, i32p, i32p, c_int]
+        L.orc_tree_graph.restype = c_int
+        L.orc_mst_pms.argtypes = [c_int, c_int, c_int, c_int, i32p, i32p, i32p, u16p, u8p, i32p, i32p, i32p, f32p,
+                                  f32p, f64p, f32p, ctypes.c_long, i32p, vp]
+        L.orc_mst_pms.restype = ctypes.c_long
         _LIB = L
     return _LIB
 
@@ -300,3 +312,113 @@ def occlusion(left_disp, right_disp, min_disp=0, thresh=1.0, remove=False):
     H, W = L.shape
     lib().orc_occlusion(_ptr(L), _ptr(R), W, H, int(min_disp), float(thresh), 1 if remove else 0)
     return L, R
+
+
+# ---------------------------------------------------------------- MST_PMS (Stereo3DMST.cpp:546-629)
+def pms_dice(n):
+    """The (-1, 1) dice stream every MST_PMS call replays (minstd_rand0 seed 1, :554 / :851-852)."""
+    out = np.empty(int(n), np.float32)
+    lib().orc_pms_dice(int(n), out)
+    return out
+
+
+def glibc_random(seed, skip, n):
+    """glibc random()/rand() outputs skip..skip+n-1 after srandom(seed) (TYPE_3)."""
+    out = np.empty(int(n), np.int32)
+    lib().orc_glibc_random(int(seed), int(skip), int(n), out)
+    return out
+
+
+def pms_init_labels(W, H, max_disp):
+    """segment_image_other_init's random plane labels (:390-430): [H*W, 3] float (a, b, c)."""
+    abc = np.empty((H * W, 3), np.float32)
+    lib().orc_pms_init_labels(W, H, int(max_disp), abc)
+    return abc
+
+
+def pms_levels(max_disp):
+    """Refinement levels per tree (:597-600): max_d = 0.5*Dmax halved while > 0.1f."""
+    md, n = np.float32(0.5) * np.float32(max_disp), 0
+    while md > np.float32(0.1):
+        n += 1
+        md = np.float32(md * np.float32(0.5))
+    return n
+
+
+def tree_graph(W, H, tree):
+    """tree_g (:377-384) as CSR (nb_start, nb), neighbours ascending."""
+    nt = tree["ntrees"]
+    nb_start = np.empty(nt + 1, np.int32)
+    cap = 4 * W * H + 4
+    nb = np.empty(cap, np.int32)
+    n = lib().orc_tree_graph(W, H, nt, tree["tree_start"], tree["node_pix"], nb_start, nb, cap)
+    if n < 0:
+        raise RuntimeError("tree_graph: capacity")
+    return nb_start, nb[:n].copy()
+
+
+def dice_budget(tree, nb_start, max_disp):
+    """Upper bound of the dice values one MST_PMS call consumes: deg(t) + 4 per refinement level."""
+    return int(nb_start[-1]) + 4 * pms_levels(max_disp) * int(tree["ntrees"]) + 4
+
+
+def mst_pms(W, H, max_disp, tree, nb_start, nb, vol, abc, min_cost, dice, rnd, stats=False):
+    """One MST_PMS call over one view, in place on abc [N,3] f32 and min_cost [N] f64.  Returns the dice
+    values consumed (and per-tree stats {dice, prop changes, refinement changes, test pixel})."""
+    st = np.empty((tree["ntrees"], 4), np.int32) if stats else None
+    k = lib().orc_mst_pms(W, H, int(max_disp), tree["ntrees"], tree["tree_start"], tree["node_pix"],
+                          tree["node_parent"], tree["node_w"], tree["node_nch"], tree["node_child"], nb_start, nb,
+                          np.ascontiguousarray(vol, dtype=np.float32), abc, min_cost, dice, dice.size,
+                          np.ascontiguousarray(rnd, dtype=np.int32), _ptr(st))
+    if k < 0:
+        raise RuntimeError("mst_pms: dice stream exhausted or a propagation index out of its tree")
+    return (k, st) if stats else k
+
+
+def pms_label_to_disp(abc, W, H, max_disp):
+    """LabelToDisp (:189-201) + *= (Dmax-1.f) (:900-902) of plane labels: [H, W] float."""
+    out = np.empty(W * H, np.float32)
+    lib().orc_pms_label_to_disp(np.ascontiguousarray(abc, dtype=np.float32), W, H, int(max_disp), out)
+    return out.reshape(H, W)
+
+
+def pms_plane_disp(abc, W, H):
+    """fma(x, a, y*b) + c per pixel (LabelToDisp's plane value before its clamp, :197): [H, W] float."""
+    out = np.empty(W * H, np.float32)
+    lib().orc_pms_plane_disp(np.ascontiguousarray(abc, dtype=np.float32), W, H, out)
+    return out.reshape(H, W)
+
+
+def stereo3dmst_pms(left, right, max_disp, iters=100, vols=None, c=5000.0, min_size=200, stats=False):
+    """The reference's stereo3dmst() after the cost volume (Stereo3DMST.cpp:805-904): segment forests
+    of both views, random plane init, `iters` MST_PMS calls on the left view then on the right, plane
+    LabelToDisp + scaling, L-R check of the left map (no fill).  vols: (left, right) [Dmax][H][W] data
+    costs (default: the AGD volumes).  glibc's rand() stream starts after random_rgb's 3 draws per pixel
+    of both views (:316)."""
+    H, W, _ = left.shape
+    if vols is None:
+        vols = cost_agd(left, right, 0, max_disp)
+    out = {}
+    trees = [build_tree(img, c, min_size) for img in (left, right)]
+    nbs = [tree_graph(W, H, t) for t in trees]
+    K = [t["ntrees"] for t in trees]
+    rnd = glibc_random(1, 6 * W * H, iters * (K[0] + K[1]))
+    dice = pms_dice(max(dice_budget(t, nb[0], max_disp) for t, nb in zip(trees, nbs)))
+    abc0 = pms_init_labels(W, H, max_disp)
+    off = 0
+    for v, name in enumerate(("left", "right")):
+        abc = abc0.copy()
+        minc = np.full(W * H, np.finfo(np.float64).max)
+        st_all = []
+        for _ in range(iters):
+            r = mst_pms(W, H, max_disp, trees[v], nbs[v][0], nbs[v][1], vols[v], abc, minc, dice,
+                        rnd[off:off + K[v]], stats)
+            if stats:
+                st_all.append(r[1])
+            off += K[v]
+        out[name] = dict(abc=abc, minc=minc, tree=trees[v], nb=nbs[v], disp=pms_label_to_disp(abc, W, H, max_disp))
+        if stats:
+            out[name]["stats"] = st_all
+    out["left"]["disp_checked"] = lr_check(out["left"]["disp"], out["right"]["disp"], max_disp, False)
+    out["abc0"] = abc0
+    return out

@@ -94,6 +94,22 @@ void orc_select_disparity(const float* vol, int nd, int d0, int dtot, size_t N, 
                           float* disp);
 void orc_occlusion(float* left, float* right, int W, int H, int min_disp, float thresh, int remove);
 
+/* ---- MST_PMS, the slanted-plane label search (Stereo3DMST.cpp:546-629; sm_oracle_pms.c) ---- */
+uint32_t orc_minstd0_next(uint32_t s);        /* minstd_rand0 step */
+float orc_canon_f(uint32_t u);                /* generate_canonical<float,24> of the shipped libstdc++ */
+void orc_pms_dice(long n, float* out);        /* the (-1,1) dice stream every MST_PMS call replays */
+void orc_glibc_random(unsigned seed, long skip, long n, int32_t* out); /* glibc random()/rand() */
+void orc_pms_init_labels(int W, int H, int max_disp, float* abc);     /* :390-430, abc[3N] */
+float orc_label_cost(const float* vol, float a, float b, float c, int pix, int max_disp, int W, size_t N); /* :103-118 */
+void orc_pms_label_to_disp(const float* abc, int W, int H, int max_disp, float* disp); /* :189-201 + :900-902 */
+void orc_pms_plane_disp(const float* abc, int W, int H, float* disp); /* fma(x, a, y*b) + c, unclamped */
+int orc_tree_graph(int W, int H, int ntrees, const int32_t* tree_start, const int32_t* node_pix, int32_t* nb_start,
+                   int32_t* nb, int nb_cap);  /* tree_g (:377-384) as CSR, ascending */
+long orc_mst_pms(int W, int H, int max_disp, int ntrees, const int32_t* tree_start, const int32_t* node_pix,
+                 const int32_t* node_parent, const uint16_t* node_w, const uint8_t* node_nch, const int32_t* node_child,
+                 const int32_t* nb_start, const int32_t* nb, const float* vol, float* abc, double* min_cost,
+                 const float* dice, long dice_n, const int32_t* rnd, int32_t* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,7 +14,7 @@ import os
 
 import numpy as np
 
-from ._lib import (SM_AGG_GUIDED, SM_AGG_TREE, SM_COST_AGD, SM_COST_VOLUME, SM_POST_LABEL_TO_DISP, SM_POST_LR_CHECK, SM_POST_LR_FILL,  # noqa: F401
+from ._lib import (SM_AGG_GUIDED, SM_AGG_PMS, SM_AGG_TREE, SM_COST_AGD, SM_COST_VOLUME, SM_POST_LABEL_TO_DISP, SM_POST_LR_CHECK, SM_POST_LR_FILL,  # noqa: F401
                    SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO, SM_POST_SUBPIXEL, Context, StereoMSTError, default_params, device_count, lib)
 
 # stereo3dmst's output step: LabelToDisp + *= (Dmax-1) on both maps, then the fill-less L-R check of

@@ -18,7 +18,7 @@ STATUS_NAMES = {0: "SM_OK", 1: "SM_ERR_ARG", 2: "SM_ERR_HIP", 3: "SM_ERR_OOM", 4
 SM_COST_AGD, SM_COST_VOLUME = 0, 1
 SM_POST_LR_CHECK, SM_POST_LABEL_TO_DISP, SM_POST_LR_FILL, SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO = 1, 2, 4, 8, 16
 SM_POST_SUBPIXEL = 32
-SM_AGG_TREE, SM_AGG_GUIDED = 0, 1
+SM_AGG_TREE, SM_AGG_GUIDED, SM_AGG_PMS = 0, 1, 2
 SM_UNIQUE_ID_BYTES = 128
 
 
@@ -31,7 +31,14 @@ class SmParams(ctypes.Structure):
     _fields_ = [("gamma", ctypes.c_float), ("c", ctypes.c_float), ("min_size", ctypes.c_int),
                 ("median_ksize", ctypes.c_int), ("cost_kind", ctypes.c_int), ("disp_begin", ctypes.c_int),
                 ("disp_total", ctypes.c_int), ("post", ctypes.c_int), ("aggregator", ctypes.c_int),
-                ("gf_radius", ctypes.c_int), ("gf_eps", ctypes.c_float), ("views", ctypes.c_int)]
+                ("gf_radius", ctypes.c_int), ("gf_eps", ctypes.c_float), ("views", ctypes.c_int),
+                ("pms_iters", ctypes.c_int)]
+
+
+class SmPmsStats(ctypes.Structure):
+    _fields_ = [("iters", ctypes.c_int), ("ntrees", ctypes.c_int * 2), ("spec_rounds", ctypes.c_int),
+                ("serial_trees", ctypes.c_int), ("prep_ms", ctypes.c_double), ("setup_ms", ctypes.c_double),
+                ("iter0_ms", ctypes.c_double), ("iters_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
 
 
 class SmFilterStats(ctypes.Structure):
@@ -88,6 +95,14 @@ def lib():
         "sm_get_filter_stats": ([vp, ctypes.POINTER(SmFilterStats)], ci),
         "sm_get_kernel_stats": ([vp, ctypes.POINTER(SmKernelStat), ci], ci),
         "sm_set_kernel_timing": ([vp, ctypes.c_uint], ci),
+        "sm_download_labels": ([vp, vp, vp], ci),
+        "sm_get_pms_stats": ([vp, ctypes.POINTER(SmPmsStats)], ci),
+        "sm_pms_forest_bfs": ([ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp], ci),
+        "sm_pms_tree_graph": ([ci, ci, vp, vp, vp, vp, vp, ci], ci),
+        "sm_pms_dice": ([ctypes.c_long, vp], None),
+        "sm_pms_glibc_random": ([ctypes.c_uint, ctypes.c_long, ctypes.c_long, vp], None),
+        "sm_pms_init_labels": ([ci, ci, ci, vp], None),
+        "sm_pms_levels": ([ci], ci),
         "sm_comm_unique_id": ([vp], ci),
         "sm_comm_init": ([vp, ci, ci, vp], ci),
         "sm_comm_destroy": ([vp], ci),
@@ -170,6 +185,7 @@ class Context:
         out = {v: dict(disp=np.empty((H, W), np.float32), idx=np.empty((H, W), np.int32),
                        minc=np.empty((H, W), np.float64)) for v in ("left", "right")}
         self._views = p.views or 3
+        self.shape = (H, W)
         self._check(lib().sm_match(self.h, ptr(left), ptr(right), W, H, W * 3, D, ctypes.byref(p),
                                    ptr(out["left"]["disp"]), ptr(out["right"]["disp"]), ptr(out["left"]["idx"]),
                                    ptr(out["right"]["idx"]), ptr(out["left"]["minc"]), ptr(out["right"]["minc"])))
@@ -246,6 +262,21 @@ class Context:
                 mask |= 1 << names.index(f)
         self._check(lib().sm_set_kernel_timing(self.h, ctypes.c_uint(mask)))
 
+    # -- MST_PMS (SM_AGG_PMS) -------------------------------------------------------------
+    def labels(self):
+        """Plane labels (a, b, c) of every pixel after the last SM_AGG_PMS call: {view: [H*W, 3] float32}."""
+        H, W = self.shape
+        out = {v: np.empty((H * W, 3), np.float32) for v in ("left", "right")}
+        self._check(lib().sm_download_labels(self.h, ptr(out["left"]), ptr(out["right"])))
+        return out
+
+    def pms_stats(self):
+        s = SmPmsStats()
+        self._check(lib().sm_get_pms_stats(self.h, ctypes.byref(s)))
+        d = {k: getattr(s, k) for k, _ in SmPmsStats._fields_}
+        d["ntrees"] = list(s.ntrees)
+        return d
+
     # -- stages ---------------------------------------------------------------------------
     def cost_volume(self, left, right, d0, D):
         left, right = as_image(left), as_image(right)
@@ -300,3 +331,47 @@ class Context:
 
     def comm_destroy(self):
         self._check(lib().sm_comm_destroy(self.h))
+
+
+# -- host-side MST_PMS helpers of the library (CPU; tests compare them with the oracle) -----------------
+def pms_forest_bfs(W, H, wR, wD, mask):
+    N = W * H
+    ts = np.empty(N + 1, np.int32); pix = np.empty(N, np.int32); par = np.empty(N, np.int32)
+    w = np.empty(N, np.uint16); nch = np.empty(N, np.uint8); ch = np.empty(4 * N, np.int32)
+    k = lib().sm_pms_forest_bfs(W, H, ptr(np.ascontiguousarray(wR, np.uint16)), ptr(np.ascontiguousarray(wD, np.uint16)),
+                                ptr(np.ascontiguousarray(mask, np.uint8)), ptr(ts), ptr(pix), ptr(par), ptr(w), ptr(nch),
+                                ptr(ch))
+    return dict(ntrees=k, tree_start=ts[:k + 1].copy(), node_pix=pix, node_parent=par, node_w=w, node_nch=nch,
+                node_child=ch)
+
+
+def pms_tree_graph(W, H, wR, wD, mask):
+    N = W * H
+    s = np.empty(N + 1, np.int32); nb = np.empty(4 * N + 4, np.int32)
+    n = lib().sm_pms_tree_graph(W, H, ptr(np.ascontiguousarray(mask, np.uint8)), ptr(np.ascontiguousarray(wR, np.uint16)),
+                                ptr(np.ascontiguousarray(wD, np.uint16)), ptr(s), ptr(nb), nb.size)
+    if n < 0:
+        raise RuntimeError("sm_pms_tree_graph: capacity")
+    return s, nb[:n].copy()
+
+
+def pms_dice(n):
+    out = np.empty(int(n), np.float32)
+    lib().sm_pms_dice(int(n), ptr(out))
+    return out
+
+
+def pms_glibc_random(seed, skip, n):
+    out = np.empty(int(n), np.int32)
+    lib().sm_pms_glibc_random(int(seed), int(skip), int(n), ptr(out))
+    return out
+
+
+def pms_init_labels(W, H, max_disp):
+    out = np.empty((W * H, 3), np.float32)
+    lib().sm_pms_init_labels(W, H, int(max_disp), ptr(out))
+    return out
+
+
+def pms_levels(max_disp):
+    return lib().sm_pms_levels(int(max_disp))

@@ -9,6 +9,8 @@
 #include <rccl/rccl.h>
 #include <sys/time.h>
 
+#include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -20,6 +22,7 @@
 #include "sm_common.h"
 #include "sm_launch.h"
 #include "sm_layout_gpu.h"
+#include "sm_pms.h"
 #include "sm_segment.h"
 #include "sm_tables.inc"
 
@@ -39,6 +42,18 @@ constexpr size_t RREC_FWD = (SM_NBUCKETS + 1) + SM_NBUCKETS + SM_NBUCKETS + 2 + 
 struct DevBuf {
     void* p = nullptr;
     size_t n = 0;
+};
+
+// MST_PMS state of one view (SM_AGG_PMS, sm_pms.hip): the host forest and schedule, their device
+// copies, labels, aggregation rows, cost rows and the speculation scratch
+struct PmsState {
+    PmsForest f;
+    DevBuf rows, rtree, paths, items, rt_path, rt_item, tree_rounds, tree_start, bfs_pix, nb_start, nb, tree_pt, tree_abase,
+        tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result;
+    std::vector<int32_t> h_rtree, h_pt, h_lab;
+    std::vector<long long> h_abase;
+    long long dice_need = 0;
+    PmsDev dev{};
 };
 
 struct MstPending {
@@ -132,6 +147,17 @@ struct sm_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     bool reduced = false;
+    // MST_PMS (SM_AGG_PMS)
+    PmsState pms[2];
+    DevBuf pms_dice, pms_rnd;
+    long long pms_dice_n = 0;  // dice values on the device (the stream prefix every call replays)
+    std::vector<float> pms_init;   // random plane labels of (W, H, Dmax) (both views start from them)
+    int pms_init_key[3] = {0, 0, 0};
+    std::vector<double> pms_dblmax;
+    std::vector<int32_t> pms_hrnd;
+    int32_t* h_pms_res = nullptr;  // pinned: the validation result
+    bool pms_last = false;         // the last call was SM_AGG_PMS (labels available)
+    sm_pms_stats pms_stats{};
 };
 
 namespace {
@@ -209,7 +235,17 @@ sm_status check_params(sm_ctx* ctx, const sm_params* p, int D) {
         return fail(ctx, SM_ERR_ARG, "SM_POST_LR_FILL needs SM_POST_LR_CHECK");
     if ((p->post & SM_POST_OCCLUSION) && (p->post & SM_POST_OCCLUSION_ZERO))
         return fail(ctx, SM_ERR_ARG, "SM_POST_OCCLUSION and SM_POST_OCCLUSION_ZERO are exclusive");
-    if (p->aggregator != SM_AGG_TREE && p->aggregator != SM_AGG_GUIDED) return fail(ctx, SM_ERR_ARG, "unknown aggregator");
+    if (p->aggregator != SM_AGG_TREE && p->aggregator != SM_AGG_GUIDED && p->aggregator != SM_AGG_PMS)
+        return fail(ctx, SM_ERR_ARG, "unknown aggregator");
+    if (p->aggregator == SM_AGG_PMS) {
+        if (p->disp_begin != 0 || (p->disp_total != 0 && p->disp_total != D))
+            return fail(ctx, SM_ERR_ARG, "SM_AGG_PMS: unsharded only (disp_begin 0, D = Dmax)");
+        if (p->views != 0 && p->views != 3) return fail(ctx, SM_ERR_ARG, "SM_AGG_PMS computes both views");
+        if (D < 2) return fail(ctx, SM_ERR_ARG, "SM_AGG_PMS needs Dmax >= 2");
+        if (p->pms_iters < 0 || p->pms_iters > 100000) return fail(ctx, SM_ERR_ARG, "SM_AGG_PMS: pms_iters out of range");
+        if (p->post & SM_POST_SUBPIXEL) return fail(ctx, SM_ERR_ARG, "SM_AGG_PMS: no subpixel step (labels are planes)");
+        return SM_OK;
+    }
     if (p->views < 0 || p->views > 3) return fail(ctx, SM_ERR_ARG, "views must be 1 (left), 2 (right) or 3 / 0 (both)");
     if (p->views == 1 || p->views == 2) {
         if (p->aggregator != SM_AGG_TREE) return fail(ctx, SM_ERR_ARG, "a one-view call needs SM_AGG_TREE");
@@ -1086,6 +1122,299 @@ sm_status stage_post(sm_ctx* ctx, int post, int dmax) {
     return SM_OK;
 }
 
+// ----------------------------------------------------------------------------- MST_PMS (SM_AGG_PMS)
+double now_ms();
+
+template <class T>
+sm_status upload_vec(sm_ctx* ctx, DevBuf& b, const std::vector<T>& v) {
+    CHECK(ensure(ctx, b, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!v.empty()) HIPC(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->st));
+    return SM_OK;
+}
+
+// SM_PMS_SERIAL=1: every MST_PMS call in serial mode (tests compare the two modes); SM_PMS_MAX_ROUNDS:
+// speculative passes per call before the rest of the call runs serially
+bool pms_serial_only() {
+    const char* e = getenv("SM_PMS_SERIAL");
+    return e && atoi(e) == 1;
+}
+int pms_max_rounds() {
+    const char* e = getenv("SM_PMS_MAX_ROUNDS");
+    return e ? std::max(1, atoi(e)) : 8;
+}
+
+// The forest, schedule and per-tree tables of view v on the device (host forest built already).
+sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
+    PmsState& S = ctx->pms[v];
+    const PmsForest& f = S.f;
+    const int K = f.K;
+    const size_t N = (size_t)f.W * f.H;
+    S.h_rtree.resize(N);
+    S.h_pt.resize(K);
+    S.h_lab.resize(K + 1);
+    S.h_abase.resize(K + 1);
+    long long abase = 0, deg_sum = 0;
+    int lab = 0;
+    for (int t = 0; t < K; ++t) {
+        const int deg = f.nb_start[t + 1] - f.nb_start[t];
+        const int pt = (std::max(deg, L) + 1) & ~1;  // proposals per A row (16-byte rows)
+        S.h_pt[t] = pt;
+        S.h_abase[t] = abase;
+        S.h_lab[t] = lab;
+        abase += (long long)(f.tree_start[t + 1] - f.tree_start[t]) * pt;
+        lab += deg + L;
+        deg_sum += deg;
+        for (int r = f.tree_start[t]; r < f.tree_start[t + 1]; ++r) S.h_rtree[r] = t;
+    }
+    S.h_abase[K] = abase;
+    S.h_lab[K] = lab;
+    S.dice_need = deg_sum + 4ll * L * K + 8;
+    CHECK(upload_vec(ctx, S.rows, f.rows));
+    CHECK(upload_vec(ctx, S.rtree, S.h_rtree));
+    CHECK(upload_vec(ctx, S.paths, f.paths));
+    CHECK(upload_vec(ctx, S.items, f.items));
+    CHECK(upload_vec(ctx, S.rt_path, f.rt_path));
+    CHECK(upload_vec(ctx, S.rt_item, f.rt_item));
+    CHECK(upload_vec(ctx, S.tree_rounds, f.tree_rounds));
+    CHECK(upload_vec(ctx, S.tree_start, f.tree_start));
+    CHECK(upload_vec(ctx, S.bfs_pix, f.bfs_pix));
+    CHECK(upload_vec(ctx, S.nb_start, f.nb_start));
+    CHECK(upload_vec(ctx, S.nb, f.nb));
+    CHECK(upload_vec(ctx, S.tree_pt, S.h_pt));
+    CHECK(upload_vec(ctx, S.tree_abase, S.h_abase));
+    CHECK(upload_vec(ctx, S.tree_lab, S.h_lab));
+    CHECK(ensure(ctx, S.nref, (size_t)std::max(K, 1) * 4));
+    CHECK(ensure(ctx, S.lab, (size_t)std::max(lab, 1) * 16));
+    CHECK(ensure(ctx, S.labq, (size_t)std::max(lab, 1) * 4));
+    CHECK(ensure(ctx, S.abc, N * 12));
+    CHECK(ensure(ctx, S.minc, N * 8));
+    CHECK(ensure(ctx, S.abc_bak, N * 12));
+    CHECK(ensure(ctx, S.minc_bak, N * 8));
+    CHECK(ensure(ctx, S.A, (size_t)std::max(abase, 1ll) * 8));
+    CHECK(ensure(ctx, S.off, 16));
+    CHECK(ensure(ctx, S.oguess, (size_t)std::max(K, 1) * 8));
+    CHECK(ensure(ctx, S.cnt, (size_t)std::max(K, 1) * 4));
+    CHECK(ensure(ctx, S.flag, (size_t)std::max(K, 1) * 4));
+    CHECK(ensure(ctx, S.result, 16));
+    return SM_OK;
+}
+
+PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
+    PmsState& S = ctx->pms[v];
+    PmsDev d{};
+    d.rows = P<PmsRow>(S.rows);
+    d.rtree = P<int32_t>(S.rtree);
+    d.paths = P<PmsPath>(S.paths);
+    d.items = P<PmsItem>(S.items);
+    d.rt_path = P<int32_t>(S.rt_path);
+    d.rt_item = P<int32_t>(S.rt_item);
+    d.tree_rounds = P<int32_t>(S.tree_rounds);
+    d.tree_start = P<int32_t>(S.tree_start);
+    d.bfs_pix = P<int32_t>(S.bfs_pix);
+    d.nb_start = P<int32_t>(S.nb_start);
+    d.nb = P<int32_t>(S.nb);
+    d.tree_pt = P<int32_t>(S.tree_pt);
+    d.tree_abase = P<long long>(S.tree_abase);
+    d.tree_lab = P<int32_t>(S.tree_lab);
+    d.nref = P<int32_t>(S.nref);
+    d.lab = P<float4>(S.lab);
+    d.labq = P<int32_t>(S.labq);
+    d.abc = P<float>(S.abc);
+    d.minc = P<double>(S.minc);
+    d.abc_bak = P<float>(S.abc_bak);
+    d.minc_bak = P<double>(S.minc_bak);
+    d.A = P<double>(S.A);
+    d.vol = P<float>(S.vrows);
+    d.dice = P<float>(ctx->pms_dice);
+    d.dice_n = ctx->pms_dice_n;
+    d.rnd = nullptr;
+    d.off = P<long long>(S.off);
+    d.oguess = P<long long>(S.oguess);
+    d.cnt = P<int32_t>(S.cnt);
+    d.flag = P<int32_t>(S.flag);
+    d.result = P<int32_t>(S.result);
+    d.err = ctx->d_err;
+    d.slut = P<double>(ctx->slut);
+    d.s2lut = P<double>(ctx->s2lut);
+    d.W = ctx->W;
+    d.Dv = D;
+    d.Dmax = D;
+    d.K = S.f.K;
+    d.nrounds = S.f.nrounds;
+    return d;
+}
+
+// One speculative MST_PMS call of one view (iteration > 0).  Passes over the trees [t_lo, K): guessed
+// offsets, every tree's propagation and refinement, validation.  The first tree whose offset or sampled
+// labels were wrong (t*) and everything after it go back to the call's starting state; t* runs serially
+// (its inputs are exact now) and the next pass speculates from t* + 1.
+sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
+    PmsState& S = ctx->pms[v];
+    const PmsForest& f = S.f;
+    const int K = f.K, R = f.nrounds;
+    const size_t N = (size_t)f.W * f.H;
+    const int max_rounds = pms_max_rounds();
+    HIPC(launch_pms_backup(ctx->st, d, N));
+    HIPC(hipMemsetAsync(S.off.p, 0, 16, ctx->st));
+    int t_lo = 0, rounds = 0;
+    while (t_lo < K) {
+        if (rounds >= max_rounds) {  // pathological: finish the call in order
+            HIPC(launch_pms_serial(ctx->st, d, t_lo, K));
+            ctx->pms_stats.serial_trees += K - t_lo;
+            break;
+        }
+        ++rounds;
+        ++ctx->pms_stats.spec_rounds;
+        const size_t K1 = (size_t)K + 1;
+        HIPC(launch_pms_guess(ctx->st, d, t_lo));
+        HIPC(launch_pms_prop_setup(ctx->st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
+        for (int r = R - 1; r >= 0; --r)
+            HIPC(launch_pms_walk(ctx->st, d, 0, true, r, f.rt_item[r * K1 + t_lo], f.rt_item[r * K1 + K]));
+        for (int r = 0; r < R; ++r)
+            HIPC(launch_pms_walk(ctx->st, d, 0, false, r, f.rt_item[r * K1 + t_lo], f.rt_item[r * K1 + K]));
+        HIPC(launch_pms_update(ctx->st, d, 0, f.tree_start[t_lo], (int)N));
+        HIPC(launch_pms_ref_setup(ctx->st, d, t_lo));
+        for (int r = R - 1; r >= 0; --r)
+            HIPC(launch_pms_walk(ctx->st, d, 1, true, r, f.rt_path[r * K1 + t_lo], f.rt_path[r * K1 + K]));
+        for (int r = 0; r < R; ++r)
+            HIPC(launch_pms_walk(ctx->st, d, 1, false, r, f.rt_path[r * K1 + t_lo], f.rt_path[r * K1 + K]));
+        HIPC(launch_pms_update(ctx->st, d, 1, f.tree_start[t_lo], (int)N));
+        HIPC(launch_pms_validate(ctx->st, d, t_lo));
+        HIPC(hipMemcpyAsync(ctx->h_pms_res, S.result.p, 16, hipMemcpyDeviceToHost, ctx->st));
+        HIPC(hipStreamSynchronize(ctx->st));
+        const int ts = ctx->h_pms_res[0];
+        if (ts < t_lo || ts > K) return fail(ctx, SM_ERR_STATE, "MST_PMS validation returned a bad tree index");
+        if (ts == K) break;
+        HIPC(launch_pms_restore(ctx->st, d, f.tree_start[ts], (int)N));
+        HIPC(hipMemcpyAsync(S.off.p, P<int32_t>(S.result) + 2, 8, hipMemcpyDeviceToDevice, ctx->st));
+        HIPC(launch_pms_serial(ctx->st, d, ts, ts + 1));
+        ctx->pms_stats.serial_trees += 1;
+        t_lo = ts + 1;
+    }
+    return SM_OK;
+}
+
+// SM_AGG_PMS: Stereo3DMST's stereo3dmst() after its cost volume (Stereo3DMST.cpp:805-904) -- segment
+// forests, random plane labels, pms_iters MST_PMS calls on the left view, then on the right, plane
+// disparities.  Runs to completion (host synchronisations between speculative passes).
+sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H;
+    const int iters = p->pms_iters;
+    const int L = sm_pms_levels(D);
+    sm_pms_stats& st = ctx->pms_stats;
+    st = sm_pms_stats{};
+    st.iters = iters;
+    const double t0 = now_ms();
+    // 1. the forests: the reference's order-dependent segmentation (c = +inf: the MST) on the host
+    CHECK(stage_segment(ctx, 3, p->c, p->min_size));
+    // 2. reference-numbered forests and walk schedules, both views in parallel
+    {
+        auto build = [ctx, W, H, N](int v) {
+            std::vector<uint8_t> mR(N), mD(N);
+            for (size_t i = 0; i < N; ++i) {
+                mR[i] = ctx->h_m[v][0][i] && ctx->h_fw[v][0][i] != SM_VIRTUAL_W;
+                mD[i] = ctx->h_m[v][1][i] && ctx->h_fw[v][1][i] != SM_VIRTUAL_W;
+            }
+            pms_build_forest(W, H, ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), mR.data(), mD.data(), ctx->pms[v].f);
+        };
+        std::thread other(build, 1);
+        build(0);
+        other.join();
+    }
+    // 3. random streams: the replayed dice prefix, the rand() values of every call (after random_rgb's
+    // 3 draws per pixel of both views), the initial labels (one stream, so both views start equal)
+    const int K0 = ctx->pms[0].f.K, K1 = ctx->pms[1].f.K;
+    ctx->pms_hrnd.resize((size_t)iters * (K0 + K1) + 1);
+    std::thread rng([ctx, iters, K0, K1, N] {
+        sm_pms_glibc_random(1u, (long)(6 * N), (long)iters * (K0 + K1), ctx->pms_hrnd.data());
+    });
+    if (ctx->pms_init_key[0] != W || ctx->pms_init_key[1] != H || ctx->pms_init_key[2] != D) {
+        ctx->pms_init.resize(3 * N);
+        sm_pms_init_labels(W, H, D, ctx->pms_init.data());
+        ctx->pms_init_key[0] = W;
+        ctx->pms_init_key[1] = H;
+        ctx->pms_init_key[2] = D;
+    }
+    if (ctx->pms_dblmax.size() != N) ctx->pms_dblmax.assign(N, DBL_MAX);
+    rng.join();
+    const double t1 = now_ms();
+    st.prep_ms = t1 - t0;
+    st.ntrees[0] = K0;
+    st.ntrees[1] = K1;
+    for (int v = 0; v < 2; ++v) CHECK(pms_upload_view(ctx, v, L));
+    const long long need = std::max(ctx->pms[0].dice_need, ctx->pms[1].dice_need);
+    if (need > ctx->pms_dice_n) {
+        std::vector<float> dice((size_t)need);
+        sm_pms_dice((long)need, dice.data());
+        CHECK(ensure(ctx, ctx->pms_dice, (size_t)need * 4));
+        HIPC(hipMemcpy(ctx->pms_dice.p, dice.data(), (size_t)need * 4, hipMemcpyHostToDevice));
+        ctx->pms_dice_n = need;
+    }
+    CHECK(upload_vec(ctx, ctx->pms_rnd, ctx->pms_hrnd));
+    // 4. cost rows [N][D]: the AGD volume, or the uploaded MC-CNN volumes with the reference's clamp
+    for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->pms[v].vrows, N * (size_t)D * 4));
+    if (ctx->use_vol) {
+        for (int v = 0; v < 2; ++v)
+            HIPC(launch_pms_vol_rows(ctx->st, P<float>(ctx->vin[v]), N, D, D, 1, P<float>(ctx->pms[v].vrows)));
+    } else {
+        for (int v = 0; v < 2; ++v) CHECK(ensure(ctx, ctx->vol[v], N * (size_t)D * 4));
+        HIPC(launch_cost_volume(ctx->st, P<uint32_t>(ctx->bgrx[0]), P<float>(ctx->gray[0]), P<uint32_t>(ctx->bgrx[1]),
+                                P<float>(ctx->gray[1]), P<float>(ctx->atab), W, H, 0, D, P<float>(ctx->vol[0]),
+                                P<float>(ctx->vol[1])));
+        for (int v = 0; v < 2; ++v)
+            HIPC(launch_pms_vol_rows(ctx->st, P<float>(ctx->vol[v]), N, D, D, 0, P<float>(ctx->pms[v].vrows)));
+    }
+    for (int v = 0; v < 2; ++v) {
+        HIPC(hipMemcpyAsync(ctx->pms[v].abc.p, ctx->pms_init.data(), N * 12, hipMemcpyHostToDevice, ctx->st));
+        HIPC(hipMemcpyAsync(ctx->pms[v].minc.p, ctx->pms_dblmax.data(), N * 8, hipMemcpyHostToDevice, ctx->st));
+    }
+    HIPC(hipStreamSynchronize(ctx->st));
+    const double t2 = now_ms();
+    st.setup_ms = t2 - t1;
+    // 5. the MST_PMS calls: left view, then right (:858-889); the rand() values follow that order
+    const bool serial_only = pms_serial_only();
+    double iter0 = 0.0, rest = 0.0;
+    size_t roff = 0;
+    for (int v = 0; v < 2; ++v) {
+        PmsDev d = pms_dev(ctx, v, D);
+        const int K = d.K;
+        for (int i = 0; i < iters; ++i) {
+            const double a = now_ms();
+            d.rnd = P<int32_t>(ctx->pms_rnd) + roff;
+            roff += (size_t)K;
+            if (i == 0 || serial_only) {
+                HIPC(hipMemsetAsync(ctx->pms[v].off.p, 0, 16, ctx->st));
+                HIPC(launch_pms_serial(ctx->st, d, 0, K));
+                st.serial_trees += K;
+            } else {
+                CHECK(pms_speculative_call(ctx, v, d));
+            }
+            HIPC(hipStreamSynchronize(ctx->st));
+            const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE);
+            if (e & 6u) {
+                __atomic_store_n(ctx->h_err, 0u, __ATOMIC_RELEASE);
+                return fail(ctx, SM_ERR_STATE, (e & 4u) ? "MST_PMS: dice stream exhausted (internal sizing error)"
+                                                        : "MST_PMS: a propagation index fell outside its tree (the "
+                                                          "reference would read outside mst_vertices_vec)");
+            }
+            (i == 0 ? iter0 : rest) += now_ms() - a;
+        }
+        // outputs: the plane disparity, the per-pixel aggregated minimum, idx = -1
+        CHECK(ensure(ctx, ctx->disp[v], N * 4));
+        CHECK(ensure(ctx, ctx->minc[v], N * 8));
+        CHECK(ensure(ctx, ctx->idx[v], N * 4));
+        HIPC(launch_pms_disp(ctx->st, P<float>(ctx->pms[v].abc), W, N, P<float>(ctx->disp[v])));
+        HIPC(hipMemcpyAsync(ctx->minc[v].p, ctx->pms[v].minc.p, N * 8, hipMemcpyDeviceToDevice, ctx->st));
+        HIPC(hipMemsetAsync(ctx->idx[v].p, 0xFF, N * 4, ctx->st));
+    }
+    st.iter0_ms = iter0;
+    st.iters_ms = rest;
+    st.total_ms = now_ms() - t0;
+    ctx->pms_last = true;
+    return SM_OK;
+}
+
 sm_status upload(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride) {
     if (!l || !r) return fail(ctx, SM_ERR_ARG, "null image");
     if (W < 1 || H < 1 || stride < 3 * W) return fail(ctx, SM_ERR_ARG, "bad image geometry");
@@ -1138,6 +1467,7 @@ void sm_default_params(sm_params* p) {
     p->gf_radius = 9;                                  // PatchMatchStereoGPU.cu:9001
     p->gf_eps = (float)(std::pow(0.01, 2.0) * 255 * 255);  // :9000
     p->views = 3;                                      // both views
+    p->pms_iters = 100;                                // Stereo3DMST.cpp:854
 }
 
 sm_status sm_device_count(int* count) {
@@ -1185,7 +1515,8 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         return SM_ERR_HIP;
     }
     ctx->h_err[0] = 0;
-    if (hipHostMalloc((void**)&ctx->h_changed, (2 * SM_MST_MAX_ROUNDS + 8) * sizeof(int)) != hipSuccess ||
+    if (hipHostMalloc((void**)&ctx->h_pms_res, 16) != hipSuccess ||
+        hipHostMalloc((void**)&ctx->h_changed, (2 * SM_MST_MAX_ROUNDS + 8) * sizeof(int)) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
         return SM_ERR_HIP;
@@ -1228,6 +1559,17 @@ void sm_destroy(sm_ctx* ctx) {
     if (ctx->ev_layout) (void)hipEventDestroy(ctx->ev_layout);
     for (auto e : ctx->fev) (void)hipEventDestroy(e);
     for (auto e : ctx->sev) (void)hipEventDestroy(e);
+    for (int v = 0; v < 2; ++v) {
+        PmsState& S = ctx->pms[v];
+        DevBuf* pb[] = {&S.rows, &S.rtree, &S.paths, &S.items, &S.rt_path, &S.rt_item, &S.tree_rounds, &S.tree_start,
+                        &S.bfs_pix, &S.nb_start, &S.nb, &S.tree_pt, &S.tree_abase, &S.tree_lab, &S.nref, &S.lab, &S.labq,
+                        &S.abc, &S.minc, &S.abc_bak, &S.minc_bak, &S.A, &S.vrows, &S.off, &S.oguess, &S.cnt, &S.flag,
+                        &S.result};
+        for (DevBuf* b : pb) if (b->p) (void)hipFree(b->p);
+    }
+    if (ctx->pms_dice.p) (void)hipFree(ctx->pms_dice.p);
+    if (ctx->pms_rnd.p) (void)hipFree(ctx->pms_rnd.p);
+    if (ctx->h_pms_res) (void)hipHostFree(ctx->h_pms_res);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
     if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
@@ -1305,6 +1647,23 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
     HIPC(hipEventRecord(ctx->ev[1], ctx->st));
+    ctx->pms_last = false;
+    if (p->aggregator == SM_AGG_PMS) {  // runs to completion here (host waits between its passes)
+        ctx->sub = false;
+        ctx->nfev = ctx->nsev = 0;
+        ctx->fam.clear();
+        ctx->fam_vox.clear();
+        ctx->fam_ev.clear();
+        HIPC(hipEventRecord(ctx->ev[2], ctx->st));
+        HIPC(hipEventRecord(ctx->ev[3], ctx->st));
+        CHECK(stage_pms(ctx, D, p));
+        HIPC(hipEventRecord(ctx->ev[6], ctx->st));
+        HIPC(hipEventRecord(ctx->ev[4], ctx->st));
+        CHECK(stage_post(ctx, p->post, D));
+        HIPC(hipEventRecord(ctx->ev[5], ctx->st));
+        ctx->pending = 2;
+        return SM_OK;
+    }
     if (p->aggregator == SM_AGG_GUIDED) {  // no tree: stage times MST / layout / down read 0
         ctx->sub = false;
         ctx->nfev = ctx->nsev = 0;
@@ -1545,6 +1904,25 @@ int sm_get_kernel_stats(sm_ctx* ctx, sm_kernel_stat* out, int n) {
 sm_status sm_get_filter_stats(sm_ctx* ctx, sm_filter_stats* out) {
     if (!ctx || !out) return SM_ERR_ARG;
     *out = ctx->stats;
+    return SM_OK;
+}
+
+sm_status sm_download_labels(sm_ctx* ctx, float* left_abc, float* right_abc) {
+    if (!ctx) return SM_ERR_ARG;
+    if (!ctx->pms_last) return fail(ctx, SM_ERR_STATE, "sm_download_labels: the last call was not SM_AGG_PMS");
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_download_labels: a begun call is not finished");
+    HIPC(hipSetDevice(ctx->device));
+    const size_t N = (size_t)ctx->W * ctx->H;
+    float* out[2] = {left_abc, right_abc};
+    for (int v = 0; v < 2; ++v)
+        if (out[v]) HIPC(hipMemcpyAsync(out[v], ctx->pms[v].abc.p, N * 12, hipMemcpyDeviceToHost, ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));
+    return SM_OK;
+}
+
+sm_status sm_get_pms_stats(sm_ctx* ctx, sm_pms_stats* out) {
+    if (!ctx || !out) return SM_ERR_ARG;
+    *out = ctx->pms_stats;
     return SM_OK;
 }
 

@@ -1,0 +1,67 @@
+// sm_pms.h -- launchers of the MST_PMS kernels (sm_pms.hip), library-internal.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_pms_host.h"
+
+// Device view of one view's MST_PMS state (kernel argument).  Rows of tree t are [tree_start[t],
+// tree_start[t+1]) in the schedule order of PmsForest; A rows of tree t start at tree_abase[t] with
+// tree_pt[t] doubles per row.  The label table of tree t (tree_lab[t]) holds deg(t) propagation
+// labels, then the refinement labels of the current iteration (compacted: nref[t] of them).
+struct PmsDev {
+    const PmsRow* rows;
+    const int32_t* rtree;        // row -> tree
+    const PmsPath* paths;
+    const PmsItem* items;
+    const int32_t* rt_path;      // nrounds x (K+1)
+    const int32_t* rt_item;
+    const int32_t* tree_rounds;
+    const int32_t* tree_start;
+    const int32_t* bfs_pix;
+    const int32_t* nb_start;
+    const int32_t* nb;
+    const int32_t* tree_pt;
+    const long long* tree_abase;
+    const int32_t* tree_lab;
+    int32_t* nref;
+    float4* lab;                 // (a, b, c, 0)
+    int32_t* labq;               // pixel each propagation label was sampled at
+    float* abc;                  // [N][3] current labels
+    double* minc;                // [N] current minimum aggregated costs
+    float* abc_bak;              // [N][3] labels at the start of the iteration (speculation)
+    double* minc_bak;
+    double* A;                   // aggregation rows
+    const float* vol;            // cost rows [N][Dv]
+    const float* dice;           // the replayed (-1, 1) dice stream
+    long long dice_n;
+    const int32_t* rnd;          // this iteration's rand() values, one per tree
+    long long* off;              // the dice offset of the next tree (serial mode); [1]: scratch
+    long long* oguess;           // per tree: its speculated dice offset
+    int32_t* cnt;                // per tree: dice values it consumed (given oguess)
+    int32_t* flag;               // per tree: its propagation inputs were stale (speculation)
+    int32_t* result;             // [0] first invalid tree (K: none), [1..2] its exact offset (int64)
+    uint32_t* err;               // bit 1: a sampled index fell outside its tree; bit 2: dice stream exhausted
+    const double* slut;
+    const double* s2lut;
+    int W, Dv, Dmax, K, nrounds;
+};
+
+// serial: trees [t0, t1) one after the other in one workgroup (the reference's order), starting at the
+// dice offset *off and leaving the next one there
+hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1);
+// speculative iteration over trees [t_lo, K): every tree at once from the guessed offsets and the
+// labels at the start of the iteration, then validation (sm_pms.hip "Speculation")
+hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo);
+hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int total_deg);
+hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi);
+hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);
+hipError_t launch_pms_ref_setup(hipStream_t st, const PmsDev& d, int t_lo);
+hipError_t launch_pms_validate(hipStream_t st, const PmsDev& d, int t_lo);
+hipError_t launch_pms_restore(hipStream_t st, const PmsDev& d, int row_lo, int row_hi);
+hipError_t launch_pms_backup(hipStream_t st, const PmsDev& d, size_t N);
+// [D][N] volume slices (MC-CNN layout; clamp: NaN -> 0.5, min(0.5, x), Stereo3DMST.cpp:785-803) ->
+// [N][Dv] cost rows
+hipError_t launch_pms_vol_rows(hipStream_t st, const float* in, size_t N, int D, int Dv, int clamp, float* out);
+// plane disparity of every pixel's label, fma(x, a, y*b) + c (LabelToDisp before its clamp, :197)
+hipError_t launch_pms_disp(hipStream_t st, const float* abc, int W, size_t N, float* disp);

@@ -1,0 +1,539 @@
+// sm_pms.hip -- MST_PMS, Stereo3DMST's slanted-plane label search (src/Stereo3DMST.cpp:546-629), on the GPU.
+//
+// One MST_PMS call visits the trees of a view in order.  Tree t evaluates deg(t) propagation labels
+// (one from each neighbour tree, at a pixel the dice pick, :562-580), then up to L refinement labels
+// around the label of a random pixel of its own (:582-625).  Each label is a full aggregation over the
+// tree (MSTCostAggregationAndLabelUpdate, :160-186): the lerp data term (:103-118) of every node, the
+// leaf->root and root->leaf passes, and a strict-< update of every pixel's (min_cost, label).
+//
+// Parallel form.  The labels of one phase (propagation or refinement) of one tree are independent of
+// each other: they are "slices".  Lane j of a wave walks proposal j along a heavy path of the tree, and
+// the per-pixel update then scans the proposals in order with strict <, which is the reference's
+// sequential rule.  Trees are scheduled as heavy paths by light depth (sm_pms_host.cpp): the up pass
+// runs depths deepest first, the down pass root first; the A rows are updated in place (A_up, then A),
+// as the reference does in agg_cost.
+//
+// Serial dependencies between trees: (1) the dice offset -- tree t's draws start where tree t-1's
+// ended, and a refinement level whose disparity falls outside [0, Dmax] consumes 1 draw instead of 4
+// (:604); (2) propagation reads a lower neighbour's label after that tree ran (Gauss-Seidel).  Two
+// modes keep these exact:
+//   * serial (k_pms_serial): one workgroup walks the trees in order;
+//   * speculative: every tree at once from guessed offsets and the labels at the start of the
+//     iteration; a validation scan finds the first tree whose offset or sampled labels differ from
+//     what the serial order gives, everything before it is exact, and the host redoes the rest.
+//
+// Arithmetic follows the shipped binary (build/StereoYin, read with objdump; DESIGN.md "MST_PMS"):
+// the data term fma(x, a, y*b) + c and fma(ceil - d, C[floor], (d - floor) * C[ceil]); the up pass
+// fma(A_child, S, acc) over children in descending BFS id then (double)C + acc; the down pass
+// fma(S, A_parent, S2 * A_up).  Compiled with -ffp-contract=off; divisions and square roots are
+// correctly rounded (sqrt_rn / div_rn), as x86's sqrtss / divss are.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "sm_pms.h"
+
+namespace {
+
+constexpr int PMS_CH = 8;  // nodes whose loads a walker issues together
+
+// x86 cvttss2si: NaN and out-of-range values give INT_MIN (the GPU's v_cvt_i32_f32 saturates)
+__device__ __forceinline__ int cvtt(float f) {
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : INT_MIN;
+}
+
+// compute3DLabelCost (:103-118), build/StereoYin 0x40f930
+__device__ __forceinline__ float label_cost(const float* __restrict__ vol, int Dv, int Dmax, float a, float b, float c,
+                                            int pix, float xf, float yf) {
+    const float disp = fmaf(xf, a, yf * b) + c;
+    const float dc = ceilf(disp), dfl = floorf(disp);
+    const int ic = cvtt(dc);
+    if (ic >= Dmax) return 0.5f;
+    const int ifl = cvtt(dfl);
+    if (ifl < 0) return 0.5f;
+    const float* r = vol + (size_t)pix * Dv;
+    return fmaf(dc - disp, r[ifl], (disp - dfl) * r[ic]);
+}
+
+// Correctly rounded float sqrt and division, as x86's sqrtss / divss.  HIP's __fsqrt_rn is the native
+// (1-ulp) sqrt unless OCML_BASIC_ROUNDED_OPERATIONS is defined, so the hardware result is fixed up here
+// and does not depend on compiler defaults: a candidate within an ulp is moved to the float whose
+// rounding interval holds the exact value, decided by exact double products (the midpoint of two
+// adjacent floats has <= 26 significant bits; its square or its product with a float is exact in
+// double).  Neither an exact square root nor an exact quotient can fall on a midpoint.
+// neighbours of a positive finite float
+__device__ __forceinline__ float next_up(float f) { return __uint_as_float(__float_as_uint(f) + 1u); }
+__device__ __forceinline__ float next_dn(float f) { return __uint_as_float(__float_as_uint(f) - 1u); }
+
+__device__ float sqrt_rn(float x) {
+    float s = __builtin_sqrtf(x);
+    if (!(x > 0.0f) || !(x < INFINITY)) return s;  // 0, negatives, NaN, inf: the hardware is exact
+    const double xd = (double)x;
+    for (int i = 0; i < 2; ++i) {
+        const float up = next_up(s), dn = next_dn(s);
+        const double mu = ((double)s + (double)up) * 0.5, md = ((double)s + (double)dn) * 0.5;
+        if (xd > mu * mu) s = up;
+        else if (xd < md * md) s = dn;
+        else break;
+    }
+    return s;
+}
+
+__device__ float div_rn(float a, float b) {
+    const float q = a / b;
+    if (!(fabsf(q) < INFINITY) || q == 0.0f || !(fabsf(a) < INFINITY) || !(fabsf(b) < INFINITY)) return q;
+    const double A = fabs((double)a), B = fabs((double)b);
+    float m = fabsf(q);
+    for (int i = 0; i < 2; ++i) {
+        const float up = next_up(m), dn = next_dn(m);
+        const double mu = ((double)m + (double)up) * 0.5, md = ((double)m + (double)dn) * 0.5;
+        if (A > mu * B) m = up;
+        else if (A < md * B) m = dn;
+        else break;
+    }
+    return q < 0.0f ? -m : m;
+}
+
+__device__ __forceinline__ int tree_deg(const PmsDev& d, int t) { return d.nb_start[t + 1] - d.nb_start[t]; }
+
+// proposals of a phase: count and label-table base
+__device__ __forceinline__ void phase_labels(const PmsDev& d, int phase, int t, int& P, int& base) {
+    const int deg = tree_deg(d, t);
+    if (phase == 0) {
+        P = deg;
+        base = d.tree_lab[t];
+    } else {
+        P = d.nref[t];
+        base = d.tree_lab[t] + deg;
+    }
+}
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Leaf->root walk of one heavy path for proposals [64*chunk, 64*chunk+64), bottom to head.  A node's
+// value folds its children in descending BFS id, the heavy child (the row below, walked just before)
+// from a register, the light ones from their rows (finished in a deeper round).
+__device__ void up_item(const PmsDev& d, int phase, int path, int chunk) {
+    const PmsPath pa = d.paths[path];
+    const int t = uni(pa.tree);
+    int P, base;
+    phase_labels(d, phase, t, P, base);
+    const int j = chunk * 64 + (int)(threadIdx.x & 63);
+    if (chunk * 64 >= P) return;
+    const bool act = j < P;
+    float4 L = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (act) L = d.lab[base + j];
+    const int ts = d.tree_start[t], pt = d.tree_pt[t];
+    double* __restrict__ A = d.A + d.tree_abase[t] + j;
+    const int row0 = uni(pa.row), len = uni(pa.len);
+    double x = 0.0;
+    for (int i0 = len - 1; i0 >= 0; i0 -= PMS_CH) {
+        const int n = i0 + 1 < PMS_CH ? i0 + 1 : PMS_CH;
+        double cv[PMS_CH][4];
+        float cost[PMS_CH];
+#pragma unroll
+        for (int k = 0; k < PMS_CH; ++k) {
+            if (k >= n) break;
+            const PmsRow m = d.rows[row0 + i0 - k];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                cv[k][q] = 0.0;
+                if (q < m.nch && q != m.hk && act) cv[k][q] = A[(size_t)(m.child[q] - ts) * pt];
+            }
+            cost[k] = act ? label_cost(d.vol, d.Dv, d.Dmax, L.x, L.y, L.z, m.pix, (float)m.x, (float)m.y) : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < PMS_CH; ++k) {
+            if (k >= n) break;
+            const int row = row0 + i0 - k;
+            const PmsRow m = d.rows[row];
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q >= m.nch) break;
+                const double v = q == m.hk ? x : cv[k][q];
+                acc = fma(v, d.slut[m.wch[q]], acc);  // A[parent] = fma(A[v], S, A[parent]) (0x40fad5)
+            }
+            x = (double)cost[k] + acc;  // A[v] = C + A[v] (0x40fac5)
+            if (act) A[(size_t)(row - ts) * pt] = x;
+        }
+    }
+}
+
+// Root->leaf walk of one heavy path, head to bottom: A(c) = fma(S_c, A(p), S2_c * A_up(c)) in place
+// (0x40fbb4-0x40fbbd); a tree root keeps A_up.
+__device__ void down_item(const PmsDev& d, int phase, int path, int chunk) {
+    const PmsPath pa = d.paths[path];
+    const int t = uni(pa.tree);
+    int P, base;
+    phase_labels(d, phase, t, P, base);
+    (void)base;
+    const int j = chunk * 64 + (int)(threadIdx.x & 63);
+    if (chunk * 64 >= P) return;
+    const bool act = j < P;
+    const int ts = d.tree_start[t], pt = d.tree_pt[t];
+    double* __restrict__ A = d.A + d.tree_abase[t] + j;
+    const int row0 = uni(pa.row), len = uni(pa.len);
+    const int parent = uni(d.rows[row0].parent);
+    double y = 0.0;
+    for (int i0 = 0; i0 < len; i0 += PMS_CH) {
+        const int n = len - i0 < PMS_CH ? len - i0 : PMS_CH;
+        double u[PMS_CH];
+        double pv = 0.0;
+        if (i0 == 0 && parent >= 0 && act) pv = A[(size_t)(parent - ts) * pt];
+#pragma unroll
+        for (int k = 0; k < PMS_CH; ++k) {
+            if (k >= n) break;
+            u[k] = act ? A[(size_t)(row0 + i0 + k - ts) * pt] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < PMS_CH; ++k) {
+            if (k >= n) break;
+            const int row = row0 + i0 + k;
+            const uint32_t w = d.rows[row].w;
+            if (i0 + k == 0) {
+                y = parent >= 0 ? fma(d.slut[w], pv, d.s2lut[w] * u[0]) : u[0];
+            } else {
+                y = fma(d.slut[w], y, d.s2lut[w] * u[k]);
+            }
+            if (act) A[(size_t)(row - ts) * pt] = y;
+        }
+    }
+}
+
+// strict-< update of one row's pixel over the phase's proposals in order (:173-185)
+__device__ void update_row(const PmsDev& d, int phase, int row, int t) {
+    int P, base;
+    phase_labels(d, phase, t, P, base);
+    if (P <= 0) return;
+    const int pix = d.rows[row].pix;
+    const double* a = d.A + d.tree_abase[t] + (size_t)(row - d.tree_start[t]) * d.tree_pt[t];
+    double m = d.minc[pix];
+    int best = -1;
+    for (int j = 0; j < P; ++j) {
+        const double v = a[j];
+        if (v < m) {
+            m = v;
+            best = j;
+        }
+    }
+    if (best >= 0) {
+        const float4 L = d.lab[base + best];
+        d.minc[pix] = m;
+        d.abc[3 * (size_t)pix] = L.x;
+        d.abc[3 * (size_t)pix + 1] = L.y;
+        d.abc[3 * (size_t)pix + 2] = L.z;
+    }
+}
+
+// propagation label j of tree t whose draws start at offset o (:567-573): the neighbour's BFS node
+// (int)(((dice + 1) * 0.5f) * size) (0x40ff6b-0x40ff9a), and that pixel's current label
+__device__ void prop_label(const PmsDev& d, int t, long long o, int j) {
+    const int u = d.nb[d.nb_start[t] + j];
+    const long long k = o + j;
+    float r = 0.0f;
+    if (k < d.dice_n) r = d.dice[k];
+    else atomicOr(d.err, 4u);
+    const int us = d.tree_start[u], sz = d.tree_start[u + 1] - us;
+    int i = cvtt(((r + 1.0f) * 0.5f) * (float)sz);
+    if (i < 0 || i >= sz) {  // the reference would read outside mst_vertices_vec[u]
+        atomicOr(d.err, 2u);
+        i = i < 0 ? 0 : sz - 1;
+    }
+    const int q = d.bfs_pix[us + i];
+    const int slot = d.tree_lab[t] + j;
+    d.lab[slot] = make_float4(d.abc[3 * (size_t)q], d.abc[3 * (size_t)q + 1], d.abc[3 * (size_t)q + 2], 0.0f);
+    d.labq[slot] = q;
+}
+
+// Random refinement of tree t (:582-625) with its draws from offset o: the labels of the in-range levels
+// (written compacted when `write`) and the number of draws.  The test pixel's label is read as it is now.
+__device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
+    const int ts = d.tree_start[t], sz = d.tree_start[t + 1] - ts;
+    const int tp = d.bfs_pix[ts + (int)((uint32_t)d.rnd[t] % (uint32_t)sz)];  // std::rand() % size()
+    const float px = (float)(tp % d.W), py = (float)(tp / d.W);
+    const float la = d.abc[3 * (size_t)tp], lb = d.abc[3 * (size_t)tp + 1], lc = d.abc[3 * (size_t)tp + 2];
+    const float nz = div_rn(1.0f, sqrt_rn(fmaf(la, la, lb * lb) + 1.0f));  // 0x410139-0x410170
+    const float nx = -la * nz, ny = -lb * nz;
+    const float dd = fmaf(la, px, lb * py) + lc;
+    const float fmax = (float)d.Dmax;
+    float max_n = 1.0f, max_d = 0.5f * fmax;
+    long long k = o;
+    int nv = 0;
+    const int base = d.tree_lab[t] + (d.nb_start[t + 1] - d.nb_start[t]);
+    for (; max_d > 0.1f; max_d *= 0.5f, max_n *= 0.5f) {
+        if (k + 4 > d.dice_n) {
+            atomicOr(d.err, 4u);
+            break;
+        }
+        const float rd = fmaf(d.dice[k++], max_d, dd);  // 0x410247
+        if (rd < 0.0f || rd > fmax) continue;           // :604
+        float rnx = fmaf(max_n, d.dice[k++], nx);
+        float rny = fmaf(max_n, d.dice[k++], ny);
+        float rnz = fmaf(max_n, d.dice[k++], nz);
+        if (!write) continue;
+        const float ni = div_rn(1.0f, sqrt_rn(fmaf(rnz, rnz, fmaf(rnx, rnx, rny * rny))));  // 0x41037b-0x4103c9
+        rnx *= ni;
+        rny *= ni;
+        rnz = fabsf(rnz * ni);
+        const float a = div_rn(-rnx, rnz), b = div_rn(-rny, rnz);
+        const float c = div_rn(fmaf(rd, rnz, fmaf(rnx, px, rny * py)), rnz);  // 0x41041f-0x41043d
+        d.lab[base + nv++] = make_float4(a, b, c, 0.0f);
+    }
+    if (write) d.nref[t] = nv;
+    return (int)(k - o);
+}
+
+// ----------------------------------------------------------------------------- serial mode
+__global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
+    __shared__ long long s_off;
+    __shared__ int s_n;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int wave = tid >> 6, nwaves = nt >> 6;
+    if (tid == 0) s_off = d.off[0];
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+        const int deg = tree_deg(d, t);
+        const int R = d.tree_rounds[t];
+        const int ts = d.tree_start[t], te = d.tree_start[t + 1];
+        const long long o = s_off;
+        for (int phase = 0; phase < 2; ++phase) {
+            if (phase == 0) {
+                for (int j = tid; j < deg; j += nt) prop_label(d, t, o, j);
+            } else if (tid == 0) {
+                s_n = ref_levels(d, t, o + deg, true);
+            }
+            __threadfence_block();
+            __syncthreads();
+            const int P = phase == 0 ? deg : d.nref[t];
+            if (P > 0) {
+                const int32_t* rt = phase == 0 ? d.rt_item : d.rt_path;
+                for (int r = R - 1; r >= 0; --r) {  // leaf -> root: deepest light depth first
+                    const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
+                    for (int it = lo + wave; it < hi; it += nwaves) {
+                        if (phase == 0) up_item(d, 0, d.items[it].path, d.items[it].chunk);
+                        else up_item(d, 1, it, 0);
+                    }
+                    __threadfence_block();
+                    __syncthreads();
+                }
+                for (int r = 0; r < R; ++r) {  // root -> leaf
+                    const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
+                    for (int it = lo + wave; it < hi; it += nwaves) {
+                        if (phase == 0) down_item(d, 0, d.items[it].path, d.items[it].chunk);
+                        else down_item(d, 1, it, 0);
+                    }
+                    __threadfence_block();
+                    __syncthreads();
+                }
+                for (int row = ts + tid; row < te; row += nt) update_row(d, phase, row, t);
+                __threadfence_block();
+                __syncthreads();
+            }
+        }
+        if (tid == 0) s_off = o + deg + s_n;
+        __syncthreads();
+    }
+    if (tid == 0) d.off[0] = s_off;
+}
+
+// ----------------------------------------------------------------------------- speculation
+// Guessed offsets of trees [t_lo, K) from the exact offset of t_lo (off[0]): each tree's refinement
+// draws counted from the label its test pixel has now, i.e. assuming propagation leaves it unchanged.
+__global__ void k_pms_guess(PmsDev d, int t_lo) {
+    if (threadIdx.x != 0) return;
+    long long o = d.off[0];
+    for (int t = t_lo; t < d.K; ++t) {
+        d.oguess[t] = o;
+        const int deg = tree_deg(d, t);
+        o += deg + ref_levels(d, t, o + deg, false);
+    }
+}
+
+__global__ void k_pms_prop_setup(PmsDev d, int t_lo) {
+    // one thread per (tree, neighbour): nb entries from nb_start[t_lo]
+    const int e = d.nb_start[t_lo] + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (e >= d.nb_start[d.K]) return;
+    // tree of entry e: binary search in nb_start
+    int lo = t_lo, hi = d.K - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (d.nb_start[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    prop_label(d, lo, d.oguess[lo], e - d.nb_start[lo]);
+}
+
+__global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, int item_lo, int item_hi) {
+    const int it = item_lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (it >= item_hi) return;
+    int path = it, chunk = 0;
+    if (phase == 0) {
+        path = d.items[it].path;
+        chunk = d.items[it].chunk;
+    }
+    if (up) up_item(d, phase, path, chunk);
+    else down_item(d, phase, path, chunk);
+}
+
+__global__ void k_pms_update(PmsDev d, int phase, int row_lo, int row_hi) {
+    const int row = row_lo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (row >= row_hi) return;
+    update_row(d, phase, row, d.rtree[row]);
+}
+
+__global__ void k_pms_ref_setup(PmsDev d, int t_lo) {
+    const int t = t_lo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= d.K) return;
+    const int deg = tree_deg(d, t);
+    d.cnt[t] = deg + ref_levels(d, t, d.oguess[t] + deg, true);
+}
+
+// Per tree: a propagation label taken from a lower neighbour differs from that pixel's label after the
+// neighbour ran (the serial order would have read the new one).  Then the scan: the first tree whose
+// guessed offset or inputs are wrong; every tree before it is exact.
+__global__ void k_pms_flags(PmsDev d, int t_lo) {
+    const int t = t_lo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= d.K) return;
+    int f = 0;
+    const int deg = tree_deg(d, t), base = d.tree_lab[t];
+    for (int j = 0; j < deg && !f; ++j) {
+        if (d.nb[d.nb_start[t] + j] >= t) continue;
+        const int q = d.labq[base + j];
+        const float4 L = d.lab[base + j];
+        f = __float_as_uint(L.x) != __float_as_uint(d.abc[3 * (size_t)q]) ||
+            __float_as_uint(L.y) != __float_as_uint(d.abc[3 * (size_t)q + 1]) ||
+            __float_as_uint(L.z) != __float_as_uint(d.abc[3 * (size_t)q + 2]);
+    }
+    d.flag[t] = f;
+}
+
+__global__ void k_pms_scan(PmsDev d, int t_lo) {
+    if (threadIdx.x != 0) return;
+    long long o = d.off[0];
+    int t = t_lo;
+    for (; t < d.K; ++t) {
+        if (d.oguess[t] != o || d.flag[t]) break;
+        o += d.cnt[t];
+    }
+    d.result[0] = t;
+    *reinterpret_cast<long long*>(d.result + 2) = o;  // the exact offset of tree t
+}
+
+__global__ void k_pms_restore(PmsDev d, int row_lo, int row_hi) {
+    const int row = row_lo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (row >= row_hi) return;
+    const size_t p = (size_t)d.rows[row].pix;
+    d.minc[p] = d.minc_bak[p];
+    d.abc[3 * p] = d.abc_bak[3 * p];
+    d.abc[3 * p + 1] = d.abc_bak[3 * p + 1];
+    d.abc[3 * p + 2] = d.abc_bak[3 * p + 2];
+}
+
+__global__ void k_pms_vol_rows(const float* __restrict__ in, size_t N, int D, int Dv, int clamp, float* __restrict__ out) {
+    // 32 x 32 tile transpose through LDS: in [D][N] -> out [N][Dv]
+    __shared__ float tile[32][33];
+    const size_t p0 = (size_t)blockIdx.x * 32;
+    const int d0 = blockIdx.y * 32;
+    for (int k = threadIdx.y; k < 32; k += blockDim.y) {
+        const int dd = d0 + k;
+        const size_t p = p0 + threadIdx.x;
+        float v = 0.0f;
+        if (dd < D && p < N) {
+            v = in[(size_t)dd * N + p];
+            if (clamp) v = isnan(v) ? 0.5f : (v < 0.5f ? v : 0.5f);  // std::min(0.5f, v)
+        }
+        tile[k][threadIdx.x] = v;
+    }
+    __syncthreads();
+    for (int k = threadIdx.y; k < 32; k += blockDim.y) {
+        const size_t p = p0 + k;
+        const int dd = d0 + threadIdx.x;
+        if (p < N && dd < Dv) out[p * Dv + dd] = dd < D ? tile[threadIdx.x][k] : 0.0f;
+    }
+}
+
+__global__ void k_pms_disp(const float* __restrict__ abc, int W, size_t N, float* __restrict__ disp) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float xf = (float)(int)(i % (size_t)W), yf = (float)(int)(i / (size_t)W);
+    disp[i] = fmaf(xf, abc[3 * i], yf * abc[3 * i + 1]) + abc[3 * i + 2];  // 0x40fdbe-0x40fdd0
+}
+
+__global__ void k_pms_backup(PmsDev d, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    d.minc_bak[i] = d.minc[i];
+    d.abc_bak[3 * i] = d.abc[3 * i];
+    d.abc_bak[3 * i + 1] = d.abc[3 * i + 1];
+    d.abc_bak[3 * i + 2] = d.abc[3 * i + 2];
+}
+
+inline unsigned blocks(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1) {
+    if (t1 <= t0) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_serial, dim3(1), dim3(1024), 0, st, d, t0, t1);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo) {
+    hipLaunchKernelGGL(k_pms_guess, dim3(1), dim3(64), 0, st, d, t_lo);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int total_deg) {
+    if (total_deg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_prop_setup, dim3(blocks((size_t)total_deg, 256)), dim3(256), 0, st, d, t_lo);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi) {
+    (void)r;
+    if (item_hi <= item_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_walk, dim3(blocks((size_t)(item_hi - item_lo) * 64, 256)), dim3(256), 0, st, d, phase,
+                       up ? 1 : 0, item_lo, item_hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi) {
+    if (row_hi <= row_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_update, dim3(blocks((size_t)(row_hi - row_lo), 256)), dim3(256), 0, st, d, phase, row_lo, row_hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_ref_setup(hipStream_t st, const PmsDev& d, int t_lo) {
+    if (t_lo >= d.K) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_ref_setup, dim3(blocks((size_t)(d.K - t_lo), 256)), dim3(256), 0, st, d, t_lo);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_validate(hipStream_t st, const PmsDev& d, int t_lo) {
+    if (t_lo < d.K) hipLaunchKernelGGL(k_pms_flags, dim3(blocks((size_t)(d.K - t_lo), 256)), dim3(256), 0, st, d, t_lo);
+    hipLaunchKernelGGL(k_pms_scan, dim3(1), dim3(64), 0, st, d, t_lo);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_restore(hipStream_t st, const PmsDev& d, int row_lo, int row_hi) {
+    if (row_hi <= row_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_restore, dim3(blocks((size_t)(row_hi - row_lo), 256)), dim3(256), 0, st, d, row_lo, row_hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_backup(hipStream_t st, const PmsDev& d, size_t N) {
+    hipLaunchKernelGGL(k_pms_backup, dim3(blocks(N, 256)), dim3(256), 0, st, d, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_vol_rows(hipStream_t st, const float* in, size_t N, int D, int Dv, int clamp, float* out) {
+    hipLaunchKernelGGL(k_pms_vol_rows, dim3(blocks(N, 32), (unsigned)((Dv + 31) / 32)), dim3(32, 8), 0, st, in, N, D, Dv,
+                       clamp, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_disp(hipStream_t st, const float* abc, int W, size_t N, float* disp) {
+    hipLaunchKernelGGL(k_pms_disp, dim3(blocks(N, 256)), dim3(256), 0, st, abc, W, N, disp);
+    return hipGetLastError();
+}

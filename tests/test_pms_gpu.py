@@ -1,0 +1,137 @@
+"""GPU parity of MST_PMS (SM_AGG_PMS), Stereo3DMST's slanted-plane label search
+(src/Stereo3DMST.cpp:546-629, driven at :851-889), through the C-ABI against the oracle's serial
+restatement (oracle/sm_oracle_pms.c).  Labels (a, b, c), the per-pixel aggregated minima and the
+plane disparities are compared BIT-EXACT after 1 and 3 calls per view, in both device modes (the
+first call of a view serial, later calls speculative with validation; SM_PMS_SERIAL=1 runs every
+call serially)."""
+import numpy as np
+import pytest
+
+import stereomatch_amd as sm
+from conftest import golden_cases, load_case
+from oracle import oracle as O
+from tools.synth import make_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def u32(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def u64(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+def run_gpu(ctx, left, right, D, iters, c=5000.0, min_size=200, post=0, vols=None):
+    p = sm.default_params(aggregator=sm.SM_AGG_PMS, c=c, min_size=min_size, pms_iters=iters, post=post,
+                          disp_total=D)
+    if vols is not None:
+        ctx.upload_cost_volumes(*vols)
+        p.cost_kind = sm.SM_COST_VOLUME
+    out = ctx.match(left, right, D, p)
+    return out, ctx.labels(), ctx.pms_stats()
+
+
+def check_view(out, labs, ref, v):
+    np.testing.assert_array_equal(u32(labs[v]), u32(ref[v]["abc"]), err_msg="%s labels" % v)
+    np.testing.assert_array_equal(u64(out[v]["minc"].ravel()), u64(ref[v]["minc"]), err_msg="%s minima" % v)
+    np.testing.assert_array_equal(u32(out[v]["disp"].ravel()), u32(plane_disp(ref[v]["abc"], out[v]["disp"].shape)),
+                                  err_msg="%s plane disparities" % v)
+    assert (out[v]["idx"] == -1).all()
+
+
+def plane_disp(abc, shape):
+    H, W = shape
+    return O.pms_plane_disp(abc, W, H).ravel()
+
+
+SMALL = [n for n in golden_cases() if n in ("smooth_64x48", "rand_37x23", "smooth_97x61", "const_16x12")]
+
+
+@pytest.mark.parametrize("name", SMALL)
+@pytest.mark.parametrize("c,min_size", [(5000.0, 200), (300.0, 20)])
+@pytest.mark.parametrize("iters", [1, 3])
+def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
+    z = load_case(name)
+    D = int(z["D"])
+    ref = O.stereo3dmst_pms(z["left"], z["right"], D, iters=iters, c=c, min_size=min_size)
+    out, labs, st = run_gpu(gpu_ctx, z["left"], z["right"], D, iters, c, min_size)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+    assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
+
+
+@pytest.mark.parametrize("serial", ["0", "1"])
+def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, serial):
+    """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs and wrong
+    offsets and must redo them; SM_PMS_SERIAL=1 is the plain serial order."""
+    monkeypatch.setenv("SM_PMS_SERIAL", serial)
+    left, right, _ = make_pair(160, 120, 48, index=3)
+    ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
+    out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+    if serial == "0":
+        assert st["spec_rounds"] >= 6  # calls 2..4 of both views
+
+
+def test_pms_max_rounds_fallback(gpu_ctx, monkeypatch):
+    """SM_PMS_MAX_ROUNDS=1: a call whose first speculative pass fails finishes in serial order."""
+    monkeypatch.setenv("SM_PMS_MAX_ROUNDS", "1")
+    left, right, _ = make_pair(128, 96, 40, index=4)
+    ref = O.stereo3dmst_pms(left, right, 40, iters=3, c=200.0, min_size=10)
+    out, labs, _ = run_gpu(gpu_ctx, left, right, 40, 3, 200.0, 10)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+
+
+def test_pms_mccnn_volumes_bitexact(gpu_ctx):
+    """MC-CNN ingest (:764-803) as the data term: NaNs and values above the clamp."""
+    left, right, _ = make_pair(96, 64, 32, index=5)
+    rng = np.random.default_rng(7)
+    vols = [rng.uniform(-0.2, 0.8, (32, 64, 96)).astype(np.float32) for _ in range(2)]
+    for v in vols:
+        v[rng.uniform(size=v.shape) < 0.01] = np.nan
+    ref = O.stereo3dmst_pms(left, right, 32, iters=2, vols=[O.mccnn_clamp(v) for v in vols], c=500.0, min_size=30)
+    out, labs, _ = run_gpu(gpu_ctx, left, right, 32, 2, 500.0, 30, vols=vols)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+
+
+def test_pms_output_step(gpu_ctx):
+    """stereo3dmst's output step on the plane labels: LabelToDisp + *= (Dmax-1.f), then the L-R check of
+    the left map (:189-201, :900-904)."""
+    left, right, _ = make_pair(128, 80, 40, index=6)
+    D = 40
+    ref = O.stereo3dmst_pms(left, right, D, iters=2, c=1000.0, min_size=50)
+    out, labs, _ = run_gpu(gpu_ctx, left, right, D, 2, 1000.0, 50, post=sm.STEREO3DMST_POST)
+    np.testing.assert_array_equal(u32(out["right"]["disp"]), u32(ref["right"]["disp"]))
+    np.testing.assert_array_equal(u32(out["left"]["disp"]), u32(ref["left"]["disp_checked"]))
+
+
+def test_pms_bad_params(gpu_ctx):
+    left, right, _ = make_pair(32, 24, 16, index=1)
+    for kw in (dict(disp_begin=4), dict(views=1), dict(post=sm.SM_POST_SUBPIXEL), dict(pms_iters=-1)):
+        p = sm.default_params(aggregator=sm.SM_AGG_PMS, c=100.0, min_size=10, pms_iters=1)
+        for k, val in kw.items():
+            setattr(p, k, val)
+        with pytest.raises(sm.StereoMSTError) as e:
+            gpu_ctx.match(left, right, 16, p)
+        assert e.value.status == 1
+    with pytest.raises(sm.StereoMSTError) as e:  # labels after a non-PMS call
+        gpu_ctx.match(left, right, 16)
+        gpu_ctx.labels()
+    assert e.value.status == 5
+
+
+@pytest.mark.timeout(600)
+def test_pms_full_c2_one_call_bitexact(gpu_ctx):
+    """Full C2 (1920x1200, Dmax 128), the reference's segment mode (c=5000, min_size 200), one MST_PMS
+    call per view."""
+    left, right, _ = make_pair(1920, 1200, 128, index=0)
+    ref = O.stereo3dmst_pms(left, right, 128, iters=1, c=5000.0, min_size=200)
+    out, labs, st = run_gpu(gpu_ctx, left, right, 128, 1)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(u32(labs[v]), u32(ref[v]["abc"]))
+        np.testing.assert_array_equal(u64(out[v]["minc"].ravel()), u64(ref[v]["minc"]))
