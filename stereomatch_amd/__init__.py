@@ -22,7 +22,7 @@ from ._lib import (SM_AGG_GUIDED, SM_AGG_PMS, SM_AGG_TREE, SM_COST_AGD, SM_COST_
 STEREO3DMST_POST = SM_POST_LABEL_TO_DISP | SM_POST_LR_CHECK
 
 __all__ = ["stereo3dmst", "startTimer", "getTimer", "Context", "default_params", "StereoMSTError", "device_count",
-           "shard_range", "partition", "STEREO3DMST_POST"]
+           "shard_range", "partition", "STEREO3DMST_POST", "SM_AGG_PMS"]
 
 
 def shard_range(d_total, nranks, rank):
@@ -65,22 +65,41 @@ def _ctx():
     return _default_ctx
 
 
-def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dmax=100):
-    """Reference-compatible entry (src/Stereo3DMST.cpp:714-912, per-slice restatement).
+# stereo3dmst's own algorithm (Stereo3DMST.cpp:830-832, 854): the Felzenszwalb forest with c = 5000 and
+# min_size = 200, random plane labels, 100 MST_PMS calls per view
+PMS_C, PMS_MIN_SIZE, PMS_ITERS = 5000.0, 200, 100
 
-    left_img/right_img: HxWx3 uint8 BGR (cv::Mat CV_8UC3).  Returns (left_disp, right_disp),
-    float32 HxW in [0, Dmax-1]: the strict-< winner-take-all slice of the MST-aggregated
-    cost, with the reference's output step applied: both maps go through
-    LabelToDisp's clamp(d/(Dmax-1.f), 0, 1) and *= (Dmax-1.f) in float (:189-201, :900-902), then
-    the left map is left-right checked without fill (:904, :632-662); the right map is unchecked.
+
+def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dmax=100, algorithm=None,
+                iters=PMS_ITERS):
+    """Reference-compatible entry (src/Stereo3DMST.cpp:714-912).
+
+    left_img/right_img: HxWx3 uint8 BGR (cv::Mat CV_8UC3).  Returns (left_disp, right_disp), float32 HxW
+    in [0, Dmax-1], after the reference's output step: both maps through LabelToDisp's
+    clamp(d/(Dmax-1.f), 0, 1) and *= (Dmax-1.f) in float (:189-201, :900-902), then the left map
+    left-right checked without fill (:904, :632-662); the right map is unchecked.
+
+    algorithm "pms" (default; env SM_STEREO3DMST_ALGO overrides): the reference's own label search --
+    segment forest (c=5000, min_size=200), random slanted-plane labels, `iters` MST_PMS calls per view
+    (:546-629, :851-889), LabelToDisp of the plane labels.  "slices": this framework's per-slice
+    restatement -- the MST tree filter of every disparity slice and a strict-< WTA.
     data_cost "AGD" builds the cost on the GPU; "MCCNN_fst"/"MCCNN_acrt" take the MC-CNN volumes
     from mc-cnn-master/{left,right}.bin (after running the network there, as the reference does).
     Like the reference, an unsupported data_cost prints a message and returns
     allocated-but-unset maps (:756-759); the names are only forwarded to the cost source.
     """
+    algorithm = algorithm or os.environ.get("SM_STEREO3DMST_ALGO", "pms")
+    if algorithm not in ("pms", "slices"):
+        raise ValueError("algorithm must be 'pms' or 'slices'")
     H, W = left_img.shape[:2]
     left_disp = np.empty((H, W), np.float32)
     right_disp = np.empty((H, W), np.float32)
+    p = default_params(post=STEREO3DMST_POST, disp_total=int(Dmax))
+    if algorithm == "pms":
+        p.aggregator = SM_AGG_PMS
+        p.c = PMS_C
+        p.min_size = PMS_MIN_SIZE
+        p.pms_iters = int(iters)
     if data_cost in ("MCCNN_fst", "MCCNN_acrt"):
         # reference: without an mc-cnn-master folder MCCNN_fst prints and returns (:727-731),
         # MCCNN_acrt returns silently (:744-745); otherwise it runs the network (./main.lua, a
@@ -95,15 +114,15 @@ def stereo3dmst(left_name, right_name, left_img, right_img, data_cost="AGD", Dma
             return left_disp, right_disp
         ctx = _ctx()
         ctx.upload_cost_volumes(*vols)
-        out = ctx.match(left_img, right_img, int(Dmax),
-                        default_params(post=STEREO3DMST_POST, cost_kind=SM_COST_VOLUME, disp_total=int(Dmax)))
+        p.cost_kind = SM_COST_VOLUME
+        out = ctx.match(left_img, right_img, int(Dmax), p)
         left_disp[...] = out["left"]["disp"]
         right_disp[...] = out["right"]["disp"]
         return left_disp, right_disp
     if data_cost != "AGD":
         print("wrong data cost")
         return left_disp, right_disp
-    out = _ctx().match(left_img, right_img, int(Dmax), default_params(post=STEREO3DMST_POST, disp_total=int(Dmax)))
+    out = _ctx().match(left_img, right_img, int(Dmax), p)
     left_disp[...] = out["left"]["disp"]
     right_disp[...] = out["right"]["disp"]
     return left_disp, right_disp

@@ -49,7 +49,7 @@ struct DevBuf {
 struct PmsState {
     PmsForest f;
     DevBuf rows, rtree, paths, items, rt_path, rt_item, tree_rounds, tree_start, bfs_pix, nb_start, nb, tree_pt, tree_abase,
-        tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result;
+        tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result, prof;
     std::vector<int32_t> h_rtree, h_pt, h_lab;
     std::vector<long long> h_abase;
     long long dice_need = 0;
@@ -1234,6 +1234,10 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.flag = P<int32_t>(S.flag);
     d.result = P<int32_t>(S.result);
     d.err = ctx->d_err;
+    d.prof = nullptr;
+    if (getenv("SM_PMS_PROF")) {  // diagnostics: serial-kernel segment times, printed per call
+        if (ensure(ctx, S.prof, 16 * 8) == SM_OK) d.prof = P<long long>(S.prof);
+    }
     d.slut = P<double>(ctx->slut);
     d.s2lut = P<double>(ctx->s2lut);
     d.W = ctx->W;
@@ -1242,6 +1246,51 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.K = S.f.K;
     d.nrounds = S.f.nrounds;
     return d;
+}
+
+// trees whose work (nodes x 64-proposal chunks) is at least this run over the whole GPU in serial mode
+long long pms_big_tree() {
+    const char* e = getenv("SM_PMS_BIG");
+    return e ? std::max(1ll, atoll(e)) : 32768;
+}
+
+// Trees [t0, t1) in the reference's order from the dice offset *off.  Runs of small trees go to one
+// workgroup (k_pms_serial); a large tree's phases are launched over the whole GPU, round by round.
+sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) {
+    const PmsForest& f = ctx->pms[v].f;
+    const int K = f.K;
+    const size_t K1 = (size_t)K + 1;
+    const long long big = pms_big_tree();
+    int run = t0;
+    for (int t = t0; t <= t1; ++t) {
+        bool is_big = false;
+        if (t < t1) {
+            const long long n = f.tree_start[t + 1] - f.tree_start[t];
+            const int deg = f.nb_start[t + 1] - f.nb_start[t];
+            is_big = n * ((std::max(deg, 1) + 63) / 64) >= big;
+        }
+        if (t < t1 && !is_big) continue;
+        HIPC(launch_pms_serial(ctx->st, d, run, t));
+        run = t + 1;
+        if (t == t1) break;
+        const int R = f.tree_rounds[t];
+        const int deg = f.nb_start[t + 1] - f.nb_start[t];
+        HIPC(launch_pms_prop_one(ctx->st, d, t, deg));
+        if (deg > 0) {
+            for (int r = R - 1; r >= 0; --r)
+                HIPC(launch_pms_walk(ctx->st, d, 0, true, r, f.rt_item[r * K1 + t], f.rt_item[r * K1 + t + 1]));
+            for (int r = 0; r < R; ++r)
+                HIPC(launch_pms_walk(ctx->st, d, 0, false, r, f.rt_item[r * K1 + t], f.rt_item[r * K1 + t + 1]));
+            HIPC(launch_pms_update(ctx->st, d, 0, f.tree_start[t], f.tree_start[t + 1]));
+        }
+        HIPC(launch_pms_ref_one(ctx->st, d, t));
+        for (int r = R - 1; r >= 0; --r)
+            HIPC(launch_pms_walk(ctx->st, d, 1, true, r, f.rt_path[r * K1 + t], f.rt_path[r * K1 + t + 1]));
+        for (int r = 0; r < R; ++r)
+            HIPC(launch_pms_walk(ctx->st, d, 1, false, r, f.rt_path[r * K1 + t], f.rt_path[r * K1 + t + 1]));
+        HIPC(launch_pms_update(ctx->st, d, 1, f.tree_start[t], f.tree_start[t + 1]));
+    }
+    return SM_OK;
 }
 
 // One speculative MST_PMS call of one view (iteration > 0).  Passes over the trees [t_lo, K): guessed
@@ -1259,7 +1308,7 @@ sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
     int t_lo = 0, rounds = 0;
     while (t_lo < K) {
         if (rounds >= max_rounds) {  // pathological: finish the call in order
-            HIPC(launch_pms_serial(ctx->st, d, t_lo, K));
+            CHECK(pms_serial_range(ctx, v, d, t_lo, K));
             ctx->pms_stats.serial_trees += K - t_lo;
             break;
         }
@@ -1287,7 +1336,7 @@ sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
         if (ts == K) break;
         HIPC(launch_pms_restore(ctx->st, d, f.tree_start[ts], (int)N));
         HIPC(hipMemcpyAsync(S.off.p, P<int32_t>(S.result) + 2, 8, hipMemcpyDeviceToDevice, ctx->st));
-        HIPC(launch_pms_serial(ctx->st, d, ts, ts + 1));
+        CHECK(pms_serial_range(ctx, v, d, ts, ts + 1));
         ctx->pms_stats.serial_trees += 1;
         t_lo = ts + 1;
     }
@@ -1383,9 +1432,30 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
             const double a = now_ms();
             d.rnd = P<int32_t>(ctx->pms_rnd) + roff;
             roff += (size_t)K;
+            if (d.prof) HIPC(hipMemsetAsync(d.prof, 0, 16 * 8, ctx->st));
             if (i == 0 || serial_only) {
                 HIPC(hipMemsetAsync(ctx->pms[v].off.p, 0, 16, ctx->st));
-                HIPC(launch_pms_serial(ctx->st, d, 0, K));
+                static const bool tree_times = getenv("SM_PMS_TREE_TIMES") != nullptr;  // diagnostics (tools)
+                if (tree_times && i == 0) {
+                    std::vector<hipEvent_t> ev(K + 1);
+                    for (auto& e : ev) HIPC(hipEventCreate(&e));
+                    HIPC(hipEventRecord(ev[0], ctx->st));
+                    for (int t = 0; t < K; ++t) {
+                        CHECK(pms_serial_range(ctx, v, d, t, t + 1));
+                        HIPC(hipEventRecord(ev[t + 1], ctx->st));
+                    }
+                    HIPC(hipStreamSynchronize(ctx->st));
+                    const PmsForest& f = ctx->pms[v].f;
+                    for (int t = 0; t < K; ++t) {
+                        float ms = 0;
+                        HIPC(hipEventElapsedTime(&ms, ev[t], ev[t + 1]));
+                        fprintf(stderr, "pms tree v%d t%d n %d deg %d rounds %d ms %.3f\n", v, t,
+                                f.tree_start[t + 1] - f.tree_start[t], f.nb_start[t + 1] - f.nb_start[t], f.tree_rounds[t], ms);
+                    }
+                    for (auto& e : ev) HIPC(hipEventDestroy(e));
+                } else {
+                    CHECK(pms_serial_range(ctx, v, d, 0, K));
+                }
                 st.serial_trees += K;
             } else {
                 CHECK(pms_speculative_call(ctx, v, d));
@@ -1399,6 +1469,13 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                                                           "reference would read outside mst_vertices_vec)");
             }
             (i == 0 ? iter0 : rest) += now_ms() - a;
+            if (d.prof) {
+                long long h[16];
+                HIPC(hipMemcpy(h, d.prof, 16 * 8, hipMemcpyDeviceToHost));
+                fprintf(stderr, "pms prof v%d call %d (ms): prop setup %.2f up %.2f down %.2f update %.2f | ref setup %.2f up %.2f "
+                        "down %.2f update %.2f | rounds %lld\n", v, i, h[0] * 1e-5, h[1] * 1e-5, h[2] * 1e-5, h[3] * 1e-5,
+                        h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5, h[8]);
+            }
         }
         // outputs: the plane disparity, the per-pixel aggregated minimum, idx = -1
         CHECK(ensure(ctx, ctx->disp[v], N * 4));
@@ -1564,7 +1641,7 @@ void sm_destroy(sm_ctx* ctx) {
         DevBuf* pb[] = {&S.rows, &S.rtree, &S.paths, &S.items, &S.rt_path, &S.rt_item, &S.tree_rounds, &S.tree_start,
                         &S.bfs_pix, &S.nb_start, &S.nb, &S.tree_pt, &S.tree_abase, &S.tree_lab, &S.nref, &S.lab, &S.labq,
                         &S.abc, &S.minc, &S.abc_bak, &S.minc_bak, &S.A, &S.vrows, &S.off, &S.oguess, &S.cnt, &S.flag,
-                        &S.result};
+                        &S.result, &S.prof};
         for (DevBuf* b : pb) if (b->p) (void)hipFree(b->p);
     }
     if (ctx->pms_dice.p) (void)hipFree(ctx->pms_dice.p);

@@ -42,6 +42,7 @@ struct PmsDev {
     int32_t* flag;               // per tree: its propagation inputs were stale (speculation)
     int32_t* result;             // [0] first invalid tree (K: none), [1..2] its exact offset (int64)
     uint32_t* err;               // bit 1: a sampled index fell outside its tree; bit 2: dice stream exhausted
+    long long* prof;             // SM_PMS_PROF: k_pms_serial segment totals (nullptr: off)
     const double* slut;
     const double* s2lut;
     int W, Dv, Dmax, K, nrounds;
@@ -50,6 +51,10 @@ struct PmsDev {
 // serial: trees [t0, t1) one after the other in one workgroup (the reference's order), starting at the
 // dice offset *off and leaving the next one there
 hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1);
+// serial mode, one large tree over the whole GPU: propagation labels from *off, and the refinement
+// labels (after the propagation update), which advance *off
+hipError_t launch_pms_prop_one(hipStream_t st, const PmsDev& d, int t, int deg);
+hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t);
 // speculative iteration over trees [t_lo, K): every tree at once from the guessed offsets and the
 // labels at the start of the iteration, then validation (sm_pms.hip "Speculation")
 hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo);

@@ -112,8 +112,10 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 
 // Leaf->root walk of one heavy path for proposals [64*chunk, 64*chunk+64), bottom to head.  A node's
 // value folds its children in descending BFS id, the heavy child (the row below, walked just before)
-// from a register, the light ones from their rows (finished in a deeper round).
-__device__ void up_item(const PmsDev& d, int phase, int path, int chunk) {
+// from a register, the light ones from their rows (finished in a deeper round).  Every load of a chunk
+// of PMS_CH nodes (rows, light children, cost rows) is issued before its serial part, which reads
+// only registers and the LDS weight tables sS / sS2.
+__device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phase, int path, int chunk) {
     const PmsPath pa = d.paths[path];
     const int t = uni(pa.tree);
     int P, base;
@@ -131,12 +133,17 @@ __device__ void up_item(const PmsDev& d, int phase, int path, int chunk) {
         const int n = i0 + 1 < PMS_CH ? i0 + 1 : PMS_CH;
         double cv[PMS_CH][4];
         float cost[PMS_CH];
+        int nch[PMS_CH], hk[PMS_CH], wc[PMS_CH][4];
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
-            if (k >= n) break;
+            nch[k] = 0;
+            if (k >= n) continue;
             const PmsRow m = d.rows[row0 + i0 - k];
+            nch[k] = m.nch;
+            hk[k] = m.hk;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
+                wc[k][q] = m.wch[q];
                 cv[k][q] = 0.0;
                 if (q < m.nch && q != m.hk && act) cv[k][q] = A[(size_t)(m.child[q] - ts) * pt];
             }
@@ -145,24 +152,26 @@ __device__ void up_item(const PmsDev& d, int phase, int path, int chunk) {
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
             if (k >= n) break;
-            const int row = row0 + i0 - k;
-            const PmsRow m = d.rows[row];
+            double sv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sv[q] = sS[wc[k][q]];
             double acc = 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                if (q >= m.nch) break;
-                const double v = q == m.hk ? x : cv[k][q];
-                acc = fma(v, d.slut[m.wch[q]], acc);  // A[parent] = fma(A[v], S, A[parent]) (0x40fad5)
+                if (q >= nch[k]) break;
+                const double v = q == hk[k] ? x : cv[k][q];
+                acc = fma(v, sv[q], acc);  // A[parent] = fma(A[v], S, A[parent]) (0x40fad5)
             }
             x = (double)cost[k] + acc;  // A[v] = C + A[v] (0x40fac5)
-            if (act) A[(size_t)(row - ts) * pt] = x;
+            if (act) A[(size_t)(row0 + i0 - k - ts) * pt] = x;
         }
     }
 }
 
 // Root->leaf walk of one heavy path, head to bottom: A(c) = fma(S_c, A(p), S2_c * A_up(c)) in place
 // (0x40fbb4-0x40fbbd); a tree root keeps A_up.
-__device__ void down_item(const PmsDev& d, int phase, int path, int chunk) {
+__device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
+                          int path, int chunk) {
     const PmsPath pa = d.paths[path];
     const int t = uni(pa.tree);
     int P, base;
@@ -179,26 +188,38 @@ __device__ void down_item(const PmsDev& d, int phase, int path, int chunk) {
     for (int i0 = 0; i0 < len; i0 += PMS_CH) {
         const int n = len - i0 < PMS_CH ? len - i0 : PMS_CH;
         double u[PMS_CH];
+        int w[PMS_CH];
         double pv = 0.0;
         if (i0 == 0 && parent >= 0 && act) pv = A[(size_t)(parent - ts) * pt];
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
-            if (k >= n) break;
+            w[k] = 0;
+            if (k >= n) continue;
+            w[k] = d.rows[row0 + i0 + k].w;
             u[k] = act ? A[(size_t)(row0 + i0 + k - ts) * pt] : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
             if (k >= n) break;
-            const int row = row0 + i0 + k;
-            const uint32_t w = d.rows[row].w;
+            const double S = sS[w[k]], S2 = sS2[w[k]];
             if (i0 + k == 0) {
-                y = parent >= 0 ? fma(d.slut[w], pv, d.s2lut[w] * u[0]) : u[0];
+                y = parent >= 0 ? fma(S, pv, S2 * u[0]) : u[0];
             } else {
-                y = fma(d.slut[w], y, d.s2lut[w] * u[k]);
+                y = fma(S, y, S2 * u[k]);
             }
-            if (act) A[(size_t)(row - ts) * pt] = y;
+            if (act) A[(size_t)(row0 + i0 + k - ts) * pt] = y;
         }
     }
+}
+
+// the S / S2 tables (766 weight codes) into LDS
+#define PMS_NW 766
+__device__ __forceinline__ void load_luts(const PmsDev& d, double* sS, double* sS2) {
+    for (int i = threadIdx.x; i < PMS_NW; i += blockDim.x) {
+        sS[i] = d.slut[i];
+        sS2[i] = d.s2lut[i];
+    }
+    __syncthreads();
 }
 
 // strict-< update of one row's pixel over the phase's proposals in order (:173-185)
@@ -288,10 +309,22 @@ __device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
 __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
     __shared__ long long s_off;
     __shared__ int s_n;
+    __shared__ double sS[PMS_NW], sS2[PMS_NW];
+    load_luts(d, sS, sS2);
     const int tid = threadIdx.x, nt = blockDim.x;
     const int wave = tid >> 6, nwaves = nt >> 6;
+    // SM_PMS_PROF builds: per-segment wall-clock totals (100 MHz ticks) of thread 0
+    long long tick = 0;
+    auto seg = [&](int k) {
+        if (d.prof && tid == 0) {
+            const long long now = (long long)wall_clock64();
+            if (k >= 0) atomicAdd((unsigned long long*)&d.prof[k], (unsigned long long)(now - tick));
+            tick = now;
+        }
+    };
     if (tid == 0) s_off = d.off[0];
     __syncthreads();
+    seg(-1);
     for (int t = t0; t < t1; ++t) {
         const int deg = tree_deg(d, t);
         const int R = d.tree_rounds[t];
@@ -305,33 +338,40 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
             }
             __threadfence_block();
             __syncthreads();
+            seg(4 * phase + 0);
             const int P = phase == 0 ? deg : d.nref[t];
             if (P > 0) {
                 const int32_t* rt = phase == 0 ? d.rt_item : d.rt_path;
                 for (int r = R - 1; r >= 0; --r) {  // leaf -> root: deepest light depth first
                     const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
                     for (int it = lo + wave; it < hi; it += nwaves) {
-                        if (phase == 0) up_item(d, 0, d.items[it].path, d.items[it].chunk);
-                        else up_item(d, 1, it, 0);
+                        if (phase == 0) up_item(d, sS, 0, d.items[it].path, d.items[it].chunk);
+                        else up_item(d, sS, 1, it, 0);
                     }
                     __threadfence_block();
                     __syncthreads();
                 }
+                seg(4 * phase + 1);
                 for (int r = 0; r < R; ++r) {  // root -> leaf
                     const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
                     for (int it = lo + wave; it < hi; it += nwaves) {
-                        if (phase == 0) down_item(d, 0, d.items[it].path, d.items[it].chunk);
-                        else down_item(d, 1, it, 0);
+                        if (phase == 0) down_item(d, sS, sS2, 0, d.items[it].path, d.items[it].chunk);
+                        else down_item(d, sS, sS2, 1, it, 0);
                     }
                     __threadfence_block();
                     __syncthreads();
                 }
+                seg(4 * phase + 2);
                 for (int row = ts + tid; row < te; row += nt) update_row(d, phase, row, t);
                 __threadfence_block();
                 __syncthreads();
+                seg(4 * phase + 3);
             }
         }
-        if (tid == 0) s_off = o + deg + s_n;
+        if (tid == 0) {
+            s_off = o + deg + s_n;
+            if (d.prof) atomicAdd((unsigned long long*)&d.prof[8], (unsigned long long)R);
+        }
         __syncthreads();
     }
     if (tid == 0) d.off[0] = s_off;
@@ -350,6 +390,20 @@ __global__ void k_pms_guess(PmsDev d, int t_lo) {
     }
 }
 
+// serial mode, one large tree with the whole GPU: its propagation labels from the running offset, and
+// after its propagation update its refinement labels, which advance the offset
+__global__ void k_pms_prop_one(PmsDev d, int t) {
+    const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (j < tree_deg(d, t)) prop_label(d, t, d.off[0], j);
+}
+
+__global__ void k_pms_ref_one(PmsDev d, int t) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const int deg = tree_deg(d, t);
+    const long long o = d.off[0];
+    d.off[0] = o + deg + ref_levels(d, t, o + deg, true);
+}
+
 __global__ void k_pms_prop_setup(PmsDev d, int t_lo) {
     // one thread per (tree, neighbour): nb entries from nb_start[t_lo]
     const int e = d.nb_start[t_lo] + (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -365,6 +419,8 @@ __global__ void k_pms_prop_setup(PmsDev d, int t_lo) {
 }
 
 __global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, int item_lo, int item_hi) {
+    __shared__ double sS[PMS_NW], sS2[PMS_NW];
+    load_luts(d, sS, sS2);
     const int it = item_lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     if (it >= item_hi) return;
     int path = it, chunk = 0;
@@ -372,8 +428,8 @@ __global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, i
         path = d.items[it].path;
         chunk = d.items[it].chunk;
     }
-    if (up) up_item(d, phase, path, chunk);
-    else down_item(d, phase, path, chunk);
+    if (up) up_item(d, sS, phase, path, chunk);
+    else down_item(d, sS, sS2, phase, path, chunk);
 }
 
 __global__ void k_pms_update(PmsDev d, int phase, int row_lo, int row_hi) {
@@ -476,6 +532,17 @@ inline unsigned blocks(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b
 hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1) {
     if (t1 <= t0) return hipSuccess;
     hipLaunchKernelGGL(k_pms_serial, dim3(1), dim3(1024), 0, st, d, t0, t1);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_prop_one(hipStream_t st, const PmsDev& d, int t, int deg) {
+    if (deg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_prop_one, dim3(blocks((size_t)deg, 256)), dim3(256), 0, st, d, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t) {
+    hipLaunchKernelGGL(k_pms_ref_one, dim3(1), dim3(64), 0, st, d, t);
     return hipGetLastError();
 }
 

@@ -5,9 +5,13 @@
 //   * data_cost "MCCNN_fst" without an mc-cnn-master folder prints "no mc-cnn-master folder" and
 //     returns (:727-731); "MCCNN_acrt" without it returns silently (:744-745); an unknown string
 //     prints "wrong data cost" (:756-759) -- maps are left allocated but unset, as the reference;
-//   * "AGD" runs this framework's GPU path: AGD cost volume, MST tree filter per disparity slice,
-//     strict-< WTA, then the reference's output step: left map left-right checked without fill
-//     (:900-904); both maps in [0, Dmax-1];
+//   * "AGD" runs this framework's GPU path on the AGD cost volume.  The algorithm is the reference's
+//     own (env SM_STEREO3DMST_ALGO unset or "pms"): the segment forest with c = 5000, min_size = 200,
+//     random plane labels and 100 MST_PMS calls per view (:830-832, :546-629, :851-889; env
+//     SM_PMS_ITERS overrides the count), or with SM_STEREO3DMST_ALGO=slices the per-slice
+//     restatement (MST tree filter per disparity slice, strict-< WTA); then the reference's output
+//     step: LabelToDisp + scaling, left map left-right checked without fill (:900-904), both maps in
+//     [0, Dmax-1];
 //   * "MCCNN_fst" / "MCCNN_acrt" with an mc-cnn-master folder: like the reference, run the network
 //     there (system(), :733-750; its exit status is ignored unless system() itself fails) and
 //     read mc-cnn-master/{left,right}.bin, [Dmax][rows][cols] float (:764-775); the clamp
@@ -17,6 +21,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <iostream>
 #include <mutex>
@@ -94,6 +99,14 @@ extern "C" void stereo3dmst(std::string left_name, std::string right_name, cv::M
     sm_default_params(&p);
     p.disp_total = Dmax;
     p.post = SM_POST_LABEL_TO_DISP | SM_POST_LR_CHECK;  // LabelToDisp + scaling, then the L-R check (:900-904)
+    const char* algo = getenv("SM_STEREO3DMST_ALGO");
+    if (!algo || std::string(algo) == "pms") {  // the reference's own label search (:830-832, :854)
+        p.aggregator = SM_AGG_PMS;
+        p.c = 5000.0f;
+        p.min_size = 200;
+        const char* it = getenv("SM_PMS_ITERS");
+        p.pms_iters = it ? atoi(it) : 100;
+    }
     if (mccnn) {
         if (sm_upload_cost_volumes(g_ctx, lv.data(), rv.data(), cols, rows, Dmax) != SM_OK) {
             std::cout << "stereo3dmst: " << sm_last_error(g_ctx) << "\n";

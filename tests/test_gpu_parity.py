@@ -444,7 +444,7 @@ def test_reference_surface(gpu_ctx, Dmax):
     import stereomatch_amd as sm
     left, right, _ = make_pair(160, 96, Dmax, index=4)
     sm.startTimer()
-    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "AGD", Dmax)
+    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "AGD", Dmax, algorithm="slices")
     assert sm.getTimer() >= 0
     ref = O.match(left, right, Dmax, nthreads=16)
     H, W = left.shape[:2]
@@ -662,7 +662,7 @@ def test_stereo3dmst_mccnn_ingest(gpu_ctx, tmp_path, monkeypatch):
     lv.tofile(str(tmp_path / "mc-cnn-master" / "left.bin"))
     rv.tofile(str(tmp_path / "mc-cnn-master" / "right.bin"))
     monkeypatch.chdir(tmp_path)
-    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "MCCNN_acrt", D)
+    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "MCCNN_acrt", D, algorithm="slices")
     ref = {}
     for v, img, vol in (("left", left, lv), ("right", right, rv)):
         ref[v] = O.tree_filter(W, H, O.build_tree(img), O.mccnn_clamp(vol), 0, True, False, 16)["idx"]

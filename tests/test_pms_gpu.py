@@ -135,3 +135,15 @@ def test_pms_full_c2_one_call_bitexact(gpu_ctx):
     for v in ("left", "right"):
         np.testing.assert_array_equal(u32(labs[v]), u32(ref[v]["abc"]))
         np.testing.assert_array_equal(u64(out[v]["minc"].ravel()), u64(ref[v]["minc"]))
+
+
+def test_pms_reference_surface_100_calls(gpu_ctx):
+    """The Python mirror of stereo3dmst() with the reference's own algorithm and constants (c=5000,
+    min_size 200, 100 MST_PMS calls per view, Stereo3DMST.cpp:830-832, 854) against the oracle."""
+    left, right, _ = make_pair(128, 96, 48, index=8)
+    sm.startTimer()
+    ld, rd = sm.stereo3dmst("l.png", "r.png", left, right, "AGD", 48)
+    assert sm.getTimer() >= 0
+    ref = O.stereo3dmst_pms(left, right, 48, iters=100)
+    np.testing.assert_array_equal(u32(ld), u32(ref["left"]["disp_checked"]))
+    np.testing.assert_array_equal(u32(rd), u32(ref["right"]["disp"]))
