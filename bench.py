@@ -59,12 +59,12 @@ def host_cpu_info():
     return dict(nproc=os.cpu_count(), affinity=usable, model=model, OMP_NUM_THREADS=omp)
 
 
-def cpu_baseline(W, H, D, slices, slices_1t):
-    """Oracle (CPU restatement, reference order, fp64) on a bounded sample of the workload: the full
-    MST build of both views (one thread: Kruskal is serial), then `slices` disparity slices of AGD cost
-    + tree filter + WTA with all usable host cores (OpenMP over slices; the box's share: OMP_NUM_THREADS when set) and `slices_1t`
-    slices with one thread, each extrapolated to D slices.  Test infrastructure, used only as the
-    reported baseline (never inside the timed region)."""
+def cpu_baseline(W, H, D, slices_1t):
+    """Oracle (CPU restatement, reference order, fp64) on the benchmarked workload: the full MST build of
+    both views (one thread: Kruskal is serial), then all D disparity slices of AGD cost + tree filter +
+    WTA with all usable host cores (OpenMP over slices; the box's share: OMP_NUM_THREADS when set).  A
+    one-thread figure from `slices_1t` slices is reported beside it (extrapolated, labelled so).  Test
+    infrastructure, used only as the reported baseline (never inside the timed region)."""
     from oracle import oracle as O
     info = host_cpu_info()
     threads = int(info["OMP_NUM_THREADS"] or 0) or info["affinity"]
@@ -74,8 +74,7 @@ def cpu_baseline(W, H, D, slices, slices_1t):
     trees = [O.build_tree(left), O.build_tree(right)]
     t_tree = time.perf_counter() - t0
 
-    def sample(n, nt):
-        d0 = D // 2 - n // 2
+    def run(d0, n, nt):
         t0 = time.perf_counter()
         lv, rv = O.cost_agd(left, right, d0, d0 + n, nt)  # OpenMP over slices
         t_cost = time.perf_counter() - t0
@@ -84,19 +83,46 @@ def cpu_baseline(W, H, D, slices, slices_1t):
             O.tree_filter(W, H, t, vol, d0, True, False, nt)
         return t_cost, time.perf_counter() - t0
 
-    tc, tf = sample(slices, threads)
-    frame = t_tree + (tc + tf) * (D / slices)
-    tc1, tf1 = sample(slices_1t, 1)
+    tc, tf = run(0, D, threads)
+    frame = t_tree + tc + tf
+    tc1, tf1 = run(D // 2 - slices_1t // 2, slices_1t, 1)
     frame1 = t_tree + (tc1 + tf1) * (D / slices_1t)
-    return dict(value=W * H * D / frame, unit="voxels/s", cores=threads, kind="port",
+    return dict(value=W * H * D / frame, unit="voxels/s", cores=threads, kind="port", ms_per_frame=frame * 1e3,
                 one_thread=dict(value=W * H * D / frame1, ms_per_frame=frame1 * 1e3, cost_s=tc1, filter_s=tf1,
-                                slices=slices_1t),
+                                slices=slices_1t, note="%d of %d slices with one thread, extrapolated to D" % (slices_1t, D)),
                 host=info,
                 stages_s=dict(tree_both_views=t_tree, cost=tc, filter_up_down_wta=tf),
-                sample="full %dx%d frame: MST+BFS of both views (1 thread) + %d of %d slices of AGD cost, "
-                       "tree filter and WTA (%d threads, OpenMP over slices), extrapolated to D=%d; est. ms/frame %.0f "
-                       "(1 thread: %d slices, %.0f ms/frame)" % (W, H, slices, D, threads, D, frame * 1e3, slices_1t,
-                                                                  frame1 * 1e3))
+                sample="one full %dx%d D=%d frame, both views: MST+BFS (1 thread), AGD cost, tree filter and WTA of "
+                       "all %d slices (%d threads, OpenMP over slices); %.0f ms/frame" % (W, H, D, D, threads, frame * 1e3))
+
+
+def pms_leg(ctx, left, right, D, iters, oracle):
+    """MST_PMS (SM_AGG_PMS), Stereo3DMST's own label search (c=5000, min_size 200): ms per MST_PMS call
+    per view on the GPU (the first call of a view runs serially, later ones speculatively), beside the
+    oracle's serial CPU restatement of one call (both views, rank 0 only)."""
+    p = sm.default_params(aggregator=sm.SM_AGG_PMS, c=5000.0, min_size=200, pms_iters=iters, disp_total=D)
+    ctx.match(left, right, D, p)  # warm-up
+    t = time.perf_counter()
+    ctx.match(left, right, D, p)
+    wall = (time.perf_counter() - t) * 1e3
+    st = ctx.pms_stats()
+    out = dict(iters_per_view=iters, wall_ms=wall, trees=st["ntrees"], host_prep_ms=st["prep_ms"],
+               first_call_ms_per_view=st["iter0_ms"] / 2,
+               later_call_ms_per_view=st["iters_ms"] / (2 * (iters - 1)) if iters > 1 else None,
+               speculative_passes=st["spec_rounds"], serially_run_trees=st["serial_trees"],
+               reference_frame_s_est=(st["prep_ms"] + st["setup_ms"] + st["iter0_ms"] +
+                                      (st["iters_ms"] / (iters - 1) * 99 if iters > 1 else 0)) / 1e3,
+               what="stereo3dmst's algorithm (segment forest c=5000 min_size 200, random plane labels, MST_PMS "
+                    "calls); reference_frame_s_est = host prep + first call + 99 later calls, both views")
+    if oracle:
+        from oracle import oracle as O
+        t = time.perf_counter()
+        O.stereo3dmst_pms(left, right, D, iters=1)
+        s = time.perf_counter() - t
+        out["oracle_one_call_both_views_s"] = s
+        out["oracle_note"] = ("oracle/sm_oracle_pms.c, 1 thread (the reference is serial), segmentation + BFS + AGD "
+                              "volume + one MST_PMS call per view")
+    return out
 
 
 def stream_frames(ctxs, steps, D, params, retire, split=True):
@@ -143,6 +169,65 @@ def spawn_ranks(n):
     return rc
 
 
+def rank_plan(args, world, rank):
+    """This rank's share of a frame: image size, its disparity range and views, and its reduce group
+    (stereomatch_amd.partition)."""
+    W, H = args.width, args.height
+    views, group, gsize, grank = 3, 0, world, rank  # this rank's views and its reduce group
+    emu = None
+    if args.emulate_rank:
+        er, en = (int(x) for x in args.emulate_rank.split("/"))
+        emu = sm.partition(args.disp, en, er, split_views=args.shard == "vd")
+        emu.update(rank=er, nranks=en)
+    if world == 1 or args.mode == "weak":
+        Dloc = args.disp
+        Dtot = Dloc * world if args.mode == "weak" else Dloc
+        dbeg = rank * Dloc
+    elif args.mode == "strong":
+        Dtot = args.disp
+        part = sm.partition(Dtot, world, rank, split_views=args.shard == "vd")
+        dbeg, Dloc, views = part["d0"], part["D"], part["views"]
+        group, gsize, grank = part["group"], part["group_size"], part["group_rank"]
+    else:  # batch
+        Dloc = Dtot = args.disp
+        dbeg = 0
+    Dtot_frame = Dloc if (args.mode == "batch" or world == 1) else Dtot
+    if emu:  # one rank's share of an N-rank frame: its views and slices of the total range
+        Dtot = Dtot_frame = args.disp
+        dbeg, Dloc, views = emu["d0"], emu["D"], emu["views"]
+    return dict(W=W, H=H, Dloc=Dloc, Dtot=Dtot, Dtot_frame=Dtot_frame, dbeg=dbeg, views=views, group=group, gsize=gsize,
+                grank=grank, emu=emu)
+
+
+def setup_comms(ctxs, world, rank, group, gsize, grank, mode, context_cls):
+    """One communicator per context (its reduce runs on that context's stream) and reduce group: the
+    group's rank 0 creates the unique id, every rank gathers all ids and joins its group leader's."""
+    if world == 1 or mode == "batch":
+        return
+    for c in ctxs:
+        ids = [None] * world
+        dist.all_gather_object(ids, context_cls.unique_id() if grank == 0 else None)
+        leader = next(r for r in range(world) if ids[r] is not None and (r // gsize if gsize < world else 0) == group)
+        c.comm_init(gsize, grank, ids[leader])
+
+
+class StubContext:
+    """--plan-only: a context that records its communicator set-up (no GPU)."""
+    _n = 0
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.comm = None
+
+    @staticmethod
+    def unique_id():
+        StubContext._n += 1
+        return ("uid-%d-%d" % (os.getpid(), StubContext._n)).encode().ljust(128, b"\0")
+
+    def comm_init(self, nranks, rank, uid):
+        self.comm = dict(nranks=nranks, rank=rank, uid=uid.rstrip(b"\0").decode())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -154,7 +239,6 @@ def main():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--disp", type=int, default=None,
                     help="disparities: total (N=1, strong, batch) or per rank (weak); default per config")
-    ap.add_argument("--cpu-slices", type=int, default=32)
     ap.add_argument("--cpu-slices-1t", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-io", action="store_true")
@@ -173,6 +257,11 @@ def main():
                     help="A/B: stream frames with sm_match_async instead of sm_match_begin/finish")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight (contexts on their own streams); 0 = 3, fewer where memory needs it")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="CPU check: start the ranks, print each rank's share and communicator set-up (stub "
+                         "contexts, no GPU), exit")
+    ap.add_argument("--no-pms", action="store_true", help="skip the MST_PMS (SM_AGG_PMS) timing leg")
+    ap.add_argument("--pms-iters", type=int, default=10, help="MST_PMS calls per view in the PMS timing leg")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -190,55 +279,33 @@ def main():
         args.width = 3840 if big else 1920
     if args.height is None:
         args.height = 2160 if big else 1200
+    if args.emulate_rank and world != 1:
+        print("bench.py: --emulate-rank runs on one GPU without torchrun", file=sys.stderr)
+        sys.exit(2)
     if args.disp is None:
-        args.disp = 256 if (big or (args.mode == "strong" and world > 1)) else 128
+        args.disp = 256 if (big or (args.mode == "strong" and world > 1) or args.emulate_rank) else 128
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-
-    W, H = args.width, args.height
-    views, group, gsize, grank = 3, 0, world, rank  # this rank's views and its reduce group
-    emu = None
-    if args.emulate_rank:
-        if world != 1:
-            print("bench.py: --emulate-rank runs on one GPU without torchrun", file=sys.stderr)
-            sys.exit(2)
-        er, en = (int(x) for x in args.emulate_rank.split("/"))
-        if args.disp is None or args.disp == 128:
-            args.disp = 256
-        emu = sm.partition(args.disp, en, er, split_views=args.shard == "vd")
-        emu.update(rank=er, nranks=en)
-    if world == 1 or args.mode == "weak":
-        Dloc = args.disp
-        Dtot = Dloc * world if args.mode == "weak" else Dloc
-        dbeg = rank * Dloc
-    elif args.mode == "strong":
-        Dtot = args.disp
-        part = sm.partition(Dtot, world, rank, split_views=args.shard == "vd")
-        dbeg, Dloc, views = part["d0"], part["D"], part["views"]
-        group, gsize, grank = part["group"], part["group_size"], part["group_rank"]
-    else:  # batch
-        Dloc = Dtot = args.disp
-        dbeg = 0
-    if args.mode == "batch" or world == 1:
-        Dtot_frame = Dloc
-    else:
-        Dtot_frame = Dtot
-    if emu:  # one rank's share of an N-rank frame: its views and slices of the total range
-        Dtot = Dtot_frame = args.disp
-        dbeg, Dloc, views = emu["d0"], emu["D"], emu["views"]
+    plan = rank_plan(args, world, rank)
+    W, H = plan["W"], plan["H"]
+    Dloc, Dtot, Dtot_frame, dbeg, views = plan["Dloc"], plan["Dtot"], plan["Dtot_frame"], plan["dbeg"], plan["views"]
+    group, gsize, grank, emu = plan["group"], plan["gsize"], plan["grank"], plan["emu"]
+    if args.plan_only:  # CPU: the rank's share and its communicator set-up against stub contexts
+        ctxs = [StubContext(rank) for _ in range(2)]
+        setup_comms(ctxs, world, rank, group, gsize, grank, args.mode, StubContext)
+        print(json.dumps(dict(rank=rank, world=world, plan={k: v for k, v in plan.items() if k != "emu"},
+                              comms=[c.comm for c in ctxs])), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # frames in flight: each context is a full pipeline on its own stream; frame i goes to context
     # i % n, so frame i+1's prep / MST / layout overlaps frame i's tree filter on the GPU
     per_ctx_gb = W * H * (64 * (1 if Dloc <= 64 else 2 if Dloc <= 128 else 4)) * 20 * 2 / 1e9 + W * H * 400 / 1e9
     inflight = args.inflight if args.inflight > 0 else max(1, min(3, int(200.0 // per_ctx_gb)))
     ctxs = [sm.Context(local) for _ in range(inflight)]
-    if world > 1 and args.mode != "batch":
-        for c in ctxs:  # one communicator per context (its reduce runs on its own stream) and group
-            ids = [None] * world
-            dist.all_gather_object(ids, sm.Context.unique_id() if grank == 0 else None)
-            leader = next(r for r in range(world) if ids[r] is not None and (r // gsize if gsize < world else 0) == group)
-            c.comm_init(gsize, grank, ids[leader])
+    setup_comms(ctxs, world, rank, group, gsize, grank, args.mode, sm.Context)
     pair_index = rank if args.mode == "batch" else 0
     left, right, _ = make_pair(W, H, Dtot_frame, index=pair_index)
     for c in ctxs:
@@ -348,11 +415,21 @@ def main():
     filt_ms = sum(v["ms"] for v in kall.values()) / diag_steps  # per frame, diagnostic pass
     filt_bytes = sum(v["voxels"] * v["bytes_per_voxel"] for v in kall.values()) / diag_steps
     traffic = None
+    traffic_src = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
             with open(tf) as f:
-                fam = json.load(f).get(dom, {})
+                pj = json.load(f)
+            fam = pj.get(dom, {})
+            import hashlib
+            with open(os.path.join(ROOT, "stereomatch_amd", "libstereomst.so"), "rb") as f:
+                cur = hashlib.sha256(f.read()).hexdigest()[:16]
+            built = pj.get("_build", "unrecorded")
+            traffic_src = dict(file="profiles/pmc_traffic.json", build=built, this_build="libstereomst.so sha256:" + cur,
+                               same_build=("sha256:" + cur) in built,
+                               note="PMC HBM bytes from a separate rocprofv3 --pmc run (tools/pmc_traffic.py), "
+                                    "not measured in this run")
             # PMC HBM bytes of the family per frame over the launches timed here (an empty bucket
             # launches nothing, so both count the same launches)
             if fam.get("hbm_bytes_per_frame") and d["launches"]:
@@ -368,7 +445,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak" if (args.mode in ("weak", "batch") or world == 1) else "strong",
+        "scaling": None if world == 1 else ("weak" if args.mode in ("weak", "batch") else "strong"),
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded slanted-plane stereo pair, tools/synth.py)",
@@ -376,9 +453,14 @@ def main():
                        W, H, Dtot_frame, CONFIG_NAMES.get((W, H, Dtot_frame), ""),
                        " = BASELINE C5's per-GPU pair" if args.mode == "batch" and (W, H, Dtot_frame) == (3840, 2160, 256) else "")
                    if world == 1 else
-                   "%dx%d D=%d, %s mode, %d disparities/rank%s%s" % (
-                       W, H, Dtot_frame, args.mode, Dloc, " of one view (view groups)" if views != 3 else "",
-                       " (BASELINE C4)" if (args.mode == "strong" and (W, H, Dtot_frame) == (1920, 1200, 256)) else
+                   "%dx%d D=%d, %s mode, %s%s" % (
+                       W, H, Dtot_frame, args.mode,
+                       ("2 view groups x %d disparity shards of %d slices: each rank one view, %d slices" % (gsize, Dloc, Dloc))
+                       if views != 3 else ("%d disparity shards of %d slices, both views per rank" % (world, Dloc))
+                       if args.mode == "strong" else "%d disparities/rank, both views" % Dloc,
+                       " (BASELINE C4 frame size; C4 names 32 disparities/GPU: here %s)" % (
+                           "view groups" if views != 3 else "%d/GPU" % Dloc)
+                       if (args.mode == "strong" and (W, H, Dtot_frame) == (1920, 1200, 256)) else
                        " (BASELINE C5: one pair per GPU)" if (args.mode == "batch" and (W, H, Dtot_frame) == (3840, 2160, 256))
                        else ""),
                    "W": W, "H": H, "D": Dtot_frame, "disparities_per_rank": Dloc,
@@ -389,7 +471,7 @@ def main():
                    "aggregator": args.aggregator,
                    "frames_in_flight": inflight},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "launches_per_step": d["launches"] / args.steps,
                      "alg_bytes_per_launch": dom_bytes / max(d["launches"], 1),
                      "avg_launch_ms": d["ms"] / max(d["launches"], 1),
@@ -420,7 +502,9 @@ def main():
         line["config"]["workload"] = "rank %d/%d of %dx%d D=%d: views %d, slices [%d, %d)" % (
             emu["rank"], emu["nranks"], W, H, Dtot_frame, views, dbeg, dbeg + Dloc)
     if rank == 0 and world == 1 and not args.no_cpu and not emu:
-        line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame, args.cpu_slices, args.cpu_slices_1t)
+        line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame, args.cpu_slices_1t)
+    if rank == 0 and world == 1 and not args.no_pms and not emu and args.aggregator == "tree":
+        line["pms"] = pms_leg(ctx, left, right, Dtot_frame, max(2, args.pms_iters), not args.no_cpu)
     if rank == 0:
         print(json.dumps(line), flush=True)
     for c in ctxs:

@@ -103,6 +103,8 @@ def lib():
         "sm_pms_glibc_random": ([ctypes.c_uint, ctypes.c_long, ctypes.c_long, vp], None),
         "sm_pms_init_labels": ([ci, ci, ci, vp], None),
         "sm_pms_levels": ([ci], ci),
+        "sm_reduce_candidates": ([vp, vp, vp, vp, ci, vp, ctypes.c_size_t], None),
+        "sm_reduce_finalize": ([vp, vp, ci, vp, vp, vp, ctypes.c_size_t], None),
         "sm_comm_unique_id": ([vp], ci),
         "sm_comm_init": ([vp, ci, ci, vp], ci),
         "sm_comm_destroy": ([vp], ci),
@@ -375,3 +377,29 @@ def pms_init_labels(W, H, max_disp):
 
 def pms_levels(max_disp):
     return lib().sm_pms_levels(int(max_disp))
+
+
+# -- the cross-rank WTA exchange rule (sm_reduce_rule.h), host form; the CPU tests' gloo exchange ---------
+def reduce_candidates(minc, gmin, idx, disp=None, sub=False):
+    """Per-pixel candidate of this rank after the MIN all-reduce of the minima: int32 index (or INT_MAX),
+    or with sub the uint64 (index << 32 | disparity bits) (or ~0)."""
+    minc = np.ascontiguousarray(minc, np.float64)
+    gmin = np.ascontiguousarray(gmin, np.float64)
+    idx = np.ascontiguousarray(idx, np.int32)
+    N = minc.size
+    cand = np.empty(N, np.uint64 if sub else np.int32)
+    d = np.ascontiguousarray(disp, np.float32) if sub else None
+    lib().sm_reduce_candidates(ptr(minc), ptr(gmin), ptr(idx), ptr(d), 1 if sub else 0, ptr(cand), N)
+    return cand
+
+
+def reduce_finalize(gmin, gcand, sub=False):
+    """The global (minimum, index, disparity) from the reduced minima and candidates."""
+    gmin = np.ascontiguousarray(gmin, np.float64)
+    gcand = np.ascontiguousarray(gcand, np.uint64 if sub else np.int32)
+    N = gmin.size
+    minc = np.empty(N, np.float64)
+    idx = np.empty(N, np.int32)
+    disp = np.empty(N, np.float32)
+    lib().sm_reduce_finalize(ptr(gmin), ptr(gcand), 1 if sub else 0, ptr(minc), ptr(idx), ptr(disp), N)
+    return minc, idx, disp

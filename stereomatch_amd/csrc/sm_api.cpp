@@ -23,6 +23,7 @@
 #include "sm_launch.h"
 #include "sm_layout_gpu.h"
 #include "sm_pms.h"
+#include "sm_reduce_rule.h"
 #include "sm_segment.h"
 #include "sm_tables.inc"
 
@@ -1620,6 +1621,8 @@ void sm_destroy(sm_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
+    if (ctx->st_tree) (void)hipStreamSynchronize(ctx->st_tree);  // tree kernels may still run there
+    if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamSynchronize(ctx->st2);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut, &ctx->post_mask, &ctx->post_scratch,
                      &ctx->gf_planes, &ctx->gf_means, &ctx->gf_pl, &ctx->gf_tmp, &ctx->gf_stats[0], &ctx->gf_stats[1],
@@ -1672,12 +1675,14 @@ const char* sm_last_error(const sm_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 
 sm_status sm_upload_images(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_upload_images: a call begun with sm_match_begin is not finished (sm_match_finish)");
     HIPC(hipSetDevice(ctx->device));
     return upload(ctx, l, r, W, H, stride);
 }
 
 sm_status sm_upload_cost_volumes(sm_ctx* ctx, const float* left_vol, const float* right_vol, int W, int H, int D) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_upload_cost_volumes: a call begun with sm_match_begin is not finished (sm_match_finish)");
     if (!left_vol || !right_vol) return fail(ctx, SM_ERR_ARG, "null volume");
     if (W < 1 || H < 1 || D < 1 || (long long)W * H > (1ll << 30)) return fail(ctx, SM_ERR_ARG, "bad volume geometry");
     HIPC(hipSetDevice(ctx->device));
@@ -1742,7 +1747,9 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
         return SM_OK;
     }
     if (p->aggregator == SM_AGG_GUIDED) {  // no tree: stage times MST / layout / down read 0
-        ctx->sub = false;
+        // with a communicator the exchange must carry the guided WTA's subpixel disparities (the 64-bit
+        // candidate path); the int32 path would overwrite them with the index
+        ctx->sub = (p->post & SM_POST_SUBPIXEL) != 0;
         ctx->nfev = ctx->nsev = 0;
         ctx->fam.clear();
         ctx->fam_vox.clear();
@@ -1800,6 +1807,7 @@ sm_status sm_match_async(sm_ctx* ctx, int D, const sm_params* p) {
 
 sm_status sm_synchronize(sm_ctx* ctx) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_synchronize: a call begun with sm_match_begin is not finished (sm_match_finish)");
     HIPC(hipSetDevice(ctx->device));
     HIPC(hipStreamSynchronize(ctx->st));
     CHECK(check_device_error(ctx));
@@ -1821,6 +1829,7 @@ sm_status sm_synchronize(sm_ctx* ctx) {
 
 sm_status sm_download_results(sm_ctx* ctx, float* ld, float* rd, int32_t* li, int32_t* ri, double* lm, double* rm) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_download_results: a call begun with sm_match_begin is not finished (sm_match_finish)");
     HIPC(hipSetDevice(ctx->device));
     const size_t N = (size_t)ctx->W * ctx->H;
     void* outs[2][3] = {{ld, li, lm}, {rd, ri, rm}};
@@ -1845,6 +1854,7 @@ sm_status sm_match(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H
 sm_status sm_cost_volume(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, int d0, int D,
                          float* lvol, float* rvol) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_cost_volume: a call begun with sm_match_begin is not finished (sm_match_finish)");
     if (D < 1 || d0 < 0) return fail(ctx, SM_ERR_ARG, "bad disparity range");
     HIPC(hipSetDevice(ctx->device));
     CHECK(upload(ctx, l, r, W, H, stride));
@@ -1863,6 +1873,7 @@ sm_status sm_cost_volume(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W,
 sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int stride, const sm_params* p, uint8_t* mask,
                           int32_t* parent_pix, int32_t* subtree_size, int32_t* slot_of_pix, int32_t* ntrees) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_build_tree_p: a call begun with sm_match_begin is not finished (sm_match_finish)");
     if (p && (std::isnan(p->c) || p->c < 0)) return fail(ctx, SM_ERR_ARG, "c must be >= 0 or +INFINITY");
     HIPC(hipSetDevice(ctx->device));
     CHECK(upload(ctx, bgr, bgr, W, H, stride));
@@ -1913,6 +1924,7 @@ sm_status sm_aggregate_debug(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, in
 sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, const sm_params* p,
                                int view, int d0, int D, double* A_up, double* A) {
     if (!ctx) return SM_ERR_ARG;
+    if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_aggregate_debug_p: a call begun with sm_match_begin is not finished (sm_match_finish)");
     if (p && (std::isnan(p->c) || p->c < 0)) return fail(ctx, SM_ERR_ARG, "c must be >= 0 or +INFINITY");
     if (view != 0 && view != 1) return fail(ctx, SM_ERR_ARG, "view must be 0 or 1");
     ctx->use_vol = false;  // AGD costs
@@ -1982,6 +1994,33 @@ sm_status sm_get_filter_stats(sm_ctx* ctx, sm_filter_stats* out) {
     if (!ctx || !out) return SM_ERR_ARG;
     *out = ctx->stats;
     return SM_OK;
+}
+
+// Host form of the exchange rule (sm_reduce_rule.h), library-internal: the CPU tests run the gloo
+// exchange through these, the GPU path through k_cand / k_finalize.  disp may be NULL when !sub.
+void sm_reduce_candidates(const double* minc, const double* gmin, const int32_t* idx, const float* disp, int sub, void* cand,
+                          size_t N) {
+    for (size_t i = 0; i < N; ++i) {
+        if (sub) {
+            uint32_t bits;
+            memcpy(&bits, disp + i, 4);
+            static_cast<unsigned long long*>(cand)[i] = sm_rule_cand64(minc[i], gmin[i], idx[i], bits);
+        } else {
+            static_cast<int32_t*>(cand)[i] = sm_rule_cand32(minc[i], gmin[i], idx[i]);
+        }
+    }
+}
+
+void sm_reduce_finalize(const double* gmin, const void* gcand, int sub, double* minc, int32_t* idx, float* disp, size_t N) {
+    for (size_t i = 0; i < N; ++i) {
+        if (sub) {
+            uint32_t bits;
+            sm_rule_finalize64(gmin[i], static_cast<const unsigned long long*>(gcand)[i], minc[i], idx[i], bits);
+            memcpy(disp + i, &bits, 4);
+        } else {
+            sm_rule_finalize32(gmin[i], static_cast<const int32_t*>(gcand)[i], minc[i], idx[i], disp[i]);
+        }
+    }
 }
 
 sm_status sm_download_labels(sm_ctx* ctx, float* left_abc, float* right_abc) {

@@ -285,7 +285,7 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 template <int SPL>
 struct UpCfg {
     static constexpr int G = SPL == 1 ? UP_G1 : SPL == 2 ? UP_G2 : UP_G4;  // nodes per group (helper registers)
-    static constexpr int NS = SPL == 1 ? UP_NS1 : SPL == 2 ? UP_NS2 : UP_NS4;  // LDS slots (~140 KB)
+    static constexpr int NS = SPL == 1 ? UP_NS1 : SPL == 2 ? UP_NS2 : UP_NS4;  // LDS slots (the ring: static_assert below)
 };
 
 struct UpNodeS {
@@ -325,6 +325,12 @@ struct UpRing {
     double slut[SM_NUM_W + 1];
     float atab[SM_MAX_W + 1];  // AGD colour term by integer L1 (helpers compute the cost rows)
 };
+// LDS budget of k_up_chain (gfx950: 160 KB per workgroup): the ring, the pieces' guess row and a few
+// words of scalars.  UP_G*/UP_NS* are A/B macros; a geometry that does not fit fails here, not at launch.
+#define SM_LDS_BYTES (160 * 1024)
+static_assert(sizeof(UpRing<1>) + 64 * 1 * 8 + 64 <= SM_LDS_BYTES, "UpRing<1> (UP_G1 x UP_NS1) exceeds the LDS");
+static_assert(sizeof(UpRing<2>) + 64 * 2 * 8 + 64 <= SM_LDS_BYTES, "UpRing<2> (UP_G2 x UP_NS2) exceeds the LDS");
+static_assert(sizeof(UpRing<4>) + 64 * 4 * 8 + 64 <= SM_LDS_BYTES, "UpRing<4> (UP_G4 x UP_NS4) exceeds the LDS");
 
 // where the up chain's cost rows come from: computed by the helpers from the image records (the
 // AGD cost, PatchMatchStereoGPU.cu:1482-1550), or read from the f32 rows k_vol_rows filled
@@ -1007,6 +1013,9 @@ struct RepCfg {
     static constexpr int CHR = (BB + NSW - 1) / NSW;  // nodes staged per wave and pass
     static_assert(BB >= 4, "repair pass");
 };
+// the repair batch follows the ring's size; its value at the shipped geometries is pinned here, so a
+// ring sweep that changes it is visible (SPL=1 4 x 18 ring -> 16-node passes)
+static_assert(UP_G1 != 4 || UP_NS1 != 18 || RepCfg<1>::BB == 16, "RepCfg<1>::BB changed with the SPL=1 ring");
 
 // one wave stages nodes k0 .. k0+nb-1 (node k = slot top - k; metadata in mv) into rn[k - kb]
 template <int SPL, bool AGD, int CHR>
@@ -1509,6 +1518,9 @@ struct DownRing {
     double slut[SM_NUM_W + 1];
     double s2lut[SM_NUM_W + 1];  // [SM_NUM_W]: S = 0, S2 = 1 (absent children; segment mode's virtual edges)
 };
+static_assert(sizeof(DownRing<1>) + 64 * 1 * 8 + 64 <= SM_LDS_BYTES, "DownRing<1> exceeds the LDS");
+static_assert(sizeof(DownRing<2>) + 64 * 2 * 8 + 64 <= SM_LDS_BYTES, "DownRing<2> exceeds the LDS");
+static_assert(sizeof(DownRing<4>) + 64 * 4 * 8 + 64 <= SM_LDS_BYTES, "DownRing<4> exceeds the LDS");
 
 template <int SPL, int NN>
 __device__ __forceinline__ void down_group(DownSlot<SPL>& sl, int k0, int e0, double (&x)[Split<SPL>::CS]) {

@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "sm_common.h"
+#include "sm_reduce_rule.h"
 
 #define WAVE 64
 
@@ -675,35 +676,29 @@ __global__ void k_crelabel(CPair P, int rnd) {
 __global__ void k_cand(const double* __restrict__ minc, const double* __restrict__ gmin, const int32_t* __restrict__ idx,
                        int32_t* __restrict__ cand, size_t N) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < N) cand[i] = minc[i] == gmin[i] ? idx[i] : 0x7fffffff;
+    if (i < N) cand[i] = sm_rule_cand32(minc[i], gmin[i], idx[i]);
 }
 
 __global__ void k_finalize(const double* __restrict__ gmin, const int32_t* __restrict__ gidx, double* __restrict__ minc,
                            int32_t* __restrict__ idx, float* __restrict__ disp, size_t N) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < N) {
-        minc[i] = gmin[i];
-        idx[i] = gidx[i];
-        disp[i] = (float)gidx[i];
-    }
+    if (i < N) sm_rule_finalize32(gmin[i], gidx[i], minc[i], idx[i], disp[i]);
 }
 
 // subpixel variant: the candidate carries the rank's subpixel disparity in its low word
 __global__ void k_cand64(const double* __restrict__ minc, const double* __restrict__ gmin, const int32_t* __restrict__ idx,
                          const float* __restrict__ disp, unsigned long long* __restrict__ cand, size_t N) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < N)
-        cand[i] = minc[i] == gmin[i] ? ((unsigned long long)(uint32_t)idx[i] << 32) | __float_as_uint(disp[i]) : ~0ull;
+    if (i < N) cand[i] = sm_rule_cand64(minc[i], gmin[i], idx[i], __float_as_uint(disp[i]));
 }
 
 __global__ void k_finalize64(const double* __restrict__ gmin, const unsigned long long* __restrict__ gkey,
                              double* __restrict__ minc, int32_t* __restrict__ idx, float* __restrict__ disp, size_t N) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < N) {
-        const unsigned long long k = gkey[i];
-        minc[i] = gmin[i];
-        idx[i] = (int32_t)(k >> 32);
-        disp[i] = __uint_as_float((uint32_t)k);
+        uint32_t bits;
+        sm_rule_finalize64(gmin[i], gkey[i], minc[i], idx[i], bits);
+        disp[i] = __uint_as_float(bits);
     }
 }
 

@@ -1,11 +1,12 @@
-"""World-size-2 gloo test of the D-sharded WTA exchange (sm_api.cpp stage_reduce).
+"""gloo tests (world sizes 2-4) of the D-sharded WTA exchange (sm_api.cpp stage_reduce).
 
 Each rank filters its contiguous disparity shard (the oracle stands in for the per-rank GPU
 result, which the -m gpu tests pin to it bit-exactly), then runs the library's two-step
-exchange on CPU tensors with gloo: all-reduce MIN of the fp64 minimum cost, candidate = own
-global index where the rank's cost equals the global minimum (else INT_MAX, as k_cand), and
-all-reduce MIN of the candidates.  Every rank must then hold exactly the unsharded strict-<
-first minimum (PatchMatchStereoGPU.cu:1700-1717, Stereo3DMST.cpp:177)."""
+exchange with gloo in place of RCCL: all-reduce MIN of the fp64 minimum cost, the library's own
+candidate rule (sm_reduce_candidates: the host form of k_cand / k_cand64, sm_reduce_rule.h), an
+all-reduce MIN of the candidates, and the library's finalize (sm_reduce_finalize).  Every rank must
+then hold exactly the unsharded strict-< first minimum (PatchMatchStereoGPU.cu:1700-1717,
+Stereo3DMST.cpp:177)."""
 import os
 import socket
 import sys
@@ -26,13 +27,26 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _exchange(minc, idx):
-    """The library's cross-rank reduce (sm_api.cpp stage_reduce + k_cand + k_finalize)."""
+def _exchange(minc, idx, group=None, disp=None):
+    """The library's cross-rank reduce (sm_api.cpp stage_reduce) with gloo in place of RCCL: MIN of the
+    minima, the library's candidate rule, MIN of the candidates, the library's finalize.  uint64
+    candidates (subpixel) are reduced as int64 with the top bit flipped (an order-preserving map: gloo
+    has no unsigned MIN; RCCL reduces ncclUint64)."""
+    from stereomatch_amd import _lib as L
+    sub = disp is not None
     gmin = torch.from_numpy(minc.copy())
-    dist.all_reduce(gmin, op=dist.ReduceOp.MIN)
-    cand = torch.where(torch.from_numpy(minc) == gmin, torch.from_numpy(idx), torch.tensor(0x7FFFFFFF, dtype=torch.int32))
-    dist.all_reduce(cand, op=dist.ReduceOp.MIN)
-    return gmin.numpy(), cand.numpy()
+    dist.all_reduce(gmin, op=dist.ReduceOp.MIN, group=group)
+    cand = L.reduce_candidates(minc, gmin.numpy(), idx, disp, sub)
+    if sub:
+        c = torch.from_numpy((cand ^ np.uint64(1 << 63)).view(np.int64).copy())
+        dist.all_reduce(c, op=dist.ReduceOp.MIN, group=group)
+        gc = c.numpy().view(np.uint64) ^ np.uint64(1 << 63)
+    else:
+        c = torch.from_numpy(cand.copy())
+        dist.all_reduce(c, op=dist.ReduceOp.MIN, group=group)
+        gc = c.numpy()
+    m, i, d = L.reduce_finalize(gmin.numpy(), gc, sub)
+    return (m, i, d) if sub else (m, i)
 
 
 def _worker(rank, world, port, W, H, D, out_q):
@@ -111,12 +125,8 @@ def _worker_vd(rank, world, port, W, H, D, out_q):
         tree = O.build_tree(left if v == "left" else right)
         lv, rv = O.cost_agd(left, right, d0, d0 + Dl)
         tf = O.tree_filter(W, H, tree, lv if v == "left" else rv, d0, True, False, 2)
-        gmin = torch.from_numpy(tf["minc"].copy())
-        dist.all_reduce(gmin, op=dist.ReduceOp.MIN, group=grp)
-        cand = torch.where(torch.from_numpy(tf["minc"]) == gmin, torch.from_numpy(tf["idx"]),
-                           torch.tensor(0x7FFFFFFF, dtype=torch.int32))
-        dist.all_reduce(cand, op=dist.ReduceOp.MIN, group=grp)
-        out_q.put((rank, (v, gmin.numpy().tolist(), cand.numpy().tolist())))
+        gmin, gidx = _exchange(tf["minc"], tf["idx"], group=grp)
+        out_q.put((rank, (v, gmin.tolist(), gidx.tolist())))
     finally:
         dist.destroy_process_group()
 
@@ -163,3 +173,52 @@ def test_partition_plans():
     assert partition(256, 8, 5, split_views=False) == dict(views=3, d0=160, D=32, group=0, group_size=8, group_rank=5)
     # one view of more than 128 slices per rank: both views instead (N = 2 at D = 256)
     assert [partition(256, 2, r)["views"] for r in range(2)] == [3, 3]
+
+
+def _worker_sub(rank, world, port, W, H, D, out_q):
+    """Subpixel exchange: each rank's winner carries its disparity (here d - 0.25 * (d % 3), a stand-in
+    for the parabola); the lowest index among the ranks holding the minimum must bring its own."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from stereomatch_amd import shard_range
+        from tools.synth import make_pair
+        left, right, _ = make_pair(W, H, D, index=9)
+        d0, Dl = shard_range(D, world, rank)
+        tree = O.build_tree(left)
+        lv, _ = O.cost_agd(left, right, d0, d0 + Dl)
+        tf = O.tree_filter(W, H, tree, lv, d0, True, False, 2)
+        disp = (tf["idx"] - 0.25 * (tf["idx"] % 3)).astype(np.float32)
+        m, i, d = _exchange(tf["minc"], tf["idx"], disp=disp)
+        out_q.put((rank, (m.tolist(), i.tolist(), d.tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_subpixel_exchange_equals_unsharded(world):
+    from oracle import oracle as O
+    from tools.synth import make_pair
+    W, H, D = 36, 22, 17
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_sub, args=(r, world, port, W, H, D, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    left, right, _ = make_pair(W, H, D, index=9)
+    tree = O.build_tree(left)
+    lv, _ = O.cost_agd(left, right, 0, D)
+    ref = O.tree_filter(W, H, tree, lv, 0, True, False, 2)
+    rdisp = (ref["idx"] - 0.25 * (ref["idx"] % 3)).astype(np.float32)
+    for r in range(world):
+        m, i, d = got[r]
+        np.testing.assert_array_equal(np.array(i, np.int32), ref["idx"])
+        np.testing.assert_array_equal(np.array(m, np.float64), ref["minc"])
+        np.testing.assert_array_equal(np.array(d, np.float32), rdisp)

@@ -917,6 +917,15 @@ def test_split_calls_interleaved_bitexact():
         with pytest.raises(StereoMSTError) as e:
             ctxs[1].match_begin(Ds[1])
         assert e.value.status == SM_ERR_STATE
+        # every entry point that would read or replace the begun call's state refuses until its finish
+        l0, r0, _ = pairs[0]
+        for call in (ctxs[0].synchronize, ctxs[0].results, lambda: ctxs[0].upload(l0, r0),
+                     lambda: ctxs[0].cost_volume(l0, r0, 0, 8), lambda: ctxs[0].build_tree(l0),
+                     lambda: ctxs[0].aggregate_debug(l0, r0, 0, 0, 4),
+                     lambda: ctxs[0].upload_cost_volumes(np.zeros((2, 160, 256), np.float32), np.zeros((2, 160, 256), np.float32))):
+            with pytest.raises(StereoMSTError) as e:
+                call()
+            assert e.value.status == SM_ERR_STATE
         ctxs[0].match_finish()
         ctxs[1].match_finish()
         with pytest.raises(StereoMSTError) as e:
@@ -932,3 +941,23 @@ def test_split_calls_interleaved_bitexact():
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_guided_subpixel_with_one_rank_comm():
+    """SM_AGG_GUIDED + SM_POST_SUBPIXEL on a context with a (one-rank) communicator: the exchange carries
+    the guided WTA's subpixel disparities (64-bit candidates), so the result equals the call without one."""
+    import stereomatch_amd as sm
+    left, right, _ = make_pair(160, 96, 32, index=2)
+    p = sm.default_params(aggregator=sm.SM_AGG_GUIDED, post=sm.SM_POST_SUBPIXEL, disp_total=32)
+    ctx = sm.Context(0)
+    try:
+        ref = ctx.match(left, right, 32, p)
+        ctx.comm_init(1, 0, sm.Context.unique_id())
+        out = ctx.match(left, right, 32, p)
+        for v in ("left", "right"):
+            np.testing.assert_array_equal(out[v]["disp"], ref[v]["disp"])
+            np.testing.assert_array_equal(out[v]["idx"], ref[v]["idx"])
+            assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"].ravel()))
+        assert not np.array_equal(out["left"]["disp"], out["left"]["idx"].astype(np.float32))  # subpixel survived
+    finally:
+        ctx.close()

@@ -12,6 +12,7 @@ beside the families as a sanity check of the units on this box.
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
 
@@ -33,6 +34,19 @@ def frames_of(d):
 def family(name):
     base = name.split("(")[0].replace("void ", "").split("<")[0].strip()
     return base if base in FAMILIES else None
+
+
+def lib_build_id():
+    """sha256 (16 hex) of the library the profiled run loaded, and the time of this summary."""
+    import hashlib
+    import time
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "stereomatch_amd", "libstereomst.so")
+    try:
+        with open(path, "rb") as f:
+            h = hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        h = "missing"
+    return "libstereomst.so sha256:%s %s" % (h, time.strftime("%Y-%m-%d %H:%M"))
 
 
 def load(d, counter):
@@ -58,7 +72,8 @@ def main():
     fetch, nf = load(fdir, "FETCH_SIZE")
     write, nw = load(wdir, "WRITE_SIZE")
     res = {"_note": "HBM bytes per frame and per launch from rocprofv3 FETCH_SIZE (x2, gfx950 16-B/lane "
-                    "correction) + WRITE_SIZE over %d frames; see tools/pmc_traffic.py" % frames}
+                    "correction) + WRITE_SIZE over %d frames; see tools/pmc_traffic.py" % frames,
+           "_build": lib_build_id()}
     for fam in FAMILIES:
         if fam not in fetch and fam not in write:
             continue
