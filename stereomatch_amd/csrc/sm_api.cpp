@@ -45,6 +45,33 @@ struct DevBuf {
     size_t n = 0;
 };
 
+// pinned host array (segment mode's weight / mask copies: the copies run asynchronously to the host
+// thread and read or fill the memory when the stream reaches them)
+template <class T>
+struct PinnedVec {
+    T* p = nullptr;
+    size_t n = 0;
+    PinnedVec() = default;
+    PinnedVec(const PinnedVec&) = delete;
+    PinnedVec& operator=(const PinnedVec&) = delete;
+    ~PinnedVec() {
+        if (p) (void)hipHostFree(p);
+    }
+    bool resize(size_t m) {  // capacity; contents undefined
+        if (p && m <= n) return true;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipHostMalloc((void**)&p, (m ? m : 1) * sizeof(T)) != hipSuccess) return false;
+        n = m;
+        return true;
+    }
+    T* data() { return p; }
+    const T* data() const { return p; }
+    T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
+};
+
 // MST_PMS state of one view (SM_AGG_PMS, sm_pms.hip): the host forest and schedule, their device
 // copies, labels, aggregation rows, cost rows and the speculation scratch
 struct PmsState {
@@ -95,8 +122,14 @@ struct sm_ctx {
     bool seg = false;  // the current tree is a segment forest (layout reads fwR / fwD)
     bool sub = false;  // the current call's WTA carries subpixel disparities (SM_POST_SUBPIXEL)
     int seg_trees[2] = {0, 0};
-    std::vector<uint16_t> h_w[2][2], h_fw[2][2];
-    std::vector<uint8_t> h_m[2][2];
+    PinnedVec<uint16_t> h_w[2][2], h_fw[2][2];
+    PinnedVec<uint8_t> h_m[2][2];
+    // asynchronous segment mode (sm_match_begin): the host segmentation runs on a worker thread that
+    // waits for the weights' copy (ev_segw), uploads the forest and enqueues the layout; sm_match_finish
+    // joins it
+    std::thread seg_worker;
+    sm_status seg_status = SM_OK;
+    hipEvent_t ev_segw = nullptr;
     size_t rec_pad_n[2] = {0, 0};  // pixel count the record pads were zeroed for
     size_t rec_pad_z[2] = {0, 0};  // pad length (records) they were zeroed with
     // records of padding on each side of the image records: the walkers read the matched image
@@ -350,10 +383,11 @@ sm_status stage_mst(sm_ctx* ctx, int views);
 
 // Segment mode: the reference's order-dependent Felzenszwalb segmentation + min-size merge on the host
 // (sm_segment.cpp), from the GPU's edge weights; the forest, linked into one tree by S = 0 virtual
-// edges, goes back as the MST masks and the layout's weights.  Replaces stage_mst.
-sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size) {
-    const int W = ctx->W, H = ctx->H;
-    const size_t N = (size_t)W * H;
+// edges, goes back as the MST masks and the layout's weights.  Replaces stage_mst.  Three parts:
+// the weights' copy to pinned host memory (recorded by ev_segw), the host segmentation of the views
+// (one thread each), the forest's copy back.
+sm_status segment_download(sm_ctx* ctx, int views) {
+    const size_t N = (size_t)ctx->W * ctx->H;
     const ViewSet vs(views);
     for (int i = 0; i < vs.n; ++i) {
         const int v = vs.v[i];
@@ -361,16 +395,21 @@ sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size) {
         CHECK(ensure(ctx, ctx->mD[v], N));
         CHECK(ensure(ctx, ctx->fwR[v], N * 2));
         CHECK(ensure(ctx, ctx->fwD[v], N * 2));
-        for (int k = 0; k < 2; ++k) {
-            ctx->h_w[v][k].resize(N);
-            ctx->h_fw[v][k].resize(N);
-            ctx->h_m[v][k].resize(N);
-        }
+        for (int k = 0; k < 2; ++k)
+            if (!ctx->h_w[v][k].resize(N) || !ctx->h_fw[v][k].resize(N) || !ctx->h_m[v][k].resize(N))
+                return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
         HIPC(hipMemcpyAsync(ctx->h_w[v][0].data(), ctx->wR[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
         HIPC(hipMemcpyAsync(ctx->h_w[v][1].data(), ctx->wD[v].p, N * 2, hipMemcpyDeviceToHost, ctx->st));
     }
     CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
-    HIPC(hipStreamSynchronize(ctx->st));
+    HIPC(hipEventRecord(ctx->ev_segw, ctx->st));
+    return SM_OK;
+}
+
+sm_status segment_host(sm_ctx* ctx, int views, float c, int min_size) {
+    const int W = ctx->W, H = ctx->H;
+    const ViewSet vs(views);
+    HIPC(hipEventSynchronize(ctx->ev_segw));
     std::thread other;
     auto run = [ctx, W, H, c, min_size](int v) {
         ctx->seg_trees[v] = sm_segment_forest(ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), W, H, c, min_size,
@@ -380,6 +419,12 @@ sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size) {
     if (vs.n > 1) other = std::thread(run, vs.v[1]);
     run(vs.v[0]);
     if (other.joinable()) other.join();
+    return SM_OK;
+}
+
+sm_status segment_upload(sm_ctx* ctx, int views) {
+    const size_t N = (size_t)ctx->W * ctx->H;
+    const ViewSet vs(views);
     for (int i = 0; i < vs.n; ++i) {
         const int v = vs.v[i];
         HIPC(hipMemcpyAsync(ctx->mR[v].p, ctx->h_m[v][0].data(), N, hipMemcpyHostToDevice, ctx->st));
@@ -388,10 +433,23 @@ sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size) {
         HIPC(hipMemcpyAsync(ctx->fwD[v].p, ctx->h_fw[v][1].data(), N * 2, hipMemcpyHostToDevice, ctx->st));
     }
     HIPC(hipMemsetAsync(ctx->mst_ok.p, 1, sizeof(int), ctx->st));
+    return SM_OK;
+}
+
+sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size) {
+    CHECK(segment_download(ctx, views));
+    CHECK(segment_host(ctx, views, c, min_size));
+    CHECK(segment_upload(ctx, views));
     HIPC(hipStreamSynchronize(ctx->st));  // the host buffers are reused by the next call
     ctx->mst_pend.active = false;
     ctx->seg = true;
     return SM_OK;
+}
+
+// SM_SEG_SYNC=1: segment mode's host segmentation inside sm_match_begin (A/B of the worker thread)
+bool seg_sync() {
+    static const bool s = getenv("SM_SEG_SYNC") != nullptr;
+    return s;
 }
 
 // tree of the call: the MST (Boruvka) or, for finite c, the segment forest
@@ -1601,7 +1659,11 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
     }
     for (auto& e : ctx->ev)  // stage-boundary timing events
         if (hipEventCreateWithFlags(&e, timing_event_flags()) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
-    if (hipEventCreateWithFlags(&ctx->ev_layout, hipEventDisableTiming) != hipSuccess) { delete ctx; return SM_ERR_HIP; }
+    if (hipEventCreateWithFlags(&ctx->ev_layout, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ev_segw, hipEventDisableTiming) != hipSuccess) {
+        delete ctx;
+        return SM_ERR_HIP;
+    }
     // tables: S/S2 (correctly rounded, tools/gen_tables.py) and the AGD colour term
     std::vector<float> atab(SM_MAX_W + 1);
     for (int i = 0; i <= SM_MAX_W; ++i) atab[i] = agd_color_term(i);
@@ -1620,6 +1682,7 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
 void sm_destroy(sm_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->seg_worker.joinable()) ctx->seg_worker.join();  // a begun segment-mode call's host worker
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     if (ctx->st_tree) (void)hipStreamSynchronize(ctx->st_tree);  // tree kernels may still run there
     if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamSynchronize(ctx->st2);
@@ -1637,6 +1700,7 @@ void sm_destroy(sm_ctx* ctx) {
     }
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->ev_layout) (void)hipEventDestroy(ctx->ev_layout);
+    if (ctx->ev_segw) (void)hipEventDestroy(ctx->ev_segw);
     for (auto e : ctx->fev) (void)hipEventDestroy(e);
     for (auto e : ctx->sev) (void)hipEventDestroy(e);
     for (int v = 0; v < 2; ++v) {
@@ -1766,6 +1830,32 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
         ctx->pending = 2;
         return SM_OK;
     }
+    if (!std::isinf(p->c) && !ts.main && !seg_sync()) {
+        // segment mode: the host segmentation on a worker thread, so begin returns at once and the
+        // caller's other contexts keep the GPU busy; the worker uploads the forest and enqueues the
+        // layout on this context's stream, and sm_match_finish joins it before using the layout
+        CHECK(segment_download(ctx, ctx->views));
+        ctx->mst_pend.active = false;
+        ctx->seg = true;
+        const int views = ctx->views;
+        const float c = p->c;
+        const int min_size = p->min_size;
+        ctx->seg_status = SM_OK;
+        ctx->seg_worker = std::thread([ctx, views, c, min_size] {
+            auto work = [&]() -> sm_status {
+                HIPC(hipSetDevice(ctx->device));
+                CHECK(segment_host(ctx, views, c, min_size));
+                CHECK(segment_upload(ctx, views));
+                HIPC(hipEventRecord(ctx->ev[2], ctx->st));
+                return stage_layout_enqueue(ctx, views);
+            };
+            ctx->seg_status = work();
+        });
+        ctx->pending = 1;
+        ctx->pend_D = D;
+        ctx->pend_p = *p;
+        return SM_OK;
+    }
     CHECK(stage_tree(ctx, ctx->views, p));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
     CHECK(stage_layout_enqueue(ctx, ctx->views));
@@ -1790,6 +1880,10 @@ sm_status sm_match_finish(sm_ctx* ctx) {
     const sm_params* p = &ctx->pend_p;
     const int D = ctx->pend_D;
     const CallRange cr = call_range(p, D);
+    if (ctx->seg_worker.joinable()) {  // the asynchronous segment-mode tree (sm_match_begin)
+        ctx->seg_worker.join();
+        CHECK(ctx->seg_status);
+    }
     CHECK(stage_layout_finish(ctx, ctx->views));
     HIPC(hipEventRecord(ctx->ev[3], ctx->st));
     CHECK(stage_filter(ctx, cr.D, cr.d0, ctx->views, false, &cr.w));
