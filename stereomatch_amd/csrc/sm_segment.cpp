@@ -14,7 +14,10 @@
 //
 // The order-dependent segmentation is inherently serial (each decision depends on every earlier
 // one), so it runs here, on the host: a stable counting sort of the edge ids by weight (the emission
-// order is ascending (a, b), so stable by w == std::sort's (w, a, b)), then two union-find sweeps.
+// order is ascending (a, b), so stable by w == std::sort's (w, a, b)), then two union-find sweeps,
+// the second over the first's rejected edges only.  The sweep is bound by the latency of its random
+// node visits: 8-byte nodes, a weight read off the bucket instead of the pixel, and prefetches of the
+// nodes (and their parents) of the edges a few places ahead.
 //
 // GPU embedding.  The tree layout and filter engine work on one spanning tree rooted at pixel 0.
 // For every tree T other than pixel 0's, its root r_T (the first pixel of T in raster order) gets a
@@ -35,11 +38,10 @@
 
 namespace {
 
-// union-find node: parent, component size and threshold together (one cache line per visit: the
-// sorted edge order makes every visit a random access)
+// union-find node: parent and component size (8 B: the nodes of a 1920x1200 view stay in one CCD's
+// L3 together with the last-join weights); roots have parent == self
 struct Node {
     uint32_t parent, size;
-    double thr;
 };
 
 uint32_t find(Node* u, uint32_t x) {
@@ -77,33 +79,53 @@ int sm_segment_forest(const uint16_t* wR, const uint16_t* wD, int W, int H, floa
             if (x + 1 < (uint32_t)W) order[count[wR[p]]++] = 2u * p;
             if (y + 1 < (uint32_t)H) order[count[wD[p]]++] = 2u * p + 1u;
         }
+    // count[w] is now the end of weight w's bucket: the sweep reads an edge's weight off its bucket
     const uint32_t step[2] = {1u, (uint32_t)W};
-    auto weight = [wR, wD](uint32_t e) { return (e & 1u) ? wD[e >> 1] : wR[e >> 1]; };
 
     std::memset(mR, 0, N);
     std::memset(mD, 0, N);
     uint8_t* mk[2] = {mR, mD};
     std::vector<Node> nodes(N);
+    std::vector<uint16_t> wl(N, 0);  // per root: the weight of its last join (thr = wl + c/size)
     Node* u = nodes.data();
-    const double thr0 = (double)(c / 1.0f);
-    for (uint32_t i = 0; i < N; ++i) u[i] = Node{i, 1u, thr0};
-    uint32_t sets = N;
+    for (uint32_t i = 0; i < N; ++i) u[i] = Node{i, 1u};
+    // Threshold of a root: w_last + c/size, the reference's w + THRESHOLD(size, c) set at the root's
+    // last join (each join sets it from the joined size; a singleton's is 0 + c/1).  Edges rejected
+    // here are the only ones the min-size pass can join (an edge whose ends were one component stays
+    // inside one), so they are kept, in order, for it.
+    std::vector<uint32_t> rejected;
+    rejected.reserve(E / 8);
+    uint32_t sets = N, w = 0;
+    constexpr uint32_t PF = 16;  // prefetch distance (edges): nodes at PF, their parents at PF/2
     for (uint32_t i = 0; i < E; ++i) {
-        const uint32_t e = order[i], pa = e >> 1, pb = pa + step[e & 1u];
-        const uint32_t a = find(u, pa), b = find(u, pb);
+        if (i + PF < E) {
+            const uint32_t e2 = order[i + PF], p2 = e2 >> 1;
+            __builtin_prefetch(&u[p2]);
+            __builtin_prefetch(&u[p2 + step[e2 & 1u]]);
+        }
+        if (i + PF / 2 < E) {
+            const uint32_t e2 = order[i + PF / 2], p2 = e2 >> 1;
+            __builtin_prefetch(&u[u[p2].parent]);
+            __builtin_prefetch(&u[u[p2 + step[e2 & 1u]].parent]);
+        }
+        while (i >= count[w]) ++w;
+        const uint32_t e = order[i], pa = e >> 1;
+        const uint32_t a = find(u, pa), b = find(u, pa + step[e & 1u]);
         if (a == b) continue;
-        const double w = (double)weight(e);
-        if (w <= u[a].thr && w <= u[b].thr) {
-            const uint32_t r = unite(u, a, b);
-            u[r].thr = w + (double)(c / (float)u[r].size);
+        const double wd = (double)w;
+        const bool ja = wd <= (double)wl[a] + (double)(c / (float)u[a].size);
+        const bool jb = wd <= (double)wl[b] + (double)(c / (float)u[b].size);
+        if (ja & jb) {
+            wl[unite(u, a, b)] = (uint16_t)w;
             mk[e & 1u][pa] = 1;
             --sets;
+        } else {
+            rejected.push_back(e);
         }
     }
     const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
-    for (uint32_t i = 0; i < E && sets > 1; ++i) {
-        const uint32_t e = order[i], pa = e >> 1;
-        if (mk[e & 1u][pa]) continue;  // joined above: both ends in one component
+    for (size_t i = 0; i < rejected.size() && sets > 1; ++i) {
+        const uint32_t e = rejected[i], pa = e >> 1;
         const uint32_t a = find(u, pa), b = find(u, pa + step[e & 1u]);
         if (a != b && (u[a].size < ms || u[b].size < ms)) {
             unite(u, a, b);
