@@ -23,6 +23,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "sm_launch.h"
 
 #define GF_BLOCK 32
@@ -284,6 +286,365 @@ __global__ void k_gf_init(GfState st, size_t N) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fused tile path (radius 9, the reference's constant).  The unfused chain above moves every slice
+// through HBM ten times (slice_in, 2 x (box x, box y), ab, q); here two kernels do it over 2-D tiles
+// with the box passes in LDS:
+//   k_gf_box1_ab : cost slice + guide -> (p, r*p, g*p, b*p) -> x pass over the tile's 32 + 2r rows ->
+//                  y pass of its 32 rows -> (b, a_r, a_g, a_b) (colorGuidedFilterHelper3/2/4) -> HBM;
+//   k_gf_box2_q  : (b, a_r, a_g, a_b) -> x pass -> y pass -> q (colorGuidedFilterHelper5) -> HBM;
+//   k_gf_wta     : q of the batch's slices in ascending order -> the running strict-< WTA.
+// The four planes of a pixel travel together as one float4 (in LDS and, between the kernels, in HBM
+// as [slice][pixel] float4), so a sliding-sum step is two 16-byte LDS reads and four independent
+// add chains.  A tile is TX (a multiple of 32) columns x one 32-row block, so the x pass runs the
+// unfused kernels' per-32-column-block sliding sums and the y pass their per-32-row-block ones, with
+// the same float operations in the same order: the staged halo (r columns each side, r rows above and
+// below) holds 0.0f outside the image exactly where the unfused kernels add 0.0f, and x-pass rows
+// outside the image are 0.0f for the y pass likewise.  Bit-identical to the unfused chain
+// (tests/test_gpu_parity.py::test_guided_fused_tiles_match_unfused).
+//
+// Work order: the work items (tile, slice) -- a tile's slices back to back, tiles in raster order --
+// are cut into one contiguous range per workgroup, and the ranges dealt to the 8 XCDs in contiguous
+// eighths (workgroup b runs on XCD b % 8): neighbouring tiles' halos and a tile's statistics / guide
+// stay in that XCD's L2 and in registers.
+template <int RR, int TX>
+struct GfTile {
+    static constexpr int R = 32 + 2 * RR;   // x-pass rows of a 32-row block
+    static constexpr int C = TX + 2 * RR;   // staged columns (from x0 - RR)
+    static constexpr int SP = C | 1;        // staging pitch in float4 (odd: 16-byte lanes on consecutive rows
+                                            // cover all banks)
+    static constexpr int XP = TX | 1;       // x-pass output pitch in float4
+    static constexpr int NB = TX / 32;      // 32-column blocks per tile
+    static constexpr int NT = 4 * TX;       // threads
+    static constexpr int NS = R * C;        // staged pixels
+    static constexpr int NPER = (NS + NT - 1) / NT;  // staged pixels per thread
+    static constexpr int PU = 32 * TX / NT; // output pixels per thread
+    static_assert(TX % 32 == 0, "tiles are whole 32-column blocks");
+    static_assert(R * SP >= 32 * XP, "the y pass writes its means over the staging rows");
+    static constexpr size_t LDS = (size_t)(R * SP + R * XP) * 16;
+};
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 f4sub(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+__device__ __forceinline__ float4 f4mul(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
+
+// the two box passes of a staged tile: x pass (job = (row, 32-column block), consecutive lanes on
+// consecutive rows) into xo, then y pass (thread = column) into the staging rows (means of tile row
+// yy at sp[yy * SP + j])
+template <int RR, int TX>
+__device__ __forceinline__ void gf_box_tile(float4* sp, float4* xo, int x0, int y0, int W, int H) {
+    using T = GfTile<RR, TX>;
+    const float scale = 1.0f / (float)(2 * RR + 1);
+    const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int job = threadIdx.x; job < T::NB * T::R; job += T::NT) {
+        const int bb = job / T::R, rr = job - bb * T::R;
+        const int xb = x0 + 32 * bb, gy = y0 - RR + rr;
+        if (xb >= W) continue;
+        const int nout = W - xb < 32 ? W - xb : 32;
+        float4* o = xo + rr * T::XP + 32 * bb;
+        if (gy < 0 || gy >= H) {
+            for (int x = 0; x < nout; ++x) o[x] = z4;
+            continue;
+        }
+        const float4* row = sp + rr * T::SP + 32 * bb + RR;  // staged column of the block start
+        float4 t = z4;
+        {
+            float4 w[2 * RR + 1];  // the first window's reads issued together
+#pragma unroll
+            for (int i = 0; i <= 2 * RR; ++i) w[i] = row[i - RR];
+#pragma unroll
+            for (int i = 0; i <= 2 * RR; ++i) t = f4add(t, w[i]);
+        }
+        o[0] = f4mul(t, scale);
+        if (nout == 32) {
+            // steps in groups of GS: the group's 2 x GS LDS reads are issued before its dependent adds
+            constexpr int GS = 8;
+#pragma unroll
+            for (int xg = 1; xg < 32; xg += GS) {
+                float4 ah[GS], bh[GS];
+#pragma unroll
+                for (int k = 0; k < GS; ++k)
+                    if (xg + k < 32) {
+                        ah[k] = row[xg + k + RR];
+                        bh[k] = row[xg + k - RR - 1];
+                    }
+#pragma unroll
+                for (int k = 0; k < GS; ++k)
+                    if (xg + k < 32) {
+                        t = f4add(t, ah[k]);
+                        t = f4sub(t, bh[k]);
+                        o[xg + k] = f4mul(t, scale);
+                    }
+            }
+        } else {
+            for (int x = 1; x < nout; ++x) {
+                t = f4add(t, row[x + RR]);
+                t = f4sub(t, row[x - RR - 1]);
+                o[x] = f4mul(t, scale);
+            }
+        }
+    }
+    __syncthreads();
+    const int j = threadIdx.x;
+    if (j < TX && x0 + j < W) {
+        const int nrow = H - y0 < 32 ? H - y0 : 32;
+        const float4* col = xo + j;
+        float4 t = z4;
+        {
+            float4 w[2 * RR + 1];
+#pragma unroll
+            for (int i = 0; i <= 2 * RR; ++i) w[i] = col[i * T::XP];
+#pragma unroll
+            for (int i = 0; i <= 2 * RR; ++i) t = f4add(t, w[i]);
+        }
+        sp[j] = f4mul(t, scale);
+        if (nrow == 32) {
+            constexpr int GS = 8;
+#pragma unroll
+            for (int yg = 1; yg < 32; yg += GS) {
+                float4 ah[GS], bh[GS];
+#pragma unroll
+                for (int k = 0; k < GS; ++k)
+                    if (yg + k < 32) {
+                        ah[k] = col[(yg + k + 2 * RR) * T::XP];
+                        bh[k] = col[(yg + k - 1) * T::XP];
+                    }
+#pragma unroll
+                for (int k = 0; k < GS; ++k)
+                    if (yg + k < 32) {
+                        t = f4add(t, ah[k]);
+                        t = f4sub(t, bh[k]);
+                        sp[(yg + k) * T::SP + j] = f4mul(t, scale);
+                    }
+            }
+        } else {
+            for (int yy = 1; yy < nrow; ++yy) {
+                t = f4add(t, col[(yy + 2 * RR) * T::XP]);
+                t = f4sub(t, col[(yy - 1) * T::XP]);
+                sp[yy * T::SP + j] = f4mul(t, scale);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// this workgroup's contiguous range [i0, i1) of the work items (G = gridDim.x, a multiple of 8;
+// workgroup b runs on XCD b % 8, so each XCD gets one contiguous eighth of the list)
+__device__ __forceinline__ void gf_range(int nitems, int& i0, int& i1) {
+    const int b = blockIdx.x, G = gridDim.x;
+    const int c = (b & 7) * (G >> 3) + (b >> 3);
+    const int per = (nitems + G - 1) / G;
+    i0 = c * per;
+    i1 = i0 + per < nitems ? i0 + per : nitems;
+}
+
+// Both kernels loop over their range with the next item's tile loads in flight (registers) while the
+// current one runs its box passes out of LDS; the per-tile operands of the epilogue (statistics,
+// guide) are loaded once per tile -- items run a tile's slices back to back.
+template <int RR, int TX>
+__global__ __launch_bounds__(4 * TX) void k_gf_box1_ab(const float* __restrict__ cost, const uint32_t* __restrict__ bgrx,
+                                                       const float* __restrict__ st, float4* __restrict__ ab, int W, int H,
+                                                       size_t N, int S, int ntx, int nitems) {
+    using T = GfTile<RR, TX>;
+    __shared__ float4 sp[T::R * T::SP];
+    __shared__ float4 xo[T::R * T::XP];
+    int i0, i1;
+    gf_range(nitems, i0, i1);
+    if (i0 >= i1) return;
+    const int tid = threadIdx.x;
+    float pv[T::NPER];
+    uint32_t gv[T::NPER];
+    auto load = [&](int item) {
+        const int s = item % S, tile = item / S;
+        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
+        const float* p = cost + (size_t)s * N;
+#pragma unroll
+        for (int u = 0; u < T::NPER; ++u) {
+            int idx = tid + u * T::NT;
+            idx = idx < T::NS ? idx : T::NS - 1;
+            const int rr = idx / T::C, cc = idx - rr * T::C;
+            const int gy = y0 - RR + rr, gx = x0 - RR + cc;
+            const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const size_t i = in ? (size_t)gy * W + gx : 0;
+            const float a = p[i];
+            const uint32_t g = bgrx[i];
+            pv[u] = in ? a : 0.0f;
+            gv[u] = in ? g : 0u;
+        }
+    };
+    load(i0);
+    int cur = -1;
+    float sv[T::PU][9];
+    for (int item = i0; item < i1; ++item) {
+        const int s = item % S, tile = item / S;
+        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
+#pragma unroll
+        for (int u = 0; u < T::NPER; ++u) {
+            const int idx = tid + u * T::NT;
+            if (idx < T::NS) {
+                const int rr = idx / T::C, cc = idx - rr * T::C;
+                float r, g, b;
+                guide_of(gv[u], r, g, b);  // k_gf_slice_in: p, r*p, g*p, b*p (outside: 0 * 0)
+                sp[rr * T::SP + cc] = make_float4(pv[u], r * pv[u], g * pv[u], b * pv[u]);
+            }
+        }
+        if (tile != cur) {
+            cur = tile;
+#pragma unroll
+            for (int u = 0; u < T::PU; ++u) {
+                const int idx = tid + u * T::NT;
+                const int yy = idx / TX, jj = idx - yy * TX;
+                const int gy = y0 + yy, gx = x0 + jj;
+                const size_t i = gy < H && gx < W ? (size_t)gy * W + gx : 0;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) sv[u][k] = st[k * N + i];
+            }
+        }
+        __syncthreads();
+        if (item + 1 < i1) load(item + 1);
+        gf_box_tile<RR, TX>(sp, xo, x0, y0, W, H);
+        // a, b per pixel (k_gf_ab's operations)
+#pragma unroll
+        for (int u = 0; u < T::PU; ++u) {
+            const int idx = tid + u * T::NT;
+            const int yy = idx / TX, jj = idx - yy * TX;
+            const int gy = y0 + yy, gx = x0 + jj;
+            if (gy >= H || gx >= W) continue;
+            const float4 m = sp[yy * T::SP + jj];
+            const float m_p = m.x;
+            const float mr = sv[u][0], mg = sv[u][1], mb = sv[u][2];
+            const float irr = sv[u][3], irg = sv[u][4], irb = sv[u][5];
+            const float igg = sv[u][6], igb = sv[u][7], ibb = sv[u][8];
+            const float cr = m.y - mr * m_p;
+            const float cg = m.z - mg * m_p;
+            const float cb = m.w - mb * m_p;
+            const float ar = irr * cr + irg * cg + irb * cb;
+            const float ag = irg * cr + igg * cg + igb * cb;
+            const float ab_ = irb * cr + igb * cg + ibb * cb;
+            const float bb = m_p - ar * mr - ag * mg - ab_ * mb;
+            ab[(size_t)s * N + (size_t)gy * W + gx] = make_float4(bb, ar, ag, ab_);
+        }
+        __syncthreads();  // the epilogue's reads of sp before the next item's staging
+    }
+}
+
+template <int RR, int TX>
+__global__ __launch_bounds__(4 * TX) void k_gf_box2_q(const float4* __restrict__ ab, const uint32_t* __restrict__ bgrx,
+                                                      float* __restrict__ q, int W, int H, size_t N, int S, int ntx,
+                                                      int nitems) {
+    using T = GfTile<RR, TX>;
+    __shared__ float4 sp[T::R * T::SP];
+    __shared__ float4 xo[T::R * T::XP];
+    int i0, i1;
+    gf_range(nitems, i0, i1);
+    if (i0 >= i1) return;
+    const int tid = threadIdx.x;
+    float4 v[T::NPER];
+    auto load = [&](int item) {
+        const int s = item % S, tile = item / S;
+        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
+        const float4* src = ab + (size_t)s * N;
+#pragma unroll
+        for (int u = 0; u < T::NPER; ++u) {
+            int idx = tid + u * T::NT;
+            idx = idx < T::NS ? idx : T::NS - 1;
+            const int rr = idx / T::C, cc = idx - rr * T::C;
+            const int gy = y0 - RR + rr, gx = x0 - RR + cc;
+            const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const float4 a = src[in ? (size_t)gy * W + gx : 0];
+            v[u] = in ? a : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+    };
+    load(i0);
+    int cur = -1;
+    uint32_t gv[T::PU];
+    for (int item = i0; item < i1; ++item) {
+        const int s = item % S, tile = item / S;
+        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
+#pragma unroll
+        for (int u = 0; u < T::NPER; ++u) {
+            const int idx = tid + u * T::NT;
+            if (idx < T::NS) {
+                const int rr = idx / T::C, cc = idx - rr * T::C;
+                sp[rr * T::SP + cc] = v[u];
+            }
+        }
+        if (tile != cur) {
+            cur = tile;
+#pragma unroll
+            for (int u = 0; u < T::PU; ++u) {
+                const int idx = tid + u * T::NT;
+                const int yy = idx / TX, jj = idx - yy * TX;
+                const int gy = y0 + yy, gx = x0 + jj;
+                gv[u] = bgrx[gy < H && gx < W ? (size_t)gy * W + gx : 0];
+            }
+        }
+        __syncthreads();
+        if (item + 1 < i1) load(item + 1);
+        gf_box_tile<RR, TX>(sp, xo, x0, y0, W, H);
+#pragma unroll
+        for (int u = 0; u < T::PU; ++u) {
+            const int idx = tid + u * T::NT;
+            const int yy = idx / TX, jj = idx - yy * TX;
+            const int gy = y0 + yy, gx = x0 + jj;
+            if (gy >= H || gx >= W) continue;
+            float r, g, b;
+            guide_of(gv[u], r, g, b);
+            const float4 m = sp[yy * T::SP + jj];  // box(b), box(a_r), box(a_g), box(a_b)
+            q[(size_t)s * N + (size_t)gy * W + gx] = m.x + m.y * r + m.z * g + m.w * b;
+        }
+        __syncthreads();
+    }
+}
+
+// k_gf_q_wta's WTA over precomputed q
+__global__ void k_gf_wta(const float* __restrict__ q, GfState st, size_t N, int S, int dloc0) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    float mn = st.mn[i], pre = st.pre[i], nxt = st.nxt[i], pq = st.prevq[i];
+    int best = st.best[i];
+    for (int s = 0; s < S; ++s) {
+        const int d = dloc0 + s;
+        const float qv = q[(size_t)s * N + i];
+        if (best >= 0 && best == d - 1) nxt = qv;
+        if (qv < mn) {
+            mn = qv;
+            best = d;
+            pre = d == 0 ? 0.0f : pq;
+            nxt = 0.0f;
+        }
+        pq = qv;
+    }
+    st.mn[i] = mn;
+    st.best[i] = best;
+    st.pre[i] = pre;
+    st.nxt[i] = nxt;
+    st.prevq[i] = pq;
+}
+
+static bool gf_fused(int r) {
+    return r == 9 && getenv("SM_GF_UNFUSED") == nullptr;  // read per batch: tests toggle it
+}
+
+static hipError_t launch_gf_batch_fused(hipStream_t st, const float* cost, const uint32_t* bgrx, const float* stats, int W,
+                                        int H, int S, int dloc0, float* pl, float* tmp, GfStateArgs sa) {
+    constexpr int RR = 9, TX = 32;
+    static_assert(GfTile<RR, TX>::LDS <= 81920, "two workgroups per CU");
+    const size_t N = (size_t)W * H;
+    const int nty = (H + 31) / 32, ntx = (W + TX - 1) / TX;
+    const int n = ntx * nty * S;  // work items (tile, slice), slice fastest
+    // two resident workgroups per CU (LDS), each looping over n / G items
+    const char* e = getenv("SM_GF_WGS");
+    int G = e ? atoi(e) : 512;
+    G = std::max(8, std::min(G, (n + 7) & ~7)) & ~7;
+    float4* ab = reinterpret_cast<float4*>(pl);  // [S][N] float4 in the 4S planes
+    hipLaunchKernelGGL((k_gf_box1_ab<RR, TX>), dim3(G), dim3(4 * TX), 0, st, cost, bgrx, stats, ab, W, H, N, S, ntx, n);
+    hipLaunchKernelGGL((k_gf_box2_q<RR, TX>), dim3(G), dim3(4 * TX), 0, st, ab, bgrx, tmp, W, H, N, S, ntx, n);
+    const GfState gs{sa.mn, sa.best, sa.pre, sa.nxt, sa.prevq};
+    hipLaunchKernelGGL(k_gf_wta, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, tmp, gs, N, S, dloc0);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 static dim3 pix_grid1(size_t N, int y = 1) { return dim3((unsigned)((N + 255) / 256), (unsigned)y); }
 
 static void box(hipStream_t st, const float* in, float* tmp, float* out, int W, int H, int r, int planes) {
@@ -314,6 +675,7 @@ hipError_t launch_gf_guide(hipStream_t st, const uint32_t* bgrx, int W, int H, i
 
 hipError_t launch_gf_batch(hipStream_t st, const float* cost, const uint32_t* bgrx, const float* stats, int W, int H, int r,
                            int S, int dloc0, float* pl, float* tmp, GfStateArgs sa) {
+    if (gf_fused(r)) return launch_gf_batch_fused(st, cost, bgrx, stats, W, H, S, dloc0, pl, tmp, sa);
     const size_t N = (size_t)W * H;
     hipLaunchKernelGGL(k_gf_slice_in, pix_grid1(N, S), dim3(256), 0, st, cost, bgrx, pl, N, S);
     box(st, pl, tmp, pl, W, H, r, 4 * S);   // means of p, r*p, g*p, b*p

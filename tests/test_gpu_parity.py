@@ -891,6 +891,28 @@ def test_guided_direct_x_pass(gpu_ctx, monkeypatch):
             np.testing.assert_array_equal(b[v]["disp"], a[v]["disp"])
 
 
+def test_guided_fused_tiles_match_unfused(gpu_ctx, monkeypatch):
+    """Radius 9 with W % 4 == 0 runs the fused tile kernels (k_gf_box1_ab / k_gf_box2_q / k_gf_wta);
+    SM_GF_UNFUSED=1 (and any other width or radius) the unfused chain.  Same bits, and the oracle's, on
+    images narrower than a tile, one row high, ragged in both 32-pixel block directions, and with
+    partial slice batches."""
+    import stereomatch_amd as sm
+    for W, H, D in ((8, 40, 4), (92, 1, 16), (204, 97, 40), (68, 33, 33), (132, 70, 24), (7, 20, 8)):
+        left, right, _ = make_pair(W, H, D, index=5)
+        p = sm.default_params(aggregator=sm.SM_AGG_GUIDED, post=sm.SM_POST_SUBPIXEL)
+        a = gpu_ctx.match(left, right, D, p)
+        monkeypatch.setenv("SM_GF_UNFUSED", "1")
+        b = gpu_ctx.match(left, right, D, p)
+        monkeypatch.delenv("SM_GF_UNFUSED")
+        ref = O.guided_match(left, right, D, sub=True, nthreads=16)
+        for v in ("left", "right"):
+            np.testing.assert_array_equal(a[v]["idx"].ravel(), ref[v]["idx"])
+            np.testing.assert_array_equal(a[v]["minc"].ravel(), ref[v]["minc"].astype(np.float64))
+            np.testing.assert_array_equal(a[v]["disp"].ravel(), ref[v]["disp"])
+            for k in ("idx", "minc", "disp"):
+                np.testing.assert_array_equal(b[v][k], a[v][k])
+
+
 def test_guided_errors(gpu_ctx):
     import stereomatch_amd as sm
     left, right, _ = make_pair(40, 30, 8)
