@@ -1121,12 +1121,13 @@ sm_status stage_guided(sm_ctx* ctx, int D, int d0, int dtot, int sub, int rad, f
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H;
     const int S = std::min(D, 32);
+    const size_t NS = std::max(N, gf_band_plane(W, H));  // planes of the row band layout (fused path)
     CHECK(ensure(ctx, ctx->gf_planes, 9 * N * 4));
     CHECK(ensure(ctx, ctx->gf_means, 9 * N * 4));
-    CHECK(ensure(ctx, ctx->gf_pl, 4 * (size_t)S * N * 4));
+    CHECK(ensure(ctx, ctx->gf_pl, 4 * (size_t)S * NS * 4));
     CHECK(ensure(ctx, ctx->gf_tmp, std::max<size_t>(9, 4 * (size_t)S) * N * 4));
     for (int v = 0; v < 2; ++v) {
-        CHECK(ensure(ctx, ctx->gf_stats[v], 9 * N * 4));
+        CHECK(ensure(ctx, ctx->gf_stats[v], 9 * NS * 4));
         CHECK(ensure(ctx, ctx->gf_state[v], 5 * N * 4));
         CHECK(ensure(ctx, ctx->vol[v], (size_t)S * N * 4));
         CHECK(ensure(ctx, ctx->idx[v], N * 4));

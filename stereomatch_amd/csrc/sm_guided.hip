@@ -141,9 +141,16 @@ __global__ void k_gf_guide_in(const uint32_t* __restrict__ bgrx, float* __restri
 
 // guide statistics from the 9 box means m[]: st = mean_r, mean_g, mean_b, inv_rr, inv_rg, inv_rb,
 // inv_gg, inv_gb, inv_bb (colorGuidedFilterHelper0 / 1 / 2, pointWiseDivison)
-__global__ void k_gf_stats(const float* __restrict__ m, float* __restrict__ st, size_t N, float eps) {
+// row band layout of the fused path: rows in bands of 32, a band stored column by column, so the 32
+// rows of one column are contiguous -- a wavefront whose lanes are consecutive rows reads one segment
+__host__ __device__ __forceinline__ size_t gf_band(int gy, int gx, int W) { return ((size_t)(gy >> 5) * W + gx) * 32 + (gy & 31); }
+
+// planes of stride NS: row-major (band = 0, NS = N) or in the row band layout (NS = 32 * ceil(H/32) * W)
+__global__ void k_gf_stats(const float* __restrict__ m, float* __restrict__ st_, size_t N, float eps, int W, int band, size_t NS) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
+    const size_t o = band ? gf_band((int)(i / W), (int)(i % W), W) : i;
+    float* st = st_;
     const float mr = m[i], mg = m[N + i], mb = m[2 * N + i];
     const float vrr = m[3 * N + i] - mr * mr + eps;
     const float vgg = m[4 * N + i] - mg * mg + eps;
@@ -158,15 +165,15 @@ __global__ void k_gf_stats(const float* __restrict__ m, float* __restrict__ st, 
     const float irb = vrg * vgb - vgg * vrb;
     const float igb = vrb * vrg - vrr * vgb;
     const float det = irr * vrr + irg * vrg + irb * vrb;
-    st[i] = mr;
-    st[N + i] = mg;
-    st[2 * N + i] = mb;
-    st[3 * N + i] = irr / det;
-    st[4 * N + i] = irg / det;
-    st[5 * N + i] = irb / det;
-    st[6 * N + i] = igg / det;
-    st[7 * N + i] = igb / det;
-    st[8 * N + i] = ibb / det;
+    st[o] = mr;
+    st[NS + o] = mg;
+    st[2 * NS + o] = mb;
+    st[3 * NS + o] = irr / det;
+    st[4 * NS + o] = irg / det;
+    st[5 * NS + o] = irb / det;
+    st[6 * NS + o] = igg / det;
+    st[7 * NS + o] = igb / det;
+    st[8 * NS + o] = ibb / det;
 }
 
 // per slice s of the batch: planes [0..S) p, [S..2S) r*p, [2S..3S) g*p, [3S..4S) b*p
@@ -287,360 +294,339 @@ __global__ void k_gf_init(GfState st, size_t N) {
 
 // ---------------------------------------------------------------------------------------------
 // Fused tile path (radius 9, the reference's constant).  The unfused chain above moves every slice
-// through HBM ten times (slice_in, 2 x (box x, box y), ab, q); here two kernels do it over 2-D tiles
-// with the box passes in LDS:
-//   k_gf_box1_ab : cost slice + guide -> (p, r*p, g*p, b*p) -> x pass over the tile's 32 + 2r rows ->
-//                  y pass of its 32 rows -> (b, a_r, a_g, a_b) (colorGuidedFilterHelper3/2/4) -> HBM;
-//   k_gf_box2_q  : (b, a_r, a_g, a_b) -> x pass -> y pass -> q (colorGuidedFilterHelper5) -> HBM;
-//   k_gf_wta     : q of the batch's slices in ascending order -> the running strict-< WTA.
-// The four planes of a pixel travel together as one float4 (in LDS and, between the kernels, in HBM
-// as [slice][pixel] float4), so a sliding-sum step is two 16-byte LDS reads and four independent
-// add chains.  A tile is TX (a multiple of 32) columns x one 32-row block, so the x pass runs the
-// unfused kernels' per-32-column-block sliding sums and the y pass their per-32-row-block ones, with
-// the same float operations in the same order: the staged halo (r columns each side, r rows above and
-// below) holds 0.0f outside the image exactly where the unfused kernels add 0.0f, and x-pass rows
-// outside the image are 0.0f for the y pass likewise.  Bit-identical to the unfused chain
+// through HBM ten times (slice_in, 2 x (box x, box y), ab, q) and runs a separate WTA pass; here two
+// kernels, one workgroup (four wavefronts) per 32 x 32 tile, loop over the batch's slices:
+//   k_gf_box1_ab    : cost slice + guide -> (p, r*p, g*p, b*p) -> x pass -> y pass -> (b, a_r, a_g,
+//                     a_b) (colorGuidedFilterHelper3/2/4) -> HBM, [slice] float4 planes;
+//   k_gf_box2_q_wta : (b, a_r, a_g, a_b) -> x pass -> y pass -> q (colorGuidedFilterHelper5) -> the
+//                     running strict-< WTA, in registers.
+// The tile is one 32-column block x one 32-row block, so the x pass runs the unfused kernels'
+// per-32-column-block sliding sums and the y pass their per-32-row-block ones, with the same float
+// operations in the same order: the staged tile (32 + 2r square) holds 0.0f outside the image
+// exactly where the unfused kernels add 0.0f, and x-pass rows outside the image are 0.0f for the y
+// pass likewise.  Each pass is one scalar chain per (row or column, plane) -- 4 x (32 + 2r) x-pass
+// chains, 4 x 32 y-pass chains -- so every wavefront has chains to run; the next slice's tile is in
+// flight in registers meanwhile, and the per-tile operands (guide, statistics, WTA state) are read
+// once per batch.  Bit-identical to the unfused chain
 // (tests/test_gpu_parity.py::test_guided_fused_tiles_match_unfused).
 //
-// Work order: the work items (tile, slice) -- a tile's slices back to back, tiles in raster order --
-// are cut into one contiguous range per workgroup, and the ranges dealt to the 8 XCDs in contiguous
-// eighths (workgroup b runs on XCD b % 8): neighbouring tiles' halos and a tile's statistics / guide
-// stay in that XCD's L2 and in registers.
-template <int RR, int TX>
-struct GfTile {
-    static constexpr int R = 32 + 2 * RR;   // x-pass rows of a 32-row block
-    static constexpr int C = TX + 2 * RR;   // staged columns (from x0 - RR)
-    static constexpr int SP = C | 1;        // staging pitch in float4 (odd: 16-byte lanes on consecutive rows
-                                            // cover all banks)
-    static constexpr int XP = TX | 1;       // x-pass output pitch in float4
-    static constexpr int NB = TX / 32;      // 32-column blocks per tile
-    static constexpr int NT = 4 * TX;       // threads
-    static constexpr int NS = R * C;        // staged pixels
-    static constexpr int NPER = (NS + NT - 1) / NT;  // staged pixels per thread
-    static constexpr int PU = 32 * TX / NT; // output pixels per thread
-    static_assert(TX % 32 == 0, "tiles are whole 32-column blocks");
-    static_assert(R * SP >= 32 * XP, "the y pass writes its means over the staging rows");
-    static constexpr size_t LDS = (size_t)(R * SP + R * XP) * 16;
-};
+// Row band layout: the statistics and the (b, a) planes are stored in bands of 32 rows, a band
+// column by column (gf_band), so the 32 rows of a column are contiguous: the epilogue (lanes on
+// consecutive rows) and k_gf_box2_q_wta's staging read and write whole segments.
+//
+// Work order: tiles in raster order, dealt to the 8 XCDs in contiguous eighths (workgroup b runs on
+// XCD b % 8), so neighbouring tiles' halos are re-read from that XCD's L2.
 
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-__device__ __forceinline__ float4 f4sub(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
-__device__ __forceinline__ float4 f4mul(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
-
-// the two box passes of a staged tile: x pass (job = (row, 32-column block), consecutive lanes on
-// consecutive rows) into xo, then y pass (thread = column) into the staging rows (means of tile row
-// yy at sp[yy * SP + j])
-template <int RR, int TX>
-__device__ __forceinline__ void gf_box_tile(float4* sp, float4* xo, int x0, int y0, int W, int H) {
-    using T = GfTile<RR, TX>;
-    const float scale = 1.0f / (float)(2 * RR + 1);
-    const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    for (int job = threadIdx.x; job < T::NB * T::R; job += T::NT) {
-        const int bb = job / T::R, rr = job - bb * T::R;
-        const int xb = x0 + 32 * bb, gy = y0 - RR + rr;
-        if (xb >= W) continue;
-        const int nout = W - xb < 32 ? W - xb : 32;
-        float4* o = xo + rr * T::XP + 32 * bb;
-        if (gy < 0 || gy >= H) {
-            for (int x = 0; x < nout; ++x) o[x] = z4;
-            continue;
-        }
-        const float4* row = sp + rr * T::SP + 32 * bb + RR;  // staged column of the block start
-        float4 t = z4;
-        {
-            float4 w[2 * RR + 1];  // the first window's reads issued together
-#pragma unroll
-            for (int i = 0; i <= 2 * RR; ++i) w[i] = row[i - RR];
-#pragma unroll
-            for (int i = 0; i <= 2 * RR; ++i) t = f4add(t, w[i]);
-        }
-        o[0] = f4mul(t, scale);
-        if (nout == 32) {
-            // steps in groups of GS: the group's 2 x GS LDS reads are issued before its dependent adds
-            constexpr int GS = 8;
-#pragma unroll
-            for (int xg = 1; xg < 32; xg += GS) {
-                float4 ah[GS], bh[GS];
-#pragma unroll
-                for (int k = 0; k < GS; ++k)
-                    if (xg + k < 32) {
-                        ah[k] = row[xg + k + RR];
-                        bh[k] = row[xg + k - RR - 1];
-                    }
-#pragma unroll
-                for (int k = 0; k < GS; ++k)
-                    if (xg + k < 32) {
-                        t = f4add(t, ah[k]);
-                        t = f4sub(t, bh[k]);
-                        o[xg + k] = f4mul(t, scale);
-                    }
-            }
-        } else {
-            for (int x = 1; x < nout; ++x) {
-                t = f4add(t, row[x + RR]);
-                t = f4sub(t, row[x - RR - 1]);
-                o[x] = f4mul(t, scale);
-            }
-        }
-    }
-    __syncthreads();
-    const int j = threadIdx.x;
-    if (j < TX && x0 + j < W) {
-        const int nrow = H - y0 < 32 ? H - y0 : 32;
-        const float4* col = xo + j;
-        float4 t = z4;
-        {
-            float4 w[2 * RR + 1];
-#pragma unroll
-            for (int i = 0; i <= 2 * RR; ++i) w[i] = col[i * T::XP];
-#pragma unroll
-            for (int i = 0; i <= 2 * RR; ++i) t = f4add(t, w[i]);
-        }
-        sp[j] = f4mul(t, scale);
-        if (nrow == 32) {
-            constexpr int GS = 8;
-#pragma unroll
-            for (int yg = 1; yg < 32; yg += GS) {
-                float4 ah[GS], bh[GS];
-#pragma unroll
-                for (int k = 0; k < GS; ++k)
-                    if (yg + k < 32) {
-                        ah[k] = col[(yg + k + 2 * RR) * T::XP];
-                        bh[k] = col[(yg + k - 1) * T::XP];
-                    }
-#pragma unroll
-                for (int k = 0; k < GS; ++k)
-                    if (yg + k < 32) {
-                        t = f4add(t, ah[k]);
-                        t = f4sub(t, bh[k]);
-                        sp[(yg + k) * T::SP + j] = f4mul(t, scale);
-                    }
-            }
-        } else {
-            for (int yy = 1; yy < nrow; ++yy) {
-                t = f4add(t, col[(yy + 2 * RR) * T::XP]);
-                t = f4sub(t, col[(yy - 1) * T::XP]);
-                sp[yy * T::SP + j] = f4mul(t, scale);
-            }
-        }
-    }
-    __syncthreads();
-}
-
-// this workgroup's contiguous range [i0, i1) of the work items (G = gridDim.x, a multiple of 8;
-// workgroup b runs on XCD b % 8, so each XCD gets one contiguous eighth of the list)
-__device__ __forceinline__ void gf_range(int nitems, int& i0, int& i1) {
+// the XCD-contiguous item of this workgroup (G = gridDim.x, a multiple of 8)
+__device__ __forceinline__ int gf_item() {
     const int b = blockIdx.x, G = gridDim.x;
-    const int c = (b & 7) * (G >> 3) + (b >> 3);
-    const int per = (nitems + G - 1) / G;
-    i0 = c * per;
-    i1 = i0 + per < nitems ? i0 + per : nitems;
+    return (b & 7) * (G >> 3) + (b >> 3);
 }
 
-// Both kernels loop over their range with the next item's tile loads in flight (registers) while the
-// current one runs its box passes out of LDS; the per-tile operands of the epilogue (statistics,
-// guide) are loaded once per tile -- items run a tile's slices back to back.
-template <int RR, int TX>
-__global__ __launch_bounds__(4 * TX) void k_gf_box1_ab(const float* __restrict__ cost, const uint32_t* __restrict__ bgrx,
-                                                       const float* __restrict__ st, float4* __restrict__ ab, int W, int H,
-                                                       size_t N, int S, int ntx, int nitems) {
-    using T = GfTile<RR, TX>;
-    __shared__ float4 sp[T::R * T::SP];
-    __shared__ float4 xo[T::R * T::XP];
-    int i0, i1;
-    gf_range(nitems, i0, i1);
-    if (i0 >= i1) return;
+constexpr int GF_XQ = 33;  // x-pass plane pitch (floats)
+
+// x pass of staged row xr, plane xk of the tile at (x0, y0): sp = the staged float4 tile (pitch CP,
+// column 0 = x0 - RR), o = the plane's x-pass row
+template <int RR, int CP>
+__device__ __forceinline__ void gf_xchain(const float4* sp, float* o, int xr, int xk, int x0, int y0, int W, int H) {
+    const int nout = W - x0 < 32 ? W - x0 : 32;
+    const int gy = y0 - RR + xr;
+    if (gy < 0 || gy >= H) {
+        for (int x = 0; x < nout; ++x) o[x] = 0.0f;
+        return;
+    }
+    const float scale = 1.0f / (float)(2 * RR + 1);
+    const float* row = reinterpret_cast<const float*>(sp + xr * CP + RR) + xk;  // staged column x0
+    auto in = [&](int c) { return row[4 * c]; };
+    float t = 0.0f;
+    if (nout == 32) {  // whole block: each staged value read once, the chain unrolled
+        float v[32 + 2 * RR];
+#pragma unroll
+        for (int i = 0; i < 32 + 2 * RR; ++i) v[i] = in(i - RR);
+#pragma unroll
+        for (int i = 0; i <= 2 * RR; ++i) t += v[i];
+        o[0] = t * scale;
+#pragma unroll
+        for (int x = 1; x < 32; ++x) {
+            t += v[x + 2 * RR];
+            t -= v[x - 1];
+            o[x] = t * scale;
+        }
+        return;
+    }
+    for (int i = -RR; i <= RR; ++i) t += in(i);
+    o[0] = t * scale;
+    for (int x = 1; x < nout; ++x) {
+        t += in(x + RR);
+        t -= in(x - RR - 1);
+        o[x] = t * scale;
+    }
+}
+
+// y pass of column j of one plane's x-pass rows (col = &plane[0][j]); the mean of tile row yy is
+// written back in place into row yy, one step after that row's last read
+template <int RR>
+__device__ __forceinline__ void gf_ychain(float* col, int y0, int H) {
+    const int nrow = H - y0 < 32 ? H - y0 : 32;
+    const float scale = 1.0f / (float)(2 * RR + 1);
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i <= 2 * RR; ++i) t += col[i * GF_XQ];
+    float prev = t * scale;
+    if (nrow == 32) {
+#pragma unroll
+        for (int yy = 1; yy < 32; ++yy) {
+            const float a = col[(yy + 2 * RR) * GF_XQ], b = col[(yy - 1) * GF_XQ];
+            t += a;
+            t -= b;
+            col[(yy - 1) * GF_XQ] = prev;
+            prev = t * scale;
+        }
+    } else {
+        for (int yy = 1; yy < nrow; ++yy) {
+            const float a = col[(yy + 2 * RR) * GF_XQ], b = col[(yy - 1) * GF_XQ];
+            t += a;
+            t -= b;
+            col[(yy - 1) * GF_XQ] = prev;
+            prev = t * scale;
+        }
+    }
+    col[(nrow - 1) * GF_XQ] = prev;
+}
+
+// k_gf_box1_ab: four wavefronts per tile, looping over the batch's slices: the tile's guide and its
+// pixels' statistics are loaded once (registers), and the next slice's cost tile (32 + 2r square,
+// coalesced row loads) is in flight in registers while the current one runs.  The staged tile holds
+// the four products (p, r*p, g*p, b*p) per pixel; both box passes run one scalar chain per (row or
+// column, plane) -- 4 x (32 + 2r) x-pass chains, 4 x 32 y-pass chains -- so all four wavefronts work
+// in each pass.  Statistics in, (b, a_r, a_g, a_b) out, both in the row band layout (NS floats /
+// float4 per plane), lanes on consecutive rows of a column.
+template <int RR>
+__global__ __launch_bounds__(256) void k_gf_box1_ab(const float* __restrict__ cost, const uint32_t* __restrict__ bgrx,
+                                                    const float* __restrict__ stb, float4* __restrict__ ab, int W, int H,
+                                                    size_t N, size_t NS, int S, int ntx, int ntiles, int dbg) {
+    constexpr int R = 32 + 2 * RR, C = 32 + 2 * RR, CP = C | 1, NST = R * C, NPER = (NST + 255) / 256;
+    constexpr int XQ = GF_XQ;
+    __shared__ float4 sp[R * CP];
+    __shared__ float xo[4 * R * XQ];
+    const int tile = gf_item();
+    if (tile >= ntiles) return;
+    const int x0 = (tile % ntx) * 32, y0 = (tile / ntx) * 32;
     const int tid = threadIdx.x;
-    float pv[T::NPER];
-    uint32_t gv[T::NPER];
-    auto load = [&](int item) {
-        const int s = item % S, tile = item / S;
-        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
+    auto stage_at = [&](int idx, size_t& i) {  // staged element idx -> pixel (false: outside)
+        const int rr = idx / C, cc = idx - rr * C;
+        const int gy = y0 - RR + rr, gx = x0 - RR + cc;
+        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        i = in ? (size_t)gy * W + gx : 0;
+        return in;
+    };
+    uint32_t gv[NPER];  // the guide of the thread's staged pixels, once
+#pragma unroll
+    for (int u = 0; u < NPER; ++u) {
+        int idx = tid + u * 256;
+        idx = idx < NST ? idx : NST - 1;
+        size_t i;
+        const bool in = stage_at(idx, i);
+        const uint32_t g = bgrx[i];
+        gv[u] = in ? g : 0u;
+    }
+    float sv[4][9];  // the statistics of the thread's 4 output pixels, once
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int gy = y0 + (tid & 31), gx = x0 + (tid >> 5) + 8 * u;
+        const size_t i = gy < H && gx < W ? gf_band(gy, gx, W) : 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) sv[u][k] = stb[k * NS + i];
+    }
+    float pv[NPER];
+    auto load = [&](int s) {
         const float* p = cost + (size_t)s * N;
 #pragma unroll
-        for (int u = 0; u < T::NPER; ++u) {
-            int idx = tid + u * T::NT;
-            idx = idx < T::NS ? idx : T::NS - 1;
-            const int rr = idx / T::C, cc = idx - rr * T::C;
-            const int gy = y0 - RR + rr, gx = x0 - RR + cc;
-            const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-            const size_t i = in ? (size_t)gy * W + gx : 0;
+        for (int u = 0; u < NPER; ++u) {
+            int idx = tid + u * 256;
+            idx = idx < NST ? idx : NST - 1;
+            size_t i;
+            const bool in = stage_at(idx, i);
             const float a = p[i];
-            const uint32_t g = bgrx[i];
             pv[u] = in ? a : 0.0f;
-            gv[u] = in ? g : 0u;
         }
     };
-    load(i0);
-    int cur = -1;
-    float sv[T::PU][9];
-    for (int item = i0; item < i1; ++item) {
-        const int s = item % S, tile = item / S;
-        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
+    load(0);
+    // x-pass chain of this thread: staged row xr, plane xk (0: p, 1..3: r*p, g*p, b*p); plane fastest
+    // across lanes, so a wavefront's scalar reads of the float4 tile hit 64 different banks
+    const int xk = tid & 3, xr = tid >> 2;
+    const bool xjob = xr < R;
+    for (int s = 0; s < S; ++s) {
 #pragma unroll
-        for (int u = 0; u < T::NPER; ++u) {
-            const int idx = tid + u * T::NT;
-            if (idx < T::NS) {
-                const int rr = idx / T::C, cc = idx - rr * T::C;
+        for (int u = 0; u < NPER; ++u) {
+            const int idx = tid + u * 256;
+            if (idx < NST) {
                 float r, g, b;
                 guide_of(gv[u], r, g, b);  // k_gf_slice_in: p, r*p, g*p, b*p (outside: 0 * 0)
-                sp[rr * T::SP + cc] = make_float4(pv[u], r * pv[u], g * pv[u], b * pv[u]);
-            }
-        }
-        if (tile != cur) {
-            cur = tile;
-#pragma unroll
-            for (int u = 0; u < T::PU; ++u) {
-                const int idx = tid + u * T::NT;
-                const int yy = idx / TX, jj = idx - yy * TX;
-                const int gy = y0 + yy, gx = x0 + jj;
-                const size_t i = gy < H && gx < W ? (size_t)gy * W + gx : 0;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) sv[u][k] = st[k * N + i];
+                const float p = pv[u];
+                sp[(idx / C) * CP + idx % C] = make_float4(p, r * p, g * p, b * p);
             }
         }
         __syncthreads();
-        if (item + 1 < i1) load(item + 1);
-        gf_box_tile<RR, TX>(sp, xo, x0, y0, W, H);
-        // a, b per pixel (k_gf_ab's operations)
+        if (s + 1 < S) load(s + 1);
+        if (xjob) gf_xchain<RR, CP>(sp, xo + (xk * R + xr) * XQ, xr, xk, x0, y0, W, H);
+        __syncthreads();
+        if (!(dbg & 2) && tid < 128 && x0 + (tid & 31) < W)  // y pass: (column, plane)
+            gf_ychain<RR>(xo + (tid >> 5) * R * XQ + (tid & 31), y0, H);
+        __syncthreads();
+        if (!(dbg & 4)) {
+            // a, b per pixel (k_gf_ab's operations)
 #pragma unroll
-        for (int u = 0; u < T::PU; ++u) {
-            const int idx = tid + u * T::NT;
-            const int yy = idx / TX, jj = idx - yy * TX;
-            const int gy = y0 + yy, gx = x0 + jj;
-            if (gy >= H || gx >= W) continue;
-            const float4 m = sp[yy * T::SP + jj];
-            const float m_p = m.x;
-            const float mr = sv[u][0], mg = sv[u][1], mb = sv[u][2];
-            const float irr = sv[u][3], irg = sv[u][4], irb = sv[u][5];
-            const float igg = sv[u][6], igb = sv[u][7], ibb = sv[u][8];
-            const float cr = m.y - mr * m_p;
-            const float cg = m.z - mg * m_p;
-            const float cb = m.w - mb * m_p;
-            const float ar = irr * cr + irg * cg + irb * cb;
-            const float ag = irg * cr + igg * cg + igb * cb;
-            const float ab_ = irb * cr + igb * cg + ibb * cb;
-            const float bb = m_p - ar * mr - ag * mg - ab_ * mb;
-            ab[(size_t)s * N + (size_t)gy * W + gx] = make_float4(bb, ar, ag, ab_);
+            for (int u = 0; u < 4; ++u) {
+                const int yy = tid & 31, jj = (tid >> 5) + 8 * u;
+                const int gy = y0 + yy, gx = x0 + jj;
+                if (gy >= H || gx >= W) continue;
+                const float m_p = xo[yy * XQ + jj];
+                const float mIr = xo[(R + yy) * XQ + jj];
+                const float mIg = xo[(2 * R + yy) * XQ + jj];
+                const float mIb = xo[(3 * R + yy) * XQ + jj];
+                const float mr = sv[u][0], mg = sv[u][1], mb = sv[u][2];
+                const float irr = sv[u][3], irg = sv[u][4], irb = sv[u][5];
+                const float igg = sv[u][6], igb = sv[u][7], ibb = sv[u][8];
+                const float cr = mIr - mr * m_p;
+                const float cg = mIg - mg * m_p;
+                const float cb = mIb - mb * m_p;
+                const float ar = irr * cr + irg * cg + irb * cb;
+                const float ag = irg * cr + igg * cg + igb * cb;
+                const float ab_ = irb * cr + igb * cg + ibb * cb;
+                const float bb = m_p - ar * mr - ag * mg - ab_ * mb;
+                ab[(size_t)s * NS + gf_band(gy, gx, W)] = make_float4(bb, ar, ag, ab_);
+            }
         }
-        __syncthreads();  // the epilogue's reads of sp before the next item's staging
+        __syncthreads();  // xo / sp reads done before the next slice overwrites them
     }
 }
 
-template <int RR, int TX>
-__global__ __launch_bounds__(4 * TX) void k_gf_box2_q(const float4* __restrict__ ab, const uint32_t* __restrict__ bgrx,
-                                                      float* __restrict__ q, int W, int H, size_t N, int S, int ntx,
-                                                      int nitems) {
-    using T = GfTile<RR, TX>;
-    __shared__ float4 sp[T::R * T::SP];
-    __shared__ float4 xo[T::R * T::XP];
-    int i0, i1;
-    gf_range(nitems, i0, i1);
-    if (i0 >= i1) return;
+// k_gf_box2_q_wta: four wavefronts per tile, looping over the batch's slices in ascending order
+// like k_gf_box1_ab (the next slice's (b, a_r, a_g, a_b) tile in flight in registers, staged from the
+// row band layout with lanes on consecutive rows), then q (colorGuidedFilterHelper5) and the running
+// strict-< WTA of the thread's 4 pixels in registers (k_gf_q_wta's update; state in and out once per
+// batch).
+template <int RR>
+__global__ __launch_bounds__(256) void k_gf_box2_q_wta(const float4* __restrict__ ab, const uint32_t* __restrict__ bgrx,
+                                                       GfState wst, int W, int H, size_t NS, int S, int dloc0, int ntx,
+                                                       int ntiles, int dbg) {
+    constexpr int R = 32 + 2 * RR, C = 32 + 2 * RR, CP = C | 1, NST = R * C, NPER = (NST + 255) / 256;
+    constexpr int XQ = GF_XQ;
+    __shared__ float4 sp[R * CP];
+    __shared__ float xo[4 * R * XQ];
+    const int tile = gf_item();
+    if (tile >= ntiles) return;
+    const int x0 = (tile % ntx) * 32, y0 = (tile / ntx) * 32;
     const int tid = threadIdx.x;
-    float4 v[T::NPER];
-    auto load = [&](int item) {
-        const int s = item % S, tile = item / S;
-        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
-        const float4* src = ab + (size_t)s * N;
+    // staged element idx: row fastest (rr = idx % R), so a wavefront's loads are row band segments
+    auto stage_at = [&](int idx, size_t& i) {
+        const int cc = idx / R, rr = idx - cc * R;
+        const int gy = y0 - RR + rr, gx = x0 - RR + cc;
+        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        i = in ? gf_band(gy, gx, W) : 0;
+        return in;
+    };
+    float4 pv[NPER];
+    auto load = [&](int s) {
+        const float4* src = ab + (size_t)s * NS;
 #pragma unroll
-        for (int u = 0; u < T::NPER; ++u) {
-            int idx = tid + u * T::NT;
-            idx = idx < T::NS ? idx : T::NS - 1;
-            const int rr = idx / T::C, cc = idx - rr * T::C;
-            const int gy = y0 - RR + rr, gx = x0 - RR + cc;
-            const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-            const float4 a = src[in ? (size_t)gy * W + gx : 0];
-            v[u] = in ? a : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int u = 0; u < NPER; ++u) {
+            int idx = tid + u * 256;
+            idx = idx < NST ? idx : NST - 1;
+            size_t i;
+            const bool in = stage_at(idx, i);
+            const float4 a = src[i];
+            pv[u] = in ? a : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
     };
-    load(i0);
-    int cur = -1;
-    uint32_t gv[T::PU];
-    for (int item = i0; item < i1; ++item) {
-        const int s = item % S, tile = item / S;
-        const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * 32;
+    load(0);
+    // the thread's 4 pixels: guide and WTA state
+    float gr[4], gg[4], gb[4], mn[4], pre[4], nxt[4], pq[4];
+    int best[4];
+    size_t pix[4];
+    bool own[4];
 #pragma unroll
-        for (int u = 0; u < T::NPER; ++u) {
-            const int idx = tid + u * T::NT;
-            if (idx < T::NS) {
-                const int rr = idx / T::C, cc = idx - rr * T::C;
-                sp[rr * T::SP + cc] = v[u];
-            }
-        }
-        if (tile != cur) {
-            cur = tile;
-#pragma unroll
-            for (int u = 0; u < T::PU; ++u) {
-                const int idx = tid + u * T::NT;
-                const int yy = idx / TX, jj = idx - yy * TX;
-                const int gy = y0 + yy, gx = x0 + jj;
-                gv[u] = bgrx[gy < H && gx < W ? (size_t)gy * W + gx : 0];
-            }
-        }
-        __syncthreads();
-        if (item + 1 < i1) load(item + 1);
-        gf_box_tile<RR, TX>(sp, xo, x0, y0, W, H);
-#pragma unroll
-        for (int u = 0; u < T::PU; ++u) {
-            const int idx = tid + u * T::NT;
-            const int yy = idx / TX, jj = idx - yy * TX;
-            const int gy = y0 + yy, gx = x0 + jj;
-            if (gy >= H || gx >= W) continue;
-            float r, g, b;
-            guide_of(gv[u], r, g, b);
-            const float4 m = sp[yy * T::SP + jj];  // box(b), box(a_r), box(a_g), box(a_b)
-            q[(size_t)s * N + (size_t)gy * W + gx] = m.x + m.y * r + m.z * g + m.w * b;
-        }
-        __syncthreads();
+    for (int u = 0; u < 4; ++u) {
+        const int gy = y0 + (tid & 31), gx = x0 + (tid >> 5) + 8 * u;
+        own[u] = gy < H && gx < W;
+        pix[u] = own[u] ? (size_t)gy * W + gx : 0;
+        guide_of(bgrx[pix[u]], gr[u], gg[u], gb[u]);
+        mn[u] = wst.mn[pix[u]];
+        best[u] = wst.best[pix[u]];
+        pre[u] = wst.pre[pix[u]];
+        nxt[u] = wst.nxt[pix[u]];
+        pq[u] = wst.prevq[pix[u]];
     }
-}
-
-// k_gf_q_wta's WTA over precomputed q
-__global__ void k_gf_wta(const float* __restrict__ q, GfState st, size_t N, int S, int dloc0) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
-    float mn = st.mn[i], pre = st.pre[i], nxt = st.nxt[i], pq = st.prevq[i];
-    int best = st.best[i];
+    const int xk = tid & 3, xr = tid >> 2;
+    const bool xjob = xr < R;
     for (int s = 0; s < S; ++s) {
-        const int d = dloc0 + s;
-        const float qv = q[(size_t)s * N + i];
-        if (best >= 0 && best == d - 1) nxt = qv;
-        if (qv < mn) {
-            mn = qv;
-            best = d;
-            pre = d == 0 ? 0.0f : pq;
-            nxt = 0.0f;
+#pragma unroll
+        for (int u = 0; u < NPER; ++u) {
+            const int idx = tid + u * 256;
+            if (idx < NST) {
+                const int cc = idx / R, rr = idx - cc * R;
+                sp[rr * CP + cc] = pv[u];
+            }
         }
-        pq = qv;
+        __syncthreads();
+        if (s + 1 < S) load(s + 1);
+        if (xjob) gf_xchain<RR, CP>(sp, xo + (xk * R + xr) * XQ, xr, xk, x0, y0, W, H);
+        __syncthreads();
+        if (!(dbg & 2) && tid < 128 && x0 + (tid & 31) < W)  // y pass: (column, plane)
+            gf_ychain<RR>(xo + (tid >> 5) * R * XQ + (tid & 31), y0, H);
+        __syncthreads();
+        if (!(dbg & 4)) {
+            const int d = dloc0 + s;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int yy = tid & 31, jj = (tid >> 5) + 8 * u;
+                // box(b), box(a_r), box(a_g), box(a_b)
+                const float q = xo[yy * XQ + jj] + xo[(R + yy) * XQ + jj] * gr[u] + xo[(2 * R + yy) * XQ + jj] * gg[u] +
+                                xo[(3 * R + yy) * XQ + jj] * gb[u];
+                if (best[u] >= 0 && best[u] == d - 1) nxt[u] = q;  // the winner's right neighbour
+                if (q < mn[u]) {
+                    mn[u] = q;
+                    best[u] = d;
+                    pre[u] = d == 0 ? 0.0f : pq[u];
+                    nxt[u] = 0.0f;
+                }
+                pq[u] = q;
+            }
+        }
+        __syncthreads();
     }
-    st.mn[i] = mn;
-    st.best[i] = best;
-    st.pre[i] = pre;
-    st.nxt[i] = nxt;
-    st.prevq[i] = pq;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (own[u]) {
+            wst.mn[pix[u]] = mn[u];
+            wst.best[pix[u]] = best[u];
+            wst.pre[pix[u]] = pre[u];
+            wst.nxt[pix[u]] = nxt[u];
+            wst.prevq[pix[u]] = pq[u];
+        }
 }
 
-static bool gf_fused(int r) {
-    return r == 9 && getenv("SM_GF_UNFUSED") == nullptr;  // read per batch: tests toggle it
-}
+bool gf_fused(int r) { return r == 9 && getenv("SM_GF_UNFUSED") == nullptr; }  // read per call: tests toggle it
+
+size_t gf_band_plane(int W, int H) { return (size_t)((H + 31) / 32) * 32 * W; }
 
 static hipError_t launch_gf_batch_fused(hipStream_t st, const float* cost, const uint32_t* bgrx, const float* stats, int W,
                                         int H, int S, int dloc0, float* pl, float* tmp, GfStateArgs sa) {
-    constexpr int RR = 9, TX = 32;
-    static_assert(GfTile<RR, TX>::LDS <= 81920, "two workgroups per CU");
+    constexpr int RR = 9;
     const size_t N = (size_t)W * H;
-    const int nty = (H + 31) / 32, ntx = (W + TX - 1) / TX;
-    const int n = ntx * nty * S;  // work items (tile, slice), slice fastest
-    // two resident workgroups per CU (LDS), each looping over n / G items
-    const char* e = getenv("SM_GF_WGS");
-    int G = e ? atoi(e) : 512;
-    G = std::max(8, std::min(G, (n + 7) & ~7)) & ~7;
-    float4* ab = reinterpret_cast<float4*>(pl);  // [S][N] float4 in the 4S planes
-    hipLaunchKernelGGL((k_gf_box1_ab<RR, TX>), dim3(G), dim3(4 * TX), 0, st, cost, bgrx, stats, ab, W, H, N, S, ntx, n);
-    hipLaunchKernelGGL((k_gf_box2_q<RR, TX>), dim3(G), dim3(4 * TX), 0, st, ab, bgrx, tmp, W, H, N, S, ntx, n);
+    const int nty = (H + 31) / 32, ntx = (W + 31) / 32;
+    const size_t NS = gf_band_plane(W, H);
+    float4* ab = reinterpret_cast<float4*>(pl);  // [S][NS] float4, row band layout
+    const char* e = getenv("SM_GF_DBG");  // timing probes only (wrong results): 2 no y pass, 4 no epilogue
+    const int dbg = e ? atoi(e) : 0;
+    const int ntiles = ntx * nty;  // one workgroup per 32 x 32 tile, looping over the batch's slices
+    hipLaunchKernelGGL((k_gf_box1_ab<RR>), dim3((ntiles + 7) & ~7), dim3(256), 0, st, cost, bgrx, stats, ab, W, H, N, NS, S,
+                       ntx, ntiles, dbg);
     const GfState gs{sa.mn, sa.best, sa.pre, sa.nxt, sa.prevq};
-    hipLaunchKernelGGL(k_gf_wta, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, tmp, gs, N, S, dloc0);
+    hipLaunchKernelGGL((k_gf_box2_q_wta<RR>), dim3((ntiles + 7) & ~7), dim3(256), 0, st, ab, bgrx, gs, W, H, NS, S, dloc0, ntx,
+                       ntiles, dbg);
+    (void)tmp;  // q never leaves the registers
     return hipGetLastError();
 }
 
@@ -669,7 +655,10 @@ hipError_t launch_gf_guide(hipStream_t st, const uint32_t* bgrx, int W, int H, i
     const size_t N = (size_t)W * H;
     hipLaunchKernelGGL(k_gf_guide_in, pix_grid1(N), dim3(256), 0, st, bgrx, planes, N);
     box(st, planes, tmp, means, W, H, r, 9);
-    hipLaunchKernelGGL(k_gf_stats, pix_grid1(N), dim3(256), 0, st, means, stats, N, eps);
+    // the fused path reads the statistics in the row band layout
+    const bool band = gf_fused(r);
+    hipLaunchKernelGGL(k_gf_stats, pix_grid1(N), dim3(256), 0, st, means, stats, N, eps, W, band ? 1 : 0,
+                       band ? gf_band_plane(W, H) : N);
     return hipGetLastError();
 }
 

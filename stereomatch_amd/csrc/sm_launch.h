@@ -124,6 +124,10 @@ hipError_t launch_gf_guide(hipStream_t st, const uint32_t* bgrx, int W, int H, i
 hipError_t launch_gf_batch(hipStream_t st, const float* cost, const uint32_t* bgrx, const float* stats, int W, int H, int r,
                            int S, int dloc0, float* pl, float* tmp, GfStateArgs sa);
 hipError_t launch_gf_init(hipStream_t st, GfStateArgs sa, size_t N);
+// the fused tile path (radius 9) keeps its statistics and (b, a) planes in the row band layout:
+// planes of gf_band_plane(W, H) elements
+bool gf_fused(int r);
+size_t gf_band_plane(int W, int H);
 hipError_t launch_gf_out(hipStream_t st, GfStateArgs sa, size_t N, int dglob0, int dtot, int sub, int32_t* idx, double* minc,
                          float* disp);
 
