@@ -1375,7 +1375,9 @@ sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
         ++rounds;
         ++ctx->pms_stats.spec_rounds;
         const size_t K1 = (size_t)K + 1;
-        HIPC(launch_pms_guess(ctx->st, d, t_lo));
+        // the draws trees [t_lo, K) can consume: their propagation draws + 4 per refinement level
+        const long long wn = (long long)(f.nb_start[K] - f.nb_start[t_lo]) + 4ll * sm_pms_levels(d.Dmax) * (K - t_lo) + 8;
+        HIPC(launch_pms_guess(ctx->st, d, t_lo, wn));
         HIPC(launch_pms_prop_setup(ctx->st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
         for (int r = R - 1; r >= 0; --r)
             HIPC(launch_pms_walk(ctx->st, d, 0, true, r, f.rt_item[r * K1 + t_lo], f.rt_item[r * K1 + K]));

@@ -57,7 +57,8 @@ hipError_t launch_pms_prop_one(hipStream_t st, const PmsDev& d, int t, int deg);
 hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t);
 // speculative iteration over trees [t_lo, K): every tree at once from the guessed offsets and the
 // labels at the start of the iteration, then validation (sm_pms.hip "Speculation")
-hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo);
+// wn: stream floats from off[0] a pass can consume (staged in LDS when the window fits)
+hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long wn);
 hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int total_deg);
 hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi);
 hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);

@@ -110,11 +110,36 @@ __device__ __forceinline__ void phase_labels(const PmsDev& d, int phase, int t, 
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Chunk metadata staged across the wave: the PmsRow words of rows [first, first + n) (10 dwords
+// each, n <= PMS_CH), word j of the block in lane j (m0) or lane j - 64 (m1).  One coalesced load per
+// lane instead of a chain of per-field loads; the walkers read fields with v_readlane (uniform index).
+struct ChunkMeta {
+    uint32_t m0, m1;
+};
+static_assert(sizeof(PmsRow) == 40, "PmsRow is 10 dwords");
+static_assert(PMS_CH * 10 <= 128, "a chunk's metadata fits two words per lane");
+
+__device__ __forceinline__ ChunkMeta meta_load(const PmsRow* rows, int first, int n) {
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(rows + first);
+    const int lane = (int)(threadIdx.x & 63), nd = n * 10;
+    ChunkMeta m;
+    m.m0 = b[lane < nd ? lane : 0];  // unconditional (clamped) loads
+    m.m1 = b[lane + 64 < nd ? lane + 64 : 0];
+    return m;
+}
+
+__device__ __forceinline__ uint32_t meta_dw(const ChunkMeta& m, int j) {  // j wave-uniform
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)m.m0, j & 63);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)m.m1, j & 63);
+    return j < 64 ? a : b;
+}
+
 // Leaf->root walk of one heavy path for proposals [64*chunk, 64*chunk+64), bottom to head.  A node's
 // value folds its children in descending BFS id, the heavy child (the row below, walked just before)
-// from a register, the light ones from their rows (finished in a deeper round).  Every load of a chunk
-// of PMS_CH nodes (rows, light children, cost rows) is issued before its serial part, which reads
-// only registers and the LDS weight tables sS / sS2.
+// from a register, the light ones from their rows (finished in a deeper round).  Software-pipelined
+// in chunks of PMS_CH nodes: a chunk's light-child rows and cost-row words are issued from metadata
+// staged during the previous chunk, then the next chunk's metadata, so each chunk pays one memory
+// latency; the serial part reads only registers and the LDS weight tables sS / sS2.
 __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phase, int path, int chunk) {
     const PmsPath pa = d.paths[path];
     const int t = uni(pa.tree);
@@ -128,9 +153,12 @@ __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phas
     const int ts = d.tree_start[t], pt = d.tree_pt[t];
     double* __restrict__ A = d.A + d.tree_abase[t] + j;
     const int row0 = uni(pa.row), len = uni(pa.len);
+    int i0 = len - 1;                                       // top (last walked) index of this chunk
+    int lo = i0 - PMS_CH + 1 > 0 ? i0 - PMS_CH + 1 : 0;     // its first index
+    ChunkMeta mc = meta_load(d.rows, row0 + lo, i0 - lo + 1);
     double x = 0.0;
-    for (int i0 = len - 1; i0 >= 0; i0 -= PMS_CH) {
-        const int n = i0 + 1 < PMS_CH ? i0 + 1 : PMS_CH;
+    while (i0 >= 0) {
+        const int n = i0 - lo + 1;
         double cv[PMS_CH][4];
         float cost[PMS_CH];
         int nch[PMS_CH], hk[PMS_CH], wc[PMS_CH][4];
@@ -138,17 +166,28 @@ __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phas
         for (int k = 0; k < PMS_CH; ++k) {
             nch[k] = 0;
             if (k >= n) continue;
-            const PmsRow m = d.rows[row0 + i0 - k];
-            nch[k] = m.nch;
-            hk[k] = m.hk;
+            const int w0 = (i0 - k - lo) * 10;  // node row0 + i0 - k
+            const uint32_t w6 = meta_dw(mc, w0 + 6), w7 = meta_dw(mc, w0 + 7), w8 = meta_dw(mc, w0 + 8);
+            const uint32_t w9 = meta_dw(mc, w0 + 9);
+            nch[k] = (int)((w6 >> 16) & 255u);
+            hk[k] = (int)(w6 >> 24);
+            wc[k][0] = (int)(w7 & 0xFFFFu);
+            wc[k][1] = (int)(w7 >> 16);
+            wc[k][2] = (int)(w8 & 0xFFFFu);
+            wc[k][3] = (int)(w8 >> 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                wc[k][q] = m.wch[q];
                 cv[k][q] = 0.0;
-                if (q < m.nch && q != m.hk && act) cv[k][q] = A[(size_t)(m.child[q] - ts) * pt];
+                if (q < nch[k] && q != hk[k] && act) cv[k][q] = A[(size_t)((int)meta_dw(mc, w0 + 2 + q) - ts) * pt];
             }
-            cost[k] = act ? label_cost(d.vol, d.Dv, d.Dmax, L.x, L.y, L.z, m.pix, (float)m.x, (float)m.y) : 0.0f;
+            const int pix = (int)meta_dw(mc, w0);
+            cost[k] = act ? label_cost(d.vol, d.Dv, d.Dmax, L.x, L.y, L.z, pix, (float)(w9 & 0xFFFFu), (float)(w9 >> 16))
+                          : 0.0f;
         }
+        const int i0n = lo - 1;
+        const int lon = i0n - PMS_CH + 1 > 0 ? i0n - PMS_CH + 1 : 0;
+        ChunkMeta mn = mc;
+        if (i0n >= 0) mn = meta_load(d.rows, row0 + lon, i0n - lon + 1);
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
             if (k >= n) break;
@@ -165,11 +204,15 @@ __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phas
             x = (double)cost[k] + acc;  // A[v] = C + A[v] (0x40fac5)
             if (act) A[(size_t)(row0 + i0 - k - ts) * pt] = x;
         }
+        mc = mn;
+        i0 = i0n;
+        lo = lon;
     }
 }
 
 // Root->leaf walk of one heavy path, head to bottom: A(c) = fma(S_c, A(p), S2_c * A_up(c)) in place
-// (0x40fbb4-0x40fbbd); a tree root keeps A_up.
+// (0x40fbb4-0x40fbbd); a tree root keeps A_up.  The next chunk's A_up rows and weights are loaded
+// while the current chunk runs.
 __device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
                           int path, int chunk) {
     const PmsPath pa = d.paths[path];
@@ -184,31 +227,50 @@ __device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const 
     double* __restrict__ A = d.A + d.tree_abase[t] + j;
     const int row0 = uni(pa.row), len = uni(pa.len);
     const int parent = uni(d.rows[row0].parent);
-    double y = 0.0;
-    for (int i0 = 0; i0 < len; i0 += PMS_CH) {
-        const int n = len - i0 < PMS_CH ? len - i0 : PMS_CH;
-        double u[PMS_CH];
-        int w[PMS_CH];
-        double pv = 0.0;
-        if (i0 == 0 && parent >= 0 && act) pv = A[(size_t)(parent - ts) * pt];
+    const int lane = (int)(threadIdx.x & 63);
+    // weights of a chunk: lane k holds rows[row0 + i0 + k].w
+    auto wload = [&](int i0, int n) {
+        const int r = row0 + i0 + (lane < n ? lane : 0);
+        return (int)d.rows[r].w;
+    };
+    auto uload = [&](double (&u)[PMS_CH], int i0, int n) {
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
-            w[k] = 0;
-            if (k >= n) continue;
-            w[k] = d.rows[row0 + i0 + k].w;
-            u[k] = act ? A[(size_t)(row0 + i0 + k - ts) * pt] : 0.0;
+            const int r = row0 + i0 + (k < n ? k : 0);  // clamped: unconditional loads
+            u[k] = act ? A[(size_t)(r - ts) * pt] : 0.0;
+        }
+    };
+    double y = 0.0;
+    if (parent >= 0 && act) y = A[(size_t)(parent - ts) * pt];
+    int i0 = 0, n = len < PMS_CH ? len : PMS_CH;
+    double uc[PMS_CH];
+    uload(uc, 0, n);
+    int wl = wload(0, n);
+    while (i0 < len) {
+        const int i0n = i0 + n, nn = len - i0n < PMS_CH ? len - i0n : PMS_CH;
+        double un[PMS_CH];
+        int wn = wl;
+        if (i0n < len) {
+            uload(un, i0n, nn);
+            wn = wload(i0n, nn);
         }
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
             if (k >= n) break;
-            const double S = sS[w[k]], S2 = sS2[w[k]];
+            const int w = __builtin_amdgcn_readlane(wl, k);
+            const double S = sS[w], S2 = sS2[w];
             if (i0 + k == 0) {
-                y = parent >= 0 ? fma(S, pv, S2 * u[0]) : u[0];
+                y = parent >= 0 ? fma(S, y, S2 * uc[0]) : uc[0];
             } else {
-                y = fma(S, y, S2 * u[k]);
+                y = fma(S, y, S2 * uc[k]);
             }
             if (act) A[(size_t)(row0 + i0 + k - ts) * pt] = y;
         }
+#pragma unroll
+        for (int k = 0; k < PMS_CH; ++k) uc[k] = un[k];
+        wl = wn;
+        i0 = i0n;
+        n = nn;
     }
 }
 
@@ -269,6 +331,33 @@ __device__ void prop_label(const PmsDev& d, int t, long long o, int j) {
 
 // Random refinement of tree t (:582-625) with its draws from offset o: the labels of the in-range levels
 // (written compacted when `write`) and the number of draws.  The test pixel's label is read as it is now.
+// the refinement's starting disparity dd of tree t (its test pixel's current plane at that pixel)
+__device__ float ref_dd(const PmsDev& d, int t) {
+    const int ts = d.tree_start[t], sz = d.tree_start[t + 1] - ts;
+    const int tp = d.bfs_pix[ts + (int)((uint32_t)d.rnd[t] % (uint32_t)sz)];
+    const float px = (float)(tp % d.W), py = (float)(tp / d.W);
+    return fmaf(d.abc[3 * (size_t)tp], px, d.abc[3 * (size_t)tp + 1] * py) + d.abc[3 * (size_t)tp + 2];
+}
+
+// draws of tree t's refinement from offset o given dd (ref_levels without the labels); dice(k) reads
+// the stream
+template <class Dice>
+__device__ int ref_count(const PmsDev& d, float dd, long long o, Dice dice) {
+    const float fmax = (float)d.Dmax;
+    float max_d = 0.5f * fmax;
+    long long k = o;
+    for (; max_d > 0.1f; max_d *= 0.5f) {
+        if (k + 4 > d.dice_n) {
+            atomicOr(d.err, 4u);
+            break;
+        }
+        const float rd = fmaf(dice(k++), max_d, dd);
+        if (rd < 0.0f || rd > fmax) continue;
+        k += 3;
+    }
+    return (int)(k - o);
+}
+
 __device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
     const int ts = d.tree_start[t], sz = d.tree_start[t + 1] - ts;
     const int tp = d.bfs_pix[ts + (int)((uint32_t)d.rnd[t] % (uint32_t)sz)];  // std::rand() % size()
@@ -380,13 +469,31 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
 // ----------------------------------------------------------------------------- speculation
 // Guessed offsets of trees [t_lo, K) from the exact offset of t_lo (off[0]): each tree's refinement
 // draws counted from the label its test pixel has now, i.e. assuming propagation leaves it unchanged.
-__global__ void k_pms_guess(PmsDev d, int t_lo) {
-    if (threadIdx.x != 0) return;
-    long long o = d.off[0];
+// The offsets are a serial chain (a tree's draws depend on the dice at its offset), so the rest is
+// taken off it: every tree's starting disparity in parallel, and the stream window the chain can
+// reach (wn floats, when it fits) staged in LDS, so each link reads LDS instead of global memory.
+__global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, int staged, long long wn) {
+    extern __shared__ float gsm[];
+    const int nt = d.K - t_lo, tid = threadIdx.x;
+    const long long o0 = d.off[0];
+    // staged: per-tree dd and degree in LDS (else computed in the chain); wn: stream floats in LDS
+    float* sdd = gsm;
+    int* sdeg = reinterpret_cast<int*>(gsm + (staged ? nt : 0));
+    float* sdice = gsm + (staged ? 2 * nt : 0);
+    if (staged)
+        for (int i = tid; i < nt; i += blockDim.x) {
+            sdd[i] = ref_dd(d, t_lo + i);
+            sdeg[i] = tree_deg(d, t_lo + i);
+        }
+    for (long long i = tid; i < wn; i += blockDim.x) sdice[i] = o0 + i < d.dice_n ? d.dice[o0 + i] : 0.0f;
+    __syncthreads();
+    if (tid != 0) return;
+    long long o = o0;
     for (int t = t_lo; t < d.K; ++t) {
         d.oguess[t] = o;
-        const int deg = tree_deg(d, t);
-        o += deg + ref_levels(d, t, o + deg, false);
+        const int deg = staged ? sdeg[t - t_lo] : tree_deg(d, t);
+        const float dd = staged ? sdd[t - t_lo] : ref_dd(d, t);
+        o += deg + ref_count(d, dd, o + deg, [&](long long k) { return k - o0 < wn ? sdice[k - o0] : d.dice[k]; });
     }
 }
 
@@ -546,8 +653,16 @@ hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t) {
     return hipGetLastError();
 }
 
-hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo) {
-    hipLaunchKernelGGL(k_pms_guess, dim3(1), dim3(64), 0, st, d, t_lo);
+hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long wn) {
+    const size_t nt = (size_t)(d.K - t_lo);
+    constexpr size_t cap = 150 * 1024;  // LDS bytes
+    const int staged = 2 * nt * 4 <= cap ? 1 : 0;
+    if ((staged * 2 * nt + (size_t)wn) * 4 > cap) wn = 0;  // the chain reads the stream from global memory
+    const size_t lds = (staged * 2 * nt + (size_t)wn) * 4;
+    static const hipError_t attr =  // once per process (thread-safe static initialisation)
+        hipFuncSetAttribute((const void*)k_pms_guess, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k_pms_guess, dim3(1), dim3(1024), lds, st, d, t_lo, staged, wn);
     return hipGetLastError();
 }
 

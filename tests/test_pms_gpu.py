@@ -76,6 +76,18 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, serial):
         assert st["spec_rounds"] >= 6  # calls 2..4 of both views
 
 
+def test_pms_many_trees_bitexact(gpu_ctx):
+    """79k trees (c=5, min_size 2): the speculative offset chain (k_pms_guess) too large to stage its
+    per-tree values in LDS takes them from global memory."""
+    left, right, _ = make_pair(640, 480, 32, index=9)
+    ref = O.stereo3dmst_pms(left, right, 32, iters=2, c=5.0, min_size=2)
+    assert ref["left"]["tree"]["ntrees"] > 20000
+    out, labs, st = run_gpu(gpu_ctx, left, right, 32, 2, 5.0, 2)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+    assert st["spec_rounds"] >= 2
+
+
 def test_pms_max_rounds_fallback(gpu_ctx, monkeypatch):
     """SM_PMS_MAX_ROUNDS=1: a call whose first speculative pass fails finishes in serial order."""
     monkeypatch.setenv("SM_PMS_MAX_ROUNDS", "1")
