@@ -48,6 +48,7 @@ def lib():
         L.orc_lr_check_fill.argtypes = [vp, vp, c_int, c_int, c_int, c_int]
         L.orc_label_to_disp.argtypes = [vp, ctypes.c_long, c_int]
         L.orc_set_agd_contract.argtypes = [c_int]
+        L.orc_set_gf_contract.argtypes = [c_int]
         L.orc_guided_filter.argtypes = [u8p, c_int, c_int, c_int, vp, c_int, c_int, c_float, vp, c_int]
         L.orc_box_mean.argtypes = [vp, vp, c_int, c_int, c_int]
         L.orc_select_disparity.argtypes = [vp, c_int, c_int, c_int, ctypes.c_size_t, c_int, vp, vp, vp]
@@ -130,6 +131,12 @@ def bfs(W, H, wR, wD, mask):
     nt = lib().orc_bfs(W, H, wR, wD, mask, tree_start, node_pix, node_parent, node_w, node_nch, node_child)
     return dict(ntrees=nt, tree_start=tree_start[:nt + 1].copy(), node_pix=node_pix, node_parent=node_parent,
                 node_w=node_w, node_nch=node_nch, node_child=node_child)
+
+
+def set_gf_contract(mode):
+    """1: the guided filter's helper kernels contracted as nvcc's default --fmad=true would (what-if
+    for tools/gf_contraction.py); 0: the shipped, uncontracted restatement."""
+    lib().orc_set_gf_contract(int(mode))
 
 
 def set_agd_contract(mode):

@@ -548,6 +548,13 @@ static void orc_box(const float* in, float* out, float* tmp, int W, int H, int r
  * costVolumeColorGuidedFilterCUDA2Streams (PatchMatchStereoGPU.cu:8251-8470) in source order,
  * no contraction: the guide statistics st[] (mean_r, mean_g, mean_b, inv_rr, inv_rg, inv_rb,
  * inv_gg, inv_gb, inv_bb; see orc_gf_guide) are precomputed. */
+/* g_gf_contract = 1: the helper kernels' a*b +/- c*d chains as nvcc's default --fmad=true would
+ * contract them (the first product of a sum fused, each later product fused into the running sum;
+ * the convention of orc_set_agd_contract) -- a what-if for tools/gf_contraction.py, never the
+ * shipped arithmetic */
+static int g_gf_contract = 0;
+void orc_set_gf_contract(int mode) { g_gf_contract = mode; }
+
 static void orc_gf_slice(const float* p, const float* gr, const float* gg, const float* gb, const float* const* st,
                          int W, int H, int rad, float* q, float* w /* 12 planes of N */) {
     const size_t N = (size_t)W * H;
@@ -563,6 +570,14 @@ static void orc_gf_slice(const float* p, const float* gr, const float* gg, const
     const float *m_r = st[0], *m_g = st[1], *m_b = st[2];
     const float *irr = st[3], *irg = st[4], *irb = st[5], *igg = st[6], *igb = st[7], *ibb = st[8];
     for (size_t i = 0; i < N; ++i) {
+        if (g_gf_contract) {
+            const float cr = fmaf(-m_r[i], mp[i], mr[i]), cg = fmaf(-m_g[i], mp[i], mg[i]), cb = fmaf(-m_b[i], mp[i], mb[i]);
+            ar[i] = fmaf(irb[i], cb, fmaf(irr[i], cr, irg[i] * cg));
+            ag[i] = fmaf(igb[i], cb, fmaf(irg[i], cr, igg[i] * cg));
+            ab[i] = fmaf(ibb[i], cb, fmaf(irb[i], cr, igb[i] * cg));
+            bb[i] = fmaf(-ab[i], m_b[i], fmaf(-ag[i], m_g[i], fmaf(-ar[i], m_r[i], mp[i])));
+            continue;
+        }
         const float cr = mr[i] - m_r[i] * mp[i];                /* Helper3: s1 - s2*s3 */
         const float cg = mg[i] - m_g[i] * mp[i];
         const float cb = mb[i] - m_b[i] * mp[i];
@@ -575,7 +590,9 @@ static void orc_gf_slice(const float* p, const float* gr, const float* gg, const
     orc_box(ag, mg, t, W, H, rad);
     orc_box(ab, mb, t, W, H, rad);
     orc_box(bb, x, t, W, H, rad);
-    for (size_t i = 0; i < N; ++i) q[i] = x[i] + mr[i] * gr[i] + mg[i] * gg[i] + mb[i] * gb[i];  /* Helper5 */
+    for (size_t i = 0; i < N; ++i)                                   /* Helper5 */
+        q[i] = g_gf_contract ? fmaf(mb[i], gb[i], fmaf(mg[i], gg[i], fmaf(mr[i], gr[i], x[i])))
+                             : x[i] + mr[i] * gr[i] + mg[i] * gg[i] + mb[i] * gb[i];
 }
 
 /* guide statistics of one view (PatchMatchStereoGPU.cu:8261-8420), eps added to the diagonal */
@@ -600,6 +617,19 @@ static void orc_gf_guide(const float* gr, const float* gg, const float* gb, int 
         }
     }
     for (size_t i = 0; i < N; ++i) {                              /* Helper1 ... */
+        if (g_gf_contract) {
+            const float irr = fmaf(vgg[i], vbb[i], -(vgb[i] * vgb[i])), igg = fmaf(vrr[i], vbb[i], -(vrb[i] * vrb[i]));
+            const float ibb = fmaf(vrr[i], vgg[i], -(vrg[i] * vrg[i])), irg = fmaf(vgb[i], vrb[i], -(vrg[i] * vbb[i]));
+            const float irb = fmaf(vrg[i], vgb[i], -(vgg[i] * vrb[i])), igb = fmaf(vrb[i], vrg[i], -(vrr[i] * vgb[i]));
+            const float det = fmaf(irb, vrb[i], fmaf(irr, vrr[i], irg * vrg[i]));
+            st[3][i] = irr / det;
+            st[4][i] = irg / det;
+            st[5][i] = irb / det;
+            st[6][i] = igg / det;
+            st[7][i] = igb / det;
+            st[8][i] = ibb / det;
+            continue;
+        }
         float irr = vgg[i] * vbb[i] - vgb[i] * vgb[i];
         float igg = vrr[i] * vbb[i] - vrb[i] * vrb[i];
         float ibb = vrr[i] * vgg[i] - vrg[i] * vrg[i];

@@ -53,6 +53,7 @@ int orc_bfs(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t*
 /* buildCostVolumeSharedMemoryBGR (PatchMatchStereoGPU.cu:1482-1550), slices d0..d1-1:
  * right[d][y][x] (right reference) and left[d][y][x+d]; invalid = 3.0f; the left column
  * the reference never writes (x = W-1, x >= d) is defined as 3.0f. Volumes [(d1-d0)][H][W]. */
+void orc_set_gf_contract(int mode);  /* 1: the guided filter helpers as nvcc --fmad=true would contract them */
 void orc_set_agd_contract(int mode); /* 0: shipped (uncontracted) AGD; 1: nvcc --fmad=true contraction */
 void orc_cost_agd(const uint8_t* left, const uint8_t* right, int W, int H, int stride, int d0, int d1,
                   float* left_vol, float* right_vol, int nthreads);

@@ -80,3 +80,21 @@ def test_select_disparity_rules():
     assert disp[0] == np.float32(1.0) - s
     idx, mn, disp = O.select_disparity(np.full((3, 1, 1), 2e10, np.float32), 0, 3, True)
     assert idx[0] == 0 and disp[0] == 0.0  # nothing below 1e10: -1 -> 0
+
+
+def test_contraction_whatif_is_separate_from_the_shipped_arithmetic():
+    """orc_set_gf_contract(1) (tools/gf_contraction.py's nvcc --fmad=true what-if) changes the filtered
+    costs but stays within float rounding of the shipped result, and setting it back restores the
+    shipped bits."""
+    left, right, _ = make_pair(96, 64, 16, index=4)
+    lv, _ = O.cost_agd(left, right, 0, 16)
+    base = O.guided_filter(left, lv)
+    try:
+        O.set_gf_contract(1)
+        fused = O.guided_filter(left, lv)
+    finally:
+        O.set_gf_contract(0)
+    again = O.guided_filter(left, lv)
+    assert np.array_equal(again.view(np.uint32), base.view(np.uint32))
+    assert not np.array_equal(fused, base)
+    np.testing.assert_allclose(fused, base, rtol=1e-3, atol=1e-3)
