@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/emu
 mkdir -p $O
-B="python bench.py --steps 12 --warmup 3 --no-cpu --no-host-io"
+B="python bench.py --steps 12 --warmup 3 --no-cpu --no-host-io --no-pms"
 timeout -k 10 200 $B --disp 256 > $O/c4_1gpu.log 2>&1 || exit 1
 for spec in "0/8 vd" "0/8 d" "4/8 vd" "0/4 vd" "0/2 vd" "0/2 d"; do
   set -- $spec
