@@ -77,7 +77,8 @@ struct PinnedVec {
 struct PmsState {
     PmsForest f;
     DevBuf rows, rtree, paths, items, rt_path, rt_item, tree_rounds, tree_start, bfs_pix, nb_start, nb, tree_pt, tree_abase,
-        tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result, prof;
+        tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result, prof, cuts, reps,
+        cut_bak, Abak;
     std::vector<int32_t> h_rtree, h_pt, h_lab;
     std::vector<long long> h_abase;
     long long dice_need = 0;
@@ -1229,6 +1230,17 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
     S.h_abase[K] = abase;
     S.h_lab[K] = lab;
     S.dice_need = deg_sum + 4ll * L * K + 8;
+    // pieces: backup offsets of the cut paths' non-head rows (A_up, saved before the down pass)
+    std::vector<long long> cut_bak(std::max<size_t>(f.cuts.size(), 1), 0);
+    long long bak = 0;
+    for (size_t c = 0; c < f.cuts.size(); ++c) {
+        cut_bak[c] = bak;
+        bak += (long long)(f.cuts[c].len - f.piece) * S.h_pt[f.cuts[c].tree];
+    }
+    CHECK(upload_vec(ctx, S.cuts, f.cuts));
+    CHECK(upload_vec(ctx, S.reps, f.reps));
+    CHECK(upload_vec(ctx, S.cut_bak, cut_bak));
+    CHECK(ensure(ctx, S.Abak, (size_t)std::max(bak, 1ll) * 8));
     CHECK(upload_vec(ctx, S.rows, f.rows));
     CHECK(upload_vec(ctx, S.rtree, S.h_rtree));
     CHECK(upload_vec(ctx, S.paths, f.paths));
@@ -1300,6 +1312,11 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     }
     d.slut = P<double>(ctx->slut);
     d.s2lut = P<double>(ctx->s2lut);
+    d.cuts = P<PmsCut>(S.cuts);
+    d.reps = P<PmsRep>(S.reps);
+    d.cut_bak = P<long long>(S.cut_bak);
+    d.Abak = P<double>(S.Abak);
+    d.piece = S.f.piece;
     d.W = ctx->W;
     d.Dv = D;
     d.Dmax = D;
@@ -1308,18 +1325,45 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     return d;
 }
 
+// MST_PMS pieces: heavy paths of at least 2 x this many rows are cut (SM_PMS_PIECE; 0: none).  512
+// balances a piece's walk against the repairs of the pieces above it (~30-60 rows each at C2).
+int pms_piece() {
+    const char* e = getenv("SM_PMS_PIECE");
+    return e ? std::max(0, atoi(e)) : 512;
+}
+
 // trees whose work (nodes x 64-proposal chunks) is at least this run over the whole GPU in serial mode
 long long pms_big_tree() {
     const char* e = getenv("SM_PMS_BIG");
     return e ? std::max(1ll, atoll(e)) : 32768;
 }
 
+// One phase (0: propagation, 1: refinement) of trees [t_lo, t_hi) over the whole GPU: the up rounds
+// deepest first, the cut paths' pieces repaired after each round, the cut paths' A_up rows saved, the
+// down rounds root first (repaired likewise), then the per-pixel update.
+sm_status pms_phase(sm_ctx* ctx, int v, const PmsDev& d, int phase, int t_lo, int t_hi) {
+    const PmsForest& f = ctx->pms[v].f;
+    const size_t K1 = (size_t)f.K + 1;
+    int R = 0;
+    for (int t = t_lo; t < t_hi; ++t) R = std::max(R, f.tree_rounds[t]);
+    const std::vector<int32_t>& rt = phase == 0 ? f.rt_item : f.rt_path;
+    for (int r = R - 1; r >= 0; --r) {
+        HIPC(launch_pms_walk(ctx->st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
+        HIPC(launch_pms_repair(ctx->st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
+    }
+    HIPC(launch_pms_cut_backup(ctx->st, d, f.tree_cut[t_lo], f.tree_cut[t_hi]));
+    for (int r = 0; r < R; ++r) {
+        HIPC(launch_pms_walk(ctx->st, d, phase, false, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
+        HIPC(launch_pms_repair(ctx->st, d, phase, false, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
+    }
+    HIPC(launch_pms_update(ctx->st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
+    return SM_OK;
+}
+
 // Trees [t0, t1) in the reference's order from the dice offset *off.  Runs of small trees go to one
 // workgroup (k_pms_serial); a large tree's phases are launched over the whole GPU, round by round.
 sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) {
     const PmsForest& f = ctx->pms[v].f;
-    const int K = f.K;
-    const size_t K1 = (size_t)K + 1;
     const long long big = pms_big_tree();
     int run = t0;
     for (int t = t0; t <= t1; ++t) {
@@ -1327,28 +1371,18 @@ sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) 
         if (t < t1) {
             const long long n = f.tree_start[t + 1] - f.tree_start[t];
             const int deg = f.nb_start[t + 1] - f.nb_start[t];
-            is_big = n * ((std::max(deg, 1) + 63) / 64) >= big;
+            // a tree with cut paths needs the repair launches: never in the one-workgroup kernel
+            is_big = n * ((std::max(deg, 1) + 63) / 64) >= big || f.tree_cut[t + 1] > f.tree_cut[t];
         }
         if (t < t1 && !is_big) continue;
         HIPC(launch_pms_serial(ctx->st, d, run, t));
         run = t + 1;
         if (t == t1) break;
-        const int R = f.tree_rounds[t];
         const int deg = f.nb_start[t + 1] - f.nb_start[t];
         HIPC(launch_pms_prop_one(ctx->st, d, t, deg));
-        if (deg > 0) {
-            for (int r = R - 1; r >= 0; --r)
-                HIPC(launch_pms_walk(ctx->st, d, 0, true, r, f.rt_item[r * K1 + t], f.rt_item[r * K1 + t + 1]));
-            for (int r = 0; r < R; ++r)
-                HIPC(launch_pms_walk(ctx->st, d, 0, false, r, f.rt_item[r * K1 + t], f.rt_item[r * K1 + t + 1]));
-            HIPC(launch_pms_update(ctx->st, d, 0, f.tree_start[t], f.tree_start[t + 1]));
-        }
+        if (deg > 0) CHECK(pms_phase(ctx, v, d, 0, t, t + 1));
         HIPC(launch_pms_ref_one(ctx->st, d, t));
-        for (int r = R - 1; r >= 0; --r)
-            HIPC(launch_pms_walk(ctx->st, d, 1, true, r, f.rt_path[r * K1 + t], f.rt_path[r * K1 + t + 1]));
-        for (int r = 0; r < R; ++r)
-            HIPC(launch_pms_walk(ctx->st, d, 1, false, r, f.rt_path[r * K1 + t], f.rt_path[r * K1 + t + 1]));
-        HIPC(launch_pms_update(ctx->st, d, 1, f.tree_start[t], f.tree_start[t + 1]));
+        CHECK(pms_phase(ctx, v, d, 1, t, t + 1));
     }
     return SM_OK;
 }
@@ -1360,7 +1394,7 @@ sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) 
 sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
     PmsState& S = ctx->pms[v];
     const PmsForest& f = S.f;
-    const int K = f.K, R = f.nrounds;
+    const int K = f.K;
     const size_t N = (size_t)f.W * f.H;
     const int max_rounds = pms_max_rounds();
     HIPC(launch_pms_backup(ctx->st, d, N));
@@ -1374,22 +1408,13 @@ sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
         }
         ++rounds;
         ++ctx->pms_stats.spec_rounds;
-        const size_t K1 = (size_t)K + 1;
         // the draws trees [t_lo, K) can consume: their propagation draws + 4 per refinement level
         const long long wn = (long long)(f.nb_start[K] - f.nb_start[t_lo]) + 4ll * sm_pms_levels(d.Dmax) * (K - t_lo) + 8;
         HIPC(launch_pms_guess(ctx->st, d, t_lo, wn));
         HIPC(launch_pms_prop_setup(ctx->st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
-        for (int r = R - 1; r >= 0; --r)
-            HIPC(launch_pms_walk(ctx->st, d, 0, true, r, f.rt_item[r * K1 + t_lo], f.rt_item[r * K1 + K]));
-        for (int r = 0; r < R; ++r)
-            HIPC(launch_pms_walk(ctx->st, d, 0, false, r, f.rt_item[r * K1 + t_lo], f.rt_item[r * K1 + K]));
-        HIPC(launch_pms_update(ctx->st, d, 0, f.tree_start[t_lo], (int)N));
+        CHECK(pms_phase(ctx, v, d, 0, t_lo, K));
         HIPC(launch_pms_ref_setup(ctx->st, d, t_lo));
-        for (int r = R - 1; r >= 0; --r)
-            HIPC(launch_pms_walk(ctx->st, d, 1, true, r, f.rt_path[r * K1 + t_lo], f.rt_path[r * K1 + K]));
-        for (int r = 0; r < R; ++r)
-            HIPC(launch_pms_walk(ctx->st, d, 1, false, r, f.rt_path[r * K1 + t_lo], f.rt_path[r * K1 + K]));
-        HIPC(launch_pms_update(ctx->st, d, 1, f.tree_start[t_lo], (int)N));
+        CHECK(pms_phase(ctx, v, d, 1, t_lo, K));
         HIPC(launch_pms_validate(ctx->st, d, t_lo));
         HIPC(hipMemcpyAsync(ctx->h_pms_res, S.result.p, 16, hipMemcpyDeviceToHost, ctx->st));
         HIPC(hipStreamSynchronize(ctx->st));
@@ -1427,7 +1452,8 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                 mR[i] = ctx->h_m[v][0][i] && ctx->h_fw[v][0][i] != SM_VIRTUAL_W;
                 mD[i] = ctx->h_m[v][1][i] && ctx->h_fw[v][1][i] != SM_VIRTUAL_W;
             }
-            pms_build_forest(W, H, ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), mR.data(), mD.data(), ctx->pms[v].f);
+            pms_build_forest(W, H, ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), mR.data(), mD.data(), ctx->pms[v].f,
+                             pms_piece());
         };
         std::thread other(build, 1);
         build(0);

@@ -45,7 +45,13 @@ struct PmsDev {
     long long* prof;             // SM_PMS_PROF: k_pms_serial segment totals (nullptr: off)
     const double* slut;
     const double* s2lut;
-    int W, Dv, Dmax, K, nrounds;
+    // pieces (sm_pms_host.h PmsCut): cut paths, repair items, per-cut backup offsets into Abak (the
+    // A_up rows of a cut path's non-head pieces, saved before the down pass overwrites them)
+    const PmsCut* cuts;
+    const PmsRep* reps;
+    const long long* cut_bak;
+    double* Abak;
+    int W, Dv, Dmax, K, nrounds, piece;
 };
 
 // serial: trees [t0, t1) one after the other in one workgroup (the reference's order), starting at the
@@ -63,6 +69,10 @@ hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int 
 hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi);
 hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);
 hipError_t launch_pms_ref_setup(hipStream_t st, const PmsDev& d, int t_lo);
+// pieces: re-walk the cut paths' guessed pieces from their exact neighbours (repair items [lo, hi)),
+// and save the A_up rows of cuts [c_lo, c_hi) before the down pass
+hipError_t launch_pms_repair(hipStream_t st, const PmsDev& d, int phase, bool up, int lo, int hi);
+hipError_t launch_pms_cut_backup(hipStream_t st, const PmsDev& d, int c_lo, int c_hi);
 hipError_t launch_pms_validate(hipStream_t st, const PmsDev& d, int t_lo);
 hipError_t launch_pms_restore(hipStream_t st, const PmsDev& d, int row_lo, int row_hi);
 hipError_t launch_pms_backup(hipStream_t st, const PmsDev& d, size_t N);

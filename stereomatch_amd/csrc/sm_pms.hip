@@ -134,15 +134,20 @@ __device__ __forceinline__ uint32_t meta_dw(const ChunkMeta& m, int j) {  // j w
     return j < 64 ? a : b;
 }
 
-// Leaf->root walk of one heavy path for proposals [64*chunk, 64*chunk+64), bottom to head.  A node's
-// value folds its children in descending BFS id, the heavy child (the row below, walked just before)
-// from a register, the light ones from their rows (finished in a deeper round).  Software-pipelined
-// in chunks of PMS_CH nodes: a chunk's light-child rows and cost-row words are issued from metadata
-// staged during the previous chunk, then the next chunk's metadata, so each chunk pays one memory
-// latency; the serial part reads only registers and the LDS weight tables sS / sS2.
-__device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phase, int path, int chunk) {
-    const PmsPath pa = d.paths[path];
-    const int t = uni(pa.tree);
+// Leaf->root walk of rows [top, bot] of tree t (a heavy path or a piece of one) for proposals
+// [64*chunk, 64*chunk+64), bottom to head, from x0 = the value of the bottom row's heavy child (a
+// path's bottom is a leaf; a cut piece's bottom takes the guess 0, or in a repair the exact row of
+// the piece below).  A node's value folds its children in descending BFS id, the heavy child (the row
+// below, walked just before) from a register, the light ones from their rows (finished in a deeper
+// round).  Software-pipelined in chunks of PMS_CH nodes: a chunk's light-child rows and cost-row
+// words are issued from metadata staged during the previous chunk, then the next chunk's metadata,
+// so each chunk pays one memory latency; the serial part reads only registers and the LDS weight
+// tables sS / sS2.  REPAIR: the stored rows are loaded with the chunk, and the walk stops at the
+// first node where every lane's recomputed value equals the stored one bitwise (two trajectories of
+// the recurrence that agree at a node agree from there on); until then it overwrites.
+template <bool REPAIR>
+__device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phase, int t, int top, int bot, int chunk,
+                        double x0) {
     int P, base;
     phase_labels(d, phase, t, P, base);
     const int j = chunk * 64 + (int)(threadIdx.x & 63);
@@ -152,15 +157,16 @@ __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phas
     if (act) L = d.lab[base + j];
     const int ts = d.tree_start[t], pt = d.tree_pt[t];
     double* __restrict__ A = d.A + d.tree_abase[t] + j;
-    const int row0 = uni(pa.row), len = uni(pa.len);
+    const int row0 = top, len = bot - top + 1;
     int i0 = len - 1;                                       // top (last walked) index of this chunk
     int lo = i0 - PMS_CH + 1 > 0 ? i0 - PMS_CH + 1 : 0;     // its first index
     ChunkMeta mc = meta_load(d.rows, row0 + lo, i0 - lo + 1);
-    double x = 0.0;
+    double x = x0;
     while (i0 >= 0) {
         const int n = i0 - lo + 1;
         double cv[PMS_CH][4];
         float cost[PMS_CH];
+        double old[PMS_CH];
         int nch[PMS_CH], hk[PMS_CH], wc[PMS_CH][4];
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
@@ -183,6 +189,7 @@ __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phas
             const int pix = (int)meta_dw(mc, w0);
             cost[k] = act ? label_cost(d.vol, d.Dv, d.Dmax, L.x, L.y, L.z, pix, (float)(w9 & 0xFFFFu), (float)(w9 >> 16))
                           : 0.0f;
+            if (REPAIR) old[k] = act ? A[(size_t)(row0 + i0 - k - ts) * pt] : 0.0;
         }
         const int i0n = lo - 1;
         const int lon = i0n - PMS_CH + 1 > 0 ? i0n - PMS_CH + 1 : 0;
@@ -202,7 +209,13 @@ __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phas
                 acc = fma(v, sv[q], acc);  // A[parent] = fma(A[v], S, A[parent]) (0x40fad5)
             }
             x = (double)cost[k] + acc;  // A[v] = C + A[v] (0x40fac5)
-            if (act) A[(size_t)(row0 + i0 - k - ts) * pt] = x;
+            if (REPAIR) {
+                const bool same = !act || __double_as_longlong(x) == __double_as_longlong(old[k]);
+                if (__all(same)) return;
+                if (!same) A[(size_t)(row0 + i0 - k - ts) * pt] = x;
+            } else if (act) {
+                A[(size_t)(row0 + i0 - k - ts) * pt] = x;
+            }
         }
         mc = mn;
         i0 = i0n;
@@ -210,13 +223,20 @@ __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phas
     }
 }
 
-// Root->leaf walk of one heavy path, head to bottom: A(c) = fma(S_c, A(p), S2_c * A_up(c)) in place
-// (0x40fbb4-0x40fbbd); a tree root keeps A_up.  The next chunk's A_up rows and weights are loaded
-// while the current chunk runs.
-__device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
-                          int path, int chunk) {
+__device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phase, int path, int chunk) {
     const PmsPath pa = d.paths[path];
-    const int t = uni(pa.tree);
+    up_walk<false>(d, sS, phase, uni(pa.tree), uni(pa.row), uni(pa.row) + uni(pa.len) - 1, chunk, 0.0);
+}
+
+// Root->leaf walk of rows [top, bot] of tree t, head to bottom: A(c) = fma(S_c, A(p), S2_c * A_up(c))
+// in place (0x40fbb4-0x40fbbd); a tree root keeps A_up.  The head's parent value: normally the row
+// A[parent] holds (a cut piece's head: whatever its neighbour piece has written so far, a guess);
+// REPAIR: yin, the exact row of the piece above, with A_up read from ub (the rows' backup, since the
+// speculative walk overwrote them) and the walk stopping at the first all-lanes bitwise agreement.
+// The next chunk's A_up rows and weights are loaded while the current chunk runs.
+template <bool REPAIR>
+__device__ void down_walk(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
+                          int t, int top, int bot, int chunk, double yin, const double* __restrict__ ub) {
     int P, base;
     phase_labels(d, phase, t, P, base);
     (void)base;
@@ -225,33 +245,38 @@ __device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const 
     const bool act = j < P;
     const int ts = d.tree_start[t], pt = d.tree_pt[t];
     double* __restrict__ A = d.A + d.tree_abase[t] + j;
-    const int row0 = uni(pa.row), len = uni(pa.len);
-    const int parent = uni(d.rows[row0].parent);
+    const int row0 = top, len = bot - top + 1;
+    const int parent = REPAIR ? row0 - 1 : uni(d.rows[row0].parent);
     const int lane = (int)(threadIdx.x & 63);
     // weights of a chunk: lane k holds rows[row0 + i0 + k].w
     auto wload = [&](int i0, int n) {
         const int r = row0 + i0 + (lane < n ? lane : 0);
         return (int)d.rows[r].w;
     };
-    auto uload = [&](double (&u)[PMS_CH], int i0, int n) {
+    auto uload = [&](double (&u)[PMS_CH], double (&o)[PMS_CH], int i0, int n) {
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
-            const int r = row0 + i0 + (k < n ? k : 0);  // clamped: unconditional loads
-            u[k] = act ? A[(size_t)(r - ts) * pt] : 0.0;
+            const int i = i0 + (k < n ? k : 0);  // clamped: unconditional loads
+            if (REPAIR) {
+                u[k] = act ? ub[(size_t)i * pt + j] : 0.0;
+                o[k] = act ? A[(size_t)(row0 + i - ts) * pt] : 0.0;
+            } else {
+                u[k] = act ? A[(size_t)(row0 + i - ts) * pt] : 0.0;
+            }
         }
     };
-    double y = 0.0;
-    if (parent >= 0 && act) y = A[(size_t)(parent - ts) * pt];
+    double y = REPAIR ? yin : 0.0;
+    if (!REPAIR && parent >= 0 && act) y = A[(size_t)(parent - ts) * pt];
     int i0 = 0, n = len < PMS_CH ? len : PMS_CH;
-    double uc[PMS_CH];
-    uload(uc, 0, n);
+    double uc[PMS_CH], oc[PMS_CH];
+    uload(uc, oc, 0, n);
     int wl = wload(0, n);
     while (i0 < len) {
         const int i0n = i0 + n, nn = len - i0n < PMS_CH ? len - i0n : PMS_CH;
-        double un[PMS_CH];
+        double un[PMS_CH], on[PMS_CH];
         int wn = wl;
         if (i0n < len) {
-            uload(un, i0n, nn);
+            uload(un, on, i0n, nn);
             wn = wload(i0n, nn);
         }
 #pragma unroll
@@ -264,14 +289,29 @@ __device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const 
             } else {
                 y = fma(S, y, S2 * uc[k]);
             }
-            if (act) A[(size_t)(row0 + i0 + k - ts) * pt] = y;
+            if (REPAIR) {
+                const bool same = !act || __double_as_longlong(y) == __double_as_longlong(oc[k]);
+                if (__all(same)) return;
+                if (!same) A[(size_t)(row0 + i0 + k - ts) * pt] = y;
+            } else if (act) {
+                A[(size_t)(row0 + i0 + k - ts) * pt] = y;
+            }
         }
 #pragma unroll
-        for (int k = 0; k < PMS_CH; ++k) uc[k] = un[k];
+        for (int k = 0; k < PMS_CH; ++k) {
+            uc[k] = un[k];
+            if (REPAIR) oc[k] = on[k];
+        }
         wl = wn;
         i0 = i0n;
         n = nn;
     }
+}
+
+__device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
+                          int path, int chunk) {
+    const PmsPath pa = d.paths[path];
+    down_walk<false>(d, sS, sS2, phase, uni(pa.tree), uni(pa.row), uni(pa.row) + uni(pa.len) - 1, chunk, 0.0, nullptr);
 }
 
 // the S / S2 tables (766 weight codes) into LDS
@@ -539,6 +579,51 @@ __global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, i
     else down_item(d, sS, sS2, phase, path, chunk);
 }
 
+// Pieces (sm_pms_host.h PmsCut): one wave per repair item (cut path, chunk) re-walks the guessed
+// pieces in dependency order from their exact neighbours -- up: from the piece above the exact bottom
+// piece to the head; down: from the piece below the exact head piece to the bottom.
+__global__ void __launch_bounds__(256) k_pms_repair(PmsDev d, int phase, int up, int lo, int hi) {
+    __shared__ double sS[PMS_NW], sS2[PMS_NW];
+    load_luts(d, sS, sS2);
+    const int it = lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (it >= hi) return;
+    const PmsRep rp = d.reps[it];
+    const PmsCut c = d.cuts[uni(rp.cut)];
+    const int t = uni(c.tree), Pn = d.piece, np = uni(c.npieces), row = uni(c.row), len = uni(c.len);
+    int P, base;
+    phase_labels(d, phase, t, P, base);
+    const int j = uni(rp.chunk) * 64 + (int)(threadIdx.x & 63);
+    if (uni(rp.chunk) * 64 >= P) return;
+    const bool act = j < P;
+    const int ts = d.tree_start[t], pt = d.tree_pt[t];
+    const double* A = d.A + d.tree_abase[t] + j;
+    if (up) {
+        for (int i = np - 2; i >= 0; --i) {
+            const int top = row + i * Pn, bot = top + Pn - 1;
+            const double x0 = act ? A[(size_t)(bot + 1 - ts) * pt] : 0.0;  // the exact head row of the piece below
+            up_walk<true>(d, sS, phase, t, top, bot, rp.chunk, x0);
+        }
+    } else {
+        const double* ub = d.Abak + d.cut_bak[uni(rp.cut)];  // A_up of rows [row + Pn, row + len)
+        for (int i = 1; i < np; ++i) {
+            const int top = row + i * Pn, bot = i + 1 < np ? top + Pn - 1 : row + len - 1;
+            const double y0 = act ? A[(size_t)(top - 1 - ts) * pt] : 0.0;  // the exact bottom row of the piece above
+            down_walk<true>(d, sS, sS2, phase, t, top, bot, rp.chunk, y0, ub + (size_t)(top - row - Pn) * pt);
+        }
+    }
+}
+
+// A_up rows of the non-head pieces of cuts [c_lo, c_hi) -> Abak (blockIdx.y = cut - c_lo)
+__global__ void k_pms_cut_backup(PmsDev d, int c_lo) {
+    const int ci = c_lo + (int)blockIdx.y;
+    const PmsCut c = d.cuts[ci];
+    const int t = c.tree, pt = d.tree_pt[t];
+    const size_t n = (size_t)(c.len - d.piece) * pt;
+    const double* src = d.A + d.tree_abase[t] + (size_t)(c.row + d.piece - d.tree_start[t]) * pt;
+    double* dst = d.Abak + d.cut_bak[ci];
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
 __global__ void k_pms_update(PmsDev d, int phase, int row_lo, int row_hi) {
     const int row = row_lo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (row >= row_hi) return;
@@ -683,6 +768,18 @@ hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, 
 hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi) {
     if (row_hi <= row_lo) return hipSuccess;
     hipLaunchKernelGGL(k_pms_update, dim3(blocks((size_t)(row_hi - row_lo), 256)), dim3(256), 0, st, d, phase, row_lo, row_hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_repair(hipStream_t st, const PmsDev& d, int phase, bool up, int lo, int hi) {
+    if (hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_repair, dim3(blocks((size_t)(hi - lo) * 64, 256)), dim3(256), 0, st, d, phase, up ? 1 : 0, lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_cut_backup(hipStream_t st, const PmsDev& d, int c_lo, int c_hi) {
+    if (c_hi <= c_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_cut_backup, dim3(64, (unsigned)(c_hi - c_lo)), dim3(256), 0, st, d, c_lo);
     return hipGetLastError();
 }
 

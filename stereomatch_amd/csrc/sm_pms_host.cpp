@@ -120,7 +120,7 @@ float canon(uint32_t u) { return (float)(int32_t)(u - 1u) * 0x1p-31f; }
 }  // namespace
 
 int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t* mR, const uint8_t* mD,
-                     PmsForest& f) {
+                     PmsForest& f, int piece) {
     const int N = W * H;
     Bfs b;
     bfs_forest(W, H, wR, wD, mR, mD, b);
@@ -196,7 +196,24 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
             if (c == heavy[n]) R.hk = (uint8_t)i;
         }
     }
-    // round-major path and item lists
+    // cut paths (tree order)
+    f.piece = piece > 0 ? piece : 0;
+    f.cuts.clear();
+    f.cut_round.clear();
+    f.tree_cut.assign(K + 1, 0);
+    std::vector<int32_t> cut_of(tpaths.size(), -1);
+    for (int t = 0; t < K; ++t) {
+        f.tree_cut[t] = (int32_t)f.cuts.size();
+        if (f.piece == 0) continue;
+        for (int i = tpath_start[t]; i < tpath_start[t + 1]; ++i)
+            if (tpaths[i].len >= 2 * f.piece) {
+                cut_of[i] = (int32_t)f.cuts.size();
+                f.cuts.push_back(PmsCut{t, tpaths[i].row, tpaths[i].len, tpaths[i].len / f.piece});
+                f.cut_round.push_back(path_ld[i]);
+            }
+    }
+    f.tree_cut[K] = (int32_t)f.cuts.size();
+    // round-major path, item and repair lists
     int rmax = 0;
     for (int t = 0; t < K; ++t) rmax = std::max(rmax, tmaxld[t] + 1);
     f.nrounds = rmax;
@@ -204,20 +221,32 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
     for (int t = 0; t < K; ++t) f.tree_rounds[t] = tmaxld[t] + 1;
     f.rt_path.assign((size_t)rmax * (K + 1), 0);
     f.rt_item.assign((size_t)rmax * (K + 1), 0);
+    f.rt_rep.assign((size_t)rmax * (K + 1), 0);
     f.paths.clear();
     f.items.clear();
+    f.reps.clear();
     std::vector<int32_t> cur(tpath_start.begin(), tpath_start.end() - 1);
     for (int r = 0; r < rmax; ++r)
         for (int t = 0; t <= K; ++t) {
             f.rt_path[(size_t)r * (K + 1) + t] = (int32_t)f.paths.size();
             f.rt_item[(size_t)r * (K + 1) + t] = (int32_t)f.items.size();
+            f.rt_rep[(size_t)r * (K + 1) + t] = (int32_t)f.reps.size();
             if (t == K) break;
             const int deg = f.nb_start[t + 1] - f.nb_start[t];
             const int chunks = (deg + 63) / 64;
             for (; cur[t] < tpath_start[t + 1] && path_ld[cur[t]] == r; ++cur[t]) {
-                const int pi = (int)f.paths.size();
-                f.paths.push_back(tpaths[cur[t]]);
-                for (int c = 0; c < chunks; ++c) f.items.push_back(PmsItem{pi, c});
+                const PmsPath pa = tpaths[cur[t]];
+                const int c = cut_of[cur[t]];
+                const int np = c < 0 ? 1 : f.cuts[c].npieces;
+                for (int i = 0; i < np; ++i) {  // the pieces, head first
+                    const int r0 = pa.row + i * f.piece;
+                    const int len = c < 0 ? pa.len : (i + 1 < np ? f.piece : pa.row + pa.len - r0);
+                    const int pi = (int)f.paths.size();
+                    f.paths.push_back(PmsPath{t, r0, len, 0});
+                    for (int k = 0; k < chunks; ++k) f.items.push_back(PmsItem{pi, k});
+                }
+                if (c >= 0)
+                    for (int k = 0; k < std::max(chunks, 1); ++k) f.reps.push_back(PmsRep{c, k});
             }
         }
     return K;

@@ -31,6 +31,20 @@ struct PmsItem {
     int32_t path, chunk;
 };
 
+// A heavy path cut into pieces (len >= 2 * piece): pieces i < npieces - 1 are rows
+// [row + i*piece, row + (i+1)*piece), the last one takes the rest.  Each piece is its own PmsPath in
+// f.paths, run from a guessed input (up: its bottom node's heavy child x = 0; down: its head's parent
+// row as found); k_pms_repair then re-walks each piece from its neighbour's exact boundary row until
+// the recomputed rows agree bitwise with the stored ones.
+struct PmsCut {
+    int32_t tree, row, len, npieces;
+};
+
+// One repair item: a cut path and the 64-proposal chunk
+struct PmsRep {
+    int32_t cut, chunk;
+};
+
 // The forest of one view, in the reference's numbering (Stereo3DMST.cpp:342-384, 434-522) and in the
 // walkers' schedule order.
 struct PmsForest {
@@ -45,12 +59,20 @@ struct PmsForest {
     std::vector<int32_t> rt_path;     // nrounds x (K+1): paths of tree t in round r
     std::vector<int32_t> rt_item;     // nrounds x (K+1): prop items of tree t in round r
     std::vector<int32_t> tree_rounds; // K
+    // pieces (piece > 0): cut paths in tree order, their repair items round-major
+    int piece = 0;                    // rows per piece, 0: no cuts
+    std::vector<PmsCut> cuts;
+    std::vector<int32_t> tree_cut;    // K+1: cuts of tree t are [tree_cut[t], tree_cut[t+1])
+    std::vector<int32_t> cut_round;   // per cut: its round (light depth)
+    std::vector<PmsRep> reps;         // round-major
+    std::vector<int32_t> rt_rep;      // nrounds x (K+1)
 };
 
 // Build the forest from the forest masks (real edges only: mR[p] = edge (p, p+1), mD[p] = (p, p+W)) and
 // the edge weights.  Returns the number of trees.
+// piece > 0 cuts every heavy path of at least 2 * piece rows into pieces.
 int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t* mR, const uint8_t* mD,
-                     PmsForest& f);
+                     PmsForest& f, int piece = 0);
 #endif
 
 #ifdef __cplusplus

@@ -76,6 +76,21 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, serial):
         assert st["spec_rounds"] >= 6  # calls 2..4 of both views
 
 
+@pytest.mark.parametrize("piece,serial", [("16", "0"), ("8", "1"), ("64", "0")])
+def test_pms_pieces_bitexact(gpu_ctx, monkeypatch, piece, serial):
+    """Long heavy paths cut into pieces of SM_PMS_PIECE rows: every piece runs from a guessed input and
+    k_pms_repair re-walks it from its neighbour's exact row until the rows agree (8-row pieces mostly
+    re-walk whole pieces).  First call serial (cut trees take the whole-GPU launches), later calls
+    speculative; SM_PMS_SERIAL=1 all serial."""
+    monkeypatch.setenv("SM_PMS_PIECE", piece)
+    monkeypatch.setenv("SM_PMS_SERIAL", serial)
+    left, right, _ = make_pair(192, 128, 48, index=7)
+    ref = O.stereo3dmst_pms(left, right, 48, iters=3, c=5000.0, min_size=200)
+    out, labs, st = run_gpu(gpu_ctx, left, right, 48, 3, 5000.0, 200)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+
+
 def test_pms_many_trees_bitexact(gpu_ctx):
     """79k trees (c=5, min_size 2): the speculative offset chain (k_pms_guess) too large to stage its
     per-tree values in LDS takes them from global memory."""
