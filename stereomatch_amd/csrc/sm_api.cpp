@@ -1333,9 +1333,12 @@ int pms_piece() {
 }
 
 // trees whose work (nodes x 64-proposal chunks) is at least this run over the whole GPU in serial mode
+// (their rounds as launches); smaller ones go to the one-workgroup k_pms_serial in runs.  C2 first
+// call per view (tools/pms_bench.py): 32768 -> 376 ms, 8192 -> 278, 2048 -> 229, 1024 -> 223, 512 ->
+// 221, 128 -> 226 ms.
 long long pms_big_tree() {
     const char* e = getenv("SM_PMS_BIG");
-    return e ? std::max(1ll, atoll(e)) : 32768;
+    return e ? std::max(1ll, atoll(e)) : 1024;
 }
 
 // One phase (0: propagation, 1: refinement) of trees [t_lo, t_hi) over the whole GPU: the up rounds
