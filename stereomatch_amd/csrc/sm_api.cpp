@@ -1199,6 +1199,12 @@ bool pms_serial_only() {
     const char* e = getenv("SM_PMS_SERIAL");
     return e && atoi(e) == 1;
 }
+// SM_PMS_REPASS=1: a stale-input failure also restores and re-speculates every later tree (A/B of
+// the single-tree fix)
+bool pms_repass() {
+    const char* e = getenv("SM_PMS_REPASS");
+    return e && atoi(e) == 1;
+}
 int pms_max_rounds() {
     const char* e = getenv("SM_PMS_MAX_ROUNDS");
     return e ? std::max(1, atoi(e)) : 8;
@@ -1317,6 +1323,7 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.cut_bak = P<long long>(S.cut_bak);
     d.Abak = P<double>(S.Abak);
     d.piece = S.f.piece;
+    d.hi_bak = 0;
     d.W = ctx->W;
     d.Dv = D;
     d.Dmax = D;
@@ -1390,10 +1397,14 @@ sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) 
     return SM_OK;
 }
 
-// One speculative MST_PMS call of one view (iteration > 0).  Passes over the trees [t_lo, K): guessed
-// offsets, every tree's propagation and refinement, validation.  The first tree whose offset or sampled
-// labels were wrong (t*) and everything after it go back to the call's starting state; t* runs serially
-// (its inputs are exact now) and the next pass speculates from t* + 1.
+// One speculative MST_PMS call of one view (iteration > 0).  A pass over the trees [t_lo, K): guessed
+// offsets, every tree's propagation and refinement, validation.  Every tree before the first invalid
+// one (t*) is exact.  t* goes back to the call's starting state and runs serially (its inputs are exact
+// now).  If t* failed on its offset, every later tree drew from the wrong place: they are restored as
+// well and the next pass speculates from t* + 1.  If only its sampled inputs were stale, the later
+// trees keep their results and are validated again against t*'s exact labels and offset (a tree whose
+// count changed shows up as the next offset failure), so a stale input costs one serial tree instead
+// of a pass.
 sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
     PmsState& S = ctx->pms[v];
     const PmsForest& f = S.f;
@@ -1403,30 +1414,38 @@ sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
     HIPC(launch_pms_backup(ctx->st, d, N));
     HIPC(hipMemsetAsync(S.off.p, 0, 16, ctx->st));
     int t_lo = 0, rounds = 0;
+    bool pass = true;
     while (t_lo < K) {
-        if (rounds >= max_rounds) {  // pathological: finish the call in order
-            CHECK(pms_serial_range(ctx, v, d, t_lo, K));
-            ctx->pms_stats.serial_trees += K - t_lo;
-            break;
+        if (pass) {
+            if (rounds >= max_rounds) {  // pathological: finish the call in order
+                CHECK(pms_serial_range(ctx, v, d, t_lo, K));
+                ctx->pms_stats.serial_trees += K - t_lo;
+                break;
+            }
+            ++rounds;
+            ++ctx->pms_stats.spec_rounds;
+            // the draws trees [t_lo, K) can consume: their propagation draws + 4 per refinement level
+            const long long wn =
+                (long long)(f.nb_start[K] - f.nb_start[t_lo]) + 4ll * sm_pms_levels(d.Dmax) * (K - t_lo) + 8;
+            HIPC(launch_pms_guess(ctx->st, d, t_lo, wn));
+            HIPC(launch_pms_prop_setup(ctx->st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
+            CHECK(pms_phase(ctx, v, d, 0, t_lo, K));
+            HIPC(launch_pms_ref_setup(ctx->st, d, t_lo));
+            CHECK(pms_phase(ctx, v, d, 1, t_lo, K));
         }
-        ++rounds;
-        ++ctx->pms_stats.spec_rounds;
-        // the draws trees [t_lo, K) can consume: their propagation draws + 4 per refinement level
-        const long long wn = (long long)(f.nb_start[K] - f.nb_start[t_lo]) + 4ll * sm_pms_levels(d.Dmax) * (K - t_lo) + 8;
-        HIPC(launch_pms_guess(ctx->st, d, t_lo, wn));
-        HIPC(launch_pms_prop_setup(ctx->st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
-        CHECK(pms_phase(ctx, v, d, 0, t_lo, K));
-        HIPC(launch_pms_ref_setup(ctx->st, d, t_lo));
-        CHECK(pms_phase(ctx, v, d, 1, t_lo, K));
         HIPC(launch_pms_validate(ctx->st, d, t_lo));
         HIPC(hipMemcpyAsync(ctx->h_pms_res, S.result.p, 16, hipMemcpyDeviceToHost, ctx->st));
         HIPC(hipStreamSynchronize(ctx->st));
-        const int ts = ctx->h_pms_res[0];
-        if (ts < t_lo || ts > K) return fail(ctx, SM_ERR_STATE, "MST_PMS validation returned a bad tree index");
+        const int ts = ctx->h_pms_res[0], why = ctx->h_pms_res[1];
+        if (ts < t_lo || ts > K || (ts < K && why != 1 && why != 2))
+            return fail(ctx, SM_ERR_STATE, "MST_PMS validation returned a bad tree index");
         if (ts == K) break;
-        HIPC(launch_pms_restore(ctx->st, d, f.tree_start[ts], (int)N));
+        pass = why == 1 || pms_repass();
+        HIPC(launch_pms_restore(ctx->st, d, f.tree_start[ts], pass ? (int)N : f.tree_start[ts + 1]));
         HIPC(hipMemcpyAsync(S.off.p, P<int32_t>(S.result) + 2, 8, hipMemcpyDeviceToDevice, ctx->st));
-        CHECK(pms_serial_range(ctx, v, d, ts, ts + 1));
+        PmsDev dk = d;
+        dk.hi_bak = pass ? 0 : 1;  // later trees keep their (modified) labels: sample the starting ones
+        CHECK(pms_serial_range(ctx, v, dk, ts, ts + 1));
         ctx->pms_stats.serial_trees += 1;
         t_lo = ts + 1;
     }

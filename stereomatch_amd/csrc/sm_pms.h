@@ -52,6 +52,8 @@ struct PmsDev {
     const long long* cut_bak;
     double* Abak;
     int W, Dv, Dmax, K, nrounds, piece;
+    int hi_bak;  // 1: propagation samples higher neighbours (u > t) from abc_bak, the call's starting labels
+                 // (a serial re-run in the middle of a speculative call, whose later trees keep results)
 };
 
 // serial: trees [t0, t1) one after the other in one workgroup (the reference's order), starting at the

@@ -365,7 +365,9 @@ __device__ void prop_label(const PmsDev& d, int t, long long o, int j) {
     }
     const int q = d.bfs_pix[us + i];
     const int slot = d.tree_lab[t] + j;
-    d.lab[slot] = make_float4(d.abc[3 * (size_t)q], d.abc[3 * (size_t)q + 1], d.abc[3 * (size_t)q + 2], 0.0f);
+    // serial order: a higher neighbour has not run yet in this call
+    const float* src = d.hi_bak && u > t ? d.abc_bak : d.abc;
+    d.lab[slot] = make_float4(src[3 * (size_t)q], src[3 * (size_t)q + 1], src[3 * (size_t)q + 2], 0.0f);
     d.labq[slot] = q;
 }
 
@@ -660,11 +662,20 @@ __global__ void k_pms_scan(PmsDev d, int t_lo) {
     if (threadIdx.x != 0) return;
     long long o = d.off[0];
     int t = t_lo;
+    int why = 0;
     for (; t < d.K; ++t) {
-        if (d.oguess[t] != o || d.flag[t]) break;
+        if (d.oguess[t] != o) {
+            why = 1;  // wrong offset: every later tree drew from the wrong place too
+            break;
+        }
+        if (d.flag[t]) {
+            why = 2;  // stale propagation inputs only: later trees may still be exact
+            break;
+        }
         o += d.cnt[t];
     }
     d.result[0] = t;
+    d.result[1] = why;
     *reinterpret_cast<long long*>(d.result + 2) = o;  // the exact offset of tree t
 }
 

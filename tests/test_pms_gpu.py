@@ -62,18 +62,22 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
     assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
 
 
-@pytest.mark.parametrize("serial", ["0", "1"])
-def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, serial):
-    """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs and wrong
-    offsets and must redo them; SM_PMS_SERIAL=1 is the plain serial order."""
-    monkeypatch.setenv("SM_PMS_SERIAL", serial)
+@pytest.mark.parametrize("mode", ["spec", "repass", "serial"])
+def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
+    """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
+    tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
+    call's starting labels) and wrong offsets (a new pass); SM_PMS_REPASS=1 re-speculates after
+    every failure; SM_PMS_SERIAL=1 is the plain serial order."""
+    monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
+    monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
     for v in ("left", "right"):
         check_view(out, labs, ref, v)
-    if serial == "0":
-        assert st["spec_rounds"] >= 6  # calls 2..4 of both views
+    if mode != "serial":
+        assert st["spec_rounds"] >= 6  # calls 2..4 of both views: one pass each at least
+        assert st["serial_trees"] > 2 * ref["left"]["tree"]["ntrees"] - 50  # first calls + the failures
 
 
 @pytest.mark.parametrize("piece,serial", [("16", "0"), ("8", "1"), ("64", "0")])
