@@ -514,28 +514,43 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
 // The offsets are a serial chain (a tree's draws depend on the dice at its offset), so the rest is
 // taken off it: every tree's starting disparity in parallel, and the stream window the chain can
 // reach (wn floats, when it fits) staged in LDS, so each link reads LDS instead of global memory.
-__global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, int staged, long long wn) {
+template <bool STAGED>
+__global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long long wn) {
     extern __shared__ float gsm[];
     const int nt = d.K - t_lo, tid = threadIdx.x;
     const long long o0 = d.off[0];
-    // staged: per-tree dd and degree in LDS (else computed in the chain); wn: stream floats in LDS
+    // STAGED: per-tree dd, degree and result offset, and the reachable stream window (wn floats), in
+    // LDS -- the chain then touches no global memory (a global access would make every link wait on
+    // the previous links' traffic)
     float* sdd = gsm;
-    int* sdeg = reinterpret_cast<int*>(gsm + (staged ? nt : 0));
-    float* sdice = gsm + (staged ? 2 * nt : 0);
-    if (staged)
+    int* sdeg = reinterpret_cast<int*>(gsm + nt);
+    long long* sog = reinterpret_cast<long long*>(gsm + 2 * ((nt + 1) & ~1));
+    float* sdice = reinterpret_cast<float*>(sog + nt);
+    if (STAGED) {
         for (int i = tid; i < nt; i += blockDim.x) {
             sdd[i] = ref_dd(d, t_lo + i);
             sdeg[i] = tree_deg(d, t_lo + i);
         }
-    for (long long i = tid; i < wn; i += blockDim.x) sdice[i] = o0 + i < d.dice_n ? d.dice[o0 + i] : 0.0f;
-    __syncthreads();
+        for (long long i = tid; i < wn; i += blockDim.x) sdice[i] = o0 + i < d.dice_n ? d.dice[o0 + i] : 0.0f;
+        __syncthreads();
+        if (tid == 0) {
+            long long o = o0;
+            for (int t = 0; t < nt; ++t) {
+                sog[t] = o;
+                const int deg = sdeg[t];
+                o += deg + ref_count(d, sdd[t], o + deg, [&](long long k) { return sdice[k - o0]; });
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < nt; i += blockDim.x) d.oguess[t_lo + i] = sog[i];
+        return;
+    }
     if (tid != 0) return;
     long long o = o0;
     for (int t = t_lo; t < d.K; ++t) {
         d.oguess[t] = o;
-        const int deg = staged ? sdeg[t - t_lo] : tree_deg(d, t);
-        const float dd = staged ? sdd[t - t_lo] : ref_dd(d, t);
-        o += deg + ref_count(d, dd, o + deg, [&](long long k) { return k - o0 < wn ? sdice[k - o0] : d.dice[k]; });
+        const int deg = tree_deg(d, t);
+        o += deg + ref_count(d, ref_dd(d, t), o + deg, [&](long long k) { return d.dice[k]; });
     }
 }
 
@@ -626,10 +641,58 @@ __global__ void k_pms_cut_backup(PmsDev d, int c_lo) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) dst[i] = src[i];
 }
 
-__global__ void k_pms_update(PmsDev d, int phase, int row_lo, int row_hi) {
-    const int row = row_lo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (row >= row_hi) return;
-    update_row(d, phase, row, d.rtree[row]);
+// Rows with few proposals (P <= 16) are updated one per lane (update_row); a row with more is updated
+// by the whole wave, lanes over its proposals (coalesced A reads), then a wave reduction to the
+// minimum value and, among equal values, the smallest index -- the same winner as the serial strict-<
+// scan from index 0 (:173-185) -- then the strict-< test against the pixel's current minimum.
+__global__ void __launch_bounds__(256) k_pms_update(PmsDev d, int phase, int row_lo, int row_hi) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int base_row = row_lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) & ~63u);
+    const int row = base_row + lane;
+    const bool valid = row < row_hi;
+    int t = 0, P = 0, lb = 0;
+    if (valid) {
+        t = d.rtree[row];
+        phase_labels(d, phase, t, P, lb);
+    }
+    const bool wide = valid && P > 16;
+    if (valid && !wide) update_row(d, phase, row, t);
+    unsigned long long m = __ballot(wide);
+    while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int r = base_row + b;
+        const int tr = __shfl(t, b), Pr = __shfl(P, b), br = __shfl(lb, b);
+        const double* a = d.A + d.tree_abase[tr] + (size_t)(r - d.tree_start[tr]) * d.tree_pt[tr];
+        double mv = 0.0;
+        int mi = INT_MAX;
+        for (int j = lane; j < Pr; j += 64) {  // per lane: the first minimum of its indices
+            const double v = a[j];
+            if (mi == INT_MAX || v < mv) {
+                mv = v;
+                mi = j;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {  // (value, index) minimum over the wave
+            const double ov = __shfl_xor(mv, o);
+            const int oi = __shfl_xor(mi, o);
+            if (oi != INT_MAX && (mi == INT_MAX || ov < mv || (ov == mv && oi < mi))) {
+                mv = ov;
+                mi = oi;
+            }
+        }
+        if (lane == 0) {
+            const int pix = d.rows[r].pix;
+            if (mv < d.minc[pix]) {
+                const float4 L = d.lab[br + mi];
+                d.minc[pix] = mv;
+                d.abc[3 * (size_t)pix] = L.x;
+                d.abc[3 * (size_t)pix + 1] = L.y;
+                d.abc[3 * (size_t)pix + 2] = L.z;
+            }
+        }
+    }
 }
 
 __global__ void k_pms_ref_setup(PmsDev d, int t_lo) {
@@ -750,15 +813,18 @@ hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t) {
 }
 
 hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long wn) {
+    // wn covers every draw trees [t_lo, K) can consume (the host's bound), so a staged chain never
+    // reads past the window; otherwise (too many trees / draws for the LDS) it reads global memory
     const size_t nt = (size_t)(d.K - t_lo);
     constexpr size_t cap = 150 * 1024;  // LDS bytes
-    const int staged = 2 * nt * 4 <= cap ? 1 : 0;
-    if ((staged * 2 * nt + (size_t)wn) * 4 > cap) wn = 0;  // the chain reads the stream from global memory
-    const size_t lds = (staged * 2 * nt + (size_t)wn) * 4;
+    const size_t lds = 4 * 2 * ((nt + 1) & ~(size_t)1) + 8 * nt + 4 * (size_t)wn;
     static const hipError_t attr =  // once per process (thread-safe static initialisation)
-        hipFuncSetAttribute((const void*)k_pms_guess, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap);
+        hipFuncSetAttribute((const void*)k_pms_guess<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap);
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_pms_guess, dim3(1), dim3(1024), lds, st, d, t_lo, staged, wn);
+    if (lds <= cap)
+        hipLaunchKernelGGL(k_pms_guess<true>, dim3(1), dim3(1024), lds, st, d, t_lo, wn);
+    else
+        hipLaunchKernelGGL(k_pms_guess<false>, dim3(1), dim3(64), 0, st, d, t_lo, 0ll);
     return hipGetLastError();
 }
 
