@@ -1348,8 +1348,8 @@ long long pms_big_tree() {
     return e ? std::max(1ll, atoll(e)) : 1024;
 }
 
-// One phase (0: propagation, 1: refinement) of trees [t_lo, t_hi) over the whole GPU: the up rounds
-// deepest first, the cut paths' pieces repaired after each round, the cut paths' A_up rows saved, the
+// One phase (0: propagation, 1: refinement) of trees [t_lo, t_hi) over the whole GPU: the data terms
+// into the A rows, the up rounds deepest first, the cut paths' pieces repaired after each round, the cut paths' A_up rows saved, the
 // down rounds root first (repaired likewise), then the per-pixel update.
 sm_status pms_phase(sm_ctx* ctx, int v, const PmsDev& d, int phase, int t_lo, int t_hi) {
     const PmsForest& f = ctx->pms[v].f;
@@ -1357,6 +1357,7 @@ sm_status pms_phase(sm_ctx* ctx, int v, const PmsDev& d, int phase, int t_lo, in
     int R = 0;
     for (int t = t_lo; t < t_hi; ++t) R = std::max(R, f.tree_rounds[t]);
     const std::vector<int32_t>& rt = phase == 0 ? f.rt_item : f.rt_path;
+    HIPC(launch_pms_cost(ctx->st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
     for (int r = R - 1; r >= 0; --r) {
         HIPC(launch_pms_walk(ctx->st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
         HIPC(launch_pms_repair(ctx->st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));

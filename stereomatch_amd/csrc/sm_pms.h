@@ -69,6 +69,7 @@ hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t);
 hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long wn);
 hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int total_deg);
 hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi);
+hipError_t launch_pms_cost(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);
 hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);
 hipError_t launch_pms_ref_setup(hipStream_t st, const PmsDev& d, int t_lo);
 // pieces: re-walk the cut paths' guessed pieces from their exact neighbours (repair items [lo, hi)),

@@ -47,12 +47,14 @@ __device__ __forceinline__ float label_cost(const float* __restrict__ vol, int D
                                             int pix, float xf, float yf) {
     const float disp = fmaf(xf, a, yf * b) + c;
     const float dc = ceilf(disp), dfl = floorf(disp);
-    const int ic = cvtt(dc);
-    if (ic >= Dmax) return 0.5f;
-    const int ifl = cvtt(dfl);
-    if (ifl < 0) return 0.5f;
+    const int ic = cvtt(dc), ifl = cvtt(dfl);
+    const bool out = ic >= Dmax || ifl < 0;  // 0.5 (:108-111)
+    // branch-free: both words are loaded from clamped indices and the result selected, so a walker's
+    // loads stay straight-line code (a load under a branch makes the wait counters fall back to a full
+    // drain before the next node's loads)
     const float* r = vol + (size_t)pix * Dv;
-    return fmaf(dc - disp, r[ifl], (disp - dfl) * r[ic]);
+    const float vf = r[out ? 0 : ifl], vc = r[out || ic < 0 ? 0 : ic];
+    return out ? 0.5f : fmaf(dc - disp, vf, (disp - dfl) * vc);
 }
 
 // Correctly rounded float sqrt and division, as x86's sqrtss / divss.  HIP's __fsqrt_rn is the native
@@ -144,8 +146,11 @@ __device__ __forceinline__ uint32_t meta_dw(const ChunkMeta& m, int j) {  // j w
 // so each chunk pays one memory latency; the serial part reads only registers and the LDS weight
 // tables sS / sS2.  REPAIR: the stored rows are loaded with the chunk, and the walk stops at the
 // first node where every lane's recomputed value equals the stored one bitwise (two trajectories of
-// the recurrence that agree at a node agree from there on); until then it overwrites.
-template <bool REPAIR>
+// the recurrence that agree at a node agree from there on); until then it overwrites.  PRE: the data
+// term of every row was written into its A row beforehand (k_pms_cost / cost_rows), so a chunk loads
+// tree-contiguous A rows instead of gathering from the cost volume (a dependent load per node, and
+// a TLB miss at most of them: the volume is ~1 GB).
+template <bool REPAIR, bool PRE>
 __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phase, int t, int top, int bot, int chunk,
                         double x0) {
     int P, base;
@@ -154,9 +159,10 @@ __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
     if (chunk * 64 >= P) return;
     const bool act = j < P;
     float4 L = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (act) L = d.lab[base + j];
+    if (!PRE && act) L = d.lab[base + j];
     const int ts = d.tree_start[t], pt = d.tree_pt[t];
     double* __restrict__ A = d.A + d.tree_abase[t] + j;
+    const double* __restrict__ Al = d.A + d.tree_abase[t] + (act ? j : 0);  // loads: every lane in bounds
     const int row0 = top, len = bot - top + 1;
     int i0 = len - 1;                                       // top (last walked) index of this chunk
     int lo = i0 - PMS_CH + 1 > 0 ? i0 - PMS_CH + 1 : 0;     // its first index
@@ -165,17 +171,20 @@ __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
     while (i0 >= 0) {
         const int n = i0 - lo + 1;
         double cv[PMS_CH][4];
-        float cost[PMS_CH];
+        double cost[PMS_CH];
         double old[PMS_CH];
         int nch[PMS_CH], hk[PMS_CH], wc[PMS_CH][4];
+        // straight-line issue: every load unconditional from a valid address (nodes past the chunk's end
+        // re-read its first node; lanes past P read column 0), and no select on a loaded value -- a
+        // select would make the compiler wait for the load where it is issued.  Lanes past P compute
+        // garbage and never store.
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
-            nch[k] = 0;
-            if (k >= n) continue;
-            const int w0 = (i0 - k - lo) * 10;  // node row0 + i0 - k
+            const int kk = k < n ? k : 0;
+            const int row = row0 + i0 - kk;
+            const int w0 = (i0 - kk - lo) * 10;  // node row0 + i0 - kk
             const uint32_t w6 = meta_dw(mc, w0 + 6), w7 = meta_dw(mc, w0 + 7), w8 = meta_dw(mc, w0 + 8);
-            const uint32_t w9 = meta_dw(mc, w0 + 9);
-            nch[k] = (int)((w6 >> 16) & 255u);
+            nch[k] = k < n ? (int)((w6 >> 16) & 255u) : 0;
             hk[k] = (int)(w6 >> 24);
             wc[k][0] = (int)(w7 & 0xFFFFu);
             wc[k][1] = (int)(w7 >> 16);
@@ -183,18 +192,24 @@ __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
             wc[k][3] = (int)(w8 >> 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                cv[k][q] = 0.0;
-                if (q < nch[k] && q != hk[k] && act) cv[k][q] = A[(size_t)((int)meta_dw(mc, w0 + 2 + q) - ts) * pt];
+                const bool use = q < nch[k] && q != hk[k];
+                const int crow = use ? (int)meta_dw(mc, w0 + 2 + q) : row;
+                cv[k][q] = Al[(size_t)(crow - ts) * pt];  // read only where used (serial part)
             }
-            const int pix = (int)meta_dw(mc, w0);
-            cost[k] = act ? label_cost(d.vol, d.Dv, d.Dmax, L.x, L.y, L.z, pix, (float)(w9 & 0xFFFFu), (float)(w9 >> 16))
-                          : 0.0f;
-            if (REPAIR) old[k] = act ? A[(size_t)(row0 + i0 - k - ts) * pt] : 0.0;
+            if (PRE) {
+                cost[k] = Al[(size_t)(row - ts) * pt];
+            } else {
+                const uint32_t w9 = meta_dw(mc, w0 + 9);
+                const float c = label_cost(d.vol, d.Dv, d.Dmax, L.x, L.y, L.z, (int)meta_dw(mc, w0), (float)(w9 & 0xFFFFu),
+                                           (float)(w9 >> 16));
+                cost[k] = (double)c;
+            }
+            if (REPAIR) old[k] = Al[(size_t)(row - ts) * pt];
         }
         const int i0n = lo - 1;
         const int lon = i0n - PMS_CH + 1 > 0 ? i0n - PMS_CH + 1 : 0;
-        ChunkMeta mn = mc;
-        if (i0n >= 0) mn = meta_load(d.rows, row0 + lon, i0n - lon + 1);
+        // unconditional (past the head: a dummy reload of row0), so no branch precedes the serial part
+        const ChunkMeta mn = meta_load(d.rows, row0 + lon, i0n >= 0 ? i0n - lon + 1 : 1);
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
             if (k >= n) break;
@@ -208,7 +223,7 @@ __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
                 const double v = q == hk[k] ? x : cv[k][q];
                 acc = fma(v, sv[q], acc);  // A[parent] = fma(A[v], S, A[parent]) (0x40fad5)
             }
-            x = (double)cost[k] + acc;  // A[v] = C + A[v] (0x40fac5)
+            x = cost[k] + acc;  // A[v] = C + A[v] (0x40fac5); cost[k] is a float widened exactly
             if (REPAIR) {
                 const bool same = !act || __double_as_longlong(x) == __double_as_longlong(old[k]);
                 if (__all(same)) return;
@@ -225,7 +240,20 @@ __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
 
 __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phase, int path, int chunk) {
     const PmsPath pa = d.paths[path];
-    up_walk<false>(d, sS, phase, uni(pa.tree), uni(pa.row), uni(pa.row) + uni(pa.len) - 1, chunk, 0.0);
+    up_walk<false, true>(d, sS, phase, uni(pa.tree), uni(pa.row), uni(pa.row) + uni(pa.len) - 1, chunk, 0.0);
+}
+
+// the data term C (:103-118) of proposals [j0, P) step js of row `row` of tree t into its A row: the
+// up walk's starting values (PRE)
+__device__ __forceinline__ void cost_row(const PmsDev& d, int row, int t, int P, int base, int j0, int js) {
+    const PmsRow& rw = d.rows[row];
+    const int pix = rw.pix;
+    const float xf = (float)rw.x, yf = (float)rw.y;
+    double* a = d.A + d.tree_abase[t] + (size_t)(row - d.tree_start[t]) * d.tree_pt[t];
+    for (int j = j0; j < P; j += js) {
+        const float4 L = d.lab[base + j];
+        a[j] = (double)label_cost(d.vol, d.Dv, d.Dmax, L.x, L.y, L.z, pix, xf, yf);
+    }
 }
 
 // Root->leaf walk of rows [top, bot] of tree t, head to bottom: A(c) = fma(S_c, A(p), S2_c * A_up(c))
@@ -245,28 +273,26 @@ __device__ void down_walk(const PmsDev& d, const double* __restrict__ sS, const 
     const bool act = j < P;
     const int ts = d.tree_start[t], pt = d.tree_pt[t];
     double* __restrict__ A = d.A + d.tree_abase[t] + j;
+    const double* __restrict__ Al = d.A + d.tree_abase[t] + (act ? j : 0);  // loads: every lane in bounds,
+    const int jl = act ? j : 0;                                               // no selects (see up_walk)
     const int row0 = top, len = bot - top + 1;
     const int parent = REPAIR ? row0 - 1 : uni(d.rows[row0].parent);
     const int lane = (int)(threadIdx.x & 63);
     // weights of a chunk: lane k holds rows[row0 + i0 + k].w
     auto wload = [&](int i0, int n) {
-        const int r = row0 + i0 + (lane < n ? lane : 0);
+        const int r = row0 + (i0 < len ? i0 + (lane < n ? lane : 0) : 0);
         return (int)d.rows[r].w;
     };
     auto uload = [&](double (&u)[PMS_CH], double (&o)[PMS_CH], int i0, int n) {
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
-            const int i = i0 + (k < n ? k : 0);  // clamped: unconditional loads
-            if (REPAIR) {
-                u[k] = act ? ub[(size_t)i * pt + j] : 0.0;
-                o[k] = act ? A[(size_t)(row0 + i - ts) * pt] : 0.0;
-            } else {
-                u[k] = act ? A[(size_t)(row0 + i - ts) * pt] : 0.0;
-            }
+            const int i = i0 < len ? i0 + (k < n ? k : 0) : 0;  // clamped: unconditional loads (see label_cost)
+            u[k] = REPAIR ? ub[(size_t)i * pt + jl] : Al[(size_t)(row0 + i - ts) * pt];
+            if (REPAIR) o[k] = Al[(size_t)(row0 + i - ts) * pt];
         }
     };
     double y = REPAIR ? yin : 0.0;
-    if (!REPAIR && parent >= 0 && act) y = A[(size_t)(parent - ts) * pt];
+    if (!REPAIR && parent >= 0) y = Al[(size_t)(parent - ts) * pt];
     int i0 = 0, n = len < PMS_CH ? len : PMS_CH;
     double uc[PMS_CH], oc[PMS_CH];
     uload(uc, oc, 0, n);
@@ -274,11 +300,8 @@ __device__ void down_walk(const PmsDev& d, const double* __restrict__ sS, const 
     while (i0 < len) {
         const int i0n = i0 + n, nn = len - i0n < PMS_CH ? len - i0n : PMS_CH;
         double un[PMS_CH], on[PMS_CH];
-        int wn = wl;
-        if (i0n < len) {
-            uload(un, on, i0n, nn);
-            wn = wload(i0n, nn);
-        }
+        uload(un, on, i0n, nn);  // past the bottom: dummy reloads of row0 (no branch before the serial part)
+        const int wn = wload(i0n, nn);
 #pragma unroll
         for (int k = 0; k < PMS_CH; ++k) {
             if (k >= n) break;
@@ -472,6 +495,14 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
             seg(4 * phase + 0);
             const int P = phase == 0 ? deg : d.nref[t];
             if (P > 0) {
+                const int base = d.tree_lab[t] + (phase == 0 ? 0 : deg);
+                if (P <= 16) {
+                    for (int row = ts + tid; row < te; row += nt) cost_row(d, row, t, P, base, 0, 1);
+                } else {
+                    for (int row = ts + wave; row < te; row += nwaves) cost_row(d, row, t, P, base, tid & 63, 64);
+                }
+                __threadfence_block();
+                __syncthreads();
                 const int32_t* rt = phase == 0 ? d.rt_item : d.rt_path;
                 for (int r = R - 1; r >= 0; --r) {  // leaf -> root: deepest light depth first
                     const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
@@ -582,6 +613,28 @@ __global__ void k_pms_prop_setup(PmsDev d, int t_lo) {
     prop_label(d, lo, d.oguess[lo], e - d.nb_start[lo]);
 }
 
+// The data term of every row of [row_lo, row_hi) for the phase's proposals, into the A rows (the up
+// walks' PRE input): rows with few proposals one per lane, wider ones by the whole wave.
+__global__ void __launch_bounds__(256) k_pms_cost(PmsDev d, int phase, int row_lo, int row_hi) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int base_row = row_lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) & ~63u);
+    const int row = base_row + lane;
+    const bool valid = row < row_hi;
+    int t = 0, P = 0, lb = 0;
+    if (valid) {
+        t = d.rtree[row];
+        phase_labels(d, phase, t, P, lb);
+    }
+    const bool wide = valid && P > 16;
+    if (valid && !wide) cost_row(d, row, t, P, lb, 0, 1);
+    unsigned long long m = __ballot(wide);
+    while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        cost_row(d, base_row + b, __shfl(t, b), __shfl(P, b), __shfl(lb, b), lane, 64);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, int item_lo, int item_hi) {
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
     load_luts(d, sS, sS2);
@@ -618,7 +671,7 @@ __global__ void __launch_bounds__(256) k_pms_repair(PmsDev d, int phase, int up,
         for (int i = np - 2; i >= 0; --i) {
             const int top = row + i * Pn, bot = top + Pn - 1;
             const double x0 = act ? A[(size_t)(bot + 1 - ts) * pt] : 0.0;  // the exact head row of the piece below
-            up_walk<true>(d, sS, phase, t, top, bot, rp.chunk, x0);
+            up_walk<true, false>(d, sS, phase, t, top, bot, rp.chunk, x0);
         }
     } else {
         const double* ub = d.Abak + d.cut_bak[uni(rp.cut)];  // A_up of rows [row + Pn, row + len)
@@ -839,6 +892,12 @@ hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, 
     if (item_hi <= item_lo) return hipSuccess;
     hipLaunchKernelGGL(k_pms_walk, dim3(blocks((size_t)(item_hi - item_lo) * 64, 256)), dim3(256), 0, st, d, phase,
                        up ? 1 : 0, item_lo, item_hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_cost(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi) {
+    if (row_hi <= row_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_cost, dim3(blocks((size_t)(row_hi - row_lo), 256)), dim3(256), 0, st, d, phase, row_lo, row_hi);
     return hipGetLastError();
 }
 
