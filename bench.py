@@ -17,6 +17,7 @@ Launched without torchrun, --gpus N > 1 starts the N rank processes itself (befo
 under torchrun, WORLD_SIZE must equal --gpus.  Rank 0 prints ONE JSON line.
 """
 import argparse
+import math
 import json
 import os
 import socket
@@ -125,11 +126,14 @@ def pms_leg(ctx, left, right, D, iters, oracle):
     return out
 
 
-def stream_frames(ctxs, steps, D, params, retire, split=True):
+def stream_frames(ctxs, steps, D, params, retire, split=True, lag=1):
     """Stream `steps` frames over the contexts, frame i on context i mod len(ctxs), keeping up to
     len(ctxs) in flight; retire(c) waits for context c's frame.  split: frame i's tree is enqueued
-    (match_begin) before the host waits for frame i-1's layout and enqueues its filter
-    (match_finish), so the GPU never idles on the host; otherwise one match_async per frame."""
+    (match_begin) before the host waits for frame i-lag's layout and enqueues its filter
+    (match_finish), so the GPU never idles on the host; otherwise one match_async per frame.
+    lag (1 .. len(ctxs) - 1): frames whose tree is begun but not finished.  1 suits the MST (its
+    tree is GPU work that finishes quickly); segment mode's tree has host steps (its worker thread),
+    and lag len(ctxs) - 1 lets that many frames segment at once."""
     n = len(ctxs)
     if n == 1 or not split:
         for i in range(steps):
@@ -137,14 +141,15 @@ def stream_frames(ctxs, steps, D, params, retire, split=True):
             if i >= n - 1:
                 retire(ctxs[(i - n + 1) % n])
     else:
+        lag = max(1, min(lag, n - 1))
         for i in range(steps):
             ctxs[i % n].match_begin(D, params)
-            if i >= 1:
-                ctxs[(i - 1) % n].match_finish()
+            if i >= lag:
+                ctxs[(i - lag) % n].match_finish()
             if i >= n - 1:
                 retire(ctxs[(i - n + 1) % n])
-        if steps > 0:
-            ctxs[(steps - 1) % n].match_finish()
+        for i in range(max(0, steps - lag), steps):
+            ctxs[i % n].match_finish()
     for i in range(max(0, steps - n + 1), steps):
         retire(ctxs[i % n])
 
@@ -353,7 +358,8 @@ def main():
         accumulate(kacc, c)
 
     t0 = time.perf_counter()
-    stream_frames(ctxs, args.steps, Dloc, params, retire, split=not args.no_split)
+    seg_mode = math.isfinite(args.segment_c)
+    stream_frames(ctxs, args.steps, Dloc, params, retire, split=not args.no_split, lag=len(ctxs) - 1 if seg_mode else 1)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0

@@ -24,6 +24,7 @@
 #include "sm_layout_gpu.h"
 #include "sm_pms.h"
 #include "sm_reduce_rule.h"
+#include "sm_seg_gpu.h"
 #include "sm_segment.h"
 #include "sm_tables.inc"
 
@@ -85,6 +86,17 @@ struct PmsState {
     PmsDev dev{};
 };
 
+// segment mode's GPU segmentation of one view (sm_seg_gpu.hip): union-find state, bucketed edges,
+// candidate / rejected / hooked lists, counters; pinned copies of the bucket starts, the counters and
+// the min-size candidates, and the host merge's hooks
+struct SegGpu {
+    DevBuf par, sz, wl, best, first, ebuf, bcnt, list0, list1, rej, hooked, cnt, mlist, hooks;
+    uint32_t gen = 0;  // next Boruvka generation (keys of older ones lose every atomicMin)
+    PinnedVec<uint32_t> h_b, h_cnt, h_hooks;
+    PinnedVec<SegMin> h_min;
+    std::vector<uint32_t> loc;  // the host merge's root -> local id table (all ~0 between calls)
+};
+
 struct MstPending {
     bool active = false;
     int nviews = 0, r = 0;  // contracted rounds enqueued
@@ -125,6 +137,9 @@ struct sm_ctx {
     int seg_trees[2] = {0, 0};
     PinnedVec<uint16_t> h_w[2][2], h_fw[2][2];
     PinnedVec<uint8_t> h_m[2][2];
+    hipStream_t st_seg = nullptr;  // the second view's GPU segmentation (created on first use)
+    hipEvent_t ev_seg[2] = {nullptr, nullptr};
+    SegGpu sg[2];  // GPU segmentation (default; SM_SEG_HOST=1: the host sweep of sm_segment.cpp)
     // asynchronous segment mode (sm_match_begin): the host segmentation runs on a worker thread that
     // waits for the weights' copy (ev_segw), uploads the forest and enqueues the layout; sm_match_finish
     // joins it
@@ -437,7 +452,262 @@ sm_status segment_upload(sm_ctx* ctx, int views) {
     return SM_OK;
 }
 
-sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size) {
+// SM_SEG_HOST=1: segment mode's segmentation by the host sweep (sm_segment.cpp) instead of the GPU
+bool seg_host() { return getenv("SM_SEG_HOST") != nullptr; }
+
+// Boruvka rounds launched over the whole GPU before a bucket's single-workgroup tail, for buckets of
+// more than SM_SEG_SMALL edges (env SM_SEG_GLOBAL_ROUNDS, default 2)
+int seg_global_rounds() { return getenv("SM_SEG_GLOBAL_ROUNDS") ? atoi(getenv("SM_SEG_GLOBAL_ROUNDS")) : 2; }
+
+// buckets of at most this many edges run in one workgroup, consecutive ones in one launch (k_seg_small;
+// env SM_SEG_SMALL, default 16384)
+uint32_t seg_small() { return getenv("SM_SEG_SMALL") ? (uint32_t)atoi(getenv("SM_SEG_SMALL")) : 16384u; }
+
+// The reference's min-size merge (Stereo3DMST.cpp:293-307) over the rejected edges that have an end
+// smaller than ms after the sweep, in (w, id) order: the serial rule on a union-find of the sweep's
+// roots.  Emits the hooks (child root, parent root) and the joined edge ids for k_seg_apply.  The order
+// is one sort of packed (w, id, index) words; roots map to dense local ids through a direct table
+// (loc, N entries, all ~0 on entry and on return).
+int seg_minsize_host(const SegMin* e, uint32_t n, uint32_t ms, uint32_t* out, std::vector<uint32_t>& loc) {
+    std::vector<uint64_t> key(n);
+    for (uint32_t i = 0; i < n; ++i) key[i] = ((uint64_t)e[i].w << 50) | ((uint64_t)e[i].id << 25) | i;
+    std::sort(key.begin(), key.end());
+    std::vector<uint32_t> par, size, root;
+    par.reserve(2 * (size_t)n);
+    size.reserve(2 * (size_t)n);
+    root.reserve(2 * (size_t)n);
+    auto local = [&](uint32_t r, uint32_t s) {
+        uint32_t& l = loc[r];
+        if (l == 0xFFFFFFFFu) {
+            l = (uint32_t)par.size();
+            par.push_back(l);
+            size.push_back(s);
+            root.push_back(r);
+        }
+        return l;
+    };
+    auto find = [&](uint32_t x) {
+        while (par[x] != x) x = par[x] = par[par[x]];
+        return x;
+    };
+    std::vector<uint32_t> ids;
+    int k = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const SegMin& m = e[key[j] & 0x1FFFFFFu];
+        uint32_t a = find(local(m.ra, m.sa)), b = find(local(m.rb, m.sb));
+        if (a == b || (size[a] >= ms && size[b] >= ms)) continue;
+        if (size[a] < size[b]) std::swap(a, b);
+        par[b] = a;
+        size[a] += size[b];
+        out[2 * k] = root[b];
+        out[2 * k + 1] = root[a];
+        ids.push_back(m.id);
+        ++k;
+    }
+    for (int i = 0; i < k; ++i) out[2 * k + i] = ids[i];
+    for (uint32_t r : root) loc[r] = 0xFFFFFFFFu;
+    return k;
+}
+
+double now_ms();
+
+// Segment mode's segmentation on the GPU (sm_seg_gpu.h): the masks and layout weights of the forest
+// land in mR / mD / fwR / fwD as segment_upload leaves them.  Host synchronisations: the bucket sizes
+// (once), the min-size candidates (twice).  With host_copy the weights, masks and layout weights are
+// copied to the h_w / h_m / h_fw host arrays as well (MST_PMS, sm_build_tree_p).
+sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_copy) {
+    static const bool dbg = getenv("SM_SEG_DEBUG") != nullptr;
+    const double t0 = dbg ? now_ms() : 0.0;
+    double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    const int W = ctx->W, H = ctx->H;
+    const size_t N = (size_t)W * H, E = 2 * N;
+    const ViewSet vs(views);
+    SegView sv[2]{};
+    // the second view on its own stream (its launches are latency-bound: the views' chains overlap)
+    hipStream_t sst[2] = {ctx->st, ctx->st};
+    if (vs.n > 1) {
+        if (!ctx->st_seg) {
+            HIPC(hipStreamCreateWithFlags(&ctx->st_seg, hipStreamNonBlocking));
+            HIPC(hipEventCreateWithFlags(&ctx->ev_seg[0], hipEventDisableTiming));
+            HIPC(hipEventCreateWithFlags(&ctx->ev_seg[1], hipEventDisableTiming));
+        }
+        HIPC(hipEventRecord(ctx->ev_seg[0], ctx->st));
+        HIPC(hipStreamWaitEvent(ctx->st_seg, ctx->ev_seg[0], 0));
+        sst[vs.v[1]] = ctx->st_seg;
+    }
+    for (int i = 0; i < vs.n; ++i) {
+        const int v = vs.v[i];
+        SegGpu& g = ctx->sg[v];
+        hipStream_t st = sst[v];
+        CHECK(ensure(ctx, ctx->mR[v], N));
+        CHECK(ensure(ctx, ctx->mD[v], N));
+        CHECK(ensure(ctx, ctx->fwR[v], N * 2));
+        CHECK(ensure(ctx, ctx->fwD[v], N * 2));
+        const bool fresh = g.best.n < N * 8;
+        CHECK(ensure(ctx, g.par, N * 4));
+        CHECK(ensure(ctx, g.sz, N * 4));
+        CHECK(ensure(ctx, g.wl, N * 2));
+        CHECK(ensure(ctx, g.best, N * 8));
+        CHECK(ensure(ctx, g.first, N * 4));
+        CHECK(ensure(ctx, g.ebuf, E * 4));
+        CHECK(ensure(ctx, g.bcnt, (3 * SM_SEG_NB + 1) * 4));
+        CHECK(ensure(ctx, g.list0, E * 16));
+        CHECK(ensure(ctx, g.list1, E * 16));
+        CHECK(ensure(ctx, g.rej, E * 4));
+        CHECK(ensure(ctx, g.hooked, N * 4));
+        CHECK(ensure(ctx, g.cnt, SM_SEG_NCOUNT * 4));
+        CHECK(ensure(ctx, g.mlist, E * sizeof(SegMin)));
+        if (!g.h_b.resize(SM_SEG_NB + 1) || !g.h_cnt.resize(8)) return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
+        if (fresh || g.gen > 0xF0000000u) {  // keys of generation >= 1 beat the initial all-ones
+            HIPC(hipMemsetAsync(g.best.p, 0xFF, N * 8, st));
+            g.gen = 1;
+        }
+        HIPC(hipMemsetAsync(g.bcnt.p, 0, (3 * SM_SEG_NB + 1) * 4, st));
+        HIPC(hipMemsetAsync(g.cnt.p, 0, SM_SEG_NCOUNT * 4, st));
+        SegView& s = sv[v];
+        s.W = W;
+        s.H = H;
+        s.wR = P<uint16_t>(ctx->wR[v]);
+        s.wD = P<uint16_t>(ctx->wD[v]);
+        s.par = P<uint32_t>(g.par);
+        s.sz = P<uint32_t>(g.sz);
+        s.wl = P<uint16_t>(g.wl);
+        s.best = P<unsigned long long>(g.best);
+        s.first = P<uint32_t>(g.first);
+        s.ebuf = P<uint32_t>(g.ebuf);
+        s.bcnt = P<uint32_t>(g.bcnt);
+        s.list[0] = P<uint4>(g.list0);
+        s.list[1] = P<uint4>(g.list1);
+        s.rej = P<uint32_t>(g.rej);
+        s.hooked = P<uint32_t>(g.hooked);
+        s.cnt = P<uint32_t>(g.cnt);
+        s.mlist = P<SegMin>(g.mlist);
+        s.mR = P<uint8_t>(ctx->mR[v]);
+        s.mD = P<uint8_t>(ctx->mD[v]);
+        s.fwR = P<uint16_t>(ctx->fwR[v]);
+        s.fwD = P<uint16_t>(ctx->fwD[v]);
+        HIPC(seg_launch_init(st, s));
+        HIPC(hipMemcpyAsync(g.h_b.data(), P<uint32_t>(g.bcnt) + SM_SEG_NB, (SM_SEG_NB + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPC(seg_launch_scatter(st, s));
+    }
+    auto sync_all = [&]() -> sm_status {
+        HIPC(hipStreamSynchronize(ctx->st));
+        if (vs.n > 1) HIPC(hipStreamSynchronize(ctx->st_seg));
+        return SM_OK;
+    };
+    CHECK(sync_all());
+    if (dbg) t1 = now_ms();
+    const int R = seg_global_rounds();
+    for (int i = 0; i < vs.n; ++i) {
+        const int v = vs.v[i];
+        SegGpu& g = ctx->sg[v];
+        const SegView& s = sv[v];
+        hipStream_t st = sst[v];
+        int L = 0;
+        const uint32_t small = seg_small();
+        for (int w = 0; w < SM_SEG_NB; ++w) {
+            const uint32_t b0 = g.h_b[w], m = g.h_b[w + 1] - b0;
+            if (!m) continue;
+            if (m <= small) {  // a run of small buckets in one workgroup: classify, rounds, sizes
+                int w1 = w + 1, nb = 1;
+                for (; w1 < SM_SEG_NB && g.h_b[w1 + 1] - g.h_b[w1] <= small; ++w1) nb += g.h_b[w1 + 1] > g.h_b[w1];
+                HIPC(seg_launch_small(st, s, w, w1, c, g.gen));
+                g.gen += SM_SEG_TAIL_GENS * (uint32_t)nb;
+                w = w1 - 1;
+                continue;
+            }
+            if (L + R + 2 >= SM_SEG_MAXL) return fail(ctx, SM_ERR_STATE, "segment mode: list counters exhausted");
+            int lin = L++;
+            HIPC(seg_launch_classify(st, s, w, b0, m, c, lin));
+            for (int r = 0; r < R; ++r) {
+                HIPC(seg_launch_round(st, s, m, lin, lin + 1, g.gen++, 0, 0));
+                lin = L++;
+            }
+            HIPC(seg_launch_tail(st, s, lin, 0, g.gen));
+            g.gen += SM_SEG_TAIL_GENS;
+            HIPC(seg_launch_sizes(st, s, w, m));
+        }
+        HIPC(seg_launch_minsize(st, s, min_size, (uint32_t)(g.h_b[SM_SEG_NB])));
+        HIPC(hipMemcpyAsync(g.h_cnt.data(), P<uint32_t>(g.cnt), 8 * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (dbg) t2 = now_ms();
+    CHECK(sync_all());
+    if (dbg) t3 = now_ms();
+    for (int i = 0; i < vs.n; ++i) {
+        const int v = vs.v[i];
+        SegGpu& g = ctx->sg[v];
+        if (g.h_cnt[SM_SEG_C_ERR]) return fail(ctx, SM_ERR_STATE, "segment mode: a Boruvka tail did not converge");
+        const uint32_t nm = g.h_cnt[SM_SEG_C_MIN];
+        if (!g.h_min.resize(nm) || !g.h_hooks.resize(3 * (size_t)nm + 1))
+            return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
+        if (nm) HIPC(hipMemcpyAsync(g.h_min.data(), g.mlist.p, nm * sizeof(SegMin), hipMemcpyDeviceToHost, sst[v]));
+    }
+    CHECK(sync_all());
+    if (dbg) t4 = now_ms();
+    const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
+    int nk[2] = {0, 0};
+    {  // the views' merges in parallel
+        auto merge = [ctx, ms, N](int v) {
+            SegGpu& g = ctx->sg[v];
+            if (g.loc.size() != N) g.loc.assign(N, 0xFFFFFFFFu);
+            return seg_minsize_host(g.h_min.data(), g.h_cnt[SM_SEG_C_MIN], ms, g.h_hooks.data(), g.loc);
+        };
+        std::thread other;
+        if (vs.n > 1) other = std::thread([&] { nk[vs.v[1]] = merge(vs.v[1]); });
+        nk[vs.v[0]] = merge(vs.v[0]);
+        if (other.joinable()) other.join();
+    }
+    for (int i = 0; i < vs.n; ++i) {
+        const int v = vs.v[i];
+        SegGpu& g = ctx->sg[v];
+        hipStream_t st = sst[v];
+        const int k = nk[v];
+        CHECK(ensure(ctx, g.hooks, (3 * (size_t)k + 1) * 4));
+        if (k) HIPC(hipMemcpyAsync(g.hooks.p, g.h_hooks.data(), 3 * (size_t)k * 4, hipMemcpyHostToDevice, st));
+        HIPC(seg_launch_apply(st, sv[v], P<uint32_t>(g.hooks), k));
+        HIPC(seg_launch_trees(st, sv[v]));
+        HIPC(hipMemcpyAsync(g.h_cnt.data() + 4, P<uint32_t>(g.cnt) + SM_SEG_C_TREES, 4, hipMemcpyDeviceToHost, st));
+        if (host_copy) {
+            for (int q = 0; q < 2; ++q)
+                if (!ctx->h_w[v][q].resize(N) || !ctx->h_fw[v][q].resize(N) || !ctx->h_m[v][q].resize(N))
+                    return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
+            HIPC(hipMemcpyAsync(ctx->h_w[v][0].data(), ctx->wR[v].p, N * 2, hipMemcpyDeviceToHost, st));
+            HIPC(hipMemcpyAsync(ctx->h_w[v][1].data(), ctx->wD[v].p, N * 2, hipMemcpyDeviceToHost, st));
+            HIPC(hipMemcpyAsync(ctx->h_m[v][0].data(), ctx->mR[v].p, N, hipMemcpyDeviceToHost, st));
+            HIPC(hipMemcpyAsync(ctx->h_m[v][1].data(), ctx->mD[v].p, N, hipMemcpyDeviceToHost, st));
+            HIPC(hipMemcpyAsync(ctx->h_fw[v][0].data(), ctx->fwR[v].p, N * 2, hipMemcpyDeviceToHost, st));
+            HIPC(hipMemcpyAsync(ctx->h_fw[v][1].data(), ctx->fwD[v].p, N * 2, hipMemcpyDeviceToHost, st));
+        }
+    }
+    if (vs.n > 1) {  // the layout (on st) waits for the second view's forest
+        HIPC(hipEventRecord(ctx->ev_seg[1], ctx->st_seg));
+        HIPC(hipStreamWaitEvent(ctx->st, ctx->ev_seg[1], 0));
+    }
+    if (host_copy) {
+        HIPC(hipStreamSynchronize(ctx->st));
+        for (int i = 0; i < vs.n; ++i) ctx->seg_trees[vs.v[i]] = (int)ctx->sg[vs.v[i]].h_cnt[4];
+    }
+    CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
+    HIPC(hipMemsetAsync(ctx->mst_ok.p, 1, sizeof(int), ctx->st));
+    if (dbg) {
+        const double t5 = now_ms();
+        fprintf(stderr, "segment_gpu: init+buckets %.2f ms, enqueue %.2f, sweep wait %.2f, min-size copy %.2f, host merge + rest %.2f;",
+                t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4);
+        for (int i = 0; i < vs.n; ++i)
+            fprintf(stderr, " view %d: rejected %u, small %u, hooks %u", vs.v[i], ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_REJ],
+                    ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_MIN], ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_HOOK]);
+        fprintf(stderr, "\n");
+    }
+    return SM_OK;
+}
+
+sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size, bool host_copy = true) {
+    if (!seg_host()) {
+        CHECK(segment_gpu(ctx, views, c, min_size, host_copy));
+        ctx->mst_pend.active = false;
+        ctx->seg = true;
+        return SM_OK;
+    }
     CHECK(segment_download(ctx, views));
     CHECK(segment_host(ctx, views, c, min_size));
     CHECK(segment_upload(ctx, views));
@@ -454,8 +724,8 @@ bool seg_sync() {
 }
 
 // tree of the call: the MST (Boruvka) or, for finite c, the segment forest
-sm_status stage_tree(sm_ctx* ctx, int views, const sm_params* p) {
-    if (p && !std::isinf(p->c)) return stage_segment(ctx, views, p->c, p->min_size);
+sm_status stage_tree(sm_ctx* ctx, int views, const sm_params* p, bool host_copy) {
+    if (p && !std::isinf(p->c)) return stage_segment(ctx, views, p->c, p->min_size, host_copy);
     ctx->seg = false;
     return stage_mst(ctx, views);
 }
@@ -1737,6 +2007,7 @@ void sm_destroy(sm_ctx* ctx) {
     if (ctx->seg_worker.joinable()) ctx->seg_worker.join();  // a begun segment-mode call's host worker
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     if (ctx->st_tree) (void)hipStreamSynchronize(ctx->st_tree);  // tree kernels may still run there
+    if (ctx->st_seg) (void)hipStreamSynchronize(ctx->st_seg);
     if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamSynchronize(ctx->st2);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut, &ctx->post_mask, &ctx->post_scratch,
@@ -1749,7 +2020,13 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->idx[v], &ctx->minc[v], &ctx->disp[v], &ctx->cand[v], &ctx->gmin[v], &ctx->gidx[v], &ctx->vol[v], &ctx->rec[v], &ctx->rec4[v], &ctx->vin[v],
                          &ctx->cedge[v], &ctx->clab[v], &ctx->chook[v], &ctx->ccnt[v], &ctx->fwR[v], &ctx->fwD[v]};
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
+        SegGpu& g = ctx->sg[v];
+        DevBuf* sg[] = {&g.par, &g.sz, &g.wl, &g.best, &g.first, &g.ebuf, &g.bcnt, &g.list0, &g.list1, &g.rej, &g.hooked,
+                        &g.cnt, &g.mlist, &g.hooks};
+        for (DevBuf* b : sg) if (b->p) (void)hipFree(b->p);
     }
+    for (auto e : ctx->ev_seg) if (e) (void)hipEventDestroy(e);
+    if (ctx->st_seg) (void)hipStreamDestroy(ctx->st_seg);
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->ev_layout) (void)hipEventDestroy(ctx->ev_layout);
     if (ctx->ev_segw) (void)hipEventDestroy(ctx->ev_segw);
@@ -1886,18 +2163,23 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
         // segment mode: the host segmentation on a worker thread, so begin returns at once and the
         // caller's other contexts keep the GPU busy; the worker uploads the forest and enqueues the
         // layout on this context's stream, and sm_match_finish joins it before using the layout
-        CHECK(segment_download(ctx, ctx->views));
+        const bool gpu = !seg_host();
+        if (!gpu) CHECK(segment_download(ctx, ctx->views));
         ctx->mst_pend.active = false;
         ctx->seg = true;
         const int views = ctx->views;
         const float c = p->c;
         const int min_size = p->min_size;
         ctx->seg_status = SM_OK;
-        ctx->seg_worker = std::thread([ctx, views, c, min_size] {
+        ctx->seg_worker = std::thread([ctx, views, c, min_size, gpu] {
             auto work = [&]() -> sm_status {
                 HIPC(hipSetDevice(ctx->device));
-                CHECK(segment_host(ctx, views, c, min_size));
-                CHECK(segment_upload(ctx, views));
+                if (gpu) {
+                    CHECK(segment_gpu(ctx, views, c, min_size, false));
+                } else {
+                    CHECK(segment_host(ctx, views, c, min_size));
+                    CHECK(segment_upload(ctx, views));
+                }
                 HIPC(hipEventRecord(ctx->ev[2], ctx->st));
                 return stage_layout_enqueue(ctx, views);
             };
@@ -1908,7 +2190,7 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
         ctx->pend_p = *p;
         return SM_OK;
     }
-    CHECK(stage_tree(ctx, ctx->views, p));
+    CHECK(stage_tree(ctx, ctx->views, p, false));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
     CHECK(stage_layout_enqueue(ctx, ctx->views));
     if (ts.main) {
@@ -2024,7 +2306,7 @@ sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int str
     HIPC(hipSetDevice(ctx->device));
     CHECK(upload(ctx, bgr, bgr, W, H, stride));
     CHECK(stage_prep(ctx));
-    CHECK(stage_tree(ctx, 1, p));  // the image is uploaded as both views: view 0 only
+    CHECK(stage_tree(ctx, 1, p, true));  // the image is uploaded as both views: view 0 only
     CHECK(stage_layout(ctx, 1));
     const size_t N = (size_t)W * H;
     // segment mode: the virtual edges that link the trees are not part of the reported forest
@@ -2080,7 +2362,7 @@ sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, 
     CHECK(upload(ctx, l, r, W, H, stride));
     CHECK(stage_prep(ctx));
     ctx->views = 3;
-    CHECK(stage_tree(ctx, 3, p));
+    CHECK(stage_tree(ctx, 3, p, false));
     CHECK(stage_layout(ctx, 3));
     const size_t N = (size_t)W * H;
     const int Dpad = dpad_for(D);

@@ -1,0 +1,78 @@
+// sm_seg_gpu.h -- segment mode's Felzenszwalb segmentation on the GPU (sm_seg_gpu.hip), driven per
+// view by segment_gpu() in sm_api.cpp.  Library-internal.
+//
+// Reference: segment_graph (include/segment-graph.h:54-89) over the (w, a, b)-sorted grid edges of
+// Stereo3DMST.cpp:242-282, then the min-size merge of :293-307.  Bit-exact restatement of the serial
+// sweep, bucket by bucket:
+//   * within one weight bucket w, a component is OPEN if w <= wl + c/size at the bucket's start (the
+//     reference's threshold).  A closed component rejects every edge of the bucket (its threshold only
+//     changes when it joins, and joining needs its acceptance), and a component that joined in the
+//     bucket has threshold w + c/size >= w, so it accepts every later edge of the bucket.  So the
+//     bucket joins exactly the open components that its open-open edges connect, whatever the order,
+//     and the edges the serial sweep marks are the first (by edge id = the reference's (a, b) order)
+//     edge to connect two groups: the minimum spanning forest of the bucket's open-open edges keyed by
+//     id, which Boruvka finds in parallel;
+//   * the sweep rejects exactly the edges whose two components differ and one of them is closed; a
+//     closed component never joins again in the sweep, so such an edge still joins two different
+//     components afterwards.  The min-size merge only joins an edge with a component smaller than
+//     min_size, and sizes only grow, so it only needs the rejected edges with a small end: those go
+//     to the host (few), which runs the merge's serial rule over them in (w, id) order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SM_SEG_NB 766        // weight buckets: |dR| + |dG| + |dB| in [0, 765]
+#define SM_SEG_TILE 4096     // pixels per block of the bucketing kernels
+#define SM_SEG_MAXL 65536    // list counters per view and frame
+#define SM_SEG_TAIL_GENS 64  // Boruvka rounds reserved for one tail launch
+
+// counters (uint32) of one view: [0] rejected, [1] hooked roots, [2] trees, [3] min-size candidates,
+// [4] error flags, [8 + L] the length of candidate list L, [8 + SM_SEG_MAXL + b] bucket b's first
+// hooked-root index
+#define SM_SEG_C_REJ 0
+#define SM_SEG_C_HOOK 1
+#define SM_SEG_C_TREES 2
+#define SM_SEG_C_MIN 3
+#define SM_SEG_C_ERR 4
+#define SM_SEG_C_LIST 8
+#define SM_SEG_C_BUCKET (8 + SM_SEG_MAXL)
+#define SM_SEG_NCOUNT (8 + SM_SEG_MAXL + SM_SEG_NB)
+
+// a rejected edge with a component smaller than min_size at the end of the sweep
+struct SegMin {
+    uint32_t id, w, ra, rb, sa, sb;
+};
+
+struct SegView {
+    int W, H;
+    const uint16_t* wR;
+    const uint16_t* wD;
+    uint32_t* par;              // [N] union-find parent (roots: par == self)
+    uint32_t* sz;               // [N] component size (roots)
+    uint16_t* wl;               // [N] weight of the root's last join (threshold wl + c/size)
+    unsigned long long* best;   // [N] Boruvka keys ((~gen) << 32 | edge id), never reset
+    uint32_t* first;            // [N] a tree's first pixel in raster order
+    uint32_t* ebuf;             // [E] edge ids grouped by weight
+    uint32_t* bcnt;             // [NB] counts, [NB + 1] starts (at bcnt + NB), [NB] cursors (at bcnt + 2 NB + 1)
+    uint4* list[2];             // candidate lists {id, ra, rb, 0}
+    uint32_t* rej;              // rejected edge ids
+    uint32_t* hooked;           // roots hooked by the sweep, bucket after bucket
+    uint32_t* cnt;              // SM_SEG_NCOUNT counters
+    SegMin* mlist;              // min-size candidates
+    uint8_t* mR;
+    uint8_t* mD;
+    uint16_t* fwR;
+    uint16_t* fwD;
+};
+
+hipError_t seg_launch_init(hipStream_t st, const SegView& v);
+hipError_t seg_launch_scatter(hipStream_t st, const SegView& v);
+hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout);
+hipError_t seg_launch_round(hipStream_t st, const SegView& v, uint32_t m, int lin, int lout, uint32_t gen, int bin,
+                            int bout);
+hipError_t seg_launch_tail(hipStream_t st, const SegView& v, int lin, int bin, uint32_t gen0);
+hipError_t seg_launch_small(hipStream_t st, const SegView& v, int w0, int w1, float c, uint32_t gen0);
+hipError_t seg_launch_sizes(hipStream_t st, const SegView& v, int w, uint32_t m);
+hipError_t seg_launch_minsize(hipStream_t st, const SegView& v, int min_size, uint32_t nrej_max);
+hipError_t seg_launch_apply(hipStream_t st, const SegView& v, const uint32_t* hooks, int nhooks);
+hipError_t seg_launch_trees(hipStream_t st, const SegView& v);

@@ -1,0 +1,458 @@
+// sm_seg_gpu.hip -- segment mode's Felzenszwalb segmentation (c finite) on the GPU, bucket by bucket.
+// The argument that makes it exact is in sm_seg_gpu.h; DESIGN.md 4.5 has the measurements.
+//
+// Per view and frame:
+//   k_seg_init      union-find reset, masks cleared, weight histogram (LDS, one atomic per bin and block)
+//   k_seg_scan      bucket starts (one block)
+//   k_seg_scatter   edge ids into their weight bucket (order inside a bucket is free: Boruvka keys by id)
+//   per non-empty bucket w, in ascending order:
+//     k_seg_classify  roots of both ends; open-open edges between two components -> candidate list,
+//                     other edges between two components -> rejected
+//     k_seg_best / k_seg_hook   global Boruvka rounds (big buckets): each root's minimum-id crossing
+//                     edge, then hooks along those edges (mutual pairs: the larger root onto the smaller)
+//     k_seg_tail      the remaining rounds in one workgroup, until no candidate crosses two components
+//     k_seg_sizes     sizes of the joined components, last-join weight w
+//     (k_seg_small: all of it in one workgroup, for a run of buckets of at most SM_SEG_SMALL edges)
+//   k_seg_minsize   rejected edges with an end smaller than min_size -> the host's serial merge
+//   k_seg_apply     the host's merges (root hooks, marked edges)
+//   k_seg_first / k_seg_virtual   first pixel of each tree, virtual edges to link the forest (sm_segment.cpp)
+#include <hip/hip_runtime.h>
+
+#include "sm_seg_gpu.h"
+#include "sm_segment.h"
+
+namespace {
+
+__device__ __forceinline__ uint32_t seg_find(uint32_t* par, uint32_t x) {
+    // path halving; a concurrent writer only ever stores an ancestor, so every value read is valid
+    for (;;) {
+        const uint32_t p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p == x) return x;
+        const uint32_t g = __hip_atomic_load(par + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g == p) return p;
+        __hip_atomic_store(par + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x = g;
+    }
+}
+
+__device__ __forceinline__ uint32_t edge_b(uint32_t id, int W) { return (id >> 1) + ((id & 1u) ? (uint32_t)W : 1u); }
+
+// the reference's acceptance test at the bucket's start: (double)w <= w_last + (double)(c / (float)size)
+__device__ __forceinline__ bool seg_open(const SegView& v, uint32_t r, double wd, float c) {
+    return wd <= (double)v.wl[r] + (double)__fdiv_rn(c, (float)v.sz[r]);
+}
+
+// wave-aggregated append: returns this lane's slot (valid where pred)
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0) return 0;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+__global__ void __launch_bounds__(256) k_seg_init(SegView v) {
+    __shared__ uint32_t hist[SM_SEG_NB];
+    const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
+    for (int i = threadIdx.x; i < SM_SEG_NB; i += 256) hist[i] = 0;
+    __syncthreads();
+    const uint32_t p0 = blockIdx.x * SM_SEG_TILE;
+    for (uint32_t k = threadIdx.x; k < SM_SEG_TILE; k += 256) {
+        const uint32_t p = p0 + k;
+        if (p >= N) break;
+        v.par[p] = p;
+        v.sz[p] = 1;
+        v.wl[p] = 0;
+        v.first[p] = 0xFFFFFFFFu;
+        v.mR[p] = 0;
+        v.mD[p] = 0;
+        const uint32_t x = p % (uint32_t)v.W, y = p / (uint32_t)v.W;
+        if (x + 1 < (uint32_t)v.W) atomicAdd(&hist[v.wR[p]], 1u);
+        if (y + 1 < (uint32_t)v.H) atomicAdd(&hist[v.wD[p]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SM_SEG_NB; i += 256)
+        if (hist[i]) atomicAdd(&v.bcnt[i], hist[i]);
+}
+
+__global__ void __launch_bounds__(1024) k_seg_scan(SegView v) {
+    // exclusive scan of SM_SEG_NB counts -> starts (NB + 1) and cursors
+    __shared__ uint32_t s[1024];
+    const int t = threadIdx.x;
+    uint32_t x = t < SM_SEG_NB ? v.bcnt[t] : 0u;
+    s[t] = x;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint32_t y = t >= o ? s[t - o] : 0u;
+        __syncthreads();
+        s[t] += y;
+        __syncthreads();
+    }
+    uint32_t* start = v.bcnt + SM_SEG_NB;
+    uint32_t* cur = v.bcnt + 2 * SM_SEG_NB + 1;
+    if (t < SM_SEG_NB) {
+        start[t] = s[t] - x;
+        cur[t] = s[t] - x;
+    }
+    if (t == SM_SEG_NB - 1) start[SM_SEG_NB] = s[t];
+}
+
+__global__ void __launch_bounds__(256) k_seg_scatter(SegView v) {
+    __shared__ uint32_t hist[SM_SEG_NB];
+    const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
+    for (int i = threadIdx.x; i < SM_SEG_NB; i += 256) hist[i] = 0;
+    __syncthreads();
+    const uint32_t p0 = blockIdx.x * SM_SEG_TILE;
+    for (uint32_t k = threadIdx.x; k < SM_SEG_TILE; k += 256) {
+        const uint32_t p = p0 + k;
+        if (p >= N) break;
+        const uint32_t x = p % (uint32_t)v.W, y = p / (uint32_t)v.W;
+        if (x + 1 < (uint32_t)v.W) atomicAdd(&hist[v.wR[p]], 1u);
+        if (y + 1 < (uint32_t)v.H) atomicAdd(&hist[v.wD[p]], 1u);
+    }
+    __syncthreads();
+    uint32_t* cur = v.bcnt + 2 * SM_SEG_NB + 1;
+    for (int i = threadIdx.x; i < SM_SEG_NB; i += 256)
+        if (hist[i]) hist[i] = atomicAdd(&cur[i], hist[i]);  // this block's range in bucket i
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < SM_SEG_TILE; k += 256) {
+        const uint32_t p = p0 + k;
+        if (p >= N) break;
+        const uint32_t x = p % (uint32_t)v.W, y = p / (uint32_t)v.W;
+        if (x + 1 < (uint32_t)v.W) v.ebuf[atomicAdd(&hist[v.wR[p]], 1u)] = 2u * p;
+        if (y + 1 < (uint32_t)v.H) v.ebuf[atomicAdd(&hist[v.wD[p]], 1u)] = 2u * p + 1u;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_seg_classify(SegView v, int w, uint32_t s, uint32_t m, float c, int lout,
+                                                      int bucket) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) v.cnt[SM_SEG_C_BUCKET + bucket] = v.cnt[SM_SEG_C_HOOK];  // first hooked root of this bucket
+    bool cand = false, rej = false;
+    uint32_t id = 0, ra = 0, rb = 0;
+    if (i < m) {
+        id = v.ebuf[s + i];
+        ra = seg_find(v.par, id >> 1);
+        rb = seg_find(v.par, edge_b(id, v.W));
+        if (ra != rb) {
+            const double wd = (double)w;
+            cand = seg_open(v, ra, wd, c) && seg_open(v, rb, wd, c);
+            rej = !cand;
+        }
+    }
+    const uint32_t pc = wave_append(v.cnt + SM_SEG_C_LIST + lout, cand);
+    if (cand) v.list[lout & 1][pc] = make_uint4(id, ra, rb, 0u);
+    const uint32_t pr = wave_append(v.cnt + SM_SEG_C_REJ, rej);
+    if (rej) v.rej[pr] = id;
+}
+
+__device__ __forceinline__ unsigned long long seg_key(uint32_t gen, uint32_t id) {
+    return ((unsigned long long)(0xFFFFFFFFu - gen) << 32) | id;
+}
+
+// one Boruvka selection over list lin: crossing edges -> list lout with their current roots, and each
+// root's minimum key
+__global__ void __launch_bounds__(256) k_seg_best(SegView v, int lin, int lout, uint32_t gen) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t n = v.cnt[SM_SEG_C_LIST + lin];
+    bool cross = false;
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (i < n) {
+        e = v.list[lin & 1][i];
+        e.y = seg_find(v.par, e.y);
+        e.z = seg_find(v.par, e.z);
+        cross = e.y != e.z;
+        if (cross) {
+            const unsigned long long key = seg_key(gen, e.x);
+            atomicMin(v.best + e.y, key);
+            atomicMin(v.best + e.z, key);
+        }
+    }
+    const uint32_t po = wave_append(v.cnt + SM_SEG_C_LIST + lout, cross);
+    if (cross) v.list[lout & 1][po] = e;
+}
+
+__device__ __forceinline__ void seg_hook_edge(const SegView& v, uint4 e, uint32_t gen, bool pred) {
+    uint32_t child = 0, parent = 0;
+    bool hook = false;
+    if (pred) {
+        const unsigned long long key = seg_key(gen, e.x);
+        const bool ba = __hip_atomic_load(v.best + e.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key;
+        const bool bb = __hip_atomic_load(v.best + e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key;
+        if (ba || bb) {
+            hook = true;
+            if (ba && bb) {  // mutual minimum: one hook, the larger root onto the smaller
+                child = e.y > e.z ? e.y : e.z;
+                parent = e.y > e.z ? e.z : e.y;
+            } else if (ba) {
+                child = e.y;
+                parent = e.z;
+            } else {
+                child = e.z;
+                parent = e.y;
+            }
+        }
+    }
+    const uint32_t ph = wave_append(v.cnt + SM_SEG_C_HOOK, hook);
+    if (hook) {
+        __hip_atomic_store(v.par + child, parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v.hooked[ph] = child;
+        const uint32_t a = e.x >> 1;
+        if (e.x & 1u)
+            v.mD[a] = 1;
+        else
+            v.mR[a] = 1;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_seg_hook(SegView v, int lout, uint32_t gen) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t n = v.cnt[SM_SEG_C_LIST + lout];
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (i < n) e = v.list[lout & 1][i];
+    seg_hook_edge(v, e, gen, i < n);
+}
+
+// workgroup barrier that also orders global memory across its waves: release before, acquire (L1
+// invalidate) after, so a wave never reads a list entry, root or key through a stale L1 line
+__device__ __forceinline__ void seg_wg_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// the rest of a bucket's Boruvka rounds in one workgroup: n candidates in buffer b ping-pong with the
+// other buffer; gens gen0, gen0 + 1, ... (at most SM_SEG_TAIL_GENS).  Returns the rounds run, or -1 if
+// they did not converge.
+__device__ int seg_wg_rounds(const SegView& v, int b, uint32_t n, uint32_t gen0, uint32_t* s_out) {
+    uint32_t g = 0;
+    for (; n > 0; ++g) {
+        if (g == SM_SEG_TAIL_GENS) {  // cannot happen (Boruvka halves the components each round)
+            if (threadIdx.x == 0) atomicOr(v.cnt + SM_SEG_C_ERR, 1u);
+            return -1;
+        }
+        const uint32_t gen = gen0 + g;
+        if (threadIdx.x == 0) *s_out = 0;
+        seg_wg_sync();
+        const uint4* in = v.list[b];
+        uint4* out = v.list[b ^ 1];
+        for (uint32_t i0 = 0; i0 < n; i0 += 1024) {
+            const uint32_t i = i0 + threadIdx.x;
+            bool cross = false;
+            uint4 e = make_uint4(0, 0, 0, 0);
+            if (i < n) {
+                e = in[i];
+                e.y = seg_find(v.par, e.y);
+                e.z = seg_find(v.par, e.z);
+                cross = e.y != e.z;
+                if (cross) {
+                    const unsigned long long key = seg_key(gen, e.x);
+                    atomicMin(v.best + e.y, key);
+                    atomicMin(v.best + e.z, key);
+                }
+            }
+            const uint32_t po = wave_append(s_out, cross);
+            if (cross) out[po] = e;
+        }
+        seg_wg_sync();
+        const uint32_t m = *s_out;
+        for (uint32_t i0 = 0; i0 < m; i0 += 1024) {
+            const uint32_t i = i0 + threadIdx.x;
+            uint4 e = make_uint4(0, 0, 0, 0);
+            if (i < m) e = out[i];
+            seg_hook_edge(v, e, gen, i < m);
+        }
+        seg_wg_sync();
+        n = m;
+        b ^= 1;
+    }
+    return (int)g;
+}
+
+__global__ void __launch_bounds__(1024) k_seg_tail(SegView v, int lin, uint32_t gen0) {
+    __shared__ uint32_t s_out;
+    seg_wg_rounds(v, lin & 1, v.cnt[SM_SEG_C_LIST + lin], gen0, &s_out);
+}
+
+__device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, int w) {
+    const uint32_t r = v.hooked[i];
+    const uint32_t t = seg_find(v.par, r);
+    atomicAdd(v.sz + t, v.sz[r]);  // r's size is its size at the bucket's start (only roots grow)
+    v.wl[t] = (uint16_t)w;
+}
+
+// a run of small buckets [w0, w1) (each of at most SM_SEG_SMALL edges) in one workgroup, one bucket
+// after the other: classify, Boruvka rounds, sizes; gens from gen0, at most SM_SEG_TAIL_GENS per bucket
+__global__ void __launch_bounds__(1024) k_seg_small(SegView v, int w0, int w1, float c, uint32_t gen0) {
+    __shared__ uint32_t s_n, s_out, s_h0;
+    const uint32_t* start = v.bcnt + SM_SEG_NB;
+    uint32_t gen = gen0;
+    for (int w = w0; w < w1; ++w) {
+        const uint32_t s = start[w], m = start[w + 1] - s;
+        if (m == 0) continue;
+        if (threadIdx.x == 0) {
+            s_n = 0;
+            s_h0 = __hip_atomic_load(v.cnt + SM_SEG_C_HOOK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        seg_wg_sync();
+        const double wd = (double)w;
+        for (uint32_t i0 = 0; i0 < m; i0 += 1024) {
+            const uint32_t i = i0 + threadIdx.x;
+            bool cand = false, rej = false;
+            uint32_t id = 0, ra = 0, rb = 0;
+            if (i < m) {
+                id = v.ebuf[s + i];
+                ra = seg_find(v.par, id >> 1);
+                rb = seg_find(v.par, edge_b(id, v.W));
+                if (ra != rb) {
+                    cand = seg_open(v, ra, wd, c) && seg_open(v, rb, wd, c);
+                    rej = !cand;
+                }
+            }
+            const uint32_t pc = wave_append(&s_n, cand);
+            if (cand) v.list[0][pc] = make_uint4(id, ra, rb, 0u);
+            const uint32_t pr = wave_append(v.cnt + SM_SEG_C_REJ, rej);
+            if (rej) v.rej[pr] = id;
+        }
+        seg_wg_sync();
+        const int r = seg_wg_rounds(v, 0, s_n, gen, &s_out);
+        if (r < 0) return;
+        gen += (uint32_t)r;
+        const uint32_t h1 = __hip_atomic_load(v.cnt + SM_SEG_C_HOOK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t i = s_h0 + threadIdx.x; i < h1; i += 1024) seg_size_update(v, i, w);
+        seg_wg_sync();  // sizes final before the next bucket's acceptance tests
+    }
+}
+
+__global__ void __launch_bounds__(256) k_seg_sizes(SegView v, int w, int bucket) {
+    const uint32_t h0 = v.cnt[SM_SEG_C_BUCKET + bucket], h1 = v.cnt[SM_SEG_C_HOOK];
+    const uint32_t i = h0 + blockIdx.x * 256 + threadIdx.x;
+    if (i >= h1) return;
+    seg_size_update(v, i, w);
+}
+
+__global__ void __launch_bounds__(256) k_seg_minsize(SegView v, uint32_t ms) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t n = v.cnt[SM_SEG_C_REJ];
+    bool keep = false;
+    SegMin r{};
+    if (i < n) {
+        const uint32_t id = v.rej[i];
+        const uint32_t a = id >> 1;
+        r.id = id;
+        r.w = (id & 1u) ? v.wD[a] : v.wR[a];
+        r.ra = seg_find(v.par, a);
+        r.rb = seg_find(v.par, edge_b(id, v.W));
+        r.sa = v.sz[r.ra];
+        r.sb = v.sz[r.rb];
+        keep = r.sa < ms || r.sb < ms;
+    }
+    const uint32_t p = wave_append(v.cnt + SM_SEG_C_MIN, keep);
+    if (keep) v.mlist[p] = r;
+}
+
+// hooks[2k] = child root, hooks[2k + 1] = parent root (0xFFFFFFFF: none) ; marked edge ids after the
+// pairs: hooks[2 * nhooks + k]
+__global__ void __launch_bounds__(256) k_seg_apply(SegView v, const uint32_t* hooks, int nhooks) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nhooks) return;
+    v.par[hooks[2 * i]] = hooks[2 * i + 1];
+    const uint32_t id = hooks[2 * nhooks + i];
+    if (id & 1u)
+        v.mD[id >> 1] = 1;
+    else
+        v.mR[id >> 1] = 1;
+}
+
+__global__ void __launch_bounds__(256) k_seg_first(SegView v) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
+    const uint32_t r = p < N ? seg_find(v.par, p) : 0xFFFFFFFFu;
+    // one atomic per run of equal roots in the wave (rows are mostly long runs of one tree), and none
+    // where the tree's first pixel is already known to be smaller
+    const uint32_t rprev = __shfl_up(r, 1);
+    if (p >= N) return;
+    if ((__lane_id() == 0 || rprev != r) && v.first[r] > p) atomicMin(v.first + r, p);
+    v.fwR[p] = v.wR[p];
+    v.fwD[p] = v.wD[p];
+}
+
+__global__ void __launch_bounds__(256) k_seg_virtual(SegView v) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
+    const bool root = p < N && v.first[seg_find(v.par, p)] == p;
+    wave_append(v.cnt + SM_SEG_C_TREES, root);
+    if (!root || p == 0) return;
+    // the tree's first pixel links to its left neighbour, in column 0 to its upper one (sm_segment.cpp)
+    if (p % (uint32_t)v.W > 0) {
+        v.mR[p - 1] = 1;
+        v.fwR[p - 1] = SM_VIRTUAL_W;
+    } else {
+        v.mD[p - (uint32_t)v.W] = 1;
+        v.fwD[p - (uint32_t)v.W] = SM_VIRTUAL_W;
+    }
+}
+
+unsigned blocks_of(size_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace
+
+hipError_t seg_launch_init(hipStream_t st, const SegView& v) {
+    const size_t N = (size_t)v.W * v.H;
+    hipLaunchKernelGGL(k_seg_init, dim3(blocks_of(N, SM_SEG_TILE)), dim3(256), 0, st, v);
+    hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(1024), 0, st, v);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_scatter(hipStream_t st, const SegView& v) {
+    const size_t N = (size_t)v.W * v.H;
+    hipLaunchKernelGGL(k_seg_scatter, dim3(blocks_of(N, SM_SEG_TILE)), dim3(256), 0, st, v);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout) {
+    hipLaunchKernelGGL(k_seg_classify, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, w, s, m, c, lout, w);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_round(hipStream_t st, const SegView& v, uint32_t m, int lin, int lout, uint32_t gen, int, int) {
+    hipLaunchKernelGGL(k_seg_best, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, lin, lout, gen);
+    hipLaunchKernelGGL(k_seg_hook, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, lout, gen);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_tail(hipStream_t st, const SegView& v, int lin, int, uint32_t gen0) {
+    hipLaunchKernelGGL(k_seg_tail, dim3(1), dim3(1024), 0, st, v, lin, gen0);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_small(hipStream_t st, const SegView& v, int w0, int w1, float c, uint32_t gen0) {
+    hipLaunchKernelGGL(k_seg_small, dim3(1), dim3(1024), 0, st, v, w0, w1, c, gen0);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_sizes(hipStream_t st, const SegView& v, int w, uint32_t m) {
+    hipLaunchKernelGGL(k_seg_sizes, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, w, w);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_minsize(hipStream_t st, const SegView& v, int min_size, uint32_t nrej_max) {
+    const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
+    if (nrej_max) hipLaunchKernelGGL(k_seg_minsize, dim3(blocks_of(nrej_max, 256)), dim3(256), 0, st, v, ms);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_apply(hipStream_t st, const SegView& v, const uint32_t* hooks, int nhooks) {
+    if (nhooks) hipLaunchKernelGGL(k_seg_apply, dim3(blocks_of((size_t)nhooks, 256)), dim3(256), 0, st, v, hooks, nhooks);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_trees(hipStream_t st, const SegView& v) {
+    const size_t N = (size_t)v.W * v.H;
+    hipLaunchKernelGGL(k_seg_first, dim3(blocks_of(N, 256)), dim3(256), 0, st, v);
+    hipLaunchKernelGGL(k_seg_virtual, dim3(blocks_of(N, 256)), dim3(256), 0, st, v);
+    return hipGetLastError();
+}

@@ -1,6 +1,7 @@
-"""bench.py's frame streaming (CPU): with split calls every frame is begun, finished and retired
-exactly once, in frame order per context, a context never holds two frames, and a frame is
-finished before it is retired (the C-ABI returns SM_ERR_STATE otherwise)."""
+"""bench.py's frame streaming (CPU): with split calls (finish lagging 1 .. n-1 frames behind begin)
+every frame is begun, finished and retired exactly once, in frame order per context, a context
+never holds two frames, and a frame is finished before it is retired (the C-ABI returns
+SM_ERR_STATE otherwise)."""
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -29,7 +30,8 @@ class FakeCtx:
 @pytest.mark.parametrize("n", [1, 2, 3, 4])
 @pytest.mark.parametrize("steps", [0, 1, 2, 3, 7, 12])
 @pytest.mark.parametrize("split", [True, False])
-def test_stream_frames_order(n, steps, split):
+@pytest.mark.parametrize("lag", [1, 2, 3])
+def test_stream_frames_order(n, steps, split, lag):
     log = []
     ctxs = [FakeCtx(k, log) for k in range(n)]
 
@@ -38,7 +40,7 @@ def test_stream_frames_order(n, steps, split):
         c.state = "idle"
         log.append(("retire", c.k))
 
-    bench.stream_frames(ctxs, steps, 64, None, retire, split=split)
+    bench.stream_frames(ctxs, steps, 64, None, retire, split=split, lag=lag)
     assert all(c.state == "idle" for c in ctxs)
     for what in ("begin", "finish", "retire"):
         seq = [k for w, k in log if w == what]

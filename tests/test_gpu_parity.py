@@ -402,8 +402,8 @@ def test_large_disp_begin_pads(gpu_ctx):
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
 
 
-def test_flir_c1_bitexact(gpu_ctx):
-    """BASELINE config 0: the FLIR 000020 pair, 2048x1536, D=64."""
+def flir_pair():
+    """The FLIR 000020 pair (BGR, 2048x1536), decode-checked against the committed sums."""
     from PIL import Image
     d = os.path.join(GOLDEN, "flir")
     L = np.ascontiguousarray(np.array(Image.open(os.path.join(d, "000020_191400042.jpg")).convert("RGB"))[:, :, ::-1])
@@ -411,6 +411,12 @@ def test_flir_c1_bitexact(gpu_ctx):
     with np.load(os.path.join(d, "decode_check.npz")) as chk:
         assert int(L.astype(np.int64).sum()) == int(chk["left_sum"])
         assert int(R.astype(np.int64).sum()) == int(chk["right_sum"])
+    return L, R
+
+
+def test_flir_c1_bitexact(gpu_ctx):
+    """BASELINE config 0: the FLIR 000020 pair, 2048x1536, D=64."""
+    L, R = flir_pair()
     D = 64
     out = gpu_ctx.match(L, R, D)
     ref = O.match(L, R, D, nthreads=16)
@@ -743,6 +749,44 @@ def test_segment_match_bitexact_synthetic(gpu_ctx, monkeypatch, W, H, D, c):
     for v in ("left", "right"):
         np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+
+
+@pytest.mark.parametrize("src,c,min_size", [("synth", 5000.0, 200), ("synth", 300.0, 20), ("synth", 40.0, 5),
+                                            ("flir", 5000.0, 200), ("flir", 150.0, 50)])
+def test_full_size_segment_forest(gpu_ctx, src, c, min_size):
+    """The GPU segmentation (sm_seg_gpu.hip, bucket-synchronous Boruvka + host min-size merge) at full
+    size: forest masks and tree count equal to the oracle's serial segment_graph + min-size merge, on a
+    synthetic C2 view and on the FLIR pair's 2048x1536 left image (a broad weight histogram)."""
+    import stereomatch_amd as sm
+    if src == "synth":
+        img, _, _ = make_pair(1920, 1200, 128, index=0)
+    else:
+        img = flir_pair()[0]
+    H, W, _ = img.shape
+    t = gpu_ctx.build_tree(img, sm.default_params(c=c, min_size=min_size))
+    wR, wD = O.edge_weights(O.median3(img))
+    mask, n = O.segment(W, H, wR, wD, c, min_size)
+    np.testing.assert_array_equal(t["mask"], mask)
+    assert t["ntrees"] == n
+
+
+@pytest.mark.parametrize("env", [{"SM_SEG_SMALL": "0"}, {"SM_SEG_SMALL": "0", "SM_SEG_GLOBAL_ROUNDS": "0"},
+                                 {"SM_SEG_SMALL": "100000000"}, {"SM_SEG_GLOBAL_ROUNDS": "7"}, {"SM_SEG_HOST": "1"}])
+def test_segment_forest_schedules(gpu_ctx, monkeypatch, env):
+    """The GPU segmentation's launch schedules give the same forest: every bucket over the whole GPU
+    (with and without global Boruvka rounds before the one-workgroup tail), every bucket in one
+    workgroup, more global rounds; and the host sweep (SM_SEG_HOST)."""
+    import stereomatch_amd as sm
+    for k, val in env.items():
+        monkeypatch.setenv(k, val)
+    img, _, _ = make_pair(640, 480, 64, index=3)
+    H, W, _ = img.shape
+    wR, wD = O.edge_weights(O.median3(img))
+    for c, ms in ((5000.0, 200), (120.0, 30)):
+        t = gpu_ctx.build_tree(img, sm.default_params(c=c, min_size=ms))
+        mask, n = O.segment(W, H, wR, wD, c, ms)
+        np.testing.assert_array_equal(t["mask"], mask)
+        assert t["ntrees"] == n
 
 
 def test_full_size_c2_segment_match_bitexact(gpu_ctx):
