@@ -90,7 +90,8 @@ struct PmsState {
 // candidate / rejected / hooked lists, counters; pinned copies of the bucket starts, the counters and
 // the min-size candidates, and the host merge's hooks
 struct SegGpu {
-    DevBuf par, sz, wl, best, first, ebuf, bcnt, list0, list1, rej, hooked, cnt, mlist, hooks;
+    DevBuf par, sz, wl, best, first, ebuf, bcnt, list0, list1, rej, hooked, cnt, mlist, hooks, mkey, mval, msorted, stemp;
+    size_t stemp_bytes = 0;
     uint32_t gen = 0;  // next Boruvka generation (keys of older ones lose every atomicMin)
     PinnedVec<uint32_t> h_b, h_cnt, h_hooks;
     PinnedVec<SegMin> h_min;
@@ -465,13 +466,10 @@ uint32_t seg_small() { return getenv("SM_SEG_SMALL") ? (uint32_t)atoi(getenv("SM
 
 // The reference's min-size merge (Stereo3DMST.cpp:293-307) over the rejected edges that have an end
 // smaller than ms after the sweep, in (w, id) order: the serial rule on a union-find of the sweep's
-// roots.  Emits the hooks (child root, parent root) and the joined edge ids for k_seg_apply.  The order
-// is one sort of packed (w, id, index) words; roots map to dense local ids through a direct table
-// (loc, N entries, all ~0 on entry and on return).
+// roots.  Emits the hooks (child root, parent root) and the joined edge ids for k_seg_apply.  The
+// candidates arrive sorted (k_seg_gather); roots map to dense local ids through a direct table (loc,
+// N entries, all ~0 on entry and on return).
 int seg_minsize_host(const SegMin* e, uint32_t n, uint32_t ms, uint32_t* out, std::vector<uint32_t>& loc) {
-    std::vector<uint64_t> key(n);
-    for (uint32_t i = 0; i < n; ++i) key[i] = ((uint64_t)e[i].w << 50) | ((uint64_t)e[i].id << 25) | i;
-    std::sort(key.begin(), key.end());
     std::vector<uint32_t> par, size, root;
     par.reserve(2 * (size_t)n);
     size.reserve(2 * (size_t)n);
@@ -493,7 +491,7 @@ int seg_minsize_host(const SegMin* e, uint32_t n, uint32_t ms, uint32_t* out, st
     std::vector<uint32_t> ids;
     int k = 0;
     for (uint32_t j = 0; j < n; ++j) {
-        const SegMin& m = e[key[j] & 0x1FFFFFFu];
+        const SegMin& m = e[j];
         uint32_t a = find(local(m.ra, m.sa)), b = find(local(m.rb, m.sb));
         if (a == b || (size[a] >= ms && size[b] >= ms)) continue;
         if (size[a] < size[b]) std::swap(a, b);
@@ -557,6 +555,11 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         CHECK(ensure(ctx, g.hooked, N * 4));
         CHECK(ensure(ctx, g.cnt, SM_SEG_NCOUNT * 4));
         CHECK(ensure(ctx, g.mlist, E * sizeof(SegMin)));
+        CHECK(ensure(ctx, g.msorted, E * sizeof(SegMin)));
+        CHECK(ensure(ctx, g.mkey, E * 16));
+        CHECK(ensure(ctx, g.mval, E * 8));
+        g.stemp_bytes = seg_sort_temp_bytes((uint32_t)E);  // enough for any candidate count (<= E)
+        CHECK(ensure(ctx, g.stemp, g.stemp_bytes));
         if (!g.h_b.resize(SM_SEG_NB + 1) || !g.h_cnt.resize(8)) return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
         if (fresh || g.gen > 0xF0000000u) {  // keys of generation >= 1 beat the initial all-ones
             HIPC(hipMemsetAsync(g.best.p, 0xFF, N * 8, st));
@@ -582,6 +585,11 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         s.hooked = P<uint32_t>(g.hooked);
         s.cnt = P<uint32_t>(g.cnt);
         s.mlist = P<SegMin>(g.mlist);
+        s.msorted = P<SegMin>(g.msorted);
+        s.mkey[0] = P<unsigned long long>(g.mkey);
+        s.mkey[1] = P<unsigned long long>(g.mkey) + E;
+        s.mval[0] = P<uint32_t>(g.mval);
+        s.mval[1] = P<uint32_t>(g.mval) + E;
         s.mR = P<uint8_t>(ctx->mR[v]);
         s.mD = P<uint8_t>(ctx->mD[v]);
         s.fwR = P<uint16_t>(ctx->fwR[v]);
@@ -618,8 +626,8 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
             }
             if (L + R + 2 >= SM_SEG_MAXL) return fail(ctx, SM_ERR_STATE, "segment mode: list counters exhausted");
             int lin = L++;
-            HIPC(seg_launch_classify(st, s, w, b0, m, c, lin));
-            for (int r = 0; r < R; ++r) {
+            HIPC(seg_launch_classify(st, s, w, b0, m, c, lin, g.gen++));  // + the first round's hooks
+            for (int r = 1; r < R; ++r) {
                 HIPC(seg_launch_round(st, s, m, lin, lin + 1, g.gen++, 0, 0));
                 lin = L++;
             }
@@ -640,7 +648,8 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         const uint32_t nm = g.h_cnt[SM_SEG_C_MIN];
         if (!g.h_min.resize(nm) || !g.h_hooks.resize(3 * (size_t)nm + 1))
             return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
-        if (nm) HIPC(hipMemcpyAsync(g.h_min.data(), g.mlist.p, nm * sizeof(SegMin), hipMemcpyDeviceToHost, sst[v]));
+        HIPC(seg_launch_sort(sst[v], sv[v], nm, g.stemp.p, g.stemp_bytes));
+        if (nm) HIPC(hipMemcpyAsync(g.h_min.data(), g.msorted.p, nm * sizeof(SegMin), hipMemcpyDeviceToHost, sst[v]));
     }
     CHECK(sync_all());
     if (dbg) t4 = now_ms();
@@ -2022,7 +2031,7 @@ void sm_destroy(sm_ctx* ctx) {
         for (DevBuf* b : per) if (b->p) (void)hipFree(b->p);
         SegGpu& g = ctx->sg[v];
         DevBuf* sg[] = {&g.par, &g.sz, &g.wl, &g.best, &g.first, &g.ebuf, &g.bcnt, &g.list0, &g.list1, &g.rej, &g.hooked,
-                        &g.cnt, &g.mlist, &g.hooks};
+                        &g.cnt, &g.mlist, &g.hooks, &g.mkey, &g.mval, &g.msorted, &g.stemp};
         for (DevBuf* b : sg) if (b->p) (void)hipFree(b->p);
     }
     for (auto e : ctx->ev_seg) if (e) (void)hipEventDestroy(e);

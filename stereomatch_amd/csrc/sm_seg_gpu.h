@@ -59,6 +59,9 @@ struct SegView {
     uint32_t* hooked;           // roots hooked by the sweep, bucket after bucket
     uint32_t* cnt;              // SM_SEG_NCOUNT counters
     SegMin* mlist;              // min-size candidates
+    unsigned long long* mkey[2];  // their (w, id) keys, unsorted / sorted
+    uint32_t* mval[2];            // their indices, unsorted / sorted
+    SegMin* msorted;              // min-size candidates in (w, id) order
     uint8_t* mR;
     uint8_t* mD;
     uint16_t* fwR;
@@ -67,12 +70,15 @@ struct SegView {
 
 hipError_t seg_launch_init(hipStream_t st, const SegView& v);
 hipError_t seg_launch_scatter(hipStream_t st, const SegView& v);
-hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout);
+hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout,
+                               uint32_t gen);
 hipError_t seg_launch_round(hipStream_t st, const SegView& v, uint32_t m, int lin, int lout, uint32_t gen, int bin,
                             int bout);
 hipError_t seg_launch_tail(hipStream_t st, const SegView& v, int lin, int bin, uint32_t gen0);
 hipError_t seg_launch_small(hipStream_t st, const SegView& v, int w0, int w1, float c, uint32_t gen0);
 hipError_t seg_launch_sizes(hipStream_t st, const SegView& v, int w, uint32_t m);
 hipError_t seg_launch_minsize(hipStream_t st, const SegView& v, int min_size, uint32_t nrej_max);
+size_t seg_sort_temp_bytes(uint32_t n);
+hipError_t seg_launch_sort(hipStream_t st, const SegView& v, uint32_t n, void* temp, size_t temp_bytes);
 hipError_t seg_launch_apply(hipStream_t st, const SegView& v, const uint32_t* hooks, int nhooks);
 hipError_t seg_launch_trees(hipStream_t st, const SegView& v);

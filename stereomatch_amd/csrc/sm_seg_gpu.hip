@@ -6,17 +6,20 @@
 //   k_seg_scan      bucket starts (one block)
 //   k_seg_scatter   edge ids into their weight bucket (order inside a bucket is free: Boruvka keys by id)
 //   per non-empty bucket w, in ascending order:
-//     k_seg_classify  roots of both ends; open-open edges between two components -> candidate list,
-//                     other edges between two components -> rejected
+//     k_seg_classify  roots of both ends; open-open edges between two components -> candidate list
+//                     (and the first Boruvka selection), other edges between two components -> rejected
 //     k_seg_best / k_seg_hook   global Boruvka rounds (big buckets): each root's minimum-id crossing
 //                     edge, then hooks along those edges (mutual pairs: the larger root onto the smaller)
 //     k_seg_tail      the remaining rounds in one workgroup, until no candidate crosses two components
 //     k_seg_sizes     sizes of the joined components, last-join weight w
 //     (k_seg_small: all of it in one workgroup, for a run of buckets of at most SM_SEG_SMALL edges)
-//   k_seg_minsize   rejected edges with an end smaller than min_size -> the host's serial merge
+//   k_seg_minsize   rejected edges with an end smaller than min_size, radix-sorted into (w, id) order
+//                   (hipcub) and gathered (k_seg_gather) -> the host's serial merge
 //   k_seg_apply     the host's merges (root hooks, marked edges)
 //   k_seg_first / k_seg_virtual   first pixel of each tree, virtual edges to link the forest (sm_segment.cpp)
 #include <hip/hip_runtime.h>
+
+#include <hipcub/device/device_radix_sort.hpp>
 
 #include "sm_seg_gpu.h"
 #include "sm_segment.h"
@@ -127,10 +130,16 @@ __global__ void __launch_bounds__(256) k_seg_scatter(SegView v) {
     }
 }
 
+__device__ __forceinline__ unsigned long long seg_key(uint32_t gen, uint32_t id) {
+    return ((unsigned long long)(0xFFFFFFFFu - gen) << 32) | id;
+}
+
+// a bucket's edges: candidates (open-open, two components) -> list lout with their roots, and the
+// first Boruvka selection (generation gen) over them; the other two-component edges -> rejected
 __global__ void __launch_bounds__(256) k_seg_classify(SegView v, int w, uint32_t s, uint32_t m, float c, int lout,
-                                                      int bucket) {
+                                                      uint32_t gen) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i == 0) v.cnt[SM_SEG_C_BUCKET + bucket] = v.cnt[SM_SEG_C_HOOK];  // first hooked root of this bucket
+    if (i == 0) v.cnt[SM_SEG_C_BUCKET + w] = v.cnt[SM_SEG_C_HOOK];  // first hooked root of this bucket
     bool cand = false, rej = false;
     uint32_t id = 0, ra = 0, rb = 0;
     if (i < m) {
@@ -141,16 +150,17 @@ __global__ void __launch_bounds__(256) k_seg_classify(SegView v, int w, uint32_t
             const double wd = (double)w;
             cand = seg_open(v, ra, wd, c) && seg_open(v, rb, wd, c);
             rej = !cand;
+            if (cand) {
+                const unsigned long long key = seg_key(gen, id);
+                atomicMin(v.best + ra, key);
+                atomicMin(v.best + rb, key);
+            }
         }
     }
     const uint32_t pc = wave_append(v.cnt + SM_SEG_C_LIST + lout, cand);
     if (cand) v.list[lout & 1][pc] = make_uint4(id, ra, rb, 0u);
     const uint32_t pr = wave_append(v.cnt + SM_SEG_C_REJ, rej);
     if (rej) v.rej[pr] = id;
-}
-
-__device__ __forceinline__ unsigned long long seg_key(uint32_t gen, uint32_t id) {
-    return ((unsigned long long)(0xFFFFFFFFu - gen) << 32) | id;
 }
 
 // one Boruvka selection over list lin: crossing edges -> list lout with their current roots, and each
@@ -227,8 +237,18 @@ __device__ __forceinline__ void seg_wg_sync() {
 // the rest of a bucket's Boruvka rounds in one workgroup: n candidates in buffer b ping-pong with the
 // other buffer; gens gen0, gen0 + 1, ... (at most SM_SEG_TAIL_GENS).  Returns the rounds run, or -1 if
 // they did not converge.
-__device__ int seg_wg_rounds(const SegView& v, int b, uint32_t n, uint32_t gen0, uint32_t* s_out) {
+__device__ int seg_wg_rounds(const SegView& v, int b, uint32_t n, uint32_t gen0, uint32_t* s_out, bool pre) {
     uint32_t g = 0;
+    if (pre && n > 0) {  // generation gen0's keys were selected while classifying: hook straight away
+        for (uint32_t i0 = 0; i0 < n; i0 += 1024) {
+            const uint32_t i = i0 + threadIdx.x;
+            uint4 e = make_uint4(0, 0, 0, 0);
+            if (i < n) e = v.list[b][i];
+            seg_hook_edge(v, e, gen0, i < n);
+        }
+        seg_wg_sync();
+        g = 1;
+    }
     for (; n > 0; ++g) {
         if (g == SM_SEG_TAIL_GENS) {  // cannot happen (Boruvka halves the components each round)
             if (threadIdx.x == 0) atomicOr(v.cnt + SM_SEG_C_ERR, 1u);
@@ -274,7 +294,7 @@ __device__ int seg_wg_rounds(const SegView& v, int b, uint32_t n, uint32_t gen0,
 
 __global__ void __launch_bounds__(1024) k_seg_tail(SegView v, int lin, uint32_t gen0) {
     __shared__ uint32_t s_out;
-    seg_wg_rounds(v, lin & 1, v.cnt[SM_SEG_C_LIST + lin], gen0, &s_out);
+    seg_wg_rounds(v, lin & 1, v.cnt[SM_SEG_C_LIST + lin], gen0, &s_out, false);
 }
 
 __device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, int w) {
@@ -310,6 +330,11 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegView v, int w0, int w1, f
                 if (ra != rb) {
                     cand = seg_open(v, ra, wd, c) && seg_open(v, rb, wd, c);
                     rej = !cand;
+                    if (cand) {
+                        const unsigned long long key = seg_key(gen, id);
+                        atomicMin(v.best + ra, key);
+                        atomicMin(v.best + rb, key);
+                    }
                 }
             }
             const uint32_t pc = wave_append(&s_n, cand);
@@ -318,7 +343,7 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegView v, int w0, int w1, f
             if (rej) v.rej[pr] = id;
         }
         seg_wg_sync();
-        const int r = seg_wg_rounds(v, 0, s_n, gen, &s_out);
+        const int r = seg_wg_rounds(v, 0, s_n, gen, &s_out, true);
         if (r < 0) return;
         gen += (uint32_t)r;
         const uint32_t h1 = __hip_atomic_load(v.cnt + SM_SEG_C_HOOK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -351,7 +376,17 @@ __global__ void __launch_bounds__(256) k_seg_minsize(SegView v, uint32_t ms) {
         keep = r.sa < ms || r.sb < ms;
     }
     const uint32_t p = wave_append(v.cnt + SM_SEG_C_MIN, keep);
-    if (keep) v.mlist[p] = r;
+    if (keep) {
+        v.mlist[p] = r;
+        v.mkey[0][p] = ((unsigned long long)r.w << 25) | r.id;  // the merge's (w, a, b) order
+        v.mval[0][p] = p;
+    }
+}
+
+// the min-size candidates in (w, id) order, for the host
+__global__ void __launch_bounds__(256) k_seg_gather(SegView v, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) v.msorted[i] = v.mlist[v.mval[1][i]];
 }
 
 // hooks[2k] = child root, hooks[2k + 1] = parent root (0xFFFFFFFF: none) ; marked edge ids after the
@@ -413,8 +448,10 @@ hipError_t seg_launch_scatter(hipStream_t st, const SegView& v) {
     return hipGetLastError();
 }
 
-hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout) {
-    hipLaunchKernelGGL(k_seg_classify, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, w, s, m, c, lout, w);
+hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout,
+                               uint32_t gen) {
+    hipLaunchKernelGGL(k_seg_classify, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, w, s, m, c, lout, gen);
+    hipLaunchKernelGGL(k_seg_hook, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, lout, gen);
     return hipGetLastError();
 }
 
@@ -442,6 +479,22 @@ hipError_t seg_launch_sizes(hipStream_t st, const SegView& v, int w, uint32_t m)
 hipError_t seg_launch_minsize(hipStream_t st, const SegView& v, int min_size, uint32_t nrej_max) {
     const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
     if (nrej_max) hipLaunchKernelGGL(k_seg_minsize, dim3(blocks_of(nrej_max, 256)), dim3(256), 0, st, v, ms);
+    return hipGetLastError();
+}
+
+size_t seg_sort_temp_bytes(uint32_t n) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 35);
+    return bytes;
+}
+
+hipError_t seg_launch_sort(hipStream_t st, const SegView& v, uint32_t n, void* temp, size_t temp_bytes) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1], (int)n, 0,
+                                                      35, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seg_gather, dim3(blocks_of(n, 256)), dim3(256), 0, st, v, n);
     return hipGetLastError();
 }
 
