@@ -174,25 +174,38 @@ def spawn_ranks(n):
     return rc
 
 
-def rank_plan(args, world, rank):
+def default_frame_groups(mode, n):
+    """Strong mode at N >= 8 ranks: 2 frame groups, else 1."""
+    return 2 if (mode == "strong" and n >= 8 and n % 4 == 0) else 1
+
+
+def rank_plan(args, world, rank, fg_arg=None):
     """This rank's share of a frame: image size, its disparity range and views, and its reduce group
     (stereomatch_amd.partition)."""
     W, H = args.width, args.height
     views, group, gsize, grank = 3, 0, world, rank  # this rank's views and its reduce group
     emu = None
-    if args.emulate_rank:
+    if args.emulate_rank:  # rank er of en (with en's frame groups: rank er % (en / G) of a group's frames)
         er, en = (int(x) for x in args.emulate_rank.split("/"))
-        emu = sm.partition(args.disp, en, er, split_views=args.shard == "vd")
-        emu.update(rank=er, nranks=en)
+        eg = fg_arg if fg_arg is not None else default_frame_groups("strong", en)
+        emu = sm.partition(args.disp, en // eg, er % (en // eg), split_views=args.shard == "vd")
+        emu.update(rank=er, nranks=en, frame_groups=eg)
     if world == 1 or args.mode == "weak":
         Dloc = args.disp
         Dtot = Dloc * world if args.mode == "weak" else Dloc
         dbeg = rank * Dloc
     elif args.mode == "strong":
+        # frame group fg of G (ranks [fg*Nf, (fg+1)*Nf)) shares frames fg, fg+G, ...; inside it the
+        # rank's view / disparity share of those frames; reduce groups are contiguous blocks of gsize
+        # ranks, so the global group id is rank // gsize
         Dtot = args.disp
-        part = sm.partition(Dtot, world, rank, split_views=args.shard == "vd")
+        G = args.frame_groups
+        nf = world // G
+        fg, lr = divmod(rank, nf)
+        part = sm.partition(Dtot, nf, lr, split_views=args.shard == "vd")
         dbeg, Dloc, views = part["d0"], part["D"], part["views"]
-        group, gsize, grank = part["group"], part["group_size"], part["group_rank"]
+        gsize, grank = part["group_size"], part["group_rank"]
+        group = fg * (nf // gsize) + part["group"]
     else:  # batch
         Dloc = Dtot = args.disp
         dbeg = 0
@@ -200,8 +213,9 @@ def rank_plan(args, world, rank):
     if emu:  # one rank's share of an N-rank frame: its views and slices of the total range
         Dtot = Dtot_frame = args.disp
         dbeg, Dloc, views = emu["d0"], emu["D"], emu["views"]
+    fgroups = args.frame_groups if (args.mode == "strong" and world > 1) else 1
     return dict(W=W, H=H, Dloc=Dloc, Dtot=Dtot, Dtot_frame=Dtot_frame, dbeg=dbeg, views=views, group=group, gsize=gsize,
-                grank=grank, emu=emu)
+                grank=grank, emu=emu, fgroups=fgroups, fgroup=rank // (world // fgroups))
 
 
 def setup_comms(ctxs, world, rank, group, gsize, grank, mode, context_cls):
@@ -255,6 +269,10 @@ def main():
     ap.add_argument("--shard", default="vd", choices=["vd", "d"],
                     help="strong mode partition: vd = view groups x disparity shards (even N: half the ranks per "
                          "view, D split inside each group), d = disparity shards of both views")
+    ap.add_argument("--frame-groups", type=int, default=None,
+                    help="strong mode: split the N ranks into G frame groups of N/G ranks; frames alternate "
+                         "between the groups and each group view- and D-shards its frames with its own RCCL "
+                         "min+argmin (default: 2 at N >= 8, else 1; 1 = every rank on every frame)")
     ap.add_argument("--emulate-rank", default=None, metavar="R/N",
                     help="one GPU runs rank R's share of an N-rank strong-mode frame (no collective): the per-rank "
                          "cost of the partition, for the multi-GPU estimate in DESIGN.md 7")
@@ -289,10 +307,16 @@ def main():
         sys.exit(2)
     if args.disp is None:
         args.disp = 256 if (big or (args.mode == "strong" and world > 1) or args.emulate_rank) else 128
+    fg_arg = args.frame_groups
+    if args.frame_groups is None:
+        args.frame_groups = default_frame_groups(args.mode, world)
+    if args.mode == "strong" and (args.frame_groups < 1 or world % args.frame_groups):
+        print("bench.py: --frame-groups must divide the rank count", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    plan = rank_plan(args, world, rank)
+    plan = rank_plan(args, world, rank, fg_arg)
     W, H = plan["W"], plan["H"]
     Dloc, Dtot, Dtot_frame, dbeg, views = plan["Dloc"], plan["Dtot"], plan["Dtot_frame"], plan["dbeg"], plan["views"]
     group, gsize, grank, emu = plan["group"], plan["gsize"], plan["grank"], plan["emu"]
@@ -359,7 +383,9 @@ def main():
 
     t0 = time.perf_counter()
     seg_mode = math.isfinite(args.segment_c)
-    stream_frames(ctxs, args.steps, Dloc, params, retire, split=not args.no_split, lag=len(ctxs) - 1 if seg_mode else 1)
+    # frame groups: the timed region is args.steps frames of the stream; group fg takes frames fg, fg+G, ...
+    my_steps = len(range(plan["fgroup"], args.steps, plan["fgroups"]))
+    stream_frames(ctxs, my_steps, Dloc, params, retire, split=not args.no_split, lag=len(ctxs) - 1 if seg_mode else 1)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -439,7 +465,7 @@ def main():
             # PMC HBM bytes of the family per frame over the launches timed here (an empty bucket
             # launches nothing, so both count the same launches)
             if fam.get("hbm_bytes_per_frame") and d["launches"]:
-                traffic = fam["hbm_bytes_per_frame"] / (d["launches"] / args.steps)
+                traffic = fam["hbm_bytes_per_frame"] / (d["launches"] / my_steps)
         except Exception:
             traffic = None
     line = {
@@ -459,10 +485,13 @@ def main():
                        W, H, Dtot_frame, CONFIG_NAMES.get((W, H, Dtot_frame), ""),
                        " = BASELINE C5's per-GPU pair" if args.mode == "batch" and (W, H, Dtot_frame) == (3840, 2160, 256) else "")
                    if world == 1 else
-                   "%dx%d D=%d, %s mode, %s%s" % (
+                   "%dx%d D=%d, %s mode, %s%s%s" % (
                        W, H, Dtot_frame, args.mode,
+                       ("%d frame groups of %d ranks (frame i on group i mod %d), each frame: " % (
+                           plan["fgroups"], world // plan["fgroups"], plan["fgroups"])) if plan["fgroups"] > 1 else "",
                        ("2 view groups x %d disparity shards of %d slices: each rank one view, %d slices" % (gsize, Dloc, Dloc))
-                       if views != 3 else ("%d disparity shards of %d slices, both views per rank" % (world, Dloc))
+                       if views != 3 else ("%d disparity shards of %d slices, both views per rank" % (
+                           world // plan["fgroups"], Dloc))
                        if args.mode == "strong" else "%d disparities/rank, both views" % Dloc,
                        " (BASELINE C4 frame size; C4 names 32 disparities/GPU: here %s)" % (
                            "view groups" if views != 3 else "%d/GPU" % Dloc)
@@ -471,14 +500,16 @@ def main():
                        else ""),
                    "W": W, "H": H, "D": Dtot_frame, "disparities_per_rank": Dloc,
                    "parallelism": "replicas" if args.mode == "batch" else
-                   ("view2 x d-shard%d" % gsize if views != 3 else "d-shard%d" % world),
+                   ("%d frame groups x (%s)" % (plan["fgroups"], "view2 x d-shard%d" % gsize if views != 3 else
+                                                "d-shard%d" % (world // plan["fgroups"])) if plan["fgroups"] > 1 else
+                    "view2 x d-shard%d" % gsize if views != 3 else "d-shard%d" % world),
                    "tree": "MST" if args.segment_c == float("inf") else "segment forest c=%g min_size=%d" % (
                        args.segment_c, args.min_size),
                    "aggregator": args.aggregator,
                    "frames_in_flight": inflight},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "launches_per_step": d["launches"] / args.steps,
+                     "launches_per_step": d["launches"] / my_steps,
                      "alg_bytes_per_launch": dom_bytes / max(d["launches"], 1),
                      "avg_launch_ms": d["ms"] / max(d["launches"], 1),
                      "timing": "HIP events on the launch stream around every %s launch of the timed region, "
@@ -496,14 +527,17 @@ def main():
                                      "wall_timing": "up + down pass spans (stage events), one frame at a time, no per-launch "
                                                     "events, best of 3"}},
         "kernels_ms_per_step": {k: v["ms"] / diag_steps for k, v in kall.items()},
-        "stages_ms": {k: v / args.steps for k, v in stage_acc.items()},
+        "stages_ms": {k: v / my_steps for k, v in stage_acc.items()},
         "latency_ms_per_frame": min(lat),
         "frames_in_flight": inflight,
         "host_io": host_io,
     }
     if emu:
         line["emulated_rank"] = dict(emu, note="one rank's share of an N-rank strong-mode frame on one GPU, no "
-                                               "collective; value counts the rank's own voxels")
+                                               "collective; value counts the rank's own voxels; with G frame groups "
+                                               "the rank takes every G-th frame of the stream, so the stream's "
+                                               "ms/frame is ms_per_step / G",
+                                     stream_ms_per_frame=ms_step / emu["frame_groups"])
         line["value"] = W * H * Dloc * bin(views).count("1") * args.steps / elapsed
         line["config"]["workload"] = "rank %d/%d of %dx%d D=%d: views %d, slices [%d, %d)" % (
             emu["rank"], emu["nranks"], W, H, Dtot_frame, views, dbeg, dbeg + Dloc)

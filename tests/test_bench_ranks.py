@@ -76,3 +76,20 @@ def test_weak_and_batch_plans():
     batch = run_plan(2, "--mode", "batch")
     assert all(x["comms"] == [None, None] for x in batch)  # replicas: no collective
     assert all((x["plan"]["W"], x["plan"]["H"], x["plan"]["Dloc"]) == (3840, 2160, 256) for x in batch)
+
+
+def test_frame_group_plan():
+    """N = 8 strong mode defaults to 2 frame groups of 4 ranks: each group is a left and a right view
+    group of 2 ranks x 128 slices with its own communicators (4 reduce groups in all), and
+    --frame-groups 1 keeps every rank on every frame (2 view groups of 4 x 64 slices)."""
+    lines = run_plan(8)
+    groups = check_groups(lines, 256)
+    assert len(groups) == 4
+    assert all(x["plan"]["fgroups"] == 2 and x["plan"]["fgroup"] == x["rank"] // 4 for x in lines)
+    assert all(x["plan"]["gsize"] == 2 and x["plan"]["Dloc"] == 128 for x in lines)
+    assert len({m["comms"][0]["uid"] for m in lines}) == 4
+    for fg in (0, 1):
+        assert sorted(x["plan"]["views"] for x in lines if x["plan"]["fgroup"] == fg) == [1, 1, 2, 2]
+    one = run_plan(8, "--frame-groups", "1")
+    groups = check_groups(one, 256)
+    assert len(groups) == 2 and all(x["plan"]["Dloc"] == 64 and x["plan"]["fgroups"] == 1 for x in one)

@@ -329,15 +329,16 @@ def test_one_view_calls_bitexact(gpu_ctx, monkeypatch, W, H, D, plen, c):
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
 
 
-@pytest.mark.parametrize("rank", [0, 6])
-def test_full_size_c4_view_group_shard_with_reduce(rank):
+@pytest.mark.parametrize("n,rank", [(8, 0), (8, 6), (4, 1), (4, 2)])
+def test_full_size_c4_view_group_shard_with_reduce(n, rank):
     """BASELINE C4 frame under the view-group partition (stereomatch_amd.partition, bench.py
-    --shard vd): rank r of 8 filters 64 slices of ONE view at full size and reduces through a
-    one-rank RCCL communicator (stage_reduce over its view only); bitwise equal to the oracle's
-    tree filter over that view's shard."""
+    --shard vd): rank r of n filters 256 / (n/2) slices of ONE view at full size and reduces
+    through a one-rank RCCL communicator (stage_reduce over its view only); bitwise equal to the
+    oracle's tree filter over that view's shard.  n = 4 is also the share of a rank at N = 8 with 2
+    frame groups (bench.py --frame-groups, the N = 8 default)."""
     import stereomatch_amd as sm
     W, H, Dt = 1920, 1200, 256
-    part = sm.partition(Dt, 8, rank)
+    part = sm.partition(Dt, n, rank)
     d0, D, views = part["d0"], part["D"], part["views"]
     v = "left" if views == 1 else "right"
     left, right, _ = make_pair(W, H, Dt, index=13)
