@@ -138,8 +138,6 @@ struct sm_ctx {
     int seg_trees[2] = {0, 0};
     PinnedVec<uint16_t> h_w[2][2], h_fw[2][2];
     PinnedVec<uint8_t> h_m[2][2];
-    hipStream_t st_seg = nullptr;  // the second view's GPU segmentation (created on first use)
-    hipEvent_t ev_seg[2] = {nullptr, nullptr};
     SegGpu sg[2];  // GPU segmentation (default; SM_SEG_HOST=1: the host sweep of sm_segment.cpp)
     // asynchronous segment mode (sm_match_begin): the host segmentation runs on a worker thread that
     // waits for the weights' copy (ev_segw), uploads the forest and enqueues the layout; sm_match_finish
@@ -510,9 +508,10 @@ int seg_minsize_host(const SegMin* e, uint32_t n, uint32_t ms, uint32_t* out, st
 double now_ms();
 
 // Segment mode's segmentation on the GPU (sm_seg_gpu.h): the masks and layout weights of the forest
-// land in mR / mD / fwR / fwD as segment_upload leaves them.  Host synchronisations: the bucket sizes
-// (once), the min-size candidates (twice).  With host_copy the weights, masks and layout weights are
-// copied to the h_w / h_m / h_fw host arrays as well (MST_PMS, sm_build_tree_p).
+// land in mR / mD / fwR / fwD as segment_upload leaves them.  Both views go through every launch, on
+// the context's stream, bucket by bucket in lockstep.  Host synchronisations: the bucket sizes (once),
+// the min-size candidates (twice).  With host_copy the weights, masks and layout weights are copied to
+// the h_w / h_m / h_fw host arrays as well (MST_PMS, sm_build_tree_p).
 sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_copy) {
     static const bool dbg = getenv("SM_SEG_DEBUG") != nullptr;
     const double t0 = dbg ? now_ms() : 0.0;
@@ -520,28 +519,24 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H, E = 2 * N;
     const ViewSet vs(views);
-    SegView sv[2]{};
-    // the second view on its own stream (its launches are latency-bound: the views' chains overlap)
-    hipStream_t sst[2] = {ctx->st, ctx->st};
-    if (vs.n > 1) {
-        if (!ctx->st_seg) {
-            HIPC(hipStreamCreateWithFlags(&ctx->st_seg, hipStreamNonBlocking));
-            HIPC(hipEventCreateWithFlags(&ctx->ev_seg[0], hipEventDisableTiming));
-            HIPC(hipEventCreateWithFlags(&ctx->ev_seg[1], hipEventDisableTiming));
-        }
-        HIPC(hipEventRecord(ctx->ev_seg[0], ctx->st));
-        HIPC(hipStreamWaitEvent(ctx->st_seg, ctx->ev_seg[0], 0));
-        sst[vs.v[1]] = ctx->st_seg;
+    hipStream_t st = ctx->st;
+    SegPair sp{};
+    sp.nv = vs.n;
+    bool reset = false;
+    uint32_t gen = 1;
+    for (int i = 0; i < vs.n; ++i) {
+        const SegGpu& g = ctx->sg[vs.v[i]];
+        reset |= g.best.n < N * 8 || g.gen > 0xF0000000u;
+        gen = std::max(gen, g.gen);
     }
+    if (reset) gen = 1;  // keys of generation >= 1 beat the initial all-ones
     for (int i = 0; i < vs.n; ++i) {
         const int v = vs.v[i];
         SegGpu& g = ctx->sg[v];
-        hipStream_t st = sst[v];
         CHECK(ensure(ctx, ctx->mR[v], N));
         CHECK(ensure(ctx, ctx->mD[v], N));
         CHECK(ensure(ctx, ctx->fwR[v], N * 2));
         CHECK(ensure(ctx, ctx->fwD[v], N * 2));
-        const bool fresh = g.best.n < N * 8;
         CHECK(ensure(ctx, g.par, N * 4));
         CHECK(ensure(ctx, g.sz, N * 4));
         CHECK(ensure(ctx, g.wl, N * 2));
@@ -561,13 +556,10 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         g.stemp_bytes = seg_sort_temp_bytes((uint32_t)E);  // enough for any candidate count (<= E)
         CHECK(ensure(ctx, g.stemp, g.stemp_bytes));
         if (!g.h_b.resize(SM_SEG_NB + 1) || !g.h_cnt.resize(8)) return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
-        if (fresh || g.gen > 0xF0000000u) {  // keys of generation >= 1 beat the initial all-ones
-            HIPC(hipMemsetAsync(g.best.p, 0xFF, N * 8, st));
-            g.gen = 1;
-        }
+        if (reset) HIPC(hipMemsetAsync(g.best.p, 0xFF, N * 8, st));
         HIPC(hipMemsetAsync(g.bcnt.p, 0, (3 * SM_SEG_NB + 1) * 4, st));
         HIPC(hipMemsetAsync(g.cnt.p, 0, SM_SEG_NCOUNT * 4, st));
-        SegView& s = sv[v];
+        SegView& s = sp.v[i];
         s.W = W;
         s.H = H;
         s.wR = P<uint16_t>(ctx->wR[v]);
@@ -594,64 +586,79 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         s.mD = P<uint8_t>(ctx->mD[v]);
         s.fwR = P<uint16_t>(ctx->fwR[v]);
         s.fwD = P<uint16_t>(ctx->fwD[v]);
-        HIPC(seg_launch_init(st, s));
-        HIPC(hipMemcpyAsync(g.h_b.data(), P<uint32_t>(g.bcnt) + SM_SEG_NB, (SM_SEG_NB + 1) * 4, hipMemcpyDeviceToHost, st));
-        HIPC(seg_launch_scatter(st, s));
     }
-    auto sync_all = [&]() -> sm_status {
-        HIPC(hipStreamSynchronize(ctx->st));
-        if (vs.n > 1) HIPC(hipStreamSynchronize(ctx->st_seg));
-        return SM_OK;
-    };
-    CHECK(sync_all());
-    if (dbg) t1 = now_ms();
-    const int R = seg_global_rounds();
+    HIPC(seg_launch_init(st, sp));
     for (int i = 0; i < vs.n; ++i) {
-        const int v = vs.v[i];
-        SegGpu& g = ctx->sg[v];
-        const SegView& s = sv[v];
-        hipStream_t st = sst[v];
-        int L = 0;
-        const uint32_t small = seg_small();
-        for (int w = 0; w < SM_SEG_NB; ++w) {
-            const uint32_t b0 = g.h_b[w], m = g.h_b[w + 1] - b0;
-            if (!m) continue;
-            if (m <= small) {  // a run of small buckets in one workgroup: classify, rounds, sizes
-                int w1 = w + 1, nb = 1;
-                for (; w1 < SM_SEG_NB && g.h_b[w1 + 1] - g.h_b[w1] <= small; ++w1) nb += g.h_b[w1 + 1] > g.h_b[w1];
-                HIPC(seg_launch_small(st, s, w, w1, c, g.gen));
-                g.gen += SM_SEG_TAIL_GENS * (uint32_t)nb;
-                w = w1 - 1;
-                continue;
-            }
-            if (L + R + 2 >= SM_SEG_MAXL) return fail(ctx, SM_ERR_STATE, "segment mode: list counters exhausted");
-            int lin = L++;
-            HIPC(seg_launch_classify(st, s, w, b0, m, c, lin, g.gen++));  // + the first round's hooks
-            for (int r = 1; r < R; ++r) {
-                HIPC(seg_launch_round(st, s, m, lin, lin + 1, g.gen++, 0, 0));
-                lin = L++;
-            }
-            HIPC(seg_launch_tail(st, s, lin, 0, g.gen));
-            g.gen += SM_SEG_TAIL_GENS;
-            HIPC(seg_launch_sizes(st, s, w, m));
+        SegGpu& g = ctx->sg[vs.v[i]];
+        HIPC(hipMemcpyAsync(g.h_b.data(), P<uint32_t>(g.bcnt) + SM_SEG_NB, (SM_SEG_NB + 1) * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPC(seg_launch_scatter(st, sp));
+    HIPC(hipStreamSynchronize(st));
+    if (dbg) t1 = now_ms();
+    // buckets in lockstep: a bucket is small if it is small in every view of the call
+    auto bsize = [&](int w) {
+        uint32_t m = 0;
+        for (int i = 0; i < vs.n; ++i) {
+            const SegGpu& g = ctx->sg[vs.v[i]];
+            m = std::max(m, g.h_b[w + 1] - g.h_b[w]);
         }
-        HIPC(seg_launch_minsize(st, s, min_size, (uint32_t)(g.h_b[SM_SEG_NB])));
+        return m;
+    };
+    const int R = seg_global_rounds();
+    const uint32_t small = seg_small();
+    int L = 0;
+    uint32_t rej_max = 0;
+    for (int i = 0; i < vs.n; ++i) rej_max = std::max(rej_max, ctx->sg[vs.v[i]].h_b[SM_SEG_NB]);
+    for (int w = 0; w < SM_SEG_NB; ++w) {
+        const uint32_t m = bsize(w);
+        if (!m) continue;
+        if (m <= small) {  // a run of small buckets in one workgroup per view: classify, rounds, sizes
+            int w1 = w + 1, nb = 1;
+            for (uint32_t m1; w1 < SM_SEG_NB && (m1 = bsize(w1)) <= small; ++w1) nb += m1 > 0;
+            HIPC(seg_launch_small(st, sp, w, w1, c, gen));
+            gen += SM_SEG_TAIL_GENS * (uint32_t)nb;
+            w = w1 - 1;
+            continue;
+        }
+        if (L + R + 2 >= SM_SEG_MAXL) return fail(ctx, SM_ERR_STATE, "segment mode: list counters exhausted");
+        int lin = L++;
+        HIPC(seg_launch_classify(st, sp, w, m, c, lin, gen++));  // + the first round's hooks
+        for (int r = 1; r < R; ++r) {
+            HIPC(seg_launch_round(st, sp, m, lin, lin + 1, gen++));
+            lin = L++;
+        }
+        HIPC(seg_launch_tail(st, sp, lin, gen));
+        gen += SM_SEG_TAIL_GENS;
+        HIPC(seg_launch_sizes(st, sp, w, m));
+    }
+    for (int i = 0; i < vs.n; ++i) ctx->sg[vs.v[i]].gen = gen;
+    HIPC(seg_launch_minsize(st, sp, min_size, rej_max));
+    for (int i = 0; i < vs.n; ++i) {
+        SegGpu& g = ctx->sg[vs.v[i]];
         HIPC(hipMemcpyAsync(g.h_cnt.data(), P<uint32_t>(g.cnt), 8 * 4, hipMemcpyDeviceToHost, st));
     }
     if (dbg) t2 = now_ms();
-    CHECK(sync_all());
+    HIPC(hipStreamSynchronize(st));
     if (dbg) t3 = now_ms();
+    void* temp[2] = {nullptr, nullptr};
+    size_t tbytes[2] = {0, 0};
     for (int i = 0; i < vs.n; ++i) {
-        const int v = vs.v[i];
-        SegGpu& g = ctx->sg[v];
+        SegGpu& g = ctx->sg[vs.v[i]];
         if (g.h_cnt[SM_SEG_C_ERR]) return fail(ctx, SM_ERR_STATE, "segment mode: a Boruvka tail did not converge");
         const uint32_t nm = g.h_cnt[SM_SEG_C_MIN];
         if (!g.h_min.resize(nm) || !g.h_hooks.resize(3 * (size_t)nm + 1))
             return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
-        HIPC(seg_launch_sort(sst[v], sv[v], nm, g.stemp.p, g.stemp_bytes));
-        if (nm) HIPC(hipMemcpyAsync(g.h_min.data(), g.msorted.p, nm * sizeof(SegMin), hipMemcpyDeviceToHost, sst[v]));
+        sp.v[i].nmin = nm;
+        temp[i] = g.stemp.p;
+        tbytes[i] = g.stemp_bytes;
     }
-    CHECK(sync_all());
+    HIPC(seg_launch_sort(st, sp, temp, tbytes));
+    for (int i = 0; i < vs.n; ++i) {
+        SegGpu& g = ctx->sg[vs.v[i]];
+        if (sp.v[i].nmin)
+            HIPC(hipMemcpyAsync(g.h_min.data(), g.msorted.p, sp.v[i].nmin * sizeof(SegMin), hipMemcpyDeviceToHost, st));
+    }
+    HIPC(hipStreamSynchronize(st));
     if (dbg) t4 = now_ms();
     const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
     int nk[2] = {0, 0};
@@ -662,19 +669,23 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
             return seg_minsize_host(g.h_min.data(), g.h_cnt[SM_SEG_C_MIN], ms, g.h_hooks.data(), g.loc);
         };
         std::thread other;
-        if (vs.n > 1) other = std::thread([&] { nk[vs.v[1]] = merge(vs.v[1]); });
-        nk[vs.v[0]] = merge(vs.v[0]);
+        if (vs.n > 1) other = std::thread([&] { nk[1] = merge(vs.v[1]); });
+        nk[0] = merge(vs.v[0]);
         if (other.joinable()) other.join();
     }
     for (int i = 0; i < vs.n; ++i) {
-        const int v = vs.v[i];
-        SegGpu& g = ctx->sg[v];
-        hipStream_t st = sst[v];
-        const int k = nk[v];
+        SegGpu& g = ctx->sg[vs.v[i]];
+        const int k = nk[i];
         CHECK(ensure(ctx, g.hooks, (3 * (size_t)k + 1) * 4));
         if (k) HIPC(hipMemcpyAsync(g.hooks.p, g.h_hooks.data(), 3 * (size_t)k * 4, hipMemcpyHostToDevice, st));
-        HIPC(seg_launch_apply(st, sv[v], P<uint32_t>(g.hooks), k));
-        HIPC(seg_launch_trees(st, sv[v]));
+        sp.v[i].hooks = P<uint32_t>(g.hooks);
+        sp.v[i].nhooks = k;
+    }
+    HIPC(seg_launch_apply(st, sp));
+    HIPC(seg_launch_trees(st, sp));
+    for (int i = 0; i < vs.n; ++i) {
+        const int v = vs.v[i];
+        SegGpu& g = ctx->sg[v];
         HIPC(hipMemcpyAsync(g.h_cnt.data() + 4, P<uint32_t>(g.cnt) + SM_SEG_C_TREES, 4, hipMemcpyDeviceToHost, st));
         if (host_copy) {
             for (int q = 0; q < 2; ++q)
@@ -688,16 +699,12 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
             HIPC(hipMemcpyAsync(ctx->h_fw[v][1].data(), ctx->fwD[v].p, N * 2, hipMemcpyDeviceToHost, st));
         }
     }
-    if (vs.n > 1) {  // the layout (on st) waits for the second view's forest
-        HIPC(hipEventRecord(ctx->ev_seg[1], ctx->st_seg));
-        HIPC(hipStreamWaitEvent(ctx->st, ctx->ev_seg[1], 0));
-    }
     if (host_copy) {
-        HIPC(hipStreamSynchronize(ctx->st));
+        HIPC(hipStreamSynchronize(st));
         for (int i = 0; i < vs.n; ++i) ctx->seg_trees[vs.v[i]] = (int)ctx->sg[vs.v[i]].h_cnt[4];
     }
     CHECK(ensure(ctx, ctx->mst_ok, sizeof(int)));
-    HIPC(hipMemsetAsync(ctx->mst_ok.p, 1, sizeof(int), ctx->st));
+    HIPC(hipMemsetAsync(ctx->mst_ok.p, 1, sizeof(int), st));
     if (dbg) {
         const double t5 = now_ms();
         fprintf(stderr, "segment_gpu: init+buckets %.2f ms, enqueue %.2f, sweep wait %.2f, min-size copy %.2f, host merge + rest %.2f;",
@@ -2016,7 +2023,6 @@ void sm_destroy(sm_ctx* ctx) {
     if (ctx->seg_worker.joinable()) ctx->seg_worker.join();  // a begun segment-mode call's host worker
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     if (ctx->st_tree) (void)hipStreamSynchronize(ctx->st_tree);  // tree kernels may still run there
-    if (ctx->st_seg) (void)hipStreamSynchronize(ctx->st_seg);
     if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamSynchronize(ctx->st2);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut, &ctx->post_mask, &ctx->post_scratch,
@@ -2034,8 +2040,6 @@ void sm_destroy(sm_ctx* ctx) {
                         &g.cnt, &g.mlist, &g.hooks, &g.mkey, &g.mval, &g.msorted, &g.stemp};
         for (DevBuf* b : sg) if (b->p) (void)hipFree(b->p);
     }
-    for (auto e : ctx->ev_seg) if (e) (void)hipEventDestroy(e);
-    if (ctx->st_seg) (void)hipStreamDestroy(ctx->st_seg);
     for (auto e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->ev_layout) (void)hipEventDestroy(ctx->ev_layout);
     if (ctx->ev_segw) (void)hipEventDestroy(ctx->ev_segw);

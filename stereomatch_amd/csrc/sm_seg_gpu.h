@@ -62,23 +62,30 @@ struct SegView {
     unsigned long long* mkey[2];  // their (w, id) keys, unsorted / sorted
     uint32_t* mval[2];            // their indices, unsorted / sorted
     SegMin* msorted;              // min-size candidates in (w, id) order
+    uint32_t nmin;                // their count (host-set before the sort)
+    const uint32_t* hooks;        // the host merge's hooks and marked edges (k_seg_apply)
+    int nhooks;
     uint8_t* mR;
     uint8_t* mD;
     uint16_t* fwR;
     uint16_t* fwD;
 };
 
-hipError_t seg_launch_init(hipStream_t st, const SegView& v);
-hipError_t seg_launch_scatter(hipStream_t st, const SegView& v);
-hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout,
-                               uint32_t gen);
-hipError_t seg_launch_round(hipStream_t st, const SegView& v, uint32_t m, int lin, int lout, uint32_t gen, int bin,
-                            int bout);
-hipError_t seg_launch_tail(hipStream_t st, const SegView& v, int lin, int bin, uint32_t gen0);
-hipError_t seg_launch_small(hipStream_t st, const SegView& v, int w0, int w1, float c, uint32_t gen0);
-hipError_t seg_launch_sizes(hipStream_t st, const SegView& v, int w, uint32_t m);
-hipError_t seg_launch_minsize(hipStream_t st, const SegView& v, int min_size, uint32_t nrej_max);
+// both views of a call in every launch (blockIdx.y, or blockIdx.x for the one-workgroup kernels)
+struct SegPair {
+    SegView v[2];
+    int nv;
+};
+
+hipError_t seg_launch_init(hipStream_t st, const SegPair& p);
+hipError_t seg_launch_scatter(hipStream_t st, const SegPair& p);
+hipError_t seg_launch_classify(hipStream_t st, const SegPair& p, int w, uint32_t m, float c, int lout, uint32_t gen);
+hipError_t seg_launch_round(hipStream_t st, const SegPair& p, uint32_t m, int lin, int lout, uint32_t gen);
+hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t gen0);
+hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0);
+hipError_t seg_launch_sizes(hipStream_t st, const SegPair& p, int w, uint32_t m);
+hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, uint32_t nrej_max);
 size_t seg_sort_temp_bytes(uint32_t n);
-hipError_t seg_launch_sort(hipStream_t st, const SegView& v, uint32_t n, void* temp, size_t temp_bytes);
-hipError_t seg_launch_apply(hipStream_t st, const SegView& v, const uint32_t* hooks, int nhooks);
-hipError_t seg_launch_trees(hipStream_t st, const SegView& v);
+hipError_t seg_launch_sort(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes);
+hipError_t seg_launch_apply(hipStream_t st, const SegPair& p);
+hipError_t seg_launch_trees(hipStream_t st, const SegPair& p);

@@ -57,7 +57,8 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-__global__ void __launch_bounds__(256) k_seg_init(SegView v) {
+__global__ void __launch_bounds__(256) k_seg_init(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
     __shared__ uint32_t hist[SM_SEG_NB];
     const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
     for (int i = threadIdx.x; i < SM_SEG_NB; i += 256) hist[i] = 0;
@@ -81,7 +82,8 @@ __global__ void __launch_bounds__(256) k_seg_init(SegView v) {
         if (hist[i]) atomicAdd(&v.bcnt[i], hist[i]);
 }
 
-__global__ void __launch_bounds__(1024) k_seg_scan(SegView v) {
+__global__ void __launch_bounds__(1024) k_seg_scan(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.x];
     // exclusive scan of SM_SEG_NB counts -> starts (NB + 1) and cursors
     __shared__ uint32_t s[1024];
     const int t = threadIdx.x;
@@ -103,7 +105,8 @@ __global__ void __launch_bounds__(1024) k_seg_scan(SegView v) {
     if (t == SM_SEG_NB - 1) start[SM_SEG_NB] = s[t];
 }
 
-__global__ void __launch_bounds__(256) k_seg_scatter(SegView v) {
+__global__ void __launch_bounds__(256) k_seg_scatter(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
     __shared__ uint32_t hist[SM_SEG_NB];
     const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
     for (int i = threadIdx.x; i < SM_SEG_NB; i += 256) hist[i] = 0;
@@ -136,8 +139,9 @@ __device__ __forceinline__ unsigned long long seg_key(uint32_t gen, uint32_t id)
 
 // a bucket's edges: candidates (open-open, two components) -> list lout with their roots, and the
 // first Boruvka selection (generation gen) over them; the other two-component edges -> rejected
-__global__ void __launch_bounds__(256) k_seg_classify(SegView v, int w, uint32_t s, uint32_t m, float c, int lout,
-                                                      uint32_t gen) {
+__global__ void __launch_bounds__(256) k_seg_classify(SegPair sp, int w, float c, int lout, uint32_t gen) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t s = v.bcnt[SM_SEG_NB + w], m = v.bcnt[SM_SEG_NB + w + 1] - s;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i == 0) v.cnt[SM_SEG_C_BUCKET + w] = v.cnt[SM_SEG_C_HOOK];  // first hooked root of this bucket
     bool cand = false, rej = false;
@@ -165,7 +169,8 @@ __global__ void __launch_bounds__(256) k_seg_classify(SegView v, int w, uint32_t
 
 // one Boruvka selection over list lin: crossing edges -> list lout with their current roots, and each
 // root's minimum key
-__global__ void __launch_bounds__(256) k_seg_best(SegView v, int lin, int lout, uint32_t gen) {
+__global__ void __launch_bounds__(256) k_seg_best(SegPair sp, int lin, int lout, uint32_t gen) {
+    const SegView& v = sp.v[blockIdx.y];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t n = v.cnt[SM_SEG_C_LIST + lin];
     bool cross = false;
@@ -218,7 +223,8 @@ __device__ __forceinline__ void seg_hook_edge(const SegView& v, uint4 e, uint32_
     }
 }
 
-__global__ void __launch_bounds__(256) k_seg_hook(SegView v, int lout, uint32_t gen) {
+__global__ void __launch_bounds__(256) k_seg_hook(SegPair sp, int lout, uint32_t gen) {
+    const SegView& v = sp.v[blockIdx.y];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t n = v.cnt[SM_SEG_C_LIST + lout];
     uint4 e = make_uint4(0, 0, 0, 0);
@@ -292,7 +298,8 @@ __device__ int seg_wg_rounds(const SegView& v, int b, uint32_t n, uint32_t gen0,
     return (int)g;
 }
 
-__global__ void __launch_bounds__(1024) k_seg_tail(SegView v, int lin, uint32_t gen0) {
+__global__ void __launch_bounds__(1024) k_seg_tail(SegPair sp, int lin, uint32_t gen0) {
+    const SegView& v = sp.v[blockIdx.x];
     __shared__ uint32_t s_out;
     seg_wg_rounds(v, lin & 1, v.cnt[SM_SEG_C_LIST + lin], gen0, &s_out, false);
 }
@@ -306,7 +313,8 @@ __device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, in
 
 // a run of small buckets [w0, w1) (each of at most SM_SEG_SMALL edges) in one workgroup, one bucket
 // after the other: classify, Boruvka rounds, sizes; gens from gen0, at most SM_SEG_TAIL_GENS per bucket
-__global__ void __launch_bounds__(1024) k_seg_small(SegView v, int w0, int w1, float c, uint32_t gen0) {
+__global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, float c, uint32_t gen0) {
+    const SegView& v = sp.v[blockIdx.x];
     __shared__ uint32_t s_n, s_out, s_h0;
     const uint32_t* start = v.bcnt + SM_SEG_NB;
     uint32_t gen = gen0;
@@ -352,14 +360,16 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegView v, int w0, int w1, f
     }
 }
 
-__global__ void __launch_bounds__(256) k_seg_sizes(SegView v, int w, int bucket) {
-    const uint32_t h0 = v.cnt[SM_SEG_C_BUCKET + bucket], h1 = v.cnt[SM_SEG_C_HOOK];
+__global__ void __launch_bounds__(256) k_seg_sizes(SegPair sp, int w) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t h0 = v.cnt[SM_SEG_C_BUCKET + w], h1 = v.cnt[SM_SEG_C_HOOK];
     const uint32_t i = h0 + blockIdx.x * 256 + threadIdx.x;
     if (i >= h1) return;
     seg_size_update(v, i, w);
 }
 
-__global__ void __launch_bounds__(256) k_seg_minsize(SegView v, uint32_t ms) {
+__global__ void __launch_bounds__(256) k_seg_minsize(SegPair sp, uint32_t ms) {
+    const SegView& v = sp.v[blockIdx.y];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t n = v.cnt[SM_SEG_C_REJ];
     bool keep = false;
@@ -384,14 +394,19 @@ __global__ void __launch_bounds__(256) k_seg_minsize(SegView v, uint32_t ms) {
 }
 
 // the min-size candidates in (w, id) order, for the host
-__global__ void __launch_bounds__(256) k_seg_gather(SegView v, uint32_t n) {
+__global__ void __launch_bounds__(256) k_seg_gather(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t n = v.nmin;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) v.msorted[i] = v.mlist[v.mval[1][i]];
 }
 
 // hooks[2k] = child root, hooks[2k + 1] = parent root (0xFFFFFFFF: none) ; marked edge ids after the
 // pairs: hooks[2 * nhooks + k]
-__global__ void __launch_bounds__(256) k_seg_apply(SegView v, const uint32_t* hooks, int nhooks) {
+__global__ void __launch_bounds__(256) k_seg_apply(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t* hooks = v.hooks;
+    const int nhooks = v.nhooks;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= nhooks) return;
     v.par[hooks[2 * i]] = hooks[2 * i + 1];
@@ -402,7 +417,8 @@ __global__ void __launch_bounds__(256) k_seg_apply(SegView v, const uint32_t* ho
         v.mR[id >> 1] = 1;
 }
 
-__global__ void __launch_bounds__(256) k_seg_first(SegView v) {
+__global__ void __launch_bounds__(256) k_seg_first(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
     const uint32_t r = p < N ? seg_find(v.par, p) : 0xFFFFFFFFu;
@@ -415,7 +431,8 @@ __global__ void __launch_bounds__(256) k_seg_first(SegView v) {
     v.fwD[p] = v.wD[p];
 }
 
-__global__ void __launch_bounds__(256) k_seg_virtual(SegView v) {
+__global__ void __launch_bounds__(256) k_seg_virtual(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
     const bool root = p < N && v.first[seg_find(v.par, p)] == p;
@@ -435,50 +452,49 @@ unsigned blocks_of(size_t n, unsigned per) { return (unsigned)((n + per - 1) / p
 
 }  // namespace
 
-hipError_t seg_launch_init(hipStream_t st, const SegView& v) {
-    const size_t N = (size_t)v.W * v.H;
-    hipLaunchKernelGGL(k_seg_init, dim3(blocks_of(N, SM_SEG_TILE)), dim3(256), 0, st, v);
-    hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(1024), 0, st, v);
+hipError_t seg_launch_init(hipStream_t st, const SegPair& p) {
+    const size_t N = (size_t)p.v[0].W * p.v[0].H;
+    hipLaunchKernelGGL(k_seg_init, dim3(blocks_of(N, SM_SEG_TILE), p.nv), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(k_seg_scan, dim3(p.nv), dim3(1024), 0, st, p);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_scatter(hipStream_t st, const SegView& v) {
-    const size_t N = (size_t)v.W * v.H;
-    hipLaunchKernelGGL(k_seg_scatter, dim3(blocks_of(N, SM_SEG_TILE)), dim3(256), 0, st, v);
+hipError_t seg_launch_scatter(hipStream_t st, const SegPair& p) {
+    const size_t N = (size_t)p.v[0].W * p.v[0].H;
+    hipLaunchKernelGGL(k_seg_scatter, dim3(blocks_of(N, SM_SEG_TILE), p.nv), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_classify(hipStream_t st, const SegView& v, int w, uint32_t s, uint32_t m, float c, int lout,
-                               uint32_t gen) {
-    hipLaunchKernelGGL(k_seg_classify, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, w, s, m, c, lout, gen);
-    hipLaunchKernelGGL(k_seg_hook, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, lout, gen);
+hipError_t seg_launch_classify(hipStream_t st, const SegPair& p, int w, uint32_t m, float c, int lout, uint32_t gen) {
+    hipLaunchKernelGGL(k_seg_classify, dim3(blocks_of(m, 256), p.nv), dim3(256), 0, st, p, w, c, lout, gen);
+    hipLaunchKernelGGL(k_seg_hook, dim3(blocks_of(m, 256), p.nv), dim3(256), 0, st, p, lout, gen);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_round(hipStream_t st, const SegView& v, uint32_t m, int lin, int lout, uint32_t gen, int, int) {
-    hipLaunchKernelGGL(k_seg_best, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, lin, lout, gen);
-    hipLaunchKernelGGL(k_seg_hook, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, lout, gen);
+hipError_t seg_launch_round(hipStream_t st, const SegPair& p, uint32_t m, int lin, int lout, uint32_t gen) {
+    hipLaunchKernelGGL(k_seg_best, dim3(blocks_of(m, 256), p.nv), dim3(256), 0, st, p, lin, lout, gen);
+    hipLaunchKernelGGL(k_seg_hook, dim3(blocks_of(m, 256), p.nv), dim3(256), 0, st, p, lout, gen);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_tail(hipStream_t st, const SegView& v, int lin, int, uint32_t gen0) {
-    hipLaunchKernelGGL(k_seg_tail, dim3(1), dim3(1024), 0, st, v, lin, gen0);
+hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t gen0) {
+    hipLaunchKernelGGL(k_seg_tail, dim3(p.nv), dim3(1024), 0, st, p, lin, gen0);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_small(hipStream_t st, const SegView& v, int w0, int w1, float c, uint32_t gen0) {
-    hipLaunchKernelGGL(k_seg_small, dim3(1), dim3(1024), 0, st, v, w0, w1, c, gen0);
+hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0) {
+    hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_sizes(hipStream_t st, const SegView& v, int w, uint32_t m) {
-    hipLaunchKernelGGL(k_seg_sizes, dim3(blocks_of(m, 256)), dim3(256), 0, st, v, w, w);
+hipError_t seg_launch_sizes(hipStream_t st, const SegPair& p, int w, uint32_t m) {
+    hipLaunchKernelGGL(k_seg_sizes, dim3(blocks_of(m, 256), p.nv), dim3(256), 0, st, p, w);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_minsize(hipStream_t st, const SegView& v, int min_size, uint32_t nrej_max) {
+hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, uint32_t nrej_max) {
     const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
-    if (nrej_max) hipLaunchKernelGGL(k_seg_minsize, dim3(blocks_of(nrej_max, 256)), dim3(256), 0, st, v, ms);
+    if (nrej_max) hipLaunchKernelGGL(k_seg_minsize, dim3(blocks_of(nrej_max, 256), p.nv), dim3(256), 0, st, p, ms);
     return hipGetLastError();
 }
 
@@ -489,23 +505,32 @@ size_t seg_sort_temp_bytes(uint32_t n) {
     return bytes;
 }
 
-hipError_t seg_launch_sort(hipStream_t st, const SegView& v, uint32_t n, void* temp, size_t temp_bytes) {
-    if (n == 0) return hipSuccess;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1], (int)n, 0,
-                                                      35, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_seg_gather, dim3(blocks_of(n, 256)), dim3(256), 0, st, v, n);
+// per view: its nmin candidates sorted by key (temp: that view's scratch), then one gather launch
+hipError_t seg_launch_sort(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes) {
+    uint32_t nmax = 0;
+    for (int i = 0; i < p.nv; ++i) {
+        const SegView& v = p.v[i];
+        if (v.nmin == 0) continue;
+        nmax = v.nmin > nmax ? v.nmin : nmax;
+        size_t tb = temp_bytes[i];
+        hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp[i], tb, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1],
+                                                          (int)v.nmin, 0, 35, st);
+        if (e != hipSuccess) return e;
+    }
+    if (nmax) hipLaunchKernelGGL(k_seg_gather, dim3(blocks_of(nmax, 256), p.nv), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_apply(hipStream_t st, const SegView& v, const uint32_t* hooks, int nhooks) {
-    if (nhooks) hipLaunchKernelGGL(k_seg_apply, dim3(blocks_of((size_t)nhooks, 256)), dim3(256), 0, st, v, hooks, nhooks);
+hipError_t seg_launch_apply(hipStream_t st, const SegPair& p) {
+    int nmax = 0;
+    for (int i = 0; i < p.nv; ++i) nmax = p.v[i].nhooks > nmax ? p.v[i].nhooks : nmax;
+    if (nmax) hipLaunchKernelGGL(k_seg_apply, dim3(blocks_of((size_t)nmax, 256), p.nv), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 
-hipError_t seg_launch_trees(hipStream_t st, const SegView& v) {
-    const size_t N = (size_t)v.W * v.H;
-    hipLaunchKernelGGL(k_seg_first, dim3(blocks_of(N, 256)), dim3(256), 0, st, v);
-    hipLaunchKernelGGL(k_seg_virtual, dim3(blocks_of(N, 256)), dim3(256), 0, st, v);
+hipError_t seg_launch_trees(hipStream_t st, const SegPair& p) {
+    const size_t N = (size_t)p.v[0].W * p.v[0].H;
+    hipLaunchKernelGGL(k_seg_first, dim3(blocks_of(N, 256), p.nv), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(k_seg_virtual, dim3(blocks_of(N, 256), p.nv), dim3(256), 0, st, p);
     return hipGetLastError();
 }
