@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(256) k_seg_minsize(SegPair sp, uint32_t ms) {
     const uint32_t p = wave_append(v.cnt + SM_SEG_C_MIN, keep);
     if (keep) {
         v.mlist[p] = r;
-        v.mkey[0][p] = ((unsigned long long)r.w << 25) | r.id;  // the merge's (w, a, b) order
+        v.mkey[0][p] = ((unsigned long long)r.w << 32) | r.id;  // the merge's (w, a, b) order
         v.mval[0][p] = p;
     }
 }
@@ -450,6 +450,8 @@ __global__ void __launch_bounds__(256) k_seg_virtual(SegPair sp) {
 
 unsigned blocks_of(size_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
+constexpr int SEG_KEY_BITS = 42;  // (w << 32) | edge id, w < 1024
+
 }  // namespace
 
 hipError_t seg_launch_init(hipStream_t st, const SegPair& p) {
@@ -501,7 +503,7 @@ hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, ui
 size_t seg_sort_temp_bytes(uint32_t n) {
     size_t bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 35);
+                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, SEG_KEY_BITS);
     return bytes;
 }
 
@@ -514,7 +516,7 @@ hipError_t seg_launch_sort(hipStream_t st, const SegPair& p, void* const* temp, 
         nmax = v.nmin > nmax ? v.nmin : nmax;
         size_t tb = temp_bytes[i];
         hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp[i], tb, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1],
-                                                          (int)v.nmin, 0, 35, st);
+                                                          (int)v.nmin, 0, SEG_KEY_BITS, st);
         if (e != hipSuccess) return e;
     }
     if (nmax) hipLaunchKernelGGL(k_seg_gather, dim3(blocks_of(nmax, 256), p.nv), dim3(256), 0, st, p);
