@@ -771,6 +771,26 @@ def test_full_size_segment_forest(gpu_ctx, src, c, min_size):
     assert t["ntrees"] == n
 
 
+def test_full_size_c3_segment_forest_and_match(gpu_ctx):
+    """BASELINE C3 size (3840x2160) in segment mode: the GPU segmentation's forest against the oracle's
+    serial sweep, then a 32-slice match of the same pair bit-exact against the oracle's forest filter
+    (the largest edge lists, bucket counts and sort keys of the GPU segmentation)."""
+    import stereomatch_amd as sm
+    W, H, d0, D = 3840, 2160, 96, 32
+    left, right, _ = make_pair(W, H, 256, index=4)
+    t = gpu_ctx.build_tree(left, sm.default_params(c=5000.0, min_size=200))
+    wR, wD = O.edge_weights(O.median3(left))
+    mask, n = O.segment(W, H, wR, wD, 5000.0, 200)
+    np.testing.assert_array_equal(t["mask"], mask)
+    assert t["ntrees"] == n
+    out = gpu_ctx.match(left, right, D, sm.default_params(c=5000.0, min_size=200, disp_begin=d0, disp_total=d0 + D))
+    lv, rv = O.cost_agd(left, right, d0, d0 + D)
+    for v, img, vol in (("left", left, lv), ("right", right, rv)):
+        r = O.tree_filter(W, H, O.build_tree(img, 5000.0, 200), vol, d0, True, False, 16)
+        np.testing.assert_array_equal(out[v]["idx"].ravel(), r["idx"])
+        assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
+
+
 @pytest.mark.parametrize("env", [{"SM_SEG_SMALL": "0"}, {"SM_SEG_SMALL": "0", "SM_SEG_GLOBAL_ROUNDS": "0"},
                                  {"SM_SEG_SMALL": "100000000"}, {"SM_SEG_GLOBAL_ROUNDS": "7"}, {"SM_SEG_HOST": "1"}])
 def test_segment_forest_schedules(gpu_ctx, monkeypatch, env):
