@@ -133,7 +133,9 @@ def stream_frames(ctxs, steps, D, params, retire, split=True, lag=1):
     (match_finish), so the GPU never idles on the host; otherwise one match_async per frame.
     lag (1 .. len(ctxs) - 1): frames whose tree is begun but not finished.  1 suits the MST (its
     tree is GPU work that finishes quickly); segment mode's tree has host steps (its worker thread),
-    and lag len(ctxs) - 1 lets that many frames segment at once."""
+    and a larger lag lets that many frames segment at once.  lag len(ctxs) - 1 would retire each
+    frame right after finishing it (the host then waits for its whole filter): len(ctxs) - 2 leaves
+    the filter one iteration to run."""
     n = len(ctxs)
     if n == 1 or not split:
         for i in range(steps):
@@ -332,7 +334,11 @@ def main():
     # frames in flight: each context is a full pipeline on its own stream; frame i goes to context
     # i % n, so frame i+1's prep / MST / layout overlaps frame i's tree filter on the GPU
     per_ctx_gb = W * H * (64 * (1 if Dloc <= 64 else 2 if Dloc <= 128 else 4)) * 20 * 2 / 1e9 + W * H * 400 / 1e9
-    inflight = args.inflight if args.inflight > 0 else max(1, min(3, int(200.0 // per_ctx_gb)))
+    # segment mode: the segmentation's host steps give a frame ~17 ms of latency before its filter,
+    # so it keeps more frames in flight (6) and begins lag = inflight - 2 frames ahead (stream_frames)
+    seg_mode = math.isfinite(args.segment_c)
+    depth = 6 if seg_mode else 3
+    inflight = args.inflight if args.inflight > 0 else max(1, min(depth, int(200.0 // per_ctx_gb)))
     ctxs = [sm.Context(local) for _ in range(inflight)]
     setup_comms(ctxs, world, rank, group, gsize, grank, args.mode, sm.Context)
     pair_index = rank if args.mode == "batch" else 0
@@ -382,10 +388,10 @@ def main():
         accumulate(kacc, c)
 
     t0 = time.perf_counter()
-    seg_mode = math.isfinite(args.segment_c)
     # frame groups: the timed region is args.steps frames of the stream; group fg takes frames fg, fg+G, ...
     my_steps = len(range(plan["fgroup"], args.steps, plan["fgroups"]))
-    stream_frames(ctxs, my_steps, Dloc, params, retire, split=not args.no_split, lag=len(ctxs) - 1 if seg_mode else 1)
+    stream_frames(ctxs, my_steps, Dloc, params, retire, split=not args.no_split,
+                  lag=max(1, len(ctxs) - 2) if seg_mode else 1)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0

@@ -28,12 +28,14 @@ namespace {
 
 __device__ __forceinline__ uint32_t seg_find(uint32_t* par, uint32_t x) {
     // path halving; a concurrent writer only ever stores an ancestor, so every value read is valid
+    // (plain accesses: parents only change by plain stores -- hooks and halving -- which a wave of the
+    // same workgroup sees through the CU's L1 after a barrier, and other kernels after their launch)
     for (;;) {
-        const uint32_t p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t p = par[x];
         if (p == x) return x;
-        const uint32_t g = __hip_atomic_load(par + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t g = par[p];
         if (g == p) return p;
-        __hip_atomic_store(par + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        par[x] = g;
         x = g;
     }
 }
@@ -41,8 +43,10 @@ __device__ __forceinline__ uint32_t seg_find(uint32_t* par, uint32_t x) {
 __device__ __forceinline__ uint32_t edge_b(uint32_t id, int W) { return (id >> 1) + ((id & 1u) ? (uint32_t)W : 1u); }
 
 // the reference's acceptance test at the bucket's start: (double)w <= w_last + (double)(c / (float)size)
+// (sizes grow by L2 atomics, which a CU's L1 does not see: read them at agent scope)
 __device__ __forceinline__ bool seg_open(const SegView& v, uint32_t r, double wd, float c) {
-    return wd <= (double)v.wl[r] + (double)__fdiv_rn(c, (float)v.sz[r]);
+    const uint32_t sz = __hip_atomic_load(v.sz + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return wd <= (double)v.wl[r] + (double)__fdiv_rn(c, (float)sz);
 }
 
 // wave-aggregated append: returns this lane's slot (valid where pred)
@@ -213,7 +217,7 @@ __device__ __forceinline__ void seg_hook_edge(const SegView& v, uint4 e, uint32_
     }
     const uint32_t ph = wave_append(v.cnt + SM_SEG_C_HOOK, hook);
     if (hook) {
-        __hip_atomic_store(v.par + child, parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v.par[child] = parent;
         v.hooked[ph] = child;
         const uint32_t a = e.x >> 1;
         if (e.x & 1u)
@@ -232,13 +236,10 @@ __global__ void __launch_bounds__(256) k_seg_hook(SegPair sp, int lout, uint32_t
     seg_hook_edge(v, e, gen, i < n);
 }
 
-// workgroup barrier that also orders global memory across its waves: release before, acquire (L1
-// invalidate) after, so a wave never reads a list entry, root or key through a stale L1 line
-__device__ __forceinline__ void seg_wg_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
+// workgroup barrier: the waves of one workgroup share the CU's L1, so plain global stores before it
+// are visible to plain loads after it (workgroup scope).  Values changed by atomics (keys, sizes,
+// counters) live in L2 and are read with agent-scope atomic loads.
+__device__ __forceinline__ void seg_wg_sync() { __syncthreads(); }
 
 // the rest of a bucket's Boruvka rounds in one workgroup: n candidates in buffer b ping-pong with the
 // other buffer; gens gen0, gen0 + 1, ... (at most SM_SEG_TAIL_GENS).  Returns the rounds run, or -1 if
@@ -307,7 +308,8 @@ __global__ void __launch_bounds__(1024) k_seg_tail(SegPair sp, int lin, uint32_t
 __device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, int w) {
     const uint32_t r = v.hooked[i];
     const uint32_t t = seg_find(v.par, r);
-    atomicAdd(v.sz + t, v.sz[r]);  // r's size is its size at the bucket's start (only roots grow)
+    // r's size is its size at the bucket's start (only roots grow); agent scope: sizes change in L2
+    atomicAdd(v.sz + t, __hip_atomic_load(v.sz + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     v.wl[t] = (uint16_t)w;
 }
 
