@@ -79,7 +79,7 @@ struct PmsState {
     PmsForest f;
     DevBuf rows, rtree, paths, items, rt_path, rt_item, tree_rounds, tree_start, bfs_pix, nb_start, nb, tree_pt, tree_abase,
         tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result, prof, cuts, reps,
-        cut_bak, Abak;
+        cut_bak, Abak, labu, nprop;
     std::vector<int32_t> h_rtree, h_pt, h_lab;
     std::vector<long long> h_abase;
     long long dice_need = 0;
@@ -1549,7 +1549,9 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
     CHECK(upload_vec(ctx, S.tree_lab, S.h_lab));
     CHECK(ensure(ctx, S.nref, (size_t)std::max(K, 1) * 4));
     CHECK(ensure(ctx, S.lab, (size_t)std::max(lab, 1) * 16));
+    CHECK(ensure(ctx, S.labu, (size_t)std::max(lab, 1) * 16));
     CHECK(ensure(ctx, S.labq, (size_t)std::max(lab, 1) * 4));
+    CHECK(ensure(ctx, S.nprop, (size_t)(f.K + 1) * 4));
     CHECK(ensure(ctx, S.abc, N * 12));
     CHECK(ensure(ctx, S.minc, N * 8));
     CHECK(ensure(ctx, S.abc_bak, N * 12));
@@ -1582,6 +1584,8 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.tree_lab = P<int32_t>(S.tree_lab);
     d.nref = P<int32_t>(S.nref);
     d.lab = P<float4>(S.lab);
+    d.labu = P<float4>(S.labu);
+    d.nprop = nullptr;  // set for the speculative passes' propagation phase only (pms_speculative_call)
     d.labq = P<int32_t>(S.labq);
     d.abc = P<float>(S.abc);
     d.minc = P<double>(S.minc);
@@ -1684,6 +1688,9 @@ sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) 
     return SM_OK;
 }
 
+// SM_PMS_NODEDUP=1: the speculative passes propagate every sampled label, repeats included (A/B)
+bool pms_dedupe() { return getenv("SM_PMS_NODEDUP") == nullptr; }
+
 // One speculative MST_PMS call of one view (iteration > 0).  A pass over the trees [t_lo, K): guessed
 // offsets, every tree's propagation and refinement, validation.  Every tree before the first invalid
 // one (t*) is exact.  t* goes back to the call's starting state and runs serially (its inputs are exact
@@ -1716,7 +1723,15 @@ sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
                 (long long)(f.nb_start[K] - f.nb_start[t_lo]) + 4ll * sm_pms_levels(d.Dmax) * (K - t_lo) + 8;
             HIPC(launch_pms_guess(ctx->st, d, t_lo, wn));
             HIPC(launch_pms_prop_setup(ctx->st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
-            CHECK(pms_phase(ctx, v, d, 0, t_lo, K));
+            if (pms_dedupe()) {  // propagation over each tree's distinct labels (k_pms_prop_dedupe)
+                PmsDev dd = d;
+                dd.nprop = P<int32_t>(S.nprop);
+                HIPC(launch_pms_prop_dedupe(ctx->st, dd, t_lo));  // lab -> labu
+                dd.lab = P<float4>(S.labu);                        // the phase reads the distinct labels
+                CHECK(pms_phase(ctx, v, dd, 0, t_lo, K));
+            } else {
+                CHECK(pms_phase(ctx, v, d, 0, t_lo, K));
+            }
             HIPC(launch_pms_ref_setup(ctx->st, d, t_lo));
             CHECK(pms_phase(ctx, v, d, 1, t_lo, K));
         }
@@ -2050,7 +2065,7 @@ void sm_destroy(sm_ctx* ctx) {
         DevBuf* pb[] = {&S.rows, &S.rtree, &S.paths, &S.items, &S.rt_path, &S.rt_item, &S.tree_rounds, &S.tree_start,
                         &S.bfs_pix, &S.nb_start, &S.nb, &S.tree_pt, &S.tree_abase, &S.tree_lab, &S.nref, &S.lab, &S.labq,
                         &S.abc, &S.minc, &S.abc_bak, &S.minc_bak, &S.A, &S.vrows, &S.off, &S.oguess, &S.cnt, &S.flag,
-                        &S.result, &S.prof};
+                        &S.result, &S.prof, &S.labu, &S.nprop};
         for (DevBuf* b : pb) if (b->p) (void)hipFree(b->p);
     }
     if (ctx->pms_dice.p) (void)hipFree(ctx->pms_dice.p);

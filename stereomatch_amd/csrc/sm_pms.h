@@ -26,6 +26,10 @@ struct PmsDev {
     const int32_t* tree_lab;
     int32_t* nref;
     float4* lab;                 // (a, b, c, 0)
+    // speculative passes: each tree's propagation labels without repeats (first occurrences, in order)
+    // and their count; nprop == nullptr: every tree's phase 0 has deg(t) proposals in lab
+    float4* labu;
+    int32_t* nprop;
     int32_t* labq;               // pixel each propagation label was sampled at
     float* abc;                  // [N][3] current labels
     double* minc;                // [N] current minimum aggregated costs
@@ -59,6 +63,8 @@ struct PmsDev {
 // serial: trees [t0, t1) one after the other in one workgroup (the reference's order), starting at the
 // dice offset *off and leaving the next one there
 hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1);
+// the propagation labels of trees [t_lo, K) without repeats -> labu / nprop (k_pms_prop_dedupe)
+hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo);
 // serial mode, one large tree over the whole GPU: propagation labels from *off, and the refinement
 // labels (after the propagation update), which advance *off
 hipError_t launch_pms_prop_one(hipStream_t st, const PmsDev& d, int t, int deg);

@@ -102,7 +102,7 @@ __device__ __forceinline__ int tree_deg(const PmsDev& d, int t) { return d.nb_st
 __device__ __forceinline__ void phase_labels(const PmsDev& d, int phase, int t, int& P, int& base) {
     const int deg = tree_deg(d, t);
     if (phase == 0) {
-        P = deg;
+        P = d.nprop ? d.nprop[t] : deg;
         base = d.tree_lab[t];
     } else {
         P = d.nref[t];
@@ -613,6 +613,40 @@ __global__ void k_pms_prop_setup(PmsDev d, int t_lo) {
     prop_label(d, lo, d.oguess[lo], e - d.nb_start[lo]);
 }
 
+// Propagation proposals of trees [t_lo, K) without repeats, one wave per tree: the first occurrence of
+// each bitwise-distinct label, in proposal order, into labu, and their count into nprop.  A repeated
+// label has the same data terms and aggregates to bitwise the same costs as its first occurrence, which
+// comes earlier in the strict-< scan (:173-185), so it can never win: the pass runs on labu / nprop
+// with every pixel's result unchanged.  (In later calls many neighbour trees propose the same plane.)
+__global__ void __launch_bounds__(256) k_pms_prop_dedupe(PmsDev d, int t_lo) {
+    const int t = t_lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (t >= d.K) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int deg = tree_deg(d, t), base = d.tree_lab[t];
+    int n = 0;
+    for (int j0 = 0; j0 < deg; j0 += 64) {
+        const int j = j0 + lane;
+        bool keep = false;
+        float4 L = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < deg) {
+            L = d.lab[base + j];
+            keep = true;
+            for (int i = 0; i < j; ++i) {
+                const float4 M = d.lab[base + i];
+                if (__float_as_uint(M.x) == __float_as_uint(L.x) && __float_as_uint(M.y) == __float_as_uint(L.y) &&
+                    __float_as_uint(M.z) == __float_as_uint(L.z)) {
+                    keep = false;
+                    break;
+                }
+            }
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) d.labu[base + n + __popcll(m & ((1ull << lane) - 1ull))] = L;
+        n += __popcll(m);
+    }
+    if (lane == 0) d.nprop[t] = n;
+}
+
 // The data term of every row of [row_lo, row_hi) for the phase's proposals, into the A rows (the up
 // walks' PRE input): rows with few proposals one per lane, wider ones by the whole wave.
 __global__ void __launch_bounds__(256) k_pms_cost(PmsDev d, int phase, int row_lo, int row_hi) {
@@ -884,6 +918,12 @@ hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long
 hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int total_deg) {
     if (total_deg <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_pms_prop_setup, dim3(blocks((size_t)total_deg, 256)), dim3(256), 0, st, d, t_lo);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo) {
+    if (d.K <= t_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_prop_dedupe, dim3(blocks((size_t)(d.K - t_lo) * 64, 256)), dim3(256), 0, st, d, t_lo);
     return hipGetLastError();
 }
 
