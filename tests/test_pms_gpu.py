@@ -62,14 +62,19 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
     assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
 
 
-@pytest.mark.parametrize("mode", ["spec", "repass", "serial"])
+@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
     call's starting labels) and wrong offsets (a new pass); SM_PMS_REPASS=1 re-speculates after
-    every failure; SM_PMS_SERIAL=1 is the plain serial order."""
+    every failure; SM_PMS_SERIAL=1 is the plain serial order; SM_PMS_NODEDUP=1 propagates every
+    sampled label, repeats included (the default drops repeats, k_pms_prop_dedupe)."""
     monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
     monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
+    if mode == "nodedup":
+        monkeypatch.setenv("SM_PMS_NODEDUP", "1")
+    else:
+        monkeypatch.delenv("SM_PMS_NODEDUP", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
