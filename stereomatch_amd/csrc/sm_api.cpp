@@ -1661,6 +1661,9 @@ sm_status pms_phase(sm_ctx* ctx, int v, const PmsDev& d, int phase, int t_lo, in
     return SM_OK;
 }
 
+// SM_PMS_NODEDUP=1: propagation over every sampled label, repeats included (A/B of k_pms_prop_dedupe)
+bool pms_dedupe() { return getenv("SM_PMS_NODEDUP") == nullptr; }
+
 // Trees [t0, t1) in the reference's order from the dice offset *off.  Runs of small trees go to one
 // workgroup (k_pms_serial); a large tree's phases are launched over the whole GPU, round by round.
 sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) {
@@ -1681,15 +1684,21 @@ sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) 
         if (t == t1) break;
         const int deg = f.nb_start[t + 1] - f.nb_start[t];
         HIPC(launch_pms_prop_one(ctx->st, d, t, deg));
-        if (deg > 0) CHECK(pms_phase(ctx, v, d, 0, t, t + 1));
+        if (deg > 0 && pms_dedupe()) {  // over the tree's distinct propagation labels (k_pms_prop_dedupe)
+            PmsDev dd = d;
+            dd.labu = P<float4>(ctx->pms[v].labu);
+            dd.nprop = P<int32_t>(ctx->pms[v].nprop);
+            HIPC(launch_pms_prop_dedupe(ctx->st, dd, t, t + 1));
+            dd.lab = dd.labu;
+            CHECK(pms_phase(ctx, v, dd, 0, t, t + 1));
+        } else if (deg > 0) {
+            CHECK(pms_phase(ctx, v, d, 0, t, t + 1));
+        }
         HIPC(launch_pms_ref_one(ctx->st, d, t));
         CHECK(pms_phase(ctx, v, d, 1, t, t + 1));
     }
     return SM_OK;
 }
-
-// SM_PMS_NODEDUP=1: the speculative passes propagate every sampled label, repeats included (A/B)
-bool pms_dedupe() { return getenv("SM_PMS_NODEDUP") == nullptr; }
 
 // One speculative MST_PMS call of one view (iteration > 0).  A pass over the trees [t_lo, K): guessed
 // offsets, every tree's propagation and refinement, validation.  Every tree before the first invalid
@@ -1726,7 +1735,7 @@ sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
             if (pms_dedupe()) {  // propagation over each tree's distinct labels (k_pms_prop_dedupe)
                 PmsDev dd = d;
                 dd.nprop = P<int32_t>(S.nprop);
-                HIPC(launch_pms_prop_dedupe(ctx->st, dd, t_lo));  // lab -> labu
+                HIPC(launch_pms_prop_dedupe(ctx->st, dd, t_lo, K));  // lab -> labu
                 dd.lab = P<float4>(S.labu);                        // the phase reads the distinct labels
                 CHECK(pms_phase(ctx, v, dd, 0, t_lo, K));
             } else {

@@ -63,8 +63,8 @@ struct PmsDev {
 // serial: trees [t0, t1) one after the other in one workgroup (the reference's order), starting at the
 // dice offset *off and leaving the next one there
 hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1);
-// the propagation labels of trees [t_lo, K) without repeats -> labu / nprop (k_pms_prop_dedupe)
-hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo);
+// the propagation labels of trees [t_lo, t_hi) without repeats -> labu / nprop (k_pms_prop_dedupe)
+hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo, int t_hi);
 // serial mode, one large tree over the whole GPU: propagation labels from *off, and the refinement
 // labels (after the propagation update), which advance *off
 hipError_t launch_pms_prop_one(hipStream_t st, const PmsDev& d, int t, int deg);

@@ -613,14 +613,14 @@ __global__ void k_pms_prop_setup(PmsDev d, int t_lo) {
     prop_label(d, lo, d.oguess[lo], e - d.nb_start[lo]);
 }
 
-// Propagation proposals of trees [t_lo, K) without repeats, one wave per tree: the first occurrence of
+// Propagation proposals of trees [t_lo, t_hi) without repeats, one wave per tree: the first occurrence of
 // each bitwise-distinct label, in proposal order, into labu, and their count into nprop.  A repeated
 // label has the same data terms and aggregates to bitwise the same costs as its first occurrence, which
 // comes earlier in the strict-< scan (:173-185), so it can never win: the pass runs on labu / nprop
 // with every pixel's result unchanged.  (In later calls many neighbour trees propose the same plane.)
-__global__ void __launch_bounds__(256) k_pms_prop_dedupe(PmsDev d, int t_lo) {
+__global__ void __launch_bounds__(256) k_pms_prop_dedupe(PmsDev d, int t_lo, int t_hi) {
     const int t = t_lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (t >= d.K) return;
+    if (t >= t_hi) return;
     const int lane = (int)(threadIdx.x & 63);
     const int deg = tree_deg(d, t), base = d.tree_lab[t];
     int n = 0;
@@ -921,9 +921,9 @@ hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int 
     return hipGetLastError();
 }
 
-hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo) {
-    if (d.K <= t_lo) return hipSuccess;
-    hipLaunchKernelGGL(k_pms_prop_dedupe, dim3(blocks((size_t)(d.K - t_lo) * 64, 256)), dim3(256), 0, st, d, t_lo);
+hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo, int t_hi) {
+    if (t_hi <= t_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_prop_dedupe, dim3(blocks((size_t)(t_hi - t_lo) * 64, 256)), dim3(256), 0, st, d, t_lo, t_hi);
     return hipGetLastError();
 }
 
