@@ -1,7 +1,7 @@
 # Kernel statistics of segment mode (GPU segmentation) -> gpurun_out/segprof/<R>/kernel_stats.csv
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for R in ${ROUNDS:-2 6}; do
+for R in ${ROUNDS:-2}; do
   O=gpurun_out/segprof/r$R
   mkdir -p $O
   SM_SEG_GLOBAL_ROUNDS=$R timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/raw -o run --output-format csv -- python3 bench.py --segment-c 5000 --no-cpu --no-pms --steps 3 --warmup 1 --inflight 1 > $O/bench.log 2>&1 || exit 1
