@@ -1,0 +1,95 @@
+"""The argument behind the GPU segmentation (sm_seg_gpu.h), checked on the CPU: the
+reference's serial Felzenszwalb sweep (segment-graph.h:54-89) plus its min-size merge
+(Stereo3DMST.cpp:293-307) equals a bucket-synchronous restatement in which, per weight bucket,
+
+  * a component is open iff w <= w_last + c/size at the bucket's start (closed ones reject the
+    whole bucket, joined ones accept the rest of it),
+  * the bucket's marked edges are the minimum spanning forest, keyed by edge id, of its open-open
+    edges between components (any order gives the same partition), and
+  * the rejected edges are its other two-component edges; the min-size merge only needs those whose
+    end is smaller than min_size after the sweep, in (w, id) order.
+
+The restatement below is plain Python over small images; the oracle (oracle/sm_oracle.c
+orc_segment, itself pinned to the reference's segment-graph.h) is the serial sweep."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tools.synth import make_pair
+
+
+def bucket_segment(W, H, wR, wD, c, min_size):
+    N = W * H
+    p = np.arange(N)
+    x, y = p % W, p // W
+    e = np.concatenate([2 * p[x + 1 < W], 2 * p[y + 1 < H] + 1])
+    w = np.concatenate([wR[x + 1 < W], wD[y + 1 < H]]).astype(np.int64)
+    par = list(range(N))
+    size = [1] * N
+    wl = [0] * N
+
+    def find(a):
+        while par[a] != a:
+            par[a] = par[par[a]]
+            a = par[a]
+        return a
+
+    mask = np.zeros(N, np.uint8)
+    rejected = []
+    cf = np.float32(c)
+    for wv in np.unique(w):
+        ids = np.sort(e[w == wv])
+        roots = [(find(i >> 1), find((i >> 1) + (W if i & 1 else 1))) for i in ids]
+        opened = {}
+
+        def is_open(r):
+            if r not in opened:  # the acceptance test at the bucket's start (float c / size, double sum)
+                opened[r] = float(wv) <= float(wl[r]) + float(np.float32(cf / np.float32(size[r])))
+            return opened[r]
+
+        cand = []
+        for i, (ra, rb) in zip(ids, roots):
+            if ra == rb:
+                continue
+            if is_open(ra) and is_open(rb):
+                cand.append((int(i), ra, rb))
+            else:
+                rejected.append((int(wv), int(i)))
+        # id-keyed minimum spanning forest of the candidates over the components: Kruskal in id order
+        joined = set()
+        for i, ra, rb in cand:
+            a, b = find(ra), find(rb)
+            if a == b:
+                continue
+            if size[a] < size[b]:
+                a, b = b, a
+            par[b] = a
+            size[a] += size[b]
+            joined.add(a)
+            mask[i >> 1] |= 2 if i & 1 else 1
+        for r in joined:
+            if find(r) == r:
+                wl[r] = int(wv)
+    # a rejected edge still joins two components after the sweep (one end's component is closed)
+    assert all(find(i >> 1) != find((i >> 1) + (W if i & 1 else 1)) for _, i in rejected)
+    ms = max(2, min_size)
+    for wv, i in sorted(rejected):
+        a, b = find(i >> 1), find((i >> 1) + (W if i & 1 else 1))
+        if a != b and (size[a] < ms or size[b] < ms):
+            if size[a] < size[b]:
+                a, b = b, a
+            par[b] = a
+            size[a] += size[b]
+            mask[i >> 1] |= 2 if i & 1 else 1
+    return mask, len({find(q) for q in range(N)})
+
+
+@pytest.mark.parametrize("W,H,c,min_size,index", [(64, 48, 5000.0, 200, 0), (64, 48, 300.0, 20, 1),
+                                                  (80, 40, 40.0, 5, 2), (48, 64, 0.0, 2, 3), (72, 54, 1000.0, 60, 4)])
+def test_bucket_sweep_equals_serial_sweep(W, H, c, min_size, index):
+    left, _, _ = make_pair(W, H, 32, index=index)
+    wR, wD = O.edge_weights(O.median3(left))
+    ref, n = O.segment(W, H, wR, wD, c, min_size)
+    got, k = bucket_segment(W, H, wR, wD, c, min_size)
+    np.testing.assert_array_equal(got, ref)
+    assert k == n
