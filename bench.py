@@ -60,12 +60,12 @@ def host_cpu_info():
     return dict(nproc=os.cpu_count(), affinity=usable, model=model, OMP_NUM_THREADS=omp)
 
 
-def cpu_baseline(W, H, D, slices_1t):
+def cpu_baseline(W, H, D):
     """Oracle (CPU restatement, reference order, fp64) on the benchmarked workload: the full MST build of
     both views (one thread: Kruskal is serial), then all D disparity slices of AGD cost + tree filter +
-    WTA with all usable host cores (OpenMP over slices; the box's share: OMP_NUM_THREADS when set).  A
-    one-thread figure from `slices_1t` slices is reported beside it (extrapolated, labelled so).  Test
-    infrastructure, used only as the reported baseline (never inside the timed region)."""
+    WTA with all usable host cores (OpenMP over slices; the box's share: OMP_NUM_THREADS when set).
+    Measured in full, no extrapolation.  Test infrastructure, used only as the reported baseline (never
+    inside the timed region)."""
     from oracle import oracle as O
     info = host_cpu_info()
     threads = int(info["OMP_NUM_THREADS"] or 0) or info["affinity"]
@@ -86,35 +86,49 @@ def cpu_baseline(W, H, D, slices_1t):
 
     tc, tf = run(0, D, threads)
     frame = t_tree + tc + tf
-    tc1, tf1 = run(D // 2 - slices_1t // 2, slices_1t, 1)
-    frame1 = t_tree + (tc1 + tf1) * (D / slices_1t)
     return dict(value=W * H * D / frame, unit="voxels/s", cores=threads, kind="port", ms_per_frame=frame * 1e3,
-                one_thread=dict(value=W * H * D / frame1, ms_per_frame=frame1 * 1e3, cost_s=tc1, filter_s=tf1,
-                                slices=slices_1t, note="%d of %d slices with one thread, extrapolated to D" % (slices_1t, D)),
                 host=info,
                 stages_s=dict(tree_both_views=t_tree, cost=tc, filter_up_down_wta=tf),
                 sample="one full %dx%d D=%d frame, both views: MST+BFS (1 thread), AGD cost, tree filter and WTA of "
                        "all %d slices (%d threads, OpenMP over slices); %.0f ms/frame" % (W, H, D, D, threads, frame * 1e3))
 
 
+PMS_BYTES_PER_EVAL = 24  # data-term gather (2 x f32) + fp64 A_up write + read per node-label
+
+
 def pms_leg(ctx, left, right, D, iters, oracle):
-    """MST_PMS (SM_AGG_PMS), Stereo3DMST's own label search (c=5000, min_size 200): ms per MST_PMS call
-    per view on the GPU (the first call of a view runs serially, later ones speculatively), beside the
-    oracle's serial CPU restatement of one call (both views, rank 0 only)."""
-    p = sm.default_params(aggregator=sm.SM_AGG_PMS, c=5000.0, min_size=200, pms_iters=iters, disp_total=D)
-    ctx.match(left, right, D, p)  # warm-up
+    """MST_PMS (SM_AGG_PMS): what stereo3dmst() actually runs (Stereo3DMST.cpp:805-904) -- segment forests
+    (c=5000, min_size 200), random plane labels, `iters` MST_PMS calls per view (the reference's 100,
+    :854), plane disparities -- measured end to end as one frame (host buffers in and out), beside the
+    oracle's serial CPU restatement of ONE call per view (rank 0 only).  The roofline of the later calls:
+    node-label evaluations they needed (counted on the device, k_pms_count) x PMS_BYTES_PER_EVAL / their
+    wall time."""
+    p = sm.default_params(aggregator=sm.SM_AGG_PMS, c=5000.0, min_size=200, pms_iters=2, disp_total=D)
+    ctx.match(left, right, D, p)  # warm-up (allocations)
+    p.pms_iters = iters
     t = time.perf_counter()
     ctx.match(left, right, D, p)
     wall = (time.perf_counter() - t) * 1e3
     st = ctx.pms_stats()
-    out = dict(iters_per_view=iters, wall_ms=wall, trees=st["ntrees"], host_prep_ms=st["prep_ms"],
-               first_call_ms_per_view=st["iter0_ms"] / 2,
-               later_call_ms_per_view=st["iters_ms"] / (2 * (iters - 1)) if iters > 1 else None,
+    later_ms = st["iters_ms"]
+    alg = st["evals_later"] * PMS_BYTES_PER_EVAL
+    out = dict(iters_per_view=iters, frame_s=wall / 1e3, trees=st["ntrees"], host_prep_ms=st["prep_ms"],
+               setup_ms=st["setup_ms"], first_call_ms=st["iter0_ms"],
+               later_call_ms=later_ms / (iters - 1) if iters > 1 else None,
+               later_call_ms_per_view=[m / (iters - 1) for m in st["later_ms_view"]] if iters > 1 else None,
+               concurrent_views=bool(st["concurrent_views"]),
                speculative_passes=st["spec_rounds"], serially_run_trees=st["serial_trees"],
-               reference_frame_s_est=(st["prep_ms"] + st["setup_ms"] + st["iter0_ms"] +
-                                      (st["iters_ms"] / (iters - 1) * 99 if iters > 1 else 0)) / 1e3,
-               what="stereo3dmst's algorithm (segment forest c=5000 min_size 200, random plane labels, MST_PMS "
-                    "calls); reference_frame_s_est = host prep + first call + 99 later calls, both views")
+               node_label_evals=dict(first_call=st["evals_first"], later_calls=st["evals_later"],
+                                     later_calls_reference_count=st["evals_later_ref"],
+                                     later_calls_run_on_device=st["evals_later_run"]),
+               roofline=dict(bound="hbm", kernel="MST_PMS later calls (walks, repairs, cost, update)",
+                             bytes_per_eval=PMS_BYTES_PER_EVAL, alg_bytes=alg,
+                             achieved=alg / (later_ms * 1e-3) / 1e9 if later_ms > 0 else 0.0, peak=HBM_PEAK_GBS,
+                             unit="GB/s", frac=alg / (later_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if later_ms > 0 else 0.0,
+                             timing="wall clock of calls 2..%d of both views (host timers around the calls)" % iters),
+               what="stereo3dmst's own algorithm, one frame: sm_match with host buffers (images up, maps down), "
+                    "host prep + first call (serial) + %d later calls (speculative), both views; measured, "
+                    "not extrapolated" % (iters - 1))
     if oracle:
         from oracle import oracle as O
         t = time.perf_counter()
@@ -260,7 +274,6 @@ def main():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--disp", type=int, default=None,
                     help="disparities: total (N=1, strong, batch) or per rank (weak); default per config")
-    ap.add_argument("--cpu-slices-1t", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-io", action="store_true")
     ap.add_argument("--segment-c", type=float, default=float("inf"),
@@ -286,7 +299,8 @@ def main():
                     help="CPU check: start the ranks, print each rank's share and communicator set-up (stub "
                          "contexts, no GPU), exit")
     ap.add_argument("--no-pms", action="store_true", help="skip the MST_PMS (SM_AGG_PMS) timing leg")
-    ap.add_argument("--pms-iters", type=int, default=10, help="MST_PMS calls per view in the PMS timing leg")
+    ap.add_argument("--pms-iters", type=int, default=100,
+                    help="MST_PMS calls per view in the PMS timing leg (the reference's 100, Stereo3DMST.cpp:854)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -548,7 +562,7 @@ def main():
         line["config"]["workload"] = "rank %d/%d of %dx%d D=%d: views %d, slices [%d, %d)" % (
             emu["rank"], emu["nranks"], W, H, Dtot_frame, views, dbeg, dbeg + Dloc)
     if rank == 0 and world == 1 and not args.no_cpu and not emu:
-        line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame, args.cpu_slices_1t)
+        line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame)
     if rank == 0 and world == 1 and not args.no_pms and not emu and args.aggregator == "tree":
         line["pms"] = pms_leg(ctx, left, right, Dtot_frame, max(2, args.pms_iters), not args.no_cpu)
     if rank == 0:

@@ -248,6 +248,17 @@ typedef struct {
     double iter0_ms;        /* the first call of both views (wall) */
     double iters_ms;        /* the remaining calls of both views (wall) */
     double total_ms;        /* the whole SM_AGG_PMS call (wall) */
+    /* appended (round 4) */
+    double calls_ms;        /* all MST_PMS calls of both views (wall) */
+    int concurrent_views;   /* 1: the two views' calls ran concurrently (own host thread + stream each) */
+    double first_ms_view[2];  /* per view: its first call (wall, its own thread) */
+    double later_ms_view[2];  /* per view: its later calls (wall, its own thread) */
+    /* node-label evaluations (one label's data term + up + down + update at one tree node), both views:
+     * needed = distinct propagation labels + refinement labels per tree, times its size; _ref = the
+     * reference's count (every sampled propagation label); _run = what the device ran, speculation and
+     * serial re-runs included */
+    double evals_first, evals_first_ref, evals_first_run;
+    double evals_later, evals_later_ref, evals_later_run;
 } sm_pms_stats;
 sm_status sm_get_pms_stats(sm_ctx* ctx, sm_pms_stats* out);
 

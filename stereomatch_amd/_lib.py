@@ -38,7 +38,12 @@ class SmParams(ctypes.Structure):
 class SmPmsStats(ctypes.Structure):
     _fields_ = [("iters", ctypes.c_int), ("ntrees", ctypes.c_int * 2), ("spec_rounds", ctypes.c_int),
                 ("serial_trees", ctypes.c_int), ("prep_ms", ctypes.c_double), ("setup_ms", ctypes.c_double),
-                ("iter0_ms", ctypes.c_double), ("iters_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+                ("iter0_ms", ctypes.c_double), ("iters_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("calls_ms", ctypes.c_double), ("concurrent_views", ctypes.c_int),
+                ("first_ms_view", ctypes.c_double * 2), ("later_ms_view", ctypes.c_double * 2),
+                ("evals_first", ctypes.c_double), ("evals_first_ref", ctypes.c_double),
+                ("evals_first_run", ctypes.c_double), ("evals_later", ctypes.c_double),
+                ("evals_later_ref", ctypes.c_double), ("evals_later_run", ctypes.c_double)]
 
 
 class SmFilterStats(ctypes.Structure):
@@ -188,6 +193,8 @@ class Context:
                        minc=np.empty((H, W), np.float64)) for v in ("left", "right")}
         self._views = p.views or 3
         self.shape = (H, W)
+        if p.aggregator == SM_AGG_PMS:
+            self._pms_shape = (H, W)
         self._check(lib().sm_match(self.h, ptr(left), ptr(right), W, H, W * 3, D, ctypes.byref(p),
                                    ptr(out["left"]["disp"]), ptr(out["right"]["disp"]), ptr(out["left"]["idx"]),
                                    ptr(out["right"]["idx"]), ptr(out["left"]["minc"]), ptr(out["right"]["minc"])))
@@ -267,7 +274,7 @@ class Context:
     # -- MST_PMS (SM_AGG_PMS) -------------------------------------------------------------
     def labels(self):
         """Plane labels (a, b, c) of every pixel after the last SM_AGG_PMS call: {view: [H*W, 3] float32}."""
-        H, W = self.shape
+        H, W = getattr(self, "_pms_shape", self.shape)  # the size of the SM_AGG_PMS call
         out = {v: np.empty((H * W, 3), np.float32) for v in ("left", "right")}
         self._check(lib().sm_download_labels(self.h, ptr(out["left"]), ptr(out["right"])))
         return out
@@ -277,6 +284,8 @@ class Context:
         self._check(lib().sm_get_pms_stats(self.h, ctypes.byref(s)))
         d = {k: getattr(s, k) for k, _ in SmPmsStats._fields_}
         d["ntrees"] = list(s.ntrees)
+        d["first_ms_view"] = list(s.first_ms_view)
+        d["later_ms_view"] = list(s.later_ms_view)
         return d
 
     # -- stages ---------------------------------------------------------------------------

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -198,7 +199,9 @@ struct sm_ctx {
     bool reduced = false;
     // MST_PMS (SM_AGG_PMS)
     PmsState pms[2];
-    DevBuf pms_dice, pms_rnd;
+    DevBuf pms_dice, pms_rnd, pms_evals;
+    hipStream_t st_pms = nullptr;  // view 1's MST_PMS calls (view 0's run on st), created on first use
+    hipEvent_t ev_pms = nullptr;
     long long pms_dice_n = 0;  // dice values on the device (the stream prefix every call replays)
     std::vector<float> pms_init;   // random plane labels of (W, H, Dmax) (both views start from them)
     int pms_init_key[3] = {0, 0, 0};
@@ -206,13 +209,19 @@ struct sm_ctx {
     std::vector<int32_t> pms_hrnd;
     int32_t* h_pms_res = nullptr;  // pinned: the validation result
     bool pms_last = false;         // the last call was SM_AGG_PMS (labels available)
+    int pms_W = 0, pms_H = 0;      // its image size (the labels' extent)
     sm_pms_stats pms_stats{};
 };
 
 namespace {
 
+// (the two view threads of an MST_PMS call may fail at once: the message is written under a lock)
+std::mutex g_err_mu;
 sm_status fail(sm_ctx* c, sm_status s, const std::string& msg) {
-    if (c) c->err = msg;
+    if (c) {
+        std::lock_guard<std::mutex> lk(g_err_mu);
+        c->err = msg;
+    }
     return s;
 }
 
@@ -1603,6 +1612,7 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.result = P<int32_t>(S.result);
     d.err = ctx->d_err;
     d.prof = nullptr;
+    d.evals = nullptr;
     if (getenv("SM_PMS_PROF")) {  // diagnostics: serial-kernel segment times, printed per call
         if (ensure(ctx, S.prof, 16 * 8) == SM_OK) d.prof = P<long long>(S.prof);
     }
@@ -1641,23 +1651,23 @@ long long pms_big_tree() {
 // One phase (0: propagation, 1: refinement) of trees [t_lo, t_hi) over the whole GPU: the data terms
 // into the A rows, the up rounds deepest first, the cut paths' pieces repaired after each round, the cut paths' A_up rows saved, the
 // down rounds root first (repaired likewise), then the per-pixel update.
-sm_status pms_phase(sm_ctx* ctx, int v, const PmsDev& d, int phase, int t_lo, int t_hi) {
+sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, int phase, int t_lo, int t_hi) {
     const PmsForest& f = ctx->pms[v].f;
     const size_t K1 = (size_t)f.K + 1;
     int R = 0;
     for (int t = t_lo; t < t_hi; ++t) R = std::max(R, f.tree_rounds[t]);
     const std::vector<int32_t>& rt = phase == 0 ? f.rt_item : f.rt_path;
-    HIPC(launch_pms_cost(ctx->st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
+    HIPC(launch_pms_cost(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
     for (int r = R - 1; r >= 0; --r) {
-        HIPC(launch_pms_walk(ctx->st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        HIPC(launch_pms_repair(ctx->st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
+        HIPC(launch_pms_walk(st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
+        HIPC(launch_pms_repair(st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
     }
-    HIPC(launch_pms_cut_backup(ctx->st, d, f.tree_cut[t_lo], f.tree_cut[t_hi]));
+    HIPC(launch_pms_cut_backup(st, d, f.tree_cut[t_lo], f.tree_cut[t_hi]));
     for (int r = 0; r < R; ++r) {
-        HIPC(launch_pms_walk(ctx->st, d, phase, false, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        HIPC(launch_pms_repair(ctx->st, d, phase, false, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
+        HIPC(launch_pms_walk(st, d, phase, false, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
+        HIPC(launch_pms_repair(st, d, phase, false, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
     }
-    HIPC(launch_pms_update(ctx->st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
+    HIPC(launch_pms_update(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
     return SM_OK;
 }
 
@@ -1666,7 +1676,7 @@ bool pms_dedupe() { return getenv("SM_PMS_NODEDUP") == nullptr; }
 
 // Trees [t0, t1) in the reference's order from the dice offset *off.  Runs of small trees go to one
 // workgroup (k_pms_serial); a large tree's phases are launched over the whole GPU, round by round.
-sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) {
+sm_status pms_serial_range(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, int t0, int t1) {
     const PmsForest& f = ctx->pms[v].f;
     const long long big = pms_big_tree();
     int run = t0;
@@ -1679,23 +1689,23 @@ sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) 
             is_big = n * ((std::max(deg, 1) + 63) / 64) >= big || f.tree_cut[t + 1] > f.tree_cut[t];
         }
         if (t < t1 && !is_big) continue;
-        HIPC(launch_pms_serial(ctx->st, d, run, t));
+        HIPC(launch_pms_serial(st, d, run, t));
         run = t + 1;
         if (t == t1) break;
         const int deg = f.nb_start[t + 1] - f.nb_start[t];
-        HIPC(launch_pms_prop_one(ctx->st, d, t, deg));
+        HIPC(launch_pms_prop_one(st, d, t, deg));
         if (deg > 0 && pms_dedupe()) {  // over the tree's distinct propagation labels (k_pms_prop_dedupe)
             PmsDev dd = d;
             dd.labu = P<float4>(ctx->pms[v].labu);
             dd.nprop = P<int32_t>(ctx->pms[v].nprop);
-            HIPC(launch_pms_prop_dedupe(ctx->st, dd, t, t + 1));
+            HIPC(launch_pms_prop_dedupe(st, dd, t, t + 1));
             dd.lab = dd.labu;
-            CHECK(pms_phase(ctx, v, dd, 0, t, t + 1));
+            CHECK(pms_phase(ctx, st, v, dd, 0, t, t + 1));
         } else if (deg > 0) {
-            CHECK(pms_phase(ctx, v, d, 0, t, t + 1));
+            CHECK(pms_phase(ctx, st, v, d, 0, t, t + 1));
         }
-        HIPC(launch_pms_ref_one(ctx->st, d, t));
-        CHECK(pms_phase(ctx, v, d, 1, t, t + 1));
+        HIPC(launch_pms_ref_one(st, d, t));
+        CHECK(pms_phase(ctx, st, v, d, 1, t, t + 1));
     }
     return SM_OK;
 }
@@ -1708,56 +1718,65 @@ sm_status pms_serial_range(sm_ctx* ctx, int v, const PmsDev& d, int t0, int t1) 
 // trees keep their results and are validated again against t*'s exact labels and offset (a tree whose
 // count changed shows up as the next offset failure), so a stale input costs one serial tree instead
 // of a pass.
-sm_status pms_speculative_call(sm_ctx* ctx, int v, PmsDev& d) {
+// Per view counters of the concurrent view threads (summed into sm_pms_stats after the calls)
+struct PmsRun {
+    hipStream_t st = nullptr;
+    int32_t* h_res = nullptr;  // pinned: the validation result
+    int spec_rounds = 0, serial_trees = 0;
+    double first_ms = 0.0, later_ms = 0.0;
+};
+
+sm_status pms_speculative_call(sm_ctx* ctx, PmsRun& run, int v, PmsDev& d) {
+    const hipStream_t st = run.st;
     PmsState& S = ctx->pms[v];
     const PmsForest& f = S.f;
     const int K = f.K;
     const size_t N = (size_t)f.W * f.H;
     const int max_rounds = pms_max_rounds();
-    HIPC(launch_pms_backup(ctx->st, d, N));
-    HIPC(hipMemsetAsync(S.off.p, 0, 16, ctx->st));
+    HIPC(launch_pms_backup(st, d, N));
+    HIPC(hipMemsetAsync(S.off.p, 0, 16, st));
     int t_lo = 0, rounds = 0;
     bool pass = true;
     while (t_lo < K) {
         if (pass) {
             if (rounds >= max_rounds) {  // pathological: finish the call in order
-                CHECK(pms_serial_range(ctx, v, d, t_lo, K));
-                ctx->pms_stats.serial_trees += K - t_lo;
+                CHECK(pms_serial_range(ctx, st, v, d, t_lo, K));
+                run.serial_trees += K - t_lo;
                 break;
             }
             ++rounds;
-            ++ctx->pms_stats.spec_rounds;
+            ++run.spec_rounds;
             // the draws trees [t_lo, K) can consume: their propagation draws + 4 per refinement level
             const long long wn =
                 (long long)(f.nb_start[K] - f.nb_start[t_lo]) + 4ll * sm_pms_levels(d.Dmax) * (K - t_lo) + 8;
-            HIPC(launch_pms_guess(ctx->st, d, t_lo, wn));
-            HIPC(launch_pms_prop_setup(ctx->st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
+            HIPC(launch_pms_guess(st, d, t_lo, wn));
+            HIPC(launch_pms_prop_setup(st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
             if (pms_dedupe()) {  // propagation over each tree's distinct labels (k_pms_prop_dedupe)
                 PmsDev dd = d;
                 dd.nprop = P<int32_t>(S.nprop);
-                HIPC(launch_pms_prop_dedupe(ctx->st, dd, t_lo, K));  // lab -> labu
+                HIPC(launch_pms_prop_dedupe(st, dd, t_lo, K));  // lab -> labu
                 dd.lab = P<float4>(S.labu);                        // the phase reads the distinct labels
-                CHECK(pms_phase(ctx, v, dd, 0, t_lo, K));
+                CHECK(pms_phase(ctx, st, v, dd, 0, t_lo, K));
             } else {
-                CHECK(pms_phase(ctx, v, d, 0, t_lo, K));
+                CHECK(pms_phase(ctx, st, v, d, 0, t_lo, K));
             }
-            HIPC(launch_pms_ref_setup(ctx->st, d, t_lo));
-            CHECK(pms_phase(ctx, v, d, 1, t_lo, K));
+            HIPC(launch_pms_ref_setup(st, d, t_lo));
+            CHECK(pms_phase(ctx, st, v, d, 1, t_lo, K));
         }
-        HIPC(launch_pms_validate(ctx->st, d, t_lo));
-        HIPC(hipMemcpyAsync(ctx->h_pms_res, S.result.p, 16, hipMemcpyDeviceToHost, ctx->st));
-        HIPC(hipStreamSynchronize(ctx->st));
-        const int ts = ctx->h_pms_res[0], why = ctx->h_pms_res[1];
+        HIPC(launch_pms_validate(st, d, t_lo));
+        HIPC(hipMemcpyAsync(run.h_res, S.result.p, 16, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        const int ts = run.h_res[0], why = run.h_res[1];
         if (ts < t_lo || ts > K || (ts < K && why != 1 && why != 2))
             return fail(ctx, SM_ERR_STATE, "MST_PMS validation returned a bad tree index");
         if (ts == K) break;
         pass = why == 1 || pms_repass();
-        HIPC(launch_pms_restore(ctx->st, d, f.tree_start[ts], pass ? (int)N : f.tree_start[ts + 1]));
-        HIPC(hipMemcpyAsync(S.off.p, P<int32_t>(S.result) + 2, 8, hipMemcpyDeviceToDevice, ctx->st));
+        HIPC(launch_pms_restore(st, d, f.tree_start[ts], pass ? (int)N : f.tree_start[ts + 1]));
+        HIPC(hipMemcpyAsync(S.off.p, P<int32_t>(S.result) + 2, 8, hipMemcpyDeviceToDevice, st));
         PmsDev dk = d;
         dk.hi_bak = pass ? 0 : 1;  // later trees keep their (modified) labels: sample the starting ones
-        CHECK(pms_serial_range(ctx, v, dk, ts, ts + 1));
-        ctx->pms_stats.serial_trees += 1;
+        CHECK(pms_serial_range(ctx, st, v, dk, ts, ts + 1));
+        run.serial_trees += 1;
         t_lo = ts + 1;
     }
     return SM_OK;
@@ -1842,30 +1861,51 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipStreamSynchronize(ctx->st));
     const double t2 = now_ms();
     st.setup_ms = t2 - t1;
-    // 5. the MST_PMS calls: left view, then right (:858-889); the rand() values follow that order
+    // 5. the MST_PMS calls: left view, then right (:858-889).  The two views share nothing but read-only
+    // tables (each view's rand() values sit at fixed offsets of the precomputed stream, the dice prefix is
+    // replayed), so each view's calls run on a host thread and stream of their own, concurrently
+    // (SM_PMS_SEQ_VIEWS=1: one after the other, on st, for A/B).  Every call is timed; the node-label
+    // evaluations each call needed are counted on the device (k_pms_count).
     const bool serial_only = pms_serial_only();
-    double iter0 = 0.0, rest = 0.0;
-    size_t roff = 0;
-    for (int v = 0; v < 2; ++v) {
+    const bool seq_views = getenv("SM_PMS_SEQ_VIEWS") && atoi(getenv("SM_PMS_SEQ_VIEWS")) == 1;
+    if (!ctx->st_pms) HIPC(hipStreamCreateWithFlags(&ctx->st_pms, hipStreamNonBlocking));
+    CHECK(ensure(ctx, ctx->pms_evals, 16 * 8));
+    HIPC(hipMemsetAsync(ctx->pms_evals.p, 0, 16 * 8, ctx->st));
+    HIPC(hipEventRecord(ctx->ev_pms, ctx->st));
+    HIPC(hipStreamWaitEvent(ctx->st_pms, ctx->ev_pms, 0));  // view 1's stream after the set-up above
+    PmsRun run[2];
+    run[0].st = ctx->st;
+    run[1].st = seq_views ? ctx->st : ctx->st_pms;
+    run[0].h_res = ctx->h_pms_res;
+    run[1].h_res = ctx->h_pms_res + 4;
+    const size_t roff0[2] = {0, (size_t)iters * K0};
+    auto calls = [ctx, D, iters, serial_only, &roff0](PmsRun& r, int v) -> sm_status {
+        HIPC(hipSetDevice(ctx->device));
+        const hipStream_t st = r.st;
         PmsDev d = pms_dev(ctx, v, D);
+        // per view: [needed, reference's count] of the first call, of the later calls; evaluations run
+        // (speculation and repeats included) of the first call, of the later calls
+        unsigned long long* acc = P<unsigned long long>(ctx->pms_evals) + 8 * v;
         const int K = d.K;
+        size_t roff = roff0[v];
         for (int i = 0; i < iters; ++i) {
             const double a = now_ms();
             d.rnd = P<int32_t>(ctx->pms_rnd) + roff;
+            d.evals = acc + (i == 0 ? 4 : 5);
             roff += (size_t)K;
-            if (d.prof) HIPC(hipMemsetAsync(d.prof, 0, 16 * 8, ctx->st));
+            if (d.prof) HIPC(hipMemsetAsync(d.prof, 0, 16 * 8, st));
             if (i == 0 || serial_only) {
-                HIPC(hipMemsetAsync(ctx->pms[v].off.p, 0, 16, ctx->st));
+                HIPC(hipMemsetAsync(ctx->pms[v].off.p, 0, 16, st));
                 static const bool tree_times = getenv("SM_PMS_TREE_TIMES") != nullptr;  // diagnostics (tools)
                 if (tree_times && i == 0) {
                     std::vector<hipEvent_t> ev(K + 1);
                     for (auto& e : ev) HIPC(hipEventCreate(&e));
-                    HIPC(hipEventRecord(ev[0], ctx->st));
+                    HIPC(hipEventRecord(ev[0], st));
                     for (int t = 0; t < K; ++t) {
-                        CHECK(pms_serial_range(ctx, v, d, t, t + 1));
-                        HIPC(hipEventRecord(ev[t + 1], ctx->st));
+                        CHECK(pms_serial_range(ctx, st, v, d, t, t + 1));
+                        HIPC(hipEventRecord(ev[t + 1], st));
                     }
-                    HIPC(hipStreamSynchronize(ctx->st));
+                    HIPC(hipStreamSynchronize(st));
                     const PmsForest& f = ctx->pms[v].f;
                     for (int t = 0; t < K; ++t) {
                         float ms = 0;
@@ -1875,13 +1915,14 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                     }
                     for (auto& e : ev) HIPC(hipEventDestroy(e));
                 } else {
-                    CHECK(pms_serial_range(ctx, v, d, 0, K));
+                    CHECK(pms_serial_range(ctx, st, v, d, 0, K));
                 }
-                st.serial_trees += K;
+                r.serial_trees += K;
             } else {
-                CHECK(pms_speculative_call(ctx, v, d));
+                CHECK(pms_speculative_call(ctx, r, v, d));
             }
-            HIPC(hipStreamSynchronize(ctx->st));
+            HIPC(launch_pms_count(st, d, acc + (i == 0 ? 0 : 2)));
+            HIPC(hipStreamSynchronize(st));
             const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE);
             if (e & 6u) {
                 __atomic_store_n(ctx->h_err, 0u, __ATOMIC_RELEASE);
@@ -1889,7 +1930,7 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                                                         : "MST_PMS: a propagation index fell outside its tree (the "
                                                           "reference would read outside mst_vertices_vec)");
             }
-            (i == 0 ? iter0 : rest) += now_ms() - a;
+            (i == 0 ? r.first_ms : r.later_ms) += now_ms() - a;
             if (d.prof) {
                 long long h[16];
                 HIPC(hipMemcpy(h, d.prof, 16 * 8, hipMemcpyDeviceToHost));
@@ -1898,7 +1939,29 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                         h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5, h[8]);
             }
         }
-        // outputs: the plane disparity, the per-pixel aggregated minimum, idx = -1
+        return SM_OK;
+    };
+    const double tc0 = now_ms();
+    sm_status rs[2] = {SM_OK, SM_OK};
+    if (seq_views) {
+        rs[0] = calls(run[0], 0);
+        if (rs[0] == SM_OK) rs[1] = calls(run[1], 1);
+    } else {
+        std::thread other([&] {
+            try {
+                rs[1] = calls(run[1], 1);
+            } catch (...) {
+                rs[1] = SM_ERR_STATE;
+            }
+        });
+        rs[0] = calls(run[0], 0);
+        other.join();
+    }
+    const double tc1 = now_ms();
+    CHECK(rs[0]);
+    CHECK(rs[1]);
+    // outputs: the plane disparity, the per-pixel aggregated minimum, idx = -1
+    for (int v = 0; v < 2; ++v) {
         CHECK(ensure(ctx, ctx->disp[v], N * 4));
         CHECK(ensure(ctx, ctx->minc[v], N * 8));
         CHECK(ensure(ctx, ctx->idx[v], N * 4));
@@ -1906,10 +1969,32 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
         HIPC(hipMemcpyAsync(ctx->minc[v].p, ctx->pms[v].minc.p, N * 8, hipMemcpyDeviceToDevice, ctx->st));
         HIPC(hipMemsetAsync(ctx->idx[v].p, 0xFF, N * 4, ctx->st));
     }
+    unsigned long long ev[16];
+    HIPC(hipMemcpyAsync(ev, ctx->pms_evals.p, sizeof(ev), hipMemcpyDeviceToHost, ctx->st));
+    HIPC(hipStreamSynchronize(ctx->st));
+    // wall clock of the calls: the first calls of the views (the longer one), then the rest
+    const double iter0 = std::max(run[0].first_ms, run[1].first_ms);
+    const double rest = seq_views ? run[0].later_ms + run[1].later_ms : (tc1 - tc0) - iter0;
+    st.spec_rounds = run[0].spec_rounds + run[1].spec_rounds;
+    st.serial_trees = run[0].serial_trees + run[1].serial_trees;
+    st.calls_ms = tc1 - tc0;
+    st.concurrent_views = seq_views ? 0 : 1;
+    for (int v = 0; v < 2; ++v) {
+        st.first_ms_view[v] = run[v].first_ms;
+        st.later_ms_view[v] = run[v].later_ms;
+    }
+    st.evals_first = (double)(ev[0] + ev[8]);
+    st.evals_first_ref = (double)(ev[1] + ev[9]);
+    st.evals_later = (double)(ev[2] + ev[10]);
+    st.evals_later_ref = (double)(ev[3] + ev[11]);
+    st.evals_first_run = (double)(ev[4] + ev[12]);
+    st.evals_later_run = (double)(ev[5] + ev[13]);
     st.iter0_ms = iter0;
     st.iters_ms = rest;
     st.total_ms = now_ms() - t0;
     ctx->pms_last = true;
+    ctx->pms_W = W;
+    ctx->pms_H = H;
     return SM_OK;
 }
 
@@ -2013,7 +2098,8 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         return SM_ERR_HIP;
     }
     ctx->h_err[0] = 0;
-    if (hipHostMalloc((void**)&ctx->h_pms_res, 16) != hipSuccess ||
+    if (hipHostMalloc((void**)&ctx->h_pms_res, 32) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ev_pms, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_changed, (2 * SM_MST_MAX_ROUNDS + 8) * sizeof(int)) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_rounds, 2 * RREC_FWD * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
@@ -2074,10 +2160,16 @@ void sm_destroy(sm_ctx* ctx) {
         DevBuf* pb[] = {&S.rows, &S.rtree, &S.paths, &S.items, &S.rt_path, &S.rt_item, &S.tree_rounds, &S.tree_start,
                         &S.bfs_pix, &S.nb_start, &S.nb, &S.tree_pt, &S.tree_abase, &S.tree_lab, &S.nref, &S.lab, &S.labq,
                         &S.abc, &S.minc, &S.abc_bak, &S.minc_bak, &S.A, &S.vrows, &S.off, &S.oguess, &S.cnt, &S.flag,
-                        &S.result, &S.prof, &S.labu, &S.nprop};
+                        &S.result, &S.prof, &S.labu, &S.nprop, &S.vrows, &S.cuts, &S.reps, &S.cut_bak, &S.Abak};
         for (DevBuf* b : pb) if (b->p) (void)hipFree(b->p);
     }
     if (ctx->pms_dice.p) (void)hipFree(ctx->pms_dice.p);
+    if (ctx->pms_evals.p) (void)hipFree(ctx->pms_evals.p);
+    if (ctx->st_pms) {
+        (void)hipStreamSynchronize(ctx->st_pms);
+        (void)hipStreamDestroy(ctx->st_pms);
+    }
+    if (ctx->ev_pms) (void)hipEventDestroy(ctx->ev_pms);
     if (ctx->pms_rnd.p) (void)hipFree(ctx->pms_rnd.p);
     if (ctx->h_pms_res) (void)hipHostFree(ctx->h_pms_res);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);
@@ -2130,6 +2222,7 @@ sm_status sm_upload_cost_volumes(sm_ctx* ctx, const float* left_vol, const float
 sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
     if (!ctx) return SM_ERR_ARG;
     if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_match_begin: the previous call was not finished (sm_match_finish)");
+    if (ctx->seg_worker.joinable()) ctx->seg_worker.join();  // a worker left by a failed finish
     if (ctx->W == 0) return fail(ctx, SM_ERR_STATE, "no images uploaded");
     CHECK(check_params(ctx, p, D));
     const CallRange cr = call_range(p, D);
@@ -2150,7 +2243,8 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
         hipStream_t main = nullptr;
         ~TreeStream() { if (main) c->st = main; }
     } ts{ctx};
-    if (ctx->st_tree && p->aggregator != SM_AGG_GUIDED) {
+    // (the guided and MST_PMS aggregators run their whole call on st: no tree stream)
+    if (ctx->st_tree && p->aggregator == SM_AGG_TREE) {
         HIPC(hipEventRecord(ctx->ev_enq, ctx->st));
         HIPC(hipStreamWaitEvent(ctx->st_tree, ctx->ev_enq, 0));
         ts.main = ctx->st;
@@ -2220,7 +2314,13 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
                 HIPC(hipEventRecord(ctx->ev[2], ctx->st));
                 return stage_layout_enqueue(ctx, views);
             };
-            ctx->seg_status = work();
+            try {
+                ctx->seg_status = work();
+            } catch (const std::bad_alloc&) {
+                ctx->seg_status = SM_ERR_OOM;
+            } catch (...) {
+                ctx->seg_status = SM_ERR_STATE;
+            }
         });
         ctx->pending = 1;
         ctx->pend_D = D;
@@ -2246,15 +2346,15 @@ sm_status sm_match_finish(sm_ctx* ctx) {
     if (!ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_match_finish without sm_match_begin");
     const int kind = ctx->pending;
     ctx->pending = 0;
-    if (kind == 2) return SM_OK;  // guided: enqueued in full by sm_match_begin
+    if (kind == 2) return SM_OK;  // guided / MST_PMS: enqueued in full by sm_match_begin
+    // the asynchronous segment-mode tree (sm_match_begin): joined before anything can return early
+    const bool had_worker = ctx->seg_worker.joinable();
+    if (had_worker) ctx->seg_worker.join();
     HIPC(hipSetDevice(ctx->device));
     const sm_params* p = &ctx->pend_p;
     const int D = ctx->pend_D;
     const CallRange cr = call_range(p, D);
-    if (ctx->seg_worker.joinable()) {  // the asynchronous segment-mode tree (sm_match_begin)
-        ctx->seg_worker.join();
-        CHECK(ctx->seg_status);
-    }
+    if (had_worker) CHECK(ctx->seg_status);
     CHECK(stage_layout_finish(ctx, ctx->views));
     HIPC(hipEventRecord(ctx->ev[3], ctx->st));
     CHECK(stage_filter(ctx, cr.D, cr.d0, ctx->views, false, &cr.w));
@@ -2493,7 +2593,8 @@ sm_status sm_download_labels(sm_ctx* ctx, float* left_abc, float* right_abc) {
     if (!ctx->pms_last) return fail(ctx, SM_ERR_STATE, "sm_download_labels: the last call was not SM_AGG_PMS");
     if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_download_labels: a begun call is not finished");
     HIPC(hipSetDevice(ctx->device));
-    const size_t N = (size_t)ctx->W * ctx->H;
+    // the labels' size is the PMS call's (a later upload may have changed W / H)
+    const size_t N = (size_t)ctx->pms_W * ctx->pms_H;
     float* out[2] = {left_abc, right_abc};
     for (int v = 0; v < 2; ++v)
         if (out[v]) HIPC(hipMemcpyAsync(out[v], ctx->pms[v].abc.p, N * 12, hipMemcpyDeviceToHost, ctx->st));

@@ -47,6 +47,7 @@ struct PmsDev {
     int32_t* result;             // [0] first invalid tree (K: none), [1..2] its exact offset (int64)
     uint32_t* err;               // bit 1: a sampled index fell outside its tree; bit 2: dice stream exhausted
     long long* prof;             // SM_PMS_PROF: k_pms_serial segment totals (nullptr: off)
+    unsigned long long* evals;   // node-label evaluations the per-pixel updates ran (nullptr: not counted)
     const double* slut;
     const double* s2lut;
     // pieces (sm_pms_host.h PmsCut): cut paths, repair items, per-cut backup offsets into Abak (the
@@ -85,6 +86,9 @@ hipError_t launch_pms_cut_backup(hipStream_t st, const PmsDev& d, int c_lo, int 
 hipError_t launch_pms_validate(hipStream_t st, const PmsDev& d, int t_lo);
 hipError_t launch_pms_restore(hipStream_t st, const PmsDev& d, int row_lo, int row_hi);
 hipError_t launch_pms_backup(hipStream_t st, const PmsDev& d, size_t N);
+// after a call: the node-label evaluations it needed, acc[0] += sum_t size(t) * (distinct propagation labels
+// + refinement labels), and the reference's count, acc[1] += sum_t size(t) * (deg(t) + refinement labels)
+hipError_t launch_pms_count(hipStream_t st, const PmsDev& d, unsigned long long* acc);
 // [D][N] volume slices (MC-CNN layout; clamp: NaN -> 0.5, min(0.5, x), Stereo3DMST.cpp:785-803) ->
 // [N][Dv] cost rows
 hipError_t launch_pms_vol_rows(hipStream_t st, const float* in, size_t N, int D, int Dv, int clamp, float* out);

@@ -524,6 +524,7 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
                     __syncthreads();
                 }
                 seg(4 * phase + 2);
+                if (d.evals && tid == 0) atomicAdd(d.evals, (unsigned long long)(te - ts) * (unsigned long long)P);
                 for (int row = ts + tid; row < te; row += nt) update_row(d, phase, row, t);
                 __threadfence_block();
                 __syncthreads();
@@ -743,6 +744,12 @@ __global__ void __launch_bounds__(256) k_pms_update(PmsDev d, int phase, int row
         phase_labels(d, phase, t, P, lb);
     }
     const bool wide = valid && P > 16;
+    if (d.evals) {  // the wave's node-label evaluations
+        int sum = valid ? P : 0;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+        if (lane == 0 && sum) atomicAdd(d.evals, (unsigned long long)sum);
+    }
     if (valid && !wide) update_row(d, phase, row, t);
     unsigned long long m = __ballot(wide);
     while (m) {
@@ -878,6 +885,38 @@ __global__ void k_pms_backup(PmsDev d, size_t N) {
     d.abc_bak[3 * i + 2] = d.abc[3 * i + 2];
 }
 
+// Per tree (one wave): the distinct propagation labels of the call (lab holds every tree's exact
+// sampled labels once the call is done, in both device modes) and the refinement labels (nref), times
+// the tree's size -- the node-label evaluations the call needed (acc[0]; repeats of a label cannot win,
+// k_pms_prop_dedupe) and the reference's count, every sampled label (acc[1]).
+__global__ void __launch_bounds__(256) k_pms_count(PmsDev d, unsigned long long* acc) {
+    const int t = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (t >= d.K) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int deg = tree_deg(d, t), base = d.tree_lab[t];
+    int n = 0;
+    for (int j0 = 0; j0 < deg; j0 += 64) {
+        const int j = j0 + lane;
+        bool keep = false;
+        if (j < deg) {
+            const float4 L = d.lab[base + j];
+            keep = true;
+            for (int i = 0; i < j && keep; ++i) {
+                const float4 M = d.lab[base + i];
+                keep = !(__float_as_uint(M.x) == __float_as_uint(L.x) && __float_as_uint(M.y) == __float_as_uint(L.y) &&
+                         __float_as_uint(M.z) == __float_as_uint(L.z));
+            }
+        }
+        n += __popcll(__ballot(keep));
+    }
+    if (lane == 0) {
+        const unsigned long long sz = (unsigned long long)(d.tree_start[t + 1] - d.tree_start[t]);
+        const unsigned long long nr = (unsigned long long)d.nref[t];
+        atomicAdd(acc, sz * ((unsigned long long)n + nr));
+        atomicAdd(acc + 1, sz * ((unsigned long long)deg + nr));
+    }
+}
+
 inline unsigned blocks(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
@@ -979,6 +1018,12 @@ hipError_t launch_pms_restore(hipStream_t st, const PmsDev& d, int row_lo, int r
 
 hipError_t launch_pms_backup(hipStream_t st, const PmsDev& d, size_t N) {
     hipLaunchKernelGGL(k_pms_backup, dim3(blocks(N, 256)), dim3(256), 0, st, d, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_count(hipStream_t st, const PmsDev& d, unsigned long long* acc) {
+    if (d.K <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_count, dim3(blocks((size_t)d.K * 64, 256)), dim3(256), 0, st, d, acc);
     return hipGetLastError();
 }
 

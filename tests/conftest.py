@@ -28,6 +28,18 @@ def load_case(name):
         return {k: z[k] for k in z.files}
 
 
+def flir_pair():
+    """The FLIR 000020 pair (BGR, 2048x1536), decode-checked against the committed sums."""
+    from PIL import Image
+    d = os.path.join(GOLDEN, "flir")
+    L = np.ascontiguousarray(np.array(Image.open(os.path.join(d, "000020_191400042.jpg")).convert("RGB"))[:, :, ::-1])
+    R = np.ascontiguousarray(np.array(Image.open(os.path.join(d, "000020_191400039.jpg")).convert("RGB"))[:, :, ::-1])
+    with np.load(os.path.join(d, "decode_check.npz")) as chk:
+        assert int(L.astype(np.int64).sum()) == int(chk["left_sum"])
+        assert int(R.astype(np.int64).sum()) == int(chk["right_sum"])
+    return L, R
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx():
     import stereomatch_amd as sm

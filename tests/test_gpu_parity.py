@@ -3,12 +3,11 @@ reference-derived golden fixtures.  Integer/index outputs and the fp64 aggregate
 are compared BIT-EXACT (the kernels perform the shipped reference's exact operation
 sequence); the north-star tolerance (1e-4 relative on aggregated costs) is
 therefore met with zero slack."""
-import os
 
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_cases, load_case
+from conftest import flir_pair, golden_cases, load_case
 from oracle import oracle as O
 from tools.synth import make_pair
 
@@ -401,18 +400,6 @@ def test_large_disp_begin_pads(gpu_ctx):
         r = O.tree_filter(W, H, O.build_tree(left if v == "left" else right), vol, d0, True, False, 16)
         np.testing.assert_array_equal(out[v]["idx"].ravel(), r["idx"])
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
-
-
-def flir_pair():
-    """The FLIR 000020 pair (BGR, 2048x1536), decode-checked against the committed sums."""
-    from PIL import Image
-    d = os.path.join(GOLDEN, "flir")
-    L = np.ascontiguousarray(np.array(Image.open(os.path.join(d, "000020_191400042.jpg")).convert("RGB"))[:, :, ::-1])
-    R = np.ascontiguousarray(np.array(Image.open(os.path.join(d, "000020_191400039.jpg")).convert("RGB"))[:, :, ::-1])
-    with np.load(os.path.join(d, "decode_check.npz")) as chk:
-        assert int(L.astype(np.int64).sum()) == int(chk["left_sum"])
-        assert int(R.astype(np.int64).sum()) == int(chk["right_sum"])
-    return L, R
 
 
 def test_flir_c1_bitexact(gpu_ctx):
@@ -1048,3 +1035,35 @@ def test_guided_subpixel_with_one_rank_comm():
         assert not np.array_equal(out["left"]["disp"], out["left"]["idx"].astype(np.float32))  # subpixel survived
     finally:
         ctx.close()
+
+
+@pytest.mark.timeout(600)
+def test_segment_mode_begin_on_many_contexts_bitexact():
+    """Segment mode (c finite) with begin/finish interleaved over 4 contexts, as bench.py streams segment
+    frames (lag inflight - 2): every context's segmentation runs on its own worker thread concurrently
+    (hipcub sorts, host waits, pinned min-size buffers of several contexts at once) before any finish.
+    Each frame's forest and match against the oracle's serial segment_graph + min-size merge."""
+    import stereomatch_amd as sm
+    cases = [(320, 200, 48, 5000.0, 200, 1), (288, 176, 64, 300.0, 20, 2), (320, 200, 32, 5000.0, 200, 3),
+             (256, 160, 48, 40.0, 5, 4)]
+    ctxs = [sm.Context(0) for _ in cases]
+    try:
+        pairs = []
+        for c, (W, H, D, cc, ms, idx) in zip(ctxs, cases):
+            l, r, _ = make_pair(W, H, D, index=idx)
+            pairs.append((l, r))
+            c.upload(l, r)
+        for c, (W, H, D, cc, ms, idx) in zip(ctxs, cases):
+            c.match_begin(D, sm.default_params(c=cc, min_size=ms))
+        for c in ctxs:
+            c.match_finish()
+        for c, (l, r), (W, H, D, cc, ms, idx) in zip(ctxs, pairs, cases):
+            c.synchronize()
+            out = c.results()
+            ref = O.match(l, r, D, c=cc, min_size=ms, nthreads=16)
+            for v in ("left", "right"):
+                np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"], err_msg="%dx%d c=%g %s" % (W, H, cc, v))
+                assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
+    finally:
+        for c in ctxs:
+            c.close()

@@ -183,3 +183,41 @@ def test_pms_reference_surface_100_calls(gpu_ctx):
     ref = O.stereo3dmst_pms(left, right, 48, iters=100)
     np.testing.assert_array_equal(u32(ld), u32(ref["left"]["disp_checked"]))
     np.testing.assert_array_equal(u32(rd), u32(ref["right"]["disp"]))
+
+
+@pytest.mark.timeout(900)
+def test_pms_full_c2_speculative_bitexact(gpu_ctx, monkeypatch):
+    """Full C2 (1920x1200, Dmax 128), c=5000, min_size 200, THREE MST_PMS calls per view: calls 2-3 take
+    the speculative path (guessed offsets, every tree at once, validation, single-tree repairs) with the
+    default 512-row pieces, propagation dedupe and whole-GPU launches -- the mode the reference's 99 later
+    calls per view run in (Stereo3DMST.cpp:546-629, 854-889).  Labels, fp64 minima and plane disparities
+    bitwise against the oracle's serial restatement."""
+    for k in ("SM_PMS_SERIAL", "SM_PMS_REPASS", "SM_PMS_NODEDUP", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS"):
+        monkeypatch.delenv(k, raising=False)
+    left, right, _ = make_pair(1920, 1200, 128, index=0)
+    ref = O.stereo3dmst_pms(left, right, 128, iters=3, c=5000.0, min_size=200)
+    out, labs, st = run_gpu(gpu_ctx, left, right, 128, 3)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+    assert st["spec_rounds"] >= 4  # calls 2..3 of both views: at least one speculative pass each
+    assert st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
+
+
+@pytest.mark.timeout(900)
+def test_pms_flir_c1_two_calls_output_step(gpu_ctx, monkeypatch):
+    """BASELINE config C1's pair (FLIR 000020, 2048x1536, Dmax 64), the reference's own constants, two
+    MST_PMS calls per view (the second speculative) and stereo3dmst's output step (LabelToDisp, *= Dmax-1,
+    L-R check of the left map; :189-201, :900-904), bitwise against the oracle."""
+    from conftest import flir_pair
+    for k in ("SM_PMS_SERIAL", "SM_PMS_REPASS", "SM_PMS_NODEDUP", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS"):
+        monkeypatch.delenv(k, raising=False)
+    L, R = flir_pair()
+    D = 64
+    ref = O.stereo3dmst_pms(L, R, D, iters=2, c=5000.0, min_size=200)
+    out, labs, st = run_gpu(gpu_ctx, L, R, D, 2, post=sm.STEREO3DMST_POST)
+    for v in ("left", "right"):
+        np.testing.assert_array_equal(u32(labs[v]), u32(ref[v]["abc"]), err_msg="%s labels" % v)
+        np.testing.assert_array_equal(u64(out[v]["minc"].ravel()), u64(ref[v]["minc"]), err_msg="%s minima" % v)
+    np.testing.assert_array_equal(u32(out["right"]["disp"].ravel()), u32(ref["right"]["disp"].ravel()))
+    np.testing.assert_array_equal(u32(out["left"]["disp"].ravel()), u32(ref["left"]["disp_checked"].ravel()))
+    assert st["spec_rounds"] >= 2
