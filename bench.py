@@ -120,7 +120,7 @@ def pms_leg(ctx, left, right, D, iters, oracle):
                speculative_passes=st["spec_rounds"], serially_run_trees=st["serial_trees"],
                node_label_evals=dict(first_call=st["evals_first"], later_calls=st["evals_later"],
                                      later_calls_reference_count=st["evals_later_ref"],
-                                     later_calls_run_on_device=st["evals_later_run"]),
+                                     later_calls_run_on_device=st["evals_later_run"] or None),
                roofline=dict(bound="hbm", kernel="MST_PMS later calls (walks, repairs, cost, update)",
                              bytes_per_eval=PMS_BYTES_PER_EVAL, alg_bytes=alg,
                              achieved=alg / (later_ms * 1e-3) / 1e9 if later_ms > 0 else 0.0, peak=HBM_PEAK_GBS,

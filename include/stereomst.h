@@ -256,9 +256,11 @@ typedef struct {
     /* node-label evaluations (one label's data term + up + down + update at one tree node), both views:
      * needed = distinct propagation labels + refinement labels per tree, times its size; _ref = the
      * reference's count (every sampled propagation label); _run = what the device ran, speculation and
-     * serial re-runs included */
+     * serial re-runs included (counted only under env SM_PMS_COUNT_RUN=1, else 0) */
     double evals_first, evals_first_ref, evals_first_run;
     double evals_later, evals_later_ref, evals_later_run;
+    double prep_seg_ms;     /* host wall of prep_ms: the segmentation (GPU) and its host copies */
+    double prep_forest_ms;  /* the reference-numbered forests and walk schedules, both views */
 } sm_pms_stats;
 sm_status sm_get_pms_stats(sm_ctx* ctx, sm_pms_stats* out);
 

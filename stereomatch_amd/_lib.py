@@ -43,7 +43,8 @@ class SmPmsStats(ctypes.Structure):
                 ("first_ms_view", ctypes.c_double * 2), ("later_ms_view", ctypes.c_double * 2),
                 ("evals_first", ctypes.c_double), ("evals_first_ref", ctypes.c_double),
                 ("evals_first_run", ctypes.c_double), ("evals_later", ctypes.c_double),
-                ("evals_later_ref", ctypes.c_double), ("evals_later_run", ctypes.c_double)]
+                ("evals_later_ref", ctypes.c_double), ("evals_later_run", ctypes.c_double),
+                ("prep_seg_ms", ctypes.c_double), ("prep_forest_ms", ctypes.c_double)]
 
 
 class SmFilterStats(ctypes.Structure):
@@ -103,6 +104,7 @@ def lib():
         "sm_download_labels": ([vp, vp, vp], ci),
         "sm_get_pms_stats": ([vp, ctypes.POINTER(SmPmsStats)], ci),
         "sm_pms_forest_bfs": ([ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp], ci),
+        "sm_pms_forest_digest": ([ci, ci, vp, vp, vp, ci, ci, vp, vp, vp], ci),
         "sm_pms_tree_graph": ([ci, ci, vp, vp, vp, vp, vp, ci], ci),
         "sm_pms_dice": ([ctypes.c_long, vp], None),
         "sm_pms_glibc_random": ([ctypes.c_uint, ctypes.c_long, ctypes.c_long, vp], None),
@@ -355,6 +357,18 @@ def pms_forest_bfs(W, H, wR, wD, mask):
     return dict(ntrees=k, tree_start=ts[:k + 1].copy(), node_pix=pix, node_parent=par, node_w=w, node_nch=nch,
                 node_child=ch)
 
+
+
+def pms_forest_digest(W, H, wR, wD, mask, piece, nthreads):
+    """The MST_PMS schedule forest (sm_pms_host.cpp pms_build_forest) on `nthreads` host threads: digests
+    of its arrays, tree_start and bfs_pix (test hook)."""
+    N = W * H
+    dig = np.zeros(6, np.uint64)
+    ts = np.empty(N + 1, np.int32)
+    pix = np.empty(N, np.int32)
+    k = lib().sm_pms_forest_digest(W, H, ptr(np.ascontiguousarray(wR, np.uint16)), ptr(np.ascontiguousarray(wD, np.uint16)),
+                                   ptr(np.ascontiguousarray(mask, np.uint8)), piece, nthreads, ptr(dig), ptr(ts), ptr(pix))
+    return dict(ntrees=k, digest=dig, tree_start=ts[:k + 1].copy(), bfs_pix=pix)
 
 def pms_tree_graph(W, H, wR, wD, mask):
     N = W * H

@@ -80,7 +80,7 @@ struct PmsState {
     PmsForest f;
     DevBuf rows, rtree, paths, items, rt_path, rt_item, tree_rounds, tree_start, bfs_pix, nb_start, nb, tree_pt, tree_abase,
         tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result, prof, cuts, reps,
-        cut_bak, Abak, labu, nprop;
+        cut_bak, Abak, labu, nprop, rep_flag, pt_ph, ab_ph, plan_cnt, plan_path, plan_item, plan_base, plan_ibase;
     std::vector<int32_t> h_rtree, h_pt, h_lab;
     std::vector<long long> h_abase;
     long long dice_need = 0;
@@ -1540,6 +1540,10 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
     }
     CHECK(upload_vec(ctx, S.cuts, f.cuts));
     CHECK(upload_vec(ctx, S.reps, f.reps));
+    CHECK(ensure(ctx, S.rep_flag, std::max<size_t>(f.reps.size(), 1) * 4));
+    CHECK(ensure(ctx, S.pt_ph, (size_t)std::max(K, 1) * 4));
+    CHECK(ensure(ctx, S.ab_ph, (size_t)std::max(K, 1) * 8));
+    HIPC(hipMemsetAsync(S.rep_flag.p, 0, std::max<size_t>(f.reps.size(), 1) * 4, ctx->st));
     CHECK(upload_vec(ctx, S.cut_bak, cut_bak));
     CHECK(ensure(ctx, S.Abak, (size_t)std::max(bak, 1ll) * 8));
     CHECK(upload_vec(ctx, S.rows, f.rows));
@@ -1571,6 +1575,21 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
     CHECK(ensure(ctx, S.cnt, (size_t)std::max(K, 1) * 4));
     CHECK(ensure(ctx, S.flag, (size_t)std::max(K, 1) * 4));
     CHECK(ensure(ctx, S.result, 16));
+    // the planned walks' lists (k_pms_plan): per round, two lane-group classes of paths, and (path, chunk)
+    // items of any phase (at most the round's prop items + one per path)
+    {
+        const int R = f.nrounds;
+        std::vector<int32_t> pb(std::max(R, 1), 0), ib(std::max(R, 1), 0);
+        for (int r = 0; r < R; ++r) {
+            pb[r] = f.rt_path[(size_t)r * (K + 1)];
+            ib[r] = f.rt_item[(size_t)r * (K + 1)] + f.rt_path[(size_t)r * (K + 1)];
+        }
+        CHECK(upload_vec(ctx, S.plan_base, pb));
+        CHECK(upload_vec(ctx, S.plan_ibase, ib));
+        CHECK(ensure(ctx, S.plan_cnt, (size_t)std::max(R, 1) * PMS_NCLS * 4));
+        CHECK(ensure(ctx, S.plan_path, (size_t)std::max<size_t>(f.paths.size(), 1) * (PMS_NCLS - 1) * 4));
+        CHECK(ensure(ctx, S.plan_item, (size_t)std::max<size_t>(f.items.size() + f.paths.size(), 1) * sizeof(PmsItem)));
+    }
     return SM_OK;
 }
 
@@ -1621,7 +1640,14 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.cuts = P<PmsCut>(S.cuts);
     d.reps = P<PmsRep>(S.reps);
     d.cut_bak = P<long long>(S.cut_bak);
+    d.plan_cnt = P<int32_t>(S.plan_cnt);
+    d.plan_path = P<int32_t>(S.plan_path);
+    d.plan_item = P<PmsItem>(S.plan_item);
+    d.plan_base = P<int32_t>(S.plan_base);
+    d.plan_ibase = P<int32_t>(S.plan_ibase);
+    d.npaths_total = (int)S.f.paths.size();
     d.Abak = P<double>(S.Abak);
+    d.rep_flag = P<uint32_t>(S.rep_flag);
     d.piece = S.f.piece;
     d.hi_bak = 0;
     d.W = ctx->W;
@@ -1651,21 +1677,55 @@ long long pms_big_tree() {
 // One phase (0: propagation, 1: refinement) of trees [t_lo, t_hi) over the whole GPU: the data terms
 // into the A rows, the up rounds deepest first, the cut paths' pieces repaired after each round, the cut paths' A_up rows saved, the
 // down rounds root first (repaired likewise), then the per-pixel update.
-sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, int phase, int t_lo, int t_hi) {
+sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int phase, int t_lo, int t_hi) {
     const PmsForest& f = ctx->pms[v].f;
+    // the phase's A rows packed by its proposal counts (k_pms_layout; SM_PMS_STATIC_ROWS=1: the static
+    // max-degree layout, A/B)
+    PmsDev d = d0;
+    if (!(getenv("SM_PMS_STATIC_ROWS") && atoi(getenv("SM_PMS_STATIC_ROWS")) == 1)) {
+        HIPC(launch_pms_layout(st, d0, phase, t_lo, t_hi, P<int32_t>(ctx->pms[v].pt_ph), P<long long>(ctx->pms[v].ab_ph)));
+        d.tree_pt = P<int32_t>(ctx->pms[v].pt_ph);
+        d.tree_abase = P<long long>(ctx->pms[v].ab_ph);
+    }
     const size_t K1 = (size_t)f.K + 1;
     int R = 0;
     for (int t = t_lo; t < t_hi; ++t) R = std::max(R, f.tree_rounds[t]);
     const std::vector<int32_t>& rt = phase == 0 ? f.rt_item : f.rt_path;
     HIPC(launch_pms_cost(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
+    const bool wave_walk = getenv("SM_PMS_WAVE_WALK") && atoi(getenv("SM_PMS_WAVE_WALK")) == 1;
+    // planned walks (k_pms_plan / k_pms_walk_plan): the round's paths in lane-group classes by their
+    // tree's proposal count, over a persistent grid of at most PMS_WALK_WAVES waves; SM_PMS_WAVE_WALK=1:
+    // one wave per (path, 64-proposal chunk) item, the round-3 walker (A/B)
+    constexpr int PMS_WALK_WAVES = 16384;
+    std::vector<int> bound(std::max(R, 1), 0);
+    if (!wave_walk) {
+        int maxp = 0;
+        for (int r = 0; r < R; ++r) {
+            const int np = f.rt_path[r * K1 + t_hi] - f.rt_path[r * K1 + t_lo];
+            maxp = std::max(maxp, np);
+            // virtual tasks: at most one per path of the classes, plus the chunks of the rest
+            bound[r] = std::min(PMS_WALK_WAVES, np + (phase == 0 ? rt[r * K1 + t_hi] - rt[r * K1 + t_lo] : 0));
+        }
+        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp));
+    }
+    // pieces: every guessed piece repairs at once, then a gated sequential pass (SM_PMS_SEQ_REPAIR=1: the
+    // sequential pass alone, A/B); maxp[r] = the most pieces of a cut repaired in round r
+    const bool seq_repair = getenv("SM_PMS_SEQ_REPAIR") && atoi(getenv("SM_PMS_SEQ_REPAIR")) == 1;
+    std::vector<int> maxp(std::max(R, 1), 0);
+    if (!seq_repair)
+        for (int r = 0; r < R; ++r)
+            for (int k = f.rt_rep[r * K1 + t_lo]; k < f.rt_rep[r * K1 + t_hi]; ++k)
+                maxp[r] = std::max(maxp[r], f.cuts[f.reps[k].cut].npieces);
     for (int r = R - 1; r >= 0; --r) {
-        HIPC(launch_pms_walk(st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        HIPC(launch_pms_repair(st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
+        if (wave_walk) HIPC(launch_pms_walk(st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
+        else HIPC(launch_pms_walk_plan(st, d, phase, true, r, bound[r]));
+        HIPC(launch_pms_repair(st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
     }
     HIPC(launch_pms_cut_backup(st, d, f.tree_cut[t_lo], f.tree_cut[t_hi]));
     for (int r = 0; r < R; ++r) {
-        HIPC(launch_pms_walk(st, d, phase, false, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        HIPC(launch_pms_repair(st, d, phase, false, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi]));
+        if (wave_walk) HIPC(launch_pms_walk(st, d, phase, false, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
+        else HIPC(launch_pms_walk_plan(st, d, phase, false, r, bound[r]));
+        HIPC(launch_pms_repair(st, d, phase, false, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
     }
     HIPC(launch_pms_update(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
     return SM_OK;
@@ -1690,6 +1750,12 @@ sm_status pms_serial_range(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, 
         }
         if (t < t1 && !is_big) continue;
         HIPC(launch_pms_serial(st, d, run, t));
+        if (pms_dedupe() && t > run) {  // the run's distinct propagation counts (nprop: k_pms_count's input)
+            PmsDev dd = d;
+            dd.labu = P<float4>(ctx->pms[v].labu);
+            dd.nprop = P<int32_t>(ctx->pms[v].nprop);
+            HIPC(launch_pms_prop_dedupe(st, dd, run, t));
+        }
         run = t + 1;
         if (t == t1) break;
         const int deg = f.nb_start[t + 1] - f.nb_start[t];
@@ -1794,8 +1860,17 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     st = sm_pms_stats{};
     st.iters = iters;
     const double t0 = now_ms();
-    // 1. the forests: the reference's order-dependent segmentation (c = +inf: the MST) on the host
-    CHECK(stage_segment(ctx, 3, p->c, p->min_size));
+    // the rand() stream's skip over random_rgb's 3 draws per pixel of both views does not depend on the
+    // forests: it runs on a thread of its own from the start (the calls' values are drawn after step 2)
+    GlibcRandom grnd;
+    std::thread skip([&grnd, N] { grnd.seed_skip(1u, (long)(6 * N)); });
+    // 1. the forests: the reference's order-dependent segmentation (c = +inf: the MST)
+    const sm_status seg_st = stage_segment(ctx, 3, p->c, p->min_size);
+    if (seg_st != SM_OK) {
+        skip.join();
+        return seg_st;
+    }
+    st.prep_seg_ms = now_ms() - t0;
     // 2. reference-numbered forests and walk schedules, both views in parallel
     {
         auto build = [ctx, W, H, N](int v) {
@@ -1807,17 +1882,18 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
             pms_build_forest(W, H, ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), mR.data(), mD.data(), ctx->pms[v].f,
                              pms_piece());
         };
+        const double tf = now_ms();
         std::thread other(build, 1);
         build(0);
         other.join();
+        st.prep_forest_ms = now_ms() - tf;
     }
     // 3. random streams: the replayed dice prefix, the rand() values of every call (after random_rgb's
     // 3 draws per pixel of both views), the initial labels (one stream, so both views start equal)
     const int K0 = ctx->pms[0].f.K, K1 = ctx->pms[1].f.K;
     ctx->pms_hrnd.resize((size_t)iters * (K0 + K1) + 1);
-    std::thread rng([ctx, iters, K0, K1, N] {
-        sm_pms_glibc_random(1u, (long)(6 * N), (long)iters * (K0 + K1), ctx->pms_hrnd.data());
-    });
+    skip.join();
+    std::thread rng([ctx, iters, K0, K1, &grnd] { grnd.draw((long)iters * (K0 + K1), ctx->pms_hrnd.data()); });
     if (ctx->pms_init_key[0] != W || ctx->pms_init_key[1] != H || ctx->pms_init_key[2] != D) {
         ctx->pms_init.resize(3 * N);
         sm_pms_init_labels(W, H, D, ctx->pms_init.data());
@@ -1879,6 +1955,8 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     run[0].h_res = ctx->h_pms_res;
     run[1].h_res = ctx->h_pms_res + 4;
     const size_t roff0[2] = {0, (size_t)iters * K0};
+    // evaluations the device ran (speculation and repeats included): a diagnostic, SM_PMS_COUNT_RUN=1
+    static const bool count_run = getenv("SM_PMS_COUNT_RUN") && atoi(getenv("SM_PMS_COUNT_RUN")) == 1;
     auto calls = [ctx, D, iters, serial_only, &roff0](PmsRun& r, int v) -> sm_status {
         HIPC(hipSetDevice(ctx->device));
         const hipStream_t st = r.st;
@@ -1891,7 +1969,7 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
         for (int i = 0; i < iters; ++i) {
             const double a = now_ms();
             d.rnd = P<int32_t>(ctx->pms_rnd) + roff;
-            d.evals = acc + (i == 0 ? 4 : 5);
+            d.evals = count_run ? acc + (i == 0 ? 4 : 5) : nullptr;
             roff += (size_t)K;
             if (d.prof) HIPC(hipMemsetAsync(d.prof, 0, 16 * 8, st));
             if (i == 0 || serial_only) {
@@ -1921,7 +1999,11 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
             } else {
                 CHECK(pms_speculative_call(ctx, r, v, d));
             }
-            HIPC(launch_pms_count(st, d, acc + (i == 0 ? 0 : 2)));
+            {  // the call's node-label evaluations (a speculative call with the dedupe: nprop holds the counts)
+                PmsDev dc = d;
+                dc.nprop = (i > 0 && !serial_only && pms_dedupe()) ? P<int32_t>(ctx->pms[v].nprop) : nullptr;
+                HIPC(launch_pms_count(st, dc, acc + (i == 0 ? 0 : 2)));
+            }
             HIPC(hipStreamSynchronize(st));
             const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE);
             if (e & 6u) {
@@ -2160,7 +2242,9 @@ void sm_destroy(sm_ctx* ctx) {
         DevBuf* pb[] = {&S.rows, &S.rtree, &S.paths, &S.items, &S.rt_path, &S.rt_item, &S.tree_rounds, &S.tree_start,
                         &S.bfs_pix, &S.nb_start, &S.nb, &S.tree_pt, &S.tree_abase, &S.tree_lab, &S.nref, &S.lab, &S.labq,
                         &S.abc, &S.minc, &S.abc_bak, &S.minc_bak, &S.A, &S.vrows, &S.off, &S.oguess, &S.cnt, &S.flag,
-                        &S.result, &S.prof, &S.labu, &S.nprop, &S.vrows, &S.cuts, &S.reps, &S.cut_bak, &S.Abak};
+                        &S.result, &S.prof, &S.labu, &S.nprop, &S.vrows, &S.cuts, &S.reps, &S.cut_bak, &S.Abak,
+                        &S.plan_cnt, &S.plan_path, &S.plan_item, &S.plan_base, &S.plan_ibase, &S.rep_flag, &S.pt_ph,
+                        &S.ab_ph};
         for (DevBuf* b : pb) if (b->p) (void)hipFree(b->p);
     }
     if (ctx->pms_dice.p) (void)hipFree(ctx->pms_dice.p);

@@ -48,6 +48,15 @@ struct PmsDev {
     uint32_t* err;               // bit 1: a sampled index fell outside its tree; bit 2: dice stream exhausted
     long long* prof;             // SM_PMS_PROF: k_pms_serial segment totals (nullptr: off)
     unsigned long long* evals;   // node-label evaluations the per-pixel updates ran (nullptr: not counted)
+    // walk plan of one phase (k_pms_plan): per round r, the paths of trees with few proposals in lists of
+    // lane-group classes (PMS_NCLS - 1 of them: P <= 2, P <= 8) and (path, chunk) items of the others;
+    // plan_cnt[r * PMS_NCLS + c] entries at plan_path + plan_base[r] (classes) / plan_item + plan_ibase[r]
+    int32_t* plan_cnt;
+    int32_t* plan_path;          // class c of round r at plan_path + c * npaths_total + plan_base[r]
+    PmsItem* plan_item;
+    const int32_t* plan_base;    // nrounds: first path of round r (rt_path[r][0])
+    const int32_t* plan_ibase;   // nrounds: rt_item[r][0] + rt_path[r][0] (big items: chunks of any phase)
+    int npaths_total;
     const double* slut;
     const double* s2lut;
     // pieces (sm_pms_host.h PmsCut): cut paths, repair items, per-cut backup offsets into Abak (the
@@ -56,6 +65,7 @@ struct PmsDev {
     const PmsRep* reps;
     const long long* cut_bak;
     double* Abak;
+    uint32_t* rep_flag;          // per repair item: pieces whose parallel repair rewrote a boundary row (bit i)
     int W, Dv, Dmax, K, nrounds, piece;
     int hi_bak;  // 1: propagation samples higher neighbours (u > t) from abc_bak, the call's starting labels
                  // (a serial re-run in the middle of a speculative call, whose later trees keep results)
@@ -76,12 +86,24 @@ hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t);
 hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long wn);
 hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int total_deg);
 hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi);
+// lane-group classes of the planned walks: paths of trees with P <= 2 / P <= 8 proposals share a wave
+// (32 / 8 paths per wave), the rest are (path, 64-proposal chunk) items of one wave each
+#define PMS_NCLS 3
+// the phase's A-row layout of trees [t_lo, t_hi): stride P rounded up to even, packed (k_pms_layout)
+hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int32_t* pt_out,
+                             long long* ab_out);
+// the walk plan of trees [t_lo, t_hi) for a phase (plan_cnt zeroed here); r_lo..r_hi: rounds to plan
+hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths);
+// one round's planned walk, a persistent grid of `waves` waves (the host's bound on the work)
+hipError_t launch_pms_walk_plan(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int waves);
 hipError_t launch_pms_cost(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);
 hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);
 hipError_t launch_pms_ref_setup(hipStream_t st, const PmsDev& d, int t_lo);
 // pieces: re-walk the cut paths' guessed pieces from their exact neighbours (repair items [lo, hi)),
 // and save the A_up rows of cuts [c_lo, c_hi) before the down pass
-hipError_t launch_pms_repair(hipStream_t st, const PmsDev& d, int phase, bool up, int lo, int hi);
+// maxp > 0: first every guessed piece at once (k_pms_repair_par, maxp = the most pieces of a cut in the
+// range), then the sequential pass only for the items it flagged; maxp = 0: the sequential pass alone
+hipError_t launch_pms_repair(hipStream_t st, const PmsDev& d, int phase, bool up, int lo, int hi, int maxp);
 hipError_t launch_pms_cut_backup(hipStream_t st, const PmsDev& d, int c_lo, int c_hi);
 hipError_t launch_pms_validate(hipStream_t st, const PmsDev& d, int t_lo);
 hipError_t launch_pms_restore(hipStream_t st, const PmsDev& d, int row_lo, int row_hi);

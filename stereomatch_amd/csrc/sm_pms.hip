@@ -29,6 +29,7 @@
 // correctly rounded (sqrt_rn / div_rn), as x86's sqrtss / divss are.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "sm_pms.h"
@@ -151,12 +152,12 @@ __device__ __forceinline__ uint32_t meta_dw(const ChunkMeta& m, int j) {  // j w
 // tree-contiguous A rows instead of gathering from the cost volume (a dependent load per node, and
 // a TLB miss at most of them: the volume is ~1 GB).
 template <bool REPAIR, bool PRE>
-__device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phase, int t, int top, int bot, int chunk,
+__device__ bool up_walk(const PmsDev& d, const double* __restrict__ sS, int phase, int t, int top, int bot, int chunk,
                         double x0) {
     int P, base;
     phase_labels(d, phase, t, P, base);
     const int j = chunk * 64 + (int)(threadIdx.x & 63);
-    if (chunk * 64 >= P) return;
+    if (chunk * 64 >= P) return true;
     const bool act = j < P;
     float4 L = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!PRE && act) L = d.lab[base + j];
@@ -226,7 +227,7 @@ __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
             x = cost[k] + acc;  // A[v] = C + A[v] (0x40fac5); cost[k] is a float widened exactly
             if (REPAIR) {
                 const bool same = !act || __double_as_longlong(x) == __double_as_longlong(old[k]);
-                if (__all(same)) return;
+                if (__all(same)) return true;
                 if (!same) A[(size_t)(row0 + i0 - k - ts) * pt] = x;
             } else if (act) {
                 A[(size_t)(row0 + i0 - k - ts) * pt] = x;
@@ -236,6 +237,7 @@ __device__ void up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
         i0 = i0n;
         lo = lon;
     }
+    return !REPAIR;  // a repair that never agreed rewrote the head row
 }
 
 __device__ void up_item(const PmsDev& d, const double* __restrict__ sS, int phase, int path, int chunk) {
@@ -263,13 +265,13 @@ __device__ __forceinline__ void cost_row(const PmsDev& d, int row, int t, int P,
 // speculative walk overwrote them) and the walk stopping at the first all-lanes bitwise agreement.
 // The next chunk's A_up rows and weights are loaded while the current chunk runs.
 template <bool REPAIR>
-__device__ void down_walk(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
+__device__ bool down_walk(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
                           int t, int top, int bot, int chunk, double yin, const double* __restrict__ ub) {
     int P, base;
     phase_labels(d, phase, t, P, base);
     (void)base;
     const int j = chunk * 64 + (int)(threadIdx.x & 63);
-    if (chunk * 64 >= P) return;
+    if (chunk * 64 >= P) return true;
     const bool act = j < P;
     const int ts = d.tree_start[t], pt = d.tree_pt[t];
     double* __restrict__ A = d.A + d.tree_abase[t] + j;
@@ -314,7 +316,7 @@ __device__ void down_walk(const PmsDev& d, const double* __restrict__ sS, const 
             }
             if (REPAIR) {
                 const bool same = !act || __double_as_longlong(y) == __double_as_longlong(oc[k]);
-                if (__all(same)) return;
+                if (__all(same)) return true;
                 if (!same) A[(size_t)(row0 + i0 + k - ts) * pt] = y;
             } else if (act) {
                 A[(size_t)(row0 + i0 + k - ts) * pt] = y;
@@ -329,6 +331,7 @@ __device__ void down_walk(const PmsDev& d, const double* __restrict__ sS, const 
         i0 = i0n;
         n = nn;
     }
+    return !REPAIR;  // a repair that never agreed rewrote the bottom row
 }
 
 __device__ void down_item(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
@@ -556,12 +559,29 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
     // the previous links' traffic)
     float* sdd = gsm;
     int* sdeg = reinterpret_cast<int*>(gsm + nt);
-    long long* sog = reinterpret_cast<long long*>(gsm + 2 * ((nt + 1) & ~1));
+    long long* sog = reinterpret_cast<long long*>(gsm + ((3 * nt + 1) & ~1));
     float* sdice = reinterpret_cast<float*>(sog + nt);
     if (STAGED) {
+        // Per tree, in parallel: each refinement level's range test rd = fmaf(dice, max_d, dd) is monotone in
+        // the draw (dice in [-1, 1], one rounding), so a level whose two extreme rd are both in [0, Dmax] is
+        // in range whatever it draws (4 draws), one whose extremes are both below 0 or both above Dmax is out
+        // (1 draw); only the others read the stream.  sdeg holds the degree and the level classes, 2 bits
+        // per level (1 always in, 0 always out, 2 draw-dependent).  The serial chain then reads one LDS
+        // word per draw-dependent level instead of one per level: the same offsets as ref_count.
+        const float fmax = (float)d.Dmax;
         for (int i = tid; i < nt; i += blockDim.x) {
-            sdd[i] = ref_dd(d, t_lo + i);
-            sdeg[i] = tree_deg(d, t_lo + i);
+            const float dd = ref_dd(d, t_lo + i);
+            sdd[i] = dd;
+            uint32_t cls = 0;
+            int l = 0;
+            for (float md = 0.5f * fmax; md > 0.1f; md *= 0.5f, ++l) {
+                const float lo = fmaf(-1.0f, md, dd), hi = fmaf(1.0f, md, dd);
+                const bool lo_in = !(lo < 0.0f || lo > fmax), hi_in = !(hi < 0.0f || hi > fmax);
+                const uint32_t c = (lo_in && hi_in) ? 1u : (hi < 0.0f || lo > fmax) ? 0u : 2u;
+                cls |= c << (2 * l);
+            }
+            sdeg[2 * i] = tree_deg(d, t_lo + i);
+            sdeg[2 * i + 1] = (int)cls;
         }
         for (long long i = tid; i < wn; i += blockDim.x) sdice[i] = o0 + i < d.dice_n ? d.dice[o0 + i] : 0.0f;
         __syncthreads();
@@ -569,8 +589,24 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
             long long o = o0;
             for (int t = 0; t < nt; ++t) {
                 sog[t] = o;
-                const int deg = sdeg[t];
-                o += deg + ref_count(d, sdd[t], o + deg, [&](long long k) { return sdice[k - o0]; });
+                const int deg = sdeg[2 * t];
+                uint32_t cls = (uint32_t)sdeg[2 * t + 1];
+                const float dd = sdd[t];
+                long long k = o + deg;
+                for (float md = 0.5f * fmax; md > 0.1f; md *= 0.5f, cls >>= 2) {  // ref_count's levels
+                    if (k + 4 > d.dice_n) {
+                        atomicOr(d.err, 4u);
+                        break;
+                    }
+                    const uint32_t c = cls & 3u;
+                    bool in = c == 1u;
+                    if (c == 2u) {
+                        const float rd = fmaf(sdice[k - o0], md, dd);
+                        in = !(rd < 0.0f || rd > fmax);
+                    }
+                    k += in ? 4 : 1;
+                }
+                o = k;
             }
         }
         __syncthreads();
@@ -684,14 +720,297 @@ __global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, i
     else down_item(d, sS, sS2, phase, path, chunk);
 }
 
+// ----------------------------------------------------------------------------- per-phase layout
+// The A rows of a phase hold its P proposals per node.  The static layout (tree_pt / tree_abase) has
+// room for the most a tree can have (max(deg, L) + 1: the first call's propagation), but a later call's
+// propagation keeps a handful of distinct labels per tree (C2: ~2 on average), so its rows were mostly
+// air: the big tree's 618k rows at 238 doubles spread a phase over 1.2 GB.  k_pms_layout packs the
+// phase's rows with a stride of P rounded up to even (16-byte rows), per tree an exclusive scan of
+// size x stride, into pt_out / ab_out, which the phase's kernels then take as tree_pt / tree_abase.
+// A rows are scratch of one phase (the outputs are minc and abc), so each phase may lay them out anew.
+__global__ void __launch_bounds__(1024) k_pms_layout(PmsDev d, int phase, int t_lo, int t_hi, int32_t* pt_out,
+                                                     long long* ab_out) {
+    __shared__ long long s_w[16];
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    long long base = 0;
+    for (int t0 = t_lo; t0 < t_hi; t0 += 1024) {
+        const int t = t0 + tid;
+        long long v = 0;
+        int stride = 2;
+        if (t < t_hi) {
+            int P, lb;
+            phase_labels(d, phase, t, P, lb);
+            stride = P > 2 ? (P + 1) & ~1 : 2;
+            v = (long long)(d.tree_start[t + 1] - d.tree_start[t]) * stride;
+        }
+        long long incl = v;
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            const long long u = __shfl_up(incl, k);
+            if (lane >= k) incl += u;
+        }
+        if (lane == 63) s_w[wv] = incl;
+        __syncthreads();
+        long long pre = 0, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            if (k < wv) pre += s_w[k];
+            tot += s_w[k];
+        }
+        if (t < t_hi) {
+            pt_out[t] = stride;
+            ab_out[t] = base + pre + incl - v;
+        }
+        base += tot;
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------------- planned walks
+// In the later (speculative) calls the propagation dedupe leaves a tree only a few distinct labels (C2:
+// ~2.4 node-label evaluations per node and call over both phases), yet a wave per (path, 64-proposal
+// chunk) walks every path: up to 350k waves per round for a handful of active lanes each.  The plan
+// (k_pms_plan) sorts a round's paths by their tree's proposal count P into lane-group classes, and the
+// walk kernel (k_pms_walk_plan, a persistent grid) lets GW lanes walk one path: lane j of the group
+// evaluates proposal j < P, so one wave walks 64 / GW paths.  Paths with P > 8 keep the wave walker
+// (up_walk / down_walk, one wave per 64-proposal chunk).  Each lane performs exactly the wave walker's
+// operations on its (path, proposal) -- the same fma order, the same guesses at cut pieces -- so the A
+// rows are bitwise the same whichever walker ran.
+constexpr int PMS_GCH = 4;  // nodes whose loads a group walker issues together
+
+__device__ __forceinline__ int pms_class_gw(int c) { return c == 0 ? 2 : 8; }
+__device__ __forceinline__ int pms_class_of(int P) { return P <= 2 ? 0 : P <= 8 ? 1 : 2; }
+
+// the up-walk fields of row r: words 2..9 of the PmsRow (children, w | nch | hk, child weights, x | y)
+struct GMeta {
+    uint2 c01, c23, w6, w8;
+};
+__device__ __forceinline__ GMeta gmeta_load(const PmsRow* rows, int r) {
+    const uint2* b = reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(rows + r) + 2);
+    GMeta m;
+    m.c01 = b[0];
+    m.c23 = b[1];
+    m.w6 = b[2];
+    m.w8 = b[3];
+    return m;
+}
+
+// Leaf->root walk of path `path` (rows [row, row + len), bottom to head, from x = 0 below the bottom: a
+// leaf, or a cut piece's guess) for proposal j of the lane's group; the up_walk<false, true> recurrence
+// per lane.  Chunks of PMS_GCH nodes: a chunk's child and cost rows are loaded together, its successor's
+// metadata behind them.
+template <int GW>
+__device__ void up_group(const PmsDev& d, const double* __restrict__ sS, int phase, int path) {
+    const int j = (int)(threadIdx.x & 63) % GW;
+    int P = 0, base = 0, t = 0, r0 = 0, len = 0;
+    if (path >= 0) {
+        const PmsPath pa = d.paths[path];
+        t = pa.tree;
+        r0 = pa.row;
+        len = pa.len;
+        phase_labels(d, phase, t, P, base);
+    }
+    if (j >= P) return;
+    const int ts = d.tree_start[t], pt = d.tree_pt[t];
+    double* __restrict__ A = d.A + d.tree_abase[t] + j;
+    double x = 0.0;
+    int i0 = len - 1;
+    GMeta mc[PMS_GCH];
+#pragma unroll
+    for (int k = 0; k < PMS_GCH; ++k) mc[k] = gmeta_load(d.rows, r0 + (i0 - k >= 0 ? i0 - k : 0));
+    while (i0 >= 0) {
+        const int n = i0 + 1 < PMS_GCH ? i0 + 1 : PMS_GCH;
+        double cv[PMS_GCH][4], cost[PMS_GCH];
+#pragma unroll
+        for (int k = 0; k < PMS_GCH; ++k) {
+            const int row = r0 + i0 - (k < n ? k : 0);
+            const int nch = (int)((mc[k].w6.x >> 16) & 255u), hk = (int)(mc[k].w6.x >> 24);
+            const uint32_t ch[4] = {mc[k].c01.x, mc[k].c01.y, mc[k].c23.x, mc[k].c23.y};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int crow = (q < nch && q != hk) ? (int)ch[q] : row;
+                cv[k][q] = A[(size_t)(crow - ts) * pt];
+            }
+            cost[k] = A[(size_t)(row - ts) * pt];
+        }
+        const int i0n = i0 - n;
+        GMeta mn[PMS_GCH];
+#pragma unroll
+        for (int k = 0; k < PMS_GCH; ++k) mn[k] = gmeta_load(d.rows, r0 + (i0n - k >= 0 ? i0n - k : 0));
+#pragma unroll
+        for (int k = 0; k < PMS_GCH; ++k) {
+            if (k >= n) break;
+            const int nch = (int)((mc[k].w6.x >> 16) & 255u), hk = (int)(mc[k].w6.x >> 24);
+            const int wc[4] = {(int)(mc[k].w6.y & 0xFFFFu), (int)(mc[k].w6.y >> 16), (int)(mc[k].w8.x & 0xFFFFu),
+                               (int)(mc[k].w8.x >> 16)};
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q >= nch) break;
+                const double v = q == hk ? x : cv[k][q];
+                acc = fma(v, sS[wc[q]], acc);  // as up_walk (0x40fad5)
+            }
+            x = cost[k] + acc;
+            A[(size_t)(r0 + i0 - k - ts) * pt] = x;
+        }
+#pragma unroll
+        for (int k = 0; k < PMS_GCH; ++k) mc[k] = mn[k];
+        i0 = i0n;
+    }
+}
+
+// Root->leaf walk of path `path`, head to bottom, A(c) = fma(S_c, A(p), S2_c * A_up(c)) per lane (the
+// down_walk<false> recurrence); the next chunk's A_up rows and weights are loaded while one runs.
+template <int GW>
+__device__ void down_group(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
+                           int path) {
+    const int j = (int)(threadIdx.x & 63) % GW;
+    int P = 0, base = 0, t = 0, r0 = 0, len = 0;
+    if (path >= 0) {
+        const PmsPath pa = d.paths[path];
+        t = pa.tree;
+        r0 = pa.row;
+        len = pa.len;
+        phase_labels(d, phase, t, P, base);
+    }
+    if (j >= P) return;
+    const int ts = d.tree_start[t], pt = d.tree_pt[t];
+    double* __restrict__ A = d.A + d.tree_abase[t] + j;
+    const int parent = d.rows[r0].parent;
+    double y = parent >= 0 ? A[(size_t)(parent - ts) * pt] : 0.0;
+    auto ld = [&](double (&u)[PMS_GCH], int (&w)[PMS_GCH], int i0) {
+#pragma unroll
+        for (int k = 0; k < PMS_GCH; ++k) {
+            const int i = i0 + k < len ? i0 + k : 0;  // clamped: every load from a valid row
+            u[k] = A[(size_t)(r0 + i - ts) * pt];
+            w[k] = (int)(d.rows[r0 + i].w);
+        }
+    };
+    double uc[PMS_GCH];
+    int wc[PMS_GCH];
+    ld(uc, wc, 0);
+    for (int i0 = 0; i0 < len; i0 += PMS_GCH) {
+        double un[PMS_GCH];
+        int wn[PMS_GCH];
+        ld(un, wn, i0 + PMS_GCH);
+#pragma unroll
+        for (int k = 0; k < PMS_GCH; ++k) {
+            if (i0 + k >= len) break;
+            const double S = sS[wc[k]], S2 = sS2[wc[k]];
+            if (i0 + k == 0) y = parent >= 0 ? fma(S, y, S2 * uc[0]) : uc[0];
+            else y = fma(S, y, S2 * uc[k]);
+            A[(size_t)(r0 + i0 + k - ts) * pt] = y;
+        }
+#pragma unroll
+        for (int k = 0; k < PMS_GCH; ++k) {
+            uc[k] = un[k];
+            wc[k] = wn[k];
+        }
+    }
+}
+
+// The plan of trees [t_lo, t_hi) for one phase: blockIdx.y = round r, one thread per path of the round.
+// A path of at least PMS_GLONG rows goes to the wave walker whatever its P: its walk is a latency chain,
+// and the wave walker issues PMS_CH nodes per memory round trip against the group walker's PMS_GCH.
+constexpr int PMS_GLONG = 48;
+
+__global__ void __launch_bounds__(1024) k_pms_plan(PmsDev d, int phase, int t_lo, int t_hi) {
+    __shared__ int s_n[PMS_NCLS], s_base[PMS_NCLS];
+    const int r = (int)blockIdx.y, K1 = d.K + 1;
+    const int p0 = d.rt_path[(size_t)r * K1 + t_lo], p1 = d.rt_path[(size_t)r * K1 + t_hi];
+    const int p = p0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int lane = (int)(threadIdx.x & 63);
+    if (threadIdx.x < PMS_NCLS) s_n[threadIdx.x] = 0;
+    __syncthreads();
+    int P = 0, base = 0, len = 0;
+    if (p < p1) {
+        const PmsPath pa = d.paths[p];
+        len = pa.len;
+        phase_labels(d, phase, pa.tree, P, base);
+    }
+    const int c = P <= 0 ? -1 : len >= PMS_GLONG ? PMS_NCLS - 1 : pms_class_of(P);
+    const int nchunk = c == PMS_NCLS - 1 ? (P + 63) / 64 : 1;
+    // block-aggregated appends: wave offsets in LDS, one global atomic per class and block
+    int wpos[PMS_NCLS];
+#pragma unroll
+    for (int k = 0; k < PMS_NCLS; ++k) {
+        const unsigned long long m = __ballot(c == k);
+        int cnt_w = 0, pre = 0;
+        if (k < PMS_NCLS - 1) {
+            cnt_w = __popcll(m);
+            pre = __popcll(m & ((1ull << lane) - 1ull));
+        } else {  // chunks: an exclusive wave scan of nchunk over the lanes of class k
+            int v = c == k ? nchunk : 0, incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            pre = incl - v;
+            cnt_w = __shfl(incl, 63);
+        }
+        int wb = 0;
+        if (lane == 0 && cnt_w) wb = atomicAdd(&s_n[k], cnt_w);
+        wpos[k] = __shfl(wb, 0) + pre;
+    }
+    __syncthreads();
+    if (threadIdx.x < PMS_NCLS) s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(d.plan_cnt + r * PMS_NCLS + threadIdx.x, s_n[threadIdx.x]) : 0;
+    __syncthreads();
+    if (c < 0) return;
+    const int pos = s_base[c] + wpos[c];
+    if (c < PMS_NCLS - 1) {
+        d.plan_path[(size_t)c * d.npaths_total + d.plan_base[r] + pos] = p;
+    } else {
+        for (int k = 0; k < nchunk; ++k) d.plan_item[d.plan_ibase[r] + pos + k] = PmsItem{p, k};
+    }
+}
+
+// One round's planned walk over a persistent grid: wave w takes virtual tasks w, w + waves, ...: first
+// the class-0 waves (32 paths each), then class 1 (8 paths each), then one (path, chunk) item each.
+__global__ void __launch_bounds__(256) k_pms_walk_plan(PmsDev d, int phase, int up, int r) {
+    __shared__ double sS[PMS_NW], sS2[PMS_NW];
+    for (int i = threadIdx.x; i < PMS_NW; i += blockDim.x) {
+        sS[i] = d.slut[i];
+        sS2[i] = d.s2lut[i];
+    }
+    __syncthreads();
+    const int* cnt = d.plan_cnt + r * PMS_NCLS;
+    const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
+    const int T0 = (n0 + 31) / 32, T1 = (n1 + 7) / 8, T = T0 + T1 + n2;
+    const int lane = (int)(threadIdx.x & 63);
+    const int nw = (int)(gridDim.x * (blockDim.x >> 6));
+    for (int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); w < T; w += nw) {
+        if (w < T0) {
+            const int k = w * 32 + lane / 2;
+            const int path = k < n0 ? d.plan_path[d.plan_base[r] + k] : -1;
+            if (up) up_group<2>(d, sS, phase, path);
+            else down_group<2>(d, sS, sS2, phase, path);
+        } else if (w < T0 + T1) {
+            const int k = (w - T0) * 8 + lane / 8;
+            const int path = k < n1 ? d.plan_path[(size_t)d.npaths_total + d.plan_base[r] + k] : -1;
+            if (up) up_group<8>(d, sS, phase, path);
+            else down_group<8>(d, sS, sS2, phase, path);
+        } else {
+            const PmsItem it = d.plan_item[d.plan_ibase[r] + (w - T0 - T1)];
+            if (up) up_item(d, sS, phase, uni(it.path), uni(it.chunk));
+            else down_item(d, sS, sS2, phase, uni(it.path), uni(it.chunk));
+        }
+    }
+}
+
 // Pieces (sm_pms_host.h PmsCut): one wave per repair item (cut path, chunk) re-walks the guessed
 // pieces in dependency order from their exact neighbours -- up: from the piece above the exact bottom
 // piece to the head; down: from the piece below the exact head piece to the bottom.
-__global__ void __launch_bounds__(256) k_pms_repair(PmsDev d, int phase, int up, int lo, int hi) {
+// gated (the parallel repair ran first): only items whose flag word is set -- a piece's repair rewrote
+// the boundary row its neighbour had started from -- run, and clear the word
+__global__ void __launch_bounds__(256) k_pms_repair(PmsDev d, int phase, int up, int lo, int hi, int gated) {
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
     load_luts(d, sS, sS2);
     const int it = lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     if (it >= hi) return;
+    if (gated) {
+        if (uni(d.rep_flag[it]) == 0) return;
+        if ((threadIdx.x & 63) == 0) d.rep_flag[it] = 0;
+    }
     const PmsRep rp = d.reps[it];
     const PmsCut c = d.cuts[uni(rp.cut)];
     const int t = uni(c.tree), Pn = d.piece, np = uni(c.npieces), row = uni(c.row), len = uni(c.len);
@@ -716,6 +1035,46 @@ __global__ void __launch_bounds__(256) k_pms_repair(PmsDev d, int phase, int up,
             down_walk<true>(d, sS, sS2, phase, t, top, bot, rp.chunk, y0, ub + (size_t)(top - row - Pn) * pt);
         }
     }
+}
+
+// Parallel repair: one wave per (repair item, piece): every guessed piece re-walks at once from its
+// neighbour's boundary row as the speculative walk left it -- up: the head row of the piece below, down:
+// the bottom row of the piece above.  That row is usually exact already: the neighbour's own guess error
+// has decayed within its >= 512 rows.  A piece whose repair reaches its far end without agreeing has
+// rewritten that boundary row, so its neighbour may have started from a stale value: the item's flag word
+// gets the piece's bit, and the gated sequential repair (k_pms_repair) redoes that item in order.
+__global__ void __launch_bounds__(256) k_pms_repair_par(PmsDev d, int phase, int up, int lo, int hi, int maxp) {
+    __shared__ double sS[PMS_NW], sS2[PMS_NW];
+    load_luts(d, sS, sS2);
+    const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int it = lo + g / maxp, i = g % maxp;
+    if (it >= hi) return;
+    const PmsRep rp = d.reps[it];
+    const PmsCut c = d.cuts[uni(rp.cut)];
+    const int t = uni(c.tree), Pn = d.piece, np = uni(c.npieces), row = uni(c.row), len = uni(c.len);
+    int P, base;
+    phase_labels(d, phase, t, P, base);
+    const int j = uni(rp.chunk) * 64 + (int)(threadIdx.x & 63);
+    if (uni(rp.chunk) * 64 >= P) return;
+    const bool act = j < P;
+    const int ts = d.tree_start[t], pt = d.tree_pt[t];
+    const double* A = d.A + d.tree_abase[t] + j;
+    bool ok;
+    if (up) {
+        if (i > np - 2) return;  // the bottom piece (np - 1) starts from the path's leaf: exact
+        const int top = row + i * Pn, bot = top + Pn - 1;
+        const double x0 = act ? A[(size_t)(bot + 1 - ts) * pt] : 0.0;
+        ok = up_walk<true, false>(d, sS, phase, t, top, bot, rp.chunk, x0);
+    } else {
+        if (i < 1 || i >= np) return;  // the head piece (0) starts from the path's exact parent
+        const double* ub = d.Abak + d.cut_bak[uni(rp.cut)];
+        const int top = row + i * Pn, bot = i + 1 < np ? top + Pn - 1 : row + len - 1;
+        const double y0 = act ? A[(size_t)(top - 1 - ts) * pt] : 0.0;
+        ok = down_walk<true>(d, sS, sS2, phase, t, top, bot, rp.chunk, y0, ub + (size_t)(top - row - Pn) * pt);
+    }
+    // the far boundary changed: the neighbour that read it (up: piece i - 1, down: i + 1) may be stale
+    const bool neighbour = up ? i > 0 : i + 1 < np;
+    if (!ok && neighbour && (threadIdx.x & 63) == 0) atomicOr(&d.rep_flag[it], 1u << (i & 31));
 }
 
 // A_up rows of the non-head pieces of cuts [c_lo, c_hi) -> Abak (blockIdx.y = cut - c_lo)
@@ -744,11 +1103,16 @@ __global__ void __launch_bounds__(256) k_pms_update(PmsDev d, int phase, int row
         phase_labels(d, phase, t, P, lb);
     }
     const bool wide = valid && P > 16;
-    if (d.evals) {  // the wave's node-label evaluations
+    if (d.evals) {  // node-label evaluations: one atomic per block (same-address atomics serialise in L2)
+        __shared__ int s_sum;
+        if (threadIdx.x == 0) s_sum = 0;
+        __syncthreads();
         int sum = valid ? P : 0;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
-        if (lane == 0 && sum) atomicAdd(d.evals, (unsigned long long)sum);
+        if (lane == 0 && sum) atomicAdd(&s_sum, sum);
+        __syncthreads();
+        if (threadIdx.x == 0 && s_sum) atomicAdd(d.evals, (unsigned long long)s_sum);
     }
     if (valid && !wide) update_row(d, phase, row, t);
     unsigned long long m = __ballot(wide);
@@ -815,25 +1179,51 @@ __global__ void k_pms_flags(PmsDev d, int t_lo) {
     d.flag[t] = f;
 }
 
-__global__ void k_pms_scan(PmsDev d, int t_lo) {
-    if (threadIdx.x != 0) return;
+// One workgroup, 1024 trees per step: the exact offsets are the running offset plus an exclusive scan of
+// the counts; the first tree whose guess differs or whose flag is set (a block minimum) ends the scan.
+__global__ void __launch_bounds__(1024) k_pms_scan(PmsDev d, int t_lo) {
+    __shared__ long long s_w[16];
+    __shared__ int s_first;
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
     long long o = d.off[0];
-    int t = t_lo;
-    int why = 0;
-    for (; t < d.K; ++t) {
-        if (d.oguess[t] != o) {
-            why = 1;  // wrong offset: every later tree drew from the wrong place too
-            break;
+    for (int t0 = t_lo; t0 < d.K; t0 += 1024) {
+        const int t = t0 + tid;
+        const long long c = t < d.K ? (long long)d.cnt[t] : 0;
+        long long incl = c;  // wave inclusive scan, then across the 16 waves
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            const long long v = __shfl_up(incl, k);
+            if (lane >= k) incl += v;
         }
-        if (d.flag[t]) {
-            why = 2;  // stale propagation inputs only: later trees may still be exact
-            break;
+        if (lane == 63) s_w[wv] = incl;
+        if (tid == 0) s_first = INT_MAX;
+        __syncthreads();
+        long long pre = 0;
+        for (int k = 0; k < wv; ++k) pre += s_w[k];
+        const long long ex = o + pre + incl - c;  // the exact offset of tree t
+        int why = 0;
+        if (t < d.K) why = d.oguess[t] != ex ? 1 : d.flag[t] ? 2 : 0;
+        if (why) atomicMin(&s_first, t);
+        __syncthreads();
+        const int first = s_first;
+        if (first != INT_MAX) {
+            if (t == first) {
+                d.result[0] = t;
+                d.result[1] = why;  // 1: wrong offset (every later tree drew from the wrong place); 2: stale inputs only
+                *reinterpret_cast<long long*>(d.result + 2) = ex;
+            }
+            return;
         }
-        o += d.cnt[t];
+        long long tot = 0;
+        for (int k = 0; k < 16; ++k) tot += s_w[k];
+        o += tot;
+        __syncthreads();
     }
-    d.result[0] = t;
-    d.result[1] = why;
-    *reinterpret_cast<long long*>(d.result + 2) = o;  // the exact offset of tree t
+    if (tid == 0) {
+        d.result[0] = d.K;
+        d.result[1] = 0;
+        *reinterpret_cast<long long*>(d.result + 2) = o;
+    }
 }
 
 __global__ void k_pms_restore(PmsDev d, int row_lo, int row_hi) {
@@ -895,7 +1285,9 @@ __global__ void __launch_bounds__(256) k_pms_count(PmsDev d, unsigned long long*
     const int lane = (int)(threadIdx.x & 63);
     const int deg = tree_deg(d, t), base = d.tree_lab[t];
     int n = 0;
-    for (int j0 = 0; j0 < deg; j0 += 64) {
+    // a speculative call leaves every tree's distinct count in nprop (k_pms_prop_dedupe ran on the exact
+    // labels of every tree: the validated pass or the tree's serial re-run)
+    for (int j0 = d.nprop ? deg : 0; j0 < deg; j0 += 64) {
         const int j = j0 + lane;
         bool keep = false;
         if (j < deg) {
@@ -909,6 +1301,7 @@ __global__ void __launch_bounds__(256) k_pms_count(PmsDev d, unsigned long long*
         }
         n += __popcll(__ballot(keep));
     }
+    if (d.nprop) n = d.nprop[t];
     if (lane == 0) {
         const unsigned long long sz = (unsigned long long)(d.tree_start[t + 1] - d.tree_start[t]);
         const unsigned long long nr = (unsigned long long)d.nref[t];
@@ -943,7 +1336,7 @@ hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long
     // reads past the window; otherwise (too many trees / draws for the LDS) it reads global memory
     const size_t nt = (size_t)(d.K - t_lo);
     constexpr size_t cap = 150 * 1024;  // LDS bytes
-    const size_t lds = 4 * 2 * ((nt + 1) & ~(size_t)1) + 8 * nt + 4 * (size_t)wn;
+    const size_t lds = 4 * ((3 * nt + 1) & ~(size_t)1) + 8 * nt + 4 * (size_t)wn;
     static const hipError_t attr =  // once per process (thread-safe static initialisation)
         hipFuncSetAttribute((const void*)k_pms_guess<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap);
     if (attr != hipSuccess) return attr;
@@ -974,6 +1367,28 @@ hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, 
     return hipGetLastError();
 }
 
+hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int32_t* pt_out,
+                             long long* ab_out) {
+    if (t_hi <= t_lo) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_layout, dim3(1), dim3(1024), 0, st, d, phase, t_lo, t_hi, pt_out, ab_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths) {
+    if (t_hi <= t_lo || nrounds <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(d.plan_cnt, 0, sizeof(int32_t) * PMS_NCLS * (size_t)nrounds, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pms_plan, dim3(blocks((size_t)std::max(max_paths, 1), 1024), (unsigned)nrounds), dim3(1024), 0, st, d,
+                       phase, t_lo, t_hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_walk_plan(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int waves) {
+    if (waves <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pms_walk_plan, dim3(blocks((size_t)waves, 4)), dim3(256), 0, st, d, phase, up ? 1 : 0, r);
+    return hipGetLastError();
+}
+
 hipError_t launch_pms_cost(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi) {
     if (row_hi <= row_lo) return hipSuccess;
     hipLaunchKernelGGL(k_pms_cost, dim3(blocks((size_t)(row_hi - row_lo), 256)), dim3(256), 0, st, d, phase, row_lo, row_hi);
@@ -986,9 +1401,13 @@ hipError_t launch_pms_update(hipStream_t st, const PmsDev& d, int phase, int row
     return hipGetLastError();
 }
 
-hipError_t launch_pms_repair(hipStream_t st, const PmsDev& d, int phase, bool up, int lo, int hi) {
+hipError_t launch_pms_repair(hipStream_t st, const PmsDev& d, int phase, bool up, int lo, int hi, int maxp) {
     if (hi <= lo) return hipSuccess;
-    hipLaunchKernelGGL(k_pms_repair, dim3(blocks((size_t)(hi - lo) * 64, 256)), dim3(256), 0, st, d, phase, up ? 1 : 0, lo, hi);
+    if (maxp > 0)  // parallel over pieces, then the gated sequential pass
+        hipLaunchKernelGGL(k_pms_repair_par, dim3(blocks((size_t)(hi - lo) * maxp * 64, 256)), dim3(256), 0, st, d, phase,
+                           up ? 1 : 0, lo, hi, maxp);
+    hipLaunchKernelGGL(k_pms_repair, dim3(blocks((size_t)(hi - lo) * 64, 256)), dim3(256), 0, st, d, phase, up ? 1 : 0, lo, hi,
+                       maxp > 0 ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -1006,7 +1425,7 @@ hipError_t launch_pms_ref_setup(hipStream_t st, const PmsDev& d, int t_lo) {
 
 hipError_t launch_pms_validate(hipStream_t st, const PmsDev& d, int t_lo) {
     if (t_lo < d.K) hipLaunchKernelGGL(k_pms_flags, dim3(blocks((size_t)(d.K - t_lo), 256)), dim3(256), 0, st, d, t_lo);
-    hipLaunchKernelGGL(k_pms_scan, dim3(1), dim3(64), 0, st, d, t_lo);
+    hipLaunchKernelGGL(k_pms_scan, dim3(1), dim3(1024), 0, st, d, t_lo);
     return hipGetLastError();
 }
 

@@ -17,8 +17,11 @@
 #include "sm_pms_host.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace {
 
@@ -119,138 +122,359 @@ float canon(uint32_t u) { return (float)(int32_t)(u - 1u) * 0x1p-31f; }
 
 }  // namespace
 
+// Runs fn(i) for i in [0, n) over nthreads host threads, indices handed out in order (dynamic).
+template <class F>
+void parallel_for(int n, int nthreads, F&& fn) {
+    if (nthreads <= 1 || n <= 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(i);
+    };
+    std::vector<std::thread> th;
+    const int nt = std::min(nthreads, n);
+    for (int k = 1; k < nt; ++k) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+}
+
+int pms_prep_threads() {
+    const char* e = getenv("SM_PREP_THREADS");
+    if (e) return std::max(1, atoi(e));
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(8u, hc / 2));  // two views build at once
+}
+
+// The forest in the reference's numbering, built tree by tree on `nthreads` host threads:
+//   1. union-find over the forest edges, each root the smallest pixel, so the raster-order scan meets every
+//      tree at its first pixel and numbers the trees as the reference does (:342-384);
+//   2. per tree (in parallel, largest first): the BFS from that pixel (bfs_forest's order, :450-522), subtree
+//      sizes, heavy children, light depths, heads by (light depth, BFS id) and the rows;
+//   3. tree_g from per-band pair lists; the cuts and the round-major lists by counting and prefix sums.
+// The result is the sequential construction's, array for array (tests/test_pms_host.py).
 int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t* mR, const uint8_t* mD,
-                     PmsForest& f, int piece) {
+                     PmsForest& f, int piece, int nthreads) {
     const int N = W * H;
-    Bfs b;
-    bfs_forest(W, H, wR, wD, mR, mD, b);
-    const int K = (int)b.tree_start.size() - 1;
+    if (nthreads <= 0) nthreads = pms_prep_threads();
+    // 1. trees
+    std::vector<int32_t> uf(N), tree_of(N);
+    for (int p = 0; p < N; ++p) uf[p] = p;
+    auto find = [&uf](int x) {
+        while (uf[x] != x) {
+            uf[x] = uf[uf[x]];
+            x = uf[x];
+        }
+        return x;
+    };
+    auto unite = [&](int a, int c) {
+        const int ra = find(a), rc = find(c);
+        if (ra < rc) uf[rc] = ra;
+        else if (rc < ra) uf[ra] = rc;
+    };
+    for (int p = 0; p < N; ++p) {
+        if (p % W + 1 < W && mR[p]) unite(p, p + 1);
+        if (p + W < N && mD[p]) unite(p, p + W);
+    }
+    std::vector<int32_t> root_pix, tsize;
+    for (int p = 0; p < N; ++p) {
+        const int r = find(p);
+        if (r == p) {
+            tree_of[p] = (int32_t)root_pix.size();
+            root_pix.push_back(p);
+            tsize.push_back(0);
+        } else {
+            tree_of[p] = tree_of[r];
+        }
+        ++tsize[tree_of[p]];
+    }
+    const int K = (int)root_pix.size();
     f.W = W;
     f.H = H;
     f.K = K;
-    f.tree_start = b.tree_start;
-    f.bfs_pix = b.pix;
-    tree_graph(W, H, b, f.nb_start, f.nb);
-
-    // heavy paths: subtree sizes (children have larger BFS ids), heavy child = the largest subtree
-    // (ties: the smallest BFS id), light depth
-    std::vector<int32_t> size(N, 1), heavy(N, -1), ld(N, 0);
-    for (int n = N - 1; n >= 0; --n)
-        if (b.parent[n] != n) size[b.parent[n]] += size[n];
-    for (int n = 0; n < N; ++n) {
-        int best = -1;
-        for (int i = 0; i < b.nch[n]; ++i) {
-            const int c = b.child[4 * (size_t)n + i];
-            if (best < 0 || size[c] > size[best]) best = c;
-        }
-        heavy[n] = best;
-        for (int i = 0; i < b.nch[n]; ++i) {
-            const int c = b.child[4 * (size_t)n + i];
-            ld[c] = ld[n] + (c == best ? 0 : 1);
-        }
-    }
-    // rows: per tree, heads by (light depth, BFS id), each path head-first
-    std::vector<int32_t> rowof(N, -1), tmaxld(K, 0);
-    std::vector<int32_t> heads;
-    std::vector<PmsPath> tpaths;  // per-tree paths in row order (by light depth)
-    std::vector<int32_t> tpath_start(K + 1, 0), path_ld;
+    f.tree_start.assign(K + 1, 0);
+    for (int t = 0; t < K; ++t) f.tree_start[t + 1] = f.tree_start[t] + tsize[t];
+    std::vector<int> order(K);
+    for (int t = 0; t < K; ++t) order[t] = t;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return tsize[a] > tsize[c]; });
+    // 2. per tree: BFS, heavy paths, rows
+    Bfs b;
+    b.pix.resize(N);
+    b.parent.resize(N);
+    b.nodeof.assign(N, -1);
+    b.w.resize(N);
+    b.nch.resize(N);
+    b.child.resize(4 * (size_t)N);
+    std::vector<int32_t> size(N), heavy(N), ld(N), rowof(N), tmaxld(K, 0);
+    std::vector<std::vector<PmsPath>> tp(K);
+    std::vector<std::vector<int32_t>> tpld(K);
     f.rows.resize(N);
-    for (int t = 0; t < K; ++t) {
-        const int ts = b.tree_start[t], te = b.tree_start[t + 1];
-        heads.clear();
-        int mld = 0;
-        for (int n = ts; n < te; ++n)
-            if (n == ts || heavy[b.parent[n]] != n) {
-                heads.push_back(n);
-                mld = std::max(mld, ld[n]);
+    parallel_for(K, nthreads, [&](int oi) {
+        const int t = order[oi];
+        const int ts = f.tree_start[t], te = f.tree_start[t + 1];
+        int tail = ts, head = ts;
+        b.pix[tail] = root_pix[t];
+        b.parent[tail] = tail;
+        b.w[tail] = 0;
+        b.nodeof[root_pix[t]] = tail++;
+        while (head < tail) {  // bfs_forest's visit, confined to the tree
+            const int n = head++;
+            const int p = b.pix[n];
+            const int x = p % W;
+            uint64_t key[4];
+            int nb[4], k = 0;
+            if (x + 1 < W && mR[p]) { key[k] = ekey(wR[p], (uint32_t)p, 0); nb[k++] = p + 1; }
+            if (p + W < N && mD[p]) { key[k] = ekey(wD[p], (uint32_t)p, 1); nb[k++] = p + W; }
+            if (x > 0 && mR[p - 1]) { key[k] = ekey(wR[p - 1], (uint32_t)(p - 1), 0); nb[k++] = p - 1; }
+            if (p >= W && mD[p - W]) { key[k] = ekey(wD[p - W], (uint32_t)(p - W), 1); nb[k++] = p - W; }
+            for (int i = 1; i < k; ++i)
+                for (int j = i; j > 0 && key[j] < key[j - 1]; --j) {
+                    std::swap(key[j], key[j - 1]);
+                    std::swap(nb[j], nb[j - 1]);
+                }
+            int c = 0;
+            for (int i = 0; i < k; ++i) {
+                const int q = nb[i];
+                if (b.nodeof[q] >= 0) continue;  // the parent (pixels of this tree only: no other thread's)
+                b.pix[tail] = q;
+                b.parent[tail] = n;
+                b.w[tail] = (uint16_t)(key[i] >> 33);
+                b.nodeof[q] = tail;
+                b.child[4 * (size_t)n + c++] = tail++;
             }
+            for (int i = c; i < 4; ++i) b.child[4 * (size_t)n + i] = -1;
+            b.nch[n] = (uint8_t)c;
+        }
+        // subtree sizes (children have larger BFS ids), heavy child = the largest subtree (ties: the
+        // smallest BFS id), light depth
+        for (int n = ts; n < te; ++n) size[n] = 1;
+        for (int n = te - 1; n > ts; --n) size[b.parent[n]] += size[n];
+        ld[ts] = 0;
+        int mld = 0;
+        for (int n = ts; n < te; ++n) {
+            int best = -1;
+            for (int i = 0; i < b.nch[n]; ++i) {
+                const int c = b.child[4 * (size_t)n + i];
+                if (best < 0 || size[c] > size[best]) best = c;
+            }
+            heavy[n] = best;
+            for (int i = 0; i < b.nch[n]; ++i) {
+                const int c = b.child[4 * (size_t)n + i];
+                ld[c] = ld[n] + (c == best ? 0 : 1);
+                mld = std::max(mld, ld[c]);
+            }
+        }
         tmaxld[t] = mld;
-        std::stable_sort(heads.begin(), heads.end(), [&](int a, int c) { return ld[a] < ld[c]; });
+        // heads by (light depth, BFS id): a counting sort; each path head-first on consecutive rows
+        std::vector<int32_t> cnt(mld + 2, 0);
+        for (int n = ts; n < te; ++n)
+            if (n == ts || heavy[b.parent[n]] != n) ++cnt[ld[n] + 1];
+        for (int l = 0; l <= mld; ++l) cnt[l + 1] += cnt[l];
+        std::vector<int32_t> heads(cnt[mld + 1]);
+        for (int n = ts; n < te; ++n)
+            if (n == ts || heavy[b.parent[n]] != n) heads[cnt[ld[n]]++] = n;
         int row = ts;
+        tp[t].reserve(heads.size());
+        tpld[t].reserve(heads.size());
         for (int h : heads) {
             const int r0 = row;
             for (int n = h; n >= 0; n = heavy[n]) rowof[n] = row++;
-            tpaths.push_back(PmsPath{t, r0, row - r0, 0});
-            path_ld.push_back(ld[h]);
+            tp[t].push_back(PmsPath{t, r0, row - r0, 0});
+            tpld[t].push_back(ld[h]);
         }
-        tpath_start[t + 1] = (int32_t)tpaths.size();
-    }
-    for (int n = 0; n < N; ++n) {
-        PmsRow& R = f.rows[rowof[n]];
-        const int p = b.pix[n];
-        R.pix = p;
-        R.x = (uint16_t)(p % W);
-        R.y = (uint16_t)(p / W);
-        R.parent = b.parent[n] == n ? -1 : rowof[b.parent[n]];
-        R.w = b.w[n];
-        R.nch = b.nch[n];
-        R.hk = 0xFF;
-        for (int i = 0; i < 4; ++i) {
-            R.child[i] = -1;
-            R.wch[i] = 0;
-        }
-        for (int i = 0; i < b.nch[n]; ++i) {  // descending BFS id: the up pass's fold order (:125)
-            const int c = b.child[4 * (size_t)n + (b.nch[n] - 1 - i)];
-            R.child[i] = rowof[c];
-            R.wch[i] = b.w[c];
-            if (c == heavy[n]) R.hk = (uint8_t)i;
-        }
-    }
-    // cut paths (tree order)
-    f.piece = piece > 0 ? piece : 0;
-    f.cuts.clear();
-    f.cut_round.clear();
-    f.tree_cut.assign(K + 1, 0);
-    std::vector<int32_t> cut_of(tpaths.size(), -1);
-    for (int t = 0; t < K; ++t) {
-        f.tree_cut[t] = (int32_t)f.cuts.size();
-        if (f.piece == 0) continue;
-        for (int i = tpath_start[t]; i < tpath_start[t + 1]; ++i)
-            if (tpaths[i].len >= 2 * f.piece) {
-                cut_of[i] = (int32_t)f.cuts.size();
-                f.cuts.push_back(PmsCut{t, tpaths[i].row, tpaths[i].len, tpaths[i].len / f.piece});
-                f.cut_round.push_back(path_ld[i]);
+        for (int n = ts; n < te; ++n) {
+            PmsRow& R = f.rows[rowof[n]];
+            const int p = b.pix[n];
+            R.pix = p;
+            R.x = (uint16_t)(p % W);
+            R.y = (uint16_t)(p / W);
+            R.parent = n == ts ? -1 : rowof[b.parent[n]];
+            R.w = b.w[n];
+            R.nch = b.nch[n];
+            R.hk = 0xFF;
+            for (int i = 0; i < 4; ++i) {
+                R.child[i] = -1;
+                R.wch[i] = 0;
             }
+            for (int i = 0; i < b.nch[n]; ++i) {  // descending BFS id: the up pass's fold order (:125)
+                const int c = b.child[4 * (size_t)n + (b.nch[n] - 1 - i)];
+                R.child[i] = rowof[c];
+                R.wch[i] = b.w[c];
+                if (c == heavy[n]) R.hk = (uint8_t)i;
+            }
+        }
+    });
+    f.bfs_pix = std::move(b.pix);
+    // 3. tree_g: inter-tree grid edges of row bands, both directions, sorted and deduplicated
+    {
+        const int nb = std::max(1, std::min(nthreads * 4, H));
+        std::vector<std::vector<uint64_t>> pr(nb);
+        parallel_for(nb, nthreads, [&](int k) {
+            const int y0 = (int)((long long)H * k / nb), y1 = (int)((long long)H * (k + 1) / nb);
+            std::vector<uint64_t>& v = pr[k];
+            for (int p = y0 * W; p < y1 * W; ++p) {
+                const int x = p % W;
+                if (x + 1 < W && tree_of[p] != tree_of[p + 1]) {
+                    v.push_back(((uint64_t)tree_of[p] << 32) | (uint32_t)tree_of[p + 1]);
+                    v.push_back(((uint64_t)tree_of[p + 1] << 32) | (uint32_t)tree_of[p]);
+                }
+                if (p + W < N && tree_of[p] != tree_of[p + W]) {
+                    v.push_back(((uint64_t)tree_of[p] << 32) | (uint32_t)tree_of[p + W]);
+                    v.push_back(((uint64_t)tree_of[p + W] << 32) | (uint32_t)tree_of[p]);
+                }
+            }
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+        });
+        std::vector<uint64_t> all;
+        for (auto& v : pr) all.insert(all.end(), v.begin(), v.end());
+        std::sort(all.begin(), all.end());
+        all.erase(std::unique(all.begin(), all.end()), all.end());
+        f.nb_start.assign(K + 1, 0);
+        f.nb.resize(all.size());
+        for (size_t i = 0; i < all.size(); ++i) {
+            f.nb_start[(all[i] >> 32) + 1]++;
+            f.nb[i] = (int32_t)(all[i] & 0xffffffffu);
+        }
+        for (int t = 0; t < K; ++t) f.nb_start[t + 1] += f.nb_start[t];
     }
-    f.tree_cut[K] = (int32_t)f.cuts.size();
-    // round-major path, item and repair lists
+    // cut paths, in tree order
+    f.piece = piece > 0 ? piece : 0;
+    f.tree_cut.assign(K + 1, 0);
+    for (int t = 0; t < K; ++t) {
+        int nc = 0;
+        if (f.piece > 0)
+            for (const PmsPath& pa : tp[t]) nc += pa.len >= 2 * f.piece;
+        f.tree_cut[t + 1] = f.tree_cut[t] + nc;
+    }
+    f.cuts.resize(f.tree_cut[K]);
+    f.cut_round.resize(f.tree_cut[K]);
+    // round-major path, item and repair lists: counts per (round, tree), prefix sums, then each tree fills its
+    // slots (a tree's paths are in light-depth order)
     int rmax = 0;
     for (int t = 0; t < K; ++t) rmax = std::max(rmax, tmaxld[t] + 1);
     f.nrounds = rmax;
     f.tree_rounds.resize(K);
     for (int t = 0; t < K; ++t) f.tree_rounds[t] = tmaxld[t] + 1;
-    f.rt_path.assign((size_t)rmax * (K + 1), 0);
-    f.rt_item.assign((size_t)rmax * (K + 1), 0);
-    f.rt_rep.assign((size_t)rmax * (K + 1), 0);
-    f.paths.clear();
-    f.items.clear();
-    f.reps.clear();
-    std::vector<int32_t> cur(tpath_start.begin(), tpath_start.end() - 1);
+    const size_t K1 = (size_t)K + 1;
+    std::vector<int32_t> cp((size_t)rmax * K1, 0), ci((size_t)rmax * K1, 0), cr((size_t)rmax * K1, 0);
+    auto chunks_of = [&f](int t) { return (f.nb_start[t + 1] - f.nb_start[t] + 63) / 64; };
+    parallel_for(K, nthreads, [&](int t) {
+        const int chunks = chunks_of(t);
+        for (size_t i = 0; i < tp[t].size(); ++i) {
+            const PmsPath& pa = tp[t][i];
+            const bool cut = f.piece > 0 && pa.len >= 2 * f.piece;
+            const int np = cut ? pa.len / f.piece : 1;
+            const size_t k = (size_t)tpld[t][i] * K1 + t;
+            cp[k] += np;
+            ci[k] += np * chunks;
+            if (cut) cr[k] += std::max(chunks, 1);
+        }
+    });
+    f.rt_path.assign((size_t)rmax * K1, 0);
+    f.rt_item.assign((size_t)rmax * K1, 0);
+    f.rt_rep.assign((size_t)rmax * K1, 0);
+    int32_t sp = 0, si = 0, sr = 0;
     for (int r = 0; r < rmax; ++r)
         for (int t = 0; t <= K; ++t) {
-            f.rt_path[(size_t)r * (K + 1) + t] = (int32_t)f.paths.size();
-            f.rt_item[(size_t)r * (K + 1) + t] = (int32_t)f.items.size();
-            f.rt_rep[(size_t)r * (K + 1) + t] = (int32_t)f.reps.size();
-            if (t == K) break;
-            const int deg = f.nb_start[t + 1] - f.nb_start[t];
-            const int chunks = (deg + 63) / 64;
-            for (; cur[t] < tpath_start[t + 1] && path_ld[cur[t]] == r; ++cur[t]) {
-                const PmsPath pa = tpaths[cur[t]];
-                const int c = cut_of[cur[t]];
-                const int np = c < 0 ? 1 : f.cuts[c].npieces;
-                for (int i = 0; i < np; ++i) {  // the pieces, head first
-                    const int r0 = pa.row + i * f.piece;
-                    const int len = c < 0 ? pa.len : (i + 1 < np ? f.piece : pa.row + pa.len - r0);
-                    const int pi = (int)f.paths.size();
-                    f.paths.push_back(PmsPath{t, r0, len, 0});
-                    for (int k = 0; k < chunks; ++k) f.items.push_back(PmsItem{pi, k});
-                }
-                if (c >= 0)
-                    for (int k = 0; k < std::max(chunks, 1); ++k) f.reps.push_back(PmsRep{c, k});
+            const size_t k = (size_t)r * K1 + t;
+            f.rt_path[k] = sp;
+            f.rt_item[k] = si;
+            f.rt_rep[k] = sr;
+            if (t < K) {
+                sp += cp[k];
+                si += ci[k];
+                sr += cr[k];
             }
         }
+    f.paths.resize(sp);
+    f.items.resize(si);
+    f.reps.resize(sr);
+    parallel_for(K, nthreads, [&](int t) {
+        const int chunks = chunks_of(t);
+        int c = f.tree_cut[t];
+        for (size_t i = 0; i < tp[t].size(); ++i) {
+            const PmsPath pa = tp[t][i];
+            const int r = tpld[t][i];
+            const size_t k = (size_t)r * K1 + t;
+            const bool cut = f.piece > 0 && pa.len >= 2 * f.piece;
+            const int np = cut ? pa.len / f.piece : 1;
+            if (cut) {
+                f.cuts[c] = PmsCut{t, pa.row, pa.len, np};
+                f.cut_round[c] = r;
+            }
+            for (int q = 0; q < np; ++q) {  // the pieces, head first
+                const int r0 = pa.row + q * f.piece;
+                const int len = !cut ? pa.len : (q + 1 < np ? f.piece : pa.row + pa.len - r0);
+                const int pi = f.rt_path[k]++;
+                f.paths[pi] = PmsPath{t, r0, len, 0};
+                for (int h = 0; h < chunks; ++h) f.items[f.rt_item[k]++] = PmsItem{pi, h};
+            }
+            if (cut) {
+                for (int h = 0; h < std::max(chunks, 1); ++h) f.reps[f.rt_rep[k]++] = PmsRep{c, h};
+                ++c;
+            }
+        }
+    });
+    // the fills advanced each (round, tree) start to the next one's: shift back
+    for (auto* v : {&f.rt_path, &f.rt_item, &f.rt_rep}) {
+        std::vector<int32_t>& a = *v;
+        for (size_t k = a.size(); k-- > 1;) a[k] = a[k - 1];
+        if (!a.empty()) a[0] = 0;
+    }
     return K;
 }
+
+// TYPE_3 additive feedback generator (degree 31, separation 3): srandom_r fills the state with
+// 16807 * x mod (2^31 - 1) (Schrage), then discards 310 outputs; each output is the new state word
+// shifted right by one.
+void GlibcRandom::seed_skip(unsigned seed, long skip) {
+    if (seed == 0) seed = 1;
+    st[0] = (int32_t)seed;
+    long word = (long)seed;
+    for (int i = 1; i < 31; ++i) {
+        const long hi = word / 127773, lo = word % 127773;
+        word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        st[i] = (int32_t)word;
+    }
+    f = 3;
+    r = 0;
+    const long total = 310 + skip;
+    for (long k = 0; k < total; ++k) {
+        st[f] = (int32_t)((uint32_t)st[f] + (uint32_t)st[r]);
+        if (++f >= 31) {
+            f = 0;
+            ++r;
+        } else if (++r >= 31) {
+            r = 0;
+        }
+    }
+}
+
+void GlibcRandom::draw(long n, int32_t* out) {
+    for (long k = 0; k < n; ++k) {
+        const uint32_t v = (uint32_t)st[f] + (uint32_t)st[r];
+        st[f] = (int32_t)v;
+        out[k] = (int32_t)(v >> 1);
+        if (++f >= 31) {
+            f = 0;
+            ++r;
+        } else if (++r >= 31) {
+            r = 0;
+        }
+    }
+}
+
+// FNV-1a digests of the built forest's arrays (tests: the build is the same for any thread count)
+static uint64_t fnv(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char* c = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+    return h;
+}
+template <class T>
+static uint64_t fnv_vec(const std::vector<T>& v) { return fnv(v.data(), v.size() * sizeof(T)); }
 
 extern "C" {
 
@@ -292,6 +516,27 @@ int sm_pms_tree_graph(int W, int H, const uint8_t* mask, const uint16_t* wR, con
     return (int)n.size();
 }
 
+int sm_pms_forest_digest(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t* mask, int piece, int nthreads,
+                         uint64_t* out, int32_t* tree_start, int32_t* bfs_pix) {
+    const int N = W * H;
+    std::vector<uint8_t> mR(N), mD(N);
+    for (int p = 0; p < N; ++p) {
+        mR[p] = mask[p] & 1;
+        mD[p] = (mask[p] >> 1) & 1;
+    }
+    PmsForest f;
+    const int K = pms_build_forest(W, H, wR, wD, mR.data(), mD.data(), f, piece, nthreads);
+    out[0] = fnv_vec(f.rows);
+    out[1] = fnv_vec(f.paths);
+    out[2] = fnv_vec(f.items);
+    out[3] = fnv_vec(f.rt_path) ^ (fnv_vec(f.rt_item) * 3) ^ (fnv_vec(f.rt_rep) * 5);
+    out[4] = fnv_vec(f.cuts) ^ (fnv_vec(f.reps) * 3) ^ (fnv_vec(f.tree_cut) * 5) ^ (fnv_vec(f.cut_round) * 7);
+    out[5] = fnv_vec(f.nb_start) ^ (fnv_vec(f.nb) * 3) ^ (fnv_vec(f.tree_rounds) * 5) ^ (uint64_t)f.nrounds;
+    if (tree_start) std::memcpy(tree_start, f.tree_start.data(), (K + 1) * sizeof(int32_t));
+    if (bfs_pix) std::memcpy(bfs_pix, f.bfs_pix.data(), N * sizeof(int32_t));
+    return K;
+}
+
 void sm_pms_dice(long n, float* out) {
     uint32_t s = 1u;
     for (long k = 0; k < n; ++k) {
@@ -301,32 +546,9 @@ void sm_pms_dice(long n, float* out) {
 }
 
 void sm_pms_glibc_random(unsigned seed, long skip, long n, int32_t* out) {
-    // TYPE_3 additive feedback generator (degree 31, separation 3): srandom_r fills the state with
-    // 16807 * x mod (2^31 - 1) (Schrage), then discards 310 outputs; each output is the new state
-    // word shifted right by one.
-    int32_t st[31];
-    if (seed == 0) seed = 1;
-    st[0] = (int32_t)seed;
-    long word = (long)seed;
-    for (int i = 1; i < 31; ++i) {
-        const long hi = word / 127773, lo = word % 127773;
-        word = 16807 * lo - 2836 * hi;
-        if (word < 0) word += 2147483647;
-        st[i] = (int32_t)word;
-    }
-    int f = 3, r = 0;
-    const long first = 310 + skip, total = first + n;
-    for (long k = 0; k < total; ++k) {
-        const uint32_t v = (uint32_t)st[f] + (uint32_t)st[r];
-        st[f] = (int32_t)v;
-        if (k >= first) out[k - first] = (int32_t)(v >> 1);
-        if (++f >= 31) {
-            f = 0;
-            ++r;
-        } else if (++r >= 31) {
-            r = 0;
-        }
-    }
+    GlibcRandom g;
+    g.seed_skip(seed, skip);
+    g.draw(n, out);
 }
 
 void sm_pms_init_labels(int W, int H, int max_disp, float* abc) {

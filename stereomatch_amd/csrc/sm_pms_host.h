@@ -68,11 +68,21 @@ struct PmsForest {
     std::vector<int32_t> rt_rep;      // nrounds x (K+1)
 };
 
+// glibc's random() after srandom(seed) (TYPE_3, the generator sm_pms_glibc_random restates), as a state:
+// seed_skip discards the first `skip` outputs, draw continues the stream
+struct GlibcRandom {
+    int32_t st[31];
+    int f = 3, r = 0;
+    void seed_skip(unsigned seed, long skip);
+    void draw(long n, int32_t* out);
+};
+
 // Build the forest from the forest masks (real edges only: mR[p] = edge (p, p+1), mD[p] = (p, p+W)) and
 // the edge weights.  Returns the number of trees.
 // piece > 0 cuts every heavy path of at least 2 * piece rows into pieces.
+// nthreads host threads (0: SM_PREP_THREADS, or min(8, cores / 2)); the result does not depend on it.
 int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t* mR, const uint8_t* mD,
-                     PmsForest& f, int piece = 0);
+                     PmsForest& f, int piece = 0, int nthreads = 0);
 #endif
 
 #ifdef __cplusplus
@@ -85,6 +95,10 @@ int sm_pms_forest_bfs(int W, int H, const uint16_t* wR, const uint16_t* wD, cons
 // tree_g of that forest as CSR (nb capacity nb_cap); returns the entries or -1.
 int sm_pms_tree_graph(int W, int H, const uint8_t* mask, const uint16_t* wR, const uint16_t* wD, int32_t* nb_start,
                       int32_t* nb, int nb_cap);
+// pms_build_forest over a mask forest: digests of its arrays (rows, paths, items, round lists, cuts, tree
+// graph) into out[6], its tree_start (K+1) and bfs_pix (N); returns K
+int sm_pms_forest_digest(int W, int H, const uint16_t* wR, const uint16_t* wD, const uint8_t* mask, int piece, int nthreads,
+                         uint64_t* out, int32_t* tree_start, int32_t* bfs_pix);
 // dice values 0..n-1 of uniform_real_distribution<float>(-1, 1) over a default-seeded minstd_rand0
 void sm_pms_dice(long n, float* out);
 // glibc random() after srandom(seed): outputs skip .. skip+n-1

@@ -62,19 +62,25 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
     assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
 
 
-@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup"])
+@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
     call's starting labels) and wrong offsets (a new pass); SM_PMS_REPASS=1 re-speculates after
     every failure; SM_PMS_SERIAL=1 is the plain serial order; SM_PMS_NODEDUP=1 propagates every
-    sampled label, repeats included (the default drops repeats, k_pms_prop_dedupe)."""
+    sampled label, repeats included (the default drops repeats, k_pms_prop_dedupe);
+    SM_PMS_WAVE_WALK=1 walks every (path, chunk) item with a wave of its own instead of the planned
+    lane-group walks (k_pms_plan / k_pms_walk_plan)."""
     monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
     monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
     if mode == "nodedup":
         monkeypatch.setenv("SM_PMS_NODEDUP", "1")
     else:
         monkeypatch.delenv("SM_PMS_NODEDUP", raising=False)
+    if mode == "wavewalk":
+        monkeypatch.setenv("SM_PMS_WAVE_WALK", "1")
+    else:
+        monkeypatch.delenv("SM_PMS_WAVE_WALK", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
@@ -85,14 +91,18 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         assert st["serial_trees"] > 2 * ref["left"]["tree"]["ntrees"] - 50  # first calls + the failures
 
 
-@pytest.mark.parametrize("piece,serial", [("16", "0"), ("8", "1"), ("64", "0")])
-def test_pms_pieces_bitexact(gpu_ctx, monkeypatch, piece, serial):
-    """Long heavy paths cut into pieces of SM_PMS_PIECE rows: every piece runs from a guessed input and
-    k_pms_repair re-walks it from its neighbour's exact row until the rows agree (8-row pieces mostly
-    re-walk whole pieces).  First call serial (cut trees take the whole-GPU launches), later calls
-    speculative; SM_PMS_SERIAL=1 all serial."""
+@pytest.mark.parametrize("piece,serial,seqrep", [("16", "0", "0"), ("8", "1", "0"), ("64", "0", "0"), ("8", "0", "0"),
+                                                 ("16", "0", "1")])
+def test_pms_pieces_bitexact(gpu_ctx, monkeypatch, piece, serial, seqrep):
+    """Long heavy paths cut into pieces of SM_PMS_PIECE rows: every piece runs from a guessed input; the
+    parallel repair (k_pms_repair_par) re-walks every piece at once from its neighbour's boundary row until
+    the rows agree, and the gated sequential pass redoes the cuts where a piece's repair rewrote the row
+    its neighbour started from (8-row pieces mostly re-walk whole pieces, so they take it; SM_PMS_SEQ_REPAIR=1
+    runs the sequential pass alone).  First call serial (cut trees take the whole-GPU launches), later
+    calls speculative; SM_PMS_SERIAL=1 all serial."""
     monkeypatch.setenv("SM_PMS_PIECE", piece)
     monkeypatch.setenv("SM_PMS_SERIAL", serial)
+    monkeypatch.setenv("SM_PMS_SEQ_REPAIR", seqrep)
     left, right, _ = make_pair(192, 128, 48, index=7)
     ref = O.stereo3dmst_pms(left, right, 48, iters=3, c=5000.0, min_size=200)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 3, 5000.0, 200)

@@ -61,6 +61,26 @@ def test_library_forest_bfs_matches_oracle(name, c, min_size):
         np.testing.assert_array_equal(nb, rnb)
 
 
+@pytest.mark.parametrize("src,c,min_size,piece", [("smooth_97x61", 5000.0, 200, 16), ("rand_37x23", 0.0, 2, 4),
+                                                  ("synth", 300.0, 20, 64), ("synth", 5000.0, 200, 8),
+                                                  ("synth", float("inf"), 200, 512)])
+def test_schedule_forest_threads_invariant(src, c, min_size, piece):
+    """The schedule forest (rows, paths, items, round lists, cuts, tree graph) built tree by tree on 1, 3
+    and 8 host threads is the same, and its numbering is the oracle's BFS (Stereo3DMST.cpp:342-384,
+    450-522)."""
+    img = load_case(src)["left"] if src != "synth" else make_pair(640, 480, 32, index=3)[0]
+    H, W, _ = img.shape
+    wR, wD = O.edge_weights(O.median3(img))
+    mask, _ = O.segment(W, H, wR, wD, c, min_size)
+    ref = O.bfs(W, H, wR, wD, mask)
+    outs = [L.pms_forest_digest(W, H, wR, wD, mask, piece, nt) for nt in (1, 3, 8)]
+    for o in outs:
+        assert o["ntrees"] == ref["ntrees"]
+        np.testing.assert_array_equal(o["tree_start"], ref["tree_start"])
+        np.testing.assert_array_equal(o["bfs_pix"], ref["node_pix"])
+        np.testing.assert_array_equal(o["digest"], outs[0]["digest"])
+
+
 # ---------------------------------------------------------------- literal transcription of MST_PMS
 def _r32(fr):
     c = np.float32(float(fr))
