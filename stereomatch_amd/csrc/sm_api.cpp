@@ -1586,9 +1586,10 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
         }
         CHECK(upload_vec(ctx, S.plan_base, pb));
         CHECK(upload_vec(ctx, S.plan_ibase, ib));
-        CHECK(ensure(ctx, S.plan_cnt, (size_t)std::max(R, 1) * PMS_NCLS * 4));
+        CHECK(ensure(ctx, S.plan_cnt, (size_t)std::max(R, 1) * PMS_NCNT * 4));
         CHECK(ensure(ctx, S.plan_path, (size_t)std::max<size_t>(f.paths.size(), 1) * (PMS_NCLS - 1) * 4));
-        CHECK(ensure(ctx, S.plan_item, (size_t)std::max<size_t>(f.items.size() + f.paths.size(), 1) * sizeof(PmsItem)));
+        // wave items at [0, cap), chain items at [cap, 2 cap)
+        CHECK(ensure(ctx, S.plan_item, 2 * (size_t)std::max<size_t>(f.items.size() + f.paths.size(), 1) * sizeof(PmsItem)));
     }
     return SM_OK;
 }
@@ -1646,6 +1647,7 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.plan_base = P<int32_t>(S.plan_base);
     d.plan_ibase = P<int32_t>(S.plan_ibase);
     d.npaths_total = (int)S.f.paths.size();
+    d.item_cap = (int)std::max<size_t>(S.f.items.size() + S.f.paths.size(), 1);
     d.Abak = P<double>(S.Abak);
     d.rep_flag = P<uint32_t>(S.rep_flag);
     d.piece = S.f.piece;
@@ -1698,6 +1700,8 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
     // one wave per (path, 64-proposal chunk) item, the round-3 walker (A/B)
     constexpr int PMS_WALK_WAVES = 16384;
     std::vector<int> bound(std::max(R, 1), 0);
+    // SM_PMS_NO_CHAIN=1: long paths on the wave walker too (A/B of k_pms_chain)
+    const bool chains = !(getenv("SM_PMS_NO_CHAIN") && atoi(getenv("SM_PMS_NO_CHAIN")) == 1);
     if (!wave_walk) {
         int maxp = 0;
         for (int r = 0; r < R; ++r) {
@@ -1706,7 +1710,7 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
             // virtual tasks: at most one per path of the classes, plus the chunks of the rest
             bound[r] = std::min(PMS_WALK_WAVES, np + (phase == 0 ? rt[r * K1 + t_hi] - rt[r * K1 + t_lo] : 0));
         }
-        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp));
+        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains));
     }
     // pieces: every guessed piece repairs at once, then a gated sequential pass (SM_PMS_SEQ_REPAIR=1: the
     // sequential pass alone, A/B); maxp[r] = the most pieces of a cut repaired in round r
@@ -1716,15 +1720,25 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
         for (int r = 0; r < R; ++r)
             for (int k = f.rt_rep[r * K1 + t_lo]; k < f.rt_rep[r * K1 + t_hi]; ++k)
                 maxp[r] = std::max(maxp[r], f.cuts[f.reps[k].cut].npieces);
+    // chain items (paths / pieces of >= SM_PMS_CHAIN_LEN rows, k_pms_chain): the host's bound per round
+    std::vector<int> nlong(std::max(R, 1), 0);
+    if (!wave_walk && chains)
+        for (int r = 0; r < R; ++r) nlong[r] = f.rt_long[r * K1 + t_hi] - f.rt_long[r * K1 + t_lo];
     for (int r = R - 1; r >= 0; --r) {
         if (wave_walk) HIPC(launch_pms_walk(st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        else HIPC(launch_pms_walk_plan(st, d, phase, true, r, bound[r]));
+        else {
+            HIPC(launch_pms_chain(st, d, phase, true, r, nlong[r]));
+            HIPC(launch_pms_walk_plan(st, d, phase, true, r, bound[r]));
+        }
         HIPC(launch_pms_repair(st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
     }
     HIPC(launch_pms_cut_backup(st, d, f.tree_cut[t_lo], f.tree_cut[t_hi]));
     for (int r = 0; r < R; ++r) {
         if (wave_walk) HIPC(launch_pms_walk(st, d, phase, false, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        else HIPC(launch_pms_walk_plan(st, d, phase, false, r, bound[r]));
+        else {
+            HIPC(launch_pms_chain(st, d, phase, false, r, nlong[r]));
+            HIPC(launch_pms_walk_plan(st, d, phase, false, r, bound[r]));
+        }
         HIPC(launch_pms_repair(st, d, phase, false, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
     }
     HIPC(launch_pms_update(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));

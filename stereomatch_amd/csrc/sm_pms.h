@@ -57,6 +57,7 @@ struct PmsDev {
     const int32_t* plan_base;    // nrounds: first path of round r (rt_path[r][0])
     const int32_t* plan_ibase;   // nrounds: rt_item[r][0] + rt_path[r][0] (big items: chunks of any phase)
     int npaths_total;
+    int item_cap;                // plan_item: wave items at [0, item_cap), chain items at [item_cap, 2 item_cap)
     const double* slut;
     const double* s2lut;
     // pieces (sm_pms_host.h PmsCut): cut paths, repair items, per-cut backup offsets into Abak (the
@@ -89,11 +90,17 @@ hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, 
 // lane-group classes of the planned walks: paths of trees with P <= 2 / P <= 8 proposals share a wave
 // (32 / 8 paths per wave), the rest are (path, 64-proposal chunk) items of one wave each
 #define PMS_NCLS 3
+// plan counters per round: the PMS_NCLS walk classes, then the chain items (paths of >= PMS_CHAIN_LEN rows)
+#define PMS_NCNT 4
+// one round's chain items (k_pms_chain): `items` workgroups (the host's bound on the round's long items)
+hipError_t launch_pms_chain(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int items);
 // the phase's A-row layout of trees [t_lo, t_hi): stride P rounded up to even, packed (k_pms_layout)
 hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int32_t* pt_out,
                              long long* ab_out);
 // the walk plan of trees [t_lo, t_hi) for a phase (plan_cnt zeroed here); r_lo..r_hi: rounds to plan
-hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths);
+// chains: paths of >= SM_PMS_CHAIN_LEN rows become chain items (k_pms_chain), else wave items
+hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths,
+                           bool chains);
 // one round's planned walk, a persistent grid of `waves` waves (the host's bound on the work)
 hipError_t launch_pms_walk_plan(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int waves);
 hipError_t launch_pms_cost(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);

@@ -912,14 +912,15 @@ __device__ void down_group(const PmsDev& d, const double* __restrict__ sS, const
 // A path of at least PMS_GLONG rows goes to the wave walker whatever its P: its walk is a latency chain,
 // and the wave walker issues PMS_CH nodes per memory round trip against the group walker's PMS_GCH.
 constexpr int PMS_GLONG = 48;
+constexpr int PMS_CHAIN_LEN = SM_PMS_CHAIN_LEN;  // from here on: k_pms_chain
 
-__global__ void __launch_bounds__(1024) k_pms_plan(PmsDev d, int phase, int t_lo, int t_hi) {
-    __shared__ int s_n[PMS_NCLS], s_base[PMS_NCLS];
+__global__ void __launch_bounds__(1024) k_pms_plan(PmsDev d, int phase, int t_lo, int t_hi, int chain_len) {
+    __shared__ int s_n[PMS_NCNT], s_base[PMS_NCNT];
     const int r = (int)blockIdx.y, K1 = d.K + 1;
     const int p0 = d.rt_path[(size_t)r * K1 + t_lo], p1 = d.rt_path[(size_t)r * K1 + t_hi];
     const int p = p0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
     const int lane = (int)(threadIdx.x & 63);
-    if (threadIdx.x < PMS_NCLS) s_n[threadIdx.x] = 0;
+    if (threadIdx.x < PMS_NCNT) s_n[threadIdx.x] = 0;
     __syncthreads();
     int P = 0, base = 0, len = 0;
     if (p < p1) {
@@ -927,40 +928,35 @@ __global__ void __launch_bounds__(1024) k_pms_plan(PmsDev d, int phase, int t_lo
         len = pa.len;
         phase_labels(d, phase, pa.tree, P, base);
     }
-    const int c = P <= 0 ? -1 : len >= PMS_GLONG ? PMS_NCLS - 1 : pms_class_of(P);
-    const int nchunk = c == PMS_NCLS - 1 ? (P + 63) / 64 : 1;
+    // classes: 0 / 1 lane groups, 2 wave items, 3 chain items (k_pms_chain)
+    const int c = P <= 0 ? -1 : len >= chain_len ? 3 : len >= PMS_GLONG ? 2 : pms_class_of(P);
+    const int nchunk = c >= 2 ? (P + 63) / 64 : 1;
     // block-aggregated appends: wave offsets in LDS, one global atomic per class and block
-    int wpos[PMS_NCLS];
+    int wpos[PMS_NCNT];
 #pragma unroll
-    for (int k = 0; k < PMS_NCLS; ++k) {
-        const unsigned long long m = __ballot(c == k);
-        int cnt_w = 0, pre = 0;
-        if (k < PMS_NCLS - 1) {
-            cnt_w = __popcll(m);
-            pre = __popcll(m & ((1ull << lane) - 1ull));
-        } else {  // chunks: an exclusive wave scan of nchunk over the lanes of class k
-            int v = c == k ? nchunk : 0, incl = v;
+    for (int k = 0; k < PMS_NCNT; ++k) {
+        int v = c == k ? nchunk : 0, incl = v;  // an exclusive wave scan of the entries of class k
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
-            pre = incl - v;
-            cnt_w = __shfl(incl, 63);
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
         }
+        const int cnt_w = __shfl(incl, 63);
         int wb = 0;
         if (lane == 0 && cnt_w) wb = atomicAdd(&s_n[k], cnt_w);
-        wpos[k] = __shfl(wb, 0) + pre;
+        wpos[k] = __shfl(wb, 0) + incl - v;
     }
     __syncthreads();
-    if (threadIdx.x < PMS_NCLS) s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(d.plan_cnt + r * PMS_NCLS + threadIdx.x, s_n[threadIdx.x]) : 0;
+    if (threadIdx.x < PMS_NCNT)
+        s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(d.plan_cnt + r * PMS_NCNT + threadIdx.x, s_n[threadIdx.x]) : 0;
     __syncthreads();
     if (c < 0) return;
     const int pos = s_base[c] + wpos[c];
-    if (c < PMS_NCLS - 1) {
+    if (c < 2) {
         d.plan_path[(size_t)c * d.npaths_total + d.plan_base[r] + pos] = p;
     } else {
-        for (int k = 0; k < nchunk; ++k) d.plan_item[d.plan_ibase[r] + pos + k] = PmsItem{p, k};
+        PmsItem* out = d.plan_item + (c == 3 ? (size_t)d.item_cap : 0) + d.plan_ibase[r] + pos;
+        for (int k = 0; k < nchunk; ++k) out[k] = PmsItem{p, k};
     }
 }
 
@@ -973,7 +969,7 @@ __global__ void __launch_bounds__(256) k_pms_walk_plan(PmsDev d, int phase, int 
         sS2[i] = d.s2lut[i];
     }
     __syncthreads();
-    const int* cnt = d.plan_cnt + r * PMS_NCLS;
+    const int* cnt = d.plan_cnt + r * PMS_NCNT;
     const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
     const int T0 = (n0 + 31) / 32, T1 = (n1 + 7) / 8, T = T0 + T1 + n2;
     const int lane = (int)(threadIdx.x & 63);
@@ -993,6 +989,198 @@ __global__ void __launch_bounds__(256) k_pms_walk_plan(PmsDev d, int phase, int 
             const PmsItem it = d.plan_item[d.plan_ibase[r] + (w - T0 - T1)];
             if (up) up_item(d, sS, phase, uni(it.path), uni(it.chunk));
             else down_item(d, sS, sS2, phase, uni(it.path), uni(it.chunk));
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- chains (long paths)
+// A path (or piece) of at least PMS_CHAIN_LEN rows is a long latency chain for the walkers: each PMS_CH
+// nodes cost a memory round trip (~3 us at C2 in rounds with many walkers).  k_pms_chain walks it with
+// one workgroup per (path, 64-proposal chunk): PC_LW loader waves take the groups of PC_G nodes in turn,
+// load everything a node needs and stage it in an LDS ring of PC_NS slots; the chain wave runs the
+// recurrence from LDS and only stores.  Up (bottom to head): a loader folds the light children that
+// precede the heavy one in fold order into pre (from +0, as the walkers do), and stages the post-heavy
+// light rows and the cost; the chain then does acc = fma(x, S_heavy, pre), the post children in order,
+// x = cost + acc -- up_walk's operations, the fold split at the heavy child.  A node with a third
+// post-heavy child (only a tree root can have one) has the chain read that row itself.  Down (head to
+// bottom): a loader stages T = S2 * A_up and S, the chain does y = fma(S, y, T); the head reads its
+// parent row (or keeps A_up at a tree root) -- down_walk's operations.  Same bits as the walkers.
+constexpr int PC_G = 8;        // nodes per group
+constexpr int PC_NSU = 6;      // up ring slots (2 KB per node)
+constexpr int PC_NSD = 16;     // down ring slots (0.5 KB per node)
+constexpr int PC_LW = 7;       // loader waves (+ the chain wave: 512 threads)
+
+struct PcUpSlot {
+    double pre[PC_G][64], p1[PC_G][64], p2[PC_G][64], cost[PC_G][64];
+    double sh[PC_G], s1[PC_G], s2[PC_G], s3[PC_G];
+    int np[PC_G], p3row[PC_G];
+};
+struct PcDnSlot {
+    double T[PC_G][64];
+    double S[PC_G];
+};
+
+__device__ __forceinline__ void pc_publish(int* p, int v) {  // after this wave's LDS writes have landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);                       // lgkmcnt(0)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ void pc_publish_ordered(int* p, int v) {  // LDS reads issued before complete first
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ void pc_wait_ge(int* p, int v) {
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+template <bool UP>
+__global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
+    extern __shared__ double pc_lds[];
+    __shared__ double sS[PMS_NW], sS2[PMS_NW];
+    __shared__ int s_staged[PC_NSD], s_freed;
+    const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int NS = UP ? PC_NSU : PC_NSD;
+    for (int i = tid; i < PMS_NW; i += blockDim.x) {
+        sS[i] = d.slut[i];
+        sS2[i] = d.s2lut[i];
+    }
+    if (tid < PC_NSD) s_staged[tid] = 0;
+    if (tid == 0) s_freed = 0;
+    __syncthreads();
+    const int ncl = d.plan_cnt[r * PMS_NCNT + PMS_NCLS];  // chain items of the round
+    if ((int)blockIdx.x >= ncl) return;
+    const PmsItem it = d.plan_item[(size_t)d.item_cap + d.plan_ibase[r] + blockIdx.x];
+    const PmsPath pa = d.paths[it.path];
+    const int t = pa.tree, r0 = pa.row, len = pa.len;
+    int P, base;
+    phase_labels(d, phase, t, P, base);
+    const int j = it.chunk * 64 + lane;
+    const bool act = j < P;
+    const int ts = d.tree_start[t], pt = d.tree_pt[t];
+    double* __restrict__ A = d.A + d.tree_abase[t] + j;
+    const double* __restrict__ Al = d.A + d.tree_abase[t] + (act ? j : 0);
+    const int ngroups = (len + PC_G - 1) / PC_G;
+    if (UP) {
+        PcUpSlot* ring = reinterpret_cast<PcUpSlot*>(pc_lds);
+        if (wave > 0) {  // loaders: groups wave - 1, wave - 1 + PC_LW, ...
+            for (int g = wave - 1; g < ngroups; g += PC_LW) {
+                const int itop = len - 1 - g * PC_G;                 // the group's first (lowest) node
+                const int ilo = itop - PC_G + 1 > 0 ? itop - PC_G + 1 : 0;
+                const int n = itop - ilo + 1;
+                const ChunkMeta m = meta_load(d.rows, r0 + ilo, n);
+                double cv[PC_G][4], cost[PC_G];
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    const int kk = k < n ? k : 0;
+                    const int row = r0 + itop - kk, w0 = (itop - kk - ilo) * 10;
+                    const uint32_t w6 = meta_dw(m, w0 + 6);
+                    const int nch = (int)((w6 >> 16) & 255u), hk = (int)(w6 >> 24);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int crow = (q < nch && q != hk) ? (int)meta_dw(m, w0 + 2 + q) : row;
+                        cv[k][q] = Al[(size_t)(crow - ts) * pt];
+                    }
+                    cost[k] = Al[(size_t)(row - ts) * pt];
+                }
+                const int s = g % NS;
+                pc_wait_ge(&s_freed, g - NS + 1);  // the slot's previous group is consumed
+                PcUpSlot& sl = ring[s];
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    if (k >= n) break;
+                    const int w0 = (itop - k - ilo) * 10;
+                    const uint32_t w6 = meta_dw(m, w0 + 6), w7 = meta_dw(m, w0 + 7), w8 = meta_dw(m, w0 + 8);
+                    const int nch = (int)((w6 >> 16) & 255u), hk = (int)(w6 >> 24);
+                    const int wc[4] = {(int)(w7 & 0xFFFFu), (int)(w7 >> 16), (int)(w8 & 0xFFFFu), (int)(w8 >> 16)};
+                    const int h = hk == 0xFF ? nch : hk;  // fold position of the heavy child (a leaf: none)
+                    double pre = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (q < h) pre = fma(cv[k][q], sS[wc[q]], pre);
+                    sl.pre[k][lane] = pre;
+                    sl.cost[k][lane] = cost[k];
+                    const int np = hk == 0xFF ? 0 : nch - 1 - hk;
+                    sl.p1[k][lane] = np >= 1 ? cv[k][(hk + 1) & 3] : 0.0;
+                    sl.p2[k][lane] = np >= 2 ? cv[k][(hk + 2) & 3] : 0.0;
+                    if (lane == 0) {
+                        sl.sh[k] = hk == 0xFF ? 0.0 : sS[wc[hk & 3]];
+                        sl.s1[k] = np >= 1 ? sS[wc[(hk + 1) & 3]] : 0.0;
+                        sl.s2[k] = np >= 2 ? sS[wc[(hk + 2) & 3]] : 0.0;
+                        sl.s3[k] = np >= 3 ? sS[wc[3]] : 0.0;
+                        sl.np[k] = np;
+                        sl.p3row[k] = np >= 3 ? (int)meta_dw(m, w0 + 5) : 0;
+                    }
+                }
+                pc_publish(&s_staged[s], g + 1);
+            }
+        } else {  // the chain wave
+            double x = 0.0;  // the bottom row's heavy child: a leaf's none, a cut piece's guess 0
+            for (int g = 0; g < ngroups; ++g) {
+                const int s = g % NS;
+                pc_wait_ge(&s_staged[s], g + 1);
+                const PcUpSlot& sl = ring[s];
+                const int itop = len - 1 - g * PC_G;
+                const int n = itop + 1 < PC_G ? itop + 1 : PC_G;
+                for (int k = 0; k < n; ++k) {
+                    double acc = fma(x, sl.sh[k], sl.pre[k][lane]);  // a leaf: fma(0, 0, +0) = +0
+                    const int np = sl.np[k];
+                    if (np >= 1) acc = fma(sl.p1[k][lane], sl.s1[k], acc);
+                    if (np >= 2) acc = fma(sl.p2[k][lane], sl.s2[k], acc);
+                    if (np >= 3) acc = fma(Al[(size_t)(sl.p3row[k] - ts) * pt], sl.s3[k], acc);
+                    x = sl.cost[k][lane] + acc;
+                    if (act) A[(size_t)(r0 + itop - k - ts) * pt] = x;
+                }
+                pc_publish_ordered(&s_freed, g + 1);
+            }
+        }
+    } else {
+        PcDnSlot* ring = reinterpret_cast<PcDnSlot*>(pc_lds);
+        if (wave > 0) {
+            for (int g = wave - 1; g < ngroups; g += PC_LW) {
+                const int i0 = g * PC_G;
+                const int n = len - i0 < PC_G ? len - i0 : PC_G;
+                double u[PC_G];
+                int w[PC_G];
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    const int i = i0 + (k < n ? k : 0);
+                    u[k] = Al[(size_t)(r0 + i - ts) * pt];
+                    w[k] = (int)d.rows[r0 + i].w;
+                }
+                const int s = g % NS;
+                pc_wait_ge(&s_freed, g - NS + 1);
+                PcDnSlot& sl = ring[s];
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    if (k >= n) break;
+                    sl.T[k][lane] = sS2[w[k]] * u[k];
+                    if (lane == 0) sl.S[k] = sS[w[k]];
+                }
+                pc_publish(&s_staged[s], g + 1);
+            }
+        } else {
+            const int parent = d.rows[r0].parent;
+            // the head: fma(S, A(parent), S2 * A_up), or A_up itself at a tree root -- loaded before any store
+            double y = parent >= 0 ? Al[(size_t)(parent - ts) * pt] : Al[(size_t)(r0 - ts) * pt];
+            for (int g = 0; g < ngroups; ++g) {
+                const int s = g % NS;
+                pc_wait_ge(&s_staged[s], g + 1);
+                const PcDnSlot& sl = ring[s];
+                const int i0 = g * PC_G;
+                const int n = len - i0 < PC_G ? len - i0 : PC_G;
+                for (int k = 0; k < n; ++k) {
+                    if (i0 + k == 0 && parent < 0) {
+                        // y already holds A_up of the root
+                    } else {
+                        y = fma(sl.S[k], y, sl.T[k][lane]);
+                    }
+                    if (act) A[(size_t)(r0 + i0 + k - ts) * pt] = y;
+                }
+                pc_publish_ordered(&s_freed, g + 1);
+            }
         }
     }
 }
@@ -1374,12 +1562,27 @@ hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_l
     return hipGetLastError();
 }
 
-hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths) {
+hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths,
+                           bool chains) {
     if (t_hi <= t_lo || nrounds <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(d.plan_cnt, 0, sizeof(int32_t) * PMS_NCLS * (size_t)nrounds, st);
+    hipError_t e = hipMemsetAsync(d.plan_cnt, 0, sizeof(int32_t) * PMS_NCNT * (size_t)nrounds, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pms_plan, dim3(blocks((size_t)std::max(max_paths, 1), 1024), (unsigned)nrounds), dim3(1024), 0, st, d,
-                       phase, t_lo, t_hi);
+                       phase, t_lo, t_hi, chains ? PMS_CHAIN_LEN : INT_MAX);
+    return hipGetLastError();
+}
+
+hipError_t launch_pms_chain(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int items) {
+    if (items <= 0) return hipSuccess;
+    const size_t lds = up ? PC_NSU * sizeof(PcUpSlot) : PC_NSD * sizeof(PcDnSlot);
+    static const hipError_t a0 = hipFuncSetAttribute((const void*)k_pms_chain<true>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_NSU * sizeof(PcUpSlot)));
+    static const hipError_t a1 = hipFuncSetAttribute((const void*)k_pms_chain<false>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_NSD * sizeof(PcDnSlot)));
+    if (a0 != hipSuccess) return a0;
+    if (a1 != hipSuccess) return a1;
+    if (up) hipLaunchKernelGGL(k_pms_chain<true>, dim3((unsigned)items), dim3(64 * (PC_LW + 1)), lds, st, d, phase, r);
+    else hipLaunchKernelGGL(k_pms_chain<false>, dim3((unsigned)items), dim3(64 * (PC_LW + 1)), lds, st, d, phase, r);
     return hipGetLastError();
 }
 

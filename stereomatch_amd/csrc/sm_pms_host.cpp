@@ -22,6 +22,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <chrono>
+#include <cstdio>
 
 namespace {
 
@@ -158,6 +160,9 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
                      PmsForest& f, int piece, int nthreads) {
     const int N = W * H;
     if (nthreads <= 0) nthreads = pms_prep_threads();
+    static const bool dbg = getenv("SM_PREP_DEBUG") != nullptr;  // phase times on stderr (diagnostics)
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double tp0 = dbg ? now() : 0.0;
     // 1. trees
     std::vector<int32_t> uf(N), tree_of(N);
     for (int p = 0; p < N; ++p) uf[p] = p;
@@ -198,6 +203,7 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
     std::vector<int> order(K);
     for (int t = 0; t < K; ++t) order[t] = t;
     std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return tsize[a] > tsize[c]; });
+    const double tp1 = dbg ? now() : 0.0;
     // 2. per tree: BFS, heavy paths, rows
     Bfs b;
     b.pix.resize(N);
@@ -206,7 +212,7 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
     b.w.resize(N);
     b.nch.resize(N);
     b.child.resize(4 * (size_t)N);
-    std::vector<int32_t> size(N), heavy(N), ld(N), rowof(N), tmaxld(K, 0);
+    std::vector<int32_t> size(N), heavy(N), ld(N), rowof(N), tmaxld(K, 0), hd(N), off(N), plen(N), rowstart(N);
     std::vector<std::vector<PmsPath>> tp(K);
     std::vector<std::vector<int32_t>> tpld(K);
     f.rows.resize(N);
@@ -266,23 +272,31 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
             }
         }
         tmaxld[t] = mld;
-        // heads by (light depth, BFS id): a counting sort; each path head-first on consecutive rows
+        // heads by (light depth, BFS id): a counting sort; each path head-first on consecutive rows.  In
+        // BFS order (parents first) every node learns its path's head and its offset on the path, so the
+        // rows come from forward passes instead of walking each heavy chain (pointer chasing)
         std::vector<int32_t> cnt(mld + 2, 0);
-        for (int n = ts; n < te; ++n)
-            if (n == ts || heavy[b.parent[n]] != n) ++cnt[ld[n] + 1];
+        for (int n = ts; n < te; ++n) {
+            const bool head = n == ts || heavy[b.parent[n]] != n;
+            hd[n] = head ? n : hd[b.parent[n]];
+            off[n] = head ? 0 : off[b.parent[n]] + 1;
+            plen[hd[n]] = off[n] + 1;  // the chain's nodes come in increasing offset
+            if (head) ++cnt[ld[n] + 1];
+        }
         for (int l = 0; l <= mld; ++l) cnt[l + 1] += cnt[l];
         std::vector<int32_t> heads(cnt[mld + 1]);
         for (int n = ts; n < te; ++n)
-            if (n == ts || heavy[b.parent[n]] != n) heads[cnt[ld[n]]++] = n;
+            if (hd[n] == n) heads[cnt[ld[n]]++] = n;
         int row = ts;
         tp[t].reserve(heads.size());
         tpld[t].reserve(heads.size());
         for (int h : heads) {
-            const int r0 = row;
-            for (int n = h; n >= 0; n = heavy[n]) rowof[n] = row++;
-            tp[t].push_back(PmsPath{t, r0, row - r0, 0});
+            rowstart[h] = row;
+            tp[t].push_back(PmsPath{t, row, plen[h], 0});
             tpld[t].push_back(ld[h]);
+            row += plen[h];
         }
+        for (int n = ts; n < te; ++n) rowof[n] = rowstart[hd[n]] + off[n];
         for (int n = ts; n < te; ++n) {
             PmsRow& R = f.rows[rowof[n]];
             const int p = b.pix[n];
@@ -305,6 +319,7 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
             }
         }
     });
+    const double tp2 = dbg ? now() : 0.0;
     f.bfs_pix = std::move(b.pix);
     // 3. tree_g: inter-tree grid edges of row bands, both directions, sorted and deduplicated
     {
@@ -358,7 +373,8 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
     f.tree_rounds.resize(K);
     for (int t = 0; t < K; ++t) f.tree_rounds[t] = tmaxld[t] + 1;
     const size_t K1 = (size_t)K + 1;
-    std::vector<int32_t> cp((size_t)rmax * K1, 0), ci((size_t)rmax * K1, 0), cr((size_t)rmax * K1, 0);
+    std::vector<int32_t> cp((size_t)rmax * K1, 0), ci((size_t)rmax * K1, 0), cr((size_t)rmax * K1, 0),
+        cl((size_t)rmax * K1, 0);
     auto chunks_of = [&f](int t) { return (f.nb_start[t + 1] - f.nb_start[t] + 63) / 64; };
     parallel_for(K, nthreads, [&](int t) {
         const int chunks = chunks_of(t);
@@ -370,22 +386,29 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
             cp[k] += np;
             ci[k] += np * chunks;
             if (cut) cr[k] += std::max(chunks, 1);
+            for (int q = 0; q < np; ++q) {  // the pieces' lengths (as the fill below)
+                const int len = !cut ? pa.len : (q + 1 < np ? f.piece : pa.len - q * f.piece);
+                if (len >= SM_PMS_CHAIN_LEN) cl[k] += std::max(chunks, 1);
+            }
         }
     });
     f.rt_path.assign((size_t)rmax * K1, 0);
     f.rt_item.assign((size_t)rmax * K1, 0);
     f.rt_rep.assign((size_t)rmax * K1, 0);
-    int32_t sp = 0, si = 0, sr = 0;
+    f.rt_long.assign((size_t)rmax * K1, 0);
+    int32_t sp = 0, si = 0, sr = 0, sl = 0;
     for (int r = 0; r < rmax; ++r)
         for (int t = 0; t <= K; ++t) {
             const size_t k = (size_t)r * K1 + t;
             f.rt_path[k] = sp;
             f.rt_item[k] = si;
             f.rt_rep[k] = sr;
+            f.rt_long[k] = sl;
             if (t < K) {
                 sp += cp[k];
                 si += ci[k];
                 sr += cr[k];
+                sl += cl[k];
             }
         }
     f.paths.resize(sp);
@@ -417,6 +440,10 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
             }
         }
     });
+    if (dbg)
+        fprintf(stderr, "pms_build_forest %dx%d K %d threads %d: trees (union-find) %.1f ms, BFS + paths + rows %.1f ms, "
+                "tree graph + lists %.1f ms (largest tree %d nodes)\n", W, H, K, nthreads, tp1 - tp0, tp2 - tp1, now() - tp2,
+                K ? tsize[order[0]] : 0);
     // the fills advanced each (round, tree) start to the next one's: shift back
     for (auto* v : {&f.rt_path, &f.rt_item, &f.rt_rep}) {
         std::vector<int32_t>& a = *v;

@@ -21,6 +21,9 @@ struct PmsRow {
     uint16_t x, y;      // pixel coordinates
 };
 
+// Paths (and pieces) of at least this many rows are walked by the chain kernel (sm_pms.hip k_pms_chain)
+#define SM_PMS_CHAIN_LEN 96
+
 // A heavy path: rows [row, row + len), head first.
 struct PmsPath {
     int32_t tree, row, len, pad;
@@ -66,6 +69,7 @@ struct PmsForest {
     std::vector<int32_t> cut_round;   // per cut: its round (light depth)
     std::vector<PmsRep> reps;         // round-major
     std::vector<int32_t> rt_rep;      // nrounds x (K+1)
+    std::vector<int32_t> rt_long;     // nrounds x (K+1): paths / pieces of >= SM_PMS_CHAIN_LEN rows x max(1, chunks)
 };
 
 // glibc's random() after srandom(seed) (TYPE_3, the generator sm_pms_glibc_random restates), as a state:
