@@ -24,6 +24,7 @@
 #include "sm_launch.h"
 #include "sm_layout_gpu.h"
 #include "sm_pms.h"
+#include "sm_pms_forest.h"
 #include "sm_reduce_rule.h"
 #include "sm_seg_gpu.h"
 #include "sm_segment.h"
@@ -76,8 +77,16 @@ struct PinnedVec {
 
 // MST_PMS state of one view (SM_AGG_PMS, sm_pms.hip): the host forest and schedule, their device
 // copies, labels, aggregation rows, cost rows and the speculation scratch
+// buffers of the GPU forest build (sm_pms_forest.hip), kept between calls
+struct PfBufs {
+    DevBuf par, flag, tree_of, nbr, nbw, root_pix, tsize, gpix, gpar, gtree, gw, gfc, gnc, gsize, ghk, glev, nlev, iota,
+        bglob, gtree_s, g2b, bpar, bch0, J0, J1, D0, D1, plen, ld, rowof, rowstart, hflag, hidx, hkey0, hkey1, cutof,
+        hcnt[4], hoff[4], rtc[4], rt[4], pairs0, pairs1, npairs, uflag, uidx, nbcnt, cut_round, tree_cut, tot, temp;
+};
+
 struct PmsState {
     PmsForest f;
+    PfBufs pf;
     DevBuf rows, rtree, paths, items, rt_path, rt_item, tree_rounds, tree_start, bfs_pix, nb_start, nb, tree_pt, tree_abase,
         tree_lab, nref, lab, labq, abc, minc, abc_bak, minc_bak, A, vrows, off, oguess, cnt, flag, result, prof, cuts, reps,
         cut_bak, Abak, labu, nprop, rep_flag, pt_ph, ab_ph, plan_cnt, plan_path, plan_item, plan_base, plan_ibase;
@@ -1526,7 +1535,8 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
         abase += (long long)(f.tree_start[t + 1] - f.tree_start[t]) * pt;
         lab += deg + L;
         deg_sum += deg;
-        for (int r = f.tree_start[t]; r < f.tree_start[t + 1]; ++r) S.h_rtree[r] = t;
+        if (!f.on_device)
+            for (int r = f.tree_start[t]; r < f.tree_start[t + 1]; ++r) S.h_rtree[r] = t;
     }
     S.h_abase[K] = abase;
     S.h_lab[K] = lab;
@@ -1538,25 +1548,29 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
         cut_bak[c] = bak;
         bak += (long long)(f.cuts[c].len - f.piece) * S.h_pt[f.cuts[c].tree];
     }
-    CHECK(upload_vec(ctx, S.cuts, f.cuts));
-    CHECK(upload_vec(ctx, S.reps, f.reps));
+    if (!f.on_device) {
+        CHECK(upload_vec(ctx, S.cuts, f.cuts));
+        CHECK(upload_vec(ctx, S.reps, f.reps));
+    }
     CHECK(ensure(ctx, S.rep_flag, std::max<size_t>(f.reps.size(), 1) * 4));
     CHECK(ensure(ctx, S.pt_ph, (size_t)std::max(K, 1) * 4));
     CHECK(ensure(ctx, S.ab_ph, (size_t)std::max(K, 1) * 8));
     HIPC(hipMemsetAsync(S.rep_flag.p, 0, std::max<size_t>(f.reps.size(), 1) * 4, ctx->st));
     CHECK(upload_vec(ctx, S.cut_bak, cut_bak));
     CHECK(ensure(ctx, S.Abak, (size_t)std::max(bak, 1ll) * 8));
-    CHECK(upload_vec(ctx, S.rows, f.rows));
-    CHECK(upload_vec(ctx, S.rtree, S.h_rtree));
-    CHECK(upload_vec(ctx, S.paths, f.paths));
-    CHECK(upload_vec(ctx, S.items, f.items));
-    CHECK(upload_vec(ctx, S.rt_path, f.rt_path));
-    CHECK(upload_vec(ctx, S.rt_item, f.rt_item));
-    CHECK(upload_vec(ctx, S.tree_rounds, f.tree_rounds));
-    CHECK(upload_vec(ctx, S.tree_start, f.tree_start));
-    CHECK(upload_vec(ctx, S.bfs_pix, f.bfs_pix));
-    CHECK(upload_vec(ctx, S.nb_start, f.nb_start));
-    CHECK(upload_vec(ctx, S.nb, f.nb));
+    if (!f.on_device) {  // the GPU build leaves these in place
+        CHECK(upload_vec(ctx, S.rows, f.rows));
+        CHECK(upload_vec(ctx, S.rtree, S.h_rtree));
+        CHECK(upload_vec(ctx, S.paths, f.paths));
+        CHECK(upload_vec(ctx, S.items, f.items));
+        CHECK(upload_vec(ctx, S.rt_path, f.rt_path));
+        CHECK(upload_vec(ctx, S.rt_item, f.rt_item));
+        CHECK(upload_vec(ctx, S.tree_rounds, f.tree_rounds));
+        CHECK(upload_vec(ctx, S.tree_start, f.tree_start));
+        CHECK(upload_vec(ctx, S.bfs_pix, f.bfs_pix));
+        CHECK(upload_vec(ctx, S.nb_start, f.nb_start));
+        CHECK(upload_vec(ctx, S.nb, f.nb));
+    }
     CHECK(upload_vec(ctx, S.tree_pt, S.h_pt));
     CHECK(upload_vec(ctx, S.tree_abase, S.h_abase));
     CHECK(upload_vec(ctx, S.tree_lab, S.h_lab));
@@ -1587,9 +1601,9 @@ sm_status pms_upload_view(sm_ctx* ctx, int v, int L) {
         CHECK(upload_vec(ctx, S.plan_base, pb));
         CHECK(upload_vec(ctx, S.plan_ibase, ib));
         CHECK(ensure(ctx, S.plan_cnt, (size_t)std::max(R, 1) * PMS_NCNT * 4));
-        CHECK(ensure(ctx, S.plan_path, (size_t)std::max<size_t>(f.paths.size(), 1) * (PMS_NCLS - 1) * 4));
+        CHECK(ensure(ctx, S.plan_path, (size_t)std::max(f.npaths, 1) * (PMS_NCLS - 1) * 4));
         // wave items at [0, cap), chain items at [cap, 2 cap)
-        CHECK(ensure(ctx, S.plan_item, 2 * (size_t)std::max<size_t>(f.items.size() + f.paths.size(), 1) * sizeof(PmsItem)));
+        CHECK(ensure(ctx, S.plan_item, 2 * (size_t)std::max(f.nitems + f.npaths, 1) * sizeof(PmsItem)));
     }
     return SM_OK;
 }
@@ -1646,8 +1660,8 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.plan_item = P<PmsItem>(S.plan_item);
     d.plan_base = P<int32_t>(S.plan_base);
     d.plan_ibase = P<int32_t>(S.plan_ibase);
-    d.npaths_total = (int)S.f.paths.size();
-    d.item_cap = (int)std::max<size_t>(S.f.items.size() + S.f.paths.size(), 1);
+    d.npaths_total = S.f.npaths;
+    d.item_cap = std::max(S.f.nitems + S.f.npaths, 1);
     d.Abak = P<double>(S.Abak);
     d.rep_flag = P<uint32_t>(S.rep_flag);
     d.piece = S.f.piece;
@@ -1710,7 +1724,9 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
             // virtual tasks: at most one per path of the classes, plus the chunks of the rest
             bound[r] = std::min(PMS_WALK_WAVES, np + (phase == 0 ? rt[r * K1 + t_hi] - rt[r * K1 + t_lo] : 0));
         }
-        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains));
+        // SM_PMS_CHAIN_MIN: the chain threshold (at least SM_PMS_CHAIN_LEN, whose counts bound the grid)
+        const char* cm = getenv("SM_PMS_CHAIN_MIN");
+        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains ? (cm ? atoi(cm) : SM_PMS_CHAIN_LEN) : 0));
     }
     // pieces: every guessed piece repairs at once, then a gated sequential pass (SM_PMS_SEQ_REPAIR=1: the
     // sequential pass alone, A/B); maxp[r] = the most pieces of a cut repaired in round r
@@ -1862,6 +1878,166 @@ sm_status pms_speculative_call(sm_ctx* ctx, PmsRun& run, int v, PmsDev& d) {
     return SM_OK;
 }
 
+// The schedule forest of view v on the GPU (sm_pms_forest.hip), from the segmentation's device masks, on
+// stream st: the outputs go straight into the PmsState buffers the kernels read; the host keeps the
+// per-tree and per-round tables (K, tree_start, nb_start, rounds, cuts, repair items, round lists).
+sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
+    PmsState& S = ctx->pms[v];
+    PfBufs& B = S.pf;
+    PmsForest& f = S.f;
+    const int W = ctx->W, H = ctx->H, N = W * H;
+    const size_t n1 = (size_t)N + 1;
+    PfView pv{};
+    pv.W = W;
+    pv.H = H;
+    pv.N = N;
+    pv.mR = P<uint8_t>(ctx->mR[v]);
+    pv.mD = P<uint8_t>(ctx->mD[v]);
+    pv.fwR = P<uint16_t>(ctx->fwR[v]);
+    pv.fwD = P<uint16_t>(ctx->fwD[v]);
+    pv.wR = P<uint16_t>(ctx->wR[v]);
+    pv.wD = P<uint16_t>(ctx->wD[v]);
+    pv.piece = piece;
+    struct A {
+        DevBuf* b;
+        size_t bytes;
+        void** out;
+    };
+    const A bufs[] = {
+        {&B.par, n1 * 4, (void**)&pv.par}, {&B.flag, n1 * 4, (void**)&pv.flag}, {&B.tree_of, n1 * 4, (void**)&pv.tree_of},
+        {&B.nbr, n1 * 16, (void**)&pv.nbr}, {&B.nbw, n1 * 8, (void**)&pv.nbw}, {&B.root_pix, n1 * 4, (void**)&pv.root_pix},
+        {&B.tsize, n1 * 4, (void**)&pv.tsize}, {&B.gpix, n1 * 4, (void**)&pv.gpix}, {&B.gpar, n1 * 4, (void**)&pv.gpar},
+        {&B.gtree, n1 * 4, (void**)&pv.gtree}, {&B.gw, n1 * 2, (void**)&pv.gw}, {&B.gfc, n1 * 4, (void**)&pv.gfc},
+        {&B.gnc, n1, (void**)&pv.gnc}, {&B.gsize, n1 * 4, (void**)&pv.gsize}, {&B.ghk, n1, (void**)&pv.ghk},
+        {&B.glev, (n1 + 2) * 4, (void**)&pv.glev}, {&B.nlev, 16, (void**)&pv.nlev}, {&B.iota, n1 * 4, (void**)&pv.iota},
+        {&B.bglob, n1 * 4, (void**)&pv.bglob}, {&B.gtree_s, n1 * 4, (void**)&pv.gtree_s}, {&B.g2b, n1 * 4, (void**)&pv.g2b},
+        {&B.bpar, n1 * 4, (void**)&pv.bpar}, {&B.bch0, n1 * 4, (void**)&pv.bch0}, {&B.J0, n1 * 4, (void**)&pv.J[0]},
+        {&B.J1, n1 * 4, (void**)&pv.J[1]}, {&B.D0, n1 * 4, (void**)&pv.Dj[0]}, {&B.D1, n1 * 4, (void**)&pv.Dj[1]},
+        {&B.plen, n1 * 4, (void**)&pv.plen}, {&B.ld, n1 * 4, (void**)&pv.ld}, {&B.rowof, n1 * 4, (void**)&pv.rowof},
+        {&B.rowstart, n1 * 4, (void**)&pv.rowstart}, {&B.hflag, n1 * 4, (void**)&pv.hflag}, {&B.hidx, n1 * 4, (void**)&pv.hidx},
+        {&B.hkey0, n1 * 8, (void**)&pv.hkey[0]}, {&B.hkey1, n1 * 8, (void**)&pv.hkey[1]}, {&B.cutof, n1 * 4, (void**)&pv.cutof},
+        {&B.hcnt[0], n1 * 4, (void**)&pv.hcnt[0]}, {&B.hcnt[1], n1 * 4, (void**)&pv.hcnt[1]},
+        {&B.hcnt[2], n1 * 4, (void**)&pv.hcnt[2]}, {&B.hcnt[3], n1 * 4, (void**)&pv.hcnt[3]},
+        {&B.hoff[0], n1 * 4, (void**)&pv.hoff[0]}, {&B.hoff[1], n1 * 4, (void**)&pv.hoff[1]},
+        {&B.hoff[2], n1 * 4, (void**)&pv.hoff[2]}, {&B.hoff[3], n1 * 4, (void**)&pv.hoff[3]},
+        {&B.pairs0, 4 * n1 * 8, (void**)&pv.pairs[0]}, {&B.pairs1, 4 * n1 * 8, (void**)&pv.pairs[1]},
+        {&B.npairs, 16, (void**)&pv.npairs}, {&B.uflag, 4 * n1 * 4, (void**)&pv.uflag}, {&B.uidx, 4 * n1 * 4, (void**)&pv.uidx},
+        {&B.nbcnt, n1 * 4, (void**)&pv.nbcnt}, {&B.cut_round, n1 * 4, (void**)&pv.cut_round},
+        {&B.tree_cut, n1 * 4, (void**)&pv.tree_cut}, {&B.tot, 64, (void**)&pv.tot},
+        // outputs the PMS kernels read (K <= N, rows = N)
+        {&S.rows, (size_t)N * sizeof(PmsRow), (void**)&pv.rows}, {&S.rtree, (size_t)N * 4, (void**)&pv.rtree},
+        {&S.bfs_pix, (size_t)N * 4, (void**)&pv.bfs_pix}, {&S.nb_start, n1 * 4, (void**)&pv.nb_start},
+        {&S.nb, 4 * n1 * 4, (void**)&pv.nb}, {&S.tree_start, n1 * 4, (void**)&pv.tree_start},
+        {&S.tree_rounds, n1 * 4, (void**)&pv.tree_rounds}, {&S.cuts, n1 * sizeof(PmsCut), (void**)&pv.cuts},
+    };
+    for (const A& a : bufs) {
+        CHECK(ensure(ctx, *a.b, a.bytes));
+        *a.out = a.b->p;
+    }
+    pv.temp_bytes = pf_temp_bytes(N);
+    CHECK(ensure(ctx, B.temp, pv.temp_bytes));
+    pv.temp = B.temp.p;
+    int K = 0;
+    HIPC(pf_trees(st, pv, &K));
+    int rb[3];
+    HIPC(pf_bfs(st, pv, K, rb));
+    if (rb[2]) return fail(ctx, SM_ERR_STATE, "MST_PMS: the segment forest's masks contain a cycle");
+    const int R = rb[0], nh = rb[1];
+    const size_t T = (size_t)R * (K + 1) + 1;
+    for (int q = 0; q < 4; ++q) {
+        CHECK(ensure(ctx, B.rtc[q], T * 4));
+        CHECK(ensure(ctx, B.rt[q], T * 4));
+        pv.rtc[q] = P<int32_t>(B.rtc[q]);
+        pv.rt[q] = P<int32_t>(B.rt[q]);
+    }
+    int cnt[6];
+    HIPC(pf_lists(st, pv, K, R, nh, cnt));
+    CHECK(ensure(ctx, S.paths, (size_t)std::max(cnt[0], 1) * sizeof(PmsPath)));
+    CHECK(ensure(ctx, S.items, (size_t)std::max(cnt[1], 1) * sizeof(PmsItem)));
+    CHECK(ensure(ctx, S.reps, (size_t)std::max(cnt[2], 1) * sizeof(PmsRep)));
+    pv.paths = P<PmsPath>(S.paths);
+    pv.items = P<PmsItem>(S.items);
+    pv.reps = P<PmsRep>(S.reps);
+    HIPC(pf_fill(st, pv, nh));
+    // the host's tables
+    f.W = W;
+    f.H = H;
+    f.K = K;
+    f.nrounds = R;
+    f.piece = piece > 0 ? piece : 0;
+    f.npaths = cnt[0];
+    f.nitems = cnt[1];
+    f.on_device = true;
+    f.tree_start.resize(K + 1);
+    f.nb_start.resize(K + 1);
+    f.tree_rounds.resize(K);
+    f.tree_cut.resize(K + 1);
+    f.cuts.resize(cnt[4]);
+    f.cut_round.resize(cnt[4]);
+    f.reps.resize(cnt[2]);
+    std::vector<int32_t>* rts[4] = {&f.rt_path, &f.rt_item, &f.rt_rep, &f.rt_long};
+    for (int q = 0; q < 4; ++q) {
+        rts[q]->resize((size_t)R * (K + 1));
+        HIPC(hipMemcpyAsync(rts[q]->data(), B.rt[q].p, (size_t)R * (K + 1) * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPC(hipMemcpyAsync(f.tree_start.data(), S.tree_start.p, (K + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(f.nb_start.data(), S.nb_start.p, (K + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(f.tree_rounds.data(), S.tree_rounds.p, K * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(f.tree_cut.data(), B.tree_cut.p, (K + 1) * 4, hipMemcpyDeviceToHost, st));
+    if (cnt[4]) {
+        HIPC(hipMemcpyAsync(f.cuts.data(), S.cuts.p, cnt[4] * sizeof(PmsCut), hipMemcpyDeviceToHost, st));
+        HIPC(hipMemcpyAsync(f.cut_round.data(), B.cut_round.p, cnt[4] * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (cnt[2]) HIPC(hipMemcpyAsync(f.reps.data(), S.reps.p, cnt[2] * sizeof(PmsRep), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    f.rows.clear();
+    f.paths.clear();
+    f.items.clear();
+    f.bfs_pix.clear();
+    f.nb.clear();
+    return SM_OK;
+}
+
+// SM_PMS_FOREST_CHECK=1 (tests): the GPU forest of view v against the host construction, array by array
+sm_status pms_forest_check(sm_ctx* ctx, int v, hipStream_t st, const PmsForest& h) {
+    const PmsState& S = ctx->pms[v];
+    const PmsForest& g = S.f;
+    auto bad = [&](const char* what) { return fail(ctx, SM_ERR_STATE, std::string("MST_PMS GPU forest differs from the host build: ") + what); };
+    if (g.K != h.K || g.nrounds != h.nrounds || g.npaths != h.npaths || g.nitems != h.nitems) return bad("sizes");
+    if (g.tree_start != h.tree_start) return bad("tree_start");
+    if (g.nb_start != h.nb_start) return bad("nb_start");
+    if (g.tree_rounds != h.tree_rounds) return bad("tree_rounds");
+    if (g.tree_cut != h.tree_cut || g.cut_round != h.cut_round) return bad("tree_cut / cut_round");
+    if (g.rt_path != h.rt_path || g.rt_item != h.rt_item || g.rt_rep != h.rt_rep || g.rt_long != h.rt_long) return bad("round lists");
+    if (g.cuts.size() != h.cuts.size() || (g.cuts.size() && memcmp(g.cuts.data(), h.cuts.data(), g.cuts.size() * sizeof(PmsCut))))
+        return bad("cuts");
+    if (g.reps.size() != h.reps.size() || (g.reps.size() && memcmp(g.reps.data(), h.reps.data(), g.reps.size() * sizeof(PmsRep))))
+        return bad("reps");
+    const size_t N = (size_t)g.W * g.H;
+    std::vector<PmsRow> rows(N);
+    std::vector<PmsPath> paths(g.npaths);
+    std::vector<PmsItem> items(g.nitems);
+    std::vector<int32_t> pix(N), nb(h.nb.size()), rtree(N);
+    HIPC(hipMemcpyAsync(rows.data(), S.rows.p, N * sizeof(PmsRow), hipMemcpyDeviceToHost, st));
+    if (g.npaths) HIPC(hipMemcpyAsync(paths.data(), S.paths.p, paths.size() * sizeof(PmsPath), hipMemcpyDeviceToHost, st));
+    if (g.nitems) HIPC(hipMemcpyAsync(items.data(), S.items.p, items.size() * sizeof(PmsItem), hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(pix.data(), S.bfs_pix.p, N * 4, hipMemcpyDeviceToHost, st));
+    if (!nb.empty()) HIPC(hipMemcpyAsync(nb.data(), S.nb.p, nb.size() * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(rtree.data(), S.rtree.p, N * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    if (pix != h.bfs_pix) return bad("bfs_pix");
+    if (nb != h.nb) return bad("nb");
+    if (memcmp(rows.data(), h.rows.data(), N * sizeof(PmsRow))) return bad("rows");
+    if (paths.size() != h.paths.size() || (paths.size() && memcmp(paths.data(), h.paths.data(), paths.size() * sizeof(PmsPath))))
+        return bad("paths");
+    if (items.size() != h.items.size() || (items.size() && memcmp(items.data(), h.items.data(), items.size() * sizeof(PmsItem))))
+        return bad("items");
+    for (int t = 0; t < h.K; ++t)
+        for (int r = h.tree_start[t]; r < h.tree_start[t + 1]; ++r)
+            if (rtree[r] != t) return bad("rtree");
+    return SM_OK;
+}
+
 // SM_AGG_PMS: Stereo3DMST's stereo3dmst() after its cost volume (Stereo3DMST.cpp:805-904) -- segment
 // forests, random plane labels, pms_iters MST_PMS calls on the left view, then on the right, plane
 // disparities.  Runs to completion (host synchronisations between speculative passes).
@@ -1879,28 +2055,70 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     GlibcRandom grnd;
     std::thread skip([&grnd, N] { grnd.seed_skip(1u, (long)(6 * N)); });
     // 1. the forests: the reference's order-dependent segmentation (c = +inf: the MST)
-    const sm_status seg_st = stage_segment(ctx, 3, p->c, p->min_size);
+    // the schedule forests are built on the GPU (sm_pms_forest.hip) from the device masks;
+    // SM_PMS_HOST_FOREST=1: on host threads (pms_build_forest, A/B); SM_PMS_FOREST_CHECK=1 (tests): both,
+    // compared array by array
+    const bool host_forest = getenv("SM_PMS_HOST_FOREST") && atoi(getenv("SM_PMS_HOST_FOREST")) == 1;
+    const bool forest_check = getenv("SM_PMS_FOREST_CHECK") && atoi(getenv("SM_PMS_FOREST_CHECK")) == 1;
+    const sm_status seg_st = stage_segment(ctx, 3, p->c, p->min_size, host_forest || forest_check);
     if (seg_st != SM_OK) {
         skip.join();
         return seg_st;
     }
     st.prep_seg_ms = now_ms() - t0;
-    // 2. reference-numbered forests and walk schedules, both views in parallel
+    // 2. reference-numbered forests and walk schedules, both views in parallel (view 1 on st_pms)
+    if (!ctx->st_pms) {
+        if (hipStreamCreateWithFlags(&ctx->st_pms, hipStreamNonBlocking) != hipSuccess) {
+            skip.join();
+            return fail(ctx, SM_ERR_HIP, "hipStreamCreateWithFlags (MST_PMS view stream)");
+        }
+    }
     {
-        auto build = [ctx, W, H, N](int v) {
+        auto host_build = [ctx, W, H, N](int v, PmsForest& f) {
             std::vector<uint8_t> mR(N), mD(N);
             for (size_t i = 0; i < N; ++i) {
                 mR[i] = ctx->h_m[v][0][i] && ctx->h_fw[v][0][i] != SM_VIRTUAL_W;
                 mD[i] = ctx->h_m[v][1][i] && ctx->h_fw[v][1][i] != SM_VIRTUAL_W;
             }
-            pms_build_forest(W, H, ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), mR.data(), mD.data(), ctx->pms[v].f,
-                             pms_piece());
+            pms_build_forest(W, H, ctx->h_w[v][0].data(), ctx->h_w[v][1].data(), mR.data(), mD.data(), f, pms_piece());
+        };
+        sm_status fs[2] = {SM_OK, SM_OK};
+        auto build = [&](int v) {
+            const hipStream_t sv = v == 0 ? ctx->st : ctx->st_pms;
+            if (host_forest) {
+                host_build(v, ctx->pms[v].f);
+                return;
+            }
+            if (hipSetDevice(ctx->device) != hipSuccess) {
+                fs[v] = SM_ERR_HIP;
+                return;
+            }
+            fs[v] = pms_forest_gpu(ctx, v, sv, pms_piece());
+            if (fs[v] == SM_OK && forest_check) {
+                PmsForest h;
+                host_build(v, h);
+                fs[v] = pms_forest_check(ctx, v, sv, h);
+            }
         };
         const double tf = now_ms();
-        std::thread other(build, 1);
+        HIPC(hipEventRecord(ctx->ev_pms, ctx->st));
+        HIPC(hipStreamWaitEvent(ctx->st_pms, ctx->ev_pms, 0));  // the segmentation's masks
+        std::thread other([&] {
+            try {
+                build(1);
+            } catch (const std::bad_alloc&) {
+                fs[1] = SM_ERR_OOM;
+            } catch (...) {
+                fs[1] = SM_ERR_STATE;
+            }
+        });
         build(0);
         other.join();
         st.prep_forest_ms = now_ms() - tf;
+        if (fs[0] != SM_OK || fs[1] != SM_OK) {
+            skip.join();
+            return fs[0] != SM_OK ? fs[0] : fs[1];
+        }
     }
     // 3. random streams: the replayed dice prefix, the rand() values of every call (after random_rgb's
     // 3 draws per pixel of both views), the initial labels (one stream, so both views start equal)
@@ -1958,7 +2176,6 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     // evaluations each call needed are counted on the device (k_pms_count).
     const bool serial_only = pms_serial_only();
     const bool seq_views = getenv("SM_PMS_SEQ_VIEWS") && atoi(getenv("SM_PMS_SEQ_VIEWS")) == 1;
-    if (!ctx->st_pms) HIPC(hipStreamCreateWithFlags(&ctx->st_pms, hipStreamNonBlocking));
     CHECK(ensure(ctx, ctx->pms_evals, 16 * 8));
     HIPC(hipMemsetAsync(ctx->pms_evals.p, 0, 16 * 8, ctx->st));
     HIPC(hipEventRecord(ctx->ev_pms, ctx->st));

@@ -98,9 +98,10 @@ hipError_t launch_pms_chain(hipStream_t st, const PmsDev& d, int phase, bool up,
 hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int32_t* pt_out,
                              long long* ab_out);
 // the walk plan of trees [t_lo, t_hi) for a phase (plan_cnt zeroed here); r_lo..r_hi: rounds to plan
-// chains: paths of >= SM_PMS_CHAIN_LEN rows become chain items (k_pms_chain), else wave items
+// chain_len > 0: paths of >= max(chain_len, SM_PMS_CHAIN_LEN) rows become chain items (k_pms_chain);
+// 0: none (wave items)
 hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths,
-                           bool chains);
+                           int chain_len);
 // one round's planned walk, a persistent grid of `waves` waves (the host's bound on the work)
 hipError_t launch_pms_walk_plan(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int waves);
 hipError_t launch_pms_cost(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);

@@ -585,23 +585,42 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
         }
         for (long long i = tid; i < wn; i += blockDim.x) sdice[i] = o0 + i < d.dice_n ? d.dice[o0 + i] : 0.0f;
         __syncthreads();
-        if (tid == 0) {
+        if (tid < 64) {
+            // The chain on one wave with wave-uniform (scalar) state: each tree's degree, classes and dd come
+            // from a 64-tree register window and each draw-dependent level's draw from a 64-draw register
+            // window, both by readlane, so a link costs no LDS round trip unless a window is refilled.
             long long o = o0;
+            int tw = -64, wdeg = 0, wcls = 0, wdd = 0;
+            long long kw = LLONG_MIN / 2;
+            float wdice = 0.0f;
             for (int t = 0; t < nt; ++t) {
-                sog[t] = o;
-                const int deg = sdeg[2 * t];
-                uint32_t cls = (uint32_t)sdeg[2 * t + 1];
-                const float dd = sdd[t];
+                if (t - tw >= 64) {  // the next 64 trees
+                    tw = t;
+                    const int ti = t + tid;
+                    wdeg = ti < nt ? sdeg[2 * ti] : 0;
+                    wcls = ti < nt ? sdeg[2 * ti + 1] : 0;
+                    wdd = ti < nt ? __float_as_int(sdd[ti]) : 0;
+                }
+                if (tid == 0) sog[t] = o;
+                const int deg = __builtin_amdgcn_readlane(wdeg, t - tw);
+                uint32_t cls = (uint32_t)__builtin_amdgcn_readlane(wcls, t - tw);
+                const float dd = __int_as_float(__builtin_amdgcn_readlane(wdd, t - tw));
                 long long k = o + deg;
                 for (float md = 0.5f * fmax; md > 0.1f; md *= 0.5f, cls >>= 2) {  // ref_count's levels
                     if (k + 4 > d.dice_n) {
-                        atomicOr(d.err, 4u);
+                        if (tid == 0) atomicOr(d.err, 4u);
                         break;
                     }
                     const uint32_t c = cls & 3u;
                     bool in = c == 1u;
                     if (c == 2u) {
-                        const float rd = fmaf(sdice[k - o0], md, dd);
+                        if (k >= kw + 64) {  // the next 64 draws from k
+                            kw = k;
+                            const long long q = k - o0 + tid;
+                            wdice = q < wn ? sdice[q] : 0.0f;
+                        }
+                        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdice), (int)(k - kw)));
+                        const float rd = fmaf(r, md, dd);
                         in = !(rd < 0.0f || rd > fmax);
                     }
                     k += in ? 4 : 1;
@@ -1006,8 +1025,8 @@ __global__ void __launch_bounds__(256) k_pms_walk_plan(PmsDev d, int phase, int 
 // bottom): a loader stages T = S2 * A_up and S, the chain does y = fma(S, y, T); the head reads its
 // parent row (or keeps A_up at a tree root) -- down_walk's operations.  Same bits as the walkers.
 constexpr int PC_G = 8;        // nodes per group
-constexpr int PC_NSU = 6;      // up ring slots (2 KB per node)
-constexpr int PC_NSD = 16;     // down ring slots (0.5 KB per node)
+constexpr int PC_NSU = 4;      // up ring slots (2 KB per node): 67 KB, two workgroups per CU
+constexpr int PC_NSD = 14;     // down ring slots (0.5 KB per node): 58 KB, two workgroups per CU
 constexpr int PC_LW = 7;       // loader waves (+ the chain wave: 512 threads)
 
 struct PcUpSlot {
@@ -1124,16 +1143,33 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
                 const PcUpSlot& sl = ring[s];
                 const int itop = len - 1 - g * PC_G;
                 const int n = itop + 1 < PC_G ? itop + 1 : PC_G;
-                for (int k = 0; k < n; ++k) {
-                    double acc = fma(x, sl.sh[k], sl.pre[k][lane]);  // a leaf: fma(0, 0, +0) = +0
-                    const int np = sl.np[k];
-                    if (np >= 1) acc = fma(sl.p1[k][lane], sl.s1[k], acc);
-                    if (np >= 2) acc = fma(sl.p2[k][lane], sl.s2[k], acc);
-                    if (np >= 3) acc = fma(Al[(size_t)(sl.p3row[k] - ts) * pt], sl.s3[k], acc);
-                    x = sl.cost[k][lane] + acc;
+                // the whole group from LDS in one batch, then the recurrence from registers (absent posts
+                // were staged as 0 with S = 0: fma(0, 0, acc) == acc, aggregates are finite and >= +0)
+                double pre[PC_G], p1[PC_G], p2[PC_G], cst[PC_G], sh[PC_G], s1[PC_G], s2[PC_G];
+                int np3 = 0;
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    pre[k] = sl.pre[k][lane];
+                    p1[k] = sl.p1[k][lane];
+                    p2[k] = sl.p2[k][lane];
+                    cst[k] = sl.cost[k][lane];
+                    sh[k] = sl.sh[k];
+                    s1[k] = sl.s1[k];
+                    s2[k] = sl.s2[k];
+                    np3 |= (sl.np[k] >= 3) << k;
+                }
+                pc_publish_ordered(&s_freed, g + 1);  // the slot's reads are issued: free it
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    if (k >= n) break;
+                    double acc = fma(x, sh[k], pre[k]);  // a leaf: fma(0, 0, +0) = +0
+                    acc = fma(p1[k], s1[k], acc);
+                    acc = fma(p2[k], s2[k], acc);
+                    if (__builtin_expect((np3 >> k) & 1, 0))  // a tree root's third post-heavy child
+                        acc = fma(Al[(size_t)(sl.p3row[k] - ts) * pt], sl.s3[k], acc);
+                    x = cst[k] + acc;
                     if (act) A[(size_t)(r0 + itop - k - ts) * pt] = x;
                 }
-                pc_publish_ordered(&s_freed, g + 1);
             }
         }
     } else {
@@ -1171,15 +1207,19 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
                 const PcDnSlot& sl = ring[s];
                 const int i0 = g * PC_G;
                 const int n = len - i0 < PC_G ? len - i0 : PC_G;
-                for (int k = 0; k < n; ++k) {
-                    if (i0 + k == 0 && parent < 0) {
-                        // y already holds A_up of the root
-                    } else {
-                        y = fma(sl.S[k], y, sl.T[k][lane]);
-                    }
-                    if (act) A[(size_t)(r0 + i0 + k - ts) * pt] = y;
+                double T[PC_G], S[PC_G];
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    T[k] = sl.T[k][lane];
+                    S[k] = sl.S[k];
                 }
                 pc_publish_ordered(&s_freed, g + 1);
+#pragma unroll
+                for (int k = 0; k < PC_G; ++k) {
+                    if (k >= n) break;
+                    if (!(i0 + k == 0 && parent < 0)) y = fma(S[k], y, T[k]);  // a tree root keeps A_up
+                    if (act) A[(size_t)(r0 + i0 + k - ts) * pt] = y;
+                }
             }
         }
     }
@@ -1563,12 +1603,12 @@ hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_l
 }
 
 hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths,
-                           bool chains) {
+                           int chain_len) {
     if (t_hi <= t_lo || nrounds <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(d.plan_cnt, 0, sizeof(int32_t) * PMS_NCNT * (size_t)nrounds, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pms_plan, dim3(blocks((size_t)std::max(max_paths, 1), 1024), (unsigned)nrounds), dim3(1024), 0, st, d,
-                       phase, t_lo, t_hi, chains ? PMS_CHAIN_LEN : INT_MAX);
+                       phase, t_lo, t_hi, chain_len > 0 ? std::max(chain_len, PMS_CHAIN_LEN) : INT_MAX);
     return hipGetLastError();
 }
 

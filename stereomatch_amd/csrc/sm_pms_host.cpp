@@ -444,6 +444,9 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
         fprintf(stderr, "pms_build_forest %dx%d K %d threads %d: trees (union-find) %.1f ms, BFS + paths + rows %.1f ms, "
                 "tree graph + lists %.1f ms (largest tree %d nodes)\n", W, H, K, nthreads, tp1 - tp0, tp2 - tp1, now() - tp2,
                 K ? tsize[order[0]] : 0);
+    f.npaths = (int)f.paths.size();
+    f.nitems = (int)f.items.size();
+    f.on_device = false;
     // the fills advanced each (round, tree) start to the next one's: shift back
     for (auto* v : {&f.rt_path, &f.rt_item, &f.rt_rep}) {
         std::vector<int32_t>& a = *v;

@@ -70,6 +70,9 @@ struct PmsForest {
     std::vector<PmsRep> reps;         // round-major
     std::vector<int32_t> rt_rep;      // nrounds x (K+1)
     std::vector<int32_t> rt_long;     // nrounds x (K+1): paths / pieces of >= SM_PMS_CHAIN_LEN rows x max(1, chunks)
+    int npaths = 0, nitems = 0;       // list sizes (the host build: paths.size(), items.size())
+    bool on_device = false;           // built on the GPU (sm_pms_forest.hip): rows, paths, items, bfs_pix, nb
+                                      // and the row -> tree map live in device buffers only
 };
 
 // glibc's random() after srandom(seed) (TYPE_3, the generator sm_pms_glibc_random restates), as a state:

@@ -235,3 +235,37 @@ def test_pms_flir_c1_two_calls_output_step(gpu_ctx, monkeypatch):
     np.testing.assert_array_equal(u32(out["right"]["disp"].ravel()), u32(ref["right"]["disp"].ravel()))
     np.testing.assert_array_equal(u32(out["left"]["disp"].ravel()), u32(ref["left"]["disp_checked"].ravel()))
     assert st["spec_rounds"] >= 2
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case", ["golden5000", "golden300", "synth300", "many_trees", "pieces16", "mst_mode", "full_c2"])
+def test_pms_gpu_forest_matches_host_build(gpu_ctx, monkeypatch, case):
+    """The schedule forest built on the GPU (sm_pms_forest.hip: union-find tree numbering, the level-order
+    BFS of every tree, heavy paths, rows, tree graph, round lists) against the host construction
+    (pms_build_forest), array by array (SM_PMS_FOREST_CHECK=1 makes the call fail on any difference), then
+    the call's labels against the oracle."""
+    monkeypatch.setenv("SM_PMS_FOREST_CHECK", "1")
+    monkeypatch.delenv("SM_PMS_HOST_FOREST", raising=False)
+    if case == "pieces16":
+        monkeypatch.setenv("SM_PMS_PIECE", "16")
+    else:
+        monkeypatch.delenv("SM_PMS_PIECE", raising=False)
+    if case.startswith("golden"):
+        z = load_case("smooth_97x61")
+        left, right, D = z["left"], z["right"], int(z["D"])
+        c, ms = (5000.0, 200) if case == "golden5000" else (300.0, 20)
+    elif case == "synth300":
+        (left, right, _), D, c, ms = make_pair(160, 120, 48, index=3), 48, 300.0, 20
+    elif case == "many_trees":
+        (left, right, _), D, c, ms = make_pair(640, 480, 32, index=9), 32, 5.0, 2
+    elif case == "pieces16":
+        (left, right, _), D, c, ms = make_pair(192, 128, 48, index=7), 48, 5000.0, 200
+    elif case == "mst_mode":
+        (left, right, _), D, c, ms = make_pair(200, 150, 32, index=2), 32, float("inf"), 200
+    else:
+        (left, right, _), D, c, ms = make_pair(1920, 1200, 128, index=0), 128, 5000.0, 200
+    iters = 1 if case == "full_c2" else 2
+    ref = O.stereo3dmst_pms(left, right, D, iters=iters, c=c, min_size=ms)
+    out, labs, st = run_gpu(gpu_ctx, left, right, D, iters, c, ms)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
