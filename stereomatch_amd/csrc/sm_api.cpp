@@ -1941,7 +1941,8 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
     HIPC(pf_trees(st, pv, &K));
     int rb[3];
     HIPC(pf_bfs(st, pv, K, rb));
-    if (rb[2]) return fail(ctx, SM_ERR_STATE, "MST_PMS: the segment forest's masks contain a cycle");
+    if (rb[2]) return fail(ctx, SM_ERR_STATE, rb[2] == 1 ? "MST_PMS: the segment forest's masks contain a cycle"
+                                                         : "MST_PMS GPU forest: unresolved light depths");
     const int R = rb[0], nh = rb[1];
     const size_t T = (size_t)R * (K + 1) + 1;
     for (int q = 0; q < 4; ++q) {
@@ -1950,8 +1951,9 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
         pv.rtc[q] = P<int32_t>(B.rtc[q]);
         pv.rt[q] = P<int32_t>(B.rt[q]);
     }
-    int cnt[6];
+    int cnt[7];
     HIPC(pf_lists(st, pv, K, R, nh, cnt));
+    if (cnt[6]) return fail(ctx, SM_ERR_STATE, "MST_PMS GPU forest: rows out of range");
     CHECK(ensure(ctx, S.paths, (size_t)std::max(cnt[0], 1) * sizeof(PmsPath)));
     CHECK(ensure(ctx, S.items, (size_t)std::max(cnt[1], 1) * sizeof(PmsItem)));
     CHECK(ensure(ctx, S.reps, (size_t)std::max(cnt[2], 1) * sizeof(PmsRep)));

@@ -89,8 +89,10 @@ struct PfView {
 size_t pf_temp_bytes(int N);
 // steps of the build; each ends with a host sync for the sizes the next one allocates by
 hipError_t pf_trees(hipStream_t st, PfView& v, int* K_out);   // union-find, tree ids, sizes
-// BFS, sizes, heavy paths, light depths; out[0] = rounds, out[1] = heads, out[2] = 1 if the masks had a cycle
+// BFS, sizes, heavy paths, light depths; out[0] = rounds, out[1] = heads, out[2] != 0: the masks had a cycle (1)
+// or a light depth stayed unresolved (2)
 hipError_t pf_bfs(hipStream_t st, PfView& v, int K, int* out);
-// rows, cuts, tree graph, round-major counts and tables; counts: paths, items, reps, chain items, cuts, pairs
+// rows, cuts, tree graph, round-major counts and tables; counts: paths, items, reps, chain items, cuts, pairs,
+// error flag
 hipError_t pf_lists(hipStream_t st, PfView& v, int K, int nrounds, int nheads, int* counts);
 hipError_t pf_fill(hipStream_t st, PfView& v, int nheads);  // paths, items, repair items

@@ -87,7 +87,9 @@ __device__ void uf_union(int32_t* par, int a, int b) {
             a = b;
             b = t;
         }
-        if (atomicCAS(&par[a], a, b) == a) return;
+        const int old = atomicCAS(&par[a], a, b);
+        if (old == a) return;
+        a = old;  // a was linked meanwhile (to a smaller root): continue from there, never from a stale read
     }
 }
 
@@ -212,11 +214,12 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
         v.glev[d] = a;
         v.nlev[0] = d;
     }
+    __syncthreads();  // the last boundary is read by every wave below
     // bottom up: subtree sizes and heavy children, a level at a time
     for (int l = d - 1; l >= 0; --l) {
-        const int la = v.glev[l], lb = v.glev[l + 1];
+        const int la = min(max(v.glev[l], 0), v.N), lb = min(max(v.glev[l + 1], la), v.N);
         for (int i = la + tid; i < lb; i += BT) {
-            const int c = v.gnc[i], f = v.gfc[i];
+            const int f = v.gfc[i], c = min((int)v.gnc[i], v.N - f);  // clamp: only a cycle overflows
             int s = 1, best = -1, bs = 0;
             for (int k = 0; k < c; ++k) {
                 const int sk = v.gsize[f + k];
@@ -295,6 +298,10 @@ __global__ void k_pf_ld_all(PfView v, const int32_t* J) {
     const int t = v.gtree_s[n];
     if (J[n] != n) return;
     const int l = v.ld[n];
+    if (l < 0 || l > 255) {  // unresolved light depth: an inconsistent schedule, flag it (never key on it)
+        v.tot[7] = 2;
+        return;
+    }
     atomicMax(&v.tree_rounds[t], l + 1);
     atomicMax(&v.tot[5], l + 1);
 }
@@ -357,6 +364,10 @@ __global__ void k_pf_rows(PfView v) {
     const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (n >= v.N) return;
     const int row = v.rowof[n];
+    if (row < 0 || row >= v.N) {  // guard: an inconsistent schedule is flagged, never written out of bounds
+        v.tot[7] = 3;
+        return;
+    }
     const int i = v.bglob[n];
     const int p = v.gpix[i];
     PmsRow R;
@@ -609,6 +620,7 @@ hipError_t pf_lists(hipStream_t st, PfView& v, int K, int R, int nh, int* counts
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
     for (int q = 0; q < 5; ++q) counts[q] = h[q];  // paths, items, reps, chain items, cuts
     counts[5] = np;
+    counts[6] = h[7];  // != 0: the schedule was inconsistent (rows out of range)
     return hipGetLastError();
 }
 
