@@ -1945,11 +1945,14 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
                                                          : "MST_PMS GPU forest: unresolved light depths");
     const int R = rb[0], nh = rb[1];
     const size_t T = (size_t)R * (K + 1) + 1;
+    // round tables: rt_path and rt_item are kernel inputs (PmsDev), built in place; rt_rep and rt_long are
+    // read on the host only
+    DevBuf* rtb[4] = {&S.rt_path, &S.rt_item, &B.rt[2], &B.rt[3]};
     for (int q = 0; q < 4; ++q) {
         CHECK(ensure(ctx, B.rtc[q], T * 4));
-        CHECK(ensure(ctx, B.rt[q], T * 4));
+        CHECK(ensure(ctx, *rtb[q], T * 4));
         pv.rtc[q] = P<int32_t>(B.rtc[q]);
-        pv.rt[q] = P<int32_t>(B.rt[q]);
+        pv.rt[q] = P<int32_t>(*rtb[q]);
     }
     int cnt[7];
     HIPC(pf_lists(st, pv, K, R, nh, cnt));
@@ -1980,7 +1983,7 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
     std::vector<int32_t>* rts[4] = {&f.rt_path, &f.rt_item, &f.rt_rep, &f.rt_long};
     for (int q = 0; q < 4; ++q) {
         rts[q]->resize((size_t)R * (K + 1));
-        HIPC(hipMemcpyAsync(rts[q]->data(), B.rt[q].p, (size_t)R * (K + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPC(hipMemcpyAsync(rts[q]->data(), rtb[q]->p, (size_t)R * (K + 1) * 4, hipMemcpyDeviceToHost, st));
     }
     HIPC(hipMemcpyAsync(f.tree_start.data(), S.tree_start.p, (K + 1) * 4, hipMemcpyDeviceToHost, st));
     HIPC(hipMemcpyAsync(f.nb_start.data(), S.nb_start.p, (K + 1) * 4, hipMemcpyDeviceToHost, st));
