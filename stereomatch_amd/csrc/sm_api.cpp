@@ -101,11 +101,14 @@ struct PmsState {
 // the min-size candidates, and the host merge's hooks
 struct SegGpu {
     DevBuf par, sz, wl, best, first, ebuf, bcnt, list0, list1, rej, hooked, cnt, mlist, hooks, mkey, mval, msorted, stemp;
+    DevBuf keep, kpos, lmark, lid, dense, lsize, lroot;  // the pair dedupe (seg_launch_dedupe)
     size_t stemp_bytes = 0;
     uint32_t gen = 0;  // next Boruvka generation (keys of older ones lose every atomicMin)
-    PinnedVec<uint32_t> h_b, h_cnt, h_hooks;
+    PinnedVec<uint32_t> h_b, h_cnt, h_hooks, h_lsize, h_lroot;
     PinnedVec<SegMin> h_min;
-    std::vector<uint32_t> loc;  // the host merge's root -> local id table (all ~0 between calls)
+    PinnedVec<SegEdge> h_dense;
+    std::vector<uint32_t> loc;         // SM_SEG_NODEDUP's root -> local id table (all ~0 between calls)
+    std::vector<uint32_t> mpar, msize;  // the merge's union-find over local ids
 };
 
 struct MstPending {
@@ -472,6 +475,9 @@ sm_status segment_upload(sm_ctx* ctx, int views) {
 // SM_SEG_HOST=1: segment mode's segmentation by the host sweep (sm_segment.cpp) instead of the GPU
 bool seg_host() { return getenv("SM_SEG_HOST") != nullptr; }
 
+// SM_SEG_NODEDUP=1: the min-size merge over every candidate (A/B of the GPU pair dedupe)
+bool seg_nodedup() { return getenv("SM_SEG_NODEDUP") != nullptr; }
+
 // Boruvka rounds launched over the whole GPU before a bucket's single-workgroup tail, for buckets of
 // more than SM_SEG_SMALL edges (env SM_SEG_GLOBAL_ROUNDS, default 2)
 int seg_global_rounds() { return getenv("SM_SEG_GLOBAL_ROUNDS") ? atoi(getenv("SM_SEG_GLOBAL_ROUNDS")) : 2; }
@@ -523,6 +529,46 @@ int seg_minsize_host(const SegMin* e, uint32_t n, uint32_t ms, uint32_t* out, st
     return k;
 }
 
+// The same serial rule over the deduplicated candidates (seg_launch_dedupe): the first candidate of each
+// pair of sweep roots, in (w, id) order, with the roots as dense local ids (lsize / lroot: their sizes
+// and pixels).  Same hooks and marked edges as seg_minsize_host over all candidates.
+int seg_minsize_dense(const SegEdge* e, uint32_t n, uint32_t nl, const uint32_t* lsize, const uint32_t* lroot, uint32_t ms,
+                      uint32_t* out, std::vector<uint32_t>& par, std::vector<uint32_t>& size) {
+    par.resize(nl);
+    size.assign(lsize, lsize + nl);
+    for (uint32_t i = 0; i < nl; ++i) par[i] = i;
+    uint32_t* P = par.data();
+    uint32_t* S = size.data();
+    auto find = [P](uint32_t x) {
+        while (P[x] != x) x = P[x] = P[P[x]];
+        return x;
+    };
+    uint32_t* ids = out + 2 * (size_t)n;  // scratch: the marked ids, moved behind the k pairs at the end
+    int k = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        if (j + 16 < n) {
+            __builtin_prefetch(&P[e[j + 16].la]);
+            __builtin_prefetch(&P[e[j + 16].lb]);
+        }
+        uint32_t a = find(e[j].la), b = find(e[j].lb);
+        if (a == b) continue;
+        uint32_t sa = S[a], sb = S[b];
+        if (sa >= ms && sb >= ms) continue;
+        if (sa < sb) {
+            std::swap(a, b);
+            std::swap(sa, sb);
+        }
+        P[b] = a;
+        S[a] = sa + sb;
+        out[2 * k] = lroot[b];
+        out[2 * k + 1] = lroot[a];
+        ids[k] = e[j].id;
+        ++k;
+    }
+    memmove(out + 2 * (size_t)k, ids, (size_t)k * 4);
+    return k;
+}
+
 double now_ms();
 
 // Segment mode's segmentation on the GPU (sm_seg_gpu.h): the masks and layout weights of the forest
@@ -532,6 +578,7 @@ double now_ms();
 // the h_w / h_m / h_fw host arrays as well (MST_PMS, sm_build_tree_p).
 sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_copy) {
     static const bool dbg = getenv("SM_SEG_DEBUG") != nullptr;
+    const bool nodedup = seg_nodedup();
     const double t0 = dbg ? now_ms() : 0.0;
     double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
     const int W = ctx->W, H = ctx->H;
@@ -571,6 +618,13 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         CHECK(ensure(ctx, g.msorted, E * sizeof(SegMin)));
         CHECK(ensure(ctx, g.mkey, E * 16));
         CHECK(ensure(ctx, g.mval, E * 8));
+        CHECK(ensure(ctx, g.keep, (E + 1) * 4));
+        CHECK(ensure(ctx, g.kpos, (E + 1) * 4));
+        CHECK(ensure(ctx, g.lmark, (N + 1) * 4));
+        CHECK(ensure(ctx, g.lid, (N + 1) * 4));
+        CHECK(ensure(ctx, g.dense, E * sizeof(SegEdge)));
+        CHECK(ensure(ctx, g.lsize, N * 4));
+        CHECK(ensure(ctx, g.lroot, N * 4));
         g.stemp_bytes = seg_sort_temp_bytes((uint32_t)E);  // enough for any candidate count (<= E)
         CHECK(ensure(ctx, g.stemp, g.stemp_bytes));
         if (!g.h_b.resize(SM_SEG_NB + 1) || !g.h_cnt.resize(8)) return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
@@ -604,6 +658,13 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         s.mD = P<uint8_t>(ctx->mD[v]);
         s.fwR = P<uint16_t>(ctx->fwR[v]);
         s.fwD = P<uint16_t>(ctx->fwD[v]);
+        s.keep = P<uint32_t>(g.keep);
+        s.kpos = P<uint32_t>(g.kpos);
+        s.lmark = P<uint32_t>(g.lmark);
+        s.lid = P<uint32_t>(g.lid);
+        s.dense = P<SegEdge>(g.dense);
+        s.lsize = P<uint32_t>(g.lsize);
+        s.lroot = P<uint32_t>(g.lroot);
     }
     HIPC(seg_launch_init(st, sp));
     for (int i = 0; i < vs.n; ++i) {
@@ -664,25 +725,48 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         SegGpu& g = ctx->sg[vs.v[i]];
         if (g.h_cnt[SM_SEG_C_ERR]) return fail(ctx, SM_ERR_STATE, "segment mode: a Boruvka tail did not converge");
         const uint32_t nm = g.h_cnt[SM_SEG_C_MIN];
-        if (!g.h_min.resize(nm) || !g.h_hooks.resize(3 * (size_t)nm + 1))
+        if ((nodedup && !g.h_min.resize(nm)) || !g.h_hooks.resize(3 * (size_t)nm + 1))
             return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
         sp.v[i].nmin = nm;
         temp[i] = g.stemp.p;
         tbytes[i] = g.stemp_bytes;
     }
     HIPC(seg_launch_sort(st, sp, temp, tbytes));
-    for (int i = 0; i < vs.n; ++i) {
-        SegGpu& g = ctx->sg[vs.v[i]];
-        if (sp.v[i].nmin)
-            HIPC(hipMemcpyAsync(g.h_min.data(), g.msorted.p, sp.v[i].nmin * sizeof(SegMin), hipMemcpyDeviceToHost, st));
+    if (nodedup) {
+        for (int i = 0; i < vs.n; ++i) {
+            SegGpu& g = ctx->sg[vs.v[i]];
+            if (sp.v[i].nmin)
+                HIPC(hipMemcpyAsync(g.h_min.data(), g.msorted.p, sp.v[i].nmin * sizeof(SegMin), hipMemcpyDeviceToHost, st));
+        }
+    } else {  // the first candidate of each root pair, dense root ids: their counts, then the lists
+        HIPC(seg_launch_dedupe(st, sp, temp, tbytes));
+        for (int i = 0; i < vs.n; ++i)
+            HIPC(hipMemcpyAsync(ctx->sg[vs.v[i]].h_cnt.data() + SM_SEG_C_UNIQ, P<uint32_t>(ctx->sg[vs.v[i]].cnt) + SM_SEG_C_UNIQ,
+                                8, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        for (int i = 0; i < vs.n; ++i) {
+            SegGpu& g = ctx->sg[vs.v[i]];
+            const uint32_t nu = g.h_cnt[SM_SEG_C_UNIQ], nl = g.h_cnt[SM_SEG_C_LOCAL];
+            if (nu > sp.v[i].nmin || nl > 2 * nu) return fail(ctx, SM_ERR_STATE, "segment mode: bad min-size dedupe counts");
+            if (!g.h_dense.resize(nu) || !g.h_lsize.resize(nl) || !g.h_lroot.resize(nl))
+                return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
+            if (nu) HIPC(hipMemcpyAsync(g.h_dense.data(), g.dense.p, nu * sizeof(SegEdge), hipMemcpyDeviceToHost, st));
+            if (nl) {
+                HIPC(hipMemcpyAsync(g.h_lsize.data(), g.lsize.p, nl * 4, hipMemcpyDeviceToHost, st));
+                HIPC(hipMemcpyAsync(g.h_lroot.data(), g.lroot.p, nl * 4, hipMemcpyDeviceToHost, st));
+            }
+        }
     }
     HIPC(hipStreamSynchronize(st));
     if (dbg) t4 = now_ms();
     const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
     int nk[2] = {0, 0};
     {  // the views' merges in parallel
-        auto merge = [ctx, ms, N](int v) {
+        auto merge = [ctx, ms, N, nodedup](int v) {
             SegGpu& g = ctx->sg[v];
+            if (!nodedup)
+                return seg_minsize_dense(g.h_dense.data(), g.h_cnt[SM_SEG_C_UNIQ], g.h_cnt[SM_SEG_C_LOCAL], g.h_lsize.data(),
+                                         g.h_lroot.data(), ms, g.h_hooks.data(), g.mpar, g.msize);
             if (g.loc.size() != N) g.loc.assign(N, 0xFFFFFFFFu);
             return seg_minsize_host(g.h_min.data(), g.h_cnt[SM_SEG_C_MIN], ms, g.h_hooks.data(), g.loc);
         };
@@ -728,8 +812,9 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         fprintf(stderr, "segment_gpu: init+buckets %.2f ms, enqueue %.2f, sweep wait %.2f, min-size copy %.2f, host merge + rest %.2f;",
                 t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4);
         for (int i = 0; i < vs.n; ++i)
-            fprintf(stderr, " view %d: rejected %u, small %u, hooks %u", vs.v[i], ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_REJ],
-                    ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_MIN], ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_HOOK]);
+            fprintf(stderr, " view %d: rejected %u, small %u, first of their pair %u, roots %u, hooks %u", vs.v[i],
+                    ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_REJ], ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_MIN], ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_UNIQ],
+                    ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_LOCAL], ctx->sg[vs.v[i]].h_cnt[SM_SEG_C_HOOK]);
         fprintf(stderr, "\n");
     }
     return SM_OK;

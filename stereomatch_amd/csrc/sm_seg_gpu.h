@@ -34,6 +34,8 @@
 #define SM_SEG_C_TREES 2
 #define SM_SEG_C_MIN 3
 #define SM_SEG_C_ERR 4
+#define SM_SEG_C_UNIQ 5   // candidates that are the first of their root pair (k_seg_dense)
+#define SM_SEG_C_LOCAL 6  // distinct roots of those (dense local ids)
 #define SM_SEG_C_LIST 8
 #define SM_SEG_C_BUCKET (8 + SM_SEG_MAXL)
 #define SM_SEG_NCOUNT (8 + SM_SEG_MAXL + SM_SEG_NB)
@@ -41,6 +43,12 @@
 // a rejected edge with a component smaller than min_size at the end of the sweep
 struct SegMin {
     uint32_t id, w, ra, rb, sa, sb;
+};
+
+// a min-size candidate that is the first (in (w, id) order) of its pair of sweep roots, with the roots
+// as dense local ids (lsize / lroot give their sizes and pixels)
+struct SegEdge {
+    uint32_t la, lb, id;
 };
 
 struct SegView {
@@ -63,6 +71,14 @@ struct SegView {
     uint32_t* mval[2];            // their indices, unsorted / sorted
     SegMin* msorted;              // min-size candidates in (w, id) order
     uint32_t nmin;                // their count (host-set before the sort)
+    // pair dedupe (seg_launch_dedupe): only the first candidate of each root pair can join
+    uint32_t* keep;               // [E + 1] first of its pair, by position -> (scan) kpos
+    uint32_t* kpos;               // [E + 1]
+    uint32_t* lmark;              // [N + 1] roots of the kept candidates -> (scan) lid
+    uint32_t* lid;                // [N + 1]
+    SegEdge* dense;               // [E] the kept candidates in (w, id) order
+    uint32_t* lsize;              // [N] per local id: the root's size at the end of the sweep
+    uint32_t* lroot;              // [N] per local id: the root pixel
     const uint32_t* hooks;        // the host merge's hooks and marked edges (k_seg_apply)
     int nhooks;
     uint8_t* mR;
@@ -87,5 +103,7 @@ hipError_t seg_launch_sizes(hipStream_t st, const SegPair& p, int w, uint32_t m)
 hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, uint32_t nrej_max);
 size_t seg_sort_temp_bytes(uint32_t n);
 hipError_t seg_launch_sort(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes);
+// after seg_launch_sort: the first candidate of each root pair, dense root ids; counts at SM_SEG_C_UNIQ / _LOCAL
+hipError_t seg_launch_dedupe(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes);
 hipError_t seg_launch_apply(hipStream_t st, const SegPair& p);
 hipError_t seg_launch_trees(hipStream_t st, const SegPair& p);

@@ -14,12 +14,16 @@
 //     k_seg_sizes     sizes of the joined components, last-join weight w
 //     (k_seg_small: all of it in one workgroup, for a run of buckets of at most SM_SEG_SMALL edges)
 //   k_seg_minsize   rejected edges with an end smaller than min_size, radix-sorted into (w, id) order
-//                   (hipcub) and gathered (k_seg_gather) -> the host's serial merge
+//                   (hipcub) and gathered (k_seg_gather); k_seg_pairkey .. k_seg_dense keep the first
+//                   candidate of each pair of roots, with dense root ids -> the host's serial merge
 //   k_seg_apply     the host's merges (root hooks, marked edges)
 //   k_seg_first / k_seg_virtual   first pixel of each tree, virtual edges to link the forest (sm_segment.cpp)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_scan.hpp>
 
 #include "sm_seg_gpu.h"
 #include "sm_segment.h"
@@ -403,6 +407,56 @@ __global__ void __launch_bounds__(256) k_seg_gather(SegPair sp) {
     if (i < n) v.msorted[i] = v.mlist[v.mval[1][i]];
 }
 
+// Pair dedupe.  A candidate whose pair of sweep roots {ra, rb} already occurred earlier in (w, id) order
+// can never join: if the first occurrence joined, the two are one set from then on; if it did not, they
+// were one set already or both had min_size pixels, and sizes only grow.  So only the first of each pair
+// goes to the host (~23k of ~260k per C2 view).  Keys: lo * N + hi; the radix sort is stable, so the
+// first of a run of equal keys is the earliest position.
+__global__ void __launch_bounds__(256) k_seg_pairkey(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= v.nmin) return;
+    const SegMin m = v.msorted[i];
+    const unsigned long long N = (unsigned long long)v.W * (unsigned long long)v.H;
+    const uint32_t lo = m.ra < m.rb ? m.ra : m.rb, hi = m.ra < m.rb ? m.rb : m.ra;
+    v.mkey[0][i] = (unsigned long long)lo * N + hi;
+    v.mval[0][i] = i;
+}
+
+__global__ void __launch_bounds__(256) k_seg_keep(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) v.keep[v.nmin] = 0;
+    if (i >= v.nmin) return;
+    v.keep[v.mval[1][i]] = (i == 0 || v.mkey[1][i] != v.mkey[1][i - 1]) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_seg_mark(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= v.nmin || !v.keep[i]) return;
+    const SegMin m = v.msorted[i];
+    v.lmark[m.ra] = 1;
+    v.lmark[m.rb] = 1;
+}
+
+__global__ void __launch_bounds__(256) k_seg_dense(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        v.cnt[SM_SEG_C_UNIQ] = v.kpos[v.nmin];
+        v.cnt[SM_SEG_C_LOCAL] = v.lid[(size_t)v.W * v.H];
+    }
+    if (i >= v.nmin || !v.keep[i]) return;
+    const SegMin m = v.msorted[i];
+    const uint32_t la = v.lid[m.ra], lb = v.lid[m.rb];
+    v.dense[v.kpos[i]] = SegEdge{la, lb, m.id};
+    v.lsize[la] = m.sa;  // (every candidate of a root writes the same values)
+    v.lroot[la] = m.ra;
+    v.lsize[lb] = m.sb;
+    v.lroot[lb] = m.rb;
+}
+
 // hooks[2k] = child root, hooks[2k + 1] = parent root (0xFFFFFFFF: none) ; marked edge ids after the
 // pairs: hooks[2 * nhooks + k]
 __global__ void __launch_bounds__(256) k_seg_apply(SegPair sp) {
@@ -503,10 +557,14 @@ hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, ui
 }
 
 size_t seg_sort_temp_bytes(uint32_t n) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+    size_t a = 0, b = 0, c = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, SEG_KEY_BITS);
-    return bytes;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64);
+    // the scans: E + 1 candidate flags, N + 1 root marks (n = E = 2N)
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n + 1);
+    return std::max(a, std::max(b, c));
 }
 
 // per view: its nmin candidates sorted by key (temp: that view's scratch), then one gather launch
@@ -522,6 +580,38 @@ hipError_t seg_launch_sort(hipStream_t st, const SegPair& p, void* const* temp, 
         if (e != hipSuccess) return e;
     }
     if (nmax) hipLaunchKernelGGL(k_seg_gather, dim3(blocks_of(nmax, 256), p.nv), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_dedupe(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes) {
+    const size_t N = (size_t)p.v[0].W * p.v[0].H;
+    int bits = 1;
+    while (bits < 64 && (1ull << bits) <= (unsigned long long)N * N) ++bits;
+    uint32_t nmax = 0;
+    for (int i = 0; i < p.nv; ++i) nmax = p.v[i].nmin > nmax ? p.v[i].nmin : nmax;
+    const unsigned nb = blocks_of(nmax ? nmax : 1, 256);
+    hipLaunchKernelGGL(k_seg_pairkey, dim3(nb, p.nv), dim3(256), 0, st, p);
+    for (int i = 0; i < p.nv; ++i) {
+        const SegView& v = p.v[i];
+        hipError_t e = hipMemsetAsync(v.lmark, 0, (N + 1) * 4, st);
+        if (e != hipSuccess) return e;
+        if (v.nmin == 0) continue;
+        size_t tb = temp_bytes[i];
+        if ((e = hipcub::DeviceRadixSort::SortPairs(temp[i], tb, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1], (int)v.nmin, 0,
+                                                    bits, st)) != hipSuccess)
+            return e;
+    }
+    hipLaunchKernelGGL(k_seg_keep, dim3(nb, p.nv), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(k_seg_mark, dim3(nb, p.nv), dim3(256), 0, st, p);
+    for (int i = 0; i < p.nv; ++i) {
+        const SegView& v = p.v[i];
+        size_t tb = temp_bytes[i];
+        hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp[i], tb, v.keep, v.kpos, (int)v.nmin + 1, st);
+        if (e != hipSuccess) return e;
+        tb = temp_bytes[i];
+        if ((e = hipcub::DeviceScan::ExclusiveSum(temp[i], tb, v.lmark, v.lid, (int)N + 1, st)) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_seg_dense, dim3(nb, p.nv), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 
