@@ -475,6 +475,10 @@ sm_status segment_upload(sm_ctx* ctx, int views) {
 // SM_SEG_HOST=1: segment mode's segmentation by the host sweep (sm_segment.cpp) instead of the GPU
 bool seg_host() { return getenv("SM_SEG_HOST") != nullptr; }
 
+// SM_SEG_FLATTEN: bit 0: point every pixel at its root before each run of one-workgroup buckets (default),
+// bit 1: before each whole-GPU bucket as well; 0: never
+int seg_flatten() { return getenv("SM_SEG_FLATTEN") ? atoi(getenv("SM_SEG_FLATTEN")) : 1; }
+
 // SM_SEG_NODEDUP=1: the min-size merge over every candidate (A/B of the GPU pair dedupe)
 bool seg_nodedup() { return getenv("SM_SEG_NODEDUP") != nullptr; }
 
@@ -579,6 +583,7 @@ double now_ms();
 sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_copy) {
     static const bool dbg = getenv("SM_SEG_DEBUG") != nullptr;
     const bool nodedup = seg_nodedup();
+    const int flatten = seg_flatten();
     const double t0 = dbg ? now_ms() : 0.0;
     double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
     const int W = ctx->W, H = ctx->H;
@@ -694,6 +699,7 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         if (m <= small) {  // a run of small buckets in one workgroup per view: classify, rounds, sizes
             int w1 = w + 1, nb = 1;
             for (uint32_t m1; w1 < SM_SEG_NB && (m1 = bsize(w1)) <= small; ++w1) nb += m1 > 0;
+            if (flatten & 1) HIPC(seg_launch_flatten(st, sp));
             HIPC(seg_launch_small(st, sp, w, w1, c, gen));
             gen += SM_SEG_TAIL_GENS * (uint32_t)nb;
             w = w1 - 1;
@@ -701,6 +707,7 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         }
         if (L + R + 2 >= SM_SEG_MAXL) return fail(ctx, SM_ERR_STATE, "segment mode: list counters exhausted");
         int lin = L++;
+        if (flatten & 2) HIPC(seg_launch_flatten(st, sp));
         HIPC(seg_launch_classify(st, sp, w, m, c, lin, gen++));  // + the first round's hooks
         for (int r = 1; r < R; ++r) {
             HIPC(seg_launch_round(st, sp, m, lin, lin + 1, gen++));

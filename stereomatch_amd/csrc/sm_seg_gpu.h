@@ -99,6 +99,8 @@ hipError_t seg_launch_classify(hipStream_t st, const SegPair& p, int w, uint32_t
 hipError_t seg_launch_round(hipStream_t st, const SegPair& p, uint32_t m, int lin, int lout, uint32_t gen);
 hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t gen0);
 hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0);
+// every pixel's parent := its root
+hipError_t seg_launch_flatten(hipStream_t st, const SegPair& p);
 hipError_t seg_launch_sizes(hipStream_t st, const SegPair& p, int w, uint32_t m);
 hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, uint32_t nrej_max);
 size_t seg_sort_temp_bytes(uint32_t n);

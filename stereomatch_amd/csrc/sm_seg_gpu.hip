@@ -457,6 +457,16 @@ __global__ void __launch_bounds__(256) k_seg_dense(SegPair sp) {
     v.lroot[lb] = m.rb;
 }
 
+// every pixel's parent set to its root (chains grow by one level per join; the one-workgroup kernels pay
+// each level as a dependent load)
+__global__ void __launch_bounds__(256) k_seg_flatten(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= (uint32_t)v.W * (uint32_t)v.H) return;
+    const uint32_t r = seg_find(v.par, p);
+    if (v.par[p] != r) v.par[p] = r;
+}
+
 // hooks[2k] = child root, hooks[2k + 1] = parent root (0xFFFFFFFF: none) ; marked edge ids after the
 // pairs: hooks[2 * nhooks + k]
 __global__ void __launch_bounds__(256) k_seg_apply(SegPair sp) {
@@ -542,6 +552,12 @@ hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t g
 
 hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0) {
     hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_flatten(hipStream_t st, const SegPair& p) {
+    const size_t N = (size_t)p.v[0].W * p.v[0].H;
+    hipLaunchKernelGGL(k_seg_flatten, dim3(blocks_of(N, 256), p.nv), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 

@@ -27,3 +27,8 @@ python3 -c "import json;d=json.loads(open('$O/seg_0.log').read().strip().splitli
 SM_SEG_NODEDUP=1 SM_SEG_DEBUG=1 timeout -k 10 300 python bench.py --segment-c 5000 --no-cpu --no-pms --steps 16 --warmup 4 --inflight 0 > $O/seg_0_nodedup.log 2> $O/seg_0_nodedup.err || exit 6
 grep segment_gpu $O/seg_0_nodedup.err | tail -2
 python3 -c "import json;d=json.loads(open('$O/seg_0_nodedup.log').read().strip().splitlines()[-1]);print('seg nodedup inflight 0', round(d['ms_per_step'],3), 'latency', d.get('latency_ms_per_frame'))"
+for fl in 0 3; do
+  SM_SEG_FLATTEN=$fl SM_SEG_DEBUG=1 timeout -k 10 300 python bench.py --segment-c 5000 --no-cpu --no-pms --steps 16 --warmup 4 --inflight 0 > $O/seg_0_fl$fl.log 2> $O/seg_0_fl$fl.err || exit 7
+  grep segment_gpu $O/seg_0_fl$fl.err | tail -1
+  python3 -c "import json;d=json.loads(open('$O/seg_0_fl$fl.log').read().strip().splitlines()[-1]);print('seg flatten $fl inflight 0', round(d['ms_per_step'],3), 'latency', d.get('latency_ms_per_frame'))"
+done
