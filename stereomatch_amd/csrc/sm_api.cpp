@@ -1818,7 +1818,7 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
         }
         // SM_PMS_CHAIN_MIN: the chain threshold (at least SM_PMS_CHAIN_LEN, whose counts bound the grid)
         const char* cm = getenv("SM_PMS_CHAIN_MIN");
-        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains ? (cm ? atoi(cm) : SM_PMS_CHAIN_LEN) : 0));
+        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains ? (cm ? atoi(cm) : SM_PMS_CHAIN_DEFAULT) : 0));
     }
     // pieces: every guessed piece repairs at once, then a gated sequential pass (SM_PMS_SEQ_REPAIR=1: the
     // sequential pass alone, A/B); maxp[r] = the most pieces of a cut repaired in round r

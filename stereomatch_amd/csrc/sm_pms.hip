@@ -1030,7 +1030,8 @@ constexpr int PC_NSD = 14;     // down ring slots (0.5 KB per node): 58 KB, two 
 constexpr int PC_LW = 7;       // loader waves (+ the chain wave: 512 threads)
 
 struct PcUpSlot {
-    double pre[PC_G][64], p1[PC_G][64], p2[PC_G][64], cost[PC_G][64];
+    double2 pc[PC_G][64];  // (pre, cost): one 16-byte LDS read per node and lane
+    double2 pp[PC_G][64];  // (post1, post2)
     double sh[PC_G], s1[PC_G], s2[PC_G], s3[PC_G];
     int np[PC_G], p3row[PC_G];
 };
@@ -1057,11 +1058,14 @@ __device__ __forceinline__ void pc_wait_ge(int* p, int v) {
 
 template <bool UP>
 __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
-    extern __shared__ double pc_lds[];
+    extern __shared__ double2 pc_lds[];  // 16-byte aligned: the up ring is read as double2
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
     __shared__ int s_staged[PC_NSD], s_freed;
     const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int NS = UP ? PC_NSU : PC_NSD;
+    // the grid is the schedule's bound (paths of >= SM_PMS_CHAIN_LEN rows); blocks past the plan's chain
+    // items leave before touching anything
+    if ((int)blockIdx.x >= d.plan_cnt[r * PMS_NCNT + PMS_NCLS]) return;
     for (int i = tid; i < PMS_NW; i += blockDim.x) {
         sS[i] = d.slut[i];
         sS2[i] = d.s2lut[i];
@@ -1069,8 +1073,6 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
     if (tid < PC_NSD) s_staged[tid] = 0;
     if (tid == 0) s_freed = 0;
     __syncthreads();
-    const int ncl = d.plan_cnt[r * PMS_NCNT + PMS_NCLS];  // chain items of the round
-    if ((int)blockIdx.x >= ncl) return;
     const PmsItem it = d.plan_item[(size_t)d.item_cap + d.plan_ibase[r] + blockIdx.x];
     const PmsPath pa = d.paths[it.path];
     const int t = pa.tree, r0 = pa.row, len = pa.len;
@@ -1119,11 +1121,9 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
                         if (q < h) pre = fma(cv[k][q], sS[wc[q]], pre);
-                    sl.pre[k][lane] = pre;
-                    sl.cost[k][lane] = cost[k];
+                    sl.pc[k][lane] = make_double2(pre, cost[k]);
                     const int np = hk == 0xFF ? 0 : nch - 1 - hk;
-                    sl.p1[k][lane] = np >= 1 ? cv[k][(hk + 1) & 3] : 0.0;
-                    sl.p2[k][lane] = np >= 2 ? cv[k][(hk + 2) & 3] : 0.0;
+                    sl.pp[k][lane] = make_double2(np >= 1 ? cv[k][(hk + 1) & 3] : 0.0, np >= 2 ? cv[k][(hk + 2) & 3] : 0.0);
                     if (lane == 0) {
                         sl.sh[k] = hk == 0xFF ? 0.0 : sS[wc[hk & 3]];
                         sl.s1[k] = np >= 1 ? sS[wc[(hk + 1) & 3]] : 0.0;
@@ -1149,10 +1149,11 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
                 int np3 = 0;
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
-                    pre[k] = sl.pre[k][lane];
-                    p1[k] = sl.p1[k][lane];
-                    p2[k] = sl.p2[k][lane];
-                    cst[k] = sl.cost[k][lane];
+                    const double2 pc = sl.pc[k][lane], pp = sl.pp[k][lane];
+                    pre[k] = pc.x;
+                    cst[k] = pc.y;
+                    p1[k] = pp.x;
+                    p2[k] = pp.y;
                     sh[k] = sl.sh[k];
                     s1[k] = sl.s1[k];
                     s2[k] = sl.s2[k];

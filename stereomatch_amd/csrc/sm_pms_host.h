@@ -21,8 +21,11 @@ struct PmsRow {
     uint16_t x, y;      // pixel coordinates
 };
 
-// Paths (and pieces) of at least this many rows are walked by the chain kernel (sm_pms.hip k_pms_chain)
-#define SM_PMS_CHAIN_LEN 96
+// Paths (and pieces) of at least SM_PMS_CHAIN_DEFAULT rows are walked by the chain kernel (sm_pms.hip
+// k_pms_chain; env SM_PMS_CHAIN_MIN moves the threshold, down to SM_PMS_CHAIN_LEN, the floor the schedule's
+// chain-item counts rt_long are kept for)
+#define SM_PMS_CHAIN_LEN 48
+#define SM_PMS_CHAIN_DEFAULT 96
 
 // A heavy path: rows [row, row + len), head first.
 struct PmsPath {
