@@ -214,6 +214,10 @@ struct sm_ctx {
     DevBuf pms_dice, pms_rnd, pms_evals;
     hipStream_t st_pms = nullptr;  // view 1's MST_PMS calls (view 0's run on st), created on first use
     hipEvent_t ev_pms = nullptr;
+    // per view: the stream a round's chain launch runs on, concurrently with the round's walkers (pms_phase)
+    hipStream_t st_pms_chain[2] = {nullptr, nullptr};
+    hipEvent_t ev_pms_fork[2] = {nullptr, nullptr}, ev_pms_join[2] = {nullptr, nullptr};
+    bool pms_chain_on = false;  // this call uses them (SM_PMS_CHAIN_STREAM != 0)
     long long pms_dice_n = 0;  // dice values on the device (the stream prefix every call replays)
     std::vector<float> pms_init;   // random plane labels of (W, H, Dmax) (both views start from them)
     int pms_init_key[3] = {0, 0, 0};
@@ -1832,23 +1836,30 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
     std::vector<int> nlong(std::max(R, 1), 0);
     if (!wave_walk && chains)
         for (int r = 0; r < R; ++r) nlong[r] = f.rt_long[r * K1 + t_hi] - f.rt_long[r * K1 + t_lo];
-    for (int r = R - 1; r >= 0; --r) {
-        if (wave_walk) HIPC(launch_pms_walk(st, d, phase, true, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        else {
-            HIPC(launch_pms_chain(st, d, phase, true, r, nlong[r]));
-            HIPC(launch_pms_walk_plan(st, d, phase, true, r, bound[r]));
+    // a round's chain items and walker tasks are disjoint paths whose inputs are final: the chain launch
+    // runs on the view's chain stream beside the walkers (fork / join events), so the round takes the
+    // longer of the two instead of their sum (SM_PMS_CHAIN_STREAM=0: one stream, A/B)
+    const hipStream_t sc = ctx->pms_chain_on ? ctx->st_pms_chain[v] : nullptr;
+    auto round = [&](int r, bool up) -> sm_status {
+        if (wave_walk) {
+            HIPC(launch_pms_walk(st, d, phase, up, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
+        } else if (sc && nlong[r] > 0 && bound[r] > 0) {
+            HIPC(hipEventRecord(ctx->ev_pms_fork[v], st));
+            HIPC(hipStreamWaitEvent(sc, ctx->ev_pms_fork[v], 0));
+            HIPC(launch_pms_chain(sc, d, phase, up, r, nlong[r]));
+            HIPC(launch_pms_walk_plan(st, d, phase, up, r, bound[r]));
+            HIPC(hipEventRecord(ctx->ev_pms_join[v], sc));
+            HIPC(hipStreamWaitEvent(st, ctx->ev_pms_join[v], 0));
+        } else {
+            HIPC(launch_pms_chain(st, d, phase, up, r, nlong[r]));
+            HIPC(launch_pms_walk_plan(st, d, phase, up, r, bound[r]));
         }
-        HIPC(launch_pms_repair(st, d, phase, true, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
-    }
+        HIPC(launch_pms_repair(st, d, phase, up, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
+        return SM_OK;
+    };
+    for (int r = R - 1; r >= 0; --r) CHECK(round(r, true));
     HIPC(launch_pms_cut_backup(st, d, f.tree_cut[t_lo], f.tree_cut[t_hi]));
-    for (int r = 0; r < R; ++r) {
-        if (wave_walk) HIPC(launch_pms_walk(st, d, phase, false, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        else {
-            HIPC(launch_pms_chain(st, d, phase, false, r, nlong[r]));
-            HIPC(launch_pms_walk_plan(st, d, phase, false, r, bound[r]));
-        }
-        HIPC(launch_pms_repair(st, d, phase, false, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
-    }
+    for (int r = 0; r < R; ++r) CHECK(round(r, false));
     HIPC(launch_pms_update(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
     return SM_OK;
 }
@@ -2168,6 +2179,15 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
         if (hipStreamCreateWithFlags(&ctx->st_pms, hipStreamNonBlocking) != hipSuccess) {
             skip.join();
             return fail(ctx, SM_ERR_HIP, "hipStreamCreateWithFlags (MST_PMS view stream)");
+        }
+    }
+    ctx->pms_chain_on = !(getenv("SM_PMS_CHAIN_STREAM") && atoi(getenv("SM_PMS_CHAIN_STREAM")) == 0);
+    for (int v = 0; v < 2 && ctx->pms_chain_on; ++v) {
+        if ((!ctx->st_pms_chain[v] && hipStreamCreateWithFlags(&ctx->st_pms_chain[v], hipStreamNonBlocking) != hipSuccess) ||
+            (!ctx->ev_pms_fork[v] && hipEventCreateWithFlags(&ctx->ev_pms_fork[v], hipEventDisableTiming) != hipSuccess) ||
+            (!ctx->ev_pms_join[v] && hipEventCreateWithFlags(&ctx->ev_pms_join[v], hipEventDisableTiming) != hipSuccess)) {
+            skip.join();
+            return fail(ctx, SM_ERR_HIP, "hipStreamCreateWithFlags (MST_PMS chain stream)");
         }
     }
     {
@@ -2582,6 +2602,14 @@ void sm_destroy(sm_ctx* ctx) {
         (void)hipStreamDestroy(ctx->st_pms);
     }
     if (ctx->ev_pms) (void)hipEventDestroy(ctx->ev_pms);
+    for (int v = 0; v < 2; ++v) {
+        if (ctx->st_pms_chain[v]) {
+            (void)hipStreamSynchronize(ctx->st_pms_chain[v]);
+            (void)hipStreamDestroy(ctx->st_pms_chain[v]);
+        }
+        if (ctx->ev_pms_fork[v]) (void)hipEventDestroy(ctx->ev_pms_fork[v]);
+        if (ctx->ev_pms_join[v]) (void)hipEventDestroy(ctx->ev_pms_join[v]);
+    }
     if (ctx->pms_rnd.p) (void)hipFree(ctx->pms_rnd.p);
     if (ctx->h_pms_res) (void)hipHostFree(ctx->h_pms_res);
     if (ctx->h_changed) (void)hipHostFree(ctx->h_changed);

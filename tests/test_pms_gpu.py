@@ -62,7 +62,7 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
     assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
 
 
-@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain"])
+@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "onestream"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
@@ -70,7 +70,9 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     every failure; SM_PMS_SERIAL=1 is the plain serial order; SM_PMS_NODEDUP=1 propagates every
     sampled label, repeats included (the default drops repeats, k_pms_prop_dedupe);
     SM_PMS_WAVE_WALK=1 walks every (path, chunk) item with a wave of its own instead of the planned
-    lane-group walks (k_pms_plan / k_pms_walk_plan)."""
+    lane-group walks (k_pms_plan / k_pms_walk_plan); SM_PMS_CHAIN_MIN=48 sends paths of >= 48 rows to the
+    chain kernel; SM_PMS_CHAIN_STREAM=0 runs the chain launches on the view's stream instead of beside the
+    walkers."""
     monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
     monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
     if mode == "nodedup":
@@ -85,6 +87,14 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         monkeypatch.setenv("SM_PMS_NO_CHAIN", "1")
     else:
         monkeypatch.delenv("SM_PMS_NO_CHAIN", raising=False)
+    if mode == "chain48":
+        monkeypatch.setenv("SM_PMS_CHAIN_MIN", "48")
+    else:
+        monkeypatch.delenv("SM_PMS_CHAIN_MIN", raising=False)
+    if mode == "onestream":
+        monkeypatch.setenv("SM_PMS_CHAIN_STREAM", "0")
+    else:
+        monkeypatch.delenv("SM_PMS_CHAIN_STREAM", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
@@ -199,17 +209,26 @@ def test_pms_reference_surface_100_calls(gpu_ctx):
     np.testing.assert_array_equal(u32(rd), u32(ref["right"]["disp"]))
 
 
+_FULL_C2_REF = {}
+
+
 @pytest.mark.timeout(900)
-def test_pms_full_c2_speculative_bitexact(gpu_ctx, monkeypatch):
+@pytest.mark.parametrize("chain_min", [None, "48"])
+def test_pms_full_c2_speculative_bitexact(gpu_ctx, monkeypatch, chain_min):
     """Full C2 (1920x1200, Dmax 128), c=5000, min_size 200, THREE MST_PMS calls per view: calls 2-3 take
     the speculative path (guessed offsets, every tree at once, validation, single-tree repairs) with the
     default 512-row pieces, propagation dedupe and whole-GPU launches -- the mode the reference's 99 later
     calls per view run in (Stereo3DMST.cpp:546-629, 854-889).  Labels, fp64 minima and plane disparities
-    bitwise against the oracle's serial restatement."""
-    for k in ("SM_PMS_SERIAL", "SM_PMS_REPASS", "SM_PMS_NODEDUP", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS"):
+    bitwise against the oracle's serial restatement.  chain_min 48: paths of >= 48 rows on the chain kernel
+    (SM_PMS_CHAIN_MIN)."""
+    for k in ("SM_PMS_SERIAL", "SM_PMS_REPASS", "SM_PMS_NODEDUP", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS", "SM_PMS_CHAIN_MIN"):
         monkeypatch.delenv(k, raising=False)
+    if chain_min:
+        monkeypatch.setenv("SM_PMS_CHAIN_MIN", chain_min)
     left, right, _ = make_pair(1920, 1200, 128, index=0)
-    ref = O.stereo3dmst_pms(left, right, 128, iters=3, c=5000.0, min_size=200)
+    if "ref" not in _FULL_C2_REF:  # the oracle's three calls once for both cases
+        _FULL_C2_REF["ref"] = O.stereo3dmst_pms(left, right, 128, iters=3, c=5000.0, min_size=200)
+    ref = _FULL_C2_REF["ref"]
     out, labs, st = run_gpu(gpu_ctx, left, right, 128, 3)
     for v in ("left", "right"):
         check_view(out, labs, ref, v)
