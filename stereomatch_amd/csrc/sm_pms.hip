@@ -1087,11 +1087,17 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
     if (UP) {
         PcUpSlot* ring = reinterpret_cast<PcUpSlot*>(pc_lds);
         if (wave > 0) {  // loaders: groups wave - 1, wave - 1 + PC_LW, ...
+            // a group's metadata is loaded during the previous group (after its row loads), so each group
+            // costs one memory round trip (metadata -> rows was two)
+            auto gmeta = [&](int gg) {
+                const int it = len - 1 - gg * PC_G, il = it - PC_G + 1 > 0 ? it - PC_G + 1 : 0;
+                return meta_load(d.rows, r0 + il, it - il + 1);
+            };
+            ChunkMeta m = gmeta(wave - 1 < ngroups ? wave - 1 : 0);  // unconditional (clamped)
             for (int g = wave - 1; g < ngroups; g += PC_LW) {
                 const int itop = len - 1 - g * PC_G;                 // the group's first (lowest) node
                 const int ilo = itop - PC_G + 1 > 0 ? itop - PC_G + 1 : 0;
                 const int n = itop - ilo + 1;
-                const ChunkMeta m = meta_load(d.rows, r0 + ilo, n);
                 double cv[PC_G][4], cost[PC_G];
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
@@ -1106,6 +1112,7 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
                     }
                     cost[k] = Al[(size_t)(row - ts) * pt];
                 }
+                const ChunkMeta mn = gmeta(g + PC_LW < ngroups ? g + PC_LW : g);  // the next group's (clamped)
                 const int s = g % NS;
                 pc_wait_ge(&s_freed, g - NS + 1);  // the slot's previous group is consumed
                 PcUpSlot& sl = ring[s];
@@ -1134,6 +1141,7 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
                     }
                 }
                 pc_publish(&s_staged[s], g + 1);
+                m = mn;
             }
         } else {  // the chain wave
             double x = 0.0;  // the bottom row's heavy child: a leaf's none, a cut piece's guess 0
