@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "sm_pms.h"
 
@@ -1057,12 +1058,12 @@ __device__ __forceinline__ void pc_wait_ge(int* p, int v) {
 }
 
 template <bool UP>
-__global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r) {
+__global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, int ns) {
     extern __shared__ double2 pc_lds[];  // 16-byte aligned: the up ring is read as double2
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
     __shared__ int s_staged[PC_NSD], s_freed;
     const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int NS = UP ? PC_NSU : PC_NSD;
+    const int NS = ns;  // ring slots (<= PC_NSU / PC_NSD): fewer slots, more workgroups per CU
     // the grid is the schedule's bound (paths of >= SM_PMS_CHAIN_LEN rows); blocks past the plan's chain
     // items leave before touching anything
     if ((int)blockIdx.x >= d.plan_cnt[r * PMS_NCNT + PMS_NCLS]) return;
@@ -1623,15 +1624,21 @@ hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo,
 
 hipError_t launch_pms_chain(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int items) {
     if (items <= 0) return hipSuccess;
-    const size_t lds = up ? PC_NSU * sizeof(PcUpSlot) : PC_NSD * sizeof(PcDnSlot);
+    // SM_PMS_CHAIN_NSU / _NSD: ring slots of the up / down chain (LDS per workgroup, so workgroups per CU)
+    const char* eu = getenv("SM_PMS_CHAIN_NSU");
+    const char* ed = getenv("SM_PMS_CHAIN_NSD");
+    const int nsu = eu ? std::min(std::max(atoi(eu), 1), PC_NSU) : PC_NSU;
+    const int nsd = ed ? std::min(std::max(atoi(ed), 1), PC_NSD) : PC_NSD;
+    const int ns = up ? nsu : nsd;
+    const size_t lds = up ? ns * sizeof(PcUpSlot) : ns * sizeof(PcDnSlot);
     static const hipError_t a0 = hipFuncSetAttribute((const void*)k_pms_chain<true>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_NSU * sizeof(PcUpSlot)));
     static const hipError_t a1 = hipFuncSetAttribute((const void*)k_pms_chain<false>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_NSD * sizeof(PcDnSlot)));
     if (a0 != hipSuccess) return a0;
     if (a1 != hipSuccess) return a1;
-    if (up) hipLaunchKernelGGL(k_pms_chain<true>, dim3((unsigned)items), dim3(64 * (PC_LW + 1)), lds, st, d, phase, r);
-    else hipLaunchKernelGGL(k_pms_chain<false>, dim3((unsigned)items), dim3(64 * (PC_LW + 1)), lds, st, d, phase, r);
+    if (up) hipLaunchKernelGGL(k_pms_chain<true>, dim3((unsigned)items), dim3(64 * (PC_LW + 1)), lds, st, d, phase, r, ns);
+    else hipLaunchKernelGGL(k_pms_chain<false>, dim3((unsigned)items), dim3(64 * (PC_LW + 1)), lds, st, d, phase, r, ns);
     return hipGetLastError();
 }
 
