@@ -1,0 +1,25 @@
+# round 4: PMS chain knobs (ring depth, threshold), 100-call C2 frame per setting, and a 20-call kernel trace
+# with the views one after the other -> gpurun_out/r04o
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r04o
+mkdir -p $O
+run() {  # tag, env...
+  local tag=$1; shift
+  env "$@" timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms100_$tag.log 2>&1 || return 1
+  python3 - $O/pms100_$tag.log $tag <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])["gpu"]
+print("%-14s frame %.1f ms  prep %.1f (forest %.1f)  first %.1f  later %.1f  views first %s later %s" % (sys.argv[2], d["total_ms"], d["prep_ms"], d.get("prep_forest_ms", 0), d["iter0_ms"], d["iters_ms"], [round(x, 1) for x in d["first_ms_view"]], [round(x, 1) for x in d["later_ms_view"]]))
+PY
+}
+run default SM_PMS_X=0 || exit 2
+run nsu2 SM_PMS_CHAIN_NSU=2 || exit 3
+run nsu2_nsd7 SM_PMS_CHAIN_NSU=2 SM_PMS_CHAIN_NSD=7 || exit 4
+run nsu3 SM_PMS_CHAIN_NSU=3 || exit 5
+run cm128 SM_PMS_CHAIN_MIN=128 || exit 6
+SM_PMS_SEQ_VIEWS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/raw -o run --output-format csv -- python3 tools/pms_bench.py 1920 1200 128 20 --reps 1 > $O/prof.log 2>&1 || exit 7
+f=$(find $O/raw -name '*kernel_trace.csv' | head -1); cp "$f" $O/kernel_trace_pms20_seq.csv
+f=$(find $O/raw -name '*kernel_stats.csv' | head -1); cp "$f" $O/kernel_stats_pms20_seq.csv
+rm -rf $O/raw
+echo traced
