@@ -7,7 +7,9 @@ reference's serial Felzenszwalb sweep (segment-graph.h:54-89) plus its min-size 
   * the bucket's marked edges are the minimum spanning forest, keyed by edge id, of its open-open
     edges between components (any order gives the same partition), and
   * the rejected edges are its other two-component edges; the min-size merge only needs those whose
-    end is smaller than min_size after the sweep, in (w, id) order.
+    end is smaller than min_size after the sweep, in (w, id) order, and of those only the first of each
+    pair of sweep roots (the GPU's pair dedupe, seg_launch_dedupe: a later edge of the same pair finds
+    the two joined, or both of at least min_size pixels, for good).
 
 The restatement below is plain Python over small images; the oracle (oracle/sm_oracle.c
 orc_segment, itself pinned to the reference's segment-graph.h) is the serial sweep."""
@@ -18,7 +20,7 @@ from oracle import oracle as O
 from tools.synth import make_pair
 
 
-def bucket_segment(W, H, wR, wD, c, min_size):
+def bucket_segment(W, H, wR, wD, c, min_size, dedupe=False):
     N = W * H
     p = np.arange(N)
     x, y = p % W, p // W
@@ -73,7 +75,18 @@ def bucket_segment(W, H, wR, wD, c, min_size):
     # a rejected edge still joins two components after the sweep (one end's component is closed)
     assert all(find(i >> 1) != find((i >> 1) + (W if i & 1 else 1)) for _, i in rejected)
     ms = max(2, min_size)
-    for wv, i in sorted(rejected):
+    ends = lambda i: (find(i >> 1), find((i >> 1) + (W if i & 1 else 1)))
+    cands = [(wv, i) for wv, i in sorted(rejected) if min(size[r] for r in ends(i)) < ms]
+    if dedupe:  # the first candidate of each unordered pair of sweep roots
+        seen, kept = set(), []
+        for wv, i in cands:
+            key = tuple(sorted(ends(i)))
+            if key not in seen:
+                seen.add(key)
+                kept.append((wv, i))
+        assert len(kept) <= len(cands)
+        cands = kept
+    for wv, i in cands:
         a, b = find(i >> 1), find((i >> 1) + (W if i & 1 else 1))
         if a != b and (size[a] < ms or size[b] < ms):
             if size[a] < size[b]:
@@ -86,10 +99,11 @@ def bucket_segment(W, H, wR, wD, c, min_size):
 
 @pytest.mark.parametrize("W,H,c,min_size,index", [(64, 48, 5000.0, 200, 0), (64, 48, 300.0, 20, 1),
                                                   (80, 40, 40.0, 5, 2), (48, 64, 0.0, 2, 3), (72, 54, 1000.0, 60, 4)])
-def test_bucket_sweep_equals_serial_sweep(W, H, c, min_size, index):
+@pytest.mark.parametrize("dedupe", [False, True])
+def test_bucket_sweep_equals_serial_sweep(W, H, c, min_size, index, dedupe):
     left, _, _ = make_pair(W, H, 32, index=index)
     wR, wD = O.edge_weights(O.median3(left))
     ref, n = O.segment(W, H, wR, wD, c, min_size)
-    got, k = bucket_segment(W, H, wR, wD, c, min_size)
+    got, k = bucket_segment(W, H, wR, wD, c, min_size, dedupe)
     np.testing.assert_array_equal(got, ref)
     assert k == n
