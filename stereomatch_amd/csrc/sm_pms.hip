@@ -427,7 +427,9 @@ __device__ int ref_count(const PmsDev& d, float dd, long long o, Dice dice) {
     return (int)(k - o);
 }
 
-__device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
+// dice(k): the stream's draw k (global memory, or a window staged in LDS)
+template <class Dice>
+__device__ int ref_levels_d(const PmsDev& d, int t, long long o, bool write, Dice dice) {
     const int ts = d.tree_start[t], sz = d.tree_start[t + 1] - ts;
     const int tp = d.bfs_pix[ts + (int)((uint32_t)d.rnd[t] % (uint32_t)sz)];  // std::rand() % size()
     const float px = (float)(tp % d.W), py = (float)(tp / d.W);
@@ -445,11 +447,11 @@ __device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
             atomicOr(d.err, 4u);
             break;
         }
-        const float rd = fmaf(d.dice[k++], max_d, dd);  // 0x410247
+        const float rd = fmaf(dice(k++), max_d, dd);  // 0x410247
         if (rd < 0.0f || rd > fmax) continue;           // :604
-        float rnx = fmaf(max_n, d.dice[k++], nx);
-        float rny = fmaf(max_n, d.dice[k++], ny);
-        float rnz = fmaf(max_n, d.dice[k++], nz);
+        float rnx = fmaf(max_n, dice(k++), nx);
+        float rny = fmaf(max_n, dice(k++), ny);
+        float rnz = fmaf(max_n, dice(k++), nz);
         if (!write) continue;
         const float ni = div_rn(1.0f, sqrt_rn(fmaf(rnz, rnz, fmaf(rnx, rnx, rny * rny))));  // 0x41037b-0x4103c9
         rnx *= ni;
@@ -463,10 +465,15 @@ __device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
     return (int)(k - o);
 }
 
+__device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
+    return ref_levels_d(d, t, o, write, [&d](long long k) { return d.dice[k]; });
+}
+
 // ----------------------------------------------------------------------------- serial mode
 __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
     __shared__ long long s_off;
     __shared__ int s_n;
+    __shared__ float s_dice[64];
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
     load_luts(d, sS, sS2);
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -491,8 +498,14 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
         for (int phase = 0; phase < 2; ++phase) {
             if (phase == 0) {
                 for (int j = tid; j < deg; j += nt) prop_label(d, t, o, j);
-            } else if (tid == 0) {
-                s_n = ref_levels(d, t, o + deg, true);
+            } else {
+                // the refinement's draws (at most 4 per level) staged in LDS first: thread 0's level loop then
+                // reads LDS instead of one dependent global load per level
+                const long long o1 = o + deg;
+                if (tid < 64) s_dice[tid] = o1 + tid < d.dice_n ? d.dice[o1 + tid] : 0.0f;
+                __syncthreads();
+                if (tid == 0)
+                    s_n = ref_levels_d(d, t, o1, true, [&](long long k) { return k - o1 < 64 ? s_dice[k - o1] : d.dice[k]; });
             }
             __threadfence_block();
             __syncthreads();
