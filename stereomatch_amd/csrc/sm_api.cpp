@@ -1836,9 +1836,9 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
     std::vector<int> nlong(std::max(R, 1), 0);
     if (!wave_walk && chains)
         for (int r = 0; r < R; ++r) nlong[r] = f.rt_long[r * K1 + t_hi] - f.rt_long[r * K1 + t_lo];
-    // a round's chain items and walker tasks are disjoint paths whose inputs are final: the chain launch
-    // runs on the view's chain stream beside the walkers (fork / join events), so the round takes the
-    // longer of the two instead of their sum (SM_PMS_CHAIN_STREAM=0: one stream, A/B)
+    // a round's chain items and walker tasks are disjoint paths whose inputs are final: with
+    // SM_PMS_CHAIN_STREAM=1 the chain launch runs on the view's chain stream beside the walkers (fork / join
+    // events; slower at C2, see stage_pms), otherwise one after the other on the view's stream
     const hipStream_t sc = ctx->pms_chain_on ? ctx->st_pms_chain[v] : nullptr;
     auto round = [&](int r, bool up) -> sm_status {
         if (wave_walk) {
@@ -2181,7 +2181,9 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
             return fail(ctx, SM_ERR_HIP, "hipStreamCreateWithFlags (MST_PMS view stream)");
         }
     }
-    ctx->pms_chain_on = !(getenv("SM_PMS_CHAIN_STREAM") && atoi(getenv("SM_PMS_CHAIN_STREAM")) == 0);
+    // measured at C2 (100 calls): 960 ms per frame with the chain stream, 670 without -- the per-round
+    // event fork / join costs more than the overlap wins -- so it is opt-in (SM_PMS_CHAIN_STREAM=1)
+    ctx->pms_chain_on = getenv("SM_PMS_CHAIN_STREAM") && atoi(getenv("SM_PMS_CHAIN_STREAM")) == 1;
     for (int v = 0; v < 2 && ctx->pms_chain_on; ++v) {
         if ((!ctx->st_pms_chain[v] && hipStreamCreateWithFlags(&ctx->st_pms_chain[v], hipStreamNonBlocking) != hipSuccess) ||
             (!ctx->ev_pms_fork[v] && hipEventCreateWithFlags(&ctx->ev_pms_fork[v], hipEventDisableTiming) != hipSuccess) ||

@@ -62,7 +62,7 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
     assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
 
 
-@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "onestream"])
+@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "chainstream"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
@@ -71,8 +71,7 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     sampled label, repeats included (the default drops repeats, k_pms_prop_dedupe);
     SM_PMS_WAVE_WALK=1 walks every (path, chunk) item with a wave of its own instead of the planned
     lane-group walks (k_pms_plan / k_pms_walk_plan); SM_PMS_CHAIN_MIN=48 sends paths of >= 48 rows to the
-    chain kernel; SM_PMS_CHAIN_STREAM=0 runs the chain launches on the view's stream instead of beside the
-    walkers."""
+    chain kernel; SM_PMS_CHAIN_STREAM=1 runs the chain launches on a side stream beside the walkers."""
     monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
     monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
     if mode == "nodedup":
@@ -91,8 +90,8 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         monkeypatch.setenv("SM_PMS_CHAIN_MIN", "48")
     else:
         monkeypatch.delenv("SM_PMS_CHAIN_MIN", raising=False)
-    if mode == "onestream":
-        monkeypatch.setenv("SM_PMS_CHAIN_STREAM", "0")
+    if mode == "chainstream":
+        monkeypatch.setenv("SM_PMS_CHAIN_STREAM", "1")
     else:
         monkeypatch.delenv("SM_PMS_CHAIN_STREAM", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)

@@ -17,8 +17,8 @@ timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms
 tail -1 $O/pms100.log | cut -c1-1500
 SM_PMS_HOST_FOREST=1 timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms100_hostforest.log 2>&1 || exit 3
 echo "host forest: $(tail -1 $O/pms100_hostforest.log | cut -c1-420)"
-SM_PMS_CHAIN_STREAM=0 timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms100_onestream.log 2>&1 || exit 3
-echo "one stream: $(tail -1 $O/pms100_onestream.log | cut -c1-420)"
+SM_PMS_CHAIN_STREAM=1 timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms100_onestream.log 2>&1 || exit 3
+echo "chain stream: $(tail -1 $O/pms100_onestream.log | cut -c1-420)"
 for cm in 48 192; do
   SM_PMS_CHAIN_MIN=$cm timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms100_cm$cm.log 2>&1 || exit 4
   echo "chain_min $cm: $(tail -1 $O/pms100_cm$cm.log | cut -c1-420)"
