@@ -150,11 +150,130 @@ __device__ __forceinline__ int block_scan(int c, int* s_w, int* total) {
     return pre + incl - c;
 }
 
+// Narrow levels (at most 64 nodes: the deep tails of the largest trees, thousands of levels at C2) run on
+// wave 0 alone, level after level without workgroup barriers: the frontier stays in registers, the next
+// one is handed over through LDS (one wave's LDS operations complete in order).  Entered at level d =
+// [a, b) whose nodes are in global memory; leaves at the first level wider than 64 (or the end) with
+// s_state = {a, b, d}.
+__device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* s_pp, int* s_tr, int* s_state) {
+    const int lane = (int)threadIdx.x;
+    int n = b - a, i = a + lane;
+    bool val = lane < n;
+    int p = 0, pp = -1, tr = 0;
+    if (val) {
+        p = v.gpix[i];
+        const int gp = v.gpar[i];
+        pp = gp >= 0 ? v.gpix[gp] : -1;
+        tr = v.gtree[i];
+    }
+    while (n > 0 && n <= 64) {
+        if (lane == 0) v.glev[d] = a;
+        int q[4] = {-1, -1, -1, -1}, c = 0;
+        uint32_t wv[4] = {0, 0, 0, 0};
+        if (val) {
+            const int4 n4 = v.nbr[p];
+            const uint2 w4 = v.nbw[p];
+            const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+            const uint32_t ww[4] = {w4.x & 0xFFFFu, w4.x >> 16, w4.y & 0xFFFFu, w4.y >> 16};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (nn[k] >= 0 && nn[k] != pp) {
+                    q[c] = nn[k];
+                    wv[c++] = ww[k];
+                }
+        }
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        const int total = __shfl(incl, 63), pos = incl - c;
+        if (val) {
+            v.gfc[i] = b + pos;
+            v.gnc[i] = (uint8_t)c;
+            for (int k = 0; k < c; ++k) {
+                const int j = b + pos + k;
+                if (j >= v.N) {  // only masks with a cycle get here (as in the workgroup levels)
+                    v.tot[7] = 1;
+                    break;
+                }
+                v.gpix[j] = q[k];
+                v.gpar[j] = i;
+                v.gtree[j] = tr;
+                v.gw[j] = (uint16_t)wv[k];
+                if (pos + k < 64) {
+                    s_q[pos + k] = q[k];
+                    s_pp[pos + k] = p;
+                    s_tr[pos + k] = tr;
+                }
+            }
+        }
+        const int nb = b + total < v.N ? b + total : v.N;
+        a = b;
+        b = nb;
+        ++d;
+        n = b - a;
+        i = a + lane;
+        val = lane < n;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the LDS writes above stay before the reads below
+        __builtin_amdgcn_wave_barrier();
+        if (n <= 64 && val) {
+            p = s_q[lane];
+            pp = s_pp[lane];
+            tr = s_tr[lane];
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // and these reads before the next level's writes
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) {
+        s_state[0] = a;
+        s_state[1] = b;
+        s_state[2] = d;
+    }
+}
+
+// Narrow levels of the bottom-up sweep on wave 0, from level l down while levels have at most 64 nodes;
+// a level's sizes stay in LDS for its parents' level.  s_state[3] = the first level left (or -1).
+__device__ void sweep_narrow(const PfView& v, int l, int* s_sz, int* s_state) {
+    const int lane = (int)threadIdx.x;
+    int pbase = -1;  // the start of level l + 1 when its sizes are in s_sz
+    for (; l >= 0; --l) {
+        const int la = min(max(v.glev[l], 0), v.N), lb = min(max(v.glev[l + 1], la), v.N);
+        const int n = lb - la;
+        if (n > 64) break;
+        const int i = la + lane;
+        int s = 1, best = -1, bs = 0;
+        if (lane < n) {
+            const int f = v.gfc[i], c = min((int)v.gnc[i], v.N - f);
+            for (int k = 0; k < c; ++k) {
+                const int o = f + k - pbase;
+                const int sk = pbase >= 0 && o >= 0 && o < 64 ? s_sz[o] : v.gsize[f + k];
+                s += sk;
+                if (sk > bs) {  // strictly larger: ties keep the smallest BFS id
+                    bs = sk;
+                    best = k;
+                }
+            }
+            v.gsize[i] = s;
+            v.ghk[i] = (int8_t)best;
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // this level's reads of s_sz before its writes
+        __builtin_amdgcn_wave_barrier();
+        if (lane < n) s_sz[lane] = s;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+        pbase = la;
+    }
+    if (lane == 0) s_state[3] = l;
+}
+
 // One workgroup: the BFS of every tree of the view at once, then the bottom-up sweep.  Level 0 is the
 // roots in tree order; a node's children follow, in key order, at the next level, after the children
 // of the nodes before it.
 __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
     __shared__ int s_w[BT / 64];
+    __shared__ int s_q[64], s_pp[64], s_tr[64], s_sz[64], s_state[4];
     const int tid = (int)threadIdx.x;
     for (int t = tid; t < K; t += BT) {
         v.gpix[t] = v.root_pix[t];
@@ -165,6 +284,16 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
     __syncthreads();
     int a = 0, b = K, next = K, d = 0;
     while (a < b) {
+        if (b - a <= 64) {  // narrow levels on wave 0 (next == b at a level's start)
+            if (tid < 64) bfs_narrow(v, a, b, d, s_q, s_pp, s_tr, s_state);
+            __syncthreads();
+            a = s_state[0];
+            b = s_state[1];
+            d = s_state[2];
+            next = b;
+            __syncthreads();  // s_state read by every wave before it is written again
+            continue;
+        }
         if (tid == 0) v.glev[d] = a;
         for (int base = a; base < b; base += BT) {
             const int i = base + tid;
@@ -218,6 +347,13 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
     // bottom up: subtree sizes and heavy children, a level at a time
     for (int l = d - 1; l >= 0; --l) {
         const int la = min(max(v.glev[l], 0), v.N), lb = min(max(v.glev[l + 1], la), v.N);
+        if (lb - la <= 64) {  // narrow levels on wave 0
+            if (tid < 64) sweep_narrow(v, l, s_sz, s_state);
+            __syncthreads();
+            l = s_state[3] + 1;  // the loop's decrement gives the first level left
+            __syncthreads();
+            continue;
+        }
         for (int i = la + tid; i < lb; i += BT) {
             const int f = v.gfc[i], c = min((int)v.gnc[i], v.N - f);  // clamp: only a cycle overflows
             int s = 1, best = -1, bs = 0;

@@ -13,6 +13,9 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])["gpu"]
 print("%-14s frame %.1f ms  prep %.1f (forest %.1f)  first %.1f  later %.1f  views first %s later %s" % (sys.argv[2], d["total_ms"], d["prep_ms"], d.get("prep_forest_ms", 0), d["iter0_ms"], d["iters_ms"], [round(x, 1) for x in d["first_ms_view"]], [round(x, 1) for x in d["later_ms_view"]]))
 PY
 }
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/test_pms_gpu.py \
+  -k "gpu_forest_matches or synthetic_modes or full_c2_speculative" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
 run default SM_PMS_X=0 || exit 2
 run nsu2 SM_PMS_CHAIN_NSU=2 || exit 3
 run nsu2_nsd7 SM_PMS_CHAIN_NSU=2 SM_PMS_CHAIN_NSD=7 || exit 4
