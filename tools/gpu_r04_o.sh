@@ -23,6 +23,8 @@ run nsu3 SM_PMS_CHAIN_NSU=3 || exit 5
 run cm128 SM_PMS_CHAIN_MIN=128 || exit 6
 run cm48 SM_PMS_CHAIN_MIN=48 || exit 6
 run cm192 SM_PMS_CHAIN_MIN=192 || exit 6
+run piece256 SM_PMS_PIECE=256 || exit 6
+run piece384 SM_PMS_PIECE=384 || exit 6
 SM_PMS_PROF=1 SM_PMS_SEQ_VIEWS=1 timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 2 --reps 1 > $O/pms2_prof.log 2>&1 || exit 8
 grep "pms prof" $O/pms2_prof.log
 SM_PMS_SEQ_VIEWS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/raw -o run --output-format csv -- python3 tools/pms_bench.py 1920 1200 128 20 --reps 1 > $O/prof.log 2>&1 || exit 7
