@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <hipcub/device/device_radix_sort.hpp>
 #include <hipcub/device/device_scan.hpp>
@@ -318,23 +319,66 @@ __device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, in
 }
 
 // a run of small buckets [w0, w1) (each of at most SM_SEG_SMALL edges) in one workgroup, one bucket
-// after the other: classify, Boruvka rounds, sizes; gens from gen0, at most SM_SEG_TAIL_GENS per bucket
-__global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, float c, uint32_t gen0) {
+// after the other.  A bucket's candidates (open-open edges between two components) are few (at most 163
+// per bucket at C2): when they fit in LDS (SEG_LC), the bucket's marked edges -- the minimum spanning
+// forest of its candidates keyed by edge id -- are Kruskal's in id order over the
+// candidates' roots in an LDS union-find (roots hashed to slots), and the joins go back to the global
+// union-find at once: each joined root hooks onto its component's final root, whose size grows by the
+// joined sizes and whose last-join weight becomes w.  Only the candidate scan and that write-back touch
+// global memory (the Boruvka rounds cost several dependent global-atomic phases per bucket).  A bucket
+// with more candidates takes the Boruvka rounds (seg_wg_rounds) and the hooked-root size update; gens
+// from gen0, at most SM_SEG_TAIL_GENS per such bucket.
+constexpr int SEG_LC = 1024;         // candidates of an LDS bucket
+constexpr int SEG_LH = 4096;         // hash slots (power of two, >= 2 SEG_LC)
+constexpr uint32_t SEG_EMPTY = 0xFFFFFFFFu;
+
+__device__ __forceinline__ int seg_lfind(uint16_t* par, int x) {
+    while (par[x] != x) {
+        const int g = par[par[x]];
+        par[x] = (uint16_t)g;
+        x = g;
+    }
+    return x;
+}
+__device__ __forceinline__ int seg_lfind_ro(const uint16_t* par, int x) {
+    while (par[x] != x) x = par[x];
+    return x;
+}
+__device__ __forceinline__ int seg_lslot(uint32_t* hk, uint32_t root) {
+    int h = (int)((root * 2654435761u) >> 20) & (SEG_LH - 1);
+    for (;;) {
+        const uint32_t prev = atomicCAS(hk + h, SEG_EMPTY, root);
+        if (prev == SEG_EMPTY || prev == root) return h;
+        h = (h + 1) & (SEG_LH - 1);
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, float c, uint32_t gen0, uint32_t lc) {
     const SegView& v = sp.v[blockIdx.x];
     __shared__ uint32_t s_n, s_out, s_h0;
+    __shared__ uint32_t s_cid[SEG_LC], s_ord[SEG_LC];
+    __shared__ uint16_t s_sa[SEG_LC], s_sb[SEG_LC];
+    __shared__ uint8_t s_mk[SEG_LC];
+    __shared__ uint32_t s_hk[SEG_LH];
+    __shared__ uint16_t s_par[SEG_LH];
+    const int tid = (int)threadIdx.x;
+    for (int i = tid; i < SEG_LH; i += 1024) {
+        s_hk[i] = SEG_EMPTY;
+        s_par[i] = (uint16_t)i;
+    }
     const uint32_t* start = v.bcnt + SM_SEG_NB;
     uint32_t gen = gen0;
     for (int w = w0; w < w1; ++w) {
         const uint32_t s = start[w], m = start[w + 1] - s;
         if (m == 0) continue;
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             s_n = 0;
             s_h0 = __hip_atomic_load(v.cnt + SM_SEG_C_HOOK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         seg_wg_sync();
         const double wd = (double)w;
         for (uint32_t i0 = 0; i0 < m; i0 += 1024) {
-            const uint32_t i = i0 + threadIdx.x;
+            const uint32_t i = i0 + tid;
             bool cand = false, rej = false;
             uint32_t id = 0, ra = 0, rb = 0;
             if (i < m) {
@@ -344,24 +388,74 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
                 if (ra != rb) {
                     cand = seg_open(v, ra, wd, c) && seg_open(v, rb, wd, c);
                     rej = !cand;
-                    if (cand) {
-                        const unsigned long long key = seg_key(gen, id);
-                        atomicMin(v.best + ra, key);
-                        atomicMin(v.best + rb, key);
-                    }
                 }
             }
             const uint32_t pc = wave_append(&s_n, cand);
-            if (cand) v.list[0][pc] = make_uint4(id, ra, rb, 0u);
+            if (cand) {
+                v.list[0][pc] = make_uint4(id, ra, rb, 0u);
+                if (pc < lc) {  // the LDS copy: id and the roots' hash slots
+                    s_cid[pc] = id;
+                    s_sa[pc] = (uint16_t)seg_lslot(s_hk, ra);
+                    s_sb[pc] = (uint16_t)seg_lslot(s_hk, rb);
+                }
+            }
             const uint32_t pr = wave_append(v.cnt + SM_SEG_C_REJ, rej);
             if (rej) v.rej[pr] = id;
         }
         seg_wg_sync();
-        const int r = seg_wg_rounds(v, 0, s_n, gen, &s_out, true);
+        const uint32_t n = s_n;
+        if (n <= lc) {
+            // Kruskal's order: each candidate's rank among the bucket's ids (distinct)
+            for (uint32_t t = tid; t < n; t += 1024) {
+                const uint32_t id = s_cid[t];
+                uint32_t r = 0;
+                for (uint32_t j = 0; j < n; ++j) r += s_cid[j] < id;
+                s_ord[r] = t;
+            }
+            seg_wg_sync();
+            if (tid == 0)
+                for (uint32_t k = 0; k < n; ++k) {
+                    const uint32_t t = s_ord[k];
+                    const int a = seg_lfind(s_par, s_sa[t]), b = seg_lfind(s_par, s_sb[t]);
+                    s_mk[t] = a != b;
+                    if (a != b) s_par[b] = (uint16_t)a;
+                }
+            seg_wg_sync();
+            // write-back: marked edges; every joined root onto its final root, sizes, last-join weights
+            for (uint32_t t = tid; t < n; t += 1024)
+                if (s_mk[t]) {
+                    const uint32_t id = s_cid[t];
+                    if (id & 1u)
+                        v.mD[id >> 1] = 1;
+                    else
+                        v.mR[id >> 1] = 1;
+                }
+            for (int l = tid; l < SEG_LH; l += 1024) {
+                const uint32_t r = s_hk[l];
+                if (r == SEG_EMPTY) continue;
+                const int f = seg_lfind_ro(s_par, l);
+                if (f == l) continue;
+                const uint32_t rf = s_hk[f];
+                v.par[r] = rf;
+                // r's size is its size at the bucket's start (r was a root); rf is never a joined root
+                atomicAdd(v.sz + rf, __hip_atomic_load(v.sz + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                v.wl[rf] = (uint16_t)w;
+            }
+            seg_wg_sync();
+            for (int l = tid; l < SEG_LH; l += 1024) {  // the table back to empty for the next bucket
+                s_hk[l] = SEG_EMPTY;
+                s_par[l] = (uint16_t)l;
+            }
+            seg_wg_sync();  // sizes final before the next bucket's acceptance tests
+            continue;
+        }
+        // more candidates than the LDS holds: the table back to empty, then the Boruvka rounds
+        for (int l = tid; l < SEG_LH; l += 1024) s_hk[l] = SEG_EMPTY;
+        const int r = seg_wg_rounds(v, 0, n, gen, &s_out, false);
         if (r < 0) return;
         gen += (uint32_t)r;
         const uint32_t h1 = __hip_atomic_load(v.cnt + SM_SEG_C_HOOK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t i = s_h0 + threadIdx.x; i < h1; i += 1024) seg_size_update(v, i, w);
+        for (uint32_t i = s_h0 + tid; i < h1; i += 1024) seg_size_update(v, i, w);
         seg_wg_sync();  // sizes final before the next bucket's acceptance tests
     }
 }
@@ -551,7 +645,9 @@ hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t g
 }
 
 hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0) {
-    hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0);
+    // SM_SEG_NOLDS=1: every small bucket takes the Boruvka rounds (A/B of the LDS Kruskal)
+    const uint32_t lc = getenv("SM_SEG_NOLDS") ? 0u : (uint32_t)SEG_LC;
+    hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0, lc);
     return hipGetLastError();
 }
 
