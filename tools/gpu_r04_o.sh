@@ -16,6 +16,14 @@ PY
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/test_pms_gpu.py \
   -k "gpu_forest_matches or synthetic_modes or full_c2_speculative" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py \
+  -k "segment" > $O/tests_seg.log 2>&1 || { tail -40 $O/tests_seg.log; exit 1; }
+tail -2 $O/tests_seg.log
+for e in SM_SEG_X=0 SM_SEG_NOLDS=1; do
+  env $e SM_SEG_DEBUG=1 timeout -k 10 300 python bench.py --segment-c 5000 --no-cpu --no-pms --steps 16 --warmup 4 > $O/seg_$e.log 2> $O/seg_$e.err || exit 9
+  grep segment_gpu $O/seg_$e.err | tail -1 | cut -c1-200
+  python3 -c "import json;d=json.loads(open('$O/seg_$e.log').read().strip().splitlines()[-1]);print('seg $e', round(d['ms_per_step'],3), 'ms/frame, latency', round(d.get('latency_ms_per_frame'),2))"
+done
 run default SM_PMS_X=0 || exit 2
 run nsu2 SM_PMS_CHAIN_NSU=2 || exit 3
 run nsu2_nsd7 SM_PMS_CHAIN_NSU=2 SM_PMS_CHAIN_NSD=7 || exit 4
