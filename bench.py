@@ -113,6 +113,7 @@ def pms_leg(ctx, left, right, D, iters, oracle):
     later_ms = st["iters_ms"]
     alg = st["evals_later"] * PMS_BYTES_PER_EVAL
     out = dict(iters_per_view=iters, frame_s=wall / 1e3, trees=st["ntrees"], host_prep_ms=st["prep_ms"],
+               prep_segmentation_ms=st.get("prep_seg_ms"), prep_schedule_forest_ms=st.get("prep_forest_ms"),
                setup_ms=st["setup_ms"], first_call_ms=st["iter0_ms"],
                later_call_ms=later_ms / (iters - 1) if iters > 1 else None,
                later_call_ms_per_view=[m / (iters - 1) for m in st["later_ms_view"]] if iters > 1 else None,
