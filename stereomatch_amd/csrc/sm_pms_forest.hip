@@ -19,6 +19,8 @@
 // Every array equals the host construction's (tests/test_pms_gpu.py, SM_PMS_FOREST_CHECK).
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include <hipcub/device/device_radix_sort.hpp>
 #include <hipcub/device/device_scan.hpp>
 
@@ -76,11 +78,40 @@ __device__ __forceinline__ int uf_find(const int32_t* par, int x) {
     return x;
 }
 
+// the same with path halving (k_pf_link: the largest tree's chains are long; every value written is an
+// ancestor, so concurrent halving and linking stay valid)
+__device__ __forceinline__ int uf_find_halve(int32_t* par, int x) {
+    for (;;) {
+        const int p = par[x];
+        if (p == x) return x;
+        const int g = par[p];
+        if (g != p) par[x] = g;
+        x = g;
+    }
+}
+
+// wave-aggregated atomicAdd of `add` to cnt[key] over the lanes with `valid` (lanes sharing a key --
+// consecutive pixels of one tree, heads of one (round, tree) -- make one atomic)
+__device__ __forceinline__ void wave_add_by_key(int32_t* cnt, long long key, int add, bool valid) {
+    unsigned long long act = __ballot(valid);
+    const int lane = __lane_id();
+    while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const long long kl = __shfl(key, leader);
+        const unsigned long long m = __ballot(valid && key == kl) & act;
+        int sum = ((m >> lane) & 1ull) ? add : 0;  // the group's sum: a full wave reduction, others zero
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+        if (lane == leader && sum) atomicAdd(cnt + kl, sum);
+        act &= ~m;
+    }
+}
+
 // link the larger root under the smaller one (the root of a tree ends as its smallest pixel)
 __device__ void uf_union(int32_t* par, int a, int b) {
     for (;;) {
-        a = uf_find(par, a);
-        b = uf_find(par, b);
+        a = uf_find_halve(par, a);
+        b = uf_find_halve(par, b);
         if (a == b) return;
         if (a < b) {
             const int t = a;
@@ -116,12 +147,15 @@ __global__ void k_pf_compress(PfView v) {
 // tid (the flags' exclusive scan, in gpix) -> tree of every pixel, root pixels, sizes
 __global__ void k_pf_trees(PfView v) {
     const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (p >= v.N) return;
-    const int r = v.par[p];
-    const int t = v.gpix[r];
-    v.tree_of[p] = t;
-    if (r == p) v.root_pix[t] = p;
-    atomicAdd(&v.tsize[t], 1);
+    const bool valid = p < v.N;
+    int t = 0;
+    if (valid) {
+        const int r = v.par[p];
+        t = v.gpix[r];
+        v.tree_of[p] = t;
+        if (r == p) v.root_pix[t] = p;
+    }
+    wave_add_by_key(v.tsize, t, 1, valid);  // one atomic per tree in the wave (not 618k on one counter)
 }
 
 // ---------------------------------------------------------------------------------------- BFS
@@ -271,9 +305,14 @@ __device__ void sweep_narrow(const PfView& v, int l, int* s_sz, int* s_state) {
 // One workgroup: the BFS of every tree of the view at once, then the bottom-up sweep.  Level 0 is the
 // roots in tree order; a node's children follow, in key order, at the next level, after the children
 // of the nodes before it.
+constexpr int PF_FC = 4096;  // a level of at most this many nodes is handed to the next one in LDS
+
 __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
     __shared__ int s_w[BT / 64];
     __shared__ int s_q[64], s_pp[64], s_tr[64], s_sz[64], s_state[4];
+    // the frontier of a level (pixel, its parent's pixel, tree), double-buffered: a level's children are
+    // written there too, so the next level reads LDS instead of three dependent global loads
+    __shared__ int s_fp[2][PF_FC], s_fpp[2][PF_FC], s_ftr[2][PF_FC];
     const int tid = (int)threadIdx.x;
     for (int t = tid; t < K; t += BT) {
         v.gpix[t] = v.root_pix[t];
@@ -282,7 +321,8 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
         v.gw[t] = 0;
     }
     __syncthreads();
-    int a = 0, b = K, next = K, d = 0;
+    int a = 0, b = K, next = K, d = 0, cur = 0;
+    bool in_lds = false;  // the roots are in global memory
     while (a < b) {
         if (b - a <= 64) {  // narrow levels on wave 0 (next == b at a level's start)
             if (tid < 64) bfs_narrow(v, a, b, d, s_q, s_pp, s_tr, s_state);
@@ -291,6 +331,7 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
             b = s_state[1];
             d = s_state[2];
             next = b;
+            in_lds = false;
             __syncthreads();  // s_state read by every wave before it is written again
             continue;
         }
@@ -300,10 +341,19 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
             int q[4] = {-1, -1, -1, -1}, c = 0;
             uint32_t wv[4] = {0, 0, 0, 0};
             int tr = 0;
+            int p = 0;
             if (i < b) {
-                const int p = v.gpix[i], gp = v.gpar[i];
-                const int pp = gp >= 0 ? v.gpix[gp] : -1;
-                tr = v.gtree[i];
+                int pp;
+                if (in_lds) {
+                    p = s_fp[cur][i - a];
+                    pp = s_fpp[cur][i - a];
+                    tr = s_ftr[cur][i - a];
+                } else {
+                    p = v.gpix[i];
+                    const int gp = v.gpar[i];
+                    pp = gp >= 0 ? v.gpix[gp] : -1;
+                    tr = v.gtree[i];
+                }
                 const int4 n4 = v.nbr[p];
                 const uint2 w4 = v.nbw[p];
                 const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
@@ -330,11 +380,18 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
                     v.gpar[j] = i;
                     v.gtree[j] = tr;
                     v.gw[j] = (uint16_t)wv[k];
+                    if (j - b < PF_FC) {
+                        s_fp[cur ^ 1][j - b] = q[k];
+                        s_fpp[cur ^ 1][j - b] = p;
+                        s_ftr[cur ^ 1][j - b] = tr;
+                    }
                 }
             }
             next = next + total < v.N ? next + total : v.N;
         }
         __syncthreads();  // this level's writes are visible to the next one's reads
+        in_lds = next - b <= PF_FC;
+        cur ^= 1;
         a = b;
         b = next;
         ++d;
@@ -380,6 +437,22 @@ __global__ void k_pf_iota(int32_t* a, int n) {
 __global__ void k_pf_g2b(PfView v) {
     const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (n < v.N) v.g2b[v.bglob[n]] = n;
+}
+
+// wave-aggregated atomicMax of `val` into cnt[key] (as wave_add_by_key)
+__device__ __forceinline__ void wave_max_by_key(int32_t* cnt, int key, int val, bool valid) {
+    unsigned long long act = __ballot(valid);
+    const int lane = __lane_id();
+    while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const int kl = __shfl(key, leader);
+        const unsigned long long m = __ballot(valid && key == kl) & act;
+        int mx = ((m >> lane) & 1ull) ? val : INT_MIN;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        if (lane == leader) atomicMax(cnt + kl, mx);
+        act &= ~m;
+    }
 }
 
 // BFS-numbered node fields; the heavy path's up-link for the pointer jumping
@@ -430,16 +503,20 @@ __global__ void k_pf_ld_step(PfView v, const int32_t* J) {
 // every node's light depth, the trees' round counts, the view's, and the heads' sort keys
 __global__ void k_pf_ld_all(PfView v, const int32_t* J) {
     const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (n >= v.N) return;
-    const int t = v.gtree_s[n];
-    if (J[n] != n) return;
-    const int l = v.ld[n];
-    if (l < 0 || l > 255) {  // unresolved light depth: an inconsistent schedule, flag it (never key on it)
-        v.tot[7] = 2;
-        return;
+    bool head = false;
+    int t = 0, l = 0;
+    if (n < v.N && J[n] == n) {
+        t = v.gtree_s[n];
+        l = v.ld[n];
+        head = true;
+        if (l < 0 || l > 255) {  // unresolved light depth: an inconsistent schedule, flag it (never key on it)
+            v.tot[7] = 2;
+            head = false;
+        }
     }
-    atomicMax(&v.tree_rounds[t], l + 1);
-    atomicMax(&v.tot[5], l + 1);
+    // one atomic per tree and wave, one per wave for the view's rounds (a tree's heads are contiguous)
+    wave_max_by_key(v.tree_rounds, t, l + 1, head);
+    wave_max_by_key(v.tot, 5, l + 1, head);
 }
 
 // head keys: A = (tree, light depth, BFS id within the tree): the rows' order; B = (light depth,
@@ -532,26 +609,36 @@ __global__ void k_pf_rows(PfView v) {
 // the grid's inter-tree edges as (tree, tree) pairs, both directions (tree_g, :377-384)
 __global__ void k_pf_pairs(PfView v) {
     const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (p >= v.N) return;
-    const int W = v.W, x = p % W, a = v.tree_of[p];
+    const int W = v.W, x = p % W, a = p < v.N ? v.tree_of[p] : 0;
     unsigned long long out[4];
     int c = 0;
-    if (x + 1 < W) {
+    if (p < v.N && x + 1 < W) {
         const int b = v.tree_of[p + 1];
         if (a != b) {
             out[c++] = ((unsigned long long)a << 32) | (uint32_t)b;
             out[c++] = ((unsigned long long)b << 32) | (uint32_t)a;
         }
     }
-    if (p + W < v.N) {
+    if (p < v.N && p + W < v.N) {
         const int b = v.tree_of[p + W];
         if (a != b) {
             out[c++] = ((unsigned long long)a << 32) | (uint32_t)b;
             out[c++] = ((unsigned long long)b << 32) | (uint32_t)a;
         }
     }
-    if (!c) return;
-    const int pos = atomicAdd(v.npairs, c);
+    // one append per wave: an exclusive wave scan of the lanes' pair counts
+    const int lane = __lane_id();
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const int total = __shfl(incl, 63);
+    int base = 0;
+    if (lane == 63 && total) base = atomicAdd(v.npairs, total);
+    base = __shfl(base, 63);
+    const int pos = base + incl - c;
     for (int k = 0; k < c; ++k) v.pairs[0][pos + k] = out[k];
 }
 
@@ -577,13 +664,21 @@ __device__ __forceinline__ void head_of_b(const PfView& v, unsigned long long k,
 
 // B order: per head its pieces, prop items, repair items and chain items (sm_pms_host.cpp's counts), and
 // the per-(round, tree) counts of the four tables
+__device__ long long pf_count_head(const PfView& v, int j, int K, int* cout);
+
 __global__ void k_pf_counts(PfView v, int nh, int K) {
     const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (j > nh) return;
-    if (j == nh) {
+    if (j == nh)
         for (int q = 0; q < 4; ++q) v.hcnt[q][j] = 0;
-        return;
-    }
+    const bool valid = j < nh;
+    int c[4] = {0, 0, 0, 0};
+    long long k = 0;
+    if (valid) k = pf_count_head(v, j, K, c);
+    // heads are in (round, tree) order: one atomic per (round, tree) and wave
+    for (int q = 0; q < 4; ++q) wave_add_by_key(v.rtc[q], k, c[q], valid && c[q] != 0);
+}
+
+__device__ long long pf_count_head(const PfView& v, int j, int K, int* cout) {
     int r, t, h;
     head_of_b(v, v.hkey[1][j], r, t, h);
     const int len = v.plen[h];
@@ -596,11 +691,11 @@ __global__ void k_pf_counts(PfView v, int nh, int K) {
         if (lq >= SM_PMS_CHAIN_LEN) lg += chunks > 1 ? chunks : 1;
     }
     const int c[4] = {np, np * chunks, cut ? (chunks > 1 ? chunks : 1) : 0, lg};
-    const size_t k = (size_t)r * (K + 1) + t;
     for (int q = 0; q < 4; ++q) {
         v.hcnt[q][j] = c[q];
-        if (c[q]) atomicAdd(&v.rtc[q][k], c[q]);
+        cout[q] = c[q];
     }
+    return (long long)r * (K + 1) + t;
 }
 
 // the lists: paths (pieces head first), items, repair items
