@@ -2367,8 +2367,8 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                 long long h[16];
                 HIPC(hipMemcpy(h, d.prof, 16 * 8, hipMemcpyDeviceToHost));
                 fprintf(stderr, "pms prof v%d call %d (ms): prop setup %.2f up %.2f down %.2f update %.2f | ref setup %.2f up %.2f "
-                        "down %.2f update %.2f | rounds %lld\n", v, i, h[0] * 1e-5, h[1] * 1e-5, h[2] * 1e-5, h[3] * 1e-5,
-                        h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5, h[8]);
+                        "down %.2f update %.2f | rounds %lld | guess staging %.3f chain %.3f\n", v, i, h[0] * 1e-5, h[1] * 1e-5,
+                        h[2] * 1e-5, h[3] * 1e-5, h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5, h[8], h[9] * 1e-5, h[10] * 1e-5);
             }
         }
         return SM_OK;

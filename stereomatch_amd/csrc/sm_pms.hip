@@ -568,6 +568,7 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
     extern __shared__ float gsm[];
     const int nt = d.K - t_lo, tid = threadIdx.x;
     const long long o0 = d.off[0];
+    const long long tks = d.prof && tid == 0 ? (long long)wall_clock64() : 0;
     // STAGED: per-tree dd, degree and result offset, and the reachable stream window (wn floats), in
     // LDS -- the chain then touches no global memory (a global access would make every link wait on
     // the previous links' traffic)
@@ -599,6 +600,11 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
         }
         for (long long i = tid; i < wn; i += blockDim.x) sdice[i] = o0 + i < d.dice_n ? d.dice[o0 + i] : 0.0f;
         __syncthreads();
+        long long tk0 = 0;  // SM_PMS_PROF builds: staging / chain wall-clock split (100 MHz ticks)
+        if (d.prof && tid == 0) {
+            tk0 = (long long)wall_clock64();
+            atomicAdd((unsigned long long*)&d.prof[9], (unsigned long long)(tk0 - tks));
+        }
         if (tid < 64) {
             // The chain on one wave with wave-uniform (scalar) state: each tree's degree, classes and dd come
             // from a 64-tree register window and each draw-dependent level's draw from a 64-draw register
@@ -643,6 +649,7 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
             }
         }
         __syncthreads();
+        if (d.prof && tid == 0) atomicAdd((unsigned long long*)&d.prof[10], (unsigned long long)((long long)wall_clock64() - tk0));
         for (int i = tid; i < nt; i += blockDim.x) d.oguess[t_lo + i] = sog[i];
         return;
     }

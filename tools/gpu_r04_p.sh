@@ -18,3 +18,5 @@ f=$(find $O/raw -name '*kernel_stats.csv' | head -1); cp "$f" $O/kernel_stats_pm
 f=$(find $O/raw -name '*kernel_trace.csv' | head -1); cp "$f" $O/kernel_trace_pms2.csv
 rm -rf $O/raw
 grep k_pf_ $O/kernel_stats_pms2.csv | cut -d, -f1-4 | head -12
+SM_PMS_PROF=1 SM_PMS_SEQ_VIEWS=1 timeout -k 10 300 python3 tools/pms_bench.py 1920 1200 128 3 --reps 1 > $O/pms3_prof.log 2>&1 || exit 4
+grep "pms prof" $O/pms3_prof.log
