@@ -1047,6 +1047,7 @@ __global__ void __launch_bounds__(256) k_pms_walk_plan(PmsDev d, int phase, int 
 // parent row (or keeps A_up at a tree root) -- down_walk's operations.  Same bits as the walkers.
 constexpr int PC_G = 8;        // nodes per group
 constexpr int PC_NSU = 4;      // up ring slots (2 KB per node): 67 KB, two workgroups per CU
+constexpr int PC_NSU_MAX = 8;  // SM_PMS_CHAIN_NSU up to this: 133 KB, one workgroup per CU
 constexpr int PC_NSD = 14;     // down ring slots (0.5 KB per node): 58 KB, two workgroups per CU
 constexpr int PC_LW = 7;       // loader waves (+ the chain wave: 512 threads)
 
@@ -1647,12 +1648,12 @@ hipError_t launch_pms_chain(hipStream_t st, const PmsDev& d, int phase, bool up,
     // SM_PMS_CHAIN_NSU / _NSD: ring slots of the up / down chain (LDS per workgroup, so workgroups per CU)
     const char* eu = getenv("SM_PMS_CHAIN_NSU");
     const char* ed = getenv("SM_PMS_CHAIN_NSD");
-    const int nsu = eu ? std::min(std::max(atoi(eu), 1), PC_NSU) : PC_NSU;
+    const int nsu = eu ? std::min(std::max(atoi(eu), 1), PC_NSU_MAX) : PC_NSU;
     const int nsd = ed ? std::min(std::max(atoi(ed), 1), PC_NSD) : PC_NSD;
     const int ns = up ? nsu : nsd;
     const size_t lds = up ? ns * sizeof(PcUpSlot) : ns * sizeof(PcDnSlot);
     static const hipError_t a0 = hipFuncSetAttribute((const void*)k_pms_chain<true>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_NSU * sizeof(PcUpSlot)));
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_NSU_MAX * sizeof(PcUpSlot)));
     static const hipError_t a1 = hipFuncSetAttribute((const void*)k_pms_chain<false>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_NSD * sizeof(PcDnSlot)));
     if (a0 != hipSuccess) return a0;
