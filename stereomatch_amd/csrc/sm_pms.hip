@@ -608,45 +608,81 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
         if (tid < 64) {
             // The chain on one wave with wave-uniform (scalar) state: each tree's degree, classes and dd come
             // from a 64-tree register window and each draw-dependent level's draw from a 64-draw register
-            // window, both by readlane, so a link costs no LDS round trip unless a window is refilled.
-            long long o = o0;
+            // window, both by readlane, so a link costs no LDS round trip unless a window is refilled.  Only
+            // the draw-dependent (class 2) levels are visited: the fixed levels between them advance the
+            // offset by popcounts (4 draws per always-in level, 1 per always-out one), and level i's
+            // max_d = (Dmax / 2) * 2^-i exactly (the loop's halvings).  A tree whose draws could pass the end
+            // of the stream takes the level-by-level loop with ref_count's checks.
+            const int lane = tid;
+            int nlev = 0;
+            for (float md = 0.5f * fmax; md > 0.1f; md *= 0.5f) ++nlev;
+            const uint32_t lvmask = nlev >= 16 ? 0xFFFFFFFFu : (1u << (2 * nlev)) - 1u;
+            long long o = o0, og_w = 0;
             int tw = -64, wdeg = 0, wcls = 0, wdd = 0;
             long long kw = LLONG_MIN / 2;
             float wdice = 0.0f;
+            auto draw = [&](long long k) {
+                if (k >= kw + 64) {  // the next 64 draws from k
+                    kw = k;
+                    const long long q = k - o0 + lane;
+                    wdice = q < wn ? sdice[q] : 0.0f;
+                }
+                return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdice), (int)(k - kw)));
+            };
             for (int t = 0; t < nt; ++t) {
-                if (t - tw >= 64) {  // the next 64 trees
+                if (t - tw >= 64) {  // the next 64 trees (the finished window's offsets to LDS)
+                    if (tw >= 0 && tw + lane < nt) sog[tw + lane] = og_w;
                     tw = t;
-                    const int ti = t + tid;
+                    const int ti = t + lane;
                     wdeg = ti < nt ? sdeg[2 * ti] : 0;
                     wcls = ti < nt ? sdeg[2 * ti + 1] : 0;
                     wdd = ti < nt ? __float_as_int(sdd[ti]) : 0;
                 }
-                if (tid == 0) sog[t] = o;
+                if (lane == t - tw) og_w = o;
                 const int deg = __builtin_amdgcn_readlane(wdeg, t - tw);
-                uint32_t cls = (uint32_t)__builtin_amdgcn_readlane(wcls, t - tw);
+                const uint32_t cls = (uint32_t)__builtin_amdgcn_readlane(wcls, t - tw) & lvmask;
                 const float dd = __int_as_float(__builtin_amdgcn_readlane(wdd, t - tw));
                 long long k = o + deg;
-                for (float md = 0.5f * fmax; md > 0.1f; md *= 0.5f, cls >>= 2) {  // ref_count's levels
-                    if (k + 4 > d.dice_n) {
-                        if (tid == 0) atomicOr(d.err, 4u);
-                        break;
-                    }
-                    const uint32_t c = cls & 3u;
-                    bool in = c == 1u;
-                    if (c == 2u) {
-                        if (k >= kw + 64) {  // the next 64 draws from k
-                            kw = k;
-                            const long long q = k - o0 + tid;
-                            wdice = q < wn ? sdice[q] : 0.0f;
+                if (k + 4ll * nlev > d.dice_n) {  // near the end of the stream: ref_count's checks level by level
+                    uint32_t c2 = cls;
+                    for (float md = 0.5f * fmax; md > 0.1f; md *= 0.5f, c2 >>= 2) {
+                        if (k + 4 > d.dice_n) {
+                            if (lane == 0) atomicOr(d.err, 4u);
+                            break;
                         }
-                        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdice), (int)(k - kw)));
-                        const float rd = fmaf(r, md, dd);
-                        in = !(rd < 0.0f || rd > fmax);
+                        const uint32_t c = c2 & 3u;
+                        bool in = c == 1u;
+                        if (c == 2u) {
+                            const float rd = fmaf(draw(k), md, dd);
+                            in = !(rd < 0.0f || rd > fmax);
+                        }
+                        k += in ? 4 : 1;
                     }
-                    k += in ? 4 : 1;
+                    o = k;
+                    continue;
                 }
+                // per level 2 bits: 01 in, 00 out, 10 draw-dependent; odd bits mark class 2, even bits class 1
+                const uint32_t hi = cls & 0xAAAAAAAAu, lo = cls & 0x55555555u;
+                uint32_t c2 = hi;
+                int lvl = 0;  // the next level not yet counted (bit 2 * lvl)
+                while (c2) {
+                    const int b = __builtin_ctz(c2);  // bit 2i + 1 of class-2 level i
+                    const int i = b >> 1;
+                    const uint32_t below = (1u << (2 * i)) - (1u << (2 * lvl));  // levels [lvl, i), both bits
+                    const int nin = __builtin_popcount(lo & below), nfix = i - lvl;
+                    k += 4 * nin + (nfix - nin);
+                    const float md = ldexpf(0.5f * fmax, -i);
+                    const float rd = fmaf(draw(k), md, dd);
+                    k += !(rd < 0.0f || rd > fmax) ? 4 : 1;
+                    lvl = i + 1;
+                    c2 &= c2 - 1;
+                }
+                const uint32_t rest = lvmask & ~((1u << (2 * lvl)) - 1u);  // levels [lvl, nlev)
+                const int nin = __builtin_popcount(lo & rest), nfix = nlev - lvl;
+                k += 4 * nin + (nfix - nin);
                 o = k;
             }
+            if (tw >= 0 && tw + lane < nt) sog[tw + lane] = og_w;
         }
         __syncthreads();
         if (d.prof && tid == 0) atomicAdd((unsigned long long*)&d.prof[10], (unsigned long long)((long long)wall_clock64() - tk0));
