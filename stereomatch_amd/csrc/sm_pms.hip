@@ -470,14 +470,24 @@ __device__ int ref_levels(const PmsDev& d, int t, long long o, bool write) {
 }
 
 // ----------------------------------------------------------------------------- serial mode
+constexpr int PMS_SER_MAXP = 1024;  // paths of a round that k_pms_serial sorts into lane groups
+// A path of at least PMS_GLONG rows goes to the wave walker whatever its P: its walk is a latency chain,
+// and the wave walker issues PMS_CH nodes per memory round trip against the group walker's PMS_GCH.
+constexpr int PMS_GLONG = 48;
+template <int GW>
+__device__ void up_group(const PmsDev& d, const double* __restrict__ sS, int phase, int path);
+template <int GW>
+__device__ void down_group(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
+                           int path);
 __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
     __shared__ long long s_off;
-    __shared__ int s_n;
+    __shared__ int s_n, s_ns, s_nl;
     __shared__ float s_dice[64];
+    __shared__ int s_short[PMS_SER_MAXP], s_long[PMS_SER_MAXP];
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
     load_luts(d, sS, sS2);
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int wave = tid >> 6, nwaves = nt >> 6;
+    const int wave = tid >> 6, nwaves = nt >> 6, lane = tid & 63;
     // SM_PMS_PROF builds: per-segment wall-clock totals (100 MHz ticks) of thread 0
     long long tick = 0;
     auto seg = [&](int k) {
@@ -521,25 +531,60 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
                 __threadfence_block();
                 __syncthreads();
                 const int32_t* rt = phase == 0 ? d.rt_item : d.rt_path;
-                for (int r = R - 1; r >= 0; --r) {  // leaf -> root: deepest light depth first
-                    const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
-                    for (int it = lo + wave; it < hi; it += nwaves) {
-                        if (phase == 0) up_item(d, sS, 0, d.items[it].path, d.items[it].chunk);
-                        else up_item(d, sS, 1, it, 0);
+                int Pw, bw;
+                phase_labels(d, phase, t, Pw, bw);  // the walkers' proposal count
+                // A round of a tree with few proposals (P <= 8): its short paths (< PMS_GLONG rows) in lane
+                // groups, 32 (P <= 2) or 8 paths per wave (the planned walks' up_group / down_group), the long
+                // ones by the wave walker -- instead of one wave per path, which left a round with many short
+                // paths waiting on 16 waves.  Otherwise one wave per (path, 64-proposal chunk) item.
+                auto round = [&](int r, bool up) {
+                    const int plo = d.rt_path[(size_t)r * (d.K + 1) + t], phi = d.rt_path[(size_t)r * (d.K + 1) + t + 1];
+                    const int np = phi - plo;
+                    if (Pw <= 8 && np <= PMS_SER_MAXP) {
+                        if (tid == 0) {
+                            s_ns = 0;
+                            s_nl = 0;
+                        }
+                        __syncthreads();
+                        for (int k = tid; k < np; k += nt) {
+                            if (d.paths[plo + k].len < PMS_GLONG) s_short[atomicAdd(&s_ns, 1)] = plo + k;
+                            else s_long[atomicAdd(&s_nl, 1)] = plo + k;
+                        }
+                        __syncthreads();
+                        const int ns = s_ns, nl = s_nl, GP = Pw <= 2 ? 32 : 8, ng = (ns + GP - 1) / GP;
+                        for (int w = wave; w < ng + nl; w += nwaves) {
+                            if (w < ng) {
+                                if (GP == 32) {
+                                    const int k = w * 32 + lane / 2;
+                                    const int path = k < ns ? s_short[k] : -1;
+                                    if (up) up_group<2>(d, sS, phase, path);
+                                    else down_group<2>(d, sS, sS2, phase, path);
+                                } else {
+                                    const int k = w * 8 + lane / 8;
+                                    const int path = k < ns ? s_short[k] : -1;
+                                    if (up) up_group<8>(d, sS, phase, path);
+                                    else down_group<8>(d, sS, sS2, phase, path);
+                                }
+                            } else {
+                                const int path = s_long[w - ng];
+                                if (up) up_item(d, sS, phase, path, 0);
+                                else down_item(d, sS, sS2, phase, path, 0);
+                            }
+                        }
+                    } else {
+                        const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
+                        for (int it = lo + wave; it < hi; it += nwaves) {
+                            const int path = phase == 0 ? d.items[it].path : it, chunk = phase == 0 ? d.items[it].chunk : 0;
+                            if (up) up_item(d, sS, phase, path, chunk);
+                            else down_item(d, sS, sS2, phase, path, chunk);
+                        }
                     }
                     __threadfence_block();
                     __syncthreads();
-                }
+                };
+                for (int r = R - 1; r >= 0; --r) round(r, true);  // leaf -> root: deepest light depth first
                 seg(4 * phase + 1);
-                for (int r = 0; r < R; ++r) {  // root -> leaf
-                    const int lo = rt[(size_t)r * (d.K + 1) + t], hi = rt[(size_t)r * (d.K + 1) + t + 1];
-                    for (int it = lo + wave; it < hi; it += nwaves) {
-                        if (phase == 0) down_item(d, sS, sS2, 0, d.items[it].path, d.items[it].chunk);
-                        else down_item(d, sS, sS2, 1, it, 0);
-                    }
-                    __threadfence_block();
-                    __syncthreads();
-                }
+                for (int r = 0; r < R; ++r) round(r, false);  // root -> leaf
                 seg(4 * phase + 2);
                 if (d.evals && tid == 0) atomicAdd(d.evals, (unsigned long long)(te - ts) * (unsigned long long)P);
                 for (int row = ts + tid; row < te; row += nt) update_row(d, phase, row, t);
@@ -985,9 +1030,6 @@ __device__ void down_group(const PmsDev& d, const double* __restrict__ sS, const
 }
 
 // The plan of trees [t_lo, t_hi) for one phase: blockIdx.y = round r, one thread per path of the round.
-// A path of at least PMS_GLONG rows goes to the wave walker whatever its P: its walk is a latency chain,
-// and the wave walker issues PMS_CH nodes per memory round trip against the group walker's PMS_GCH.
-constexpr int PMS_GLONG = 48;
 constexpr int PMS_CHAIN_LEN = SM_PMS_CHAIN_LEN;  // from here on: k_pms_chain
 
 __global__ void __launch_bounds__(1024) k_pms_plan(PmsDev d, int phase, int t_lo, int t_hi, int chain_len) {
