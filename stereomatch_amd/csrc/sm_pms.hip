@@ -1205,10 +1205,12 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                     const int row = r0 + itop - kk, w0 = (itop - kk - ilo) * 10;
                     const uint32_t w6 = meta_dw(m, w0 + 6);
                     const int nch = (int)((w6 >> 16) & 255u), hk = (int)(w6 >> 24);
+                    // only the light children's rows (wave-uniform tests): most nodes have none, and the
+                    // dummy reloads of absent children made the up loaders 5 row loads per node
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const int crow = (q < nch && q != hk) ? (int)meta_dw(m, w0 + 2 + q) : row;
-                        cv[k][q] = Al[(size_t)(crow - ts) * pt];
+                        cv[k][q] = 0.0;
+                        if (q < nch && q != hk) cv[k][q] = Al[(size_t)((int)meta_dw(m, w0 + 2 + q) - ts) * pt];
                     }
                     cost[k] = Al[(size_t)(row - ts) * pt];
                 }
