@@ -193,10 +193,9 @@ __device__ bool up_walk(const PmsDev& d, const double* __restrict__ sS, int phas
             wc[k][2] = (int)(w8 & 0xFFFFu);
             wc[k][3] = (int)(w8 >> 16);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const bool use = q < nch[k] && q != hk[k];
-                const int crow = use ? (int)meta_dw(mc, w0 + 2 + q) : row;
-                cv[k][q] = Al[(size_t)(crow - ts) * pt];  // read only where used (serial part)
+            for (int q = 0; q < 4; ++q) {  // only the light children's rows (wave-uniform tests, no dummy loads)
+                cv[k][q] = 0.0;
+                if (q < nch[k] && q != hk[k]) cv[k][q] = Al[(size_t)((int)meta_dw(mc, w0 + 2 + q) - ts) * pt];
             }
             if (PRE) {
                 cost[k] = Al[(size_t)(row - ts) * pt];
@@ -948,8 +947,8 @@ __device__ void up_group(const PmsDev& d, const double* __restrict__ sS, int pha
             const uint32_t ch[4] = {mc[k].c01.x, mc[k].c01.y, mc[k].c23.x, mc[k].c23.y};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int crow = (q < nch && q != hk) ? (int)ch[q] : row;
-                cv[k][q] = A[(size_t)(crow - ts) * pt];
+                cv[k][q] = 0.0;  // only the light children's rows (no dummy loads of absent ones)
+                if (q < nch && q != hk) cv[k][q] = A[(size_t)((int)ch[q] - ts) * pt];
             }
             cost[k] = A[(size_t)(row - ts) * pt];
         }
