@@ -1904,6 +1904,15 @@ sm_status pms_serial_range(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, 
             CHECK(pms_phase(ctx, st, v, d, 0, t, t + 1));
         }
         HIPC(launch_pms_ref_one(st, d, t));
+        // a refinement that drew no in-range level (nref == 0, most of a first call's trees) has nothing to
+        // walk: its ~20 launches would all be empty, so read the count back (the view's pinned result slot)
+        // and skip the phase (SM_PMS_REF_ALWAYS=1: always launch it, A/B)
+        int32_t* h_nref = ctx->h_pms_res + 4 * v + 3;
+        if (!(getenv("SM_PMS_REF_ALWAYS") && atoi(getenv("SM_PMS_REF_ALWAYS")) == 1)) {
+            HIPC(hipMemcpyAsync(h_nref, P<int32_t>(ctx->pms[v].nref) + t, 4, hipMemcpyDeviceToHost, st));
+            HIPC(hipStreamSynchronize(st));
+            if (*h_nref == 0) continue;
+        }
         CHECK(pms_phase(ctx, st, v, d, 1, t, t + 1));
     }
     return SM_OK;

@@ -62,7 +62,8 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
     assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
 
 
-@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "chainstream"])
+@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "chainstream",
+                                  "refalways"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
@@ -94,6 +95,10 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         monkeypatch.setenv("SM_PMS_CHAIN_STREAM", "1")
     else:
         monkeypatch.delenv("SM_PMS_CHAIN_STREAM", raising=False)
+    if mode == "refalways":  # a large tree's empty refinement phase launched anyway (default: skipped)
+        monkeypatch.setenv("SM_PMS_REF_ALWAYS", "1")
+    else:
+        monkeypatch.delenv("SM_PMS_REF_ALWAYS", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
