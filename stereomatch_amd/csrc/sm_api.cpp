@@ -1794,14 +1794,16 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
     // the phase's A rows packed by its proposal counts (k_pms_layout; SM_PMS_STATIC_ROWS=1: the static
     // max-degree layout, A/B)
     PmsDev d = d0;
-    if (!(getenv("SM_PMS_STATIC_ROWS") && atoi(getenv("SM_PMS_STATIC_ROWS")) == 1)) {
-        HIPC(launch_pms_layout(st, d0, phase, t_lo, t_hi, P<int32_t>(ctx->pms[v].pt_ph), P<long long>(ctx->pms[v].ab_ph)));
-        d.tree_pt = P<int32_t>(ctx->pms[v].pt_ph);
-        d.tree_abase = P<long long>(ctx->pms[v].ab_ph);
-    }
     const size_t K1 = (size_t)f.K + 1;
     int R = 0;
     for (int t = t_lo; t < t_hi; ++t) R = std::max(R, f.tree_rounds[t]);
+    const bool packed = !(getenv("SM_PMS_STATIC_ROWS") && atoi(getenv("SM_PMS_STATIC_ROWS")) == 1);
+    if (packed) {  // (the layout launch also zeroes the plan's counters)
+        HIPC(launch_pms_layout(st, d0, phase, t_lo, t_hi, P<int32_t>(ctx->pms[v].pt_ph), P<long long>(ctx->pms[v].ab_ph),
+                               d0.plan_cnt, PMS_NCNT * R));
+        d.tree_pt = P<int32_t>(ctx->pms[v].pt_ph);
+        d.tree_abase = P<long long>(ctx->pms[v].ab_ph);
+    }
     const std::vector<int32_t>& rt = phase == 0 ? f.rt_item : f.rt_path;
     HIPC(launch_pms_cost(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
     const bool wave_walk = getenv("SM_PMS_WAVE_WALK") && atoi(getenv("SM_PMS_WAVE_WALK")) == 1;
@@ -1822,7 +1824,7 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
         }
         // SM_PMS_CHAIN_MIN: the chain threshold (at least SM_PMS_CHAIN_LEN, whose counts bound the grid)
         const char* cm = getenv("SM_PMS_CHAIN_MIN");
-        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains ? (cm ? atoi(cm) : SM_PMS_CHAIN_DEFAULT) : 0));
+        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains ? (cm ? atoi(cm) : SM_PMS_CHAIN_DEFAULT) : 0, packed));
     }
     // pieces: every guessed piece repairs at once, then a gated sequential pass (SM_PMS_SEQ_REPAIR=1: the
     // sequential pass alone, A/B); maxp[r] = the most pieces of a cut repaired in round r
@@ -2376,8 +2378,11 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                 long long h[16];
                 HIPC(hipMemcpy(h, d.prof, 16 * 8, hipMemcpyDeviceToHost));
                 fprintf(stderr, "pms prof v%d call %d (ms): prop setup %.2f up %.2f down %.2f update %.2f | ref setup %.2f up %.2f "
-                        "down %.2f update %.2f | rounds %lld | guess staging %.3f chain %.3f\n", v, i, h[0] * 1e-5, h[1] * 1e-5,
-                        h[2] * 1e-5, h[3] * 1e-5, h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5, h[8], h[9] * 1e-5, h[10] * 1e-5);
+                        "down %.2f update %.2f | rounds %lld | guess staging %.3f chain %.3f | up chain items %lld: longest %.1f us "
+                        "(%lld rows), mean %.1f us, mean %.0f rows\n", v, i, h[0] * 1e-5, h[1] * 1e-5,
+                        h[2] * 1e-5, h[3] * 1e-5, h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5, h[8], h[9] * 1e-5, h[10] * 1e-5,
+                        h[14], (double)(h[11] >> 24) * 1e-2, h[11] & 0xFFFFFF, h[14] ? h[12] * 1e-2 / h[14] : 0.0,
+                        h[14] ? (double)h[13] / h[14] : 0.0);
             }
         }
         return SM_OK;

@@ -95,13 +95,14 @@ hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, 
 // one round's chain items (k_pms_chain): `items` workgroups (the host's bound on the round's long items)
 hipError_t launch_pms_chain(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int items);
 // the phase's A-row layout of trees [t_lo, t_hi): stride P rounded up to even, packed (k_pms_layout)
+// (and zeroes zero[0, nzero): the phase's plan counters, so launch_pms_plan needs no memset)
 hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int32_t* pt_out,
-                             long long* ab_out);
-// the walk plan of trees [t_lo, t_hi) for a phase (plan_cnt zeroed here); r_lo..r_hi: rounds to plan
+                             long long* ab_out, int32_t* zero = nullptr, int nzero = 0);
+// the walk plan of trees [t_lo, t_hi) for a phase (plan_cnt zeroed here unless `zeroed`); r_lo..r_hi: rounds to plan
 // chain_len > 0: paths of >= max(chain_len, SM_PMS_CHAIN_LEN) rows become chain items (k_pms_chain);
 // 0: none (wave items)
 hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths,
-                           int chain_len);
+                           int chain_len, bool zeroed = false);
 // one round's planned walk, a persistent grid of `waves` waves (the host's bound on the work)
 hipError_t launch_pms_walk_plan(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int waves);
 hipError_t launch_pms_cost(hipStream_t st, const PmsDev& d, int phase, int row_lo, int row_hi);

@@ -849,9 +849,10 @@ __global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, i
 // size x stride, into pt_out / ab_out, which the phase's kernels then take as tree_pt / tree_abase.
 // A rows are scratch of one phase (the outputs are minc and abc), so each phase may lay them out anew.
 __global__ void __launch_bounds__(1024) k_pms_layout(PmsDev d, int phase, int t_lo, int t_hi, int32_t* pt_out,
-                                                     long long* ab_out) {
+                                                     long long* ab_out, int32_t* zero, int nzero) {
     __shared__ long long s_w[16];
     const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < nzero; i += 1024) zero[i] = 0;  // the phase's plan counters (k_pms_plan), one launch fewer
     long long base = 0;
     for (int t0 = t_lo; t0 < t_hi; t0 += 1024) {
         const int t = t0 + tid;
@@ -1246,6 +1247,7 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
             }
         } else {  // the chain wave
             double x = 0.0;  // the bottom row's heavy child: a leaf's none, a cut piece's guess 0
+            const long long tc0 = d.prof ? (long long)wall_clock64() : 0;  // SM_PMS_PROF: per-item timing
             for (int g = 0; g < ngroups; ++g) {
                 const int s = g % NS;
                 pc_wait_ge(&s_staged[s], g + 1);
@@ -1280,6 +1282,13 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                     x = cst[k] + acc;
                     if (act) A[(size_t)(r0 + itop - k - ts) * pt] = x;
                 }
+            }
+            if (d.prof && lane == 0) {  // the call's longest up item (ticks << 24 | rows), totals
+                const long long dt = (long long)wall_clock64() - tc0;
+                atomicMax((unsigned long long*)&d.prof[11], (unsigned long long)((dt << 24) | (long long)len));
+                atomicAdd((unsigned long long*)&d.prof[12], (unsigned long long)dt);
+                atomicAdd((unsigned long long*)&d.prof[13], (unsigned long long)len);
+                atomicAdd((unsigned long long*)&d.prof[14], 1ull);
             }
         }
     } else {
@@ -1706,17 +1715,19 @@ hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, 
 }
 
 hipError_t launch_pms_layout(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int32_t* pt_out,
-                             long long* ab_out) {
+                             long long* ab_out, int32_t* zero, int nzero) {
     if (t_hi <= t_lo) return hipSuccess;
-    hipLaunchKernelGGL(k_pms_layout, dim3(1), dim3(1024), 0, st, d, phase, t_lo, t_hi, pt_out, ab_out);
+    hipLaunchKernelGGL(k_pms_layout, dim3(1), dim3(1024), 0, st, d, phase, t_lo, t_hi, pt_out, ab_out, zero, nzero);
     return hipGetLastError();
 }
 
 hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo, int t_hi, int nrounds, int max_paths,
-                           int chain_len) {
+                           int chain_len, bool zeroed) {
     if (t_hi <= t_lo || nrounds <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(d.plan_cnt, 0, sizeof(int32_t) * PMS_NCNT * (size_t)nrounds, st);
-    if (e != hipSuccess) return e;
+    if (!zeroed) {  // (k_pms_layout zeroes the counters when it runs first)
+        hipError_t e = hipMemsetAsync(d.plan_cnt, 0, sizeof(int32_t) * PMS_NCNT * (size_t)nrounds, st);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_pms_plan, dim3(blocks((size_t)std::max(max_paths, 1), 1024), (unsigned)nrounds), dim3(1024), 0, st, d,
                        phase, t_lo, t_hi, chain_len > 0 ? std::max(chain_len, PMS_CHAIN_LEN) : INT_MAX);
     return hipGetLastError();
