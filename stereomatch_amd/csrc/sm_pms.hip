@@ -1128,7 +1128,6 @@ constexpr int PC_NSU = 4;      // up ring slots (2 KB per node): 67 KB, two work
 constexpr int PC_NSU_MAX = 8;  // SM_PMS_CHAIN_NSU up to this: 133 KB, one workgroup per CU
 constexpr int PC_NSD = 14;     // down ring slots (0.5 KB per node): 58 KB, two workgroups per CU
 constexpr int PC_LW = 7;       // loader waves (+ the chain wave: 512 threads)
-constexpr int PC_LWU = PC_LW - 1;  // up: one of them is the storer wave
 
 struct PcUpSlot {
     double2 pc[PC_G][64];  // (pre, cost): one 16-byte LDS read per node and lane
@@ -1161,7 +1160,7 @@ template <bool UP>
 __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, int ns) {
     extern __shared__ double2 pc_lds[];  // 16-byte aligned: the up ring is read as double2
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
-    __shared__ int s_staged[PC_NSD], s_freed, s_done;
+    __shared__ int s_staged[PC_NSD], s_freed;
     const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int NS = ns;  // ring slots (<= PC_NSU / PC_NSD): fewer slots, more workgroups per CU
     // the grid is the schedule's bound (paths of >= SM_PMS_CHAIN_LEN rows); blocks past the plan's chain
@@ -1172,10 +1171,7 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
         sS2[i] = d.s2lut[i];
     }
     if (tid < PC_NSD) s_staged[tid] = 0;
-    if (tid == 0) {
-        s_freed = 0;
-        s_done = 0;
-    }
+    if (tid == 0) s_freed = 0;
     __syncthreads();
     const PmsItem it = d.plan_item[(size_t)d.item_cap + d.plan_ibase[r] + blockIdx.x];
     const PmsPath pa = d.paths[it.path];
@@ -1190,18 +1186,15 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
     const int ngroups = (len + PC_G - 1) / PC_G;
     if (UP) {
         PcUpSlot* ring = reinterpret_cast<PcUpSlot*>(pc_lds);
-        // Up: wave 0 runs the chain and writes each node's result back into its slot, wave 1 stores the
-        // results (no global store on the chain wave: with the stores there, the chain wave ran at ~200 ns
-        // per node, its outstanding stores waiting on memory), waves 2.. load
-        if (wave >= 2) {  // loaders: groups wave - 2, wave - 2 + PC_LWU, ...
+        if (wave > 0) {  // loaders: groups wave - 1, wave - 1 + PC_LW, ...
             // a group's metadata is loaded during the previous group (after its row loads), so each group
             // costs one memory round trip (metadata -> rows was two)
             auto gmeta = [&](int gg) {
                 const int it = len - 1 - gg * PC_G, il = it - PC_G + 1 > 0 ? it - PC_G + 1 : 0;
                 return meta_load(d.rows, r0 + il, it - il + 1);
             };
-            ChunkMeta m = gmeta(wave - 2 < ngroups ? wave - 2 : 0);  // unconditional (clamped)
-            for (int g = wave - 2; g < ngroups; g += PC_LWU) {
+            ChunkMeta m = gmeta(wave - 1 < ngroups ? wave - 1 : 0);  // unconditional (clamped)
+            for (int g = wave - 1; g < ngroups; g += PC_LW) {
                 const int itop = len - 1 - g * PC_G;                 // the group's first (lowest) node
                 const int ilo = itop - PC_G + 1 > 0 ? itop - PC_G + 1 : 0;
                 const int n = itop - ilo + 1;
@@ -1221,9 +1214,9 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                     }
                     cost[k] = Al[(size_t)(row - ts) * pt];
                 }
-                const ChunkMeta mn = gmeta(g + PC_LWU < ngroups ? g + PC_LWU : g);  // the next group's (clamped)
+                const ChunkMeta mn = gmeta(g + PC_LW < ngroups ? g + PC_LW : g);  // the next group's (clamped)
                 const int s = g % NS;
-                pc_wait_ge(&s_freed, g - NS + 1);  // the slot's previous group is stored
+                pc_wait_ge(&s_freed, g - NS + 1);  // the slot's previous group is consumed
                 PcUpSlot& sl = ring[s];
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
@@ -1252,28 +1245,13 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                 pc_publish(&s_staged[s], g + 1);
                 m = mn;
             }
-        } else if (wave == 1) {  // the storer: a group's results from its slot to the A rows, then free the slot
-            for (int g = 0; g < ngroups; ++g) {
-                const int s = g % NS;
-                pc_wait_ge(&s_done, g + 1);
-                const PcUpSlot& sl = ring[s];
-                const int itop = len - 1 - g * PC_G;
-                const int n = itop + 1 < PC_G ? itop + 1 : PC_G;
-                double res[PC_G];
-#pragma unroll
-                for (int k = 0; k < PC_G; ++k) res[k] = sl.pc[k][lane].x;
-                pc_publish(&s_freed, g + 1);  // (after the reads have landed)
-#pragma unroll
-                for (int k = 0; k < PC_G; ++k)
-                    if (k < n && act) A[(size_t)(r0 + itop - k - ts) * pt] = res[k];
-            }
         } else {  // the chain wave
             double x = 0.0;  // the bottom row's heavy child: a leaf's none, a cut piece's guess 0
             const long long tc0 = d.prof ? (long long)wall_clock64() : 0;  // SM_PMS_PROF: per-item timing
             for (int g = 0; g < ngroups; ++g) {
                 const int s = g % NS;
                 pc_wait_ge(&s_staged[s], g + 1);
-                PcUpSlot& sl = ring[s];
+                const PcUpSlot& sl = ring[s];
                 const int itop = len - 1 - g * PC_G;
                 const int n = itop + 1 < PC_G ? itop + 1 : PC_G;
                 // the whole group from LDS in one batch, then the recurrence from registers (absent posts
@@ -1292,22 +1270,18 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                     s2[k] = sl.s2[k];
                     np3 |= (sl.np[k] >= 3) << k;
                 }
-                double res[PC_G];
+                pc_publish_ordered(&s_freed, g + 1);  // the slot's reads are issued: free it
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
-                    res[k] = 0.0;
-                    if (k >= n) continue;
+                    if (k >= n) break;
                     double acc = fma(x, sh[k], pre[k]);  // a leaf: fma(0, 0, +0) = +0
                     acc = fma(p1[k], s1[k], acc);
                     acc = fma(p2[k], s2[k], acc);
                     if (__builtin_expect((np3 >> k) & 1, 0))  // a tree root's third post-heavy child
                         acc = fma(Al[(size_t)(sl.p3row[k] - ts) * pt], sl.s3[k], acc);
                     x = cst[k] + acc;
-                    res[k] = x;
+                    if (act) A[(size_t)(r0 + itop - k - ts) * pt] = x;
                 }
-#pragma unroll
-                for (int k = 0; k < PC_G; ++k) sl.pc[k][lane].x = res[k];  // the results for the storer
-                pc_publish(&s_done, g + 1);
             }
             if (d.prof && lane == 0) {  // the call's longest up item (ticks << 24 | rows), totals
                 const long long dt = (long long)wall_clock64() - tc0;
