@@ -1270,6 +1270,14 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                     s2[k] = sl.s2[k];
                     np3 |= (sl.np[k] >= 3) << k;
                 }
+                // a tree root's third post-heavy child (rare): its row and S read before the slot is released
+                int p3row = 0;
+                double s3 = 0.0;
+                if (np3) {
+                    const int k3 = __builtin_ctz(np3);  // at most one root per path
+                    p3row = sl.p3row[k3];
+                    s3 = sl.s3[k3];
+                }
                 pc_publish_ordered(&s_freed, g + 1);  // the slot's reads are issued: free it
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
@@ -1278,7 +1286,7 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                     acc = fma(p1[k], s1[k], acc);
                     acc = fma(p2[k], s2[k], acc);
                     if (__builtin_expect((np3 >> k) & 1, 0))  // a tree root's third post-heavy child
-                        acc = fma(Al[(size_t)(sl.p3row[k] - ts) * pt], sl.s3[k], acc);
+                        acc = fma(Al[(size_t)(p3row - ts) * pt], s3, acc);
                     x = cst[k] + acc;
                     if (act) A[(size_t)(r0 + itop - k - ts) * pt] = x;
                 }
