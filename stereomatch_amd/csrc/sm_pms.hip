@@ -1132,8 +1132,9 @@ constexpr int PC_LW = 7;       // loader waves (+ the chain wave: 512 threads)
 struct PcUpSlot {
     double2 pc[PC_G][64];  // (pre, cost): one 16-byte LDS read per node and lane
     double2 pp[PC_G][64];  // (post1, post2)
-    double sh[PC_G], s1[PC_G], s2[PC_G], s3[PC_G];
-    int np[PC_G], p3row[PC_G];
+    double sh[PC_G], s1[PC_G], s2[PC_G];
+    double s3;   // the group's node with a third post-heavy child (a tree root; at most one): its S,
+    int k3, p3;  // its index in the group (-1: none) and the child's row
 };
 struct PcDnSlot {
     double T[PC_G][64];
@@ -1218,6 +1219,8 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                 const int s = g % NS;
                 pc_wait_ge(&s_freed, g - NS + 1);  // the slot's previous group is consumed
                 PcUpSlot& sl = ring[s];
+                int k3 = -1, p3 = 0;
+                double s3 = 0.0;
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
                     if (k >= n) break;
@@ -1237,10 +1240,17 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                         sl.sh[k] = hk == 0xFF ? 0.0 : sS[wc[hk & 3]];
                         sl.s1[k] = np >= 1 ? sS[wc[(hk + 1) & 3]] : 0.0;
                         sl.s2[k] = np >= 2 ? sS[wc[(hk + 2) & 3]] : 0.0;
-                        sl.s3[k] = np >= 3 ? sS[wc[3]] : 0.0;
-                        sl.np[k] = np;
-                        sl.p3row[k] = np >= 3 ? (int)meta_dw(m, w0 + 5) : 0;
                     }
+                    if (np >= 3) {
+                        k3 = k;
+                        p3 = (int)meta_dw(m, w0 + 5);
+                        s3 = sS[wc[3]];
+                    }
+                }
+                if (lane == 0) {
+                    sl.k3 = k3;
+                    sl.p3 = p3;
+                    sl.s3 = s3;
                 }
                 pc_publish(&s_staged[s], g + 1);
                 m = mn;
@@ -1257,7 +1267,6 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                 // the whole group from LDS in one batch, then the recurrence from registers (absent posts
                 // were staged as 0 with S = 0: fma(0, 0, acc) == acc, aggregates are finite and >= +0)
                 double pre[PC_G], p1[PC_G], p2[PC_G], cst[PC_G], sh[PC_G], s1[PC_G], s2[PC_G];
-                int np3 = 0;
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
                     const double2 pc = sl.pc[k][lane], pp = sl.pp[k][lane];
@@ -1268,17 +1277,12 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                     sh[k] = sl.sh[k];
                     s1[k] = sl.s1[k];
                     s2[k] = sl.s2[k];
-                    np3 |= (sl.np[k] >= 3) << k;
                 }
-                // a tree root's third post-heavy child (rare): its row and S read before the slot is released
-                int p3row = 0;
-                double s3 = 0.0;
-                if (np3) {
-                    const int k3 = __builtin_ctz(np3);  // at most one root per path
-                    p3row = sl.p3row[k3];
-                    s3 = sl.s3[k3];
-                }
+                // a tree root's third post-heavy child (rare): read with the group, before the slot is released
+                const int k3 = sl.k3, p3row = sl.p3;
+                const double s3 = sl.s3;
                 pc_publish_ordered(&s_freed, g + 1);  // the slot's reads are issued: free it
+                const int np3 = k3 >= 0 ? 1 << k3 : 0;
 #pragma unroll
                 for (int k = 0; k < PC_G; ++k) {
                     if (k >= n) break;
