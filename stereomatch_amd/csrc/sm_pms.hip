@@ -478,7 +478,7 @@ __device__ void up_group(const PmsDev& d, const double* __restrict__ sS, int pha
 template <int GW>
 __device__ void down_group(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
                            int path);
-__global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
+__global__ void __launch_bounds__(1024, 1) k_pms_serial(PmsDev d, int t0, int t1) {  // (1 per CU: no spills)
     __shared__ long long s_off;
     __shared__ int s_n, s_ns, s_nl;
     __shared__ float s_dice[64];
@@ -489,7 +489,7 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
     const int wave = tid >> 6, nwaves = nt >> 6, lane = tid & 63;
     // SM_PMS_PROF builds: per-segment wall-clock totals (100 MHz ticks) of thread 0
     long long tick = 0;
-    auto seg = [&](int k) {
+    auto seg = [&](int k) __attribute__((always_inline)) {
         if (d.prof && tid == 0) {
             const long long now = (long long)wall_clock64();
             if (k >= 0) atomicAdd((unsigned long long*)&d.prof[k], (unsigned long long)(now - tick));
@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(1024) k_pms_serial(PmsDev d, int t0, int t1) {
                 // groups, 32 (P <= 2) or 8 paths per wave (the planned walks' up_group / down_group), the long
                 // ones by the wave walker -- instead of one wave per path, which left a round with many short
                 // paths waiting on 16 waves.  Otherwise one wave per (path, 64-proposal chunk) item.
-                auto round = [&](int r, bool up) {
+                auto round = [&](int r, bool up) __attribute__((always_inline)) {  // (inlined: no captures in scratch)
                     const int plo = d.rt_path[(size_t)r * (d.K + 1) + t], phi = d.rt_path[(size_t)r * (d.K + 1) + t + 1];
                     const int np = phi - plo;
                     if (Pw <= 8 && np <= PMS_SER_MAXP) {
@@ -1124,6 +1124,13 @@ __global__ void __launch_bounds__(256) k_pms_walk_plan(PmsDev d, int phase, int 
 // bottom): a loader stages T = S2 * A_up and S, the chain does y = fma(S, y, T); the head reads its
 // parent row (or keeps A_up at a tree root) -- down_walk's operations.  Same bits as the walkers.
 constexpr int PC_G = 8;        // nodes per group
+
+// a[i] of a 4-element register array by selects: a runtime index into a local array would put the array
+// in scratch memory (the up loaders had 272 bytes of it per lane)
+__device__ __forceinline__ double pc_sel(const double (&a)[4], int i) {
+    return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+__device__ __forceinline__ int pc_sel(const int (&a)[4], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3]; }
 constexpr int PC_NSU = 4;      // up ring slots (2 KB per node): 67 KB, two workgroups per CU
 constexpr int PC_NSU_MAX = 8;  // SM_PMS_CHAIN_NSU up to this: 133 KB, one workgroup per CU
 constexpr int PC_NSD = 14;     // down ring slots (0.5 KB per node): 58 KB, two workgroups per CU
@@ -1157,8 +1164,10 @@ __device__ __forceinline__ void pc_wait_ge(int* p, int v) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// (512, 2): two workgroups per CU -- 4 waves per SIMD, so up to 128 VGPRs.  With the bare bound the compiler
+// aimed at 8 waves per SIMD, gave the kernel 64 VGPRs and spilled the up loaders' rows to scratch.
 template <bool UP>
-__global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, int ns) {
+__global__ void __launch_bounds__(512, 2) k_pms_chain(PmsDev d, int phase, int r, int ns) {
     extern __shared__ double2 pc_lds[];  // 16-byte aligned: the up ring is read as double2
     __shared__ double sS[PMS_NW], sS2[PMS_NW];
     __shared__ int s_staged[PC_NSD], s_freed;
@@ -1235,11 +1244,12 @@ __global__ void __launch_bounds__(512) k_pms_chain(PmsDev d, int phase, int r, i
                         if (q < h) pre = fma(cv[k][q], sS[wc[q]], pre);
                     sl.pc[k][lane] = make_double2(pre, cost[k]);
                     const int np = hk == 0xFF ? 0 : nch - 1 - hk;
-                    sl.pp[k][lane] = make_double2(np >= 1 ? cv[k][(hk + 1) & 3] : 0.0, np >= 2 ? cv[k][(hk + 2) & 3] : 0.0);
+                    sl.pp[k][lane] = make_double2(np >= 1 ? pc_sel(cv[k], (hk + 1) & 3) : 0.0,
+                                                  np >= 2 ? pc_sel(cv[k], (hk + 2) & 3) : 0.0);
                     if (lane == 0) {
-                        sl.sh[k] = hk == 0xFF ? 0.0 : sS[wc[hk & 3]];
-                        sl.s1[k] = np >= 1 ? sS[wc[(hk + 1) & 3]] : 0.0;
-                        sl.s2[k] = np >= 2 ? sS[wc[(hk + 2) & 3]] : 0.0;
+                        sl.sh[k] = hk == 0xFF ? 0.0 : sS[pc_sel(wc, hk & 3)];
+                        sl.s1[k] = np >= 1 ? sS[pc_sel(wc, (hk + 1) & 3)] : 0.0;
+                        sl.s2[k] = np >= 2 ? sS[pc_sel(wc, (hk + 2) & 3)] : 0.0;
                     }
                     if (np >= 3) {
                         k3 = k;

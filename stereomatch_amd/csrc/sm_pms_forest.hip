@@ -184,6 +184,23 @@ __device__ __forceinline__ int block_scan(int c, int* s_w, int* total) {
     return pre + incl - c;
 }
 
+// the children of a node (its tree neighbours but the parent, in key order) compacted into q / wv by static
+// selects: a runtime index into the local arrays (q[c++] = ...) would put them in scratch memory
+__device__ __forceinline__ void pf_children(const int (&nn)[4], const uint32_t (&ww)[4], int pp, int (&q)[4], uint32_t (&wv)[4],
+                                            int& c) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool keep = nn[k] >= 0 && nn[k] != pp;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            if (keep && c == s) {
+                q[s] = nn[k];
+                wv[s] = ww[k];
+            }
+        c += keep ? 1 : 0;
+    }
+}
+
 // Narrow levels (at most 64 nodes: the deep tails of the largest trees, thousands of levels at C2) run on
 // wave 0 alone, level after level without workgroup barriers: the frontier stays in registers, the next
 // one is handed over through LDS (one wave's LDS operations complete in order).  Entered at level d =
@@ -209,12 +226,7 @@ __device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* 
             const uint2 w4 = v.nbw[p];
             const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
             const uint32_t ww[4] = {w4.x & 0xFFFFu, w4.x >> 16, w4.y & 0xFFFFu, w4.y >> 16};
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (nn[k] >= 0 && nn[k] != pp) {
-                    q[c] = nn[k];
-                    wv[c++] = ww[k];
-                }
+            pf_children(nn, ww, pp, q, wv, c);
         }
         int incl = c;
 #pragma unroll
@@ -226,7 +238,9 @@ __device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* 
         if (val) {
             v.gfc[i] = b + pos;
             v.gnc[i] = (uint8_t)c;
-            for (int k = 0; k < c; ++k) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k >= c) break;
                 const int j = b + pos + k;
                 if (j >= v.N) {  // only masks with a cycle get here (as in the workgroup levels)
                     v.tot[7] = 1;
@@ -358,19 +372,16 @@ __global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
                 const uint2 w4 = v.nbw[p];
                 const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
                 const uint32_t ww[4] = {w4.x & 0xFFFFu, w4.x >> 16, w4.y & 0xFFFFu, w4.y >> 16};
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (nn[k] >= 0 && nn[k] != pp) {  // every tree neighbour but the parent is a child
-                        q[c] = nn[k];
-                        wv[c++] = ww[k];
-                    }
+                pf_children(nn, ww, pp, q, wv, c);  // every tree neighbour but the parent is a child
             }
             int total;
             const int pos = block_scan(c, s_w, &total);
             if (i < b) {
                 v.gfc[i] = next + pos;
                 v.gnc[i] = (uint8_t)c;
-                for (int k = 0; k < c; ++k) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k >= c) break;
                     const int j = next + pos + k;
                     if (j >= v.N) {  // only masks with a cycle (not a forest) get here: flag, never write out of bounds
                         v.tot[7] = 1;
