@@ -530,38 +530,51 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
         uint64_t nr[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) nr[k] = (adj & (1u << k)) ? V.prec[nbr_of(v, k, W)] : 0ull;
+        // the children in descending key order by a fixed 5-comparator network over the 4 directions
+        // (absent ones sort last; keys are unique): no local array is indexed at run time, which
+        // would put them in scratch memory
         uint64_t ck[4];
-        uint32_t cs[4] = {SM_NONE, SM_NONE, SM_NONE, SM_NONE}, cw[4] = {0, 0, 0, 0};
+        uint32_t cs[4], cw[4];
         int cq[4];
-        int nch = 0;
+        bool cv[4];
         uint32_t wp = 0, parent = SM_NONE;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (!(adj & (1u << k))) continue;
+            const bool in = (adj & (1u << k)) != 0;
             // key_dir without the weight loads: right / down edges are v's own, left / up the neighbour's
             const uint32_t w = k == 0 ? PR_WR(me) : k == 1 ? PR_WD(me) : k == 2 ? PR_WR(nr[k]) : PR_WD(nr[k]);
             const uint32_t a = k == 0 || k == 1 ? v : nbr_of(v, k, W);
             const uint64_t key = sm_edge_key(w, a, (uint32_t)(k & 1));
-            if (k == pd) {
+            if (in && k == pd) {
                 wp = (uint32_t)(key >> 33);
                 parent = PR_SLOT(nr[k]);
-                continue;
             }
-            ck[nch] = key;
-            cq[nch] = k;
-            cs[nch] = PR_SLOT(nr[k]);
-            ++nch;
+            ck[k] = key;
+            cq[k] = k;
+            cs[k] = PR_SLOT(nr[k]);
+            cv[k] = in && k != pd;
         }
-        for (int i = 1; i < nch; ++i)  // descending key
-            for (int j = i; j > 0 && ck[j] > ck[j - 1]; --j) {
-                const uint64_t tk = ck[j]; ck[j] = ck[j - 1]; ck[j - 1] = tk;
-                const int tq = cq[j]; cq[j] = cq[j - 1]; cq[j - 1] = tq;
-                const uint32_t ts = cs[j]; cs[j] = cs[j - 1]; cs[j - 1] = ts;
-            }
+        auto cswap = [&](int i, int j) __attribute__((always_inline)) {  // i, j constants after unrolling
+            const bool sw = cv[j] && (!cv[i] || ck[j] > ck[i]);
+            const uint64_t tk = ck[i]; const int tq = cq[i]; const uint32_t ts = cs[i]; const bool tv = cv[i];
+            ck[i] = sw ? ck[j] : ck[i]; cq[i] = sw ? cq[j] : cq[i]; cs[i] = sw ? cs[j] : cs[i]; cv[i] = sw ? cv[j] : cv[i];
+            ck[j] = sw ? tk : ck[j]; cq[j] = sw ? tq : cq[j]; cs[j] = sw ? ts : cs[j]; cv[j] = sw ? tv : cv[j];
+        };
+        cswap(0, 1);
+        cswap(2, 3);
+        cswap(0, 2);
+        cswap(1, 3);
+        cswap(1, 2);
+        int nch = 0;
         uint32_t hidx = 0, has_light = 0;
-        for (int i = 0; i < nch; ++i) {
-            cw[i] = (uint32_t)(ck[i] >> 33);
-            if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            nch += cv[i] ? 1 : 0;
+            cw[i] = cv[i] ? (uint32_t)(ck[i] >> 33) : 0u;
+            cs[i] = cv[i] ? cs[i] : SM_NONE;
+            if (cv[i]) {
+                if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
+            }
         }
         V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
         nlight += has_light;

@@ -478,7 +478,10 @@ __device__ void up_group(const PmsDev& d, const double* __restrict__ sS, int pha
 template <int GW>
 __device__ void down_group(const PmsDev& d, const double* __restrict__ sS, const double* __restrict__ sS2, int phase,
                            int path);
-__global__ void __launch_bounds__(1024, 1) k_pms_serial(PmsDev d, int t0, int t1) {  // (1 per CU: no spills)
+// NT threads: 1024 caps a lane at 128 registers (4 waves per SIMD), below what the inlined walkers
+// hold; 768 gives 168 (SM_PMS_SER_NT A/B)
+template <int NT>
+__global__ void __launch_bounds__(NT, 1) k_pms_serial(PmsDev d, int t0, int t1) {
     __shared__ long long s_off;
     __shared__ int s_n, s_ns, s_nl;
     __shared__ float s_dice[64];
@@ -1685,7 +1688,14 @@ inline unsigned blocks(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b
 
 hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1) {
     if (t1 <= t0) return hipSuccess;
-    hipLaunchKernelGGL(k_pms_serial, dim3(1), dim3(1024), 0, st, d, t0, t1);
+    const char* e = getenv("SM_PMS_SER_NT");  // A/B: 1024 or 512 threads (default 768)
+    const int nt = e && atoi(e) == 1024 ? 1024 : e && atoi(e) == 512 ? 512 : 768;
+    if (nt == 1024)
+        hipLaunchKernelGGL(k_pms_serial<1024>, dim3(1), dim3(1024), 0, st, d, t0, t1);
+    else if (nt == 512)
+        hipLaunchKernelGGL(k_pms_serial<512>, dim3(1), dim3(512), 0, st, d, t0, t1);
+    else
+        hipLaunchKernelGGL(k_pms_serial<768>, dim3(1), dim3(768), 0, st, d, t0, t1);
     return hipGetLastError();
 }
 

@@ -205,11 +205,17 @@ struct WtaCfg {
 };
 #endif
 
+// slice k of lane l's row (k and l wave-uniform): every slice is read at lane l and the scalars are
+// selected -- a select among the row's registers by a run-time k can be folded into one load at a
+// computed index, which puts the whole row array in scratch memory (seen at SPL = 4)
 template <int SPL>
-__device__ __forceinline__ double sel_slice(const double (&r)[SPL], int k) {
-    double v = r[0];
+__device__ __forceinline__ double readlane_slice(const double (&r)[SPL], int k, int l) {
+    double v = readlane_f64(r[0], l);
 #pragma unroll
-    for (int q = 1; q < SPL; ++q) v = k == q ? r[q] : v;
+    for (int q = 1; q < SPL; ++q) {
+        const double t = readlane_f64(r[q], l);
+        v = k == q ? t : v;
+    }
     return v;
 }
 
@@ -234,11 +240,11 @@ __device__ __forceinline__ void wta_nodes(const double (&x)[CH][SPL], int lane, 
             float pre = 0.0f, nxt = 0.0f;
             if (g > 0) {
                 const int t = m - 1;
-                pre = (float)readlane_f64(sel_slice<SPL>(x[j], t % SPL), t / SPL);
+                pre = (float)readlane_slice<SPL>(x[j], t % SPL, t / SPL);
             }
             if (g < w.dtot - 1) {
                 const int t = m + 1;
-                nxt = (float)readlane_f64(sel_slice<SPL>(x[j], t % SPL), t / SPL);
+                nxt = (float)readlane_slice<SPL>(x[j], t % SPL, t / SPL);
             }
             const float s = (nxt - pre) * 0.5f / (nxt - 2.0f * cur + pre);
             const float dj = fabsf(s) < 1.0f ? (float)g - s : (float)g;

@@ -63,7 +63,7 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
 
 
 @pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "chainstream",
-                                  "refalways"])
+                                  "refalways", "ser1024", "ser512"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
@@ -72,7 +72,8 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     sampled label, repeats included (the default drops repeats, k_pms_prop_dedupe);
     SM_PMS_WAVE_WALK=1 walks every (path, chunk) item with a wave of its own instead of the planned
     lane-group walks (k_pms_plan / k_pms_walk_plan); SM_PMS_CHAIN_MIN=48 sends paths of >= 48 rows to the
-    chain kernel; SM_PMS_CHAIN_STREAM=1 runs the chain launches on a side stream beside the walkers."""
+    chain kernel; SM_PMS_CHAIN_STREAM=1 runs the chain launches on a side stream beside the walkers;
+    SM_PMS_SER_NT=1024 / 512 runs the serial kernel with that many threads (default 768)."""
     monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
     monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
     if mode == "nodedup":
@@ -99,6 +100,10 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         monkeypatch.setenv("SM_PMS_REF_ALWAYS", "1")
     else:
         monkeypatch.delenv("SM_PMS_REF_ALWAYS", raising=False)
+    if mode in ("ser1024", "ser512"):
+        monkeypatch.setenv("SM_PMS_SER_NT", mode[3:])
+    else:
+        monkeypatch.delenv("SM_PMS_SER_NT", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
