@@ -8,3 +8,13 @@ f=$(find $O/raw -name '*kernel_trace.csv' | head -1); cp "$f" $O/kernel_trace_se
 f=$(find $O/raw -name '*kernel_stats.csv' | head -1); cp "$f" $O/kernel_stats_seg1.csv
 rm -rf $O/raw
 tail -1 $O/seg1.log | cut -c1-300
+lat() {  # tag, env...: segment-mode single-frame latency and streamed ms/frame
+  local tag=$1; shift
+  env "$@" timeout -k 10 300 python3 bench.py --segment-c 5000 --min-size 200 --steps 8 --warmup 2 --no-cpu --no-pms > $O/lat_$tag.log 2>&1 || return 1
+  python3 -c "import json;d=json.loads(open('$O/lat_$tag.log').read().strip().splitlines()[-1]);print('$tag', 'latency %.2f ms' % d['latency_ms_per_frame'], 'stream %.2f ms/frame' % d['ms_per_step'])"
+}
+lat default SM_SEG_X=0 || exit 2
+lat rounds1 SM_SEG_GLOBAL_ROUNDS=1 || exit 3
+lat rounds3 SM_SEG_GLOBAL_ROUNDS=3 || exit 4
+lat flatten3 SM_SEG_FLATTEN=3 || exit 5
+lat default2 SM_SEG_X=0 || exit 6
