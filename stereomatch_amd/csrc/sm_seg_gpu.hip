@@ -25,6 +25,7 @@
 
 #include <hipcub/device/device_radix_sort.hpp>
 #include <hipcub/device/device_scan.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "sm_seg_gpu.h"
 #include "sm_segment.h"
@@ -64,6 +65,42 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
     if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
     base = __shfl(base, leader);
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// block-aggregated appends to K counters: every thread of the block calls it (it has barriers); one global
+// atomic per counter and block instead of one per wave.  Every wave appending to one counter serialised the
+// appends at the L2 (~6-10 ns per atomic on one address: 11-25k of them per launch in the big buckets of
+// synthetic C2 made k_seg_hook / k_seg_best / k_seg_classify 0.1-0.16 ms).  Returns each lane's slots (valid
+// where pred).
+template <int K>
+__device__ __forceinline__ void block_append(uint32_t* const (&counter)[K], const bool (&pred)[K], uint32_t (&slot)[K]) {
+    __shared__ uint32_t s_cnt[K][16], s_base[K];
+    const int lane = __lane_id(), wv = (int)(threadIdx.x >> 6), nw = (int)((blockDim.x + 63) >> 6);
+    unsigned long long m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        m[k] = __ballot(pred[k]);
+        if (lane == 0) s_cnt[k][wv] = (uint32_t)__popcll(m[k]);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < K) {  // thread k: the waves' offsets (exclusive scan) and the block's base
+        const int k = (int)threadIdx.x;
+        uint32_t run = 0;
+        for (int j = 0; j < nw; ++j) {
+            const uint32_t c = s_cnt[k][j];
+            s_cnt[k][j] = run;
+            run += c;
+        }
+        uint32_t* ctr = counter[0];
+#pragma unroll
+        for (int q = 1; q < K; ++q) ctr = k == q ? counter[q] : ctr;
+        s_base[k] = run ? atomicAdd(ctr, run) : 0u;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int k = 0; k < K; ++k) slot[k] = s_base[k] + s_cnt[k][wv] + (uint32_t)__popcll(m[k] & lt);
+    __syncthreads();  // s_cnt / s_base free for the next call
 }
 
 __global__ void __launch_bounds__(256) k_seg_init(SegPair sp) {
@@ -170,10 +207,12 @@ __global__ void __launch_bounds__(256) k_seg_classify(SegPair sp, int w, float c
             }
         }
     }
-    const uint32_t pc = wave_append(v.cnt + SM_SEG_C_LIST + lout, cand);
-    if (cand) v.list[lout & 1][pc] = make_uint4(id, ra, rb, 0u);
-    const uint32_t pr = wave_append(v.cnt + SM_SEG_C_REJ, rej);
-    if (rej) v.rej[pr] = id;
+    uint32_t* const ctr[2] = {v.cnt + SM_SEG_C_LIST + lout, v.cnt + SM_SEG_C_REJ};
+    const bool pred[2] = {cand, rej};
+    uint32_t slot[2];
+    block_append<2>(ctr, pred, slot);
+    if (cand) v.list[lout & 1][slot[0]] = make_uint4(id, ra, rb, 0u);
+    if (rej) v.rej[slot[1]] = id;
 }
 
 // one Boruvka selection over list lin: crossing edges -> list lout with their current roots, and each
@@ -195,8 +234,11 @@ __global__ void __launch_bounds__(256) k_seg_best(SegPair sp, int lin, int lout,
             atomicMin(v.best + e.z, key);
         }
     }
-    const uint32_t po = wave_append(v.cnt + SM_SEG_C_LIST + lout, cross);
-    if (cross) v.list[lout & 1][po] = e;
+    uint32_t* const ctr[1] = {v.cnt + SM_SEG_C_LIST + lout};
+    const bool pred[1] = {cross};
+    uint32_t po[1];
+    block_append<1>(ctr, pred, po);
+    if (cross) v.list[lout & 1][po[0]] = e;
 }
 
 __device__ __forceinline__ void seg_hook_edge(const SegView& v, uint4 e, uint32_t gen, bool pred) {
@@ -220,10 +262,13 @@ __device__ __forceinline__ void seg_hook_edge(const SegView& v, uint4 e, uint32_
             }
         }
     }
-    const uint32_t ph = wave_append(v.cnt + SM_SEG_C_HOOK, hook);
+    uint32_t* const ctr[1] = {v.cnt + SM_SEG_C_HOOK};
+    const bool hk[1] = {hook};
+    uint32_t ph[1];
+    block_append<1>(ctr, hk, ph);  // (every thread of the block calls seg_hook_edge)
     if (hook) {
         v.par[child] = parent;
-        v.hooked[ph] = child;
+        v.hooked[ph[0]] = child;
         const uint32_t a = e.x >> 1;
         if (e.x & 1u)
             v.mD[a] = 1;
@@ -310,12 +355,33 @@ __global__ void __launch_bounds__(1024) k_seg_tail(SegPair sp, int lin, uint32_t
     seg_wg_rounds(v, lin & 1, v.cnt[SM_SEG_C_LIST + lin], gen0, &s_out, false);
 }
 
-__device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, int w) {
-    const uint32_t r = v.hooked[i];
-    const uint32_t t = seg_find(v.par, r);
-    // r's size is its size at the bucket's start (only roots grow); agent scope: sizes change in L2
-    atomicAdd(v.sz + t, __hip_atomic_load(v.sz + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    v.wl[t] = (uint16_t)w;
+// hooked root i (valid lanes) adds its size to its component's root, whose last-join weight becomes w.
+// r's size is its size at the bucket's start (only roots grow; r is no root any more, so no lane adds into
+// it); agent scope: sizes change in L2.  Call with the whole wave: the lanes whose root equals the first
+// valid lane's add their sizes in one atomic -- one join of synthetic C2 (w = 9) hooks 25.6k roots into one
+// component, i.e. 25.6k atomics on one address (0.3 ms) without it.
+__device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, int w, bool valid) {
+    uint32_t t = 0, sz = 0;
+    if (valid) {
+        const uint32_t r = v.hooked[i];
+        t = seg_find(v.par, r);
+        sz = __hip_atomic_load(v.sz + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long act = __ballot(valid);
+    if (act == 0) return;
+    const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
+    const uint32_t tl = __shfl(t, leader);
+    const bool grp = valid && t == tl;
+    uint32_t sum = grp ? sz : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+    if (lane == leader) {
+        atomicAdd(v.sz + tl, sum);
+        v.wl[tl] = (uint16_t)w;
+    } else if (valid && !grp) {
+        atomicAdd(v.sz + t, sz);
+        v.wl[t] = (uint16_t)w;
+    }
 }
 
 // a run of small buckets [w0, w1) (each of at most SM_SEG_SMALL edges) in one workgroup, one bucket
@@ -366,10 +432,14 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
         s_hk[i] = SEG_EMPTY;
         s_par[i] = (uint16_t)i;
     }
-    const uint32_t* start = v.bcnt + SM_SEG_NB;
+    // the run's bucket starts in LDS: most buckets of a run are empty (synthetic C2: 24 of ~740 hold edges),
+    // and a global load per bucket just to skip it cost ~1 us each, one after the other
+    __shared__ uint32_t s_start[SM_SEG_NB + 1];
+    for (int i = w0 + tid; i <= w1; i += 1024) s_start[i - w0] = v.bcnt[SM_SEG_NB + i];
+    seg_wg_sync();
     uint32_t gen = gen0;
     for (int w = w0; w < w1; ++w) {
-        const uint32_t s = start[w], m = start[w + 1] - s;
+        const uint32_t s = s_start[w - w0], m = s_start[w + 1 - w0] - s;
         if (m == 0) continue;
         if (tid == 0) {
             s_n = 0;
@@ -399,8 +469,11 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
                     s_sb[pc] = (uint16_t)seg_lslot(s_hk, rb);
                 }
             }
-            const uint32_t pr = wave_append(v.cnt + SM_SEG_C_REJ, rej);
-            if (rej) v.rej[pr] = id;
+            uint32_t* const ctr[1] = {v.cnt + SM_SEG_C_REJ};
+            const bool pred[1] = {rej};
+            uint32_t pr[1];
+            block_append<1>(ctr, pred, pr);
+            if (rej) v.rej[pr[0]] = id;
         }
         seg_wg_sync();
         const uint32_t n = s_n;
@@ -455,7 +528,7 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
         if (r < 0) return;
         gen += (uint32_t)r;
         const uint32_t h1 = __hip_atomic_load(v.cnt + SM_SEG_C_HOOK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t i = s_h0 + tid; i < h1; i += 1024) seg_size_update(v, i, w);
+        for (uint32_t i0 = s_h0; i0 < h1; i0 += 1024) seg_size_update(v, i0 + tid, w, i0 + tid < h1);
         seg_wg_sync();  // sizes final before the next bucket's acceptance tests
     }
 }
@@ -464,8 +537,8 @@ __global__ void __launch_bounds__(256) k_seg_sizes(SegPair sp, int w) {
     const SegView& v = sp.v[blockIdx.y];
     const uint32_t h0 = v.cnt[SM_SEG_C_BUCKET + w], h1 = v.cnt[SM_SEG_C_HOOK];
     const uint32_t i = h0 + blockIdx.x * 256 + threadIdx.x;
-    if (i >= h1) return;
-    seg_size_update(v, i, w);
+    if (h0 + blockIdx.x * 256 >= h1) return;  // block-uniform
+    seg_size_update(v, i, w, i < h1);
 }
 
 __global__ void __launch_bounds__(256) k_seg_minsize(SegPair sp, uint32_t ms) {
@@ -485,7 +558,11 @@ __global__ void __launch_bounds__(256) k_seg_minsize(SegPair sp, uint32_t ms) {
         r.sb = v.sz[r.rb];
         keep = r.sa < ms || r.sb < ms;
     }
-    const uint32_t p = wave_append(v.cnt + SM_SEG_C_MIN, keep);
+    uint32_t* const ctr[1] = {v.cnt + SM_SEG_C_MIN};
+    const bool pred[1] = {keep};
+    uint32_t ps[1];
+    block_append<1>(ctr, pred, ps);
+    const uint32_t p = ps[0];
     if (keep) {
         v.mlist[p] = r;
         v.mkey[0][p] = ((unsigned long long)r.w << 32) | r.id;  // the merge's (w, a, b) order
@@ -668,12 +745,29 @@ hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, ui
     return hipGetLastError();
 }
 
+// The min-size candidates' sorts (~260k pairs per C2 view): rocprim's onesweep radix sort (one histogram
+// launch + one launch per 8-bit digit, stable) instead of hipcub's choice below 2^20 items, the merge-sort
+// path (~20 launches per sort, 0.2-0.36 ms each at C2).  SM_SEG_MERGESORT=1 keeps hipcub's choice (A/B).
+using SegOnesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+bool seg_mergesort() { return getenv("SM_SEG_MERGESORT") != nullptr; }
+hipError_t seg_sort_pairs(void* temp, size_t& bytes, const unsigned long long* kin, unsigned long long* kout,
+                          const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t st) {
+    if (seg_mergesort())
+        return hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
+    return rocprim::radix_sort_pairs<SegOnesweep>(temp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)bits, st);
+}
+
 size_t seg_sort_temp_bytes(uint32_t n) {
-    size_t a = 0, b = 0, c = 0;
+    size_t a = 0, b = 0, c = 0, d = 0, e = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, SEG_KEY_BITS);
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64);
+    (void)rocprim::radix_sort_pairs<SegOnesweep>(nullptr, d, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                                 (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u, 64u);
+    (void)rocprim::radix_sort_pairs<SegOnesweep>(nullptr, e, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                                 (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u, (unsigned)SEG_KEY_BITS);
+    a = std::max(a, std::max(d, e));
     // the scans: E + 1 candidate flags, N + 1 root marks (n = E = 2N)
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n + 1);
     return std::max(a, std::max(b, c));
@@ -687,8 +781,7 @@ hipError_t seg_launch_sort(hipStream_t st, const SegPair& p, void* const* temp, 
         if (v.nmin == 0) continue;
         nmax = v.nmin > nmax ? v.nmin : nmax;
         size_t tb = temp_bytes[i];
-        hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp[i], tb, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1],
-                                                          (int)v.nmin, 0, SEG_KEY_BITS, st);
+        hipError_t e = seg_sort_pairs(temp[i], tb, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1], v.nmin, SEG_KEY_BITS, st);
         if (e != hipSuccess) return e;
     }
     if (nmax) hipLaunchKernelGGL(k_seg_gather, dim3(blocks_of(nmax, 256), p.nv), dim3(256), 0, st, p);
@@ -709,8 +802,7 @@ hipError_t seg_launch_dedupe(hipStream_t st, const SegPair& p, void* const* temp
         if (e != hipSuccess) return e;
         if (v.nmin == 0) continue;
         size_t tb = temp_bytes[i];
-        if ((e = hipcub::DeviceRadixSort::SortPairs(temp[i], tb, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1], (int)v.nmin, 0,
-                                                    bits, st)) != hipSuccess)
+        if ((e = seg_sort_pairs(temp[i], tb, v.mkey[0], v.mkey[1], v.mval[0], v.mval[1], v.nmin, bits, st)) != hipSuccess)
             return e;
     }
     hipLaunchKernelGGL(k_seg_keep, dim3(nb, p.nv), dim3(256), 0, st, p);

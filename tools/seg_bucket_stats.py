@@ -56,6 +56,8 @@ def main():
     sz = np.ones(N, dtype=np.int64)
     wl = np.zeros(N, dtype=np.int64)
     tot_tail = 0
+    small = dict(buckets=0, live=0, cand=0, edges=0, live_edges=0, cand_edges=0, open_end=0, open_end_edges=0)
+    w_first, thr0 = None, None
     print("   w      edges  candidates  crossing after rounds 1, 2, ...")
     for w in range(766):
         s, e = bstart[w], bstart[w + 1]
@@ -68,6 +70,21 @@ def main():
         cand = two & thr(ra) & thr(rb)
         ca, cb, cid = ra[cand], rb[cand], ids[s:e][cand]
         n = len(cid)
+        if m <= a.small:  # small buckets: live (two-component) edges, and those with both ends open at the
+            # first small bucket (the others are rejected whatever happens: a closed component never joins)
+            if w_first is None:
+                w_first = w
+                thr0 = wl + (np.float32(a.c) / sz.astype(np.float32)).astype(np.float64)
+            small["buckets"] += 1
+            small["edges"] += m
+            nl = int(two.sum())
+            small["live"] += nl > 0
+            small["live_edges"] += nl
+            small["cand"] += n > 0
+            small["cand_edges"] += n
+            oo = two & (thr0[ra] >= w_first) & (thr0[rb] >= w_first)
+            small["open_end"] += int(oo.sum()) > 0
+            small["open_end_edges"] += int(oo.sum())
         if n == 0:
             continue
         # Boruvka rounds over the candidates' roots (components relabelled after each round)
@@ -116,6 +133,7 @@ def main():
             print("%4d %10d %11d  %-28s max cand/root %7d  max roots/comp %7d  distinct roots/wave %.1f (of 128)"
                   % (w, m, n, left_n[:8], inc.max(), per.max(), float(np.mean(dist)) if nw else 0.0))
     print("big-bucket tail scans (sum over rounds >= 3 of the crossing candidates): %d" % tot_tail)
+    print("small buckets (from w = %s): %s" % (w_first, small))
 
 
 if __name__ == "__main__":
