@@ -485,6 +485,8 @@ int seg_flatten() { return getenv("SM_SEG_FLATTEN") ? atoi(getenv("SM_SEG_FLATTE
 
 // SM_SEG_NODEDUP=1: the min-size merge over every candidate (A/B of the GPU pair dedupe)
 bool seg_nodedup() { return getenv("SM_SEG_NODEDUP") != nullptr; }
+// a small-bucket run starts with k_seg_split (SM_SEG_NOSPLIT=1: every edge of the run through k_seg_small)
+bool seg_split() { return getenv("SM_SEG_NOSPLIT") == nullptr; }
 
 // Boruvka rounds launched over the whole GPU before a bucket's single-workgroup tail, for buckets of
 // more than SM_SEG_SMALL edges (env SM_SEG_GLOBAL_ROUNDS, default 2)
@@ -668,6 +670,7 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         s.fwR = P<uint16_t>(ctx->fwR[v]);
         s.fwD = P<uint16_t>(ctx->fwD[v]);
         s.keep = P<uint32_t>(g.keep);
+        s.act = P<uint32_t>(g.keep);  // the sweep's small-run active lists; the pair dedupe reuses it afterwards
         s.kpos = P<uint32_t>(g.kpos);
         s.lmark = P<uint32_t>(g.lmark);
         s.lid = P<uint32_t>(g.lid);
@@ -704,7 +707,16 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
             int w1 = w + 1, nb = 1;
             for (uint32_t m1; w1 < SM_SEG_NB && (m1 = bsize(w1)) <= small; ++w1) nb += m1 > 0;
             if (flatten & 1) HIPC(seg_launch_flatten(st, sp));
-            HIPC(seg_launch_small(st, sp, w, w1, c, gen));
+            const bool split = seg_split();
+            if (split) {
+                uint32_t ne = 0;
+                for (int i = 0; i < vs.n; ++i) {
+                    const SegGpu& g = ctx->sg[vs.v[i]];
+                    ne = std::max(ne, g.h_b[w1] - g.h_b[w]);
+                }
+                HIPC(seg_launch_split(st, sp, w, w1, c, ne));
+            }
+            HIPC(seg_launch_small(st, sp, w, w1, c, gen, split));
             gen += SM_SEG_TAIL_GENS * (uint32_t)nb;
             w = w1 - 1;
             continue;

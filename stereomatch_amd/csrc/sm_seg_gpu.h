@@ -36,6 +36,7 @@
 #define SM_SEG_C_ERR 4
 #define SM_SEG_C_UNIQ 5   // candidates that are the first of their root pair (k_seg_dense)
 #define SM_SEG_C_LOCAL 6  // distinct roots of those (dense local ids)
+#define SM_SEG_C_ACT 7    // edges of a small-bucket run with both ends open at its start (k_seg_split)
 #define SM_SEG_C_LIST 8
 #define SM_SEG_C_BUCKET (8 + SM_SEG_MAXL)
 #define SM_SEG_NCOUNT (8 + SM_SEG_MAXL + SM_SEG_NB)
@@ -73,6 +74,7 @@ struct SegView {
     uint32_t nmin;                // their count (host-set before the sort)
     // pair dedupe (seg_launch_dedupe): only the first candidate of each root pair can join
     uint32_t* keep;               // [E + 1] first of its pair, by position -> (scan) kpos
+    uint32_t* act;                // [E] a small-bucket run's active edges (k_seg_split; the keep buffer, free then)
     uint32_t* kpos;               // [E + 1]
     uint32_t* lmark;              // [N + 1] roots of the kept candidates -> (scan) lid
     uint32_t* lid;                // [N + 1]
@@ -98,7 +100,11 @@ hipError_t seg_launch_scatter(hipStream_t st, const SegPair& p);
 hipError_t seg_launch_classify(hipStream_t st, const SegPair& p, int w, uint32_t m, float c, int lout, uint32_t gen);
 hipError_t seg_launch_round(hipStream_t st, const SegPair& p, uint32_t m, int lin, int lout, uint32_t gen);
 hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t gen0);
-hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0);
+// split = the run's edges were classified by seg_launch_split first (the run then only walks its active edges)
+hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0, bool split);
+// a small-bucket run's edges at its start: internal ones dropped, those with a closed end rejected at once,
+// the rest listed (SM_SEG_C_ACT); nedges = the run's largest edge count over the views
+hipError_t seg_launch_split(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t nedges);
 // every pixel's parent := its root
 hipError_t seg_launch_flatten(hipStream_t st, const SegPair& p);
 hipError_t seg_launch_sizes(hipStream_t st, const SegPair& p, int w, uint32_t m);

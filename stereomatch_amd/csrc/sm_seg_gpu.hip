@@ -419,7 +419,45 @@ __device__ __forceinline__ int seg_lslot(uint32_t* hk, uint32_t root) {
     }
 }
 
-__global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, float c, uint32_t gen0, uint32_t lc) {
+constexpr uint32_t SEG_DONE = 0x80000000u;  // an ebuf entry k_seg_split rejected already (ids < 2^31)
+constexpr int SEG_ACT_MAX = 4096;           // active edges of a run that k_seg_small buckets in LDS
+
+// The start of a run of small buckets [w0, w1), over the whole GPU.  An edge whose ends are in one component
+// stays internal for the rest of the sweep.  An edge with an end that is closed at w0 is rejected now: a
+// closed component never joins again (a join needs its own acceptance, and its threshold only changes by
+// joining), so in its own bucket the edge still joins two components, one of them closed.  The rest (both
+// ends open at w0: 538 of the 48k small-bucket edges of a synthetic C2 view) go to the active list, the
+// only edges k_seg_small then walks.  Rejected ebuf entries get SEG_DONE (its full-scan fallback skips them).
+__global__ void __launch_bounds__(256) k_seg_split(SegPair sp, int w0, int w1, float c) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t s = v.bcnt[SM_SEG_NB + w0], e = v.bcnt[SM_SEG_NB + w1];
+    const uint32_t j = s + blockIdx.x * 256 + threadIdx.x;
+    bool act = false, rej = false;
+    uint32_t id = 0;
+    if (j < e) {
+        id = v.ebuf[j];
+        const uint32_t ra = seg_find(v.par, id >> 1), rb = seg_find(v.par, edge_b(id, v.W));
+        if (ra != rb) {
+            const double wd = (double)w0;
+            act = seg_open(v, ra, wd, c) && seg_open(v, rb, wd, c);
+            rej = !act;
+        }
+    }
+    uint32_t* const ctr[2] = {v.cnt + SM_SEG_C_ACT, v.cnt + SM_SEG_C_REJ};
+    const bool pred[2] = {act, rej};
+    uint32_t slot[2];
+    block_append<2>(ctr, pred, slot);
+    if (act) v.act[slot[0]] = id;
+    if (rej) {
+        v.rej[slot[1]] = id;
+        v.ebuf[j] = id | SEG_DONE;
+    }
+}
+
+// split: k_seg_split ran first; its active edges (at most amax) are bucketed by weight in LDS and walked
+// instead of the run's ebuf ranges (otherwise the full scan, skipping the entries it rejected)
+__global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, float c, uint32_t gen0, uint32_t lc,
+                                                    int split, uint32_t amax) {
     const SegView& v = sp.v[blockIdx.x];
     __shared__ uint32_t s_n, s_out, s_h0;
     __shared__ uint32_t s_cid[SEG_LC], s_ord[SEG_LC];
@@ -435,8 +473,46 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
     // the run's bucket starts in LDS: most buckets of a run are empty (synthetic C2: 24 of ~740 hold edges),
     // and a global load per bucket just to skip it cost ~1 us each, one after the other
     __shared__ uint32_t s_start[SM_SEG_NB + 1];
-    for (int i = w0 + tid; i <= w1; i += 1024) s_start[i - w0] = v.bcnt[SM_SEG_NB + i];
+    __shared__ uint32_t s_wc[SM_SEG_NB + 1];
+    __shared__ uint32_t s_aid[SEG_ACT_MAX];
+    const int nb = w1 - w0;
+    const uint32_t na = split ? __hip_atomic_load(v.cnt + SM_SEG_C_ACT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const bool lact = split && na <= amax && na <= (uint32_t)SEG_ACT_MAX;  // block-uniform
+    if (lact) {  // the active edges bucketed by weight: counts, exclusive offsets (s_start), scatter (s_aid)
+        for (int i = tid; i <= nb; i += 1024) s_wc[i] = 0;
+        seg_wg_sync();
+        for (uint32_t k = tid; k < na; k += 1024) {
+            const uint32_t id = v.act[k], a = id >> 1;
+            atomicAdd(&s_wc[((id & 1u) ? v.wD[a] : v.wR[a]) - w0], 1u);
+        }
+        seg_wg_sync();
+        if (tid < 64) {  // one wave: exclusive scan of nb + 1 <= 767 counts, 64 at a time
+            uint32_t run = 0;
+            for (int b = 0; b <= nb; b += 64) {
+                const int i = b + tid;
+                const uint32_t x = i <= nb ? s_wc[i] : 0u;
+                uint32_t incl = x;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o);
+                    if (tid >= o) incl += y;
+                }
+                if (i <= nb) s_start[i] = run + incl - x;
+                run += __shfl(incl, 63);
+            }
+        }
+        seg_wg_sync();
+        for (int i = tid; i <= nb; i += 1024) s_wc[i] = s_start[i];  // cursors
+        seg_wg_sync();
+        for (uint32_t k = tid; k < na; k += 1024) {
+            const uint32_t id = v.act[k], a = id >> 1;
+            s_aid[atomicAdd(&s_wc[((id & 1u) ? v.wD[a] : v.wR[a]) - w0], 1u)] = id;
+        }
+    } else {
+        for (int i = w0 + tid; i <= w1; i += 1024) s_start[i - w0] = v.bcnt[SM_SEG_NB + i];
+    }
     seg_wg_sync();
+    if (split && tid == 0) v.cnt[SM_SEG_C_ACT] = 0;  // for the next run (read above by every thread, before the barrier)
     uint32_t gen = gen0;
     for (int w = w0; w < w1; ++w) {
         const uint32_t s = s_start[w - w0], m = s_start[w + 1 - w0] - s;
@@ -451,8 +527,8 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
             const uint32_t i = i0 + tid;
             bool cand = false, rej = false;
             uint32_t id = 0, ra = 0, rb = 0;
-            if (i < m) {
-                id = v.ebuf[s + i];
+            if (i < m) id = lact ? s_aid[s + i] : v.ebuf[s + i];
+            if (i < m && !(id & SEG_DONE)) {
                 ra = seg_find(v.par, id >> 1);
                 rb = seg_find(v.par, edge_b(id, v.W));
                 if (ra != rb) {
@@ -721,10 +797,17 @@ hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t g
     return hipGetLastError();
 }
 
-hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0) {
-    // SM_SEG_NOLDS=1: every small bucket takes the Boruvka rounds (A/B of the LDS Kruskal)
+hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0, bool split) {
+    // SM_SEG_NOLDS=1: every small bucket takes the Boruvka rounds (A/B of the LDS Kruskal); SM_SEG_ACT_MAX: the
+    // most active edges bucketed in LDS (0: always the full scan; tests)
     const uint32_t lc = getenv("SM_SEG_NOLDS") ? 0u : (uint32_t)SEG_LC;
-    hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0, lc);
+    const uint32_t amax = getenv("SM_SEG_ACT_MAX") ? (uint32_t)atoi(getenv("SM_SEG_ACT_MAX")) : (uint32_t)SEG_ACT_MAX;
+    hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0, lc, split ? 1 : 0, amax);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_split(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t nedges) {
+    if (nedges) hipLaunchKernelGGL(k_seg_split, dim3(blocks_of(nedges, 256), p.nv), dim3(256), 0, st, p, w0, w1, c);
     return hipGetLastError();
 }
 

@@ -6,6 +6,10 @@ reference's serial Felzenszwalb sweep (segment-graph.h:54-89) plus its min-size 
     whole bucket, joined ones accept the rest of it),
   * the bucket's marked edges are the minimum spanning forest, keyed by edge id, of its open-open
     edges between components (any order gives the same partition), and
+  * from any bucket w0 on (the GPU: the start of a run of small buckets, k_seg_split), every later edge can
+    be classified once against the state at w0's start: internal ones stay internal, one with an end
+    closed at w0 is rejected (a closed component never joins again: a join needs its own acceptance), and
+    only the rest (both ends open at w0) need the per-bucket sweep,
   * the rejected edges are its other two-component edges; the min-size merge only needs those whose
     end is smaller than min_size after the sweep, in (w, id) order, and of those only the first of each
     pair of sweep roots (the GPU's pair dedupe, seg_launch_dedupe: a later edge of the same pair finds
@@ -20,7 +24,7 @@ from oracle import oracle as O
 from tools.synth import make_pair
 
 
-def bucket_segment(W, H, wR, wD, c, min_size, dedupe=False):
+def bucket_segment(W, H, wR, wD, c, min_size, dedupe=False, split_at=None):
     N = W * H
     p = np.arange(N)
     x, y = p % W, p // W
@@ -39,8 +43,22 @@ def bucket_segment(W, H, wR, wD, c, min_size, dedupe=False):
     mask = np.zeros(N, np.uint8)
     rejected = []
     cf = np.float32(c)
+    active = None  # after the split: the edges still to sweep
     for wv in np.unique(w):
+        if split_at is not None and active is None and wv >= split_at:
+            # the split at this bucket's start (k_seg_split): every edge of weight >= wv classified once
+            active = set()
+            for i in e[w >= wv]:
+                ra, rb = find(i >> 1), find((i >> 1) + (W if i & 1 else 1))
+                if ra == rb:
+                    continue
+                if all(float(wv) <= float(wl[r]) + float(np.float32(cf / np.float32(size[r]))) for r in (ra, rb)):
+                    active.add(int(i))
+                else:
+                    rejected.append((int(w[e == i][0]), int(i)))
         ids = np.sort(e[w == wv])
+        if active is not None:
+            ids = np.array([i for i in ids if int(i) in active], dtype=np.int64)
         roots = [(find(i >> 1), find((i >> 1) + (W if i & 1 else 1))) for i in ids]
         opened = {}
 
@@ -105,5 +123,19 @@ def test_bucket_sweep_equals_serial_sweep(W, H, c, min_size, index, dedupe):
     wR, wD = O.edge_weights(O.median3(left))
     ref, n = O.segment(W, H, wR, wD, c, min_size)
     got, k = bucket_segment(W, H, wR, wD, c, min_size, dedupe)
+    np.testing.assert_array_equal(got, ref)
+    assert k == n
+
+
+@pytest.mark.parametrize("W,H,c,min_size,index", [(64, 48, 5000.0, 200, 0), (64, 48, 300.0, 20, 1),
+                                                  (80, 40, 40.0, 5, 2), (72, 54, 1000.0, 60, 4)])
+@pytest.mark.parametrize("q", [0.0, 0.3, 0.6, 0.9])
+def test_split_sweep_equals_serial_sweep(W, H, c, min_size, index, q):
+    """k_seg_split's argument: the sweep split at the bucket holding the q-quantile of the weights."""
+    left, _, _ = make_pair(W, H, 32, index=index)
+    wR, wD = O.edge_weights(O.median3(left))
+    ref, n = O.segment(W, H, wR, wD, c, min_size)
+    ws = np.sort(np.concatenate([wR.reshape(H, W)[:, :-1].ravel(), wD.reshape(H, W)[:-1, :].ravel()]))
+    got, k = bucket_segment(W, H, wR, wD, c, min_size, True, split_at=int(ws[int(q * (len(ws) - 1))]))
     np.testing.assert_array_equal(got, ref)
     assert k == n
