@@ -742,6 +742,21 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
     if (dbg) t2 = now_ms();
     HIPC(hipStreamSynchronize(st));
     if (dbg) t3 = now_ms();
+    if (getenv("SM_SEG_PROF")) {  // k_seg_small's timings (sm_seg_gpu.hip SEG_PROF_SLOT): prologue, then per bucket
+        for (int i = 0; i < vs.n; ++i) {
+            std::vector<uint32_t> pr(2 + SM_SEG_NB);
+            HIPC(hipMemcpy(pr.data(), P<uint32_t>(ctx->sg[vs.v[i]].cnt) + SM_SEG_C_LIST + 60000, pr.size() * 4,
+                           hipMemcpyDeviceToHost));
+            fprintf(stderr, "seg prof view %d: small-run prologue %.1f us, active %u; buckets (us):", i, pr[0] * 0.01, pr[1]);
+            double tot = 0;
+            for (int w = 0; w < SM_SEG_NB; ++w)
+                if (pr[2 + w]) {
+                    fprintf(stderr, " %d:%.1f%s", w, (pr[2 + w] & 0x7FFFFFFFu) * 0.01, (pr[2 + w] >> 31) ? "B" : "");
+                    tot += (pr[2 + w] & 0x7FFFFFFFu) * 0.01;
+                }
+            fprintf(stderr, " | total %.1f us\n", tot);
+        }
+    }
     void* temp[2] = {nullptr, nullptr};
     size_t tbytes[2] = {0, 0};
     for (int i = 0; i < vs.n; ++i) {

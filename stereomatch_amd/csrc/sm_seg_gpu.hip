@@ -456,9 +456,174 @@ __global__ void __launch_bounds__(256) k_seg_split(SegPair sp, int w0, int w1, f
 
 // split: k_seg_split ran first; its active edges (at most amax) are bucketed by weight in LDS and walked
 // instead of the run's ebuf ranges (otherwise the full scan, skipping the entries it rejected)
-__global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, float c, uint32_t gen0, uint32_t lc,
-                                                    int split, uint32_t amax) {
+constexpr int SEG_PROF_SLOT = 60000;  // SM_SEG_PROF: k_seg_small's timings at cnt[SM_SEG_C_LIST + 60000 ..]
+constexpr int SEG_RUN_DONE = 59990;   // cnt[SM_SEG_C_LIST + 59990]: k_seg_run did the run (k_seg_small skips it)
+constexpr int SEG_RUN_MAX = 6144;     // active edges of a run that k_seg_run holds in LDS
+constexpr int SEG_RUN_RS = 6144;      // its root slots
+
+__device__ __forceinline__ int seg_rslot(uint32_t* hk, uint32_t root, uint32_t* nfull) {
+    int h = (int)(((root * 2654435761u) >> 8) % (uint32_t)SEG_RUN_RS);
+    for (int probe = 0; probe < 256; ++probe) {
+        const uint32_t prev = atomicCAS(hk + h, SEG_EMPTY, root);
+        if (prev == SEG_EMPTY || prev == root) return h;
+        h = h + 1 == SEG_RUN_RS ? 0 : h + 1;
+    }
+    atomicAdd(nfull, 1u);  // (table too full: the run falls back to k_seg_small)
+    return 0;
+}
+
+// A run of small buckets [w0, w1) after k_seg_split, entirely in LDS.  Only the run's active edges (both
+// ends open at w0) can join anything (k_seg_split), and they only join components that were open at w0, so
+// the run's whole union-find state lives in LDS: the active edges bucketed by weight and sorted by id
+// within a bucket, and their roots at the run's start (hashed slots with size and last-join weight).  Per
+// bucket: every edge's current roots and the acceptance test at the bucket's start in parallel, then the
+// candidates' Kruskal in id order (thread 0): the minimum spanning forest keyed by id of the bucket's open-open
+// edges, sizes summed, last-join weight w.  No global memory is touched between buckets --
+// k_seg_small's buckets each paid ~5 dependent global round trips (4-8 us; 250 buckets in one synthetic C2
+// view).  At the end: joined roots' parents, the roots' sizes and weights, and the rejected edges go back.
+// A run that does not fit (more than SEG_RUN_MAX active edges, or its roots overflow the table) sets no done
+// flag and k_seg_small runs it instead (nothing global was written).
+__global__ void __launch_bounds__(1024) k_seg_run(SegPair sp, int w0, int w1, float c) {
     const SegView& v = sp.v[blockIdx.x];
+    const int tid = (int)threadIdx.x, nb = w1 - w0;
+    __shared__ uint32_t s_start[SM_SEG_NB + 1], s_wc[SM_SEG_NB + 1];
+    __shared__ uint32_t s_aid[SEG_RUN_MAX];
+    __shared__ uint16_t s_ea[SEG_RUN_MAX], s_eb[SEG_RUN_MAX], s_ord[SEG_RUN_MAX];
+    __shared__ uint8_t s_fl[SEG_RUN_MAX];
+    __shared__ uint32_t s_hk[SEG_RUN_RS], s_sz[SEG_RUN_RS];
+    __shared__ uint16_t s_par[SEG_RUN_RS], s_wl[SEG_RUN_RS];
+    __shared__ uint32_t s_full;
+    const uint32_t na = __hip_atomic_load(v.cnt + SM_SEG_C_ACT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (na > (uint32_t)SEG_RUN_MAX) return;  // block-uniform: k_seg_small runs it
+    for (int i = tid; i <= nb; i += 1024) s_wc[i] = 0;
+    for (int i = tid; i < SEG_RUN_RS; i += 1024) {
+        s_hk[i] = SEG_EMPTY;
+        s_par[i] = (uint16_t)i;
+    }
+    if (tid == 0) s_full = 0;
+    __syncthreads();
+    // the active edges by weight: counts, exclusive offsets (s_start), scatter
+    for (uint32_t k = tid; k < na; k += 1024) {
+        const uint32_t id = v.act[k], a = id >> 1;
+        atomicAdd(&s_wc[((id & 1u) ? v.wD[a] : v.wR[a]) - w0], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {
+        uint32_t run = 0;
+        for (int b = 0; b <= nb; b += 64) {
+            const int i = b + tid;
+            const uint32_t x = i <= nb ? s_wc[i] : 0u;
+            uint32_t incl = x;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (tid >= o) incl += y;
+            }
+            if (i <= nb) s_start[i] = run + incl - x;
+            run += __shfl(incl, 63);
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i <= nb; i += 1024) s_wc[i] = s_start[i];
+    __syncthreads();
+    for (uint32_t k = tid; k < na; k += 1024) {
+        const uint32_t id = v.act[k], a = id >> 1;
+        s_aid[atomicAdd(&s_wc[((id & 1u) ? v.wD[a] : v.wR[a]) - w0], 1u)] = id;
+    }
+    __syncthreads();
+    // per edge: its rank by id within its bucket (Kruskal's order), and its ends' roots at the run's start
+    for (uint32_t k = tid; k < na; k += 1024) {
+        const uint32_t id = s_aid[k], a = id >> 1;
+        const int wb = ((id & 1u) ? v.wD[a] : v.wR[a]) - w0;
+        const uint32_t lo = s_start[wb], hi = s_start[wb + 1];
+        uint32_t r = 0;
+        for (uint32_t j = lo; j < hi; ++j) r += s_aid[j] < id;
+        s_ord[lo + r] = (uint16_t)k;
+        s_ea[k] = (uint16_t)seg_rslot(s_hk, seg_find(v.par, a), &s_full);
+        s_eb[k] = (uint16_t)seg_rslot(s_hk, seg_find(v.par, edge_b(id, v.W)), &s_full);
+        s_fl[k] = 0;
+    }
+    __syncthreads();
+    if (s_full) return;  // block-uniform (nothing global written): k_seg_small runs it
+    for (int i = tid; i < SEG_RUN_RS; i += 1024) {
+        const uint32_t r = s_hk[i];
+        if (r != SEG_EMPTY) {
+            s_sz[i] = __hip_atomic_load(v.sz + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_wl[i] = v.wl[r];
+        }
+    }
+    __syncthreads();
+    for (int w = w0; w < w1; ++w) {
+        const uint32_t lo = s_start[w - w0], hi = s_start[w + 1 - w0];
+        if (lo == hi) continue;  // uniform
+        const double wd = (double)w;
+        for (uint32_t k = lo + tid; k < hi; k += 1024) {  // current roots, acceptance at the bucket's start
+            int a = s_ea[k], b = s_eb[k];
+            while (s_par[a] != a) a = s_par[a];
+            while (s_par[b] != b) b = s_par[b];
+            uint8_t f = 0;
+            if (a != b) {
+                const bool oa = wd <= (double)s_wl[a] + (double)__fdiv_rn(c, (float)s_sz[a]);
+                const bool ob = wd <= (double)s_wl[b] + (double)__fdiv_rn(c, (float)s_sz[b]);
+                f = (oa && ob) ? 1 : 2;  // candidate / rejected
+            }
+            s_fl[k] = f;
+        }
+        __syncthreads();
+        if (tid == 0)  // Kruskal in id order over the candidates
+            for (uint32_t q = lo; q < hi; ++q) {
+                const uint32_t k = s_ord[q];
+                if (s_fl[k] != 1) continue;
+                const int a = seg_lfind(s_par, s_ea[k]), b = seg_lfind(s_par, s_eb[k]);
+                if (a == b) continue;
+                s_par[b] = (uint16_t)a;
+                s_sz[a] += s_sz[b];
+                s_wl[a] = (uint16_t)w;
+                const uint32_t id = s_aid[k];
+                if (id & 1u)
+                    v.mD[id >> 1] = 1;
+                else
+                    v.mR[id >> 1] = 1;
+            }
+        __syncthreads();
+    }
+    // write-back: joined roots onto their final roots, the roots' sizes and last-join weights
+    for (int i = tid; i < SEG_RUN_RS; i += 1024) {
+        const uint32_t r = s_hk[i];
+        if (r == SEG_EMPTY) continue;
+        int f = i;
+        while (s_par[f] != f) f = s_par[f];
+        if (f != i) {
+            v.par[r] = s_hk[f];
+        } else {
+            v.sz[r] = s_sz[i];
+            v.wl[r] = s_wl[i];
+        }
+    }
+    // the rejected edges (flag 2)
+    for (uint32_t k0 = 0; k0 < na; k0 += 1024) {
+        const uint32_t k = k0 + tid;
+        const bool rj = k < na && s_fl[k] == 2;
+        uint32_t* const ctr[1] = {v.cnt + SM_SEG_C_REJ};
+        const bool pred[1] = {rj};
+        uint32_t slot[1];
+        block_append<1>(ctr, pred, slot);
+        if (rj) v.rej[slot[0]] = s_aid[k];
+    }
+    if (tid == 0) {
+        v.cnt[SM_SEG_C_ACT] = 0;
+        v.cnt[SM_SEG_C_LIST + SEG_RUN_DONE] = 1;
+    }
+}
+__global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, float c, uint32_t gen0, uint32_t lc,
+                                                    int split, uint32_t amax, int prof_on) {
+    const unsigned long long tk0 = prof_on && threadIdx.x == 0 ? wall_clock64() : 0ull;
+    const SegView& v = sp.v[blockIdx.x];
+    if (split && __hip_atomic_load(v.cnt + SM_SEG_C_LIST + SEG_RUN_DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __syncthreads();  // every thread has read the flag
+        if (threadIdx.x == 0) v.cnt[SM_SEG_C_LIST + SEG_RUN_DONE] = 0;
+        return;  // k_seg_run did this run
+    }
     __shared__ uint32_t s_n, s_out, s_h0;
     __shared__ uint32_t s_cid[SEG_LC], s_ord[SEG_LC];
     __shared__ uint16_t s_sa[SEG_LC], s_sb[SEG_LC];
@@ -513,6 +678,13 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
     }
     seg_wg_sync();
     if (split && tid == 0) v.cnt[SM_SEG_C_ACT] = 0;  // for the next run (read above by every thread, before the barrier)
+    // SM_SEG_PROF builds: wall-clock ticks (100 MHz) of the prologue and of each bucket in spare list counters
+    uint32_t* const prof = prof_on ? v.cnt + SM_SEG_C_LIST + SEG_PROF_SLOT : nullptr;
+    unsigned long long tk = prof && tid == 0 ? wall_clock64() : 0ull;
+    if (prof && tid == 0) {
+        prof[0] = (uint32_t)(tk - tk0);
+        prof[1] = na;
+    }
     uint32_t gen = gen0;
     for (int w = w0; w < w1; ++w) {
         const uint32_t s = s_start[w - w0], m = s_start[w + 1 - w0] - s;
@@ -596,6 +768,11 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
                 s_par[l] = (uint16_t)l;
             }
             seg_wg_sync();  // sizes final before the next bucket's acceptance tests
+            if (prof && tid == 0) {
+                const unsigned long long t = wall_clock64();
+                prof[2 + w] = (uint32_t)(t - tk);
+                tk = t;
+            }
             continue;
         }
         // more candidates than the LDS holds: the table back to empty, then the Boruvka rounds
@@ -606,6 +783,11 @@ __global__ void __launch_bounds__(1024) k_seg_small(SegPair sp, int w0, int w1, 
         const uint32_t h1 = __hip_atomic_load(v.cnt + SM_SEG_C_HOOK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (uint32_t i0 = s_h0; i0 < h1; i0 += 1024) seg_size_update(v, i0 + tid, w, i0 + tid < h1);
         seg_wg_sync();  // sizes final before the next bucket's acceptance tests
+        if (prof && tid == 0) {
+            const unsigned long long t = wall_clock64();
+            prof[2 + w] = (uint32_t)(t - tk) | 0x80000000u;  // (Boruvka rounds)
+            tk = t;
+        }
     }
 }
 
@@ -802,7 +984,10 @@ hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, fl
     // most active edges bucketed in LDS (0: always the full scan; tests)
     const uint32_t lc = getenv("SM_SEG_NOLDS") ? 0u : (uint32_t)SEG_LC;
     const uint32_t amax = getenv("SM_SEG_ACT_MAX") ? (uint32_t)atoi(getenv("SM_SEG_ACT_MAX")) : (uint32_t)SEG_ACT_MAX;
-    hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0, lc, split ? 1 : 0, amax);
+    const int prof = getenv("SM_SEG_PROF") ? 1 : 0;
+    // SM_SEG_NORUN=1: no k_seg_run (every split run through k_seg_small)
+    if (split && !getenv("SM_SEG_NORUN")) hipLaunchKernelGGL(k_seg_run, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c);
+    hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0, lc, split ? 1 : 0, amax, prof);
     return hipGetLastError();
 }
 

@@ -782,7 +782,8 @@ def test_full_size_c3_segment_forest_and_match(gpu_ctx):
                                  {"SM_SEG_SMALL": "100000000"}, {"SM_SEG_GLOBAL_ROUNDS": "7"}, {"SM_SEG_HOST": "1"},
                                  {"SM_SEG_NODEDUP": "1"}, {"SM_SEG_FLATTEN": "0"}, {"SM_SEG_FLATTEN": "3"},
                                  {"SM_SEG_NOLDS": "1"}, {"SM_SEG_NOLDS": "1", "SM_SEG_SMALL": "100000000"},
-                                 {"SM_SEG_NOSPLIT": "1"}, {"SM_SEG_ACT_MAX": "0"}, {"SM_SEG_ACT_MAX": "0", "SM_SEG_NOLDS": "1"}])
+                                 {"SM_SEG_NOSPLIT": "1"}, {"SM_SEG_NORUN": "1"}, {"SM_SEG_NORUN": "1", "SM_SEG_ACT_MAX": "0"},
+                                 {"SM_SEG_NORUN": "1", "SM_SEG_ACT_MAX": "0", "SM_SEG_NOLDS": "1"}])
 def test_segment_forest_schedules(gpu_ctx, monkeypatch, env):
     """The GPU segmentation's launch schedules give the same forest: every bucket over the whole GPU
     (with and without global Boruvka rounds before the one-workgroup tail), every bucket in one
@@ -790,8 +791,9 @@ def test_segment_forest_schedules(gpu_ctx, monkeypatch, env):
     candidate instead of the first of each root pair (SM_SEG_NODEDUP); no root flattening, or
     flattening before every bucket (SM_SEG_FLATTEN); the one-workgroup buckets by Boruvka rounds instead
     of the LDS Kruskal (SM_SEG_NOLDS); small-bucket runs without the k_seg_split pre-pass
-    (SM_SEG_NOSPLIT), or with it but the full scan instead of the LDS-bucketed active edges
-    (SM_SEG_ACT_MAX=0: the scan skips the edges the pre-pass rejected)."""
+    (SM_SEG_NOSPLIT), or with it but without the LDS-resident run (SM_SEG_NORUN: k_seg_small over the
+    LDS-bucketed active edges, or with SM_SEG_ACT_MAX=0 the full scan, which skips the edges the pre-pass
+    rejected)."""
     import stereomatch_amd as sm
     for k, val in env.items():
         monkeypatch.setenv(k, val)

@@ -34,10 +34,11 @@ def main():
     ap.add_argument("H", type=int, nargs="?", default=1200)
     ap.add_argument("--c", type=float, default=5000.0)
     ap.add_argument("--small", type=int, default=16384)
+    ap.add_argument("--view", default="left", choices=["left", "right"])
     a = ap.parse_args()
     W, H = a.W, a.H
-    left, _, _ = make_pair(W, H, 128, index=0)
-    wR, wD = O.edge_weights(O.median3(left))
+    left, right, _ = make_pair(W, H, 128, index=0)
+    wR, wD = O.edge_weights(O.median3(left if a.view == "left" else right))
     wR = np.asarray(wR, dtype=np.int64).reshape(-1)
     wD = np.asarray(wD, dtype=np.int64).reshape(-1)
     N = W * H
