@@ -553,40 +553,59 @@ __global__ void __launch_bounds__(1024) k_seg_run(SegPair sp, int w0, int w1, fl
         }
     }
     __syncthreads();
-    for (int w = w0; w < w1; ++w) {
-        const uint32_t lo = s_start[w - w0], hi = s_start[w + 1 - w0];
-        if (lo == hi) continue;  // uniform
-        const double wd = (double)w;
-        for (uint32_t k = lo + tid; k < hi; k += 1024) {  // current roots, acceptance at the bucket's start
-            int a = s_ea[k], b = s_eb[k];
-            while (s_par[a] != a) a = s_par[a];
-            while (s_par[b] != b) b = s_par[b];
-            uint8_t f = 0;
-            if (a != b) {
-                const bool oa = wd <= (double)s_wl[a] + (double)__fdiv_rn(c, (float)s_sz[a]);
-                const bool ob = wd <= (double)s_wl[b] + (double)__fdiv_rn(c, (float)s_sz[b]);
-                f = (oa && ob) ? 1 : 2;  // candidate / rejected
+    // the sweep on wave 0 alone (no workgroup barriers between buckets): its lanes take a bucket's edges in
+    // id order, 64 at a time -- current roots and the acceptance test at the bucket's start, all chunks of
+    // the bucket first -- then lane 0 joins the candidates in id order (Kruskal)
+    if (tid < 64) {
+        const int lane = tid;
+        for (int w = w0; w < w1; ++w) {
+            const uint32_t lo = s_start[w - w0], hi = s_start[w + 1 - w0];
+            if (lo == hi) continue;  // uniform
+            const double wd = (double)w;
+            for (uint32_t q0 = lo; q0 < hi; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                if (q < hi) {
+                    const uint32_t k = s_ord[q];
+                    int a = s_ea[k], b = s_eb[k];
+                    while (s_par[a] != a) a = s_par[a];
+                    while (s_par[b] != b) b = s_par[b];
+                    uint8_t f = 0;
+                    if (a != b) {
+                        const bool oa = wd <= (double)s_wl[a] + (double)__fdiv_rn(c, (float)s_sz[a]);
+                        const bool ob = wd <= (double)s_wl[b] + (double)__fdiv_rn(c, (float)s_sz[b]);
+                        f = (oa && ob) ? 1 : 2;  // candidate / rejected
+                    }
+                    s_fl[k] = f;
+                }
             }
-            s_fl[k] = f;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (uint32_t q0 = lo; q0 < hi; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                const uint32_t k = q < hi ? s_ord[q] : 0u;
+                unsigned long long m = __ballot(q < hi && s_fl[k] == 1);
+                while (m) {  // uniform: the candidates of this chunk in id order
+                    const int j = __ffsll((long long)m) - 1;
+                    m &= m - 1ull;
+                    const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)k, j);
+                    if (lane == 0) {
+                        const int a = seg_lfind(s_par, s_ea[kk]), b = seg_lfind(s_par, s_eb[kk]);
+                        if (a != b) {
+                            s_par[b] = (uint16_t)a;
+                            s_sz[a] += s_sz[b];
+                            s_wl[a] = (uint16_t)w;
+                            const uint32_t id = s_aid[kk];
+                            if (id & 1u)
+                                v.mD[id >> 1] = 1;
+                            else
+                                v.mR[id >> 1] = 1;
+                        }
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
-        __syncthreads();
-        if (tid == 0)  // Kruskal in id order over the candidates
-            for (uint32_t q = lo; q < hi; ++q) {
-                const uint32_t k = s_ord[q];
-                if (s_fl[k] != 1) continue;
-                const int a = seg_lfind(s_par, s_ea[k]), b = seg_lfind(s_par, s_eb[k]);
-                if (a == b) continue;
-                s_par[b] = (uint16_t)a;
-                s_sz[a] += s_sz[b];
-                s_wl[a] = (uint16_t)w;
-                const uint32_t id = s_aid[k];
-                if (id & 1u)
-                    v.mD[id >> 1] = 1;
-                else
-                    v.mR[id >> 1] = 1;
-            }
-        __syncthreads();
     }
+    __syncthreads();
     // write-back: joined roots onto their final roots, the roots' sizes and last-join weights
     for (int i = tid; i < SEG_RUN_RS; i += 1024) {
         const uint32_t r = s_hk[i];
