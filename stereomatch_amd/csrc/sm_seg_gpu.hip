@@ -179,6 +179,8 @@ __global__ void __launch_bounds__(256) k_seg_scatter(SegPair sp) {
     }
 }
 
+constexpr uint32_t SEG_EMPTY = 0xFFFFFFFFu;  // an empty LDS hash slot
+
 __device__ __forceinline__ unsigned long long seg_key(uint32_t gen, uint32_t id) {
     return ((unsigned long long)(0xFFFFFFFFu - gen) << 32) | id;
 }
@@ -349,10 +351,122 @@ __device__ int seg_wg_rounds(const SegView& v, int b, uint32_t n, uint32_t gen0,
     return (int)g;
 }
 
-__global__ void __launch_bounds__(1024) k_seg_tail(SegPair sp, int lin, uint32_t gen0) {
+// The tail's rounds on an LDS union-find (big buckets): the n (<= SEG_TAIL_MAX) crossing candidates left
+// after the global rounds, their current roots hashed into LDS slots, then Boruvka rounds with LDS atomics
+// (keys (~round << 32) | id, never reset) until no candidate crosses two components; the bucket's minimum
+// spanning forest keyed by id is unique, so these rounds mark the same edges as the global ones.  Then every
+// joined root goes onto its final root in the global union-find and into `hooked` (k_seg_sizes adds the
+// sizes).  Synthetic C2: at most 2.7k candidates; the global-memory rounds took up to 120 us per bucket
+// (several dependent global round trips and barriers per round).  Returns false, having written nothing
+// global, when the roots overflow the table (then the global rounds run).
+constexpr int SEG_TAIL_MAX = 4096;
+constexpr int SEG_TAIL_RS = 8192;
+constexpr uint16_t SEG_NOSLOT = 0xFFFFu;
+__device__ __forceinline__ int seg_tslot(uint32_t* hk, uint32_t root, uint32_t* full) {
+    int h = (int)((root * 2654435761u) >> 19) & (SEG_TAIL_RS - 1);
+    for (int probe = 0; probe < 256; ++probe) {
+        const uint32_t prev = atomicCAS(hk + h, SEG_EMPTY, root);
+        if (prev == SEG_EMPTY || prev == root) return h;
+        h = (h + 1) & (SEG_TAIL_RS - 1);
+    }
+    atomicAdd(full, 1u);
+    return 0;
+}
+__device__ bool seg_tail_lds(const SegView& v, int b, uint32_t n) {
+    __shared__ uint32_t s_id[SEG_TAIL_MAX];
+    __shared__ uint16_t s_a[SEG_TAIL_MAX], s_b[SEG_TAIL_MAX];
+    __shared__ uint32_t s_hk[SEG_TAIL_RS];
+    __shared__ uint16_t s_par[SEG_TAIL_RS];
+    __shared__ unsigned long long s_best[SEG_TAIL_RS];
+    __shared__ uint32_t s_full, s_cross;
+    const int tid = (int)threadIdx.x;
+    for (int i = tid; i < SEG_TAIL_RS; i += 1024) {
+        s_hk[i] = SEG_EMPTY;
+        s_par[i] = (uint16_t)i;
+        s_best[i] = ~0ull;
+    }
+    if (tid == 0) s_full = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < n; k += 1024) {
+        const uint4 e = v.list[b][k];
+        const uint32_t ra = seg_find(v.par, e.y), rb = seg_find(v.par, e.z);
+        s_id[k] = e.x;
+        s_a[k] = ra == rb ? SEG_NOSLOT : (uint16_t)seg_tslot(s_hk, ra, &s_full);
+        s_b[k] = ra == rb ? SEG_NOSLOT : (uint16_t)seg_tslot(s_hk, rb, &s_full);
+    }
+    __syncthreads();
+    if (s_full) return false;  // block-uniform
+    for (uint32_t round = 0;; ++round) {
+        if (tid == 0) s_cross = 0;
+        __syncthreads();
+        // each root's minimum crossing key; the edge's slots become its current roots (s_par is only read
+        // in this phase), which the hook phase then uses as they are -- finds there would race the hooks
+        for (uint32_t k = tid; k < n; k += 1024) {
+            if (s_a[k] == SEG_NOSLOT) continue;
+            int a = s_a[k], c = s_b[k];
+            while (s_par[a] != a) a = s_par[a];
+            while (s_par[c] != c) c = s_par[c];
+            if (a == c) {  // internal for good
+                s_a[k] = SEG_NOSLOT;
+                continue;
+            }
+            s_a[k] = (uint16_t)a;
+            s_b[k] = (uint16_t)c;
+            const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - round) << 32) | s_id[k];
+            atomicMin(&s_best[a], key);
+            atomicMin(&s_best[c], key);
+            s_cross = 1;
+        }
+        __syncthreads();
+        if (!s_cross) break;  // block-uniform
+        for (uint32_t k = tid; k < n; k += 1024) {  // hooks along those keys (mutual pairs: larger slot onto smaller)
+            if (s_a[k] == SEG_NOSLOT) continue;
+            const int a = s_a[k], c = s_b[k];  // roots at the selection
+            const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - round) << 32) | s_id[k];
+            const bool ba = s_best[a] == key, bc = s_best[c] == key;
+            if (!ba && !bc) continue;
+            const int child = ba && bc ? (a > c ? a : c) : ba ? a : c;
+            const int parent = ba && bc ? (a > c ? c : a) : ba ? c : a;
+            s_par[child] = (uint16_t)parent;
+            const uint32_t id = s_id[k];
+            if (id & 1u)
+                v.mD[id >> 1] = 1;
+            else
+                v.mR[id >> 1] = 1;
+        }
+        __syncthreads();
+        if (round + 1 >= (uint32_t)SM_SEG_TAIL_GENS) {  // cannot happen (Boruvka halves the components)
+            if (tid == 0) atomicOr(v.cnt + SM_SEG_C_ERR, 1u);
+            break;
+        }
+    }
+    // joined roots onto their final roots (global), and into `hooked` for k_seg_sizes
+    for (int i0 = 0; i0 < SEG_TAIL_RS; i0 += 1024) {
+        const int i = i0 + tid;
+        const uint32_t r = s_hk[i];
+        int f = i;
+        if (r != SEG_EMPTY)
+            while (s_par[f] != f) f = s_par[f];
+        const bool joined = r != SEG_EMPTY && f != i;
+        uint32_t* const ctr[1] = {v.cnt + SM_SEG_C_HOOK};
+        const bool pred[1] = {joined};
+        uint32_t slot[1];
+        block_append<1>(ctr, pred, slot);
+        if (joined) {
+            v.par[r] = s_hk[f];
+            v.hooked[slot[0]] = r;
+        }
+    }
+    return true;
+}
+
+// lds: try seg_tail_lds first (SM_SEG_TAIL_GLOBAL=1: always the global-memory rounds)
+__global__ void __launch_bounds__(1024) k_seg_tail(SegPair sp, int lin, uint32_t gen0, int lds) {
     const SegView& v = sp.v[blockIdx.x];
     __shared__ uint32_t s_out;
-    seg_wg_rounds(v, lin & 1, v.cnt[SM_SEG_C_LIST + lin], gen0, &s_out, false);
+    const uint32_t n = v.cnt[SM_SEG_C_LIST + lin];
+    if (lds && n <= (uint32_t)SEG_TAIL_MAX && seg_tail_lds(v, lin & 1, n)) return;
+    seg_wg_rounds(v, lin & 1, n, gen0, &s_out, false);
 }
 
 // hooked root i (valid lanes) adds its size to its component's root, whose last-join weight becomes w.
@@ -396,7 +510,6 @@ __device__ __forceinline__ void seg_size_update(const SegView& v, uint32_t i, in
 // from gen0, at most SM_SEG_TAIL_GENS per such bucket.
 constexpr int SEG_LC = 1024;         // candidates of an LDS bucket
 constexpr int SEG_LH = 4096;         // hash slots (power of two, >= 2 SEG_LC)
-constexpr uint32_t SEG_EMPTY = 0xFFFFFFFFu;
 
 __device__ __forceinline__ int seg_lfind(uint16_t* par, int x) {
     while (par[x] != x) {
@@ -994,7 +1107,8 @@ hipError_t seg_launch_round(hipStream_t st, const SegPair& p, uint32_t m, int li
 }
 
 hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t gen0) {
-    hipLaunchKernelGGL(k_seg_tail, dim3(p.nv), dim3(1024), 0, st, p, lin, gen0);
+    const int lds = getenv("SM_SEG_TAIL_GLOBAL") ? 0 : 1;
+    hipLaunchKernelGGL(k_seg_tail, dim3(p.nv), dim3(1024), 0, st, p, lin, gen0, lds);
     return hipGetLastError();
 }
 

@@ -1,4 +1,4 @@
-# round 4: segment mode -- k_seg_run (a small-bucket run resident in LDS)
+# round 4: segment mode -- k_seg_run on one wave, big-bucket tails on an LDS union-find
 # onesweep sorts -> gpurun_out/r04ae
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -14,6 +14,7 @@ lat() {  # tag, env...: segment-mode single-frame latency and streamed ms/frame
 }
 lat default SM_SEG_X=0 || exit 2
 lat norun SM_SEG_NORUN=1 || exit 3
+lat tailglobal SM_SEG_TAIL_GLOBAL=1 || exit 7
 lat default2 SM_SEG_X=0 || exit 4
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/raw -o run --output-format csv -- python3 bench.py --segment-c 5000 --min-size 200 --inflight 1 --steps 4 --warmup 2 --no-cpu --no-pms > $O/seg1.log 2>&1 || exit 5
 f=$(find $O/raw -name '*kernel_trace.csv' | head -1); cp "$f" $O/kernel_trace_seg1.csv
