@@ -107,6 +107,7 @@ struct SegGpu {
     PinnedVec<uint32_t> h_b, h_cnt, h_hooks, h_lsize, h_lroot;
     PinnedVec<SegMin> h_min;
     PinnedVec<SegEdge> h_dense;
+    std::vector<SegEdge> h_dsort;  // seg_sort_dense's scratch
     std::vector<uint32_t> loc;         // SM_SEG_NODEDUP's root -> local id table (all ~0 between calls)
     std::vector<uint32_t> mpar, msize;  // the merge's union-find over local ids
 };
@@ -542,6 +543,36 @@ int seg_minsize_host(const SegMin* e, uint32_t n, uint32_t ms, uint32_t* out, st
 // The same serial rule over the deduplicated candidates (seg_launch_dedupe): the first candidate of each
 // pair of sweep roots, in (w, id) order, with the roots as dense local ids (lsize / lroot: their sizes
 // and pixels).  Same hooks and marked edges as seg_minsize_host over all candidates.
+// the hashed pair dedupe's kept candidates (unordered) into the merge's (w, id) order: LSD radix sort of the
+// key (w << 32) | id in four 11-bit digits (w < 2^10, id < 2^23 for images below 4.19 M pixels; the full
+// 42 bits otherwise) -- ~23k edges per C2 view, well under 0.1 ms
+void seg_sort_dense(SegEdge* e, uint32_t n, std::vector<SegEdge>& tmp) {
+    if (n < 2) return;
+    uint32_t idmax = 0;
+    for (uint32_t i = 0; i < n; ++i) idmax = std::max(idmax, e[i].id);
+    int idbits = 1;
+    while (idbits < 32 && (1ull << idbits) <= idmax) ++idbits;
+    const int bits = idbits + 10;  // w < 1024
+    tmp.resize(n);
+    SegEdge* src = e;
+    SegEdge* dst = tmp.data();
+    auto key = [idbits](const SegEdge& x) { return ((unsigned long long)x.w << idbits) | x.id; };
+    std::vector<uint32_t> cnt(2048);
+    for (int sh = 0; sh < bits; sh += 11) {
+        std::fill(cnt.begin(), cnt.end(), 0u);
+        for (uint32_t i = 0; i < n; ++i) ++cnt[(key(src[i]) >> sh) & 2047u];
+        uint32_t run = 0;
+        for (uint32_t& c : cnt) {
+            const uint32_t t = c;
+            c = run;
+            run += t;
+        }
+        for (uint32_t i = 0; i < n; ++i) dst[cnt[(key(src[i]) >> sh) & 2047u]++] = src[i];
+        std::swap(src, dst);
+    }
+    if (src != e) std::copy(src, src + n, e);
+}
+
 int seg_minsize_dense(const SegEdge* e, uint32_t n, uint32_t nl, const uint32_t* lsize, const uint32_t* lroot, uint32_t ms,
                       uint32_t* out, std::vector<uint32_t>& par, std::vector<uint32_t>& size) {
     par.resize(nl);
@@ -769,7 +800,16 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         temp[i] = g.stemp.p;
         tbytes[i] = g.stemp_bytes;
     }
-    HIPC(seg_launch_sort(st, sp, temp, tbytes));
+    // the pair dedupe by hashing (default): no sort of the ~260k candidates; SM_SEG_SORTDEDUP=1 sorts them
+    uint32_t hcap = 0;
+    if (!nodedup && !getenv("SM_SEG_SORTDEDUP")) {
+        uint32_t nmax = 0;
+        for (int i = 0; i < vs.n; ++i) nmax = std::max(nmax, sp.v[i].nmin);
+        hcap = 1024;
+        while (hcap < 2 * nmax) hcap <<= 1;
+        if ((size_t)hcap > E) hcap = 0;  // (the table lives in the E-entry key buffers)
+    }
+    if (!hcap) HIPC(seg_launch_sort(st, sp, temp, tbytes));
     if (nodedup) {
         for (int i = 0; i < vs.n; ++i) {
             SegGpu& g = ctx->sg[vs.v[i]];
@@ -777,7 +817,10 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
                 HIPC(hipMemcpyAsync(g.h_min.data(), g.msorted.p, sp.v[i].nmin * sizeof(SegMin), hipMemcpyDeviceToHost, st));
         }
     } else {  // the first candidate of each root pair, dense root ids: their counts, then the lists
-        HIPC(seg_launch_dedupe(st, sp, temp, tbytes));
+        if (hcap)
+            HIPC(seg_launch_dedupe_hash(st, sp, temp, tbytes, hcap));
+        else
+            HIPC(seg_launch_dedupe(st, sp, temp, tbytes));
         for (int i = 0; i < vs.n; ++i)
             HIPC(hipMemcpyAsync(ctx->sg[vs.v[i]].h_cnt.data() + SM_SEG_C_UNIQ, P<uint32_t>(ctx->sg[vs.v[i]].cnt) + SM_SEG_C_UNIQ,
                                 8, hipMemcpyDeviceToHost, st));
@@ -800,8 +843,9 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
     const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
     int nk[2] = {0, 0};
     {  // the views' merges in parallel
-        auto merge = [ctx, ms, N, nodedup](int v) {
+        auto merge = [ctx, ms, N, nodedup, hcap](int v) {
             SegGpu& g = ctx->sg[v];
+            if (hcap) seg_sort_dense(g.h_dense.data(), g.h_cnt[SM_SEG_C_UNIQ], g.h_dsort);  // hashed: unordered
             if (!nodedup)
                 return seg_minsize_dense(g.h_dense.data(), g.h_cnt[SM_SEG_C_UNIQ], g.h_cnt[SM_SEG_C_LOCAL], g.h_lsize.data(),
                                          g.h_lroot.data(), ms, g.h_hooks.data(), g.mpar, g.msize);

@@ -49,7 +49,7 @@ struct SegMin {
 // a min-size candidate that is the first (in (w, id) order) of its pair of sweep roots, with the roots
 // as dense local ids (lsize / lroot give their sizes and pixels)
 struct SegEdge {
-    uint32_t la, lb, id;
+    uint32_t la, lb, id, w;
 };
 
 struct SegView {
@@ -113,5 +113,10 @@ size_t seg_sort_temp_bytes(uint32_t n);
 hipError_t seg_launch_sort(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes);
 // after seg_launch_sort: the first candidate of each root pair, dense root ids; counts at SM_SEG_C_UNIQ / _LOCAL
 hipError_t seg_launch_dedupe(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes);
+// the same without sorting (SM_SEG_SORTDEDUP=1 keeps the sorts): each root pair's minimum (w, id) key by
+// atomicMin in a hash table over the pair keys (cap slots, a power of two >= 2 nmin, in mkey[0] / mkey[1]);
+// dense is then unordered (the host sorts its kept candidates); needs 2 nmin <= cap <= E
+hipError_t seg_launch_dedupe_hash(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes,
+                                  uint32_t cap);
 hipError_t seg_launch_apply(hipStream_t st, const SegPair& p);
 hipError_t seg_launch_trees(hipStream_t st, const SegPair& p);

@@ -1011,8 +1011,61 @@ __global__ void __launch_bounds__(256) k_seg_dense(SegPair sp) {
     if (i >= v.nmin || !v.keep[i]) return;
     const SegMin m = v.msorted[i];
     const uint32_t la = v.lid[m.ra], lb = v.lid[m.rb];
-    v.dense[v.kpos[i]] = SegEdge{la, lb, m.id};
+    v.dense[v.kpos[i]] = SegEdge{la, lb, m.id, m.w};
     v.lsize[la] = m.sa;  // (every candidate of a root writes the same values)
+    v.lroot[la] = m.ra;
+    v.lsize[lb] = m.sb;
+    v.lroot[lb] = m.rb;
+}
+
+// Pair dedupe by hashing (seg_launch_dedupe_hash): the pair key lo * N + hi of each candidate into an
+// open-addressing table (keys in mkey[0], each pair's minimum (w, id) key in mkey[1]), the slot kept in mval[0]
+__global__ void __launch_bounds__(256) k_seg_hins(SegPair sp, uint32_t cap) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= v.nmin) return;
+    const SegMin m = v.mlist[i];
+    const unsigned long long N = (unsigned long long)v.W * (unsigned long long)v.H;
+    const uint32_t lo = m.ra < m.rb ? m.ra : m.rb, hi = m.ra < m.rb ? m.rb : m.ra;
+    const unsigned long long pk = (unsigned long long)lo * N + hi;
+    uint32_t h = (uint32_t)((pk * 0x9E3779B97F4A7C15ull) >> 32) & (cap - 1u);
+    for (uint32_t probe = 0; probe < cap; ++probe) {  // load <= 1/2: a few probes
+        const unsigned long long prev = atomicCAS(v.mkey[0] + h, ~0ull, pk);
+        if (prev == ~0ull || prev == pk) break;
+        h = (h + 1u) & (cap - 1u);
+    }
+    atomicMin(v.mkey[1] + h, ((unsigned long long)m.w << 32) | m.id);
+    v.mval[0][i] = h;
+}
+
+// a candidate is kept iff it holds its pair's minimum key; its roots get dense ids (lmark)
+__global__ void __launch_bounds__(256) k_seg_hkeep(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) v.keep[v.nmin] = 0;
+    if (i >= v.nmin) return;
+    const SegMin m = v.mlist[i];
+    const bool k = v.mkey[1][v.mval[0][i]] == (((unsigned long long)m.w << 32) | m.id);
+    v.keep[i] = k ? 1u : 0u;
+    if (k) {
+        v.lmark[m.ra] = 1;
+        v.lmark[m.rb] = 1;
+    }
+}
+
+// k_seg_dense over the unsorted candidates
+__global__ void __launch_bounds__(256) k_seg_hdense(SegPair sp) {
+    const SegView& v = sp.v[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        v.cnt[SM_SEG_C_UNIQ] = v.kpos[v.nmin];
+        v.cnt[SM_SEG_C_LOCAL] = v.lid[(size_t)v.W * v.H];
+    }
+    if (i >= v.nmin || !v.keep[i]) return;
+    const SegMin m = v.mlist[i];
+    const uint32_t la = v.lid[m.ra], lb = v.lid[m.rb];
+    v.dense[v.kpos[i]] = SegEdge{la, lb, m.id, m.w};
+    v.lsize[la] = m.sa;
     v.lroot[la] = m.ra;
     v.lsize[lb] = m.sb;
     v.lroot[lb] = m.rb;
@@ -1217,6 +1270,33 @@ hipError_t seg_launch_dedupe(hipStream_t st, const SegPair& p, void* const* temp
         if ((e = hipcub::DeviceScan::ExclusiveSum(temp[i], tb, v.lmark, v.lid, (int)N + 1, st)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_seg_dense, dim3(nb, p.nv), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t seg_launch_dedupe_hash(hipStream_t st, const SegPair& p, void* const* temp, const size_t* temp_bytes,
+                                  uint32_t cap) {
+    const size_t N = (size_t)p.v[0].W * p.v[0].H;
+    uint32_t nmax = 0;
+    for (int i = 0; i < p.nv; ++i) {
+        const SegView& v = p.v[i];
+        nmax = v.nmin > nmax ? v.nmin : nmax;
+        hipError_t e;
+        if ((e = hipMemsetAsync(v.mkey[0], 0xFF, (size_t)cap * 8, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(v.mkey[1], 0xFF, (size_t)cap * 8, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(v.lmark, 0, (N + 1) * 4, st)) != hipSuccess) return e;
+    }
+    const unsigned nb = blocks_of(nmax ? nmax : 1, 256);
+    hipLaunchKernelGGL(k_seg_hins, dim3(nb, p.nv), dim3(256), 0, st, p, cap);
+    hipLaunchKernelGGL(k_seg_hkeep, dim3(nb, p.nv), dim3(256), 0, st, p);
+    for (int i = 0; i < p.nv; ++i) {
+        const SegView& v = p.v[i];
+        size_t tb = temp_bytes[i];
+        hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp[i], tb, v.keep, v.kpos, (int)v.nmin + 1, st);
+        if (e != hipSuccess) return e;
+        tb = temp_bytes[i];
+        if ((e = hipcub::DeviceScan::ExclusiveSum(temp[i], tb, v.lmark, v.lid, (int)N + 1, st)) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_seg_hdense, dim3(nb, p.nv), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 
