@@ -359,15 +359,17 @@ __device__ int seg_wg_rounds(const SegView& v, int b, uint32_t n, uint32_t gen0,
 // sizes).  Synthetic C2: at most 2.7k candidates; the global-memory rounds took up to 120 us per bucket
 // (several dependent global round trips and barriers per round).  Returns false, having written nothing
 // global, when the roots overflow the table (then the global rounds run).
-constexpr int SEG_TAIL_MAX = 4096;
-constexpr int SEG_TAIL_RS = 8192;
+constexpr int SEG_TAIL_MAX = 4096;    // crossing candidates an LDS tail holds
+constexpr int SEG_TAIL_RS = 6144;     // its root slots
+constexpr uint32_t SEG_TAIL_MIN = 256;  // shorter lists keep the global-memory rounds (the LDS setup costs more)
 constexpr uint16_t SEG_NOSLOT = 0xFFFFu;
-__device__ __forceinline__ int seg_tslot(uint32_t* hk, uint32_t root, uint32_t* full) {
-    int h = (int)((root * 2654435761u) >> 19) & (SEG_TAIL_RS - 1);
+__device__ __forceinline__ int seg_tslot(uint32_t* hk, uint16_t* used, uint32_t* nused, uint32_t root, uint32_t* full) {
+    int h = (int)(((root * 2654435761u) >> 8) % (uint32_t)SEG_TAIL_RS);
     for (int probe = 0; probe < 256; ++probe) {
         const uint32_t prev = atomicCAS(hk + h, SEG_EMPTY, root);
+        if (prev == SEG_EMPTY) used[atomicAdd(nused, 1u)] = (uint16_t)h;  // (at most RS inserts)
         if (prev == SEG_EMPTY || prev == root) return h;
-        h = (h + 1) & (SEG_TAIL_RS - 1);
+        h = h + 1 == SEG_TAIL_RS ? 0 : h + 1;
     }
     atomicAdd(full, 1u);
     return 0;
@@ -376,32 +378,41 @@ __device__ bool seg_tail_lds(const SegView& v, int b, uint32_t n) {
     __shared__ uint32_t s_id[SEG_TAIL_MAX];
     __shared__ uint16_t s_a[SEG_TAIL_MAX], s_b[SEG_TAIL_MAX];
     __shared__ uint32_t s_hk[SEG_TAIL_RS];
-    __shared__ uint16_t s_par[SEG_TAIL_RS];
+    __shared__ uint16_t s_par[SEG_TAIL_RS], s_used[SEG_TAIL_RS];
     __shared__ unsigned long long s_best[SEG_TAIL_RS];
-    __shared__ uint32_t s_full, s_cross;
+    __shared__ uint32_t s_full, s_cross, s_m, s_nused;
     const int tid = (int)threadIdx.x;
     for (int i = tid; i < SEG_TAIL_RS; i += 1024) {
         s_hk[i] = SEG_EMPTY;
         s_par[i] = (uint16_t)i;
         s_best[i] = ~0ull;
     }
-    if (tid == 0) s_full = 0;
+    if (tid == 0) {
+        s_full = 0;
+        s_m = 0;
+        s_nused = 0;
+    }
     __syncthreads();
+    // the list's edges that still cross two components (after the last global hooks), roots hashed
     for (uint32_t k = tid; k < n; k += 1024) {
         const uint4 e = v.list[b][k];
         const uint32_t ra = seg_find(v.par, e.y), rb = seg_find(v.par, e.z);
-        s_id[k] = e.x;
-        s_a[k] = ra == rb ? SEG_NOSLOT : (uint16_t)seg_tslot(s_hk, ra, &s_full);
-        s_b[k] = ra == rb ? SEG_NOSLOT : (uint16_t)seg_tslot(s_hk, rb, &s_full);
+        if (ra == rb) continue;
+        const uint32_t pos = atomicAdd(&s_m, 1u);
+        if (pos >= (uint32_t)SEG_TAIL_MAX) continue;  // (overflow: the global rounds run)
+        s_id[pos] = e.x;
+        s_a[pos] = (uint16_t)seg_tslot(s_hk, s_used, &s_nused, ra, &s_full);
+        s_b[pos] = (uint16_t)seg_tslot(s_hk, s_used, &s_nused, rb, &s_full);
     }
     __syncthreads();
-    if (s_full) return false;  // block-uniform
+    const uint32_t m = s_m;
+    if (s_full || m > (uint32_t)SEG_TAIL_MAX) return false;  // block-uniform, nothing global written
     for (uint32_t round = 0;; ++round) {
         if (tid == 0) s_cross = 0;
         __syncthreads();
         // each root's minimum crossing key; the edge's slots become its current roots (s_par is only read
         // in this phase), which the hook phase then uses as they are -- finds there would race the hooks
-        for (uint32_t k = tid; k < n; k += 1024) {
+        for (uint32_t k = tid; k < m; k += 1024) {
             if (s_a[k] == SEG_NOSLOT) continue;
             int a = s_a[k], c = s_b[k];
             while (s_par[a] != a) a = s_par[a];
@@ -419,7 +430,7 @@ __device__ bool seg_tail_lds(const SegView& v, int b, uint32_t n) {
         }
         __syncthreads();
         if (!s_cross) break;  // block-uniform
-        for (uint32_t k = tid; k < n; k += 1024) {  // hooks along those keys (mutual pairs: larger slot onto smaller)
+        for (uint32_t k = tid; k < m; k += 1024) {  // hooks along those keys (mutual pairs: larger slot onto smaller)
             if (s_a[k] == SEG_NOSLOT) continue;
             const int a = s_a[k], c = s_b[k];  // roots at the selection
             const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - round) << 32) | s_id[k];
@@ -441,18 +452,22 @@ __device__ bool seg_tail_lds(const SegView& v, int b, uint32_t n) {
         }
     }
     // joined roots onto their final roots (global), and into `hooked` for k_seg_sizes
-    for (int i0 = 0; i0 < SEG_TAIL_RS; i0 += 1024) {
-        const int i = i0 + tid;
-        const uint32_t r = s_hk[i];
-        int f = i;
-        if (r != SEG_EMPTY)
+    const uint32_t nu = s_nused;
+    for (uint32_t u0 = 0; u0 < nu; u0 += 1024) {
+        const uint32_t u = u0 + tid;
+        int i = 0, f = 0;
+        if (u < nu) {
+            i = s_used[u];
+            f = i;
             while (s_par[f] != f) f = s_par[f];
-        const bool joined = r != SEG_EMPTY && f != i;
+        }
+        const bool joined = u < nu && f != i;
         uint32_t* const ctr[1] = {v.cnt + SM_SEG_C_HOOK};
         const bool pred[1] = {joined};
         uint32_t slot[1];
         block_append<1>(ctr, pred, slot);
         if (joined) {
+            const uint32_t r = s_hk[i];
             v.par[r] = s_hk[f];
             v.hooked[slot[0]] = r;
         }
@@ -461,11 +476,11 @@ __device__ bool seg_tail_lds(const SegView& v, int b, uint32_t n) {
 }
 
 // lds: try seg_tail_lds first (SM_SEG_TAIL_GLOBAL=1: always the global-memory rounds)
-__global__ void __launch_bounds__(1024) k_seg_tail(SegPair sp, int lin, uint32_t gen0, int lds) {
+__global__ void __launch_bounds__(1024) k_seg_tail(SegPair sp, int lin, uint32_t gen0, int lds, uint32_t tmin) {
     const SegView& v = sp.v[blockIdx.x];
     __shared__ uint32_t s_out;
     const uint32_t n = v.cnt[SM_SEG_C_LIST + lin];
-    if (lds && n <= (uint32_t)SEG_TAIL_MAX && seg_tail_lds(v, lin & 1, n)) return;
+    if (lds && n >= tmin && seg_tail_lds(v, lin & 1, n)) return;
     seg_wg_rounds(v, lin & 1, n, gen0, &s_out, false);
 }
 
@@ -1161,7 +1176,8 @@ hipError_t seg_launch_round(hipStream_t st, const SegPair& p, uint32_t m, int li
 
 hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t gen0) {
     const int lds = getenv("SM_SEG_TAIL_GLOBAL") ? 0 : 1;
-    hipLaunchKernelGGL(k_seg_tail, dim3(p.nv), dim3(1024), 0, st, p, lin, gen0, lds);
+    const uint32_t tmin = getenv("SM_SEG_TAIL_MIN") ? (uint32_t)atoi(getenv("SM_SEG_TAIL_MIN")) : SEG_TAIL_MIN;
+    hipLaunchKernelGGL(k_seg_tail, dim3(p.nv), dim3(1024), 0, st, p, lin, gen0, lds, tmin);
     return hipGetLastError();
 }
 
