@@ -223,6 +223,7 @@ __global__ void __launch_bounds__(256) k_seg_best(SegPair sp, int lin, int lout,
     const SegView& v = sp.v[blockIdx.y];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t n = v.cnt[SM_SEG_C_LIST + lin];
+    if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the bucket, the list is shorter
     bool cross = false;
     uint4 e = make_uint4(0, 0, 0, 0);
     if (i < n) {
@@ -283,6 +284,7 @@ __global__ void __launch_bounds__(256) k_seg_hook(SegPair sp, int lout, uint32_t
     const SegView& v = sp.v[blockIdx.y];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const uint32_t n = v.cnt[SM_SEG_C_LIST + lout];
+    if (blockIdx.x * 256 >= n) return;  // block-uniform (as k_seg_best)
     uint4 e = make_uint4(0, 0, 0, 0);
     if (i < n) e = v.list[lout & 1][i];
     seg_hook_edge(v, e, gen, i < n);
@@ -1117,6 +1119,7 @@ __global__ void __launch_bounds__(256) k_seg_first(SegPair sp) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     const uint32_t N = (uint32_t)v.W * (uint32_t)v.H;
     const uint32_t r = p < N ? seg_find(v.par, p) : 0xFFFFFFFFu;
+    if (p < N && v.par[p] != r) v.par[p] = r;  // flattened: k_seg_virtual's finds take one step
     // one atomic per run of equal roots in the wave (rows are mostly long runs of one tree), and none
     // where the tree's first pixel is already known to be smaller
     const uint32_t rprev = __shfl_up(r, 1);
