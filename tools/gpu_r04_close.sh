@@ -6,6 +6,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 case "$1" in
 final)
   bash tools/gpu_final.sh || exit 2
+  timeout -k 10 300 python bench.py --segment-c 5000 --min-size 200 --no-cpu --no-pms > gpurun_out/final/bench_segment.log 2>&1 || exit 5
+  python3 -c "import json;d=json.loads(open('gpurun_out/final/bench_segment.log').read().strip().splitlines()[-1]);print('segment', round(d['ms_per_step'],3), 'latency', round(d['latency_ms_per_frame'],2))"
   ;;
 prof)
   bash tools/gpu_prof_round.sh r04 || exit 3
