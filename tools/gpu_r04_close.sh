@@ -16,6 +16,10 @@ prof)
   f=$(find $O/pmsraw -name '*kernel_stats.csv' | head -1); cp "$f" $O/pms100_kernel_stats.csv
   rm -rf $O/pmsraw
   tail -1 $O/pms100_prof.log | cut -c1-600
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/segraw -o run --output-format csv -- python3 bench.py --segment-c 5000 --min-size 200 --inflight 1 --steps 4 --warmup 2 --no-cpu --no-pms --no-host-io > $O/seg1_prof.log 2>&1 || exit 6
+  f=$(find $O/segraw -name '*kernel_stats.csv' | head -1); cp "$f" $O/seg1_kernel_stats.csv
+  rm -rf $O/segraw
+  echo seg traced
   ;;
 *) echo "usage: $0 final|prof"; exit 1 ;;
 esac
