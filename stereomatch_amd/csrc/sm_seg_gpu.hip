@@ -718,18 +718,23 @@ __global__ void __launch_bounds__(1024) k_seg_run(SegPair sp, int w0, int w1, fl
             for (uint32_t q0 = lo; q0 < hi; q0 += 64) {
                 const uint32_t q = q0 + lane;
                 const uint32_t k = q < hi ? s_ord[q] : 0u;
-                unsigned long long m = __ballot(q < hi && s_fl[k] == 1);
+                const bool cnd = q < hi && s_fl[k] == 1;
+                // the candidate's id and its ends' slots, loaded by its own lane (lane 0 then reads them by
+                // readlane instead of one LDS round trip after another)
+                const uint32_t kid = cnd ? s_aid[k] : 0u;
+                const int ka = cnd ? (int)s_ea[k] : 0, kb = cnd ? (int)s_eb[k] : 0;
+                unsigned long long m = __ballot(cnd);
                 while (m) {  // uniform: the candidates of this chunk in id order
                     const int j = __ffsll((long long)m) - 1;
                     m &= m - 1ull;
-                    const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)k, j);
+                    const int a0 = __builtin_amdgcn_readlane(ka, j), b0 = __builtin_amdgcn_readlane(kb, j);
+                    const uint32_t id = (uint32_t)__builtin_amdgcn_readlane((int)kid, j);
                     if (lane == 0) {
-                        const int a = seg_lfind(s_par, s_ea[kk]), b = seg_lfind(s_par, s_eb[kk]);
+                        const int a = seg_lfind(s_par, a0), b = seg_lfind(s_par, b0);
                         if (a != b) {
                             s_par[b] = (uint16_t)a;
                             s_sz[a] += s_sz[b];
                             s_wl[a] = (uint16_t)w;
-                            const uint32_t id = s_aid[kk];
                             if (id & 1u)
                                 v.mD[id >> 1] = 1;
                             else
