@@ -1,7 +1,7 @@
-# round 4: the last build's smoke + full -m gpu suite -> gpurun_out/r04ai
+# round 4: the final build's smoke + full -m gpu suite -> gpurun_out/r04ak
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r04ai
+O=gpurun_out/r04ak
 mkdir -p $O
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 tail -1 $O/smoke.log
