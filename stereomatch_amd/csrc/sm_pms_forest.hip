@@ -211,25 +211,19 @@ __device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* 
     int n = b - a, i = a + lane;
     bool val = lane < n;
     int p = 0, pp = -1, tr = 0;
-    int4 n4 = make_int4(-1, -1, -1, -1);
-    uint2 w4 = make_uint2(0, 0);
     if (val) {
         p = v.gpix[i];
         const int gp = v.gpar[i];
         pp = gp >= 0 ? v.gpix[gp] : -1;
         tr = v.gtree[i];
-        n4 = v.nbr[p];
-        w4 = v.nbw[p];
     }
-    // Each level: the children (from the adjacency loaded one level ahead), the next level's nodes handed
-    // over in LDS, the next level's adjacency loads issued, and only then this level's global stores --
-    // gfx9 counts loads and stores in one vmcnt, so a load issued after the stores waited for them too
-    // (two memory round trips per level instead of one, over the deep trees' thousands of narrow levels)
     while (n > 0 && n <= 64) {
         if (lane == 0) v.glev[d] = a;
         int q[4] = {-1, -1, -1, -1}, c = 0;
         uint32_t wv[4] = {0, 0, 0, 0};
         if (val) {
+            const int4 n4 = v.nbr[p];
+            const uint2 w4 = v.nbw[p];
             const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
             const uint32_t ww[4] = {w4.x & 0xFFFFu, w4.x >> 16, w4.y & 0xFFFFu, w4.y >> 16};
             pf_children(nn, ww, pp, q, wv, c);
@@ -241,11 +235,21 @@ __device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* 
             if (lane >= o) incl += u;
         }
         const int total = __shfl(incl, 63), pos = incl - c;
-        if (val) {  // the next level's nodes (pixel, parent pixel, tree) for its lanes
+        if (val) {
+            v.gfc[i] = b + pos;
+            v.gnc[i] = (uint8_t)c;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (k >= c) break;
-                if (b + pos + k >= v.N) break;  // (a cycle: flagged with the stores below)
+                const int j = b + pos + k;
+                if (j >= v.N) {  // only masks with a cycle get here (as in the workgroup levels)
+                    v.tot[7] = 1;
+                    break;
+                }
+                v.gpix[j] = q[k];
+                v.gpar[j] = i;
+                v.gtree[j] = tr;
+                v.gw[j] = (uint16_t)wv[k];
                 if (pos + k < 64) {
                     s_q[pos + k] = q[k];
                     s_pp[pos + k] = p;
@@ -253,9 +257,6 @@ __device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* 
                 }
             }
         }
-        // this level's values for its stores
-        const bool val_s = val;
-        const int i_s = i, base_s = b + pos, tr_s = tr;
         const int nb = b + total < v.N ? b + total : v.N;
         a = b;
         b = nb;
@@ -272,27 +273,6 @@ __device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* 
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);  // and these reads before the next level's writes
         __builtin_amdgcn_wave_barrier();
-        if (n <= 64 && val) {  // the next level's adjacency, ahead of this level's stores
-            n4 = v.nbr[p];
-            w4 = v.nbw[p];
-        }
-        if (val_s) {
-            v.gfc[i_s] = base_s;
-            v.gnc[i_s] = (uint8_t)c;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (k >= c) break;
-                const int j = base_s + k;
-                if (j >= v.N) {  // only masks with a cycle get here (as in the workgroup levels)
-                    v.tot[7] = 1;
-                    break;
-                }
-                v.gpix[j] = q[k];
-                v.gpar[j] = i_s;
-                v.gtree[j] = tr_s;
-                v.gw[j] = (uint16_t)wv[k];
-            }
-        }
     }
     if (lane == 0) {
         s_state[0] = a;
