@@ -1134,7 +1134,9 @@ __device__ __forceinline__ double pc_sel(const double (&a)[4], int i) {
     return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
 }
 __device__ __forceinline__ int pc_sel(const int (&a)[4], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3]; }
-constexpr int PC_NSU = 4;      // up ring slots (2 KB per node): 67 KB, two workgroups per CU
+// up ring slots (2 KB per node): 6 = ~100 KB, one workgroup per CU.  4 (67 KB, two per CU) was faster while
+// the loaders' rows sat in scratch memory; without it 6 is: 100-call C2 frame 487-491 -> 473 ms (profiles/r04/nsu/)
+constexpr int PC_NSU = 6;
 constexpr int PC_NSU_MAX = 8;  // SM_PMS_CHAIN_NSU up to this: 133 KB, one workgroup per CU
 constexpr int PC_NSD = 14;     // down ring slots (0.5 KB per node): 58 KB, two workgroups per CU
 constexpr int PC_LW = 7;       // loader waves (+ the chain wave: 512 threads)
