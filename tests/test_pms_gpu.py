@@ -63,7 +63,7 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
 
 
 @pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "chainstream",
-                                  "refalways", "ser1024", "ser512"])
+                                  "refalways", "ser1024", "ser512", "nsu4", "nsu8"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
@@ -73,7 +73,8 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     SM_PMS_WAVE_WALK=1 walks every (path, chunk) item with a wave of its own instead of the planned
     lane-group walks (k_pms_plan / k_pms_walk_plan); SM_PMS_CHAIN_MIN=48 sends paths of >= 48 rows to the
     chain kernel; SM_PMS_CHAIN_STREAM=1 runs the chain launches on a side stream beside the walkers;
-    SM_PMS_SER_NT=1024 / 512 runs the serial kernel with that many threads (default 768)."""
+    SM_PMS_SER_NT=1024 / 512 runs the serial kernel with that many threads (default 768);
+    SM_PMS_CHAIN_NSU=4 / 8 gives the up chain that many ring slots (default 6)."""
     monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
     monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
     if mode == "nodedup":
@@ -100,6 +101,11 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         monkeypatch.setenv("SM_PMS_REF_ALWAYS", "1")
     else:
         monkeypatch.delenv("SM_PMS_REF_ALWAYS", raising=False)
+    if mode in ("nsu4", "nsu8"):
+        monkeypatch.setenv("SM_PMS_CHAIN_NSU", mode[3:])
+        monkeypatch.setenv("SM_PMS_CHAIN_MIN", "48")  # (more chain items at this size)
+    else:
+        monkeypatch.delenv("SM_PMS_CHAIN_NSU", raising=False)
     if mode in ("ser1024", "ser512"):
         monkeypatch.setenv("SM_PMS_SER_NT", mode[3:])
     else:
