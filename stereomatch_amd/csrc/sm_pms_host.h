@@ -25,7 +25,7 @@ struct PmsRow {
 // k_pms_chain; env SM_PMS_CHAIN_MIN moves the threshold, down to SM_PMS_CHAIN_LEN, the floor the schedule's
 // chain-item counts rt_long are kept for)
 #define SM_PMS_CHAIN_LEN 48
-#define SM_PMS_CHAIN_DEFAULT 96
+#define SM_PMS_CHAIN_DEFAULT 64  // (96 before the chain loaders lost their scratch memory: 100-call frame 470 -> 465 ms)
 
 // A heavy path: rows [row, row + len), head first.
 struct PmsPath {

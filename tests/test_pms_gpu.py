@@ -85,7 +85,7 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         monkeypatch.setenv("SM_PMS_WAVE_WALK", "1")
     else:
         monkeypatch.delenv("SM_PMS_WAVE_WALK", raising=False)
-    if mode == "nochain":  # paths of >= 96 rows on the wave walker instead of k_pms_chain
+    if mode == "nochain":  # paths of >= 64 rows on the wave walker instead of k_pms_chain
         monkeypatch.setenv("SM_PMS_NO_CHAIN", "1")
     else:
         monkeypatch.delenv("SM_PMS_NO_CHAIN", raising=False)
