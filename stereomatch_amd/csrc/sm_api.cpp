@@ -490,8 +490,9 @@ bool seg_nodedup() { return getenv("SM_SEG_NODEDUP") != nullptr; }
 bool seg_split() { return getenv("SM_SEG_NOSPLIT") == nullptr; }
 
 // Boruvka rounds launched over the whole GPU before a bucket's single-workgroup tail, for buckets of
-// more than SM_SEG_SMALL edges (env SM_SEG_GLOBAL_ROUNDS, default 2)
-int seg_global_rounds() { return getenv("SM_SEG_GLOBAL_ROUNDS") ? atoi(getenv("SM_SEG_GLOBAL_ROUNDS")) : 2; }
+// more than SM_SEG_SMALL edges (env SM_SEG_GLOBAL_ROUNDS, default 3: the LDS tail then gets the ~2.7k
+// still-crossing candidates at most; latency 9.96 -> 9.7 ms, profiles/r04/seg/r04ao/)
+int seg_global_rounds() { return getenv("SM_SEG_GLOBAL_ROUNDS") ? atoi(getenv("SM_SEG_GLOBAL_ROUNDS")) : 3; }
 
 // buckets of at most this many edges run in one workgroup, consecutive ones in one launch (k_seg_small;
 // env SM_SEG_SMALL, default 16384)
