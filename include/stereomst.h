@@ -234,6 +234,9 @@ sm_status sm_set_kernel_timing(sm_ctx* ctx, unsigned family_mask);
  * The plane labels (a, b, c) of every pixel after the last SM_AGG_PMS call, [H*W][3] float per view
  * (abc_map, Stereo3DMST.cpp:814-815); either pointer may be NULL. */
 sm_status sm_download_labels(sm_ctx* ctx, float* left_abc, float* right_abc);
+/* The extent (W, H) of the labels sm_download_labels copies: the last SM_AGG_PMS call's image size,
+ * which a later upload does not change.  Size the label buffers from this (W*H*3 floats each). */
+sm_status sm_labels_extent(sm_ctx* ctx, int* W, int* H);
 /* Timings and counters of the last SM_AGG_PMS call.  The first MST_PMS call of a view runs its trees
  * one after the other (serial); later calls run every tree at once from guessed dice offsets and the
  * labels at the start of the call, validate, and redo from the first tree whose inputs differed
@@ -263,6 +266,10 @@ typedef struct {
     double prep_forest_ms;  /* the reference-numbered forests and walk schedules, both views */
 } sm_pms_stats;
 sm_status sm_get_pms_stats(sm_ctx* ctx, sm_pms_stats* out);
+/* The same, writing at most out_bytes bytes (pass sizeof(sm_pms_stats) of the header the caller was
+ * compiled against): a caller built against an older, shorter struct gets its prefix only.  Fields
+ * are only ever appended. */
+sm_status sm_get_pms_stats_n(sm_ctx* ctx, sm_pms_stats* out, size_t out_bytes);
 
 /* Multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------- */
 #define SM_UNIQUE_ID_BYTES 128

@@ -103,6 +103,8 @@ def lib():
         "sm_set_kernel_timing": ([vp, ctypes.c_uint], ci),
         "sm_download_labels": ([vp, vp, vp], ci),
         "sm_get_pms_stats": ([vp, ctypes.POINTER(SmPmsStats)], ci),
+        "sm_get_pms_stats_n": ([vp, ctypes.POINTER(SmPmsStats), ctypes.c_size_t], ci),
+        "sm_labels_extent": ([vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ci),
         "sm_pms_forest_bfs": ([ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp], ci),
         "sm_pms_forest_digest": ([ci, ci, vp, vp, vp, ci, ci, vp, vp, vp], ci),
         "sm_pms_tree_graph": ([ci, ci, vp, vp, vp, vp, vp, ci], ci),
@@ -195,8 +197,6 @@ class Context:
                        minc=np.empty((H, W), np.float64)) for v in ("left", "right")}
         self._views = p.views or 3
         self.shape = (H, W)
-        if p.aggregator == SM_AGG_PMS:
-            self._pms_shape = (H, W)
         self._check(lib().sm_match(self.h, ptr(left), ptr(right), W, H, W * 3, D, ctypes.byref(p),
                                    ptr(out["left"]["disp"]), ptr(out["right"]["disp"]), ptr(out["left"]["idx"]),
                                    ptr(out["right"]["idx"]), ptr(out["left"]["minc"]), ptr(out["right"]["minc"])))
@@ -276,14 +276,18 @@ class Context:
     # -- MST_PMS (SM_AGG_PMS) -------------------------------------------------------------
     def labels(self):
         """Plane labels (a, b, c) of every pixel after the last SM_AGG_PMS call: {view: [H*W, 3] float32}."""
-        H, W = getattr(self, "_pms_shape", self.shape)  # the size of the SM_AGG_PMS call
+        # sized from the library's own record of the SM_AGG_PMS call (not Python-side bookkeeping: a
+        # match_begin / match_async call or a later upload must not change what this allocates)
+        w, h = ctypes.c_int(0), ctypes.c_int(0)
+        self._check(lib().sm_labels_extent(self.h, ctypes.byref(w), ctypes.byref(h)))
+        H, W = h.value, w.value
         out = {v: np.empty((H * W, 3), np.float32) for v in ("left", "right")}
         self._check(lib().sm_download_labels(self.h, ptr(out["left"]), ptr(out["right"])))
         return out
 
     def pms_stats(self):
         s = SmPmsStats()
-        self._check(lib().sm_get_pms_stats(self.h, ctypes.byref(s)))
+        self._check(lib().sm_get_pms_stats_n(self.h, ctypes.byref(s), ctypes.sizeof(s)))
         d = {k: getattr(s, k) for k, _ in SmPmsStats._fields_}
         d["ntrees"] = list(s.ntrees)
         d["first_ms_view"] = list(s.first_ms_view)

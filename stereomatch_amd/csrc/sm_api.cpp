@@ -192,6 +192,7 @@ struct sm_ctx {
     // fully enqueued by begin)
     int pending = 0;
     int pend_D = 0;
+    bool exp_layout_ok = false;  // SM_EXP_FILTER_ONLY (timing experiment): a layout of these images exists
     sm_params pend_p{};
     // tree-filter launch timing: timed launch k runs between events fev[fam_ev[k]] on its stream
     std::vector<hipEvent_t> fev;
@@ -1812,7 +1813,7 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.cnt = P<int32_t>(S.cnt);
     d.flag = P<int32_t>(S.flag);
     d.result = P<int32_t>(S.result);
-    d.err = ctx->d_err;
+    d.err = ctx->d_err + 1 + v;  // a word per view: the views' calls run concurrently (h_err[1 + v])
     d.prof = nullptr;
     d.evals = nullptr;
     if (getenv("SM_PMS_PROF")) {  // diagnostics: serial-kernel segment times, printed per call
@@ -2232,6 +2233,16 @@ sm_status pms_forest_check(sm_ctx* ctx, int v, hipStream_t st, const PmsForest& 
 // SM_AGG_PMS: Stereo3DMST's stereo3dmst() after its cost volume (Stereo3DMST.cpp:805-904) -- segment
 // forests, random plane labels, pms_iters MST_PMS calls on the left view, then on the right, plane
 // disparities.  Runs to completion (host synchronisations between speculative passes).
+// Joins a thread on every way out of a scope: destroying a joinable std::thread calls std::terminate,
+// so an early return (HIPC, CHECK) or an exception between its start and its join would kill the host
+// process instead of returning an error.
+struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+        if (t.joinable()) t.join();
+    }
+};
+
 sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     const int W = ctx->W, H = ctx->H;
     const size_t N = (size_t)W * H;
@@ -2245,6 +2256,7 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     // forests: it runs on a thread of its own from the start (the calls' values are drawn after step 2)
     GlibcRandom grnd;
     std::thread skip([&grnd, N] { grnd.seed_skip(1u, (long)(6 * N)); });
+    Joiner jskip{skip};  // joined on every way out (early returns, exceptions)
     // 1. the forests: the reference's order-dependent segmentation (c = +inf: the MST)
     // the schedule forests are built on the GPU (sm_pms_forest.hip) from the device masks;
     // SM_PMS_HOST_FOREST=1: on host threads (pms_build_forest, A/B); SM_PMS_FOREST_CHECK=1 (tests): both,
@@ -2305,16 +2317,18 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
         const double tf = now_ms();
         HIPC(hipEventRecord(ctx->ev_pms, ctx->st));
         HIPC(hipStreamWaitEvent(ctx->st_pms, ctx->ev_pms, 0));  // the segmentation's masks
-        std::thread other([&] {
+        auto guarded = [&](int v) {
             try {
-                build(1);
+                build(v);
             } catch (const std::bad_alloc&) {
-                fs[1] = SM_ERR_OOM;
+                fs[v] = SM_ERR_OOM;
             } catch (...) {
-                fs[1] = SM_ERR_STATE;
+                fs[v] = SM_ERR_STATE;
             }
-        });
-        build(0);
+        };
+        std::thread other([&] { guarded(1); });
+        Joiner jother{other};
+        guarded(0);
         other.join();
         st.prep_forest_ms = now_ms() - tf;
         if (fs[0] != SM_OK || fs[1] != SM_OK) {
@@ -2328,6 +2342,7 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     ctx->pms_hrnd.resize((size_t)iters * (K0 + K1) + 1);
     skip.join();
     std::thread rng([ctx, iters, K0, K1, &grnd] { grnd.draw((long)iters * (K0 + K1), ctx->pms_hrnd.data()); });
+    Joiner jrng{rng};
     if (ctx->pms_init_key[0] != W || ctx->pms_init_key[1] != H || ctx->pms_init_key[2] != D) {
         ctx->pms_init.resize(3 * N);
         sm_pms_init_labels(W, H, D, ctx->pms_init.data());
@@ -2438,9 +2453,9 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
                 HIPC(launch_pms_count(st, dc, acc + (i == 0 ? 0 : 2)));
             }
             HIPC(hipStreamSynchronize(st));
-            const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE);
-            if (e & 6u) {
-                __atomic_store_n(ctx->h_err, 0u, __ATOMIC_RELEASE);
+            const uint32_t e = __atomic_load_n(ctx->h_err + 1 + v, __ATOMIC_ACQUIRE);  // this view's word
+            if (e) {
+                __atomic_store_n(ctx->h_err + 1 + v, 0u, __ATOMIC_RELEASE);
                 return fail(ctx, SM_ERR_STATE, (e & 4u) ? "MST_PMS: dice stream exhausted (internal sizing error)"
                                                         : "MST_PMS: a propagation index fell outside its tree (the "
                                                           "reference would read outside mst_vertices_vec)");
@@ -2465,14 +2480,18 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
         rs[0] = calls(run[0], 0);
         if (rs[0] == SM_OK) rs[1] = calls(run[1], 1);
     } else {
-        std::thread other([&] {
+        auto guarded = [&](int v) {
             try {
-                rs[1] = calls(run[1], 1);
+                rs[v] = calls(run[v], v);
+            } catch (const std::bad_alloc&) {
+                rs[v] = SM_ERR_OOM;
             } catch (...) {
-                rs[1] = SM_ERR_STATE;
+                rs[v] = SM_ERR_STATE;
             }
-        });
-        rs[0] = calls(run[0], 0);
+        };
+        std::thread other([&] { guarded(1); });
+        Joiner jother{other};
+        guarded(0);
         other.join();
     }
     const double tc1 = now_ms();
@@ -2747,7 +2766,32 @@ sm_status sm_upload_cost_volumes(sm_ctx* ctx, const float* left_vol, const float
     return SM_OK;
 }
 
+static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p);
+static sm_status match_finish_impl(sm_ctx* ctx);
+
+// No C++ exception crosses the C-ABI: host allocations (std::vector, std::thread) that throw in a
+// stage become SM_ERR_OOM / SM_ERR_STATE.
 sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
+    try {
+        return match_begin_impl(ctx, D, p);
+    } catch (const std::bad_alloc&) {
+        return ctx ? fail(ctx, SM_ERR_OOM, "sm_match_begin: host allocation failed") : SM_ERR_OOM;
+    } catch (...) {
+        return ctx ? fail(ctx, SM_ERR_STATE, "sm_match_begin: host exception") : SM_ERR_STATE;
+    }
+}
+
+sm_status sm_match_finish(sm_ctx* ctx) {
+    try {
+        return match_finish_impl(ctx);
+    } catch (const std::bad_alloc&) {
+        return ctx ? fail(ctx, SM_ERR_OOM, "sm_match_finish: host allocation failed") : SM_ERR_OOM;
+    } catch (...) {
+        return ctx ? fail(ctx, SM_ERR_STATE, "sm_match_finish: host exception") : SM_ERR_STATE;
+    }
+}
+
+static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
     if (!ctx) return SM_ERR_ARG;
     if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_match_begin: the previous call was not finished (sm_match_finish)");
     if (ctx->seg_worker.joinable()) ctx->seg_worker.join();  // a worker left by a failed finish
@@ -2777,6 +2821,16 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
         HIPC(hipStreamWaitEvent(ctx->st_tree, ctx->ev_enq, 0));
         ts.main = ctx->st;
         ctx->st = ctx->st_tree;
+    }
+    // timing experiment only (tools): SM_EXP_FILTER_ONLY=1 re-filters the previous frame's tree (same
+    // images) without re-running prep / MST / layout -- the filter's streaming cost alone
+    static const bool exp_filter_only = getenv("SM_EXP_FILTER_ONLY") != nullptr;
+    if (exp_filter_only && ctx->exp_layout_ok && !ts.main && p->aggregator == SM_AGG_TREE && std::isinf(p->c)) {
+        for (int i = 0; i < 3; ++i) HIPC(hipEventRecord(ctx->ev[i], ctx->st));
+        ctx->pending = 3;
+        ctx->pend_D = D;
+        ctx->pend_p = *p;
+        return SM_OK;
     }
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
@@ -2869,7 +2923,7 @@ sm_status sm_match_begin(sm_ctx* ctx, int D, const sm_params* p) {
     return SM_OK;
 }
 
-sm_status sm_match_finish(sm_ctx* ctx) {
+static sm_status match_finish_impl(sm_ctx* ctx) {
     if (!ctx) return SM_ERR_ARG;
     if (!ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_match_finish without sm_match_begin");
     const int kind = ctx->pending;
@@ -2883,7 +2937,8 @@ sm_status sm_match_finish(sm_ctx* ctx) {
     const int D = ctx->pend_D;
     const CallRange cr = call_range(p, D);
     if (had_worker) CHECK(ctx->seg_status);
-    CHECK(stage_layout_finish(ctx, ctx->views));
+    if (kind != 3) CHECK(stage_layout_finish(ctx, ctx->views));
+    ctx->exp_layout_ok = kind == 3 || (!ctx->seg && ctx->views == 3);
     HIPC(hipEventRecord(ctx->ev[3], ctx->st));
     CHECK(stage_filter(ctx, cr.D, cr.d0, ctx->views, false, &cr.w));
     HIPC(hipEventRecord(ctx->ev[4], ctx->st));
@@ -3131,8 +3186,20 @@ sm_status sm_download_labels(sm_ctx* ctx, float* left_abc, float* right_abc) {
 }
 
 sm_status sm_get_pms_stats(sm_ctx* ctx, sm_pms_stats* out) {
+    return sm_get_pms_stats_n(ctx, out, sizeof(sm_pms_stats));
+}
+
+sm_status sm_get_pms_stats_n(sm_ctx* ctx, sm_pms_stats* out, size_t out_bytes) {
     if (!ctx || !out) return SM_ERR_ARG;
-    *out = ctx->pms_stats;
+    memcpy(out, &ctx->pms_stats, std::min(out_bytes, sizeof(sm_pms_stats)));
+    return SM_OK;
+}
+
+sm_status sm_labels_extent(sm_ctx* ctx, int* W, int* H) {
+    if (!ctx || !W || !H) return SM_ERR_ARG;
+    if (!ctx->pms_last) return fail(ctx, SM_ERR_STATE, "sm_labels_extent: the last call was not SM_AGG_PMS");
+    *W = ctx->pms_W;
+    *H = ctx->pms_H;
     return SM_OK;
 }
 
