@@ -79,7 +79,8 @@ struct PinnedVec {
 // copies, labels, aggregation rows, cost rows and the speculation scratch
 // buffers of the GPU forest build (sm_pms_forest.hip), kept between calls
 struct PfBufs {
-    DevBuf par, flag, tree_of, nbr, nbw, root_pix, tsize, gpix, gpar, gtree, gw, gfc, gnc, gsize, ghk, glev, nlev, iota,
+    DevBuf par, flag, tree_of, nbr, nbw, root_pix, tsize, gpix, gpar, gtree, gw, gfc, gnc, gsize, ghk, iota, rot, pdir, psize,
+        bpos, a_dist, a_cid, a_head, nchains, c_last, c_len, c_head, cnw, tval, tval_s, tkey0, tkey1, tpix0, tpix1,
         bglob, gtree_s, g2b, bpar, bch0, J0, J1, D0, D1, plen, ld, rowof, rowstart, hflag, hidx, hkey0, hkey1, cutof,
         hcnt[4], hoff[4], rtc[4], rt[4], pairs0, pairs1, npairs, uflag, uidx, nbcnt, cut_round, tree_cut, tot, temp;
 };
@@ -2096,7 +2097,12 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
         {&B.tsize, n1 * 4, (void**)&pv.tsize}, {&B.gpix, n1 * 4, (void**)&pv.gpix}, {&B.gpar, n1 * 4, (void**)&pv.gpar},
         {&B.gtree, n1 * 4, (void**)&pv.gtree}, {&B.gw, n1 * 2, (void**)&pv.gw}, {&B.gfc, n1 * 4, (void**)&pv.gfc},
         {&B.gnc, n1, (void**)&pv.gnc}, {&B.gsize, n1 * 4, (void**)&pv.gsize}, {&B.ghk, n1, (void**)&pv.ghk},
-        {&B.glev, (n1 + 2) * 4, (void**)&pv.glev}, {&B.nlev, 16, (void**)&pv.nlev}, {&B.iota, n1 * 4, (void**)&pv.iota},
+        {&B.iota, n1 * 4, (void**)&pv.iota}, {&B.rot, n1 * 4, (void**)&pv.rot}, {&B.pdir, n1, (void**)&pv.pdir},
+        {&B.psize, n1 * 4, (void**)&pv.psize}, {&B.bpos, n1 * 4, (void**)&pv.bpos}, {&B.a_dist, 4 * n1 * 2, (void**)&pv.a_dist},
+        {&B.a_cid, 4 * n1 * 4, (void**)&pv.a_cid}, {&B.a_head, 4 * n1 * 4, (void**)&pv.a_head},
+        {&B.nchains, 16, (void**)&pv.nchains}, {&B.tval, 2 * n1 * 8, (void**)&pv.tval}, {&B.tval_s, 2 * n1 * 8, (void**)&pv.tval_s},
+        {&B.tkey0, n1 * 8, (void**)&pv.tkey[0]}, {&B.tkey1, n1 * 8, (void**)&pv.tkey[1]}, {&B.tpix0, n1 * 4, (void**)&pv.tpix[0]},
+        {&B.tpix1, n1 * 4, (void**)&pv.tpix[1]},
         {&B.bglob, n1 * 4, (void**)&pv.bglob}, {&B.gtree_s, n1 * 4, (void**)&pv.gtree_s}, {&B.g2b, n1 * 4, (void**)&pv.g2b},
         {&B.bpar, n1 * 4, (void**)&pv.bpar}, {&B.bch0, n1 * 4, (void**)&pv.bch0}, {&B.J0, n1 * 4, (void**)&pv.J[0]},
         {&B.J1, n1 * 4, (void**)&pv.J[1]}, {&B.D0, n1 * 4, (void**)&pv.Dj[0]}, {&B.D1, n1 * 4, (void**)&pv.Dj[1]},
@@ -2126,10 +2132,22 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
     pv.temp = B.temp.p;
     int K = 0;
     HIPC(pf_trees(st, pv, &K));
+    // the BFS tours' chains (sm_tour.h): their count depends on K
+    const size_t mch = pf_max_chains(W, H, K);
+    CHECK(ensure(ctx, B.c_last, mch * 4));
+    CHECK(ensure(ctx, B.c_len, mch * 4));
+    CHECK(ensure(ctx, B.c_head, mch * 4));
+    CHECK(ensure(ctx, B.cnw, mch * 8));
+    pv.c_last = P<uint32_t>(B.c_last);
+    pv.c_len = P<uint32_t>(B.c_len);
+    pv.c_head = P<uint32_t>(B.c_head);
+    pv.cnw = P<uint64_t>(B.cnw);
+    pv.max_chains = (uint32_t)mch;
     int rb[3];
     HIPC(pf_bfs(st, pv, K, rb));
-    if (rb[2]) return fail(ctx, SM_ERR_STATE, rb[2] == 1 ? "MST_PMS: the segment forest's masks contain a cycle"
-                                                         : "MST_PMS GPU forest: unresolved light depths");
+    if (rb[2]) return fail(ctx, SM_ERR_STATE, rb[2] == 1   ? "MST_PMS: the segment forest's masks contain a cycle"
+                                              : rb[2] == 4 ? "MST_PMS GPU forest: inconsistent tree tour"
+                                                           : "MST_PMS GPU forest: unresolved light depths");
     const int R = rb[0], nh = rb[1];
     const size_t T = (size_t)R * (K + 1) + 1;
     // round tables: rt_path and rt_item are kernel inputs (PmsDev), built in place; rt_rep and rt_long are
@@ -2611,13 +2629,15 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
     }
     ctx->st2 = ctx->st;
     {
+        // 1: the tree on a lowest-priority stream, the filter highest; 2: the reverse (A/B)
         const char* e = getenv("SM_TREE_STREAM");
-        if (e && atoi(e) == 1) {
+        if (e && (atoi(e) == 1 || atoi(e) == 2)) {
             int least = 0, greatest = 0;
+            const bool hi_tree = atoi(e) == 2;
             if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
                 hipStreamDestroy(ctx->st) != hipSuccess ||
-                hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, greatest) != hipSuccess ||
-                hipStreamCreateWithPriority(&ctx->st_tree, hipStreamNonBlocking, least) != hipSuccess ||
+                hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, hi_tree ? least : greatest) != hipSuccess ||
+                hipStreamCreateWithPriority(&ctx->st_tree, hipStreamNonBlocking, hi_tree ? greatest : least) != hipSuccess ||
                 hipEventCreateWithFlags(&ctx->ev_enq, hipEventDisableTiming) != hipSuccess) {
                 delete ctx;
                 return SM_ERR_HIP;
@@ -2822,10 +2842,31 @@ static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
         ts.main = ctx->st;
         ctx->st = ctx->st_tree;
     }
-    // timing experiment only (tools): SM_EXP_FILTER_ONLY=1 re-filters the previous frame's tree (same
-    // images) without re-running prep / MST / layout -- the filter's streaming cost alone
+    // timing experiments only (tools): with a layout of these images from an earlier frame,
+    // SM_EXP_FILTER_ONLY=1 re-filters it without re-running prep / MST / layout (the filter's streaming
+    // cost alone); SM_EXP_SKIP=mst keeps the previous MST (prep + layout + filter), SM_EXP_SKIP=layout
+    // keeps the previous layout (prep + MST + filter): the tree stages' streaming cost, stage by stage
     static const bool exp_filter_only = getenv("SM_EXP_FILTER_ONLY") != nullptr;
-    if (exp_filter_only && ctx->exp_layout_ok && !ts.main && p->aggregator == SM_AGG_TREE && std::isinf(p->c)) {
+    static const int exp_skip = getenv("SM_EXP_SKIP") ? (strcmp(getenv("SM_EXP_SKIP"), "mst") == 0 ? 1 : 2) : 0;
+    const bool exp_on = ctx->exp_layout_ok && !ts.main && p->aggregator == SM_AGG_TREE && std::isinf(p->c);
+    if (exp_on && exp_skip) {
+        HIPC(hipEventRecord(ctx->ev[0], ctx->st));
+        CHECK(stage_prep(ctx));
+        HIPC(hipEventRecord(ctx->ev[1], ctx->st));
+        if (exp_skip == 2) CHECK(stage_tree(ctx, ctx->views, p, false));
+        HIPC(hipEventRecord(ctx->ev[2], ctx->st));
+        if (exp_skip == 1) {
+            ctx->mst_pend.active = false;
+            CHECK(stage_layout_enqueue(ctx, ctx->views));
+        } else {
+            HIPC(hipEventRecord(ctx->ev_layout, ctx->st));  // (finish waits for the MST's rounds record)
+        }
+        ctx->pending = 1;
+        ctx->pend_D = D;
+        ctx->pend_p = *p;
+        return SM_OK;
+    }
+    if (exp_filter_only && exp_on) {
         for (int i = 0; i < 3; ++i) HIPC(hipEventRecord(ctx->ev[i], ctx->st));
         ctx->pending = 3;
         ctx->pend_D = D;

@@ -22,20 +22,12 @@
 
 #include "sm_common.h"
 #include "sm_layout_gpu.h"
+#include "sm_tour.h"
 
 #ifndef SM_RUN_DIV
 #define SM_RUN_DIV 384  // run window = bucket nodes / SM_RUN_DIV (~3 runs per CU, both views)
 #endif
-#define TL 32                 // tile side
-#define TLP (TL * TL)         // pixels per tile
-#define TLS (4 * TLP)         // arc slots per tile
-#define TL_THREADS 256
-#define L_EXIT 0xFFFFu        // successor leaves the tile
-#define L_NIL 0xFFFEu         // end of the tour (cut before the start arc)
-
-__device__ __forceinline__ uint32_t nbr_of(uint32_t p, int k, int W) {
-    return k == 0 ? p + 1 : k == 1 ? p + (uint32_t)W : k == 2 ? p - 1 : p - (uint32_t)W;
-}
+__device__ __forceinline__ uint32_t nbr_of(uint32_t p, int k, int W) { return tour_nbr(p, k, W); }
 
 // next MST direction of pixel q after direction j, cyclic (j itself if q is a leaf)
 __device__ __forceinline__ int next_dir(uint32_t adjq, int j) {
@@ -88,151 +80,41 @@ __device__ __forceinline__ uint32_t succ_arc(const uint8_t* adj, int W, uint32_t
     return s == start ? SM_NONE : s;
 }
 
-// L1: contract the tour inside each 32x32 tile.  One 64-bit LDS word per arc slot,
-// nxt | dist << 16 | last << 32 (bits 48..63: the chain head, written once the jumping is done),
-// so a jump is one gathered word; every thread keeps its 16 words in registers.
+// The MST's tour as a tour_tile graph (sm_tour.h): arcs along MST edges, the successor leaves a
+// pixel through the next MST direction after the one it arrived from; one list, cut before the start
+struct MstTour {
+    const uint8_t* adj;
+    int W;
+    uint32_t start;
+    __device__ bool has(uint32_t p, int k) const { return (adj[p] >> k) & 1u; }
+    __device__ uint32_t succ(uint32_t a) const { return succ_arc(adj, W, a, start); }
+};
+
+__device__ __forceinline__ TourBufs tour_bufs(const LayoutView& V) {
+    return TourBufs{V.a_dist, V.a_cid, V.a_head, V.nchains, V.c_last, V.c_len, V.c_head, V.cnw};
+}
+
+// L1: contract the tour inside each 32x32 tile (sm_tour.h)
 __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    __shared__ union {
-        uint64_t w[TLS];
-        uint16_t h[4 * TLS];  // h[4*s + 3]: head slot of the chain whose last slot is s
-    } st;
-    __shared__ uint8_t haspred[TLS];
-    const int tx0 = blockIdx.x * TL, ty0 = blockIdx.y * TL;
-    const uint32_t start = start_arc(V.adj);
-    constexpr int PER = TLS / TL_THREADS;  // 16 slots per thread
-    for (int i = 0; i < PER; ++i) haspred[threadIdx.x + i * TL_THREADS] = 0;
-    __syncthreads();
-    uint64_t own[PER];
-    for (int i = 0; i < PER; ++i) {
-        const int s = threadIdx.x + i * TL_THREADS;
-        const int lp = s >> 2, k = s & 3;
-        const int lx = lp % TL, ly = lp / TL;
-        const int x = tx0 + lx, y = ty0 + ly;
-        uint32_t n = L_NIL, dd = 0;
-        if (x < W && y < H) {
-            const uint32_t p = (uint32_t)(y * W + x);
-            if (V.adj[p] & (1u << k)) {
-                dd = 1;
-                const uint32_t sa = succ_arc(V.adj, W, 4u * p + (uint32_t)k, start);
-                if (sa != SM_NONE) {
-                    // the successor leaves from q = the neighbour of p in direction k: its tile
-                    // coordinates follow from p's without a division by W
-                    const int qx = lx + (k == 0 ? 1 : k == 2 ? -1 : 0), qy = ly + (k == 1 ? 1 : k == 3 ? -1 : 0);
-                    if (qx >= 0 && qx < TL && qy >= 0 && qy < TL) {
-                        n = (uint32_t)(4 * (qy * TL + qx) + (int)(sa & 3u));
-                        haspred[n] = 1;
-                    } else {
-                        n = L_EXIT;
-                    }
-                }
-            }
-        }
-        own[i] = (uint64_t)n | ((uint64_t)dd << 16) | ((uint64_t)s << 32);
-        st.w[s] = own[i];
-    }
-    __syncthreads();
-    // pointer jumping: dist -> arcs to chain end (inclusive), last -> chain's last slot
-    for (int it = 0; it < 13; ++it) {
-        bool any = false;
-        for (int i = 0; i < PER; ++i) {
-            const uint32_t n = (uint32_t)own[i] & 0xFFFFu;
-            if (n < L_NIL) {
-                const uint64_t nb = st.w[n];
-                const uint32_t d = (uint32_t)(own[i] >> 16) + (uint32_t)(nb >> 16);  // low 16 bits: the sum
-                own[i] = (nb & 0xFFFF0000FFFFull) | ((uint64_t)(d & 0xFFFFu) << 16);
-                any = true;
-            }
-        }
-        any = __syncthreads_or(any);
-        if (!any) break;
-        for (int i = 0; i < PER; ++i) st.w[threadIdx.x + i * TL_THREADS] = own[i];
-        __syncthreads();
-    }
-    // heads: existing arcs without an in-tile predecessor; register chains
-    __shared__ uint32_t nheads, cbase;
-    if (threadIdx.x == 0) nheads = 0;
-    __syncthreads();
-    uint32_t myhead[PER];
-    for (int i = 0; i < PER; ++i) {
-        const int s = threadIdx.x + i * TL_THREADS;
-        const uint32_t dist = (uint32_t)(own[i] >> 16) & 0xFFFFu, last = (uint32_t)(own[i] >> 32) & 0xFFFFu;
-        myhead[i] = SM_NONE;
-        if (dist != 0 && !haspred[s]) {
-            st.h[4 * last + 3] = (uint16_t)s;
-            myhead[i] = atomicAdd(&nheads, 1u);  // LDS atomic: rank of this chain inside the tile
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) cbase = atomicAdd(V.nchains, nheads);  // one global atomic per tile
-    __syncthreads();
-    for (int i = 0; i < PER; ++i) {
-        const int s = threadIdx.x + i * TL_THREADS;
-        const uint32_t dist = (uint32_t)(own[i] >> 16) & 0xFFFFu, last = (uint32_t)(own[i] >> 32) & 0xFFFFu;
-        if (dist == 0) continue;
-        const int lp = s >> 2, k = s & 3;
-        const uint32_t p = (uint32_t)((ty0 + lp / TL) * W + tx0 + lp % TL);
-        const uint32_t a = 4u * p + (uint32_t)k;
-        V.a_dist[a] = (uint16_t)dist;
-        if (myhead[i] != SM_NONE) {
-            const uint32_t cid = cbase + myhead[i];
-            V.a_cid[a] = cid;        // head's chain id (read below by the chain's other arcs: next kernel)
-            const int llp = (int)last >> 2;
-            const uint32_t lpix = (uint32_t)((ty0 + llp / TL) * W + tx0 + llp % TL);
-            V.c_last[cid] = 4u * lpix + (last & 3u);
-            V.c_len[cid] = dist;
-            V.c_head[cid] = a;
-        }
-        // every arc remembers its chain head (global arc id)
-        const int hs = st.h[4 * last + 3];
-        const int hlp = hs >> 2;
-        const uint32_t hpix = (uint32_t)((ty0 + hlp / TL) * W + tx0 + hlp % TL);
-        V.a_head[a] = 4u * hpix + (uint32_t)(hs & 3);
-    }
+    tour_tile(MstTour{V.adj, W, start_arc(V.adj)}, tour_bufs(V), W, H);
 }
 
 // L2 init: chain successor + weight
 __global__ void k_chain_init(LayoutPair LP, int W) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= *V.nchains) return;
-    const uint32_t start = start_arc(V.adj);
-    const uint32_t s = succ_arc(V.adj, W, V.c_last[c], start);
-    const uint32_t n = s == SM_NONE ? SM_NONE : V.a_cid[s];
-    V.cnw[c] = ((uint64_t)V.c_len[c] << 32) | n;
+    tour_chain_init(MstTour{V.adj, W, start_arc(V.adj)}, tour_bufs(V), blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// L2: suffix sums over the chain list by in-place pointer jumping, one launch.  Every word
-// {n, w} satisfies "w = arcs from this chain up to (not including) chain n" whichever update of
-// it a reader sees (the pair is one 64-bit access), so no step needs a grid barrier.  The grid is
-// at most CR_BLOCKS blocks (co-resident) and every thread sweeps its chains, one jump each per
-// sweep, until all have reached the tour end: with one thread per chain, threads that were not
-// yet resident left the resident ones reading never-updated words, i.e. advancing one chain per
-// step (19.7 ms at 3840x2160).  Every jump moves strictly forward, so the loop ends; with fresh
-// words it takes ~log2(chains) sweeps.  Integer sums: the result is exact.
+// L2: suffix sums over the chain list by in-place pointer jumping, one launch (sm_tour.h).  The grid
+// is at most CR_BLOCKS blocks (co-resident).
 #define CR_BLOCKS 1024  // per view, 256 threads each: half the chip's resident threads for both views
 
 __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.y];
-    const uint32_t nch = *V.nchains;
-    uint64_t* nw = V.cnw;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (;;) {
-        bool any = false;
-        for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += stride) {
-            const uint64_t me = __hip_atomic_load(nw + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t n = (uint32_t)me;
-            if (n == SM_NONE) continue;
-            const uint64_t nb = __hip_atomic_load(nw + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t w = (uint32_t)(me >> 32) + (uint32_t)(nb >> 32);
-            __hip_atomic_store(nw + c, ((uint64_t)w << 32) | (uint32_t)nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            any = true;
-        }
-        if (!any) break;
-    }
+    tour_chain_rank(tour_bufs(LP.v[blockIdx.y]));
 }
 
 // L3: arc ranks.  suffix(c) = arcs from chain c's head to the tour end; rank = total - suffix + offset
@@ -247,9 +129,7 @@ __global__ void k_tour_rank(LayoutPair LP, int W, int H) {
     for (int k = 0; k < 4; ++k) {
         if (!(adj & (1u << k))) continue;
         const uint32_t a = 4u * p + (uint32_t)k;
-        const uint32_t c = V.a_cid[V.a_head[a]];
-        const uint32_t chain_rank = total - (uint32_t)(V.cnw[c] >> 32);
-        V.rank[a] = chain_rank + (V.c_len[c] - V.a_dist[a]);
+        V.rank[a] = total - tour_suffix(tour_bufs(V), a);
     }
 }
 

@@ -28,7 +28,26 @@ struct PfView {
     int32_t* tsize;     // K + 1 -> (scan) tree_start
     int32_t* tree_start;
     int32_t* tree_rounds;
-    // global level order (N): the BFS of every tree at once, level by level
+    // the BFS by Euler tours (sm_tour.h): per pixel
+    uint32_t* rot;      // rotation word: real edges by direction, the tour's next direction per arrival
+    int8_t* pdir;       // direction to the parent (-1: a root)
+    int32_t* psize;     // subtree size
+    int32_t* bpos;      // BFS position
+    // per arc (4N) and per chain (max_chains) of the list ranking
+    uint16_t* a_dist;
+    uint32_t* a_cid;
+    uint32_t* a_head;
+    uint32_t* nchains;
+    uint32_t* c_last;
+    uint32_t* c_len;
+    uint32_t* c_head;
+    uint64_t* cnw;
+    uint32_t max_chains;
+    long long* tval;    // 2(N - K): the tours' values, concatenated by tree, and their inclusive scan
+    long long* tval_s;
+    unsigned long long* tkey[2];  // (tree, depth) at the global preorder position, sorted
+    int32_t* tpix[2];
+    // BFS order (N) of every tree at once (tree-major: the level-order arrays of the round-4 build)
     int32_t* gpix;
     int32_t* gpar;      // parent's index (-1: a root)
     int32_t* gtree;
@@ -37,8 +56,6 @@ struct PfView {
     uint8_t* gnc;       // children
     int32_t* gsize;     // subtree size
     int8_t* ghk;        // heavy child (index among the children, -1: a leaf)
-    int32_t* glev;      // level boundaries (<= N + 2)
-    int32_t* nlev;      // [0]: levels
     // BFS numbering (N): the stable sort of the level order by tree
     int32_t* iota;
     int32_t* bglob;     // BFS node -> level-order index
@@ -79,7 +96,7 @@ struct PfView {
     PmsRep* reps;
     int32_t* tree_cut;  // K + 1
     int32_t* rt[4];     // nrounds x (K + 1): rt_path, rt_item, rt_rep, rt_long
-    int32_t* tot;       // [0..3] paths, items, reps, long; [4] cuts; [5] nrounds; [6] heads; [7] not a forest
+    int32_t* tot;       // [0..3] paths, items, reps, long; [4] cuts; [5] nrounds; [6] heads; [7] inconsistent; [8] edges
     void* temp;         // hipcub scratch
     size_t temp_bytes;
     int piece;
@@ -89,8 +106,9 @@ struct PfView {
 size_t pf_temp_bytes(int N);
 // steps of the build; each ends with a host sync for the sizes the next one allocates by
 hipError_t pf_trees(hipStream_t st, PfView& v, int* K_out);   // union-find, tree ids, sizes
-// BFS, sizes, heavy paths, light depths; out[0] = rounds, out[1] = heads, out[2] != 0: the masks had a cycle (1)
-// or a light depth stayed unresolved (2)
+size_t pf_max_chains(int W, int H, int K);                      // chain capacity of the BFS's tours
+// BFS, sizes, heavy paths, light depths; out[0] = rounds, out[1] = heads, out[2] != 0: the masks had a cycle (1),
+// a light depth stayed unresolved (2) or a tour was inconsistent (4)
 hipError_t pf_bfs(hipStream_t st, PfView& v, int K, int* out);
 // rows, cuts, tree graph, round-major counts and tables; counts: paths, items, reps, chain items, cuts, pairs,
 // error flag

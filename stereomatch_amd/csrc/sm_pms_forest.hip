@@ -26,6 +26,7 @@
 
 #include "sm_pms_forest.h"
 #include "sm_segment.h"
+#include "sm_tour.h"
 
 #define SM_VIRTUAL_W_PF SM_VIRTUAL_W
 
@@ -159,290 +160,227 @@ __global__ void k_pf_trees(PfView v) {
 }
 
 // ---------------------------------------------------------------------------------------- BFS
-constexpr int BT = 1024;  // threads of the BFS workgroup
+// Every tree's BFS numbering (Stereo3DMST.cpp:450-522: root first, then level by level, a node's
+// children in ascending (w, a, b) key order after the children of the nodes before it) in O(log) depth,
+// from two Euler tours per tree (sm_tour.h list ranking; round 5, replacing a level-synchronous BFS in
+// one workgroup that took ~2.5 us per level: 26 ms for the 8.6k-level tree at C2):
+//   tour 1 : the successor leaves a node through its next neighbour in cyclic key order; ranked per
+//            tree, an arc p->q precedes its reverse iff p is q's parent (orientation), and the distance
+//            between the two is twice q's subtree size
+//   tour 2 : children in key order, then back to the parent: a depth-first order whose preorder, among
+//            the nodes of one depth, is the lexicographic order of their root paths' key ranks -- i.e.
+//            the BFS order.  An int64 prefix sum over the tours (+1 | +1 down, -1 | 0 up) gives every
+//            node's depth and preorder, and a stable radix sort of the preorder sequence by (tree, depth)
+//            is the BFS numbering of every tree at once.
+// Rotation words (rot): bits 0..3 the node's real tree edges by direction; nibble 1 + j: the direction
+// the tour leaves by after arriving from direction j (PF_END: the end of the tree's list).
+#define PF_END 4u
 
-// exclusive block scan of c (all BT threads), returns the thread's offset; *total the sum
-__device__ __forceinline__ int block_scan(int c, int* s_w, int* total) {
-    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    int incl = c;
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const int u = __shfl_up(incl, k);
-        if (lane >= k) incl += u;
+struct PfTourG {
+    const uint32_t* rot;
+    int W;
+    __device__ bool has(uint32_t p, int k) const { return (rot[p] >> k) & 1u; }
+    __device__ uint32_t succ(uint32_t a) const {
+        const uint32_t q = tour_nbr(a >> 2, (int)(a & 3u), W);
+        const uint32_t nd = (rot[q] >> (4 + 4 * (((a & 3u) + 2u) & 3u))) & 0xFu;
+        return nd == PF_END ? SM_NONE : 4u * q + nd;
     }
-    if (lane == 63) s_w[wv] = incl;
-    __syncthreads();
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < BT / 64; ++k) {
-        const int x = s_w[k];
-        if (k < wv) pre += x;
-        tot += x;
-    }
-    __syncthreads();
-    *total = tot;
-    return pre + incl - c;
+};
+
+__device__ __forceinline__ TourBufs pf_tour_bufs(const PfView& v) {
+    return TourBufs{v.a_dist, v.a_cid, v.a_head, v.nchains, v.c_last, v.c_len, v.c_head, v.cnw};
 }
 
-// the children of a node (its tree neighbours but the parent, in key order) compacted into q / wv by static
-// selects: a runtime index into the local arrays (q[c++] = ...) would put them in scratch memory
-__device__ __forceinline__ void pf_children(const int (&nn)[4], const uint32_t (&ww)[4], int pp, int (&q)[4], uint32_t (&wv)[4],
-                                            int& c) {
+// direction from p to its grid neighbour n
+__device__ __forceinline__ int pf_dir(int p, int n, int W) { return n == p + 1 ? 0 : n == p + W ? 1 : n == p - 1 ? 2 : 3; }
+
+// the real tree neighbours' directions in key order (nbr, k_pf_prep); returns their count
+__device__ __forceinline__ int pf_dirs(const PfView& v, int p, int (&d)[4]) {
+    const int4 n4 = v.nbr[p];
+    const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+    int c = 0;
 #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        d[i] = nn[i] >= 0 ? pf_dir(p, nn[i], v.W) : 0;
+        c += nn[i] >= 0 ? 1 : 0;
+    }
+    return c;
+}
+
+// tour 1's rotation: cyclic key order; a tree's list starts at root -> its first neighbour, so the root
+// ends it after its last one
+__global__ void k_pf_rot1(PfView v) {
+    const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= v.N) return;
+    int d[4];
+    const int c = pf_dirs(v, p, d);
+    const bool root = v.par[p] == p;
+    uint32_t r = 0;
+    for (int i = 0; i < c; ++i) {
+        r |= 1u << d[i];
+        const uint32_t nx = (root && i == c - 1) ? PF_END : (uint32_t)d[(i + 1) % c];
+        r |= nx << (4 + 4 * d[i]);
+    }
+    v.rot[p] = r;
+}
+
+// tour 2's rotation from tour 1's orientation: arriving from the parent, the first child in key order;
+// from a child, the next child, then the parent (the root: the end of the list)
+__global__ void k_pf_rot2(PfView v) {
+    const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= v.N) return;
+    int d[4];
+    const int c = pf_dirs(v, p, d);
+    const int pd = v.pdir[p];
+    uint32_t r = 0;
+    int prev = pd;  // the direction whose successor is set next (the parent's arrival first)
+    for (int i = 0; i < c; ++i) {
+        r |= 1u << d[i];
+        if (d[i] == pd) continue;
+        if (prev >= 0) r |= (uint32_t)d[i] << (4 + 4 * prev);
+        prev = d[i];
+    }
+    if (prev >= 0) r |= (pd >= 0 ? (uint32_t)pd : PF_END) << (4 + 4 * prev);  // a leaf: straight back up
+    v.rot[p] = r;
+}
+
+__global__ void k_pf_tour_tile(PfView v) { tour_tile(PfTourG{v.rot, v.W}, pf_tour_bufs(v), v.W, v.H); }
+
+__global__ void k_pf_chain_init(PfView v) {
+    tour_chain_init(PfTourG{v.rot, v.W}, pf_tour_bufs(v), blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+constexpr int PF_CR_BLOCKS = 512;  // per view (the two views' forests build concurrently)
+__global__ __launch_bounds__(256) void k_pf_chain_rank(PfView v) { tour_chain_rank(pf_tour_bufs(v)); }
+
+// tour 1: orientation (pdir: direction to the parent, -1 at a root) and subtree sizes.  Arc ranks per
+// tree are its list length minus the suffix, so rank(p->q) < rank(q->p) iff suffix(p->q) > suffix(q->p)
+__global__ void k_pf_orient(PfView v) {
+    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= v.N) return;
+    const uint32_t adj = v.rot[q] & 0xFu;
+    int pd = -1;
+    int sz = v.tsize[v.tree_of[q]];  // a root: its tree
+    const TourBufs T = pf_tour_bufs(v);
     for (int k = 0; k < 4; ++k) {
-        const bool keep = nn[k] >= 0 && nn[k] != pp;
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-            if (keep && c == s) {
-                q[s] = nn[k];
-                wv[s] = ww[k];
-            }
-        c += keep ? 1 : 0;
+        if (!((adj >> k) & 1u)) continue;
+        const uint32_t p = tour_nbr((uint32_t)q, k, v.W);
+        const uint32_t si = tour_suffix(T, 4u * p + (uint32_t)((k + 2) & 3)), so = tour_suffix(T, 4u * (uint32_t)q + (uint32_t)k);
+        if (si > so) {
+            pd = k;
+            sz = (int)((si - so + 1u) / 2u);
+        }
+    }
+    v.pdir[q] = (int8_t)pd;
+    v.psize[q] = sz;
+}
+
+// tour 2: the arcs' +-1 values at their positions in the concatenation of the trees' lists (tree t's
+// 2(|t| - 1) arcs start at 2(tree_start[t] - t)): down (1 << 32 | 1), up -(1 << 32)
+__global__ void k_pf_tourval(PfView v) {
+    const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= v.N) return;
+    const uint32_t adj = v.rot[p] & 0xFu;
+    if (!adj) return;
+    const int t = v.tree_of[p];
+    const uint32_t len = 2u * (uint32_t)(v.tsize[t] - 1);
+    const uint32_t base = 2u * (uint32_t)(v.tree_start[t] - t);
+    const TourBufs T = pf_tour_bufs(v);
+    for (int k = 0; k < 4; ++k) {
+        if (!((adj >> k) & 1u)) continue;
+        const uint32_t a = 4u * (uint32_t)p + (uint32_t)k;
+        const uint32_t q = tour_nbr((uint32_t)p, k, v.W);
+        const bool down = v.pdir[q] == ((k + 2) & 3);
+        const uint32_t rank = len - tour_suffix(T, a);
+        v.tval[base + rank] = down ? (long long)((1ull << 32) | 1ull) : -(long long)(1ull << 32);
     }
 }
 
-// Narrow levels (at most 64 nodes: the deep tails of the largest trees, thousands of levels at C2) run on
-// wave 0 alone, level after level without workgroup barriers: the frontier stays in registers, the next
-// one is handed over through LDS (one wave's LDS operations complete in order).  Entered at level d =
-// [a, b) whose nodes are in global memory; leaves at the first level wider than 64 (or the end) with
-// s_state = {a, b, d}.
-__device__ void bfs_narrow(const PfView& v, int a, int b, int d, int* s_q, int* s_pp, int* s_tr, int* s_state) {
-    const int lane = (int)threadIdx.x;
-    int n = b - a, i = a + lane;
-    bool val = lane < n;
-    int p = 0, pp = -1, tr = 0;
-    if (val) {
-        p = v.gpix[i];
-        const int gp = v.gpar[i];
-        pp = gp >= 0 ? v.gpix[gp] : -1;
-        tr = v.gtree[i];
+// depth and preorder of every node from the scanned values at its down arc; the sort input: key
+// (tree, depth) at the node's global preorder position (trees in order), value the pixel
+__global__ void k_pf_depth(PfView v, int dbits) {
+    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= v.N) return;
+    const int t = v.tree_of[q], pd = v.pdir[q];
+    long long depth = 0, pre = 0;
+    if (pd >= 0) {
+        const uint32_t p = tour_nbr((uint32_t)q, pd, v.W);
+        const uint32_t a = 4u * p + (uint32_t)((pd + 2) & 3);
+        const uint32_t len = 2u * (uint32_t)(v.tsize[t] - 1);
+        const uint32_t pos = 2u * (uint32_t)(v.tree_start[t] - t) + len - tour_suffix(pf_tour_bufs(v), a);
+        const long long s = v.tval_s[pos];
+        depth = s >> 32;
+        pre = (s & 0xFFFFFFFFll) - (long long)(v.tree_start[t] - t);
     }
-    while (n > 0 && n <= 64) {
-        if (lane == 0) v.glev[d] = a;
-        int q[4] = {-1, -1, -1, -1}, c = 0;
-        uint32_t wv[4] = {0, 0, 0, 0};
-        if (val) {
-            const int4 n4 = v.nbr[p];
-            const uint2 w4 = v.nbw[p];
-            const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
-            const uint32_t ww[4] = {w4.x & 0xFFFFu, w4.x >> 16, w4.y & 0xFFFFu, w4.y >> 16};
-            pf_children(nn, ww, pp, q, wv, c);
-        }
-        int incl = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int u = __shfl_up(incl, o);
-            if (lane >= o) incl += u;
-        }
-        const int total = __shfl(incl, 63), pos = incl - c;
-        if (val) {
-            v.gfc[i] = b + pos;
-            v.gnc[i] = (uint8_t)c;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (k >= c) break;
-                const int j = b + pos + k;
-                if (j >= v.N) {  // only masks with a cycle get here (as in the workgroup levels)
-                    v.tot[7] = 1;
-                    break;
-                }
-                v.gpix[j] = q[k];
-                v.gpar[j] = i;
-                v.gtree[j] = tr;
-                v.gw[j] = (uint16_t)wv[k];
-                if (pos + k < 64) {
-                    s_q[pos + k] = q[k];
-                    s_pp[pos + k] = p;
-                    s_tr[pos + k] = tr;
-                }
-            }
-        }
-        const int nb = b + total < v.N ? b + total : v.N;
-        a = b;
-        b = nb;
-        ++d;
-        n = b - a;
-        i = a + lane;
-        val = lane < n;
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the LDS writes above stay before the reads below
-        __builtin_amdgcn_wave_barrier();
-        if (n <= 64 && val) {
-            p = s_q[lane];
-            pp = s_pp[lane];
-            tr = s_tr[lane];
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // and these reads before the next level's writes
-        __builtin_amdgcn_wave_barrier();
+    const int g = v.tree_start[t] + (int)pre;
+    if (g < v.tree_start[t] || g >= v.tree_start[t + 1] || depth < 0 || depth >= (1ll << dbits)) {
+        v.tot[7] = 4;  // an inconsistent tour: flag it, never write out of range
+        return;
     }
-    if (lane == 0) {
-        s_state[0] = a;
-        s_state[1] = b;
-        s_state[2] = d;
-    }
+    v.tkey[0][g] = ((unsigned long long)t << dbits) | (unsigned long long)depth;
+    v.tpix[0][g] = q;
 }
 
-// Narrow levels of the bottom-up sweep on wave 0, from level l down while levels have at most 64 nodes;
-// a level's sizes stay in LDS for its parents' level.  s_state[3] = the first level left (or -1).
-__device__ void sweep_narrow(const PfView& v, int l, int* s_sz, int* s_state) {
-    const int lane = (int)threadIdx.x;
-    int pbase = -1;  // the start of level l + 1 when its sizes are in s_sz
-    for (; l >= 0; --l) {
-        const int la = min(max(v.glev[l], 0), v.N), lb = min(max(v.glev[l + 1], la), v.N);
-        const int n = lb - la;
-        if (n > 64) break;
-        const int i = la + lane;
-        int s = 1, best = -1, bs = 0;
-        if (lane < n) {
-            const int f = v.gfc[i], c = min((int)v.gnc[i], v.N - f);
-            for (int k = 0; k < c; ++k) {
-                const int o = f + k - pbase;
-                const int sk = pbase >= 0 && o >= 0 && o < 64 ? s_sz[o] : v.gsize[f + k];
-                s += sk;
-                if (sk > bs) {  // strictly larger: ties keep the smallest BFS id
-                    bs = sk;
-                    best = k;
-                }
-            }
-            v.gsize[i] = s;
-            v.ghk[i] = (int8_t)best;
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // this level's reads of s_sz before its writes
-        __builtin_amdgcn_wave_barrier();
-        if (lane < n) s_sz[lane] = s;
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_wave_barrier();
-        pbase = la;
-    }
-    if (lane == 0) s_state[3] = l;
+// BFS position of every pixel, tree of every BFS node
+__global__ void k_pf_bpos(PfView v) {
+    const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (n >= v.N) return;
+    const int q = v.gpix[n];
+    v.bpos[q] = n;
+    v.gtree[n] = v.tree_of[q];
 }
 
-// One workgroup: the BFS of every tree of the view at once, then the bottom-up sweep.  Level 0 is the
-// roots in tree order; a node's children follow, in key order, at the next level, after the children
-// of the nodes before it.
-constexpr int PF_FC = 4096;  // a level of at most this many nodes is handed to the next one in LDS
+// the BFS-numbered node fields the rest of the build reads (as the level-order arrays of the round-4
+// BFS, whose level order is now the BFS order itself): parent, edge weight to it, children (consecutive
+// in BFS order, key order), subtree size, heavy child (the largest subtree, ties: the smallest BFS id)
+__global__ void k_pf_fields(PfView v) {
+    const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (n >= v.N) return;
+    const int q = v.gpix[n], pd = v.pdir[q];
+    const int4 n4 = v.nbr[q];
+    const uint2 w4 = v.nbw[q];
+    const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+    const uint32_t ww[4] = {w4.x & 0xFFFFu, w4.x >> 16, w4.y & 0xFFFFu, w4.y >> 16};
+    const int par = pd >= 0 ? (int)tour_nbr((uint32_t)q, pd, v.W) : -1;
+    int nc = 0, fc = -1, best = -1, bs = 0;
+    for (int i = 0; i < 4; ++i) {
+        if (nn[i] < 0 || nn[i] == par) continue;
+        if (nc == 0) fc = v.bpos[nn[i]];
+        const int sk = v.psize[nn[i]];
+        if (sk > bs) {
+            bs = sk;
+            best = nc;
+        }
+        ++nc;
+    }
+    uint32_t w = 0;  // the weight code of the edge to the parent
+    for (int i = 0; i < 4; ++i)
+        if (par >= 0 && nn[i] == par) w = ww[i];
+    v.gpar[n] = par >= 0 ? v.bpos[par] : -1;
+    v.gw[n] = (uint16_t)w;
+    v.gnc[n] = (uint8_t)nc;
+    v.gfc[n] = nc ? fc : n;
+    v.gsize[n] = v.psize[q];
+    v.ghk[n] = (int8_t)best;
+}
 
-__global__ void __launch_bounds__(BT) k_pf_bfs(PfView v, int K) {
-    __shared__ int s_w[BT / 64];
-    __shared__ int s_q[64], s_pp[64], s_tr[64], s_sz[64], s_state[4];
-    // the frontier of a level (pixel, its parent's pixel, tree), double-buffered: a level's children are
-    // written there too, so the next level reads LDS instead of three dependent global loads
-    __shared__ int s_fp[2][PF_FC], s_fpp[2][PF_FC], s_ftr[2][PF_FC];
-    const int tid = (int)threadIdx.x;
-    for (int t = tid; t < K; t += BT) {
-        v.gpix[t] = v.root_pix[t];
-        v.gpar[t] = -1;
-        v.gtree[t] = t;
-        v.gw[t] = 0;
-    }
-    __syncthreads();
-    int a = 0, b = K, next = K, d = 0, cur = 0;
-    bool in_lds = false;  // the roots are in global memory
-    while (a < b) {
-        if (b - a <= 64) {  // narrow levels on wave 0 (next == b at a level's start)
-            if (tid < 64) bfs_narrow(v, a, b, d, s_q, s_pp, s_tr, s_state);
-            __syncthreads();
-            a = s_state[0];
-            b = s_state[1];
-            d = s_state[2];
-            next = b;
-            in_lds = false;
-            __syncthreads();  // s_state read by every wave before it is written again
-            continue;
-        }
-        if (tid == 0) v.glev[d] = a;
-        for (int base = a; base < b; base += BT) {
-            const int i = base + tid;
-            int q[4] = {-1, -1, -1, -1}, c = 0;
-            uint32_t wv[4] = {0, 0, 0, 0};
-            int tr = 0;
-            int p = 0;
-            if (i < b) {
-                int pp;
-                if (in_lds) {
-                    p = s_fp[cur][i - a];
-                    pp = s_fpp[cur][i - a];
-                    tr = s_ftr[cur][i - a];
-                } else {
-                    p = v.gpix[i];
-                    const int gp = v.gpar[i];
-                    pp = gp >= 0 ? v.gpix[gp] : -1;
-                    tr = v.gtree[i];
-                }
-                const int4 n4 = v.nbr[p];
-                const uint2 w4 = v.nbw[p];
-                const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
-                const uint32_t ww[4] = {w4.x & 0xFFFFu, w4.x >> 16, w4.y & 0xFFFFu, w4.y >> 16};
-                pf_children(nn, ww, pp, q, wv, c);  // every tree neighbour but the parent is a child
-            }
-            int total;
-            const int pos = block_scan(c, s_w, &total);
-            if (i < b) {
-                v.gfc[i] = next + pos;
-                v.gnc[i] = (uint8_t)c;
+// real tree edges of the view (a forest of N nodes in K trees has exactly N - K)
+__global__ void k_pf_edges(PfView v) {
+    const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    int c = p < v.N ? __popc(pf_real(v, p)) : 0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k >= c) break;
-                    const int j = next + pos + k;
-                    if (j >= v.N) {  // only masks with a cycle (not a forest) get here: flag, never write out of bounds
-                        v.tot[7] = 1;
-                        break;
-                    }
-                    v.gpix[j] = q[k];
-                    v.gpar[j] = i;
-                    v.gtree[j] = tr;
-                    v.gw[j] = (uint16_t)wv[k];
-                    if (j - b < PF_FC) {
-                        s_fp[cur ^ 1][j - b] = q[k];
-                        s_fpp[cur ^ 1][j - b] = p;
-                        s_ftr[cur ^ 1][j - b] = tr;
-                    }
-                }
-            }
-            next = next + total < v.N ? next + total : v.N;
-        }
-        __syncthreads();  // this level's writes are visible to the next one's reads
-        in_lds = next - b <= PF_FC;
-        cur ^= 1;
-        a = b;
-        b = next;
-        ++d;
-    }
-    if (tid == 0) {
-        v.glev[d] = a;
-        v.nlev[0] = d;
-    }
-    __syncthreads();  // the last boundary is read by every wave below
-    // bottom up: subtree sizes and heavy children, a level at a time
-    for (int l = d - 1; l >= 0; --l) {
-        const int la = min(max(v.glev[l], 0), v.N), lb = min(max(v.glev[l + 1], la), v.N);
-        if (lb - la <= 64) {  // narrow levels on wave 0
-            if (tid < 64) sweep_narrow(v, l, s_sz, s_state);
-            __syncthreads();
-            l = s_state[3] + 1;  // the loop's decrement gives the first level left
-            __syncthreads();
-            continue;
-        }
-        for (int i = la + tid; i < lb; i += BT) {
-            const int f = v.gfc[i], c = min((int)v.gnc[i], v.N - f);  // clamp: only a cycle overflows
-            int s = 1, best = -1, bs = 0;
-            for (int k = 0; k < c; ++k) {
-                const int sk = v.gsize[f + k];
-                s += sk;
-                if (sk > bs) {  // strictly larger: ties keep the smallest BFS id (children are in BFS order)
-                    bs = sk;
-                    best = k;
-                }
-            }
-            v.gsize[i] = s;
-            v.ghk[i] = (int8_t)best;
-        }
-        __syncthreads();
-    }
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+    if (__lane_id() == 0 && c) atomicAdd(v.tot + 8, c);
 }
 
 __global__ void k_pf_iota(int32_t* a, int n) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i < n) a[i] = i;
+}
+
+__global__ void k_pf_fill1(int32_t* a, int n) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) a[i] = 1;
 }
 
 __global__ void k_pf_g2b(PfView v) {
@@ -736,13 +674,16 @@ __global__ void k_pf_emit(PfView v, int nh) {
 }  // namespace
 
 size_t pf_temp_bytes(int N) {
-    size_t a = 0, b = 0, c = 0;
+    size_t a = 0, b = 0, c = 0, d = 0, f = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, d, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, N, 0, 64);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, f, (const long long*)nullptr, (long long*)nullptr, 2 * N);
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr,
                                              (int32_t*)nullptr, N, 0, 32);
     (void)hipcub::DeviceRadixSort::SortKeys(nullptr, b, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                             4 * N, 0, 64);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const int32_t*)nullptr, (int32_t*)nullptr, 32 * N + 1);
-    return std::max(a, std::max(b, c)) + 256;
+    return std::max(std::max(a, std::max(b, c)), std::max(d, f)) + 256;
 }
 
 static int bits_for(int n) {
@@ -770,16 +711,64 @@ hipError_t pf_trees(hipStream_t st, PfView& v, int* K_out) {
     return hipGetLastError();
 }
 
+// one tree tour (rotation words in v.rot): contraction, chain ranking (sm_tour.h)
+static hipError_t pf_tour(hipStream_t st, PfView& v) {
+    hipError_t e = hipMemsetAsync(v.nchains, 0, 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pf_tour_tile, dim3((v.W + TL - 1) / TL, (v.H + TL - 1) / TL), dim3(TL_THREADS), 0, st, v);
+    hipLaunchKernelGGL(k_pf_chain_init, dim3(nblk(v.max_chains, 256)), dim3(256), 0, st, v);
+    hipLaunchKernelGGL(k_pf_chain_rank, dim3(PF_CR_BLOCKS), dim3(256), 0, st, v);
+    return hipGetLastError();
+}
+
+size_t pf_max_chains(int W, int H, int K) {
+    // a chain head enters its 32x32 tile across the border (<= 128 per tile) or starts a tree's list
+    return (size_t)((W + TL - 1) / TL) * ((H + TL - 1) / TL) * 129 + (size_t)K + 1;
+}
+
 hipError_t pf_bfs(hipStream_t st, PfView& v, int K, int* out) {
     const int N = v.N;
-    hipError_t e0 = hipMemsetAsync(v.tot, 0, 8 * 4, st);
-    if (e0 != hipSuccess) return e0;
-    hipLaunchKernelGGL(k_pf_bfs, dim3(1), dim3(BT), 0, st, v, K);
-    hipLaunchKernelGGL(k_pf_iota, dim3(nblk(N, 256)), dim3(256), 0, st, v.iota, N);
-    size_t tb = v.temp_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(v.temp, tb, v.gtree, v.gtree_s, v.iota, v.bglob, N, 0, bits_for(K), st);
+    out[0] = out[1] = out[2] = 0;
+    hipError_t e = hipMemsetAsync(v.tot, 0, 16 * 4, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pf_g2b, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+    // a forest of N nodes in K trees has N - K edges; anything else has a cycle, whose tour would not
+    // be a list (the chain ranking would never reach an end): refuse before any tour
+    hipLaunchKernelGGL(k_pf_edges, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+    int32_t E = 0;
+    if ((e = hipMemcpyAsync(&E, v.tot + 8, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (E != N - K) {
+        out[2] = 1;
+        return hipSuccess;
+    }
+    const int dbits = bits_for(N), tbits = bits_for(K);
+    if (N - K > 0) {
+        hipLaunchKernelGGL(k_pf_rot1, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+        if ((e = pf_tour(st, v)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_pf_orient, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+        hipLaunchKernelGGL(k_pf_rot2, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+        if ((e = pf_tour(st, v)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_pf_tourval, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+        size_t tb = v.temp_bytes;
+        if ((e = hipcub::DeviceScan::InclusiveSum(v.temp, tb, v.tval, v.tval_s, 2 * (N - K), st)) != hipSuccess) return e;
+    } else {  // single-pixel trees only: no arcs, every node a root
+        if ((e = hipMemsetAsync(v.pdir, 0xFF, (size_t)N, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_pf_fill1, dim3(nblk(N, 256)), dim3(256), 0, st, v.psize, N);
+    }
+    hipLaunchKernelGGL(k_pf_depth, dim3(nblk(N, 256)), dim3(256), 0, st, v, dbits);
+    {
+        size_t tb = v.temp_bytes;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(v.temp, tb, v.tkey[0], v.tkey[1], v.tpix[0], v.gpix, N, 0, tbits + dbits,
+                                                    st)) != hipSuccess)
+            return e;
+    }
+    hipLaunchKernelGGL(k_pf_bpos, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+    hipLaunchKernelGGL(k_pf_fields, dim3(nblk(N, 256)), dim3(256), 0, st, v);
+    // the BFS order is final: identity maps where the round-4 build sorted the level order by tree
+    hipLaunchKernelGGL(k_pf_iota, dim3(nblk(N, 256)), dim3(256), 0, st, v.bglob, N);
+    hipLaunchKernelGGL(k_pf_iota, dim3(nblk(N, 256)), dim3(256), 0, st, v.g2b, N);
+    if ((e = hipMemcpyAsync(v.gtree_s, v.gtree, (size_t)N * 4, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+    size_t tb;
     hipLaunchKernelGGL(k_pf_nodes, dim3(nblk(N, 256)), dim3(256), 0, st, v);
     int c = 0;
     for (int it = 0; it < 24; ++it, c ^= 1)  // 2^24 > any depth of a <= 2^24-pixel image
@@ -801,7 +790,7 @@ hipError_t pf_bfs(hipStream_t st, PfView& v, int K, int* out) {
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
     out[0] = h[5];  // rounds
     out[1] = h[6];  // heads
-    out[2] = h[7];  // 1: the masks were not a forest
+    out[2] = h[7];  // 2: an unresolved light depth, 4: an inconsistent tour (1, above: not a forest)
     return hipGetLastError();
 }
 
