@@ -80,7 +80,7 @@ struct PinnedVec {
 // buffers of the GPU forest build (sm_pms_forest.hip), kept between calls
 struct PfBufs {
     DevBuf par, flag, tree_of, nbr, nbw, root_pix, tsize, gpix, gpar, gtree, gw, gfc, gnc, gsize, ghk, iota, rot, pdir, psize,
-        bpos, a_dist, a_cid, a_head, nchains, c_last, c_len, c_head, cnw, tval, tval_s, tkey0, tkey1, tpix0, tpix1,
+        bpos, a_dist, a_cid, nchains, c_last, c_len, cnw, tval, tval_s, tkey0, tkey1, tpix0, tpix1,
         bglob, gtree_s, g2b, bpar, bch0, J0, J1, D0, D1, plen, ld, rowof, rowstart, hflag, hidx, hkey0, hkey1, cutof,
         hcnt[4], hoff[4], rtc[4], rt[4], pairs0, pairs1, npairs, uflag, uidx, nbcnt, cut_round, tree_cut, tot, temp;
 };
@@ -106,10 +106,8 @@ struct SegGpu {
     size_t stemp_bytes = 0;
     uint32_t gen = 0;  // next Boruvka generation (keys of older ones lose every atomicMin)
     PinnedVec<uint32_t> h_b, h_cnt, h_hooks, h_lsize, h_lroot;
-    PinnedVec<SegMin> h_min;
     PinnedVec<SegEdge> h_dense;
     std::vector<SegEdge> h_dsort;  // seg_sort_dense's scratch
-    std::vector<uint32_t> loc;         // SM_SEG_NODEDUP's root -> local id table (all ~0 between calls)
     std::vector<uint32_t> mpar, msize;  // the merge's union-find over local ids
 };
 
@@ -130,13 +128,9 @@ struct sm_ctx {
     // ~30 us cross-stream join and the throughput-bound k_up_pre only competes with the walkers --
     // so it aliases st; the round code keeps the two-stream structure (join() is then a no-op).
     hipStream_t st2 = nullptr;
-    // A/B (env SM_TREE_STREAM=1): sm_match_begin's prep / MST / layout on st_tree, a lower-priority
-    // stream, with st (the filter) waiting for the layout by event, so that with frames in flight
-    // the filter's launches dispatch ahead of the other frames' tree kernels.  Measured slower
-    // (C2 4.82 -> 5.43-5.50 ms/frame, N = 8 share 2.28 -> 2.90 ms; GPU_MAX_HW_QUEUES=8 the same):
-    // nullptr by default, everything on st.
-    hipStream_t st_tree = nullptr;
-    hipEvent_t ev_enq = nullptr;  // recorded on st at sm_match_begin: st_tree waits for it
+    // Everything of a call runs on st.  A tree stream of its own (prep / MST / layout, the filter
+    // waiting by event) was measured slower at either priority: the tree at the lowest priority, C2
+    // 4.82 -> 5.43-5.50 ms/frame (round 2); at the highest, 4.80-4.82 -> 5.12-5.16 (round 5).
     std::string err;
     int W = 0, H = 0, stride = 0;
     DevBuf img[2], bgrx[2], gray[2], med[2], wR[2], wD[2], comp[2], best[2], root[2], mR[2], mD[2];
@@ -172,9 +166,9 @@ struct sm_ctx {
     DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
     uint32_t epoch = 0;      // bumped per filter call; status words are zeroed only on (re)allocation
     // GPU layout buffers (sm_layout_gpu.hip)
-    DevBuf adj[2], pdir[2], heavy[2], size[2], off_in[2], light_in[2], pre[2], ld[2];
-    DevBuf a_dist[2], a_cid[2], a_head[2], arank[2], ccount[2], c_last[2], c_len[2], c_head[2];
-    DevBuf segtab[2], pathpos[2], plen[2], nslot[2], slotpix[2], slot2pix[2], prec[2];
+    DevBuf adj[2], pdir[2], heavy[2], size[2], rio[2], pre[2], ld[2];
+    DevBuf a_dist[2], a_cid[2], ccount[2], c_last[2], c_len[2];
+    DevBuf segtab[2], pathpos[2], plen[2], slotpix[2], slot2pix[2], prec[2];
     DevBuf pieces[2], pieces_tmp[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
     DevBuf cnw[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
     int* h_changed = nullptr;
@@ -217,10 +211,6 @@ struct sm_ctx {
     DevBuf pms_dice, pms_rnd, pms_evals;
     hipStream_t st_pms = nullptr;  // view 1's MST_PMS calls (view 0's run on st), created on first use
     hipEvent_t ev_pms = nullptr;
-    // per view: the stream a round's chain launch runs on, concurrently with the round's walkers (pms_phase)
-    hipStream_t st_pms_chain[2] = {nullptr, nullptr};
-    hipEvent_t ev_pms_fork[2] = {nullptr, nullptr}, ev_pms_join[2] = {nullptr, nullptr};
-    bool pms_chain_on = false;  // this call uses them (SM_PMS_CHAIN_STREAM != 0)
     long long pms_dice_n = 0;  // dice values on the device (the stream prefix every call replays)
     std::vector<float> pms_init;   // random plane labels of (W, H, Dmax) (both views start from them)
     int pms_init_key[3] = {0, 0, 0};
@@ -486,8 +476,6 @@ bool seg_host() { return getenv("SM_SEG_HOST") != nullptr; }
 // bit 1: before each whole-GPU bucket as well; 0: never
 int seg_flatten() { return getenv("SM_SEG_FLATTEN") ? atoi(getenv("SM_SEG_FLATTEN")) : 1; }
 
-// SM_SEG_NODEDUP=1: the min-size merge over every candidate (A/B of the GPU pair dedupe)
-bool seg_nodedup() { return getenv("SM_SEG_NODEDUP") != nullptr; }
 // a small-bucket run starts with k_seg_split (SM_SEG_NOSPLIT=1: every edge of the run through k_seg_small)
 bool seg_split() { return getenv("SM_SEG_NOSPLIT") == nullptr; }
 
@@ -500,52 +488,6 @@ int seg_global_rounds() { return getenv("SM_SEG_GLOBAL_ROUNDS") ? atoi(getenv("S
 // env SM_SEG_SMALL, default 16384)
 uint32_t seg_small() { return getenv("SM_SEG_SMALL") ? (uint32_t)atoi(getenv("SM_SEG_SMALL")) : 16384u; }
 
-// The reference's min-size merge (Stereo3DMST.cpp:293-307) over the rejected edges that have an end
-// smaller than ms after the sweep, in (w, id) order: the serial rule on a union-find of the sweep's
-// roots.  Emits the hooks (child root, parent root) and the joined edge ids for k_seg_apply.  The
-// candidates arrive sorted (k_seg_gather); roots map to dense local ids through a direct table (loc,
-// N entries, all ~0 on entry and on return).
-int seg_minsize_host(const SegMin* e, uint32_t n, uint32_t ms, uint32_t* out, std::vector<uint32_t>& loc) {
-    std::vector<uint32_t> par, size, root;
-    par.reserve(2 * (size_t)n);
-    size.reserve(2 * (size_t)n);
-    root.reserve(2 * (size_t)n);
-    auto local = [&](uint32_t r, uint32_t s) {
-        uint32_t& l = loc[r];
-        if (l == 0xFFFFFFFFu) {
-            l = (uint32_t)par.size();
-            par.push_back(l);
-            size.push_back(s);
-            root.push_back(r);
-        }
-        return l;
-    };
-    auto find = [&](uint32_t x) {
-        while (par[x] != x) x = par[x] = par[par[x]];
-        return x;
-    };
-    std::vector<uint32_t> ids;
-    int k = 0;
-    for (uint32_t j = 0; j < n; ++j) {
-        const SegMin& m = e[j];
-        uint32_t a = find(local(m.ra, m.sa)), b = find(local(m.rb, m.sb));
-        if (a == b || (size[a] >= ms && size[b] >= ms)) continue;
-        if (size[a] < size[b]) std::swap(a, b);
-        par[b] = a;
-        size[a] += size[b];
-        out[2 * k] = root[b];
-        out[2 * k + 1] = root[a];
-        ids.push_back(m.id);
-        ++k;
-    }
-    for (int i = 0; i < k; ++i) out[2 * k + i] = ids[i];
-    for (uint32_t r : root) loc[r] = 0xFFFFFFFFu;
-    return k;
-}
-
-// The same serial rule over the deduplicated candidates (seg_launch_dedupe): the first candidate of each
-// pair of sweep roots, in (w, id) order, with the roots as dense local ids (lsize / lroot: their sizes
-// and pixels).  Same hooks and marked edges as seg_minsize_host over all candidates.
 // the hashed pair dedupe's kept candidates (unordered) into the merge's (w, id) order: LSD radix sort of the
 // key (w << 32) | id in four 11-bit digits (w < 2^10, id < 2^23 for images below 4.19 M pixels; the full
 // 42 bits otherwise) -- ~23k edges per C2 view, well under 0.1 ms
@@ -576,6 +518,10 @@ void seg_sort_dense(SegEdge* e, uint32_t n, std::vector<SegEdge>& tmp) {
     if (src != e) std::copy(src, src + n, e);
 }
 
+// The reference's min-size merge (Stereo3DMST.cpp:293-307) over the deduplicated candidates (the first
+// candidate of each pair of sweep roots, in (w, id) order, with the roots as dense local ids; lsize /
+// lroot: their sizes and pixels): the serial rule on a union-find.  Emits the hooks (child root, parent
+// root) and the joined edge ids for k_seg_apply.
 int seg_minsize_dense(const SegEdge* e, uint32_t n, uint32_t nl, const uint32_t* lsize, const uint32_t* lroot, uint32_t ms,
                       uint32_t* out, std::vector<uint32_t>& par, std::vector<uint32_t>& size) {
     par.resize(nl);
@@ -622,7 +568,6 @@ double now_ms();
 // the h_w / h_m / h_fw host arrays as well (MST_PMS, sm_build_tree_p).
 sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_copy) {
     static const bool dbg = getenv("SM_SEG_DEBUG") != nullptr;
-    const bool nodedup = seg_nodedup();
     const int flatten = seg_flatten();
     const double t0 = dbg ? now_ms() : 0.0;
     double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
@@ -797,15 +742,16 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         SegGpu& g = ctx->sg[vs.v[i]];
         if (g.h_cnt[SM_SEG_C_ERR]) return fail(ctx, SM_ERR_STATE, "segment mode: a Boruvka tail did not converge");
         const uint32_t nm = g.h_cnt[SM_SEG_C_MIN];
-        if ((nodedup && !g.h_min.resize(nm)) || !g.h_hooks.resize(3 * (size_t)nm + 1))
+        if (!g.h_hooks.resize(3 * (size_t)nm + 1))
             return fail(ctx, SM_ERR_OOM, "segment mode: pinned host buffers");
         sp.v[i].nmin = nm;
         temp[i] = g.stemp.p;
         tbytes[i] = g.stemp_bytes;
     }
-    // the pair dedupe by hashing (default): no sort of the ~260k candidates; SM_SEG_SORTDEDUP=1 sorts them
+    // the pair dedupe by hashing: no sort of the ~260k candidates (round 4: the sorts cost 0.55 ms of
+    // kernels plus their gaps); a table that would not fit the key buffers sorts them instead
     uint32_t hcap = 0;
-    if (!nodedup && !getenv("SM_SEG_SORTDEDUP")) {
+    {
         uint32_t nmax = 0;
         for (int i = 0; i < vs.n; ++i) nmax = std::max(nmax, sp.v[i].nmin);
         hcap = 1024;
@@ -813,13 +759,7 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
         if ((size_t)hcap > E) hcap = 0;  // (the table lives in the E-entry key buffers)
     }
     if (!hcap) HIPC(seg_launch_sort(st, sp, temp, tbytes));
-    if (nodedup) {
-        for (int i = 0; i < vs.n; ++i) {
-            SegGpu& g = ctx->sg[vs.v[i]];
-            if (sp.v[i].nmin)
-                HIPC(hipMemcpyAsync(g.h_min.data(), g.msorted.p, sp.v[i].nmin * sizeof(SegMin), hipMemcpyDeviceToHost, st));
-        }
-    } else {  // the first candidate of each root pair, dense root ids: their counts, then the lists
+    {  // the first candidate of each root pair, dense root ids: their counts, then the lists
         if (hcap)
             HIPC(seg_launch_dedupe_hash(st, sp, temp, tbytes, hcap));
         else
@@ -846,14 +786,11 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
     const uint32_t ms = (uint32_t)(min_size < 2 ? 2 : min_size);
     int nk[2] = {0, 0};
     {  // the views' merges in parallel
-        auto merge = [ctx, ms, N, nodedup, hcap](int v) {
+        auto merge = [ctx, ms, hcap](int v) {
             SegGpu& g = ctx->sg[v];
             if (hcap) seg_sort_dense(g.h_dense.data(), g.h_cnt[SM_SEG_C_UNIQ], g.h_dsort);  // hashed: unordered
-            if (!nodedup)
-                return seg_minsize_dense(g.h_dense.data(), g.h_cnt[SM_SEG_C_UNIQ], g.h_cnt[SM_SEG_C_LOCAL], g.h_lsize.data(),
-                                         g.h_lroot.data(), ms, g.h_hooks.data(), g.mpar, g.msize);
-            if (g.loc.size() != N) g.loc.assign(N, 0xFFFFFFFFu);
-            return seg_minsize_host(g.h_min.data(), g.h_cnt[SM_SEG_C_MIN], ms, g.h_hooks.data(), g.loc);
+            return seg_minsize_dense(g.h_dense.data(), g.h_cnt[SM_SEG_C_UNIQ], g.h_cnt[SM_SEG_C_LOCAL], g.h_lsize.data(),
+                                     g.h_lroot.data(), ms, g.h_hooks.data(), g.mpar, g.msize);
         };
         std::thread other;
         if (vs.n > 1) other = std::thread([&] { nk[1] = merge(vs.v[1]); });
@@ -1091,18 +1028,14 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->pdir[v], N));
         CHECK(ensure(ctx, ctx->heavy[v], N));
         CHECK(ensure(ctx, ctx->size[v], N * 4));
-        CHECK(ensure(ctx, ctx->off_in[v], N * 4));
-        CHECK(ensure(ctx, ctx->light_in[v], N));
+        CHECK(ensure(ctx, ctx->rio[v], N * 8));
         CHECK(ensure(ctx, ctx->pre[v], N * 4));
         CHECK(ensure(ctx, ctx->ld[v], N * 4));
         CHECK(ensure(ctx, ctx->a_dist[v], 4 * N * 2));
         CHECK(ensure(ctx, ctx->a_cid[v], 4 * N * 4));
-        CHECK(ensure(ctx, ctx->a_head[v], 4 * N * 4));
-        CHECK(ensure(ctx, ctx->arank[v], 4 * N * 4));
         CHECK(ensure(ctx, ctx->ccount[v], 16));
         CHECK(ensure(ctx, ctx->c_last[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->c_len[v], max_chains * 4));
-        CHECK(ensure(ctx, ctx->c_head[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->cnw[v], max_chains * 8));
         CHECK(ensure(ctx, ctx->tour[v], 2 * N * 8 + 16));
         CHECK(ensure(ctx, ctx->bsum[v], nscan * 8));
@@ -1117,7 +1050,6 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->pieces_tmp[v], (N / 16 + 64) * sizeof(uint4)));
         CHECK(ensure(ctx, ctx->pathpos[v], N * 4));
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
-        CHECK(ensure(ctx, ctx->nslot[v], N * 4));
         CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
         CHECK(ensure(ctx, ctx->slot2pix[v], N * 4));
         CHECK(ensure(ctx, ctx->prec[v], N * 8));
@@ -1133,18 +1065,14 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.pdir = P<int8_t>(ctx->pdir[v]);
         L.heavy = P<int8_t>(ctx->heavy[v]);
         L.size = P<uint32_t>(ctx->size[v]);
-        L.off_in = P<uint32_t>(ctx->off_in[v]);
-        L.light_in = P<uint8_t>(ctx->light_in[v]);
+        L.rio = P<uint2>(ctx->rio[v]);
         L.pre = P<uint32_t>(ctx->pre[v]);
         L.ld = P<uint32_t>(ctx->ld[v]);
         L.a_dist = P<uint16_t>(ctx->a_dist[v]);
         L.a_cid = P<uint32_t>(ctx->a_cid[v]);
-        L.a_head = P<uint32_t>(ctx->a_head[v]);
-        L.rank = P<uint32_t>(ctx->arank[v]);
         L.nchains = P<uint32_t>(ctx->ccount[v]);
         L.c_last = P<uint32_t>(ctx->c_last[v]);
         L.c_len = P<uint32_t>(ctx->c_len[v]);
-        L.c_head = P<uint32_t>(ctx->c_head[v]);
         L.cnw = P<uint64_t>(ctx->cnw[v]);
         L.tour = P<long long>(ctx->tour[v]);
         L.bsum = P<long long>(ctx->bsum[v]);
@@ -1155,7 +1083,6 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.paths = P<SmPath>(ctx->paths[v]);
         L.pathpos = P<uint32_t>(ctx->pathpos[v]);
         L.plen = P<uint32_t>(ctx->plen[v]);
-        L.nslot = P<uint32_t>(ctx->nslot[v]);
         L.slotpix = P<uint32_t>(ctx->slotpix[v]);
         L.slot2pix = P<uint32_t>(ctx->slot2pix[v]);
         L.prec = P<uint64_t>(ctx->prec[v]);
@@ -1673,12 +1600,6 @@ bool pms_serial_only() {
     const char* e = getenv("SM_PMS_SERIAL");
     return e && atoi(e) == 1;
 }
-// SM_PMS_REPASS=1: a stale-input failure also restores and re-speculates every later tree (A/B of
-// the single-tree fix)
-bool pms_repass() {
-    const char* e = getenv("SM_PMS_REPASS");
-    return e && atoi(e) == 1;
-}
 int pms_max_rounds() {
     const char* e = getenv("SM_PMS_MAX_ROUNDS");
     return e ? std::max(1, atoi(e)) : 8;
@@ -1865,30 +1786,25 @@ long long pms_big_tree() {
 // down rounds root first (repaired likewise), then the per-pixel update.
 sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int phase, int t_lo, int t_hi) {
     const PmsForest& f = ctx->pms[v].f;
-    // the phase's A rows packed by its proposal counts (k_pms_layout; SM_PMS_STATIC_ROWS=1: the static
-    // max-degree layout, A/B)
+    // the phase's A rows packed by its proposal counts (k_pms_layout; round 4: 1.2 GB of static max-degree
+    // rows per phase at C2 before)
     PmsDev d = d0;
     const size_t K1 = (size_t)f.K + 1;
     int R = 0;
     for (int t = t_lo; t < t_hi; ++t) R = std::max(R, f.tree_rounds[t]);
-    const bool packed = !(getenv("SM_PMS_STATIC_ROWS") && atoi(getenv("SM_PMS_STATIC_ROWS")) == 1);
-    if (packed) {  // (the layout launch also zeroes the plan's counters)
-        HIPC(launch_pms_layout(st, d0, phase, t_lo, t_hi, P<int32_t>(ctx->pms[v].pt_ph), P<long long>(ctx->pms[v].ab_ph),
-                               d0.plan_cnt, PMS_NCNT * R));
-        d.tree_pt = P<int32_t>(ctx->pms[v].pt_ph);
-        d.tree_abase = P<long long>(ctx->pms[v].ab_ph);
-    }
+    // (the layout launch also zeroes the plan's counters)
+    HIPC(launch_pms_layout(st, d0, phase, t_lo, t_hi, P<int32_t>(ctx->pms[v].pt_ph), P<long long>(ctx->pms[v].ab_ph),
+                           d0.plan_cnt, PMS_NCNT * R));
+    d.tree_pt = P<int32_t>(ctx->pms[v].pt_ph);
+    d.tree_abase = P<long long>(ctx->pms[v].ab_ph);
     const std::vector<int32_t>& rt = phase == 0 ? f.rt_item : f.rt_path;
     HIPC(launch_pms_cost(st, d, phase, f.tree_start[t_lo], f.tree_start[t_hi]));
-    const bool wave_walk = getenv("SM_PMS_WAVE_WALK") && atoi(getenv("SM_PMS_WAVE_WALK")) == 1;
     // planned walks (k_pms_plan / k_pms_walk_plan): the round's paths in lane-group classes by their
-    // tree's proposal count, over a persistent grid of at most PMS_WALK_WAVES waves; SM_PMS_WAVE_WALK=1:
-    // one wave per (path, 64-proposal chunk) item, the round-3 walker (A/B)
+    // tree's proposal count, over a persistent grid of at most PMS_WALK_WAVES waves (round 4; one wave per
+    // (path, 64-proposal chunk) item before)
     constexpr int PMS_WALK_WAVES = 16384;
     std::vector<int> bound(std::max(R, 1), 0);
-    // SM_PMS_NO_CHAIN=1: long paths on the wave walker too (A/B of k_pms_chain)
-    const bool chains = !(getenv("SM_PMS_NO_CHAIN") && atoi(getenv("SM_PMS_NO_CHAIN")) == 1);
-    if (!wave_walk) {
+    {
         int maxp = 0;
         for (int r = 0; r < R; ++r) {
             const int np = f.rt_path[r * K1 + t_hi] - f.rt_path[r * K1 + t_lo];
@@ -1896,40 +1812,26 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
             // virtual tasks: at most one per path of the classes, plus the chunks of the rest
             bound[r] = std::min(PMS_WALK_WAVES, np + (phase == 0 ? rt[r * K1 + t_hi] - rt[r * K1 + t_lo] : 0));
         }
-        // SM_PMS_CHAIN_MIN: the chain threshold (at least SM_PMS_CHAIN_LEN, whose counts bound the grid)
+        // SM_PMS_CHAIN_MIN: the chain threshold (at least SM_PMS_CHAIN_LEN, whose counts bound the grid;
+        // tests lower it to put more chain items on small images)
         const char* cm = getenv("SM_PMS_CHAIN_MIN");
-        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, chains ? (cm ? atoi(cm) : SM_PMS_CHAIN_DEFAULT) : 0, packed));
+        HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, cm ? atoi(cm) : SM_PMS_CHAIN_DEFAULT, true));
     }
-    // pieces: every guessed piece repairs at once, then a gated sequential pass (SM_PMS_SEQ_REPAIR=1: the
-    // sequential pass alone, A/B); maxp[r] = the most pieces of a cut repaired in round r
-    const bool seq_repair = getenv("SM_PMS_SEQ_REPAIR") && atoi(getenv("SM_PMS_SEQ_REPAIR")) == 1;
+    // pieces: every guessed piece repairs at once, then a gated sequential pass; maxp[r] = the most pieces
+    // of a cut repaired in round r
     std::vector<int> maxp(std::max(R, 1), 0);
-    if (!seq_repair)
-        for (int r = 0; r < R; ++r)
-            for (int k = f.rt_rep[r * K1 + t_lo]; k < f.rt_rep[r * K1 + t_hi]; ++k)
-                maxp[r] = std::max(maxp[r], f.cuts[f.reps[k].cut].npieces);
+    for (int r = 0; r < R; ++r)
+        for (int k = f.rt_rep[r * K1 + t_lo]; k < f.rt_rep[r * K1 + t_hi]; ++k)
+            maxp[r] = std::max(maxp[r], f.cuts[f.reps[k].cut].npieces);
     // chain items (paths / pieces of >= SM_PMS_CHAIN_LEN rows, k_pms_chain): the host's bound per round
     std::vector<int> nlong(std::max(R, 1), 0);
-    if (!wave_walk && chains)
-        for (int r = 0; r < R; ++r) nlong[r] = f.rt_long[r * K1 + t_hi] - f.rt_long[r * K1 + t_lo];
-    // a round's chain items and walker tasks are disjoint paths whose inputs are final: with
-    // SM_PMS_CHAIN_STREAM=1 the chain launch runs on the view's chain stream beside the walkers (fork / join
-    // events; slower at C2, see stage_pms), otherwise one after the other on the view's stream
-    const hipStream_t sc = ctx->pms_chain_on ? ctx->st_pms_chain[v] : nullptr;
+    for (int r = 0; r < R; ++r) nlong[r] = f.rt_long[r * K1 + t_hi] - f.rt_long[r * K1 + t_lo];
+    // a round's chain items and walker tasks are disjoint paths whose inputs are final; one after the
+    // other on the view's stream (a chain stream beside the walkers cost more in event fork / join than
+    // the overlap won: 960 against 670 ms per 100-call frame, round 4)
     auto round = [&](int r, bool up) -> sm_status {
-        if (wave_walk) {
-            HIPC(launch_pms_walk(st, d, phase, up, r, rt[r * K1 + t_lo], rt[r * K1 + t_hi]));
-        } else if (sc && nlong[r] > 0 && bound[r] > 0) {
-            HIPC(hipEventRecord(ctx->ev_pms_fork[v], st));
-            HIPC(hipStreamWaitEvent(sc, ctx->ev_pms_fork[v], 0));
-            HIPC(launch_pms_chain(sc, d, phase, up, r, nlong[r]));
-            HIPC(launch_pms_walk_plan(st, d, phase, up, r, bound[r]));
-            HIPC(hipEventRecord(ctx->ev_pms_join[v], sc));
-            HIPC(hipStreamWaitEvent(st, ctx->ev_pms_join[v], 0));
-        } else {
-            HIPC(launch_pms_chain(st, d, phase, up, r, nlong[r]));
-            HIPC(launch_pms_walk_plan(st, d, phase, up, r, bound[r]));
-        }
+        HIPC(launch_pms_chain(st, d, phase, up, r, nlong[r]));
+        HIPC(launch_pms_walk_plan(st, d, phase, up, r, bound[r]));
         HIPC(launch_pms_repair(st, d, phase, up, f.rt_rep[r * K1 + t_lo], f.rt_rep[r * K1 + t_hi], maxp[r]));
         return SM_OK;
     };
@@ -1940,8 +1842,6 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
     return SM_OK;
 }
 
-// SM_PMS_NODEDUP=1: propagation over every sampled label, repeats included (A/B of k_pms_prop_dedupe)
-bool pms_dedupe() { return getenv("SM_PMS_NODEDUP") == nullptr; }
 
 // Trees [t0, t1) in the reference's order from the dice offset *off.  Runs of small trees go to one
 // workgroup (k_pms_serial); a large tree's phases are launched over the whole GPU, round by round.
@@ -1959,7 +1859,7 @@ sm_status pms_serial_range(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, 
         }
         if (t < t1 && !is_big) continue;
         HIPC(launch_pms_serial(st, d, run, t));
-        if (pms_dedupe() && t > run) {  // the run's distinct propagation counts (nprop: k_pms_count's input)
+        if (t > run) {  // the run's distinct propagation counts (nprop: k_pms_count's input)
             PmsDev dd = d;
             dd.labu = P<float4>(ctx->pms[v].labu);
             dd.nprop = P<int32_t>(ctx->pms[v].nprop);
@@ -1969,26 +1869,22 @@ sm_status pms_serial_range(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, 
         if (t == t1) break;
         const int deg = f.nb_start[t + 1] - f.nb_start[t];
         HIPC(launch_pms_prop_one(st, d, t, deg));
-        if (deg > 0 && pms_dedupe()) {  // over the tree's distinct propagation labels (k_pms_prop_dedupe)
+        if (deg > 0) {  // over the tree's distinct propagation labels (k_pms_prop_dedupe)
             PmsDev dd = d;
             dd.labu = P<float4>(ctx->pms[v].labu);
             dd.nprop = P<int32_t>(ctx->pms[v].nprop);
             HIPC(launch_pms_prop_dedupe(st, dd, t, t + 1));
             dd.lab = dd.labu;
             CHECK(pms_phase(ctx, st, v, dd, 0, t, t + 1));
-        } else if (deg > 0) {
-            CHECK(pms_phase(ctx, st, v, d, 0, t, t + 1));
         }
         HIPC(launch_pms_ref_one(st, d, t));
         // a refinement that drew no in-range level (nref == 0, most of a first call's trees) has nothing to
         // walk: its ~20 launches would all be empty, so read the count back (the view's pinned result slot)
-        // and skip the phase (SM_PMS_REF_ALWAYS=1: always launch it, A/B)
+        // and skip the phase
         int32_t* h_nref = ctx->h_pms_res + 4 * v + 3;
-        if (!(getenv("SM_PMS_REF_ALWAYS") && atoi(getenv("SM_PMS_REF_ALWAYS")) == 1)) {
-            HIPC(hipMemcpyAsync(h_nref, P<int32_t>(ctx->pms[v].nref) + t, 4, hipMemcpyDeviceToHost, st));
-            HIPC(hipStreamSynchronize(st));
-            if (*h_nref == 0) continue;
-        }
+        HIPC(hipMemcpyAsync(h_nref, P<int32_t>(ctx->pms[v].nref) + t, 4, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        if (*h_nref == 0) continue;
         CHECK(pms_phase(ctx, st, v, d, 1, t, t + 1));
     }
     return SM_OK;
@@ -2035,14 +1931,12 @@ sm_status pms_speculative_call(sm_ctx* ctx, PmsRun& run, int v, PmsDev& d) {
                 (long long)(f.nb_start[K] - f.nb_start[t_lo]) + 4ll * sm_pms_levels(d.Dmax) * (K - t_lo) + 8;
             HIPC(launch_pms_guess(st, d, t_lo, wn));
             HIPC(launch_pms_prop_setup(st, d, t_lo, f.nb_start[K] - f.nb_start[t_lo]));
-            if (pms_dedupe()) {  // propagation over each tree's distinct labels (k_pms_prop_dedupe)
+            {  // propagation over each tree's distinct labels (k_pms_prop_dedupe)
                 PmsDev dd = d;
                 dd.nprop = P<int32_t>(S.nprop);
                 HIPC(launch_pms_prop_dedupe(st, dd, t_lo, K));  // lab -> labu
                 dd.lab = P<float4>(S.labu);                        // the phase reads the distinct labels
                 CHECK(pms_phase(ctx, st, v, dd, 0, t_lo, K));
-            } else {
-                CHECK(pms_phase(ctx, st, v, d, 0, t_lo, K));
             }
             HIPC(launch_pms_ref_setup(st, d, t_lo));
             CHECK(pms_phase(ctx, st, v, d, 1, t_lo, K));
@@ -2054,7 +1948,7 @@ sm_status pms_speculative_call(sm_ctx* ctx, PmsRun& run, int v, PmsDev& d) {
         if (ts < t_lo || ts > K || (ts < K && why != 1 && why != 2))
             return fail(ctx, SM_ERR_STATE, "MST_PMS validation returned a bad tree index");
         if (ts == K) break;
-        pass = why == 1 || pms_repass();
+        pass = why == 1;
         HIPC(launch_pms_restore(st, d, f.tree_start[ts], pass ? (int)N : f.tree_start[ts + 1]));
         HIPC(hipMemcpyAsync(S.off.p, P<int32_t>(S.result) + 2, 8, hipMemcpyDeviceToDevice, st));
         PmsDev dk = d;
@@ -2099,7 +1993,7 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
         {&B.gnc, n1, (void**)&pv.gnc}, {&B.gsize, n1 * 4, (void**)&pv.gsize}, {&B.ghk, n1, (void**)&pv.ghk},
         {&B.iota, n1 * 4, (void**)&pv.iota}, {&B.rot, n1 * 4, (void**)&pv.rot}, {&B.pdir, n1, (void**)&pv.pdir},
         {&B.psize, n1 * 4, (void**)&pv.psize}, {&B.bpos, n1 * 4, (void**)&pv.bpos}, {&B.a_dist, 4 * n1 * 2, (void**)&pv.a_dist},
-        {&B.a_cid, 4 * n1 * 4, (void**)&pv.a_cid}, {&B.a_head, 4 * n1 * 4, (void**)&pv.a_head},
+        {&B.a_cid, 4 * n1 * 4, (void**)&pv.a_cid},
         {&B.nchains, 16, (void**)&pv.nchains}, {&B.tval, 2 * n1 * 8, (void**)&pv.tval}, {&B.tval_s, 2 * n1 * 8, (void**)&pv.tval_s},
         {&B.tkey0, n1 * 8, (void**)&pv.tkey[0]}, {&B.tkey1, n1 * 8, (void**)&pv.tkey[1]}, {&B.tpix0, n1 * 4, (void**)&pv.tpix[0]},
         {&B.tpix1, n1 * 4, (void**)&pv.tpix[1]},
@@ -2136,11 +2030,9 @@ sm_status pms_forest_gpu(sm_ctx* ctx, int v, hipStream_t st, int piece) {
     const size_t mch = pf_max_chains(W, H, K);
     CHECK(ensure(ctx, B.c_last, mch * 4));
     CHECK(ensure(ctx, B.c_len, mch * 4));
-    CHECK(ensure(ctx, B.c_head, mch * 4));
     CHECK(ensure(ctx, B.cnw, mch * 8));
     pv.c_last = P<uint32_t>(B.c_last);
     pv.c_len = P<uint32_t>(B.c_len);
-    pv.c_head = P<uint32_t>(B.c_head);
     pv.cnw = P<uint64_t>(B.cnw);
     pv.max_chains = (uint32_t)mch;
     int rb[3];
@@ -2294,17 +2186,6 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
             return fail(ctx, SM_ERR_HIP, "hipStreamCreateWithFlags (MST_PMS view stream)");
         }
     }
-    // measured at C2 (100 calls): 960 ms per frame with the chain stream, 670 without -- the per-round
-    // event fork / join costs more than the overlap wins -- so it is opt-in (SM_PMS_CHAIN_STREAM=1)
-    ctx->pms_chain_on = getenv("SM_PMS_CHAIN_STREAM") && atoi(getenv("SM_PMS_CHAIN_STREAM")) == 1;
-    for (int v = 0; v < 2 && ctx->pms_chain_on; ++v) {
-        if ((!ctx->st_pms_chain[v] && hipStreamCreateWithFlags(&ctx->st_pms_chain[v], hipStreamNonBlocking) != hipSuccess) ||
-            (!ctx->ev_pms_fork[v] && hipEventCreateWithFlags(&ctx->ev_pms_fork[v], hipEventDisableTiming) != hipSuccess) ||
-            (!ctx->ev_pms_join[v] && hipEventCreateWithFlags(&ctx->ev_pms_join[v], hipEventDisableTiming) != hipSuccess)) {
-            skip.join();
-            return fail(ctx, SM_ERR_HIP, "hipStreamCreateWithFlags (MST_PMS chain stream)");
-        }
-    }
     {
         auto host_build = [ctx, W, H, N](int v, PmsForest& f) {
             std::vector<uint8_t> mR(N), mD(N);
@@ -2406,18 +2287,17 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     st.setup_ms = t2 - t1;
     // 5. the MST_PMS calls: left view, then right (:858-889).  The two views share nothing but read-only
     // tables (each view's rand() values sit at fixed offsets of the precomputed stream, the dice prefix is
-    // replayed), so each view's calls run on a host thread and stream of their own, concurrently
-    // (SM_PMS_SEQ_VIEWS=1: one after the other, on st, for A/B).  Every call is timed; the node-label
+    // replayed), so each view's calls run on a host thread and stream of their own, concurrently (round
+    // 4: one after the other took 0.81 -> 0.67 s per 100-call frame).  Every call is timed; the node-label
     // evaluations each call needed are counted on the device (k_pms_count).
     const bool serial_only = pms_serial_only();
-    const bool seq_views = getenv("SM_PMS_SEQ_VIEWS") && atoi(getenv("SM_PMS_SEQ_VIEWS")) == 1;
     CHECK(ensure(ctx, ctx->pms_evals, 16 * 8));
     HIPC(hipMemsetAsync(ctx->pms_evals.p, 0, 16 * 8, ctx->st));
     HIPC(hipEventRecord(ctx->ev_pms, ctx->st));
     HIPC(hipStreamWaitEvent(ctx->st_pms, ctx->ev_pms, 0));  // view 1's stream after the set-up above
     PmsRun run[2];
     run[0].st = ctx->st;
-    run[1].st = seq_views ? ctx->st : ctx->st_pms;
+    run[1].st = ctx->st_pms;
     run[0].h_res = ctx->h_pms_res;
     run[1].h_res = ctx->h_pms_res + 4;
     const size_t roff0[2] = {0, (size_t)iters * K0};
@@ -2467,7 +2347,7 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
             }
             {  // the call's node-label evaluations (a speculative call with the dedupe: nprop holds the counts)
                 PmsDev dc = d;
-                dc.nprop = (i > 0 && !serial_only && pms_dedupe()) ? P<int32_t>(ctx->pms[v].nprop) : nullptr;
+                dc.nprop = (i > 0 && !serial_only) ? P<int32_t>(ctx->pms[v].nprop) : nullptr;
                 HIPC(launch_pms_count(st, dc, acc + (i == 0 ? 0 : 2)));
             }
             HIPC(hipStreamSynchronize(st));
@@ -2494,10 +2374,7 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     };
     const double tc0 = now_ms();
     sm_status rs[2] = {SM_OK, SM_OK};
-    if (seq_views) {
-        rs[0] = calls(run[0], 0);
-        if (rs[0] == SM_OK) rs[1] = calls(run[1], 1);
-    } else {
+    {
         auto guarded = [&](int v) {
             try {
                 rs[v] = calls(run[v], v);
@@ -2529,11 +2406,11 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipStreamSynchronize(ctx->st));
     // wall clock of the calls: the first calls of the views (the longer one), then the rest
     const double iter0 = std::max(run[0].first_ms, run[1].first_ms);
-    const double rest = seq_views ? run[0].later_ms + run[1].later_ms : (tc1 - tc0) - iter0;
+    const double rest = (tc1 - tc0) - iter0;
     st.spec_rounds = run[0].spec_rounds + run[1].spec_rounds;
     st.serial_trees = run[0].serial_trees + run[1].serial_trees;
     st.calls_ms = tc1 - tc0;
-    st.concurrent_views = seq_views ? 0 : 1;
+    st.concurrent_views = 1;
     for (int v = 0; v < 2; ++v) {
         st.first_ms_view[v] = run[v].first_ms;
         st.later_ms_view[v] = run[v].later_ms;
@@ -2627,28 +2504,7 @@ sm_status sm_create(sm_ctx** out, const sm_config* cfg) {
         delete ctx;
         return SM_ERR_HIP;
     }
-    ctx->st2 = ctx->st;
-    {
-        // 1: the tree on a lowest-priority stream, the filter highest; 2: the reverse (A/B)
-        const char* e = getenv("SM_TREE_STREAM");
-        if (e && (atoi(e) == 1 || atoi(e) == 2)) {
-            int least = 0, greatest = 0;
-            const bool hi_tree = atoi(e) == 2;
-            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
-                hipStreamDestroy(ctx->st) != hipSuccess ||
-                hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, hi_tree ? least : greatest) != hipSuccess ||
-                hipStreamCreateWithPriority(&ctx->st_tree, hipStreamNonBlocking, hi_tree ? greatest : least) != hipSuccess ||
-                hipEventCreateWithFlags(&ctx->ev_enq, hipEventDisableTiming) != hipSuccess) {
-                delete ctx;
-                return SM_ERR_HIP;
-            }
-            ctx->st2 = ctx->st;
-        }
-    }
-    if (getenv("SM_TWO_STREAMS") && hipStreamCreateWithFlags(&ctx->st2, hipStreamNonBlocking) != hipSuccess) {
-        delete ctx;
-        return SM_ERR_HIP;
-    }
+    ctx->st2 = ctx->st;  // (the chain engine's stream: an alias, see sm_ctx::st2)
     if (hipHostMalloc((void**)&ctx->h_err, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&ctx->d_err, ctx->h_err, 0) != hipSuccess) {
         delete ctx;
@@ -2689,7 +2545,6 @@ void sm_destroy(sm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->seg_worker.joinable()) ctx->seg_worker.join();  // a begun segment-mode call's host worker
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
-    if (ctx->st_tree) (void)hipStreamSynchronize(ctx->st_tree);  // tree kernels may still run there
     if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamSynchronize(ctx->st2);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* all[] = {&ctx->changed, &ctx->mst_ok, &ctx->atab, &ctx->slut, &ctx->s2lut, &ctx->post_mask, &ctx->post_scratch,
@@ -2730,12 +2585,6 @@ void sm_destroy(sm_ctx* ctx) {
     }
     if (ctx->ev_pms) (void)hipEventDestroy(ctx->ev_pms);
     for (int v = 0; v < 2; ++v) {
-        if (ctx->st_pms_chain[v]) {
-            (void)hipStreamSynchronize(ctx->st_pms_chain[v]);
-            (void)hipStreamDestroy(ctx->st_pms_chain[v]);
-        }
-        if (ctx->ev_pms_fork[v]) (void)hipEventDestroy(ctx->ev_pms_fork[v]);
-        if (ctx->ev_pms_join[v]) (void)hipEventDestroy(ctx->ev_pms_join[v]);
     }
     if (ctx->pms_rnd.p) (void)hipFree(ctx->pms_rnd.p);
     if (ctx->h_pms_res) (void)hipHostFree(ctx->h_pms_res);
@@ -2743,18 +2592,15 @@ void sm_destroy(sm_ctx* ctx) {
     if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
     for (int v = 0; v < 2; ++v) {
-        DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->off_in[v], &ctx->light_in[v],
-                         &ctx->pre[v], &ctx->ld[v], &ctx->a_dist[v], &ctx->a_cid[v], &ctx->a_head[v], &ctx->arank[v],
-                         &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->c_head[v], &ctx->cnw[v],
+        DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->rio[v],
+                         &ctx->pre[v], &ctx->ld[v], &ctx->a_dist[v], &ctx->a_cid[v],
+                         &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->cnw[v],
                          &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
                          &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
-                         &ctx->nslot[v], &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->prec[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
+                         &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->prec[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
-    if (ctx->st_tree) (void)hipStreamSynchronize(ctx->st_tree);
-    if (ctx->st_tree) (void)hipStreamDestroy(ctx->st_tree);
-    if (ctx->ev_enq) (void)hipEventDestroy(ctx->ev_enq);
     if (ctx->st2 && ctx->st2 != ctx->st) (void)hipStreamDestroy(ctx->st2);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     delete ctx;
@@ -2828,27 +2674,13 @@ static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipSetDevice(ctx->device));
     ctx->rec_pad = rec_pad_for(cr.d0, cr.D);
     ctx->sub = cr.w.sub != 0;
-    // the tree stages on st_tree (after everything enqueued on st so far: the image upload and the
-    // previous frame, whose buffers the tree overwrites); st waits for the layout's event
-    struct TreeStream {
-        sm_ctx* c;
-        hipStream_t main = nullptr;
-        ~TreeStream() { if (main) c->st = main; }
-    } ts{ctx};
-    // (the guided and MST_PMS aggregators run their whole call on st: no tree stream)
-    if (ctx->st_tree && p->aggregator == SM_AGG_TREE) {
-        HIPC(hipEventRecord(ctx->ev_enq, ctx->st));
-        HIPC(hipStreamWaitEvent(ctx->st_tree, ctx->ev_enq, 0));
-        ts.main = ctx->st;
-        ctx->st = ctx->st_tree;
-    }
     // timing experiments only (tools): with a layout of these images from an earlier frame,
     // SM_EXP_FILTER_ONLY=1 re-filters it without re-running prep / MST / layout (the filter's streaming
     // cost alone); SM_EXP_SKIP=mst keeps the previous MST (prep + layout + filter), SM_EXP_SKIP=layout
     // keeps the previous layout (prep + MST + filter): the tree stages' streaming cost, stage by stage
     static const bool exp_filter_only = getenv("SM_EXP_FILTER_ONLY") != nullptr;
     static const int exp_skip = getenv("SM_EXP_SKIP") ? (strcmp(getenv("SM_EXP_SKIP"), "mst") == 0 ? 1 : 2) : 0;
-    const bool exp_on = ctx->exp_layout_ok && !ts.main && p->aggregator == SM_AGG_TREE && std::isinf(p->c);
+    const bool exp_on = ctx->exp_layout_ok && p->aggregator == SM_AGG_TREE && std::isinf(p->c);
     if (exp_on && exp_skip) {
         HIPC(hipEventRecord(ctx->ev[0], ctx->st));
         CHECK(stage_prep(ctx));
@@ -2913,7 +2745,7 @@ static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
         ctx->pending = 2;
         return SM_OK;
     }
-    if (!std::isinf(p->c) && !ts.main && !seg_sync()) {
+    if (!std::isinf(p->c) && !seg_sync()) {
         // segment mode: the host segmentation on a worker thread, so begin returns at once and the
         // caller's other contexts keep the GPU busy; the worker uploads the forest and enqueues the
         // layout on this context's stream, and sm_match_finish joins it before using the layout
@@ -2953,11 +2785,6 @@ static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
     CHECK(stage_tree(ctx, ctx->views, p, false));
     HIPC(hipEventRecord(ctx->ev[2], ctx->st));
     CHECK(stage_layout_enqueue(ctx, ctx->views));
-    if (ts.main) {
-        ctx->st = ts.main;
-        ts.main = nullptr;
-        HIPC(hipStreamWaitEvent(ctx->st, ctx->ev_layout, 0));
-    }
     ctx->pending = 1;
     ctx->pend_D = D;
     ctx->pend_p = *p;

@@ -92,20 +92,16 @@ struct LayoutView {
     int8_t* pdir;       // direction to the parent (-1: root)
     int8_t* heavy;      // direction of the heavy child (-1: leaf)
     uint32_t* size;     // subtree size
-    uint32_t* off_in;   // heavy-first preorder offset within the parent
-    uint8_t* light_in;  // 1 if a light child
+    uint2* rio;         // tour ranks of the arcs parent -> pixel (x) and pixel -> parent (y)
     uint32_t* pre;      // heavy-first preorder (layout-internal numbering)
     uint32_t* ld;       // light depth
     // per arc (4N)
     uint16_t* a_dist;
     uint32_t* a_cid;
-    uint32_t* a_head;
-    uint32_t* rank;
     // per chain
     uint32_t* nchains;  // device counter
     uint32_t* c_last;
     uint32_t* c_len;
-    uint32_t* c_head;
     uint64_t* cnw;      // per chain: successor chain (low 32 bits) | arcs to it (high 32 bits)
     // tour (2N-2) + scan scratch
     long long* tour;
@@ -113,13 +109,12 @@ struct LayoutView {
     uint32_t* bsum32;
     // per slot
     SmMeta* meta;
-    uint32_t* headflag;
-    uint32_t* headpos;
+    uint32_t* headflag;  // [preorder] 0, or 1 + light depth at a path head
+    uint32_t* headpos;   // [preorder] 1 + the preorder of the head of its path (after the max-scan)
     // paths
     SmPath* paths;           // {head slot, len}, bucket-major; slots of a bucket are contiguous
     uint32_t* pathpos;       // [preorder of a head] -> index of its path in paths[]
     uint32_t* plen;          // [path] -> len, inclusive-scanned into the path's end slot
-    uint32_t* nslot;         // [preorder] -> slot
     uint32_t* slotpix;       // [pixel] -> slot
     uint32_t* slot2pix;      // [slot] -> pixel
     uint64_t* prec;          // [pixel] -> packed record (k_slotpix)

@@ -7,7 +7,7 @@
 //   L1  k_tour_tile   : per 32x32 tile, LDS pointer jumping contracts every maximal run of the
 //                       tour inside the tile into one chain (distance-to-chain-end, chain id)
 //   L2  k_chain_*     : in-place pointer jumping over the ~1e5 chains in global memory
-//   L3  k_tour_rank   : arc rank = chain rank + offset in chain
+//   L3  (k_orient)    : arc rank = tour length - arcs to the tour end (sm_tour.h)
 // then orientation (an arc is "down" iff it precedes its reverse), subtree size
 // (rank distance / 2), heavy child (max size, ties -> smallest direction), and a single int64
 // prefix sum over the tour of (light<<32 | preorder offset) that yields every node's heavy-first
@@ -91,7 +91,7 @@ struct MstTour {
 };
 
 __device__ __forceinline__ TourBufs tour_bufs(const LayoutView& V) {
-    return TourBufs{V.a_dist, V.a_cid, V.a_head, V.nchains, V.c_last, V.c_len, V.c_head, V.cnw};
+    return TourBufs{V.a_dist, V.a_cid, V.nchains, V.c_last, V.c_len, V.cnw};
 }
 
 // L1: contract the tour inside each 32x32 tile (sm_tour.h)
@@ -117,23 +117,11 @@ __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
     tour_chain_rank(tour_bufs(LP.v[blockIdx.y]));
 }
 
-// L3: arc ranks.  suffix(c) = arcs from chain c's head to the tour end; rank = total - suffix + offset
-__global__ void k_tour_rank(LayoutPair LP, int W, int H) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const uint32_t p = (uint32_t)(y * W + x);
-    const uint32_t adj = V.adj[p];
-    const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
-    for (int k = 0; k < 4; ++k) {
-        if (!(adj & (1u << k))) continue;
-        const uint32_t a = 4u * p + (uint32_t)k;
-        V.rank[a] = total - tour_suffix(tour_bufs(V), a);
-    }
-}
-
-// orientation + subtree size
+// L3 + orientation: an arc's rank is the tour length minus its suffix (sm_tour.h); an arc precedes its
+// reverse iff it goes down, and the rank distance between the two is twice the subtree size.  Per
+// pixel: the direction to its parent, its subtree size and the ranks of its two parent arcs (down
+// into it, up out of it), the only ranks later kernels read (round 5: one pass instead of a rank for
+// every arc in k_tour_rank and k_orient's re-read of them)
 __global__ void k_orient(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
@@ -141,24 +129,30 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
     if (x >= W) return;
     const uint32_t q = (uint32_t)(y * W + x);
     const uint32_t adj = V.adj[q];
+    const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
+    const TourBufs T = tour_bufs(V);
     int8_t pd = -1;
     uint32_t sz = (uint32_t)(W * H);
+    uint2 rio = make_uint2(0u, 0u);
     for (int k = 0; k < 4; ++k) {
         if (!(adj & (1u << k))) continue;
         const uint32_t p = nbr_of(q, k, W);
-        const uint32_t a_in = 4u * p + (uint32_t)((k + 2) & 3);  // p -> q
-        const uint32_t a_out = 4u * q + (uint32_t)k;             // q -> p
-        const uint32_t ri = V.rank[a_in], ro = V.rank[a_out];
-        if (ri < ro) {
+        const uint32_t si = tour_suffix(T, 4u * p + (uint32_t)((k + 2) & 3));  // p -> q
+        const uint32_t so = tour_suffix(T, 4u * q + (uint32_t)k);              // q -> p
+        if (si > so) {  // rank(p -> q) < rank(q -> p): p is the parent
             pd = (int8_t)k;
-            sz = (ro - ri + 1u) / 2u;
+            sz = (si - so + 1u) / 2u;
+            rio = make_uint2(total - si, total - so);
         }
     }
     V.pdir[q] = pd;
     V.size[q] = sz;
+    V.rio[q] = rio;
 }
 
-// heavy child + per-child preorder offset and light flag (written by the parent into the child)
+// Heavy child (max subtree, ties -> smallest direction) and the tour values of the children's edges,
+// written straight at their ranks: down arc into child c +(light << 32 | preorder offset of c within
+// v's subtree, heavy child first), up arc out of c the negation (round 5: k_tour_values fused in)
 __global__ void k_heavy(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
@@ -170,44 +164,28 @@ __global__ void k_heavy(LayoutPair LP, int W, int H) {
     int heavy = -1;
     uint32_t best = 0;
     uint32_t csz[4] = {0, 0, 0, 0};
+    uint2 crio[4];
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
+        crio[k] = make_uint2(0u, 0u);
         if (!(adj & (1u << k)) || k == pd) continue;
-        csz[k] = V.size[nbr_of(v, k, W)];
+        const uint32_t c = nbr_of(v, k, W);
+        csz[k] = V.size[c];
+        crio[k] = V.rio[c];
         if (csz[k] > best) { best = csz[k]; heavy = k; }
     }
     V.heavy[v] = (int8_t)heavy;
     uint32_t off = 1u + (heavy >= 0 ? csz[heavy] : 0u);
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (!(adj & (1u << k)) || k == pd) continue;
-        const uint32_t c = nbr_of(v, k, W);
-        if (k == heavy) {
-            V.off_in[c] = 1u;
-            V.light_in[c] = 0;
-        } else {
-            V.off_in[c] = off;
-            V.light_in[c] = 1;
+        long long val = 1;  // the heavy child: offset 1, not light
+        if (k != heavy) {
+            val = (1ll << 32) + (long long)off;
             off += csz[k];
         }
-    }
-    if (pd < 0) { V.off_in[v] = 0u; V.light_in[v] = 0; }
-}
-
-// tour values: down arc into c: +(light<<32 | off), up arc out of c: -(...)
-__global__ void k_tour_values(LayoutPair LP, int W, int H) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const uint32_t p = (uint32_t)(y * W + x);
-    const uint32_t adj = V.adj[p];
-    for (int k = 0; k < 4; ++k) {
-        if (!(adj & (1u << k))) continue;
-        const uint32_t q = nbr_of(p, k, W);
-        const uint32_t a = 4u * p + (uint32_t)k;
-        const bool down = V.pdir[q] == ((k + 2) & 3);
-        const uint32_t c = down ? q : p;
-        const long long val = ((long long)V.light_in[c] << 32) + (long long)V.off_in[c];
-        V.tour[V.rank[a]] = down ? val : -val;
+        V.tour[crio[k].x] = val;
+        V.tour[crio[k].y] = -val;
     }
 }
 
@@ -320,7 +298,10 @@ static void launch_scan(hipStream_t st, const ScanBufs<T>& B, int nviews, int ne
     hipLaunchKernelGGL((k_scan_apply<T, Op>), dim3(nblocks, nviews), dim3(SCAN_BLOCK), 0, st, B, nelem);
 }
 
-// preorder + light depth per pixel from the scanned tour
+// preorder + light depth per pixel from the scanned tour; path heads in preorder numbering:
+// headflag[pre] = 0 (not a head) or 1 + light depth, headpos[pre] = pre + 1 at heads (0 elsewhere; the
+// max-scan's input).  A node is a head iff it is the root or not its parent's heavy child (round 5:
+// k_heads and k_path_prep fused in)
 __global__ void k_assign(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
@@ -329,42 +310,17 @@ __global__ void k_assign(LayoutPair LP, int W, int H) {
     const uint32_t q = (uint32_t)(y * W + x);
     const int pd = V.pdir[q];
     uint32_t pre = 0, ld = 0;
+    bool head = true;
     if (pd >= 0) {
-        const uint32_t p = nbr_of(q, pd, W);
-        const uint32_t a_in = 4u * p + (uint32_t)((pd + 2) & 3);
-        const long long v = V.tour[V.rank[a_in]];
+        const long long v = V.tour[V.rio[q].x];
         pre = (uint32_t)(v & 0xFFFFFFFFll);
         ld = (uint32_t)(v >> 32);
+        head = V.heavy[nbr_of(q, pd, W)] != ((pd + 2) & 3);
     }
     V.pre[q] = pre;
     V.ld[q] = ld;
-}
-
-// path heads in preorder numbering: headflag[pre] = 0 (not a head) or 1 + light depth
-__global__ void k_heads(LayoutPair LP, int W, int H) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const uint32_t v = (uint32_t)(y * W + x);
-    const bool head = V.pdir[v] < 0 || V.light_in[v];
-    V.headflag[V.pre[v]] = head ? 1u + V.ld[v] : 0u;
-}
-
-// slot of every preorder position: the paths of one (light depth, long/short) bucket occupy a
-// contiguous slot range, each path contiguous from its head (= preorder contiguity of heavy
-// paths), in paths[] order.  plen holds the inclusive scan of the lengths: end slot of a path.
-__global__ void k_newslot(LayoutPair LP, int N) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.y];
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= (uint32_t)N) return;
-    const uint32_t head = V.headpos[s] - 1u;
-    const uint32_t P = V.pathpos[head];
-    const uint32_t len = V.paths[P].len;
-    const uint32_t nh = V.plen[P] - len;
-    V.nslot[s] = nh + (s - head);
-    if (s == head) V.paths[P].head = nh;
+    V.headflag[pre] = head ? 1u + ld : 0u;
+    V.headpos[pre] = head ? pre + 1u : 0u;
 }
 
 // Per pixel: its slot, the pixel of every slot, and one packed 64-bit record
@@ -385,7 +341,16 @@ __global__ void k_slotpix(LayoutPair LP, int W, int H) {
     const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
     const uint32_t v = (uint32_t)(y * W + x);
-    const uint32_t slot = V.nslot[V.pre[v]];
+    // the slot: the paths of one (light depth, long/short) bucket occupy a contiguous slot range, each
+    // path contiguous from its head (= preorder contiguity of heavy paths), in paths[] order; plen holds
+    // the inclusive scan of the lengths, i.e. the end slot of a path (round 5: k_newslot fused in)
+    const uint32_t s = V.pre[v];
+    const uint32_t head = V.headpos[s] - 1u;
+    const uint32_t P = V.pathpos[head];
+    const uint32_t len = V.paths[P].len;
+    const uint32_t nh = V.plen[P] - len;
+    const uint32_t slot = nh + (s - head);
+    if (s == head) V.paths[P].head = nh;  // (other threads read .len only)
     V.slotpix[v] = slot;
     V.slot2pix[slot] = v;
     V.prec[v] = (uint64_t)slot | ((uint64_t)V.adj[v] << 32) | ((uint64_t)(V.pdir[v] + 1) << 36) |
@@ -467,23 +432,11 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
     if (threadIdx.x == 0 && nl) atomicAdd(V.n_has_light, nl);
 }
 
-// heads in slot order -> path lengths -> bucketed by light depth (order inside a round is free).
-// headpos[s] = s+1 at heads (0 elsewhere); after an inclusive max-scan it is 1 + the slot of
-// the head of s's path (heavy paths are contiguous in preorder).
+// heads in preorder -> path lengths -> bucketed by light depth (order inside a round is free).
+// headpos[s] = s+1 at heads (0 elsewhere, k_assign); after an inclusive max-scan it is 1 + the
+// preorder position of the head of s's path (heavy paths are contiguous in preorder).
 #define PATH_BLOCK 1024
 #define PATH_ITEMS 8   // slots per thread -> 8192 per block (few global atomics per round bin)
-
-__global__ __launch_bounds__(PATH_BLOCK) void k_path_prep(LayoutPair LP, int N) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.y];
-    const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
-    for (int i = 0; i < PATH_ITEMS; ++i) {
-        const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
-        if (s >= (uint32_t)N) break;
-        const uint32_t h = V.headflag[s];
-        V.headpos[s] = h ? s + 1u : 0u;
-    }
-}
 
 // after the max-scan: count paths per (round, long/short) bucket at their last slot
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N) {
@@ -556,7 +509,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
         const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
         const uint32_t P = gbase[myr[i]] + myrank[i];
         const uint32_t len = s - myhead[i] + 1u;
-        V.paths[P] = SmPath{myhead[i], len};  // head in preorder numbering until k_newslot
+        V.paths[P] = SmPath{myhead[i], len};  // head in preorder numbering until k_slotpix
         V.pathpos[myhead[i]] = P;
         V.plen[P] = len;
     }
@@ -735,16 +688,12 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     const dim3 cg((max_chains + 255) / 256, nviews);
     hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
-    hipLaunchKernelGGL(k_tour_rank, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_orient, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_heavy, pg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_tour_values, pg, dim3(256), 0, st, LP, W, H);
     ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}, {LP.v[0].bsum, LP.v[1].bsum}};
     launch_scan<long long, OpAdd>(st, tb, nviews, 2 * N - 2);
     hipLaunchKernelGGL(k_assign, pg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_heads, pg, dim3(256), 0, st, LP, W, H);
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
-    hipLaunchKernelGGL(k_path_prep, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     ScanBufs<uint32_t> hb{{LP.v[0].headpos, LP.v[1].headpos}, {LP.v[0].bsum32, LP.v[1].bsum32}};
     launch_scan<uint32_t, OpMax>(st, hb, nviews, N);
     hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
@@ -754,7 +703,6 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     // path), slot of every preorder position, then the metadata in slot numbering
     ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}, {LP.v[0].bsum32, LP.v[1].bsum32}};
     launch_scan<uint32_t, OpAdd>(st, lb, nviews, N);
-    hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
     hipLaunchKernelGGL(k_slotpix, pg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, N);
     // run sizing (A/B knobs: SM_RUN_DIV, SM_RUN_CAP = the window cap in nodes)

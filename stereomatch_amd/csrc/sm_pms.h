@@ -86,7 +86,6 @@ hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t);
 // wn: stream floats from off[0] a pass can consume (staged in LDS when the window fits)
 hipError_t launch_pms_guess(hipStream_t st, const PmsDev& d, int t_lo, long long wn);
 hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int total_deg);
-hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi);
 // lane-group classes of the planned walks: paths of trees with P <= 2 / P <= 8 proposals share a wave
 // (32 / 8 paths per wave), the rest are (path, 64-proposal chunk) items of one wave each
 #define PMS_NCLS 3

@@ -829,19 +829,6 @@ __global__ void __launch_bounds__(256) k_pms_cost(PmsDev d, int phase, int row_l
     }
 }
 
-__global__ void __launch_bounds__(256) k_pms_walk(PmsDev d, int phase, int up, int item_lo, int item_hi) {
-    __shared__ double sS[PMS_NW], sS2[PMS_NW];
-    load_luts(d, sS, sS2);
-    const int it = item_lo + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (it >= item_hi) return;
-    int path = it, chunk = 0;
-    if (phase == 0) {
-        path = d.items[it].path;
-        chunk = d.items[it].chunk;
-    }
-    if (up) up_item(d, sS, phase, path, chunk);
-    else down_item(d, sS, sS2, phase, path, chunk);
-}
 
 // ----------------------------------------------------------------------------- per-phase layout
 // The A rows of a phase hold its P proposals per node.  The static layout (tree_pt / tree_abase) has
@@ -1690,14 +1677,8 @@ inline unsigned blocks(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b
 
 hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1) {
     if (t1 <= t0) return hipSuccess;
-    const char* e = getenv("SM_PMS_SER_NT");  // A/B: 1024 or 512 threads (default 768)
-    const int nt = e && atoi(e) == 1024 ? 1024 : e && atoi(e) == 512 ? 512 : 768;
-    if (nt == 1024)
-        hipLaunchKernelGGL(k_pms_serial<1024>, dim3(1), dim3(1024), 0, st, d, t0, t1);
-    else if (nt == 512)
-        hipLaunchKernelGGL(k_pms_serial<512>, dim3(1), dim3(512), 0, st, d, t0, t1);
-    else
-        hipLaunchKernelGGL(k_pms_serial<768>, dim3(1), dim3(768), 0, st, d, t0, t1);
+    // 768 threads: 1024 spilled VGPRs; 512 / 768 / 1024 within noise once it did not (round 4)
+    hipLaunchKernelGGL(k_pms_serial<768>, dim3(1), dim3(768), 0, st, d, t0, t1);
     return hipGetLastError();
 }
 
@@ -1737,14 +1718,6 @@ hipError_t launch_pms_prop_setup(hipStream_t st, const PmsDev& d, int t_lo, int 
 hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo, int t_hi) {
     if (t_hi <= t_lo) return hipSuccess;
     hipLaunchKernelGGL(k_pms_prop_dedupe, dim3(blocks((size_t)(t_hi - t_lo) * 64, 256)), dim3(256), 0, st, d, t_lo, t_hi);
-    return hipGetLastError();
-}
-
-hipError_t launch_pms_walk(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int item_lo, int item_hi) {
-    (void)r;
-    if (item_hi <= item_lo) return hipSuccess;
-    hipLaunchKernelGGL(k_pms_walk, dim3(blocks((size_t)(item_hi - item_lo) * 64, 256)), dim3(256), 0, st, d, phase,
-                       up ? 1 : 0, item_lo, item_hi);
     return hipGetLastError();
 }
 

@@ -36,11 +36,9 @@ struct PfView {
     // per arc (4N) and per chain (max_chains) of the list ranking
     uint16_t* a_dist;
     uint32_t* a_cid;
-    uint32_t* a_head;
     uint32_t* nchains;
     uint32_t* c_last;
     uint32_t* c_len;
-    uint32_t* c_head;
     uint64_t* cnw;
     uint32_t max_chains;
     long long* tval;    // 2(N - K): the tours' values, concatenated by tree, and their inclusive scan

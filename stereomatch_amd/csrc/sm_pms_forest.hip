@@ -188,7 +188,7 @@ struct PfTourG {
 };
 
 __device__ __forceinline__ TourBufs pf_tour_bufs(const PfView& v) {
-    return TourBufs{v.a_dist, v.a_cid, v.a_head, v.nchains, v.c_last, v.c_len, v.c_head, v.cnw};
+    return TourBufs{v.a_dist, v.a_cid, v.nchains, v.c_last, v.c_len, v.cnw};
 }
 
 // direction from p to its grid neighbour n

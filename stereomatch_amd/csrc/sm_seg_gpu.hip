@@ -1196,9 +1196,8 @@ hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t g
 }
 
 hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0, bool split) {
-    // SM_SEG_NOLDS=1: every small bucket takes the Boruvka rounds (A/B of the LDS Kruskal); SM_SEG_ACT_MAX: the
-    // most active edges bucketed in LDS (0: always the full scan; tests)
-    const uint32_t lc = getenv("SM_SEG_NOLDS") ? 0u : (uint32_t)SEG_LC;
+    // SM_SEG_ACT_MAX: the most active edges bucketed in LDS (0: always the full scan; tests)
+    const uint32_t lc = (uint32_t)SEG_LC;
     const uint32_t amax = getenv("SM_SEG_ACT_MAX") ? (uint32_t)atoi(getenv("SM_SEG_ACT_MAX")) : (uint32_t)SEG_ACT_MAX;
     const int prof = getenv("SM_SEG_PROF") ? 1 : 0;
     // SM_SEG_NORUN=1: no k_seg_run (every split run through k_seg_small)
@@ -1231,22 +1230,16 @@ hipError_t seg_launch_minsize(hipStream_t st, const SegPair& p, int min_size, ui
 
 // The min-size candidates' sorts (~260k pairs per C2 view): rocprim's onesweep radix sort (one histogram
 // launch + one launch per 8-bit digit, stable) instead of hipcub's choice below 2^20 items, the merge-sort
-// path (~20 launches per sort, 0.2-0.36 ms each at C2).  SM_SEG_MERGESORT=1 keeps hipcub's choice (A/B).
+// path (~20 launches per sort, 0.2-0.36 ms each at C2).  (Only when the hashed pair dedupe's table does
+// not fit: the default dedupe sorts nothing.)
 using SegOnesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
-bool seg_mergesort() { return getenv("SM_SEG_MERGESORT") != nullptr; }
 hipError_t seg_sort_pairs(void* temp, size_t& bytes, const unsigned long long* kin, unsigned long long* kout,
                           const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t st) {
-    if (seg_mergesort())
-        return hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
     return rocprim::radix_sort_pairs<SegOnesweep>(temp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)bits, st);
 }
 
 size_t seg_sort_temp_bytes(uint32_t n) {
     size_t a = 0, b = 0, c = 0, d = 0, e = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, SEG_KEY_BITS);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64);
     (void)rocprim::radix_sort_pairs<SegOnesweep>(nullptr, d, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u, 64u);
     (void)rocprim::radix_sort_pairs<SegOnesweep>(nullptr, e, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,

@@ -9,7 +9,7 @@
 //   L2 tour_chain_init : chain successor + length; tour_chain_rank: in-place pointer jumping over the
 //                        chains, cnw[c] >> 32 = arcs from chain c's head to the end of its list
 //   L3 (caller)        : arcs from arc a to its list's end, inclusive =
-//                        (cnw[c] >> 32) - (c_len[c] - a_dist[a]), c = a_cid[a_head[a]]
+//                        (cnw[c] >> 32) - (c_len[c] - a_dist[a]), c = a_cid[a]
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,13 +26,11 @@
 struct TourBufs {
     // per arc (4N)
     uint16_t* a_dist;   // arcs from the arc to its chain's end, inclusive
-    uint32_t* a_cid;    // chain id (written at chain heads)
-    uint32_t* a_head;   // the arc's chain head (global arc id)
+    uint32_t* a_cid;    // the arc's chain
     // per chain
     uint32_t* nchains;  // device counter
     uint32_t* c_last;
     uint32_t* c_len;
-    uint32_t* c_head;
     uint64_t* cnw;      // successor chain (low 32 bits) | arcs to it (high 32 bits)
 };
 
@@ -41,13 +39,14 @@ __device__ __forceinline__ uint32_t tour_nbr(uint32_t p, int k, int W) {
 }
 
 // L1: contract the lists inside the 32x32 tile (blockIdx.x, blockIdx.y).  One 64-bit LDS word per arc
-// slot, nxt | dist << 16 | last << 32 (bits 48..63: the chain head, written once the jumping is done),
-// so a jump is one gathered word; every thread keeps its 16 words in registers.
+// slot, nxt | dist << 16 | last << 32, so a jump is one gathered word; every thread keeps its 16 words
+// in registers.
 template <class G>
 __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, int H) {
     __shared__ union {
         uint64_t w[TLS];
-        uint16_t h[4 * TLS];  // h[4*s + 3]: head slot of the chain whose last slot is s
+        uint16_t h[4 * TLS];  // once the jumping is done, h[4*s + 2]: the tile-local id of the chain whose
+                              // last slot is s (bits 32..47 of w[s], which nobody reads any more)
     } st;
     __shared__ uint8_t haspred[TLS];
     const int tx0 = blockIdx.x * TL, ty0 = blockIdx.y * TL;
@@ -110,8 +109,8 @@ __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, 
         const uint32_t dist = (uint32_t)(own[i] >> 16) & 0xFFFFu, last = (uint32_t)(own[i] >> 32) & 0xFFFFu;
         myhead[i] = SM_NONE;
         if (dist != 0 && !haspred[s]) {
-            st.h[4 * last + 3] = (uint16_t)s;
             myhead[i] = atomicAdd(&nheads, 1u);  // LDS atomic: rank of this chain inside the tile
+            st.h[4 * last + 2] = (uint16_t)myhead[i];
         }
     }
     __syncthreads();
@@ -124,21 +123,15 @@ __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, 
         const int lp = s >> 2, k = s & 3;
         const uint32_t p = (uint32_t)((ty0 + lp / TL) * W + tx0 + lp % TL);
         const uint32_t a = 4u * p + (uint32_t)k;
+        const uint32_t cid = cbase + st.h[4 * last + 2];  // every arc its chain's id
         T.a_dist[a] = (uint16_t)dist;
+        T.a_cid[a] = cid;
         if (myhead[i] != SM_NONE) {
-            const uint32_t cid = cbase + myhead[i];
-            T.a_cid[a] = cid;  // head's chain id (read below by the chain's other arcs: next kernel)
             const int llp = (int)last >> 2;
             const uint32_t lpix = (uint32_t)((ty0 + llp / TL) * W + tx0 + llp % TL);
             T.c_last[cid] = 4u * lpix + (last & 3u);
             T.c_len[cid] = dist;
-            T.c_head[cid] = a;
         }
-        // every arc remembers its chain head (global arc id)
-        const int hs = st.h[4 * last + 3];
-        const int hlp = hs >> 2;
-        const uint32_t hpix = (uint32_t)((ty0 + hlp / TL) * W + tx0 + hlp % TL);
-        T.a_head[a] = 4u * hpix + (uint32_t)(hs & 3);
     }
 }
 
@@ -181,6 +174,6 @@ __device__ __forceinline__ void tour_chain_rank(const TourBufs& T) {
 
 // L3: arcs from arc a to the end of its list, inclusive
 __device__ __forceinline__ uint32_t tour_suffix(const TourBufs& T, uint32_t a) {
-    const uint32_t c = T.a_cid[T.a_head[a]];
+    const uint32_t c = T.a_cid[a];
     return (uint32_t)(T.cnw[c] >> 32) - (T.c_len[c] - T.a_dist[a]);
 }

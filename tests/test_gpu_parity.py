@@ -780,25 +780,21 @@ def test_full_size_c3_segment_forest_and_match(gpu_ctx):
 
 @pytest.mark.parametrize("env", [{"SM_SEG_SMALL": "0"}, {"SM_SEG_SMALL": "0", "SM_SEG_GLOBAL_ROUNDS": "0"},
                                  {"SM_SEG_SMALL": "100000000"}, {"SM_SEG_GLOBAL_ROUNDS": "7"}, {"SM_SEG_HOST": "1"},
-                                 {"SM_SEG_NODEDUP": "1"}, {"SM_SEG_FLATTEN": "0"}, {"SM_SEG_FLATTEN": "3"},
-                                 {"SM_SEG_NOLDS": "1"}, {"SM_SEG_NOLDS": "1", "SM_SEG_SMALL": "100000000"},
+                                 {"SM_SEG_FLATTEN": "0"}, {"SM_SEG_FLATTEN": "3"},
                                  {"SM_SEG_NOSPLIT": "1"}, {"SM_SEG_NORUN": "1"}, {"SM_SEG_NORUN": "1", "SM_SEG_ACT_MAX": "0"},
-                                 {"SM_SEG_NORUN": "1", "SM_SEG_ACT_MAX": "0", "SM_SEG_NOLDS": "1"},
-                                 {"SM_SEG_TAIL_GLOBAL": "1"}, {"SM_SEG_GLOBAL_ROUNDS": "1"}, {"SM_SEG_SORTDEDUP": "1"},
+                                 {"SM_SEG_TAIL_GLOBAL": "1"}, {"SM_SEG_GLOBAL_ROUNDS": "1"},
                                  {"SM_SEG_TAIL_MIN": "0"}, {"SM_SEG_TAIL_MIN": "0", "SM_SEG_GLOBAL_ROUNDS": "1"}])
 def test_segment_forest_schedules(gpu_ctx, monkeypatch, env):
     """The GPU segmentation's launch schedules give the same forest: every bucket over the whole GPU
     (with and without global Boruvka rounds before the one-workgroup tail), every bucket in one
-    workgroup, more global rounds; the host sweep (SM_SEG_HOST); the min-size merge over every
-    candidate instead of the first of each root pair (SM_SEG_NODEDUP); no root flattening, or
-    flattening before every bucket (SM_SEG_FLATTEN); the one-workgroup buckets by Boruvka rounds instead
-    of the LDS Kruskal (SM_SEG_NOLDS); small-bucket runs without the k_seg_split pre-pass
+    workgroup, more global rounds; the host sweep (SM_SEG_HOST); no root flattening, or flattening
+    before every bucket (SM_SEG_FLATTEN); small-bucket runs without the k_seg_split pre-pass
     (SM_SEG_NOSPLIT), or with it but without the LDS-resident run (SM_SEG_NORUN: k_seg_small over the
     LDS-bucketed active edges, or with SM_SEG_ACT_MAX=0 the full scan, which skips the edges the pre-pass
     rejected); the big buckets' tails by global-memory rounds instead of the LDS rounds (SM_SEG_TAIL_GLOBAL),
     or after one global round (SM_SEG_GLOBAL_ROUNDS=1: larger tails), or in LDS whatever their length
-    (SM_SEG_TAIL_MIN=0; the default keeps lists under 256 edges on the global rounds); the pair
-    dedupe by the two radix sorts instead of the hash table (SM_SEG_SORTDEDUP)."""
+    (SM_SEG_TAIL_MIN=0; the default keeps lists under 256 edges on the global rounds).  (The pair
+    dedupe's sort fallback, for tables that do not fit, runs on the smallest golden images.)"""
     import stereomatch_amd as sm
     for k, val in env.items():
         monkeypatch.setenv(k, val)

@@ -62,54 +62,22 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
     assert st["iters"] == iters and st["ntrees"] == [ref["left"]["tree"]["ntrees"], ref["right"]["tree"]["ntrees"]]
 
 
-@pytest.mark.parametrize("mode", ["spec", "repass", "serial", "nodedup", "wavewalk", "nochain", "chain48", "chainstream",
-                                  "refalways", "ser1024", "ser512", "nsu4", "nsu8"])
+@pytest.mark.parametrize("mode", ["spec", "serial", "chain48", "nsu4", "nsu8"])
 def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
-    call's starting labels) and wrong offsets (a new pass); SM_PMS_REPASS=1 re-speculates after
-    every failure; SM_PMS_SERIAL=1 is the plain serial order; SM_PMS_NODEDUP=1 propagates every
-    sampled label, repeats included (the default drops repeats, k_pms_prop_dedupe);
-    SM_PMS_WAVE_WALK=1 walks every (path, chunk) item with a wave of its own instead of the planned
-    lane-group walks (k_pms_plan / k_pms_walk_plan); SM_PMS_CHAIN_MIN=48 sends paths of >= 48 rows to the
-    chain kernel; SM_PMS_CHAIN_STREAM=1 runs the chain launches on a side stream beside the walkers;
-    SM_PMS_SER_NT=1024 / 512 runs the serial kernel with that many threads (default 768);
-    SM_PMS_CHAIN_NSU=4 / 8 gives the up chain that many ring slots (default 6)."""
+    call's starting labels) and wrong offsets (a new pass); SM_PMS_SERIAL=1 is the plain serial order;
+    SM_PMS_CHAIN_MIN=48 sends paths of >= 48 rows to the chain kernel; SM_PMS_CHAIN_NSU=4 / 8 gives the
+    up chain that many ring slots (default 6)."""
     monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
-    monkeypatch.setenv("SM_PMS_REPASS", "1" if mode == "repass" else "0")
-    if mode == "nodedup":
-        monkeypatch.setenv("SM_PMS_NODEDUP", "1")
-    else:
-        monkeypatch.delenv("SM_PMS_NODEDUP", raising=False)
-    if mode == "wavewalk":
-        monkeypatch.setenv("SM_PMS_WAVE_WALK", "1")
-    else:
-        monkeypatch.delenv("SM_PMS_WAVE_WALK", raising=False)
-    if mode == "nochain":  # paths of >= 64 rows on the wave walker instead of k_pms_chain
-        monkeypatch.setenv("SM_PMS_NO_CHAIN", "1")
-    else:
-        monkeypatch.delenv("SM_PMS_NO_CHAIN", raising=False)
-    if mode == "chain48":
-        monkeypatch.setenv("SM_PMS_CHAIN_MIN", "48")
-    else:
-        monkeypatch.delenv("SM_PMS_CHAIN_MIN", raising=False)
-    if mode == "chainstream":
-        monkeypatch.setenv("SM_PMS_CHAIN_STREAM", "1")
-    else:
-        monkeypatch.delenv("SM_PMS_CHAIN_STREAM", raising=False)
-    if mode == "refalways":  # a large tree's empty refinement phase launched anyway (default: skipped)
-        monkeypatch.setenv("SM_PMS_REF_ALWAYS", "1")
-    else:
-        monkeypatch.delenv("SM_PMS_REF_ALWAYS", raising=False)
-    if mode in ("nsu4", "nsu8"):
-        monkeypatch.setenv("SM_PMS_CHAIN_NSU", mode[3:])
+    if mode in ("chain48", "nsu4", "nsu8"):
         monkeypatch.setenv("SM_PMS_CHAIN_MIN", "48")  # (more chain items at this size)
     else:
-        monkeypatch.delenv("SM_PMS_CHAIN_NSU", raising=False)
-    if mode in ("ser1024", "ser512"):
-        monkeypatch.setenv("SM_PMS_SER_NT", mode[3:])
+        monkeypatch.delenv("SM_PMS_CHAIN_MIN", raising=False)
+    if mode in ("nsu4", "nsu8"):
+        monkeypatch.setenv("SM_PMS_CHAIN_NSU", mode[3:])
     else:
-        monkeypatch.delenv("SM_PMS_SER_NT", raising=False)
+        monkeypatch.delenv("SM_PMS_CHAIN_NSU", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
@@ -120,18 +88,15 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
         assert st["serial_trees"] > 2 * ref["left"]["tree"]["ntrees"] - 50  # first calls + the failures
 
 
-@pytest.mark.parametrize("piece,serial,seqrep", [("16", "0", "0"), ("8", "1", "0"), ("64", "0", "0"), ("8", "0", "0"),
-                                                 ("16", "0", "1")])
-def test_pms_pieces_bitexact(gpu_ctx, monkeypatch, piece, serial, seqrep):
+@pytest.mark.parametrize("piece,serial", [("16", "0"), ("8", "1"), ("64", "0"), ("8", "0")])
+def test_pms_pieces_bitexact(gpu_ctx, monkeypatch, piece, serial):
     """Long heavy paths cut into pieces of SM_PMS_PIECE rows: every piece runs from a guessed input; the
     parallel repair (k_pms_repair_par) re-walks every piece at once from its neighbour's boundary row until
     the rows agree, and the gated sequential pass redoes the cuts where a piece's repair rewrote the row
-    its neighbour started from (8-row pieces mostly re-walk whole pieces, so they take it; SM_PMS_SEQ_REPAIR=1
-    runs the sequential pass alone).  First call serial (cut trees take the whole-GPU launches), later
+    its neighbour started from (8-row pieces mostly re-walk whole pieces, so they take it).  First call serial (cut trees take the whole-GPU launches), later
     calls speculative; SM_PMS_SERIAL=1 all serial."""
     monkeypatch.setenv("SM_PMS_PIECE", piece)
     monkeypatch.setenv("SM_PMS_SERIAL", serial)
-    monkeypatch.setenv("SM_PMS_SEQ_REPAIR", seqrep)
     left, right, _ = make_pair(192, 128, 48, index=7)
     ref = O.stereo3dmst_pms(left, right, 48, iters=3, c=5000.0, min_size=200)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 3, 5000.0, 200)
@@ -236,7 +201,7 @@ def test_pms_full_c2_speculative_bitexact(gpu_ctx, monkeypatch, chain_min):
     calls per view run in (Stereo3DMST.cpp:546-629, 854-889).  Labels, fp64 minima and plane disparities
     bitwise against the oracle's serial restatement.  chain_min 48: paths of >= 48 rows on the chain kernel
     (SM_PMS_CHAIN_MIN)."""
-    for k in ("SM_PMS_SERIAL", "SM_PMS_REPASS", "SM_PMS_NODEDUP", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS", "SM_PMS_CHAIN_MIN"):
+    for k in ("SM_PMS_SERIAL", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS", "SM_PMS_CHAIN_MIN"):
         monkeypatch.delenv(k, raising=False)
     if chain_min:
         monkeypatch.setenv("SM_PMS_CHAIN_MIN", chain_min)
@@ -257,7 +222,7 @@ def test_pms_flir_c1_two_calls_output_step(gpu_ctx, monkeypatch):
     MST_PMS calls per view (the second speculative) and stereo3dmst's output step (LabelToDisp, *= Dmax-1,
     L-R check of the left map; :189-201, :900-904), bitwise against the oracle."""
     from conftest import flir_pair
-    for k in ("SM_PMS_SERIAL", "SM_PMS_REPASS", "SM_PMS_NODEDUP", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS"):
+    for k in ("SM_PMS_SERIAL", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS"):
         monkeypatch.delenv(k, raising=False)
     L, R = flir_pair()
     D = 64
