@@ -171,6 +171,42 @@ def stream_frames(ctxs, steps, D, params, retire, split=True, lag=1):
         retire(ctxs[i % n])
 
 
+def segment_leg(ctxs, left, right, D, steps, warmup, c=5000.0, min_size=200, inflight=6):
+    """Stereo3DMST's own tree configuration, the segment forest (c = 5000, min_size = 200,
+    Stereo3DMST.cpp:831-832), through the per-slice filter on the same pair: streamed ms/frame with
+    `inflight` frames in flight (the segment-mode default; each frame segments on its context's worker
+    thread) and the single-frame latency.  Reported beside the MST-mode metric, never as it."""
+    extra = [sm.Context(ctxs[0].device) for _ in range(max(0, inflight - len(ctxs)))]
+    cs = (list(ctxs) + extra)[:inflight]
+    for cx in extra:
+        cx.upload(left, right)
+    p = sm.default_params(c=c, min_size=min_size)
+    for cx in cs:
+        cx.set_kernel_timing([])
+    for _ in range(max(warmup, 1)):
+        for cx in cs:
+            cx.match_async(D, p)
+            cx.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stream_frames(cs, steps, D, p, lambda cx: cx.synchronize(), lag=max(1, len(cs) - 2))
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    lat = []
+    for _ in range(3):
+        t = time.perf_counter()
+        cs[0].match_async(D, p)
+        cs[0].synchronize()
+        lat.append((time.perf_counter() - t) * 1e3)
+    for cx in extra:
+        cx.close()
+    return dict(ms_per_frame=ms, value=left.shape[0] * left.shape[1] * D / (ms * 1e-3), unit="voxels/s",
+                latency_ms=min(lat), frames=steps, frames_in_flight=len(cs), c=c, min_size=min_size,
+                what="segment forest (Stereo3DMST's own tree, c=%g, min_size=%d) + per-slice tree filter + WTA, "
+                     "both views, same pair; %d frames streamed with %d in flight, latency best of 3"
+                     % (c, min_size, steps, len(cs)))
+
+
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -300,6 +336,8 @@ def main():
                     help="CPU check: start the ranks, print each rank's share and communicator set-up (stub "
                          "contexts, no GPU), exit")
     ap.add_argument("--no-pms", action="store_true", help="skip the MST_PMS (SM_AGG_PMS) timing leg")
+    ap.add_argument("--no-segment", action="store_true",
+                    help="skip the segment-mode leg (Stereo3DMST's own forest, reported beside the MST metric)")
     ap.add_argument("--pms-iters", type=int, default=100,
                     help="MST_PMS calls per view in the PMS timing leg (the reference's 100, Stereo3DMST.cpp:854)")
     args = ap.parse_args()
@@ -562,6 +600,8 @@ def main():
         line["value"] = W * H * Dloc * bin(views).count("1") * args.steps / elapsed
         line["config"]["workload"] = "rank %d/%d of %dx%d D=%d: views %d, slices [%d, %d)" % (
             emu["rank"], emu["nranks"], W, H, Dtot_frame, views, dbeg, dbeg + Dloc)
+    if rank == 0 and world == 1 and not args.no_segment and not emu and not seg_mode and args.aggregator == "tree":
+        line["segment"] = segment_leg(ctxs, left, right, Dloc, max(args.steps, 12), args.warmup)
     if rank == 0 and world == 1 and not args.no_cpu and not emu:
         line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame)
     if rank == 0 and world == 1 and not args.no_pms and not emu and args.aggregator == "tree":

@@ -169,6 +169,7 @@ class Context:
         if st != SM_OK:
             raise StereoMSTError(st, "sm_create failed (no HIP device?)")
         self.h = h
+        self.device = device
 
     def close(self):
         if getattr(self, "h", None):

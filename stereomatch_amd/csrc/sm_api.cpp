@@ -166,11 +166,12 @@ struct sm_ctx {
     DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
     uint32_t epoch = 0;      // bumped per filter call; status words are zeroed only on (re)allocation
     // GPU layout buffers (sm_layout_gpu.hip)
-    DevBuf adj[2], pdir[2], heavy[2], size[2], rio[2], pre[2], ld[2];
+    DevBuf adj[2], pdir[2], heavy[2], size[2], rio[2], hk[2], pixpre[2];
     DevBuf a_dist[2], a_cid[2], ccount[2], c_last[2], c_len[2];
-    DevBuf segtab[2], pathpos[2], plen[2], slotpix[2], slot2pix[2], prec[2];
+    DevBuf segtab[2], pathpos[2], plen[2], slotpix[2], slot2pix[2];
     DevBuf pieces[2], pieces_tmp[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
-    DevBuf cnw[2], tour[2], bsum[2], bsum32[2], headflag[2], headpos[2], rounds[2];
+    DevBuf cnw[2], tour[2], sctr[2], sflag[2], sagg[2], sincl[2], rounds[2];
+    uint32_t scan_epoch = 1;  // the layout scans' look-back epochs (3 per layout)
     int* h_changed = nullptr;
     uint32_t* h_err = nullptr;  // pinned, device-visible error word of the chain engine's waits
     uint32_t* d_err = nullptr;  // its device address
@@ -1019,7 +1020,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
     const size_t N = (size_t)W * H;
     const uint32_t ntiles = (uint32_t)(((W + 31) / 32) * ((H + 31) / 32));
     const uint32_t max_chains = ntiles * 129u + 1u;
-    const size_t nscan = (2 * N + 8191) / 8192 + 1;
+    const size_t nscan = scan_tiles(N);
     LayoutPair LP{};
     ZeroList z{};
     for (int i = 0; i < nviews; ++i) {
@@ -1029,8 +1030,8 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->heavy[v], N));
         CHECK(ensure(ctx, ctx->size[v], N * 4));
         CHECK(ensure(ctx, ctx->rio[v], N * 8));
-        CHECK(ensure(ctx, ctx->pre[v], N * 4));
-        CHECK(ensure(ctx, ctx->ld[v], N * 4));
+        CHECK(ensure(ctx, ctx->hk[v], N * 8));
+        CHECK(ensure(ctx, ctx->pixpre[v], N * 4));
         CHECK(ensure(ctx, ctx->a_dist[v], 4 * N * 2));
         CHECK(ensure(ctx, ctx->a_cid[v], 4 * N * 4));
         CHECK(ensure(ctx, ctx->ccount[v], 16));
@@ -1038,11 +1039,13 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->c_len[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->cnw[v], max_chains * 8));
         CHECK(ensure(ctx, ctx->tour[v], 2 * N * 8 + 16));
-        CHECK(ensure(ctx, ctx->bsum[v], nscan * 8));
-        CHECK(ensure(ctx, ctx->bsum32[v], nscan * 4));
+        CHECK(ensure(ctx, ctx->sctr[v], 16));
+        const bool fresh = ctx->sflag[v].n < nscan * 4;  // status words start at epoch 0 (never current)
+        CHECK(ensure(ctx, ctx->sflag[v], nscan * 4));
+        if (fresh) HIPC(hipMemsetAsync(ctx->sflag[v].p, 0, nscan * 4, ctx->st));
+        CHECK(ensure(ctx, ctx->sagg[v], nscan * 8));
+        CHECK(ensure(ctx, ctx->sincl[v], nscan * 8));
         CHECK(ensure(ctx, ctx->meta[v], N * sizeof(SmMeta)));
-        CHECK(ensure(ctx, ctx->headflag[v], N * 4));
-        CHECK(ensure(ctx, ctx->headpos[v], N * 4));
         CHECK(ensure(ctx, ctx->paths[v], N * sizeof(SmPath)));
         CHECK(ensure(ctx, ctx->rounds[v], RREC * 4));
         CHECK(ensure(ctx, ctx->segtab[v], (N / 16 + 64) * sizeof(uint2)));  // <= N/32 segments + N/32 long paths
@@ -1052,10 +1055,10 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
         CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
         CHECK(ensure(ctx, ctx->slot2pix[v], N * 4));
-        CHECK(ensure(ctx, ctx->prec[v], N * 8));
         z.add(ctx->plen[v].p, N * 4);  // lengths past the last path stay 0
         z.add(ctx->ccount[v].p, 16);
         z.add(ctx->rounds[v].p, RREC * 4);
+        z.add(ctx->sctr[v].p, 16);
         LayoutView& L = LP.v[i];
         L.mR = P<uint8_t>(ctx->mR[v]);
         L.mD = P<uint8_t>(ctx->mD[v]);
@@ -1066,8 +1069,8 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.heavy = P<int8_t>(ctx->heavy[v]);
         L.size = P<uint32_t>(ctx->size[v]);
         L.rio = P<uint2>(ctx->rio[v]);
-        L.pre = P<uint32_t>(ctx->pre[v]);
-        L.ld = P<uint32_t>(ctx->ld[v]);
+        L.hk = P<uint64_t>(ctx->hk[v]);
+        L.pixpre = P<uint32_t>(ctx->pixpre[v]);
         L.a_dist = P<uint16_t>(ctx->a_dist[v]);
         L.a_cid = P<uint32_t>(ctx->a_cid[v]);
         L.nchains = P<uint32_t>(ctx->ccount[v]);
@@ -1075,17 +1078,16 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.c_len = P<uint32_t>(ctx->c_len[v]);
         L.cnw = P<uint64_t>(ctx->cnw[v]);
         L.tour = P<long long>(ctx->tour[v]);
-        L.bsum = P<long long>(ctx->bsum[v]);
-        L.bsum32 = P<uint32_t>(ctx->bsum32[v]);
+        L.sctr = P<uint32_t>(ctx->sctr[v]);
+        LP.scan.flag[i] = P<uint32_t>(ctx->sflag[v]);
+        LP.scan.agg[i] = P<uint64_t>(ctx->sagg[v]);
+        LP.scan.incl[i] = P<uint64_t>(ctx->sincl[v]);
         L.meta = P<SmMeta>(ctx->meta[v]);
-        L.headflag = P<uint32_t>(ctx->headflag[v]);
-        L.headpos = P<uint32_t>(ctx->headpos[v]);
         L.paths = P<SmPath>(ctx->paths[v]);
         L.pathpos = P<uint32_t>(ctx->pathpos[v]);
         L.plen = P<uint32_t>(ctx->plen[v]);
         L.slotpix = P<uint32_t>(ctx->slotpix[v]);
         L.slot2pix = P<uint32_t>(ctx->slot2pix[v]);
-        L.prec = P<uint64_t>(ctx->prec[v]);
         uint32_t* R = P<uint32_t>(ctx->rounds[v]);
         L.round_begin = R;
         L.round_count = R + SM_NBUCKETS + 1;
@@ -1102,6 +1104,20 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
     LP.mst_ok = P<int>(ctx->mst_ok);
+    if (nviews == 1) {
+        LP.scan.flag[1] = LP.scan.flag[0];
+        LP.scan.agg[1] = LP.scan.agg[0];
+        LP.scan.incl[1] = LP.scan.incl[0];
+    }
+    LP.scan.err = ctx->d_err;
+    // (a fixed bound: SM_WAIT_ITERS, which the forced-timeout test lowers, is the chain engine's)
+    LP.scan.wait_iters = 1 << 22;
+    if (ctx->scan_epoch >= (1u << 29)) {  // wrapped: clear every status word
+        for (int i = 0; i < nviews; ++i) HIPC(hipMemsetAsync(ctx->sflag[vs.v[i]].p, 0, nscan * 4, ctx->st));
+        ctx->scan_epoch = 1;
+    }
+    LP.scan_epoch = ctx->scan_epoch;
+    ctx->scan_epoch += 3;
     HIPC(launch_zero(ctx->st, z));
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains, (uint32_t)piece_len()));
     // the host needs the per-round path counts to size the walker grids
@@ -1113,6 +1129,13 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
 
 sm_status stage_layout_finish(sm_ctx* ctx, int views) {
     HIPC(hipEventSynchronize(ctx->ev_layout));
+    // a layout scan whose look-back wait gave up (bit 0) or an index it produced out of range (bit 1):
+    // the metadata is not a tree layout, so no filter may run over it (its indices would be wild)
+    if (const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(ctx->h_err, 0u, __ATOMIC_RELEASE);
+        return fail(ctx, SM_ERR_STATE, (e & 2u) ? "tree layout: an index out of range after a scan's look-back gave up"
+                                                : "tree layout: a scan's look-back wait timed out");
+    }
     bool grew = false;
     CHECK(mst_finish(ctx, &grew));
     if (grew) return stage_layout(ctx, views);  // the forest was incomplete: lay out the final MST
@@ -2593,11 +2616,11 @@ void sm_destroy(sm_ctx* ctx) {
     if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
     for (int v = 0; v < 2; ++v) {
         DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->rio[v],
-                         &ctx->pre[v], &ctx->ld[v], &ctx->a_dist[v], &ctx->a_cid[v],
+                         &ctx->hk[v], &ctx->pixpre[v], &ctx->a_dist[v], &ctx->a_cid[v],
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->cnw[v],
-                         &ctx->tour[v], &ctx->bsum[v], &ctx->bsum32[v], &ctx->headflag[v],
-                         &ctx->headpos[v], &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
-                         &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->prec[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
+                         &ctx->tour[v], &ctx->sctr[v], &ctx->sflag[v], &ctx->sagg[v], &ctx->sincl[v],
+                         &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
+                         &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }

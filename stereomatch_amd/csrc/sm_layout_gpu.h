@@ -93,8 +93,6 @@ struct LayoutView {
     int8_t* heavy;      // direction of the heavy child (-1: leaf)
     uint32_t* size;     // subtree size
     uint2* rio;         // tour ranks of the arcs parent -> pixel (x) and pixel -> parent (y)
-    uint32_t* pre;      // heavy-first preorder (layout-internal numbering)
-    uint32_t* ld;       // light depth
     // per arc (4N)
     uint16_t* a_dist;
     uint32_t* a_cid;
@@ -103,21 +101,21 @@ struct LayoutView {
     uint32_t* c_last;
     uint32_t* c_len;
     uint64_t* cnw;      // per chain: successor chain (low 32 bits) | arcs to it (high 32 bits)
-    // tour (2N-2) + scan scratch
+    // tour (2N-2); the scans' tile tickets (3, zeroed with the layout's other counters)
     long long* tour;
-    long long* bsum;
-    uint32_t* bsum32;
+    uint32_t* sctr;
+    // per heavy-first preorder position (layout-internal numbering)
+    uint64_t* hk;        // (1 + head position) << 32 | (1 + light depth) at a path head, 0 elsewhere;
+                         // after the max-scan: the position's path head and its light depth
+    uint32_t* pixpre;    // the pixel at the position
     // per slot
     SmMeta* meta;
-    uint32_t* headflag;  // [preorder] 0, or 1 + light depth at a path head
-    uint32_t* headpos;   // [preorder] 1 + the preorder of the head of its path (after the max-scan)
     // paths
     SmPath* paths;           // {head slot, len}, bucket-major; slots of a bucket are contiguous
     uint32_t* pathpos;       // [preorder of a head] -> index of its path in paths[]
     uint32_t* plen;          // [path] -> len, inclusive-scanned into the path's end slot
     uint32_t* slotpix;       // [pixel] -> slot
     uint32_t* slot2pix;      // [slot] -> pixel
-    uint64_t* prec;          // [pixel] -> packed record (k_slotpix)
     uint32_t* round_count;   // SM_NBUCKETS
     uint32_t* round_cursor;  // SM_NBUCKETS
     uint32_t* round_begin;   // SM_NBUCKETS + 1
@@ -133,9 +131,23 @@ struct LayoutView {
     uint32_t* n_has_light;   // nodes with at least one light child (roofline accounting)
 };
 
+// the single-pass scans' look-back state (sm_layout_gpu.hip k_scan), per view: per tile its status word
+// (epoch << 2 | 1 aggregate / 2 inclusive prefix) and the two values (64-bit slots)
+struct ScanState {
+    uint32_t* flag[2];
+    uint64_t* agg[2];
+    uint64_t* incl[2];
+    uint32_t* err;   // the call's device error word: bit 0, a wait gave up
+    int wait_iters;  // polls before a wait gives up
+};
+// tiles of the scans (4096 elements each) over at most 2N elements
+static inline size_t scan_tiles(size_t N) { return (2 * N + 4095) / 4096 + 1; }
+
 struct LayoutPair {
     LayoutView v[2];
     const int* mst_ok;  // != 0 once the MST is complete (k_mst_done); every layout kernel checks it
+    ScanState scan;
+    uint32_t scan_epoch;  // this layout's three scans use epochs scan_epoch .. scan_epoch + 2
 };
 
 hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains,

@@ -49,6 +49,39 @@ __device__ __forceinline__ uint64_t key_dir(const uint16_t* wR, const uint16_t* 
 }
 
 // ------------------------------------------------------------------------------------------
+// 32x32 pixel tiles of the layout's per-pixel kernels, XCD-aware (round 5): block b of the 1D grid
+// (8 x per blocks, per = ceil(tiles / 8)) takes tile (b % 8) * per + b / 8.  Blocks b and b + 8 share an
+// XCD (round-robin dispatch), so each XCD takes a band of consecutive tiles, and a tile sits on the same
+// XCD in every kernel.  A tile touches the arrays indexed by tour rank (its chains are tile runs of the
+// tour, sm_tour.h), by preorder or by slot in a few contiguous runs, which then stay in that XCD's L2;
+// in row order the same passes were scattered over every L2.  Placement is for speed only: nothing
+// depends on it.
+struct TileRef {
+    int x0, y0;
+    bool ok;
+};
+__device__ __forceinline__ TileRef layout_tile(int W, int H, int b) {
+    const int ntx = (W + TL - 1) / TL, nt = ntx * ((H + TL - 1) / TL);
+    const int per = (nt + 7) / 8;
+    const int t = (b & 7) * per + (b >> 3);
+    return TileRef{(t % ntx) * TL, (t / ntx) * TL, t < nt};
+}
+__host__ __device__ inline int layout_tile_blocks(int W, int H) {
+    const int nt = ((W + TL - 1) / TL) * ((H + TL - 1) / TL);
+    return 8 * ((nt + 7) / 8);
+}
+// f(pixel) over tile t's pixels: 256 threads x 4 rows of 32 (a wave: two 32-pixel row segments)
+template <class F>
+__device__ __forceinline__ void tile_pixels(const TileRef& t, int W, int H, F&& f) {
+    if (!t.ok) return;
+    const int lx = (int)threadIdx.x & 31, ly = (int)threadIdx.x >> 5;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int x = t.x0 + lx, y = t.y0 + ly + 8 * i;
+        if (x < W && y < H) f((uint32_t)(y * W + x));
+    }
+}
+
 __global__ void k_adj(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
@@ -98,7 +131,9 @@ __device__ __forceinline__ TourBufs tour_bufs(const LayoutView& V) {
 __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    tour_tile(MstTour{V.adj, W, start_arc(V.adj)}, tour_bufs(V), W, H);
+    const TileRef t = layout_tile(W, H, (int)blockIdx.x);
+    if (!t.ok) return;  // (block-uniform)
+    tour_tile(MstTour{V.adj, W, start_arc(V.adj)}, tour_bufs(V), W, H, t.x0, t.y0);
 }
 
 // L2 init: chain successor + weight
@@ -125,29 +160,28 @@ __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
 __global__ void k_orient(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const uint32_t q = (uint32_t)(y * W + x);
-    const uint32_t adj = V.adj[q];
-    const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
-    const TourBufs T = tour_bufs(V);
-    int8_t pd = -1;
-    uint32_t sz = (uint32_t)(W * H);
-    uint2 rio = make_uint2(0u, 0u);
-    for (int k = 0; k < 4; ++k) {
-        if (!(adj & (1u << k))) continue;
-        const uint32_t p = nbr_of(q, k, W);
-        const uint32_t si = tour_suffix(T, 4u * p + (uint32_t)((k + 2) & 3));  // p -> q
-        const uint32_t so = tour_suffix(T, 4u * q + (uint32_t)k);              // q -> p
-        if (si > so) {  // rank(p -> q) < rank(q -> p): p is the parent
-            pd = (int8_t)k;
-            sz = (si - so + 1u) / 2u;
-            rio = make_uint2(total - si, total - so);
+    tile_pixels(layout_tile(W, H, (int)blockIdx.x), W, H, [&](uint32_t q) {
+        const uint32_t adj = V.adj[q];
+        const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
+        const TourBufs T = tour_bufs(V);
+        int8_t pd = -1;
+        uint32_t sz = (uint32_t)(W * H);
+        uint2 rio = make_uint2(0u, 0u);
+        for (int k = 0; k < 4; ++k) {
+            if (!(adj & (1u << k))) continue;
+            const uint32_t p = nbr_of(q, k, W);
+            const uint32_t si = tour_suffix(T, 4u * p + (uint32_t)((k + 2) & 3));  // p -> q
+            const uint32_t so = tour_suffix(T, 4u * q + (uint32_t)k);              // q -> p
+            if (si > so) {  // rank(p -> q) < rank(q -> p): p is the parent
+                pd = (int8_t)k;
+                sz = (si - so + 1u) / 2u;
+                rio = make_uint2(total - si, total - so);
+            }
         }
-    }
-    V.pdir[q] = pd;
-    V.size[q] = sz;
-    V.rio[q] = rio;
+        V.pdir[q] = pd;
+        V.size[q] = sz;
+        V.rio[q] = rio;
+    });
 }
 
 // Heavy child (max subtree, ties -> smallest direction) and the tour values of the children's edges,
@@ -156,42 +190,49 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
 __global__ void k_heavy(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const uint32_t v = (uint32_t)(y * W + x);
-    const uint32_t adj = V.adj[v];
-    const int pd = V.pdir[v];
-    int heavy = -1;
-    uint32_t best = 0;
-    uint32_t csz[4] = {0, 0, 0, 0};
-    uint2 crio[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        crio[k] = make_uint2(0u, 0u);
-        if (!(adj & (1u << k)) || k == pd) continue;
-        const uint32_t c = nbr_of(v, k, W);
-        csz[k] = V.size[c];
-        crio[k] = V.rio[c];
-        if (csz[k] > best) { best = csz[k]; heavy = k; }
-    }
-    V.heavy[v] = (int8_t)heavy;
-    uint32_t off = 1u + (heavy >= 0 ? csz[heavy] : 0u);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (!(adj & (1u << k)) || k == pd) continue;
-        long long val = 1;  // the heavy child: offset 1, not light
-        if (k != heavy) {
-            val = (1ll << 32) + (long long)off;
-            off += csz[k];
+    tile_pixels(layout_tile(W, H, (int)blockIdx.x), W, H, [&](uint32_t v) {
+        const uint32_t adj = V.adj[v];
+        const int pd = V.pdir[v];
+        int heavy = -1;
+        uint32_t best = 0;
+        uint32_t csz[4] = {0, 0, 0, 0};
+        uint2 crio[4];
+    #pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            crio[k] = make_uint2(0u, 0u);
+            if (!(adj & (1u << k)) || k == pd) continue;
+            const uint32_t c = nbr_of(v, k, W);
+            csz[k] = V.size[c];
+            crio[k] = V.rio[c];
+            if (csz[k] > best) { best = csz[k]; heavy = k; }
         }
-        V.tour[crio[k].x] = val;
-        V.tour[crio[k].y] = -val;
-    }
+        V.heavy[v] = (int8_t)heavy;
+        uint32_t off = 1u + (heavy >= 0 ? csz[heavy] : 0u);
+    #pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!(adj & (1u << k)) || k == pd) continue;
+            long long val = 1;  // the heavy child: offset 1, not light
+            if (k != heavy) {
+                val = (1ll << 32) + (long long)off;
+                off += csz[k];
+            }
+            V.tour[crio[k].x] = val;
+            V.tour[crio[k].y] = -val;
+        }
+    });
 }
 
-// ---- generic inclusive scan, 3 phases (block sums, scan of block sums, block scan + carry)
-#define SCAN_BLOCK 1024
-#define SCAN_ITEMS 8   // items per thread -> 8192 per block
+// ---- inclusive scans: single pass with decoupled look-back (round 5; a 3-phase scan read everything
+// twice, with 8-item per-thread strides: 210 us of the layout's ~950 at C2).  A tile of SP_TILE elements
+// per 256-thread block takes its tile id from a ticket (tiles start in id order, so every tile a block
+// waits for has started: no deadlock), scans in registers (each wave 16 chunks of 64 consecutive
+// elements, coalesced), publishes its aggregate, looks back over its predecessors' aggregates / inclusive
+// prefixes until an inclusive one, publishes its own inclusive prefix and writes its results in place.
+// Status words hold (epoch << 2 | status): no reset between scans; the hand-off is the agent-scope
+// release / acquire protocol of sm_chain.hip, and a wait that gives up sets the call's error word.
+#define SP_THREADS 256
+#define SP_ITEMS 16
+#define SP_TILE (SP_THREADS * SP_ITEMS)
 
 struct OpAdd {
     template <class T> __device__ static T apply(T a, T b) { return a + b; }
@@ -201,6 +242,9 @@ struct OpMax {
     template <class T> __device__ static T apply(T a, T b) { return a > b ? a : b; }
     template <class T> __device__ static T ident() { return T(0); }
 };
+
+// block-wide exclusive scan of one value per thread (SCAN_BLOCK threads; k_long_segments)
+#define SCAN_BLOCK 1024
 
 template <class T, class Op>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* sh, T* total) {
@@ -236,145 +280,151 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* sh, T* total) {
 template <class T>
 struct ScanBufs {
     T* data[2];
-    T* bsum[2];
+    uint32_t* ctr[2];  // tile tickets (zeroed before the launch)
 };
 
 template <class T, class Op>
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(ScanBufs<T> B, int nelem) {
-    __shared__ T sh[SCAN_BLOCK / 64];
-    const T* d = B.data[blockIdx.y];
-    const size_t base = (size_t)blockIdx.x * SCAN_BLOCK * SCAN_ITEMS;
-    T s = Op::template ident<T>();
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const size_t j = base + (size_t)threadIdx.x * SCAN_ITEMS + i;
-        if (j < (size_t)nelem) s = Op::apply(s, d[j]);
+__global__ __launch_bounds__(SP_THREADS) void k_scan(ScanBufs<T> B, ScanState S, int nelem, uint32_t epoch) {
+    const int v = blockIdx.y;
+    __shared__ uint32_t s_tile;
+    __shared__ T s_w[SP_THREADS / 64];
+    __shared__ T s_prefix;
+    if (threadIdx.x == 0) s_tile = atomicAdd(B.ctr[v], 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    T* d = B.data[v];
+    const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+    const size_t wbase = (size_t)tile * SP_TILE + (size_t)w * 64 * SP_ITEMS;
+    T x[SP_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SP_ITEMS; ++j) {
+        const size_t i = wbase + (size_t)j * 64 + lane;
+        x[j] = i < (size_t)nelem ? d[i] : Op::template ident<T>();
     }
-    T tot;
-    block_exclusive_scan<T, Op>(s, sh, &tot);
-    if (threadIdx.x == 0) B.bsum[blockIdx.y][blockIdx.x] = tot;
-}
-
-template <class T, class Op>
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_bsums(ScanBufs<T> B, int nblocks) {
-    __shared__ T sh[SCAN_BLOCK / 64];
-    T* bs = B.bsum[blockIdx.y];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < SP_ITEMS; ++j) {
+            const T y = __shfl_up(x[j], off);
+            if (lane >= off) x[j] = Op::apply(y, x[j]);
+        }
     T carry = Op::template ident<T>();
-    for (int b0 = 0; b0 < nblocks; b0 += SCAN_BLOCK) {
-        const int b = b0 + threadIdx.x;
-        const T v = b < nblocks ? bs[b] : Op::template ident<T>();
-        T tot;
-        const T ex = block_exclusive_scan<T, Op>(v, sh, &tot);
-        if (b < nblocks) bs[b] = Op::apply(carry, ex);  // exclusive block offsets
+#pragma unroll
+    for (int j = 0; j < SP_ITEMS; ++j) {
+        const T tot = __shfl(x[j], 63);
+        x[j] = Op::apply(carry, x[j]);
         carry = Op::apply(carry, tot);
     }
+    if (lane == 0) s_w[w] = carry;
+    __syncthreads();
+    T wpre = Op::template ident<T>(), btot = Op::template ident<T>();
+#pragma unroll
+    for (int k = 0; k < SP_THREADS / 64; ++k) {
+        if (k < w) wpre = Op::apply(wpre, s_w[k]);
+        btot = Op::apply(btot, s_w[k]);
+    }
+    if (threadIdx.x == 0) {
+        T* agg = reinterpret_cast<T*>(S.agg[v]);
+        T* incl = reinterpret_cast<T*>(S.incl[v]);
+        uint32_t* flag = S.flag[v];
+        T prefix = Op::template ident<T>();
+        if (tile > 0) {
+            __hip_atomic_store(agg + tile, btot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag + tile, (epoch << 2) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int t = (int)tile - 1; t >= 0;) {
+                uint32_t f = 0;
+                int it = 0;
+                for (; it < S.wait_iters; ++it) {
+                    f = __hip_atomic_load(flag + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((f >> 2) == epoch && (f & 3u)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (it == S.wait_iters) {  // a predecessor never published: flag the call, give up
+                    __hip_atomic_fetch_or(S.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if ((f & 3u) == 2u) {
+                    prefix = Op::apply(__hip_atomic_load(incl + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prefix);
+                    break;
+                }
+                prefix = Op::apply(__hip_atomic_load(agg + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prefix);
+                --t;
+            }
+        }
+        __hip_atomic_store(incl + tile, Op::apply(prefix, btot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flag + tile, (epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = prefix;
+    }
+    __syncthreads();
+    const T pre = Op::apply(s_prefix, wpre);
+#pragma unroll
+    for (int j = 0; j < SP_ITEMS; ++j) {
+        const size_t i = wbase + (size_t)j * 64 + lane;
+        if (i < (size_t)nelem) d[i] = Op::apply(pre, x[j]);  // inclusive
+    }
 }
 
 template <class T, class Op>
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(ScanBufs<T> B, int nelem) {
-    __shared__ T sh[SCAN_BLOCK / 64];
-    T* d = B.data[blockIdx.y];
-    const size_t base = (size_t)blockIdx.x * SCAN_BLOCK * SCAN_ITEMS;
-    T loc[SCAN_ITEMS];
-    T s = Op::template ident<T>();
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const size_t j = base + (size_t)threadIdx.x * SCAN_ITEMS + i;
-        loc[i] = j < (size_t)nelem ? d[j] : Op::template ident<T>();
-        s = Op::apply(s, loc[i]);
-    }
-    T acc = Op::apply(B.bsum[blockIdx.y][blockIdx.x], block_exclusive_scan<T, Op>(s, sh, nullptr));
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const size_t j = base + (size_t)threadIdx.x * SCAN_ITEMS + i;
-        acc = Op::apply(acc, loc[i]);
-        if (j < (size_t)nelem) d[j] = acc;  // inclusive
-    }
-}
-
-template <class T, class Op>
-static void launch_scan(hipStream_t st, const ScanBufs<T>& B, int nviews, int nelem) {
+static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S, int nviews, int nelem, uint32_t epoch) {
     if (nelem <= 0) return;
-    const int nblocks = (nelem + SCAN_BLOCK * SCAN_ITEMS - 1) / (SCAN_BLOCK * SCAN_ITEMS);
-    hipLaunchKernelGGL((k_scan_sums<T, Op>), dim3(nblocks, nviews), dim3(SCAN_BLOCK), 0, st, B, nelem);
-    hipLaunchKernelGGL((k_scan_bsums<T, Op>), dim3(1, nviews), dim3(SCAN_BLOCK), 0, st, B, nblocks);
-    hipLaunchKernelGGL((k_scan_apply<T, Op>), dim3(nblocks, nviews), dim3(SCAN_BLOCK), 0, st, B, nelem);
+    const int ntiles = (nelem + SP_TILE - 1) / SP_TILE;
+    hipLaunchKernelGGL((k_scan<T, Op>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem, epoch);
 }
 
-// preorder + light depth per pixel from the scanned tour; path heads in preorder numbering:
-// headflag[pre] = 0 (not a head) or 1 + light depth, headpos[pre] = pre + 1 at heads (0 elsewhere; the
-// max-scan's input).  A node is a head iff it is the root or not its parent's heavy child (round 5:
-// k_heads and k_path_prep fused in)
+// Preorder + light depth per pixel from the scanned tour, written by preorder position (the layout's
+// random-access passes are its cost when frames are in flight; round 5 packs what the later passes
+// read into two scatters here): hk[pre] = (pre + 1) << 32 | (light depth + 1) at a path head, 0
+// elsewhere -- after an inclusive max-scan every position holds its path's head and that head's light
+// depth -- and pixpre[pre] = the pixel.  A node is a head iff it is the root or not its parent's heavy
+// child.
 __global__ void k_assign(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const uint32_t q = (uint32_t)(y * W + x);
-    const int pd = V.pdir[q];
-    uint32_t pre = 0, ld = 0;
-    bool head = true;
-    if (pd >= 0) {
-        const long long v = V.tour[V.rio[q].x];
-        pre = (uint32_t)(v & 0xFFFFFFFFll);
-        ld = (uint32_t)(v >> 32);
-        head = V.heavy[nbr_of(q, pd, W)] != ((pd + 2) & 3);
-    }
-    V.pre[q] = pre;
-    V.ld[q] = ld;
-    V.headflag[pre] = head ? 1u + ld : 0u;
-    V.headpos[pre] = head ? pre + 1u : 0u;
+    tile_pixels(layout_tile(W, H, (int)blockIdx.x), W, H, [&](uint32_t q) {
+        const int pd = V.pdir[q];
+        uint32_t pre = 0, ld = 0;
+        bool head = true;
+        if (pd >= 0) {
+            const long long v = V.tour[V.rio[q].x];
+            pre = (uint32_t)(v & 0xFFFFFFFFll);
+            ld = (uint32_t)(v >> 32);
+            head = V.heavy[nbr_of(q, pd, W)] != ((pd + 2) & 3);
+        }
+        if (pre >= (uint32_t)(W * H) || ld >= (uint32_t)SM_MAX_ROUNDS) {  // only after a scan gave up (err set)
+            __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        V.hk[pre] = head ? ((uint64_t)(pre + 1u) << 32) | (uint64_t)(ld + 1u) : 0ull;
+        V.pixpre[pre] = q;
+    });
 }
 
-// Per pixel: its slot, the pixel of every slot, and one packed 64-bit record
-//   slot:32 | adj:4 | pdir+1:3 | heavy+1:3 | wR:10 | wD:10
-// so that k_meta, which runs in slot order (consecutive slots walk heavy paths, i.e. neighbouring
-// pixels, and the 32-byte metadata records are written contiguously), reads one word for itself
-// and one per tree neighbour instead of ~15 scattered byte / short / word loads.
-#define PR_SLOT(r) ((uint32_t)(r))
-#define PR_ADJ(r) ((uint32_t)((r) >> 32) & 15u)
-#define PR_PDIR(r) ((int)((uint32_t)((r) >> 36) & 7u) - 1)
-#define PR_HEAVY(r) ((int)((uint32_t)((r) >> 39) & 7u) - 1)
-#define PR_WR(r) ((uint32_t)((r) >> 42) & 1023u)
-#define PR_WD(r) ((uint32_t)((r) >> 52) & 1023u)
-
-__global__ void k_slotpix(LayoutPair LP, int W, int H) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.z];
-    const int y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const uint32_t v = (uint32_t)(y * W + x);
-    // the slot: the paths of one (light depth, long/short) bucket occupy a contiguous slot range, each
-    // path contiguous from its head (= preorder contiguity of heavy paths), in paths[] order; plen holds
-    // the inclusive scan of the lengths, i.e. the end slot of a path (round 5: k_newslot fused in)
-    const uint32_t s = V.pre[v];
-    const uint32_t head = V.headpos[s] - 1u;
-    const uint32_t P = V.pathpos[head];
-    const uint32_t len = V.paths[P].len;
-    const uint32_t nh = V.plen[P] - len;
-    const uint32_t slot = nh + (s - head);
-    if (s == head) V.paths[P].head = nh;  // (other threads read .len only)
-    V.slotpix[v] = slot;
-    V.slot2pix[slot] = v;
-    V.prec[v] = (uint64_t)slot | ((uint64_t)V.adj[v] << 32) | ((uint64_t)(V.pdir[v] + 1) << 36) |
-                ((uint64_t)(V.heavy[v] + 1) << 39) | ((uint64_t)(V.wR[v] & 1023u) << 42) |
-                ((uint64_t)(V.wD[v] & 1023u) << 52);
-}
-
-// per-slot metadata in slot numbering: pixel, parent slot, child weights and slots in
-// descending (w,a,b) key order (the reference's fold order), heavy-child position, light flag
+// Per-slot metadata: pixel, parent slot, child weights and slots in descending (w,a,b) key order (the
+// reference's fold order), heavy-child position, light flag.  Round 5: computed in pixel order, where a
+// node's tree neighbours are its grid neighbours (local reads), and written to its slot (one random
+// 32-byte store) -- in slot order it had gathered a packed record of the node and of every neighbour.
 #define META_BLOCKS 1024  // blocks per view (grid-stride): one has-light atomic per block
 
-__global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
+__global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
     uint32_t nlight = 0;
-    for (uint32_t slot = blockIdx.x * 256 + threadIdx.x; slot < (uint32_t)N; slot += META_BLOCKS * 256) {
-        const uint32_t v = V.slot2pix[slot];
-        const uint64_t me = V.prec[v];
-        const uint32_t adj = PR_ADJ(me);
-        const int pd = PR_PDIR(me), hv = PR_HEAVY(me);
-        // the tree neighbours' records: slot, and the weight of the edge to v for left / up ones
-        uint64_t nr[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) nr[k] = (adj & (1u << k)) ? V.prec[nbr_of(v, k, W)] : 0ull;
+    // tiles in the XCD-aware order, grid-stride (META_BLOCKS is a multiple of 8: a block keeps its XCD band)
+    const int nb = layout_tile_blocks(W, H);
+    for (int b = (int)blockIdx.x; b < nb; b += META_BLOCKS) tile_pixels(layout_tile(W, H, b), W, H, [&](uint32_t v) {
+        const uint32_t adj = V.adj[v];
+        const int pd = V.pdir[v], hv = V.heavy[v];
+        const uint32_t slot = V.slotpix[v];
+        if (slot >= (uint32_t)(W * H)) {  // (a layout whose scan gave up: err set, never write out of range)
+            __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
         // the children in descending key order by a fixed 5-comparator network over the 4 directions
         // (absent ones sort last; keys are unique): no local array is indexed at run time, which
         // would put them in scratch memory
@@ -386,17 +436,19 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const bool in = (adj & (1u << k)) != 0;
-            // key_dir without the weight loads: right / down edges are v's own, left / up the neighbour's
-            const uint32_t w = k == 0 ? PR_WR(me) : k == 1 ? PR_WD(me) : k == 2 ? PR_WR(nr[k]) : PR_WD(nr[k]);
-            const uint32_t a = k == 0 || k == 1 ? v : nbr_of(v, k, W);
-            const uint64_t key = sm_edge_key(w, a, (uint32_t)(k & 1));
+            const uint32_t n = in ? nbr_of(v, k, W) : v;
+            // right / down edges are v's own, left / up the neighbour's
+            const uint32_t w = k == 0 ? V.wR[v] : k == 1 ? V.wD[v] : k == 2 ? V.wR[n] : V.wD[n];
+            const uint32_t a = k == 0 || k == 1 ? v : n;
+            const uint64_t key = sm_edge_key(w & 1023u, a, (uint32_t)(k & 1));
+            const uint32_t ns = in ? V.slotpix[n] : SM_NONE;
             if (in && k == pd) {
                 wp = (uint32_t)(key >> 33);
-                parent = PR_SLOT(nr[k]);
+                parent = ns;
             }
             ck[k] = key;
             cq[k] = k;
-            cs[k] = PR_SLOT(nr[k]);
+            cs[k] = ns;
             cv[k] = in && k != pd;
         }
         auto cswap = [&](int i, int j) __attribute__((always_inline)) {  // i, j constants after unrolling
@@ -423,7 +475,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
         }
         V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
         nlight += has_light;
-    }
+    });
     __shared__ uint32_t nl;
     if (threadIdx.x == 0) nl = 0;
     __syncthreads();
@@ -433,8 +485,25 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int N) {
 }
 
 // heads in preorder -> path lengths -> bucketed by light depth (order inside a round is free).
-// headpos[s] = s+1 at heads (0 elsewhere, k_assign); after an inclusive max-scan it is 1 + the
-// preorder position of the head of s's path (heavy paths are contiguous in preorder).
+// After the inclusive max-scan of hk (k_assign), hk[s] >> 32 is 1 + the preorder position of the head
+// of s's path (heavy paths are contiguous in preorder) and its low word 1 + that head's light depth;
+// s is the last node of its path iff s + 1 is a head.
+__device__ __forceinline__ bool path_last(const LayoutView& V, uint32_t s, int N) {
+    return s + 1 == (uint32_t)N || (uint32_t)(V.hk[s + 1] >> 32) == s + 2u;
+}
+// the path ending at s: its head and (light depth, long/short) bucket; false (and the error word set)
+// only for a layout whose scan gave up -- nothing is then written out of range
+__device__ __forceinline__ bool path_of(const LayoutPair& LP, const LayoutView& V, uint32_t s, uint32_t& head, uint32_t& b) {
+    const uint64_t h = V.hk[s];
+    head = (uint32_t)(h >> 32) - 1u;
+    const uint32_t ld = (uint32_t)h - 1u;
+    if (head > s || ld >= (uint32_t)SM_MAX_ROUNDS) {
+        __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+    }
+    b = 2u * ld + (s - head + 1u >= SM_LONG_PATH ? 0u : 1u);
+    return true;
+}
 #define PATH_BLOCK 1024
 #define PATH_ITEMS 8   // slots per thread -> 8192 per block (few global atomics per round bin)
 
@@ -449,10 +518,9 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N)
     for (int i = 0; i < PATH_ITEMS; ++i) {
         const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
         if (s >= (uint32_t)N) break;
-        if (s + 1 == (uint32_t)N || V.headflag[s + 1] != 0) {
-            const uint32_t head = V.headpos[s] - 1u;
+        uint32_t head, b;
+        if (path_last(V, s, N) && path_of(LP, V, s, head, b)) {
             const uint32_t len = s - head + 1u;
-            const uint32_t b = 2u * (V.headflag[head] - 1u) + (len >= SM_LONG_PATH ? 0u : 1u);
             atomicAdd(&hist[b], 1u);
             atomicAdd(&nodes[b], len);
             if (len >= SM_LONG_PATH) atomicMax(&mlen[b], len);
@@ -493,11 +561,10 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
         const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
         myr[i] = SM_NONE;
         if (s >= (uint32_t)N) continue;
-        const bool is_last = s + 1 == (uint32_t)N || V.headflag[s + 1] != 0;
-        if (!is_last) continue;
-        const uint32_t head = V.headpos[s] - 1u;
+        uint32_t head, b;
+        if (!path_last(V, s, N) || !path_of(LP, V, s, head, b)) continue;
         myhead[i] = head;
-        myr[i] = 2u * (V.headflag[head] - 1u) + (s - head + 1u >= SM_LONG_PATH ? 0u : 1u);
+        myr[i] = b;
         myrank[i] = atomicAdd(&hist[myr[i]], 1u);
     }
     __syncthreads();
@@ -509,10 +576,36 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
         const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
         const uint32_t P = gbase[myr[i]] + myrank[i];
         const uint32_t len = s - myhead[i] + 1u;
-        V.paths[P] = SmPath{myhead[i], len};  // head in preorder numbering until k_slotpix
+        V.paths[P] = SmPath{myhead[i], len};  // head in preorder numbering until k_newslot
         V.pathpos[myhead[i]] = P;
         V.plen[P] = len;
     }
+}
+
+// Slots, in preorder order (coalesced): the paths of one (light depth, long/short) bucket occupy a
+// contiguous slot range, each path contiguous from its head, in paths[] order; plen holds the inclusive
+// scan of the lengths, i.e. the end slot of a path.  slot2pix is written nearly in order (a path's slots
+// are consecutive), slotpix is the pass's one random store.
+__global__ void k_newslot(LayoutPair LP, int N) {
+    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
+    const LayoutView& V = LP.v[blockIdx.y];
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= (uint32_t)N) return;
+    const uint32_t head = (uint32_t)(V.hk[s] >> 32) - 1u;
+    // every index below comes from the scans: a layout whose scan gave up (err set) must not write out
+    // of range (round 5: a forced-timeout run did)
+    const uint32_t P = head <= s ? V.pathpos[head] : SM_NONE;
+    const uint32_t len = P < (uint32_t)N ? V.paths[P].len : 0u;
+    const uint32_t nh = P < (uint32_t)N ? V.plen[P] - len : SM_NONE;
+    const uint32_t slot = nh + (s - head);
+    const uint32_t pix = V.pixpre[s];
+    if (P >= (uint32_t)N || slot >= (uint32_t)N || pix >= (uint32_t)N) {
+        __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    V.slotpix[pix] = slot;
+    V.slot2pix[slot] = pix;
+    if (s == head) V.paths[P].head = nh;  // (other threads read .len only)
 }
 
 // segment table of the long-path buckets: segment i of bucket b -> {path within b, SM_PRE_SEG-node
@@ -684,27 +777,28 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     const int N = W * H;
     const dim3 pg = pix_grid(W, H, nviews);
     hipLaunchKernelGGL(k_adj, pg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_tour_tile, dim3((W + TL - 1) / TL, (H + TL - 1) / TL, nviews), dim3(TL_THREADS), 0, st, LP, W, H);
+    const dim3 tg(layout_tile_blocks(W, H), 1, nviews);  // XCD-aware 32x32 tiles (layout_tile)
+    hipLaunchKernelGGL(k_tour_tile, tg, dim3(TL_THREADS), 0, st, LP, W, H);
     const dim3 cg((max_chains + 255) / 256, nviews);
     hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
-    hipLaunchKernelGGL(k_orient, pg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_heavy, pg, dim3(256), 0, st, LP, W, H);
-    ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}, {LP.v[0].bsum, LP.v[1].bsum}};
-    launch_scan<long long, OpAdd>(st, tb, nviews, 2 * N - 2);
-    hipLaunchKernelGGL(k_assign, pg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_orient, tg, dim3(256), 0, st, LP, W, H);
+    hipLaunchKernelGGL(k_heavy, tg, dim3(256), 0, st, LP, W, H);
+    ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}, {LP.v[0].sctr, LP.v[1].sctr}};
+    launch_scan<long long, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, LP.scan_epoch);
+    hipLaunchKernelGGL(k_assign, tg, dim3(256), 0, st, LP, W, H);
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
-    ScanBufs<uint32_t> hb{{LP.v[0].headpos, LP.v[1].headpos}, {LP.v[0].bsum32, LP.v[1].bsum32}};
-    launch_scan<uint32_t, OpMax>(st, hb, nviews, N);
+    ScanBufs<uint64_t> hb{{LP.v[0].hk, LP.v[1].hk}, {LP.v[0].sctr + 1, LP.v[1].sctr + 1}};
+    launch_scan<uint64_t, OpMax>(st, hb, LP.scan, nviews, N, LP.scan_epoch + 1);
     hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     hipLaunchKernelGGL(k_path_offsets, dim3(nviews), dim3(64), 0, st, LP);
     hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     // contiguous bucket slots: scan of path lengths in paths[] order (plen is zero past the last
     // path), slot of every preorder position, then the metadata in slot numbering
-    ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}, {LP.v[0].bsum32, LP.v[1].bsum32}};
-    launch_scan<uint32_t, OpAdd>(st, lb, nviews, N);
-    hipLaunchKernelGGL(k_slotpix, pg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, N);
+    ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}, {LP.v[0].sctr + 2, LP.v[1].sctr + 2}};
+    launch_scan<uint32_t, OpAdd>(st, lb, LP.scan, nviews, N, LP.scan_epoch + 2);
+    hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
+    hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, H);
     // run sizing (A/B knobs: SM_RUN_DIV, SM_RUN_CAP = the window cap in nodes)
     const char* ed = getenv("SM_RUN_DIV");
     const char* ec = getenv("SM_RUN_CAP");

@@ -244,7 +244,9 @@ __global__ void k_pf_rot2(PfView v) {
     v.rot[p] = r;
 }
 
-__global__ void k_pf_tour_tile(PfView v) { tour_tile(PfTourG{v.rot, v.W}, pf_tour_bufs(v), v.W, v.H); }
+__global__ void k_pf_tour_tile(PfView v) {
+    tour_tile(PfTourG{v.rot, v.W}, pf_tour_bufs(v), v.W, v.H, (int)blockIdx.x * TL, (int)blockIdx.y * TL);
+}
 
 __global__ void k_pf_chain_init(PfView v) {
     tour_chain_init(PfTourG{v.rot, v.W}, pf_tour_bufs(v), blockIdx.x * blockDim.x + threadIdx.x);

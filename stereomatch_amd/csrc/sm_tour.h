@@ -38,18 +38,17 @@ __device__ __forceinline__ uint32_t tour_nbr(uint32_t p, int k, int W) {
     return k == 0 ? p + 1 : k == 1 ? p + (uint32_t)W : k == 2 ? p - 1 : p - (uint32_t)W;
 }
 
-// L1: contract the lists inside the 32x32 tile (blockIdx.x, blockIdx.y).  One 64-bit LDS word per arc
+// L1: contract the lists inside the 32x32 tile at (tx0, ty0).  One 64-bit LDS word per arc
 // slot, nxt | dist << 16 | last << 32, so a jump is one gathered word; every thread keeps its 16 words
 // in registers.
 template <class G>
-__device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, int H) {
+__device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, int H, int tx0, int ty0) {
     __shared__ union {
         uint64_t w[TLS];
         uint16_t h[4 * TLS];  // once the jumping is done, h[4*s + 2]: the tile-local id of the chain whose
                               // last slot is s (bits 32..47 of w[s], which nobody reads any more)
     } st;
     __shared__ uint8_t haspred[TLS];
-    const int tx0 = blockIdx.x * TL, ty0 = blockIdx.y * TL;
     constexpr int PER = TLS / TL_THREADS;  // 16 slots per thread
     for (int i = 0; i < PER; ++i) haspred[threadIdx.x + i * TL_THREADS] = 0;
     __syncthreads();
@@ -82,21 +81,25 @@ __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, 
         st.w[s] = own[i];
     }
     __syncthreads();
-    // pointer jumping: dist -> arcs to chain end (inclusive), last -> chain's last slot
+    // pointer jumping: dist -> arcs to chain end (inclusive), last -> chain's last slot.  Only the words
+    // that moved are written back (a word that reached its chain's end is final in LDS already): the
+    // loop is bound by LDS traffic, and most chains finish long before the tile's longest
     for (int it = 0; it < 13; ++it) {
-        bool any = false;
+        uint32_t moved = 0;
+#pragma unroll
         for (int i = 0; i < PER; ++i) {
             const uint32_t n = (uint32_t)own[i] & 0xFFFFu;
             if (n < L_NIL) {
                 const uint64_t nb = st.w[n];
                 const uint32_t d = (uint32_t)(own[i] >> 16) + (uint32_t)(nb >> 16);  // low 16 bits: the sum
                 own[i] = (nb & 0xFFFF0000FFFFull) | ((uint64_t)(d & 0xFFFFu) << 16);
-                any = true;
+                moved |= 1u << i;
             }
         }
-        any = __syncthreads_or(any);
-        if (!any) break;
-        for (int i = 0; i < PER; ++i) st.w[threadIdx.x + i * TL_THREADS] = own[i];
+        if (!__syncthreads_or(moved != 0)) break;
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+            if ((moved >> i) & 1u) st.w[threadIdx.x + i * TL_THREADS] = own[i];
         __syncthreads();
     }
     // heads: existing arcs without an in-tile predecessor; register chains

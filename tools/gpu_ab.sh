@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/ab
 mkdir -p $O
 REPS=${REPS:-1}
-BASE_ARGS=${BASE_ARGS:---steps 20 --warmup 5 --no-cpu --no-host-io --no-pms}
+BASE_ARGS=${BASE_ARGS:---steps 20 --warmup 5 --no-cpu --no-host-io --no-pms --no-segment}
 for rep in $(seq 1 $REPS); do
   for spec in "$@"; do
     label=${spec%%|*}; rest=${spec#*|}; envs=${rest%%|*}; args=${rest#*|}
