@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 
 #include <hipcub/device/device_radix_sort.hpp>
 #include <hipcub/device/device_scan.hpp>
@@ -366,6 +367,21 @@ __global__ void k_pf_fields(PfView v) {
     v.ghk[n] = (int8_t)best;
 }
 
+// test hook (SM_TEST_PMS_CYCLE=1, tests/test_pms_gpu.py): the square of pixels 0, 1, W, W + 1 becomes four
+// real edges -- a cycle, which the build must refuse (k_pf_edges) rather than tour
+__global__ void k_pf_test_cycle(PfView v) {
+    if (threadIdx.x != 0 || v.W < 2 || v.H < 2) return;
+    uint8_t* mR = const_cast<uint8_t*>(v.mR);
+    uint8_t* mD = const_cast<uint8_t*>(v.mD);
+    uint16_t* fwR = const_cast<uint16_t*>(v.fwR);
+    uint16_t* fwD = const_cast<uint16_t*>(v.fwD);
+    mR[0] = mD[0] = mR[v.W] = mD[1] = 1;
+    fwR[0] = v.wR[0];
+    fwD[0] = v.wD[0];
+    fwR[v.W] = v.wR[v.W];
+    fwD[1] = v.wD[1];
+}
+
 // real tree edges of the view (a forest of N nodes in K trees has exactly N - K)
 __global__ void k_pf_edges(PfView v) {
     const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -696,6 +712,8 @@ static int bits_for(int n) {
 
 hipError_t pf_trees(hipStream_t st, PfView& v, int* K_out) {
     const int N = v.N;
+    if (getenv("SM_TEST_PMS_CYCLE") && atoi(getenv("SM_TEST_PMS_CYCLE")) == 1)
+        hipLaunchKernelGGL(k_pf_test_cycle, dim3(1), dim3(64), 0, st, v);
     hipLaunchKernelGGL(k_pf_prep, dim3(nblk(N, 256)), dim3(256), 0, st, v);
     hipLaunchKernelGGL(k_pf_link, dim3(nblk(N, 256)), dim3(256), 0, st, v);
     hipLaunchKernelGGL(k_pf_compress, dim3(nblk(N + 1, 256)), dim3(256), 0, st, v);

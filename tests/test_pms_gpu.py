@@ -165,6 +165,22 @@ def test_pms_bad_params(gpu_ctx):
     assert e.value.status == 5
 
 
+def test_pms_forest_cycle_is_an_error(gpu_ctx, monkeypatch):
+    """Masks that are not a forest (SM_TEST_PMS_CYCLE=1 turns the square of pixels 0, 1, W, W + 1 into
+    four real edges) are refused before any Euler tour -- whose list ranking would never end -- with
+    SM_ERR_STATE; the next call on the same context is exact again."""
+    left, right, _ = make_pair(96, 64, 24, index=2)
+    monkeypatch.setenv("SM_TEST_PMS_CYCLE", "1")
+    with pytest.raises(sm.StereoMSTError, match="cycle") as e:
+        run_gpu(gpu_ctx, left, right, 24, 1, 300.0, 20)
+    assert e.value.status == 5
+    monkeypatch.delenv("SM_TEST_PMS_CYCLE")
+    ref = O.stereo3dmst_pms(left, right, 24, iters=1, c=300.0, min_size=20)
+    out, labs, st = run_gpu(gpu_ctx, left, right, 24, 1, 300.0, 20)
+    for v in ("left", "right"):
+        check_view(out, labs, ref, v)
+
+
 @pytest.mark.timeout(600)
 def test_pms_full_c2_one_call_bitexact(gpu_ctx):
     """Full C2 (1920x1200, Dmax 128), the reference's segment mode (c=5000, min_size 200), one MST_PMS
