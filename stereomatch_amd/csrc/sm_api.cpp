@@ -170,8 +170,7 @@ struct sm_ctx {
     DevBuf a_dist[2], a_cid[2], ccount[2], c_last[2], c_len[2];
     DevBuf segtab[2], pathpos[2], plen[2], slotpix[2], slot2pix[2];
     DevBuf pieces[2], pieces_tmp[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
-    DevBuf cnw[2], tour[2], sctr[2], sflag[2], sagg[2], sincl[2], rounds[2];
-    uint32_t scan_epoch = 1;  // the layout scans' look-back epochs (3 per layout)
+    DevBuf cnw[2], tour[2], spart[2], rounds[2];
     int* h_changed = nullptr;
     uint32_t* h_err = nullptr;  // pinned, device-visible error word of the chain engine's waits
     uint32_t* d_err = nullptr;  // its device address
@@ -1039,12 +1038,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->c_len[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->cnw[v], max_chains * 8));
         CHECK(ensure(ctx, ctx->tour[v], 2 * N * 8 + 16));
-        CHECK(ensure(ctx, ctx->sctr[v], 16));
-        const bool fresh = ctx->sflag[v].n < nscan * 4;  // status words start at epoch 0 (never current)
-        CHECK(ensure(ctx, ctx->sflag[v], nscan * 4));
-        if (fresh) HIPC(hipMemsetAsync(ctx->sflag[v].p, 0, nscan * 4, ctx->st));
-        CHECK(ensure(ctx, ctx->sagg[v], nscan * 8));
-        CHECK(ensure(ctx, ctx->sincl[v], nscan * 8));
+        CHECK(ensure(ctx, ctx->spart[v], nscan * 8));
         CHECK(ensure(ctx, ctx->meta[v], N * sizeof(SmMeta)));
         CHECK(ensure(ctx, ctx->paths[v], N * sizeof(SmPath)));
         CHECK(ensure(ctx, ctx->rounds[v], RREC * 4));
@@ -1058,7 +1052,6 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         z.add(ctx->plen[v].p, N * 4);  // lengths past the last path stay 0
         z.add(ctx->ccount[v].p, 16);
         z.add(ctx->rounds[v].p, RREC * 4);
-        z.add(ctx->sctr[v].p, 16);
         LayoutView& L = LP.v[i];
         L.mR = P<uint8_t>(ctx->mR[v]);
         L.mD = P<uint8_t>(ctx->mD[v]);
@@ -1078,10 +1071,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.c_len = P<uint32_t>(ctx->c_len[v]);
         L.cnw = P<uint64_t>(ctx->cnw[v]);
         L.tour = P<long long>(ctx->tour[v]);
-        L.sctr = P<uint32_t>(ctx->sctr[v]);
-        LP.scan.flag[i] = P<uint32_t>(ctx->sflag[v]);
-        LP.scan.agg[i] = P<uint64_t>(ctx->sagg[v]);
-        LP.scan.incl[i] = P<uint64_t>(ctx->sincl[v]);
+        LP.scan.part[i] = P<uint64_t>(ctx->spart[v]);
         L.meta = P<SmMeta>(ctx->meta[v]);
         L.paths = P<SmPath>(ctx->paths[v]);
         L.pathpos = P<uint32_t>(ctx->pathpos[v]);
@@ -1104,20 +1094,8 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
     }
     if (nviews == 1) LP.v[1] = LP.v[0];
     LP.mst_ok = P<int>(ctx->mst_ok);
-    if (nviews == 1) {
-        LP.scan.flag[1] = LP.scan.flag[0];
-        LP.scan.agg[1] = LP.scan.agg[0];
-        LP.scan.incl[1] = LP.scan.incl[0];
-    }
+    if (nviews == 1) LP.scan.part[1] = LP.scan.part[0];
     LP.scan.err = ctx->d_err;
-    // (a fixed bound: SM_WAIT_ITERS, which the forced-timeout test lowers, is the chain engine's)
-    LP.scan.wait_iters = 1 << 22;
-    if (ctx->scan_epoch >= (1u << 29)) {  // wrapped: clear every status word
-        for (int i = 0; i < nviews; ++i) HIPC(hipMemsetAsync(ctx->sflag[vs.v[i]].p, 0, nscan * 4, ctx->st));
-        ctx->scan_epoch = 1;
-    }
-    LP.scan_epoch = ctx->scan_epoch;
-    ctx->scan_epoch += 3;
     HIPC(launch_zero(ctx->st, z));
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains, (uint32_t)piece_len()));
     // the host needs the per-round path counts to size the walker grids
@@ -1129,13 +1107,11 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
 
 sm_status stage_layout_finish(sm_ctx* ctx, int views) {
     HIPC(hipEventSynchronize(ctx->ev_layout));
-    // a layout scan whose look-back wait gave up (bit 0) or an index it produced out of range (bit 1):
-    // the metadata is not a tree layout, so no filter may run over it (its indices would be wild)
-    if (const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE)) {
-        __atomic_store_n(ctx->h_err, 0u, __ATOMIC_RELEASE);
-        return fail(ctx, SM_ERR_STATE, (e & 2u) ? "tree layout: an index out of range after a scan's look-back gave up"
-                                                : "tree layout: a scan's look-back wait timed out");
-    }
+    // a layout index out of range (bit 1, the layout kernels' guards): the metadata is not a tree
+    // layout, so no filter may run over it (its indices would be wild).  Only bit 1 is the layout's: the
+    // other bits belong to the filter of a frame still in flight.
+    if (__atomic_fetch_and(ctx->h_err, ~2u, __ATOMIC_ACQ_REL) & 2u)
+        return fail(ctx, SM_ERR_STATE, "tree layout: an index out of range (the MST tour is not a spanning tree's)");
     bool grew = false;
     CHECK(mst_finish(ctx, &grew));
     if (grew) return stage_layout(ctx, views);  // the forest was incomplete: lay out the final MST
@@ -2470,9 +2446,9 @@ sm_status upload(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, 
 // the chain engine's error word (written by the device through the host mapping): reported once,
 // then cleared so the context stays usable
 sm_status check_device_error(sm_ctx* ctx) {
-    const uint32_t e = __atomic_load_n(ctx->h_err, __ATOMIC_ACQUIRE);
+    // (bit 1 is the tree layout's, checked by stage_layout_finish: a later frame's may be in flight)
+    const uint32_t e = __atomic_fetch_and(ctx->h_err, 2u, __ATOMIC_ACQ_REL) & ~2u;
     if (!e) return SM_OK;
-    __atomic_store_n(ctx->h_err, 0u, __ATOMIC_RELEASE);
     return fail(ctx, SM_ERR_STATE,
                 "long-path chain engine: a cross-workgroup wait timed out (piece status word never published); "
                 "the results of this call are invalid");
@@ -2618,7 +2594,7 @@ void sm_destroy(sm_ctx* ctx) {
         DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->rio[v],
                          &ctx->hk[v], &ctx->pixpre[v], &ctx->a_dist[v], &ctx->a_cid[v],
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->cnw[v],
-                         &ctx->tour[v], &ctx->sctr[v], &ctx->sflag[v], &ctx->sagg[v], &ctx->sincl[v],
+                         &ctx->tour[v], &ctx->spart[v],
                          &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
                          &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);

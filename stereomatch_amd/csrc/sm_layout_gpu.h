@@ -103,7 +103,6 @@ struct LayoutView {
     uint64_t* cnw;      // per chain: successor chain (low 32 bits) | arcs to it (high 32 bits)
     // tour (2N-2); the scans' tile tickets (3, zeroed with the layout's other counters)
     long long* tour;
-    uint32_t* sctr;
     // per heavy-first preorder position (layout-internal numbering)
     uint64_t* hk;        // (1 + head position) << 32 | (1 + light depth) at a path head, 0 elsewhere;
                          // after the max-scan: the position's path head and its light depth
@@ -131,14 +130,10 @@ struct LayoutView {
     uint32_t* n_has_light;   // nodes with at least one light child (roofline accounting)
 };
 
-// the single-pass scans' look-back state (sm_layout_gpu.hip k_scan), per view: per tile its status word
-// (epoch << 2 | 1 aggregate / 2 inclusive prefix) and the two values (64-bit slots)
+// the layout scans' tile totals (sm_layout_gpu.hip k_scan_reduce), per view, one 64-bit slot per tile
 struct ScanState {
-    uint32_t* flag[2];
-    uint64_t* agg[2];
-    uint64_t* incl[2];
-    uint32_t* err;   // the call's device error word: bit 0, a wait gave up
-    int wait_iters;  // polls before a wait gives up
+    uint64_t* part[2];
+    uint32_t* err;  // the call's device error word: bit 1, a layout index out of range
 };
 // tiles of the scans (4096 elements each) over at most 2N elements
 static inline size_t scan_tiles(size_t N) { return (2 * N + 4095) / 4096 + 1; }
@@ -147,7 +142,6 @@ struct LayoutPair {
     LayoutView v[2];
     const int* mst_ok;  // != 0 once the MST is complete (k_mst_done); every layout kernel checks it
     ScanState scan;
-    uint32_t scan_epoch;  // this layout's three scans use epochs scan_epoch .. scan_epoch + 2
 };
 
 hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains,

@@ -222,14 +222,14 @@ __global__ void k_heavy(LayoutPair LP, int W, int H) {
     });
 }
 
-// ---- inclusive scans: single pass with decoupled look-back (round 5; a 3-phase scan read everything
-// twice, with 8-item per-thread strides: 210 us of the layout's ~950 at C2).  A tile of SP_TILE elements
-// per 256-thread block takes its tile id from a ticket (tiles start in id order, so every tile a block
-// waits for has started: no deadlock), scans in registers (each wave 16 chunks of 64 consecutive
-// elements, coalesced), publishes its aggregate, looks back over its predecessors' aggregates / inclusive
-// prefixes until an inclusive one, publishes its own inclusive prefix and writes its results in place.
-// Status words hold (epoch << 2 | status): no reset between scans; the hand-off is the agent-scope
-// release / acquire protocol of sm_chain.hip, and a wait that gives up sets the call's error word.
+// ---- inclusive scans: reduce, then scan (round 5).  A tile is SP_TILE elements per 256-thread block,
+// each wave 16 chunks of 64 consecutive elements (coalesced).  k_scan_reduce writes every tile's total;
+// k_scan_tiles re-reads its tile, takes its exclusive prefix as the reduction of the lower tiles' totals
+// (<= a few thousand L2-resident words per block, so no third launch scans the totals), scans in
+// registers and writes in place.  Nothing waits on another block.  (A single-pass decoupled look-back
+// was tried this round: its status words cross XCDs, so each look-back hop is an agent-scope round trip,
+// and the int64 scan took 193 us at C2 against 89 for the old 3-phase scan; this one reads its data
+// twice but never serialises.)
 #define SP_THREADS 256
 #define SP_ITEMS 16
 #define SP_TILE (SP_THREADS * SP_ITEMS)
@@ -280,18 +280,45 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* sh, T* total) {
 template <class T>
 struct ScanBufs {
     T* data[2];
-    uint32_t* ctr[2];  // tile tickets (zeroed before the launch)
 };
 
+// block-wide reduction of one value per thread (SP_THREADS threads), the result on every thread
 template <class T, class Op>
-__global__ __launch_bounds__(SP_THREADS) void k_scan(ScanBufs<T> B, ScanState S, int nelem, uint32_t epoch) {
-    const int v = blockIdx.y;
-    __shared__ uint32_t s_tile;
-    __shared__ T s_w[SP_THREADS / 64];
-    __shared__ T s_prefix;
-    if (threadIdx.x == 0) s_tile = atomicAdd(B.ctr[v], 1u);
+__device__ __forceinline__ T sp_block_reduce(T x, T* sh) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x = Op::apply(x, __shfl_xor(x, off));  // (add / max: order-free)
+    const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+    __syncthreads();  // sh may still be read by a previous call
+    if (lane == 0) sh[w] = x;
     __syncthreads();
-    const uint32_t tile = s_tile;
+    T r = sh[0];
+#pragma unroll
+    for (int k = 1; k < SP_THREADS / 64; ++k) r = Op::apply(r, sh[k]);
+    return r;
+}
+
+template <class T, class Op>
+__global__ __launch_bounds__(SP_THREADS) void k_scan_reduce(ScanBufs<T> B, ScanState S, int nelem) {
+    const int v = blockIdx.y;
+    __shared__ T sh[SP_THREADS / 64];
+    const T* d = B.data[v];
+    const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+    const size_t wbase = (size_t)blockIdx.x * SP_TILE + (size_t)w * 64 * SP_ITEMS;
+    T x = Op::template ident<T>();
+#pragma unroll
+    for (int j = 0; j < SP_ITEMS; ++j) {
+        const size_t i = wbase + (size_t)j * 64 + lane;
+        if (i < (size_t)nelem) x = Op::apply(x, d[i]);
+    }
+    const T tot = sp_block_reduce<T, Op>(x, sh);
+    if (threadIdx.x == 0) reinterpret_cast<T*>(S.part[v])[blockIdx.x] = tot;
+}
+
+template <class T, class Op>
+__global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanState S, int nelem) {
+    const int v = blockIdx.y;
+    const uint32_t tile = blockIdx.x;
+    __shared__ T s_w[SP_THREADS / 64];
     T* d = B.data[v];
     const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
     const size_t wbase = (size_t)tile * SP_TILE + (size_t)w * 64 * SP_ITEMS;
@@ -301,6 +328,10 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan(ScanBufs<T> B, ScanState S,
         const size_t i = wbase + (size_t)j * 64 + lane;
         x[j] = i < (size_t)nelem ? d[i] : Op::template ident<T>();
     }
+    // the tile's exclusive prefix: the lower tiles' totals (loads in flight with the tile's)
+    const T* part = reinterpret_cast<const T*>(S.part[v]);
+    T pre = Op::template ident<T>();
+    for (uint32_t t = threadIdx.x; t < tile; t += SP_THREADS) pre = Op::apply(pre, part[t]);
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1)
 #pragma unroll
@@ -315,54 +346,13 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan(ScanBufs<T> B, ScanState S,
         x[j] = Op::apply(carry, x[j]);
         carry = Op::apply(carry, tot);
     }
+    pre = sp_block_reduce<T, Op>(pre, s_w);
+    __syncthreads();
     if (lane == 0) s_w[w] = carry;
     __syncthreads();
-    T wpre = Op::template ident<T>(), btot = Op::template ident<T>();
 #pragma unroll
-    for (int k = 0; k < SP_THREADS / 64; ++k) {
-        if (k < w) wpre = Op::apply(wpre, s_w[k]);
-        btot = Op::apply(btot, s_w[k]);
-    }
-    if (threadIdx.x == 0) {
-        T* agg = reinterpret_cast<T*>(S.agg[v]);
-        T* incl = reinterpret_cast<T*>(S.incl[v]);
-        uint32_t* flag = S.flag[v];
-        T prefix = Op::template ident<T>();
-        if (tile > 0) {
-            __hip_atomic_store(agg + tile, btot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(flag + tile, (epoch << 2) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int t = (int)tile - 1; t >= 0;) {
-                uint32_t f = 0;
-                int it = 0;
-                for (; it < S.wait_iters; ++it) {
-                    f = __hip_atomic_load(flag + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((f >> 2) == epoch && (f & 3u)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                if (it == S.wait_iters) {  // a predecessor never published: flag the call, give up
-                    __hip_atomic_fetch_or(S.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if ((f & 3u) == 2u) {
-                    prefix = Op::apply(__hip_atomic_load(incl + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prefix);
-                    break;
-                }
-                prefix = Op::apply(__hip_atomic_load(agg + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prefix);
-                --t;
-            }
-        }
-        __hip_atomic_store(incl + tile, Op::apply(prefix, btot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(flag + tile, (epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_prefix = prefix;
-    }
-    __syncthreads();
-    const T pre = Op::apply(s_prefix, wpre);
+    for (int k = 0; k < SP_THREADS / 64; ++k)
+        if (k < w) pre = Op::apply(pre, s_w[k]);
 #pragma unroll
     for (int j = 0; j < SP_ITEMS; ++j) {
         const size_t i = wbase + (size_t)j * 64 + lane;
@@ -371,10 +361,11 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan(ScanBufs<T> B, ScanState S,
 }
 
 template <class T, class Op>
-static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S, int nviews, int nelem, uint32_t epoch) {
+static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S, int nviews, int nelem) {
     if (nelem <= 0) return;
     const int ntiles = (nelem + SP_TILE - 1) / SP_TILE;
-    hipLaunchKernelGGL((k_scan<T, Op>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem, epoch);
+    hipLaunchKernelGGL((k_scan_reduce<T, Op>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem);
+    hipLaunchKernelGGL((k_scan_tiles<T, Op>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem);
 }
 
 // Preorder + light depth per pixel from the scanned tour, written by preorder position (the layout's
@@ -396,7 +387,7 @@ __global__ void k_assign(LayoutPair LP, int W, int H) {
             ld = (uint32_t)(v >> 32);
             head = V.heavy[nbr_of(q, pd, W)] != ((pd + 2) & 3);
         }
-        if (pre >= (uint32_t)(W * H) || ld >= (uint32_t)SM_MAX_ROUNDS) {  // only after a scan gave up (err set)
+        if (pre >= (uint32_t)(W * H) || ld >= (uint32_t)SM_MAX_ROUNDS) {  // never for a spanning tree's tour (defensive)
             __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
@@ -421,7 +412,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
         const uint32_t adj = V.adj[v];
         const int pd = V.pdir[v], hv = V.heavy[v];
         const uint32_t slot = V.slotpix[v];
-        if (slot >= (uint32_t)(W * H)) {  // (a layout whose scan gave up: err set, never write out of range)
+        if (slot >= (uint32_t)(W * H)) {  // (never for a spanning tree's tour: defensive, err set)
             __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
@@ -492,7 +483,7 @@ __device__ __forceinline__ bool path_last(const LayoutView& V, uint32_t s, int N
     return s + 1 == (uint32_t)N || (uint32_t)(V.hk[s + 1] >> 32) == s + 2u;
 }
 // the path ending at s: its head and (light depth, long/short) bucket; false (and the error word set)
-// only for a layout whose scan gave up -- nothing is then written out of range
+// only for a corrupt layout (defensive) -- nothing is then written out of range
 __device__ __forceinline__ bool path_of(const LayoutPair& LP, const LayoutView& V, uint32_t s, uint32_t& head, uint32_t& b) {
     const uint64_t h = V.hk[s];
     head = (uint32_t)(h >> 32) - 1u;
@@ -592,8 +583,8 @@ __global__ void k_newslot(LayoutPair LP, int N) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= (uint32_t)N) return;
     const uint32_t head = (uint32_t)(V.hk[s] >> 32) - 1u;
-    // every index below comes from the scans: a layout whose scan gave up (err set) must not write out
-    // of range (round 5: a forced-timeout run did)
+    // every index below comes from the scans: a corrupt layout (err set) must not write out of range
+    // (round 5: a look-back scan that gave up did)
     const uint32_t P = head <= s ? V.pathpos[head] : SM_NONE;
     const uint32_t len = P < (uint32_t)N ? V.paths[P].len : 0u;
     const uint32_t nh = P < (uint32_t)N ? V.plen[P] - len : SM_NONE;
@@ -784,19 +775,19 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
     hipLaunchKernelGGL(k_orient, tg, dim3(256), 0, st, LP, W, H);
     hipLaunchKernelGGL(k_heavy, tg, dim3(256), 0, st, LP, W, H);
-    ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}, {LP.v[0].sctr, LP.v[1].sctr}};
-    launch_scan<long long, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, LP.scan_epoch);
+    ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}};
+    launch_scan<long long, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2);
     hipLaunchKernelGGL(k_assign, tg, dim3(256), 0, st, LP, W, H);
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
-    ScanBufs<uint64_t> hb{{LP.v[0].hk, LP.v[1].hk}, {LP.v[0].sctr + 1, LP.v[1].sctr + 1}};
-    launch_scan<uint64_t, OpMax>(st, hb, LP.scan, nviews, N, LP.scan_epoch + 1);
+    ScanBufs<uint64_t> hb{{LP.v[0].hk, LP.v[1].hk}};
+    launch_scan<uint64_t, OpMax>(st, hb, LP.scan, nviews, N);
     hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     hipLaunchKernelGGL(k_path_offsets, dim3(nviews), dim3(64), 0, st, LP);
     hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     // contiguous bucket slots: scan of path lengths in paths[] order (plen is zero past the last
     // path), slot of every preorder position, then the metadata in slot numbering
-    ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}, {LP.v[0].sctr + 2, LP.v[1].sctr + 2}};
-    launch_scan<uint32_t, OpAdd>(st, lb, LP.scan, nviews, N, LP.scan_epoch + 2);
+    ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}};
+    launch_scan<uint32_t, OpAdd>(st, lb, LP.scan, nviews, N);
     hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
     hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, H);
     // run sizing (A/B knobs: SM_RUN_DIV, SM_RUN_CAP = the window cap in nodes)
