@@ -152,63 +152,55 @@ __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
     tour_chain_rank(tour_bufs(LP.v[blockIdx.y]));
 }
 
-// L3 + orientation: an arc's rank is the tour length minus its suffix (sm_tour.h); an arc precedes its
-// reverse iff it goes down, and the rank distance between the two is twice the subtree size.  Per
-// pixel: the direction to its parent, its subtree size and the ranks of its two parent arcs (down
-// into it, up out of it), the only ranks later kernels read (round 5: one pass instead of a rank for
-// every arc in k_tour_rank and k_orient's re-read of them)
+// L3 + orientation + heavy child, one pass per pixel v: an arc's rank is the tour length minus its
+// suffix (sm_tour.h); an arc precedes its reverse iff it goes down, and the rank distance between the
+// two is twice the subtree size below it.  From the two suffixes of each tree edge at v, v knows its
+// parent direction, its own subtree size and parent-arc ranks (rio: down into v, up out of v), and
+// every child's subtree size and arc ranks.  So it picks its heavy child (max size, ties -> smallest
+// direction) and writes the tour values of its children's edges straight at their ranks: down arc into
+// child c +(light << 32 | preorder offset of c within v's subtree, heavy child first), up arc out of c
+// the negation.  (Round 5: k_orient and k_heavy fused; k_heavy had re-read every child's size and rio.)
 __global__ void k_orient(LayoutPair LP, int W, int H) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.z];
-    tile_pixels(layout_tile(W, H, (int)blockIdx.x), W, H, [&](uint32_t q) {
-        const uint32_t adj = V.adj[q];
-        const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
-        const TourBufs T = tour_bufs(V);
-        int8_t pd = -1;
-        uint32_t sz = (uint32_t)(W * H);
-        uint2 rio = make_uint2(0u, 0u);
-        for (int k = 0; k < 4; ++k) {
-            if (!(adj & (1u << k))) continue;
-            const uint32_t p = nbr_of(q, k, W);
-            const uint32_t si = tour_suffix(T, 4u * p + (uint32_t)((k + 2) & 3));  // p -> q
-            const uint32_t so = tour_suffix(T, 4u * q + (uint32_t)k);              // q -> p
-            if (si > so) {  // rank(p -> q) < rank(q -> p): p is the parent
-                pd = (int8_t)k;
-                sz = (si - so + 1u) / 2u;
-                rio = make_uint2(total - si, total - so);
-            }
-        }
-        V.pdir[q] = pd;
-        V.size[q] = sz;
-        V.rio[q] = rio;
-    });
-}
-
-// Heavy child (max subtree, ties -> smallest direction) and the tour values of the children's edges,
-// written straight at their ranks: down arc into child c +(light << 32 | preorder offset of c within
-// v's subtree, heavy child first), up arc out of c the negation (round 5: k_tour_values fused in)
-__global__ void k_heavy(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     tile_pixels(layout_tile(W, H, (int)blockIdx.x), W, H, [&](uint32_t v) {
         const uint32_t adj = V.adj[v];
-        const int pd = V.pdir[v];
-        int heavy = -1;
-        uint32_t best = 0;
-        uint32_t csz[4] = {0, 0, 0, 0};
+        const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
+        const TourBufs T = tour_bufs(V);
+        int pd = -1, heavy = -1;
+        uint32_t sz = (uint32_t)(W * H), best = 0;
+        uint2 rio = make_uint2(0u, 0u);
+        uint32_t csz[4] = {0u, 0u, 0u, 0u};
         uint2 crio[4];
-    #pragma unroll
+        bool bad = false;
+#pragma unroll
         for (int k = 0; k < 4; ++k) {
             crio[k] = make_uint2(0u, 0u);
-            if (!(adj & (1u << k)) || k == pd) continue;
-            const uint32_t c = nbr_of(v, k, W);
-            csz[k] = V.size[c];
-            crio[k] = V.rio[c];
-            if (csz[k] > best) { best = csz[k]; heavy = k; }
+            if (!(adj & (1u << k))) continue;
+            const uint32_t n = nbr_of(v, k, W);
+            const uint32_t si = tour_suffix(T, 4u * n + (uint32_t)((k + 2) & 3));  // n -> v
+            const uint32_t so = tour_suffix(T, 4u * v + (uint32_t)k);              // v -> n
+            bad |= si - 1u >= total || so - 1u >= total;  // (never for a spanning tree's tour)
+            if (si > so) {  // rank(n -> v) < rank(v -> n): n is the parent
+                pd = k;
+                sz = (si - so + 1u) / 2u;
+                rio = make_uint2(total - si, total - so);
+            } else {        // n is a child
+                csz[k] = (so - si + 1u) / 2u;
+                crio[k] = make_uint2(total - so, total - si);
+                if (csz[k] > best) { best = csz[k]; heavy = k; }
+            }
         }
+        if (bad) {
+            __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        V.pdir[v] = (int8_t)pd;
+        V.size[v] = sz;
+        V.rio[v] = rio;
         V.heavy[v] = (int8_t)heavy;
         uint32_t off = 1u + (heavy >= 0 ? csz[heavy] : 0u);
-    #pragma unroll
+#pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(adj & (1u << k)) || k == pd) continue;
             long long val = 1;  // the heavy child: offset 1, not light
@@ -525,26 +517,32 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N)
     }
 }
 
-__global__ void k_path_offsets(LayoutPair LP) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.x];
-    if (threadIdx.x != 0) return;
-    uint32_t acc = 0, nr = 0;
-    for (int b = 0; b < SM_NBUCKETS; ++b) {
-        V.round_begin[b] = acc;
-        V.round_cursor[b] = acc;
-        acc += V.round_count[b];
-        if (V.round_count[b]) nr = (uint32_t)(b / 2) + 1;
-    }
-    V.round_begin[SM_NBUCKETS] = acc;
-    *V.nrounds = nr;
-}
-
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
-    __shared__ uint32_t hist[SM_NBUCKETS], gbase[SM_NBUCKETS];
+    __shared__ uint32_t hist[SM_NBUCKETS], gbase[SM_NBUCKETS], begin[SM_NBUCKETS + 1];
     if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = 0;
+    static_assert(SM_NBUCKETS <= 64, "one wave scans the bucket counts");
+    // every block derives the bucket offsets from the final counts (round 5: no k_path_offsets launch);
+    // block 0 publishes them and the round count
+    if (threadIdx.x < 64) {
+        const int b = (int)threadIdx.x;
+        const uint32_t c = b < SM_NBUCKETS ? V.round_count[b] : 0u;
+        uint32_t x = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (b >= off) x += y;
+        }
+        if (b < SM_NBUCKETS) begin[b] = x - c;
+        if (b == SM_NBUCKETS - 1) begin[SM_NBUCKETS] = x;
+        const uint64_t nz = __ballot(c != 0u);
+        if (blockIdx.x == 0) {
+            if (b < SM_NBUCKETS) V.round_begin[b] = x - c;
+            if (b == SM_NBUCKETS - 1) V.round_begin[SM_NBUCKETS] = x;
+            if (b == 0) *V.nrounds = nz ? (uint32_t)(63 - __builtin_clzll(nz)) / 2u + 1u : 0u;
+        }
+    }
     __syncthreads();
     const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
     uint32_t myr[PATH_ITEMS], myrank[PATH_ITEMS], myhead[PATH_ITEMS];
@@ -560,7 +558,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
     }
     __syncthreads();
     if (threadIdx.x < SM_NBUCKETS && hist[threadIdx.x])
-        gbase[threadIdx.x] = atomicAdd(&V.round_cursor[threadIdx.x], hist[threadIdx.x]);
+        gbase[threadIdx.x] = begin[threadIdx.x] + atomicAdd(&V.round_cursor[threadIdx.x], hist[threadIdx.x]);
     __syncthreads();
     for (int i = 0; i < PATH_ITEMS; ++i) {
         if (myr[i] == SM_NONE) continue;
@@ -774,7 +772,6 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
     hipLaunchKernelGGL(k_orient, tg, dim3(256), 0, st, LP, W, H);
-    hipLaunchKernelGGL(k_heavy, tg, dim3(256), 0, st, LP, W, H);
     ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}};
     launch_scan<long long, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2);
     hipLaunchKernelGGL(k_assign, tg, dim3(256), 0, st, LP, W, H);
@@ -782,7 +779,6 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     ScanBufs<uint64_t> hb{{LP.v[0].hk, LP.v[1].hk}};
     launch_scan<uint64_t, OpMax>(st, hb, LP.scan, nviews, N);
     hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
-    hipLaunchKernelGGL(k_path_offsets, dim3(nviews), dim3(64), 0, st, LP);
     hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     // contiguous bucket slots: scan of path lengths in paths[] order (plen is zero past the last
     // path), slot of every preorder position, then the metadata in slot numbering

@@ -10,7 +10,7 @@ for d in sys.argv[1:]:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
             tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
-for k, c in sorted(tot.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:12]:
+for k, c in sorted(tot.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:int(__import__("os").environ.get("TOP", "12"))]:
     w = c.get("SQ_WAVES", 1) or 1
     wc = c.get("SQ_WAVE_CYCLES", 0)
     print("%-28s waves %9.0f  cyc/wave %9.0f  wait %4.0f%%  waitinst %4.0f%%  active %4.0f%%  valu/w %7.0f vmem/w %6.0f lds/w %6.0f"
