@@ -166,7 +166,7 @@ struct sm_ctx {
     DevBuf cedge[2], clab[2], chook[2], ccnt[2];  // contracted Boruvka (component graph)
     uint32_t epoch = 0;      // bumped per filter call; status words are zeroed only on (re)allocation
     // GPU layout buffers (sm_layout_gpu.hip)
-    DevBuf adj[2], pdir[2], heavy[2], size[2], rio[2], hk[2], pixpre[2];
+    DevBuf adj[2], pdir[2], heavy[2], size[2], arcpix[2], hk[2], pixpre[2];
     DevBuf a_dist[2], a_cid[2], ccount[2], c_last[2], c_len[2];
     DevBuf segtab[2], pathpos[2], plen[2], slotpix[2], slot2pix[2];
     DevBuf pieces[2], pieces_tmp[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
@@ -1028,7 +1028,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->pdir[v], N));
         CHECK(ensure(ctx, ctx->heavy[v], N));
         CHECK(ensure(ctx, ctx->size[v], N * 4));
-        CHECK(ensure(ctx, ctx->rio[v], N * 8));
+        CHECK(ensure(ctx, ctx->arcpix[v], 2 * N * 4));
         CHECK(ensure(ctx, ctx->hk[v], N * 8));
         CHECK(ensure(ctx, ctx->pixpre[v], N * 4));
         CHECK(ensure(ctx, ctx->a_dist[v], 4 * N * 2));
@@ -1061,7 +1061,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.pdir = P<int8_t>(ctx->pdir[v]);
         L.heavy = P<int8_t>(ctx->heavy[v]);
         L.size = P<uint32_t>(ctx->size[v]);
-        L.rio = P<uint2>(ctx->rio[v]);
+        L.arcpix = P<uint32_t>(ctx->arcpix[v]);
         L.hk = P<uint64_t>(ctx->hk[v]);
         L.pixpre = P<uint32_t>(ctx->pixpre[v]);
         L.a_dist = P<uint16_t>(ctx->a_dist[v]);
@@ -2591,7 +2591,7 @@ void sm_destroy(sm_ctx* ctx) {
     if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     if (ctx->h_rounds) (void)hipHostFree(ctx->h_rounds);
     for (int v = 0; v < 2; ++v) {
-        DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->rio[v],
+        DevBuf* lay[] = {&ctx->adj[v], &ctx->pdir[v], &ctx->heavy[v], &ctx->size[v], &ctx->arcpix[v],
                          &ctx->hk[v], &ctx->pixpre[v], &ctx->a_dist[v], &ctx->a_cid[v],
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->cnw[v],
                          &ctx->tour[v], &ctx->spart[v],

@@ -92,7 +92,7 @@ struct LayoutView {
     int8_t* pdir;       // direction to the parent (-1: root)
     int8_t* heavy;      // direction of the heavy child (-1: leaf)
     uint32_t* size;     // subtree size
-    uint2* rio;         // tour ranks of the arcs parent -> pixel (x) and pixel -> parent (y)
+    uint32_t* arcpix;   // per tour rank of a down arc: the child pixel it enters
     // per arc (4N)
     uint16_t* a_dist;
     uint32_t* a_cid;

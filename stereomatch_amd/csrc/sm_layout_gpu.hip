@@ -155,11 +155,11 @@ __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
 // L3 + orientation + heavy child, one pass per pixel v: an arc's rank is the tour length minus its
 // suffix (sm_tour.h); an arc precedes its reverse iff it goes down, and the rank distance between the
 // two is twice the subtree size below it.  From the two suffixes of each tree edge at v, v knows its
-// parent direction, its own subtree size and parent-arc ranks (rio: down into v, up out of v), and
-// every child's subtree size and arc ranks.  So it picks its heavy child (max size, ties -> smallest
+// parent direction and its own subtree size, and every child's subtree size and arc ranks.  So it picks its heavy child (max size, ties -> smallest
 // direction) and writes the tour values of its children's edges straight at their ranks: down arc into
 // child c +(light << 32 | preorder offset of c within v's subtree, heavy child first), up arc out of c
-// the negation.  (Round 5: k_orient and k_heavy fused; k_heavy had re-read every child's size and rio.)
+// the negation, and c itself at the down arc's rank (arcpix).  (Round 5: k_orient and k_heavy fused;
+// k_heavy had re-read every child's size and ranks.)
 __global__ void k_orient(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
@@ -169,7 +169,6 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
         const TourBufs T = tour_bufs(V);
         int pd = -1, heavy = -1;
         uint32_t sz = (uint32_t)(W * H), best = 0;
-        uint2 rio = make_uint2(0u, 0u);
         uint32_t csz[4] = {0u, 0u, 0u, 0u};
         uint2 crio[4];
         bool bad = false;
@@ -184,7 +183,6 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
             if (si > so) {  // rank(n -> v) < rank(v -> n): n is the parent
                 pd = k;
                 sz = (si - so + 1u) / 2u;
-                rio = make_uint2(total - si, total - so);
             } else {        // n is a child
                 csz[k] = (so - si + 1u) / 2u;
                 crio[k] = make_uint2(total - so, total - si);
@@ -197,8 +195,11 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
         }
         V.pdir[v] = (int8_t)pd;
         V.size[v] = sz;
-        V.rio[v] = rio;
         V.heavy[v] = (int8_t)heavy;
+        if (pd < 0) {  // the root: preorder 0, light depth 0, a path head (the tour scan writes the others)
+            V.hk[0] = (1ull << 32) | 1ull;
+            V.pixpre[0] = v;
+        }
         uint32_t off = 1u + (heavy >= 0 ? csz[heavy] : 0u);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -210,6 +211,7 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
             }
             V.tour[crio[k].x] = val;
             V.tour[crio[k].y] = -val;
+            V.arcpix[crio[k].x] = nbr_of(v, k, W);  // the child, for the scan's epilogue
         }
     });
 }
@@ -306,19 +308,49 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_reduce(ScanBufs<T> B, ScanS
     if (threadIdx.x == 0) reinterpret_cast<T*>(S.part[v])[blockIdx.x] = tot;
 }
 
-template <class T, class Op>
-__global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanState S, int nelem) {
+// the scans' outputs: in place (the max-scan of hk, the add-scan of the path lengths) ...
+struct ScanInPlace {
+    __device__ bool active() const { return true; }
+    template <class T> __device__ void operator()(T* d, int, size_t i, T incl, T) const { d[i] = incl; }
+};
+// ... or, for the tour, the preorder records: at the down arc into node q (orig > 0) the inclusive sum is
+// (light depth of q) << 32 | (heavy-first preorder of q), and orig == 1 iff q is its parent's heavy child,
+// so hk[pre] = (pre + 1) << 32 | (light depth + 1) at a path head (0 elsewhere: after the inclusive
+// max-scan of hk every position holds its path's head and that head's light depth) and pixpre[pre] = q.
+// The root's record comes from k_orient.  (Round 5: this epilogue replaces k_assign, which re-read each
+// pixel's parent arc rank, its tour sum and its parent's heavy child; the tour itself is not written back.)
+struct ScanTourOut {
+    LayoutPair LP;
+    int N;
+    // an incomplete MST (k_orient wrote nothing: the tour holds a previous call's values) has no records
+    __device__ bool active() const { return *LP.mst_ok != 0; }
+    __device__ void operator()(long long*, int v, size_t i, long long incl, long long orig) const {
+        if (orig <= 0) return;  // an up arc
+        const LayoutView& V = LP.v[v];
+        const uint32_t pre = (uint32_t)(incl & 0xFFFFFFFFll), ld = (uint32_t)(incl >> 32);
+        if (pre >= (uint32_t)N || ld >= (uint32_t)SM_MAX_ROUNDS) {  // never for a spanning tree's tour (defensive)
+            __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        V.hk[pre] = orig != 1 ? ((uint64_t)(pre + 1u) << 32) | (uint64_t)(ld + 1u) : 0ull;
+        V.pixpre[pre] = V.arcpix[i];
+    }
+};
+
+template <class T, class Op, class Out>
+__global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanState S, int nelem, Out out) {
+    if (!out.active()) return;  // (block-uniform)
     const int v = blockIdx.y;
     const uint32_t tile = blockIdx.x;
     __shared__ T s_w[SP_THREADS / 64];
     T* d = B.data[v];
     const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
     const size_t wbase = (size_t)tile * SP_TILE + (size_t)w * 64 * SP_ITEMS;
-    T x[SP_ITEMS];
+    T x[SP_ITEMS], x0[SP_ITEMS];
 #pragma unroll
     for (int j = 0; j < SP_ITEMS; ++j) {
         const size_t i = wbase + (size_t)j * 64 + lane;
-        x[j] = i < (size_t)nelem ? d[i] : Op::template ident<T>();
+        x[j] = x0[j] = i < (size_t)nelem ? d[i] : Op::template ident<T>();
     }
     // the tile's exclusive prefix: the lower tiles' totals (loads in flight with the tile's)
     const T* part = reinterpret_cast<const T*>(S.part[v]);
@@ -348,44 +380,16 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanSt
 #pragma unroll
     for (int j = 0; j < SP_ITEMS; ++j) {
         const size_t i = wbase + (size_t)j * 64 + lane;
-        if (i < (size_t)nelem) d[i] = Op::apply(pre, x[j]);  // inclusive
+        if (i < (size_t)nelem) out(d, v, i, Op::apply(pre, x[j]), x0[j]);  // inclusive
     }
 }
 
-template <class T, class Op>
-static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S, int nviews, int nelem) {
+template <class T, class Op, class Out = ScanInPlace>
+static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S, int nviews, int nelem, Out out = Out{}) {
     if (nelem <= 0) return;
     const int ntiles = (nelem + SP_TILE - 1) / SP_TILE;
     hipLaunchKernelGGL((k_scan_reduce<T, Op>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem);
-    hipLaunchKernelGGL((k_scan_tiles<T, Op>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem);
-}
-
-// Preorder + light depth per pixel from the scanned tour, written by preorder position (the layout's
-// random-access passes are its cost when frames are in flight; round 5 packs what the later passes
-// read into two scatters here): hk[pre] = (pre + 1) << 32 | (light depth + 1) at a path head, 0
-// elsewhere -- after an inclusive max-scan every position holds its path's head and that head's light
-// depth -- and pixpre[pre] = the pixel.  A node is a head iff it is the root or not its parent's heavy
-// child.
-__global__ void k_assign(LayoutPair LP, int W, int H) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.z];
-    tile_pixels(layout_tile(W, H, (int)blockIdx.x), W, H, [&](uint32_t q) {
-        const int pd = V.pdir[q];
-        uint32_t pre = 0, ld = 0;
-        bool head = true;
-        if (pd >= 0) {
-            const long long v = V.tour[V.rio[q].x];
-            pre = (uint32_t)(v & 0xFFFFFFFFll);
-            ld = (uint32_t)(v >> 32);
-            head = V.heavy[nbr_of(q, pd, W)] != ((pd + 2) & 3);
-        }
-        if (pre >= (uint32_t)(W * H) || ld >= (uint32_t)SM_MAX_ROUNDS) {  // never for a spanning tree's tour (defensive)
-            __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
-        }
-        V.hk[pre] = head ? ((uint64_t)(pre + 1u) << 32) | (uint64_t)(ld + 1u) : 0ull;
-        V.pixpre[pre] = q;
-    });
+    hipLaunchKernelGGL((k_scan_tiles<T, Op, Out>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem, out);
 }
 
 // Per-slot metadata: pixel, parent slot, child weights and slots in descending (w,a,b) key order (the
@@ -468,7 +472,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
 }
 
 // heads in preorder -> path lengths -> bucketed by light depth (order inside a round is free).
-// After the inclusive max-scan of hk (k_assign), hk[s] >> 32 is 1 + the preorder position of the head
+// After the inclusive max-scan of hk (ScanTourOut), hk[s] >> 32 is 1 + the preorder position of the head
 // of s's path (heavy paths are contiguous in preorder) and its low word 1 + that head's light depth;
 // s is the last node of its path iff s + 1 is a head.
 __device__ __forceinline__ bool path_last(const LayoutView& V, uint32_t s, int N) {
@@ -773,8 +777,7 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
     hipLaunchKernelGGL(k_orient, tg, dim3(256), 0, st, LP, W, H);
     ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}};
-    launch_scan<long long, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2);
-    hipLaunchKernelGGL(k_assign, tg, dim3(256), 0, st, LP, W, H);
+    launch_scan<long long, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, ScanTourOut{LP, N});
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
     ScanBufs<uint64_t> hb{{LP.v[0].hk, LP.v[1].hk}};
     launch_scan<uint64_t, OpMax>(st, hb, LP.scan, nviews, N);
