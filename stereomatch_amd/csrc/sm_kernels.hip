@@ -518,7 +518,7 @@ __global__ __launch_bounds__(CBLK) void k_cid(CPair P, uint32_t N) {
 // round's minimum per component is a minimum over whole pairs, so the MST is unchanged, and every
 // round sweeps ~3x fewer edges.  Pairs that find no slot (tile caps of 0/1 make ~4k components per
 // tile) are listed unmerged.
-#define EH 2048                      // hash slots per block
+#define EH 1024                      // hash slots per block (~500 pairs per tile at C2; 16 KB of LDS)
 #define EH_EMPTY 0xFFFFFFFFFFFFFFFFull
 __global__ __launch_bounds__(CBLK) void k_cedges(CPair P, int W, int H) {
     const CView V = P.v[blockIdx.y];
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(CBLK) void k_cedges(CPair P, int W, int H) {
             const uint32_t cu = V.cid[c], cv = V.cid[cq];
             const unsigned long long pr = cu < cv ? ((unsigned long long)cu << 32) | cv : ((unsigned long long)cv << 32) | cu;
             const unsigned long long key = sm_edge_key(d == 0 ? V.wR[p] : V.wD[p], p, (uint32_t)d);
-            uint32_t h = (uint32_t)((pr * 0x9E3779B97F4A7C15ull) >> 53);  // 11 bits
+            uint32_t h = (uint32_t)((pr * 0x9E3779B97F4A7C15ull) >> 54);  // 10 bits
             bool done = false;
             for (int probe = 0; probe < 8 && !done; ++probe) {
                 const unsigned long long old = atomicCAS(&hpair[h], EH_EMPTY, pr);

@@ -135,8 +135,8 @@ struct ScanState {
     uint64_t* part[2];
     uint32_t* err;  // the call's device error word: bit 1, a layout index out of range
 };
-// tiles of the scans (4096 elements each) over at most 2N elements
-static inline size_t scan_tiles(size_t N) { return (2 * N + 4095) / 4096 + 1; }
+// tiles of the scans (at least 2048 elements each) over at most 2N elements
+static inline size_t scan_tiles(size_t N) { return (2 * N + 2047) / 2048 + 1; }
 
 struct LayoutPair {
     LayoutView v[2];

@@ -124,7 +124,7 @@ struct MstTour {
 };
 
 __device__ __forceinline__ TourBufs tour_bufs(const LayoutView& V) {
-    return TourBufs{V.a_dist, V.a_cid, V.nchains, V.c_last, V.c_len, V.cnw};
+    return TourBufs{V.a_dist, V.a_cid, V.nchains, V.c_last, V.c_len, V.cnw, nullptr, 0};
 }
 
 // L1: contract the tour inside each 32x32 tile (sm_tour.h)
@@ -133,7 +133,10 @@ __global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, 
     const LayoutView& V = LP.v[blockIdx.z];
     const TileRef t = layout_tile(W, H, (int)blockIdx.x);
     if (!t.ok) return;  // (block-uniform)
-    tour_tile(MstTour{V.adj, W, start_arc(V.adj)}, tour_bufs(V), W, H, t.x0, t.y0);
+    TourBufs T = tour_bufs(V);
+    T.err = reinterpret_cast<int32_t*>(LP.scan.err);  // the layout's error bit
+    T.errv = 2;
+    tour_tile(MstTour{V.adj, W, start_arc(V.adj)}, T, W, H, t.x0, t.y0);
 }
 
 // L2 init: chain successor + weight
@@ -145,7 +148,8 @@ __global__ void k_chain_init(LayoutPair LP, int W) {
 
 // L2: suffix sums over the chain list by in-place pointer jumping, one launch (sm_tour.h).  The grid
 // is at most CR_BLOCKS blocks (co-resident).
-#define CR_BLOCKS 1024  // per view, 256 threads each: half the chip's resident threads for both views
+#define CR_BLOCKS 256  // per view, 256 threads each (1024 / 256 / 128: the same frame rate at C2, round 5;
+                       // the smaller grid leaves the other frames' kernels room)
 
 __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
@@ -216,7 +220,7 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
     });
 }
 
-// ---- inclusive scans: reduce, then scan (round 5).  A tile is SP_TILE elements per 256-thread block,
+// ---- inclusive scans: reduce, then scan (round 5).  A tile is SP_TILE elements (4096 of 32 bits, 2048 of 64) per 256-thread block,
 // each wave 16 chunks of 64 consecutive elements (coalesced).  k_scan_reduce writes every tile's total;
 // k_scan_tiles re-reads its tile, takes its exclusive prefix as the reduction of the lower tiles' totals
 // (<= a few thousand L2-resident words per block, so no third launch scans the totals), scans in
@@ -225,7 +229,10 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
 // and the int64 scan took 193 us at C2 against 89 for the old 3-phase scan; this one reads its data
 // twice but never serialises.)
 #define SP_THREADS 256
-#define SP_ITEMS 16
+// items per thread: 16 of 32 bits, 8 of 64 bits (16 64-bit items and their interleaved shuffles took
+// 120 VGPRs: 4 waves per SIMD)
+template <class T> struct SpItems { static constexpr int n = sizeof(T) == 8 ? 8 : 16; };
+#define SP_ITEMS (SpItems<T>::n)
 #define SP_TILE (SP_THREADS * SP_ITEMS)
 
 struct OpAdd {
@@ -311,7 +318,8 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_reduce(ScanBufs<T> B, ScanS
 // the scans' outputs: in place (the max-scan of hk, the add-scan of the path lengths) ...
 struct ScanInPlace {
     __device__ bool active() const { return true; }
-    template <class T> __device__ void operator()(T* d, int, size_t i, T incl, T) const { d[i] = incl; }
+    template <class T> __device__ static uint32_t tag(T) { return 0u; }
+    template <class T> __device__ void operator()(T* d, int, size_t i, T incl, uint32_t) const { d[i] = incl; }
 };
 // ... or, for the tour, the preorder records: at the down arc into node q (orig > 0) the inclusive sum is
 // (light depth of q) << 32 | (heavy-first preorder of q), and orig == 1 iff q is its parent's heavy child,
@@ -324,15 +332,18 @@ struct ScanTourOut {
     int N;
     // an incomplete MST (k_orient wrote nothing: the tour holds a previous call's values) has no records
     __device__ bool active() const { return *LP.mst_ok != 0; }
-    __device__ void operator()(long long*, int v, size_t i, long long incl, long long orig) const {
-        if (orig <= 0) return;  // an up arc
+    // what the epilogue needs of an element's own value, 2 bits (kept in one register for all 16 items
+    // instead of a copy of the items): 1 = a down arc, 2 = the heavy child's
+    __device__ static uint32_t tag(long long orig) { return orig > 0 ? (orig == 1 ? 3u : 1u) : 0u; }
+    __device__ void operator()(long long*, int v, size_t i, long long incl, uint32_t tg) const {
+        if (!(tg & 1u)) return;  // an up arc
         const LayoutView& V = LP.v[v];
         const uint32_t pre = (uint32_t)(incl & 0xFFFFFFFFll), ld = (uint32_t)(incl >> 32);
         if (pre >= (uint32_t)N || ld >= (uint32_t)SM_MAX_ROUNDS) {  // never for a spanning tree's tour (defensive)
             __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        V.hk[pre] = orig != 1 ? ((uint64_t)(pre + 1u) << 32) | (uint64_t)(ld + 1u) : 0ull;
+        V.hk[pre] = !(tg & 2u) ? ((uint64_t)(pre + 1u) << 32) | (uint64_t)(ld + 1u) : 0ull;
         V.pixpre[pre] = V.arcpix[i];
     }
 };
@@ -346,11 +357,13 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanSt
     T* d = B.data[v];
     const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
     const size_t wbase = (size_t)tile * SP_TILE + (size_t)w * 64 * SP_ITEMS;
-    T x[SP_ITEMS], x0[SP_ITEMS];
+    T x[SP_ITEMS];
+    uint32_t tags = 0;  // 2 bits per item (Out::tag)
 #pragma unroll
     for (int j = 0; j < SP_ITEMS; ++j) {
         const size_t i = wbase + (size_t)j * 64 + lane;
-        x[j] = x0[j] = i < (size_t)nelem ? d[i] : Op::template ident<T>();
+        x[j] = i < (size_t)nelem ? d[i] : Op::template ident<T>();
+        tags |= Out::tag(x[j]) << (2 * j);
     }
     // the tile's exclusive prefix: the lower tiles' totals (loads in flight with the tile's)
     const T* part = reinterpret_cast<const T*>(S.part[v]);
@@ -380,7 +393,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanSt
 #pragma unroll
     for (int j = 0; j < SP_ITEMS; ++j) {
         const size_t i = wbase + (size_t)j * 64 + lane;
-        if (i < (size_t)nelem) out(d, v, i, Op::apply(pre, x[j]), x0[j]);  // inclusive
+        if (i < (size_t)nelem) out(d, v, i, Op::apply(pre, x[j]), (tags >> (2 * j)) & 3u);  // inclusive
     }
 }
 
@@ -415,7 +428,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
         // the children in descending key order by a fixed 5-comparator network over the 4 directions
         // (absent ones sort last; keys are unique): no local array is indexed at run time, which
         // would put them in scratch memory
-        uint64_t ck[4];
+        uint32_t ck[4];
         uint32_t cs[4], cw[4];
         int cq[4];
         bool cv[4];
@@ -426,11 +439,13 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
             const uint32_t n = in ? nbr_of(v, k, W) : v;
             // right / down edges are v's own, left / up the neighbour's
             const uint32_t w = k == 0 ? V.wR[v] : k == 1 ? V.wD[v] : k == 2 ? V.wR[n] : V.wD[n];
-            const uint32_t a = k == 0 || k == 1 ? v : n;
-            const uint64_t key = sm_edge_key(w & 1023u, a, (uint32_t)(k & 1));
+            // the (w, a, vertical) key order among v's own edges: for equal w, up (a = v - W) < left
+            // (a = v - 1) < right (a = v, horizontal) < down (a = v, vertical), so a 32-bit key
+            // w << 2 | that rank orders them as sm_edge_key does (round 5: 64-bit keys in the network)
+            const uint32_t key = ((w & 1023u) << 2) | (k == 3 ? 0u : k == 2 ? 1u : k == 0 ? 2u : 3u);
             const uint32_t ns = in ? V.slotpix[n] : SM_NONE;
             if (in && k == pd) {
-                wp = (uint32_t)(key >> 33);
+                wp = key >> 2;
                 parent = ns;
             }
             ck[k] = key;
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
         }
         auto cswap = [&](int i, int j) __attribute__((always_inline)) {  // i, j constants after unrolling
             const bool sw = cv[j] && (!cv[i] || ck[j] > ck[i]);
-            const uint64_t tk = ck[i]; const int tq = cq[i]; const uint32_t ts = cs[i]; const bool tv = cv[i];
+            const uint32_t tk = ck[i]; const int tq = cq[i]; const uint32_t ts = cs[i]; const bool tv = cv[i];
             ck[i] = sw ? ck[j] : ck[i]; cq[i] = sw ? cq[j] : cq[i]; cs[i] = sw ? cs[j] : cs[i]; cv[i] = sw ? cv[j] : cv[i];
             ck[j] = sw ? tk : ck[j]; cq[j] = sw ? tq : cq[j]; cs[j] = sw ? ts : cs[j]; cv[j] = sw ? tv : cv[j];
         };
@@ -454,7 +469,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             nch += cv[i] ? 1 : 0;
-            cw[i] = cv[i] ? (uint32_t)(ck[i] >> 33) : 0u;
+            cw[i] = cv[i] ? ck[i] >> 2 : 0u;
             cs[i] = cv[i] ? cs[i] : SM_NONE;
             if (cv[i]) {
                 if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;

@@ -189,7 +189,7 @@ struct PfTourG {
 };
 
 __device__ __forceinline__ TourBufs pf_tour_bufs(const PfView& v) {
-    return TourBufs{v.a_dist, v.a_cid, v.nchains, v.c_last, v.c_len, v.cnw};
+    return TourBufs{v.a_dist, v.a_cid, v.nchains, v.c_last, v.c_len, v.cnw, v.tot + 7, 4};  // (4: an inconsistent tour)
 }
 
 // direction from p to its grid neighbour n

@@ -9,7 +9,8 @@
 //   L2 tour_chain_init : chain successor + length; tour_chain_rank: in-place pointer jumping over the
 //                        chains, cnw[c] >> 32 = arcs from chain c's head to the end of its list
 //   L3 (caller)        : arcs from arc a to its list's end, inclusive =
-//                        (cnw[c] >> 32) - (c_len[c] - a_dist[a]), c = a_cid[a]
+//                        (cnw[c] >> 32) - (c_len[c] - a_dist[a]), c = a_cid[a]; tour_chain_rank leaves
+//                        the first two terms folded in c_len, so this is one gather
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,6 +23,10 @@
 #define TL_THREADS 256
 #define L_EXIT 0xFFFFu        // successor leaves the tile
 #define L_NIL 0xFFFEu         // end of a list
+// arcs leaving a tile's pixels along a forest: 2 per edge inside the tile (<= TLP - 1 edges) plus one per
+// edge across its border (<= 4 TL): the compact word array's size (round 5: 18 KB of LDS instead of 32,
+// 7 blocks per CU instead of 4)
+#define TL_ARCS (2 * (TLP - 1) + 4 * TL)
 
 struct TourBufs {
     // per arc (4N)
@@ -30,109 +35,172 @@ struct TourBufs {
     // per chain
     uint32_t* nchains;  // device counter
     uint32_t* c_last;
-    uint32_t* c_len;
+    uint32_t* c_len;    // the chain's arcs; after tour_chain_rank its suffix base: (arcs from its head to
+                        // its list's end) - (its arcs), so an arc's suffix is one gather (tour_suffix)
     uint64_t* cnw;      // successor chain (low 32 bits) | arcs to it (high 32 bits)
+    int32_t* err;       // a tile with more than TL_ARCS arcs (not a forest) ORs errv in here
+    int32_t errv;
 };
 
 __device__ __forceinline__ uint32_t tour_nbr(uint32_t p, int k, int W) {
     return k == 0 ? p + 1 : k == 1 ? p + (uint32_t)W : k == 2 ? p - 1 : p - (uint32_t)W;
 }
 
-// L1: contract the lists inside the 32x32 tile at (tx0, ty0).  One 64-bit LDS word per arc
-// slot, nxt | dist << 16 | last << 32, so a jump is one gathered word; every thread keeps its 16 words
-// in registers.
+// L1: contract the lists inside the 32x32 tile at (tx0, ty0).  One 64-bit LDS word per arc,
+// nxt | dist << 16 | last << 32 | slot << 48, so a jump is one gathered word; every thread keeps its words
+// in registers.  The tile's arcs that exist (about half of its 4096 slots: a tree has ~2 arcs per pixel)
+// are first compacted in slot order (round 5: the jumping loop issued all 16 slots per thread every
+// iteration, live or not), so the loop runs over ceil(arcs / 256) words per thread.
 template <class G>
 __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, int H, int tx0, int ty0) {
     __shared__ union {
-        uint64_t w[TLS];
-        uint16_t h[4 * TLS];  // once the jumping is done, h[4*s + 2]: the tile-local id of the chain whose
-                              // last slot is s (bits 32..47 of w[s], which nobody reads any more)
+        uint64_t w[TL_ARCS];
+        uint16_t h[4 * TL_ARCS];  // h[s] (s < TLS) during the compaction: slot s's compact index; once the
+                                  // jumping is done, h[4*j + 2]: the tile-local id of the chain whose last
+                                  // arc is j (bits 32..47 of w[j], which nobody reads any more), h[4*j + 3]:
+                                  // j's slot
     } st;
-    __shared__ uint8_t haspred[TLS];
+    static_assert(4 * TL_ARCS >= TLS, "the compaction's index table fits the word array");
+    __shared__ uint8_t haspred[TL_ARCS];
+    __shared__ uint32_t s_cnt[64];
     constexpr int PER = TLS / TL_THREADS;  // 16 slots per thread
-    for (int i = 0; i < PER; ++i) haspred[threadIdx.x + i * TL_THREADS] = 0;
-    __syncthreads();
-    uint64_t own[PER];
+    static_assert(PER * (TL_THREADS / 64) == 64, "one wave scans the per-(slot row, wave) counts");
+    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < TL_ARCS; i += TL_THREADS) haspred[i] = 0;
+    // successors in slot space; compact ranks in slot order: slot s = threadIdx.x + 256 i, so for each i
+    // the waves hold consecutive runs of 64 slots
+    uint32_t nxt[PER], rk[PER], live = 0;
+#pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int s = threadIdx.x + i * TL_THREADS;
         const int lp = s >> 2, k = s & 3;
         const int lx = lp % TL, ly = lp / TL;
         const int x = tx0 + lx, y = ty0 + ly;
-        uint32_t n = L_NIL, dd = 0;
+        uint32_t n = L_NIL;
+        bool has = false;
         if (x < W && y < H) {
             const uint32_t p = (uint32_t)(y * W + x);
             if (g.has(p, k)) {
-                dd = 1;
+                has = true;
                 const uint32_t sa = g.succ(4u * p + (uint32_t)k);
                 if (sa != SM_NONE) {
                     // the successor leaves from q = the neighbour of p in direction k: its tile
                     // coordinates follow from p's without a division by W
                     const int qx = lx + (k == 0 ? 1 : k == 2 ? -1 : 0), qy = ly + (k == 1 ? 1 : k == 3 ? -1 : 0);
-                    if (qx >= 0 && qx < TL && qy >= 0 && qy < TL) {
-                        n = (uint32_t)(4 * (qy * TL + qx) + (int)(sa & 3u));
-                        haspred[n] = 1;
-                    } else {
-                        n = L_EXIT;
-                    }
+                    n = (qx >= 0 && qx < TL && qy >= 0 && qy < TL) ? (uint32_t)(4 * (qy * TL + qx) + (int)(sa & 3u)) : L_EXIT;
                 }
             }
         }
-        own[i] = (uint64_t)n | ((uint64_t)dd << 16) | ((uint64_t)s << 32);
-        st.w[s] = own[i];
+        nxt[i] = n;
+        const uint64_t b = __ballot(has);
+        rk[i] = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        if (has) live |= 1u << i;
+        if (lane == 0) s_cnt[i * (TL_THREADS / 64) + wave] = (uint32_t)__popcll(b);
     }
     __syncthreads();
-    // pointer jumping: dist -> arcs to chain end (inclusive), last -> chain's last slot.  Only the words
-    // that moved are written back (a word that reached its chain's end is final in LDS already): the
-    // loop is bound by LDS traffic, and most chains finish long before the tile's longest
+    __shared__ uint32_t s_base[64], s_count;
+    if (wave == 0) {
+        const uint32_t c = s_cnt[lane];
+        uint32_t x = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        s_base[lane] = x - c;
+        if (lane == 63) s_count = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        rk[i] += s_base[i * (TL_THREADS / 64) + wave];
+        if ((live >> i) & 1u) st.h[threadIdx.x + i * TL_THREADS] = (uint16_t)rk[i];
+    }
+    const uint32_t count = s_count;
+    if (count > (uint32_t)TL_ARCS) {  // (block-uniform) not a forest: never write past the LDS arrays
+        if (threadIdx.x == 0 && T.err) atomicOr(T.err, T.errv);
+        return;
+    }
+    __syncthreads();
+    // the compact words: successor remapped, distance 1, last = itself, slot
+    uint64_t nw[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        nw[i] = 0;
+        if (!((live >> i) & 1u)) continue;
+        const uint32_t n = nxt[i];
+        const uint32_t nc = n < L_NIL ? (uint32_t)st.h[n] : n;
+        if (n < L_NIL) haspred[nc] = 1;
+        nw[i] = (uint64_t)nc | (1ull << 16) | ((uint64_t)rk[i] << 32) | ((uint64_t)(threadIdx.x + i * TL_THREADS) << 48);
+    }
+    __syncthreads();  // (h read: now the words overwrite it)
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+        if ((live >> i) & 1u) st.w[rk[i]] = nw[i];
+    __syncthreads();
+    // compact word j is owned by thread j % 256
+    const int nper = (int)((count + TL_THREADS - 1) / TL_THREADS);
+    uint64_t own[PER];
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+        const uint32_t j = threadIdx.x + m * TL_THREADS;
+        own[m] = (m < nper && j < count) ? st.w[j] : (uint64_t)L_NIL;  // (dist 0: no arc)
+    }
+    // pointer jumping: dist -> arcs to chain end (inclusive), last -> chain's last arc.  Only the words
+    // that moved are written back (a word that reached its chain's end is final in LDS already)
     for (int it = 0; it < 13; ++it) {
         uint32_t moved = 0;
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const uint32_t n = (uint32_t)own[i] & 0xFFFFu;
+        for (int m = 0; m < PER; ++m) {
+            if (m >= nper) break;  // (block-uniform)
+            const uint32_t n = (uint32_t)own[m] & 0xFFFFu;
             if (n < L_NIL) {
                 const uint64_t nb = st.w[n];
-                const uint32_t d = (uint32_t)(own[i] >> 16) + (uint32_t)(nb >> 16);  // low 16 bits: the sum
-                own[i] = (nb & 0xFFFF0000FFFFull) | ((uint64_t)(d & 0xFFFFu) << 16);
-                moved |= 1u << i;
+                const uint32_t d = (uint32_t)(own[m] >> 16) + (uint32_t)(nb >> 16);  // low 16 bits: the sum
+                own[m] = (nb & 0x0000FFFF0000FFFFull) | ((uint64_t)(d & 0xFFFFu) << 16) | (own[m] & 0xFFFF000000000000ull);
+                moved |= 1u << m;
             }
         }
         if (!__syncthreads_or(moved != 0)) break;
 #pragma unroll
-        for (int i = 0; i < PER; ++i)
-            if ((moved >> i) & 1u) st.w[threadIdx.x + i * TL_THREADS] = own[i];
+        for (int m = 0; m < PER; ++m)
+            if ((moved >> m) & 1u) st.w[threadIdx.x + m * TL_THREADS] = own[m];
         __syncthreads();
     }
-    // heads: existing arcs without an in-tile predecessor; register chains
+    // heads: arcs without an in-tile predecessor; register chains
     __shared__ uint32_t nheads, cbase;
     if (threadIdx.x == 0) nheads = 0;
     __syncthreads();
     uint32_t myhead[PER];
-    for (int i = 0; i < PER; ++i) {
-        const int s = threadIdx.x + i * TL_THREADS;
-        const uint32_t dist = (uint32_t)(own[i] >> 16) & 0xFFFFu, last = (uint32_t)(own[i] >> 32) & 0xFFFFu;
-        myhead[i] = SM_NONE;
-        if (dist != 0 && !haspred[s]) {
-            myhead[i] = atomicAdd(&nheads, 1u);  // LDS atomic: rank of this chain inside the tile
-            st.h[4 * last + 2] = (uint16_t)myhead[i];
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+        const uint32_t j = threadIdx.x + m * TL_THREADS;
+        const uint32_t dist = (uint32_t)(own[m] >> 16) & 0xFFFFu, last = (uint32_t)(own[m] >> 32) & 0xFFFFu;
+        myhead[m] = SM_NONE;
+        if (m < nper && dist != 0 && !haspred[j]) {
+            myhead[m] = atomicAdd(&nheads, 1u);  // LDS atomic: rank of this chain inside the tile
+            st.h[4 * last + 2] = (uint16_t)myhead[m];
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) cbase = atomicAdd(T.nchains, nheads);  // one global atomic per tile
     __syncthreads();
-    for (int i = 0; i < PER; ++i) {
-        const int s = threadIdx.x + i * TL_THREADS;
-        const uint32_t dist = (uint32_t)(own[i] >> 16) & 0xFFFFu, last = (uint32_t)(own[i] >> 32) & 0xFFFFu;
-        if (dist == 0) continue;
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+        const uint32_t dist = (uint32_t)(own[m] >> 16) & 0xFFFFu, last = (uint32_t)(own[m] >> 32) & 0xFFFFu;
+        if (m >= nper || dist == 0) continue;
+        const int s = (int)(own[m] >> 48);
         const int lp = s >> 2, k = s & 3;
         const uint32_t p = (uint32_t)((ty0 + lp / TL) * W + tx0 + lp % TL);
         const uint32_t a = 4u * p + (uint32_t)k;
         const uint32_t cid = cbase + st.h[4 * last + 2];  // every arc its chain's id
         T.a_dist[a] = (uint16_t)dist;
         T.a_cid[a] = cid;
-        if (myhead[i] != SM_NONE) {
-            const int llp = (int)last >> 2;
+        if (myhead[m] != SM_NONE) {
+            const int ls = (int)st.h[4 * last + 3];  // the last arc's slot
+            const int llp = ls >> 2;
             const uint32_t lpix = (uint32_t)((ty0 + llp / TL) * W + tx0 + llp % TL);
-            T.c_last[cid] = 4u * lpix + (last & 3u);
+            T.c_last[cid] = 4u * lpix + (uint32_t)(ls & 3);
             T.c_len[cid] = dist;
         }
     }
@@ -173,10 +241,13 @@ __device__ __forceinline__ void tour_chain_rank(const TourBufs& T) {
         }
         if (!any) break;
     }
+    // every chain of this thread has reached its list's end: its word is final
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += stride)
+        T.c_len[c] = (uint32_t)(__hip_atomic_load(nw + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) - T.c_len[c];
 }
 
 // L3: arcs from arc a to the end of its list, inclusive
 __device__ __forceinline__ uint32_t tour_suffix(const TourBufs& T, uint32_t a) {
     const uint32_t c = T.a_cid[a];
-    return (uint32_t)(T.cnw[c] >> 32) - (T.c_len[c] - T.a_dist[a]);
+    return T.c_len[c] + T.a_dist[a];  // (c_len: the suffix base after tour_chain_rank)
 }
