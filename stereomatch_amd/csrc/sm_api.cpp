@@ -907,8 +907,13 @@ sm_status stage_mst(sm_ctx* ctx, int views) {
     HIPC(launch_zero(ctx->st, z));
     a.flags[0] = P<int>(ctx->changed);
     a.flags[1] = P<int>(ctx->changed) + SM_MST_MAX_ROUNDS;
-    HIPC(launch_bor_local(ctx->st, a, W, H));
     const bool pixel_rounds = getenv("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B path (tests, tools)
+    {
+        uint32_t* cc[2] = {nullptr, nullptr};
+        if (!pixel_rounds)
+            for (int i = 0; i < nviews; ++i) cc[i] = P<uint32_t>(ctx->ccnt[vs.v[i]]);
+        HIPC(launch_bor_local(ctx->st, a, W, H, cc));
+    }
     if (pixel_rounds) {
         for (int i = 0; i < nviews; ++i) HIPC(hipMemsetAsync(ctx->best[vs.v[i]].p, 0xFF, N * 8, ctx->st));
         // global rounds: every kernel of round r exits at once if round r-1 hooked nothing, so the

@@ -227,6 +227,8 @@ struct MstView {
     uint8_t* mR;
     uint8_t* mD;
     int* flags;               // flags[r] = 1 if global round r hooked anything
+    uint32_t* ccount;         // contracted rounds: [0] K, and root[] = the representatives' compact ids
+                              // (k_bor_local assigns them: k_cid folded in, round 5); null otherwise
 };
 struct MstPair {
     MstView v[2];
@@ -333,11 +335,49 @@ __global__ __launch_bounds__(BTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         for (int i = threadIdx.x; i < n; i += BTHREADS) comp[i] = hk[comp[i]];
         __syncthreads();
     }
-    for (int i = threadIdx.x; i < n; i += BTHREADS) {
+    constexpr int IPT = BTN / BTHREADS;  // (i = threadIdx.x + BTHREADS j below)
+    uint32_t reps = 0;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const int i = threadIdx.x + j * BTHREADS;
+        if (i >= n) break;
         const int lx = i % tw, ly = i / tw;
         const int r = comp[i];
         const uint32_t gr = (uint32_t)((ty0 + r / tw) * W + tx0 + r % tw);
         V.comp[(size_t)(ty0 + ly) * W + tx0 + lx] = gr;
+        if (r == i) reps |= 1u << j;
+    }
+    if (V.ccount == nullptr) return;  // (uniform: the pixel-round engine)
+    // compact ids of the tile's components: a block scan of the representative counts, one atomic per
+    // tile (any id order is fine: ids only name components; the mutual-choice tie-break on ids picks
+    // which of two components stays root, never which edge joins the MST)
+    __shared__ uint32_t s_w[BTHREADS / 64], s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t c = (uint32_t)__builtin_popcount(reps);
+    uint32_t x = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < BTHREADS / 64; ++k) {
+            const uint32_t u = s_w[k];
+            s_w[k] = t;
+            t += u;
+        }
+        s_base = atomicAdd(V.ccount, t);
+    }
+    __syncthreads();
+    uint32_t id = s_base + s_w[wv] + x - c;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (!((reps >> j) & 1u)) continue;
+        const int i = threadIdx.x + j * BTHREADS;
+        V.root[(size_t)(ty0 + i / tw) * W + tx0 + i % tw] = id++;
     }
 }
 
@@ -433,7 +473,7 @@ __global__ void k_bor_relabel(MstPair P, int W, int H, int rnd) {
 
 // ---------------------------------------------------------------------------------------------
 // Contracted Boruvka.  After k_bor_local most pixels share a tile component; the remaining rounds
-// run on the component graph: compact component ids (k_cid), the list of inter-component pixel
+// run on the component graph: compact component ids (k_bor_local), the list of inter-component pixel
 // edges (k_cedges, same 64-bit keys), then per round min over edges (k_cmin), hook (k_chook),
 // root chase (k_croot) and relabel (k_crelabel) over K components / E' edges instead of N pixels.
 // The keys and the mutual-choice rule are those of the pixel rounds, so the MST is identical.
@@ -466,7 +506,6 @@ struct CPair {
 // Compaction appends: every block reserves its whole range with ONE atomic (same-address
 // atomics serialise in L2 at ~10 ns each; a per-wave append over 2.3M pixels cost 0.6-1.5 ms).
 #define CBLK 256   // threads per compaction block
-#define CPT 16     // pixels per thread (k_cid, k_cedges)
 #define EPT 4      // edges per thread (k_cmin: latency-bound, wants more waves)
 
 // exclusive block scan of cnt + one atomicAdd on counter: returns this thread's first slot
@@ -494,21 +533,6 @@ __device__ __forceinline__ uint32_t block_append(uint32_t cnt, uint32_t* counter
     }
     __syncthreads();
     return s_base + s_w[wave] + x - cnt;
-}
-
-__global__ __launch_bounds__(CBLK) void k_cid(CPair P, uint32_t N) {
-    const CView V = P.v[blockIdx.y];
-    const uint32_t base = blockIdx.x * (CBLK * CPT) + threadIdx.x;
-    uint32_t bits = 0;
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-        const uint32_t p = base + i * CBLK;
-        if (p < N && V.comp[p] == p) bits |= 1u << i;
-    }
-    uint32_t id = block_append(__builtin_popcount(bits), &V.counts[0]);
-#pragma unroll
-    for (int i = 0; i < CPT; ++i)
-        if (bits & (1u << i)) V.cid[base + i * CBLK] = id++;
 }
 
 // One block per BT x BT tile of the tile phase.  Tile-phase components never cross a tile border,
@@ -614,13 +638,13 @@ __device__ __forceinline__ bool wave_seg_min(bool active, uint32_t& c, unsigned 
 // Per-block direct-mapped LDS table of component minima: late rounds have few components with
 // thousands of incident edges each, and global atomics on one best[] word serialise in L2.  A
 // slot is claimed by CAS on its tag; a collision falls through to the global atomic.
-#define CTAB 2048
+#define CTAB 1024  // (12 KB: 8 waves per SIMD; 2048 slots held k_cmin to 6)
 struct CTable {
     uint32_t tag[CTAB];
     unsigned long long mn[CTAB];
 };
 __device__ __forceinline__ void ctab_min(CTable& T, uint32_t c, unsigned long long k, unsigned long long* best) {
-    const uint32_t slot = (c * 2654435761u) >> 21;  // 11-bit multiplicative hash
+    const uint32_t slot = (c * 2654435761u) >> 22;  // 10-bit multiplicative hash
     const uint32_t old = atomicCAS(&T.tag[slot], 0xFFFFFFFFu, c);
     if (old == 0xFFFFFFFFu || old == c) atomicMin(&T.mn[slot], k);
     else atomicMin(&best[c], k);
@@ -824,10 +848,10 @@ hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* l
     return hipGetLastError();
 }
 
-hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H) {
+hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H, uint32_t* const ccount[2]) {
     MstPair P;
     for (int v = 0; v < 2; ++v)
-        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v]};
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v], ccount[v]};
     dim3 g((W + BT - 1) / BT, (H + BT - 1) / BT, a.nviews);
     // Tile-phase Boruvka iterations: any cap is exact (unfinished components continue in the
     // contracted rounds); 4 is the measured optimum at C2 (tools/gpu_mst_sweep.sh).
@@ -840,7 +864,7 @@ hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H) {
 hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r) {
     MstPair P;
     for (int v = 0; v < 2; ++v)
-        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v]};
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v], nullptr};
     dim3 g((W + 255) / 256, H, a.nviews);
     hipLaunchKernelGGL(k_bor_min, g, dim3(256), 0, st, P, W, H, r);
     hipLaunchKernelGGL(k_bor_hook, g, dim3(256), 0, st, P, W, H, r);
@@ -920,9 +944,6 @@ static CPair make_cpair(const MstArgs& a, const MstCompact& c) {
 
 hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int H) {
     const CPair P = make_cpair(a, c);
-    const uint32_t N = (uint32_t)W * (uint32_t)H;
-    const dim3 g((N + CBLK * CPT - 1) / (CBLK * CPT), a.nviews);
-    hipLaunchKernelGGL(k_cid, g, dim3(CBLK), 0, st, P, N);
     const dim3 gt((unsigned)(((W + BT - 1) / BT) * ((H + BT - 1) / BT)), a.nviews);
     hipLaunchKernelGGL(k_cedges, gt, dim3(CBLK), 0, st, P, W, H);
     return hipGetLastError();

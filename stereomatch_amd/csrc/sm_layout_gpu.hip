@@ -176,13 +176,18 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
         uint32_t csz[4] = {0u, 0u, 0u, 0u};
         uint2 crio[4];
         bool bad = false;
+        // v's own four arcs are one 16-byte chain-id record and one 8-byte distance record
+        const uint4 oc = *reinterpret_cast<const uint4*>(V.a_cid + 4u * v);
+        const uint2 od = *reinterpret_cast<const uint2*>(V.a_dist + 4u * v);
+        const uint32_t ocid[4] = {oc.x, oc.y, oc.z, oc.w};
+        const uint32_t odist[4] = {od.x & 0xFFFFu, od.x >> 16, od.y & 0xFFFFu, od.y >> 16};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             crio[k] = make_uint2(0u, 0u);
             if (!(adj & (1u << k))) continue;
             const uint32_t n = nbr_of(v, k, W);
             const uint32_t si = tour_suffix(T, 4u * n + (uint32_t)((k + 2) & 3));  // n -> v
-            const uint32_t so = tour_suffix(T, 4u * v + (uint32_t)k);              // v -> n
+            const uint32_t so = T.c_len[ocid[k]] + odist[k];                       // v -> n (tour_suffix)
             bad |= si - 1u >= total || so - 1u >= total;  // (never for a spanning tree's tour)
             if (si > so) {  // rank(n -> v) < rank(v -> n): n is the parent
                 pd = k;
