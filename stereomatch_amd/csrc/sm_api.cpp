@@ -1025,6 +1025,8 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
     const uint32_t ntiles = (uint32_t)(((W + 31) / 32) * ((H + 31) / 32));
     const uint32_t max_chains = ntiles * 129u + 1u;
     const size_t nscan = scan_tiles(N);
+    if (N > ((size_t)1 << 27))  // the 32-bit tour values hold the preorder in 27 bits (sm_layout_gpu.hip)
+        return fail(ctx, SM_ERR_ARG, "tree layout: images above 2^27 pixels are not supported");
     LayoutPair LP{};
     ZeroList z{};
     for (int i = 0; i < nviews; ++i) {
@@ -1042,7 +1044,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->c_last[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->c_len[v], max_chains * 4));
         CHECK(ensure(ctx, ctx->cnw[v], max_chains * 8));
-        CHECK(ensure(ctx, ctx->tour[v], 2 * N * 8 + 16));
+        CHECK(ensure(ctx, ctx->tour[v], 2 * N * 4 + 16));
         CHECK(ensure(ctx, ctx->spart[v], nscan * 8));
         CHECK(ensure(ctx, ctx->meta[v], N * sizeof(SmMeta)));
         CHECK(ensure(ctx, ctx->paths[v], N * sizeof(SmPath)));
@@ -1075,7 +1077,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.c_last = P<uint32_t>(ctx->c_last[v]);
         L.c_len = P<uint32_t>(ctx->c_len[v]);
         L.cnw = P<uint64_t>(ctx->cnw[v]);
-        L.tour = P<long long>(ctx->tour[v]);
+        L.tour = P<uint32_t>(ctx->tour[v]);
         LP.scan.part[i] = P<uint64_t>(ctx->spart[v]);
         L.meta = P<SmMeta>(ctx->meta[v]);
         L.paths = P<SmPath>(ctx->paths[v]);

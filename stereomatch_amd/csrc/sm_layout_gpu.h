@@ -102,7 +102,7 @@ struct LayoutView {
     uint32_t* c_len;
     uint64_t* cnw;      // per chain: successor chain (low 32 bits) | arcs to it (high 32 bits)
     // tour (2N-2); the scans' tile tickets (3, zeroed with the layout's other counters)
-    long long* tour;
+    uint32_t* tour;         // per tour rank: the arc's value (light << 27 | preorder offset, negated going up)
     // per heavy-first preorder position (layout-internal numbering)
     uint64_t* hk;        // (1 + head position) << 32 | (1 + light depth) at a path head, 0 elsewhere;
                          // after the max-scan: the position's path head and its light depth

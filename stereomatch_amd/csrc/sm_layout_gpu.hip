@@ -156,12 +156,18 @@ __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
     tour_chain_rank(tour_bufs(LP.v[blockIdx.y]));
 }
 
+// Tour values are 32-bit, light << 27 | preorder offset, summed mod 2^32 (round 5; int64 before): a
+// prefix sum is (light depth) << 27 | (preorder), exactly, while N <= 2^27 (the host checks) and the
+// light depth < 32 (SM_MAX_ROUNDS); an up arc's value, the negation, is >= 2^31 and a down arc's < 2^28.
+#define TOUR_SHIFT 27
+#define TOUR_LIGHT (1u << TOUR_SHIFT)
+
 // L3 + orientation + heavy child, one pass per pixel v: an arc's rank is the tour length minus its
 // suffix (sm_tour.h); an arc precedes its reverse iff it goes down, and the rank distance between the
 // two is twice the subtree size below it.  From the two suffixes of each tree edge at v, v knows its
 // parent direction and its own subtree size, and every child's subtree size and arc ranks.  So it picks its heavy child (max size, ties -> smallest
 // direction) and writes the tour values of its children's edges straight at their ranks: down arc into
-// child c +(light << 32 | preorder offset of c within v's subtree, heavy child first), up arc out of c
+// child c +(light << 27 | preorder offset of c within v's subtree, heavy child first), up arc out of c
 // the negation, and c itself at the down arc's rank (arcpix).  (Round 5: k_orient and k_heavy fused;
 // k_heavy had re-read every child's size and ranks.)
 __global__ void k_orient(LayoutPair LP, int W, int H) {
@@ -213,13 +219,13 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(adj & (1u << k)) || k == pd) continue;
-            long long val = 1;  // the heavy child: offset 1, not light
+            uint32_t val = 1u;  // the heavy child: offset 1, not light
             if (k != heavy) {
-                val = (1ll << 32) + (long long)off;
+                val = TOUR_LIGHT + off;
                 off += csz[k];
             }
             V.tour[crio[k].x] = val;
-            V.tour[crio[k].y] = -val;
+            V.tour[crio[k].y] = 0u - val;
             V.arcpix[crio[k].x] = nbr_of(v, k, W);  // the child, for the scan's epilogue
         }
     });
@@ -326,8 +332,8 @@ struct ScanInPlace {
     template <class T> __device__ static uint32_t tag(T) { return 0u; }
     template <class T> __device__ void operator()(T* d, int, size_t i, T incl, uint32_t) const { d[i] = incl; }
 };
-// ... or, for the tour, the preorder records: at the down arc into node q (orig > 0) the inclusive sum is
-// (light depth of q) << 32 | (heavy-first preorder of q), and orig == 1 iff q is its parent's heavy child,
+// ... or, for the tour, the preorder records: at the down arc into node q (orig < 2^31) the inclusive sum is
+// (light depth of q) << 27 | (heavy-first preorder of q), and orig == 1 iff q is its parent's heavy child,
 // so hk[pre] = (pre + 1) << 32 | (light depth + 1) at a path head (0 elsewhere: after the inclusive
 // max-scan of hk every position holds its path's head and that head's light depth) and pixpre[pre] = q.
 // The root's record comes from k_orient.  (Round 5: this epilogue replaces k_assign, which re-read each
@@ -339,11 +345,11 @@ struct ScanTourOut {
     __device__ bool active() const { return *LP.mst_ok != 0; }
     // what the epilogue needs of an element's own value, 2 bits (kept in one register for all 16 items
     // instead of a copy of the items): 1 = a down arc, 2 = the heavy child's
-    __device__ static uint32_t tag(long long orig) { return orig > 0 ? (orig == 1 ? 3u : 1u) : 0u; }
-    __device__ void operator()(long long*, int v, size_t i, long long incl, uint32_t tg) const {
+    __device__ static uint32_t tag(uint32_t orig) { return orig < 0x80000000u ? (orig == 1u ? 3u : 1u) : 0u; }
+    __device__ void operator()(uint32_t*, int v, size_t i, uint32_t incl, uint32_t tg) const {
         if (!(tg & 1u)) return;  // an up arc
         const LayoutView& V = LP.v[v];
-        const uint32_t pre = (uint32_t)(incl & 0xFFFFFFFFll), ld = (uint32_t)(incl >> 32);
+        const uint32_t pre = incl & (TOUR_LIGHT - 1u), ld = incl >> TOUR_SHIFT;
         if (pre >= (uint32_t)N || ld >= (uint32_t)SM_MAX_ROUNDS) {  // never for a spanning tree's tour (defensive)
             __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
@@ -796,8 +802,8 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
     hipLaunchKernelGGL(k_orient, tg, dim3(256), 0, st, LP, W, H);
-    ScanBufs<long long> tb{{LP.v[0].tour, LP.v[1].tour}};
-    launch_scan<long long, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, ScanTourOut{LP, N});
+    ScanBufs<uint32_t> tb{{LP.v[0].tour, LP.v[1].tour}};
+    launch_scan<uint32_t, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, ScanTourOut{LP, N});
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
     ScanBufs<uint64_t> hb{{LP.v[0].hk, LP.v[1].hk}};
     launch_scan<uint64_t, OpMax>(st, hb, LP.scan, nviews, N);
