@@ -1025,8 +1025,8 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
     const uint32_t ntiles = (uint32_t)(((W + 31) / 32) * ((H + 31) / 32));
     const uint32_t max_chains = ntiles * 129u + 1u;
     const size_t nscan = scan_tiles(N);
-    if (N > ((size_t)1 << 27))  // the 32-bit tour values hold the preorder in 27 bits (sm_layout_gpu.hip)
-        return fail(ctx, SM_ERR_ARG, "tree layout: images above 2^27 pixels are not supported");
+    if (N >= ((size_t)1 << 27))  // 32-bit tour values and path records hold the preorder in 27 bits (sm_layout_gpu.hip)
+        return fail(ctx, SM_ERR_ARG, "tree layout: images of 2^27 pixels or more are not supported");
     LayoutPair LP{};
     ZeroList z{};
     for (int i = 0; i < nviews; ++i) {
@@ -1036,7 +1036,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->heavy[v], N));
         CHECK(ensure(ctx, ctx->size[v], N * 4));
         CHECK(ensure(ctx, ctx->arcpix[v], 2 * N * 4));
-        CHECK(ensure(ctx, ctx->hk[v], N * 8));
+        CHECK(ensure(ctx, ctx->hk[v], N * 4));
         CHECK(ensure(ctx, ctx->pixpre[v], N * 4));
         CHECK(ensure(ctx, ctx->a_dist[v], 4 * N * 2));
         CHECK(ensure(ctx, ctx->a_cid[v], 4 * N * 4));
@@ -1069,7 +1069,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.heavy = P<int8_t>(ctx->heavy[v]);
         L.size = P<uint32_t>(ctx->size[v]);
         L.arcpix = P<uint32_t>(ctx->arcpix[v]);
-        L.hk = P<uint64_t>(ctx->hk[v]);
+        L.hk = P<uint32_t>(ctx->hk[v]);
         L.pixpre = P<uint32_t>(ctx->pixpre[v]);
         L.a_dist = P<uint16_t>(ctx->a_dist[v]);
         L.a_cid = P<uint32_t>(ctx->a_cid[v]);

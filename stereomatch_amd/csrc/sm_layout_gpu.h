@@ -104,7 +104,7 @@ struct LayoutView {
     // tour (2N-2); the scans' tile tickets (3, zeroed with the layout's other counters)
     uint32_t* tour;         // per tour rank: the arc's value (light << 27 | preorder offset, negated going up)
     // per heavy-first preorder position (layout-internal numbering)
-    uint64_t* hk;        // (1 + head position) << 32 | (1 + light depth) at a path head, 0 elsewhere;
+    uint32_t* hk;        // (1 + head position) << 5 | light depth at a path head, 0 elsewhere;
                          // after the max-scan: the position's path head and its light depth
     uint32_t* pixpre;    // the pixel at the position
     // per slot

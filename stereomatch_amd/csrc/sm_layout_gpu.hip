@@ -161,6 +161,9 @@ __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
 // light depth < 32 (SM_MAX_ROUNDS); an up arc's value, the negation, is >= 2^31 and a down arc's < 2^28.
 #define TOUR_SHIFT 27
 #define TOUR_LIGHT (1u << TOUR_SHIFT)
+// a path head's preorder record: (1 + position) << 5 | light depth (32 bits while N < 2^27; the max-scan
+// carries it to the path's other positions, which hold 0)
+#define HK_REC(pre, ld) ((((pre) + 1u) << 5) | (ld))
 
 // L3 + orientation + heavy child, one pass per pixel v: an arc's rank is the tour length minus its
 // suffix (sm_tour.h); an arc precedes its reverse iff it goes down, and the rank distance between the
@@ -212,7 +215,7 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
         V.size[v] = sz;
         V.heavy[v] = (int8_t)heavy;
         if (pd < 0) {  // the root: preorder 0, light depth 0, a path head (the tour scan writes the others)
-            V.hk[0] = (1ull << 32) | 1ull;
+            V.hk[0] = HK_REC(0u, 0u);
             V.pixpre[0] = v;
         }
         uint32_t off = 1u + (heavy >= 0 ? csz[heavy] : 0u);
@@ -334,7 +337,7 @@ struct ScanInPlace {
 };
 // ... or, for the tour, the preorder records: at the down arc into node q (orig < 2^31) the inclusive sum is
 // (light depth of q) << 27 | (heavy-first preorder of q), and orig == 1 iff q is its parent's heavy child,
-// so hk[pre] = (pre + 1) << 32 | (light depth + 1) at a path head (0 elsewhere: after the inclusive
+// so hk[pre] = HK_REC(pre, light depth) at a path head (0 elsewhere: after the inclusive
 // max-scan of hk every position holds its path's head and that head's light depth) and pixpre[pre] = q.
 // The root's record comes from k_orient.  (Round 5: this epilogue replaces k_assign, which re-read each
 // pixel's parent arc rank, its tour sum and its parent's heavy child; the tour itself is not written back.)
@@ -354,7 +357,7 @@ struct ScanTourOut {
             __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        V.hk[pre] = !(tg & 2u) ? ((uint64_t)(pre + 1u) << 32) | (uint64_t)(ld + 1u) : 0ull;
+        V.hk[pre] = !(tg & 2u) ? HK_REC(pre, ld) : 0u;
         V.pixpre[pre] = V.arcpix[i];
     }
 };
@@ -498,19 +501,19 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
 }
 
 // heads in preorder -> path lengths -> bucketed by light depth (order inside a round is free).
-// After the inclusive max-scan of hk (ScanTourOut), hk[s] >> 32 is 1 + the preorder position of the head
+// After the inclusive max-scan of hk (ScanTourOut), hk[s] >> 5 is 1 + the preorder position of the head
 // of s's path (heavy paths are contiguous in preorder) and its low word 1 + that head's light depth;
 // s is the last node of its path iff s + 1 is a head.
 __device__ __forceinline__ bool path_last(const LayoutView& V, uint32_t s, int N) {
-    return s + 1 == (uint32_t)N || (uint32_t)(V.hk[s + 1] >> 32) == s + 2u;
+    return s + 1 == (uint32_t)N || (V.hk[s + 1] >> 5) == s + 2u;
 }
 // the path ending at s: its head and (light depth, long/short) bucket; false (and the error word set)
 // only for a corrupt layout (defensive) -- nothing is then written out of range
 __device__ __forceinline__ bool path_of(const LayoutPair& LP, const LayoutView& V, uint32_t s, uint32_t& head, uint32_t& b) {
-    const uint64_t h = V.hk[s];
-    head = (uint32_t)(h >> 32) - 1u;
-    const uint32_t ld = (uint32_t)h - 1u;
-    if (head > s || ld >= (uint32_t)SM_MAX_ROUNDS) {
+    const uint32_t h = V.hk[s];
+    head = (h >> 5) - 1u;
+    const uint32_t ld = h & 31u;
+    if (head > s) {
         __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return false;
     }
@@ -610,7 +613,7 @@ __global__ void k_newslot(LayoutPair LP, int N) {
     const LayoutView& V = LP.v[blockIdx.y];
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= (uint32_t)N) return;
-    const uint32_t head = (uint32_t)(V.hk[s] >> 32) - 1u;
+    const uint32_t head = (V.hk[s] >> 5) - 1u;
     // every index below comes from the scans: a corrupt layout (err set) must not write out of range
     // (round 5: a look-back scan that gave up did)
     const uint32_t P = head <= s ? V.pathpos[head] : SM_NONE;
@@ -805,8 +808,8 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     ScanBufs<uint32_t> tb{{LP.v[0].tour, LP.v[1].tour}};
     launch_scan<uint32_t, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, ScanTourOut{LP, N});
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
-    ScanBufs<uint64_t> hb{{LP.v[0].hk, LP.v[1].hk}};
-    launch_scan<uint64_t, OpMax>(st, hb, LP.scan, nviews, N);
+    ScanBufs<uint32_t> hb{{LP.v[0].hk, LP.v[1].hk}};
+    launch_scan<uint32_t, OpMax>(st, hb, LP.scan, nviews, N);
     hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
     // contiguous bucket slots: scan of path lengths in paths[] order (plen is zero past the last

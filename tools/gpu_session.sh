@@ -7,4 +7,3 @@ timeout -k 10 300 python -u -m pytest tests/test_pms_gpu.py -k "cycle or golden_
 REPS=2 bash tools/gpu_ab.sh "prev|SM_LIB=$GRAFT_REPO_ROOT/variants/prev/libstereomst.so|" "new||" "skl|SM_EXP_SKIP=layout|" || exit 4
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s/stats1 -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-host-io --no-pms --no-segment --inflight 1 > gpurun_out/s/stats1_bench.log 2>&1 || exit 5
 f=$(find gpurun_out/s/stats1 -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/s/kernel_stats_1frame.csv; rm -rf gpurun_out/s/stats1
-SM_PMS_TREE_TIMES=1 timeout -k 10 300 python tools/pms_bench.py 1920 1200 128 2 --reps 1 > gpurun_out/s/tree_times_out.log 2> gpurun_out/s/tree_times.log || exit 8
