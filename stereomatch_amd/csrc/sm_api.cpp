@@ -899,9 +899,7 @@ sm_status stage_mst(sm_ctx* ctx, int views) {
     for (int i = 0; i < nviews; ++i) {  // the active views only: an inactive view's buffers may not exist
         const int v = vs.v[i];
         CHECK(ensure(ctx, ctx->ccnt[v], 16));
-        z.add(ctx->mR[v].p, N);
-        z.add(ctx->mD[v].p, N);
-        z.add(ctx->ccnt[v].p, 16);
+        z.add(ctx->ccnt[v].p, 16);  // (the masks are zeroed by k_bor_local, tile by tile)
     }
     z.add(ctx->changed.p, 2 * SM_MST_MAX_ROUNDS * sizeof(int));
     HIPC(launch_zero(ctx->st, z));
@@ -910,9 +908,15 @@ sm_status stage_mst(sm_ctx* ctx, int views) {
     const bool pixel_rounds = getenv("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B path (tests, tools)
     {
         uint32_t* cc[2] = {nullptr, nullptr};
+        uint32_t* cl[2] = {nullptr, nullptr};
         if (!pixel_rounds)
-            for (int i = 0; i < nviews; ++i) cc[i] = P<uint32_t>(ctx->ccnt[vs.v[i]]);
-        HIPC(launch_bor_local(ctx->st, a, W, H, cc));
+            for (int i = 0; i < nviews; ++i) {
+                const int v = vs.v[i];
+                CHECK(ensure(ctx, ctx->clab[v], N * 4));
+                cc[i] = P<uint32_t>(ctx->ccnt[v]);
+                cl[i] = P<uint32_t>(ctx->clab[v]);
+            }
+        HIPC(launch_bor_local(ctx->st, a, W, H, cc, cl, N));
     }
     if (pixel_rounds) {
         for (int i = 0; i < nviews; ++i) HIPC(hipMemsetAsync(ctx->best[vs.v[i]].p, 0xFF, N * 8, ctx->st));
@@ -948,7 +952,6 @@ sm_status stage_mst(sm_ctx* ctx, int views) {
         c.hook[i] = P<uint32_t>(ctx->chook[v]);
     }
     HIPC(launch_bor_compact(ctx->st, a, c, W, H));
-    HIPC(launch_bor_cinit(ctx->st, a, c));
     // Enqueue the rounds the previous frame needed (the last of them hooked nothing) and the copy
     // of the hook flags, without waiting: the layout is enqueued behind them and the flags are
     // checked after the layout's own synchronisation (mst_finish).  Every kernel of round r exits
@@ -1056,7 +1059,6 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
         CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
         CHECK(ensure(ctx, ctx->slot2pix[v], N * 4));
-        z.add(ctx->plen[v].p, N * 4);  // lengths past the last path stay 0
         z.add(ctx->ccount[v].p, 16);
         z.add(ctx->rounds[v].p, RREC * 4);
         LayoutView& L = LP.v[i];

@@ -229,6 +229,8 @@ struct MstView {
     int* flags;               // flags[r] = 1 if global round r hooked anything
     uint32_t* ccount;         // contracted rounds: [0] K, and root[] = the representatives' compact ids
                               // (k_bor_local assigns them: k_cid folded in, round 5); null otherwise
+    uint32_t* clab;           // contracted rounds: compact id -> label (k_bor_local starts it at the id)
+    size_t bstride;           // contracted rounds: the second minima array is best + bstride
 };
 struct MstPair {
     MstView v[2];
@@ -264,6 +266,14 @@ __global__ __launch_bounds__(BTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     const int tw = min(BT, W - tx0), th = min(BT, H - ty0);
     const int n = tw * th;
     for (int i = threadIdx.x; i < BTN; i += BTHREADS) comp[i] = (uint16_t)i;
+    // the tile's mask bytes start at 0 here (round 5: no separate zero-fill): only this block writes
+    // them before the global rounds, because it hooks intra-tile edges only (a, b both in the tile)
+    for (int i = threadIdx.x; i < n; i += BTHREADS) {
+        const size_t p = (size_t)(ty0 + i / tw) * W + tx0 + i % tw;
+        V.mR[p] = 0;
+        V.mD[p] = 0;
+    }
+    __syncthreads();
     constexpr int PPT = BTN / BTHREADS;  // thread t, slot j: tile pixel (lx, ly) = ((t + 1024 j) % 64, (t + 1024 j) / 64)
     uint32_t ek[PPT][4];
 #pragma unroll
@@ -377,7 +387,12 @@ __global__ __launch_bounds__(BTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     for (int j = 0; j < IPT; ++j) {
         if (!((reps >> j) & 1u)) continue;
         const int i = threadIdx.x + j * BTHREADS;
-        V.root[(size_t)(ty0 + i / tw) * W + tx0 + i % tw] = id++;
+        V.root[(size_t)(ty0 + i / tw) * W + tx0 + i % tw] = id;
+        // the contracted rounds' initial state of component id (round 5: k_cinit folded in)
+        V.clab[id] = id;
+        V.best[id] = SM_KEY_NONE;
+        V.best[V.bstride + id] = SM_KEY_NONE;
+        ++id;
     }
 }
 
@@ -604,16 +619,6 @@ __global__ __launch_bounds__(CBLK) void k_cedges(CPair P, int W, int H) {
         const uint32_t p = (uint32_t)y * (uint32_t)W + (uint32_t)x;
         const uint32_t q = d == 0 ? p + 1 : p + (uint32_t)W;
         V.edges[slot++] = CEdge{sm_edge_key(d == 0 ? V.wR[p] : V.wD[p], p, (uint32_t)d), V.cid[V.comp[p]], V.cid[V.comp[q]]};
-    }
-}
-
-__global__ void k_cinit(CPair P) {
-    const CView V = P.v[blockIdx.y];
-    const uint32_t K = V.counts[0];
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < K; i += gridDim.x * blockDim.x) {
-        V.lab[i] = i;
-        V.best[i] = SM_KEY_NONE;
-        V.best[V.bstride + i] = SM_KEY_NONE;
     }
 }
 
@@ -848,10 +853,12 @@ hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* l
     return hipGetLastError();
 }
 
-hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H, uint32_t* const ccount[2]) {
+hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H, uint32_t* const ccount[2],
+                            uint32_t* const clab[2], size_t bstride) {
     MstPair P;
     for (int v = 0; v < 2; ++v)
-        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v], ccount[v]};
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v], ccount[v],
+                         clab[v], bstride};
     dim3 g((W + BT - 1) / BT, (H + BT - 1) / BT, a.nviews);
     // Tile-phase Boruvka iterations: any cap is exact (unfinished components continue in the
     // contracted rounds); 4 is the measured optimum at C2 (tools/gpu_mst_sweep.sh).
@@ -864,7 +871,8 @@ hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H, uint
 hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r) {
     MstPair P;
     for (int v = 0; v < 2; ++v)
-        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v], nullptr};
+        P.v[v] = MstView{a.wR[v], a.wD[v], a.comp[v], a.best[v], a.root[v], a.mR[v], a.mD[v], a.flags[v], nullptr,
+                         nullptr, 0};
     dim3 g((W + 255) / 256, H, a.nviews);
     hipLaunchKernelGGL(k_bor_min, g, dim3(256), 0, st, P, W, H, r);
     hipLaunchKernelGGL(k_bor_hook, g, dim3(256), 0, st, P, W, H, r);
@@ -953,11 +961,6 @@ hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact
 #define CGRID_K 256    // blocks of 256 over components
 #define CGRID_E 512    // blocks of CBLK * EPT over edges
 
-hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c) {
-    const CPair P = make_cpair(a, c);
-    hipLaunchKernelGGL(k_cinit, dim3(CGRID_K, a.nviews), dim3(256), 0, st, P);
-    return hipGetLastError();
-}
 
 hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r) {
     const CPair P = make_cpair(a, c);

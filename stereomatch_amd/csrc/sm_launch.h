@@ -102,10 +102,12 @@ hipError_t launch_median_weights(hipStream_t st, const uint32_t* lb, const uint3
                                  uint16_t* lwR, uint16_t* lwD, uint16_t* rwR, uint16_t* rwD, int W, int H);
 hipError_t launch_cost_volume(hipStream_t st, const uint32_t* lb, const float* lg, const uint32_t* rb, const float* rg,
                               const float* atab, int W, int H, int d0, int D, float* lvol, float* rvol);
-hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H, uint32_t* const ccount[2]);  // ccount: null for the pixel rounds
+// ccount / clab: null for the pixel rounds; otherwise the contracted rounds' K counter and label array,
+// whose initial state k_bor_local writes with the compact ids (minima: best, best + bstride)
+hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H, uint32_t* const ccount[2],
+                            uint32_t* const clab[2], size_t bstride);
 hipError_t launch_bor_round(hipStream_t st, const MstArgs& a, int W, int H, int r);
 hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int H);
-hipError_t launch_bor_cinit(hipStream_t st, const MstArgs& a, const MstCompact& c);
 hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r);
 hipError_t launch_zero(hipStream_t st, const ZeroList& z);
 hipError_t launch_mst_done(hipStream_t st, const MstArgs& a, int r, int* ok);

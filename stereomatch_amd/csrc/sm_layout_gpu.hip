@@ -295,7 +295,12 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* sh, T* total) {
 template <class T>
 struct ScanBufs {
     T* data[2];
+    const uint32_t* len[2];  // optional: the element count, read on the device (min with nelem)
 };
+template <class T>
+__device__ __forceinline__ int scan_len(const ScanBufs<T>& B, int v, int nelem) {
+    return B.len[v] ? min(nelem, (int)*B.len[v]) : nelem;
+}
 
 // block-wide reduction of one value per thread (SP_THREADS threads), the result on every thread
 template <class T, class Op>
@@ -315,6 +320,7 @@ __device__ __forceinline__ T sp_block_reduce(T x, T* sh) {
 template <class T, class Op>
 __global__ __launch_bounds__(SP_THREADS) void k_scan_reduce(ScanBufs<T> B, ScanState S, int nelem) {
     const int v = blockIdx.y;
+    nelem = scan_len(B, v, nelem);
     __shared__ T sh[SP_THREADS / 64];
     const T* d = B.data[v];
     const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
@@ -331,9 +337,12 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_reduce(ScanBufs<T> B, ScanS
 
 // the scans' outputs: in place (the max-scan of hk, the add-scan of the path lengths) ...
 struct ScanInPlace {
+    static constexpr bool kNext = false;  // the epilogue needs the next element's tag bit 0
     __device__ bool active() const { return true; }
+    __device__ void begin() const {}
+    __device__ void end(int) const {}
     template <class T> __device__ static uint32_t tag(T) { return 0u; }
-    template <class T> __device__ void operator()(T* d, int, size_t i, T incl, uint32_t) const { d[i] = incl; }
+    template <class T> __device__ void operator()(T* d, int, size_t i, T incl, uint32_t, bool) const { d[i] = incl; }
 };
 // ... or, for the tour, the preorder records: at the down arc into node q (orig < 2^31) the inclusive sum is
 // (light depth of q) << 27 | (heavy-first preorder of q), and orig == 1 iff q is its parent's heavy child,
@@ -345,11 +354,14 @@ struct ScanTourOut {
     LayoutPair LP;
     int N;
     // an incomplete MST (k_orient wrote nothing: the tour holds a previous call's values) has no records
+    static constexpr bool kNext = false;
     __device__ bool active() const { return *LP.mst_ok != 0; }
+    __device__ void begin() const {}
+    __device__ void end(int) const {}
     // what the epilogue needs of an element's own value, 2 bits (kept in one register for all 16 items
     // instead of a copy of the items): 1 = a down arc, 2 = the heavy child's
     __device__ static uint32_t tag(uint32_t orig) { return orig < 0x80000000u ? (orig == 1u ? 3u : 1u) : 0u; }
-    __device__ void operator()(uint32_t*, int v, size_t i, uint32_t incl, uint32_t tg) const {
+    __device__ void operator()(uint32_t*, int v, size_t i, uint32_t incl, uint32_t tg, bool) const {
         if (!(tg & 1u)) return;  // an up arc
         const LayoutView& V = LP.v[v];
         const uint32_t pre = incl & (TOUR_LIGHT - 1u), ld = incl >> TOUR_SHIFT;
@@ -362,10 +374,60 @@ struct ScanTourOut {
     }
 };
 
+// ... or, for the max-scan of the path records, in place plus the path histogram (round 5: replaces
+// k_path_count): position s ends its path iff s + 1 is a head (tag: the raw record is not 0), and its
+// scanned record names the path's head and light depth -> per (light depth, long / short) bucket the
+// paths, their nodes and the longest, block-aggregated in LDS.
+struct ScanPathCount {
+    static constexpr bool kNext = true;
+    LayoutPair LP;
+    __device__ bool active() const { return *LP.mst_ok != 0; }
+    __device__ static uint32_t* lds() {
+        __shared__ uint32_t h[3 * SM_NBUCKETS];  // paths, nodes, longest
+        return h;
+    }
+    __device__ void begin() const {
+        for (int i = threadIdx.x; i < 3 * SM_NBUCKETS; i += blockDim.x) lds()[i] = 0;
+        __syncthreads();
+    }
+    __device__ static uint32_t tag(uint32_t raw) { return raw != 0u ? 1u : 0u; }
+    // another wave's element k, raw or already scanned (in place) by now: a head's record names k itself
+    // either way, any other position holds 0 or an earlier head's record
+    __device__ static bool tag_of_stored(uint32_t stored, size_t k) { return (stored >> 5) == (uint32_t)k + 1u; }
+    __device__ void operator()(uint32_t* d, int v, size_t i, uint32_t incl, uint32_t, bool next_head) const {
+        d[i] = incl;
+        if (!next_head) return;
+        const uint32_t s = (uint32_t)i, head = (incl >> 5) - 1u, ld = incl & 31u;
+        if (head > s) {  // (never for a spanning tree's tour: defensive)
+            __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        const uint32_t len = s - head + 1u, b = 2u * ld + (len >= SM_LONG_PATH ? 0u : 1u);
+        uint32_t* h = lds();
+        atomicAdd(&h[b], 1u);
+        atomicAdd(&h[SM_NBUCKETS + b], len);
+        if (len >= SM_LONG_PATH) atomicMax(&h[2 * SM_NBUCKETS + b], len);
+        (void)v;
+    }
+    __device__ void end(int v) const {
+        __syncthreads();
+        const LayoutView& V = LP.v[v];
+        const uint32_t* h = lds();
+        const int b = threadIdx.x;
+        if (b < SM_NBUCKETS && h[b]) {
+            atomicAdd(&V.round_count[b], h[b]);
+            atomicAdd(&V.round_nodes[b], h[SM_NBUCKETS + b]);
+            if (h[2 * SM_NBUCKETS + b]) atomicMax(&V.round_maxlen[b], h[2 * SM_NBUCKETS + b]);
+        }
+    }
+};
+
 template <class T, class Op, class Out>
 __global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanState S, int nelem, Out out) {
     if (!out.active()) return;  // (block-uniform)
     const int v = blockIdx.y;
+    nelem = scan_len(B, v, nelem);
+    if ((size_t)blockIdx.x * SP_TILE >= (size_t)nelem) return;  // (block-uniform) past a dynamic length
     const uint32_t tile = blockIdx.x;
     __shared__ T s_w[SP_THREADS / 64];
     T* d = B.data[v];
@@ -404,11 +466,24 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanSt
 #pragma unroll
     for (int k = 0; k < SP_THREADS / 64; ++k)
         if (k < w) pre = Op::apply(pre, s_w[k]);
+    out.begin();
 #pragma unroll
     for (int j = 0; j < SP_ITEMS; ++j) {
         const size_t i = wbase + (size_t)j * 64 + lane;
-        if (i < (size_t)nelem) out(d, v, i, Op::apply(pre, x[j]), (tags >> (2 * j)) & 3u);  // inclusive
+        bool nxt = false;
+        if constexpr (Out::kNext) {  // the next element's tag bit 0: a neighbour lane, the next chunk, or memory
+            const uint32_t t0 = (tags >> (2 * j)) & 1u;
+            const uint32_t dn = __shfl_down(t0, 1);
+            uint32_t t1 = 0;
+            if (j + 1 < SP_ITEMS) t1 = __shfl((tags >> (2 * (j + 1))) & 1u, 0);
+            if (lane < 63) nxt = dn != 0u;
+            else if (j + 1 < SP_ITEMS) nxt = t1 != 0u;
+            else if (i + 1 < (size_t)nelem) nxt = Out::tag_of_stored(d[i + 1], i + 1);
+            if (i + 1 == (size_t)nelem) nxt = true;  // the last element ends its path
+        }
+        if (i < (size_t)nelem) out(d, v, i, Op::apply(pre, x[j]), (tags >> (2 * j)) & 3u, nxt);  // inclusive
     }
+    out.end(v);
 }
 
 template <class T, class Op, class Out = ScanInPlace>
@@ -522,33 +597,6 @@ __device__ __forceinline__ bool path_of(const LayoutPair& LP, const LayoutView& 
 }
 #define PATH_BLOCK 1024
 #define PATH_ITEMS 8   // slots per thread -> 8192 per block (few global atomics per round bin)
-
-// after the max-scan: count paths per (round, long/short) bucket at their last slot
-__global__ __launch_bounds__(PATH_BLOCK) void k_path_count(LayoutPair LP, int N) {
-    if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
-    const LayoutView& V = LP.v[blockIdx.y];
-    __shared__ uint32_t hist[SM_NBUCKETS], nodes[SM_NBUCKETS], mlen[SM_NBUCKETS];
-    if (threadIdx.x < SM_NBUCKETS) hist[threadIdx.x] = nodes[threadIdx.x] = mlen[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t base = blockIdx.x * PATH_BLOCK * PATH_ITEMS;
-    for (int i = 0; i < PATH_ITEMS; ++i) {
-        const uint32_t s = base + i * PATH_BLOCK + threadIdx.x;
-        if (s >= (uint32_t)N) break;
-        uint32_t head, b;
-        if (path_last(V, s, N) && path_of(LP, V, s, head, b)) {
-            const uint32_t len = s - head + 1u;
-            atomicAdd(&hist[b], 1u);
-            atomicAdd(&nodes[b], len);
-            if (len >= SM_LONG_PATH) atomicMax(&mlen[b], len);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < SM_NBUCKETS && hist[threadIdx.x]) {
-        atomicAdd(&V.round_count[threadIdx.x], hist[threadIdx.x]);
-        atomicAdd(&V.round_nodes[threadIdx.x], nodes[threadIdx.x]);
-        if (mlen[threadIdx.x]) atomicMax(&V.round_maxlen[threadIdx.x], mlen[threadIdx.x]);
-    }
-}
 
 __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
@@ -805,16 +853,16 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
     hipLaunchKernelGGL(k_orient, tg, dim3(256), 0, st, LP, W, H);
-    ScanBufs<uint32_t> tb{{LP.v[0].tour, LP.v[1].tour}};
+    ScanBufs<uint32_t> tb{{LP.v[0].tour, LP.v[1].tour}, {nullptr, nullptr}};
     launch_scan<uint32_t, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, ScanTourOut{LP, N});
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);
-    ScanBufs<uint32_t> hb{{LP.v[0].hk, LP.v[1].hk}};
-    launch_scan<uint32_t, OpMax>(st, hb, LP.scan, nviews, N);
-    hipLaunchKernelGGL(k_path_count, sg, dim3(PATH_BLOCK), 0, st, LP, N);
+    ScanBufs<uint32_t> hb{{LP.v[0].hk, LP.v[1].hk}, {nullptr, nullptr}};
+    launch_scan<uint32_t, OpMax>(st, hb, LP.scan, nviews, N, ScanPathCount{LP});
     hipLaunchKernelGGL(k_path_emit, sg, dim3(PATH_BLOCK), 0, st, LP, N);
-    // contiguous bucket slots: scan of path lengths in paths[] order (plen is zero past the last
+    // contiguous bucket slots: scan of path lengths in paths[] order (plen past the last path is not read
     // path), slot of every preorder position, then the metadata in slot numbering
-    ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}};
+    // (only the paths' lengths: the path count, round_begin[SM_NBUCKETS], is read on the device)
+    ScanBufs<uint32_t> lb{{LP.v[0].plen, LP.v[1].plen}, {LP.v[0].round_begin + SM_NBUCKETS, LP.v[1].round_begin + SM_NBUCKETS}};
     launch_scan<uint32_t, OpAdd>(st, lb, LP.scan, nviews, N);
     hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
     hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, H);

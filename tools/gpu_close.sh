@@ -18,6 +18,8 @@ bash tools/gpu_prof_round.sh $TAG || exit 3
 python3 -c "import json;d=json.loads(open('$O/bench_default.log').read().strip().splitlines()[-1]);print('default', round(d['ms_per_step'],3), 'frac', round(d['roofline']['frac'],3), 'same_build', d['roofline'].get('traffic_src',{}).get('same_build'))" || true
 timeout -k 10 300 python tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms100.log 2>&1 || exit 4
 tail -1 $O/pms100.log | cut -c1-200
+timeout -k 10 300 python bench.py --disp 256 --steps 20 --warmup 5 --no-cpu --no-host-io --no-pms --no-segment > $O/c4_1gpu.log 2>&1 || exit 6
+python3 -c "import json;d=json.loads(open('$O/c4_1gpu.log').read().strip().splitlines()[-1]);print('C4 on 1 GPU', round(d['ms_per_step'],3))" || true
 for spec in "0/8 --frame-groups 1" "0/8 --frame-groups 2" "0/8 --shard d --frame-groups 1"; do
   set -- $spec
   tagn=$(echo "$spec" | tr ' /' '__' | tr -d '-')
