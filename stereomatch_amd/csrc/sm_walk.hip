@@ -48,7 +48,8 @@
 #define WALK_DN_CH4 4
 #endif
 #ifndef WALK_DN_CH2
-#define WALK_DN_CH2 6
+#define WALK_DN_CH2 4  // round 5: 6 -> 4 (81 -> 64 VGPRs, 5 -> 8 waves per SIMD): the same kernel time one
+                       // frame at a time, C2 4.37 -> 4.30 ms/frame with frames in flight (5: 7 waves, 4.30-4.34)
 #endif
 #ifndef WALK_UP_CH1
 #define WALK_UP_CH1 4
@@ -302,7 +303,8 @@ __device__ __forceinline__ uint32_t hfield_v(uint32_t w, int hl, int j, int f) {
 }
 
 #ifndef WALK_UP_CHH
-#define WALK_UP_CHH 3
+#define WALK_UP_CHH 2  // round 5: 3 -> 2 (76 -> 72 VGPRs, 6 -> 7 waves per SIMD), with WALK_DN_CHH 4 -> 3
+                       // (5 -> 7): the N = 8 share 2.009-2.016 -> 1.967-1.987 ms/frame
 #endif
 
 template <int CH>
@@ -887,7 +889,7 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
 
 // SPL = 1 calls with 64-double rows take the half-wave down walker (env SM_NO_HALF_WAVE: A/B)
 #ifndef WALK_DN_CHH
-#define WALK_DN_CHH 4
+#define WALK_DN_CHH 3
 #endif
 static bool half_wave_down(const WalkArgs& a, int spl) { return half_wave(a, spl) && !a.wta.sub; }
 
