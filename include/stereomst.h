@@ -133,7 +133,8 @@ sm_status sm_device_count(int* count);
  * per view, the strict-< argmin slice (global index), its aggregated cost (fp64) and the
  * disparity as float.  Any output pointer may be NULL.  When the context has an RCCL
  * communicator (sm_comm_init) the per-rank results are reduced (min+argmin) across ranks
- * and every rank receives the global answer. */
+ * and every rank receives the global answer.  W * H must be below 2^27 pixels (the tree layout
+ * packs preorder positions in 27 bits): larger images return SM_ERR_ARG. */
 sm_status sm_match(sm_ctx* ctx, const uint8_t* left_bgr, const uint8_t* right_bgr, int W, int H,
                    int row_stride, int D, const sm_params* p,
                    float* left_disp, float* right_disp, int32_t* left_idx, int32_t* right_idx,
