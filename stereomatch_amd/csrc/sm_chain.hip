@@ -274,7 +274,9 @@ __device__ __forceinline__ void lds_wait_all(int* p, int n, int v) {  // p[0..n)
 #define UP_G1 4  // SPL = 1 (one-view 64-slice shares, D <= 64); 6 x 10 -> 4 x 18: k_up_chain 0.529 -> 0.504 ms at the N = 8 share
 #endif
 #ifndef UP_NS1
-#define UP_NS1 18
+#define UP_NS1 10  // round 5: 18 -> 10 slots (150 -> ~85 KB of LDS, so other frames' walker blocks fit beside
+                   // a chain workgroup): the N = 8 share 1.945-1.948 -> 1.907-1.918 ms/frame, the kernel itself
+                   // unchanged (SPL = 2's ring at 5 / 6 slots did not help C2: DESIGN.md 5.-2)
 #endif
 #ifndef UP_G2
 #define UP_G2 4  // even: the chain's two-half pipeline
@@ -1014,8 +1016,8 @@ struct RepCfg {
     static_assert(BB >= 4, "repair pass");
 };
 // the repair batch follows the ring's size; its value at the shipped geometries is pinned here, so a
-// ring sweep that changes it is visible (SPL=1 4 x 18 ring -> 16-node passes)
-static_assert(UP_G1 != 4 || UP_NS1 != 18 || RepCfg<1>::BB == 16, "RepCfg<1>::BB changed with the SPL=1 ring");
+// ring sweep that changes it is visible (SPL=1 4 x 10 ring, 78 KB -> still 16-node passes)
+static_assert(UP_G1 != 4 || UP_NS1 != 10 || RepCfg<1>::BB == 16, "RepCfg<1>::BB changed with the SPL=1 ring");
 
 // one wave stages nodes k0 .. k0+nb-1 (node k = slot top - k; metadata in mv) into rn[k - kb]
 template <int SPL, bool AGD, int CHR>

@@ -604,12 +604,21 @@ __global__ __launch_bounds__(CBLK) void k_cedges(CPair P, int W, int H) {
 #pragma unroll
     for (int j = 0; j < SPT; ++j)
         if (hpair[threadIdx.x + j * CBLK] != EH_EMPTY) occ |= 1u << j;
-    uint32_t slot = block_append(__builtin_popcount(occ) + __builtin_popcount(ovf), &V.counts[1]);
+    // Round 0 of the contracted rounds happens here (round 5: its k_cmin is not launched): every listed
+    // edge joins two distinct components (labels are the ids), so the list is round 0's output list
+    // (list 1) as it stands, and each edge offers its key to both endpoints' round-0 minima
+    CEdge* out = V.edges + V.emax;
+    uint32_t slot = block_append(__builtin_popcount(occ) + __builtin_popcount(ovf), &V.counts[2]);
+    auto emit = [&](const CEdge& E) __attribute__((always_inline)) {
+        out[slot++] = E;
+        atomicMin(&V.best[E.u], E.key);
+        atomicMin(&V.best[E.v], E.key);
+    };
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
         if (!(occ & (1u << j))) continue;
         const unsigned long long pr = hpair[threadIdx.x + j * CBLK];
-        V.edges[slot++] = CEdge{hmin[threadIdx.x + j * CBLK], (uint32_t)(pr >> 32), (uint32_t)pr};
+        emit(CEdge{hmin[threadIdx.x + j * CBLK], (uint32_t)(pr >> 32), (uint32_t)pr});
     }
     while (ovf) {
         const int b = __builtin_ctz(ovf);
@@ -618,7 +627,7 @@ __global__ __launch_bounds__(CBLK) void k_cedges(CPair P, int W, int H) {
         const int y = ty0 + (int)(threadIdx.x / BT) + i * (CBLK / BT);
         const uint32_t p = (uint32_t)y * (uint32_t)W + (uint32_t)x;
         const uint32_t q = d == 0 ? p + 1 : p + (uint32_t)W;
-        V.edges[slot++] = CEdge{sm_edge_key(d == 0 ? V.wR[p] : V.wD[p], p, (uint32_t)d), V.cid[V.comp[p]], V.cid[V.comp[q]]};
+        emit(CEdge{sm_edge_key(d == 0 ? V.wR[p] : V.wD[p], p, (uint32_t)d), V.cid[V.comp[p]], V.cid[V.comp[q]]});
     }
 }
 
@@ -964,7 +973,7 @@ hipError_t launch_bor_compact(hipStream_t st, const MstArgs& a, const MstCompact
 
 hipError_t launch_bor_cround(hipStream_t st, const MstArgs& a, const MstCompact& c, int W, int r) {
     const CPair P = make_cpair(a, c);
-    hipLaunchKernelGGL(k_cmin, dim3(CGRID_E, a.nviews), dim3(CBLK), 0, st, P, r);
+    if (r > 0) hipLaunchKernelGGL(k_cmin, dim3(CGRID_E, a.nviews), dim3(CBLK), 0, st, P, r);  // (round 0: k_cedges)
     hipLaunchKernelGGL(k_chook, dim3(CGRID_K, a.nviews), dim3(256), 0, st, P, W, r);
     hipLaunchKernelGGL(k_crelabel, dim3(CGRID_K, a.nviews), dim3(256), 0, st, P, r);
     return hipGetLastError();
