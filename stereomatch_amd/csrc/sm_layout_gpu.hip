@@ -128,7 +128,8 @@ __device__ __forceinline__ TourBufs tour_bufs(const LayoutView& V) {
 }
 
 // L1: contract the tour inside each 32x32 tile (sm_tour.h)
-__global__ __launch_bounds__(TL_THREADS) void k_tour_tile(LayoutPair LP, int W, int H) {
+// (waves_per_eu 8: 66 -> 64 VGPRs, no scratch; with the bit-packed predecessor flags the LDS fits 8 per CU)
+__global__ __launch_bounds__(TL_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_tour_tile(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
     const TileRef t = layout_tile(W, H, (int)blockIdx.x);
@@ -245,9 +246,12 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
 #define SP_THREADS 256
 // items per thread: 16 of 32 bits, 8 of 64 bits (16 64-bit items and their interleaved shuffles took
 // 120 VGPRs: 4 waves per SIMD)
+// (an epilogue may ask for fewer: Out::kItems, e.g. the path histogram's, whose 16 unrolled items took 95
+// VGPRs)
 template <class T> struct SpItems { static constexpr int n = sizeof(T) == 8 ? 8 : 16; };
-#define SP_ITEMS (SpItems<T>::n)
-#define SP_TILE (SP_THREADS * SP_ITEMS)
+template <class T, class Out> struct SpItemsOut { static constexpr int n = Out::kItems ? Out::kItems : SpItems<T>::n; };
+#define SP_ITEMS IT
+#define SP_TILE (SP_THREADS * IT)
 
 struct OpAdd {
     template <class T> __device__ static T apply(T a, T b) { return a + b; }
@@ -317,7 +321,7 @@ __device__ __forceinline__ T sp_block_reduce(T x, T* sh) {
     return r;
 }
 
-template <class T, class Op>
+template <class T, class Op, int IT>
 __global__ __launch_bounds__(SP_THREADS) void k_scan_reduce(ScanBufs<T> B, ScanState S, int nelem) {
     const int v = blockIdx.y;
     nelem = scan_len(B, v, nelem);
@@ -337,6 +341,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_reduce(ScanBufs<T> B, ScanS
 
 // the scans' outputs: in place (the max-scan of hk, the add-scan of the path lengths) ...
 struct ScanInPlace {
+    static constexpr int kItems = 0;      // items per thread (0: by element size)
     static constexpr bool kNext = false;  // the epilogue needs the next element's tag bit 0
     __device__ bool active() const { return true; }
     __device__ void begin() const {}
@@ -353,8 +358,9 @@ struct ScanInPlace {
 struct ScanTourOut {
     LayoutPair LP;
     int N;
-    // an incomplete MST (k_orient wrote nothing: the tour holds a previous call's values) has no records
+    static constexpr int kItems = 0;
     static constexpr bool kNext = false;
+    // an incomplete MST (k_orient wrote nothing: the tour holds a previous call's values) has no records
     __device__ bool active() const { return *LP.mst_ok != 0; }
     __device__ void begin() const {}
     __device__ void end(int) const {}
@@ -379,6 +385,7 @@ struct ScanTourOut {
 // scanned record names the path's head and light depth -> per (light depth, long / short) bucket the
 // paths, their nodes and the longest, block-aggregated in LDS.
 struct ScanPathCount {
+    static constexpr int kItems = 8;
     static constexpr bool kNext = true;
     LayoutPair LP;
     __device__ bool active() const { return *LP.mst_ok != 0; }
@@ -422,7 +429,7 @@ struct ScanPathCount {
     }
 };
 
-template <class T, class Op, class Out>
+template <class T, class Op, class Out, int IT>
 __global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanState S, int nelem, Out out) {
     if (!out.active()) return;  // (block-uniform)
     const int v = blockIdx.y;
@@ -489,9 +496,10 @@ __global__ __launch_bounds__(SP_THREADS) void k_scan_tiles(ScanBufs<T> B, ScanSt
 template <class T, class Op, class Out = ScanInPlace>
 static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S, int nviews, int nelem, Out out = Out{}) {
     if (nelem <= 0) return;
+    constexpr int IT = SpItemsOut<T, Out>::n;
     const int ntiles = (nelem + SP_TILE - 1) / SP_TILE;
-    hipLaunchKernelGGL((k_scan_reduce<T, Op>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem);
-    hipLaunchKernelGGL((k_scan_tiles<T, Op, Out>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem, out);
+    hipLaunchKernelGGL((k_scan_reduce<T, Op, IT>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem);
+    hipLaunchKernelGGL((k_scan_tiles<T, Op, Out, IT>), dim3(ntiles, nviews), dim3(SP_THREADS), 0, st, B, S, nelem, out);
 }
 
 // Per-slot metadata: pixel, parent slot, child weights and slots in descending (w,a,b) key order (the

@@ -61,12 +61,12 @@ __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, 
                                   // j's slot
     } st;
     static_assert(4 * TL_ARCS >= TLS, "the compaction's index table fits the word array");
-    __shared__ uint8_t haspred[TL_ARCS];
+    __shared__ uint32_t haspred[(TL_ARCS + 31) / 32];  // a bit per arc (bytes held the block to 7 per CU)
     __shared__ uint32_t s_cnt[64];
     constexpr int PER = TLS / TL_THREADS;  // 16 slots per thread
     static_assert(PER * (TL_THREADS / 64) == 64, "one wave scans the per-(slot row, wave) counts");
     const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < TL_ARCS; i += TL_THREADS) haspred[i] = 0;
+    for (int i = threadIdx.x; i < (TL_ARCS + 31) / 32; i += TL_THREADS) haspred[i] = 0u;
     // successors in slot space; compact ranks in slot order: slot s = threadIdx.x + 256 i, so for each i
     // the waves hold consecutive runs of 64 slots
     uint32_t nxt[PER], rk[PER], live = 0;
@@ -130,7 +130,7 @@ __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, 
         if (!((live >> i) & 1u)) continue;
         const uint32_t n = nxt[i];
         const uint32_t nc = n < L_NIL ? (uint32_t)st.h[n] : n;
-        if (n < L_NIL) haspred[nc] = 1;
+        if (n < L_NIL) atomicOr(&haspred[nc >> 5], 1u << (nc & 31u));
         nw[i] = (uint64_t)nc | (1ull << 16) | ((uint64_t)rk[i] << 32) | ((uint64_t)(threadIdx.x + i * TL_THREADS) << 48);
     }
     __syncthreads();  // (h read: now the words overwrite it)
@@ -177,7 +177,7 @@ __device__ __forceinline__ void tour_tile(const G& g, const TourBufs& T, int W, 
         const uint32_t j = threadIdx.x + m * TL_THREADS;
         const uint32_t dist = (uint32_t)(own[m] >> 16) & 0xFFFFu, last = (uint32_t)(own[m] >> 32) & 0xFFFFu;
         myhead[m] = SM_NONE;
-        if (m < nper && dist != 0 && !haspred[j]) {
+        if (m < nper && dist != 0 && !((haspred[j >> 5] >> (j & 31u)) & 1u)) {
             myhead[m] = atomicAdd(&nheads, 1u);  // LDS atomic: rank of this chain inside the tile
             st.h[4 * last + 2] = (uint16_t)myhead[m];
         }
