@@ -143,6 +143,7 @@ struct sm_ctx {
     // segment mode (finite c, sm_segment.cpp): layout weights with the virtual edges, and host copies
     DevBuf fwR[2], fwD[2];
     bool seg = false;  // the current tree is a segment forest (layout reads fwR / fwD)
+    bool want_size = false;  // the layout writes subtree sizes (sm_build_tree reports them)
     bool sub = false;  // the current call's WTA carries subpixel disparities (SM_POST_SUBPIXEL)
     int seg_trees[2] = {0, 0};
     PinnedVec<uint16_t> h_w[2][2], h_fw[2][2];
@@ -168,7 +169,7 @@ struct sm_ctx {
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], arcpix[2], hk[2], pixpre[2];
     DevBuf a_dist[2], a_cid[2], ccount[2], c_last[2], c_len[2];
-    DevBuf segtab[2], pathpos[2], plen[2], slotpix[2], slot2pix[2];
+    DevBuf segtab[2], pathpos[2], plen[2], slotpix[2];
     DevBuf pieces[2], pieces_tmp[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
     DevBuf cnw[2], tour[2], spart[2], rounds[2];
     int* h_changed = nullptr;
@@ -1058,7 +1059,6 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->pathpos[v], N * 4));
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
         CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
-        CHECK(ensure(ctx, ctx->slot2pix[v], N * 4));
         z.add(ctx->ccount[v].p, 16);
         z.add(ctx->rounds[v].p, RREC * 4);
         LayoutView& L = LP.v[i];
@@ -1086,7 +1086,6 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.pathpos = P<uint32_t>(ctx->pathpos[v]);
         L.plen = P<uint32_t>(ctx->plen[v]);
         L.slotpix = P<uint32_t>(ctx->slotpix[v]);
-        L.slot2pix = P<uint32_t>(ctx->slot2pix[v]);
         uint32_t* R = P<uint32_t>(ctx->rounds[v]);
         L.round_begin = R;
         L.round_count = R + SM_NBUCKETS + 1;
@@ -1105,6 +1104,7 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
     LP.mst_ok = P<int>(ctx->mst_ok);
     if (nviews == 1) LP.scan.part[1] = LP.scan.part[0];
     LP.scan.err = ctx->d_err;
+    LP.want_size = ctx->want_size ? 1 : 0;
     HIPC(launch_zero(ctx->st, z));
     HIPC(launch_layout(ctx->st, LP, nviews, W, H, max_chains, (uint32_t)piece_len()));
     // the host needs the per-round path counts to size the walker grids
@@ -2605,7 +2605,7 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->cnw[v],
                          &ctx->tour[v], &ctx->spart[v],
                          &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
-                         &ctx->slotpix[v], &ctx->slot2pix[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
+                         &ctx->slotpix[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
@@ -2903,7 +2903,10 @@ sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int str
     CHECK(upload(ctx, bgr, bgr, W, H, stride));
     CHECK(stage_prep(ctx));
     CHECK(stage_tree(ctx, 1, p, true));  // the image is uploaded as both views: view 0 only
-    CHECK(stage_layout(ctx, 1));
+    ctx->want_size = true;
+    const sm_status ls = stage_layout(ctx, 1);
+    ctx->want_size = false;
+    CHECK(ls);
     const size_t N = (size_t)W * H;
     // segment mode: the virtual edges that link the trees are not part of the reported forest
     const bool seg = ctx->seg;

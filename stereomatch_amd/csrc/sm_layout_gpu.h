@@ -114,7 +114,6 @@ struct LayoutView {
     uint32_t* pathpos;       // [preorder of a head] -> index of its path in paths[]
     uint32_t* plen;          // [path] -> len, inclusive-scanned into the path's end slot
     uint32_t* slotpix;       // [pixel] -> slot
-    uint32_t* slot2pix;      // [slot] -> pixel
     uint32_t* round_count;   // SM_NBUCKETS
     uint32_t* round_cursor;  // SM_NBUCKETS
     uint32_t* round_begin;   // SM_NBUCKETS + 1
@@ -142,6 +141,7 @@ struct LayoutPair {
     LayoutView v[2];
     const int* mst_ok;  // != 0 once the MST is complete (k_mst_done); every layout kernel checks it
     ScanState scan;
+    int want_size;  // write the subtree sizes (V.size): only sm_build_tree reports them
 };
 
 hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W, int H, uint32_t max_chains,

@@ -213,7 +213,7 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
             return;
         }
         V.pdir[v] = (int8_t)pd;
-        V.size[v] = sz;
+        if (LP.want_size) V.size[v] = sz;  // (only sm_build_tree reports subtree sizes)
         V.heavy[v] = (int8_t)heavy;
         if (pd < 0) {  // the root: preorder 0, light depth 0, a path head (the tour scan writes the others)
             V.hk[0] = HK_REC(0u, 0u);
@@ -662,8 +662,8 @@ __global__ __launch_bounds__(PATH_BLOCK) void k_path_emit(LayoutPair LP, int N) 
 
 // Slots, in preorder order (coalesced): the paths of one (light depth, long/short) bucket occupy a
 // contiguous slot range, each path contiguous from its head, in paths[] order; plen holds the inclusive
-// scan of the lengths, i.e. the end slot of a path.  slot2pix is written nearly in order (a path's slots
-// are consecutive), slotpix is the pass's one random store.
+// scan of the lengths, i.e. the end slot of a path.  slotpix is the pass's one (random) store (round 5: the
+// inverse slot2pix, which no pass read, is gone).
 __global__ void k_newslot(LayoutPair LP, int N) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
@@ -682,7 +682,6 @@ __global__ void k_newslot(LayoutPair LP, int N) {
         return;
     }
     V.slotpix[pix] = slot;
-    V.slot2pix[slot] = pix;
     if (s == head) V.paths[P].head = nh;  // (other threads read .len only)
 }
 
