@@ -1876,12 +1876,11 @@ sm_status pms_serial_range(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d, 
         run = t + 1;
         if (t == t1) break;
         const int deg = f.nb_start[t + 1] - f.nb_start[t];
-        HIPC(launch_pms_prop_one(st, d, t, deg));
-        if (deg > 0) {  // over the tree's distinct propagation labels (k_pms_prop_dedupe)
+        if (deg > 0) {  // its labels, then over its distinct propagation labels (one launch: k_pms_prop_tree)
             PmsDev dd = d;
             dd.labu = P<float4>(ctx->pms[v].labu);
             dd.nprop = P<int32_t>(ctx->pms[v].nprop);
-            HIPC(launch_pms_prop_dedupe(st, dd, t, t + 1));
+            HIPC(launch_pms_prop_tree(st, dd, t));
             dd.lab = dd.labu;
             CHECK(pms_phase(ctx, st, v, dd, 0, t, t + 1));
         }

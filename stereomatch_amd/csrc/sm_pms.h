@@ -79,7 +79,7 @@ hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1);
 hipError_t launch_pms_prop_dedupe(hipStream_t st, const PmsDev& d, int t_lo, int t_hi);
 // serial mode, one large tree over the whole GPU: propagation labels from *off, and the refinement
 // labels (after the propagation update), which advance *off
-hipError_t launch_pms_prop_one(hipStream_t st, const PmsDev& d, int t, int deg);
+hipError_t launch_pms_prop_tree(hipStream_t st, const PmsDev& d, int t);  // d: labu / nprop set (labels + dedupe)
 hipError_t launch_pms_ref_one(hipStream_t st, const PmsDev& d, int t);
 // speculative iteration over trees [t_lo, K): every tree at once from the guessed offsets and the
 // labels at the start of the iteration, then validation (sm_pms.hip "Speculation")

@@ -745,13 +745,8 @@ __global__ void __launch_bounds__(1024) k_pms_guess(PmsDev d, int t_lo, long lon
     }
 }
 
-// serial mode, one large tree with the whole GPU: its propagation labels from the running offset, and
-// after its propagation update its refinement labels, which advance the offset
-__global__ void k_pms_prop_one(PmsDev d, int t) {
-    const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (j < tree_deg(d, t)) prop_label(d, t, d.off[0], j);
-}
-
+// serial mode, one large tree with the whole GPU: after its propagation update, its refinement labels, which
+// advance the offset (its propagation labels: k_pms_prop_tree below)
 __global__ void k_pms_ref_one(PmsDev d, int t) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     const int deg = tree_deg(d, t);
@@ -783,6 +778,42 @@ __global__ void __launch_bounds__(256) k_pms_prop_dedupe(PmsDev d, int t_lo, int
     if (t >= t_hi) return;
     const int lane = (int)(threadIdx.x & 63);
     const int deg = tree_deg(d, t), base = d.tree_lab[t];
+    int n = 0;
+    for (int j0 = 0; j0 < deg; j0 += 64) {
+        const int j = j0 + lane;
+        bool keep = false;
+        float4 L = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < deg) {
+            L = d.lab[base + j];
+            keep = true;
+            for (int i = 0; i < j; ++i) {
+                const float4 M = d.lab[base + i];
+                if (__float_as_uint(M.x) == __float_as_uint(L.x) && __float_as_uint(M.y) == __float_as_uint(L.y) &&
+                    __float_as_uint(M.z) == __float_as_uint(L.z)) {
+                    keep = false;
+                    break;
+                }
+            }
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) d.labu[base + n + __popcll(m & ((1ull << lane) - 1ull))] = L;
+        n += __popcll(m);
+    }
+    if (lane == 0) d.nprop[t] = n;
+}
+
+// serial mode, one large tree: its propagation labels from the running offset and k_pms_prop_dedupe of that
+// tree in one block (round 5: k_pms_prop_one and the dedupe were two launches per large tree; the first
+// call is bound by its ~10k launches): the labels, a block barrier, then wave 0 keeps the first occurrence
+// of each distinct label, as k_pms_prop_dedupe does
+__global__ void __launch_bounds__(256) k_pms_prop_tree(PmsDev d, int t) {
+    const int deg = tree_deg(d, t);
+    const long long o = d.off[0];
+    for (int j = (int)threadIdx.x; j < deg; j += (int)blockDim.x) prop_label(d, t, o, j);
+    __threadfence_block();
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const int lane = (int)threadIdx.x, base = d.tree_lab[t];
     int n = 0;
     for (int j0 = 0; j0 < deg; j0 += 64) {
         const int j = j0 + lane;
@@ -1682,9 +1713,9 @@ hipError_t launch_pms_serial(hipStream_t st, const PmsDev& d, int t0, int t1) {
     return hipGetLastError();
 }
 
-hipError_t launch_pms_prop_one(hipStream_t st, const PmsDev& d, int t, int deg) {
-    if (deg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pms_prop_one, dim3(blocks((size_t)deg, 256)), dim3(256), 0, st, d, t);
+
+hipError_t launch_pms_prop_tree(hipStream_t st, const PmsDev& d, int t) {
+    hipLaunchKernelGGL(k_pms_prop_tree, dim3(1), dim3(256), 0, st, d, t);
     return hipGetLastError();
 }
 
