@@ -440,6 +440,7 @@ def main():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
         accumulate(kacc, c)
 
+    clk0 = (time.clock_gettime_ns(time.CLOCK_BOOTTIME), time.monotonic_ns())
     t0 = time.perf_counter()
     # frame groups: the timed region is args.steps frames of the stream; group fg takes frames fg, fg+G, ...
     my_steps = len(range(plan["fgroup"], args.steps, plan["fgroups"]))
@@ -448,6 +449,11 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    clk1 = (time.clock_gettime_ns(time.CLOCK_BOOTTIME), time.monotonic_ns())
+    # the timed region's clock span on stderr: tools/timed_region.py picks this region's launches out of
+    # a rocprofv3 kernel trace of the same command (its timestamps are one of these two clocks)
+    print("# timed region rank %d boottime_ns %d %d monotonic_ns %d %d" % (rank, clk0[0], clk1[0], clk0[1], clk1[1]),
+          file=sys.stderr, flush=True)
     # diagnostic pass, one frame at a time: every family timed (kernels_ms_per_step, tree_filter,
     # roofline.isolated) and the single-frame latency
     for c in ctxs:

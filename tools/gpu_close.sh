@@ -15,7 +15,7 @@ if [ "$2" != "skip-tests" ]; then
   tail -1 $O/tests_gpu.log
 fi
 bash tools/gpu_prof_round.sh $TAG || exit 3
-python3 -c "import json;d=json.loads(open('$O/bench_default.log').read().strip().splitlines()[-1]);print('default', round(d['ms_per_step'],3), 'frac', round(d['roofline']['frac'],3), 'same_build', d['roofline'].get('traffic_src',{}).get('same_build'))" || true
+python3 -c "import json;d=json.loads(open('$O/bench_default.log').read().strip().splitlines()[-1]);print('default', round(d['ms_per_step'],3), 'frac', round(d['roofline']['frac'],3), 'same_build', d['roofline'].get('traffic_source',{}).get('same_build'))" || true
 timeout -k 10 300 python tools/pms_bench.py 1920 1200 128 100 --reps 2 > $O/pms100.log 2>&1 || exit 4
 tail -1 $O/pms100.log | cut -c1-200
 timeout -k 10 300 python bench.py --disp 256 --steps 20 --warmup 5 --no-cpu --no-host-io --no-pms --no-segment > $O/c4_1gpu.log 2>&1 || exit 6
