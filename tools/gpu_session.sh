@@ -1,17 +1,17 @@
 # One GPU session (edited per session; logs under gpurun_out/s/)
-# This session: the up chain's per-launch spans and the chain wave's wait / compute split at C2, from
-# prebuilt diagnostic libraries (variants/ct: -DSM_CHAIN_TIMES, variants/prof: -DSM_CHAIN_PROF).
+# This session: the up chain's next-half reads pinned ahead of the recurrence by a scheduling barrier
+# (-DSM_UP_SB), with two or three register sets (-DSM_UP_PIPE3): chain-wave cycles (prof builds), the GPU
+# parity suite through the SB builds, an interleaved C2 A/B and the N = 8 share against the in-tree build.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/s
-SM_LIB=$GRAFT_REPO_ROOT/variants/ct/libstereomst.so timeout -k 10 300 python tools/chain_prof_run.py > gpurun_out/s/chain_times.log 2>&1 || exit 2
-python tools/chain_times.py gpurun_out/s/chain_times.log > gpurun_out/s/chain_times.txt || exit 3
-grep -E "total span|repair|wait" gpurun_out/s/chain_times.txt
-SM_LIB=$GRAFT_REPO_ROOT/variants/prof/libstereomst.so timeout -k 10 300 python tools/chain_prof_run.py > gpurun_out/s/chain_prof.log 2>&1 || exit 4
-grep -E "^up chain" gpurun_out/s/chain_prof.log | sort -t' ' -k6 -n -r | head -12 || true
-# the driver's bench command under a kernel trace: the timed region's launches against the line's HIP events
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/s/drv -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/s/drv_bench.log 2>&1 || exit 5
-python tools/timed_region.py gpurun_out/s/drv/run_kernel_trace.csv gpurun_out/s/drv_bench.log > gpurun_out/s/timed_region.txt 2>&1 || exit 6
-grep -h '^{' gpurun_out/s/drv_bench.log | python3 -c "import json,sys;d=json.loads(sys.stdin.read());r=d['roofline'];print('same run: %.3f ms/frame, HIP events: %s avg %.1f us' % (d['ms_per_step'], r['kernel'], r['avg_launch_ms'] * 1e3))" >> gpurun_out/s/timed_region.txt || true
-cat gpurun_out/s/timed_region.txt
-rm -f gpurun_out/s/drv/run_kernel_trace.csv.gz
+V=$GRAFT_REPO_ROOT/variants
+for v in prof sbp p3sbp; do
+  SM_LIB=$V/$v/libstereomst.so timeout -k 10 300 python tools/chain_prof_run.py > gpurun_out/s/cp_$v.log 2>&1 || exit 2
+  echo "== $v"; grep -E "^up chain" gpurun_out/s/cp_$v.log | sort -t' ' -k6 -n -r | head -3 || true
+done
+for v in sb p3sb; do
+  SM_LIB=$V/$v/libstereomst.so timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/s/tests_$v.log 2>&1; rc=$?; tail -1 gpurun_out/s/tests_$v.log; [ $rc -eq 0 ] || exit 7
+done
+REPS=2 bash tools/gpu_ab.sh "base||" "sb|SM_LIB=$V/sb/libstereomst.so|" "p3sb|SM_LIB=$V/p3sb/libstereomst.so|" || exit 3
+REPS=1 bash tools/gpu_ab.sh "e8base||--emulate-rank 0/8 --frame-groups 1" "e8sb|SM_LIB=$V/sb/libstereomst.so|--emulate-rank 0/8 --frame-groups 1" "e8p3sb|SM_LIB=$V/p3sb/libstereomst.so|--emulate-rank 0/8 --frame-groups 1" || exit 4
