@@ -228,6 +228,10 @@ __global__ __launch_bounds__(256) void k_up_walk(WalkView V0, WalkView V1, const
                                                  const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
                                                  int W, int Dpad, int dcall, int dglob0, const float* __restrict__ Cv0,
                                                  const float* __restrict__ Cv1, int ppw, int leaf_cost, UpPreArgs pa) {
+    // issue priority 1 (chain waves run at 3, everything else at 0): where a walker wave shares a SIMD
+    // with another frame's tree-stage waves, the filter's latency chains issue first.  Round 5, C2, 7
+    // interleaved pairs: 4.288 -> 4.257 ms/frame (priority 2: no gain); profiles/r05/walk_prio/
+    __builtin_amdgcn_s_setprio(1);
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
@@ -509,6 +513,7 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
                                                    const SmPath* __restrict__ paths1, const float* __restrict__ atab_g,
                                                    const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
                                                    int Dpad, WtaCfg w, int store_all, int ppw, int leaf_cost) {
+    __builtin_amdgcn_s_setprio(1);  // as k_up_walk
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
