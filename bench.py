@@ -613,7 +613,10 @@ def main():
         line["config"]["workload"] = "rank %d/%d of %dx%d D=%d: views %d, slices [%d, %d)" % (
             emu["rank"], emu["nranks"], W, H, Dtot_frame, views, dbeg, dbeg + Dloc)
     if rank == 0 and world == 1 and not args.no_segment and not emu and not seg_mode and args.aggregator == "tree":
-        line["segment"] = segment_leg(ctxs, left, right, Dloc, max(args.steps, 12), args.warmup)
+        # 6 frames in flight where they fit (the same ~200 GB budget as the main leg: a C3-size pair
+        # needs ~85 GB per context, so the batch line's segment leg keeps 2)
+        seg_inflight = max(1, min(6, int(200.0 // per_ctx_gb)))
+        line["segment"] = segment_leg(ctxs, left, right, Dloc, max(args.steps, 12), args.warmup, inflight=seg_inflight)
     if rank == 0 and world == 1 and not args.no_cpu and not emu:
         line["cpu_baseline"] = cpu_baseline(W, H, Dtot_frame)
     if rank == 0 and world == 1 and not args.no_pms and not emu and args.aggregator == "tree":
