@@ -207,6 +207,11 @@ def segment_leg(ctxs, left, right, D, steps, warmup, c=5000.0, min_size=200, inf
                      % (c, min_size, steps, len(cs)))
 
 
+def sm_environment():
+    """Every SM_* variable of this process's environment (recorded in the line; refused without --dev)."""
+    return {k: v for k, v in os.environ.items() if k.startswith("SM_")}
+
+
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -340,7 +345,18 @@ def main():
                     help="skip the segment-mode leg (Stereo3DMST's own forest, reported beside the MST metric)")
     ap.add_argument("--pms-iters", type=int, default=100,
                     help="MST_PMS calls per view in the PMS timing leg (the reference's 100, Stereo3DMST.cpp:854)")
+    ap.add_argument("--dev", action="store_true",
+                    help="allow SM_* environment variables (a dev library through SM_LIB, tools' A/B runs): the line "
+                         "then records them and is marked headline: false")
     args = ap.parse_args()
+    sm_env = sm_environment()
+    if sm_env and not args.dev:
+        # the product library reads no environment variable, but a dev build (SM_LIB) does, and its
+        # experiment switches can skip work: a headline is never printed with any of them set
+        print("bench.py: refusing to print a headline with SM_* variables set (%s); unset them, or pass --dev "
+              "for a line marked headline: false" % ", ".join("%s=%s" % kv for kv in sorted(sm_env.items())),
+              file=sys.stderr)
+        sys.exit(2)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
@@ -602,6 +618,8 @@ def main():
         "latency_ms_per_frame": min(lat),
         "frames_in_flight": inflight,
         "host_io": host_io,
+        "env": sm_env,
+        "headline": not sm_env,
     }
     if emu:
         line["emulated_rank"] = dict(emu, note="one rank's share of an N-rank strong-mode frame on one GPU, no "

@@ -21,7 +21,8 @@
  *   sm_start_timer/sm_get_timer_ms <- startTimer/getTimer         src/Stereo3DMST.cpp:15-26
  *   SM_AGG_PMS, sm_download_labels <- MST_PMS label search + abc_map  src/Stereo3DMST.cpp:546-629, 851-889
  *
- * Threading: one sm_ctx per host thread; no global mutable state in the library.
+ * Threading: one sm_ctx per host thread; the only global mutable state is the knob table
+ * (sm_set_knob), which tests set between calls.
  * All calls are synchronous w.r.t. the host unless named *_async.
  */
 #ifndef STEREOMST_H
@@ -281,6 +282,17 @@ sm_status sm_comm_destroy(sm_ctx* ctx);
 /* Timers (reference startTimer/getTimer semantics, but per call site, no global). */
 void sm_start_timer(double* t0);
 double sm_get_timer_ms(const double* t0);
+
+/* Tuning / diagnostic knobs (test and tool hook; no reference counterpart).  Schedule knobs never
+ * change a result (every engine is exact under any schedule: piece lengths, repair caps, launch
+ * schedules of the segmentation and MST); diagnostic knobs print or count; SM_TEST_PMS_CYCLE is
+ * the MST_PMS forest test's fault injection.  The library reads knobs only from this process-wide
+ * table, never from the environment (builds with -DSM_DEV excepted).  value: decimal string, or
+ * NULL to restore the default.  Set knobs between calls, not while one is running.  Returns
+ * SM_ERR_ARG for a name that is not a knob; sm_knob_names lists them (returns the count, writes
+ * at most cap names). */
+sm_status sm_set_knob(const char* name, const char* value);
+int sm_knob_names(const char** out, int cap);
 
 #ifdef __cplusplus
 }

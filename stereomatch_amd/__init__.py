@@ -15,7 +15,8 @@ import os
 import numpy as np
 
 from ._lib import (SM_AGG_GUIDED, SM_AGG_PMS, SM_AGG_TREE, SM_COST_AGD, SM_COST_VOLUME, SM_POST_LABEL_TO_DISP, SM_POST_LR_CHECK, SM_POST_LR_FILL,  # noqa: F401
-                   SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO, SM_POST_SUBPIXEL, Context, StereoMSTError, default_params, device_count, lib)
+                   SM_POST_OCCLUSION, SM_POST_OCCLUSION_ZERO, SM_POST_SUBPIXEL, Context, StereoMSTError, default_params, device_count, lib,
+                   knob_names, set_knob)
 
 # stereo3dmst's output step: LabelToDisp + *= (Dmax-1) on both maps, then the fill-less L-R check of
 # the left map (Stereo3DMST.cpp:189-201, 900-904)

@@ -119,6 +119,8 @@ def lib():
         "sm_comm_destroy": ([vp], ci),
         "sm_start_timer": ([ctypes.POINTER(ctypes.c_double)], None),
         "sm_get_timer_ms": ([ctypes.POINTER(ctypes.c_double)], ctypes.c_double),
+        "sm_set_knob": ([ctypes.c_char_p, ctypes.c_char_p], ci),
+        "sm_knob_names": ([ctypes.POINTER(ctypes.c_char_p), ci], ci),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -126,6 +128,21 @@ def lib():
         f.restype = res
     _lib = L
     return L
+
+
+def set_knob(name, value):
+    """sm_set_knob: a tuning / diagnostic knob of the library (include/stereomst.h); value None restores
+    the default.  Knobs are never read from the environment by the product library."""
+    st = lib().sm_set_knob(name.encode(), None if value is None else str(value).encode())
+    if st != SM_OK:
+        raise StereoMSTError(st, "sm_set_knob(%s): not a knob" % name)
+
+
+def knob_names():
+    n = lib().sm_knob_names(None, 0)
+    buf = (ctypes.c_char_p * n)()
+    lib().sm_knob_names(buf, n)
+    return [buf[i].decode() for i in range(n)]
 
 
 def default_params(**overrides):

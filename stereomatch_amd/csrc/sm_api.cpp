@@ -29,6 +29,7 @@
 #include "sm_seg_gpu.h"
 #include "sm_segment.h"
 #include "sm_tables.inc"
+#include "sm_knob.h"
 
 hipError_t launch_cand(hipStream_t st, const double* minc, const double* gmin, const int32_t* idx, int32_t* cand, size_t N);
 hipError_t launch_finalize(hipStream_t st, const double* gmin, const int32_t* gidx, double* minc, int32_t* idx, float* disp,
@@ -274,7 +275,7 @@ int spl_for(int D) { return D <= 64 ? 1 : D <= 128 ? 2 : 4; }
 // row length of a call of D slices: 64 * SPL, or 32 for D <= 32 (a 32-slice shard moves 32-slice
 // rows; SM_NO_DPAD32=1 restores 64 for A/B)
 int dpad_for(int D) {
-    static const bool off = getenv("SM_NO_DPAD32") != nullptr;
+    static const bool off = sm_dev_knob("SM_NO_DPAD32") != nullptr;
     return (D <= 32 && !off) ? 32 : 64 * spl_for(D);
 }
 
@@ -471,23 +472,23 @@ sm_status segment_upload(sm_ctx* ctx, int views) {
 }
 
 // SM_SEG_HOST=1: segment mode's segmentation by the host sweep (sm_segment.cpp) instead of the GPU
-bool seg_host() { return getenv("SM_SEG_HOST") != nullptr; }
+bool seg_host() { return sm_knob("SM_SEG_HOST") != nullptr; }
 
 // SM_SEG_FLATTEN: bit 0: point every pixel at its root before each run of one-workgroup buckets (default),
 // bit 1: before each whole-GPU bucket as well; 0: never
-int seg_flatten() { return getenv("SM_SEG_FLATTEN") ? atoi(getenv("SM_SEG_FLATTEN")) : 1; }
+int seg_flatten() { return sm_knob("SM_SEG_FLATTEN") ? atoi(sm_knob("SM_SEG_FLATTEN")) : 1; }
 
 // a small-bucket run starts with k_seg_split (SM_SEG_NOSPLIT=1: every edge of the run through k_seg_small)
-bool seg_split() { return getenv("SM_SEG_NOSPLIT") == nullptr; }
+bool seg_split() { return sm_knob("SM_SEG_NOSPLIT") == nullptr; }
 
 // Boruvka rounds launched over the whole GPU before a bucket's single-workgroup tail, for buckets of
 // more than SM_SEG_SMALL edges (env SM_SEG_GLOBAL_ROUNDS, default 3: the LDS tail then gets the ~2.7k
 // still-crossing candidates at most; latency 9.96 -> 9.7 ms, profiles/r04/seg/r04ao/)
-int seg_global_rounds() { return getenv("SM_SEG_GLOBAL_ROUNDS") ? atoi(getenv("SM_SEG_GLOBAL_ROUNDS")) : 3; }
+int seg_global_rounds() { return sm_knob("SM_SEG_GLOBAL_ROUNDS") ? atoi(sm_knob("SM_SEG_GLOBAL_ROUNDS")) : 3; }
 
 // buckets of at most this many edges run in one workgroup, consecutive ones in one launch (k_seg_small;
 // env SM_SEG_SMALL, default 16384)
-uint32_t seg_small() { return getenv("SM_SEG_SMALL") ? (uint32_t)atoi(getenv("SM_SEG_SMALL")) : 16384u; }
+uint32_t seg_small() { return sm_knob("SM_SEG_SMALL") ? (uint32_t)atoi(sm_knob("SM_SEG_SMALL")) : 16384u; }
 
 // the hashed pair dedupe's kept candidates (unordered) into the merge's (w, id) order: LSD radix sort of the
 // key (w << 32) | id in four 11-bit digits (w < 2^10, id < 2^23 for images below 4.19 M pixels; the full
@@ -568,7 +569,7 @@ double now_ms();
 // the min-size candidates (twice).  With host_copy the weights, masks and layout weights are copied to
 // the h_w / h_m / h_fw host arrays as well (MST_PMS, sm_build_tree_p).
 sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_copy) {
-    static const bool dbg = getenv("SM_SEG_DEBUG") != nullptr;
+    const bool dbg = sm_knob("SM_SEG_DEBUG") != nullptr;
     const int flatten = seg_flatten();
     const double t0 = dbg ? now_ms() : 0.0;
     double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
@@ -722,7 +723,7 @@ sm_status segment_gpu(sm_ctx* ctx, int views, float c, int min_size, bool host_c
     if (dbg) t2 = now_ms();
     HIPC(hipStreamSynchronize(st));
     if (dbg) t3 = now_ms();
-    if (getenv("SM_SEG_PROF")) {  // k_seg_small's timings (sm_seg_gpu.hip SEG_PROF_SLOT): prologue, then per bucket
+    if (sm_knob("SM_SEG_PROF")) {  // k_seg_small's timings (sm_seg_gpu.hip SEG_PROF_SLOT): prologue, then per bucket
         for (int i = 0; i < vs.n; ++i) {
             std::vector<uint32_t> pr(2 + SM_SEG_NB);
             HIPC(hipMemcpy(pr.data(), P<uint32_t>(ctx->sg[vs.v[i]].cnt) + SM_SEG_C_LIST + 60000, pr.size() * 4,
@@ -861,7 +862,7 @@ sm_status stage_segment(sm_ctx* ctx, int views, float c, int min_size, bool host
 
 // SM_SEG_SYNC=1: segment mode's host segmentation inside sm_match_begin (A/B of the worker thread)
 bool seg_sync() {
-    static const bool s = getenv("SM_SEG_SYNC") != nullptr;
+    static const bool s = sm_dev_knob("SM_SEG_SYNC") != nullptr;
     return s;
 }
 
@@ -906,7 +907,7 @@ sm_status stage_mst(sm_ctx* ctx, int views) {
     HIPC(launch_zero(ctx->st, z));
     a.flags[0] = P<int>(ctx->changed);
     a.flags[1] = P<int>(ctx->changed) + SM_MST_MAX_ROUNDS;
-    const bool pixel_rounds = getenv("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B path (tests, tools)
+    const bool pixel_rounds = sm_knob("SM_MST_PIXEL_ROUNDS") != nullptr;  // A/B path (tests, tools)
     {
         uint32_t* cc[2] = {nullptr, nullptr};
         uint32_t* cl[2] = {nullptr, nullptr};
@@ -958,7 +959,7 @@ sm_status stage_mst(sm_ctx* ctx, int views) {
     // checked after the layout's own synchronisation (mst_finish).  Every kernel of round r exits
     // at once when round r-1 hooked nothing.
     const int first = std::min(std::max(ctx->mst_rounds, 2), SM_MST_MAX_ROUNDS);
-    static const bool dbg = getenv("SM_MST_DEBUG") != nullptr;
+    const bool dbg = sm_knob("SM_MST_DEBUG") != nullptr;
     int r = 0;
     for (; r < first; ++r) {
         HIPC(launch_bor_cround(ctx->st, a, c, W, r));
@@ -1002,7 +1003,7 @@ sm_status mst_finish(sm_ctx* ctx, bool* grew) {
 
 // nodes per piece: SM_PIECE, or env SM_PIECE_LEN (multiple of SM_PRE_SEG, >= 64)
 int piece_len() {  // read per call: tests switch it between matches
-    const char* e = getenv("SM_PIECE_LEN");
+    const char* e = sm_knob("SM_PIECE_LEN");
     const int v = e ? atoi(e) : SM_PIECE;
     return (v >= 64 && v % SM_PRE_SEG == 0) ? v : SM_PIECE;
 }
@@ -1137,7 +1138,7 @@ sm_status stage_layout_finish(sm_ctx* ctx, int views) {
         L.piece_begin.assign(R + 6 * SM_NBUCKETS + 4, R + 7 * SM_NBUCKETS + 5);
         L.npaths = R[SM_NBUCKETS];
         if (L.nrounds == 0 || L.npaths == 0) return fail(ctx, SM_ERR_STATE, "layout produced no paths");
-        if (getenv("SM_LAYOUT_DEBUG"))  // per-round path statistics (tools/gpu_layout_dbg.sh)
+        if (sm_knob("SM_LAYOUT_DEBUG"))  // per-round path statistics (tools/gpu_layout_dbg.sh)
             for (uint32_t r = 0; r < L.nrounds; ++r)
                 fprintf(stderr, "view %d round %u: long %u paths %u nodes maxlen %u | short %u paths %u nodes maxlen %u\n", v, r,
                         L.begin[2 * r + 1] - L.begin[2 * r], L.nodes[2 * r], L.maxlen[2 * r], L.begin[2 * r + 2] - L.begin[2 * r + 1],
@@ -1172,7 +1173,7 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     return a;
 }
 
-bool no_pieces() { return getenv("SM_NO_PIECES") != nullptr; }
+bool no_pieces() { return sm_dev_knob("SM_NO_PIECES") != nullptr; }
 
 // capacity of the per-view piece arrays (<= N/32 long paths + N/SM_PIECE pieces)
 size_t piece_cap(size_t N) { return N / 16 + 64; }
@@ -1212,7 +1213,7 @@ void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int views
 // the bracketed launches and left the next kernel with cold caches.  Elapsed times are read after
 // a stream synchronisation, so nothing needs the fence.  SM_EVENT_FENCE=1: default events (A/B).
 static unsigned timing_event_flags() {
-    static const bool fence = getenv("SM_EVENT_FENCE") != nullptr;
+    static const bool fence = sm_dev_knob("SM_EVENT_FENCE") != nullptr;
     return fence ? hipEventDefault : hipEventDisableSystemFence;
 }
 
@@ -1248,7 +1249,7 @@ template <class F>
 sm_status timed(sm_ctx* ctx, hipStream_t s, int f, double vox, F&& launch, double acct = -1.0) {
     // vox: voxels of the launch (0: nothing to launch); acct: voxels its algorithmic bytes count
     // (default vox)
-    static const bool off = getenv("SM_NO_KTIMING") != nullptr;  // A/B: no events at all
+    static const bool off = sm_dev_knob("SM_NO_KTIMING") != nullptr;  // A/B: no events at all
     if (vox <= 0) return SM_OK;                                   // empty bucket: nothing to launch
     if (off || vox < SM_TIMED_MIN_VOX || !((ctx->ktiming >> f) & 1u)) {
         HIPC(launch());
@@ -1361,19 +1362,19 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
     a.pstride = (int)pcap;
     a.piece_len = piece_len();
     {
-        const char* e = getenv("SM_REPAIR_MAX");
+        const char* e = sm_knob("SM_REPAIR_MAX");
         a.repair_max = e ? std::max(1, atoi(e)) : 1 << 30;
     }
     a.err = ctx->d_err;
     {
-        const char* e = getenv("SM_WAIT_ITERS");  // read per call: the forced-timeout test lowers it
+        const char* e = sm_knob("SM_WAIT_ITERS");  // read per call: the forced-timeout test lowers it
         a.wait_iters = e ? std::max(0, atoi(e)) : 1 << 24;
     }
     a.piece_dbg = nullptr;
-    if (getenv("SM_PIECE_DEBUG")) {  // per-call repair statistics on stderr (tools)
+    if (sm_knob("SM_PIECE_DEBUG")) {  // per-call repair statistics on stderr (tools)
         CHECK(ensure(ctx, ctx->pdbg, 128));
         HIPC(hipMemsetAsync(ctx->pdbg.p, 0, 128, ctx->st));
-        if (atoi(getenv("SM_PIECE_DEBUG")) == 2) {
+        if (atoi(sm_knob("SM_PIECE_DEBUG")) == 2) {
             const unsigned long long one = 1;
             HIPC(hipMemcpyAsync(P<unsigned long long>(ctx->pdbg) + 15, &one, 8, hipMemcpyHostToDevice, ctx->st));
             HIPC(hipStreamSynchronize(ctx->st));
@@ -1412,7 +1413,7 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int views, bool debug_sto
     if (wta) a.wta = *wta;
     CHECK(setup_sync(ctx, a, N, Dpad));
     a.vol = ctx->use_vol ? 1 : 0;
-    a.leaf_cost = (!a.vol && !debug_store_all && !getenv("SM_NO_LEAF_COST")) ? 1 : 0;  // SM_NO_LEAF_COST: A/B
+    a.leaf_cost = (!a.vol && !debug_store_all && !sm_knob("SM_NO_LEAF_COST")) ? 1 : 0;  // SM_NO_LEAF_COST: A/B
     if (a.vol)  // cost rows of every slot from the caller's volumes (slots come from the layout)
         for (int v = 0; v < 2; ++v)
             if (view_on(views, v))
@@ -1605,11 +1606,11 @@ sm_status upload_vec(sm_ctx* ctx, DevBuf& b, const std::vector<T>& v) {
 // SM_PMS_SERIAL=1: every MST_PMS call in serial mode (tests compare the two modes); SM_PMS_MAX_ROUNDS:
 // speculative passes per call before the rest of the call runs serially
 bool pms_serial_only() {
-    const char* e = getenv("SM_PMS_SERIAL");
+    const char* e = sm_knob("SM_PMS_SERIAL");
     return e && atoi(e) == 1;
 }
 int pms_max_rounds() {
-    const char* e = getenv("SM_PMS_MAX_ROUNDS");
+    const char* e = sm_knob("SM_PMS_MAX_ROUNDS");
     return e ? std::max(1, atoi(e)) : 8;
 }
 
@@ -1746,7 +1747,7 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
     d.err = ctx->d_err + 1 + v;  // a word per view: the views' calls run concurrently (h_err[1 + v])
     d.prof = nullptr;
     d.evals = nullptr;
-    if (getenv("SM_PMS_PROF")) {  // diagnostics: serial-kernel segment times, printed per call
+    if (sm_knob("SM_PMS_PROF")) {  // diagnostics: serial-kernel segment times, printed per call
         if (ensure(ctx, S.prof, 16 * 8) == SM_OK) d.prof = P<long long>(S.prof);
     }
     d.slut = P<double>(ctx->slut);
@@ -1776,7 +1777,7 @@ PmsDev pms_dev(sm_ctx* ctx, int v, int D) {
 // MST_PMS pieces: heavy paths of at least 2 x this many rows are cut (SM_PMS_PIECE; 0: none).  512
 // balances a piece's walk against the repairs of the pieces above it (~30-60 rows each at C2).
 int pms_piece() {
-    const char* e = getenv("SM_PMS_PIECE");
+    const char* e = sm_knob("SM_PMS_PIECE");
     return e ? std::max(0, atoi(e)) : 512;
 }
 
@@ -1785,7 +1786,7 @@ int pms_piece() {
 // call per view (tools/pms_bench.py): 32768 -> 376 ms, 8192 -> 278, 2048 -> 229, 1024 -> 223, 512 ->
 // 221, 128 -> 226 ms.
 long long pms_big_tree() {
-    const char* e = getenv("SM_PMS_BIG");
+    const char* e = sm_knob("SM_PMS_BIG");
     return e ? std::max(1ll, atoll(e)) : 1024;
 }
 
@@ -1822,7 +1823,7 @@ sm_status pms_phase(sm_ctx* ctx, hipStream_t st, int v, const PmsDev& d0, int ph
         }
         // SM_PMS_CHAIN_MIN: the chain threshold (at least SM_PMS_CHAIN_LEN, whose counts bound the grid;
         // tests lower it to put more chain items on small images)
-        const char* cm = getenv("SM_PMS_CHAIN_MIN");
+        const char* cm = sm_knob("SM_PMS_CHAIN_MIN");
         HIPC(launch_pms_plan(st, d, phase, t_lo, t_hi, R, maxp, cm ? atoi(cm) : SM_PMS_CHAIN_DEFAULT, true));
     }
     // pieces: every guessed piece repairs at once, then a gated sequential pass; maxp[r] = the most pieces
@@ -2178,8 +2179,8 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     // the schedule forests are built on the GPU (sm_pms_forest.hip) from the device masks;
     // SM_PMS_HOST_FOREST=1: on host threads (pms_build_forest, A/B); SM_PMS_FOREST_CHECK=1 (tests): both,
     // compared array by array
-    const bool host_forest = getenv("SM_PMS_HOST_FOREST") && atoi(getenv("SM_PMS_HOST_FOREST")) == 1;
-    const bool forest_check = getenv("SM_PMS_FOREST_CHECK") && atoi(getenv("SM_PMS_FOREST_CHECK")) == 1;
+    const bool host_forest = sm_knob("SM_PMS_HOST_FOREST") && atoi(sm_knob("SM_PMS_HOST_FOREST")) == 1;
+    const bool forest_check = sm_knob("SM_PMS_FOREST_CHECK") && atoi(sm_knob("SM_PMS_FOREST_CHECK")) == 1;
     const sm_status seg_st = stage_segment(ctx, 3, p->c, p->min_size, host_forest || forest_check);
     if (seg_st != SM_OK) {
         skip.join();
@@ -2309,8 +2310,8 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     run[1].h_res = ctx->h_pms_res + 4;
     const size_t roff0[2] = {0, (size_t)iters * K0};
     // evaluations the device ran (speculation and repeats included): a diagnostic, SM_PMS_COUNT_RUN=1
-    static const bool count_run = getenv("SM_PMS_COUNT_RUN") && atoi(getenv("SM_PMS_COUNT_RUN")) == 1;
-    auto calls = [ctx, D, iters, serial_only, &roff0](PmsRun& r, int v) -> sm_status {
+    const bool count_run = sm_knob("SM_PMS_COUNT_RUN") && atoi(sm_knob("SM_PMS_COUNT_RUN")) == 1;
+    auto calls = [ctx, D, iters, serial_only, count_run, &roff0](PmsRun& r, int v) -> sm_status {
         HIPC(hipSetDevice(ctx->device));
         const hipStream_t st = r.st;
         PmsDev d = pms_dev(ctx, v, D);
@@ -2327,7 +2328,7 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
             if (d.prof) HIPC(hipMemsetAsync(d.prof, 0, 16 * 8, st));
             if (i == 0 || serial_only) {
                 HIPC(hipMemsetAsync(ctx->pms[v].off.p, 0, 16, st));
-                static const bool tree_times = getenv("SM_PMS_TREE_TIMES") != nullptr;  // diagnostics (tools)
+                const bool tree_times = sm_knob("SM_PMS_TREE_TIMES") != nullptr;  // diagnostics (tools)
                 if (tree_times && i == 0) {
                     std::vector<hipEvent_t> ev(K + 1);
                     for (auto& e : ev) HIPC(hipEventCreate(&e));
@@ -2434,6 +2435,16 @@ sm_status stage_pms(sm_ctx* ctx, int D, const sm_params* p) {
     ctx->pms_last = true;
     ctx->pms_W = W;
     ctx->pms_H = H;
+    return SM_OK;
+}
+
+// the tree layout packs preorder positions in 27 bits (sm_layout_gpu.hip): every tree-based call
+// (MST, segment forest, MST_PMS) refuses images of 2^27 pixels or more with its other argument checks,
+// before anything is uploaded or allocated (stage_layout_enqueue keeps its own check as a backstop)
+sm_status check_tree_size(sm_ctx* ctx, long long W, long long H, const sm_params* p) {
+    if (p && p->aggregator == SM_AGG_GUIDED) return SM_OK;
+    if (W > 0 && H > 0 && W * H >= (1ll << 27))
+        return fail(ctx, SM_ERR_ARG, "images of 2^27 pixels or more are not supported by the tree layout");
     return SM_OK;
 }
 
@@ -2670,6 +2681,7 @@ static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
     if (ctx->seg_worker.joinable()) ctx->seg_worker.join();  // a worker left by a failed finish
     if (ctx->W == 0) return fail(ctx, SM_ERR_STATE, "no images uploaded");
     CHECK(check_params(ctx, p, D));
+    CHECK(check_tree_size(ctx, ctx->W, ctx->H, p));
     const CallRange cr = call_range(p, D);
     ctx->use_vol = p->cost_kind == SM_COST_VOLUME;
     ctx->views = p->views == 0 ? 3 : p->views;
@@ -2681,12 +2693,13 @@ static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
     HIPC(hipSetDevice(ctx->device));
     ctx->rec_pad = rec_pad_for(cr.d0, cr.D);
     ctx->sub = cr.w.sub != 0;
+#ifdef SM_DEV  // (compiled out of product builds: these skip work)
     // timing experiments only (tools): with a layout of these images from an earlier frame,
     // SM_EXP_FILTER_ONLY=1 re-filters it without re-running prep / MST / layout (the filter's streaming
     // cost alone); SM_EXP_SKIP=mst keeps the previous MST (prep + layout + filter), SM_EXP_SKIP=layout
     // keeps the previous layout (prep + MST + filter): the tree stages' streaming cost, stage by stage
-    static const bool exp_filter_only = getenv("SM_EXP_FILTER_ONLY") != nullptr;
-    static const int exp_skip = getenv("SM_EXP_SKIP") ? (strcmp(getenv("SM_EXP_SKIP"), "mst") == 0 ? 1 : 2) : 0;
+    static const bool exp_filter_only = sm_dev_knob("SM_EXP_FILTER_ONLY") != nullptr;
+    static const int exp_skip = sm_dev_knob("SM_EXP_SKIP") ? (strcmp(sm_dev_knob("SM_EXP_SKIP"), "mst") == 0 ? 1 : 2) : 0;
     const bool exp_on = ctx->exp_layout_ok && p->aggregator == SM_AGG_TREE && std::isinf(p->c);
     if (exp_on && exp_skip) {
         HIPC(hipEventRecord(ctx->ev[0], ctx->st));
@@ -2712,6 +2725,7 @@ static sm_status match_begin_impl(sm_ctx* ctx, int D, const sm_params* p) {
         ctx->pend_p = *p;
         return SM_OK;
     }
+#endif
     HIPC(hipEventRecord(ctx->ev[0], ctx->st));
     CHECK(stage_prep(ctx));
     HIPC(hipEventRecord(ctx->ev[1], ctx->st));
@@ -2868,6 +2882,9 @@ sm_status sm_download_results(sm_ctx* ctx, float* ld, float* rd, int32_t* li, in
 
 sm_status sm_match(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, int stride, int D, const sm_params* p,
                    float* ld, float* rd, int32_t* li, int32_t* ri, double* lm, double* rm) {
+    if (!ctx) return SM_ERR_ARG;
+    if (!p) return fail(ctx, SM_ERR_ARG, "null params");
+    CHECK(check_tree_size(ctx, W, H, p));
     CHECK(sm_upload_images(ctx, l, r, W, H, stride));
     CHECK(sm_match_async(ctx, D, p));
     CHECK(sm_synchronize(ctx));
@@ -2898,6 +2915,7 @@ sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int str
     if (!ctx) return SM_ERR_ARG;
     if (ctx->pending) return fail(ctx, SM_ERR_STATE, "sm_build_tree_p: a call begun with sm_match_begin is not finished (sm_match_finish)");
     if (p && (std::isnan(p->c) || p->c < 0)) return fail(ctx, SM_ERR_ARG, "c must be >= 0 or +INFINITY");
+    CHECK(check_tree_size(ctx, W, H, nullptr));
     HIPC(hipSetDevice(ctx->device));
     CHECK(upload(ctx, bgr, bgr, W, H, stride));
     CHECK(stage_prep(ctx));
@@ -2955,6 +2973,7 @@ sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, 
     if (view != 0 && view != 1) return fail(ctx, SM_ERR_ARG, "view must be 0 or 1");
     ctx->use_vol = false;  // AGD costs
     if (D < 1 || D > 256 || d0 < 0 || d0 > (1 << 20)) return fail(ctx, SM_ERR_ARG, "bad disparity range");
+    CHECK(check_tree_size(ctx, W, H, nullptr));
     HIPC(hipSetDevice(ctx->device));
     ctx->rec_pad = rec_pad_for(d0, D);
     CHECK(upload(ctx, l, r, W, H, stride));

@@ -26,6 +26,7 @@
 #include <algorithm>
 
 #include "sm_launch.h"
+#include "sm_knob.h"
 
 #define GF_BLOCK 32
 
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(256) void k_gf_box2_q_wta(const float4* __restrict_
         }
 }
 
-bool gf_fused(int r) { return r == 9 && getenv("SM_GF_UNFUSED") == nullptr; }  // read per call: tests toggle it
+bool gf_fused(int r) { return r == 9 && sm_knob("SM_GF_UNFUSED") == nullptr; }  // read per call: tests toggle it
 
 size_t gf_band_plane(int W, int H) { return (size_t)((H + 31) / 32) * 32 * W; }
 
@@ -618,7 +619,7 @@ static hipError_t launch_gf_batch_fused(hipStream_t st, const float* cost, const
     const int nty = (H + 31) / 32, ntx = (W + 31) / 32;
     const size_t NS = gf_band_plane(W, H);
     float4* ab = reinterpret_cast<float4*>(pl);  // [S][NS] float4, row band layout
-    const char* e = getenv("SM_GF_DBG");  // timing probes only (wrong results): 2 no y pass, 4 no epilogue
+    const char* e = sm_dev_knob("SM_GF_DBG");  // timing probes only (wrong results): 2 no y pass, 4 no epilogue
     const int dbg = e ? atoi(e) : 0;
     const int ntiles = ntx * nty;  // one workgroup per 32 x 32 tile, looping over the batch's slices
     hipLaunchKernelGGL((k_gf_box1_ab<RR>), dim3((ntiles + 7) & ~7), dim3(256), 0, st, cost, bgrx, stats, ab, W, H, N, NS, S,
@@ -642,7 +643,7 @@ static void box(hipStream_t st, const float* in, float* tmp, float* out, int W, 
     if (rows < 1) rows = 1;
     while (rows > 1 && (size_t)2 * rows * (W + nblk) * 4 > 65536) --rows;
     const size_t lds = (size_t)2 * rows * (W + nblk) * 4;
-    if (lds <= 65536 && getenv("SM_GF_DIRECT_X") == nullptr)
+    if (lds <= 65536 && sm_knob("SM_GF_DIRECT_X") == nullptr)
         hipLaunchKernelGGL(k_gf_box_x_lds, dim3((H + rows - 1) / rows, planes), dim3(256), lds, st, in, tmp, W, H, r, N, rows);
     else
         hipLaunchKernelGGL(k_gf_box_x, dim3((H + 63) / 64, nblk, planes), dim3(64), 0, st, in, tmp, W, H, r, N);

@@ -836,6 +836,7 @@ __global__ void k_rows_to_volume(const SmMeta* __restrict__ meta, const double* 
 // ---------------------------------------------------------------------------------------------
 #include <cstdlib>
 #include "sm_launch.h"
+#include "sm_knob.h"
 
 hipError_t launch_prep(hipStream_t st, const uint8_t* l, const uint8_t* r, int W, int H, int stride, uint32_t* lb,
                        float* lg, uint32_t* rb, float* rg, uint2* lrec, uint2* rrec, uint32_t* lrec4, uint32_t* rrec4) {
@@ -871,7 +872,7 @@ hipError_t launch_bor_local(hipStream_t st, const MstArgs& a, int W, int H, uint
     dim3 g((W + BT - 1) / BT, (H + BT - 1) / BT, a.nviews);
     // Tile-phase Boruvka iterations: any cap is exact (unfinished components continue in the
     // contracted rounds); 4 is the measured optimum at C2 (tools/gpu_mst_sweep.sh).
-    const char* e = getenv("SM_MST_LOCAL_ITERS");
+    const char* e = sm_knob("SM_MST_LOCAL_ITERS");
     const int max_iter = e ? atoi(e) : 4;
     hipLaunchKernelGGL(k_bor_local, g, dim3(BTHREADS), 0, st, P, W, H, max_iter);
     return hipGetLastError();

@@ -23,6 +23,7 @@
 #include "sm_common.h"
 #include "sm_layout_gpu.h"
 #include "sm_tour.h"
+#include "sm_knob.h"
 
 #ifndef SM_RUN_DIV
 #define SM_RUN_DIV 384  // run window = bucket nodes / SM_RUN_DIV (~3 runs per CU, both views)
@@ -874,8 +875,8 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_newslot, dim3((N + 255) / 256, nviews), dim3(256), 0, st, LP, N);
     hipLaunchKernelGGL(k_meta, dim3(META_BLOCKS, nviews), dim3(256), 0, st, LP, W, H);
     // run sizing (A/B knobs: SM_RUN_DIV, SM_RUN_CAP = the window cap in nodes)
-    const char* ed = getenv("SM_RUN_DIV");
-    const char* ec = getenv("SM_RUN_CAP");
+    const char* ed = sm_dev_knob("SM_RUN_DIV");
+    const char* ec = sm_dev_knob("SM_RUN_CAP");
     const uint32_t rdiv = ed && atoi(ed) > 0 ? (uint32_t)atoi(ed) : (uint32_t)SM_RUN_DIV;
     const uint32_t rcap = ec && atoi(ec) >= 64 ? (uint32_t)atoi(ec) : piece_len;
     hipLaunchKernelGGL(k_long_segments, dim3(nviews), dim3(1024), 0, st, LP, piece_len, rdiv, rcap);

@@ -34,6 +34,7 @@
 #include <cstdlib>
 
 #include "sm_pms.h"
+#include "sm_knob.h"
 
 namespace {
 
@@ -1774,8 +1775,8 @@ hipError_t launch_pms_plan(hipStream_t st, const PmsDev& d, int phase, int t_lo,
 hipError_t launch_pms_chain(hipStream_t st, const PmsDev& d, int phase, bool up, int r, int items) {
     if (items <= 0) return hipSuccess;
     // SM_PMS_CHAIN_NSU / _NSD: ring slots of the up / down chain (LDS per workgroup, so workgroups per CU)
-    const char* eu = getenv("SM_PMS_CHAIN_NSU");
-    const char* ed = getenv("SM_PMS_CHAIN_NSD");
+    const char* eu = sm_knob("SM_PMS_CHAIN_NSU");
+    const char* ed = sm_knob("SM_PMS_CHAIN_NSD");
     const int nsu = eu ? std::min(std::max(atoi(eu), 1), PC_NSU_MAX) : PC_NSU;
     const int nsd = ed ? std::min(std::max(atoi(ed), 1), PC_NSD) : PC_NSD;
     const int ns = up ? nsu : nsd;

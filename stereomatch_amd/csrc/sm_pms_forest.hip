@@ -28,6 +28,7 @@
 #include "sm_pms_forest.h"
 #include "sm_segment.h"
 #include "sm_tour.h"
+#include "sm_knob.h"
 
 #define SM_VIRTUAL_W_PF SM_VIRTUAL_W
 
@@ -712,7 +713,7 @@ static int bits_for(int n) {
 
 hipError_t pf_trees(hipStream_t st, PfView& v, int* K_out) {
     const int N = v.N;
-    if (getenv("SM_TEST_PMS_CYCLE") && atoi(getenv("SM_TEST_PMS_CYCLE")) == 1)
+    if (sm_knob("SM_TEST_PMS_CYCLE") && atoi(sm_knob("SM_TEST_PMS_CYCLE")) == 1)
         hipLaunchKernelGGL(k_pf_test_cycle, dim3(1), dim3(64), 0, st, v);
     hipLaunchKernelGGL(k_pf_prep, dim3(nblk(N, 256)), dim3(256), 0, st, v);
     hipLaunchKernelGGL(k_pf_link, dim3(nblk(N, 256)), dim3(256), 0, st, v);

@@ -15,6 +15,7 @@
 // heads of paths one light depth deeper, so the up pass runs light depths deepest first and the down
 // pass root first, each depth one round of independent paths (DESIGN.md "MST_PMS").
 #include "sm_pms_host.h"
+#include "sm_knob.h"
 
 #include <algorithm>
 #include <atomic>
@@ -143,7 +144,7 @@ void parallel_for(int n, int nthreads, F&& fn) {
 }
 
 int pms_prep_threads() {
-    const char* e = getenv("SM_PREP_THREADS");
+    const char* e = sm_knob("SM_PREP_THREADS");
     if (e) return std::max(1, atoi(e));
     const unsigned hc = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(8u, hc / 2));  // two views build at once
@@ -160,7 +161,7 @@ int pms_build_forest(int W, int H, const uint16_t* wR, const uint16_t* wD, const
                      PmsForest& f, int piece, int nthreads) {
     const int N = W * H;
     if (nthreads <= 0) nthreads = pms_prep_threads();
-    static const bool dbg = getenv("SM_PREP_DEBUG") != nullptr;  // phase times on stderr (diagnostics)
+    const bool dbg = sm_knob("SM_PREP_DEBUG") != nullptr;  // phase times on stderr (diagnostics)
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double tp0 = dbg ? now() : 0.0;
     // 1. trees

@@ -29,6 +29,7 @@
 
 #include "sm_seg_gpu.h"
 #include "sm_segment.h"
+#include "sm_knob.h"
 
 namespace {
 
@@ -1189,8 +1190,8 @@ hipError_t seg_launch_round(hipStream_t st, const SegPair& p, uint32_t m, int li
 }
 
 hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t gen0) {
-    const int lds = getenv("SM_SEG_TAIL_GLOBAL") ? 0 : 1;
-    const uint32_t tmin = getenv("SM_SEG_TAIL_MIN") ? (uint32_t)atoi(getenv("SM_SEG_TAIL_MIN")) : SEG_TAIL_MIN;
+    const int lds = sm_knob("SM_SEG_TAIL_GLOBAL") ? 0 : 1;
+    const uint32_t tmin = sm_knob("SM_SEG_TAIL_MIN") ? (uint32_t)atoi(sm_knob("SM_SEG_TAIL_MIN")) : SEG_TAIL_MIN;
     hipLaunchKernelGGL(k_seg_tail, dim3(p.nv), dim3(1024), 0, st, p, lin, gen0, lds, tmin);
     return hipGetLastError();
 }
@@ -1198,10 +1199,10 @@ hipError_t seg_launch_tail(hipStream_t st, const SegPair& p, int lin, uint32_t g
 hipError_t seg_launch_small(hipStream_t st, const SegPair& p, int w0, int w1, float c, uint32_t gen0, bool split) {
     // SM_SEG_ACT_MAX: the most active edges bucketed in LDS (0: always the full scan; tests)
     const uint32_t lc = (uint32_t)SEG_LC;
-    const uint32_t amax = getenv("SM_SEG_ACT_MAX") ? (uint32_t)atoi(getenv("SM_SEG_ACT_MAX")) : (uint32_t)SEG_ACT_MAX;
-    const int prof = getenv("SM_SEG_PROF") ? 1 : 0;
+    const uint32_t amax = sm_knob("SM_SEG_ACT_MAX") ? (uint32_t)atoi(sm_knob("SM_SEG_ACT_MAX")) : (uint32_t)SEG_ACT_MAX;
+    const int prof = sm_knob("SM_SEG_PROF") ? 1 : 0;
     // SM_SEG_NORUN=1: no k_seg_run (every split run through k_seg_small)
-    if (split && !getenv("SM_SEG_NORUN")) hipLaunchKernelGGL(k_seg_run, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c);
+    if (split && !sm_knob("SM_SEG_NORUN")) hipLaunchKernelGGL(k_seg_run, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c);
     hipLaunchKernelGGL(k_seg_small, dim3(p.nv), dim3(1024), 0, st, p, w0, w1, c, gen0, lc, split ? 1 : 0, amax, prof);
     return hipGetLastError();
 }

@@ -26,6 +26,7 @@
 #include "sm_common.h"
 #include "sm_launch.h"
 #include "sm_walk_util.h"
+#include "sm_knob.h"
 
 // segment blocks of the fused up launch (up_pre_segment): 4 waves x CH x NSUB nodes
 #define UP_PRE_CH(SPL) ((SPL) == 4 ? 4 : 8)
@@ -803,7 +804,7 @@ static WalkView to_view(const WalkArgs& a, int v) {
 
 // A/B knob: extra dynamic LDS per block (limits walker occupancy; experiments only)
 static size_t walk_lds_pad() {
-    static const char* e = getenv("SM_WALK_LDS_PAD");
+    static const char* e = sm_dev_knob("SM_WALK_LDS_PAD");
     return e ? (size_t)atoi(e) : 0;
 }
 
@@ -813,11 +814,11 @@ static size_t walk_lds_pad() {
 // down walker (0: always the default).
 static int walk_ppw(int np, int dflt, bool down) {
     static const int fill_up = [] {
-        const char* e = getenv("SM_WALK_FILL");
+        const char* e = sm_dev_knob("SM_WALK_FILL");
         return e ? atoi(e) : 8192;
     }();
     static const int fill_dn = [] {
-        const char* e = getenv("SM_WALK_FILL_DN");
+        const char* e = sm_dev_knob("SM_WALK_FILL_DN");
         return e ? atoi(e) : 8192;
     }();
     const int fill = down ? fill_dn : fill_up;
@@ -850,7 +851,7 @@ static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all
 
 // SPL = 1 calls with 64-double rows take the half-wave walkers (env SM_NO_HALF_WAVE: A/B)
 static bool half_wave(const WalkArgs& a, int spl) {
-    static const bool off = getenv("SM_NO_HALF_WAVE") != nullptr;
+    static const bool off = sm_dev_knob("SM_NO_HALF_WAVE") != nullptr;
     return !off && spl == 1 && a.Dpad == 64;
 }
 

@@ -48,3 +48,33 @@ def gpu_ctx():
     ctx = sm.Context(0)
     yield ctx
     ctx.close()
+
+
+class Knobs:
+    """Library knobs (sm_set_knob) with monkeypatch's setenv / delenv surface; every knob set through it
+    is restored to its default when the test ends.  The product library never reads the environment."""
+
+    def __init__(self):
+        self.touched = set()
+
+    def setenv(self, name, value):
+        import stereomatch_amd as sm
+        sm.set_knob(name, value)
+        self.touched.add(name)
+
+    def delenv(self, name, raising=True):
+        import stereomatch_amd as sm
+        sm.set_knob(name, None)
+        self.touched.add(name)
+
+    def restore(self):
+        import stereomatch_amd as sm
+        for n in self.touched:
+            sm.set_knob(n, None)
+
+
+@pytest.fixture
+def knobs():
+    k = Knobs()
+    yield k
+    k.restore()

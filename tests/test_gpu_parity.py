@@ -55,15 +55,15 @@ def test_mst_matches_reference_segment_graph(gpu_ctx, name):
 
 @pytest.mark.parametrize("iters", ["0", "1", "64"])
 @pytest.mark.parametrize("pixel_rounds", [False, True])
-def test_mst_phase_split_exact(gpu_ctx, monkeypatch, iters, pixel_rounds):
+def test_mst_phase_split_exact(gpu_ctx, knobs, iters, pixel_rounds):
     """Any tile-phase iteration cap (SM_MST_LOCAL_ITERS: 0 = pure global Boruvka, 64 = tile
     phase to completion) and either global-round engine (contracted component graph, or the
     pixel rounds kept as the SM_MST_PIXEL_ROUNDS A/B path) gives the reference's MST."""
-    monkeypatch.setenv("SM_MST_LOCAL_ITERS", iters)
+    knobs.setenv("SM_MST_LOCAL_ITERS", iters)
     if pixel_rounds:
-        monkeypatch.setenv("SM_MST_PIXEL_ROUNDS", "1")
+        knobs.setenv("SM_MST_PIXEL_ROUNDS", "1")
     else:
-        monkeypatch.delenv("SM_MST_PIXEL_ROUNDS", raising=False)
+        knobs.delenv("SM_MST_PIXEL_ROUNDS", raising=False)
     z = load_case(CASES[-1])
     for v in ("left", "right"):
         t = gpu_ctx.build_tree(z[v])
@@ -105,15 +105,15 @@ def test_match_bitexact_synthetic(gpu_ctx, W, H, D):
 
 @pytest.mark.parametrize("plen,rmax", [("64", None), ("96", None), ("64", "1"), ("128", "2")])
 @pytest.mark.parametrize("W,H,D", [(320, 240, 64), (256, 160, 128), (200, 120, 200)])
-def test_pieces_match_bitexact(gpu_ctx, monkeypatch, plen, rmax, W, H, D):
+def test_pieces_match_bitexact(gpu_ctx, knobs, plen, rmax, W, H, D):
     """Long heavy paths cut into pieces of SM_PIECE_LEN nodes that run from guessed inputs and are
     repaired exactly (sm_chain.hip "Pieces"); SM_REPAIR_MAX=1/2 makes most repairs give up, which
     sends those pieces through the serial slow path.  SPL = 1, 2, 4."""
-    monkeypatch.setenv("SM_PIECE_LEN", plen)
+    knobs.setenv("SM_PIECE_LEN", plen)
     if rmax:
-        monkeypatch.setenv("SM_REPAIR_MAX", rmax)
+        knobs.setenv("SM_REPAIR_MAX", rmax)
     else:
-        monkeypatch.delenv("SM_REPAIR_MAX", raising=False)
+        knobs.delenv("SM_REPAIR_MAX", raising=False)
     left, right, _ = make_pair(W, H, D, index=4)
     out = gpu_ctx.match(left, right, D)
     ref = O.match(left, right, D, nthreads=16)
@@ -123,13 +123,13 @@ def test_pieces_match_bitexact(gpu_ctx, monkeypatch, plen, rmax, W, H, D):
 
 
 @pytest.mark.parametrize("plen,rmax", [("64", None), ("64", "1")])
-def test_pieces_rows_bitexact(gpu_ctx, monkeypatch, plen, rmax):
+def test_pieces_rows_bitexact(gpu_ctx, knobs, plen, rmax):
     """Every fp64 A_up / A value of 4 slices with short pieces, bitwise."""
-    monkeypatch.setenv("SM_PIECE_LEN", plen)
+    knobs.setenv("SM_PIECE_LEN", plen)
     if rmax:
-        monkeypatch.setenv("SM_REPAIR_MAX", rmax)
+        knobs.setenv("SM_REPAIR_MAX", rmax)
     else:
-        monkeypatch.delenv("SM_REPAIR_MAX", raising=False)
+        knobs.delenv("SM_REPAIR_MAX", raising=False)
     W, H, d0, D = 400, 300, 20, 4
     left, right, _ = make_pair(W, H, 64, index=5)
     lv, rv = O.cost_agd(left, right, d0, d0 + D)
@@ -143,11 +143,11 @@ def test_pieces_rows_bitexact(gpu_ctx, monkeypatch, plen, rmax):
 
 @pytest.mark.parametrize("plen", ["64", "512"])
 @pytest.mark.parametrize("D", [32, 64, 100, 200])
-def test_chain_helper_costs_bitexact(gpu_ctx, monkeypatch, plen, D):
+def test_chain_helper_costs_bitexact(gpu_ctx, knobs, plen, D):
     """The up chain's helpers fold the pre-heavy children and compute the AGD cost rows from the
     image records themselves (SPL 1, 2, 4; 32-double rows at D=32): bit-exact against the oracle,
     cut paths (k_up_pre's aggregates and the repair walks compute costs too) included."""
-    monkeypatch.setenv("SM_PIECE_LEN", plen)
+    knobs.setenv("SM_PIECE_LEN", plen)
     W, H = 400, 300
     left, right, _ = make_pair(W, H, D, index=6)
     ref = O.match(left, right, D, nthreads=16)
@@ -158,7 +158,7 @@ def test_chain_helper_costs_bitexact(gpu_ctx, monkeypatch, plen, D):
 
 
 @pytest.mark.parametrize("D", [32, 64, 128, 256])
-def test_leaf_f32_rows_bitexact(gpu_ctx, monkeypatch, D):
+def test_leaf_f32_rows_bitexact(gpu_ctx, knobs, D):
     """Heavy leaves keep an f32 cost row in their U slot (WalkArgs::leaf_cost): the walkers' results
     with it equal the full-row path (SM_NO_LEAF_COST=1) and the oracle bitwise (SPL 1, 2, 4; 32-double
     rows at D=32; segment forest too)."""
@@ -168,9 +168,9 @@ def test_leaf_f32_rows_bitexact(gpu_ctx, monkeypatch, D):
     for params, ref in ((None, O.match(left, right, D, nthreads=16)),
                         (sm.default_params(c=5000.0, min_size=200), O.match(left, right, D, c=5000.0, nthreads=16))):
         out = gpu_ctx.match(left, right, D, params)
-        monkeypatch.setenv("SM_NO_LEAF_COST", "1")
+        knobs.setenv("SM_NO_LEAF_COST", "1")
         full = gpu_ctx.match(left, right, D, params)
-        monkeypatch.delenv("SM_NO_LEAF_COST")
+        knobs.delenv("SM_NO_LEAF_COST")
         for v in ("left", "right"):
             np.testing.assert_array_equal(out[v]["idx"], full[v]["idx"])
             assert np.array_equal(bits(out[v]["minc"]), bits(full[v]["minc"]))
@@ -311,14 +311,14 @@ def test_full_size_c4_shard_with_reduce_bitexact(rank):
 
 @pytest.mark.parametrize("c", [float("inf"), 5000.0])
 @pytest.mark.parametrize("W,H,D,plen", [(320, 240, 64, "64"), (256, 160, 128, None), (160, 90, 200, "64"), (200, 150, 32, None)])
-def test_one_view_calls_bitexact(gpu_ctx, monkeypatch, W, H, D, plen, c):
+def test_one_view_calls_bitexact(gpu_ctx, knobs, W, H, D, plen, c):
     """sm_params.views = 1 / 2: a call builds and filters only that view (the multi-GPU view
     groups); bit-exact against the oracle, MST and segment forest, cut paths too."""
     import stereomatch_amd as sm
     if plen:
-        monkeypatch.setenv("SM_PIECE_LEN", plen)
+        knobs.setenv("SM_PIECE_LEN", plen)
     else:
-        monkeypatch.delenv("SM_PIECE_LEN", raising=False)
+        knobs.delenv("SM_PIECE_LEN", raising=False)
     left, right, _ = make_pair(W, H, D, index=9)
     ref = O.match(left, right, D, nthreads=16, c=c)
     for views, v in ((1, "left"), (2, "right")):
@@ -365,20 +365,20 @@ def test_one_view_rejects_two_map_post(gpu_ctx):
         gpu_ctx.match(left, right, 16, sm.default_params(views=4))
 
 
-def test_chain_wait_timeout_is_an_error(monkeypatch):
+def test_chain_wait_timeout_is_an_error(knobs):
     """A cross-workgroup wait of the chain engine that never sees its status word must not return
     SM_OK: SM_WAIT_ITERS=0 makes every such wait give up at once, which sets the call's device error
     word; sm_synchronize reports SM_ERR_STATE.  The next call (normal waits) is exact again."""
     import stereomatch_amd as sm
-    monkeypatch.setenv("SM_PIECE_LEN", "64")  # cut paths: pieces wait for their neighbours
+    knobs.setenv("SM_PIECE_LEN", "64")  # cut paths: pieces wait for their neighbours
     W, H, D = 320, 240, 64
     left, right, _ = make_pair(W, H, D, index=4)
     ctx = sm.Context(0)
     try:
-        monkeypatch.setenv("SM_WAIT_ITERS", "0")
+        knobs.setenv("SM_WAIT_ITERS", "0")
         with pytest.raises(sm.StereoMSTError, match="SM_ERR_STATE.*timed out"):
             ctx.match(left, right, D)
-        monkeypatch.delenv("SM_WAIT_ITERS")
+        knobs.delenv("SM_WAIT_ITERS")
         out = ctx.match(left, right, D)
     finally:
         ctx.close()
@@ -612,10 +612,10 @@ def test_volume_ingest_bitexact(gpu_ctx, W, H, D, Dv, d0):
         assert np.array_equal(bits(out[v]["minc"].ravel()), bits(r["minc"]))
 
 
-def test_volume_ingest_pieces_bitexact(gpu_ctx, monkeypatch):
+def test_volume_ingest_pieces_bitexact(gpu_ctx, knobs):
     """Volume costs through cut paths (64-node pieces) and runs."""
     import stereomatch_amd as sm
-    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    knobs.setenv("SM_PIECE_LEN", "64")
     W, H, D = 320, 240, 64
     left, right, _ = make_pair(W, H, D, index=9)
     lv, rv = _mccnn_like(D, H, W, 3), _mccnn_like(D, H, W, 4)
@@ -727,10 +727,10 @@ def test_segment_aggregate_bitexact(gpu_ctx, c, min_size):
 
 @pytest.mark.parametrize("W,H,D,c", [(320, 240, 64, 5000.0), (200, 150, 128, 5000.0), (160, 90, 256, 5000.0),
                                      (256, 160, 128, 800.0)])
-def test_segment_match_bitexact_synthetic(gpu_ctx, monkeypatch, W, H, D, c):
+def test_segment_match_bitexact_synthetic(gpu_ctx, knobs, W, H, D, c):
     """Segment mode at SPL 1 / 2 / 4 with short pieces (cut paths inside the trees)."""
     import stereomatch_amd as sm
-    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    knobs.setenv("SM_PIECE_LEN", "64")
     left, right, _ = make_pair(W, H, D, index=7)
     out = gpu_ctx.match(left, right, D, sm.default_params(c=c, min_size=200))
     ref = O.match(left, right, D, c=c, min_size=200, nthreads=16)
@@ -784,7 +784,7 @@ def test_full_size_c3_segment_forest_and_match(gpu_ctx):
                                  {"SM_SEG_NOSPLIT": "1"}, {"SM_SEG_NORUN": "1"}, {"SM_SEG_NORUN": "1", "SM_SEG_ACT_MAX": "0"},
                                  {"SM_SEG_TAIL_GLOBAL": "1"}, {"SM_SEG_GLOBAL_ROUNDS": "1"},
                                  {"SM_SEG_TAIL_MIN": "0"}, {"SM_SEG_TAIL_MIN": "0", "SM_SEG_GLOBAL_ROUNDS": "1"}])
-def test_segment_forest_schedules(gpu_ctx, monkeypatch, env):
+def test_segment_forest_schedules(gpu_ctx, knobs, env):
     """The GPU segmentation's launch schedules give the same forest: every bucket over the whole GPU
     (with and without global Boruvka rounds before the one-workgroup tail), every bucket in one
     workgroup, more global rounds; the host sweep (SM_SEG_HOST); no root flattening, or flattening
@@ -797,7 +797,7 @@ def test_segment_forest_schedules(gpu_ctx, monkeypatch, env):
     dedupe's sort fallback, for tables that do not fit, runs on the smallest golden images.)"""
     import stereomatch_amd as sm
     for k, val in env.items():
-        monkeypatch.setenv(k, val)
+        knobs.setenv(k, val)
     img, _, _ = make_pair(640, 480, 64, index=3)
     H, W, _ = img.shape
     wR, wD = O.edge_weights(O.median3(img))
@@ -823,12 +823,12 @@ def test_full_size_c2_segment_match_bitexact(gpu_ctx):
 
 # ---- subpixel WTA (SM_POST_SUBPIXEL; PatchMatchStereoGPU.cu:1726-1736) ----
 @pytest.mark.parametrize("W,H,D", [(160, 120, 48), (200, 96, 100), (256, 128, 128), (128, 64, 200)])
-def test_subpixel_bitexact(gpu_ctx, monkeypatch, W, H, D):
+def test_subpixel_bitexact(gpu_ctx, knobs, W, H, D):
     """Subpixel disparities of both views (SPL 1 / 2 / 4, cut paths through the chain engine and
     its repair walks) against the oracle's parabola over its own aggregated volumes; idx / min are
     the integral WTA's."""
     import stereomatch_amd as sm
-    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    knobs.setenv("SM_PIECE_LEN", "64")
     left, right, _ = make_pair(W, H, D, index=9)
     out = gpu_ctx.match(left, right, D, sm.default_params(post=sm.SM_POST_SUBPIXEL))
     ref = O.match(left, right, D, want_volumes=True, nthreads=16)
@@ -868,26 +868,26 @@ def test_subpixel_shard_halo_with_reduce(d0, D, Dt):
 
 # ---- 32-slice rows (Dpad = 32 for calls of <= 32 slices: a C4 shard moves 32 slices of rows) ----
 @pytest.mark.parametrize("W,H,D,plen", [(320, 240, 32, "64"), (256, 160, 17, "64"), (200, 150, 32, None)])
-def test_dpad32_match_bitexact(gpu_ctx, monkeypatch, W, H, D, plen):
+def test_dpad32_match_bitexact(gpu_ctx, knobs, W, H, D, plen):
     """Calls of <= 32 slices use 32-double rows (lanes 32..63 load nothing, store nothing): matches
     with cut paths (fast and forced-slow repair) against the oracle, bitwise."""
     if plen:
-        monkeypatch.setenv("SM_PIECE_LEN", plen)
+        knobs.setenv("SM_PIECE_LEN", plen)
     left, right, _ = make_pair(W, H, D, index=12)
     ref = O.match(left, right, D, nthreads=16)
     for rmax in (None, "1"):
         if rmax:
-            monkeypatch.setenv("SM_REPAIR_MAX", rmax)
+            knobs.setenv("SM_REPAIR_MAX", rmax)
         out = gpu_ctx.match(left, right, D)
         for v in ("left", "right"):
             np.testing.assert_array_equal(out[v]["idx"].ravel(), ref[v]["idx"])
             assert np.array_equal(bits(out[v]["minc"].ravel()), bits(ref[v]["minc"]))
 
 
-def test_dpad32_volume_ingest_and_rows(gpu_ctx, monkeypatch):
+def test_dpad32_volume_ingest_and_rows(gpu_ctx, knobs):
     """MC-CNN volume rows and every A_up / A value at 32-slice rows, with 64-node pieces."""
     import stereomatch_amd as sm
-    monkeypatch.setenv("SM_PIECE_LEN", "64")
+    knobs.setenv("SM_PIECE_LEN", "64")
     W, H, D, d0 = 240, 160, 30, 2
     left, right, _ = make_pair(W, H, 64, index=13)
     lv, rv = _mccnn_like(40, H, W, 7), _mccnn_like(40, H, W, 8)
@@ -935,7 +935,7 @@ def test_guided_match_full_size_c2(gpu_ctx):
         np.testing.assert_array_equal(out[v]["disp"].ravel(), ref[v]["disp"])
 
 
-def test_guided_direct_x_pass(gpu_ctx, monkeypatch):
+def test_guided_direct_x_pass(gpu_ctx, knobs):
     """The direct x box pass (the path for rows too wide for the LDS tile) gives the same bits as the
     LDS-tiled one; a 7 px wide and a 1 px high image exercise the tile edges."""
     import stereomatch_amd as sm
@@ -943,9 +943,9 @@ def test_guided_direct_x_pass(gpu_ctx, monkeypatch):
         left, right, _ = make_pair(W, H, D, index=3)
         p = sm.default_params(aggregator=sm.SM_AGG_GUIDED, gf_radius=5, post=sm.SM_POST_SUBPIXEL)
         a = gpu_ctx.match(left, right, D, p)
-        monkeypatch.setenv("SM_GF_DIRECT_X", "1")
+        knobs.setenv("SM_GF_DIRECT_X", "1")
         b = gpu_ctx.match(left, right, D, p)
-        monkeypatch.delenv("SM_GF_DIRECT_X")
+        knobs.delenv("SM_GF_DIRECT_X")
         ref = O.guided_match(left, right, D, radius=5, sub=True, nthreads=16)
         for v in ("left", "right"):
             np.testing.assert_array_equal(a[v]["idx"].ravel(), ref[v]["idx"])
@@ -954,7 +954,7 @@ def test_guided_direct_x_pass(gpu_ctx, monkeypatch):
             np.testing.assert_array_equal(b[v]["disp"], a[v]["disp"])
 
 
-def test_guided_fused_tiles_match_unfused(gpu_ctx, monkeypatch):
+def test_guided_fused_tiles_match_unfused(gpu_ctx, knobs):
     """Radius 9 with W % 4 == 0 runs the fused tile kernels (k_gf_box1_ab / k_gf_box2_q / k_gf_wta);
     SM_GF_UNFUSED=1 (and any other width or radius) the unfused chain.  Same bits, and the oracle's, on
     images narrower than a tile, one row high, ragged in both 32-pixel block directions, and with
@@ -964,9 +964,9 @@ def test_guided_fused_tiles_match_unfused(gpu_ctx, monkeypatch):
         left, right, _ = make_pair(W, H, D, index=5)
         p = sm.default_params(aggregator=sm.SM_AGG_GUIDED, post=sm.SM_POST_SUBPIXEL)
         a = gpu_ctx.match(left, right, D, p)
-        monkeypatch.setenv("SM_GF_UNFUSED", "1")
+        knobs.setenv("SM_GF_UNFUSED", "1")
         b = gpu_ctx.match(left, right, D, p)
-        monkeypatch.delenv("SM_GF_UNFUSED")
+        knobs.delenv("SM_GF_UNFUSED")
         ref = O.guided_match(left, right, D, sub=True, nthreads=16)
         for v in ("left", "right"):
             np.testing.assert_array_equal(a[v]["idx"].ravel(), ref[v]["idx"])

@@ -63,21 +63,21 @@ def test_pms_golden_bitexact(gpu_ctx, name, c, min_size, iters):
 
 
 @pytest.mark.parametrize("mode", ["spec", "serial", "chain48", "nsu4", "nsu8"])
-def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
+def test_pms_synthetic_modes_bitexact(gpu_ctx, knobs, mode):
     """Many trees (c=300, min_size 20) and 4 calls: the speculative passes meet stale inputs (one
     tree re-run serially, later trees kept and re-validated, higher neighbours sampled from the
     call's starting labels) and wrong offsets (a new pass); SM_PMS_SERIAL=1 is the plain serial order;
     SM_PMS_CHAIN_MIN=48 sends paths of >= 48 rows to the chain kernel; SM_PMS_CHAIN_NSU=4 / 8 gives the
     up chain that many ring slots (default 6)."""
-    monkeypatch.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
+    knobs.setenv("SM_PMS_SERIAL", "1" if mode == "serial" else "0")
     if mode in ("chain48", "nsu4", "nsu8"):
-        monkeypatch.setenv("SM_PMS_CHAIN_MIN", "48")  # (more chain items at this size)
+        knobs.setenv("SM_PMS_CHAIN_MIN", "48")  # (more chain items at this size)
     else:
-        monkeypatch.delenv("SM_PMS_CHAIN_MIN", raising=False)
+        knobs.delenv("SM_PMS_CHAIN_MIN", raising=False)
     if mode in ("nsu4", "nsu8"):
-        monkeypatch.setenv("SM_PMS_CHAIN_NSU", mode[3:])
+        knobs.setenv("SM_PMS_CHAIN_NSU", mode[3:])
     else:
-        monkeypatch.delenv("SM_PMS_CHAIN_NSU", raising=False)
+        knobs.delenv("SM_PMS_CHAIN_NSU", raising=False)
     left, right, _ = make_pair(160, 120, 48, index=3)
     ref = O.stereo3dmst_pms(left, right, 48, iters=4, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 4, 300.0, 20)
@@ -89,14 +89,14 @@ def test_pms_synthetic_modes_bitexact(gpu_ctx, monkeypatch, mode):
 
 
 @pytest.mark.parametrize("piece,serial", [("16", "0"), ("8", "1"), ("64", "0"), ("8", "0")])
-def test_pms_pieces_bitexact(gpu_ctx, monkeypatch, piece, serial):
+def test_pms_pieces_bitexact(gpu_ctx, knobs, piece, serial):
     """Long heavy paths cut into pieces of SM_PMS_PIECE rows: every piece runs from a guessed input; the
     parallel repair (k_pms_repair_par) re-walks every piece at once from its neighbour's boundary row until
     the rows agree, and the gated sequential pass redoes the cuts where a piece's repair rewrote the row
     its neighbour started from (8-row pieces mostly re-walk whole pieces, so they take it).  First call serial (cut trees take the whole-GPU launches), later
     calls speculative; SM_PMS_SERIAL=1 all serial."""
-    monkeypatch.setenv("SM_PMS_PIECE", piece)
-    monkeypatch.setenv("SM_PMS_SERIAL", serial)
+    knobs.setenv("SM_PMS_PIECE", piece)
+    knobs.setenv("SM_PMS_SERIAL", serial)
     left, right, _ = make_pair(192, 128, 48, index=7)
     ref = O.stereo3dmst_pms(left, right, 48, iters=3, c=5000.0, min_size=200)
     out, labs, st = run_gpu(gpu_ctx, left, right, 48, 3, 5000.0, 200)
@@ -116,9 +116,9 @@ def test_pms_many_trees_bitexact(gpu_ctx):
     assert st["spec_rounds"] >= 2
 
 
-def test_pms_max_rounds_fallback(gpu_ctx, monkeypatch):
+def test_pms_max_rounds_fallback(gpu_ctx, knobs):
     """SM_PMS_MAX_ROUNDS=1: a call whose first speculative pass fails finishes in serial order."""
-    monkeypatch.setenv("SM_PMS_MAX_ROUNDS", "1")
+    knobs.setenv("SM_PMS_MAX_ROUNDS", "1")
     left, right, _ = make_pair(128, 96, 40, index=4)
     ref = O.stereo3dmst_pms(left, right, 40, iters=3, c=200.0, min_size=10)
     out, labs, _ = run_gpu(gpu_ctx, left, right, 40, 3, 200.0, 10)
@@ -165,16 +165,16 @@ def test_pms_bad_params(gpu_ctx):
     assert e.value.status == 5
 
 
-def test_pms_forest_cycle_is_an_error(gpu_ctx, monkeypatch):
+def test_pms_forest_cycle_is_an_error(gpu_ctx, knobs):
     """Masks that are not a forest (SM_TEST_PMS_CYCLE=1 turns the square of pixels 0, 1, W, W + 1 into
     four real edges) are refused before any Euler tour -- whose list ranking would never end -- with
     SM_ERR_STATE; the next call on the same context is exact again."""
     left, right, _ = make_pair(96, 64, 24, index=2)
-    monkeypatch.setenv("SM_TEST_PMS_CYCLE", "1")
+    knobs.setenv("SM_TEST_PMS_CYCLE", "1")
     with pytest.raises(sm.StereoMSTError, match="cycle") as e:
         run_gpu(gpu_ctx, left, right, 24, 1, 300.0, 20)
     assert e.value.status == 5
-    monkeypatch.delenv("SM_TEST_PMS_CYCLE")
+    knobs.delenv("SM_TEST_PMS_CYCLE")
     ref = O.stereo3dmst_pms(left, right, 24, iters=1, c=300.0, min_size=20)
     out, labs, st = run_gpu(gpu_ctx, left, right, 24, 1, 300.0, 20)
     for v in ("left", "right"):
@@ -210,7 +210,7 @@ _FULL_C2_REF = {}
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("chain_min", [None, "48"])
-def test_pms_full_c2_speculative_bitexact(gpu_ctx, monkeypatch, chain_min):
+def test_pms_full_c2_speculative_bitexact(gpu_ctx, knobs, chain_min):
     """Full C2 (1920x1200, Dmax 128), c=5000, min_size 200, THREE MST_PMS calls per view: calls 2-3 take
     the speculative path (guessed offsets, every tree at once, validation, single-tree repairs) with the
     default 512-row pieces, propagation dedupe and whole-GPU launches -- the mode the reference's 99 later
@@ -218,9 +218,9 @@ def test_pms_full_c2_speculative_bitexact(gpu_ctx, monkeypatch, chain_min):
     bitwise against the oracle's serial restatement.  chain_min 48: paths of >= 48 rows on the chain kernel
     (SM_PMS_CHAIN_MIN)."""
     for k in ("SM_PMS_SERIAL", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS", "SM_PMS_CHAIN_MIN"):
-        monkeypatch.delenv(k, raising=False)
+        knobs.delenv(k, raising=False)
     if chain_min:
-        monkeypatch.setenv("SM_PMS_CHAIN_MIN", chain_min)
+        knobs.setenv("SM_PMS_CHAIN_MIN", chain_min)
     left, right, _ = make_pair(1920, 1200, 128, index=0)
     if "ref" not in _FULL_C2_REF:  # the oracle's three calls once for both cases
         _FULL_C2_REF["ref"] = O.stereo3dmst_pms(left, right, 128, iters=3, c=5000.0, min_size=200)
@@ -233,13 +233,13 @@ def test_pms_full_c2_speculative_bitexact(gpu_ctx, monkeypatch, chain_min):
 
 
 @pytest.mark.timeout(900)
-def test_pms_flir_c1_two_calls_output_step(gpu_ctx, monkeypatch):
+def test_pms_flir_c1_two_calls_output_step(gpu_ctx, knobs):
     """BASELINE config C1's pair (FLIR 000020, 2048x1536, Dmax 64), the reference's own constants, two
     MST_PMS calls per view (the second speculative) and stereo3dmst's output step (LabelToDisp, *= Dmax-1,
     L-R check of the left map; :189-201, :900-904), bitwise against the oracle."""
     from conftest import flir_pair
     for k in ("SM_PMS_SERIAL", "SM_PMS_PIECE", "SM_PMS_MAX_ROUNDS"):
-        monkeypatch.delenv(k, raising=False)
+        knobs.delenv(k, raising=False)
     L, R = flir_pair()
     D = 64
     ref = O.stereo3dmst_pms(L, R, D, iters=2, c=5000.0, min_size=200)
@@ -254,17 +254,17 @@ def test_pms_flir_c1_two_calls_output_step(gpu_ctx, monkeypatch):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("case", ["golden5000", "golden300", "synth300", "many_trees", "pieces16", "mst_mode", "full_c2"])
-def test_pms_gpu_forest_matches_host_build(gpu_ctx, monkeypatch, case):
+def test_pms_gpu_forest_matches_host_build(gpu_ctx, knobs, case):
     """The schedule forest built on the GPU (sm_pms_forest.hip: union-find tree numbering, the level-order
     BFS of every tree, heavy paths, rows, tree graph, round lists) against the host construction
     (pms_build_forest), array by array (SM_PMS_FOREST_CHECK=1 makes the call fail on any difference), then
     the call's labels against the oracle."""
-    monkeypatch.setenv("SM_PMS_FOREST_CHECK", "1")
-    monkeypatch.delenv("SM_PMS_HOST_FOREST", raising=False)
+    knobs.setenv("SM_PMS_FOREST_CHECK", "1")
+    knobs.delenv("SM_PMS_HOST_FOREST", raising=False)
     if case == "pieces16":
-        monkeypatch.setenv("SM_PMS_PIECE", "16")
+        knobs.setenv("SM_PMS_PIECE", "16")
     else:
-        monkeypatch.delenv("SM_PMS_PIECE", raising=False)
+        knobs.delenv("SM_PMS_PIECE", raising=False)
     if case.startswith("golden"):
         z = load_case("smooth_97x61")
         left, right, D = z["left"], z["right"], int(z["D"])

@@ -13,7 +13,7 @@ for rep in $(seq 1 $REPS); do
   for spec in "$@"; do
     label=${spec%%|*}; rest=${spec#*|}; envs=${rest%%|*}; args=${rest#*|}
     log=$O/${label}_$rep.log
-    env $envs timeout -k 10 300 python bench.py $BASE_ARGS $args > $log 2>&1 || { echo "FAILED $label"; tail -5 $log; exit 2; }
+    env $envs timeout -k 10 300 python bench.py --dev $BASE_ARGS $args > $log 2>&1 || { echo "FAILED $label"; tail -5 $log; exit 2; }
     python3 - "$label" "$log" <<'EOF'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
