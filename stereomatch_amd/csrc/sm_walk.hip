@@ -311,15 +311,18 @@ __device__ __forceinline__ uint32_t hfield_v(uint32_t w, int hl, int j, int f) {
 #define WALK_UP_CHH 2  // round 5: 3 -> 2 (76 -> 72 VGPRs, 6 -> 7 waves per SIMD), with WALK_DN_CHH 4 -> 3
                        // (5 -> 7): the N = 8 share 2.009-2.016 -> 1.967-1.987 ms/frame
 #endif
+#ifndef WALK_UP_CHH1
+#define WALK_UP_CHH1 2  // 32-slice rows (1 slice per half-lane)
+#endif
 
-template <int CH>
+template <int CH, int SH>
 __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int view, int lane, int W, int dbase, int dend,
                                             const uint2* __restrict__ own, const uint32_t* __restrict__ oth4,
-                                            double* __restrict__ U, const WalkShared& sh, double (&xc)[2], uint32_t& nxt,
+                                            double* __restrict__ U, const WalkShared& sh, double (&xc)[SH], uint32_t& nxt,
                                             const uint32_t* __restrict__ meta32, int mtop, int mn, int leaf_cost) {
     static_assert(CH <= 4, "lane 32h + 8j + f holds word f of half h's node j");
     constexpr int LR = WALK_UP_LR;
-    constexpr int DP = 64;
+    constexpr int DP = 32 * SH;  // row length: 64 doubles (2 slices per half-lane) or 32 (1)
     const int hl = lane >> 5, hlane = lane & 31;
     const int nv = n > 0 ? n : 1;  // rows / records of a finished half: its chunk's first node
     // ---- light-row bookkeeping (per half): node j's light children are compact rows off[j] ..
@@ -331,7 +334,7 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
         off[j] = tot;
         tot += nch > 0 ? (int)nch - 1 : 0;
     }
-    double lr[LR][2];
+    double lr[LR][SH];
 #pragma unroll
     for (int q = 0; q < LR; ++q) {
         int jq = 0, oq = off[0];
@@ -345,10 +348,10 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
         const int pos = kk + (kk >= (int)hidx ? 1 : 0);
         const uint32_t slot = hfield_v(mv, hl, jq, 4 + min(max(pos, 0), 3));
         if (q < tot) {
-            load_row<2>(U, slot, DP, hlane, lr[q]);
+            load_row<SH>(U, slot, DP, hlane, lr[q]);
         } else {
-            lr[q][0] = 0.0;
-            lr[q][1] = 0.0;
+#pragma unroll
+            for (int k = 0; k < SH; ++k) lr[q][k] = 0.0;
         }
     }
     // ---- image records: lane 32h + i (i < 16) own(x) of node min(i, n-1), lane 32h + 16 + i own(x+1)
@@ -360,20 +363,22 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
         for (int j = 1; j < CH; ++j) pl = node == j ? hfield<CH>(mv, hl, j, 0) : pl;
         ownr = own[(long long)pl + (hlane >> 4)];
     }
-    uint32_t ob[CH][3];
+    // matched-image records x + dbase .. x + dbase + SH (right view) or x - dbase - (SH - 1) .. x - dbase + 1
+    // (left view): slice k reads records q = k, k + 1 (right) or SH - 1 - k, SH - k (left)
+    uint32_t ob[CH][SH + 1];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         // node j >= n: its metadata lanes already hold node n - 1's words (clamped load); the
         // readlane index must stay uniform
         const long long pix = (long long)hfield<CH>(mv, hl, j, 0);
-        const long long base = view ? pix + dbase : pix - dbase - 1;
+        const long long base = view ? pix + dbase : pix - dbase - (SH - 1);
 #pragma unroll
-        for (int q = 0; q <= 2; ++q) ob[j][q] = oth4[base + q];
+        for (int q = 0; q <= SH; ++q) ob[j][q] = oth4[base + q];
     }
     nxt = meta32[(size_t)(mtop - min(hlane >> 3, mn - 1)) * 8 + (lane & 7)];
     walk_vm_drain();
-    // ---- costs (chunk_costs4 at SPL = 2, per half) and edge factors
-    float c[CH][2];
+    // ---- costs (chunk_costs4 at SPL = SH, per half) and edge factors
+    float c[CH][SH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
         const int x = pix_col((int)hfield<CH>(mv, hl, j, 0), W);
@@ -381,11 +386,11 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
         const uint32_t ox0 = hfield<CH>(ownr.x, hl, 0, j), oy0 = hfield<CH>(ownr.y, hl, 0, j);
         const uint32_t oy1 = hfield<CH>(ownr.y, hl, 2, j);
         const float go0 = __uint_as_float(oy0), go1 = __uint_as_float(oy1);
-        float g[3];
+        float g[SH + 1];
 #pragma unroll
-        for (int q = 0; q <= 2; ++q) g[q] = gray4(ob[j][q]);
+        for (int q = 0; q <= SH; ++q) g[q] = gray4(ob[j][q]);
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < SH; ++k) {
             const int d = dbase + k;
             float v;
             bool ok;
@@ -394,7 +399,7 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
                 v = agd4(ox0, ob[j][k], go0, g[k], go1, g[k + 1], sh.atab);
             } else {
                 ok = d < dend && x - d >= 0 && x + 1 < W;
-                v = agd4(ob[j][1 - k], ox0, g[1 - k], go0, g[2 - k], go1, sh.atab);
+                v = agd4(ob[j][SH - 1 - k], ox0, g[SH - 1 - k], go0, g[SH - k], go1, sh.atab);
             }
             c[j][k] = ok ? v : 3.0f;
         }
@@ -419,43 +424,45 @@ __device__ __forceinline__ void up_chunk_h2(uint32_t mv, int n, int top, int vie
         for (int i = 0; i < 4; ++i) cs[i] = hfield<CH>(mv, hl, j, 4 + i);
         if (j < n) {
             const uint32_t nch = hi_nch(hi), hidx = hi_hidx(hi);
-            double acc[2] = {0.0, 0.0};
+            double acc[SH];
+#pragma unroll
+            for (int k = 0; k < SH; ++k) acc[k] = 0.0;
 #pragma unroll
             for (uint32_t i = 0; i < 4; ++i) {
                 if (i < nch) {
-                    double v[2];
+                    double v[SH];
                     if (i == hidx) {
-                        v[0] = xc[0];
-                        v[1] = xc[1];
+#pragma unroll
+                        for (int k = 0; k < SH; ++k) v[k] = xc[k];
                     } else {
                         const int q = off[j] + (int)i - (i > hidx ? 1 : 0);
                         bool held = false;
 #pragma unroll
                         for (int r = 0; r < LR; ++r) {
                             if (q == r) {
-                                v[0] = lr[r][0];
-                                v[1] = lr[r][1];
+#pragma unroll
+                                for (int k = 0; k < SH; ++k) v[k] = lr[r][k];
                                 held = true;
                             }
                         }
-                        if (!held) load_row<2>(U, cs[i], DP, hlane, v);  // rare: loaded here
+                        if (!held) load_row<SH>(U, cs[i], DP, hlane, v);  // rare: loaded here
                     }
                     const double S = i < 2 ? Sv[j][i < 2 ? i : 0] : sh.slut[cw_of(hfield<CH>(mv, hl, j, 2), hi, (int)i)];
 #pragma unroll
-                    for (int k = 0; k < 2; ++k) acc[k] = __builtin_fma(S, v[k], acc[k]);
+                    for (int k = 0; k < SH; ++k) acc[k] = __builtin_fma(S, v[k], acc[k]);
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 2; ++k) xc[k] = acc[k] + (double)c[j][k];
+            for (int k = 0; k < SH; ++k) xc[k] = acc[k] + (double)c[j][k];
             if (leaf_cost && nch == 0 && par != SM_NONE && par == (uint32_t)(top - j) - 1u)
-                store_leaf_row<2>(U, (uint32_t)(top - j), DP, hlane, c[j]);
+                store_leaf_row<SH>(U, (uint32_t)(top - j), DP, hlane, c[j]);
             else
-                store_row<2>(U, (uint32_t)(top - j), DP, hlane, xc);
+                store_row<SH>(U, (uint32_t)(top - j), DP, hlane, xc);
         }
     }
 }
 
-template <int CH>
+template <int CH, int SH>
 __global__ __launch_bounds__(256) void k_up_walk_h2(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                     const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
                                                     const SmPath* __restrict__ paths1, const uint2* __restrict__ Lrec,
@@ -479,11 +486,13 @@ __global__ __launch_bounds__(256) void k_up_walk_h2(WalkView V0, WalkView V1, co
         head = (int)pp[pi0].head;
         len = (int)(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
     }
-    const int dbase = dglob0 + hlane * 2;
+    const int dbase = dglob0 + hlane * SH;
     const int dend = dglob0 + dcall;
     const uint2* __restrict__ own = view ? Rrec : Lrec;
     const uint32_t* __restrict__ oth4 = view ? Lrec4 : Rrec4;
-    double xc[2] = {0.0, 0.0};
+    double xc[SH];
+#pragma unroll
+    for (int k = 0; k < SH; ++k) xc[k] = 0.0;
     int top = len > 0 ? head + len - 1 : 0;
     int n = min(CH, len);
     uint32_t cur = meta32[(size_t)(top - min(hlane >> 3, max(n, 1) - 1)) * 8 + (lane & 7)];
@@ -492,7 +501,7 @@ __global__ __launch_bounds__(256) void k_up_walk_h2(WalkView V0, WalkView V1, co
         const int ntop = top - CH;
         const int nn = (n > 0 && ntop >= head) ? min(CH, ntop - head + 1) : 0;
         uint32_t nxt;
-        up_chunk_h2<CH>(cur, n, top, view, lane, W, dbase, dend, own, oth4, V.U, sh, xc, nxt, meta32, nn > 0 ? ntop : top,
+        up_chunk_h2<CH, SH>(cur, n, top, view, lane, W, dbase, dend, own, oth4, V.U, sh, xc, nxt, meta32, nn > 0 ? ntop : top,
                         nn > 0 ? nn : max(n, 1), leaf_cost);
         if (__ballot(nn > 0) == 0) break;
         cur = nxt;
@@ -642,9 +651,9 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
 // k_down_walk's exactly.  A half whose item is finished keeps re-reading its last chunk and stores
 // nothing.
 // wta_chunk per half-wave: lane 32h + j (< CH) gets node j of half h's strict-< first minimum
-template <int CH>
-__device__ __forceinline__ void wta_half(const double (&x)[CH][2], int lane, int lo, int hi, double& out_min, int& out_idx) {
-    const int hl = lane >> 5, hlane = lane & 31, dloc0 = hlane * 2;
+template <int CH, int SH>
+__device__ __forceinline__ void wta_half(const double (&x)[CH][SH], int lane, int lo, int hi, double& out_min, int& out_idx) {
+    const int hl = lane >> 5, hlane = lane & 31, dloc0 = hlane * SH;
     double bv[CH], g[CH];
     int bi[CH];
 #pragma unroll
@@ -652,7 +661,7 @@ __device__ __forceinline__ void wta_half(const double (&x)[CH][2], int lane, int
         bv[j] = __builtin_huge_val();
         bi[j] = 0x7fffffff;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < SH; ++k) {
             const int d = dloc0 + k;
             if (d >= lo && d < hi && x[j][k] < bv[j]) { bv[j] = x[j][k]; bi[j] = d; }
         }
@@ -681,14 +690,14 @@ __device__ __forceinline__ void wta_half(const double (&x)[CH][2], int lane, int
     }
 }
 
-template <int CH>
+template <int CH, int SH>
 __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, const uint32_t* __restrict__ meta0,
                                                       const uint32_t* __restrict__ meta1, const SmPath* __restrict__ paths0,
                                                       const SmPath* __restrict__ paths1, const float* __restrict__ atab_g,
                                                       const double* __restrict__ slut_g, const double* __restrict__ s2lut_g,
                                                       WtaCfg w, int store_all, int ppw, int leaf_cost) {
     static_assert(CH <= 4, "lane 32h + 8j + f holds word f of half h's node j");
-    constexpr int DP = 64;  // row length (doubles)
+    constexpr int DP = 32 * SH;  // row length (doubles): 2 slices per half-lane, or 1 (32-slice rows)
     __shared__ WalkShared sh;
     load_tables(sh, atab_g, slut_g, s2lut_g);
     const int view = blockIdx.y;
@@ -706,7 +715,9 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
         head = (int)pp[pi0].head;
         len = (int)(pp[pi1 - 1].head + pp[pi1 - 1].len) - head;
     }
-    double xc[2] = {0.0, 0.0};
+    double xc[SH];
+#pragma unroll
+    for (int k = 0; k < SH; ++k) xc[k] = 0.0;
     int c0 = head;
     int n = min(CH, len);  // 0: this half is finished (or empty)
     // metadata: lane 32h + 8j + f holds word f of node j of half h (clamped to a valid node)
@@ -715,7 +726,7 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
     while (true) {
         const int nc0 = c0 + CH;
         const int nn = (n > 0 && nc0 < head + len) ? min(CH, head + len - nc0) : 0;
-        double u[CH][2], xp[CH][2];
+        double u[CH][SH], xp[CH][SH];
         uint32_t par[CH], hiw[CH];
         bool leaf[CH];
 #pragma unroll
@@ -728,14 +739,14 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
             const bool head_j = par[j] == SM_NONE || par[j] != slot - 1u;
             leaf[j] = leaf_cost && !head_j && hi_nch(hiw[j]) == 0u;
             if (!leaf[j])
-                load_row<2>(V.U, slot, DP, hlane, u[j]);
+                load_row<SH>(V.U, slot, DP, hlane, u[j]);
             else
-                load_leaf_row<2>(V.U, slot, DP, hlane, u[j]);
+                load_leaf_row<SH>(V.U, slot, DP, hlane, u[j]);
             if (head_j && par[j] != SM_NONE) {
-                load_row<2>(V.A, par[j], DP, hlane, xp[j]);
+                load_row<SH>(V.A, par[j], DP, hlane, xp[j]);
             } else {
-                xp[j][0] = 0.0;
-                xp[j][1] = 0.0;
+#pragma unroll
+                for (int k = 0; k < SH; ++k) xp[j][k] = 0.0;
             }
         }
         // the next chunk's metadata behind the rows (a finished half re-reads its last chunk's)
@@ -745,7 +756,7 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
         walk_vm_drain();
 #pragma unroll
         for (int j = 0; j < CH; ++j)
-            if (leaf[j]) widen_leaf_row<2>(u[j]);
+            if (leaf[j]) widen_leaf_row<SH>(u[j]);
         double S[CH], S2[CH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -753,7 +764,7 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
             S[j] = sh.slut[wp];
             S2[j] = sh.s2lut[wp];
         }
-        double xs[CH][2];
+        double xs[CH][SH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             if (j < n) {
@@ -761,22 +772,22 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
                 const bool root = par[j] == SM_NONE;
                 const bool hd = !root && par[j] != slot - 1u;
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
+                for (int k = 0; k < SH; ++k) {
                     const double b = hd ? xp[j][k] : xc[k];
                     const double f = __builtin_fma(S[j], b, S2[j] * u[j][k]);
                     xc[k] = root ? u[j][k] : f;
                 }
             }
-            xs[j][0] = xc[0];
-            xs[j][1] = xc[1];
+#pragma unroll
+            for (int k = 0; k < SH; ++k) xs[j][k] = xc[k];
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            if (j < n && (store_all || hi_light(hiw[j]))) store_row<2>(V.A, (uint32_t)(c0 + j), DP, hlane, xs[j]);
+            if (j < n && (store_all || hi_light(hiw[j]))) store_row<SH>(V.A, (uint32_t)(c0 + j), DP, hlane, xs[j]);
         }
         double mn;
         int mi;
-        wta_half<CH>(xs, lane, w.lo, w.hi, mn, mi);
+        wta_half<CH, SH>(xs, lane, w.lo, w.hi, mn, mi);
         const int gi = w.dglob0 + mi;
         // lane 32h + j (< CH) stores node j of half h: its pixel is word 0 at lane 32h + 8j
         const int src = ((hl << 5) + ((hlane & 3) << 3)) << 2;
@@ -849,10 +860,11 @@ static void down_launch(hipStream_t st, dim3 g, const WalkArgs& a, int store_all
                        store_all ? 0 : a.leaf_cost);
 }
 
-// SPL = 1 calls with 64-double rows take the half-wave walkers (env SM_NO_HALF_WAVE: A/B)
+// SPL = 1 calls take the half-wave walkers: 64-double rows with 2 slices per half-lane, 32-double rows
+// (a call of <= 32 slices, e.g. a d-shard rank at N = 8) with 1 (dev builds: SM_NO_HALF_WAVE for A/B)
 static bool half_wave(const WalkArgs& a, int spl) {
     static const bool off = sm_dev_knob("SM_NO_HALF_WAVE") != nullptr;
-    return !off && spl == 1 && a.Dpad == 64;
+    return !off && spl == 1 && (a.Dpad == 64 || a.Dpad == 32);
 }
 
 hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths, const WalkArgs* pre) {
@@ -863,10 +875,16 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
         const int items = (np + ppw - 1) / ppw;
         const int waves = (items + 1) / 2;
         const dim3 g((waves + 3) / 4, 2);
-        hipLaunchKernelGGL((k_up_walk_h2<WALK_UP_CHH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
-                           reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                           a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.dcall,
-                           a.dglob0, ppw, a.leaf_cost);
+        if (a.Dpad == 64)
+            hipLaunchKernelGGL((k_up_walk_h2<WALK_UP_CHH, 2>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
+                               reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                               a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.dcall,
+                               a.dglob0, ppw, a.leaf_cost);
+        else
+            hipLaunchKernelGGL((k_up_walk_h2<WALK_UP_CHH1, 1>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
+                               reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                               a.paths[0], a.paths[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.slut, a.s2lut, a.W, a.dcall,
+                               a.dglob0, ppw, a.leaf_cost);
         return hipGetLastError();
     }
     const int ppw = walk_ppw(np, WALK_PPW_UP, false);
@@ -897,6 +915,9 @@ hipError_t launch_up(hipStream_t st, const WalkArgs& a, int spl, bool long_paths
 #ifndef WALK_DN_CHH
 #define WALK_DN_CHH 3
 #endif
+#ifndef WALK_DN_CHH1
+#define WALK_DN_CHH1 3  // 32-slice rows (1 slice per half-lane)
+#endif
 static bool half_wave_down(const WalkArgs& a, int spl) { return half_wave(a, spl) && !a.wta.sub; }
 
 static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, int store_all, bool long_paths) {
@@ -907,9 +928,14 @@ static hipError_t launch_down_impl(hipStream_t st, const WalkArgs& a, int spl, i
         const int items = (np + ppw - 1) / ppw;
         const int waves = (items + 1) / 2;
         const dim3 g((waves + 3) / 4, 2);
-        hipLaunchKernelGGL((k_down_walk_h2<WALK_DN_CHH>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
-                           reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                           a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.wta, store_all, ppw, store_all ? 0 : a.leaf_cost);
+        if (a.Dpad == 64)
+            hipLaunchKernelGGL((k_down_walk_h2<WALK_DN_CHH, 2>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
+                               reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                               a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.wta, store_all, ppw, store_all ? 0 : a.leaf_cost);
+        else
+            hipLaunchKernelGGL((k_down_walk_h2<WALK_DN_CHH1, 1>), g, dim3(256), walk_lds_pad(), st, to_view(a, 0), to_view(a, 1),
+                               reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
+                               a.paths[0], a.paths[1], a.atab, a.slut, a.s2lut, a.wta, store_all, ppw, store_all ? 0 : a.leaf_cost);
         return hipGetLastError();
     }
     const int ppw = walk_ppw(np, WALK_PPW_DN, true);
