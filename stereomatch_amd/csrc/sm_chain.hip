@@ -338,11 +338,43 @@ static_assert(sizeof(UpRing<4>) + 64 * 4 * 8 + 64 <= SM_LDS_BYTES, "UpRing<4> (U
 // AGD cost, PatchMatchStereoGPU.cu:1482-1550), or read from the f32 rows k_vol_rows filled
 // (MC-CNN ingest)
 struct UpCost {
-    const uint2* own;  // the view's reference image records
-    const uint2* oth;  // the matched image's records
-    const float* Cst;  // cost rows [slot][Dpad] (ingest)
+    const uint2* own;      // the view's reference image records
+    const uint2* oth;      // the matched image's records
+    const uint32_t* oth4;  // the matched image's 4-byte records (bgrx; the gray is recomputed)
+    const float* Cst;      // cost rows [slot][Dpad] (ingest)
     int W, dbase, dend, view;
 };
+
+// The up chain's image records (helpers and repair walks).  Round 6: the walkers' 4-byte records (bgrx
+// alone, the gray recomputed in k_prep's operation order, so the costs are bit-identical): per node a
+// lane loads SPL + 1 dwords instead of SPL {bgrx, gray} pairs and a gray word.  At C2 the chain's
+// fetched bytes were ~1 KB per node, mostly these windows missing L2.  -DSM_CHAIN_REC8: the 8-byte
+// records (A/B).
+#ifdef SM_CHAIN_REC8
+template <int SPL, int CH>
+using ChainRecs = ImgRecs<SPL, CH>;
+template <int SPL, int CH>
+__device__ __forceinline__ void chain_load_recs(const MetaVec<CH>& mv, int n, int lane, const UpCost& cs, ChainRecs<SPL, CH>& r) {
+    load_recs<SPL, CH>(mv, n, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, r);
+}
+template <int SPL, int CH, class T>
+__device__ __forceinline__ void chain_costs(const MetaVec<CH>& mv, const UpCost& cs, const ChainRecs<SPL, CH>& r,
+                                            const float* __restrict__ atab, T (&c)[CH][SPL]) {
+    chunk_costs<SPL, CH>(mv, cs.view, cs.W, cs.dbase, cs.dend, r, atab, c);
+}
+#else
+template <int SPL, int CH>
+using ChainRecs = ImgRecs4<SPL, CH>;
+template <int SPL, int CH>
+__device__ __forceinline__ void chain_load_recs(const MetaVec<CH>& mv, int n, int lane, const UpCost& cs, ChainRecs<SPL, CH>& r) {
+    load_recs4<SPL, CH>(mv, n, cs.view, lane, cs.dbase, cs.own, cs.oth4, r);
+}
+template <int SPL, int CH, class T>
+__device__ __forceinline__ void chain_costs(const MetaVec<CH>& mv, const UpCost& cs, const ChainRecs<SPL, CH>& r,
+                                            const float* __restrict__ atab, T (&c)[CH][SPL]) {
+    chunk_costs4<SPL, CH>(mv, cs.view, cs.W, cs.dbase, cs.dend, r, atab, c);
+}
+#endif
 
 // NN consecutive nodes k0.. of a staged group; NN is a compile-time count so the LDS waits are
 // exact; THIRD = the node-by-node path that also applies a root's third post-heavy child.
@@ -617,7 +649,7 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
     // children) in l2 -- at most one such node per group
     double l0[G][SPL], l1[G][SPL], l2[SPL];
     float cr[G][SPL];
-    ImgRecs<SPL, G> rec;
+    ChainRecs<SPL, G> rec;
     auto issue = [&](int gg, const MetaVec<G>& m) {
         const int n = min(G, len - gg * G);
         uint32_t s2 = (uint32_t)head;
@@ -636,7 +668,7 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
             if (nl >= 3) s2 = mfield(m, kk, hidx == 3 ? 6 : 7);
         }
         load_row<SPL>(U, s2, Dpad, lane, l2);
-        if constexpr (AGD) load_recs<SPL, G>(m, n, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
+        if constexpr (AGD) chain_load_recs<SPL, G>(m, n, lane, cs, rec);
     };
     issue(g, mv);
 #ifdef SM_CHAIN_PROF
@@ -675,15 +707,7 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
         const int gl = gn < ngroups ? gn : g;
         // ---- Pre and C of the group (registers; the loads have landed by now in all but the
         // first group, whose wait is here)
-#ifdef SM_EXP_HELPER_NOCOST  // timing experiment only (wrong results): no cost computation
-        if constexpr (AGD)
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-#pragma unroll
-                for (int q = 0; q < SPL; ++q) cr[k][q] = 0.5f + 0.0f * __uint_as_float(rec.ob[k][q].y);
-#else
-        if constexpr (AGD) chunk_costs<SPL, G>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, ring.atab, cr);
-#endif
+        if constexpr (AGD) chain_costs<SPL, G>(mv, cs, rec, ring.atab, cr);
         // Pre replaces l0 (with hidx >= 1 the first light child is a pre-heavy one, folded here)
 #pragma unroll
         for (int k = 0; k < G; ++k) {
@@ -911,7 +935,7 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
         load_meta<CHR>(mn, meta32, lane, top - n1, -1, min(CHR, nmax - n1));
         double spec[CHR][SPL], r0[CHR][SPL];
         float cr[CHR][SPL];
-        ImgRecs<SPL, CHR> rec;
+        ChainRecs<SPL, CHR> rec;
 #pragma unroll
         for (int k = 0; k < CHR; ++k) {
             const int kk = min(k, nb - 1);
@@ -923,15 +947,8 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
             agent_row_read<SPL>(U, slot, Dpad, lane, spec[k]);  // own piece's rows (this launch)
         }
         if constexpr (AGD) {
-            load_recs<SPL, CHR>(mv, nb, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
-#ifdef SM_EXP_HELPER_NOCOST
-#pragma unroll
-            for (int k = 0; k < CHR; ++k)
-#pragma unroll
-                for (int q = 0; q < SPL; ++q) cr[k][q] = 0.5f + 0.0f * __uint_as_float(rec.ob[k][q].y);
-#else
-            chunk_costs<SPL, CHR>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, atab, cr);
-#endif
+            chain_load_recs<SPL, CHR>(mv, nb, lane, cs, rec);
+            chain_costs<SPL, CHR>(mv, cs, rec, atab, cr);
         }
 #pragma unroll
         for (int k = 0; k < CHR; ++k) {
@@ -1026,7 +1043,7 @@ __device__ __forceinline__ void up_repair_stage(RepNode<SPL>* rn, int kb, int k0
                                                 const double* slut, const float* atab, int Dpad, int head) {
     double l0[CHR][SPL], l1[CHR][SPL], l2[SPL], sp[CHR][SPL];
     float cr[CHR][SPL];
-    ImgRecs<SPL, CHR> rec;
+    ChainRecs<SPL, CHR> rec;
     uint32_t s2 = (uint32_t)head;
 #pragma unroll
     for (int k = 0; k < CHR; ++k) {
@@ -1043,8 +1060,8 @@ __device__ __forceinline__ void up_repair_stage(RepNode<SPL>* rn, int kb, int k0
     }
     load_row<SPL>(U, s2, Dpad, lane, l2);
     if constexpr (AGD) {
-        load_recs<SPL, CHR>(mv, nb, cs.view, lane, cs.W, cs.dbase, cs.own, cs.oth, rec);
-        chunk_costs<SPL, CHR>(mv, cs.view, cs.W, cs.dbase, cs.dend, rec, atab, cr);
+        chain_load_recs<SPL, CHR>(mv, nb, lane, cs, rec);
+        chain_costs<SPL, CHR>(mv, cs, rec, atab, cr);
     }
 #pragma unroll
     for (int k = 0; k < CHR; ++k) {
@@ -1380,6 +1397,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
                                                           const SmPath* __restrict__ paths1,
                                                           const float* __restrict__ Cst0, const float* __restrict__ Cst1,
                                                           const uint2* __restrict__ Lrec, const uint2* __restrict__ Rrec,
+                                                          const uint32_t* __restrict__ Lrec4,
+                                                          const uint32_t* __restrict__ Rrec4,
                                                           const float* __restrict__ atab_g, int W, int dcall, int dglob0,
                                                           const double* __restrict__ slut_g, int Dpad, PieceView Q0,
                                                           PieceView Q1, uint32_t epoch) {
@@ -1446,6 +1465,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     UpCost cs;
     cs.own = view ? Rrec : Lrec;
     cs.oth = view ? Lrec : Rrec;
+    cs.oth4 = view ? Lrec4 : Rrec4;
     cs.Cst = view ? Cst1 : Cst0;
     cs.W = W;
     cs.dbase = dglob0 + lane * SPL;
@@ -2196,8 +2216,8 @@ template <int SPL, bool AGD>
 static void up_chain_launch_k(hipStream_t st, const WalkArgs& a, int np) {
     hipLaunchKernelGGL((k_up_chain<SPL, AGD>), dim3(np, 2), dim3(CHN_THREADS), 0, st, chain_view(a, 0), chain_view(a, 1),
                        reinterpret_cast<const uint32_t*>(a.meta[0]), reinterpret_cast<const uint32_t*>(a.meta[1]),
-                       a.paths[0], a.paths[1], a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.atab, a.W, a.dcall, a.dglob0, a.slut,
-                       a.Dpad, piece_view(a, 0), piece_view(a, 1), a.epoch);
+                       a.paths[0], a.paths[1], a.Cst[0], a.Cst[1], a.Lrec, a.Rrec, a.Lrec4, a.Rrec4, a.atab, a.W, a.dcall,
+                       a.dglob0, a.slut, a.Dpad, piece_view(a, 0), piece_view(a, 1), a.epoch);
 }
 template <int SPL>
 static void up_chain_launch(hipStream_t st, const WalkArgs& a, int np) {

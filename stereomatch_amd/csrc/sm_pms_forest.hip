@@ -778,6 +778,17 @@ hipError_t pf_bfs(hipStream_t st, PfView& v, int K, int* out) {
     }
     hipLaunchKernelGGL(k_pf_depth, dim3(nblk(N, 256)), dim3(256), 0, st, v, dbits);
     {
+        // an inconsistent tour (a tile over TL_ARCS arcs, or k_pf_depth's range check) leaves positions of
+        // the sort input unwritten: stop here, before the sort and the gathers that would read them
+        int32_t bad = 0;
+        if ((e = hipMemcpyAsync(&bad, v.tot + 7, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        if (bad) {
+            out[2] = bad;
+            return hipSuccess;
+        }
+    }
+    {
         size_t tb = v.temp_bytes;
         if ((e = hipcub::DeviceRadixSort::SortPairs(v.temp, tb, v.tkey[0], v.tkey[1], v.tpix[0], v.gpix, N, 0, tbits + dbits,
                                                     st)) != hipSuccess)

@@ -253,12 +253,14 @@ def test_pms_flir_c1_two_calls_output_step(gpu_ctx, knobs):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("case", ["golden5000", "golden300", "synth300", "many_trees", "pieces16", "mst_mode", "full_c2"])
+@pytest.mark.parametrize("case", ["golden5000", "golden300", "synth300", "many_trees", "pieces16", "mst_mode", "one_pixel",
+                                  "full_c2"])
 def test_pms_gpu_forest_matches_host_build(gpu_ctx, knobs, case):
     """The schedule forest built on the GPU (sm_pms_forest.hip: union-find tree numbering, the level-order
     BFS of every tree, heavy paths, rows, tree graph, round lists) against the host construction
     (pms_build_forest), array by array (SM_PMS_FOREST_CHECK=1 makes the call fail on any difference), then
-    the call's labels against the oracle."""
+    the call's labels against the oracle.  "one_pixel": a 1 x 1 image, the only forest of single-pixel trees
+    the reference's min-size merge (min_size >= 2, Stereo3DMST.cpp:293) lets through (N - K == 0: no tour)."""
     knobs.setenv("SM_PMS_FOREST_CHECK", "1")
     knobs.delenv("SM_PMS_HOST_FOREST", raising=False)
     if case == "pieces16":
@@ -275,6 +277,10 @@ def test_pms_gpu_forest_matches_host_build(gpu_ctx, knobs, case):
         (left, right, _), D, c, ms = make_pair(640, 480, 32, index=9), 32, 5.0, 2
     elif case == "pieces16":
         (left, right, _), D, c, ms = make_pair(192, 128, 48, index=7), 48, 5000.0, 200
+    elif case == "one_pixel":
+        rng = np.random.default_rng(5)
+        left, right = (rng.integers(0, 256, (1, 1, 3), dtype=np.uint8) for _ in range(2))
+        D, c, ms = 4, 5000.0, 200
     elif case == "mst_mode":
         (left, right, _), D, c, ms = make_pair(200, 150, 32, index=2), 32, float("inf"), 200
     else:
