@@ -402,7 +402,10 @@ def main():
 
     # frames in flight: each context is a full pipeline on its own stream; frame i goes to context
     # i % n, so frame i+1's prep / MST / layout overlaps frame i's tree filter on the GPU
-    per_ctx_gb = W * H * (64 * (1 if Dloc <= 64 else 2 if Dloc <= 128 else 4)) * 20 * 2 / 1e9 + W * H * 400 / 1e9
+    # context footprint (round 6, compact A rows): ~25 B per pixel and padded slice (A_up rows 16, both
+    # views; compact A rows + cut-path rows ~5) + ~400 B per pixel (layout, MST); measured by
+    # tools/mem_probe.py: 8.26 GB at C2, 53.4 GB at C3 (round 5: 20 B x 2 -> C3 held 2 frames, now 3)
+    per_ctx_gb = W * H * (64 * (1 if Dloc <= 64 else 2 if Dloc <= 128 else 4)) * 25 / 1e9 + W * H * 400 / 1e9
     # segment mode: the segmentation's host steps give a frame ~17 ms of latency before its filter,
     # so it keeps more frames in flight (6) and begins lag = inflight - 2 frames ahead (stream_frames)
     seg_mode = math.isfinite(args.segment_c)

@@ -170,8 +170,11 @@ struct sm_ctx {
     // GPU layout buffers (sm_layout_gpu.hip)
     DevBuf adj[2], pdir[2], heavy[2], size[2], arcpix[2], hk[2], pixpre[2];
     DevBuf a_dist[2], a_cid[2], ccount[2], c_last[2], c_len[2];
-    DevBuf segtab[2], pathpos[2], plen[2], slotpix[2];
+    DevBuf segtab[2], pathpos[2], plen[2], slotpix[2], lrank[2], wrow[2];
     DevBuf pieces[2], pieces_tmp[2], agg[2], pstat[2], fix[2], pdbg;  // long-path pieces: table, segment aggregates, status words
+    // the down pass's A rows of light children's parents (compact: n_has_light rows, SmMeta::cslot[3]), and
+    // every node's A row by slot for the debug calls only (round 6: A was one dense row per slot)
+    DevBuf acmp[2], adbg[2];
     DevBuf cnw[2], tour[2], spart[2], rounds[2];
     int* h_changed = nullptr;
     uint32_t* h_err = nullptr;  // pinned, device-visible error word of the chain engine's waits
@@ -1060,6 +1063,8 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         CHECK(ensure(ctx, ctx->pathpos[v], N * 4));
         CHECK(ensure(ctx, ctx->plen[v], N * 4));
         CHECK(ensure(ctx, ctx->slotpix[v], N * 4));
+        CHECK(ensure(ctx, ctx->lrank[v], N));
+        CHECK(ensure(ctx, ctx->wrow[v], 4 * (size_t)ntiles * 4));
         z.add(ctx->ccount[v].p, 16);
         z.add(ctx->rounds[v].p, RREC * 4);
         LayoutView& L = LP.v[i];
@@ -1087,6 +1092,8 @@ sm_status stage_layout_enqueue(sm_ctx* ctx, int views) {
         L.pathpos = P<uint32_t>(ctx->pathpos[v]);
         L.plen = P<uint32_t>(ctx->plen[v]);
         L.slotpix = P<uint32_t>(ctx->slotpix[v]);
+        L.lrank = P<uint8_t>(ctx->lrank[v]);
+        L.wrow = P<uint32_t>(ctx->wrow[v]);
         uint32_t* R = P<uint32_t>(ctx->rounds[v]);
         L.round_begin = R;
         L.round_count = R + SM_NBUCKETS + 1;
@@ -1152,7 +1159,8 @@ WalkArgs walk_args(sm_ctx* ctx, int Dpad, int D, int dglob0) {
     for (int v = 0; v < 2; ++v) {
         a.meta[v] = P<SmMeta>(ctx->meta[v]);
         a.U[v] = P<double>(ctx->U[v]);
-        a.A[v] = nullptr;  // set by setup_sync (the fix buffer)
+        a.A[v] = nullptr;  // set by setup_sync (compact rows)
+        a.Adbg[v] = nullptr;  // debug calls only (stage_filter)
         a.Cst[v] = P<float>(ctx->Cst[v]);
         a.idx[v] = P<int32_t>(ctx->idx[v]);
         a.minc[v] = P<double>(ctx->minc[v]);
@@ -1203,6 +1211,8 @@ void set_bucket(sm_ctx* ctx, WalkArgs& a, uint32_t r, bool long_paths, int views
             a.bucket_plen[v] = (int)sm_bucket_piece_len(L.nodes[b], (uint32_t)a.piece_len);
             a.npieces[v] = pieces ? (int)(L.piece_begin[b + 1] - L.piece_begin[b]) : 0;
             a.agg[v] = pieces ? P<double>(ctx->agg[v]) + (size_t)L.seg_begin[b] * 2 * a.Dpad : nullptr;
+            // the bucket's cut paths' rows (sm_chain.hip FixRows): 32 per segment
+            a.fix[v] = P<double>(ctx->fix[v]) + (size_t)L.seg_begin[b] * SM_PRE_SEG * a.Dpad;
             a.pstat[v] = pieces ? P<uint32_t>(ctx->pstat[v]) + L.piece_begin[b] : nullptr;
         }
     }
@@ -1384,10 +1394,16 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
     for (int v = 0; v < 2; ++v) {
         if (view_on(ctx->views, v)) {
             CHECK(ensure(ctx, ctx->agg[v], pcap * 2 * (size_t)Dpad * 8));
-            CHECK(ensure(ctx, ctx->fix[v], N * (size_t)Dpad * 8));
+            // rows of the cut paths' nodes (32 per segment: the up repair's corrections, the down pieces'
+            // last rows) and the compact A rows of light children's parents; a quarter of headroom, so
+            // frames whose counts vary a little do not reallocate (hipFree synchronises the device)
+            const auto& L = ctx->layout[v];
+            const size_t nfix = (size_t)L.seg_begin[SM_NBUCKETS] * SM_PRE_SEG, nacmp = L.n_has_light;
+            if (ctx->fix[v].n < nfix * Dpad * 8) CHECK(ensure(ctx, ctx->fix[v], (nfix + nfix / 4 + 64) * Dpad * 8));
+            if (ctx->acmp[v].n < nacmp * Dpad * 8) CHECK(ensure(ctx, ctx->acmp[v], (nacmp + nacmp / 4 + 64) * Dpad * 8));
         }
-        a.fix[v] = P<double>(ctx->fix[v]);  // up pass: buffered repair rows
-        a.A[v] = a.fix[v];                  // down pass: A rows
+        a.fix[v] = P<double>(ctx->fix[v]);   // (set per bucket by set_bucket)
+        a.A[v] = P<double>(ctx->acmp[v]);
         const bool fresh = ctx->pstat[v].n < pcap * 8 * 4;
         CHECK(ensure(ctx, ctx->pstat[v], pcap * 8 * 4));
         if (fresh) HIPC(hipMemsetAsync(ctx->pstat[v].p, 0, pcap * 8 * 4, ctx->st));
@@ -1412,6 +1428,12 @@ sm_status stage_filter(sm_ctx* ctx, int D, int dglob0, int views, bool debug_sto
     WalkArgs a = walk_args(ctx, Dpad, D, dglob0);
     if (wta) a.wta = *wta;
     CHECK(setup_sync(ctx, a, N, Dpad));
+    if (debug_store_all)  // every node's A row by slot (sm_aggregate_debug)
+        for (int v = 0; v < 2; ++v)
+            if (view_on(views, v)) {
+                CHECK(ensure(ctx, ctx->adbg[v], N * (size_t)Dpad * 8));
+                a.Adbg[v] = P<double>(ctx->adbg[v]);
+            }
     a.vol = ctx->use_vol ? 1 : 0;
     a.leaf_cost = (!a.vol && !debug_store_all && !sm_knob("SM_NO_LEAF_COST")) ? 1 : 0;  // SM_NO_LEAF_COST: A/B
     if (a.vol)  // cost rows of every slot from the caller's volumes (slots come from the layout)
@@ -2462,6 +2484,45 @@ sm_status upload(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, int W, int H, 
     return SM_OK;
 }
 
+// Host check of one view's tree metadata (knob SM_LAYOUT_CHECK, tests): every light children's parent
+// holds a distinct compact A row below n_has_light in cslot[3], every path head's parent word is
+// SM_HEAD | its parent's row, every other node's the previous slot (or SM_NONE at the root)
+sm_status layout_check(sm_ctx* ctx, int v, size_t N) {
+    std::vector<SmMeta> m(N);
+    HIPC(hipMemcpy(m.data(), ctx->meta[v].p, N * sizeof(SmMeta), hipMemcpyDeviceToHost));
+    const uint32_t nl = ctx->layout[v].n_has_light;
+    std::vector<uint8_t> seen(nl + 1, 0);
+    size_t nlight = 0, nroot = 0;
+    char msg[160];
+    for (size_t s = 0; s < N; ++s) {
+        const SmMeta& x = m[s];
+        if (sm_meta_has_light(x)) {
+            ++nlight;
+            const uint32_t r = x.cslot[3];
+            if (r >= nl || seen[r]) {
+                snprintf(msg, sizeof msg, "layout check: slot %zu compact row %u (n_has_light %u)%s", s, r, nl, r < nl ? " twice" : "");
+                return fail(ctx, SM_ERR_STATE, msg);
+            }
+            seen[r] = 1;
+            if (sm_meta_nch(x) > 3) return fail(ctx, SM_ERR_STATE, "layout check: a light children's parent with 4 children");
+        }
+        const uint32_t w = x.parent;
+        if (w == SM_NONE) {
+            ++nroot;
+        } else if (w != (uint32_t)s - 1u) {
+            if (!(w & SM_HEAD) || sm_arow(w) >= nl) {
+                snprintf(msg, sizeof msg, "layout check: slot %zu parent word %08x (n_has_light %u)", s, w, nl);
+                return fail(ctx, SM_ERR_STATE, msg);
+            }
+        }
+    }
+    if (nlight != nl || nroot != 1) {
+        snprintf(msg, sizeof msg, "layout check: %zu light parents against n_has_light %u, %zu roots", nlight, nl, nroot);
+        return fail(ctx, SM_ERR_STATE, msg);
+    }
+    return SM_OK;
+}
+
 // the chain engine's error word (written by the device through the host mapping): reported once,
 // then cleared so the context stays usable
 sm_status check_device_error(sm_ctx* ctx) {
@@ -2615,7 +2676,8 @@ void sm_destroy(sm_ctx* ctx) {
                          &ctx->ccount[v], &ctx->c_last[v], &ctx->c_len[v], &ctx->cnw[v],
                          &ctx->tour[v], &ctx->spart[v],
                          &ctx->rounds[v], &ctx->segtab[v], &ctx->pathpos[v], &ctx->plen[v],
-                         &ctx->slotpix[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v]};
+                         &ctx->slotpix[v], &ctx->pieces[v], &ctx->pieces_tmp[v], &ctx->agg[v], &ctx->pstat[v], &ctx->fix[v],
+                         &ctx->acmp[v], &ctx->adbg[v], &ctx->lrank[v], &ctx->wrow[v]};
         if (v == 0 && ctx->pdbg.p) (void)hipFree(ctx->pdbg.p);
         for (DevBuf* b : lay) if (b->p) (void)hipFree(b->p);
     }
@@ -2925,6 +2987,7 @@ sm_status sm_build_tree_p(sm_ctx* ctx, const uint8_t* bgr, int W, int H, int str
     ctx->want_size = false;
     CHECK(ls);
     const size_t N = (size_t)W * H;
+    if (sm_knob("SM_LAYOUT_CHECK")) CHECK(layout_check(ctx, 0, N));  // diagnostics: the metadata's invariants
     // segment mode: the virtual edges that link the trees are not part of the reported forest
     const bool seg = ctx->seg;
     auto virt = [&](size_t i, int k) { return seg && ctx->h_fw[0][k][i] == SM_VIRTUAL_W; };
@@ -3004,7 +3067,7 @@ sm_status sm_aggregate_debug_p(sm_ctx* ctx, const uint8_t* l, const uint8_t* r, 
         CHECK(check_device_error(ctx));
     }
     CHECK(stage_filter(ctx, D, d0, 3, true));
-    HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->fix[view]), (int)N, Dpad, D, N,
+    HIPC(launch_rows_to_volume(ctx->st, P<SmMeta>(ctx->meta[view]), P<double>(ctx->adbg[view]), (int)N, Dpad, D, N,
                                P<double>(ctx->vol[0])));
     if (A) HIPC(hipMemcpyAsync(A, ctx->vol[0].p, N * D * 8, hipMemcpyDeviceToHost, ctx->st));
     HIPC(hipStreamSynchronize(ctx->st));

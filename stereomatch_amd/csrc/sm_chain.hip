@@ -823,11 +823,19 @@ __device__ __forceinline__ void up_helper_wave(UpRing<SPL>& ring, int hh, int he
 // failure, not a hang.  Status words hold the filter call's epoch, so nothing is reset per call.
 // ---------------------------------------------------------------------------------------------
 
+// rows of a cut path's nodes (the fix buffer, 32 rows per segment, WalkArgs::fix): node slot s of the
+// path whose first segment is f (bucket-relative, the piece entry's .w) has row s + off, off = 32 f - head
+struct FixRows {
+    double* p;      // the bucket's first row (nullptr: write through / none)
+    long long off;  // row = slot + off
+    __device__ uint32_t row(uint32_t slot) const { return (uint32_t)((long long)slot + off); }
+};
+
 struct PieceView {
     const uint4* pieces;  // {path, j, M, first segment of the path} per piece, bottom piece first
     int npieces;
     const double* agg;    // per bucket segment: [P row | B row]
-    double* fix;          // buffered repair rows (by slot, like U)
+    double* fix;          // the bucket's fix rows (FixRows): up repair corrections, down pieces' last rows
     uint32_t* stat;       // done [i], merged [i + stride], final [i + 2 * stride]
     int stride;
     int plen;             // nodes per piece
@@ -921,7 +929,7 @@ __device__ void up_guess(double* scratch, double* guess, const double* __restric
 template <int SPL, int CHR, bool AGD>
 __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32, double* __restrict__ U,
                                           const UpCost& cs, const double* slut, const float* atab, int top, int nmax,
-                                          int Dpad, int lane, double* xio, double* __restrict__ fix, bool write,
+                                          int Dpad, int lane, double* xio, FixRows fix, bool write,
                                           double* lfix = nullptr, int lcap = 0) {
     double x[SPL];
 #pragma unroll
@@ -991,8 +999,8 @@ __device__ __forceinline__ int up_exact_walk(const uint32_t* __restrict__ meta32
             const uint32_t slot = (uint32_t)(top - (n0 + k));
             if (n0 + k < lcap)  // buffered in LDS (the free ring): no global store between the batches'
                 lds_row_write<SPL>(lfix + (size_t)(n0 + k) * 64 * SPL, lane, x);  // loads and their waits
-            else if (fix)
-                store_row<SPL>(fix, slot, Dpad, lane, x);
+            else if (fix.p)
+                store_row<SPL>(fix.p, fix.row(slot), Dpad, lane, x);
             else
                 agent_row_write<SPL>(U, slot, Dpad, lane, x);
         }
@@ -1131,7 +1139,7 @@ __device__ __forceinline__ void up_repair_stage(RepNode<SPL>* rn, int kb, int k0
 // recomputed row equals the stored one, or -1.
 template <int SPL, bool AGD, class Pro>
 __device__ int up_repair_coop(UpRing<SPL>& ring, int* res2, const uint32_t* __restrict__ meta32, double* __restrict__ U,
-                              double* __restrict__ fix, const UpCost& cs, int Dpad, int wave, int lane, int top, int nmax,
+                              FixRows fix, const UpCost& cs, int Dpad, int wave, int lane, int top, int nmax,
                               int head, int write, Pro&& pro) {
     constexpr int BB = RepCfg<SPL>::BB, CHR = RepCfg<SPL>::CHR;
     RepNode<SPL>* rn = reinterpret_cast<RepNode<SPL>*>(ring.s);
@@ -1194,7 +1202,7 @@ __device__ int up_repair_coop(UpRing<SPL>& ring, int* res2, const uint32_t* __re
                 }
                 const uint32_t slot = (uint32_t)(top - (n0 + k));
                 if (write == 1)
-                    store_row<SPL>(fix, slot, Dpad, lane, x);
+                    store_row<SPL>(fix.p, fix.row(slot), Dpad, lane, x);
                 else if (write == 2)
                     agent_row_write<SPL>(U, slot, Dpad, lane, x);
             }
@@ -1223,7 +1231,7 @@ __device__ int up_repair_coop(UpRing<SPL>& ring, int* res2, const uint32_t* __re
 // merged.
 template <int SPL, bool AGD>
 __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restrict__ meta32, double* __restrict__ U,
-                          double* __restrict__ fix, const UpCost& cs, int Dpad, int lane, int head, int len, int j, int M,
+                          FixRows fix, const UpCost& cs, int Dpad, int lane, int head, int len, int j, int M,
                           int e, const PieceView& Q, uint32_t epoch) {
     uint32_t* done = Q.stat;
     uint32_t* merged = Q.stat + Q.stride;
@@ -1248,7 +1256,7 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     const unsigned long long tf1 = __builtin_amdgcn_s_memrealtime();
 #endif
     if (Q.dbg && Q.dbg[15] == 1) {  // probe (SM_PIECE_DEBUG=2): merge distance histogram, no writes
-        const int mp = up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, len, Dpad, lane, x, nullptr, false);
+        const int mp = up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, len, Dpad, lane, x, FixRows{nullptr, 0}, false);
         int b = 8;  // 8: < 8 nodes, 9: < 16, ... 13: >= 128 (merged), 14: never merged
         while (b < 13 && mp >= (8 << (b - 8))) ++b;
         if (lane == 0) atomicAdd(Q.dbg + (mp < 0 ? 14 : b), 1ull);
@@ -1283,7 +1291,7 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
             if (k < lcap)
                 lds_row_read<SPL>(lfix + (size_t)k * 64 * SPL, lane, r);
             else
-                load_row<SPL>(fix, (uint32_t)(top - k), Dpad, lane, r);
+                load_row<SPL>(fix.p, fix.row((uint32_t)(top - k)), Dpad, lane, r);
             store_row<SPL>(U, (uint32_t)(top - k), Dpad, lane, r);
         }
         if (lane == 0) publish_word(fin + e, epoch);
@@ -1295,7 +1303,7 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
     vm_drain();
     agent_row_read<SPL>(U, below, Dpad, lane, x);
     vm_drain();
-    up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, len, Dpad, lane, x, nullptr, true);
+    up_exact_walk<SPL, UP_WALK_CH(SPL), AGD>(meta32, U, cs, ring.slut, ring.atab, top, len, Dpad, lane, x, FixRows{nullptr, 0}, true);
     vm_drain();
     if (lane == 0) publish_word(fin + e, epoch);
 }
@@ -1304,7 +1312,7 @@ __device__ void up_finish(UpRing<SPL>& ring, int* hdone, const uint32_t* __restr
 // status words, the walk is up_repair_coop).  xin: the guess buffer, free after the chain.
 template <int SPL, bool AGD>
 __device__ void up_finish_coop(UpRing<SPL>& ring, double* xin, const uint32_t* __restrict__ meta32, double* __restrict__ U,
-                               double* __restrict__ fix, const UpCost& cs, int Dpad, int wave, int lane, int head, int len,
+                               FixRows fix, const UpCost& cs, int Dpad, int wave, int lane, int head, int len,
                                int j, int M, int e, const PieceView& Q, uint32_t epoch) {
     uint32_t* done = Q.stat;
     uint32_t* merged = Q.stat + Q.stride;
@@ -1374,7 +1382,7 @@ __device__ void up_finish_coop(UpRing<SPL>& ring, double* xin, const uint32_t* _
     if (all_s) {  // commit the corrections: rows 0 .. m-1 from fix, spread over the waves
         for (int k = wave; k < m; k += CHN_WAVES) {
             double r[SPL];
-            load_row<SPL>(fix, (uint32_t)(top - k), Dpad, lane, r);
+            load_row<SPL>(fix.p, fix.row((uint32_t)(top - k)), Dpad, lane, r);
             store_row<SPL>(U, (uint32_t)(top - k), Dpad, lane, r);
         }
         vm_drain();
@@ -1442,6 +1450,8 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
     const int o1 = (int)sm_piece_begin_p((uint32_t)plen, (uint32_t)M, (uint32_t)j + 1u, (uint32_t)Q.plen);
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
     const bool lower = j + 1 < M;
+    // a cut path's repair rows: 32 per segment of the path, from its first segment pc.w
+    const FixRows fx{Q.fix, (long long)pc.w * SM_PRE_SEG - (long long)path.head};
     const int wave = (int)uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
 #ifdef SM_CHAIN_TIMES  // diagnostic build: per-workgroup start / end (100 MHz) of every chain launch
     const unsigned long long tt0 = __builtin_amdgcn_s_memrealtime();
@@ -1475,7 +1485,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
         up_chain_wave<SPL>(ring, wave, head, len, lane, V.U, Dpad, lower ? guess : nullptr);
 #ifdef SM_UP_SOLO_REPAIR  // A/B: round 1's repair, wave 0 alone
         if (wave == 0 && M > 1)
-            up_finish<SPL, AGD>(ring, &hdone, meta32, V.U, Q.fix, cs, Dpad, lane, head, len, j, M, e, Q, epoch);
+            up_finish<SPL, AGD>(ring, &hdone, meta32, V.U, fx, cs, Dpad, lane, head, len, j, M, e, Q, epoch);
 #endif
     } else if (Split<SPL>::helper_of(wave) >= 0) {
         up_helper_wave<SPL, AGD>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V.U, cs, Dpad, lower,
@@ -1486,7 +1496,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_up_chain(WalkView V0, WalkView 
 #ifndef SM_UP_SOLO_REPAIR
     if (M > 1) {  // uniform over the block
         __syncthreads();  // the chain is done and every helper's stores have completed (vm_drain)
-        up_finish_coop<SPL, AGD>(ring, guess, meta32, V.U, Q.fix, cs, Dpad, wave, lane, head, len, j, M, e, Q, epoch);
+        up_finish_coop<SPL, AGD>(ring, guess, meta32, V.U, fx, cs, Dpad, wave, lane, head, len, j, M, e, Q, epoch);
     }
 #endif
 #ifdef SM_CHAIN_TIMES
@@ -1528,7 +1538,7 @@ struct DownSlot {
     double x[G][64 * SPL];  // T = S2 * A_up in, A out
     double S[G];
     uint32_t pix[G];
-    uint32_t st[G];         // row needed by light children (or the debug path)
+    uint32_t st[G];         // 1 + compact A row of a light children's parent, else 0
     int staged;             // g+1: group g staged          (helper -> chain waves)
     int done[2];            // g+1: chain wave w computed g (chain wave -> owner helper)
     int freed;              // g+1: slot of group g free     (owner helper -> next helper)
@@ -1676,7 +1686,7 @@ template <int SPL>
 __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, int head, int len, int lane,
                                                  const uint32_t* __restrict__ meta32, const WalkView& V, int Dpad,
                                                  const WtaCfg& w, int store_all, uint32_t epoch,
-                                                 uint32_t* done_word) {
+                                                 uint32_t* done_word, double* last_row) {
     constexpr int G = DownCfg<SPL>::G, NS = DownCfg<SPL>::NS, NCW = Split<SPL>::NCW;
     constexpr int NST = DN_STORERS, NL = Split<SPL>::NH - NST;
     const int ngroups = (len + G - 1) / G;
@@ -1706,8 +1716,10 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
             float dsp;
             wta_nodes<SPL, G>(xs, lane, w, mn, gi, dsp);
 #pragma unroll
-            for (int k = 0; k < G; ++k)
-                if (k < n && (store_all || st[k])) store_row<SPL>(V.A, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
+            for (int k = 0; k < G; ++k) {
+                if (k < n && st[k]) store_row<SPL>(V.A, st[k] - 1u, Dpad, lane, xs[k]);
+                if (k < n && store_all) store_row<SPL>(V.Adbg, (uint32_t)(head + g * G + k), Dpad, lane, xs[k]);
+            }
             if (lane < n) {
                 V.idx[pix] = gi;
                 V.minc[pix] = mn;
@@ -1715,7 +1727,7 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
             }
             if (done_word && g == ngroups - 1) {
                 // the piece's last row is the next piece's input: device scope, then the done word
-                double* row = V.A + (size_t)(head + len - 1) * Dpad + lane * SPL;
+                double* row = last_row + lane * SPL;
 #pragma unroll
                 for (int k = 0; k < G; ++k)
                     if (k == n - 1 && row_lane<SPL>(lane, Dpad))
@@ -1759,7 +1771,7 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
             Sk[k] = root || phead ? 0.0 : S;
             if (k < n && phead) {  // uniform; one node per path
                 double ap[SPL];
-                load_row<SPL>(V.A, par, Dpad, lane, ap);
+                load_row<SPL>(V.A, sm_arow(par), Dpad, lane, ap);
 #pragma unroll
                 for (int q = 0; q < SPL; ++q) t[k][q] = __builtin_fma(S, ap[q], t[k][q]);
             }
@@ -1768,7 +1780,7 @@ __device__ __forceinline__ void down_helper_wave(DownRing<SPL>& ring, int hh, in
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             pixk[k] = mfield(mv, k, 0);
-            stk[k] = hi_light(mfield(mv, k, 3));
+            stk[k] = hi_light(mfield(mv, k, 3)) ? mfield(mv, k, 7) + 1u : 0u;
         }
         // ---- next group's loads go out now (unconditional, clamped)
         const int gn = g + NL;
@@ -1897,7 +1909,7 @@ __device__ void down_guess(double* scratch, double* guess, const double* __restr
     if (wave == 0) {
         double x[SPL];
         if (hp != SM_NONE) {
-            load_row<SPL>(A, hp, Dpad, lane, x);  // finished in an earlier launch
+            load_row<SPL>(A, sm_arow(hp), Dpad, lane, x);  // finished in an earlier launch
         } else {
 #pragma unroll
             for (int k = 0; k < SPL; ++k) x[k] = 0.0;  // the root's S is 0
@@ -1922,7 +1934,8 @@ template <int SPL, int CHR>
 __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta32, const double* __restrict__ U,
                                                const WalkView& V, const double* slut, const double* s2lut, int head,
                                                int len, int nmax, int Dpad, int lane, double* xio, const WtaCfg& w,
-                                               int store_all, bool last_pub, bool check) {
+                                               int store_all, const double* last_row, bool check) {
+    const bool last_pub = last_row != nullptr;
     double x[SPL];
 #pragma unroll
     for (int q = 0; q < SPL; ++q) x[q] = xio[q];
@@ -1936,9 +1949,19 @@ __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta
         double u[CHR][SPL], spec[CHR][SPL], ys[CHR][SPL];
 #pragma unroll
         for (int k = 0; k < CHR; ++k) {
-            const uint32_t slot = (uint32_t)(head + n0 + min(k, nb - 1));
+            const int kk = min(k, nb - 1);
+            const uint32_t slot = (uint32_t)(head + n0 + kk);
             load_row<SPL>(U, slot, Dpad, lane, u[k]);
-            if (check) agent_row_read<SPL>(V.A, slot, Dpad, lane, spec[k]);
+            // the row stored for this node, if any: every row (debug), the piece's last row, or the
+            // compact A row of a light children's parent; another node reads its own U row (never
+            // compared).  Scalar selects and one unconditional load: the batch's loads stay one batch
+            if (check) {
+                const double* src = store_all ? V.Adbg + (size_t)slot * Dpad
+                                    : (last_pub && n0 + kk == len - 1) ? last_row
+                                    : hi_light(mfield(mv, kk, 3)) ? V.A + (size_t)mfield(mv, kk, 7) * Dpad
+                                    : U + (size_t)slot * Dpad;
+                agent_row_read<SPL>(src, 0, Dpad, lane, spec[k]);
+            }
         }
         int mk = nb;  // nodes of this batch before the merge
 #pragma unroll
@@ -1975,10 +1998,9 @@ __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta
         for (int k = 0; k < CHR; ++k) {
             if (k < mk) {
                 const uint32_t slot = (uint32_t)(head + n0 + k);
-                if (last_pub && n0 + k == len - 1)
-                    agent_row_write<SPL>(V.A, slot, Dpad, lane, ys[k]);
-                else if (store_all || hi_light(mfield(mv, k, 3)))
-                    store_row<SPL>(V.A, slot, Dpad, lane, ys[k]);
+                if (last_pub && n0 + k == len - 1) agent_row_write<SPL>(const_cast<double*>(last_row), 0, Dpad, lane, ys[k]);
+                if (hi_light(mfield(mv, k, 3))) store_row<SPL>(V.A, mfield(mv, k, 7), Dpad, lane, ys[k]);
+                if (store_all) store_row<SPL>(V.Adbg, slot, Dpad, lane, ys[k]);
             }
         }
         if (mk < nb) return n0 + mk;
@@ -1996,7 +2018,7 @@ __device__ __forceinline__ int down_exact_walk(const uint32_t* __restrict__ meta
 template <int SPL>
 __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __restrict__ meta32, const WalkView& V,
                             int Dpad, const WtaCfg& w, int store_all, int lane, int head, int len, int i, int M,
-                            int e, const PieceView& Q, uint32_t epoch) {
+                            int e, const PieceView& Q, uint32_t epoch, FixRows fx) {
     uint32_t* done = Q.stat;
     uint32_t* merged = Q.stat + Q.stride;
     uint32_t* fin = Q.stat + 2 * Q.stride;
@@ -2005,21 +2027,22 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
         return;
     }
     while (__hip_atomic_load(hdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < Split<SPL>::NH) __builtin_amdgcn_s_sleep(1);
-    const bool last_pub = i + 1 < M;
-    const uint32_t above = (uint32_t)(head - 1);  // last node of the piece above
+    // this piece's published last row (none for the bottom piece) and the piece above's
+    const double* last_row = i + 1 < M ? fx.p + (size_t)fx.row((uint32_t)(head + len - 1)) * Dpad : nullptr;
+    const double* above = fx.p + (size_t)fx.row((uint32_t)(head - 1)) * Dpad;
     double x[SPL];
 #ifdef SM_CHAIN_TIMES
     const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
 #endif
     wait_word(done + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
-    agent_row_read<SPL>(V.A, above, Dpad, lane, x);
+    agent_row_read<SPL>(above, 0, Dpad, lane, x);
     vm_drain();
 #ifdef SM_CHAIN_TIMES
     const unsigned long long tf1 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int m = down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, min(Q.rmax, len), Dpad,
-                                                        lane, x, w, store_all, last_pub, true);
+                                                        lane, x, w, store_all, last_row, true);
     vm_drain();
 #ifdef SM_CHAIN_TIMES
     if (lane == 0) {
@@ -2043,10 +2066,10 @@ __device__ void down_finish(DownRing<SPL>& ring, int* hdone, const uint32_t* __r
     }
     wait_word(fin + e - 1, epoch, epoch, Q.err, Q.wait_iters);
     vm_drain();
-    agent_row_read<SPL>(V.A, above, Dpad, lane, x);
+    agent_row_read<SPL>(above, 0, Dpad, lane, x);
     vm_drain();
     down_exact_walk<SPL, DN_WALK_CH(SPL)>(meta32, V.U, V, ring.slut, ring.s2lut, head, len, len, Dpad, lane, x, w,
-                                          store_all, last_pub, false);
+                                          store_all, last_row, false);
     vm_drain();
     if (lane == 0) publish_word(fin + e, epoch);
 }
@@ -2073,11 +2096,12 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     V.minc = view ? V1.minc : V0.minc;
     V.disp = view ? V1.disp : V0.disp;
     V.A = view ? V1.A : V0.A;
+    V.Adbg = view ? V1.Adbg : V0.Adbg;
     PieceView Q;
     Q.pieces = view ? Q1.pieces : Q0.pieces;
     Q.npieces = view ? Q1.npieces : Q0.npieces;
     Q.agg = view ? Q1.agg : Q0.agg;
-    Q.fix = nullptr;
+    Q.fix = view ? Q1.fix : Q0.fix;  // the pieces' published last rows
     Q.stat = view ? Q1.stat : Q0.stat;
     Q.stride = Q0.stride;
     Q.plen = view ? Q1.plen : Q0.plen;
@@ -2106,6 +2130,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     const int o0 = (int)sm_piece_begin_dn((uint32_t)plen, (uint32_t)M, (uint32_t)i, (uint32_t)Q.plen);
     const int o1 = (int)sm_piece_begin_dn((uint32_t)plen, (uint32_t)M, (uint32_t)i + 1u, (uint32_t)Q.plen);
     const int head = (int)uniform(path.head) + o0, len = o1 - o0;
+    const FixRows fx{Q.fix, (long long)pc.w * SM_PRE_SEG - (long long)path.head};  // (cut paths: M > 1)
 #ifdef SM_CHAIN_TIMES
     const unsigned long long tt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2159,10 +2184,11 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
     if (wave < Split<SPL>::NCW) {
         down_chain_wave<SPL>(ring, wave, len, lane, i > 0 ? guess : nullptr);
         if (wave == 0 && M > 1)
-            down_finish<SPL>(ring, &hdone, meta32, V, Dpad, w, store_all, lane, head, len, i, M, pidx, Q, epoch);
+            down_finish<SPL>(ring, &hdone, meta32, V, Dpad, w, store_all, lane, head, len, i, M, pidx, Q, epoch, fx);
     } else if (Split<SPL>::helper_of(wave) >= 0) {
-        down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V, Dpad, w, store_all,
-                              epoch, (M > 1 && i + 1 < M) ? Q.stat + pidx : nullptr);
+        const bool pub = M > 1 && i + 1 < M;
+        down_helper_wave<SPL>(ring, Split<SPL>::helper_of(wave), head, len, lane, meta32, V, Dpad, w, store_all, epoch,
+                              pub ? Q.stat + pidx : nullptr, pub ? Q.fix + (size_t)fx.row((uint32_t)(head + len - 1)) * Dpad : nullptr);
         vm_drain();  // this helper's stores are complete before the repair overwrites them
         if (lane == 0) atomicAdd(&hdone, 1);
     }
@@ -2174,7 +2200,7 @@ __global__ __launch_bounds__(CHN_THREADS) void k_down_chain(WalkView V0, WalkVie
 
 // ---------------------------------------------------------------------------------------------
 static WalkView chain_view(const WalkArgs& a, int v) {
-    return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v]};
+    return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v], a.Adbg[v]};
 }
 
 UpPreArgs up_pre_args(const WalkArgs& a) {

@@ -12,13 +12,21 @@
 #define SM_NONE 0xFFFFFFFFu
 
 // 32-byte per-slot record read by the walkers with one scalar load.
+//   parent: the previous slot for a node on its parent's heavy path; SM_HEAD | (compact A row of the
+//           parent) for a path head (the only reader of the parent's A row is the head); SM_NONE: root
+//   cslot[3]: a node with a light child has at most 3 children (every node but the root has a parent,
+//           and the root is the image's first pixel, a corner of its tree), so the fourth child word
+//           holds the node's own compact A row: the down pass stores A only for light children's
+//           parents, in a buffer of n_has_light rows instead of one row per slot (round 6)
 struct alignas(32) SmMeta {
     uint32_t pix;        // pixel index y*W+x
-    uint32_t parent;     // parent slot (SM_NONE for a root)
+    uint32_t parent;     // see above
     uint32_t lo;         // wp:10 | cw0:10 | cw1:10
     uint32_t hi;         // cw2:10 | cw3:10 | nch:3 | hidx:2 | has_light:1
-    uint32_t cslot[4];   // child slots in DESCENDING (w,a,b) key order (the up-pass order)
+    uint32_t cslot[4];   // child slots in DESCENDING (w,a,b) key order (the up-pass order); see above
 };
+#define SM_HEAD 0x80000000u  // parent word of a path head: SM_HEAD | compact A row of its parent
+__host__ __device__ static inline uint32_t sm_arow(uint32_t parent_word) { return parent_word & ~SM_HEAD; }
 
 // child ordering: the reference sums children in descending BFS id (Stereo3DMST.cpp:125),
 // BFS ids of siblings follow ascending edge key (:436-446, :492-516), so the up pass folds

@@ -29,7 +29,7 @@ const char* const kKnobs[] = {
     // guided-filter kernel variants (sm_guided.hip)
     "SM_GF_UNFUSED", "SM_GF_DIRECT_X",
     // diagnostics (stderr, counters)
-    "SM_LAYOUT_DEBUG", "SM_MST_DEBUG", "SM_SEG_DEBUG", "SM_SEG_PROF", "SM_PIECE_DEBUG", "SM_PMS_PROF",
+    "SM_LAYOUT_DEBUG", "SM_LAYOUT_CHECK", "SM_MST_DEBUG", "SM_SEG_DEBUG", "SM_SEG_PROF", "SM_PIECE_DEBUG", "SM_PMS_PROF",
     "SM_PMS_TREE_TIMES", "SM_PMS_COUNT_RUN", "SM_PREP_DEBUG",
     // fault injection of test_pms_forest_cycle_is_an_error
     "SM_TEST_PMS_CYCLE",

@@ -55,7 +55,8 @@ struct WalkArgs {
     const SmPath* paths[2];
     int npaths[2];
     double* U[2];
-    double* A[2];        // down-pass A rows (the up repair's scratch: free during the down pass)
+    double* A[2];        // down-pass A rows of light children's parents (compact: SmMeta::cslot[3])
+    double* Adbg[2];     // every node's A row by slot (debug calls, store_all), else nullptr
     int32_t* idx[2];
     double* minc[2];
     float* disp[2];
@@ -84,7 +85,10 @@ struct WalkArgs {
     // one workgroup per path, no pieces
     const uint4* pieces[2];
     int npieces[2];
-    double* fix[2];       // buffered repair rows, like U (by slot)
+    // rows of cut paths' nodes, 32 per segment (row = 32 * segment of the path + node offset in the
+    // path; per bucket from its first segment): the up repair's buffered corrections, the down
+    // pieces' published last rows
+    double* fix[2];
     double* agg[2];       // per bucket segment: [P row | B row] (2 * Dpad doubles), affine aggregates
     uint32_t* pstat[2];   // status words of the bucket's first piece: done / merged / final at
     int pstride;          // offsets 0, pstride, 2 * pstride

@@ -126,7 +126,11 @@ struct LayoutView {
     uint4* pieces;           // {path index within its bucket, j, M, first segment of the path
                              //  within the bucket}; piece j of M (0 = top), per path bottom first
     uint32_t* nrounds;
-    uint32_t* n_has_light;   // nodes with at least one light child (roofline accounting)
+    uint32_t* n_has_light;   // nodes with at least one light child: the compact A rows (SmMeta::cslot[3])
+    // compact A rows (round 6): a light children's parent's row is wrow's exclusive prefix at its
+    // (tile, wave) of the layout's 32x32 pixel tiles plus its rank among that wave's (k_orient)
+    uint8_t* lrank;          // [pixel] rank among the light children's parents of its tile wave (< 256)
+    uint32_t* wrow;          // [4 * tile + wave]: their count, then (inclusive scan) the running total
 };
 
 // the layout scans' tile totals (sm_layout_gpu.hip k_scan_reduce), per view, one 64-bit slot per tile

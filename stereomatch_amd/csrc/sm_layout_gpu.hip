@@ -82,6 +82,17 @@ __device__ __forceinline__ void tile_pixels(const TileRef& t, int W, int H, F&& 
         if (x < W && y < H) f((uint32_t)(y * W + x));
     }
 }
+// ... with the pixel's coordinates: f(pixel, x, y)
+template <class F>
+__device__ __forceinline__ void tile_pixels_xy(const TileRef& t, int W, int H, F&& f) {
+    if (!t.ok) return;
+    const int lx = (int)threadIdx.x & 31, ly = (int)threadIdx.x >> 5;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int x = t.x0 + lx, y = t.y0 + ly + 8 * i;
+        if (x < W && y < H) f((uint32_t)(y * W + x), (uint32_t)x, (uint32_t)y);
+    }
+}
 
 __global__ void k_adj(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
@@ -178,7 +189,10 @@ __global__ __launch_bounds__(256) void k_chain_rank(LayoutPair LP) {
 __global__ void k_orient(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.z];
-    tile_pixels(layout_tile(W, H, (int)blockIdx.x), W, H, [&](uint32_t v) {
+    const TileRef tr = layout_tile(W, H, (int)blockIdx.x);
+    const unsigned long long below = (1ull << (threadIdx.x & 63)) - 1ull;
+    uint32_t wacc = 0;  // this wave's light children's parents so far (every active lane holds it)
+    tile_pixels(tr, W, H, [&](uint32_t v) {
         const uint32_t adj = V.adj[v];
         const uint32_t total = 2u * (uint32_t)(W * H) - 2u;
         const TourBufs T = tour_bufs(V);
@@ -209,6 +223,12 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
                 if (csz[k] > best) { best = csz[k]; heavy = k; }
             }
         }
+        // compact A row, part 1 (SmMeta::cslot[3]): a node of >= 2 children has a light one; its rank
+        // among its tile wave's (the wave's lanes active here were active in every earlier pass)
+        const int nc = __popc(adj & 15u) - (pd >= 0 ? 1 : 0);
+        const unsigned long long bal = __ballot(!bad && nc >= 2);
+        if (!bad && nc >= 2) V.lrank[v] = (uint8_t)(wacc + (uint32_t)__popcll(bal & below));
+        wacc += (uint32_t)__popcll(bal);
         if (bad) {
             __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
@@ -234,6 +254,9 @@ __global__ void k_orient(LayoutPair LP, int W, int H) {
             V.arcpix[crio[k].x] = nbr_of(v, k, W);  // the child, for the scan's epilogue
         }
     });
+    // the wave's count (lane 0 is active wherever any lane of its wave is), scanned after this pass
+    if (tr.ok && (threadIdx.x & 63) == 0)
+        V.wrow[4 * ((tr.y0 / TL) * ((W + TL - 1) / TL) + tr.x0 / TL) + (threadIdx.x >> 6)] = wacc;
 }
 
 // ---- inclusive scans: reduce, then scan (round 5).  A tile is SP_TILE elements (4096 of 32 bits, 2048 of 64) per 256-thread block,
@@ -507,15 +530,28 @@ static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S
 // reference's fold order), heavy-child position, light flag.  Round 5: computed in pixel order, where a
 // node's tree neighbours are its grid neighbours (local reads), and written to its slot (one random
 // 32-byte store) -- in slot order it had gathered a packed record of the node and of every neighbour.
-#define META_BLOCKS 1024  // blocks per view (grid-stride): one has-light atomic per block
+// Round 6: compact A rows (SmMeta::cslot[3], sm_common.h) without atomics: a light children's parent's
+// row is its tile wave's first row (wrow, exclusive) plus its rank in the wave (lrank, k_orient), so a
+// path head writes its parent's row into its own parent word here too (SM_HEAD | row).
+#define META_BLOCKS 1024  // blocks per view (grid-stride)
+
+// pixel u = (x, y); ntx tiles per image row
+__device__ __forceinline__ uint32_t compact_row(const LayoutView& V, uint32_t u, uint32_t x, uint32_t y, uint32_t ntx) {
+    const uint32_t k = 4u * ((y / TL) * ntx + x / TL) + ((y & 7u) >> 1);
+    return (k ? V.wrow[k - 1u] : 0u) + V.lrank[u];
+}
 
 __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
     if (*LP.mst_ok == 0) return;  // the MST is still a forest: nothing to lay out yet (stage_layout redoes it)
     const LayoutView& V = LP.v[blockIdx.y];
-    uint32_t nlight = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the rows' total: the scan's last entry
+        const uint32_t nw = 4u * (uint32_t)(((W + TL - 1) / TL) * ((H + TL - 1) / TL));
+        *V.n_has_light = V.wrow[nw - 1u];
+    }
     // tiles in the XCD-aware order, grid-stride (META_BLOCKS is a multiple of 8: a block keeps its XCD band)
     const int nb = layout_tile_blocks(W, H);
-    for (int b = (int)blockIdx.x; b < nb; b += META_BLOCKS) tile_pixels(layout_tile(W, H, b), W, H, [&](uint32_t v) {
+    const uint32_t ntx = (uint32_t)(W + TL - 1) / TL;
+    for (int b = (int)blockIdx.x; b < nb; b += META_BLOCKS) tile_pixels_xy(layout_tile(W, H, b), W, H, [&](uint32_t v, uint32_t px, uint32_t py) {
         const uint32_t adj = V.adj[v];
         const int pd = V.pdir[v], hv = V.heavy[v];
         const uint32_t slot = V.slotpix[v];
@@ -544,7 +580,9 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
             const uint32_t ns = in ? V.slotpix[n] : SM_NONE;
             if (in && k == pd) {
                 wp = key >> 2;
-                parent = ns;
+                // a path head (not its parent's heavy child): SM_HEAD | the parent's compact A row
+                const uint32_t nx = k == 0 ? px + 1u : k == 2 ? px - 1u : px, ny = k == 1 ? py + 1u : k == 3 ? py - 1u : py;
+                parent = V.heavy[n] == ((k + 2) & 3) ? ns : (SM_HEAD | compact_row(V, n, nx, ny, ntx));
             }
             ck[k] = key;
             cq[k] = k;
@@ -573,15 +611,13 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
                 if (cq[i] == hv) hidx = (uint32_t)i; else has_light = 1;
             }
         }
+        if (has_light) {
+            // a light children's parent has at most 3 children (sm_common.h): its fourth child word is free
+            if (nch > 3) __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            cs[3] = compact_row(V, v, px, py, ntx);
+        }
         V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
-        nlight += has_light;
     });
-    __shared__ uint32_t nl;
-    if (threadIdx.x == 0) nl = 0;
-    __syncthreads();
-    if (nlight) atomicAdd(&nl, nlight);
-    __syncthreads();
-    if (threadIdx.x == 0 && nl) atomicAdd(V.n_has_light, nl);
 }
 
 // heads in preorder -> path lengths -> bucketed by light depth (order inside a round is free).
@@ -861,6 +897,8 @@ hipError_t launch_layout(hipStream_t st, const LayoutPair& LP, int nviews, int W
     hipLaunchKernelGGL(k_chain_init, cg, dim3(256), 0, st, LP, W);
     hipLaunchKernelGGL(k_chain_rank, dim3(std::min<uint32_t>((max_chains + 255) / 256, CR_BLOCKS), nviews), dim3(256), 0, st, LP);
     hipLaunchKernelGGL(k_orient, tg, dim3(256), 0, st, LP, W, H);
+    ScanBufs<uint32_t> wb{{LP.v[0].wrow, LP.v[1].wrow}, {nullptr, nullptr}};  // compact A rows per tile wave
+    launch_scan<uint32_t, OpAdd>(st, wb, LP.scan, nviews, 4 * ((W + TL - 1) / TL) * ((H + TL - 1) / TL));
     ScanBufs<uint32_t> tb{{LP.v[0].tour, LP.v[1].tour}, {nullptr, nullptr}};
     launch_scan<uint32_t, OpAdd>(st, tb, LP.scan, nviews, 2 * N - 2, ScanTourOut{LP, N});
     const dim3 sg((N + PATH_BLOCK * PATH_ITEMS - 1) / (PATH_BLOCK * PATH_ITEMS), nviews);

@@ -572,7 +572,7 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
                 load_leaf_row<SPL>(V.U, slot, Dpad, lane, u[j]);  // f32 bits in u[j]'s registers
 #endif
             if (head_j && par[j] != SM_NONE) {  // wave-uniform: only path heads read their parent's row
-                load_row<SPL>(V.A, par[j], Dpad, lane, xp[j]);
+                load_row<SPL>(V.A, sm_arow(par[j]), Dpad, lane, xp[j]);
             } else {
 #pragma unroll
                 for (int q = 0; q < SPL; ++q) xp[j][q] = 0.0;
@@ -615,8 +615,9 @@ __global__ __launch_bounds__(256) void k_down_walk(WalkView V0, WalkView V1, con
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            if (j < n && (store_all || hi_light(mfield(cur, j, 3))))  // the root too: A is a separate buffer
-                store_row<SPL>(V.A, (uint32_t)(c0 + j), Dpad, lane, xs[j]);
+            // light children's parents (the root too: A is a separate buffer) at their compact row
+            if (j < n && hi_light(mfield(cur, j, 3))) store_row<SPL>(V.A, mfield(cur, j, 7), Dpad, lane, xs[j]);
+            if (j < n && store_all) store_row<SPL>(V.Adbg, (uint32_t)(c0 + j), Dpad, lane, xs[j]);
         }
         double mn;
         int gi;
@@ -742,8 +743,10 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
                 load_row<SH>(V.U, slot, DP, hlane, u[j]);
             else
                 load_leaf_row<SH>(V.U, slot, DP, hlane, u[j]);
-            if (head_j && par[j] != SM_NONE) {
-                load_row<SH>(V.A, par[j], DP, hlane, xp[j]);
+            // a finished half's re-read chunk pairs node j's words with slot c0: no A row is read
+            // there (its parent word may be a slot, not a compact A row)
+            if (n > 0 && head_j && par[j] != SM_NONE) {
+                load_row<SH>(V.A, sm_arow(par[j]), DP, hlane, xp[j]);
             } else {
 #pragma unroll
                 for (int k = 0; k < SH; ++k) xp[j][k] = 0.0;
@@ -783,7 +786,8 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            if (j < n && (store_all || hi_light(hiw[j]))) store_row<SH>(V.A, (uint32_t)(c0 + j), DP, hlane, xs[j]);
+            if (j < n && hi_light(hiw[j])) store_row<SH>(V.A, hfield<CH>(cur, hl, j, 7), DP, hlane, xs[j]);
+            if (j < n && store_all) store_row<SH>(V.Adbg, (uint32_t)(c0 + j), DP, hlane, xs[j]);
         }
         double mn;
         int mi;
@@ -810,7 +814,7 @@ __global__ __launch_bounds__(256) void k_down_walk_h2(WalkView V0, WalkView V1, 
 
 // ---------------------------------------------------------------------------------------------
 static WalkView to_view(const WalkArgs& a, int v) {
-    return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v]};
+    return WalkView{a.npaths[v], a.U[v], a.idx[v], a.minc[v], a.disp[v], a.A[v], a.Adbg[v]};
 }
 
 // A/B knob: extra dynamic LDS per block (limits walker occupancy; experiments only)

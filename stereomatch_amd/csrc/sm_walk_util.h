@@ -17,8 +17,10 @@ struct WalkView {
     int32_t* idx;          // W*H   (down pass)
     double* minc;          // W*H   (down pass)
     float* disp;           // W*H   (down pass)
-    double* A;             // [slots][Dpad]: A rows of the down pass (rows light children or the
-                           // debug path read); separate from U so A_up stays intact (down repair)
+    double* A;             // [n_has_light][Dpad]: A rows of the down pass for the parents of light
+                           // children (row = SmMeta::cslot[3]; a head reads sm_arow(parent word));
+                           // separate from U so A_up stays intact (down repair)
+    double* Adbg;          // [slots][Dpad]: every node's A row (debug calls, store_all), else unused
 };
 
 #define SM_NUM_W 766
