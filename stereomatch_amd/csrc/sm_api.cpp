@@ -1395,12 +1395,13 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
         if (view_on(ctx->views, v)) {
             CHECK(ensure(ctx, ctx->agg[v], pcap * 2 * (size_t)Dpad * 8));
             // rows of the cut paths' nodes (32 per segment: the up repair's corrections, the down pieces'
-            // last rows) and the compact A rows of light children's parents; a quarter of headroom, so
-            // frames whose counts vary a little do not reallocate (hipFree synchronises the device)
+            // last rows) and the compact A rows of light children's parents; 1/16 of headroom, so frames
+            // whose counts vary a little do not reallocate (hipFree synchronises the device) while a C3
+            // context stays near 50 GB
             const auto& L = ctx->layout[v];
             const size_t nfix = (size_t)L.seg_begin[SM_NBUCKETS] * SM_PRE_SEG, nacmp = L.n_has_light;
-            if (ctx->fix[v].n < nfix * Dpad * 8) CHECK(ensure(ctx, ctx->fix[v], (nfix + nfix / 4 + 64) * Dpad * 8));
-            if (ctx->acmp[v].n < nacmp * Dpad * 8) CHECK(ensure(ctx, ctx->acmp[v], (nacmp + nacmp / 4 + 64) * Dpad * 8));
+            if (ctx->fix[v].n < nfix * Dpad * 8) CHECK(ensure(ctx, ctx->fix[v], (nfix + nfix / 16 + 64) * Dpad * 8));
+            if (ctx->acmp[v].n < nacmp * Dpad * 8) CHECK(ensure(ctx, ctx->acmp[v], (nacmp + nacmp / 16 + 64) * Dpad * 8));
         }
         a.fix[v] = P<double>(ctx->fix[v]);   // (set per bucket by set_bucket)
         a.A[v] = P<double>(ctx->acmp[v]);

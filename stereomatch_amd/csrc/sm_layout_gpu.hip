@@ -535,10 +535,10 @@ static void launch_scan(hipStream_t st, const ScanBufs<T>& B, const ScanState& S
 // path head writes its parent's row into its own parent word here too (SM_HEAD | row).
 #define META_BLOCKS 1024  // blocks per view (grid-stride)
 
-// pixel u = (x, y); ntx tiles per image row
-__device__ __forceinline__ uint32_t compact_row(const LayoutView& V, uint32_t u, uint32_t x, uint32_t y, uint32_t ntx) {
+// the first compact row of pixel (x, y)'s tile wave; ntx tiles per image row
+__device__ __forceinline__ uint32_t wave_row0(const LayoutView& V, uint32_t x, uint32_t y, uint32_t ntx) {
     const uint32_t k = 4u * ((y / TL) * ntx + x / TL) + ((y & 7u) >> 1);
-    return (k ? V.wrow[k - 1u] : 0u) + V.lrank[u];
+    return k ? V.wrow[k - 1u] : 0u;
 }
 
 __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
@@ -555,6 +555,13 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
         const uint32_t adj = V.adj[v];
         const int pd = V.pdir[v], hv = V.heavy[v];
         const uint32_t slot = V.slotpix[v];
+        // compact rows: v's own and its parent's inputs, loaded up front (unconditional: a root or a
+        // node without light children reads its own words and ignores them)
+        const uint32_t pn = pd >= 0 ? nbr_of(v, pd, W) : v;
+        const uint32_t pnx = pd == 0 ? px + 1u : pd == 2 ? px - 1u : px, pny = pd == 1 ? py + 1u : pd == 3 ? py - 1u : py;
+        const int par_heavy = V.heavy[pn];
+        const uint32_t par_row = wave_row0(V, pnx, pny, ntx) + V.lrank[pn];
+        const uint32_t own_row = wave_row0(V, px, py, ntx) + V.lrank[v];
         if (slot >= (uint32_t)(W * H)) {  // (never for a spanning tree's tour: defensive, err set)
             __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
@@ -581,8 +588,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
             if (in && k == pd) {
                 wp = key >> 2;
                 // a path head (not its parent's heavy child): SM_HEAD | the parent's compact A row
-                const uint32_t nx = k == 0 ? px + 1u : k == 2 ? px - 1u : px, ny = k == 1 ? py + 1u : k == 3 ? py - 1u : py;
-                parent = V.heavy[n] == ((k + 2) & 3) ? ns : (SM_HEAD | compact_row(V, n, nx, ny, ntx));
+                parent = par_heavy == ((k + 2) & 3) ? ns : (SM_HEAD | par_row);
             }
             ck[k] = key;
             cq[k] = k;
@@ -614,7 +620,7 @@ __global__ __launch_bounds__(256) void k_meta(LayoutPair LP, int W, int H) {
         if (has_light) {
             // a light children's parent has at most 3 children (sm_common.h): its fourth child word is free
             if (nch > 3) __hip_atomic_fetch_or(LP.scan.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            cs[3] = compact_row(V, v, px, py, ntx);
+            cs[3] = own_row;
         }
         V.meta[slot] = sm_make_meta(v, parent, wp, cw, (uint32_t)nch, hidx, has_light, cs);
     });
