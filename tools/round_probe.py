@@ -34,7 +34,7 @@ ctx.set_kernel_timing([])
 for _ in range(a.warmup):
     ctx.match_async(a.D, p)
     ctx.synchronize()
-os.environ["SM_LAYOUT_DEBUG"] = "1"
+sm.set_knob("SM_LAYOUT_DEBUG", "1")  # knobs only through sm_set_knob (round 6)
 for i in range(a.frames):
     print("# frame %d" % i, file=sys.stderr, flush=True)
     t = time.perf_counter()
