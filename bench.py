@@ -337,6 +337,9 @@ def main():
                     help="A/B: stream frames with sm_match_async instead of sm_match_begin/finish")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight (contexts on their own streams); 0 = 3, fewer where memory needs it")
+    ap.add_argument("--lag", type=int, default=0,
+                    help="frames whose tree is enqueued before the host waits for an earlier frame's layout "
+                         "(stream_frames; 0 = 1 in MST mode, inflight - 2 in segment mode)")
     ap.add_argument("--plan-only", action="store_true",
                     help="CPU check: start the ranks, print each rank's share and communicator set-up (stub "
                          "contexts, no GPU), exit")
@@ -464,7 +467,7 @@ def main():
     # frame groups: the timed region is args.steps frames of the stream; group fg takes frames fg, fg+G, ...
     my_steps = len(range(plan["fgroup"], args.steps, plan["fgroups"]))
     stream_frames(ctxs, my_steps, Dloc, params, retire, split=not args.no_split,
-                  lag=max(1, len(ctxs) - 2) if seg_mode else 1)
+                  lag=args.lag if args.lag > 0 else (max(1, len(ctxs) - 2) if seg_mode else 1))
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0

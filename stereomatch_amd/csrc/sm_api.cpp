@@ -1319,7 +1319,11 @@ sm_status up_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views) {
         cut = cut || (al.pieces[v] && sm_piece_cut((uint32_t)al.maxlen, (uint32_t)al.bucket_plen[v]));
     set_bucket(ctx, a, r, false, views);
     const WalkArgs as = a;
-    const double vs = bucket_voxels(ctx, r, false, views, a.dcall);
+    double vs = bucket_voxels(ctx, r, false, views, a.dcall);
+#ifdef SM_DEV  // timing experiment only (wrong results): no walker launch for buckets below this many nodes
+    if (const char* e = sm_dev_knob("SM_EXP_SKIP_SMALL_WALK"))
+        if (vs < atof(e) * a.dcall) vs = 0.0;
+#endif
 #ifndef SM_PRE_FUSED  // the aggregates in a launch of their own, before the chains
     if (cut) CHECK(timed(ctx, ctx->st2, KF_UP_PRE, vl, [&] { return launch_up_pre(ctx->st2, al, spl); }, 0.0));
     CHECK(timed(ctx, ctx->st2, KF_UP_CHAIN, vl, [&] { return launch_up_chain(ctx->st2, al, spl); }));
@@ -1344,7 +1348,12 @@ sm_status down_round(sm_ctx* ctx, WalkArgs& a, uint32_t r, int spl, int views, b
                 [&] { return launch_down_long(ctx->st2, al, spl, store_all ? 1 : 0); }));
     set_bucket(ctx, a, r, false, views);
     const WalkArgs as = a;
-    CHECK(timed(ctx, ctx->st, KF_DOWN_WALK, bucket_voxels(ctx, r, false, views, a.dcall), [&] {
+    double vs = bucket_voxels(ctx, r, false, views, a.dcall);
+#ifdef SM_DEV  // timing experiment only (wrong results), as up_round
+    if (const char* e = sm_dev_knob("SM_EXP_SKIP_SMALL_WALK"))
+        if (vs < atof(e) * a.dcall) vs = 0.0;
+#endif
+    CHECK(timed(ctx, ctx->st, KF_DOWN_WALK, vs, [&] {
         return store_all ? launch_down_debug(ctx->st, as, spl, false) : launch_down(ctx->st, as, spl, false);
     }));
     return SM_OK;
@@ -1393,13 +1402,19 @@ sm_status setup_sync(sm_ctx* ctx, WalkArgs& a, size_t N, int Dpad) {
     }
     for (int v = 0; v < 2; ++v) {
         if (view_on(ctx->views, v)) {
-            CHECK(ensure(ctx, ctx->agg[v], pcap * 2 * (size_t)Dpad * 8));
-            // rows of the cut paths' nodes (32 per segment: the up repair's corrections, the down pieces'
-            // last rows) and the compact A rows of light children's parents; 1/16 of headroom, so frames
-            // whose counts vary a little do not reallocate (hipFree synchronises the device) while a C3
-            // context stays near 50 GB
+            // the segment aggregates of the cut paths (2 rows per 32-node segment; a bucket's down pieces,
+            // listed first among its items, write theirs at the piece index, below the bucket's segment
+            // count since a piece spans >= 16 segments), the rows of the cut paths' nodes (32 per segment:
+            // the up repair's corrections, the down pieces' last rows) and the compact A rows of light
+            // children's parents, all sized by this layout's counts with 1/16 of headroom, so frames whose
+            // counts vary a little do not reallocate (hipFree synchronises the device).  Round 6: the
+            // aggregates were sized by the piece capacity (N/16 segments: 4.2 GB of a C3 context, against
+            // ~0.5 GB used); a C3 context is now below 50 GB
             const auto& L = ctx->layout[v];
-            const size_t nfix = (size_t)L.seg_begin[SM_NBUCKETS] * SM_PRE_SEG, nacmp = L.n_has_light;
+            const size_t nseg = (size_t)L.seg_begin[SM_NBUCKETS];
+            if (ctx->agg[v].n < nseg * 2 * Dpad * 8 || !ctx->agg[v].p)
+                CHECK(ensure(ctx, ctx->agg[v], (nseg + nseg / 16 + 64) * 2 * (size_t)Dpad * 8));
+            const size_t nfix = nseg * SM_PRE_SEG, nacmp = L.n_has_light;
             if (ctx->fix[v].n < nfix * Dpad * 8) CHECK(ensure(ctx, ctx->fix[v], (nfix + nfix / 16 + 64) * Dpad * 8));
             if (ctx->acmp[v].n < nacmp * Dpad * 8) CHECK(ensure(ctx, ctx->acmp[v], (nacmp + nacmp / 16 + 64) * Dpad * 8));
         }
